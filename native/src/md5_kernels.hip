@@ -1,0 +1,221 @@
+// N5: chunked MD5 tree hash on gfx950 — the GPU analogue of the reference's "/cpu" benchmark
+// (docs/benchmarks.md:11-12: md5 of 268435456 random bytes, 16.86 s on a Triton KVM).
+//
+// MD5 is a Merkle-Damgard chain, so one digest over 256 MiB is a serial dependency chain.
+// The GPU form splits the input into fixed chunks (default 1 KiB), one chunk per lane, hashes
+// every chunk with standard RFC 1321 MD5 (padding + length included), then hashes the
+// concatenated 16-byte digests the same way, level after level, until one digest remains.
+// The exact host oracle is hashlib-based: tritonk8ssupervisor_amd/ops/reference.py:md5_tree.
+//
+// Per lane: 16 message words per 64-byte block via four 16-byte loads (the next block is
+// loaded before the current one is compressed, so its latency hides under 64 ALU steps);
+// the 64 steps are fully unrolled with constant K/s (VALU: v_bfi / v_alignbit / v_add3).
+// With 1 KiB chunks a 256 MiB input is 262144 lanes = 4096 wave64s = 16 waves per CU on
+// 256 CUs, enough to keep the HBM stream and the integer pipes busy together.
+#include <hip/hip_runtime.h>
+
+#include "tk8s/common.h"
+#include "tk8s/kernels.h"
+
+namespace tk8s {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kMd5Block = 256;
+
+#define TK8S_F(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
+#define TK8S_G(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
+#define TK8S_H(x, y, z) ((x) ^ (y) ^ (z))
+#define TK8S_I(x, y, z) ((y) ^ ((x) | ~(z)))
+#define TK8S_STEP(f, a, b, c, d, x, k, s)               \
+  do {                                                  \
+    (a) += f((b), (c), (d)) + (x) + (k);                \
+    (a) = __builtin_rotateleft32((a), (s)) + (b);       \
+  } while (0)
+
+__device__ __forceinline__ void md5_compress(unsigned st[4], const unsigned m[16]) {
+  unsigned a = st[0], b = st[1], c = st[2], d = st[3];
+  TK8S_STEP(TK8S_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+  TK8S_STEP(TK8S_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+  TK8S_STEP(TK8S_F, c, d, a, b, m[2], 0x242070dbu, 17);
+  TK8S_STEP(TK8S_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+  TK8S_STEP(TK8S_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+  TK8S_STEP(TK8S_F, d, a, b, c, m[5], 0x4787c62au, 12);
+  TK8S_STEP(TK8S_F, c, d, a, b, m[6], 0xa8304613u, 17);
+  TK8S_STEP(TK8S_F, b, c, d, a, m[7], 0xfd469501u, 22);
+  TK8S_STEP(TK8S_F, a, b, c, d, m[8], 0x698098d8u, 7);
+  TK8S_STEP(TK8S_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+  TK8S_STEP(TK8S_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+  TK8S_STEP(TK8S_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+  TK8S_STEP(TK8S_F, a, b, c, d, m[12], 0x6b901122u, 7);
+  TK8S_STEP(TK8S_F, d, a, b, c, m[13], 0xfd987193u, 12);
+  TK8S_STEP(TK8S_F, c, d, a, b, m[14], 0xa679438eu, 17);
+  TK8S_STEP(TK8S_F, b, c, d, a, m[15], 0x49b40821u, 22);
+
+  TK8S_STEP(TK8S_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+  TK8S_STEP(TK8S_G, d, a, b, c, m[6], 0xc040b340u, 9);
+  TK8S_STEP(TK8S_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+  TK8S_STEP(TK8S_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+  TK8S_STEP(TK8S_G, a, b, c, d, m[5], 0xd62f105du, 5);
+  TK8S_STEP(TK8S_G, d, a, b, c, m[10], 0x02441453u, 9);
+  TK8S_STEP(TK8S_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+  TK8S_STEP(TK8S_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+  TK8S_STEP(TK8S_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+  TK8S_STEP(TK8S_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+  TK8S_STEP(TK8S_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+  TK8S_STEP(TK8S_G, b, c, d, a, m[8], 0x455a14edu, 20);
+  TK8S_STEP(TK8S_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+  TK8S_STEP(TK8S_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+  TK8S_STEP(TK8S_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+  TK8S_STEP(TK8S_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+
+  TK8S_STEP(TK8S_H, a, b, c, d, m[5], 0xfffa3942u, 4);
+  TK8S_STEP(TK8S_H, d, a, b, c, m[8], 0x8771f681u, 11);
+  TK8S_STEP(TK8S_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
+  TK8S_STEP(TK8S_H, b, c, d, a, m[14], 0xfde5380cu, 23);
+  TK8S_STEP(TK8S_H, a, b, c, d, m[1], 0xa4beea44u, 4);
+  TK8S_STEP(TK8S_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+  TK8S_STEP(TK8S_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+  TK8S_STEP(TK8S_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
+  TK8S_STEP(TK8S_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
+  TK8S_STEP(TK8S_H, d, a, b, c, m[0], 0xeaa127fau, 11);
+  TK8S_STEP(TK8S_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
+  TK8S_STEP(TK8S_H, b, c, d, a, m[6], 0x04881d05u, 23);
+  TK8S_STEP(TK8S_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
+  TK8S_STEP(TK8S_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
+  TK8S_STEP(TK8S_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+  TK8S_STEP(TK8S_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+
+  TK8S_STEP(TK8S_I, a, b, c, d, m[0], 0xf4292244u, 6);
+  TK8S_STEP(TK8S_I, d, a, b, c, m[7], 0x432aff97u, 10);
+  TK8S_STEP(TK8S_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+  TK8S_STEP(TK8S_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+  TK8S_STEP(TK8S_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+  TK8S_STEP(TK8S_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+  TK8S_STEP(TK8S_I, c, d, a, b, m[10], 0xffeff47du, 15);
+  TK8S_STEP(TK8S_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+  TK8S_STEP(TK8S_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+  TK8S_STEP(TK8S_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+  TK8S_STEP(TK8S_I, c, d, a, b, m[6], 0xa3014314u, 15);
+  TK8S_STEP(TK8S_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+  TK8S_STEP(TK8S_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+  TK8S_STEP(TK8S_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+  TK8S_STEP(TK8S_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+  TK8S_STEP(TK8S_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+}
+
+#undef TK8S_F
+#undef TK8S_G
+#undef TK8S_H
+#undef TK8S_I
+#undef TK8S_STEP
+
+__device__ __forceinline__ void load_block(const u32x4* __restrict__ p, u32x4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = p[q];
+}
+
+__device__ __forceinline__ void unpack(const u32x4 (&v)[4], unsigned (&m)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    m[4 * q + 0] = v[q].x;
+    m[4 * q + 1] = v[q].y;
+    m[4 * q + 2] = v[q].z;
+    m[4 * q + 3] = v[q].w;
+  }
+}
+
+// Tail of a message: `rem` (< 64) bytes at p, total message length `len` bytes.
+// Byte loads only here (at most once per chunk, for the final partial chunk).
+__device__ void md5_finish(unsigned st[4], const unsigned char* __restrict__ p, unsigned rem,
+                           unsigned long long len) {
+  unsigned m[16];
+#pragma unroll
+  for (int w = 0; w < 16; ++w) m[w] = 0;
+  for (unsigned i = 0; i < rem; ++i) m[i >> 2] |= static_cast<unsigned>(p[i]) << (8 * (i & 3));
+  m[rem >> 2] |= 0x80u << (8 * (rem & 3));
+  const unsigned long long bits = len * 8ull;
+  if (rem >= 56) {
+    md5_compress(st, m);
+#pragma unroll
+    for (int w = 0; w < 16; ++w) m[w] = 0;
+  }
+  m[14] = static_cast<unsigned>(bits);
+  m[15] = static_cast<unsigned>(bits >> 32);
+  md5_compress(st, m);
+}
+
+__global__ __launch_bounds__(kMd5Block) void md5_chunks_kernel(const unsigned char* __restrict__ src,
+                                                              unsigned long long nbytes,
+                                                              unsigned chunk_bytes,
+                                                              unsigned long long nchunks,
+                                                              u32x4* __restrict__ digests) {
+  const unsigned long long c = static_cast<unsigned long long>(blockIdx.x) * kMd5Block + threadIdx.x;
+  if (c >= nchunks) return;
+  const unsigned long long start = c * chunk_bytes;
+  const unsigned long long left = nbytes > start ? nbytes - start : 0;
+  const unsigned long long len = left < chunk_bytes ? left : chunk_bytes;
+  unsigned st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+
+  const unsigned nfull = static_cast<unsigned>(len >> 6);
+  const u32x4* blk = reinterpret_cast<const u32x4*>(src + start);
+  if (nfull) {
+    u32x4 cur[4], nxt[4];
+    load_block(blk, cur);
+    for (unsigned b = 0; b < nfull; ++b) {
+      if (b + 1 < nfull) load_block(blk + 4 * (b + 1), nxt);
+      unsigned m[16];
+      unpack(cur, m);
+      md5_compress(st, m);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    }
+  }
+  md5_finish(st, src + start + (static_cast<unsigned long long>(nfull) << 6),
+             static_cast<unsigned>(len & 63), len);
+  digests[c] = u32x4{st[0], st[1], st[2], st[3]};
+}
+
+static unsigned long long n_chunks(size_t nbytes, uint32_t chunk_bytes) {
+  return nbytes == 0 ? 1ull : (nbytes + chunk_bytes - 1) / chunk_bytes;
+}
+
+void md5_chunks(const void* src, size_t nbytes, uint32_t chunk_bytes, void* digests,
+                hipStream_t stream) {
+  if (chunk_bytes == 0 || chunk_bytes % 64)
+    throw std::invalid_argument("md5_chunks: chunk_bytes must be a positive multiple of 64");
+  if (reinterpret_cast<uintptr_t>(src) % 16)
+    throw std::invalid_argument("md5_chunks: src must be 16-byte aligned");
+  const unsigned long long nchunks = n_chunks(nbytes, chunk_bytes);
+  const unsigned grid = static_cast<unsigned>((nchunks + kMd5Block - 1) / kMd5Block);
+  hipLaunchKernelGGL(md5_chunks_kernel, dim3(grid), dim3(kMd5Block), 0, stream,
+                     static_cast<const unsigned char*>(src), static_cast<unsigned long long>(nbytes),
+                     chunk_bytes, nchunks, static_cast<u32x4*>(digests));
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+size_t md5_tree_workspace(size_t nbytes, uint32_t chunk_bytes) {
+  if (chunk_bytes == 0 || chunk_bytes % 64)
+    throw std::invalid_argument("md5_tree_workspace: chunk_bytes must be a positive multiple of 64");
+  return static_cast<size_t>(n_chunks(nbytes, chunk_bytes)) * 16;
+}
+
+void md5_tree(const void* src, size_t nbytes, uint32_t chunk_bytes, void* ws_a, void* ws_b,
+              void* out16, hipStream_t stream) {
+  const void* in = src;
+  size_t n = nbytes;
+  void* bufs[2] = {ws_a, ws_b};
+  for (int level = 0;; ++level) {
+    const unsigned long long nchunks = n_chunks(n, chunk_bytes);
+    void* dst = nchunks == 1 ? out16 : bufs[level & 1];
+    md5_chunks(in, n, chunk_bytes, dst, stream);
+    if (nchunks == 1) return;
+    in = dst;
+    n = static_cast<size_t>(nchunks) * 16;
+  }
+}
+
+}  // namespace tk8s

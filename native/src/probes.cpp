@@ -1,0 +1,280 @@
+// Node-validation probes (N1 gpuinfo, N4 HBM write, N5 MD5 tree, N7 copy/xGMI). Host code;
+// compiled with hipcc and linked against the kernels in stream_kernels.hip / md5_kernels.hip.
+#include "tk8s/probes.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "tk8s/common.h"
+
+namespace tk8s {
+
+namespace {
+
+std::string hex(const unsigned char* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (size_t i = 0; i < n; ++i) {
+    s += d[p[i] >> 4];
+    s += d[p[i] & 15];
+  }
+  return s;
+}
+
+std::string link_type_name(uint32_t t) {
+  switch (t) {
+    case 0: return "hypertransport";
+    case 1: return "qpi";
+    case 2: return "pcie";
+    case 3: return "infiniband";
+    case 4: return "xgmi";
+    default: return "unknown";
+  }
+}
+
+std::string error_json(const std::string& what) {
+  return Json().kv("ok", false).kv("error", what).str();
+}
+
+struct DeviceGuard {
+  int prev = 0;
+  explicit DeviceGuard(int dev) {
+    TK8S_HIP_CHECK(hipGetDevice(&prev));
+    TK8S_HIP_CHECK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+struct Stream {
+  hipStream_t s{};
+  Stream() { TK8S_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
+  ~Stream() { (void)hipStreamDestroy(s); }
+};
+
+}  // namespace
+
+std::string gpuinfo_json(bool with_links) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    return Json()
+        .kv("ok", false)
+        .kv("device_count", 0)
+        .kv("error", std::string("hipGetDeviceCount: ") + hipGetErrorString(e))
+        .str();
+  }
+  int rt = 0, drv = 0;
+  (void)hipRuntimeGetVersion(&rt);
+  (void)hipDriverGetVersion(&drv);
+  std::vector<std::string> devs;
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
+    char bdf[64] = {0};
+    (void)hipDeviceGetPCIBusId(bdf, sizeof bdf, i);
+    hipUUID uuid;
+    std::memset(&uuid, 0, sizeof uuid);
+    (void)hipDeviceGetUuid(&uuid, i);
+    std::string arch = p.gcnArchName;
+    const std::string gfx = arch.substr(0, arch.find(':'));
+    devs.push_back(Json()
+                       .kv("index", i)
+                       .kv("name", std::string(p.name))
+                       .kv("arch", arch)
+                       .kv("gfx", gfx)
+                       .kv("total_mem_bytes", static_cast<uint64_t>(p.totalGlobalMem))
+                       .kv("cu_count", p.multiProcessorCount)
+                       .kv("clock_khz", p.clockRate)
+                       .kv("mem_clock_khz", p.memoryClockRate)
+                       .kv("mem_bus_width", p.memoryBusWidth)
+                       .kv("wavefront_size", p.warpSize)
+                       .kv("lds_per_block_bytes", static_cast<uint64_t>(p.sharedMemPerBlock))
+                       .kv("pci_bus_id", std::string(bdf))
+                       .kv("uuid", hex(reinterpret_cast<const unsigned char*>(uuid.bytes), 16))
+                       .str());
+  }
+  std::vector<std::string> rows;
+  if (with_links) {
+    for (int i = 0; i < n; ++i) {
+      std::vector<std::string> row;
+      for (int j = 0; j < n; ++j) {
+        if (i == j) {
+          row.push_back(Json().kv("type", "self").kv("hops", 0).kv("p2p", true).str());
+          continue;
+        }
+        uint32_t type = 0, hops = 0;
+        const bool ok = hipExtGetLinkTypeAndHopCount(i, j, &type, &hops) == hipSuccess;
+        int can = 0;
+        (void)hipDeviceCanAccessPeer(&can, i, j);
+        row.push_back(Json()
+                          .kv("type", ok ? link_type_name(type) : std::string("unknown"))
+                          .kv("hops", static_cast<int>(ok ? hops : 0))
+                          .kv("p2p", can != 0)
+                          .str());
+      }
+      rows.push_back(Json::array(row));
+    }
+  }
+  const double ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  Json j;
+  j.kv("ok", true)
+      .kv("device_count", n)
+      .kv("runtime_version", rt)
+      .kv("driver_version", drv)
+      .raw("devices", Json::array(devs));
+  if (with_links) j.raw("links", Json::array(rows));
+  j.kv("discovery_ms", ms);
+  return j.str();
+}
+
+std::string hbm_write_probe(size_t bytes, int iters, StoreMode mode, int device, uint32_t value) {
+  try {
+    if (bytes % 16 || bytes == 0) return error_json("bytes must be a positive multiple of 16");
+    iters = std::max(iters, 1);
+    DeviceGuard g(device);
+    Stream st;
+    DeviceBuffer buf(bytes), bad(sizeof(unsigned long long));
+    EventTimer cold, warm;
+    cold.start(st.s);
+    hbm_fill(buf.get(), bytes, value ^ 0xFFFFFFFFu, mode, st.s);  // cold write (first touch)
+    cold.stop(st.s);
+    const float cold_ms = cold.elapsed_ms();
+    warm.start(st.s);
+    for (int i = 0; i < iters; ++i) hbm_fill(buf.get(), bytes, value, mode, st.s);
+    warm.stop(st.s);
+    const float ms = warm.elapsed_ms() / iters;
+    TK8S_HIP_CHECK(hipMemsetAsync(bad.get(), 0, sizeof(unsigned long long), st.s));
+    verify_fill(buf.get(), bytes, value, bad.as<unsigned long long>(), st.s);
+    unsigned long long nbad = 0;
+    TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad.get(), sizeof nbad, hipMemcpyDeviceToHost, st.s));
+    TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
+    return Json()
+        .kv("ok", nbad == 0)
+        .kv("probe", "hbm_write")
+        .kv("device", device)
+        .kv("bytes", static_cast<uint64_t>(bytes))
+        .kv("iters", iters)
+        .kv("mode", mode == StoreMode::kNonTemporal ? "nontemporal" : "plain")
+        .kv("cold_ms", static_cast<double>(cold_ms))
+        .kv("ms", static_cast<double>(ms))
+        .kv("seconds", ms * 1e-3)
+        .kv("gbps", bytes / (ms * 1e-3) / 1e9)
+        .kv("bad_words", static_cast<uint64_t>(nbad))
+        .str();
+  } catch (const std::exception& ex) {
+    return error_json(ex.what());
+  }
+}
+
+std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int iters, int device) {
+  try {
+    if (bytes % 16) return error_json("bytes must be a multiple of 16");
+    if (chunk_bytes == 0 || chunk_bytes % 64) return error_json("chunk must be a multiple of 64");
+    iters = std::max(iters, 1);
+    DeviceGuard g(device);
+    Stream st;
+    const size_t ws = md5_tree_workspace(bytes, chunk_bytes);
+    DeviceBuffer data(std::max<size_t>(bytes, 16)), wa(ws), wb(ws), out(16);
+    EventTimer fill_t, cold_t, warm_t;
+    fill_t.start(st.s);
+    philox_fill(data.get(), bytes, seed, st.s);
+    fill_t.stop(st.s);
+    const float fill_ms = fill_t.elapsed_ms();
+    cold_t.start(st.s);
+    md5_tree(data.get(), bytes, chunk_bytes, wa.get(), wb.get(), out.get(), st.s);
+    cold_t.stop(st.s);
+    const float cold_ms = cold_t.elapsed_ms();
+    warm_t.start(st.s);
+    for (int i = 0; i < iters; ++i)
+      md5_tree(data.get(), bytes, chunk_bytes, wa.get(), wb.get(), out.get(), st.s);
+    warm_t.stop(st.s);
+    const float ms = warm_t.elapsed_ms() / iters;
+    unsigned char digest[16];
+    TK8S_HIP_CHECK(hipMemcpyAsync(digest, out.get(), 16, hipMemcpyDeviceToHost, st.s));
+    TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
+    return Json()
+        .kv("ok", true)
+        .kv("probe", "md5_tree")
+        .kv("device", device)
+        .kv("bytes", static_cast<uint64_t>(bytes))
+        .kv("chunk_bytes", chunk_bytes)
+        .kv("seed", static_cast<uint64_t>(seed))
+        .kv("iters", iters)
+        .kv("digest", hex(digest, 16))
+        .kv("fill_ms", static_cast<double>(fill_ms))
+        .kv("fill_gbps", bytes / (fill_ms * 1e-3) / 1e9)
+        .kv("cold_ms", static_cast<double>(cold_ms))
+        .kv("ms", static_cast<double>(ms))
+        .kv("seconds", ms * 1e-3)
+        .kv("mbps", bytes / (ms * 1e-3) / 1e6)
+        .str();
+  } catch (const std::exception& ex) {
+    return error_json(ex.what());
+  }
+}
+
+std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters) {
+  try {
+    if (bytes % 16 || bytes == 0) return error_json("bytes must be a positive multiple of 16");
+    iters = std::max(iters, 1);
+    const bool peer = src_device != dst_device;
+    int can = 1;
+    if (peer) {
+      TK8S_HIP_CHECK(hipDeviceCanAccessPeer(&can, dst_device, src_device));
+      if (!can) return error_json("no peer access from dst to src");
+    }
+    DeviceBuffer* src_buf = nullptr;
+    {
+      DeviceGuard g(src_device);
+      src_buf = new DeviceBuffer(bytes);
+      hbm_fill(src_buf->get(), bytes, 0xA5A5A5A5u, StoreMode::kPlain, nullptr);
+      TK8S_HIP_CHECK(hipDeviceSynchronize());
+    }
+    std::unique_ptr<DeviceBuffer> src_owner(src_buf);
+    DeviceGuard g(dst_device);
+    if (peer) {
+      const hipError_t pe = hipDeviceEnablePeerAccess(src_device, 0);
+      if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) TK8S_HIP_CHECK(pe);
+      (void)hipGetLastError();
+    }
+    Stream st;
+    DeviceBuffer dst(bytes), bad(sizeof(unsigned long long));
+    stream_copy(dst.get(), src_buf->get(), bytes, st.s);  // warm-up
+    EventTimer kt, dt;
+    kt.start(st.s);
+    for (int i = 0; i < iters; ++i) stream_copy(dst.get(), src_buf->get(), bytes, st.s);
+    kt.stop(st.s);
+    const float kernel_ms = kt.elapsed_ms() / iters;
+    TK8S_HIP_CHECK(hipMemsetAsync(bad.get(), 0, sizeof(unsigned long long), st.s));
+    verify_fill(dst.get(), bytes, 0xA5A5A5A5u, bad.as<unsigned long long>(), st.s);
+    unsigned long long nbad = 0;
+    TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad.get(), sizeof nbad, hipMemcpyDeviceToHost, st.s));
+    dt.start(st.s);
+    for (int i = 0; i < iters; ++i)
+      TK8S_HIP_CHECK(hipMemcpyPeerAsync(dst.get(), dst_device, src_buf->get(), src_device, bytes, st.s));
+    dt.stop(st.s);
+    const float dma_ms = dt.elapsed_ms() / iters;
+    return Json()
+        .kv("ok", nbad == 0)
+        .kv("probe", peer ? "xgmi_peer_copy" : "local_copy")
+        .kv("src_device", src_device)
+        .kv("dst_device", dst_device)
+        .kv("bytes", static_cast<uint64_t>(bytes))
+        .kv("iters", iters)
+        .kv("kernel_ms", static_cast<double>(kernel_ms))
+        .kv("kernel_gbps", bytes / (kernel_ms * 1e-3) / 1e9)
+        .kv("dma_ms", static_cast<double>(dma_ms))
+        .kv("dma_gbps", bytes / (dma_ms * 1e-3) / 1e9)
+        .kv("bad_words", static_cast<uint64_t>(nbad))
+        .str();
+  } catch (const std::exception& ex) {
+    return error_json(ex.what());
+  }
+}
+
+}  // namespace tk8s

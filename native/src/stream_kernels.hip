@@ -1,0 +1,290 @@
+// Streaming validation kernels for gfx950 (CDNA4): HBM fill/verify (N4), Philox fill (N5 input),
+// copy (N7 local + xGMI peer pull), all-reduce fill/check (N6).
+//
+// Design notes (MI355X-first, see /opt/skills/guides):
+//  * 16 B per lane per access (global_{load,store}_dwordx4): 1 KiB per wave-instruction, the
+//    coalescing sweet spot (cdna_hip_programming.md Guideline 13).
+//  * Grid-stride loops over min(work, CUs x 8) 256-thread workgroups (Guideline 11): enough
+//    waves to cover HBM latency on all 256 CUs / 8 XCDs without launch-overhead blow-up.
+//  * 4-way unrolled stores so each wave keeps several 1 KiB stores in flight.
+//  * Non-temporal stores for the once-written 1 GiB fill (no reason to pollute L2/MALL).
+//  * Reductions: wave64 __shfl_xor butterfly -> LDS across the 4 waves -> ONE atomic per block
+//    (Guideline 12).
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
+
+#include "tk8s/common.h"
+#include "tk8s/kernels.h"
+
+namespace tk8s {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBlock = 256;  // 4 wave64s
+constexpr int kWaves = kBlock / 64;
+
+int streaming_grid(int blocks_per_cu) {
+  static std::mutex mu;
+  static std::vector<int> cu_count;
+  int dev = 0;
+  TK8S_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  if (static_cast<int>(cu_count.size()) <= dev) cu_count.resize(dev + 1, 0);
+  if (cu_count[dev] == 0) {
+    int cus = 0;
+    TK8S_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    cu_count[dev] = cus > 0 ? cus : 1;
+  }
+  return cu_count[dev] * blocks_per_cu;
+}
+
+static unsigned grid_for(size_t items, int blocks_per_cu = 8) {
+  size_t need = (items + kBlock - 1) / kBlock;
+  size_t cap = static_cast<size_t>(streaming_grid(blocks_per_cu));
+  size_t g = need < cap ? need : cap;
+  return static_cast<unsigned>(g ? g : 1);
+}
+
+// ------------------------------------------------------------------------------------------
+// N4: HBM fill
+// ------------------------------------------------------------------------------------------
+template <bool kNT>
+__global__ __launch_bounds__(kBlock) void hbm_fill_kernel(u32x4* __restrict__ dst, size_t n16,
+                                                          unsigned value) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const u32x4 v = {value, value, value, value};
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if constexpr (kNT) __builtin_nontemporal_store(v, dst + i + u * stride);
+      else dst[i + u * stride] = v;
+    }
+  }
+  for (; i < n16; i += stride) {
+    if constexpr (kNT) __builtin_nontemporal_store(v, dst + i);
+    else dst[i] = v;
+  }
+}
+
+void hbm_fill(void* dst, size_t nbytes, uint32_t value, StoreMode mode, hipStream_t stream) {
+  if (nbytes % 16) throw std::invalid_argument("hbm_fill: nbytes must be a multiple of 16");
+  const size_t n16 = nbytes / 16;
+  if (!n16) return;
+  const unsigned grid = grid_for(n16);
+  if (mode == StoreMode::kNonTemporal)
+    hipLaunchKernelGGL(hbm_fill_kernel<true>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<u32x4*>(dst), n16, value);
+  else
+    hipLaunchKernelGGL(hbm_fill_kernel<false>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<u32x4*>(dst), n16, value);
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void verify_fill_kernel(const u32x4* __restrict__ src,
+                                                             size_t n16, unsigned value,
+                                                             unsigned long long* bad_words) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  unsigned long long bad = 0;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += stride) {
+    const u32x4 v = src[i];
+    bad += (v.x != value) + (v.y != value) + (v.z != value) + (v.w != value);
+  }
+  __shared__ unsigned long long part[kWaves];
+  bad = wave_sum_u64(bad);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) part[wid] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += part[w];
+    if (s) atomicAdd(bad_words, s);
+  }
+}
+
+void verify_fill(const void* src, size_t nbytes, uint32_t value, unsigned long long* bad_words,
+                 hipStream_t stream) {
+  if (nbytes % 16) throw std::invalid_argument("verify_fill: nbytes must be a multiple of 16");
+  const size_t n16 = nbytes / 16;
+  if (!n16) return;
+  hipLaunchKernelGGL(verify_fill_kernel, dim3(grid_for(n16)), dim3(kBlock), 0, stream,
+                     static_cast<const u32x4*>(src), n16, value, bad_words);
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// N5 input: Philox4x32-10 (Salmon et al., Random123). Counter = (block index lo, hi, 0, 0),
+// key = (seed lo, seed hi). Bit-identical host reference: tritonk8ssupervisor_amd/ops/reference.py
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ u32x4 philox4x32_10(unsigned long long idx, unsigned k0, unsigned k1) {
+  unsigned c0 = static_cast<unsigned>(idx), c1 = static_cast<unsigned>(idx >> 32), c2 = 0, c3 = 0;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const unsigned lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const unsigned lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const unsigned n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  return u32x4{c0, c1, c2, c3};
+}
+
+__global__ __launch_bounds__(kBlock) void philox_fill_kernel(u32x4* __restrict__ dst, size_t n16,
+                                                             unsigned k0, unsigned k1) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += stride)
+    dst[i] = philox4x32_10(i, k0, k1);
+}
+
+void philox_fill(void* dst, size_t nbytes, uint64_t seed, hipStream_t stream) {
+  if (nbytes % 16) throw std::invalid_argument("philox_fill: nbytes must be a multiple of 16");
+  const size_t n16 = nbytes / 16;
+  if (!n16) return;
+  hipLaunchKernelGGL(philox_fill_kernel, dim3(grid_for(n16)), dim3(kBlock), 0, stream,
+                     static_cast<u32x4*>(dst), n16, static_cast<unsigned>(seed),
+                     static_cast<unsigned>(seed >> 32));
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// N7: copy (local D2D, or peer pull when src is another GPU's memory with peer access enabled)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void stream_copy_kernel(u32x4* __restrict__ dst,
+                                                             const u32x4* __restrict__ src,
+                                                             size_t n16) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+void stream_copy(void* dst, const void* src, size_t nbytes, hipStream_t stream) {
+  if (nbytes % 16) throw std::invalid_argument("stream_copy: nbytes must be a multiple of 16");
+  const size_t n16 = nbytes / 16;
+  if (!n16) return;
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(grid_for(n16)), dim3(kBlock), 0, stream,
+                     static_cast<u32x4*>(dst), static_cast<const u32x4*>(src), n16);
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// N6: all-reduce pattern + checker. Values are small integers, exact in f32 and bf16 for
+// nranks <= 16, so any |err| > 0 is a real transport/reduction error.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float bf16_bits_to_f32(unsigned short h) {
+  return __uint_as_float(static_cast<unsigned>(h) << 16);
+}
+__device__ __forceinline__ unsigned short f32_to_bf16_bits(float f) {
+  const unsigned u = __float_as_uint(f);
+  return static_cast<unsigned short>((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void ar_fill_kernel(T* __restrict__ buf, size_t count,
+                                                         float base) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
+    const float v = base + static_cast<float>(i % 7);
+    if constexpr (sizeof(T) == 4) buf[i] = v;
+    else buf[i] = f32_to_bf16_bits(v);
+  }
+}
+
+void ar_fill(void* buf, size_t count, int rank, DType dtype, hipStream_t stream) {
+  if (!count) return;
+  const unsigned grid = grid_for(count);
+  const float base = static_cast<float>(rank + 1);
+  if (dtype == DType::kF32)
+    hipLaunchKernelGGL(ar_fill_kernel<float>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<float*>(buf), count, base);
+  else
+    hipLaunchKernelGGL(ar_fill_kernel<unsigned short>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<unsigned short*>(buf), count, base);
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+template <class T>
+__global__ __launch_bounds__(kBlock) void ar_check_kernel(const T* __restrict__ buf, size_t count,
+                                                          float base, float per_mod, float tol,
+                                                          unsigned* max_err_bits,
+                                                          unsigned long long* bad_count) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  float emax = 0.f;
+  unsigned long long bad = 0;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
+    float v;
+    if constexpr (sizeof(T) == 4) v = buf[i];
+    else v = bf16_bits_to_f32(buf[i]);
+    const float expect = base + per_mod * static_cast<float>(i % 7);
+    float e = fabsf(v - expect);
+    if (!(e == e)) e = __int_as_float(0x7f800000);  // NaN -> +inf so it wins the max
+    emax = fmaxf(emax, e);
+    bad += e > tol;
+  }
+  __shared__ float pmax[kWaves];
+  __shared__ unsigned long long pbad[kWaves];
+  emax = wave_max_f32(emax);
+  bad = wave_sum_u64(bad);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    pmax[wid] = emax;
+    pbad[wid] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = 0.f;
+    unsigned long long b = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      m = fmaxf(m, pmax[w]);
+      b += pbad[w];
+    }
+    // Non-negative floats order like their bit patterns.
+    atomicMax(max_err_bits, __float_as_uint(m));
+    if (b) atomicAdd(bad_count, b);
+  }
+}
+
+void ar_check(const void* buf, size_t count, int nranks, DType dtype, float tol,
+              unsigned int* max_err_bits, unsigned long long* bad, hipStream_t stream) {
+  if (!count) return;
+  const unsigned grid = grid_for(count);
+  const float base = 0.5f * static_cast<float>(nranks) * static_cast<float>(nranks + 1);
+  const float per_mod = static_cast<float>(nranks);
+  if (dtype == DType::kF32)
+    hipLaunchKernelGGL(ar_check_kernel<float>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<const float*>(buf), count, base, per_mod, tol, max_err_bits, bad);
+  else
+    hipLaunchKernelGGL(ar_check_kernel<unsigned short>, dim3(grid), dim3(kBlock), 0, stream,
+                       static_cast<const unsigned short*>(buf), count, base, per_mod, tol,
+                       max_err_bits, bad);
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace tk8s

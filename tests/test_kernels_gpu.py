@@ -1,0 +1,124 @@
+"""Numerics of the gfx950 HIP kernels against exact host / PyTorch fp32 references (GPU only)."""
+import json
+
+import numpy as np
+import pytest
+
+from tritonk8ssupervisor_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def nat(native_build):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tritonk8ssupervisor_amd.ops import native
+
+    return native()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def test_gpuinfo_reports_gfx950(nat):
+    info = json.loads(nat.gpuinfo_json(True))
+    assert info["ok"] and info["device_count"] >= 1
+    d0 = info["devices"][0]
+    assert d0["gfx"] == "gfx950"
+    assert d0["wavefront_size"] == 64
+    assert d0["cu_count"] >= 256
+    assert d0["total_mem_bytes"] > 250 * 2**30
+    assert len(info["links"]) == info["device_count"]
+
+
+@pytest.mark.parametrize("nbytes", [16, 4096, 3 * 2**20 + 48])
+def test_philox_fill_matches_host(nat, nbytes):
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    nat.philox_fill(buf.data_ptr(), nbytes, 0x1234_5678_9ABC, _stream())
+    torch.cuda.synchronize()
+    assert bytes(buf.cpu().numpy()) == ref.philox_bytes(nbytes, 0x1234_5678_9ABC)
+
+
+@pytest.mark.parametrize("nbytes,chunk", [(0, 1024), (16, 1024), (1024, 1024), (1040, 1024),
+                                          (70000 * 16, 1024), (2**20, 256), (5 * 2**20 + 32, 4096)])
+def test_md5_tree_matches_hashlib(nat, nbytes, chunk):
+    data = ref.philox_bytes(nbytes, seed=11) if nbytes else b""
+    src = torch.frombuffer(bytearray(data) or bytearray(16), dtype=torch.uint8).cuda()
+    ws = max(nat.md5_tree_workspace(nbytes, chunk), 16)
+    wa = torch.empty(ws, dtype=torch.uint8, device="cuda")
+    wb = torch.empty(ws, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    nat.md5_tree(src.data_ptr(), nbytes, chunk, wa.data_ptr(), wb.data_ptr(), out.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert bytes(out.cpu().numpy()) == ref.md5_tree(data, chunk)
+
+
+@pytest.mark.parametrize("mode", ["nontemporal", "plain"])
+def test_hbm_fill_and_verify(nat, mode):
+    n = 64 * 2**20 + 16 * 5
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    nat.hbm_fill(buf.data_ptr(), n, 0xDEADBEEF, mode, _stream())
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    nat.verify_fill(buf.data_ptr(), n, 0xDEADBEEF, bad.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    words = buf.view(torch.int32).cpu().numpy().view(np.uint32)
+    assert (words == 0xDEADBEEF).all()
+    assert int(bad.item()) == 0
+    # verify must catch a corrupted word
+    buf[4096:4100] = 0
+    nat.verify_fill(buf.data_ptr(), n, 0xDEADBEEF, bad.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 1
+
+
+@pytest.mark.parametrize("dtype,tdt", [("float32", torch.float32), ("bfloat16", torch.bfloat16)])
+def test_allreduce_fill_and_check_vs_torch(nat, dtype, tdt):
+    count, nranks = 1_000_003, 8
+    bufs = []
+    for r in range(nranks):
+        b = torch.empty(count, dtype=tdt, device="cuda")
+        nat.ar_fill(b.data_ptr(), count, r, dtype, _stream())
+        bufs.append(b)
+    total = torch.stack([b.float() for b in bufs]).sum(0)  # plain PyTorch fp32 reduction
+    expect = torch.from_numpy(ref.allreduce_expected(count, nranks)).cuda()
+    assert torch.equal(total, expect)
+    summed = total.to(tdt)
+    stats = torch.zeros(2, dtype=torch.int64, device="cuda")
+    nat.ar_check(summed.data_ptr(), count, nranks, dtype, 0.0, stats.data_ptr(), stats.data_ptr() + 8, _stream())
+    torch.cuda.synchronize()
+    assert int(stats[1].item()) == 0 and int(stats[0].item()) == 0
+    summed[12345] += 4
+    stats.zero_()
+    nat.ar_check(summed.data_ptr(), count, nranks, dtype, 0.0, stats.data_ptr(), stats.data_ptr() + 8, _stream())
+    torch.cuda.synchronize()
+    max_err = np.array([int(stats[0].item())], dtype=np.uint64).astype(np.uint32).view(np.float32)[0]
+    assert int(stats[1].item()) == 1 and max_err == pytest.approx(4.0)
+
+
+def test_stream_copy_matches_torch(nat):
+    n = 32 * 2**20
+    src = torch.randint(0, 255, (n,), dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    nat.stream_copy(dst.data_ptr(), src.data_ptr(), n, _stream())
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+
+
+def test_probes_json(nat):
+    h = json.loads(nat.hbm_write_probe(256 * 2**20, 3, "nontemporal", 0, 0))
+    assert h["ok"] and h["bad_words"] == 0 and h["gbps"] > 500
+    m = json.loads(nat.md5_probe(16 * 2**20, 1024, 5, 2, 0))
+    assert m["ok"]
+    assert m["digest"] == ref.md5_tree(ref.philox_bytes(16 * 2**20, 5), 1024).hex()
+    c = json.loads(nat.copy_probe(0, 0, 64 * 2**20, 3))
+    assert c["ok"] and c["kernel_gbps"] > 100
+
+
+def test_rccl_single_gpu(nat):
+    r = json.loads(nat.rccl_allreduce([0], 8, 1 << 20, 16, 3, 1, "float32", True))
+    assert r["ok"], r
+    assert r["nranks"] == 1 and all(x["bad"] == 0 for x in r["results"])

@@ -1,0 +1,171 @@
+"""In-tree build of the tk8s native layer for gfx950 (MI355X).
+
+Outputs (all in-tree so they travel to the GPU box with the repo snapshot):
+
+* ``tritonk8ssupervisor_amd/lib/libtk8s.so`` — HIP kernels (N4-N7), probes (N1) and the RCCL
+  validator (N3); links ``libamdhip64`` and ``librccl``.
+* ``tritonk8ssupervisor_amd/_tk8s_native*.so`` — pybind11 module over ``libtk8s.so``.
+* ``tritonk8ssupervisor_amd/_tk8s_topo*.so`` — pybind11 module of the CPU-only xGMI-aware
+  allocator (N2 core); no HIP dependency so the node agent can load it safely.
+* ``tritonk8ssupervisor_amd/bin/tk8s-{gpuinfo,probe,rccl}`` — the validation pod payloads.
+
+The reference has no native code at all; this build replaces nothing there.
+Incremental: an output is rebuilt when any of its inputs or any header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[2]
+PKG = REPO / "tritonk8ssupervisor_amd"
+NATIVE = REPO / "native"
+OBJ = REPO / "build" / "native"
+LIBDIR = PKG / "lib"
+BINDIR = PKG / "bin"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+HIPCC = str(ROCM / "bin" / "hipcc")
+CXX = shutil.which("g++") or "c++"
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", f"-I{NATIVE / 'include'}", "-Wall", "-Wno-unused-result"]
+HIP_FLAGS = COMMON + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+
+LIB_SOURCES = [
+    "src/stream_kernels.hip",
+    "src/md5_kernels.hip",
+    "src/probes.cpp",
+    "src/rccl_bench.cpp",
+]
+TOOLS = {
+    "tk8s-gpuinfo": "tools/tk8s_gpuinfo.cpp",
+    "tk8s-probe": "tools/tk8s_probe.cpp",
+    "tk8s-rccl": "tools/tk8s_rccl.cpp",
+}
+
+
+def ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def native_module_path() -> Path:
+    return PKG / f"_tk8s_native{ext_suffix()}"
+
+
+def topo_module_path() -> Path:
+    return PKG / f"_tk8s_topo{ext_suffix()}"
+
+
+def lib_path() -> Path:
+    return LIBDIR / "libtk8s.so"
+
+
+def tool_path(name: str) -> Path:
+    return BINDIR / name
+
+
+def _headers() -> list[Path]:
+    return sorted((NATIVE / "include").rglob("*.h")) + sorted((NATIVE / "tools").glob("*.h"))
+
+
+def _stale(out: Path, inputs: list[Path]) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(p.stat().st_mtime > t for p in inputs + _headers())
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print("+", " ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"native build failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+
+
+def _pybind_includes() -> list[str]:
+    import pybind11  # noqa: PLC0415 (build-time only)
+
+    return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> dict:
+    """Compile everything; returns {name: path} of the produced artefacts."""
+    OBJ.mkdir(parents=True, exist_ok=True)
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    BINDIR.mkdir(parents=True, exist_ok=True)
+    jobs = jobs or min(8, os.cpu_count() or 4)
+
+    # 1. objects of libtk8s.so (hipcc, gfx950 device code)
+    objs: list[tuple[Path, list[str]]] = []
+    for rel in LIB_SOURCES:
+        src = NATIVE / rel
+        obj = OBJ / (src.stem + src.suffix.replace(".", "_") + ".o")
+        if force or _stale(obj, [src]):
+            objs.append((obj, [HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)]))
+    # tool objects and module objects compile in the same pool
+    tool_objs = {}
+    for name, rel in TOOLS.items():
+        src = NATIVE / rel
+        obj = OBJ / (src.stem + ".o")
+        tool_objs[name] = obj
+        if force or _stale(obj, [src]):
+            objs.append((obj, [HIPCC, *COMMON, "-c", str(src), "-o", str(obj)]))
+    py_inc = _pybind_includes()
+    nat_obj = OBJ / "native_module.o"
+    nat_src = NATIVE / "bindings" / "native_module.cpp"
+    if force or _stale(nat_obj, [nat_src]):
+        objs.append((nat_obj, [HIPCC, *COMMON, *py_inc, "-fvisibility=hidden", "-c", str(nat_src), "-o", str(nat_obj)]))
+    topo_srcs = [NATIVE / "src" / "topology.cpp", NATIVE / "bindings" / "topo_module.cpp"]
+    topo_objs = [OBJ / (s.stem + "_topo.o") for s in topo_srcs]
+    for s, o in zip(topo_srcs, topo_objs):
+        if force or _stale(o, [s]):
+            objs.append((o, [CXX, *COMMON, *py_inc, "-fvisibility=hidden", "-c", str(s), "-o", str(o)]))
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(lambda oc: _run(oc[1], verbose), objs))
+
+    lib_objs = [OBJ / (Path(r).stem + Path(r).suffix.replace(".", "_") + ".o") for r in LIB_SOURCES]
+    hip_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
+    lib = lib_path()
+    if force or _stale(lib, lib_objs):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *[str(o) for o in lib_objs],
+              "-o", str(lib), *hip_libs], verbose)
+
+    links = []
+    nat = native_module_path()
+    if force or _stale(nat, [nat_obj, lib]):
+        links.append([HIPCC, "-shared", "-fPIC", str(nat_obj), "-o", str(nat), f"-L{LIBDIR}", "-ltk8s",
+                      "-Wl,-rpath,$ORIGIN/lib", *hip_libs])
+    topo = topo_module_path()
+    if force or _stale(topo, topo_objs):
+        links.append([CXX, "-shared", "-fPIC", *[str(o) for o in topo_objs], "-o", str(topo)])
+    for name, obj in tool_objs.items():
+        out = tool_path(name)
+        if force or _stale(out, [obj, lib]):
+            links.append([HIPCC, str(obj), "-o", str(out), f"-L{LIBDIR}", "-ltk8s",
+                          "-Wl,-rpath,$ORIGIN/../lib", *hip_libs, "-lpthread"])
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(lambda c: _run(c, verbose), links))
+
+    out = {"libtk8s": lib, "native_module": nat, "topo_module": topo}
+    out.update({n: tool_path(n) for n in TOOLS})
+    return out
+
+
+def main(argv: list[str] | None = None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    res = build(force="--force" in argv, verbose="-v" in argv)
+    for k, v in res.items():
+        print(f"{k}: {v}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
