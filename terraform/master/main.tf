@@ -1,0 +1,37 @@
+# One master machine. Engine: tritonk8ssupervisor_amd/provision.py (Terraform-compatible subset).
+# resource type tk8s_machine is served by the provider configured in rancher.tf
+# (provider "local" = a worker sandbox + loopback IP + GPU slice on this MI355X host,
+#  provider "triton" = a Triton KVM as in the reference).
+resource "tk8s_machine" "master" {
+  name    = "${var.hostname}"
+  package = "${var.package}"
+  image   = "${var.image}"
+
+  networks             = "${var.networks}"
+  root_authorized_keys = "${var.root_authorized_keys}"
+
+  tags = {
+    name = "${var.hostname}"
+    role = "master"
+  }
+
+  # Bootstrap (reference: sleep 30; copy keys; apt-get install python-minimal). Here: check the
+  # sandbox layout and that the node runtime (python3 >= 3.8) is usable. No fixed sleeps.
+  provisioner "remote-exec" {
+    connection {
+      host = "${tk8s_machine.master.primaryip}"
+      user = "root"
+    }
+
+    inline = [
+      "test -d run && test -d logs && test -d pods",
+      "python3 -c 'import sys; sys.exit(0 if sys.version_info >= (3, 8) else 1)'",
+    ]
+  }
+
+  # Inventory hand-off to Ansible. The engine serialises local-exec and rewrites the file in
+  # module order after apply, so concurrent creates cannot reorder it.
+  provisioner "local-exec" {
+    command = "echo ${tk8s_machine.master.primaryip} >> masters.ip"
+  }
+}

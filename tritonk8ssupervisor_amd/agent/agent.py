@@ -1,0 +1,289 @@
+"""tk8s node agent: joins a worker to the control plane and runs its pods.
+
+Plays the part of ``rancher/agent`` + kubelet on every HOST (ansible/roles/rancherhost/tasks/
+main.yml:26-34 starts the agent with the registration URL as its only argument):
+
+  1. GET  <registrationUrl>          bootstrap (project, API prefix, heartbeat period)
+  2. device plugin discovery          sysfs only — the agent never initialises the GPU
+  3. POST <registrationUrl>          register the node (capacity incl. amd.com/gpu) -> node token
+  4. heartbeat thread                 PUT nodes/<name>/status every period (the node lease)
+  5. pod watch thread                 long-poll pods bound to this node; start/stop them via the
+                                      pod runtime with the device plugin's Allocate() env
+
+Fault points (utils/faults.py): ``agent.crash@<node>:N`` exits after registering, the first N
+times (counted in the sandbox, so a restarted agent sees the count); ``agent.no_heartbeat@<node>``
+stops heartbeats (lease expiry -> NotReady).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import platform
+import sys
+import threading
+import time
+from pathlib import Path
+
+from ..controlplane.client import ApiError, Client
+from ..utils.faults import fault
+from .deviceplugin import DevicePlugin
+from .runtime import PodProc, PodRuntime, install_sigterm
+
+GPU = "amd.com/gpu"
+ALL_GPUS = "tk8s.amd.com/all-gpus"
+VALIDATION_LABEL = "tk8s.amd.com/validation"
+TERMINAL = ("Succeeded", "Failed")
+
+
+def pod_gpus(p: dict) -> int:
+    total = 0
+    for c in p.get("spec", {}).get("containers", []):
+        r = c.get("resources", {})
+        total += int(r.get("limits", {}).get(GPU, r.get("requests", {}).get(GPU, 0)) or 0)
+    return total
+
+
+class Agent:
+    def __init__(self, url: str, name: str, ip: str, sandbox: str, gpus: list[int],
+                 labels: dict | None = None, tool_dirs: list[str] | None = None, timeout: float = 60.0):
+        self.reg_url = url
+        self.name = name
+        self.ip = ip
+        self.sandbox = Path(sandbox)
+        self.labels = labels or {}
+        self.timeout = timeout
+        self.plugin = DevicePlugin(gpus)
+        self.runtime = PodRuntime(self.sandbox / "pods", self._on_status, tool_dirs)
+        self.api: Client | None = None
+        self.stop = threading.Event()
+        self.hb_period = 1.0
+        self._devices_dirty = False
+        self._pods_meta: dict[str, dict] = {}
+        scheme_rest = url.split("://", 1)[1]
+        self.base = "http://" + scheme_rest.split("/", 1)[0]
+        self.reg_path = "/" + scheme_rest.split("/", 1)[1]
+
+    # ---- join -------------------------------------------------------------------------
+    def join(self) -> None:
+        c = Client(self.base, timeout=10.0)
+        deadline = time.monotonic() + self.timeout
+        delay = 0.01
+        while True:
+            try:
+                boot = c.get(self.reg_path)
+                break
+            except (ApiError, OSError) as e:
+                if time.monotonic() > deadline:
+                    raise RuntimeError(f"{self.name}: control plane unreachable at {self.base}: {e}") from e
+                time.sleep(delay)
+                delay = min(delay * 2, 1.0)
+        cap = {"cpu": str(os.cpu_count() or 1), "pods": "110"}
+        try:
+            cap["memory"] = f"{os.sysconf('SC_PAGE_SIZE') * os.sysconf('SC_PHYS_PAGES') // 1024}Ki"
+        except (ValueError, OSError):
+            pass
+        body = {"name": self.name, "ip": self.ip, "capacity": cap, "labels": self.labels,
+                "devices": self.plugin.devices(),
+                "nodeInfo": {"osImage": platform.platform(), "kernelVersion": platform.release(),
+                             "architecture": platform.machine(), "containerRuntimeVersion": "tk8s-process://0.1",
+                             "kubeletVersion": "tk8s-agent/0.1", "gpuInventory": self.plugin.inventory.source}}
+        r = c.post(self.reg_path, body)
+        self.hb_period = float(r.get("heartbeatSeconds", boot.get("heartbeatSeconds", 1.0)))
+        self.api = Client(self.base, token=r["nodeToken"], prefix=r["apiPrefix"], timeout=10.0)
+        c.close()
+        n = fault("agent.crash", self.name)
+        if n is not None:
+            counter = self.sandbox / "run" / "crash.count"
+            count = int(counter.read_text()) if counter.exists() else 0
+            if count < (int(n) if n is not True else 1):
+                counter.parent.mkdir(parents=True, exist_ok=True)
+                counter.write_text(str(count + 1))
+                print(f"{self.name}: injected crash #{count + 1}", flush=True)
+                os._exit(17)
+
+    # ---- heartbeat --------------------------------------------------------------------
+    def heartbeat_loop(self) -> None:
+        api = Client(self.api.base, token=self.api.token, prefix=self.api.prefix, timeout=10.0)
+        last_health = time.monotonic()
+        while not self.stop.is_set():
+            if fault("agent.no_heartbeat", self.name) is None:
+                body = {}
+                if time.monotonic() - last_health > 10.0:
+                    last_health = time.monotonic()
+                    if self.plugin.refresh_health():
+                        self._devices_dirty = True
+                if self._devices_dirty:
+                    self._devices_dirty = False
+                    body["devices"] = self.plugin.devices()
+                try:
+                    api.put(api.k8s(f"/api/v1/nodes/{self.name}/status"), body)
+                except ApiError as e:
+                    if e.status in (401, 404):
+                        print(f"{self.name}: node unknown to control plane ({e}); exiting for restart", flush=True)
+                        os._exit(3)
+                except OSError:
+                    pass
+            self.stop.wait(self.hb_period)
+
+    # ---- pods -------------------------------------------------------------------------
+    def _free_devices(self) -> list[str]:
+        used = set()
+        for pp in self.runtime.running().values():
+            used.update(pp.gpu_ids)
+        return [d["id"] for d in self.plugin.devices() if d["health"] == "Healthy" and d["id"] not in used]
+
+    def _start_pod(self, pod: dict) -> None:
+        md, spec = pod["metadata"], pod["spec"]
+        key = f"{md['namespace']}/{md['name']}"
+        if key in self.runtime.running():
+            return
+        c = spec["containers"][0]
+        all_gpus = md.get("annotations", {}).get(ALL_GPUS) == "true"
+        need = len(self.plugin.devices()) if all_gpus else pod_gpus(pod)
+        free = self._free_devices()
+        pp_dir = self.sandbox / "pods" / md["name"]
+        if need > len(free):
+            self._report(key, md["name"], md["namespace"], "Failed",
+                         {"reason": "UnexpectedAdmissionError",
+                          "message": f"Allocate failed: requested {need} {GPU}, {len(free)} free"}, None)
+            return
+        ids = self.plugin.preferred(free, [], need) if need else []
+        alloc = self.plugin.allocate(ids) if ids else {"env": {}, "devices": [], "annotations": {}}
+        env = {k: v for k, v in os.environ.items() if not k.startswith("TK8S_FAULT")}
+        env.update(alloc["env"])
+        env.update({"POD_NAME": md["name"], "POD_NAMESPACE": md["namespace"], "POD_UID": md.get("uid", ""),
+                    "NODE_NAME": self.name, "NODE_IP": self.ip, "TK8S_API_URL": self.base,
+                    "TK8S_KV_URL": f"{self.base}/v1/kv", "TK8S_GPU_IDS": ",".join(ids),
+                    "TK8S_GPU_COUNT": str(len(ids))})
+        for e in c.get("env", []):
+            env[e["name"]] = _expand(str(e.get("value", "")), env)
+        argv = [_expand(str(x), env) for x in (c.get("command") or []) + (c.get("args") or [])]
+        if not argv:
+            self._report(key, md["name"], md["namespace"], "Failed", {"reason": "NoCommand",
+                                                                       "message": "container has no command"}, None)
+            return
+        pp = PodProc(key=key, uid=md.get("uid", ""), dir=pp_dir, argv=argv, env=env,
+                     restart_policy=spec.get("restartPolicy", "Always"), gpu_ids=ids)
+        self._pods_meta[key] = {"name": md["name"], "namespace": md["namespace"],
+                                "validation": md.get("labels", {}).get(VALIDATION_LABEL) == "true",
+                                "annotations": {**alloc["annotations"], "tk8s.amd.com/log-path": str(pp_dir / "log")}}
+        self.runtime.start(pp)
+
+    def _on_status(self, pp: PodProc, phase: str, extra: dict) -> None:
+        meta = self._pods_meta.get(pp.key, {})
+        result = extra.get("result")
+        if meta.get("validation") and phase in TERMINAL and isinstance(result, dict):
+            result["_allocated_ids"] = pp.gpu_ids
+            self.plugin.update_from_probe(result)
+            self._devices_dirty = True
+        self._report(pp.key, meta.get("name", pp.key.split("/")[1]), meta.get("namespace", "default"), phase, extra,
+                     pp, meta.get("annotations"))
+
+    def _report(self, key: str, name: str, ns: str, phase: str, extra: dict, pp: PodProc | None,
+                annotations: dict | None = None) -> None:
+        st = {"phase": phase, "hostIP": self.ip, "podIP": self.ip}
+        if pp is not None:
+            state = {"running": {"startedAt": pp.started}} if phase == "Running" else \
+                {"terminated": {"exitCode": extra.get("exitCode", pp.exit_code), "reason": "Completed" if phase == "Succeeded" else "Error"}}
+            st["containerStatuses"] = [{"name": "main", "restartCount": pp.restarts, "state": state,
+                                        "ready": phase == "Running"}]
+            st["startTime"] = pp.started
+        for k in ("message", "reason", "result"):
+            if extra.get(k) is not None:
+                st[k] = extra[k]
+        body = {"status": st}
+        if annotations:
+            body["annotations"] = annotations
+        try:
+            self.api.put(self.api.k8s(f"/api/v1/namespaces/{ns}/pods/{name}/status"), body)
+        except (ApiError, OSError) as e:
+            print(f"{self.name}: status report for {key} failed: {e}", flush=True)
+
+    def watch_loop(self) -> None:
+        api = Client(self.api.base, token=self.api.token, prefix=self.api.prefix, timeout=40.0)
+        path = api.k8s("/api/v1/pods")
+        q = {"fieldSelector": f"spec.nodeName={self.name}"}
+        rv = 0
+        first = True
+        while not self.stop.is_set():
+            try:
+                if first:
+                    lst = api.get(path, query=q)
+                    rv = int(lst["metadata"]["resourceVersion"])
+                    for pod in lst["items"]:
+                        self._handle("ADDED", pod)
+                    first = False
+                rv, events = api.watch(path, rv, timeout=20.0, query=q)
+                for ev in events:
+                    self._handle(ev["type"], ev["object"])
+            except (ApiError, OSError) as e:
+                if self.stop.is_set():
+                    return
+                print(f"{self.name}: watch error {e}; retrying", flush=True)
+                first = True
+                self.stop.wait(0.2)
+
+    def _handle(self, etype: str, pod: dict) -> None:
+        md = pod["metadata"]
+        key = f"{md['namespace']}/{md['name']}"
+        if etype == "DELETED":
+            self.runtime.stop(key)
+            self._pods_meta.pop(key, None)
+            return
+        phase = pod.get("status", {}).get("phase", "Pending")
+        if phase in TERMINAL:
+            return
+        if key not in self.runtime.running():
+            self._start_pod(pod)
+
+    # ---- lifecycle --------------------------------------------------------------------
+    def run(self) -> int:
+        install_sigterm()
+        t0 = time.monotonic()
+        self.join()
+        print(f"{self.name}: registered in {time.monotonic() - t0:.3f}s "
+              f"({len(self.plugin.devices())} GPU, inventory={self.plugin.inventory.source})", flush=True)
+        threads = [threading.Thread(target=self.heartbeat_loop, name="heartbeat", daemon=True),
+                   threading.Thread(target=self.watch_loop, name="pods", daemon=True)]
+        for t in threads:
+            t.start()
+        try:
+            while not self.stop.is_set():
+                self.stop.wait(1.0)
+        except (SystemExit, KeyboardInterrupt):
+            pass
+        finally:
+            self.stop.set()
+            self.runtime.stop_all()
+        return 0
+
+
+def _expand(s: str, env: dict) -> str:
+    from .runtime import expand
+
+    return expand(s, env)
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(prog="tk8s-agent", description="tk8s node agent")
+    ap.add_argument("url", nargs="?", help="registration URL (http://master:port/v1/scripts/TOKEN)")
+    ap.add_argument("--url", dest="url_opt")
+    ap.add_argument("--name", default=os.environ.get("TK8S_MACHINE", platform.node()))
+    ap.add_argument("--ip", default=os.environ.get("TK8S_MACHINE_IP", "127.0.0.1"))
+    ap.add_argument("--sandbox", default=os.environ.get("TK8S_MACHINE_DIR", "."))
+    ap.add_argument("--gpus", default=os.environ.get("TK8S_MACHINE_GPUS", ""))
+    ap.add_argument("--labels", default="")
+    ap.add_argument("--tool-dir", action="append", default=[])
+    ap.add_argument("--timeout", type=float, default=60.0)
+    a = ap.parse_args(argv)
+    url = a.url_opt or a.url
+    if not url:
+        ap.error("registration URL is required")
+    gpus = [int(x) for x in a.gpus.split(",") if x.strip() != ""]
+    labels = dict(kv.split("=", 1) for kv in a.labels.split(",") if "=" in kv)
+    tools = a.tool_dir or [str(Path(__file__).resolve().parents[1] / "bin")]
+    return Agent(url, a.name, a.ip, a.sandbox, gpus, labels, tools, a.timeout).run()
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,158 @@
+"""Pod runtime of the node agent: pods are process groups in the node sandbox.
+
+The reference's nodes run Docker containers started by the Rancher agent (rancher/agent:v1.2.0,
+ansible/roles/rancherhost/tasks/main.yml:26-34). Here a pod is a process group: its env gets the
+device plugin's Allocate() result and the downward-API values, ``$(VAR)`` references in
+command/args are expanded like Kubernetes does, stdout/stderr go to ``pods/<pod>/log``, and
+restartPolicy Always/OnFailure/Never is honoured with capped exponential back-off.
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import signal
+import subprocess
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+from ..utils.fsutil import atomic_write_json
+from ..utils.procs import kill_group
+
+_VAR = re.compile(r"\$\(([A-Za-z_][A-Za-z0-9_]*)\)")
+
+
+def expand(s: str, env: dict) -> str:
+    """Kubernetes `$(VAR)` expansion; `$$(VAR)` escapes; unknown refs stay verbatim."""
+    out, i = [], 0
+    while i < len(s):
+        if s.startswith("$$(", i):
+            out.append("$(")
+            i += 3
+            continue
+        m = _VAR.match(s, i)
+        if m:
+            out.append(env.get(m.group(1), m.group(0)))
+            i = m.end()
+        else:
+            out.append(s[i])
+            i += 1
+    return "".join(out)
+
+
+def last_json_line(text: str) -> dict | None:
+    for line in reversed(text.strip().splitlines()):
+        line = line.strip()
+        if line.startswith("{") and line.endswith("}"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                continue
+    return None
+
+
+@dataclass
+class PodProc:
+    key: str                      # namespace/name
+    uid: str
+    dir: Path
+    argv: list[str]
+    env: dict
+    restart_policy: str
+    gpu_ids: list[str] = field(default_factory=list)
+    proc: subprocess.Popen | None = None
+    restarts: int = 0
+    started: float = 0.0
+    exit_code: int | None = None
+    stopping: bool = False
+    done: threading.Event = field(default_factory=threading.Event)
+
+
+class PodRuntime:
+    def __init__(self, sandbox: Path, on_status, tool_dirs: list[str] | None = None):
+        self.sandbox = Path(sandbox)
+        self.on_status = on_status        # callback(podproc, phase, extra: dict)
+        self.pods: dict[str, PodProc] = {}
+        self.lock = threading.Lock()
+        self.tool_dirs = tool_dirs or []
+
+    def start(self, pp: PodProc) -> None:
+        with self.lock:
+            self.pods[pp.key] = pp
+        threading.Thread(target=self._run, args=(pp,), name=f"pod-{pp.key}", daemon=True).start()
+
+    def _spawn(self, pp: PodProc) -> subprocess.Popen:
+        pp.dir.mkdir(parents=True, exist_ok=True)
+        env = dict(pp.env)
+        if self.tool_dirs:
+            env["PATH"] = os.pathsep.join(self.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
+        log = open(pp.dir / "log", "ab", buffering=0)
+        try:
+            p = subprocess.Popen(pp.argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
+                                 stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
+        finally:
+            log.close()
+        atomic_write_json(pp.dir / "pod.pid", {"pid": p.pid, "pgid": p.pid, "argv": pp.argv})
+        return p
+
+    def _run(self, pp: PodProc) -> None:
+        backoff = 0.1
+        while not pp.stopping:
+            pp.started = time.time()
+            try:
+                pp.proc = self._spawn(pp)
+            except OSError as e:
+                pp.exit_code = 127
+                self.on_status(pp, "Failed", {"message": f"failed to start {pp.argv[0]!r}: {e}", "reason": "StartError"})
+                break
+            self.on_status(pp, "Running", {})
+            rc = pp.proc.wait()
+            pp.exit_code = rc
+            (pp.dir / "pod.pid").unlink(missing_ok=True)
+            if pp.stopping:
+                break
+            ok = rc == 0
+            again = pp.restart_policy == "Always" or (pp.restart_policy == "OnFailure" and not ok)
+            if not again:
+                text = ""
+                try:
+                    text = (pp.dir / "log").read_text(errors="replace")
+                except OSError:
+                    pass
+                extra = {"exitCode": rc, "result": last_json_line(text),
+                         "message": "" if ok else text.strip()[-800:]}
+                self.on_status(pp, "Succeeded" if ok else "Failed", extra)
+                break
+            pp.restarts += 1
+            self.on_status(pp, "Running", {"restarts": pp.restarts, "lastExitCode": rc})
+            time.sleep(backoff)
+            backoff = min(backoff * 2, 10.0)
+        pp.done.set()
+
+    def stop(self, key: str, grace: float = 2.0) -> PodProc | None:
+        with self.lock:
+            pp = self.pods.pop(key, None)
+        if pp is None:
+            return None
+        pp.stopping = True
+        if pp.proc is not None and pp.proc.poll() is None:
+            kill_group(pp.proc.pid, grace)
+        return pp
+
+    def stop_all(self) -> None:
+        for key in list(self.pods):
+            self.stop(key, grace=1.0)
+
+    def running(self) -> dict[str, PodProc]:
+        with self.lock:
+            return dict(self.pods)
+
+
+def _sigterm_to_exit(*_):
+    raise SystemExit(0)
+
+
+def install_sigterm():
+    signal.signal(signal.SIGTERM, _sigterm_to_exit)

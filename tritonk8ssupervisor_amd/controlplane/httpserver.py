@@ -1,0 +1,187 @@
+"""Minimal asyncio HTTP/1.1 server (stdlib only; keep-alive; long-poll friendly).
+
+Why not FastAPI/uvicorn: the control plane's start-up time is on the critical path of the
+bring-up metric (the reference waits up to 300 s for Rancher to log "Listening on",
+ansible/roles/ranchermaster/tasks/main.yml:14-20); importing this module costs milliseconds.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import re
+import traceback
+from dataclasses import dataclass, field
+from typing import Any, Awaitable, Callable
+from urllib.parse import parse_qs, unquote, urlsplit
+
+REASONS = {200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
+           401: "Unauthorized", 403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed",
+           409: "Conflict", 422: "Unprocessable Entity", 500: "Internal Server Error",
+           503: "Service Unavailable", 504: "Gateway Timeout"}
+
+
+@dataclass
+class Request:
+    method: str
+    path: str
+    query: dict[str, str]
+    headers: dict[str, str]
+    body: bytes
+    peer: str = ""
+
+    def json(self) -> Any:
+        if not self.body:
+            return {}
+        try:
+            return json.loads(self.body)
+        except ValueError as e:
+            raise HttpError(400, f"invalid JSON body: {e}") from e
+
+    def q(self, key: str, default: str | None = None) -> str | None:
+        return self.query.get(key, default)
+
+    @property
+    def bearer(self) -> str | None:
+        a = self.headers.get("authorization", "")
+        return a[7:].strip() if a.lower().startswith("bearer ") else None
+
+
+@dataclass
+class Response:
+    status: int = 200
+    body: Any = None
+    headers: dict[str, str] = field(default_factory=dict)
+    content_type: str | None = None
+
+    def encode(self) -> tuple[bytes, str]:
+        if isinstance(self.body, (bytes, bytearray)):
+            return bytes(self.body), self.content_type or "application/octet-stream"
+        if isinstance(self.body, str):
+            return self.body.encode(), self.content_type or "text/plain; charset=utf-8"
+        if self.body is None:
+            return b"", self.content_type or "text/plain"
+        return (json.dumps(self.body, separators=(",", ":"), default=str).encode(),
+                self.content_type or "application/json")
+
+
+class HttpError(Exception):
+    def __init__(self, status: int, message: str, body: Any = None):
+        super().__init__(message)
+        self.status = status
+        self.body = body if body is not None else {"type": "error", "status": status, "message": message}
+
+
+Handler = Callable[..., Awaitable[Response | Any]]
+
+
+class Router:
+    def __init__(self):
+        self.routes: list[tuple[str, re.Pattern, Handler]] = []
+
+    def add(self, method: str, pattern: str, handler: Handler) -> None:
+        self.routes.append((method, re.compile("^" + pattern + "$"), handler))
+
+    def route(self, method: str, pattern: str):
+        def deco(fn):
+            self.add(method, pattern, fn)
+            return fn
+        return deco
+
+    def match(self, method: str, path: str):
+        allowed = False
+        for m, rx, h in self.routes:
+            mt = rx.match(path)
+            if mt:
+                if m == method or (m == "GET" and method == "HEAD"):
+                    return h, {k: unquote(v) for k, v in mt.groupdict().items()}
+                allowed = True
+        if allowed:
+            raise HttpError(405, f"method {method} not allowed on {path}")
+        raise HttpError(404, f"no route for {method} {path}")
+
+
+async def _read_request(reader: asyncio.StreamReader, peer: str) -> Request | None:
+    try:
+        head = await reader.readuntil(b"\r\n\r\n")
+    except (asyncio.IncompleteReadError, ConnectionError):
+        return None
+    except asyncio.LimitOverrunError:
+        raise HttpError(400, "headers too large")
+    lines = head.decode("latin-1").split("\r\n")
+    try:
+        method, target, _ = lines[0].split(" ", 2)
+    except ValueError:
+        raise HttpError(400, "bad request line")
+    headers = {}
+    for line in lines[1:]:
+        if ":" in line:
+            k, v = line.split(":", 1)
+            headers[k.strip().lower()] = v.strip()
+    body = b""
+    n = int(headers.get("content-length", "0") or 0)
+    if n:
+        body = await reader.readexactly(n)
+    u = urlsplit(target)
+    query = {k: v[-1] for k, v in parse_qs(u.query, keep_blank_values=True).items()}
+    return Request(method.upper(), u.path or "/", query, headers, body, peer)
+
+
+class HttpServer:
+    def __init__(self, router: Router, on_error: Callable[[str], None] | None = None):
+        self.router = router
+        self.on_error = on_error
+        self.server: asyncio.base_events.Server | None = None
+
+    async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
+        peer = "%s:%s" % (writer.get_extra_info("peername") or ("?", 0))[:2]
+        try:
+            while True:
+                try:
+                    req = await _read_request(reader, peer)
+                except HttpError as e:
+                    await self._send(writer, Response(e.status, e.body), keep=False, head=False)
+                    return
+                if req is None:
+                    return
+                try:
+                    handler, params = self.router.match(req.method, req.path)
+                    res = await handler(req, **params)
+                    if not isinstance(res, Response):
+                        res = Response(200, res)
+                except HttpError as e:
+                    res = Response(e.status, e.body)
+                except Exception as e:  # noqa: BLE001 - keep the server alive
+                    if self.on_error:
+                        self.on_error(traceback.format_exc())
+                    res = Response(500, {"type": "error", "status": 500, "message": repr(e)})
+                keep = req.headers.get("connection", "").lower() != "close"
+                await self._send(writer, res, keep=keep, head=req.method == "HEAD")
+                if not keep:
+                    return
+        except (ConnectionError, asyncio.IncompleteReadError):
+            return
+        finally:
+            try:
+                writer.close()
+            except Exception:  # noqa: BLE001
+                pass
+
+    @staticmethod
+    async def _send(writer: asyncio.StreamWriter, res: Response, keep: bool, head: bool) -> None:
+        body, ctype = res.encode()
+        hdr = [f"HTTP/1.1 {res.status} {REASONS.get(res.status, 'Status')}",
+               f"Content-Type: {ctype}", f"Content-Length: {len(body)}",
+               f"Connection: {'keep-alive' if keep else 'close'}"]
+        hdr += [f"{k}: {v}" for k, v in res.headers.items()]
+        writer.write(("\r\n".join(hdr) + "\r\n\r\n").encode("latin-1") + (b"" if head else body))
+        await writer.drain()
+
+    async def start(self, host: str, port: int) -> tuple[str, int]:
+        self.server = await asyncio.start_server(self._handle, host, port, reuse_address=True, limit=1 << 20)
+        sock = self.server.sockets[0].getsockname()
+        return sock[0], sock[1]
+
+    async def close(self) -> None:
+        if self.server:
+            self.server.close()
+            await self.server.wait_closed()

@@ -1,0 +1,1038 @@
+"""tk8s control plane: Rancher-1.x-style environment API + a Kubernetes API subset.
+
+Replaces the `rancher/server:stable` container (ansible/roles/ranchermaster/tasks/main.yml:6-13)
+and the Rancher-managed Kubernetes control plane it deployed onto the hosts (SURVEY.md §2.4
+P1/P3). One process serves:
+
+Rancher-compatible REST (what the reference's Ansible roles call):
+  GET  /v2-beta/projectTemplates?name=kubernetes        ranchermaster/tasks/main.yml:29-35
+  POST /v2-beta/projects              -> 201 {id}        ranchermaster/tasks/main.yml:37-49
+  POST /v1/registrationtokens?projectId=ID -> 201 {links.self}   rancherhost/tasks/main.yml:11-17
+  GET  /v1/registrationtokens/ID      -> {registrationUrl}        rancherhost/tasks/main.yml:19-24
+  GET/POST /v1/scripts/TOKEN          agent bootstrap / node registration (rancher/agent join)
+  GET  /r/projects/ENV/kubernetes-dashboard:9090/   the readiness oracle of setup.sh:66
+  GET  /env/ENV/kubernetes/kubectl    kubeconfig  (setup.sh:89)
+  GET  /env/ENV/infra/containers      what runs where (setup.sh:53)
+
+Kubernetes subset under /r/projects/ENV/kubernetes and /api, /apis (default project):
+  nodes (leases, Ready/NotReady), pods, daemonsets, jobs (Indexed), deployments, services,
+  events; watch = long-poll batches (?watch=1&resourceVersion=N&timeoutSeconds=T).
+  Extended resource ``amd.com/gpu`` is scheduled like the AMD k8s-device-plugin exposes it.
+
+Extras: /v1/kv/KEY (rendezvous store, e.g. RCCL unique ids), /v1/cluster/wait (event-driven
+readiness, replaces the unbounded 15 s polling loop of setup.sh:59-85), /metrics.
+
+Everything runs on one asyncio loop; the store is the single source of truth.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import copy
+import html
+import json
+import os
+import secrets
+import signal
+import sys
+import time
+from pathlib import Path
+
+from .httpserver import HttpError, HttpServer, Request, Response, Router
+from .store import Conflict, Store, now_iso
+
+GPU = "amd.com/gpu"
+VALIDATION_LABEL = "tk8s.amd.com/validation"
+TERMINAL = ("Succeeded", "Failed")
+
+
+def _key(*parts: str) -> str:
+    return "/".join(parts)
+
+
+def _cond(obj: dict, ctype: str) -> dict | None:
+    for c in obj.get("status", {}).get("conditions", []):
+        if c.get("type") == ctype:
+            return c
+    return None
+
+
+def _set_cond(obj: dict, ctype: str, status: str, reason: str = "", message: str = "") -> bool:
+    conds = obj.setdefault("status", {}).setdefault("conditions", [])
+    for c in conds:
+        if c["type"] == ctype:
+            changed = c.get("status") != status or c.get("reason") != reason
+            if changed:
+                c["lastTransitionTime"] = now_iso()
+            c.update(status=status, reason=reason, message=message)
+            return changed
+    conds.append({"type": ctype, "status": status, "reason": reason, "message": message,
+                  "lastTransitionTime": now_iso()})
+    return True
+
+
+def node_ready(n: dict) -> bool:
+    c = _cond(n, "Ready")
+    return bool(c and c["status"] == "True")
+
+
+def node_validated(n: dict) -> bool:
+    c = _cond(n, "AMDGPUValidated")
+    return bool(c and c["status"] == "True")
+
+
+def pod_gpus(p: dict) -> int:
+    total = 0
+    for c in p.get("spec", {}).get("containers", []):
+        r = c.get("resources", {})
+        v = r.get("limits", {}).get(GPU, r.get("requests", {}).get(GPU, 0))
+        total += int(v or 0)
+    return total
+
+
+def labels_match(selector: dict | None, labels: dict | None) -> bool:
+    if not selector:
+        return True
+    labels = labels or {}
+    return all(labels.get(k) == v for k, v in selector.items())
+
+
+class ControlPlane:
+    def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
+                 advertise: str | None = None):
+        self.host, self.port = host, port
+        self.advertise = advertise
+        self.state_dir = Path(state_dir) if state_dir else None
+        self.node_grace = node_grace
+        self.store = Store()
+        self.router = Router()
+        self.http = HttpServer(self.router, on_error=self._log_error)
+        self.leases: dict[str, float] = {}   # node key -> monotonic time of last heartbeat
+        self.started = time.time()
+        self._stop = None
+        self._seq = 0
+        self._reconciling = False
+        self._again = False
+        self._routes()
+
+    # ---- utilities --------------------------------------------------------------------
+    def _log_error(self, text: str) -> None:
+        sys.stderr.write(text)
+        sys.stderr.flush()
+
+    @property
+    def base(self) -> str:
+        return f"http://{self.advertise or self.host}:{self.port}"
+
+    def _next_id(self, prefix: str) -> str:
+        self._seq += 1
+        return f"{prefix}{self._seq}"
+
+    def _event(self, project: str, ns: str, involved: dict, reason: str, message: str, etype: str = "Normal") -> None:
+        self._seq += 1
+        name = f"{involved.get('name', 'x')}.{self._seq:x}"
+        self.store.put("events", _key(project, ns, name), {
+            "kind": "Event", "metadata": {"name": name, "namespace": ns},
+            "involvedObject": involved, "reason": reason, "message": message, "type": etype,
+            "firstTimestamp": now_iso(), "count": 1,
+        })
+        evs = self.store.keys("events")
+        if len(evs) > 5000:
+            for k in evs[: len(evs) - 5000]:
+                self.store.delete("events", k)
+
+    def project(self, pid: str | None) -> dict:
+        if pid in (None, "", "default"):
+            projects = self.store.list("projects")
+            if not projects:
+                raise HttpError(404, "no project/environment exists yet")
+            return sorted(projects, key=lambda p: p["created_seq"])[0]
+        p = self.store.get("projects", pid)
+        if p is None:
+            raise HttpError(404, f"project {pid} not found")
+        return p
+
+    def _auth(self, req: Request, project: dict) -> None:
+        tok = req.bearer
+        if req.method in ("GET", "HEAD"):
+            return
+        valid = {project.get("apiToken")}
+        if tok in valid:
+            return
+        # node tokens may update their own node / pods
+        if tok and any(n.get("nodeToken") == tok for n in self.store.list("nodesecrets")):
+            return
+        raise HttpError(401, "missing or invalid bearer token")
+
+    # ---- routes -----------------------------------------------------------------------
+    def _routes(self) -> None:
+        r = self.router
+        r.add("GET", r"/(ping|healthz)?", self.h_ping)
+        r.add("GET", r"/version", self.h_version)
+        r.add("GET", r"/metrics", self.h_metrics)
+        # Rancher-style API
+        r.add("GET", r"/v2-beta/projectTemplates", self.h_templates)
+        r.add("GET", r"/v2-beta/projects", self.h_projects)
+        r.add("POST", r"/v2-beta/projects", self.h_project_create)
+        r.add("GET", r"/v2-beta/projects/(?P<pid>[^/]+)", self.h_project_get)
+        r.add("DELETE", r"/v2-beta/projects/(?P<pid>[^/]+)", self.h_project_delete)
+        r.add("POST", r"/v1/registrationtokens", self.h_token_create)
+        r.add("GET", r"/v1/registrationtokens/(?P<tid>[^/]+)", self.h_token_get)
+        r.add("GET", r"/v1/scripts/(?P<token>[^/]+)", self.h_script)
+        r.add("POST", r"/v1/scripts/(?P<token>[^/]+)", self.h_register)
+        r.add("GET", r"/r/projects/(?P<pid>[^/]+)/kubernetes-dashboard:9090/?", self.h_dashboard)
+        r.add("GET", r"/env/(?P<pid>[^/]+)/kubernetes/kubectl", self.h_kubeconfig)
+        r.add("GET", r"/env/(?P<pid>[^/]+)/infra/containers", self.h_containers)
+        # KV + cluster readiness
+        r.add("GET", r"/v1/kv/(?P<key>.+)", self.h_kv_get)
+        r.add("PUT", r"/v1/kv/(?P<key>.+)", self.h_kv_put)
+        r.add("POST", r"/v1/kv/(?P<key>.+)", self.h_kv_put)
+        r.add("DELETE", r"/v1/kv/(?P<key>.+)", self.h_kv_delete)
+        r.add("GET", r"/v1/cluster/status", self.h_cluster_status)
+        r.add("GET", r"/v1/cluster/wait", self.h_cluster_wait)
+        r.add("GET", r"/v1/events", self.h_cp_events)
+        # Kubernetes subset, with and without the Rancher project prefix
+        for pre in (r"/r/projects/(?P<pid>[^/]+)/kubernetes", r""):
+            def add(method, path, h, pre=pre):
+                r.add(method, pre + path, h)
+            add("GET", r"/api/v1/nodes", self.h_nodes)
+            add("GET", r"/api/v1/nodes/(?P<name>[^/]+)", self.h_node_get)
+            add("PUT", r"/api/v1/nodes/(?P<name>[^/]+)/status", self.h_node_status)
+            add("PATCH", r"/api/v1/nodes/(?P<name>[^/]+)", self.h_node_patch)
+            add("DELETE", r"/api/v1/nodes/(?P<name>[^/]+)", self.h_node_delete)
+            add("GET", r"/api/v1/namespaces", self.h_namespaces)
+            add("GET", r"/api/v1/pods", self.h_pods)
+            for kind, grp in (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1"),
+                              ("daemonsets", "/apis/apps/v1"), ("deployments", "/apis/apps/v1"),
+                              ("jobs", "/apis/batch/v1")):
+                add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._lister(kind))
+                add("POST", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._creator(kind))
+                add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._getter(kind))
+                add("DELETE", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._deleter(kind))
+            add("GET", r"/api/v1/events", self._lister("events", all_ns=True))
+            add("GET", r"/apis/apps/v1/daemonsets", self._lister("daemonsets", all_ns=True))
+            add("GET", r"/apis/batch/v1/jobs", self._lister("jobs", all_ns=True))
+            add("PUT", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/status", self.h_pod_status)
+            add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/log", self.h_pod_log)
+
+    # ---- misc handlers ---------------------------------------------------------------
+    async def h_ping(self, req: Request, **_):
+        return Response(200, "pong")
+
+    async def h_version(self, req: Request):
+        from .. import __version__
+
+        return {"major": "1", "minor": "30", "gitVersion": f"v1.30.0-tk8s{__version__}", "platform": "linux/amd64",
+                "tk8sVersion": __version__}
+
+    async def h_metrics(self, req: Request):
+        lines = []
+        for p in self.store.list("projects"):
+            pid = p["id"]
+            s = self.summary(pid)
+            lab = f'project="{pid}"'
+            lines += [f"tk8s_nodes{{{lab}}} {s['nodes']}", f"tk8s_nodes_ready{{{lab}}} {s['nodes_ready']}",
+                      f"tk8s_nodes_validated{{{lab}}} {s['nodes_validated']}",
+                      f"tk8s_gpus_capacity{{{lab}}} {s['gpus_capacity']}",
+                      f"tk8s_gpus_allocatable{{{lab}}} {s['gpus_allocatable']}",
+                      f"tk8s_gpus_in_use{{{lab}}} {s['gpus_in_use']}"]
+            for phase, n in s["pods_by_phase"].items():
+                lines.append(f'tk8s_pods{{{lab},phase="{phase}"}} {n}')
+        now = time.monotonic()
+        for k, t in self.leases.items():
+            lines.append(f'tk8s_node_heartbeat_age_seconds{{node="{k}"}} {now - t:.3f}')
+        lines.append(f"tk8s_store_resource_version {self.store.rv}")
+        return Response(200, "\n".join(lines) + "\n", content_type="text/plain; version=0.0.4")
+
+    # ---- Rancher API -----------------------------------------------------------------
+    def _ensure_templates(self) -> None:
+        if not self.store.list("projecttemplates"):
+            for i, (name, desc) in enumerate([("cattle", "Default Cattle template"),
+                                              ("kubernetes", "Kubernetes on MI355X (tk8s control plane)")], 1):
+                tid = f"1pt{i}"
+                self.store.put("projecttemplates", tid, {"id": tid, "type": "projectTemplate", "name": name,
+                                                          "description": desc, "isPublic": True,
+                                                          "metadata": {"name": name}})
+
+    async def h_templates(self, req: Request):
+        self._ensure_templates()
+        name = req.q("name")
+        data = [t for t in self.store.list("projecttemplates") if name is None or t["name"] == name]
+        return {"type": "collection", "resourceType": "projectTemplate", "data": data}
+
+    async def h_projects(self, req: Request):
+        return {"type": "collection", "resourceType": "project", "data": [self._public_project(p) for p in self.store.list("projects")]}
+
+    def _public_project(self, p: dict) -> dict:
+        return {k: v for k, v in p.items() if k not in ("apiToken",)}
+
+    async def h_project_create(self, req: Request):
+        self._ensure_templates()
+        body = req.json()
+        name = str(body.get("name") or "").strip()
+        tid = body.get("projectTemplateId")
+        if not name:
+            raise HttpError(422, "name is required")
+        tmpl = self.store.get("projecttemplates", str(tid))
+        if tmpl is None:
+            raise HttpError(422, f"projectTemplateId {tid!r} does not exist")
+        pid = self._next_id("1a")
+        self._seq += 1
+        p = {"id": pid, "type": "project", "name": name, "description": body.get("description", ""),
+             "projectTemplateId": tid, "orchestration": tmpl["name"], "state": "active",
+             "allowSystemRole": bool(body.get("allowSystemRole", False)), "members": body.get("members", []),
+             "virtualMachine": bool(body.get("virtualMachine", False)),
+             "servicesPortRange": body.get("servicesPortRange"), "projectLinks": body.get("projectLinks", []),
+             "created": now_iso(), "created_seq": self._seq, "apiToken": secrets.token_hex(16),
+             "links": {"self": f"{self.base}/v2-beta/projects/{pid}"},
+             "metadata": {"name": pid}}
+        self.store.put("projects", pid, p)
+        return Response(201, self._public_project(p))
+
+    async def h_project_get(self, req: Request, pid: str):
+        return self._public_project(self.project(pid))
+
+    async def h_project_delete(self, req: Request, pid: str):
+        p = self.project(pid)
+        for kind in list(self.store.objs):
+            for k in self.store.keys(kind):
+                if k.startswith(pid + "/"):
+                    self.store.delete(kind, k)
+        self.store.delete("projects", p["id"])
+        return {"id": pid, "state": "removed"}
+
+    async def h_token_create(self, req: Request):
+        pid = req.q("projectId") or req.json().get("projectId")
+        p = self.project(pid)
+        tid = self._next_id("1c")
+        token = secrets.token_hex(20)
+        t = {"id": tid, "type": "registrationToken", "projectId": p["id"], "token": token, "state": "active",
+             "registrationUrl": f"{self.base}/v1/scripts/{token}",
+             "command": f"python3 -m tritonk8ssupervisor_amd.agent --url {self.base}/v1/scripts/{token}",
+             "links": {"self": f"{self.base}/v1/registrationtokens/{tid}"}, "metadata": {"name": tid}}
+        self.store.put("registrationtokens", tid, t)
+        return Response(201, {k: v for k, v in t.items() if k not in ("token", "registrationUrl", "command")})
+
+    async def h_token_get(self, req: Request, tid: str):
+        t = self.store.get("registrationtokens", tid)
+        if t is None:
+            raise HttpError(404, f"registration token {tid} not found")
+        return t
+
+    def _token(self, token: str) -> dict:
+        for t in self.store.list("registrationtokens"):
+            if t["token"] == token and t["state"] == "active":
+                return t
+        raise HttpError(403, "invalid registration token")
+
+    async def h_script(self, req: Request, token: str):
+        t = self._token(token)
+        pid = t["projectId"]
+        return {"projectId": pid, "apiUrl": self.base, "apiPrefix": f"/r/projects/{pid}/kubernetes",
+                "heartbeatSeconds": max(0.2, self.node_grace / 5), "nodeGraceSeconds": self.node_grace}
+
+    async def h_register(self, req: Request, token: str):
+        t = self._token(token)
+        pid = t["projectId"]
+        body = req.json()
+        name = str(body.get("name") or "").strip()
+        if not name:
+            raise HttpError(422, "node name is required")
+        key = _key(pid, name)
+        ntok = secrets.token_hex(16)
+        gpus = body.get("devices", [])
+        healthy = sum(1 for d in gpus if d.get("health", "Healthy") == "Healthy")
+        cap = dict(body.get("capacity", {}))
+        cap[GPU] = str(len(gpus))
+        alloc = dict(cap)
+        alloc[GPU] = str(healthy)
+        node = {
+            "kind": "Node", "apiVersion": "v1", "_project": pid,
+            "metadata": {"name": name, "labels": {"kubernetes.io/hostname": name, "kubernetes.io/os": "linux",
+                                                  **({"amd.com/gpu.family": "gfx950"} if gpus else {}),
+                                                  **body.get("labels", {})},
+                         "annotations": body.get("annotations", {})},
+            "spec": {"unschedulable": False},
+            "status": {"capacity": cap, "allocatable": alloc, "devices": gpus,
+                       "addresses": [{"type": "InternalIP", "address": body.get("ip", "")},
+                                     {"type": "Hostname", "address": name}],
+                       "nodeInfo": body.get("nodeInfo", {}), "conditions": []},
+        }
+        _set_cond(node, "Ready", "True", "AgentReady", "tk8s agent registered and heartbeating")
+        _set_cond(node, "AMDGPUValidated", "Unknown" if gpus else "True",
+                  "Pending" if gpus else "NoGPUs", "validation pod not finished" if gpus else "")
+        self.store.put("nodes", key, node)
+        self.store.put("nodesecrets", key, {"metadata": {"name": name}, "nodeToken": ntok, "_project": pid})
+        self.leases[key] = time.monotonic()
+        self._event(pid, "default", {"kind": "Node", "name": name}, "RegisteredNode", f"Node {name} registered ({len(gpus)} GPU)")
+        self.reconcile()
+        return Response(201, {"node": name, "nodeToken": ntok, "projectId": pid,
+                              "apiPrefix": f"/r/projects/{pid}/kubernetes",
+                              "heartbeatSeconds": max(0.2, self.node_grace / 5)})
+
+    async def h_dashboard(self, req: Request, pid: str):
+        p = self.project(pid)
+        s = self.summary(p["id"])
+        if s["nodes_ready"] == 0:
+            return Response(503, "Service Unavailable", content_type="text/plain")
+        rows = "".join(
+            f"<tr><td>{html.escape(n['metadata']['name'])}</td><td>{'Ready' if node_ready(n) else 'NotReady'}</td>"
+            f"<td>{n['status']['allocatable'].get(GPU, '0')}</td><td>{'yes' if node_validated(n) else 'no'}</td></tr>"
+            for n in self.store.list("nodes", lambda n: self._in(p['id'], n)))
+        body = (f"<html><head><title>Kubernetes Dashboard - {html.escape(p['name'])}</title></head><body>"
+                f"<h1>kubernetes dashboard</h1><p>environment {html.escape(p['name'])} ({p['id']})</p>"
+                f"<table><tr><th>node</th><th>status</th><th>{GPU}</th><th>validated</th></tr>{rows}</table>"
+                f"<pre>{html.escape(json.dumps(s, indent=1))}</pre></body></html>")
+        return Response(200, body, content_type="text/html; charset=utf-8")
+
+    async def h_kubeconfig(self, req: Request, pid: str):
+        p = self.project(pid)
+        server = f"{self.base}/r/projects/{p['id']}/kubernetes"
+        cfg = {"apiVersion": "v1", "kind": "Config", "current-context": p["name"].replace(" ", "-"),
+               "clusters": [{"name": p["name"].replace(" ", "-"), "cluster": {"server": server}}],
+               "users": [{"name": p["name"].replace(" ", "-"), "user": {"token": p["apiToken"]}}],
+               "contexts": [{"name": p["name"].replace(" ", "-"),
+                             "context": {"cluster": p["name"].replace(" ", "-"), "user": p["name"].replace(" ", "-")}}]}
+        if req.q("format") == "json":
+            return cfg
+        import yaml  # local import: only this endpoint needs it
+
+        return Response(200, yaml.safe_dump(cfg, sort_keys=False), content_type="text/yaml")
+
+    async def h_containers(self, req: Request, pid: str):
+        p = self.project(pid)
+        pods = self.store.list("pods", lambda o: self._in(p["id"], o))
+        return {"project": p["id"], "containers": [
+            {"name": o["metadata"]["name"], "namespace": o["metadata"].get("namespace"),
+             "node": o["spec"].get("nodeName"), "phase": o.get("status", {}).get("phase"),
+             "gpus": o["metadata"].get("annotations", {}).get(GPU + "-ids")} for o in pods]}
+
+    # ---- KV -------------------------------------------------------------------------
+    async def h_kv_get(self, req: Request, key: str):
+        wait = float(req.q("wait", "0") or 0)
+        v = await self.store.wait_until(lambda: self.store.get("kv", key), min(wait, 120.0))
+        if not v:
+            raise HttpError(404, f"key {key} not found")
+        return Response(200, v["value"], content_type="text/plain")
+
+    async def h_kv_put(self, req: Request, key: str):
+        self.store.put("kv", key, {"metadata": {"name": key}, "value": req.body.decode()})
+        return Response(201, {"key": key})
+
+    async def h_kv_delete(self, req: Request, key: str):
+        self.store.delete("kv", key)
+        return Response(200, {"key": key, "deleted": True})
+
+    # ---- readiness -----------------------------------------------------------------------
+    @staticmethod
+    def _in(pid: str, obj: dict) -> bool:
+        return obj.get("_project") == pid
+
+    def summary(self, pid: str) -> dict:
+        nodes = self.store.list("nodes", lambda n: self._in(pid, n))
+        pods = self.store.list("pods", lambda o: self._in(pid, o))
+        by_phase: dict[str, int] = {}
+        for o in pods:
+            ph = o.get("status", {}).get("phase", "Pending")
+            by_phase[ph] = by_phase.get(ph, 0) + 1
+        in_use = sum(pod_gpus(o) for o in pods if o.get("spec", {}).get("nodeName")
+                     and o.get("status", {}).get("phase") not in TERMINAL)
+        ready = [n for n in nodes if node_ready(n)]
+        return {
+            "project": pid, "nodes": len(nodes), "nodes_ready": len(ready),
+            "nodes_validated": sum(1 for n in ready if node_validated(n)),
+            "nodes_validation_failed": sum(1 for n in nodes if (_cond(n, "AMDGPUValidated") or {}).get("status") == "False"),
+            "gpus_capacity": sum(int(n["status"]["capacity"].get(GPU, 0)) for n in nodes),
+            "gpus_allocatable": sum(int(n["status"]["allocatable"].get(GPU, 0)) for n in ready),
+            "gpus_in_use": in_use, "pods_by_phase": by_phase, "resourceVersion": self.store.rv,
+            "node_names": sorted(n["metadata"]["name"] for n in nodes),
+        }
+
+    def _job_state(self, pid: str, ref: str | None) -> str | None:
+        if not ref:
+            return None
+        ns, _, name = ref.rpartition("/")
+        j = self.store.get("jobs", _key(pid, ns or "default", name))
+        if j is None:
+            return "Missing"
+        for c in j.get("status", {}).get("conditions", []):
+            if c["type"] in ("Complete", "Failed") and c["status"] == "True":
+                return c["type"]
+        return "Running"
+
+    async def h_cluster_status(self, req: Request):
+        p = self.project(req.q("project"))
+        s = self.summary(p["id"])
+        s["job"] = self._job_state(p["id"], req.q("job"))
+        return s
+
+    async def h_cluster_wait(self, req: Request):
+        """Long-poll until `nodes` Ready (+validated) with >= `gpus` allocatable (+ job done)."""
+        pid = req.q("project")
+        want_nodes = int(req.q("nodes", "1"))
+        want_gpus = int(req.q("gpus", "0"))
+        validated = req.q("validated", "1") not in ("0", "false")
+        job = req.q("job")
+        timeout = min(float(req.q("timeout", "30")), 300.0)
+
+        def check():
+            try:
+                p = self.project(pid)
+            except HttpError:
+                return None
+            s = self.summary(p["id"])
+            js = self._job_state(p["id"], job)
+            failed = s["nodes_validation_failed"] > 0 or js in ("Failed", "Missing")
+            ok = (s["nodes_ready"] >= want_nodes and (not validated or s["nodes_validated"] >= want_nodes)
+                  and s["gpus_allocatable"] >= want_gpus and (js in (None, "Complete")))
+            if ok or failed:
+                s.update(ready=ok, failed=failed and not ok, job=js)
+                return s
+            return None
+
+        res = await self.store.wait_until(check, timeout)
+        if res:
+            return res
+        p = self.project(pid)
+        s = self.summary(p["id"])
+        s.update(ready=False, failed=False, timed_out=True, job=self._job_state(p["id"], job))
+        return Response(200, s)
+
+    async def h_cp_events(self, req: Request):
+        since = int(req.q("resourceVersion", "0") or 0)
+        wait = min(float(req.q("timeoutSeconds", "0") or 0), 60.0)
+        ev = await self.store.wait_events(since, None, wait)
+        return {"resourceVersion": self.store.rv,
+                "events": [{"type": e["type"], "kind": e["kind"], "name": e["object"].get("metadata", {}).get("name"),
+                            "resourceVersion": e["resourceVersion"]} for e in ev]}
+
+    # ---- k8s: nodes ----------------------------------------------------------------------
+    def _pid(self, pid: str | None, req: Request) -> str:
+        return self.project(pid or req.q("project")).get("id")
+
+    def _strip(self, obj: dict) -> dict:
+        return {k: v for k, v in obj.items() if not k.startswith("_")}
+
+    async def _list_or_watch(self, req: Request, kind: str, pred) -> dict:
+        if req.q("watch") in ("1", "true"):
+            since = int(req.q("resourceVersion", "0") or 0)
+            timeout = min(float(req.q("timeoutSeconds", "30") or 30), 300.0)
+            ev = await self.store.wait_events(since, kind, timeout, pred)
+            return {"kind": "WatchEventList", "resourceVersion": str(self.store.rv),
+                    "events": [{"type": e["type"], "object": self._strip(e["object"])} for e in ev]}
+        items = [self._strip(o) for o in self.store.list(kind, pred)]
+        items.sort(key=lambda o: (o["metadata"].get("namespace", ""), o["metadata"]["name"]))
+        return {"kind": "List", "apiVersion": "v1", "metadata": {"resourceVersion": str(self.store.rv)}, "items": items}
+
+    async def h_nodes(self, req: Request, pid: str | None = None):
+        p = self._pid(pid, req)
+        sel = _parse_selector(req.q("labelSelector"))
+        return await self._list_or_watch(req, "nodes", lambda n: self._in(p, n) and labels_match(sel, n["metadata"].get("labels")))
+
+    async def h_node_get(self, req: Request, name: str, pid: str | None = None):
+        p = self._pid(pid, req)
+        n = self.store.get("nodes", _key(p, name))
+        if n is None:
+            raise HttpError(404, f"node {name} not found")
+        return self._strip(n)
+
+    def _node_secret_ok(self, req: Request, key: str) -> None:
+        sec = self.store.get("nodesecrets", key)
+        if sec is None or req.bearer != sec["nodeToken"]:
+            raise HttpError(401, "invalid node token")
+
+    async def h_node_status(self, req: Request, name: str, pid: str | None = None):
+        """Heartbeat / status update from the node agent (the node lease)."""
+        p = self._pid(pid, req)
+        key = _key(p, name)
+        self._node_secret_ok(req, key)
+        body = req.json()
+        self.leases[key] = time.monotonic()
+        cur = self.store.get("nodes", key)
+        if cur is None:
+            raise HttpError(404, f"node {name} not found")
+        changed = False
+        new = copy.deepcopy(cur)
+        st = new["status"]
+        if "devices" in body:
+            st["devices"] = body["devices"]
+            healthy = sum(1 for d in body["devices"] if d.get("health", "Healthy") == "Healthy")
+            if st["allocatable"].get(GPU) != str(healthy):
+                st["allocatable"][GPU] = str(healthy)
+            changed = True
+        if "nodeInfo" in body:
+            st["nodeInfo"] = body["nodeInfo"]
+            changed = True
+        if "annotations" in body:
+            new["metadata"].setdefault("annotations", {}).update(body["annotations"])
+            changed = True
+        changed |= _set_cond(new, "Ready", "True", "AgentReady", "tk8s agent heartbeating")
+        if changed:
+            self.store.put("nodes", key, new)
+            self.reconcile()
+        return {"ok": True, "resourceVersion": self.store.rv}
+
+    async def h_node_patch(self, req: Request, name: str, pid: str | None = None):
+        p = self._pid(pid, req)
+        self._auth(req, self.project(p))
+        body = req.json()
+
+        def fn(n):
+            md = body.get("metadata", {})
+            n["metadata"].setdefault("labels", {}).update(md.get("labels", {}))
+            n["metadata"].setdefault("annotations", {}).update(md.get("annotations", {}))
+            if "spec" in body:
+                n["spec"].update(body["spec"])
+
+        n = self.store.patch("nodes", _key(p, name), fn)
+        if n is None:
+            raise HttpError(404, f"node {name} not found")
+        self.reconcile()
+        return self._strip(n)
+
+    async def h_node_delete(self, req: Request, name: str, pid: str | None = None):
+        p = self._pid(pid, req)
+        key = _key(p, name)
+        sec = self.store.get("nodesecrets", key)
+        if not (sec and req.bearer == sec["nodeToken"]):
+            self._auth(req, self.project(p))
+        n = self.store.delete("nodes", key)
+        self.store.delete("nodesecrets", key)
+        self.leases.pop(key, None)
+        if n is None:
+            raise HttpError(404, f"node {name} not found")
+        self.reconcile()
+        return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": "nodes"}}
+
+    async def h_namespaces(self, req: Request, pid: str | None = None):
+        self._pid(pid, req)
+        names = {"default", "kube-system", "amd-gpu"}
+        for kind in ("pods", "daemonsets", "jobs", "deployments", "services"):
+            names |= {o["metadata"].get("namespace", "default") for o in self.store.list(kind)}
+        return {"kind": "NamespaceList", "items": [{"metadata": {"name": n}} for n in sorted(names)]}
+
+    # ---- k8s: generic namespaced kinds ------------------------------------------------
+    async def h_pods(self, req: Request, pid: str | None = None):
+        p = self._pid(pid, req)
+        node = None
+        fs = req.q("fieldSelector") or ""
+        if fs.startswith("spec.nodeName="):
+            node = fs.split("=", 1)[1]
+        sel = _parse_selector(req.q("labelSelector"))
+        return await self._list_or_watch(req, "pods", lambda o: self._in(p, o) and (node is None or o["spec"].get("nodeName") == node)
+                                         and labels_match(sel, o["metadata"].get("labels")))
+
+    def _lister(self, kind: str, all_ns: bool = False):
+        async def h(req: Request, pid: str | None = None, ns: str | None = None):
+            p = self._pid(pid, req)
+            sel = _parse_selector(req.q("labelSelector"))
+            return await self._list_or_watch(req, kind, lambda o: self._in(p, o) and (all_ns or o["metadata"].get("namespace") == ns)
+                                             and labels_match(sel, o["metadata"].get("labels")))
+        return h
+
+    def _getter(self, kind: str):
+        async def h(req: Request, ns: str, name: str, pid: str | None = None):
+            p = self._pid(pid, req)
+            o = self.store.get(kind, _key(p, ns, name))
+            if o is None:
+                raise HttpError(404, f'{kind} "{name}" not found')
+            return self._strip(o)
+        return h
+
+    def _creator(self, kind: str):
+        async def h(req: Request, ns: str, pid: str | None = None):
+            p = self._pid(pid, req)
+            self._auth(req, self.project(p))
+            body = req.json()
+            return Response(201, self._strip(self.create(p, kind, ns, body)))
+        return h
+
+    def _deleter(self, kind: str):
+        async def h(req: Request, ns: str, name: str, pid: str | None = None):
+            p = self._pid(pid, req)
+            self._auth(req, self.project(p))
+            o = self.store.delete(kind, _key(p, ns, name))
+            if o is None:
+                raise HttpError(404, f'{kind} "{name}" not found')
+            if kind != "pods":
+                for pod in self.store.list("pods", lambda x: self._in(p, x) and any(
+                        r.get("uid") == o["metadata"]["uid"] for r in x["metadata"].get("ownerReferences", []))):
+                    self.store.delete("pods", _key(p, ns, pod["metadata"]["name"]))
+            self.reconcile()
+            return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
+        return h
+
+    def create(self, pid: str, kind: str, ns: str, body: dict) -> dict:
+        md = body.setdefault("metadata", {})
+        name = md.get("name")
+        if not name and md.get("generateName"):
+            name = md["generateName"] + secrets.token_hex(3)
+        if not name:
+            raise HttpError(422, "metadata.name is required")
+        md["name"] = name
+        md["namespace"] = ns
+        md.setdefault("labels", {})
+        md.setdefault("annotations", {})
+        body["_project"] = pid
+        key = _key(pid, ns, name)
+        if self.store.get(kind, key) is not None:
+            raise HttpError(409, f'{kind} "{name}" already exists')
+        if kind == "pods":
+            spec = body.setdefault("spec", {})
+            if not spec.get("containers"):
+                raise HttpError(422, "spec.containers is required")
+            spec.setdefault("restartPolicy", "Always")
+            body["status"] = {"phase": "Pending", "conditions": []}
+        elif kind in ("daemonsets", "deployments", "jobs"):
+            tmpl = body.get("spec", {}).get("template", {})
+            if not tmpl.get("spec", {}).get("containers"):
+                raise HttpError(422, "spec.template.spec.containers is required")
+            body.setdefault("status", {})
+        o = self.store.put(kind, key, body)
+        self.reconcile()
+        return o
+
+    async def h_pod_status(self, req: Request, ns: str, name: str, pid: str | None = None):
+        p = self._pid(pid, req)
+        key = _key(p, ns, name)
+        cur = self.store.get("pods", key)
+        if cur is None:
+            raise HttpError(404, f'pod "{name}" not found')
+        node = cur["spec"].get("nodeName")
+        if node:
+            self._node_secret_ok(req, _key(p, node))
+        body = req.json()
+        st = body.get("status", body)
+        ann = body.get("annotations")
+
+        def fn(o):
+            o.setdefault("status", {}).update(st)
+            if ann:
+                o["metadata"].setdefault("annotations", {}).update(ann)
+
+        o = self.store.patch("pods", key, fn)
+        phase = st.get("phase")
+        if phase in ("Running", "Succeeded", "Failed"):
+            self._event(p, ns, {"kind": "Pod", "name": name}, {"Running": "Started", "Succeeded": "Completed",
+                                                               "Failed": "Failed"}[phase],
+                        f"pod {name} {phase.lower()} on {node}", "Warning" if phase == "Failed" else "Normal")
+        self.reconcile()
+        return self._strip(o)
+
+    async def h_pod_log(self, req: Request, ns: str, name: str, pid: str | None = None):
+        p = self._pid(pid, req)
+        o = self.store.get("pods", _key(p, ns, name))
+        if o is None:
+            raise HttpError(404, f'pod "{name}" not found')
+        path = o["metadata"].get("annotations", {}).get("tk8s.amd.com/log-path")
+        if not path or not os.path.exists(path):
+            return Response(200, "", content_type="text/plain")
+        tail = int(req.q("tailLines", "0") or 0)
+        text = Path(path).read_text(errors="replace")
+        if tail:
+            text = "\n".join(text.splitlines()[-tail:]) + "\n"
+        return Response(200, text, content_type="text/plain")
+
+    # ---- controllers ------------------------------------------------------------------
+    def reconcile(self) -> None:
+        """Run every controller once (cheap at this scale; called after each mutation)."""
+        if getattr(self, "_reconciling", False):
+            self._again = True
+            return
+        self._reconciling = True
+        try:
+            for _ in range(8):
+                self._again = False
+                for p in self.store.list("projects"):
+                    pid = p["id"]
+                    self._ctl_daemonsets(pid)
+                    self._ctl_jobs(pid)
+                    self._ctl_deployments(pid)
+                    self._ctl_validation(pid)
+                    self._scheduler(pid)
+                if not self._again:
+                    break
+        finally:
+            self._reconciling = False
+
+    def _new_pod(self, pid: str, ns: str, name: str, owner: dict, owner_kind: str, template: dict,
+                 node: str | None = None, extra_env: dict | None = None, labels: dict | None = None,
+                 annotations: dict | None = None) -> dict:
+        spec = copy.deepcopy(template.get("spec", {}))
+        if extra_env:
+            for c in spec.get("containers", []):
+                c.setdefault("env", []).extend({"name": k, "value": str(v)} for k, v in extra_env.items())
+        if node:
+            spec["nodeName"] = node
+        md = copy.deepcopy(template.get("metadata", {}))
+        md.update(name=name, namespace=ns)
+        md.setdefault("labels", {}).update(labels or {})
+        md.setdefault("annotations", {}).update(annotations or {})
+        md["ownerReferences"] = [{"kind": owner_kind, "name": owner["metadata"]["name"], "uid": owner["metadata"]["uid"]}]
+        pod = {"kind": "Pod", "apiVersion": "v1", "metadata": md, "spec": spec, "_project": pid,
+               "status": {"phase": "Pending", "conditions": []}}
+        spec.setdefault("restartPolicy", "Always")
+        return self.store.put("pods", _key(pid, ns, name), pod)
+
+    def _owned(self, pid: str, owner: dict) -> list[dict]:
+        uid = owner["metadata"]["uid"]
+        return self.store.list("pods", lambda o: self._in(pid, o) and any(
+            r.get("uid") == uid for r in o["metadata"].get("ownerReferences", [])))
+
+    def _ctl_daemonsets(self, pid: str) -> None:
+        nodes = self.store.list("nodes", lambda n: self._in(pid, n))
+        for ds in self.store.list("daemonsets", lambda o: self._in(pid, o)):
+            ns = ds["metadata"]["namespace"]
+            tmpl = ds["spec"]["template"]
+            sel = tmpl.get("spec", {}).get("nodeSelector")
+            pods = {o["spec"].get("nodeName"): o for o in self._owned(pid, ds)}
+            eligible = [n for n in nodes if labels_match(sel, n["metadata"].get("labels"))
+                        and not n["spec"].get("unschedulable")]
+            for n in eligible:
+                nn = n["metadata"]["name"]
+                if nn not in pods:
+                    pods[nn] = self._new_pod(pid, ns, f"{ds['metadata']['name']}-{nn}", ds, "DaemonSet", tmpl, node=nn,
+                                             labels=ds["spec"].get("selector", {}).get("matchLabels"))
+            phases = [o.get("status", {}).get("phase") for o in pods.values()]
+            status = {"desiredNumberScheduled": len(eligible), "currentNumberScheduled": len(pods),
+                      "numberReady": phases.count("Running") + phases.count("Succeeded"),
+                      "numberSucceeded": phases.count("Succeeded"), "numberFailed": phases.count("Failed")}
+            if ds.get("status") != status:
+                self.store.patch("daemonsets", _key(pid, ns, ds["metadata"]["name"]), lambda o, s=status: o.__setitem__("status", s))
+
+    def _ctl_validation(self, pid: str) -> None:
+        """Node condition AMDGPUValidated from the validation DaemonSet's pod on that node."""
+        for ds in self.store.list("daemonsets", lambda o: self._in(pid, o) and o["metadata"].get("labels", {}).get(VALIDATION_LABEL) == "true"):
+            for pod in self._owned(pid, ds):
+                nn = pod["spec"].get("nodeName")
+                phase = pod.get("status", {}).get("phase")
+                if not nn or phase not in TERMINAL:
+                    continue
+                key = _key(pid, nn)
+                n = self.store.get("nodes", key)
+                if n is None:
+                    continue
+                want = ("True", "ProbesPassed") if phase == "Succeeded" else ("False", "ProbesFailed")
+                c = _cond(n, "AMDGPUValidated")
+                if c and (c["status"], c["reason"]) == want:
+                    continue
+                result = pod.get("status", {}).get("result") or {}
+
+                def fn(node, want=want, result=result, pod=pod):
+                    _set_cond(node, "AMDGPUValidated", want[0], want[1],
+                              pod.get("status", {}).get("message", "")[:500])
+                    ann = node["metadata"].setdefault("annotations", {})
+                    for k, path in (("hbm-write-gbps", ("hbm", "gbps")), ("md5-mbps", ("md5", "mbps")),
+                                    ("copy-gbps", ("copy", "kernel_gbps"))):
+                        v = result.get(path[0], {}).get(path[1]) if isinstance(result.get(path[0]), dict) else None
+                        if v is not None:
+                            ann[f"tk8s.amd.com/{k}"] = f"{v:.1f}"
+
+                self.store.patch("nodes", key, fn)
+
+    def _ctl_jobs(self, pid: str) -> None:
+        for job in self.store.list("jobs", lambda o: self._in(pid, o)):
+            ns, jname = job["metadata"]["namespace"], job["metadata"]["name"]
+            spec = job["spec"]
+            completions = int(spec.get("completions", 1))
+            parallelism = int(spec.get("parallelism", completions))
+            backoff = int(spec.get("backoffLimit", 6))
+            indexed = spec.get("completionMode") == "Indexed"
+            pods = self._owned(pid, job)
+            succeeded_idx, active, failed = set(), 0, 0
+            for o in pods:
+                ph = o.get("status", {}).get("phase")
+                idx = int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
+                if ph == "Succeeded":
+                    succeeded_idx.add(idx if indexed else o["metadata"]["name"])
+                elif ph == "Failed":
+                    failed += 1
+                else:
+                    active += 1
+            done = any(c["type"] in ("Complete", "Failed") and c["status"] == "True" for c in job.get("status", {}).get("conditions", []))
+            if not done and failed > backoff:
+                for o in pods:  # stop the rest (a gang job cannot finish without all ranks)
+                    if o.get("status", {}).get("phase") not in TERMINAL:
+                        self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+            elif not done:
+                running_idx = {int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
+                               for o in pods if o.get("status", {}).get("phase") not in TERMINAL}
+                need = [i for i in range(completions) if i not in succeeded_idx and i not in running_idx] if indexed \
+                    else list(range(max(0, completions - len(succeeded_idx) - active)))
+                for i in need[: max(0, parallelism - active)]:
+                    self._seq += 1
+                    name = f"{jname}-{i}-{self._seq:x}" if indexed else f"{jname}-{self._seq:x}"
+                    env = {"JOB_COMPLETION_INDEX": i, "JOB_COMPLETIONS": completions, "JOB_NAME": jname} if indexed else {"JOB_NAME": jname}
+                    self._new_pod(pid, ns, name, job, "Job", spec["template"], extra_env=env,
+                                  labels={"job-name": jname},
+                                  annotations={"batch.kubernetes.io/job-completion-index": str(i)} if indexed else None)
+                    active += 1
+            status = dict(job.get("status", {}))
+            status.update(active=active, succeeded=len(succeeded_idx), failed=failed)
+            conds = [c for c in status.get("conditions", [])]
+            if not done:
+                if len(succeeded_idx) >= completions:
+                    conds.append({"type": "Complete", "status": "True", "lastTransitionTime": now_iso()})
+                    status["completionTime"] = now_iso()
+                elif failed > backoff:
+                    conds.append({"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded",
+                                  "lastTransitionTime": now_iso()})
+            status["conditions"] = conds
+            if status != job.get("status"):
+                self.store.patch("jobs", _key(pid, ns, jname), lambda o, s=status: o.__setitem__("status", s))
+
+    def _ctl_deployments(self, pid: str) -> None:
+        for d in self.store.list("deployments", lambda o: self._in(pid, o)):
+            ns, dname = d["metadata"]["namespace"], d["metadata"]["name"]
+            want = int(d["spec"].get("replicas", 1))
+            pods = [o for o in self._owned(pid, d) if o.get("status", {}).get("phase") not in TERMINAL]
+            for _ in range(want - len(pods)):
+                self._seq += 1
+                self._new_pod(pid, ns, f"{dname}-{self._seq:x}", d, "Deployment", d["spec"]["template"],
+                              labels=d["spec"].get("selector", {}).get("matchLabels"))
+            for o in sorted(pods, key=lambda o: o["metadata"]["name"])[want:]:
+                self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+            pods = self._owned(pid, d)
+            status = {"replicas": want, "readyReplicas": sum(1 for o in pods if o.get("status", {}).get("phase") == "Running"),
+                      "availableReplicas": sum(1 for o in pods if o.get("status", {}).get("phase") == "Running")}
+            if d.get("status") != status:
+                self.store.patch("deployments", _key(pid, ns, dname), lambda o, s=status: o.__setitem__("status", s))
+
+    def _scheduler(self, pid: str) -> None:
+        pending = [o for o in self.store.list("pods", lambda o: self._in(pid, o))
+                   if not o["spec"].get("nodeName") and o.get("status", {}).get("phase") == "Pending"]
+        if not pending:
+            return
+        nodes = [n for n in self.store.list("nodes", lambda n: self._in(pid, n))
+                 if node_ready(n) and not n["spec"].get("unschedulable")]
+        used: dict[str, int] = {}
+        count: dict[str, int] = {}
+        for o in self.store.list("pods", lambda o: self._in(pid, o)):
+            nn = o["spec"].get("nodeName")
+            if nn and o.get("status", {}).get("phase") not in TERMINAL:
+                used[nn] = used.get(nn, 0) + pod_gpus(o)
+                count[nn] = count.get(nn, 0) + 1
+        for pod in sorted(pending, key=lambda o: o["metadata"]["name"]):
+            need = pod_gpus(pod)
+            sel = pod["spec"].get("nodeSelector")
+            best = None
+            for n in nodes:
+                nn = n["metadata"]["name"]
+                free = int(n["status"]["allocatable"].get(GPU, 0)) - used.get(nn, 0)
+                if need > free or not labels_match(sel, n["metadata"].get("labels")):
+                    continue
+                if need and not node_validated(n):
+                    continue  # GPU pods only land on validated nodes
+                score = (count.get(nn, 0), -free, nn)
+                if best is None or score < best[0]:
+                    best = (score, nn, free)
+            key = _key(pid, pod["metadata"]["namespace"], pod["metadata"]["name"])
+            if best is None:
+                c = _cond(pod, "PodScheduled")
+                if not c or c["status"] != "False":
+                    self.store.patch("pods", key, lambda o, need=need: _set_cond(
+                        o, "PodScheduled", "False", "Unschedulable", f"0/{len(nodes)} nodes available: need {need} {GPU}"))
+                continue
+            nn = best[1]
+            used[nn] = used.get(nn, 0) + need
+            count[nn] = count.get(nn, 0) + 1
+
+            def bind(o, nn=nn):
+                o["spec"]["nodeName"] = nn
+                _set_cond(o, "PodScheduled", "True", "Scheduled", f"assigned to {nn}")
+
+            self.store.patch("pods", key, bind)
+            self._event(pid, pod["metadata"]["namespace"], {"kind": "Pod", "name": pod["metadata"]["name"]},
+                        "Scheduled", f"Successfully assigned {pod['metadata']['name']} to {nn}")
+
+    # ---- node lifecycle ---------------------------------------------------------------
+    async def lease_loop(self) -> None:
+        while True:
+            await asyncio.sleep(min(0.25, self.node_grace / 4))
+            now = time.monotonic()
+            changed = False
+            for key, t in list(self.leases.items()):
+                if now - t > self.node_grace:
+                    n = self.store.get("nodes", key)
+                    if n is None:
+                        self.leases.pop(key, None)
+                        continue
+                    c = _cond(n, "Ready")
+                    if c and c["status"] == "True":
+                        self.store.patch("nodes", key, lambda o: _set_cond(
+                            o, "Ready", "Unknown", "NodeStatusUnknown", "tk8s agent stopped posting node status"))
+                        pid = key.split("/", 1)[0]
+                        self._event(pid, "default", {"kind": "Node", "name": n["metadata"]["name"]}, "NodeNotReady",
+                                    f"lease expired after {self.node_grace:.1f}s", "Warning")
+                        changed = True
+            if changed:
+                self.reconcile()
+
+    async def snapshot_loop(self) -> None:
+        if not self.state_dir:
+            return
+        last = -1
+        while True:
+            await asyncio.sleep(1.0)
+            if self.store.rv != last:
+                last = self.store.rv
+                self.store.snapshot(self.state_dir / "controlplane.json")
+
+    # ---- run --------------------------------------------------------------------------
+    async def run(self, ready_file: str | None = None) -> None:
+        if self.state_dir:
+            self.state_dir.mkdir(parents=True, exist_ok=True)
+            if self.store.restore(self.state_dir / "controlplane.json"):
+                now = time.monotonic()
+                for key in self.store.keys("nodes"):
+                    self.leases[key] = now  # grace period for agents to resume heartbeats
+                self._seq = self.store.rv + 1000
+        self._ensure_templates()
+        host, port = await self.http.start(self.host, self.port)
+        self.port = port
+        tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop())]
+        # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
+        print(f"Listening on {host}:{port}", flush=True)
+        if ready_file:
+            from ..utils.fsutil import atomic_write_json
+
+            atomic_write_json(ready_file, {"host": host, "port": port, "pid": os.getpid(), "base": self.base})
+        self._stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            loop.add_signal_handler(sig, self._stop.set)
+        await self._stop.wait()
+        for t in tasks:
+            t.cancel()
+        if self.state_dir:
+            self.store.snapshot(self.state_dir / "controlplane.json")
+        await self.http.close()
+
+
+def _parse_selector(s: str | None) -> dict | None:
+    if not s:
+        return None
+    out = {}
+    for part in s.split(","):
+        if "=" in part:
+            k, v = part.split("=", 1)
+            out[k.strip().rstrip("=")] = v.strip()
+    return out
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(prog="tk8s-controlplane", description=__doc__.splitlines()[0])
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--advertise", default=None, help="address put into URLs handed to agents")
+    ap.add_argument("--state-dir", default=None)
+    ap.add_argument("--node-grace", type=float, default=float(os.environ.get("TK8S_NODE_GRACE", "5")))
+    ap.add_argument("--ready-file", default=None)
+    a = ap.parse_args(argv)
+    cp = ControlPlane(a.host, a.port, a.state_dir, a.node_grace, a.advertise)
+    asyncio.run(cp.run(a.ready_file))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

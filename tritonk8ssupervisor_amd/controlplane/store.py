@@ -1,0 +1,142 @@
+"""Versioned object store with watch (the etcd + apiserver core of the control plane).
+
+Single-threaded (one asyncio loop owns it), so no locks: every mutation bumps a global
+resourceVersion, is appended to a bounded history and wakes long-poll watchers. Snapshots to
+JSON let a restarted control plane resume.
+"""
+from __future__ import annotations
+
+import asyncio
+import copy
+import time
+import uuid
+from collections import deque
+from typing import Any, Callable, Iterable
+
+from ..utils.fsutil import atomic_write_json, read_json
+
+HISTORY = 50_000
+
+
+def now_iso() -> str:
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+
+
+class Conflict(Exception):
+    pass
+
+
+class Store:
+    def __init__(self):
+        self.rv = 0
+        self.objs: dict[str, dict[str, dict]] = {}
+        self.history: deque[tuple[int, str, str, dict]] = deque(maxlen=HISTORY)
+        self._waiters: list[asyncio.Future] = []
+        self.listeners: list[Callable[[str, str, dict], None]] = []
+
+    # ---- reads ------------------------------------------------------------------------
+    def get(self, kind: str, key: str) -> dict | None:
+        return self.objs.get(kind, {}).get(key)
+
+    def list(self, kind: str, pred: Callable[[dict], bool] | None = None) -> list[dict]:
+        items = self.objs.get(kind, {}).values()
+        return [o for o in items if pred is None or pred(o)]
+
+    def keys(self, kind: str) -> Iterable[str]:
+        return list(self.objs.get(kind, {}).keys())
+
+    # ---- writes -----------------------------------------------------------------------
+    def _notify(self, kind: str, etype: str, obj: dict) -> None:
+        self.history.append((self.rv, kind, etype, obj))
+        for fn in list(self.listeners):
+            fn(kind, etype, obj)
+        waiters, self._waiters = self._waiters, []
+        for f in waiters:
+            if not f.done():
+                f.set_result(None)
+
+    async def wait_change(self, timeout: float) -> None:
+        """Sleep until the next mutation (or timeout)."""
+        if timeout <= 0:
+            return
+        f = asyncio.get_running_loop().create_future()
+        self._waiters.append(f)
+        try:
+            await asyncio.wait_for(f, timeout)
+        except asyncio.TimeoutError:
+            pass
+
+    def put(self, kind: str, key: str, obj: dict, expect_rv: str | None = None) -> dict:
+        table = self.objs.setdefault(kind, {})
+        old = table.get(key)
+        if expect_rv is not None and old is not None and old["metadata"].get("resourceVersion") != expect_rv:
+            raise Conflict(f"{kind}/{key}: resourceVersion {expect_rv} is stale")
+        self.rv += 1
+        md = obj.setdefault("metadata", {})
+        md["resourceVersion"] = str(self.rv)
+        md.setdefault("uid", old["metadata"]["uid"] if old else str(uuid.uuid4()))
+        md.setdefault("creationTimestamp", old["metadata"].get("creationTimestamp") if old else now_iso())
+        table[key] = obj
+        self._notify(kind, "MODIFIED" if old else "ADDED", obj)
+        return obj
+
+    def patch(self, kind: str, key: str, fn: Callable[[dict], None]) -> dict | None:
+        cur = self.get(kind, key)
+        if cur is None:
+            return None
+        new = copy.deepcopy(cur)
+        fn(new)
+        return self.put(kind, key, new)
+
+    def delete(self, kind: str, key: str) -> dict | None:
+        table = self.objs.get(kind, {})
+        old = table.pop(key, None)
+        if old is not None:
+            self.rv += 1
+            old = copy.deepcopy(old)
+            old["metadata"]["resourceVersion"] = str(self.rv)
+            self._notify(kind, "DELETED", old)
+        return old
+
+    # ---- watch ------------------------------------------------------------------------
+    def events_since(self, since: int, kind: str | None, pred: Callable[[dict], bool] | None = None) -> list[dict]:
+        out = []
+        for rv, k, etype, obj in reversed(self.history):  # newest first; stop at `since`
+            if rv <= since:
+                break
+            if (kind is None or k == kind) and (pred is None or pred(obj)):
+                out.append({"type": etype, "kind": k, "object": obj, "resourceVersion": rv})
+        out.reverse()
+        return out
+
+    async def wait_events(self, since: int, kind: str | None, timeout: float,
+                          pred: Callable[[dict], bool] | None = None) -> list[dict]:
+        deadline = time.monotonic() + timeout
+        while True:
+            ev = self.events_since(since, kind, pred)
+            left = deadline - time.monotonic()
+            if ev or left <= 0:
+                return ev
+            await self.wait_change(left)
+
+    async def wait_until(self, cond: Callable[[], Any], timeout: float) -> Any:
+        """Long-poll helper: re-evaluate `cond` after every mutation until truthy or timeout."""
+        deadline = time.monotonic() + timeout
+        while True:
+            v = cond()
+            left = deadline - time.monotonic()
+            if v or left <= 0:
+                return v
+            await self.wait_change(min(left, 1.0))
+
+    # ---- persistence ------------------------------------------------------------------
+    def snapshot(self, path) -> None:
+        atomic_write_json(path, {"rv": self.rv, "objs": self.objs})
+
+    def restore(self, path) -> bool:
+        d = read_json(path)
+        if not d:
+            return False
+        self.rv = int(d.get("rv", 0))
+        self.objs = d.get("objs", {})
+        return True

@@ -1,0 +1,231 @@
+"""Local bare-metal provider: worker "machines" are sandboxes on this MI355X host.
+
+Replaces the Triton KVM of terraform/master/main.tf:1-11 / terraform/host/main.tf:1-11:
+
+* a machine = a sandbox directory (``<state>/machines/<name>``) + its own loopback IP (one per
+  network, from 127.0.<net>.0/24) + an exclusive slice of the host's GPUs (by package shape);
+* ``networks()`` are loopback subnets; the default ``local-public`` plays Joyent-SDC-Public;
+* ``packages()`` are worker shapes of the 8x MI355X node (``mi355x-<k>gpu``); the default
+  ``mi355x-1gpu`` gives 8 workers x 1 GPU = all 8 GPUs allocatable (BASELINE.json configs 3-5).
+  The master never takes GPUs (it only runs the control plane, like rancher/server).
+* ``exec`` runs a command in the sandbox (remote-exec), ``delete_machine`` kills every process
+  group recorded under the sandbox and frees its IPs and GPUs.
+
+IP/GPU allocation is serialised by an flock on ``<state>/alloc.lock`` so concurrent creates
+(the Terraform fan-out) are race-free.
+"""
+from __future__ import annotations
+
+import getpass
+import ipaddress
+import os
+import shutil
+import socket
+import subprocess
+import uuid
+from pathlib import Path
+
+from ..models.hostinfo import discover
+from ..utils.fsutil import atomic_write_json, file_lock, read_json
+from ..utils.procs import kill_pidfile
+from . import keys
+from .base import Machine, Network, Package, Provider, ProvisionError
+
+_NS = uuid.UUID("5f1c0d3e-8a4b-4c6e-9b1a-7e2f3d4c5b6a")
+
+NETWORKS = [
+    ("local-fabric", "127.0.2.0/24", False),
+    ("local-public", "127.0.1.0/24", True),
+    ("local-storage", "127.0.3.0/24", False),
+]
+# (name, gpus) ; cpus/memory derived from the host
+SHAPES = [("cpu-only", 0), ("mi355x-1gpu", 1), ("mi355x-2gpu", 2), ("mi355x-4gpu", 4), ("mi355x-8gpu", 8)]
+
+
+def _uid(kind: str, name: str) -> str:
+    return str(uuid.uuid5(_NS, f"tk8s/{kind}/{name}"))
+
+
+def _loopback_multi_ok() -> bool:
+    """Can we bind non-127.0.0.1 loopback addresses (true on stock Linux)?"""
+    if os.environ.get("TK8S_SINGLE_IP") == "1":
+        return False
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    try:
+        s.bind(("127.0.1.254", 0))
+        return True
+    except OSError:
+        return False
+    finally:
+        s.close()
+
+
+class LocalProvider(Provider):
+    name = "local"
+    default_network = "local-public"
+    default_package = "mi355x-1gpu"
+
+    def __init__(self, state_dir: str | os.PathLike, key_dir: str | os.PathLike | None = None):
+        self.state_dir = Path(state_dir).resolve()
+        self.machines_dir = self.state_dir / "machines"
+        self.key_dir = Path(key_dir) if key_dir else self.state_dir / "keys"
+        self.alloc_file = self.state_dir / "alloc.json"
+        self.lock_file = self.state_dir / "alloc.lock"
+        self._multi_ip = None
+
+    # ---- inventory ----------------------------------------------------------------
+    def env(self) -> dict[str, str]:
+        _, _, fp = keys.ensure_cluster_key(self.key_dir)
+        return {
+            "SDC_URL": f"local://{socket.gethostname()}",
+            "SDC_ACCOUNT": getpass.getuser(),
+            "SDC_KEY_ID": fp,
+        }
+
+    def find_key(self, key_id: str) -> str | None:
+        return keys.find_key(key_id, [self.key_dir, "~/.ssh"])
+
+    def networks(self) -> list[Network]:
+        return sorted((Network(n, _uid("network", n), subnet, pub) for n, subnet, pub in NETWORKS),
+                      key=lambda x: x.name)
+
+    def packages(self) -> list[Package]:
+        cpus = os.cpu_count() or 8
+        try:
+            mem_mb = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES") // 2**20
+        except (ValueError, OSError):
+            mem_mb = 64 * 1024
+        out = []
+        for name, g in SHAPES:
+            share = max(g, 1) / 8
+            out.append(Package(name, _uid("package", name), gpus=g, cpus=max(1, int(cpus * share)),
+                               memory_mb=int(mem_mb * share),
+                               description=f"{g}x MI355X (gfx950) worker" if g else "CPU-only worker"))
+        return sorted(out, key=lambda p: p.name)
+
+    # ---- allocation ---------------------------------------------------------------
+    def _multi(self) -> bool:
+        if self._multi_ip is None:
+            self._multi_ip = _loopback_multi_ok()
+        return self._multi_ip
+
+    def _alloc_ips(self, alloc: dict, name: str, nets: list[Network]) -> list[str]:
+        used = alloc.setdefault("ips", {})
+        out = []
+        for net in nets:
+            if not self._multi():
+                out.append("127.0.0.1")
+                continue
+            subnet = ipaddress.ip_network(net.subnet)
+            for host in subnet.hosts():
+                ip = str(host)
+                if ip not in used:
+                    used[ip] = name
+                    out.append(ip)
+                    break
+            else:
+                raise ProvisionError(f"network {net.name} exhausted")
+        return out
+
+    def _alloc_gpus(self, alloc: dict, name: str, count: int) -> list[int]:
+        if count == 0:
+            return []
+        inv = discover()
+        taken = {int(k) for k in alloc.setdefault("gpus", {})}
+        free = [g.ordinal for g in inv.gpus if g.ordinal not in taken]
+        if len(free) < count:
+            raise ProvisionError(
+                f"{name}: package needs {count} GPU(s) but only {len(free)} of {inv.count} are free "
+                "(the local analogue of reaching the provisioning limit)")
+        try:
+            from ..ops import topo
+
+            n = inv.count
+            from ..agent.deviceplugin import link_matrix
+
+            res = topo().preferred_allocation(n, link_matrix(inv.links), free, [], count)
+            pick = list(res["devices"])
+        except Exception:  # noqa: BLE001 - allocator module optional at provision time
+            pick = free[:count]
+        for g in pick:
+            alloc["gpus"][str(g)] = name
+        return pick
+
+    # ---- lifecycle ----------------------------------------------------------------
+    def create_machine(self, name: str, package: str, networks: list[str], image: str = "",
+                       root_authorized_keys: str = "", tags: dict | None = None) -> Machine:
+        pkg = self.package_by_id_or_name(package)
+        nets = [self.network_by_id_or_name(n) for n in networks] or [self.network_by_id_or_name(self.default_network)]
+        role = (tags or {}).get("role", "host")
+        sandbox = self.machines_dir / name
+        with file_lock(self.lock_file):
+            alloc = read_json(self.alloc_file, {}) or {}
+            if name in alloc.get("machines", {}):
+                raise ProvisionError(f"machine {name} already exists")
+            ips = self._alloc_ips(alloc, name, nets)
+            gpus = self._alloc_gpus(alloc, name, 0 if role == "master" else pkg.gpus)
+            alloc.setdefault("machines", {})[name] = {"ips": ips, "gpus": gpus}
+            atomic_write_json(self.alloc_file, alloc)
+        for sub in ("run", "logs", "pods", "etc"):
+            (sandbox / sub).mkdir(parents=True, exist_ok=True)
+        if root_authorized_keys:
+            (sandbox / "etc" / "authorized_keys").write_text(root_authorized_keys.rstrip() + "\n")
+        m = Machine(name=name, id=_uid("machine", f"{name}/{ips[0]}"), package=pkg.name,
+                    networks=[n.id for n in nets], primaryip=ips[0], ips=ips, gpus=gpus, image=image,
+                    tags=dict(tags or {}), sandbox=str(sandbox))
+        atomic_write_json(sandbox / "machine.json", m.to_dict())
+        return m
+
+    def get_machine(self, name: str) -> Machine | None:
+        d = read_json(self.machines_dir / name / "machine.json")
+        return Machine.from_dict(d) if d else None
+
+    def list_machines(self) -> list[Machine]:
+        out = []
+        if self.machines_dir.is_dir():
+            for d in sorted(self.machines_dir.iterdir()):
+                m = self.get_machine(d.name)
+                if m:
+                    out.append(m)
+        return out
+
+    def machine_env(self, m: Machine) -> dict[str, str]:
+        return {
+            "TK8S_MACHINE": m.name,
+            "TK8S_MACHINE_DIR": m.sandbox,
+            "TK8S_MACHINE_IP": m.primaryip,
+            "TK8S_MACHINE_GPUS": ",".join(map(str, m.gpus)),
+            "TK8S_MACHINE_PACKAGE": m.package,
+        }
+
+    def exec(self, machine: Machine, command: str, timeout: float = 300, env: dict | None = None) -> tuple[int, str]:
+        e = dict(os.environ)
+        e.update(self.machine_env(machine))
+        e.update(env or {})
+        try:
+            r = subprocess.run(["bash", "-c", command], cwd=machine.sandbox, env=e, capture_output=True,
+                               text=True, timeout=timeout)
+        except subprocess.TimeoutExpired as ex:
+            return 124, f"timeout after {timeout}s: {ex}"
+        return r.returncode, (r.stdout or "") + (r.stderr or "")
+
+    def delete_machine(self, machine: Machine) -> None:
+        sandbox = Path(machine.sandbox or self.machines_dir / machine.name)
+        run = sandbox / "run"
+        if run.is_dir():
+            for pidfile in sorted(run.glob("*.pid")):
+                kill_pidfile(pidfile, grace=2.0)
+        # pods write their pidfiles under pods/<pod>/pid
+        pods = sandbox / "pods"
+        if pods.is_dir():
+            for pidfile in sorted(pods.glob("*/*.pid")):
+                kill_pidfile(pidfile, grace=1.0)
+        with file_lock(self.lock_file):
+            alloc = read_json(self.alloc_file, {}) or {}
+            alloc.get("machines", {}).pop(machine.name, None)
+            for k in ("ips", "gpus"):
+                table = alloc.get(k, {})
+                for key in [key for key, owner in table.items() if owner == machine.name]:
+                    del table[key]
+            atomic_write_json(self.alloc_file, alloc)
+        shutil.rmtree(sandbox, ignore_errors=True)

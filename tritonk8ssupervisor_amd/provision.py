@@ -1,0 +1,290 @@
+"""Provisioning engine: a Terraform-compatible subset over the tk8s providers (L3a).
+
+Reads the generated root config ``terraform/rancher.tf`` (setup.sh:145-152) and the module
+definitions ``terraform/{master,host}/*.tf``; commands mirror what setup.sh runs:
+
+  get      — resolve module sources into .terraform/modules   (setup.sh:156 `terraform get`)
+  plan     — diff desired resources against terraform.tfstate  (BASELINE.json config 1)
+  apply    — create machines concurrently, run their provisioners (setup.sh:157)
+  destroy  — delete every machine in the state                 (setup.sh:501 `destroy -force`)
+
+Differences from the reference's Terraform usage:
+  * parallelism defaults to ALL resources at once (Terraform's default is 10);
+  * local-exec provisioners are serialised and the .ip hand-off files are rewritten in module
+    order after apply (no nondeterministic `>>` interleaving, terraform/*/main.tf:30);
+  * idempotent creates are retried (``retries``) and failures leave a "tainted" state entry;
+  * every step is timed into the event log.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+from . import hcl
+from .provider.base import Machine, Provider, ProvisionError
+from .utils.events import EventLog
+from .utils.fsutil import atomic_write, atomic_write_json, file_lock, read_json
+from .utils.faults import fault
+
+STATE_FILE = "terraform.tfstate"
+RESOURCE_TYPE = "tk8s_machine"
+
+
+@dataclass
+class ResourceSpec:
+    address: str          # module.<name>.tk8s_machine.<rname>
+    module: str
+    source: str
+    rname: str
+    attrs: dict           # interpolated machine attributes
+    provisioners: list    # hcl.Block list (unevaluated: they reference the created machine)
+    module_dir: Path
+
+
+@dataclass
+class PlanAction:
+    address: str
+    action: str           # create | no-op | destroy | replace
+    attrs: dict = field(default_factory=dict)
+
+
+@dataclass
+class ApplyResult:
+    created: list[str] = field(default_factory=list)
+    unchanged: list[str] = field(default_factory=list)
+    failed: dict[str, str] = field(default_factory=dict)
+    seconds: float = 0.0
+
+    @property
+    def ok(self) -> bool:
+        return not self.failed
+
+
+class Engine:
+    def __init__(self, tf_dir: str | os.PathLike, provider: Provider, events: EventLog | None = None,
+                 parallelism: int | None = None, retries: int = 1):
+        self.dir = Path(tf_dir).resolve()
+        self.provider = provider
+        self.events = events or EventLog(None)
+        self.parallelism = parallelism
+        self.retries = retries
+        self._state_lock = threading.Lock()
+        self._exec_lock = threading.Lock()
+
+    # ---- config ----------------------------------------------------------------------
+    def root(self) -> hcl.Block:
+        f = self.dir / "rancher.tf"
+        if not f.exists():
+            raise ProvisionError(f"{f} not found (run setup first)")
+        return hcl.parse_file(f)
+
+    def get(self) -> list[str]:
+        """`terraform get`: link each module source into .terraform/modules/<name>."""
+        mods = []
+        mdir = self.dir / ".terraform" / "modules"
+        mdir.mkdir(parents=True, exist_ok=True)
+        for m in self.root().children("module"):
+            name = m.labels[0]
+            src = (self.dir / str(m.attrs["source"])).resolve()
+            if not src.is_dir():
+                raise ProvisionError(f"module {name}: source {src} not found")
+            link = mdir / name
+            if link.is_symlink() or link.exists():
+                link.unlink()
+            link.symlink_to(src)
+            mods.append(name)
+        return mods
+
+    def specs(self) -> list[ResourceSpec]:
+        out = []
+        for m in self.root().children("module"):
+            name = m.labels[0]
+            src = (self.dir / str(m.attrs["source"])).resolve()
+            mod = hcl.parse_dir(src)
+            variables = {}
+            for v in mod.children("variable"):
+                vname = v.labels[0]
+                if vname in m.attrs:
+                    variables[vname] = hcl.interpolate(m.attrs[vname], {"__dir__": str(self.dir)})
+                elif "default" in v.attrs:
+                    variables[vname] = v.attrs["default"]
+                else:
+                    raise ProvisionError(f"module {name}: required variable {vname!r} not set")
+            unknown = set(m.attrs) - {"source"} - set(variables)
+            if unknown:
+                raise ProvisionError(f"module {name}: unknown arguments {sorted(unknown)}")
+            ctx = {"var": variables, "__dir__": str(src)}
+            for r in mod.children("resource"):
+                rtype, rname = r.labels
+                if rtype != RESOURCE_TYPE:
+                    raise ProvisionError(f"module {name}: unsupported resource type {rtype}")
+                attrs = {k: hcl.interpolate(v, ctx) for k, v in r.attrs.items()}
+                if isinstance(attrs.get("networks"), str):
+                    attrs["networks"] = [x for x in attrs["networks"].split(",") if x]
+                out.append(ResourceSpec(f"module.{name}.{rtype}.{rname}", name, str(m.attrs["source"]),
+                                        rname, attrs, r.children("provisioner"), src))
+        return out
+
+    # ---- state -----------------------------------------------------------------------
+    def state(self) -> dict:
+        return read_json(self.dir / STATE_FILE, None) or {"version": 1, "resources": {}}
+
+    def _save_resource(self, address: str, rec: dict | None) -> None:
+        with self._state_lock, file_lock(self.dir / ".tfstate.lock"):
+            st = self.state()
+            if rec is None:
+                st["resources"].pop(address, None)
+            else:
+                st["resources"][address] = rec
+            st["serial"] = st.get("serial", 0) + 1
+            atomic_write_json(self.dir / STATE_FILE, st)
+
+    # ---- plan ------------------------------------------------------------------------
+    def plan(self) -> list[PlanAction]:
+        st = self.state()["resources"]
+        want = {s.address: s for s in self.specs()}
+        acts = []
+        for addr, s in want.items():
+            cur = st.get(addr)
+            if cur is None:
+                acts.append(PlanAction(addr, "create", s.attrs))
+            elif cur.get("tainted"):
+                acts.append(PlanAction(addr, "replace", s.attrs))
+            else:
+                acts.append(PlanAction(addr, "no-op", s.attrs))
+        for addr in st:
+            if addr not in want:
+                acts.append(PlanAction(addr, "destroy"))
+        return acts
+
+    @staticmethod
+    def plan_summary(acts: list[PlanAction]) -> str:
+        add = sum(a.action in ("create", "replace") for a in acts)
+        destroy = sum(a.action in ("destroy", "replace") for a in acts)
+        lines = [f"  {'+' if a.action == 'create' else '-/+' if a.action == 'replace' else '-' if a.action == 'destroy' else ' '} {a.address}"
+                 for a in acts if a.action != "no-op"]
+        lines.append(f"Plan: {add} to add, 0 to change, {destroy} to destroy.")
+        return "\n".join(lines)
+
+    # ---- apply -----------------------------------------------------------------------
+    def _provision(self, spec: ResourceSpec, m: Machine) -> None:
+        ctx = {"var": {}, RESOURCE_TYPE: {spec.rname: m.to_dict()}, "self": m.to_dict(), "__dir__": str(spec.module_dir)}
+        for p in spec.provisioners:
+            kind = p.labels[0] if p.labels else ""
+            if kind == "remote-exec":
+                for cmd in hcl.interpolate(p.attrs.get("inline", []), ctx):
+                    rc, out = self.provider.exec(m, cmd)
+                    if rc != 0:
+                        raise ProvisionError(f"{spec.address}: remote-exec {cmd!r} failed rc={rc}: {out.strip()[-400:]}")
+            elif kind == "local-exec":
+                cmd = hcl.interpolate(p.attrs["command"], ctx)
+                with self._exec_lock:
+                    r = subprocess.run(["bash", "-c", cmd], cwd=self.dir, capture_output=True, text=True, timeout=300)
+                if r.returncode != 0:
+                    raise ProvisionError(f"{spec.address}: local-exec {cmd!r} failed: {r.stderr.strip()}")
+            else:
+                raise ProvisionError(f"{spec.address}: unsupported provisioner {kind!r}")
+
+    def _create(self, spec: ResourceSpec) -> Machine:
+        a = spec.attrs
+        last_err: Exception | None = None
+        for attempt in range(1, self.retries + 2):
+            t = time.monotonic()
+            try:
+                if fault("provision.create", a["name"]) and attempt == 1:
+                    raise ProvisionError(f"injected create failure for {a['name']}")
+                pub = a.get("root_authorized_keys", "")
+                m = self.provider.create_machine(a["name"], a["package"], list(a.get("networks", [])),
+                                                 image=a.get("image", ""), root_authorized_keys=pub,
+                                                 tags=a.get("tags", {}))
+            except ProvisionError as e:
+                last_err = e
+                self.events.emit("machine_create_retry", address=spec.address, attempt=attempt, error=str(e))
+                continue
+            try:
+                self._provision(spec, m)
+            except Exception as e:  # tainted: machine exists but bootstrap failed
+                self._save_resource(spec.address, {"module": spec.module, "machine": m.to_dict(), "tainted": True,
+                                                   "error": str(e)})
+                raise
+            self._save_resource(spec.address, {"module": spec.module, "machine": m.to_dict(), "tainted": False})
+            self.events.emit("machine_created", address=spec.address, name=m.name, ip=m.primaryip,
+                             gpus=m.gpus, seconds=round(time.monotonic() - t, 6))
+            return m
+        raise ProvisionError(f"{spec.address}: create failed after {self.retries + 1} attempts: {last_err}")
+
+    def apply(self) -> ApplyResult:
+        t0 = time.monotonic()
+        res = ApplyResult()
+        specs = self.specs()
+        st = self.state()["resources"]
+        todo = []
+        for s in specs:
+            cur = st.get(s.address)
+            if cur and not cur.get("tainted"):
+                res.unchanged.append(s.address)
+                continue
+            if cur and cur.get("tainted"):
+                self.provider.delete_machine(Machine.from_dict(cur["machine"]))
+                self._save_resource(s.address, None)
+            todo.append(s)
+        workers = self.parallelism or max(1, len(todo))
+        with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+            futs = {ex.submit(self._create, s): s for s in todo}
+            for f in cf.as_completed(futs):
+                s = futs[f]
+                try:
+                    f.result()
+                    res.created.append(s.address)
+                except Exception as e:  # noqa: BLE001 - report per resource
+                    res.failed[s.address] = str(e)
+                    self.events.emit("machine_failed", address=s.address, error=str(e))
+        self.write_ip_files(specs)
+        res.seconds = time.monotonic() - t0
+        return res
+
+    def write_ip_files(self, specs: list[ResourceSpec] | None = None) -> None:
+        """Rewrite masters.ip / hosts.ip in module order from the state (race-free hand-off)."""
+        specs = specs if specs is not None else self.specs()
+        st = self.state()["resources"]
+        files: dict[str, list[str]] = {"masters.ip": [], "hosts.ip": []}
+        for s in specs:
+            rec = st.get(s.address)
+            if not rec or rec.get("tainted"):
+                continue
+            key = "masters.ip" if s.source.rstrip("/").endswith("master") else "hosts.ip"
+            files[key].append(rec["machine"]["primaryip"])
+        for name, ips in files.items():
+            if ips:
+                atomic_write(self.dir / name, "".join(ip + "\n" for ip in ips))
+            else:
+                (self.dir / name).unlink(missing_ok=True)
+
+    def machines(self) -> dict[str, Machine]:
+        """Created machines keyed by module name (tainted ones excluded)."""
+        out = {}
+        for rec in self.state()["resources"].values():
+            if not rec.get("tainted"):
+                m = Machine.from_dict(rec["machine"])
+                out[rec["module"]] = m
+        return out
+
+    # ---- destroy ---------------------------------------------------------------------
+    def destroy(self) -> list[str]:
+        st = self.state()["resources"]
+        gone = []
+
+        def one(addr: str, rec: dict) -> str:
+            self.provider.delete_machine(Machine.from_dict(rec["machine"]))
+            self._save_resource(addr, None)
+            return addr
+
+        with cf.ThreadPoolExecutor(max_workers=max(1, len(st))) as ex:
+            for f in cf.as_completed([ex.submit(one, a, r) for a, r in st.items()]):
+                gone.append(f.result())
+        return gone

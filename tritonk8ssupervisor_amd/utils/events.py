@@ -1,0 +1,60 @@
+"""JSONL event log with monotonic per-phase timestamps.
+
+The reference never measures its own bring-up (no timers); phases here are
+timed so the BASELINE metric (``./setup.sh`` -> all nodes Ready) falls out of the log.
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import os
+import threading
+import time
+from pathlib import Path
+from typing import Any, Iterator
+
+_lock = threading.Lock()
+
+
+class EventLog:
+    def __init__(self, path: str | os.PathLike | None, echo: bool = False):
+        self.path = Path(path) if path else None
+        self.echo = echo
+        self.t0 = time.monotonic()
+        self.phases: dict[str, float] = {}
+        if self.path:
+            self.path.parent.mkdir(parents=True, exist_ok=True)
+
+    def emit(self, event: str, **fields: Any) -> dict:
+        rec = {"ts": time.time(), "t": round(time.monotonic() - self.t0, 6), "event": event, **fields}
+        if self.path:
+            line = json.dumps(rec, sort_keys=True, default=str)
+            with _lock, open(self.path, "a") as f:
+                f.write(line + "\n")
+        if self.echo:
+            print(f"[{rec['t']:8.3f}s] {event} " + " ".join(f"{k}={v}" for k, v in fields.items()), flush=True)
+        return rec
+
+    @contextlib.contextmanager
+    def phase(self, name: str, **fields: Any) -> Iterator[None]:
+        t = time.monotonic()
+        self.emit("phase_start", phase=name, **fields)
+        ok = False
+        try:
+            yield
+            ok = True
+        finally:
+            dt = time.monotonic() - t
+            self.phases[name] = dt
+            self.emit("phase_end", phase=name, seconds=round(dt, 6), ok=ok)
+
+
+def read_events(path: str | os.PathLike) -> list[dict]:
+    out = []
+    with contextlib.suppress(FileNotFoundError):
+        with open(path) as f:
+            for line in f:
+                line = line.strip()
+                if line:
+                    out.append(json.loads(line))
+    return out

@@ -1,0 +1,84 @@
+"""Race-free filesystem helpers.
+
+The reference appends machine IPs from concurrent Terraform provisioners with ``>>``
+(terraform/master/main.tf:29-31), so ``masters.ip``/``hosts.ip`` order is nondeterministic
+(SURVEY.md §5.2). Everything here is atomic (tmp + rename) or serialised by an flock.
+"""
+from __future__ import annotations
+
+import contextlib
+import fcntl
+import json
+import os
+import tempfile
+from pathlib import Path
+from typing import Any, Iterator
+
+
+def atomic_write(path: str | os.PathLike, data: str | bytes, mode: int | None = None) -> None:
+    """Write ``data`` to ``path`` atomically (readers see the old or the new file, never half)."""
+    p = Path(path)
+    p.parent.mkdir(parents=True, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(prefix=f".{p.name}.", suffix=".tmp", dir=p.parent)
+    try:
+        with os.fdopen(fd, "wb") as f:
+            f.write(data.encode() if isinstance(data, str) else data)
+            f.flush()
+            os.fsync(f.fileno())
+        if mode is not None:
+            os.chmod(tmp, mode)
+        os.replace(tmp, p)
+    except BaseException:
+        with contextlib.suppress(FileNotFoundError):
+            os.unlink(tmp)
+        raise
+
+
+def atomic_write_json(path: str | os.PathLike, obj: Any) -> None:
+    atomic_write(path, json.dumps(obj, indent=2, sort_keys=True) + "\n")
+
+
+def read_json(path: str | os.PathLike, default: Any = None) -> Any:
+    try:
+        with open(path, "rb") as f:
+            return json.loads(f.read() or b"null")
+    except FileNotFoundError:
+        return default
+
+
+@contextlib.contextmanager
+def file_lock(path: str | os.PathLike) -> Iterator[None]:
+    """Exclusive advisory lock on ``path`` (created if missing)."""
+    p = Path(path)
+    p.parent.mkdir(parents=True, exist_ok=True)
+    with open(p, "a+") as f:
+        fcntl.flock(f.fileno(), fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f.fileno(), fcntl.LOCK_UN)
+
+
+def locked_append_line(path: str | os.PathLike, line: str) -> None:
+    """Append one line under a lock (the safe form of ``echo ip >> hosts.ip``)."""
+    p = Path(path)
+    with file_lock(str(p) + ".lock"):
+        with open(p, "a") as f:
+            f.write(line.rstrip("\n") + "\n")
+            f.flush()
+
+
+def remove_paths(paths: list[str | os.PathLike]) -> list[str]:
+    """rm -rf each path; returns the ones that existed."""
+    import shutil
+
+    removed = []
+    for p in paths:
+        p = Path(p)
+        if p.is_symlink() or p.is_file():
+            p.unlink()
+            removed.append(str(p))
+        elif p.is_dir():
+            shutil.rmtree(p, ignore_errors=True)
+            removed.append(str(p))
+    return removed

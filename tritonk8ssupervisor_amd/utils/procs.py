@@ -1,0 +1,103 @@
+"""Daemon process management (the local analogue of `docker run -d --restart=unless-stopped`).
+
+Daemons run in their own session/process group so teardown can signal the whole tree, and
+their pid/pgid is recorded in a pidfile under the owning machine's sandbox. Nothing here ever
+uses ``os.exec*`` in-process: every program starts as a child (the GPU-box rule that processes
+which initialised the GPU must not exec; spawners here never touch the GPU anyway).
+"""
+from __future__ import annotations
+
+import contextlib
+import errno
+import json
+import os
+import signal
+import subprocess
+import time
+from pathlib import Path
+
+
+def spawn_daemon(argv: list[str], *, env: dict | None = None, cwd: str | None = None,
+                 log_path: str | None = None, pidfile: str | None = None) -> subprocess.Popen:
+    log = open(log_path, "ab", buffering=0) if log_path else subprocess.DEVNULL
+    try:
+        p = subprocess.Popen(argv, env=env, cwd=cwd, stdin=subprocess.DEVNULL, stdout=log,
+                             stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
+    finally:
+        if log_path:
+            log.close()
+    if pidfile:
+        Path(pidfile).parent.mkdir(parents=True, exist_ok=True)
+        from .fsutil import atomic_write_json
+
+        atomic_write_json(pidfile, {"pid": p.pid, "pgid": p.pid, "argv": argv, "started": time.time()})
+    return p
+
+
+def pid_alive(pid: int) -> bool:
+    if pid <= 0:
+        return False
+    try:
+        os.kill(pid, 0)
+    except OSError as e:
+        return e.errno == errno.EPERM
+    # a zombie child of ours still "exists"; reap if possible
+    with contextlib.suppress(ChildProcessError, OSError):
+        r, _ = os.waitpid(pid, os.WNOHANG)
+        if r == pid:
+            return False
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(")")[-1].split()[0] != "Z"
+    except OSError:
+        return True
+
+
+def read_pidfile(pidfile: str | os.PathLike) -> dict | None:
+    try:
+        return json.loads(Path(pidfile).read_text())
+    except (OSError, ValueError):
+        return None
+
+
+def kill_group(pgid: int, grace: float = 3.0) -> bool:
+    """SIGTERM the process group, wait up to `grace` s, then SIGKILL. True if it was alive."""
+    try:
+        os.killpg(pgid, signal.SIGTERM)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return False
+    deadline = time.monotonic() + grace
+    while time.monotonic() < deadline:
+        try:
+            os.killpg(pgid, 0)
+        except ProcessLookupError:
+            return True
+        with contextlib.suppress(ChildProcessError, OSError):
+            os.waitpid(-pgid, os.WNOHANG)
+        time.sleep(0.02)
+    with contextlib.suppress(ProcessLookupError, PermissionError):
+        os.killpg(pgid, signal.SIGKILL)
+    return True
+
+
+def kill_pidfile(pidfile: str | os.PathLike, grace: float = 3.0) -> bool:
+    info = read_pidfile(pidfile)
+    if not info:
+        return False
+    alive = kill_group(int(info.get("pgid") or info["pid"]), grace)
+    with contextlib.suppress(FileNotFoundError):
+        Path(pidfile).unlink()
+    return alive
+
+
+def wait_for_file_text(path: str | os.PathLike, needle: str, timeout: float, interval: float = 0.01) -> bool:
+    """Poll a log file until it contains `needle` (the `docker logs | grep "Listening on"` wait)."""
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        with contextlib.suppress(OSError):
+            if needle in Path(path).read_text(errors="replace"):
+                return True
+        time.sleep(interval)
+    return False
