@@ -1,0 +1,144 @@
+// tk8s-supervise: restart-policy process supervisor (the `docker run --restart=unless-stopped`
+// of the reference's rancher/server and rancher/agent containers,
+// ansible/roles/ranchermaster/tasks/main.yml:11, rancherhost/tasks/main.yml:26-34).
+//
+//   tk8s-supervise --pidfile F [--log L] [--restart no|on-failure|always|unless-stopped]
+//                  [--max-restarts N] [--backoff-ms M] -- PROGRAM [ARGS...]
+//
+// * Starts a new session; the child stays in the supervisor's process group, so one
+//   killpg(pgid) from teardown stops both.
+// * SIGTERM/SIGINT: stop restarting, forward SIGTERM to the child, wait, exit with its code.
+// * Child exit: restart per policy with capped exponential back-off (reset after 10 s up).
+// * Pidfile (JSON, atomic rename): {"pid": supervisor, "pgid": pgid, "child": child, "restarts": n}.
+// Pure POSIX (no HIP): it never touches the GPU, so it may spawn freely.
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+volatile sig_atomic_t g_stop = 0;
+volatile pid_t g_child = -1;
+
+void on_signal(int) {
+  g_stop = 1;
+  if (g_child > 0) kill(g_child, SIGTERM);
+}
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+void write_pidfile(const std::string& path, pid_t child, int restarts) {
+  if (path.empty()) return;
+  const std::string tmp = path + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "w");
+  if (!f) return;
+  std::fprintf(f, "{\"pid\": %d, \"pgid\": %d, \"child\": %d, \"restarts\": %d, \"supervisor\": \"tk8s-supervise\"}\n",
+               static_cast<int>(getpid()), static_cast<int>(getpgrp()), static_cast<int>(child), restarts);
+  std::fclose(f);
+  std::rename(tmp.c_str(), path.c_str());
+}
+
+int usage() {
+  std::fprintf(stderr,
+               "usage: tk8s-supervise --pidfile F [--log L] [--restart no|on-failure|always|unless-stopped]\n"
+               "                      [--max-restarts N] [--backoff-ms M] -- PROGRAM [ARGS...]\n");
+  return 2;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string pidfile, log, policy = "unless-stopped";
+  long max_restarts = -1, backoff_ms = 100;
+  int i = 1;
+  for (; i < argc; ++i) {
+    const std::string a = argv[i];
+    if (a == "--") { ++i; break; }
+    if (i + 1 >= argc) return usage();
+    if (a == "--pidfile") pidfile = argv[++i];
+    else if (a == "--log") log = argv[++i];
+    else if (a == "--restart") policy = argv[++i];
+    else if (a == "--max-restarts") max_restarts = std::strtol(argv[++i], nullptr, 10);
+    else if (a == "--backoff-ms") backoff_ms = std::strtol(argv[++i], nullptr, 10);
+    else return usage();
+  }
+  if (i >= argc) return usage();
+  if (policy != "no" && policy != "on-failure" && policy != "always" && policy != "unless-stopped")
+    return usage();
+  std::vector<char*> child_argv(argv + i, argv + argc);
+  child_argv.push_back(nullptr);
+
+  if (getpgrp() != getpid()) setsid();
+  if (!log.empty()) {
+    const int fd = open(log.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+    if (fd >= 0) {
+      dup2(fd, STDOUT_FILENO);
+      dup2(fd, STDERR_FILENO);
+      close(fd);
+    }
+  }
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof sa);
+  sa.sa_handler = on_signal;
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
+  signal(SIGHUP, SIG_IGN);
+
+  int restarts = 0, status = 0;
+  long delay = backoff_ms;
+  while (!g_stop) {
+    const double started = now_s();
+    const pid_t pid = fork();
+    if (pid < 0) {
+      std::perror("tk8s-supervise: fork");
+      return 1;
+    }
+    if (pid == 0) {
+      signal(SIGTERM, SIG_DFL);
+      signal(SIGINT, SIG_DFL);
+      signal(SIGHUP, SIG_DFL);
+      execvp(child_argv[0], child_argv.data());
+      std::fprintf(stderr, "tk8s-supervise: exec %s: %s\n", child_argv[0], std::strerror(errno));
+      _exit(127);
+    }
+    g_child = pid;
+    write_pidfile(pidfile, pid, restarts);
+    while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+    }
+    g_child = -1;
+    const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + WTERMSIG(status);
+    if (g_stop) break;
+    const bool failed = code != 0;
+    const bool again = policy == "always" || policy == "unless-stopped" || (policy == "on-failure" && failed);
+    if (!again || (max_restarts >= 0 && restarts >= max_restarts)) {
+      std::fprintf(stderr, "tk8s-supervise: %s exited with %d; not restarting\n", child_argv[0], code);
+      if (!pidfile.empty()) unlink(pidfile.c_str());
+      return code;
+    }
+    if (now_s() - started > 10.0) delay = backoff_ms;  // it ran fine for a while: reset back-off
+    std::fprintf(stderr, "tk8s-supervise: %s exited with %d; restart #%d in %ld ms\n", child_argv[0], code,
+                 restarts + 1, delay);
+    std::fflush(stderr);
+    timespec ts{delay / 1000, (delay % 1000) * 1000000L};
+    while (nanosleep(&ts, &ts) < 0 && errno == EINTR && !g_stop) {
+    }
+    delay = delay * 2 > 10000 ? 10000 : delay * 2;
+    ++restarts;
+  }
+  if (!pidfile.empty()) unlink(pidfile.c_str());
+  return WIFEXITED(status) ? WEXITSTATUS(status) : 0;
+}

@@ -1,0 +1,14 @@
+#!/usr/bin/env bash
+# MI355X cluster bring-up wizard (same surface as the reference's setup.sh):
+#   ./setup.sh            create: prompts, provisioning, configuration, readiness wait
+#   ./setup.sh -c         teardown: destroy machines and reset configuration
+# Non-interactive: ./setup.sh --answers answers.yaml --yes   (see docs/usage.md)
+set -o errexit
+set -o pipefail
+cd "$(dirname "$0")"
+PY="${TK8S_PYTHON:-python3}"
+if [[ "${1:-}" == "-c" ]]; then
+    shift
+    exec "$PY" -m tritonk8ssupervisor_amd.cli clean "$@"
+fi
+exec "$PY" -m tritonk8ssupervisor_amd.cli setup "$@"

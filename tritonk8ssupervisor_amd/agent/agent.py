@@ -129,7 +129,8 @@ class Agent:
     def _free_devices(self) -> list[str]:
         used = set()
         for pp in self.runtime.running().values():
-            used.update(pp.gpu_ids)
+            if not pp.done.is_set():
+                used.update(pp.gpu_ids)
         return [d["id"] for d in self.plugin.devices() if d["health"] == "Healthy" and d["id"] not in used]
 
     def _start_pod(self, pod: dict) -> None:

@@ -1,0 +1,221 @@
+"""`tk8s` command line: setup / clean / status / provider listings / engines / kubectl.
+
+  ./setup.sh [--answers FILE] [--yes] [--resume] [--timeout S] ...   -> tk8s setup
+  ./setup.sh -c [--yes]                                               -> tk8s clean
+  ./tk8s networks|packages [-l]     (triton networks / triton packages)
+  ./tk8s env                        (triton env)
+  ./tk8s terraform get|plan|apply|destroy     (provisioning engine, in terraform/)
+  ./tk8s ansible-playbook [--check] [-i hosts] clusterUp.yml           (playbook engine)
+  ./tk8s status [--json]            (phases, nodes, GPUs, last RCCL busbw)
+  ./kubectl ...                     (see cli/kubectl.py)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+
+def _ws(args):
+    from ..orchestrator import Workspace
+
+    return Workspace(Path(args.workdir).resolve())
+
+
+def cmd_setup(args) -> int:
+    from ..orchestrator import Setup, SetupError
+    from ..wizard import WizardAbort, load_answers
+
+    answers = load_answers(args.answers) if args.answers else None
+    if answers is None and args.nodes:
+        answers = {}
+    if answers is not None:
+        for k in ("nodes", "package", "name", "master_hostname", "node_prefix"):
+            v = getattr(args, k, None)
+            if v is not None:
+                answers[k] = v
+    s = Setup(_ws(args), answers=answers, assume_yes=args.yes, resume=args.resume, timeout=args.timeout,
+              validate=not args.no_validate, rccl=(None if args.rccl is None else args.rccl == "on"),
+              quiet_ansible=not args.verbose, backend=args.backend, master_port=args.port,
+              hbm_bytes=args.hbm_bytes, md5_bytes=args.md5_bytes, probe_iters=args.probe_iters,
+              node_grace=args.node_grace)
+    try:
+        summary = s.run()
+    except WizardAbort:
+        return 0
+    except SetupError as e:
+        print(str(e), file=sys.stderr)
+        return e.code
+    if args.json:
+        print(json.dumps(summary))
+    return 0
+
+
+def cmd_clean(args) -> int:
+    from ..orchestrator import clean
+
+    return clean(_ws(args), assume_yes=args.yes, backend=args.backend)
+
+
+def cmd_status(args) -> int:
+    ws = _ws(args)
+    st = ws.state()
+    out = {"completed": st.get("completed", []), "timings": st.get("timings", {}), "summary": st.get("summary")}
+    summ = st.get("summary") or {}
+    if summ.get("api"):
+        from ..controlplane.client import Client
+
+        try:
+            out["cluster"] = Client(summ["api"], timeout=5).get("/v1/cluster/status", query={"project": summ.get("project")})
+        except Exception as e:  # noqa: BLE001
+            out["cluster"] = {"error": str(e)}
+    if args.json:
+        print(json.dumps(out, indent=1))
+    else:
+        print(f"completed phases: {', '.join(out['completed']) or '-'}")
+        for k, v in out["timings"].items():
+            print(f"  {k:<16} {v:8.3f}s")
+        c = out.get("cluster") or {}
+        if c and "error" not in c:
+            print(f"nodes: {c['nodes_ready']}/{c['nodes']} Ready, {c['nodes_validated']} validated; "
+                  f"amd.com/gpu allocatable {c['gpus_allocatable']} (in use {c['gpus_in_use']})")
+        if summ.get("rccl"):
+            print(f"last RCCL all-reduce: peak busbw {summ['rccl']['peak_busbw_gbps']:.1f} GB/s over {summ['rccl']['nranks']} GPU(s)")
+    return 0
+
+
+def _provider(args):
+    from ..provider import get_provider
+
+    ws = _ws(args)
+    return get_provider(args.backend or os.environ.get("TK8S_BACKEND", "local"), ws.state_dir)
+
+
+def cmd_networks(args) -> int:
+    for n in _provider(args).networks():
+        print(f"{n.name:<20} {n.id}" + (f"  {n.subnet}{'  public' if n.public else ''}" if args.l else ""))
+    return 0
+
+
+def cmd_packages(args) -> int:
+    for p in _provider(args).packages():
+        extra = f"  gpus={p.gpus} cpus={p.cpus} memory={p.memory_mb}M  {p.description}" if args.l else ""
+        print(f"{p.name:<16} {p.id}{extra}")
+    return 0
+
+
+def cmd_env(args) -> int:
+    for k, v in _provider(args).env().items():
+        print(f'export {k}="{v}"')
+    return 0
+
+
+def cmd_terraform(args) -> int:
+    from ..provision import Engine
+
+    ws = _ws(args)
+    eng = Engine(ws.tf, _provider(args))
+    if args.action == "get":
+        print("\n".join(f"- module.{m}" for m in eng.get()))
+    elif args.action == "plan":
+        print(Engine.plan_summary(eng.plan()))
+    elif args.action == "apply":
+        r = eng.apply()
+        print(f"Apply complete! Resources: {len(r.created)} added, 0 changed, 0 destroyed ({r.seconds:.3f}s)")
+        for a, e in r.failed.items():
+            print(f"Error: {a}: {e}", file=sys.stderr)
+        return 0 if r.ok else 1
+    elif args.action == "destroy":
+        print(f"Destroy complete! Resources: {len(eng.destroy())} destroyed.")
+    return 0
+
+
+def cmd_playbook(args) -> int:
+    from ..orchestrator import MachineExecutor
+    from ..playbook import Playbook
+    from ..provision import Engine
+
+    ws = _ws(args)
+    prov = _provider(args)
+    machines = {}
+    if (ws.tf / "terraform.tfstate").exists():
+        machines = Engine(ws.tf, prov).machines()
+    pb = Path(args.playbook)
+    if not pb.is_absolute():
+        pb = ws.ansible / pb
+    inv = Path(args.inventory) if args.inventory else ws.ansible / "hosts"
+    if not inv.is_absolute() and not inv.exists():
+        inv = ws.ansible / inv
+    extra = dict(kv.split("=", 1) for kv in args.extra_vars) if args.extra_vars else {}
+    res = Playbook(pb, inv, executor=MachineExecutor(prov, machines) if machines else None, extra_vars=extra,
+                   check=args.check).run()
+    return 0 if res.ok else 2
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="tk8s", description="MI355X-native cluster bring-up")
+    ap.add_argument("--workdir", default=os.environ.get("TK8S_WORKDIR", os.getcwd()))
+    ap.add_argument("--backend", default=None, help="local (default) or triton")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+
+    s = sub.add_parser("setup", help="create the cluster (./setup.sh)")
+    s.add_argument("--answers", help="YAML/JSON answers file (non-interactive)")
+    s.add_argument("--yes", action="store_true", help="answer yes to the confirmation")
+    s.add_argument("--resume", action="store_true", help="continue a partial run")
+    s.add_argument("--timeout", type=float, default=600.0, help="bound on the readiness wait (s)")
+    s.add_argument("--nodes", type=int)
+    s.add_argument("--package")
+    s.add_argument("--name")
+    s.add_argument("--master-hostname")
+    s.add_argument("--node-prefix")
+    s.add_argument("--port", type=int, default=None)
+    s.add_argument("--no-validate", action="store_true", help="skip the GPU validation DaemonSet")
+    s.add_argument("--rccl", choices=["on", "off"], default=None, help="cluster RCCL all-reduce (default: on if >= 2 GPUs)")
+    s.add_argument("--hbm-bytes", type=int, default=1 << 30)
+    s.add_argument("--md5-bytes", type=int, default=256 << 20)
+    s.add_argument("--probe-iters", type=int, default=3)
+    s.add_argument("--node-grace", type=float, default=5.0)
+    s.add_argument("--json", action="store_true")
+    s.add_argument("-v", "--verbose", action="store_true")
+    s.set_defaults(fn=cmd_setup)
+
+    c = sub.add_parser("clean", help="destroy machines and reset configuration (./setup.sh -c)")
+    c.add_argument("--yes", action="store_true")
+    c.set_defaults(fn=cmd_clean)
+
+    st = sub.add_parser("status")
+    st.add_argument("--json", action="store_true")
+    st.set_defaults(fn=cmd_status)
+
+    for name, fn in (("networks", cmd_networks), ("packages", cmd_packages)):
+        p = sub.add_parser(name)
+        p.add_argument("-l", action="store_true")
+        p.set_defaults(fn=fn)
+    sub.add_parser("env").set_defaults(fn=cmd_env)
+
+    t = sub.add_parser("terraform")
+    t.add_argument("action", choices=["get", "plan", "apply", "destroy"])
+    t.set_defaults(fn=cmd_terraform)
+
+    pb = sub.add_parser("ansible-playbook")
+    pb.add_argument("playbook", nargs="?", default="clusterUp.yml")
+    pb.add_argument("-i", "--inventory", default=None)
+    pb.add_argument("--check", "-C", action="store_true")
+    pb.add_argument("-e", "--extra-vars", action="append")
+    pb.set_defaults(fn=cmd_playbook)
+
+    k = sub.add_parser("kubectl", add_help=False)
+    k.add_argument("rest", nargs=argparse.REMAINDER)
+    k.set_defaults(fn=lambda a: __import__("tritonk8ssupervisor_amd.cli.kubectl", fromlist=["main"]).main(a.rest, workdir=a.workdir))
+    return ap
+
+
+def main(argv: list[str] | None = None) -> int:
+    args = build_parser().parse_args(argv)
+    return args.fn(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

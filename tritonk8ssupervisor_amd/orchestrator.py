@@ -1,0 +1,543 @@
+"""Bring-up orchestrator: ``./setup.sh`` (create) and ``./setup.sh -c`` (teardown).
+
+Reference: main setup.sh:8-92 (W1), runTerraformTasks/updateTerraformConfig :138-198 (W9/W10),
+createAnsibleConfigs :116-137 (W12), runAnsible :111-115 (W16), cleanRunner :484-521 (W13),
+readiness loop :56-85 (W14). Phase order is the same; what changed:
+
+  * no fixed sleeps (the reference sleeps 2 s x3 between phases, 30 s per VM, 15 s pause);
+  * readiness is event-driven (control-plane long-poll) and BOUNDED (--timeout), instead of a
+    1 s tick / 15 s curl loop that can run forever; "Ready" means every worker heartbeating,
+    every GPU worker validated by tk8s-probe, amd.com/gpu allocatable == expected, and (with
+    >= 2 GPUs) an RCCL all-reduce across all of them reduced exactly;
+  * every phase is timed into .tk8s/events.jsonl and .tk8s/state.json (``--resume`` skips
+    completed phases; the reference can only be cleaned and restarted);
+  * teardown also removes ansible/tmp/kubernetes_environment.id and vars.yml (W13 bug).
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import sys
+import time
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Callable
+
+from . import hcl
+from .config import ClusterConfig, export_vars, read_config, write_config
+from .provider import get_provider
+from .provider.base import Machine, ProvisionError
+from .provision import Engine
+from .utils.events import EventLog
+from .utils.fsutil import atomic_write, atomic_write_json, read_json, remove_paths
+from .utils.procs import kill_pidfile, pid_alive, read_pidfile, spawn_daemon, wait_for_file_text
+
+REPO = Path(__file__).resolve().parents[1]
+TEMPLATE_DIRS = ["terraform/master", "terraform/host", "ansible/roles", "manifests"]
+TEMPLATE_FILES = ["ansible/ansible.cfg", "ansible/clusterUp.yml"]
+PHASES = ["configure", "provision", "ansible-config", "ansible", "ready", "rccl"]
+
+
+class SetupError(RuntimeError):
+    def __init__(self, msg: str, code: int = 1):
+        super().__init__(msg)
+        self.code = code
+
+
+@dataclass
+class Workspace:
+    root: Path
+
+    @property
+    def config(self) -> Path: return self.root / "config"
+    @property
+    def tf(self) -> Path: return self.root / "terraform"
+    @property
+    def ansible(self) -> Path: return self.root / "ansible"
+    @property
+    def manifests(self) -> Path: return self.root / "manifests"
+    @property
+    def state_dir(self) -> Path: return self.root / ".tk8s"
+    @property
+    def state_file(self) -> Path: return self.state_dir / "state.json"
+    @property
+    def events(self) -> Path: return self.state_dir / "events.jsonl"
+    @property
+    def env_id_file(self) -> Path: return self.ansible / "tmp" / "kubernetes_environment.id"
+    @property
+    def vars_file(self) -> Path: return self.ansible / "roles" / "ranchermaster" / "vars" / "vars.yml"
+
+    def state(self) -> dict:
+        return read_json(self.state_file, {}) or {}
+
+    def save_state(self, **kw) -> dict:
+        st = self.state()
+        st.update(kw)
+        atomic_write_json(self.state_file, st)
+        return st
+
+
+def init_workspace(dst: str | os.PathLike, src: Path = REPO) -> Workspace:
+    """Copy the module/role/manifest templates into a fresh workspace directory."""
+    d = Path(dst)
+    for rel in TEMPLATE_DIRS:
+        if (d / rel).exists():
+            shutil.rmtree(d / rel)
+        shutil.copytree(src / rel, d / rel, ignore=shutil.ignore_patterns("vars.yml", "__pycache__"))
+    for rel in TEMPLATE_FILES:
+        (d / rel).parent.mkdir(parents=True, exist_ok=True)
+        shutil.copy2(src / rel, d / rel)
+    (d / "ansible" / "tmp").mkdir(parents=True, exist_ok=True)
+    (d / "ansible" / "roles" / "ranchermaster" / "vars").mkdir(parents=True, exist_ok=True)
+    return Workspace(d)
+
+
+# ---- machine executor for the playbook engine ---------------------------------------------
+class MachineExecutor:
+    """Runs playbook commands / daemons "on" provisioned machines through the provider."""
+
+    def __init__(self, provider, machines: dict[str, Machine]):
+        self.provider = provider
+        self.machines = machines  # inventory host name -> Machine
+        sup = REPO / "tritonk8ssupervisor_amd" / "bin" / "tk8s-supervise"
+        self.supervise = str(sup) if sup.exists() else None
+
+    def _m(self, host: str) -> Machine:
+        if host not in self.machines:
+            raise ProvisionError(f"unknown machine {host}")
+        return self.machines[host]
+
+    def exec(self, host: str, cmd: str, env: dict | None = None, timeout: float = 600) -> tuple[int, str]:
+        return self.provider.exec(self._m(host), cmd, timeout=timeout, env=env)
+
+    def machine_dir(self, host: str) -> str:
+        return self._m(host).sandbox
+
+    def machine_gpus(self, host: str) -> list[int]:
+        return list(self._m(host).gpus)
+
+    def _paths(self, host: str, name: str) -> tuple[Path, Path]:
+        sb = Path(self._m(host).sandbox)
+        return sb / "run" / f"{name}.pid", sb / "logs" / f"{name}.log"
+
+    def daemon_status(self, host: str, name: str) -> dict:
+        pidfile, _ = self._paths(host, name)
+        info = read_pidfile(pidfile)
+        if not info:
+            return {"running": False}
+        return {"running": pid_alive(int(info["pid"])), "pid": info["pid"]}
+
+    def start_daemon(self, host: str, name: str, argv: list[str], env: dict, restart: str,
+                     wait_for_log: str | None, timeout: float) -> dict:
+        m = self._m(host)
+        pidfile, log = self._paths(host, name)
+        full_env = dict(os.environ)
+        full_env.update(getattr(self.provider, "machine_env", lambda _m: {})(m))
+        full_env.update(env)
+        log.parent.mkdir(parents=True, exist_ok=True)
+        offset = log.stat().st_size if log.exists() else 0
+        if self.supervise and restart != "no":
+            cmd = [self.supervise, "--pidfile", str(pidfile), "--log", str(log), "--restart", restart, "--", *argv]
+            p = spawn_daemon(cmd, env=full_env, cwd=m.sandbox)
+            deadline = time.monotonic() + 5
+            while not pidfile.exists() and time.monotonic() < deadline and p.poll() is None:
+                time.sleep(0.001)
+        else:
+            p = spawn_daemon(argv, env=full_env, cwd=m.sandbox, log_path=str(log), pidfile=str(pidfile))
+        info = {"ok": True, "pid": p.pid, "log": str(log)}
+        if wait_for_log:
+            t = time.monotonic()
+            deadline = t + timeout
+            while time.monotonic() < deadline:
+                try:
+                    with open(log, "rb") as f:
+                        f.seek(offset)
+                        if wait_for_log.encode() in f.read():
+                            info["wait_seconds"] = round(time.monotonic() - t, 6)
+                            return info
+                except OSError:
+                    pass
+                if p.poll() is not None:
+                    break
+                time.sleep(0.002)
+            tail = log.read_text(errors="replace")[-600:] if log.exists() else ""
+            return {"ok": False, "msg": f"{name} on {host} did not log {wait_for_log!r} within {timeout}s: {tail}"}
+        return info
+
+    def stop_daemon(self, host: str, name: str) -> bool:
+        pidfile, _ = self._paths(host, name)
+        return kill_pidfile(pidfile)
+
+
+# ---- setup ---------------------------------------------------------------------------------
+class Setup:
+    def __init__(self, ws: Workspace, *, answers: dict | None = None, assume_yes: bool = False,
+                 resume: bool = False, timeout: float = 600.0, validate: bool = True, rccl: bool | None = None,
+                 out: Callable[[str], None] = None, quiet_ansible: bool = True, hbm_bytes: int = 1 << 30,
+                 md5_bytes: int = 256 << 20, probe_iters: int = 3, rccl_max_bytes: int = 64 << 20,
+                 node_grace: float = 5.0, backend: str | None = None, master_port: int | None = None):
+        self.ws = ws
+        self.answers = answers
+        self.assume_yes = assume_yes
+        self.resume = resume
+        self.timeout = timeout
+        self.validate = validate
+        self.rccl = rccl
+        self.out = out or _flush_print
+        self.quiet_ansible = quiet_ansible
+        self.hbm_bytes, self.md5_bytes, self.probe_iters = hbm_bytes, md5_bytes, probe_iters
+        self.rccl_max_bytes = rccl_max_bytes
+        self.node_grace = node_grace
+        self.backend = backend or os.environ.get("TK8S_BACKEND", "local")
+        self.master_port = master_port
+        ws.state_dir.mkdir(parents=True, exist_ok=True)
+        self.events = EventLog(ws.events, echo=False)
+        self.provider = get_provider(self.backend, ws.state_dir)
+        self.engine = Engine(ws.tf, self.provider, self.events)
+        self.cfg: ClusterConfig | None = None
+        self.summary: dict = {}
+
+    def banner(self, text: str) -> None:
+        self.out("#" * 80)
+        self.out(f"### {text}")
+        self.out("#" * 80)
+
+    def done(self, phase: str) -> bool:
+        return self.resume and phase in self.ws.state().get("completed", [])
+
+    def mark(self, phase: str) -> None:
+        st = self.ws.state()
+        comp = [p for p in st.get("completed", []) if p != phase] + [phase]
+        timings = st.get("timings", {})
+        timings[phase] = round(self.events.phases.get(phase, 0.0), 6)
+        self.ws.save_state(completed=comp, timings=timings)
+
+    # -- phases --------------------------------------------------------------------------
+    def configure(self) -> ClusterConfig:
+        from .wizard import run_wizard
+
+        ws = self.ws
+        if self.resume and ws.config.exists():
+            cfg = read_config(ws.config)
+        else:
+            if ws.config.exists():
+                raise SetupError("error: old configuration found\n    clean the configuration (./setup.sh -c)")
+            cfg = ClusterConfig(TK8S_BACKEND=self.backend)
+            if self.master_port:
+                cfg.TK8S_MASTER_PORT = self.master_port
+            env = self.provider.env()
+            cfg.SDC_URL, cfg.SDC_ACCOUNT, cfg.SDC_KEY_ID = env["SDC_URL"], env["SDC_ACCOUNT"], env["SDC_KEY_ID"]
+            key = self.provider.find_key(cfg.SDC_KEY_ID)
+            if not key:
+                raise SetupError(f"error: couldn't find the key associated with fingerprint {cfg.SDC_KEY_ID}\n"
+                                 "    Clean the setup and make sure your provider profile is set up.")
+            cfg.SDC_KEY = key
+            answers = self.answers
+            if answers is not None and self.assume_yes:
+                answers = dict(answers)
+                answers.setdefault("confirm", "yes")
+            run_wizard(cfg, self.provider, answers=answers, out=None if answers is None else _Sink(self.out))
+            write_config(ws.config, cfg)
+        export_vars(cfg)
+        self.cfg = cfg
+        return cfg
+
+    def provision(self) -> None:
+        cfg = self.cfg
+        ws = self.ws
+        key = cfg.SDC_KEY
+        pub = key + ".pub" if Path(key + ".pub").exists() else key
+        text = hcl.render_root(self.provider.name, cfg.SDC_ACCOUNT, key, pub, cfg.SDC_KEY_ID, cfg.SDC_URL,
+                               cfg.RANCHER_MASTER_HOSTNAME, cfg.master_networks(), cfg.node_names(),
+                               cfg.node_networks(), cfg.HOST_PACKAGE)
+        if not (ws.tf / "rancher.tf").exists() or not self.resume:
+            atomic_write(ws.tf / "rancher.tf", text)
+        self.out("Generating terraform configs for environment...")
+        self.out(f"    Master hostname: {cfg.RANCHER_MASTER_HOSTNAME}")
+        for i, n in enumerate(cfg.node_names(), 1):
+            self.out(f"    Kubernetes node {i}: {n}")
+        self.engine.get()
+        res = self.engine.apply()
+        self.out(f"    terraform tasks completed: {len(res.created)} created, {len(res.unchanged)} unchanged "
+                 f"in {res.seconds:.3f}s")
+        if not res.ok:
+            for a, e in res.failed.items():
+                self.out(f"    {a}: {e}")
+            raise SetupError("Terraform had too many errors. Make sure you haven't reached your provisioning limit.")
+
+    def ansible_config(self) -> None:
+        """createAnsibleConfigs (setup.sh:116-137)."""
+        ws, cfg = self.ws, self.cfg
+        masters = (ws.tf / "masters.ip").read_text().split() if (ws.tf / "masters.ip").exists() else []
+        hosts_ = (ws.tf / "hosts.ip").read_text().split() if (ws.tf / "hosts.ip").exists() else []
+        if not masters or not hosts_:
+            raise SetupError("Terraform had too many errors. Make sure you haven't reached your provisioning limit.")
+        machines = self.engine.machines()
+        lines = ["[MASTER]"]
+        lines.append(f"{cfg.RANCHER_MASTER_HOSTNAME} ansible_host={machines[cfg.RANCHER_MASTER_HOSTNAME].primaryip}")
+        lines.append("[HOST]")
+        for n in cfg.node_names():
+            lines.append(f"{n} ansible_host={machines[n].primaryip}")
+        atomic_write(ws.ansible / "hosts", "\n".join(lines) + "\n")
+        self.out("Creating ansible hosts file and variable files")
+        self.out("    created: ansible/hosts")
+        master = masters[-1]
+        atomic_write(ws.vars_file, f"master: {master}\nkubernetes_name: {json.dumps(cfg.KUBERNETES_NAME)}\n"
+                                   f"kubernetes_description: {json.dumps(cfg.KUBERNETES_DESCRIPTION)}\n")
+        _set_ini_value(ws.ansible / "ansible.cfg", "private_key_file", cfg.SDC_KEY)
+        self.out("    created: ansible/roles/ranchermaster/vars/vars.yml")
+
+    def _validation_command(self) -> list[str]:
+        if os.environ.get("TK8S_FAKE_GPUS"):
+            return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
+        return ["tk8s-probe", "--all-devices", "--gpuinfo", "--hbm-bytes", str(self.hbm_bytes),
+                "--md5-bytes", str(self.md5_bytes), "--iters", str(self.probe_iters)]
+
+    def ansible(self) -> None:
+        from .playbook import Playbook
+
+        ws, cfg = self.ws, self.cfg
+        machines = self.engine.machines()
+        m = machines[cfg.RANCHER_MASTER_HOSTNAME]
+        extra = {
+            "tk8s_python": sys.executable,
+            "tk8s_pythonpath": os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]),
+            "tk8s_master_port": int(cfg.TK8S_MASTER_PORT),
+            "tk8s_bind_host": m.primaryip,
+            "tk8s_cp_state_dir": str(Path(m.sandbox) / "controlplane"),
+            "tk8s_node_grace": self.node_grace,
+            "tk8s_manifests": str(ws.manifests),
+            "tk8s_validation_command": self._validation_command(),
+            "tk8s_validate": self.validate,
+            "tk8s_fake_gpus": os.environ.get("TK8S_FAKE_GPUS", ""),
+        }
+        lines: list[str] = []
+        pb = Playbook(ws.ansible / "clusterUp.yml", ws.ansible / "hosts", executor=MachineExecutor(self.provider, machines),
+                      extra_vars=extra, events=self.events, out=(lines.append if self.quiet_ansible else self.out))
+        res = pb.run()
+        atomic_write(ws.state_dir / "ansible.log", "\n".join(lines) + "\n")
+        if not res.ok:
+            if self.quiet_ansible:
+                for line in lines[-40:]:
+                    self.out(line)
+            raise SetupError("ansible-playbook failed: " + "; ".join(res.failures[:5]))
+
+    def _client(self):
+        from .controlplane.client import Client
+
+        m = self.engine.machines()[self.cfg.RANCHER_MASTER_HOSTNAME]
+        return Client(f"{m.primaryip}:{self.cfg.TK8S_MASTER_PORT}", timeout=30.0)
+
+    def project_id(self) -> str:
+        return self.ws.env_id_file.read_text().strip()
+
+    def expected_gpus(self) -> int:
+        pkg = self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE)
+        return int(self.cfg.KUBERNETES_NUMBER_OF_NODES) * int(getattr(pkg, "gpus", 0) or 0)
+
+    def wait_ready(self) -> dict:
+        """Event-driven, bounded replacement of the readiness loop (setup.sh:56-85)."""
+        c = self._client()
+        pid = self.project_id()
+        n = int(self.cfg.KUBERNETES_NUMBER_OF_NODES)
+        g = self.expected_gpus()
+        self.out("Waiting on the cluster: all nodes Ready" + (f", {g} x amd.com/gpu validated" if g else ""))
+        deadline = time.monotonic() + self.timeout
+        last = {}
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise SetupError(f"cluster not ready after {self.timeout:.0f}s: {json.dumps(last)}", code=124)
+            last = c.get("/v1/cluster/wait", query={"project": pid, "nodes": n, "gpus": g,
+                                                    "validated": int(self.validate), "timeout": min(left, 30.0)},
+                         timeout=min(left, 30.0) + 10)
+            if last.get("ready"):
+                return last
+            if last.get("failed"):
+                raise SetupError(f"GPU validation failed on {last.get('nodes_validation_failed')} node(s): "
+                                 f"see `./kubectl get pods -n kube-system` and pod logs", code=2)
+
+    def run_rccl(self) -> dict | None:
+        from .controlplane.client import client_from_kubeconfig
+        from .kube import apply_objects, load_manifests, pods_of, wait_job
+
+        g = self.expected_gpus()
+        enabled = self.rccl if self.rccl is not None else g >= 2
+        if not enabled or g < 1:
+            return None
+        c = self._client()
+        pid = self.project_id()
+        k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
+        job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
+        if os.environ.get("TK8S_FAKE_GPUS"):
+            cmd = [sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.fake_rccl", "--rank", "$(JOB_COMPLETION_INDEX)",
+                   "--nranks", str(g), "--kv-url", f"$(TK8S_KV_URL)/{job}/uid"]
+        else:
+            cmd = ["tk8s-rccl", "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "0",
+                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
+                   "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
+        objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
+                              {"job_name": job, "nranks": g, "rccl_command": cmd})
+        apply_objects(k, objs)
+        self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job})")
+        left = max(10.0, self.timeout)
+        j = wait_job(k, job, "kube-system", timeout=left)
+        pods = pods_of(k, f"job-name={job}", "kube-system")
+        results = [p.get("status", {}).get("result") or {} for p in pods]
+        peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)
+        ok = j["status"].get("succeeded", 0) >= g and all(r.get("ok") for r in results)
+        rep = {"job": job, "ok": ok, "nranks": g, "peak_busbw_gbps": peak,
+               "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),
+                                 "ok": (p.get("status", {}).get("result") or {}).get("ok")} for p in pods]}
+        if not ok:
+            raise SetupError(f"RCCL all-reduce validation failed: {json.dumps(rep)[:800]}", code=2)
+        return rep
+
+    # -- main ------------------------------------------------------------------------------
+    def run(self) -> dict:
+        ws = self.ws
+        t0 = time.monotonic()
+        if (ws.tf / "rancher.tf").exists() and not self.resume:
+            raise SetupError("error: configuration for a previous run has been found\n"
+                             "    clean the configuration (./setup.sh -c) or continue it (./setup.sh --resume)")
+        self.events.emit("setup_start", backend=self.backend, resume=self.resume)
+        if not self.resume:
+            ws.save_state(completed=[], timings={}, started=time.time())
+        steps = [("configure", self.configure, None), ("provision", self.provision, "Starting terraform tasks..."),
+                 ("ansible-config", self.ansible_config, "Creating ansible configs..."),
+                 ("ansible", self.ansible, "Running ansible tasks...")]
+        for name, fn, title in steps:
+            if name == "configure" or not self.done(name):
+                if title:
+                    self.banner(title)
+                with self.events.phase(name):
+                    fn()
+                self.mark(name)
+        with self.events.phase("ready"):
+            ready = self.wait_ready()
+        self.mark("ready")
+        t_ready = time.monotonic() - t0
+        rccl = None
+        with self.events.phase("rccl"):
+            rccl = self.run_rccl()
+        self.mark("rccl")
+        total = time.monotonic() - t0
+        m = self.engine.machines()[self.cfg.RANCHER_MASTER_HOSTNAME]
+        base = f"http://{m.primaryip}:{self.cfg.TK8S_MASTER_PORT}"
+        pid = self.project_id()
+        self._write_kubeconfig(base, pid)
+        self.summary = {
+            "ready_seconds": round(t_ready, 4), "total_seconds": round(total, 4),
+            "nodes": int(self.cfg.KUBERNETES_NUMBER_OF_NODES), "gpus_allocatable": ready.get("gpus_allocatable", 0),
+            "nodes_validated": ready.get("nodes_validated", 0), "rccl": rccl,
+            "phases": {k: round(v, 4) for k, v in self.events.phases.items()},
+            "dashboard": f"{base}/r/projects/{pid}/kubernetes-dashboard:9090/",
+            "kubectl_config": f"{base}/env/{pid}/kubernetes/kubectl", "project": pid, "api": base,
+        }
+        ws.save_state(summary=self.summary, finished=time.time())
+        self.events.emit("setup_done", **{k: v for k, v in self.summary.items() if k != "phases"})
+        self.out("")
+        self.out("Congratulations, your Kubernetes cluster setup has been complete.")
+        self.out(f"----> To check what processes/containers are running, go to {base}/env/{pid}/infra/containers")
+        self.out(f"----> Kubernetes dashboard is at {self.summary['dashboard']}")
+        self.out(f"----> Kubernetes CLI config is at {self.summary['kubectl_config']}")
+        self.out(f"----> {self.summary['nodes']} node(s) Ready, {self.summary['gpus_allocatable']} x amd.com/gpu allocatable"
+                 + (f", RCCL all-reduce peak busbw {rccl['peak_busbw_gbps']:.1f} GB/s over {rccl['nranks']} GPU(s)" if rccl else ""))
+        self.out(f"----> bring-up: {t_ready:.3f}s to all nodes Ready ({total:.3f}s including fabric validation)")
+        self.out("")
+        self.out("    CONGRATULATIONS, YOU HAVE CONFIGURED YOUR KUBERNETES ENVIRONMENT!")
+        return self.summary
+
+    def _write_kubeconfig(self, base: str, pid: str) -> None:
+        from .controlplane.client import Client
+
+        kc = Client(base).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
+        atomic_write_json(self.ws.state_dir / "kubeconfig.json", kc)
+
+
+def _flush_print(s: str) -> None:
+    print(s, flush=True)
+
+
+class _Sink:
+    """File-like adapter so the wizard's prompt echo goes to an out() callback line by line."""
+
+    def __init__(self, out):
+        self.out = out
+        self.buf = ""
+
+    def write(self, s: str) -> None:
+        self.buf += s
+        while "\n" in self.buf:
+            line, self.buf = self.buf.split("\n", 1)
+            self.out(line)
+
+    def flush(self) -> None:
+        pass
+
+
+def _set_ini_value(path: Path, key: str, value: str) -> None:
+    """Replace `key = ...` in an ini file without sed (the reference's sed uses `;` as the
+    delimiter on a user path, setup.sh:133)."""
+    lines = path.read_text().splitlines() if path.exists() else ["[defaults]"]
+    out, done = [], False
+    for line in lines:
+        if line.split("=", 1)[0].strip() == key:
+            out.append(f"{key} = {value}")
+            done = True
+        else:
+            out.append(line)
+    if not done:
+        out.append(f"{key} = {value}")
+    atomic_write(path, "\n".join(out) + "\n")
+
+
+# ---- teardown --------------------------------------------------------------------------------
+def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out: Callable[[str], None] = print,
+          backend: str | None = None) -> int:
+    """cleanRunner (setup.sh:484-521), non-destructive unless confirmed."""
+    inp = inp or sys.stdin
+    out("Clearing settings....")
+    masters, hosts_ = ws.tf / "masters.ip", ws.tf / "hosts.ip"
+    while True:
+        if masters.exists():
+            out("WARNING: You are about to destroy the following machines associated with the cluster:")
+            for f in (masters, hosts_):
+                if f.exists():
+                    out(f.read_text().rstrip())
+            q = "Do you wish to destroy the machines and reset configuration (yes | no)? "
+        else:
+            q = "Do you wish to reset configuration (yes | no)? "
+        if assume_yes:
+            yn = "yes"
+        else:
+            sys.stdout.write(q)
+            sys.stdout.flush()
+            yn = (inp.readline() or "no").strip()
+        if yn == "no":
+            return 0
+        if yn == "yes":
+            break
+        out("Please answer yes or no.")
+    backend = backend or (read_config(ws.config).TK8S_BACKEND if ws.config.exists() else os.environ.get("TK8S_BACKEND", "local"))
+    provider = get_provider(backend, ws.state_dir)
+    if (ws.tf / "rancher.tf").exists() or (ws.tf / "terraform.tfstate").exists():
+        out("    destroying machines...")
+        try:
+            Engine(ws.tf, provider).destroy()
+        except Exception as e:  # noqa: BLE001 - keep cleaning
+            out(f"    warning: destroy: {e}")
+    if hasattr(provider, "list_machines"):  # leftovers of an interrupted apply
+        for m in provider.list_machines():
+            provider.delete_machine(m)
+    remove_paths([ws.tf / n for n in ("hosts.ip", "masters.ip", "rancher.tf", "terraform.tfstate", ".tfstate.lock",
+                                      "hosts.ip.lock", "masters.ip.lock", ".terraform")]
+                 + list(ws.tf.glob("terraform.tfstate*")))
+    if (ws.ansible / "ansible.cfg").exists():
+        _set_ini_value(ws.ansible / "ansible.cfg", "private_key_file", "")
+    remove_paths([ws.ansible / "hosts", ws.vars_file, *ws.ansible.glob("*.retry"), *(ws.ansible / "tmp").glob("*"),
+                  ws.config, ws.state_dir / "machines", ws.state_dir / "alloc.json", ws.state_dir / "alloc.lock",
+                  ws.state_dir / "state.json", ws.state_dir / "kubeconfig.json", ws.state_dir / "ansible.log"])
+    out("    All clear!")
+    return 0

@@ -1,0 +1,392 @@
+"""Playbook engine: the Ansible subset that ``ansible/clusterUp.yml`` and its roles use (L3b).
+
+``ansible-playbook`` is not available offline; this engine executes the same YAML files
+(reference: ansible/clusterUp.yml:1-26 + roles/*/tasks/main.yml) against the machines the
+provisioning engine created. Semantics kept from Ansible:
+
+  * plays in order; a play's tasks run host-parallel (``forks`` from ansible.cfg — default ALL
+    hosts, not Ansible's 5), task after task (a barrier per task);
+  * task keywords: name, register, when, until/retries/delay, with_items/loop, run_once,
+    delegate_to, local_action, action, ignore_errors, failed_when, changed_when, environment;
+  * a failed host leaves the play; the run fails if any host failed;
+  * ``--check``: nothing mutates (BASELINE.json config 1 dry-run); templating errors that come
+    from results a skipped task would have produced are reported as skips.
+
+Bugs of the reference not replicated: inverted ``when:`` truthiness (dockersetup main.yml:10;
+our role uses explicit tests), ``playbook_dir: $(pwd)`` (clusterUp.yml:12 — the real
+``playbook_dir`` magic variable is provided), env-id file never cleaned (teardown removes it).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import configparser
+import copy
+import os
+import shlex
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Callable
+
+import yaml
+
+from . import templating
+from .templating import TemplateError, Undefined
+from .utils.events import EventLog
+
+MODULE_ALIASES = {"command", "shell", "uri", "slurp", "pause", "debug", "set_fact", "wait_for", "fail",
+                  "assert", "copy", "file", "stat", "tk8s_daemon", "tk8s_gpu_facts", "tk8s_build", "tk8s_kube",
+                  "include_vars", "meta", "ping"}
+TASK_KEYS = {"name", "register", "when", "until", "retries", "delay", "with_items", "loop", "run_once",
+             "delegate_to", "local_action", "action", "ignore_errors", "failed_when", "changed_when",
+             "environment", "no_log", "tags", "vars", "check_mode", "loop_control", "become", "args"}
+
+
+class PlaybookError(RuntimeError):
+    pass
+
+
+@dataclass
+class Host:
+    name: str
+    vars: dict = field(default_factory=dict)
+    groups: list[str] = field(default_factory=list)
+
+    @property
+    def address(self) -> str:
+        return str(self.vars.get("ansible_host", self.name))
+
+
+def parse_inventory(text: str) -> dict[str, Host]:
+    """INI inventory: ``[GROUP]`` sections, ``name [k=v ...]`` lines."""
+    hosts: dict[str, Host] = {}
+    group = "ungrouped"
+    for raw in text.splitlines():
+        line = raw.split("#", 1)[0].strip()
+        if not line:
+            continue
+        if line.startswith("[") and line.endswith("]"):
+            group = line[1:-1].strip()
+            continue
+        parts = shlex.split(line)
+        name, kv = parts[0], dict(p.split("=", 1) for p in parts[1:] if "=" in p)
+        h = hosts.setdefault(name, Host(name))
+        h.vars.update(kv)
+        if group not in h.groups:
+            h.groups.append(group)
+    return hosts
+
+
+def _free_form(text: str) -> tuple[dict, str]:
+    """Split ``k=v k2="v 2" rest`` into (kv-dict, free-form remainder)."""
+    kv, free = {}, []
+    lex = shlex.shlex(text, posix=True)
+    lex.whitespace_split = True
+    lex.commenters = ""
+    for tok in lex:
+        if "=" in tok and tok.split("=", 1)[0].replace("_", "").replace("-", "").isalnum() and not free:
+            k, v = tok.split("=", 1)
+            kv[k] = v
+        else:
+            free.append(tok)
+    return kv, " ".join(free)
+
+
+@dataclass
+class TaskResult:
+    host: str
+    status: str            # ok | changed | failed | skipped
+    result: dict
+    seconds: float = 0.0
+
+
+@dataclass
+class PlaybookResult:
+    ok: bool
+    stats: dict[str, dict[str, int]]
+    failures: list[str]
+    seconds: float
+    hostvars: dict[str, dict]
+
+
+class Playbook:
+    def __init__(self, playbook: str | os.PathLike, inventory: str | os.PathLike, *, executor=None,
+                 extra_vars: dict | None = None, check: bool = False, events: EventLog | None = None,
+                 out: Callable[[str], None] | None = print, forks: int | None = None):
+        self.path = Path(playbook).resolve()
+        self.dir = self.path.parent
+        self.hosts = parse_inventory(Path(inventory).read_text())
+        self.executor = executor           # provider-backed remote executor (see modules.Executor)
+        self.extra_vars = extra_vars or {}
+        self.check = check
+        self.events = events or EventLog(None)
+        self.out = out or (lambda s: None)
+        self.cfg = self._read_cfg()
+        self.forks = forks or int(self.cfg.get("forks", "0") or 0) or None
+        self.hostvars: dict[str, dict] = {h: {} for h in self.hosts}
+        self.stats = {h: {"ok": 0, "changed": 0, "failed": 0, "skipped": 0, "unreachable": 0} for h in self.hosts}
+        self._print_lock = threading.Lock()
+
+    def _read_cfg(self) -> dict:
+        p = self.dir / "ansible.cfg"
+        cp = configparser.ConfigParser()
+        if p.exists():
+            cp.read(p)
+        return dict(cp["defaults"]) if cp.has_section("defaults") else {}
+
+    def say(self, s: str) -> None:
+        with self._print_lock:
+            self.out(s)
+
+    # ---- variables ---------------------------------------------------------------------
+    def _groups(self) -> dict[str, list[str]]:
+        g: dict[str, list[str]] = {"all": list(self.hosts)}
+        for h in self.hosts.values():
+            for grp in h.groups:
+                g.setdefault(grp, []).append(h.name)
+        return g
+
+    def host_vars(self, host: Host, play_vars: dict) -> dict:
+        v = {"inventory_hostname": host.name, "ansible_host": host.address, "playbook_dir": str(self.dir),
+             "groups": self._groups(), "group_names": host.groups, "ansible_check_mode": self.check,
+             "ansible_default_ipv4": {"address": host.address}, "hostvars": self.hostvars}
+        v.update(host.vars)
+        v.update(play_vars)
+        v.update(self.hostvars.get(host.name, {}))
+        v.update(self.extra_vars)
+        return v
+
+    def select(self, pattern: str) -> list[Host]:
+        names: list[str] = []
+        groups = self._groups()
+        for part in str(pattern).replace(";", ":").split(":"):
+            part = part.strip()
+            if part in groups:
+                names += groups[part]
+            elif part in self.hosts:
+                names.append(part)
+        seen = set()
+        return [self.hosts[n] for n in names if not (n in seen or seen.add(n))]
+
+    # ---- task normalisation ------------------------------------------------------------
+    def _module_of(self, task: dict) -> tuple[str, Any, bool]:
+        """Returns (module, args, is_local)."""
+        if "local_action" in task:
+            spec = task["local_action"]
+            if isinstance(spec, dict):
+                spec = dict(spec)
+                mod = spec.pop("module")
+                return mod, spec, True
+            mod, _, rest = str(spec).strip().partition(" ")
+            return mod, rest, True
+        if "action" in task:
+            spec = task["action"]
+            if isinstance(spec, dict):
+                spec = dict(spec)
+                return spec.pop("module"), spec, False
+            mod, _, rest = " ".join(str(spec).split()).partition(" ")
+            return mod, rest, False
+        for k, v in task.items():
+            if k not in TASK_KEYS and not k.startswith("_"):
+                return k, v, False
+        raise PlaybookError(f"task {task.get('name')!r} has no module")
+
+    @staticmethod
+    def _args(mod: str, raw: Any, extra: dict | None = None) -> dict:
+        if isinstance(raw, dict):
+            args = dict(raw)
+        elif raw is None:
+            args = {}
+        elif mod in ("command", "shell"):
+            args = {"_raw_params": str(raw)}
+        else:
+            kv, free = _free_form(str(raw))
+            args = kv
+            if free:
+                args["_raw_params"] = free
+        if extra:
+            args.update(extra)
+        return args
+
+    # ---- run -----------------------------------------------------------------------------
+    def run(self) -> PlaybookResult:
+        t0 = time.monotonic()
+        plays = yaml.safe_load(self.path.read_text()) or []
+        failures: list[str] = []
+        for play in plays:
+            failures += self.run_play(play)
+            if failures and not self.check:
+                break
+        self.say("")
+        self.say("PLAY RECAP " + "*" * 68)
+        for h, s in self.stats.items():
+            self.say(f"{h:<26}: ok={s['ok']:<4} changed={s['changed']:<4} unreachable={s['unreachable']:<4} "
+                     f"failed={s['failed']:<4} skipped={s['skipped']}")
+        return PlaybookResult(not failures, self.stats, failures, time.monotonic() - t0, self.hostvars)
+
+    def _role_tasks(self, role: str) -> list[dict]:
+        p = self.dir / "roles" / role / "tasks" / "main.yml"
+        if not p.exists():
+            raise PlaybookError(f"role {role!r} not found at {p}")
+        tasks = yaml.safe_load(p.read_text()) or []
+        for t in tasks:
+            t.setdefault("_role", role)
+        return tasks
+
+    def run_play(self, play: dict) -> list[str]:
+        name = play.get("name", play.get("hosts"))
+        self.say("")
+        self.say(f"PLAY [{name}] " + "*" * max(3, 72 - len(str(name))))
+        hosts = self.select(play.get("hosts", "all"))
+        with self.events.phase(f"play:{name}", hosts=[h.name for h in hosts]):
+            play_vars = dict(play.get("vars") or {})
+            play_vars.pop("playbook_dir", None)  # reference sets the literal "$(pwd)"; use the real one
+            for vf in play.get("vars_files") or []:
+                f = templating.render(vf, {"playbook_dir": str(self.dir), **self.extra_vars})
+                fp = Path(f) if Path(f).is_absolute() else self.dir / f
+                if fp.exists():
+                    play_vars.update(yaml.safe_load(fp.read_text()) or {})
+                elif not self.check:
+                    raise PlaybookError(f"vars_files entry {fp} not found")
+            tasks: list[dict] = []
+            for role in play.get("roles") or []:
+                tasks += self._role_tasks(role if isinstance(role, str) else role["role"])
+            tasks += play.get("tasks") or []
+            alive = list(hosts)
+            failures: list[str] = []
+            for task in tasks:
+                if not alive:
+                    break
+                res = self.run_task(task, alive, play_vars)
+                for r in res:
+                    if r.status == "failed":
+                        failures.append(f"{r.host}: {task.get('name', '?')}: {r.result.get('msg', '')}")
+                alive = [h for h in alive if not any(r.host == h.name and r.status == "failed" for r in res)]
+        return failures
+
+    def run_task(self, task: dict, hosts: list[Host], play_vars: dict) -> list[TaskResult]:
+        title = task.get("name") or next(iter(k for k in task if k not in TASK_KEYS and not k.startswith("_")), "task")
+        prefix = f"{task['_role']} : " if task.get("_role") else ""
+        self.say("")
+        self.say(f"TASK [{prefix}{title}] " + "*" * max(3, 70 - len(prefix + str(title))))
+        t = time.monotonic()
+        if task.get("run_once"):
+            res = [self._run_on_host(task, hosts[0], play_vars)]
+            if res[0].status != "skipped":  # run_once results are shared by every host
+                for h in hosts[1:]:
+                    if task.get("register"):
+                        self.hostvars[h.name][task["register"]] = res[0].result
+        else:
+            workers = min(len(hosts), self.forks or len(hosts)) or 1
+            with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+                res = list(ex.map(lambda h: self._run_on_host(task, h, play_vars), hosts))
+        self.events.emit("task", task=f"{prefix}{title}", seconds=round(time.monotonic() - t, 6),
+                         results={r.host: r.status for r in res})
+        return res
+
+    def _run_on_host(self, task: dict, host: Host, play_vars: dict) -> TaskResult:
+        t0 = time.monotonic()
+        v = self.host_vars(host, {**play_vars, **(task.get("vars") or {})})
+        try:
+            if "when" in task and not templating.test(task["when"], v):
+                r = TaskResult(host.name, "skipped", {"skipped": True, "changed": False})
+                return self._record(task, host, r)
+        except Undefined as e:
+            if self.check:
+                return self._record(task, host, TaskResult(host.name, "skipped", {"skipped": True, "msg": f"check mode: {e}"}))
+            return self._record(task, host, TaskResult(host.name, "failed", {"failed": True, "msg": f"when: {e}"}))
+        mod, raw, local = self._module_of(task)
+        if task.get("delegate_to"):
+            target = templating.render(task["delegate_to"], v)
+            local = local or target in ("localhost", "127.0.0.1")
+            deleg = self._host_by_addr(target)
+        else:
+            deleg = None
+        items = task.get("with_items", task.get("loop"))
+        try:
+            if items is not None:
+                items = templating.render(items, v)
+                results = []
+                for item in items:
+                    iv = dict(v, item=item)
+                    results.append(self._exec(task, mod, raw, iv, host, deleg, local))
+                failed = any(r.get("failed") for r in results)
+                changed = any(r.get("changed") for r in results)
+                result = {"results": results, "changed": changed, "failed": failed,
+                          "msg": next((r.get("msg") for r in results if r.get("failed")), "")}
+            else:
+                result = self._exec(task, mod, raw, v, host, deleg, local)
+        except Undefined as e:
+            if self.check:
+                result = {"skipped": True, "changed": False, "msg": f"check mode: {e}"}
+            else:
+                result = {"failed": True, "msg": f"template error: {e}"}
+        except TemplateError as e:
+            result = {"failed": True, "msg": f"template error: {e}"}
+        status = "skipped" if result.get("skipped") else "failed" if result.get("failed") else \
+            "changed" if result.get("changed") else "ok"
+        if status == "failed" and task.get("ignore_errors"):
+            status = "ok"
+            result["ignored"] = True
+        r = TaskResult(host.name, status, result, time.monotonic() - t0)
+        return self._record(task, host, r)
+
+    def _host_by_addr(self, target: str) -> Host | None:
+        for h in self.hosts.values():
+            if target in (h.name, h.address):
+                return h
+        return None
+
+    def _exec(self, task, mod, raw, v, host, deleg, local) -> dict:
+        from .playbook_modules import run_module
+
+        extra = task.get("args")
+        args = templating.render(self._args(mod, raw, extra), v)
+        env = templating.render(task.get("environment") or {}, v)
+        retries = int(task.get("retries", 3)) if "until" in task else 0
+        delay = float(task.get("delay", 5))
+        attempt = 0
+        while True:
+            attempt += 1
+            result = run_module(mod, args, ctx=self, host=host, target=deleg or host, local=local, env=env,
+                                check=self.check and task.get("check_mode", True) is not False, variables=v)
+            if "until" in task and not result.get("skipped"):
+                rv = dict(v)
+                if task.get("register"):
+                    rv[task["register"]] = result
+                if not templating.test(task["until"], rv):
+                    if attempt <= retries:
+                        time.sleep(delay)
+                        continue
+                    result["failed"] = True
+                    result["msg"] = f"until condition not met after {attempt} attempts"
+                result["attempts"] = attempt
+            break
+        vv = dict(v)
+        if task.get("register"):
+            vv[task["register"]] = result
+        if "failed_when" in task:
+            result["failed"] = templating.test(task["failed_when"], vv)
+        if "changed_when" in task:
+            result["changed"] = templating.test(task["changed_when"], vv)
+        return result
+
+    def _record(self, task: dict, host: Host, r: TaskResult) -> TaskResult:
+        if task.get("register"):
+            self.hostvars[host.name][task["register"]] = r.result
+        if r.status == "ok" and r.result.get("ansible_facts"):
+            self.hostvars[host.name].update(r.result["ansible_facts"])
+        self.stats[host.name][r.status] = self.stats[host.name].get(r.status, 0) + 1
+        word = {"ok": "ok", "changed": "changed", "failed": "fatal", "skipped": "skipping"}[r.status]
+        msg = ""
+        if r.status == "failed":
+            msg = f" => {{\"msg\": {r.result.get('msg', '')!r}}}"
+        elif task.get("debug") is not None or "msg_out" in r.result:
+            msg = f" => {r.result.get('msg_out', '')}"
+        self.say(f"{word}: [{host.name}]{msg}")
+        return r
+
+
+def copy_vars(d: dict) -> dict:
+    return copy.deepcopy(d)

@@ -1,0 +1,384 @@
+"""Modules for the playbook engine.
+
+Ansible built-ins used by the reference roles: command, shell, uri, slurp, pause, debug
+(ansible/roles/*/tasks/main.yml) plus set_fact, wait_for, fail, assert, copy, file, stat,
+include_vars, meta, ping. tk8s modules replace the Docker ones:
+
+  tk8s_daemon    — start/stop/query a supervised long-running process on a machine
+                   (replaces docker_container rancher/server and docker rancher/agent)
+  tk8s_gpu_facts — ROCm/KFD facts of a machine (replaces the docker --version probe)
+  tk8s_build     — ensure the native validation stack is built (replaces apt docker-engine)
+  tk8s_kube      — create/delete/wait Kubernetes objects on the control plane
+"""
+from __future__ import annotations
+
+import base64
+import json
+import os
+import re
+import shlex
+import socket
+import subprocess
+import time
+import urllib.error
+import urllib.request
+from pathlib import Path
+from typing import Any
+
+import yaml
+
+from . import templating
+
+
+def _bool(v: Any, default: bool = False) -> bool:
+    if v is None:
+        return default
+    if isinstance(v, bool):
+        return v
+    return str(v).lower() in ("1", "yes", "true", "on")
+
+
+def run_module(mod: str, args: dict, *, ctx, host, target, local: bool, env: dict, check: bool,
+               variables: dict) -> dict:
+    fn = MODULES.get(mod)
+    if fn is None:
+        return {"failed": True, "msg": f"module {mod!r} is not supported by the tk8s playbook engine"}
+    try:
+        return fn(args, ctx=ctx, host=host, target=target, local=local, env=env, check=check, variables=variables)
+    except templating.Undefined:
+        raise
+    except Exception as e:  # noqa: BLE001 - module failure becomes a task failure
+        return {"failed": True, "msg": f"{mod}: {type(e).__name__}: {e}"}
+
+
+# ---- command / shell ---------------------------------------------------------------------
+def _run_cmd(cmd: str | list[str], *, ctx, target, local, env, shell: bool, timeout: float = 600) -> dict:
+    t = time.monotonic()
+    if local or ctx.executor is None:
+        argv = ["bash", "-c", cmd] if shell else (cmd if isinstance(cmd, list) else shlex.split(cmd))
+        r = subprocess.run(argv, cwd=ctx.dir, env={**os.environ, **env}, capture_output=True, text=True, timeout=timeout)
+        rc, out, err = r.returncode, r.stdout, r.stderr
+    else:
+        line = cmd if shell else " ".join(shlex.quote(a) for a in (cmd if isinstance(cmd, list) else shlex.split(cmd)))
+        rc, out = ctx.executor.exec(target.name, line, env=env, timeout=timeout)
+        err = ""
+    out = out or ""
+    return {"rc": rc, "stdout": out.rstrip("\n"), "stderr": err.rstrip("\n"), "stdout_lines": out.splitlines(),
+            "changed": True, "failed": rc != 0, "delta": round(time.monotonic() - t, 6),
+            "msg": "" if rc == 0 else f"non-zero return code {rc}: {(err or out).strip()[-300:]}"}
+
+
+def m_command(args, *, ctx, target, local, env, check, **_):
+    if check:
+        return {"skipped": True, "changed": False, "msg": "command skipped in check mode"}
+    cmd = args.get("_raw_params") or args.get("cmd") or args.get("argv")
+    return _run_cmd(cmd, ctx=ctx, target=target, local=local, env=env, shell=False)
+
+
+def m_shell(args, *, ctx, target, local, env, check, **_):
+    if check:
+        return {"skipped": True, "changed": False, "msg": "shell skipped in check mode"}
+    cmd = args.get("_raw_params") or args.get("cmd")
+    return _run_cmd(cmd, ctx=ctx, target=target, local=local, env=env, shell=True)
+
+
+# ---- uri ----------------------------------------------------------------------------------
+def m_uri(args, *, check, **_):
+    method = str(args.get("method", "GET")).upper()
+    if check and method != "GET":
+        return {"skipped": True, "changed": False, "msg": f"{method} skipped in check mode"}
+    url = str(args["url"])
+    codes = args.get("status_code", 200)
+    if isinstance(codes, str):
+        codes = [int(c) for c in codes.split(",")]
+    elif isinstance(codes, int):
+        codes = [codes]
+    else:
+        codes = [int(c) for c in codes]
+    headers = {k[len("HEADER_"):]: str(v) for k, v in args.items() if k.startswith("HEADER_")}
+    headers.update({k: str(v) for k, v in (args.get("headers") or {}).items()})
+    body = args.get("body")
+    data = None
+    if body is not None:
+        if args.get("body_format") == "json":
+            if isinstance(body, str):
+                body = json.loads(body)
+            data = json.dumps(body).encode()
+            headers.setdefault("Content-Type", "application/json")
+        else:
+            data = body.encode() if isinstance(body, str) else json.dumps(body).encode()
+    if method in ("POST", "PUT", "PATCH") and data is None:
+        data = b""
+    req = urllib.request.Request(url, data=data, method=method, headers=headers)
+    timeout = float(args.get("timeout", 30))
+    try:
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            status, content = r.status, r.read()
+    except urllib.error.HTTPError as e:
+        status, content = e.code, e.read()
+    except (urllib.error.URLError, OSError) as e:
+        return {"failed": True, "status": -1, "msg": f"request to {url} failed: {e}", "url": url}
+    res = {"status": status, "url": url, "changed": method != "GET", "failed": status not in codes}
+    text = content.decode(errors="replace")
+    try:
+        res["json"] = json.loads(text) if text else {}
+    except ValueError:
+        pass
+    if _bool(args.get("return_content")) or res["failed"]:
+        res["content"] = text
+    if res["failed"]:
+        res["msg"] = f"Status code was {status} and not {codes}: {text[:300]}"
+    return res
+
+
+# ---- files ----------------------------------------------------------------------------------
+def _path(p: str, ctx, target, local) -> Path:
+    pp = Path(os.path.expanduser(str(p)))
+    if pp.is_absolute():
+        return pp
+    if local or ctx.executor is None:
+        return ctx.dir / pp
+    return Path(ctx.executor.machine_dir(target.name)) / pp
+
+
+def m_slurp(args, *, ctx, target, local, **_):
+    p = _path(args.get("src") or args.get("path"), ctx, target, local)
+    data = p.read_bytes()
+    return {"content": base64.b64encode(data).decode(), "encoding": "base64", "source": str(p), "changed": False}
+
+
+def m_copy(args, *, ctx, target, local, check, **_):
+    dest = _path(args["dest"], ctx, target, local)
+    if "content" in args:
+        data = str(args["content"]).encode()
+    else:
+        data = _path(args["src"], ctx, target, True).read_bytes()
+    old = dest.read_bytes() if dest.exists() else None
+    changed = old != data
+    if changed and not check:
+        from .utils.fsutil import atomic_write
+
+        atomic_write(dest, data)
+        if "mode" in args:
+            os.chmod(dest, int(str(args["mode"]), 8))
+    return {"changed": changed, "dest": str(dest)}
+
+
+def m_file(args, *, ctx, target, local, check, **_):
+    p = _path(args.get("path") or args.get("dest"), ctx, target, local)
+    state = args.get("state", "file")
+    changed = False
+    if state == "directory":
+        changed = not p.is_dir()
+        if changed and not check:
+            p.mkdir(parents=True, exist_ok=True)
+    elif state == "absent":
+        changed = p.exists()
+        if changed and not check:
+            from .utils.fsutil import remove_paths
+
+            remove_paths([p])
+    elif state == "touch":
+        changed = True
+        if not check:
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.touch()
+    elif not p.exists():
+        return {"failed": True, "msg": f"file {p} does not exist"}
+    return {"changed": changed, "path": str(p), "state": state}
+
+
+def m_stat(args, *, ctx, target, local, **_):
+    p = _path(args["path"], ctx, target, local)
+    if not p.exists():
+        return {"stat": {"exists": False}, "changed": False}
+    st = p.stat()
+    return {"stat": {"exists": True, "isdir": p.is_dir(), "size": st.st_size, "mtime": st.st_mtime, "path": str(p)},
+            "changed": False}
+
+
+def m_include_vars(args, *, ctx, target, local, **_):
+    p = _path(args.get("file") or args.get("_raw_params"), ctx, target, True)
+    return {"ansible_facts": yaml.safe_load(p.read_text()) or {}, "changed": False}
+
+
+# ---- control flow ---------------------------------------------------------------------------
+def m_pause(args, *, check, **_):
+    secs = float(args.get("seconds", 0)) + 60 * float(args.get("minutes", 0))
+    if not check:
+        time.sleep(secs)
+    return {"changed": False, "delta": secs, "msg_out": args.get("prompt", "")}
+
+
+def m_debug(args, *, variables, **_):
+    if "var" in args:
+        msg = templating.evaluate(str(args["var"]), variables, strict=False)
+        return {"changed": False, "msg_out": json.dumps({str(args["var"]): msg}, default=str)}
+    return {"changed": False, "msg_out": str(args.get("msg", args.get("_raw_params", "Hello world!")))}
+
+
+def m_set_fact(args, **_):
+    facts = {k: v for k, v in args.items() if k != "_raw_params"}
+    return {"ansible_facts": facts, "changed": False}
+
+
+def m_fail(args, **_):
+    return {"failed": True, "msg": str(args.get("msg", "Failed as requested from task"))}
+
+
+def m_assert(args, *, variables, **_):
+    that = args.get("that", [])
+    for cond in that if isinstance(that, list) else [that]:
+        if not templating.test(cond, variables):
+            return {"failed": True, "msg": args.get("fail_msg") or args.get("msg") or f"Assertion failed: {cond}",
+                    "assertion": cond}
+    return {"changed": False, "msg_out": args.get("success_msg", "All assertions passed")}
+
+
+def m_wait_for(args, *, ctx, target, local, check, **_):
+    if check:
+        return {"skipped": True, "changed": False}
+    timeout = float(args.get("timeout", 300))
+    time.sleep(float(args.get("delay", 0)))
+    deadline = time.monotonic() + timeout
+    state = args.get("state", "started")
+    while time.monotonic() < deadline:
+        if "port" in args:
+            host = args.get("host", "127.0.0.1")
+            s = socket.socket()
+            s.settimeout(1.0)
+            try:
+                s.connect((host, int(args["port"])))
+                up = True
+            except OSError:
+                up = False
+            finally:
+                s.close()
+            if up == (state in ("started", "present")):
+                return {"changed": False, "elapsed": round(timeout - (deadline - time.monotonic()), 3)}
+        elif "path" in args:
+            p = _path(args["path"], ctx, target, local)
+            if state == "absent":
+                if not p.exists():
+                    return {"changed": False}
+            elif p.exists():
+                rx = args.get("search_regex")
+                if not rx or re.search(rx, p.read_text(errors="replace")):
+                    return {"changed": False}
+        else:
+            return {"changed": False}
+        time.sleep(0.02)
+    return {"failed": True, "msg": f"Timeout when waiting for {args}"}
+
+
+def m_meta(args, **_):
+    return {"changed": False}
+
+
+def m_ping(args, **_):
+    return {"ping": "pong", "changed": False}
+
+
+# ---- tk8s modules -------------------------------------------------------------------------------
+def m_tk8s_daemon(args, *, ctx, target, local, env, check, **_):
+    """name, argv|cmd, state started|stopped|query, env, restart_policy, wait_for_log, timeout."""
+    ex = ctx.executor
+    if ex is None:
+        return {"failed": True, "msg": "tk8s_daemon needs a machine executor"}
+    name = args["name"]
+    state = args.get("state", "started")
+    status = ex.daemon_status(target.name, name)
+    if state == "query":
+        return {"changed": False, "running": status["running"], "pid": status.get("pid"), "stdout": name if status["running"] else ""}
+    if state == "stopped":
+        if check or not status["running"]:
+            return {"changed": status["running"], "running": False}
+        ex.stop_daemon(target.name, name)
+        return {"changed": True, "running": False}
+    if status["running"]:
+        return {"changed": False, "running": True, "pid": status.get("pid")}
+    if check:
+        return {"changed": True, "running": False, "msg": "would start"}
+    argv = args.get("argv") or shlex.split(str(args.get("cmd", "")))
+    denv = {str(k): str(v) for k, v in (args.get("env") or {}).items()}
+    denv.update(env or {})
+    info = ex.start_daemon(target.name, name, [str(a) for a in argv], env=denv,
+                           restart=str(args.get("restart_policy", "unless-stopped")),
+                           wait_for_log=args.get("wait_for_log"), timeout=float(args.get("timeout", 300)))
+    if not info.get("ok"):
+        return {"failed": True, "msg": info.get("msg", "daemon failed to start"), **info}
+    return {"changed": True, "running": True, **info}
+
+
+def m_tk8s_gpu_facts(args, *, ctx, target, local, **_):
+    from .models.hostinfo import discover
+
+    facts = {}
+    ver = Path("/opt/rocm/.info/version")
+    facts["tk8s_rocm_version"] = ver.read_text().strip() if ver.exists() else ""
+    facts["tk8s_kfd"] = os.path.exists("/dev/kfd")
+    inv = discover()
+    facts["tk8s_host_gpus"] = inv.count
+    facts["tk8s_inventory_source"] = inv.source
+    if ctx.executor is not None and not local:
+        facts["tk8s_machine_gpus"] = ctx.executor.machine_gpus(target.name)
+    from .ops import BIN
+
+    facts["tk8s_native_built"] = all((BIN / t).exists() for t in ("tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl"))
+    return {"ansible_facts": facts, "changed": False}
+
+
+def m_tk8s_build(args, *, check, **_):
+    from .utils import build_native
+
+    if check:
+        return {"changed": False, "msg": "build checked only"}
+    t = time.monotonic()
+    before = {k: (p.stat().st_mtime if p.exists() else 0) for k, p in _artefacts(build_native).items()}
+    build_native.build()
+    after = {k: p.stat().st_mtime for k, p in _artefacts(build_native).items()}
+    return {"changed": before != after, "seconds": round(time.monotonic() - t, 3)}
+
+
+def _artefacts(bn) -> dict:
+    out = {"lib": bn.lib_path(), "native": bn.native_module_path(), "topo": bn.topo_module_path()}
+    out.update({n: bn.tool_path(n) for n in list(bn.TOOLS) + ["tk8s-supervise"]})
+    return out
+
+
+def m_tk8s_kube(args, *, ctx, check, **_):
+    """api, project, state present|absent|wait, definition|src, timeout."""
+    from .controlplane.client import ApiError, Client
+    from .kube import apply_objects, delete_objects, load_manifests
+
+    api = str(args["api"])
+    pid = str(args["project"])
+    base = Client(api)
+    kc = base.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
+    from .controlplane.client import client_from_kubeconfig
+
+    k = client_from_kubeconfig(kc)
+    if "definition" in args:
+        objs = args["definition"] if isinstance(args["definition"], list) else [args["definition"]]
+    else:
+        objs = load_manifests(_path(args["src"], ctx, None, True), args.get("vars") or {})
+    state = args.get("state", "present")
+    if check:
+        return {"changed": state != "wait", "objects": len(objs), "msg": "check mode"}
+    try:
+        if state == "absent":
+            n = delete_objects(k, objs)
+            return {"changed": n > 0, "deleted": n}
+        res = apply_objects(k, objs)
+        return {"changed": any(r["created"] for r in res), "objects": res}
+    except ApiError as e:
+        return {"failed": True, "msg": str(e)}
+
+
+MODULES = {
+    "command": m_command, "shell": m_shell, "uri": m_uri, "slurp": m_slurp, "copy": m_copy, "file": m_file,
+    "stat": m_stat, "include_vars": m_include_vars, "pause": m_pause, "debug": m_debug, "set_fact": m_set_fact,
+    "fail": m_fail, "assert": m_assert, "wait_for": m_wait_for, "meta": m_meta, "ping": m_ping,
+    "tk8s_daemon": m_tk8s_daemon, "tk8s_gpu_facts": m_tk8s_gpu_facts, "tk8s_build": m_tk8s_build,
+    "tk8s_kube": m_tk8s_kube,
+}

@@ -154,7 +154,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), links))
 
-    out = {"libtk8s": lib, "native_module": nat, "topo_module": topo}
+    sup_src = NATIVE / "tools" / "tk8s_supervise.cpp"
+    sup = tool_path("tk8s-supervise")
+    if force or _stale(sup, [sup_src]):
+        _run([CXX, "-O2", "-std=c++17", "-Wall", str(sup_src), "-o", str(sup)], verbose)
+
+    out = {"libtk8s": lib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup}
     out.update({n: tool_path(n) for n in TOOLS})
     return out
 
