@@ -1,0 +1,305 @@
+#!/usr/bin/env python3
+"""Headline benchmark: wall-clock of ``./setup.sh`` -> all nodes Ready on the MI355X host.
+
+Metric (BASELINE.json): "wall-clock (s) ./setup.sh -> all nodes Ready; 1/2/4/8 workers".
+``--gpus N`` brings up 1 master + N workers with the ``mi355x-1gpu`` package, i.e. one
+MI355X per worker, so N workers make N x ``amd.com/gpu`` allocatable (weak scaling: the
+per-worker work is fixed, the cluster grows with N).
+
+One *step* is one complete, non-interactive bring-up in a fresh workspace:
+
+    ./setup.sh --answers <N workers, mi355x-1gpu> --yes
+      configure -> provision (terraform/{master,host}) -> ansible/clusterUp.yml
+      (rocmsetup, control plane + environment, worker join + device plugin)
+      -> every worker heartbeating AND validated on its GPU (tk8s-probe: gfx950 discovery,
+         1 GiB HBM write, 256 MiB MD5; the benchmarks.md analogues) -> amd.com/gpu == N
+      -> (N >= 2) RCCL all-reduce Job over all N GPUs, one rank per GPU, checked exactly
+
+The timed interval is the whole ``./setup.sh`` child process, launch to exit, so it
+includes Python start-up, the GPU validation and (N >= 2) the RCCL fabric check; it is
+the conservative reading of "setup.sh -> all nodes Ready". The teardown (``./setup.sh
+-c``) after each step runs outside the timed brackets. The reference publishes no
+bring-up time (BASELINE.json ``published: {}``); ``vs_baseline`` is quoted against the
+51 s of fixed sleeps in the reference's bring-up path, a floor the
+reference can never go below (setup.sh:36,41,46; terraform/*/main.tf:22;
+ansible/roles/ranchermaster/tasks/main.yml:25).
+
+Multi-GPU launch (driver): ``torch.distributed.run --nproc-per-node N bench.py --gpus N``.
+Rank 0 drives the bring-up (it is the operator's shell); every rank joins the barriers
+and synchronises its own device around the timed region; the time reported is the MAX
+over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+if str(REPO) not in sys.path:
+    sys.path.insert(0, str(REPO))
+
+BASELINE_FLOOR_S = 51.0  # reference fixed-sleep floor
+METRIC = "wall-clock (s) ./setup.sh → all nodes Ready; 1/2/4/8 workers"
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Dist:
+    """Barrier + device sync across the torchrun ranks (RCCL on GPU, gloo on CPU)."""
+
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        self.cuda = False
+        self.pg = False
+        try:
+            import torch
+
+            self.torch = torch
+            self.cuda = torch.cuda.is_available()
+        except Exception:  # noqa: BLE001 - torch is optional for the CPU bring-up
+            pass
+        if self.world > 1 and self.torch is not None:
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if self.cuda:
+                self.torch.cuda.set_device(self.local_rank)
+            dist.init_process_group("nccl" if self.cuda else "gloo")
+            self.pg = True
+
+    def sync(self) -> None:
+        if self.cuda:
+            self.torch.cuda.synchronize()
+        if self.pg:
+            import torch.distributed as dist
+
+            if self.cuda:
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+        if self.cuda:
+            self.torch.cuda.synchronize()
+
+    def max(self, v: float) -> float:
+        if not self.pg:
+            return v
+        import torch.distributed as dist
+
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=f"cuda:{self.local_rank}" if self.cuda else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_obj(self, obj):
+        if not self.pg:
+            return obj
+        import torch.distributed as dist
+
+        box = [obj]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def close(self) -> None:
+        if self.pg:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+
+
+def make_workspace(root: Path) -> Path:
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    init_workspace(root)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, root / f)
+    return root
+
+
+def child_env(fake_gpus: int | None) -> dict:
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([str(REPO)] + [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p])
+    env["TK8S_PYTHON"] = sys.executable
+    # the torchrun rank env must not leak into the cluster's own processes
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+              "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+              "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_ERROR_FILE",
+              "GROUP_WORLD_SIZE", "ROLE_NAME", "OMP_NUM_THREADS_SET"):
+        env.pop(k, None)
+    if fake_gpus is not None:
+        env["TK8S_FAKE_GPUS"] = str(fake_gpus)
+    return env
+
+
+def one_bringup(ws: Path, n: int, args, env: dict, log) -> dict:
+    answers = {"nodes": n, "package": args.package, "name": "k8s bench", "confirm": "yes"}
+    (ws / "answers.json").write_text(json.dumps(answers))
+    cmd = ["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", str(_free_port()),
+           "--timeout", str(args.timeout)]
+    if args.no_validate:
+        cmd.append("--no-validate")
+    if args.rccl:
+        cmd += ["--rccl", args.rccl]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, cwd=ws, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=args.timeout + 120)
+    wall = time.perf_counter() - t0
+    log.write(p.stdout)
+    log.flush()
+    if p.returncode != 0:
+        raise RuntimeError(f"./setup.sh exited {p.returncode}:\n{p.stdout[-3000:]}")
+    summary = json.loads(p.stdout.strip().splitlines()[-1])
+    summary["wall_seconds"] = wall
+    return summary
+
+
+def teardown(ws: Path, env: dict, log) -> float:
+    t0 = time.perf_counter()
+    p = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=120)
+    log.write(p.stdout)
+    log.flush()
+    if p.returncode != 0:
+        raise RuntimeError(f"./setup.sh -c exited {p.returncode}:\n{p.stdout[-2000:]}")
+    return time.perf_counter() - t0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1, help="workers (one MI355X each)")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--package", default="mi355x-1gpu")
+    ap.add_argument("--timeout", type=float, default=300.0, help="bound on one bring-up's readiness wait (s)")
+    ap.add_argument("--no-validate", action="store_true", help="skip per-worker GPU validation (not the headline)")
+    ap.add_argument("--rccl", choices=["on", "off"], default=None)
+    ap.add_argument("--fake-gpus", type=int, default=None,
+                    help="CPU rehearsal: N fake gfx950 devices (default: fake 8 when no GPU is present)")
+    ap.add_argument("--workdir", default=None, help="parent of the per-step workspaces (default: a tempdir)")
+    ap.add_argument("--log", default=None, help="append setup.sh output here")
+    args = ap.parse_args(argv)
+
+    d = Dist()
+    n = args.gpus
+    fake = args.fake_gpus
+    if fake is None and not d.cuda and not _has_kfd_gpus():
+        fake = max(8, n)
+    root = Path(args.workdir) if args.workdir else Path(tempfile.mkdtemp(prefix="tk8s-bench-", dir=os.environ.get("TMPDIR", "/tmp")))
+    root.mkdir(parents=True, exist_ok=True)
+    times: list[float] = []
+    summaries: list[dict] = []
+    teardown_s: list[float] = []
+    err = None
+    if d.rank == 0:
+        from tritonk8ssupervisor_amd.utils.build_native import build
+
+        build()  # incremental; no-op when the in-tree build is current
+    env = child_env(fake)
+    log = open(args.log, "a") if (args.log and d.rank == 0) else open(os.devnull, "w")
+    try:
+        for i in range(args.warmup + args.steps):
+            timed = i >= args.warmup
+            ws = root / f"step{i}"
+            if d.rank == 0:
+                make_workspace(ws)
+            d.sync()
+            t0 = time.perf_counter()
+            s = None
+            if d.rank == 0 and err is None:
+                try:
+                    s = one_bringup(ws, n, args, env, log)
+                except Exception as e:  # noqa: BLE001 - reported after the collective
+                    err = str(e)
+            d.sync()
+            dt = time.perf_counter() - t0
+            err = d.bcast_obj(err)
+            if d.rank == 0:
+                try:
+                    teardown_s.append(teardown(ws, env, log))
+                except Exception as e:  # noqa: BLE001 - a failed step is already reported
+                    if err is None:
+                        err = str(e)
+                shutil.rmtree(ws, ignore_errors=True)
+            err = d.bcast_obj(err)
+            if err is not None:
+                break
+            if timed:
+                times.append(d.max(dt))
+                if s is not None:
+                    summaries.append(s)
+            if d.rank == 0:
+                print(f"[bench] step {i} ({'timed' if timed else 'warmup'}): {dt:.3f}s", file=sys.stderr, flush=True)
+    finally:
+        log.close()
+        if d.rank == 0 and not args.workdir:
+            shutil.rmtree(root, ignore_errors=True)
+    d.close()
+    if d.rank != 0:
+        return 0 if err is None else 1
+    if err is not None:
+        print(json.dumps({"metric": METRIC, "value": None, "error": err[-2000:]}))
+        return 1
+    mean = sum(times) / len(times)
+    ready = [s["ready_seconds"] for s in summaries]
+    phases: dict[str, float] = {}
+    for s in summaries:
+        for k, v in s.get("phases", {}).items():
+            phases[k] = phases.get(k, 0.0) + v / len(summaries)
+    last = summaries[-1] if summaries else {}
+    out = {
+        "metric": METRIC,
+        "value": round(mean, 4),
+        "unit": "s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(mean * 1000.0, 2),
+        "higher_is_better": False,
+        "scaling": "weak",
+        "vs_baseline": round(mean / BASELINE_FLOOR_S, 5),
+        "baseline": {"value": BASELINE_FLOOR_S, "what": "reference bring-up fixed-sleep floor (BASELINE.md); "
+                     "the reference publishes no bring-up time"},
+        "dtype": "fp32",
+        "data": "synthetic" + (" (fake GPUs: CPU rehearsal, not a GPU measurement)" if fake else ""),
+        "config": {"model": f"1 master + {n} workers x {args.package}", "global_batch": n, "seq_len": 0,
+                   "parallelism": f"workers{n}", "validate": not args.no_validate,
+                   "rccl": (args.rccl or ("on" if n >= 2 else "off"))},
+        "min_s": round(min(times), 4),
+        "max_s": round(max(times), 4),
+        "ready_s_inside_setup": round(sum(ready) / len(ready), 4) if ready else None,
+        "teardown_s": round(sum(teardown_s) / len(teardown_s), 4) if teardown_s else None,
+        "phases_s": {k: round(v, 4) for k, v in phases.items()},
+        "gpus_allocatable": last.get("gpus_allocatable"),
+        "nodes_validated": last.get("nodes_validated"),
+        "rccl_peak_busbw_gbps": (last.get("rccl") or {}).get("peak_busbw_gbps"),
+    }
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def _has_kfd_gpus() -> bool:
+    try:
+        from tritonk8ssupervisor_amd.models.hostinfo import discover
+
+        return discover().count > 0
+    except Exception:  # noqa: BLE001
+        return False
+
+
+if __name__ == "__main__":
+    sys.exit(main())
