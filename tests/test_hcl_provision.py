@@ -1,0 +1,240 @@
+"""HCL subset, rancher.tf rendering (setup.sh:162-198) and the provisioning engine
+(terraform get/plan/apply/destroy, setup.sh:154-159, 498-503) over the local provider."""
+import json
+import os
+from pathlib import Path
+
+import pytest
+
+from tritonk8ssupervisor_amd import hcl
+from tritonk8ssupervisor_amd.orchestrator import init_workspace
+from tritonk8ssupervisor_amd.provider.local import LocalProvider
+from tritonk8ssupervisor_amd.provision import Engine
+
+REF = Path("/root/reference")
+
+
+def test_parse_blocks_lists_maps_comments():
+    b = hcl.parse('''
+    # comment
+    // another
+    /* block
+       comment */
+    provider "triton" { account = "me"  url = "https://x" }
+    module "m1" {
+      source = "master"
+      networks = ["a", "b",]
+      n = 3
+      ok = true
+      tags = { role = "host", "k" = "v" }
+      key = "${file("/etc/hostname")}"
+    }
+    ''')
+    (p,) = b.children("provider")
+    assert p.labels == ["triton"] and p.attrs == {"account": "me", "url": "https://x"}
+    (m,) = b.children("module")
+    assert m.attrs["networks"] == ["a", "b"] and m.attrs["n"] == 3 and m.attrs["ok"] is True
+    assert m.attrs["tags"] == {"role": "host", "k": "v"}
+    assert m.attrs["key"] == '${file("/etc/hostname")}'
+
+
+def test_duplicate_attribute_is_reported():
+    b = hcl.parse('resource "t" "r" {\n tags = { a = "1" }\n tags = { a = "2" }\n}\n')
+    (r,) = b.children("resource")
+    assert r.attrs["tags"] == {"a": "2"}
+    assert r.duplicates  # the reference declares tags twice (terraform/master/main.tf:6-8, 33-35)
+
+
+def test_parse_errors():
+    with pytest.raises(hcl.HclError):
+        hcl.parse('module "x" { a = ')
+    with pytest.raises(hcl.HclError):
+        hcl.parse("/* never closed")
+
+
+def test_interpolation_types_and_functions(tmp_path):
+    (tmp_path / "k.pub").write_text("ssh-ed25519 AAA me\n")
+    ctx = {"var": {"networks": ["n1", "n2"], "hostname": "kubenode1"}, "__dir__": str(tmp_path),
+           "tk8s_machine": {"host": {"primaryip": "127.0.1.2"}}}
+    assert hcl.interpolate("${var.networks}", ctx) == ["n1", "n2"]  # exact interpolation keeps list type
+    assert hcl.interpolate("nets=${var.networks}", ctx) == "nets=n1,n2"
+    assert hcl.interpolate('${file("k.pub")}', ctx) == "ssh-ed25519 AAA me\n"
+    assert hcl.interpolate("echo ${tk8s_machine.host.primaryip} >> hosts.ip", ctx) == "echo 127.0.1.2 >> hosts.ip"
+    assert hcl.interpolate({"a": ["${var.hostname}"]}, ctx) == {"a": ["kubenode1"]}
+    with pytest.raises(hcl.HclError):
+        hcl.interpolate("${var.nope}", ctx)
+    with pytest.raises(hcl.HclError):
+        hcl.interpolate('${file("missing")}', ctx)
+
+
+def test_render_root_golden():
+    text = hcl.render_root("local", "me", "/k/id_ed25519", "/k/id_ed25519.pub", "SHA256:abc", "local://h",
+                           "kubemaster", ["net-a"], ["kubenode1", "kubenode2"], ["net-a", "net-b"], "pkg-1")
+    want = '''provider "local" {
+    account = "me"
+    key_material = "${file("/k/id_ed25519")}"
+    key_id = "SHA256:abc"
+    url = "local://h"
+}
+
+module "kubemaster" {
+    source = "master"
+    hostname = "kubemaster"
+    networks = ["net-a"]
+    root_authorized_keys = "${file("/k/id_ed25519.pub")}"
+    package = "pkg-1"
+}
+
+module "kubenode1" {
+    source = "host"
+    hostname = "kubenode1"
+    networks = ["net-a","net-b"]
+    root_authorized_keys = "${file("/k/id_ed25519.pub")}"
+    package = "pkg-1"
+}
+
+module "kubenode2" {
+    source = "host"
+    hostname = "kubenode2"
+    networks = ["net-a","net-b"]
+    root_authorized_keys = "${file("/k/id_ed25519.pub")}"
+    package = "pkg-1"
+}
+'''
+    assert text == want
+    parsed = hcl.parse(text)
+    assert [m.labels[0] for m in parsed.children("module")] == ["kubemaster", "kubenode1", "kubenode2"]
+
+
+@pytest.mark.skipif(not (REF / "terraform").is_dir(), reason="reference checkout not mounted")
+def test_parses_the_reference_terraform_modules():
+    # the engine must read Terraform-0.9-era files like the reference's own modules
+    for mod in ("master", "host"):
+        b = hcl.parse_dir(REF / "terraform" / mod)
+        (r,) = b.children("resource")
+        assert r.labels[0] == "triton_machine"
+        assert {"hostname", "networks", "root_authorized_keys", "image", "package"} <= {v.labels[0] for v in b.children("variable")}
+        assert "tags" in r.duplicates
+        kinds = [p.labels[0] for p in r.children("provisioner")]
+        assert kinds == ["remote-exec", "local-exec"]
+
+
+def test_own_modules_keep_reference_variables():
+    for mod in ("master", "host"):
+        b = hcl.parse_dir(Path(__file__).resolve().parents[1] / "terraform" / mod)
+        assert {"hostname", "networks", "root_authorized_keys", "image", "package"} == {v.labels[0] for v in b.children("variable")}
+        (r,) = b.children("resource")
+        assert not r.duplicates
+
+
+# ---- engine -------------------------------------------------------------------------------
+@pytest.fixture
+def ws(tmp_path, monkeypatch):
+    monkeypatch.setenv("TK8S_FAKE_GPUS", "8")
+    monkeypatch.delenv("TK8S_FAULTS", raising=False)
+    return init_workspace(tmp_path)
+
+
+def _rancher_tf(ws, prov, nodes, package="mi355x-1gpu"):
+    env = prov.env()
+    key = prov.find_key(env["SDC_KEY_ID"])
+    pub = prov.network_by_id_or_name("local-public").id
+    text = hcl.render_root("local", env["SDC_ACCOUNT"], key, key + ".pub", env["SDC_KEY_ID"], env["SDC_URL"],
+                           "kubemaster", [pub], [f"kubenode{i}" for i in range(1, nodes + 1)], [pub],
+                           prov.package_by_id_or_name(package).id)
+    (ws.tf / "rancher.tf").write_text(text)
+
+
+def test_engine_get_plan_apply_destroy(ws):
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 3)
+    eng = Engine(ws.tf, prov)
+    assert eng.get() == ["kubemaster", "kubenode1", "kubenode2", "kubenode3"]
+    assert (ws.tf / ".terraform" / "modules" / "kubenode1").resolve() == (ws.tf / "host").resolve()
+    plan = eng.plan()
+    assert [a.action for a in plan] == ["create"] * 4
+    assert "Plan: 4 to add, 0 to change, 0 to destroy." in Engine.plan_summary(plan)
+    res = eng.apply()
+    assert res.ok and len(res.created) == 4
+    ms = eng.machines()
+    assert ms["kubemaster"].gpus == []  # the master never takes a GPU
+    gpus = sorted(g for n in ("kubenode1", "kubenode2", "kubenode3") for g in ms[n].gpus)
+    assert len(gpus) == 3 and len(set(gpus)) == 3  # exclusive GPU slices
+    # hand-off files in module order, one IP per line (race-free rewrite of terraform/*/main.tf:30)
+    assert (ws.tf / "masters.ip").read_text().split() == [ms["kubemaster"].primaryip]
+    assert (ws.tf / "hosts.ip").read_text().split() == [ms[f"kubenode{i}"].primaryip for i in (1, 2, 3)]
+    assert len({m.primaryip for m in ms.values()}) == 4 or os.environ.get("TK8S_SINGLE_IP") == "1"
+    # second apply is a no-op
+    assert [a.action for a in eng.plan()] == ["no-op"] * 4
+    res2 = eng.apply()
+    assert res2.ok and not res2.created and len(res2.unchanged) == 4
+    # destroy frees everything
+    assert len(eng.destroy()) == 4
+    assert eng.state()["resources"] == {}
+    assert prov.list_machines() == []
+    alloc = json.loads((ws.state_dir / "alloc.json").read_text())
+    assert alloc["machines"] == {} and alloc["gpus"] == {}
+
+
+def test_engine_scale_down_plans_destroy(ws):
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 2)
+    eng = Engine(ws.tf, prov)
+    eng.get()
+    assert eng.apply().ok
+    _rancher_tf(ws, prov, 1)
+    acts = {a.address: a.action for a in eng.plan()}
+    assert acts["module.kubenode2.tk8s_machine.host"] == "destroy"
+
+
+def test_engine_gpu_capacity_is_the_provisioning_limit(ws, monkeypatch):
+    monkeypatch.setenv("TK8S_FAKE_GPUS", "2")
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 3)
+    eng = Engine(ws.tf, prov)
+    eng.get()
+    res = eng.apply()
+    assert not res.ok and len(res.failed) == 1 and len(res.created) == 3
+    assert "provisioning limit" in next(iter(res.failed.values()))
+
+
+def test_engine_retries_injected_create_failure(ws, monkeypatch):
+    monkeypatch.setenv("TK8S_FAULTS", "provision.create@kubenode2")
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 2)
+    eng = Engine(ws.tf, prov, retries=1)
+    eng.get()
+    res = eng.apply()
+    assert res.ok, res.failed  # first attempt fails, the retry succeeds
+
+
+def test_engine_no_retries_marks_failure(ws, monkeypatch):
+    monkeypatch.setenv("TK8S_FAULTS", "provision.create@kubenode1")
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 1)
+    eng = Engine(ws.tf, prov, retries=0)
+    eng.get()
+    res = eng.apply()
+    assert not res.ok and "module.kubenode1.tk8s_machine.host" in res.failed
+    assert not (ws.tf / "hosts.ip").exists()  # missing hand-off file == setup.sh:117-120 error path
+
+
+def test_engine_tainted_resource_is_replaced(ws):
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 1)
+    eng = Engine(ws.tf, prov)
+    eng.get()
+    assert eng.apply().ok
+    st = eng.state()
+    st["resources"]["module.kubenode1.tk8s_machine.host"]["tainted"] = True
+    (ws.tf / "terraform.tfstate").write_text(json.dumps(st))
+    assert {a.address: a.action for a in eng.plan()}["module.kubenode1.tk8s_machine.host"] == "replace"
+    res = eng.apply()
+    assert res.ok and res.created == ["module.kubenode1.tk8s_machine.host"]
+
+
+def test_engine_rejects_unknown_module_argument(ws):
+    prov = LocalProvider(ws.state_dir)
+    (ws.tf / "rancher.tf").write_text('module "x" {\n source = "host"\n hostname = "x"\n networks = []\n bogus = 1\n}\n')
+    with pytest.raises(Exception, match="unknown arguments"):
+        Engine(ws.tf, prov).specs()

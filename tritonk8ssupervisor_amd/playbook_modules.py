@@ -117,6 +117,8 @@ def m_uri(args, *, check, **_):
     except urllib.error.HTTPError as e:
         status, content = e.code, e.read()
     except (urllib.error.URLError, OSError) as e:
+        if check:  # dry run: the service this GET targets is not up yet
+            return {"skipped": True, "changed": False, "status": -1, "msg": f"check mode: {url} unreachable: {e}"}
         return {"failed": True, "status": -1, "msg": f"request to {url} failed: {e}", "url": url}
     res = {"status": status, "url": url, "changed": method != "GET", "failed": status not in codes}
     text = content.decode(errors="replace")
@@ -141,8 +143,10 @@ def _path(p: str, ctx, target, local) -> Path:
     return Path(ctx.executor.machine_dir(target.name)) / pp
 
 
-def m_slurp(args, *, ctx, target, local, **_):
+def m_slurp(args, *, ctx, target, local, check, **_):
     p = _path(args.get("src") or args.get("path"), ctx, target, local)
+    if check and not p.exists():  # produced by a task that check mode did not run
+        return {"skipped": True, "changed": False, "msg": f"check mode: {p} does not exist yet"}
     data = p.read_bytes()
     return {"content": base64.b64encode(data).decode(), "encoding": "base64", "source": str(p), "changed": False}
 
@@ -283,10 +287,12 @@ def m_ping(args, **_):
 def m_tk8s_daemon(args, *, ctx, target, local, env, check, **_):
     """name, argv|cmd, state started|stopped|query, env, restart_policy, wait_for_log, timeout."""
     ex = ctx.executor
-    if ex is None:
-        return {"failed": True, "msg": "tk8s_daemon needs a machine executor"}
     name = args["name"]
     state = args.get("state", "started")
+    if ex is None:
+        if check:  # dry run without provisioned machines (BASELINE.json config 1)
+            return {"changed": state == "started", "running": False, "msg": "check mode: no machine executor"}
+        return {"failed": True, "msg": "tk8s_daemon needs a machine executor"}
     status = ex.daemon_status(target.name, name)
     if state == "query":
         return {"changed": False, "running": status["running"], "pid": status.get("pid"), "stdout": name if status["running"] else ""}
@@ -351,13 +357,8 @@ def m_tk8s_kube(args, *, ctx, check, **_):
     from .controlplane.client import ApiError, Client
     from .kube import apply_objects, delete_objects, load_manifests
 
-    api = str(args["api"])
-    pid = str(args["project"])
-    base = Client(api)
-    kc = base.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
     from .controlplane.client import client_from_kubeconfig
 
-    k = client_from_kubeconfig(kc)
     if "definition" in args:
         objs = args["definition"] if isinstance(args["definition"], list) else [args["definition"]]
     else:
@@ -365,6 +366,10 @@ def m_tk8s_kube(args, *, ctx, check, **_):
     state = args.get("state", "present")
     if check:
         return {"changed": state != "wait", "objects": len(objs), "msg": "check mode"}
+    api = str(args["api"])
+    pid = str(args["project"])
+    kc = Client(api).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
+    k = client_from_kubeconfig(kc)
     try:
         if state == "absent":
             n = delete_objects(k, objs)

@@ -14,6 +14,8 @@ from __future__ import annotations
 
 import ast
 import base64
+import io
+import tokenize
 import json
 import os
 import re
@@ -81,37 +83,6 @@ class _UndefinedValue:
 
     def __repr__(self):
         return f"Undefined({self.name})"
-
-
-def _split_filters(expr: str) -> list[str]:
-    parts, depth, cur, quote = [], 0, [], None
-    i = 0
-    while i < len(expr):
-        c = expr[i]
-        if quote:
-            cur.append(c)
-            if c == "\\" and i + 1 < len(expr):
-                cur.append(expr[i + 1])
-                i += 1
-            elif c == quote:
-                quote = None
-        elif c in "'\"":
-            quote = c
-            cur.append(c)
-        elif c in "([{":
-            depth += 1
-            cur.append(c)
-        elif c in ")]}":
-            depth -= 1
-            cur.append(c)
-        elif c == "|" and depth == 0 and not (i + 1 < len(expr) and expr[i + 1] == "|"):
-            parts.append("".join(cur))
-            cur = []
-        else:
-            cur.append(c)
-        i += 1
-    parts.append("".join(cur))
-    return [p.strip() for p in parts]
 
 
 _WORDS = re.compile(r"\b(true|false|none|True|False|None)\b")
@@ -205,7 +176,26 @@ class _Eval:
         key = self(n.slice)
         return self._get(base, key, ast.unparse(n.value))
 
+    def _lenient(self, node):
+        saved, self.strict = self.strict, False
+        try:
+            return self(node)
+        finally:
+            self.strict = saved
+
     def v_Call(self, n):
+        if isinstance(n.func, ast.Name) and n.func.id == "__filter__":
+            name = n.args[0].value
+            if name not in FILTERS:
+                raise TemplateError(f"unknown filter {name!r}")
+            val = self._lenient(n.args[1])
+            if isinstance(val, _UndefinedValue) and name not in ("default", "d"):
+                if self.strict:
+                    raise Undefined(f"'{val.name}' is undefined")
+                return val  # propagate to the enclosing (strict) expression
+            return FILTERS[name](val, *[self(a) for a in n.args[2:]])
+        if isinstance(n.func, ast.Name) and n.func.id == "__test__":
+            return _jinja_test(n.args[0].value, self._lenient(n.args[1]))
         fn = self(n.func)
         if not callable(fn) or getattr(fn, "__self__", None) is None:
             raise TemplateError(f"call of {ast.unparse(n.func)} not allowed")
@@ -260,27 +250,124 @@ class _Eval:
         return self(n.body) if self(n.test) else self(n.orelse)
 
 
-def evaluate(expr: str, variables: dict, strict: bool = True) -> Any:
-    parts = _split_filters(expr.strip())
+_KEYWORDS = {"and", "or", "not", "in", "is", "if", "else", "True", "False", "None"}
+_OPEN = {")": "(", "]": "[", "}": "{"}
+
+
+def _operand_start(out: list[str]) -> int:
+    """Index in ``out`` where the postfix expression ending at ``out[-1]`` starts
+    (atom followed by ``.name`` / ``[...]`` / ``(...)`` trailers)."""
+    i = len(out) - 1
+    while i >= 0:
+        t = out[i]
+        if t in _OPEN:
+            depth = 0
+            while i >= 0:
+                if out[i] in _OPEN:
+                    depth += 1
+                elif out[i] in _OPEN.values():
+                    depth -= 1
+                    if depth == 0:
+                        break
+                i -= 1
+            if i < 0:
+                raise TemplateError("unbalanced brackets before filter")
+        elif not (t[:1].isalnum() or t[:1] in "_'\"") or t in _KEYWORDS - {"True", "False", "None"}:
+            raise TemplateError(f"filter/test without an operand near {t!r}")
+        # out[i] is the first token of this piece; a trailer continues the chain
+        if i > 1 and out[i - 1] == ".":
+            i -= 2
+            continue
+        prev = out[i - 1] if i > 0 else ""
+        if out[i] in _OPEN.values() and prev and (prev in _OPEN or ((prev[:1].isalpha() or prev[:1] == "_")
+                                                                    and prev not in _KEYWORDS)):
+            i -= 1
+            continue
+        return i
+    raise TemplateError("filter/test without an operand")
+
+
+def _rewrite(expr: str) -> str:
+    """Jinja filters/tests -> calls the evaluator understands, with Jinja precedence:
+    ``x | f(a) + 1`` -> ``__filter__('f', x, a) + 1``; ``x is not defined`` -> ``not __test__('defined', x)``."""
     try:
-        tree = ast.parse(_pyify(parts[0]) or "None", mode="eval")
+        toks = [t for t in tokenize.generate_tokens(io.StringIO(expr).readline)
+                if t.type not in (tokenize.NEWLINE, tokenize.NL, tokenize.ENDMARKER, tokenize.INDENT, tokenize.DEDENT)]
+    except (tokenize.TokenError, IndentationError, SyntaxError) as e:
+        raise TemplateError(f"cannot tokenize {expr!r}: {e}") from e
+    words = [t.string for t in toks]
+    out: list[str] = []
+    i = 0
+    while i < len(words):
+        w = words[i]
+        nxt = words[i + 1] if i + 1 < len(words) else ""
+        if w == "|" and nxt and (nxt[:1].isalpha() or nxt[:1] == "_"):
+            start = _operand_start(out)
+            operand = " ".join(out[start:])
+            del out[start:]
+            name, i = nxt, i + 2
+            args = ""
+            if i < len(words) and words[i] == "(":
+                depth, j = 0, i
+                while j < len(words):
+                    depth += words[j] == "(" or words[j] in ("[", "{")
+                    depth -= words[j] == ")" or words[j] in ("]", "}")
+                    if depth == 0:
+                        break
+                    j += 1
+                args = _rewrite(" ".join(words[i + 1:j])) if j > i + 1 else ""
+                i = j + 1
+            out += ["__filter__", "(", repr(name), ",", "(", operand, ")"] + ([",", args] if args.strip() else []) + [")"]
+            continue
+        if w == "is" and out:
+            neg = nxt == "not"
+            k = i + 2 if neg else i + 1
+            if k < len(words):
+                start = _operand_start(out)
+                operand = " ".join(out[start:])
+                del out[start:]
+                name = words[k]
+                out += (["not"] if neg else []) + ["__test__", "(", repr(name.lower()), ",", "(", operand, ")", ")"]
+                i = k + 1
+                continue
+        if w == "~":
+            w = "+"  # Jinja string concatenation (string operands)
+        out.append(w)
+        i += 1
+    return " ".join(out)
+
+
+def _jinja_test(name: str, v: Any) -> bool:
+    undef = isinstance(v, _UndefinedValue)
+    if name == "defined":
+        return not undef
+    if name == "undefined":
+        return undef
+    if undef:
+        raise Undefined(f"'{v.name}' is undefined")
+    r = v if isinstance(v, dict) else {}
+    table = {
+        "none": lambda: v is None, "string": lambda: isinstance(v, str),
+        "number": lambda: isinstance(v, (int, float)) and not isinstance(v, bool),
+        "mapping": lambda: isinstance(v, dict), "sequence": lambda: isinstance(v, (list, tuple, str)),
+        "iterable": lambda: isinstance(v, (list, tuple, str, dict)),
+        "true": lambda: v is True, "false": lambda: v is False, "boolean": lambda: isinstance(v, bool),
+        "failed": lambda: bool(r.get("failed")), "failure": lambda: bool(r.get("failed")),
+        "succeeded": lambda: not r.get("failed"), "success": lambda: not r.get("failed"),
+        "changed": lambda: bool(r.get("changed")), "skipped": lambda: bool(r.get("skipped")),
+    }
+    if name not in table:
+        raise TemplateError(f"unknown test {name!r}")
+    return table[name]()
+
+
+def evaluate(expr: str, variables: dict, strict: bool = True) -> Any:
+    src = _rewrite(_pyify(expr.strip()))
+    try:
+        tree = ast.parse(src or "None", mode="eval")
     except SyntaxError as e:
-        raise TemplateError(f"cannot parse {parts[0]!r}: {e}") from e
-    val = _Eval(variables, strict and len(parts) == 1)(tree)
-    for f in parts[1:]:
-        m = re.fullmatch(r"([A-Za-z_][A-Za-z0-9_]*)\s*(\((.*)\))?", f, re.S)
-        if not m:
-            raise TemplateError(f"bad filter {f!r}")
-        name, args = m.group(1), m.group(3)
-        if name not in FILTERS:
-            raise TemplateError(f"unknown filter {name!r}")
-        argv = []
-        if args and args.strip():
-            argv = list(_Eval(variables, strict)(ast.parse("(" + _pyify(args) + ",)", mode="eval")))
-        if isinstance(val, _UndefinedValue) and name not in ("default", "d"):
-            if strict:
-                raise Undefined(f"'{val.name}' is undefined")
-        val = FILTERS[name](val, *argv)
+        raise TemplateError(f"cannot parse {expr!r}: {e}") from e
+    val = _Eval(variables, strict)(tree)
     if isinstance(val, _UndefinedValue) and strict:
         raise Undefined(f"'{val.name}' is undefined")
     return val
