@@ -1,0 +1,230 @@
+"""End-to-end bring-up on the CPU box: ``./setup.sh`` -> all nodes Ready -> ``./setup.sh -c``.
+
+The local provider runs every machine as a sandbox + process group on this host; the GPU
+inventory is faked (TK8S_FAKE_GPUS=8 virtual gfx950 devices) so the allocation, validation
+and RCCL-job paths run without a GPU (BASELINE.json configs 1-2).
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture
+def ws(tmp_path):
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, tmp_path / f)
+    yield tmp_path
+    # never leave processes behind, whatever the test did
+    subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=_env(), capture_output=True, timeout=120)
+
+
+def _env(**kw):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(REPO)
+    env["TK8S_PYTHON"] = sys.executable
+    env["TK8S_FAKE_GPUS"] = "8"
+    env.pop("TK8S_FAULTS", None)
+    env.update({k: str(v) for k, v in kw.items()})
+    return env
+
+
+def _setup(ws, *args, env=None, timeout=180):
+    return subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", *args], cwd=ws, env=env or _env(),
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _summary(r):
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _pids(ws):
+    out = []
+    for pf in (ws / ".tk8s" / "machines").glob("*/run/*.pid"):
+        try:
+            out.append(int(json.loads(pf.read_text())["pid"]))
+        except (ValueError, KeyError, OSError):
+            pass
+    return out
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except OSError:
+        return False
+    try:  # zombies count as gone
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split(") ", 1)[1][0] != "Z"
+    except OSError:
+        return False
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_setup_ready_and_clean_teardown(ws, n):
+    t = time.monotonic()
+    s = _summary(_setup(ws, "--nodes", str(n)))
+    wall = time.monotonic() - t
+    assert s["nodes"] == n and s["gpus_allocatable"] == n and s["nodes_validated"] == n
+    if n >= 2:  # the RCCL fabric check ran across all GPUs, one rank per GPU
+        assert s["rccl"]["ok"] and s["rccl"]["nranks"] == n
+        assert len({r["node"] for r in s["rccl"]["rank_results"]}) == n
+    assert wall < 60  # the reference's fixed sleeps alone are 51 s
+    # reference artefacts exist, with reference names
+    for rel in ("config", "terraform/rancher.tf", "terraform/masters.ip", "terraform/hosts.ip", "ansible/hosts",
+                "ansible/roles/ranchermaster/vars/vars.yml", "ansible/tmp/kubernetes_environment.id"):
+        assert (ws / rel).exists(), rel
+    assert len((ws / "terraform" / "hosts.ip").read_text().split()) == n
+    cfg = (ws / "config").read_text()
+    assert f"KUBERNETES_NUMBER_OF_NODES={n}" in cfg and "ANSIBLE_HOST_KEY_CHECKING=False" in cfg
+    # kubectl sees every node Ready with its GPU
+    r = subprocess.run(["./kubectl", "get", "nodes", "-o", "json"], cwd=ws, env=_env(), capture_output=True, text=True)
+    items = json.loads(r.stdout)["items"]
+    assert sorted(i["metadata"]["name"] for i in items) == [f"kubenode{i}" for i in range(1, n + 1)]
+    assert all(i["status"]["allocatable"]["amd.com/gpu"] == "1" for i in items)
+    # distinct GPUs per worker
+    ids = [i["status"]["devices"][0]["id"] for i in items]
+    assert len(set(ids)) == n
+    pids = _pids(ws)
+    assert len(pids) >= n + 1 and all(_alive(p) for p in pids)
+    # teardown: machines gone, every artefact removed -- including the env-id file the
+    # reference never cleans (setup.sh:513 removes ./tmp/* instead of ansible/tmp/*)
+    r = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "All clear!" in r.stdout
+    for rel in ("config", "terraform/rancher.tf", "terraform/masters.ip", "terraform/hosts.ip", "terraform/terraform.tfstate",
+                "ansible/hosts", "ansible/roles/ranchermaster/vars/vars.yml", "ansible/tmp/kubernetes_environment.id",
+                "terraform/.terraform"):
+        assert not (ws / rel).exists(), rel
+    assert (ws / "ansible" / "ansible.cfg").read_text().count("private_key_file = \n") == 1
+    deadline = time.monotonic() + 10
+    while any(_alive(p) for p in pids) and time.monotonic() < deadline:
+        time.sleep(0.05)
+    assert not any(_alive(p) for p in pids)
+
+
+def test_refuses_to_run_over_a_previous_configuration(ws):
+    _summary(_setup(ws, "--nodes", "1"))
+    r = _setup(ws, "--nodes", "1")
+    assert r.returncode != 0 and "./setup.sh -c" in (r.stdout + r.stderr)
+
+
+def test_clean_without_confirmation_keeps_everything(ws):
+    _summary(_setup(ws, "--nodes", "1"))
+    r = subprocess.run(["./setup.sh", "-c"], cwd=ws, env=_env(), input="no\n", capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "WARNING: You are about to destroy" in r.stdout
+    assert (ws / "config").exists() and (ws / "terraform" / "rancher.tf").exists()
+
+
+def test_interactive_prompts_via_stdin(ws):
+    # 8 prompts (all defaults except 2 nodes) + yes
+    answers = "\n".join(["", "", "", "", "2", "", "", "", "yes"]) + "\n"
+    r = subprocess.run(["./setup.sh", "--json", "--port", "0"], cwd=ws, env=_env(), input=answers,
+                       capture_output=True, text=True, timeout=180)
+    s = _summary(r)
+    assert s["nodes"] == 2
+    assert "Verify that the following configuration is correct" in r.stdout
+
+
+def test_no_at_confirmation_exits_zero_and_creates_nothing(ws):
+    answers = "\n" * 8 + "no\n"
+    r = subprocess.run(["./setup.sh"], cwd=ws, env=_env(), input=answers, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    assert not (ws / "terraform" / "rancher.tf").exists()
+
+
+def test_agent_crash_mid_join_is_restarted(ws):
+    # fault injection: kubenode1's agent dies right after registering, once; the supervisor
+    # (tk8s-supervise, restart unless-stopped) brings it back and the cluster still converges
+    s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=_env(TK8S_FAULTS="agent.crash@kubenode1:1")))
+    assert s["nodes_validated"] == 2
+    assert (ws / ".tk8s" / "machines" / "kubenode1" / "run" / "crash.count").read_text() == "1"
+
+
+def test_validation_failure_fails_setup_fast(ws):
+    t = time.monotonic()
+    r = _setup(ws, "--nodes", "2", env=_env(TK8S_FAKE_PROBE_FAIL="kubenode2"))
+    assert r.returncode == 2 and "GPU validation failed" in r.stderr
+    assert time.monotonic() - t < 60
+
+
+def test_stalled_node_hits_the_bounded_timeout(ws):
+    # the reference's readiness loop has no timeout (setup.sh:59-85); ours exits 124
+    t = time.monotonic()
+    r = _setup(ws, "--nodes", "1", "--timeout", "3", env=_env(TK8S_FAKE_PROBE_HANG="kubenode1"))
+    assert r.returncode == 124 and "not ready after" in r.stderr
+    assert time.monotonic() - t < 60
+
+
+def test_lost_heartbeats_mark_node_not_ready(ws):
+    _summary(_setup(ws, "--nodes", "2", "--rccl", "off", "--node-grace", "0.5"))
+    # stop kubenode2's agent (and its supervisor): the lease expires and the node goes NotReady
+    from tritonk8ssupervisor_amd.utils.procs import kill_pidfile
+
+    assert kill_pidfile(ws / ".tk8s" / "machines" / "kubenode2" / "run" / "agent.pid")
+    deadline = time.monotonic() + 10
+    while time.monotonic() < deadline:
+        r = subprocess.run(["./kubectl", "get", "nodes"], cwd=ws, env=_env(), capture_output=True, text=True)
+        if "NotReady" in r.stdout:
+            break
+        time.sleep(0.1)
+    line = next(l for l in r.stdout.splitlines() if l.startswith("kubenode2"))
+    assert "NotReady" in line
+
+
+def test_provision_failure_then_resume(ws):
+    r = _setup(ws, "--nodes", "2", env=_env(TK8S_FAKE_GPUS=1))
+    assert r.returncode != 0 and "provisioning limit" in r.stdout
+    st = json.loads((ws / ".tk8s" / "state.json").read_text())
+    assert "provision" not in st["completed"]
+    s = _summary(_setup(ws, "--resume", "--rccl", "off"))
+    assert s["nodes"] == 2 and s["gpus_allocatable"] == 2
+    st = json.loads((ws / ".tk8s" / "state.json").read_text())
+    assert set(st["completed"]) >= {"configure", "provision", "ansible-config", "ansible", "ready"}
+
+
+def test_status_and_events_log(ws):
+    _summary(_setup(ws, "--nodes", "2", "--rccl", "off"))
+    r = subprocess.run(["./tk8s", "status", "--json"], cwd=ws, env=_env(), capture_output=True, text=True)
+    st = json.loads(r.stdout)
+    assert st["cluster"]["nodes_ready"] == 2 and st["cluster"]["gpus_allocatable"] == 2
+    assert set(st["timings"]) >= {"provision", "ansible", "ready"}
+    from tritonk8ssupervisor_amd.utils.events import read_events
+
+    evs = read_events(ws / ".tk8s" / "events.jsonl")
+    names = [e["event"] for e in evs]
+    assert "setup_start" in names and "setup_done" in names and names.count("machine_created") == 3
+
+
+def test_kubectl_workload_on_the_cluster(ws, tmp_path_factory):
+    _summary(_setup(ws, "--nodes", "2", "--rccl", "off"))
+    d = tmp_path_factory.mktemp("m")
+    (d / "job.yaml").write_text(
+        "apiVersion: batch/v1\nkind: Job\nmetadata:\n  name: hello\nspec:\n  completions: 2\n  parallelism: 2\n"
+        "  completionMode: Indexed\n  template:\n    spec:\n      restartPolicy: Never\n      containers:\n"
+        "        - name: c\n          command: [\"sh\", \"-c\", \"echo rank=$JOB_COMPLETION_INDEX gpus=$HIP_VISIBLE_DEVICES\"]\n"
+        "          resources:\n            limits:\n              amd.com/gpu: 1\n")
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=_env(), capture_output=True, text=True, timeout=60)
+    r = kc("apply", "-f", str(d / "job.yaml"))
+    assert r.returncode == 0, r.stderr
+    r = kc("wait", "job/hello", "--timeout", "30")
+    assert r.returncode == 0, r.stdout + r.stderr
+    pods = json.loads(kc("get", "pods", "-l", "job-name=hello", "-o", "json").stdout)["items"]
+    assert len(pods) == 2 and all(p["status"]["phase"] == "Succeeded" for p in pods)
+    logs = [kc("logs", p["metadata"]["name"]).stdout.strip() for p in pods]
+    assert sorted(l.split()[0] for l in logs) == ["rank=0", "rank=1"]
+    vis = {l.split("gpus=")[1] for l in logs}
+    assert len(vis) == 2  # each rank saw exactly its own GPU
+    r = kc("describe", "node", "kubenode1")
+    assert "amd.com/gpu" in r.stdout

@@ -1,0 +1,294 @@
+"""Control plane: the Rancher-style environment/registration API the roles call
+(ranchermaster/tasks/main.yml:29-52, rancherhost/tasks/main.yml:11-34), node leases,
+the amd.com/gpu scheduler and the DaemonSet / Job / Deployment controllers."""
+import json
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import pytest
+
+from tritonk8ssupervisor_amd.controlplane.client import ApiError, Client, client_from_kubeconfig
+
+REPO = Path(__file__).resolve().parents[1]
+GPU = "amd.com/gpu"
+
+
+def _start(tmp_path, grace=0.6, state_dir=None):
+    ready = tmp_path / f"ready-{time.monotonic_ns()}.json"
+    argv = [sys.executable, "-m", "tritonk8ssupervisor_amd.controlplane", "--host", "127.0.0.1", "--port", "0",
+            "--node-grace", str(grace), "--ready-file", str(ready)]
+    if state_dir:
+        argv += ["--state-dir", str(state_dir)]
+    p = subprocess.Popen(argv, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    deadline = time.monotonic() + 30
+    while not ready.exists():
+        assert p.poll() is None, p.stdout.read().decode()
+        assert time.monotonic() < deadline
+        time.sleep(0.01)
+    info = json.loads(ready.read_text())
+    return p, Client(info["base"], timeout=10)
+
+
+def _stop(p):
+    p.terminate()
+    try:
+        p.wait(10)
+    except subprocess.TimeoutExpired:
+        p.kill()
+
+
+@pytest.fixture
+def cp(tmp_path):
+    p, c = _start(tmp_path)
+    yield c
+    _stop(p)
+
+
+def _env(c, name="k8s dev"):
+    tmpl = c.get("/v2-beta/projectTemplates", query={"name": "kubernetes"})
+    body = {"description": name, "name": name, "projectTemplateId": tmpl["data"][0]["id"], "allowSystemRole": False,
+            "members": [], "virtualMachine": False, "servicesPortRange": None, "projectLinks": []}
+    proj = c.post("/v2-beta/projects", body)
+    return proj
+
+
+def _join(c, pid, name, ngpu=1, validated=True):
+    tok = c.post("/v1/registrationtokens", query={"projectId": pid})
+    url = c.get(tok["links"]["self"].split(c.base, 1)[1])["registrationUrl"]
+    path = url.split(c.base, 1)[1]
+    boot = c.get(path)
+    assert boot["projectId"] == pid
+    devs = [{"id": f"gpu{i}", "health": "Healthy"} for i in range(ngpu)]
+    reg = c.post(path, {"name": name, "ip": "127.0.0.1", "devices": devs, "capacity": {"cpu": "8"}})
+    nc = Client(c.base, token=reg["nodeToken"], prefix=reg["apiPrefix"])
+    return nc, reg
+
+
+def _heartbeat(nc, name):
+    return nc.put(nc.k8s(f"/api/v1/nodes/{name}/status"), {})
+
+
+def _set_pod(nc, ns, pod, phase, result=None):
+    st = {"phase": phase}
+    if result is not None:
+        st["result"] = result
+    return nc.put(nc.k8s(f"/api/v1/namespaces/{ns}/pods/{pod}/status"), {"status": st})
+
+
+def test_environment_and_registration_flow(cp):
+    # exactly the calls of ranchermaster (29-49) and rancherhost (11-24): 201s and links.self
+    tmpl = cp.get("/v2-beta/projectTemplates", query={"name": "kubernetes"})
+    assert tmpl["data"][0]["name"] == "kubernetes"
+    proj = _env(cp)
+    assert proj["id"] and proj["name"] == "k8s dev"
+    with pytest.raises(ApiError) as ei:
+        cp.post("/v1/registrationtokens", query={"projectId": "nope"})
+    assert ei.value.status == 404
+    nc, reg = _join(cp, proj["id"], "kubenode1", ngpu=2)
+    kc = cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"})
+    k = client_from_kubeconfig(kc)
+    n = k.get(k.k8s("/api/v1/nodes/kubenode1"))
+    assert n["status"]["capacity"][GPU] == "2" and n["status"]["allocatable"][GPU] == "2"
+    assert n["metadata"]["labels"]["amd.com/gpu.family"] == "gfx950"
+    conds = {c["type"]: c["status"] for c in n["status"]["conditions"]}
+    assert conds["Ready"] == "True" and conds["AMDGPUValidated"] == "Unknown"
+    with pytest.raises(ApiError):
+        cp.post(reg["apiPrefix"].replace("/kubernetes", "") + "/bad")  # unknown route
+    with pytest.raises(ApiError) as ei:
+        cp.get("/v1/scripts/not-a-token")
+    assert ei.value.status == 403
+
+
+def test_dashboard_is_the_readiness_oracle(cp):
+    proj = _env(cp)
+    with pytest.raises(ApiError) as ei:  # setup.sh:66-68: "Service Unavailable" until a node is up
+        cp.get(f"/r/projects/{proj['id']}/kubernetes-dashboard:9090/", raw=True)
+    assert ei.value.status == 503
+    _join(cp, proj["id"], "kubenode1", ngpu=0)
+    body = cp.get(f"/r/projects/{proj['id']}/kubernetes-dashboard:9090/", raw=True)
+    assert "kubernetes" in body and "kubenode1" in body
+
+
+def test_writes_need_the_project_token(cp):
+    proj = _env(cp)
+    pod = {"metadata": {"name": "p"}, "spec": {"containers": [{"name": "c", "command": ["true"]}]}}
+    with pytest.raises(ApiError) as ei:
+        cp.post(f"/r/projects/{proj['id']}/kubernetes/api/v1/namespaces/default/pods", pod)
+    assert ei.value.status == 401
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    assert k.post(k.k8s("/api/v1/namespaces/default/pods"), pod)["metadata"]["name"] == "p"
+    with pytest.raises(ApiError) as ei:
+        k.post(k.k8s("/api/v1/namespaces/default/pods"), pod)
+    assert ei.value.status == 409
+
+
+def test_node_lease_expiry_and_recovery(cp):
+    proj = _env(cp)
+    nc, _ = _join(cp, proj["id"], "kubenode1", ngpu=1)
+    st = cp.get("/v1/cluster/status", query={"project": proj["id"]})
+    assert st["nodes_ready"] == 1
+    time.sleep(1.5)  # grace 0.6 s, no heartbeats
+    st = cp.get("/v1/cluster/status", query={"project": proj["id"]})
+    assert st["nodes_ready"] == 0 and st["gpus_allocatable"] == 0
+    _heartbeat(nc, "kubenode1")
+    st = cp.get("/v1/cluster/status", query={"project": proj["id"]})
+    assert st["nodes_ready"] == 1
+    evs = cp.get(f"/r/projects/{proj['id']}/kubernetes/api/v1/events")["items"]
+    assert any(e["reason"] == "NodeNotReady" for e in evs)
+
+
+def test_gpu_scheduler_respects_capacity_and_validation(cp):
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    n1, _ = _join(cp, proj["id"], "kubenode1", ngpu=1)
+    n2, _ = _join(cp, proj["id"], "kubenode2", ngpu=2)
+
+    def gpod(name, g):
+        return {"metadata": {"name": name}, "spec": {"restartPolicy": "Never", "containers": [
+            {"name": "c", "command": ["true"], "resources": {"limits": {GPU: g}}}]}}
+
+    k.post(k.k8s("/api/v1/namespaces/default/pods"), gpod("a", 1))
+    p = k.get(k.k8s("/api/v1/namespaces/default/pods/a"))
+    assert "nodeName" not in p["spec"]  # nodes not validated yet: GPU pods wait
+    assert any(c["type"] == "PodScheduled" and c["status"] == "False" for c in p["status"]["conditions"])
+    # validate both nodes through the validation DaemonSet
+    ds = {"metadata": {"name": "val", "labels": {"tk8s.amd.com/validation": "true"}},
+          "spec": {"selector": {"matchLabels": {"app": "val"}}, "template": {"spec": {"restartPolicy": "Never",
+                   "nodeSelector": {"amd.com/gpu.family": "gfx950"}, "containers": [{"name": "p", "command": ["true"]}]}}}}
+    k.post(k.k8s("/apis/apps/v1/namespaces/kube-system/daemonsets"), ds)
+    pods = k.get(k.k8s("/api/v1/namespaces/kube-system/pods"))["items"]
+    assert sorted(o["spec"]["nodeName"] for o in pods) == ["kubenode1", "kubenode2"]
+    for o, nc in zip(sorted(pods, key=lambda o: o["spec"]["nodeName"]), (n1, n2)):
+        _set_pod(nc, "kube-system", o["metadata"]["name"], "Succeeded", {"hbm": {"gbps": 4400.0}})
+    st = cp.get("/v1/cluster/status", query={"project": proj["id"]})
+    assert st["nodes_validated"] == 2 and st["gpus_allocatable"] == 3
+    node = k.get(k.k8s("/api/v1/nodes/kubenode1"))
+    assert node["metadata"]["annotations"]["tk8s.amd.com/hbm-write-gbps"] == "4400.0"
+    # now the pending pod binds; a 2-GPU pod can only go to kubenode2; a third GPU pod cannot fit
+    assert k.get(k.k8s("/api/v1/namespaces/default/pods/a"))["spec"].get("nodeName")
+    k.post(k.k8s("/api/v1/namespaces/default/pods"), gpod("b", 2))
+    b = k.get(k.k8s("/api/v1/namespaces/default/pods/b"))
+    a = k.get(k.k8s("/api/v1/namespaces/default/pods/a"))
+    assert b["spec"].get("nodeName") == "kubenode2" and a["spec"]["nodeName"] == "kubenode1"
+    k.post(k.k8s("/api/v1/namespaces/default/pods"), gpod("c", 1))
+    assert "nodeName" not in k.get(k.k8s("/api/v1/namespaces/default/pods/c"))["spec"]
+    # finishing "a" frees its GPU for "c"
+    _set_pod(n1, "default", "a", "Succeeded")
+    assert k.get(k.k8s("/api/v1/namespaces/default/pods/c"))["spec"]["nodeName"] == "kubenode1"
+
+
+def test_validation_failure_marks_node(cp):
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    nc, _ = _join(cp, proj["id"], "kubenode1", ngpu=1)
+    ds = {"metadata": {"name": "val", "labels": {"tk8s.amd.com/validation": "true"}},
+          "spec": {"template": {"spec": {"restartPolicy": "Never", "containers": [{"name": "p", "command": ["true"]}]}}}}
+    k.post(k.k8s("/apis/apps/v1/namespaces/kube-system/daemonsets"), ds)
+    (pod,) = k.get(k.k8s("/api/v1/namespaces/kube-system/pods"))["items"]
+    _set_pod(nc, "kube-system", pod["metadata"]["name"], "Failed")
+    w = cp.get("/v1/cluster/wait", query={"project": proj["id"], "nodes": 1, "gpus": 1, "validated": 1, "timeout": 5})
+    assert w["failed"] and not w["ready"] and w["nodes_validation_failed"] == 1
+
+
+def test_indexed_job_gang_and_completion(cp):
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    ncs = [_join(cp, proj["id"], f"kubenode{i}", ngpu=0)[0] for i in (1, 2)]
+    job = {"metadata": {"name": "rccl"}, "spec": {"completions": 2, "parallelism": 2, "completionMode": "Indexed",
+                                                  "backoffLimit": 0, "template": {"spec": {"restartPolicy": "Never",
+                                                  "containers": [{"name": "r", "command": ["true"]}]}}}}
+    k.post(k.k8s("/apis/batch/v1/namespaces/kube-system/jobs"), job)
+    pods = k.get(k.k8s("/api/v1/namespaces/kube-system/pods"), query={"labelSelector": "job-name=rccl"})["items"]
+    assert len(pods) == 2
+    idx = sorted(int(next(e["value"] for e in o["spec"]["containers"][0]["env"] if e["name"] == "JOB_COMPLETION_INDEX"))
+                 for o in pods)
+    assert idx == [0, 1]
+    assert len({o["spec"]["nodeName"] for o in pods}) == 2  # spread: one rank per node
+    by_node = {f"kubenode{i}": nc for i, nc in zip((1, 2), ncs)}
+    for o in pods:
+        _set_pod(by_node[o["spec"]["nodeName"]], "kube-system", o["metadata"]["name"], "Succeeded")
+    j = k.get(k.k8s("/apis/batch/v1/namespaces/kube-system/jobs/rccl"))
+    assert j["status"]["succeeded"] == 2
+    assert any(c["type"] == "Complete" and c["status"] == "True" for c in j["status"]["conditions"])
+    w = cp.get("/v1/cluster/wait", query={"project": proj["id"], "nodes": 2, "validated": 0, "job": "kube-system/rccl",
+                                          "timeout": 2})
+    assert w["ready"] and w["job"] == "Complete"
+
+
+def test_job_backoff_exceeded_fails(cp):
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    nc, _ = _join(cp, proj["id"], "kubenode1", ngpu=0)
+    job = {"metadata": {"name": "j"}, "spec": {"completions": 1, "backoffLimit": 0, "template": {"spec": {
+        "restartPolicy": "Never", "containers": [{"name": "r", "command": ["false"]}]}}}}
+    k.post(k.k8s("/apis/batch/v1/namespaces/default/jobs"), job)
+    (pod,) = k.get(k.k8s("/api/v1/namespaces/default/pods"))["items"]
+    _set_pod(nc, "default", pod["metadata"]["name"], "Failed")
+    j = k.get(k.k8s("/apis/batch/v1/namespaces/default/jobs/j"))
+    assert any(c["type"] == "Failed" and c.get("reason") == "BackoffLimitExceeded" for c in j["status"]["conditions"])
+
+
+def test_deployment_scales_and_delete_cascades(cp):
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    _join(cp, proj["id"], "kubenode1", ngpu=0)
+    dep = {"metadata": {"name": "guestbook"}, "spec": {"replicas": 3, "selector": {"matchLabels": {"app": "gb"}},
+                                                       "template": {"spec": {"containers": [{"name": "c", "command": ["sleep", "1"]}]}}}}
+    k.post(k.k8s("/apis/apps/v1/namespaces/default/deployments"), dep)
+    pods = k.get(k.k8s("/api/v1/namespaces/default/pods"), query={"labelSelector": "app=gb"})["items"]
+    assert len(pods) == 3 and all(o["spec"].get("nodeName") == "kubenode1" for o in pods)
+    k.delete(k.k8s("/apis/apps/v1/namespaces/default/deployments/guestbook"))
+    assert k.get(k.k8s("/api/v1/namespaces/default/pods"))["items"] == []
+
+
+def test_kv_rendezvous_long_poll(cp):
+    import threading
+
+    got = {}
+
+    def reader():
+        got["v"] = cp.get("/v1/kv/job/uid", query={"wait": "5"}, raw=True)
+
+    t = threading.Thread(target=reader)
+    t.start()
+    time.sleep(0.2)
+    Client(cp.base).put("/v1/kv/job/uid", "abc123")
+    t.join(10)
+    assert got["v"] == "abc123"
+    with pytest.raises(ApiError):
+        cp.get("/v1/kv/none", raw=True)
+
+
+def test_watch_returns_events_after_resource_version(cp):
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    rv = int(k.get(k.k8s("/api/v1/nodes"))["metadata"]["resourceVersion"])
+    _join(cp, proj["id"], "kubenode1", ngpu=0)
+    rv2, evs = k.watch(k.k8s("/api/v1/nodes"), rv, timeout=5)
+    assert rv2 > rv and any(e["object"]["metadata"]["name"] == "kubenode1" for e in evs)
+
+
+def test_state_snapshot_survives_restart(tmp_path):
+    sd = tmp_path / "cpstate"
+    p, c = _start(tmp_path, grace=30, state_dir=sd)
+    try:
+        proj = _env(c)
+        _join(c, proj["id"], "kubenode1", ngpu=1)
+    finally:
+        _stop(p)
+    p, c = _start(tmp_path, grace=30, state_dir=sd)
+    try:
+        st = c.get("/v1/cluster/status", query={"project": proj["id"]})
+        assert st["nodes"] == 1 and st["node_names"] == ["kubenode1"]
+    finally:
+        _stop(p)
+
+
+def test_metrics_and_version(cp):
+    proj = _env(cp)
+    _join(cp, proj["id"], "kubenode1", ngpu=1)
+    text = cp.get("/metrics", raw=True)
+    assert "tk8s_nodes" in text
+    assert "version" in json.dumps(cp.get("/version")).lower()

@@ -132,7 +132,7 @@ class ControlPlane:
         self._seq += 1
         name = f"{involved.get('name', 'x')}.{self._seq:x}"
         self.store.put("events", _key(project, ns, name), {
-            "kind": "Event", "metadata": {"name": name, "namespace": ns},
+            "kind": "Event", "metadata": {"name": name, "namespace": ns}, "_project": project,
             "involvedObject": involved, "reason": reason, "message": message, "type": etype,
             "firstTimestamp": now_iso(), "count": 1,
         })

@@ -224,7 +224,9 @@ class Setup:
             if ws.config.exists():
                 raise SetupError("error: old configuration found\n    clean the configuration (./setup.sh -c)")
             cfg = ClusterConfig(TK8S_BACKEND=self.backend)
-            if self.master_port:
+            if self.master_port == 0:  # any free port (benchmarks / tests run clusters side by side)
+                cfg.TK8S_MASTER_PORT = _free_port()
+            elif self.master_port:
                 cfg.TK8S_MASTER_PORT = self.master_port
             env = self.provider.env()
             cfg.SDC_URL, cfg.SDC_ACCOUNT, cfg.SDC_KEY_ID = env["SDC_URL"], env["SDC_ACCOUNT"], env["SDC_KEY_ID"]
@@ -454,6 +456,14 @@ class Setup:
 
         kc = Client(base).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
         atomic_write_json(self.ws.state_dir / "kubeconfig.json", kc)
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("0.0.0.0", 0))
+        return s.getsockname()[1]
 
 
 def _flush_print(s: str) -> None:
