@@ -116,6 +116,7 @@ int main(int argc, char** argv) {
       _exit(127);
     }
     g_child = pid;
+    if (g_stop) kill(pid, SIGTERM);  // a signal that landed between fork() and the store above
     write_pidfile(pidfile, pid, restarts);
     while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
     }

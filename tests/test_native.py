@@ -1,0 +1,104 @@
+"""Native layer on the CPU box: the gfx950 build (hipcc cross-compiles without a GPU), the
+restart-policy supervisor (tk8s-supervise, the `docker --restart` of the reference's
+rancher/server and rancher/agent, ranchermaster/tasks/main.yml:11) and the tools' no-GPU
+failure mode (fail loudly, never a silent fallback)."""
+import json
+import os
+import signal
+import subprocess
+import time
+from pathlib import Path
+
+import pytest
+
+BIN = Path(__file__).resolve().parents[1] / "tritonk8ssupervisor_amd" / "bin"
+
+
+def test_build_produces_gfx950_code_objects(native_build):
+    for name in ("libtk8s", "native_module", "topo_module", "tk8s-supervise", "tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl"):
+        assert Path(native_build[name]).exists(), name
+    lib = Path(native_build["libtk8s"]).read_bytes()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in lib  # device code is built for MI355X only
+    assert b"gfx942" not in lib and b"gfx90a" not in lib
+
+
+def test_build_is_incremental(native_build):
+    from tritonk8ssupervisor_amd.utils.build_native import build
+
+    before = {k: Path(v).stat().st_mtime for k, v in native_build.items()}
+    t = time.monotonic()
+    out = build()
+    assert time.monotonic() - t < 5
+    assert {k: Path(v).stat().st_mtime for k, v in out.items()} == before
+
+
+def test_native_module_imports_without_a_gpu(native_build):
+    from tritonk8ssupervisor_amd.ops import native
+
+    nat = native()
+    info = json.loads(nat.gpuinfo_json(False))
+    if info.get("ok"):
+        pytest.skip("a GPU is visible here")
+    assert info["device_count"] == 0 and "error" in info
+
+
+@pytest.mark.parametrize("tool", ["tk8s-gpuinfo", "tk8s-probe"])
+def test_tools_fail_loudly_without_a_gpu(native_build, tool):
+    if Path("/dev/kfd").exists():
+        pytest.skip("GPU host")
+    r = subprocess.run([str(BIN / tool)], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert json.loads(r.stdout)["ok"] is False
+
+
+def _pidfile(p):
+    deadline = time.monotonic() + 5
+    while time.monotonic() < deadline:
+        try:
+            return json.loads(Path(p).read_text())
+        except (OSError, ValueError):
+            time.sleep(0.01)
+    raise AssertionError("no pidfile")
+
+
+def test_supervise_restarts_on_failure_then_gives_up(native_build, tmp_path):
+    pf, log, cnt = tmp_path / "x.pid", tmp_path / "x.log", tmp_path / "count"
+    r = subprocess.run([str(BIN / "tk8s-supervise"), "--pidfile", str(pf), "--log", str(log), "--restart", "on-failure",
+                        "--max-restarts", "2", "--backoff-ms", "10", "--", "sh", "-c", f"echo run >> {cnt}; exit 3"],
+                       timeout=30)
+    assert r.returncode == 3
+    assert cnt.read_text().count("run") == 3  # first run + 2 restarts
+    assert "not restarting" in log.read_text()
+    assert not pf.exists()
+
+
+def test_supervise_on_failure_does_not_restart_success(native_build, tmp_path):
+    cnt = tmp_path / "count"
+    r = subprocess.run([str(BIN / "tk8s-supervise"), "--pidfile", str(tmp_path / "p"), "--restart", "on-failure", "--",
+                        "sh", "-c", f"echo run >> {cnt}"], timeout=30, capture_output=True)
+    assert r.returncode == 0 and cnt.read_text().count("run") == 1
+
+
+def test_supervise_sigterm_stops_child_and_group(native_build, tmp_path):
+    pf = tmp_path / "s.pid"
+    p = subprocess.Popen([str(BIN / "tk8s-supervise"), "--pidfile", str(pf), "--restart", "unless-stopped", "--",
+                          "sleep", "600"], start_new_session=True)
+    info = _pidfile(pf)
+    assert info["pid"] == p.pid and info["pgid"] == p.pid and info["restarts"] == 0
+    child = info["child"]
+    os.kill(child, signal.SIGKILL)  # crash the child: it comes back
+    deadline = time.monotonic() + 5
+    while time.monotonic() < deadline and _pidfile(pf)["child"] == child:
+        time.sleep(0.01)
+    info2 = _pidfile(pf)
+    assert info2["child"] != child and info2["restarts"] == 1
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(10) is not None
+    assert not pf.exists()
+    with pytest.raises(ProcessLookupError):
+        os.kill(info2["child"], 0)
+
+
+def test_supervise_usage_errors(native_build):
+    r = subprocess.run([str(BIN / "tk8s-supervise"), "--restart", "sometimes", "--", "true"], capture_output=True)
+    assert r.returncode == 2 and b"usage" in r.stderr

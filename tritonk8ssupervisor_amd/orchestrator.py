@@ -373,8 +373,8 @@ class Setup:
         k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
         job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
         if os.environ.get("TK8S_FAKE_GPUS"):
-            cmd = [sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.fake_rccl", "--rank", "$(JOB_COMPLETION_INDEX)",
-                   "--nranks", str(g), "--kv-url", f"$(TK8S_KV_URL)/{job}/uid"]
+            cmd = [sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.gloo_allreduce", "--rank", "$(JOB_COMPLETION_INDEX)",
+                   "--nranks", str(g), "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
         else:
             cmd = ["tk8s-rccl", "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "0",
                    "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",

@@ -1,0 +1,125 @@
+"""CPU twin of ``tk8s-rccl`` (N3): one process per rank, torch.distributed **gloo** all-reduce.
+
+Used for the cluster fabric check when the GPUs are faked (``TK8S_FAKE_GPUS``, CPU-only
+hosts and tests). It follows the real job's protocol step by step so the control-plane path is
+exercised unchanged: rank 0 publishes its rendezvous address to the control-plane KV store
+(HTTP PUT), the other ranks long-poll it (GET ``?wait=``), then every rank runs an
+RCCL-tests-style sweep with an exact result check and prints ONE JSON line with the same keys
+as native/tools/tk8s_rccl.cpp (``ok``, ``nranks``, ``rank``, ``peak_busbw_gbps``, ``results``).
+
+Check (N6 semantics): rank r contributes ``(r + 1) * p[i]`` with ``p[i] = (i % m) + 1``;
+every element must equal ``n (n + 1) / 2 * p[i]`` exactly. ``m`` keeps every partial sum an
+exactly representable integer: 251 for fp32 (< 2^24), 4 for bf16 (sums <= 256 up to n = 8).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+import urllib.request
+
+
+def _publish(url: str, value: str) -> None:
+    urllib.request.urlopen(urllib.request.Request(url, data=value.encode(), method="PUT"), timeout=10).read()
+
+
+def _fetch(url: str, timeout: float) -> str:
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        try:
+            v = urllib.request.urlopen(url + "?wait=10", timeout=15).read().decode().strip()
+            if v:
+                return v
+        except OSError:
+            time.sleep(0.02)
+    raise TimeoutError(f"no rendezvous address at {url} after {timeout:.0f}s")
+
+
+def _free_port(host: str) -> int:
+    with socket.socket() as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters: int, warmup: int,
+          dtype: str = "float32") -> dict:
+    import torch
+    import torch.distributed as dist
+
+    dt = {"float32": torch.float32, "bfloat16": torch.bfloat16}[dtype]
+    esize = torch.tensor([], dtype=dt).element_size()
+    results, ok, peak = [], True, 0.0
+    size = max(min_bytes, esize)
+    while size <= max_bytes:
+        count = max(1, size // esize)
+        pat = (torch.arange(count, dtype=torch.int64) % (251 if dt == torch.float32 else 4) + 1)
+        want = (pat * (n * (n + 1) // 2)).to(dt)
+        buf = torch.empty(count, dtype=dt)
+        for _ in range(warmup):
+            buf.copy_(pat * (rank + 1))
+            dist.all_reduce(buf)
+        times = []
+        bad = 0
+        for _ in range(max(1, iters)):
+            buf.copy_(pat * (rank + 1))
+            dist.barrier()
+            t = time.perf_counter()
+            dist.all_reduce(buf)
+            times.append(time.perf_counter() - t)
+            bad = max(bad, int((buf != want).sum()))
+        sec = sorted(times)[len(times) // 2]
+        algbw = count * esize / sec / 1e9
+        busbw = algbw * (2 * (n - 1) / n if n > 1 else 1.0)
+        peak = max(peak, busbw)
+        ok &= bad == 0
+        results.append({"bytes": count * esize, "count": count, "time_us": sec * 1e6, "algbw_gbps": algbw,
+                        "busbw_gbps": busbw, "bad": bad})
+        size *= factor
+    return {"ok": ok, "results": results, "peak_busbw_gbps": peak}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--nranks", type=int, required=True)
+    ap.add_argument("--kv-url", required=True)
+    ap.add_argument("--min-bytes", type=int, default=1024)
+    ap.add_argument("--max-bytes", type=int, default=4 << 20)
+    ap.add_argument("--factor", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--dtype", choices=["float32", "bfloat16"], default="float32")
+    ap.add_argument("--timeout", type=float, default=60.0)
+    a = ap.parse_args(argv)
+    t0 = time.monotonic()
+    host = os.environ.get("NODE_IP", "127.0.0.1")
+    try:
+        if a.rank == 0:
+            addr = f"{host}:{_free_port(host)}"
+            _publish(a.kv_url, addr)
+        else:
+            addr = _fetch(a.kv_url, a.timeout)
+        import torch.distributed as dist
+        from datetime import timedelta
+
+        dist.init_process_group("gloo", init_method=f"tcp://{addr}", rank=a.rank, world_size=a.nranks,
+                                timeout=timedelta(seconds=a.timeout))
+        init_s = time.monotonic() - t0
+        res = sweep(a.rank, a.nranks, a.min_bytes, a.max_bytes, a.factor, a.iters, a.warmup, a.dtype)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 - reported as the pod result
+        print(json.dumps({"ok": False, "rank": a.rank, "nranks": a.nranks, "error": f"{type(e).__name__}: {e}"}))
+        return 2
+    out = {"ok": res["ok"], "backend": "gloo", "mode": "multi_process", "nranks": a.nranks, "rank": a.rank,
+           "dtype": a.dtype, "init_seconds": round(init_s, 4), "peak_busbw_gbps": res["peak_busbw_gbps"],
+           "results": res["results"]}
+    print(json.dumps(out))
+    return 0 if res["ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
