@@ -192,6 +192,7 @@ def main(argv=None) -> int:
                     help="CPU rehearsal: N fake gfx950 devices (default: fake 8 when no GPU is present)")
     ap.add_argument("--workdir", default=None, help="parent of the per-step workspaces (default: a tempdir)")
     ap.add_argument("--log", default=None, help="append setup.sh output here")
+    ap.add_argument("--keep-events", default=None, help="copy each step's .tk8s/events.jsonl into this directory")
     args = ap.parse_args(argv)
 
     d = Dist()
@@ -229,6 +230,9 @@ def main(argv=None) -> int:
             dt = time.perf_counter() - t0
             err = d.bcast_obj(err)
             if d.rank == 0:
+                if args.keep_events and (ws / ".tk8s" / "events.jsonl").exists():
+                    Path(args.keep_events).mkdir(parents=True, exist_ok=True)
+                    shutil.copy2(ws / ".tk8s" / "events.jsonl", Path(args.keep_events) / f"step{i}.events.jsonl")
                 try:
                     teardown_s.append(teardown(ws, env, log))
                 except Exception as e:  # noqa: BLE001 - a failed step is already reported

@@ -1,15 +1,20 @@
 // Streaming validation kernels for gfx950 (CDNA4): HBM fill/verify (N4), Philox fill (N5 input),
 // copy (N7 local + xGMI peer pull), all-reduce fill/check (N6).
 //
-// Design notes (MI355X-first, see /opt/skills/guides):
-//  * 16 B per lane per access (global_{load,store}_dwordx4): 1 KiB per wave-instruction, the
-//    coalescing sweet spot (cdna_hip_programming.md Guideline 13).
-//  * Grid-stride loops over min(work, CUs x 8) 256-thread workgroups (Guideline 11): enough
-//    waves to cover HBM latency on all 256 CUs / 8 XCDs without launch-overhead blow-up.
-//  * 4-way unrolled stores so each wave keeps several 1 KiB stores in flight.
-//  * Non-temporal stores for the once-written 1 GiB fill (no reason to pollute L2/MALL).
+// Design notes (MI355X-first, see /opt/skills/guides; shapes picked by measurement with
+// native/bench/stream_variants.hip on one MI355X, profiles/r1_bd2/stream_variants.jsonl):
+//  * 16 B per lane per access (global_{load,store}_dwordx4): 1 KiB per wave-instruction.
+//  * Block-contiguous SLABS, not a grid-stride interleave: block b owns bytes
+//    [b*per, (b+1)*per) and walks them 4 KiB (one block-instruction) at a time, 4 instructions
+//    in flight per lane. Each block then streams through whole DRAM pages instead of touching
+//    a new page per instruction. Measured on 1 GiB fill: grid-stride 4.3 TB/s -> slab 6.2 TB/s
+//    (hipMemsetD32 6.66); 256 MiB copy (read + write counted): 4.96 -> 6.42 TB/s (hipMemcpy
+//    D2D 4.96-5.43). HBM3E spec peak is 8 TB/s.
+//  * Grid = CUs x 16 blocks of 256 threads for the fill, CUs x 32 for the copy (best of the
+//    4/8/16/32 per-CU sweep); plain stores for the fill (non-temporal measured 3-9 % slower),
+//    non-temporal loads+stores for the once-touched copy.
 //  * Reductions: wave64 __shfl_xor butterfly -> LDS across the 4 waves -> ONE atomic per block
-//    (Guideline 12).
+//    (cdna_hip_programming.md Guideline 12).
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -49,20 +54,29 @@ static unsigned grid_for(size_t items, int blocks_per_cu = 8) {
 // ------------------------------------------------------------------------------------------
 // N4: HBM fill
 // ------------------------------------------------------------------------------------------
+// Slab bounds of block b over n items: [lo, hi).
+__device__ __forceinline__ void slab_bounds(size_t n, size_t* lo, size_t* hi) {
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  *lo = per * blockIdx.x;
+  const size_t end = *lo + per;
+  *hi = end < n ? end : n;
+}
+
 template <bool kNT>
 __global__ __launch_bounds__(kBlock) void hbm_fill_kernel(u32x4* __restrict__ dst, size_t n16,
                                                           unsigned value) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+  size_t lo, hi;
+  slab_bounds(n16, &lo, &hi);
   const u32x4 v = {value, value, value, value};
-  for (; i + 3 * stride < n16; i += 4 * stride) {
+  size_t i = lo + threadIdx.x;
+  for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if constexpr (kNT) __builtin_nontemporal_store(v, dst + i + u * stride);
-      else dst[i + u * stride] = v;
+      if constexpr (kNT) __builtin_nontemporal_store(v, dst + i + u * kBlock);
+      else dst[i + u * kBlock] = v;
     }
   }
-  for (; i < n16; i += stride) {
+  for (; i < hi; i += kBlock) {
     if constexpr (kNT) __builtin_nontemporal_store(v, dst + i);
     else dst[i] = v;
   }
@@ -72,7 +86,7 @@ void hbm_fill(void* dst, size_t nbytes, uint32_t value, StoreMode mode, hipStrea
   if (nbytes % 16) throw std::invalid_argument("hbm_fill: nbytes must be a multiple of 16");
   const size_t n16 = nbytes / 16;
   if (!n16) return;
-  const unsigned grid = grid_for(n16);
+  const unsigned grid = grid_for(n16 / 4, 16);
   if (mode == StoreMode::kNonTemporal)
     hipLaunchKernelGGL(hbm_fill_kernel<true>, dim3(grid), dim3(kBlock), 0, stream,
                        static_cast<u32x4*>(dst), n16, value);
@@ -97,9 +111,18 @@ __device__ __forceinline__ float wave_max_f32(float v) {
 __global__ __launch_bounds__(kBlock) void verify_fill_kernel(const u32x4* __restrict__ src,
                                                              size_t n16, unsigned value,
                                                              unsigned long long* bad_words) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  size_t lo, hi;
+  slab_bounds(n16, &lo, &hi);
   unsigned long long bad = 0;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += stride) {
+  size_t i = lo + threadIdx.x;
+  for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bad += (v[u].x != value) + (v[u].y != value) + (v[u].z != value) + (v[u].w != value);
+  }
+  for (; i < hi; i += kBlock) {
     const u32x4 v = src[i];
     bad += (v.x != value) + (v.y != value) + (v.z != value) + (v.w != value);
   }
@@ -121,7 +144,7 @@ void verify_fill(const void* src, size_t nbytes, uint32_t value, unsigned long l
   if (nbytes % 16) throw std::invalid_argument("verify_fill: nbytes must be a multiple of 16");
   const size_t n16 = nbytes / 16;
   if (!n16) return;
-  hipLaunchKernelGGL(verify_fill_kernel, dim3(grid_for(n16)), dim3(kBlock), 0, stream,
+  hipLaunchKernelGGL(verify_fill_kernel, dim3(grid_for(n16 / 4, 16)), dim3(kBlock), 0, stream,
                      static_cast<const u32x4*>(src), n16, value, bad_words);
   TK8S_HIP_CHECK(hipGetLastError());
 }
@@ -172,23 +195,24 @@ void philox_fill(void* dst, size_t nbytes, uint64_t seed, hipStream_t stream) {
 __global__ __launch_bounds__(kBlock) void stream_copy_kernel(u32x4* __restrict__ dst,
                                                              const u32x4* __restrict__ src,
                                                              size_t n16) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
+  size_t lo, hi;
+  slab_bounds(n16, &lo, &hi);
+  size_t i = lo + threadIdx.x;
+  for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
     u32x4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * kBlock);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * kBlock);
   }
-  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  for (; i < hi; i += kBlock) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 void stream_copy(void* dst, const void* src, size_t nbytes, hipStream_t stream) {
   if (nbytes % 16) throw std::invalid_argument("stream_copy: nbytes must be a multiple of 16");
   const size_t n16 = nbytes / 16;
   if (!n16) return;
-  hipLaunchKernelGGL(stream_copy_kernel, dim3(grid_for(n16)), dim3(kBlock), 0, stream,
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(grid_for(n16 / 4, 32)), dim3(kBlock), 0, stream,
                      static_cast<u32x4*>(dst), static_cast<const u32x4*>(src), n16);
   TK8S_HIP_CHECK(hipGetLastError());
 }

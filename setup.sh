@@ -9,6 +9,8 @@ cd "$(dirname "$0")"
 PY="${TK8S_PYTHON:-python3}"
 if [[ "${1:-}" == "-c" ]]; then
     shift
-    exec "$PY" -m tritonk8ssupervisor_amd.cli clean "$@"
+    exec "$PY" -S -m tritonk8ssupervisor_amd.cli clean "$@"
 fi
-exec "$PY" -m tritonk8ssupervisor_amd.cli setup "$@"
+# -S: skip site-packages .pth processing at start-up (tritonk8ssupervisor_amd/__init__.py adds
+# the site directories back); the CLI's start-up is part of the bring-up time.
+exec "$PY" -S -m tritonk8ssupervisor_amd.cli setup "$@"

@@ -25,7 +25,7 @@ resource "tk8s_machine" "master" {
 
     inline = [
       "test -d run && test -d logs && test -d pods",
-      "python3 -c 'import sys; sys.exit(0 if sys.version_info >= (3, 8) else 1)'",
+      "python3 -S -E -c 'import sys; sys.exit(0 if sys.version_info >= (3, 8) else 1)'",
     ]
   }
 

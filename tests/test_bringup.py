@@ -52,7 +52,7 @@ def _summary(r):
 
 def _pids(ws):
     out = []
-    for pf in (ws / ".tk8s" / "machines").glob("*/run/*.pid"):
+    for pf in [*(ws / ".tk8s" / "machines").glob("*/run/agent.pid"), *(ws / ".tk8s" / "machines").glob("*/run/controlplane.pid")]:
         try:
             out.append(int(json.loads(pf.read_text())["pid"]))
         except (ValueError, KeyError, OSError):
@@ -98,7 +98,11 @@ def test_setup_ready_and_clean_teardown(ws, n):
     ids = [i["status"]["devices"][0]["id"] for i in items]
     assert len(set(ids)) == n
     pids = _pids(ws)
-    assert len(pids) >= n + 1 and all(_alive(p) for p in pids)
+    assert len(pids) == n + 1 and all(_alive(p) for p in pids)
+    # the early GPU burn-in ran on every worker and the validation pods reused its result
+    for i in range(1, n + 1):
+        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
+        assert burn["ok"] and burn["probed"] == 1
     # teardown: machines gone, every artefact removed -- including the env-id file the
     # reference never cleans (setup.sh:513 removes ./tmp/* instead of ansible/tmp/*)
     r = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=_env(), capture_output=True, text=True, timeout=120)

@@ -122,3 +122,85 @@ def test_rccl_single_gpu(nat):
     r = json.loads(nat.rccl_allreduce([0], 8, 1 << 20, 16, 3, 1, "float32", True))
     assert r["ok"], r
     assert r["nranks"] == 1 and all(x["bad"] == 0 for x in r["results"])
+
+
+@pytest.mark.parametrize("n16", [1, 3, 1023, 4097, 1_000_003])
+def test_slab_kernels_handle_ragged_tails(nat, n16):
+    n = 16 * n16
+    buf = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    nat.hbm_fill(buf.data_ptr(), n, 0x01020304, "plain", _stream())
+    dst = torch.empty_like(buf)
+    nat.stream_copy(dst.data_ptr(), buf.data_ptr(), n, _stream())
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    nat.verify_fill(dst.data_ptr(), n, 0x01020304, bad.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0 and torch.equal(buf, dst)
+    dst[-1] = 0  # the very last word belongs to the last slab's tail loop
+    nat.verify_fill(dst.data_ptr(), n, 0x01020304, bad.data_ptr(), _stream())
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 1
+
+
+def _probe(*args, timeout=120):
+    import subprocess
+
+    from tritonk8ssupervisor_amd.ops import tool
+
+    r = subprocess.run([str(tool("tk8s-probe")), *args], capture_output=True, text=True, timeout=timeout)
+    return r.returncode, json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_probe_cli_all_devices_known_answer(nat):
+    rc, out = _probe("--all-devices", "--gpuinfo", "--peers", "--iters", "2", "--copy-bytes", str(64 << 20),
+                     "--peer-bytes", str(16 << 20))
+    assert rc == 0 and out["ok"], out
+    assert out["probed"] == out["device_count"] >= 1
+    assert out["md5_expected"] == "55af80380d572d36cc8cc7d50edd90ab"  # host oracle, 256 MiB seed 0
+    for d in out["devices"]:
+        assert d["ok"] and d["digest_ok"] and d["hbm"]["bad_words"] == 0
+        assert d["hbm"]["gbps"] > 3000 and d["copy"]["kernel_gbps"] > 1500
+        assert len(d.get("peers", [])) == out["device_count"] - 1
+    assert out["gpuinfo"]["devices"][0]["gfx"] == "gfx950"
+    assert out["timings_ms"]["total"] >= out["timings_ms"]["hip_init"] > 0
+
+
+def test_probe_cli_out_and_reuse(nat, tmp_path):
+    f = tmp_path / "burn.json"
+    (tmp_path / "burn.json.pending").write_text("")
+    rc, out = _probe("--out", str(f), "--hbm-bytes", str(64 << 20), "--md5-bytes", str(1 << 20), "--iters", "1")
+    assert rc == 0 and out["ok"] and f.exists() and not (tmp_path / "burn.json.pending").exists()
+    rc2, again = _probe("--reuse", str(f), "--hbm-bytes", "16")
+    assert rc2 == 0 and again == out  # the pod reports the burn-in's result verbatim
+
+
+def test_setup_on_a_real_gpu(tmp_path):
+    """./setup.sh with one MI355X worker: the real tk8s-probe validates the GPU before Ready."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable)
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120"],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1
+        k = subprocess.run(["./kubectl", "get", "node", "kubenode1", "-o", "json"], cwd=tmp_path, env=env,
+                           capture_output=True, text=True, timeout=60)
+        node = json.loads(k.stdout)
+        assert float(node["metadata"]["annotations"]["tk8s.amd.com/hbm-write-gbps"]) > 3000
+        assert node["status"]["devices"][0]["gfx"] == "gfx950"
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)

@@ -12,3 +12,22 @@ and their start-up time is part of the bring-up metric.
 """
 
 __version__ = "0.1.0"
+
+
+def _fast_site() -> None:
+    """Our daemons and the CLI start with ``python3 -S`` (no ``site`` processing: ~30 ms less
+    per interpreter on the bring-up's critical path, where three start one after another).
+    Append the site-packages directories ourselves -- without executing their ``.pth`` hooks --
+    so third-party packages (PyYAML) stay importable."""
+    import sys
+
+    if not sys.flags.no_site:
+        return
+    import site
+
+    for d in site.getsitepackages() + [site.getusersitepackages()]:
+        if d not in sys.path:
+            sys.path.append(d)
+
+
+_fast_site()

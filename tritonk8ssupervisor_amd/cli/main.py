@@ -214,7 +214,16 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv: list[str] | None = None) -> int:
     args = build_parser().parse_args(argv)
-    return args.fn(args)
+    prof = os.environ.get("TK8S_PROFILE")
+    if not prof:
+        return args.fn(args)
+    import cProfile  # TK8S_PROFILE=<file>: where does a bring-up spend its host time?
+
+    pr = cProfile.Profile()
+    try:
+        return pr.runcall(args.fn, args)
+    finally:
+        pr.dump_stats(prof)
 
 
 if __name__ == "__main__":

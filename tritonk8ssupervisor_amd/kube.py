@@ -8,10 +8,9 @@ from __future__ import annotations
 import time
 from pathlib import Path
 
-import yaml
-
 from . import templating
 from .controlplane.client import ApiError, Client
+from .utils import yamlio
 
 KINDS = {
     "pod": ("Pod", "/api/v1", "pods"),
@@ -46,7 +45,7 @@ def object_path(kind: str, name: str, ns: str = "default") -> str:
 
 
 def load_manifests(path: str | Path, variables: dict | None = None) -> list[dict]:
-    docs = [d for d in yaml.safe_load_all(Path(path).read_text()) if d]
+    docs = [d for d in yamlio.load_all(Path(path).read_text()) if d]
     if variables:
         docs = templating.render(docs, variables)
     out = []

@@ -1,20 +1,68 @@
 """CPU stand-in for tk8s-probe when ``TK8S_FAKE_GPUS`` is set (tests on hosts without a GPU).
 
-Emits the same JSON shape as native/tools/tk8s_probe.cpp so the validation DaemonSet, the
-node condition logic and the device-plugin refresh run unchanged; never used on a GPU host
-(setup picks the real tool whenever TK8S_FAKE_GPUS is unset).
+Emits the same JSON shape as native/tools/tk8s_probe.cpp and honours the same pipelining flags
+(``--out FILE`` for the early burn-in, ``--reuse FILE [--reuse-wait S]`` for the validation
+pod), so the validation DaemonSet, the node condition logic and the device-plugin refresh run
+unchanged; never used on a GPU host (setup picks the real tool whenever TK8S_FAKE_GPUS is unset).
+Test hooks: ``TK8S_FAKE_PROBE_FAIL=<node>`` fails, ``TK8S_FAKE_PROBE_HANG=<node>`` wedges.
 """
 import json
 import os
+import sys
 import time
 
-n = len([x for x in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if x])
-fail = os.environ.get("TK8S_FAKE_PROBE_FAIL", "") == os.environ.get("NODE_NAME", "-")
-if os.environ.get("TK8S_FAKE_PROBE_HANG", "") == os.environ.get("NODE_NAME", "-"):
-    time.sleep(3600)  # a wedged validation pod (the analogue of the reference's stuck dashboard)
-dev = {"ok": not fail, "hbm": {"ok": True, "gbps": 4400.0}, "md5": {"ok": True, "mbps": 2.3e6}}
-out = {"ok": not fail, "fake": True, "device_count": n, "devices": [dev] * n, "hbm": dev["hbm"], "md5": dev["md5"],
-       "gpuinfo": {"ok": True, "device_count": n, "devices": [{"index": i, "gfx": "gfx950", "pci_bus_id": f"0000:{i:02x}:00.0",
-                                                                "uuid": f"fake-{i}"} for i in range(n)]}}
-print(json.dumps(out))
-raise SystemExit(0 if not fail else 1)
+
+def _arg(name, default=None):
+    a = sys.argv[1:]
+    return a[a.index(name) + 1] if name in a and a.index(name) + 1 < len(a) else default
+
+
+def _reuse(path, wait):
+    t = time.monotonic()
+    while not os.path.exists(path) and os.path.exists(path + ".pending") and time.monotonic() - t < wait:
+        time.sleep(0.002)
+    try:
+        with open(path) as f:
+            text = f.read().strip()
+    except OSError:
+        return None
+    if not text.startswith("{"):
+        return None
+    print(text)
+    return 0 if json.loads(text).get("ok") else 1
+
+
+def _emit(out, path):
+    text = json.dumps(out)
+    if path:
+        with open(path + ".tmp", "w") as f:
+            f.write(text + "\n")
+        os.replace(path + ".tmp", path)
+        try:
+            os.remove(path + ".pending")
+        except OSError:
+            pass
+    print(text)
+
+
+def main():
+    if "--reuse" in sys.argv:
+        rc = _reuse(_arg("--reuse"), float(_arg("--reuse-wait", "120")))
+        if rc is not None:
+            return rc
+    node = os.environ.get("NODE_NAME") or os.environ.get("TK8S_MACHINE", "-")
+    if os.environ.get("TK8S_FAKE_PROBE_HANG", "") == node:
+        time.sleep(3600)  # a wedged validation (the analogue of the reference's stuck dashboard)
+    n = len([x for x in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if x])
+    fail = os.environ.get("TK8S_FAKE_PROBE_FAIL", "") == node
+    dev = {"ok": not fail, "hbm": {"ok": True, "gbps": 6200.0}, "md5": {"ok": True, "mbps": 2.3e6}}
+    out = {"ok": not fail, "fake": True, "device_count": n, "probed": n, "devices": [dict(dev, device=i) for i in range(n)],
+           "hbm": dev["hbm"], "md5": dev["md5"],
+           "gpuinfo": {"ok": True, "device_count": n, "devices": [{"index": i, "gfx": "gfx950", "pci_bus_id": f"0000:{i:02x}:00.0",
+                                                                    "uuid": f"fake-{i}"} for i in range(n)]}}
+    _emit(out, _arg("--out"))
+    return 0 if not fail else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -293,7 +293,9 @@ class Setup:
     def _validation_command(self) -> list[str]:
         if os.environ.get("TK8S_FAKE_GPUS"):
             return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
-        return ["tk8s-probe", "--all-devices", "--gpuinfo", "--hbm-bytes", str(self.hbm_bytes),
+        from .ops import BIN
+
+        return [str(BIN / "tk8s-probe"), "--all-devices", "--gpuinfo", "--peers", "--hbm-bytes", str(self.hbm_bytes),
                 "--md5-bytes", str(self.md5_bytes), "--iters", str(self.probe_iters)]
 
     def ansible(self) -> None:

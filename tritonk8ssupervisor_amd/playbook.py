@@ -29,10 +29,9 @@ from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Any, Callable
 
-import yaml
-
 from . import templating
 from .templating import TemplateError, Undefined
+from .utils import yamlio
 from .utils.events import EventLog
 
 MODULE_ALIASES = {"command", "shell", "uri", "slurp", "pause", "debug", "set_fact", "wait_for", "fail",
@@ -212,7 +211,7 @@ class Playbook:
     # ---- run -----------------------------------------------------------------------------
     def run(self) -> PlaybookResult:
         t0 = time.monotonic()
-        plays = yaml.safe_load(self.path.read_text()) or []
+        plays = yamlio.load(self.path.read_text()) or []
         failures: list[str] = []
         for play in plays:
             failures += self.run_play(play)
@@ -229,7 +228,7 @@ class Playbook:
         p = self.dir / "roles" / role / "tasks" / "main.yml"
         if not p.exists():
             raise PlaybookError(f"role {role!r} not found at {p}")
-        tasks = yaml.safe_load(p.read_text()) or []
+        tasks = yamlio.load(p.read_text()) or []
         for t in tasks:
             t.setdefault("_role", role)
         return tasks
@@ -246,7 +245,7 @@ class Playbook:
                 f = templating.render(vf, {"playbook_dir": str(self.dir), **self.extra_vars})
                 fp = Path(f) if Path(f).is_absolute() else self.dir / f
                 if fp.exists():
-                    play_vars.update(yaml.safe_load(fp.read_text()) or {})
+                    play_vars.update(yamlio.load(fp.read_text()) or {})
                 elif not self.check:
                     raise PlaybookError(f"vars_files entry {fp} not found")
             tasks: list[dict] = []

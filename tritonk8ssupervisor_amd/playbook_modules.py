@@ -326,8 +326,12 @@ def m_tk8s_gpu_facts(args, *, ctx, target, local, **_):
     inv = discover()
     facts["tk8s_host_gpus"] = inv.count
     facts["tk8s_inventory_source"] = inv.source
+    facts["tk8s_machine_gpus"] = []
     if ctx.executor is not None and not local:
         facts["tk8s_machine_gpus"] = ctx.executor.machine_gpus(target.name)
+    from .models.hostinfo import compose_visible_devices
+
+    facts["tk8s_machine_visible_devices"] = compose_visible_devices(facts["tk8s_machine_gpus"])["HIP_VISIBLE_DEVICES"]
     from .ops import BIN
 
     facts["tk8s_native_built"] = all((BIN / t).exists() for t in ("tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl"))
