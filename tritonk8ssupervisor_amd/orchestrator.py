@@ -422,6 +422,10 @@ class Setup:
             ready = self.wait_ready()
         self.mark("ready")
         t_ready = time.monotonic() - t0
+        # One greppable line the moment every node is Ready (bench.py timestamps it): the RCCL
+        # fabric check that follows is reported on its own, it is not part of "all nodes Ready".
+        self.out(f"ALL NODES READY: {ready.get('nodes_ready', 0)} node(s), "
+                 f"{ready.get('gpus_allocatable', 0)} x amd.com/gpu allocatable after {t_ready:.3f}s")
         rccl = None
         with self.events.phase("rccl"):
             rccl = self.run_rccl()
