@@ -232,3 +232,47 @@ def test_kubectl_workload_on_the_cluster(ws, tmp_path_factory):
     assert len(vis) == 2  # each rank saw exactly its own GPU
     r = kc("describe", "node", "kubenode1")
     assert "amd.com/gpu" in r.stdout
+
+
+def test_manual_flow(ws):
+    """docs/manual-setup.md, command for command: tk8s env/networks/packages, a hand-written
+    rancher.tf, tk8s terraform get/plan/apply, hand-written inventory + vars, tk8s
+    ansible-playbook (--check, then for real), kubectl with the served kubeconfig."""
+    import urllib.request
+
+    env = _env()
+    sh = lambda *a, **kw: subprocess.run(list(a), cwd=ws, env=env, capture_output=True, text=True, timeout=120, **kw)
+    exports = sh("./tk8s", "env").stdout
+    assert "SDC_KEY_ID" in exports
+    pub = next(l.split()[1] for l in sh("./tk8s", "networks").stdout.splitlines() if l.startswith("local-public"))
+    pkg = next(l.split()[1] for l in sh("./tk8s", "packages").stdout.splitlines() if l.startswith("mi355x-1gpu"))
+    key = ws / ".tk8s" / "keys" / "tk8s_cluster_key"
+    mods = "".join(f'\nmodule "{n}" {{\n    source = "{src}"\n    hostname = "{n}"\n    networks = ["{pub}"]\n'
+                   f'    root_authorized_keys = "${{file("{key}.pub")}}"\n    package = "{pkg}"\n}}\n'
+                   for n, src in (("kubemaster", "master"), ("kubenode1", "host")))
+    (ws / "terraform" / "rancher.tf").write_text(
+        f'provider "local" {{\n    account = "root"\n    key_material = "${{file("{key}")}}"\n    key_id = "x"\n'
+        f'    url = "local://h"\n}}\n' + mods)
+    assert sh("./tk8s", "terraform", "get").returncode == 0
+    assert "Plan: 2 to add" in sh("./tk8s", "terraform", "plan").stdout
+    assert sh("./tk8s", "terraform", "apply").returncode == 0
+    m_ip = (ws / "terraform" / "masters.ip").read_text().split()[0]
+    h_ip = (ws / "terraform" / "hosts.ip").read_text().split()[0]
+    (ws / "ansible" / "hosts").write_text(f"[MASTER]\nkubemaster ansible_host={m_ip}\n[HOST]\nkubenode1 ansible_host={h_ip}\n")
+    (ws / "ansible" / "roles" / "ranchermaster" / "vars" / "vars.yml").write_text(
+        f"master: {m_ip}\nkubernetes_name: manual\nkubernetes_description: manual\n")
+    port = __import__("tritonk8ssupervisor_amd.orchestrator", fromlist=["_free_port"])._free_port()
+    (ws / "config").write_text(f'RANCHER_MASTER_HOSTNAME="kubemaster"\nTK8S_MASTER_PORT={port}\n')
+    r = sh("./tk8s", "ansible-playbook", "--check", "-i", "hosts", "clusterUp.yml")
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert not (ws / "ansible" / "tmp" / "kubernetes_environment.id").exists()
+    r = sh("./tk8s", "ansible-playbook", "-i", "hosts", "clusterUp.yml")
+    assert r.returncode == 0, r.stdout[-2000:]
+    env_id = (ws / "ansible" / "tmp" / "kubernetes_environment.id").read_text().strip()
+    base = f"http://{m_ip}:{port}"
+    w = json.loads(urllib.request.urlopen(f"{base}/v1/cluster/wait?project={env_id}&nodes=1&gpus=1&timeout=30",
+                                          timeout=40).read())
+    assert w["ready"], w
+    (ws / "kc.json").write_bytes(urllib.request.urlopen(f"{base}/env/{env_id}/kubernetes/kubectl?format=json").read())
+    out = sh("./kubectl", "--kubeconfig", "kc.json", "get", "nodes").stdout
+    assert "kubenode1" in out and "Ready" in out

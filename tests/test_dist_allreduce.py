@@ -17,7 +17,7 @@ def test_gloo_allreduce_ranks_agree_exactly(tmp_path, nranks, dtype):
     p, c = _start(tmp_path)
     try:
         url = f"{c.base}/v1/kv/job-{nranks}/uid"
-        procs = [subprocess.Popen([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.gloo_allreduce", "--rank", str(r),
+        procs = [subprocess.Popen([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", str(r),
                                    "--nranks", str(nranks), "--kv-url", url, "--max-bytes", str(256 << 10), "--dtype", dtype],
                                   cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
                  for r in range(nranks)]
@@ -36,7 +36,7 @@ def test_gloo_allreduce_ranks_agree_exactly(tmp_path, nranks, dtype):
 def test_missing_peer_times_out_with_a_json_error(tmp_path):
     p, c = _start(tmp_path)
     try:
-        r = subprocess.run([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.gloo_allreduce", "--rank", "1",
+        r = subprocess.run([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", "1",
                             "--nranks", "2", "--kv-url", f"{c.base}/v1/kv/none/uid", "--timeout", "1"],
                            cwd=REPO, capture_output=True, text=True, timeout=60)
     finally:

@@ -204,3 +204,25 @@ def test_setup_on_a_real_gpu(tmp_path):
         assert node["status"]["devices"][0]["gfx"] == "gfx950"
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+def test_torch_rccl_allreduce_single_rank(tmp_path):
+    """The PyTorch (RCCL) twin of tk8s-rccl, rendezvous through a real control-plane KV."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from test_controlplane import _start, _stop
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    p, c = _start(tmp_path)
+    try:
+        r = subprocess.run([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--backend", "nccl",
+                            "--rank", "0", "--nranks", "1", "--kv-url", f"{c.base}/v1/kv/t/addr", "--max-bytes", str(16 << 20)],
+                           cwd=Path(__file__).resolve().parents[1], capture_output=True, text=True, timeout=180)
+    finally:
+        _stop(p)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and out["ok"] and out["backend"] == "nccl", r.stderr[-2000:]
+    assert all(x["bad"] == 0 for x in out["results"])

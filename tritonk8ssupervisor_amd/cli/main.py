@@ -148,7 +148,16 @@ def cmd_playbook(args) -> int:
     inv = Path(args.inventory) if args.inventory else ws.ansible / "hosts"
     if not inv.is_absolute() and not inv.exists():
         inv = ws.ansible / inv
-    extra = dict(kv.split("=", 1) for kv in args.extra_vars) if args.extra_vars else {}
+    extra = {}
+    if machines and ws.config.exists():
+        from ..config import read_config
+        from ..orchestrator import playbook_extra_vars
+
+        cfg = read_config(ws.config)
+        if cfg.RANCHER_MASTER_HOSTNAME in machines:
+            extra = playbook_extra_vars(ws, cfg, machines)
+    if args.extra_vars:
+        extra.update(dict(kv.split("=", 1) for kv in args.extra_vars))
     res = Playbook(pb, inv, executor=MachineExecutor(prov, machines) if machines else None, extra_vars=extra,
                    check=args.check).run()
     return 0 if res.ok else 2

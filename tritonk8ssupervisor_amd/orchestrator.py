@@ -170,6 +170,35 @@ class MachineExecutor:
         return kill_pidfile(pidfile)
 
 
+def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 << 20, iters: int = 3) -> list[str]:
+    """The validation DaemonSet payload (and the early burn-in): every GPU of a worker."""
+    if os.environ.get("TK8S_FAKE_GPUS"):
+        return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
+    from .ops import BIN
+
+    return [str(BIN / "tk8s-probe"), "--all-devices", "--gpuinfo", "--peers", "--hbm-bytes", str(hbm_bytes),
+            "--md5-bytes", str(md5_bytes), "--iters", str(iters)]
+
+
+def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, Machine], *, node_grace: float = 5.0,
+                        validate: bool = True, validation_command: list[str] | None = None) -> dict:
+    """Variables the roles need beyond inventory + vars.yml (shared by setup and
+    `./tk8s ansible-playbook`, so a by-hand run of clusterUp.yml behaves like setup's)."""
+    m = machines[cfg.RANCHER_MASTER_HOSTNAME]
+    return {
+        "tk8s_python": sys.executable,
+        "tk8s_pythonpath": os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]),
+        "tk8s_master_port": int(cfg.TK8S_MASTER_PORT),
+        "tk8s_bind_host": m.primaryip,
+        "tk8s_cp_state_dir": str(Path(m.sandbox) / "controlplane"),
+        "tk8s_node_grace": node_grace,
+        "tk8s_manifests": str(ws.manifests),
+        "tk8s_validation_command": validation_command or default_validation_command(),
+        "tk8s_validate": validate,
+        "tk8s_fake_gpus": os.environ.get("TK8S_FAKE_GPUS", ""),
+    }
+
+
 # ---- setup ---------------------------------------------------------------------------------
 class Setup:
     def __init__(self, ws: Workspace, *, answers: dict | None = None, assume_yes: bool = False,
@@ -291,31 +320,15 @@ class Setup:
         self.out("    created: ansible/roles/ranchermaster/vars/vars.yml")
 
     def _validation_command(self) -> list[str]:
-        if os.environ.get("TK8S_FAKE_GPUS"):
-            return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
-        from .ops import BIN
-
-        return [str(BIN / "tk8s-probe"), "--all-devices", "--gpuinfo", "--peers", "--hbm-bytes", str(self.hbm_bytes),
-                "--md5-bytes", str(self.md5_bytes), "--iters", str(self.probe_iters)]
+        return default_validation_command(self.hbm_bytes, self.md5_bytes, self.probe_iters)
 
     def ansible(self) -> None:
         from .playbook import Playbook
 
         ws, cfg = self.ws, self.cfg
         machines = self.engine.machines()
-        m = machines[cfg.RANCHER_MASTER_HOSTNAME]
-        extra = {
-            "tk8s_python": sys.executable,
-            "tk8s_pythonpath": os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]),
-            "tk8s_master_port": int(cfg.TK8S_MASTER_PORT),
-            "tk8s_bind_host": m.primaryip,
-            "tk8s_cp_state_dir": str(Path(m.sandbox) / "controlplane"),
-            "tk8s_node_grace": self.node_grace,
-            "tk8s_manifests": str(ws.manifests),
-            "tk8s_validation_command": self._validation_command(),
-            "tk8s_validate": self.validate,
-            "tk8s_fake_gpus": os.environ.get("TK8S_FAKE_GPUS", ""),
-        }
+        extra = playbook_extra_vars(ws, cfg, machines, node_grace=self.node_grace, validate=self.validate,
+                                    validation_command=self._validation_command())
         lines: list[str] = []
         pb = Playbook(ws.ansible / "clusterUp.yml", ws.ansible / "hosts", executor=MachineExecutor(self.provider, machines),
                       extra_vars=extra, events=self.events, out=(lines.append if self.quiet_ansible else self.out))
@@ -375,7 +388,7 @@ class Setup:
         k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
         job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
         if os.environ.get("TK8S_FAKE_GPUS"):
-            cmd = [sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.gloo_allreduce", "--rank", "$(JOB_COMPLETION_INDEX)",
+            cmd = [sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", "$(JOB_COMPLETION_INDEX)",
                    "--nranks", str(g), "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
         else:
             cmd = ["tk8s-rccl", "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "0",

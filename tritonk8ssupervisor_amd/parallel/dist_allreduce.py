@@ -1,8 +1,10 @@
-"""CPU twin of ``tk8s-rccl`` (N3): one process per rank, torch.distributed **gloo** all-reduce.
+"""torch.distributed all-reduce validator, one process per rank: the PyTorch twin of ``tk8s-rccl`` (N3).
 
-Used for the cluster fabric check when the GPUs are faked (``TK8S_FAKE_GPUS``, CPU-only
-hosts and tests). It follows the real job's protocol step by step so the control-plane path is
-exercised unchanged: rank 0 publishes its rendezvous address to the control-plane KV store
+``--backend gloo`` (CPU tensors) is the cluster fabric check when the GPUs are faked
+(``TK8S_FAKE_GPUS``, CPU-only hosts and tests); ``--backend nccl`` (= RCCL on ROCm, tensors on
+the pod's one visible MI355X) is what a PyTorch user's job sees on the real cluster
+(manifests/examples/torch-allreduce-job.yaml). It follows the native job's protocol step by
+step so the control-plane path is exercised unchanged: rank 0 publishes its rendezvous address to the control-plane KV store
 (HTTP PUT), the other ranks long-poll it (GET ``?wait=``), then every rank runs an
 RCCL-tests-style sweep with an exact result check and prints ONE JSON line with the same keys
 as native/tools/tk8s_rccl.cpp (``ok``, ``nranks``, ``rank``, ``peak_busbw_gbps``, ``results``).
@@ -45,19 +47,20 @@ def _free_port(host: str) -> int:
 
 
 def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters: int, warmup: int,
-          dtype: str = "float32") -> dict:
+          dtype: str = "float32", device: str = "cpu") -> dict:
     import torch
     import torch.distributed as dist
 
+    sync = torch.cuda.synchronize if device != "cpu" else (lambda: None)
     dt = {"float32": torch.float32, "bfloat16": torch.bfloat16}[dtype]
     esize = torch.tensor([], dtype=dt).element_size()
     results, ok, peak = [], True, 0.0
     size = max(min_bytes, esize)
     while size <= max_bytes:
         count = max(1, size // esize)
-        pat = (torch.arange(count, dtype=torch.int64) % (251 if dt == torch.float32 else 4) + 1)
+        pat = (torch.arange(count, dtype=torch.int64, device=device) % (251 if dt == torch.float32 else 4) + 1)
         want = (pat * (n * (n + 1) // 2)).to(dt)
-        buf = torch.empty(count, dtype=dt)
+        buf = torch.empty(count, dtype=dt, device=device)
         for _ in range(warmup):
             buf.copy_(pat * (rank + 1))
             dist.all_reduce(buf)
@@ -65,9 +68,11 @@ def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters:
         bad = 0
         for _ in range(max(1, iters)):
             buf.copy_(pat * (rank + 1))
+            sync()
             dist.barrier()
             t = time.perf_counter()
             dist.all_reduce(buf)
+            sync()
             times.append(time.perf_counter() - t)
             bad = max(bad, int((buf != want).sum()))
         sec = sorted(times)[len(times) // 2]
@@ -93,6 +98,7 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--dtype", choices=["float32", "bfloat16"], default="float32")
     ap.add_argument("--timeout", type=float, default=60.0)
+    ap.add_argument("--backend", choices=["gloo", "nccl"], default="gloo", help="nccl = RCCL on ROCm (GPU tensors)")
     a = ap.parse_args(argv)
     t0 = time.monotonic()
     host = os.environ.get("NODE_IP", "127.0.0.1")
@@ -105,16 +111,22 @@ def main(argv=None) -> int:
         import torch.distributed as dist
         from datetime import timedelta
 
-        dist.init_process_group("gloo", init_method=f"tcp://{addr}", rank=a.rank, world_size=a.nranks,
+        device = "cpu"
+        if a.backend == "nccl":
+            import torch
+
+            torch.cuda.set_device(0)  # the device plugin exposes exactly this pod's GPU(s)
+            device = "cuda:0"
+        dist.init_process_group(a.backend, init_method=f"tcp://{addr}", rank=a.rank, world_size=a.nranks,
                                 timeout=timedelta(seconds=a.timeout))
         init_s = time.monotonic() - t0
-        res = sweep(a.rank, a.nranks, a.min_bytes, a.max_bytes, a.factor, a.iters, a.warmup, a.dtype)
+        res = sweep(a.rank, a.nranks, a.min_bytes, a.max_bytes, a.factor, a.iters, a.warmup, a.dtype, device)
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001 - reported as the pod result
         print(json.dumps({"ok": False, "rank": a.rank, "nranks": a.nranks, "error": f"{type(e).__name__}: {e}"}))
         return 2
-    out = {"ok": res["ok"], "backend": "gloo", "mode": "multi_process", "nranks": a.nranks, "rank": a.rank,
+    out = {"ok": res["ok"], "backend": a.backend, "mode": "multi_process", "nranks": a.nranks, "rank": a.rank,
            "dtype": a.dtype, "init_seconds": round(init_s, 4), "peak_busbw_gbps": res["peak_busbw_gbps"],
            "results": res["results"]}
     print(json.dumps(out))

@@ -60,6 +60,30 @@ def read_pidfile(pidfile: str | os.PathLike) -> dict | None:
         return None
 
 
+def group_alive(pgid: int) -> bool:
+    """True while the process group has a member that is not a zombie. A daemon reparented to
+    an init that reaps lazily lingers as a zombie, which `killpg(pgid, 0)` still counts."""
+    try:
+        os.killpg(pgid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        pids = [d for d in os.listdir("/proc") if d.isdigit()]
+    except OSError:
+        return True
+    for d in pids:
+        try:
+            with open(f"/proc/{d}/stat", "rb") as f:
+                rest = f.read().rsplit(b")", 1)[1].split()
+        except (OSError, IndexError):
+            continue
+        if len(rest) > 2 and int(rest[2]) == pgid and rest[0] != b"Z":
+            return True
+    return False
+
+
 def kill_group(pgid: int, grace: float = 3.0) -> bool:
     """SIGTERM the process group, wait up to `grace` s, then SIGKILL. True if it was alive."""
     try:
@@ -69,14 +93,14 @@ def kill_group(pgid: int, grace: float = 3.0) -> bool:
     except PermissionError:
         return False
     deadline = time.monotonic() + grace
+    delay = 0.001
     while time.monotonic() < deadline:
-        try:
-            os.killpg(pgid, 0)
-        except ProcessLookupError:
-            return True
         with contextlib.suppress(ChildProcessError, OSError):
             os.waitpid(-pgid, os.WNOHANG)
-        time.sleep(0.02)
+        if not group_alive(pgid):
+            return True
+        time.sleep(delay)
+        delay = min(delay * 2, 0.02)
     with contextlib.suppress(ProcessLookupError, PermissionError):
         os.killpg(pgid, signal.SIGKILL)
     return True
