@@ -200,6 +200,8 @@ def test_provision_failure_then_resume(ws):
 
 def test_status_and_events_log(ws):
     _summary(_setup(ws, "--nodes", "2", "--rccl", "off"))
+    dv = subprocess.run(["./tk8s", "debug-vars"], cwd=ws, env=_env(), capture_output=True, text=True).stdout
+    assert "KUBERNETES_NUMBER_OF_NODES=2" in dv and dv.splitlines()[0].startswith("KUBERNETES_NAME=")
     r = subprocess.run(["./tk8s", "status", "--json"], cwd=ws, env=_env(), capture_output=True, text=True)
     st = json.loads(r.stdout)
     assert st["cluster"]["nodes_ready"] == 2 and st["cluster"]["gpus_allocatable"] == 2

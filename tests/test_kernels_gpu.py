@@ -226,3 +226,42 @@ def test_torch_rccl_allreduce_single_rank(tmp_path):
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert r.returncode == 0 and out["ok"] and out["backend"] == "nccl", r.stderr[-2000:]
     assert all(x["bad"] == 0 for x in out["results"])
+
+
+def test_setup_rccl_job_under_rocprof(tmp_path):
+    """BASELINE.json config 5 on one GPU: the RCCL Job's rank runs under rocprofv3
+    --kernel-trace --stats and the per-kernel summary lands in the setup summary."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, TMPDIR="/tmp")
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "240",
+                            "--rccl", "on", "--rocprof", "--rccl-max-bytes", str(16 << 20)],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=400)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["rccl"]["ok"] and s["rccl"]["nranks"] == 1
+        prof = s["rccl"]["rocprof"]
+        assert prof["ranks"], prof
+        kernels = [k["kernel"] for ks in prof["ranks"].values() for k in ks]
+        assert kernels and all(k["calls"] > 0 for ks in prof["ranks"].values() for k in ks)
+        out = Path(os.environ.get("GRAFT_REPO_ROOT", repo)) / "gpurun_out" / "rccl_rocprof"
+        out.mkdir(parents=True, exist_ok=True)
+        (out / "summary.json").write_text(json.dumps(s["rccl"], indent=1))
+        for f in Path(prof["dir"]).rglob("*_kernel_stats.csv"):
+            shutil.copy2(f, out / f.name)
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)

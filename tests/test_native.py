@@ -102,3 +102,16 @@ def test_supervise_sigterm_stops_child_and_group(native_build, tmp_path):
 def test_supervise_usage_errors(native_build):
     r = subprocess.run([str(BIN / "tk8s-supervise"), "--restart", "sometimes", "--", "true"], capture_output=True)
     assert r.returncode == 2 and b"usage" in r.stderr
+
+
+def test_summarize_rocprof_stats(tmp_path):
+    from tritonk8ssupervisor_amd.orchestrator import summarize_rocprof
+
+    d = tmp_path / "prof" / "host"
+    d.mkdir(parents=True)
+    (d / "rank0_kernel_stats.csv").write_text(
+        '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+        '"small",2,100,50,1,40,60,1\n"ncclDevKernel_Generic",10,90000,9000,99,8000,10000,5\n')
+    s = summarize_rocprof(tmp_path / "prof")
+    assert list(s["ranks"]) == ["rank0"]
+    assert s["ranks"]["rank0"][0] == {"kernel": "ncclDevKernel_Generic", "calls": 10, "total_us": 90.0, "avg_us": 9.0}

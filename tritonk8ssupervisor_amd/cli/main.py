@@ -4,6 +4,7 @@
   ./setup.sh -c [--yes]                                               -> tk8s clean
   ./tk8s networks|packages [-l]     (triton networks / triton packages)
   ./tk8s env                        (triton env)
+  ./tk8s debug-vars                 (debugVars: the exported ./config)
   ./tk8s terraform get|plan|apply|destroy     (provisioning engine, in terraform/)
   ./tk8s ansible-playbook [--check] [-i hosts] clusterUp.yml           (playbook engine)
   ./tk8s status [--json]            (phases, nodes, GPUs, last RCCL busbw)
@@ -40,7 +41,7 @@ def cmd_setup(args) -> int:
               validate=not args.no_validate, rccl=(None if args.rccl is None else args.rccl == "on"),
               quiet_ansible=not args.verbose, backend=args.backend, master_port=args.port,
               hbm_bytes=args.hbm_bytes, md5_bytes=args.md5_bytes, probe_iters=args.probe_iters,
-              node_grace=args.node_grace)
+              node_grace=args.node_grace, rocprof=args.rocprof, rccl_max_bytes=args.rccl_max_bytes)
     try:
         summary = s.run()
     except WizardAbort:
@@ -83,6 +84,22 @@ def cmd_status(args) -> int:
                   f"amd.com/gpu allocatable {c['gpus_allocatable']} (in use {c['gpus_in_use']})")
         if summ.get("rccl"):
             print(f"last RCCL all-reduce: peak busbw {summ['rccl']['peak_busbw_gbps']:.1f} GB/s over {summ['rccl']['nranks']} GPU(s)")
+    return 0
+
+
+def cmd_debug_vars(args) -> int:
+    """debugVars (setup.sh:522-531, never called there): the exported configuration."""
+    from ..config import read_config
+
+    ws = _ws(args)
+    if not ws.config.exists():
+        print("no ./config yet (run ./setup.sh first)", file=sys.stderr)
+        return 1
+    env = read_config(ws.config).as_env()
+    for k in ("KUBERNETES_NAME", "KUBERNETES_DESCRIPTION", "RANCHER_MASTER_HOSTNAME",
+              "KUBERNETES_NODE_HOSTNAME_BEGINSWITH", "KUBERNETES_NUMBER_OF_NODES", "RANCHER_MASTER_NETWORKS",
+              "KUBERNETES_NODE_NETWORKS", "HOST_PACKAGE"):
+        print(f"{k}={env.get(k, '')}")
     return 0
 
 
@@ -186,6 +203,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--md5-bytes", type=int, default=256 << 20)
     s.add_argument("--probe-iters", type=int, default=3)
     s.add_argument("--node-grace", type=float, default=5.0)
+    s.add_argument("--rocprof", action="store_true",
+                   help="run the RCCL Job's ranks under rocprofv3 --kernel-trace --stats (.tk8s/profiles/)")
+    s.add_argument("--rccl-max-bytes", type=int, default=64 << 20)
     s.add_argument("--json", action="store_true")
     s.add_argument("-v", "--verbose", action="store_true")
     s.set_defaults(fn=cmd_setup)
@@ -203,6 +223,7 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("-l", action="store_true")
         p.set_defaults(fn=fn)
     sub.add_parser("env").set_defaults(fn=cmd_env)
+    sub.add_parser("debug-vars", help="print the exported configuration (debugVars)").set_defaults(fn=cmd_debug_vars)
 
     t = sub.add_parser("terraform")
     t.add_argument("action", choices=["get", "plan", "apply", "destroy"])

@@ -205,7 +205,8 @@ class Setup:
                  resume: bool = False, timeout: float = 600.0, validate: bool = True, rccl: bool | None = None,
                  out: Callable[[str], None] = None, quiet_ansible: bool = True, hbm_bytes: int = 1 << 30,
                  md5_bytes: int = 256 << 20, probe_iters: int = 3, rccl_max_bytes: int = 64 << 20,
-                 node_grace: float = 5.0, backend: str | None = None, master_port: int | None = None):
+                 node_grace: float = 5.0, backend: str | None = None, master_port: int | None = None,
+                 rocprof: bool = False):
         self.ws = ws
         self.answers = answers
         self.assume_yes = assume_yes
@@ -220,6 +221,7 @@ class Setup:
         self.node_grace = node_grace
         self.backend = backend or os.environ.get("TK8S_BACKEND", "local")
         self.master_port = master_port
+        self.rocprof = rocprof
         ws.state_dir.mkdir(parents=True, exist_ok=True)
         self.events = EventLog(ws.events, echo=False)
         self.provider = get_provider(self.backend, ws.state_dir)
@@ -391,9 +393,23 @@ class Setup:
             cmd = [sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", "$(JOB_COMPLETION_INDEX)",
                    "--nranks", str(g), "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
         else:
-            cmd = ["tk8s-rccl", "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "0",
+            from .ops import BIN
+
+            cmd = [str(BIN / "tk8s-rccl"), "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "0",
                    "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
                    "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
+        prof_dir = None
+        if self.rocprof:
+            rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+            if os.environ.get("TK8S_FAKE_GPUS") or not os.path.exists(rp):
+                self.out("    --rocprof: rocprofv3 unavailable here (or GPUs are faked); profiling skipped")
+            else:
+                # N8 (BASELINE.json config 5): kernel trace + per-kernel stats of every rank. Counter
+                # collection (--pmc) is a separate run by design: never mixed with tracing.
+                prof_dir = self.ws.state_dir / "profiles" / job
+                prof_dir.mkdir(parents=True, exist_ok=True)
+                cmd = [rp, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
+                       "--output-format", "csv", "--", *cmd]
         objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
                               {"job_name": job, "nranks": g, "rccl_command": cmd})
         apply_objects(k, objs)
@@ -407,6 +423,8 @@ class Setup:
         rep = {"job": job, "ok": ok, "nranks": g, "peak_busbw_gbps": peak,
                "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),
                                  "ok": (p.get("status", {}).get("result") or {}).get("ok")} for p in pods]}
+        if prof_dir is not None:
+            rep["rocprof"] = summarize_rocprof(prof_dir)
         if not ok:
             raise SetupError(f"RCCL all-reduce validation failed: {json.dumps(rep)[:800]}", code=2)
         return rep
@@ -475,6 +493,22 @@ class Setup:
 
         kc = Client(base).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
         atomic_write_json(self.ws.state_dir / "kubeconfig.json", kc)
+
+
+def summarize_rocprof(prof_dir: Path, top: int = 5) -> dict:
+    """Top kernels per rank from rocprofv3 `*_kernel_stats.csv` files under prof_dir."""
+    import csv
+
+    out = {"dir": str(prof_dir), "ranks": {}}
+    for f in sorted(prof_dir.rglob("*kernel_stats.csv")):
+        with open(f, newline="") as fh:
+            rows = list(csv.DictReader(fh))
+        rows.sort(key=lambda r: -float(r.get("TotalDurationNs", 0) or 0))
+        out["ranks"][f.name.split("_kernel_stats")[0]] = [
+            {"kernel": r.get("Name", "")[:120], "calls": int(r.get("Calls", 0) or 0),
+             "total_us": round(float(r.get("TotalDurationNs", 0) or 0) / 1e3, 2),
+             "avg_us": round(float(r.get("AverageNs", 0) or 0) / 1e3, 3)} for r in rows[:top]]
+    return out
 
 
 def _free_port() -> int:
