@@ -1,0 +1,223 @@
+"""Unit tests: pod runtime (restart policies, $(VAR) expansion, results), cluster keys, fs/event
+helpers, fault parsing, and the Joyent `triton` provider driven by a fake `triton` CLI."""
+import json
+import os
+import subprocess
+import sys
+import threading
+import time
+from pathlib import Path
+
+import pytest
+
+from tritonk8ssupervisor_amd.agent.runtime import PodProc, PodRuntime, expand, last_json_line
+from tritonk8ssupervisor_amd.provider import keys
+from tritonk8ssupervisor_amd.utils import faults
+from tritonk8ssupervisor_amd.utils.events import EventLog, read_events
+from tritonk8ssupervisor_amd.utils.fsutil import atomic_write, atomic_write_json, file_lock, locked_append_line, read_json
+
+
+# ---- pod runtime ---------------------------------------------------------------------------
+def test_expand_kubernetes_style():
+    env = {"A": "1", "JOB_COMPLETION_INDEX": "3"}
+    assert expand("rank=$(JOB_COMPLETION_INDEX)", env) == "rank=3"
+    assert expand("$(A)$(A)-$(MISSING)", env) == "11-$(MISSING)"
+    assert expand("$$(A)", env) == "$(A)"
+
+
+def test_last_json_line():
+    assert last_json_line('noise\n{"ok": true}\nmore noise\n') == {"ok": True}
+    assert last_json_line('{"a": 1}\n{"b": 2}\n') == {"b": 2}
+    assert last_json_line("{broken\n") is None
+
+
+def _runtime(tmp_path):
+    events = []
+    cond = threading.Condition()
+
+    def on_status(pp, phase, extra):
+        with cond:
+            events.append((pp.key, phase, extra))
+            cond.notify_all()
+
+    def wait_for(pred, timeout=10):
+        with cond:
+            assert cond.wait_for(lambda: pred(events), timeout), events
+
+    return PodRuntime(tmp_path / "pods", on_status), events, wait_for
+
+
+def _pod(tmp_path, name, argv, policy):
+    return PodProc(key=f"default/{name}", uid=name, dir=tmp_path / "pods" / name, argv=argv,
+                   env=dict(os.environ), restart_policy=policy)
+
+
+def test_pod_succeeds_with_result(tmp_path):
+    rt, events, wait_for = _runtime(tmp_path)
+    rt.start(_pod(tmp_path, "ok", [sys.executable, "-c", "print('hi'); print('{\"ok\": true, \"v\": 7}')"], "Never"))
+    wait_for(lambda ev: any(p == "Succeeded" for _, p, _ in ev))
+    final = [e for e in events if e[1] == "Succeeded"][0][2]
+    assert final["exitCode"] == 0 and final["result"] == {"ok": True, "v": 7}
+    assert (tmp_path / "pods" / "ok" / "log").read_text().startswith("hi")
+
+
+def test_pod_onfailure_restarts_until_success(tmp_path):
+    rt, events, wait_for = _runtime(tmp_path)
+    cnt = tmp_path / "n"
+    code = f"import pathlib,sys; p=pathlib.Path({str(cnt)!r}); n=int(p.read_text()) if p.exists() else 0; p.write_text(str(n+1)); sys.exit(0 if n>=2 else 1)"
+    rt.start(_pod(tmp_path, "flaky", [sys.executable, "-c", code], "OnFailure"))
+    wait_for(lambda ev: any(p == "Succeeded" for _, p, _ in ev))
+    assert cnt.read_text() == "3"
+    assert any(e[2].get("restarts") == 2 for e in events)
+
+
+def test_pod_never_reports_failure_with_log_tail(tmp_path):
+    rt, events, wait_for = _runtime(tmp_path)
+    rt.start(_pod(tmp_path, "bad", ["sh", "-c", "echo boom >&2; exit 5"], "Never"))
+    wait_for(lambda ev: any(p == "Failed" for _, p, _ in ev))
+    extra = [e for e in events if e[1] == "Failed"][0][2]
+    assert extra["exitCode"] == 5 and "boom" in extra["message"]
+
+
+def test_pod_start_error_and_stop(tmp_path):
+    rt, events, wait_for = _runtime(tmp_path)
+    rt.start(_pod(tmp_path, "nope", ["/nonexistent/binary"], "Never"))
+    wait_for(lambda ev: any(p == "Failed" and x.get("reason") == "StartError" for _, p, x in ev))
+    pp = _pod(tmp_path, "sleeper", ["sleep", "600"], "Always")
+    rt.start(pp)
+    wait_for(lambda ev: any(k == "default/sleeper" and p == "Running" for k, p, _ in ev))
+    t = time.monotonic()
+    assert rt.stop("default/sleeper", grace=2.0) is pp
+    assert pp.done.wait(5) and time.monotonic() - t < 5
+    assert "default/sleeper" not in rt.running()
+
+
+# ---- keys / fs / events / faults ----------------------------------------------------------------
+def test_cluster_key_and_fingerprint_scan(tmp_path):
+    priv, pub, fp = keys.ensure_cluster_key(tmp_path / "k")
+    assert oct(priv.stat().st_mode & 0o777) == "0o600" and len(fp.split(":")) == 16
+    assert keys.ensure_cluster_key(tmp_path / "k")[2] == fp  # stable
+    assert keys.find_key(fp, [tmp_path / "nowhere", tmp_path / "k"]) == str(priv)
+    assert keys.find_key("MD5:" + fp.upper(), [tmp_path / "k"]) == str(priv)
+    assert keys.find_key("00:11", [tmp_path / "k"]) is None
+    assert pub.read_text() != priv.read_text()  # machines get the public half, never the private key
+
+
+def test_atomic_write_and_locked_append(tmp_path):
+    atomic_write(tmp_path / "a" / "f", "x", mode=0o640)
+    assert (tmp_path / "a" / "f").read_text() == "x" and oct((tmp_path / "a" / "f").stat().st_mode & 0o777) == "0o640"
+    atomic_write_json(tmp_path / "j.json", {"k": [1, 2]})
+    assert read_json(tmp_path / "j.json") == {"k": [1, 2]}
+    assert read_json(tmp_path / "missing.json", 5) == 5
+    (tmp_path / "bad.json").write_text("{")
+    with pytest.raises(ValueError):  # corrupt state is loud, never silently "empty"
+        read_json(tmp_path / "bad.json", "d")
+
+    def writer(i):
+        for j in range(50):
+            locked_append_line(tmp_path / "ips", f"{i}-{j}")
+
+    ts = [threading.Thread(target=writer, args=(i,)) for i in range(4)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    lines = (tmp_path / "ips").read_text().splitlines()
+    assert len(lines) == 200 and len(set(lines)) == 200  # no torn / interleaved lines
+    with file_lock(tmp_path / "l"):
+        pass
+
+
+def test_event_log_phases(tmp_path):
+    ev = EventLog(tmp_path / "e.jsonl")
+    with ev.phase("provision", n=2):
+        ev.emit("machine_created", name="kubenode1")
+    with pytest.raises(RuntimeError):
+        with ev.phase("ansible"):
+            raise RuntimeError("x")
+    recs = read_events(tmp_path / "e.jsonl")
+    assert [r["event"] for r in recs] == ["phase_start", "machine_created", "phase_end", "phase_start", "phase_end"]
+    assert recs[2]["ok"] is True and recs[4]["ok"] is False
+    assert set(ev.phases) == {"provision", "ansible"}
+
+
+def test_fault_spec_parsing(monkeypatch):
+    monkeypatch.setenv("TK8S_FAULTS", "provision.create@kubenode2,agent.crash@kubenode1:3,cp.delay:0.5")
+    assert faults.fault("provision.create", "kubenode2") is True
+    assert faults.fault("provision.create", "kubenode1") is None
+    assert faults.fault("agent.crash", "kubenode1") == "3"
+    assert faults.fault("cp.delay") == "0.5"
+    with pytest.raises(faults.InjectedFault):
+        faults.maybe_fail("provision.create", "kubenode2")
+    monkeypatch.delenv("TK8S_FAULTS")
+    assert faults.fault("provision.create", "kubenode2") is None
+
+
+# ---- triton provider against a fake CLI ------------------------------------------------------------
+FAKE_TRITON = r'''#!/usr/bin/env python3
+import json, os, sys
+a = sys.argv[1:]
+with open(os.environ["FAKE_TRITON_LOG"], "a") as f:
+    f.write(" ".join(a) + "\n")
+if a[0] == "env":
+    print('export SDC_URL="https://us-east-1.api.joyent.com"')
+    print('export SDC_ACCOUNT="me"')
+    print('export SDC_KEY_ID="%s"' % os.environ["FAKE_KEY_ID"])
+elif a[0] == "networks":
+    print("NAME                ID")
+    print("Joyent-SDC-Public   1111-aaaa")
+    print("Joyent-SDC-Private  2222-bbbb")
+elif a[0] == "packages":
+    print("NAME                  ID")
+    print("k4-highcpu-kvm-7.75G  3333")
+    print("g4-highcpu-1G         4444")
+    print("k4-highcpu-kvm-1.75G  5555")
+elif a[:2] == ["instance", "create"]:
+    name = [x for x in a if x.startswith("--name=")][0].split("=", 1)[1]
+    print(json.dumps({"id": "id-" + name, "name": name, "primaryIp": "10.0.0.9", "ips": ["10.0.0.9"]}))
+elif a[:2] == ["instance", "delete"]:
+    pass
+else:
+    sys.exit(2)
+'''
+
+
+def test_triton_provider_with_fake_cli(tmp_path, monkeypatch):
+    from tritonk8ssupervisor_amd.provider.triton import TritonProvider
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    (bindir / "triton").write_text(FAKE_TRITON)
+    (bindir / "triton").chmod(0o755)
+    home = tmp_path / "home"
+    (home / ".ssh").mkdir(parents=True)
+    subprocess.run(["ssh-keygen", "-q", "-t", "ed25519", "-N", "", "-f", str(home / ".ssh" / "id_ed25519")], check=True)
+    md5 = subprocess.run(["ssh-keygen", "-E", "md5", "-lf", str(home / ".ssh" / "id_ed25519")], capture_output=True,
+                         text=True, check=True).stdout.split()[1].removeprefix("MD5:")
+    monkeypatch.setenv("PATH", f"{bindir}{os.pathsep}{os.environ['PATH']}")
+    monkeypatch.setenv("HOME", str(home))
+    monkeypatch.setenv("FAKE_TRITON_LOG", str(tmp_path / "calls"))
+    monkeypatch.setenv("FAKE_KEY_ID", md5)
+    p = TritonProvider(tmp_path / "state")
+    env = p.env()
+    assert env == {"SDC_URL": "https://us-east-1.api.joyent.com", "SDC_ACCOUNT": "me", "SDC_KEY_ID": md5}
+    # setup.sh:215-230: the private key whose MD5 fingerprint is SDC_KEY_ID
+    assert p.find_key(md5) == str(home / ".ssh" / "id_ed25519")
+    nets = p.networks()
+    assert [n.name for n in nets] == ["Joyent-SDC-Private", "Joyent-SDC-Public"]  # sorted (setup.sh:257)
+    assert next(i for i, n in enumerate(nets, 1) if n.name == p.default_network) == 2
+    pk = p.packages()
+    assert [x.name for x in pk] == ["k4-highcpu-kvm-1.75G", "k4-highcpu-kvm-7.75G"]  # -kvm- only (setup.sh:259)
+    m = p.create_machine("kubenode1", "3333", ["1111-aaaa"], tags={"role": "host"})
+    assert m.primaryip == "10.0.0.9" and m.id == "id-kubenode1"
+    p.delete_machine(m)
+    calls = (tmp_path / "calls").read_text().splitlines()
+    assert any(c.startswith("instance create --wait --json --name=kubenode1 -N 1111-aaaa -t role=host") for c in calls)
+    assert "instance delete --wait id-kubenode1" in calls
+
+
+def test_triton_provider_without_cli_is_a_clear_error(tmp_path, monkeypatch):
+    from tritonk8ssupervisor_amd.provider.base import ProvisionError
+    from tritonk8ssupervisor_amd.provider.triton import TritonProvider
+
+    monkeypatch.setenv("PATH", str(tmp_path))
+    with pytest.raises(ProvisionError, match="CLI not found"):
+        TritonProvider(tmp_path).networks()
