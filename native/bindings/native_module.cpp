@@ -70,6 +70,7 @@ PYBIND11_MODULE(_tk8s_native, m) {
       py::arg("factor") = 4, py::arg("iters") = 10, py::arg("warmup") = 2,
       py::arg("dtype") = "float32", py::arg("check") = true, G());
   m.def("rccl_version", &tk8s::rccl_version);
+  m.def("release_probe_scratch", &tk8s::release_probe_scratch, G());
 
   // ---- raw launchers --------------------------------------------------------------------
   m.def("streaming_grid", &tk8s::streaming_grid, py::arg("blocks_per_cu") = 8);

@@ -29,4 +29,8 @@ std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int ite
 // over xGMI (peer access enabled) and the SDMA engine path (hipMemcpyPeerAsync).
 std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters);
 
+// The local probes share one grow-on-demand device allocation per device (see probes.cpp);
+// free them (e.g. from a long-lived process once validation is done).
+void release_probe_scratch();
+
 }  // namespace tk8s

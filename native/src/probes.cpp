@@ -5,7 +5,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "tk8s/common.h"
@@ -54,7 +56,44 @@ struct Stream {
   ~Stream() { (void)hipStreamDestroy(s); }
 };
 
+// Per-device scratch arena for the local probes. The validation payload runs HBM, MD5 and copy
+// probes back to back; giving each its own hipMalloc/hipFree of 0.25-1 GiB cost ~70 ms per
+// device on MI355X (more than all the kernels together), so they share one allocation that
+// grows on demand and lives until release_probe_scratch() / process exit. Peer copies keep
+// their own buffers (another device's thread may be using its arena concurrently).
+std::mutex g_scratch_mu;
+std::map<int, std::pair<void*, size_t>> g_scratch;
+
+char* scratch(int device, size_t bytes) {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  auto& slot = g_scratch[device];
+  if (slot.second < bytes) {
+    if (slot.first) TK8S_HIP_CHECK(hipFree(slot.first));
+    slot.first = nullptr;
+    slot.second = 0;
+    TK8S_HIP_CHECK(hipMalloc(&slot.first, bytes));
+    slot.second = bytes;
+  }
+  return static_cast<char*>(slot.first);
+}
+
+constexpr size_t kAlign = 4096;
+size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
 }  // namespace
+
+void release_probe_scratch() {
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  for (auto& kv : g_scratch) {
+    if (!kv.second.first) continue;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(kv.first);
+    (void)hipFree(kv.second.first);
+    (void)hipSetDevice(prev);
+  }
+  g_scratch.clear();
+}
 
 std::string gpuinfo_json(bool with_links) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -138,20 +177,22 @@ std::string hbm_write_probe(size_t bytes, int iters, StoreMode mode, int device,
     iters = std::max(iters, 1);
     DeviceGuard g(device);
     Stream st;
-    DeviceBuffer buf(bytes), bad(sizeof(unsigned long long));
+    char* base = scratch(device, align_up(bytes) + kAlign);
+    void* buf = base;
+    auto* bad = reinterpret_cast<unsigned long long*>(base + align_up(bytes));
     EventTimer cold, warm;
     cold.start(st.s);
-    hbm_fill(buf.get(), bytes, value ^ 0xFFFFFFFFu, mode, st.s);  // cold write (first touch)
+    hbm_fill(buf, bytes, value ^ 0xFFFFFFFFu, mode, st.s);  // cold write (first touch)
     cold.stop(st.s);
     const float cold_ms = cold.elapsed_ms();
     warm.start(st.s);
-    for (int i = 0; i < iters; ++i) hbm_fill(buf.get(), bytes, value, mode, st.s);
+    for (int i = 0; i < iters; ++i) hbm_fill(buf, bytes, value, mode, st.s);
     warm.stop(st.s);
     const float ms = warm.elapsed_ms() / iters;
-    TK8S_HIP_CHECK(hipMemsetAsync(bad.get(), 0, sizeof(unsigned long long), st.s));
-    verify_fill(buf.get(), bytes, value, bad.as<unsigned long long>(), st.s);
+    TK8S_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), st.s));
+    verify_fill(buf, bytes, value, bad, st.s);
     unsigned long long nbad = 0;
-    TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad.get(), sizeof nbad, hipMemcpyDeviceToHost, st.s));
+    TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad, sizeof nbad, hipMemcpyDeviceToHost, st.s));
     TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
     return Json()
         .kv("ok", nbad == 0)
@@ -179,23 +220,24 @@ std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int ite
     DeviceGuard g(device);
     Stream st;
     const size_t ws = md5_tree_workspace(bytes, chunk_bytes);
-    DeviceBuffer data(std::max<size_t>(bytes, 16)), wa(ws), wb(ws), out(16);
+    const size_t o_wa = align_up(std::max<size_t>(bytes, 16)), o_wb = o_wa + align_up(ws), o_out = o_wb + align_up(ws);
+    char* base = scratch(device, o_out + kAlign);
+    void *data = base, *wa = base + o_wa, *wb = base + o_wb, *out = base + o_out;
     EventTimer fill_t, cold_t, warm_t;
     fill_t.start(st.s);
-    philox_fill(data.get(), bytes, seed, st.s);
+    philox_fill(data, bytes, seed, st.s);
     fill_t.stop(st.s);
     const float fill_ms = fill_t.elapsed_ms();
     cold_t.start(st.s);
-    md5_tree(data.get(), bytes, chunk_bytes, wa.get(), wb.get(), out.get(), st.s);
+    md5_tree(data, bytes, chunk_bytes, wa, wb, out, st.s);
     cold_t.stop(st.s);
     const float cold_ms = cold_t.elapsed_ms();
     warm_t.start(st.s);
-    for (int i = 0; i < iters; ++i)
-      md5_tree(data.get(), bytes, chunk_bytes, wa.get(), wb.get(), out.get(), st.s);
+    for (int i = 0; i < iters; ++i) md5_tree(data, bytes, chunk_bytes, wa, wb, out, st.s);
     warm_t.stop(st.s);
     const float ms = warm_t.elapsed_ms() / iters;
     unsigned char digest[16];
-    TK8S_HIP_CHECK(hipMemcpyAsync(digest, out.get(), 16, hipMemcpyDeviceToHost, st.s));
+    TK8S_HIP_CHECK(hipMemcpyAsync(digest, out, 16, hipMemcpyDeviceToHost, st.s));
     TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
     return Json()
         .kv("ok", true)
@@ -228,35 +270,51 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters) 
       TK8S_HIP_CHECK(hipDeviceCanAccessPeer(&can, dst_device, src_device));
       if (!can) return error_json("no peer access from dst to src");
     }
-    DeviceBuffer* src_buf = nullptr;
+    // Local: src, dst and the error counter are carved from this device's scratch arena.
+    // Peer: own buffers (the source device's arena may be busy in another thread).
+    std::unique_ptr<DeviceBuffer> src_own, dst_own, bad_own;
+    void *src = nullptr, *dst = nullptr;
+    unsigned long long* bad = nullptr;
+    if (!peer) {
+      DeviceGuard g(src_device);
+      char* base = scratch(src_device, 2 * align_up(bytes) + kAlign);
+      src = base;
+      dst = base + align_up(bytes);
+      bad = reinterpret_cast<unsigned long long*>(base + 2 * align_up(bytes));
+    } else {
+      DeviceGuard g(src_device);
+      src_own.reset(new DeviceBuffer(bytes));
+      src = src_own->get();
+    }
     {
       DeviceGuard g(src_device);
-      src_buf = new DeviceBuffer(bytes);
-      hbm_fill(src_buf->get(), bytes, 0xA5A5A5A5u, StoreMode::kPlain, nullptr);
-      TK8S_HIP_CHECK(hipDeviceSynchronize());
+      hbm_fill(src, bytes, 0xA5A5A5A5u, StoreMode::kPlain, nullptr);
+      TK8S_HIP_CHECK(hipStreamSynchronize(nullptr));
     }
-    std::unique_ptr<DeviceBuffer> src_owner(src_buf);
     DeviceGuard g(dst_device);
     if (peer) {
       const hipError_t pe = hipDeviceEnablePeerAccess(src_device, 0);
       if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) TK8S_HIP_CHECK(pe);
       (void)hipGetLastError();
+      dst_own.reset(new DeviceBuffer(bytes));
+      bad_own.reset(new DeviceBuffer(sizeof(unsigned long long)));
+      dst = dst_own->get();
+      bad = bad_own->as<unsigned long long>();
     }
     Stream st;
-    DeviceBuffer dst(bytes), bad(sizeof(unsigned long long));
-    stream_copy(dst.get(), src_buf->get(), bytes, st.s);  // warm-up
+    stream_copy(dst, src, bytes, st.s);  // warm-up
     EventTimer kt, dt;
     kt.start(st.s);
-    for (int i = 0; i < iters; ++i) stream_copy(dst.get(), src_buf->get(), bytes, st.s);
+    for (int i = 0; i < iters; ++i) stream_copy(dst, src, bytes, st.s);
     kt.stop(st.s);
     const float kernel_ms = kt.elapsed_ms() / iters;
-    TK8S_HIP_CHECK(hipMemsetAsync(bad.get(), 0, sizeof(unsigned long long), st.s));
-    verify_fill(dst.get(), bytes, 0xA5A5A5A5u, bad.as<unsigned long long>(), st.s);
+    TK8S_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), st.s));
+    verify_fill(dst, bytes, 0xA5A5A5A5u, bad, st.s);
     unsigned long long nbad = 0;
-    TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad.get(), sizeof nbad, hipMemcpyDeviceToHost, st.s));
+    TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad, sizeof nbad, hipMemcpyDeviceToHost, st.s));
     dt.start(st.s);
     for (int i = 0; i < iters; ++i)
-      TK8S_HIP_CHECK(hipMemcpyPeerAsync(dst.get(), dst_device, src_buf->get(), src_device, bytes, st.s));
+      TK8S_HIP_CHECK(hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, st.s));
     dt.stop(st.s);
     const float dma_ms = dt.elapsed_ms() / iters;
     return Json()

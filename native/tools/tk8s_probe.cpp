@@ -22,8 +22,10 @@
 // the Philox stream is 55af80380d572d36cc8cc7d50edd90ab (host oracle:
 // tritonk8ssupervisor_amd/ops/reference.py md5_tree(philox_bytes(256 MiB, 0), 1024)); every
 // device must reproduce it, and for other sizes every device must agree with device 0.
+#include <signal.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <fstream>
@@ -63,11 +65,22 @@ struct DeviceResult {
 
 bool exists(const std::string& p) { return access(p.c_str(), F_OK) == 0; }
 
-// --reuse: print a finished (or still running) burn-in's result. Returns -1 when there is none.
+// pid written into FILE.pending by the launcher (0 / absent: unknown, assume alive).
+bool burnin_alive(const std::string& pending) {
+  std::ifstream f(pending);
+  long pid = 0;
+  if (!(f >> pid) || pid <= 0) return true;
+  return kill(static_cast<pid_t>(pid), 0) == 0 || errno == EPERM;
+}
+
+// --reuse: print a finished (or still running) burn-in's result. Returns -1 when there is none
+// (no burn-in, or it died without writing a result): the caller then probes itself.
 int reuse(const std::string& file, double wait_s) {
   const auto t = std::chrono::steady_clock::now();
-  while (!exists(file) && exists(file + ".pending") && ms_since(t) < wait_s * 1e3)
+  while (!exists(file) && exists(file + ".pending") && ms_since(t) < wait_s * 1e3) {
+    if (!burnin_alive(file + ".pending") && !exists(file)) break;
     std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  }
   std::ifstream f(file);
   if (!f) return -1;
   std::stringstream ss;

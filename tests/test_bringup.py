@@ -163,6 +163,14 @@ def test_validation_failure_fails_setup_fast(ws):
     assert time.monotonic() - t < 60
 
 
+def test_crashed_burnin_falls_back_to_probing_in_the_pod(ws):
+    t = time.monotonic()
+    s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=_env(TK8S_FAKE_BURNIN_CRASH="kubenode2")))
+    assert s["nodes_validated"] == 2 and time.monotonic() - t < 30  # no 120 s --reuse wait
+    assert not (ws / ".tk8s" / "machines" / "kubenode2" / "run" / "gpu-burnin.json").exists()
+    assert (ws / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json").exists()
+
+
 def test_stalled_node_hits_the_bounded_timeout(ws):
     # the reference's readiness loop has no timeout (setup.sh:59-85); ours exits 124
     t = time.monotonic()

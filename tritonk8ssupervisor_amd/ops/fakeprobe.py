@@ -4,7 +4,8 @@ Emits the same JSON shape as native/tools/tk8s_probe.cpp and honours the same pi
 (``--out FILE`` for the early burn-in, ``--reuse FILE [--reuse-wait S]`` for the validation
 pod), so the validation DaemonSet, the node condition logic and the device-plugin refresh run
 unchanged; never used on a GPU host (setup picks the real tool whenever TK8S_FAKE_GPUS is unset).
-Test hooks: ``TK8S_FAKE_PROBE_FAIL=<node>`` fails, ``TK8S_FAKE_PROBE_HANG=<node>`` wedges.
+Test hooks: ``TK8S_FAKE_PROBE_FAIL=<node>`` fails, ``TK8S_FAKE_PROBE_HANG=<node>`` wedges,
+``TK8S_FAKE_BURNIN_CRASH=<node>`` kills the early burn-in before it writes a result.
 """
 import json
 import os
@@ -17,9 +18,27 @@ def _arg(name, default=None):
     return a[a.index(name) + 1] if name in a and a.index(name) + 1 < len(a) else default
 
 
+def _alive(pending):
+    try:
+        pid = int(open(pending).read().strip() or 0)
+    except (OSError, ValueError):
+        return True
+    if pid <= 0:
+        return True
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        pass
+    return True
+
+
 def _reuse(path, wait):
     t = time.monotonic()
     while not os.path.exists(path) and os.path.exists(path + ".pending") and time.monotonic() - t < wait:
+        if not _alive(path + ".pending") and not os.path.exists(path):
+            break
         time.sleep(0.002)
     try:
         with open(path) as f:
@@ -51,6 +70,8 @@ def main():
         if rc is not None:
             return rc
     node = os.environ.get("NODE_NAME") or os.environ.get("TK8S_MACHINE", "-")
+    if "--out" in sys.argv and os.environ.get("TK8S_FAKE_BURNIN_CRASH", "") == node:
+        return 139  # the burn-in dies without a result; the validation pod must probe by itself
     if os.environ.get("TK8S_FAKE_PROBE_HANG", "") == node:
         time.sleep(3600)  # a wedged validation (the analogue of the reference's stuck dashboard)
     n = len([x for x in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if x])

@@ -35,7 +35,7 @@ from .utils import yamlio
 from .utils.events import EventLog
 
 MODULE_ALIASES = {"command", "shell", "uri", "slurp", "pause", "debug", "set_fact", "wait_for", "fail",
-                  "assert", "copy", "file", "stat", "tk8s_daemon", "tk8s_gpu_facts", "tk8s_build", "tk8s_kube",
+                  "assert", "copy", "file", "stat", "tk8s_daemon", "tk8s_gpu_facts", "tk8s_burnin", "tk8s_build", "tk8s_kube",
                   "include_vars", "meta", "ping"}
 TASK_KEYS = {"name", "register", "when", "until", "retries", "delay", "with_items", "loop", "run_once",
              "delegate_to", "local_action", "action", "ignore_errors", "failed_when", "changed_when",

@@ -316,6 +316,46 @@ def m_tk8s_daemon(args, *, ctx, target, local, env, check, **_):
     return {"changed": True, "running": True, **info}
 
 
+def m_tk8s_burnin(args, *, ctx, target, local, env, check, **_):
+    """Start the early GPU burn-in on a machine's GPUs (no-op for GPU-less machines).
+
+    command: the validation command (list); out: result file relative to the machine dir.
+    Creates ``<out>.pending`` first (the validation pod's ``--reuse`` waits on it), then starts
+    ``command --out <out>`` as a one-shot daemon (pidfile under run/, killed on teardown)
+    with HIP_VISIBLE_DEVICES = the machine's GPUs composed onto this process's view.
+    """
+    ex = ctx.executor
+    if ex is None or local:
+        return {"changed": False, "skipped": True, "msg": "no machine executor"}
+    gpus = ex.machine_gpus(target.name)
+    if not gpus:
+        return {"changed": False, "skipped": True, "msg": "machine has no GPUs"}
+    if check:
+        return {"changed": True, "msg": "would start the GPU burn-in"}
+    from .models.hostinfo import compose_visible_devices
+
+    out = str(args.get("out", "run/gpu-burnin.json"))
+    pending = Path(ex.machine_dir(target.name)) / (out + ".pending")
+    pending.parent.mkdir(parents=True, exist_ok=True)
+    pending.touch()
+    denv = dict(compose_visible_devices(gpus))
+    denv["NODE_NAME"] = target.name
+    denv.update({str(k): str(v) for k, v in (env or {}).items()})
+    argv = [str(a) for a in args["command"]] + ["--out", out]
+    if os.sep in argv[0] and not os.access(argv[0], os.X_OK):
+        pending.unlink(missing_ok=True)  # not built yet: the validation pod will probe itself
+        return {"changed": False, "skipped": True, "msg": f"{argv[0]} is not built yet"}
+    info = ex.start_daemon(target.name, str(args.get("name", "gpu-burnin")), argv, env=denv, restart="no",
+                           wait_for_log=None, timeout=0)
+    if not info.get("ok"):
+        pending.unlink(missing_ok=True)
+        return {"failed": True, "msg": info.get("msg", "burn-in failed to start")}
+    if not (Path(ex.machine_dir(target.name)) / out).exists():
+        # the pid lets `--reuse` stop waiting if the burn-in dies without a result
+        pending.write_text(f"{info.get('pid', 0)}\n")
+    return {"changed": True, "pid": info.get("pid"), "gpus": gpus, "out": out}
+
+
 def m_tk8s_gpu_facts(args, *, ctx, target, local, **_):
     from .models.hostinfo import discover
 
@@ -388,6 +428,6 @@ MODULES = {
     "command": m_command, "shell": m_shell, "uri": m_uri, "slurp": m_slurp, "copy": m_copy, "file": m_file,
     "stat": m_stat, "include_vars": m_include_vars, "pause": m_pause, "debug": m_debug, "set_fact": m_set_fact,
     "fail": m_fail, "assert": m_assert, "wait_for": m_wait_for, "meta": m_meta, "ping": m_ping,
-    "tk8s_daemon": m_tk8s_daemon, "tk8s_gpu_facts": m_tk8s_gpu_facts, "tk8s_build": m_tk8s_build,
+    "tk8s_daemon": m_tk8s_daemon, "tk8s_gpu_facts": m_tk8s_gpu_facts, "tk8s_burnin": m_tk8s_burnin, "tk8s_build": m_tk8s_build,
     "tk8s_kube": m_tk8s_kube,
 }
