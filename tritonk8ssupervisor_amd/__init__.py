@@ -30,4 +30,26 @@ def _fast_site() -> None:
             sys.path.append(d)
 
 
+def _pycache_prefix() -> None:
+    """Keep byte code in a writable in-tree cache (``build/pycache``) for every interpreter of a
+    bring-up and its children. On the GPU hosts the daemons' user cannot write the system
+    ``__pycache__`` dirs and part of the stdlib and site-packages ships without valid .pyc
+    files: measured there, each interpreter start compiled 66 modules from source (~50 ms),
+    three times on the critical path. ``build()`` warms this cache once."""
+    import os
+    import sys
+
+    if sys.pycache_prefix or os.environ.get("PYTHONPYCACHEPREFIX") or os.environ.get("TK8S_NO_PYCACHE_PREFIX"):
+        return
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "pycache")
+    try:
+        os.makedirs(d, exist_ok=True)
+    except OSError:
+        return
+    if os.access(d, os.W_OK):
+        sys.pycache_prefix = d
+        os.environ["PYTHONPYCACHEPREFIX"] = d
+
+
 _fast_site()
+_pycache_prefix()

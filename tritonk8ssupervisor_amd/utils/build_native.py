@@ -178,8 +178,25 @@ def precompile_python() -> None:
     import compileall
     import py_compile
 
-    compileall.compile_dir(str(PKG), quiet=2, workers=1, force=True,
-                           invalidation_mode=py_compile.PycInvalidationMode.CHECKED_HASH)
+    prefix = sys.pycache_prefix
+    sys.pycache_prefix = None  # the in-package __pycache__ copies, for interpreters without the prefix
+    try:
+        compileall.compile_dir(str(PKG), quiet=2, workers=1, force=True,
+                               invalidation_mode=py_compile.PycInvalidationMode.CHECKED_HASH)
+    finally:
+        sys.pycache_prefix = prefix
+    # Warm the shared prefix cache (tritonk8ssupervisor_amd/__init__.py) with everything the CLI,
+    # the control plane and the agents import, stdlib and PyYAML included.
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([str(REPO)] + [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p])
+    mods = ["tritonk8ssupervisor_amd.cli.main", "tritonk8ssupervisor_amd.cli.kubectl", "tritonk8ssupervisor_amd.orchestrator",
+            "tritonk8ssupervisor_amd.playbook", "tritonk8ssupervisor_amd.playbook_modules", "tritonk8ssupervisor_amd.kube",
+            "tritonk8ssupervisor_amd.wizard", "tritonk8ssupervisor_amd.controlplane.server",
+            "tritonk8ssupervisor_amd.agent.agent", "tritonk8ssupervisor_amd.ops.fakeprobe", "yaml", "argparse", "asyncio",
+            "tritonk8ssupervisor_amd.controlplane.client", "tritonk8ssupervisor_amd.parallel.dist_allreduce"]
+    code = "import importlib\nfor m in %r:\n    importlib.import_module(m)\n" % (mods[:-1] + ["tritonk8ssupervisor_amd.provision"],)
+    for flag in (["-S"], []):
+        subprocess.run([sys.executable, *flag, "-c", code], env=env, cwd=str(REPO), capture_output=True, timeout=120)
 
 
 def main(argv: list[str] | None = None) -> int:
