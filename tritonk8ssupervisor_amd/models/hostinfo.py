@@ -92,7 +92,24 @@ def fake_inventory(n: int) -> HostInventory:
     return HostInventory(gpus=gpus, links=links, source="fake")
 
 
-def discover(root: Path = KFD_ROOT) -> HostInventory:
+_CACHE: dict[tuple, HostInventory] = {}
+
+
+def discover(root: Path = KFD_ROOT, cache: bool = True) -> HostInventory:
+    """Host inventory; memoised per process for the same root and visibility environment
+    (provisioning asks once per machine, the playbook once per host: on an 8-GPU host each
+    sysfs walk reads ~100 property files). The result is shared: treat it as read-only."""
+    key = (str(root), os.environ.get("TK8S_FAKE_GPUS"), os.environ.get("HIP_VISIBLE_DEVICES"),
+           os.environ.get("CUDA_VISIBLE_DEVICES"))
+    if cache and key in _CACHE:
+        return _CACHE[key]
+    inv = _discover(root)
+    if cache:
+        _CACHE[key] = inv
+    return inv
+
+
+def _discover(root: Path) -> HostInventory:
     fake = os.environ.get("TK8S_FAKE_GPUS")
     if fake is not None and fake.strip() != "":
         return fake_inventory(int(fake))

@@ -206,7 +206,7 @@ class Setup:
                  out: Callable[[str], None] = None, quiet_ansible: bool = True, hbm_bytes: int = 1 << 30,
                  md5_bytes: int = 256 << 20, probe_iters: int = 3, rccl_max_bytes: int = 64 << 20,
                  node_grace: float = 5.0, backend: str | None = None, master_port: int | None = None,
-                 rocprof: bool = False):
+                 rocprof: bool = False, rccl_timeout: float | None = None):
         self.ws = ws
         self.answers = answers
         self.assume_yes = assume_yes
@@ -222,6 +222,7 @@ class Setup:
         self.backend = backend or os.environ.get("TK8S_BACKEND", "local")
         self.master_port = master_port
         self.rocprof = rocprof
+        self.rccl_timeout = rccl_timeout
         ws.state_dir.mkdir(parents=True, exist_ok=True)
         self.events = EventLog(ws.events, echo=False)
         self.provider = get_provider(self.backend, ws.state_dir)
@@ -414,8 +415,11 @@ class Setup:
                               {"job_name": job, "nranks": g, "rccl_command": cmd})
         apply_objects(k, objs)
         self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job})")
-        left = max(10.0, self.timeout)
-        j = wait_job(k, job, "kube-system", timeout=left)
+        left = max(10.0, self.rccl_timeout or self.timeout)
+        try:
+            j = wait_job(k, job, "kube-system", timeout=left)
+        except TimeoutError as e:
+            raise SetupError(f"RCCL all-reduce Job {job} did not finish within {left:.0f}s: {e}", code=124) from e
         pods = pods_of(k, f"job-name={job}", "kube-system")
         results = [p.get("status", {}).get("result") or {} for p in pods]
         peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)

@@ -177,10 +177,14 @@ class Engine:
         for p in spec.provisioners:
             kind = p.labels[0] if p.labels else ""
             if kind == "remote-exec":
-                for cmd in hcl.interpolate(p.attrs.get("inline", []), ctx):
-                    rc, out = self.provider.exec(m, cmd)
+                # Like Terraform, the inline list runs as ONE script on the machine, in order,
+                # stopping at the first failing command (one shell spawn per machine, not per line).
+                cmds = list(hcl.interpolate(p.attrs.get("inline", []), ctx))
+                if cmds:
+                    script = "set -e\n" + "\n".join(cmds)
+                    rc, out = self.provider.exec(m, script)
                     if rc != 0:
-                        raise ProvisionError(f"{spec.address}: remote-exec {cmd!r} failed rc={rc}: {out.strip()[-400:]}")
+                        raise ProvisionError(f"{spec.address}: remote-exec failed rc={rc}: {out.strip()[-400:]}")
             elif kind == "local-exec":
                 cmd = hcl.interpolate(p.attrs["command"], ctx)
                 with self._exec_lock:
