@@ -70,7 +70,13 @@ bool burnin_alive(const std::string& pending) {
   std::ifstream f(pending);
   long pid = 0;
   if (!(f >> pid) || pid <= 0) return true;
-  return kill(static_cast<pid_t>(pid), 0) == 0 || errno == EPERM;
+  if (kill(static_cast<pid_t>(pid), 0) != 0 && errno != EPERM) return false;
+  // An exited burn-in its launcher has not reaped yet is a zombie: dead for our purpose.
+  std::ifstream st("/proc/" + std::to_string(pid) + "/stat");
+  std::string line;
+  if (!std::getline(st, line)) return true;
+  const auto rp = line.rfind(')');
+  return rp == std::string::npos || rp + 2 >= line.size() || line[rp + 2] != 'Z';
 }
 
 // --reuse: print a finished (or still running) burn-in's result. Returns -1 when there is none

@@ -286,3 +286,17 @@ def test_manual_flow(ws):
     (ws / "kc.json").write_bytes(urllib.request.urlopen(f"{base}/env/{env_id}/kubernetes/kubectl?format=json").read())
     out = sh("./kubectl", "--kubeconfig", "kc.json", "get", "nodes").stdout
     assert "kubenode1" in out and "Ready" in out
+
+
+def test_rerunning_the_playbook_is_idempotent(ws):
+    """Re-running clusterUp.yml on a live cluster changes nothing: the control plane and the
+    agents keep running, no second environment and no second node registration appear."""
+    s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off"))
+    pids = sorted(_pids(ws))
+    r = subprocess.run(["./tk8s", "ansible-playbook", "-i", "hosts", "clusterUp.yml"], cwd=ws, env=_env(),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert sorted(_pids(ws)) == pids
+    assert (ws / "ansible" / "tmp" / "kubernetes_environment.id").read_text().strip() == s["project"]
+    out = subprocess.run(["./kubectl", "get", "nodes", "-o", "json"], cwd=ws, env=_env(), capture_output=True, text=True)
+    assert len(json.loads(out.stdout)["items"]) == 2

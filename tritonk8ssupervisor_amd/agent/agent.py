@@ -3,6 +3,7 @@
 Plays the part of ``rancher/agent`` + kubelet on every HOST (ansible/roles/rancherhost/tasks/
 main.yml:26-34 starts the agent with the registration URL as its only argument):
 
+  0. (optional standby, --await-url)  start before the control plane exists; wait for the URL
   1. GET  <registrationUrl>          bootstrap (project, API prefix, heartbeat period)
   2. device plugin discovery          sysfs only — the agent never initialises the GPU
   3. POST <registrationUrl>          register the node (capacity incl. amd.com/gpu) -> node token
@@ -43,7 +44,7 @@ def pod_gpus(p: dict) -> int:
 
 
 class Agent:
-    def __init__(self, url: str, name: str, ip: str, sandbox: str, gpus: list[int],
+    def __init__(self, url: str | None, name: str, ip: str, sandbox: str, gpus: list[int],
                  labels: dict | None = None, tool_dirs: list[str] | None = None, timeout: float = 60.0):
         self.reg_url = url
         self.name = name
@@ -58,9 +59,31 @@ class Agent:
         self.hb_period = 1.0
         self._devices_dirty = False
         self._pods_meta: dict[str, dict] = {}
+        if url:
+            self.set_url(url)
+
+    def set_url(self, url: str) -> None:
+        self.reg_url = url
         scheme_rest = url.split("://", 1)[1]
         self.base = "http://" + scheme_rest.split("/", 1)[0]
         self.reg_path = "/" + scheme_rest.split("/", 1)[1]
+
+    def await_url(self, path: Path) -> None:
+        """Standby (kubelet started before `join`): the interpreter, imports and device discovery
+        are done before the control plane even exists; registration starts the moment the
+        rancherhost role drops the registration URL into `path`."""
+        delay = 0.0005
+        while not self.stop.is_set():
+            try:
+                url = path.read_text().strip()
+            except OSError:
+                url = ""
+            if url:
+                self.set_url(url)
+                return
+            time.sleep(delay)
+            delay = min(delay * 2, 0.005)
+        raise SystemExit(0)
 
     # ---- join -------------------------------------------------------------------------
     def join(self) -> None:
@@ -90,6 +113,11 @@ class Agent:
         self.hb_period = float(r.get("heartbeatSeconds", boot.get("heartbeatSeconds", 1.0)))
         self.api = Client(self.base, token=r["nodeToken"], prefix=r["apiPrefix"], timeout=10.0)
         c.close()
+        try:  # lets a re-run of the rancherhost role see that this host has joined
+            (self.sandbox / "run").mkdir(parents=True, exist_ok=True)
+            (self.sandbox / "run" / "node-registered").write_text(f"{self.base} {r.get('projectId', '')}\n")
+        except OSError:
+            pass
         n = fault("agent.crash", self.name)
         if n is not None:
             counter = self.sandbox / "run" / "crash.count"
@@ -237,8 +265,10 @@ class Agent:
             self._start_pod(pod)
 
     # ---- lifecycle --------------------------------------------------------------------
-    def run(self) -> int:
+    def run(self, await_url: Path | None = None) -> int:
         install_sigterm()
+        if not self.reg_url and await_url is not None:
+            self.await_url(await_url)
         t0 = time.monotonic()
         self.join()
         print(f"{self.name}: registered in {time.monotonic() - t0:.3f}s "
@@ -286,14 +316,17 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--labels", default="")
     ap.add_argument("--tool-dir", action="append", default=[])
     ap.add_argument("--timeout", type=float, default=60.0)
+    ap.add_argument("--await-url", default=None,
+                    help="standby: wait for a file holding the registration URL (relative to --sandbox)")
     a = ap.parse_args(argv)
     url = a.url_opt or a.url
-    if not url:
-        ap.error("registration URL is required")
+    if not url and not a.await_url:
+        ap.error("registration URL (or --await-url FILE) is required")
     gpus = [int(x) for x in a.gpus.split(",") if x.strip() != ""]
     labels = dict(kv.split("=", 1) for kv in a.labels.split(",") if "=" in kv)
     tools = a.tool_dir or [str(Path(__file__).resolve().parents[1] / "bin")]
-    return Agent(url, a.name, a.ip, a.sandbox, gpus, labels, tools, a.timeout).run()
+    wait = Path(a.sandbox) / a.await_url if a.await_url else None
+    return Agent(url, a.name, a.ip, a.sandbox, gpus, labels, tools, a.timeout).run(wait)
 
 
 if __name__ == "__main__":

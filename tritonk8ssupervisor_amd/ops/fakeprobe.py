@@ -31,7 +31,11 @@ def _alive(pending):
         return False
     except PermissionError:
         pass
-    return True
+    try:  # an exited burn-in its launcher has not reaped yet is a zombie: dead for our purpose
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except (OSError, IndexError):
+        return True
 
 
 def _reuse(path, wait):
