@@ -321,6 +321,7 @@ def main(argv=None) -> int:
         "gpus_allocatable": last.get("gpus_allocatable"),
         "nodes_validated": last.get("nodes_validated"),
         "rccl_peak_busbw_gbps": (last.get("rccl") or {}).get("peak_busbw_gbps"),
+        "validation_last_step": last.get("validation"),
     }
     errs = [s["post_ready_error"] for s in summaries if s.get("post_ready_error")]
     if errs:

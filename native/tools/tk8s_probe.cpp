@@ -59,7 +59,7 @@ double ms_since(std::chrono::steady_clock::time_point t) {
 struct DeviceResult {
   std::string hbm, md5, copy, digest;
   std::vector<std::string> peers;
-  double wall_ms = 0;
+  double wall_ms = 0, hbm_ms = 0, md5_ms = 0, copy_ms = 0, peers_ms = 0;  // host wall clock per phase
   bool ok = true;
 };
 
@@ -150,26 +150,36 @@ int main(int argc, char** argv) {
       devices.push_back(d);
     }
     std::string info;
+    const auto tg = std::chrono::steady_clock::now();
     if (a.has("gpuinfo")) info = tk8s::gpuinfo_json(true);
+    const double gpuinfo_ms = ms_since(tg);
 
     std::vector<DeviceResult> res(devices.size());
     auto run_one = [&](size_t k) {
       const auto td = std::chrono::steady_clock::now();
       DeviceResult& r = res[k];
       const int dev = devices[k];
+      auto t = std::chrono::steady_clock::now();
       r.hbm = hbm ? tk8s::hbm_write_probe(hbm, iters, mode, dev) : std::string("{\"ok\":true,\"skipped\":true}");
+      r.hbm_ms = ms_since(t);
+      t = std::chrono::steady_clock::now();
       if (md5) {
         r.md5 = tk8s::md5_probe(md5, chunk, seed, iters, dev);
         r.digest = field(r.md5, "digest");
       }
+      r.md5_ms = ms_since(t);
+      t = std::chrono::steady_clock::now();
       if (copy) r.copy = tk8s::copy_probe(dev, dev, copy, iters);
+      r.copy_ms = ms_since(t);
       r.ok = ok_of(r.hbm) && (r.md5.empty() || ok_of(r.md5)) && (r.copy.empty() || ok_of(r.copy));
+      t = std::chrono::steady_clock::now();
       if (a.has("peers"))
         for (int s : devices)
           if (s != dev) {
             r.peers.push_back(tk8s::copy_probe(s, dev, peer_bytes, iters));
             r.ok = r.ok && ok_of(r.peers.back());
           }
+      r.peers_ms = ms_since(t);
       r.wall_ms = ms_since(td);
     };
     std::vector<std::thread> threads;
@@ -189,7 +199,10 @@ int main(int argc, char** argv) {
       r.ok = r.ok && digest_ok;
       ok = ok && r.ok;
       tk8s::Json d;
-      d.kv("device", devices[k]).kv("ok", r.ok).kv("wall_ms", r.wall_ms).raw("hbm", r.hbm);
+      d.kv("device", devices[k]).kv("ok", r.ok).kv("wall_ms", r.wall_ms)
+          .raw("phase_ms", tk8s::Json().kv("hbm", r.hbm_ms).kv("md5", r.md5_ms).kv("copy", r.copy_ms)
+                               .kv("peers", r.peers_ms).str())
+          .raw("hbm", r.hbm);
       if (md5) d.raw("md5", r.md5).kv("digest_ok", digest_ok);
       if (copy) d.raw("copy", r.copy);
       if (!r.peers.empty()) d.raw("peers", tk8s::Json::array(r.peers));
@@ -203,7 +216,7 @@ int main(int argc, char** argv) {
     if (copy) out.raw("copy", res[0].copy);
     out.raw("devices", tk8s::Json::array(per_dev));
     if (!info.empty()) out.raw("gpuinfo", info);
-    out.raw("timings_ms", tk8s::Json().kv("hip_init", init_ms).kv("total", ms_since(t0)).str());
+    out.raw("timings_ms", tk8s::Json().kv("hip_init", init_ms).kv("gpuinfo", gpuinfo_ms).kv("total", ms_since(t0)).str());
     emit(out.str(), out_file);
     return ok ? 0 : 1;
   } catch (const std::exception& e) {

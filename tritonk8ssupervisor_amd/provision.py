@@ -67,12 +67,13 @@ class ApplyResult:
 
 class Engine:
     def __init__(self, tf_dir: str | os.PathLike, provider: Provider, events: EventLog | None = None,
-                 parallelism: int | None = None, retries: int = 1):
+                 parallelism: int | None = None, retries: int = 1, on_created=None):
         self.dir = Path(tf_dir).resolve()
         self.provider = provider
         self.events = events or EventLog(None)
         self.parallelism = parallelism
         self.retries = retries
+        self.on_created = on_created  # callback(spec address, Machine) once a machine is bootstrapped
         self._state_lock = threading.Lock()
         self._exec_lock = threading.Lock()
 
@@ -219,6 +220,11 @@ class Engine:
             self._save_resource(spec.address, {"module": spec.module, "machine": m.to_dict(), "tainted": False})
             self.events.emit("machine_created", address=spec.address, name=m.name, ip=m.primaryip,
                              gpus=m.gpus, seconds=round(time.monotonic() - t, 6))
+            if self.on_created is not None:
+                try:
+                    self.on_created(spec.address, m)
+                except Exception as e:  # noqa: BLE001 - a boot hook never fails provisioning
+                    self.events.emit("machine_boot_hook_failed", name=m.name, error=str(e))
             return m
         raise ProvisionError(f"{spec.address}: create failed after {self.retries + 1} attempts: {last_err}")
 
