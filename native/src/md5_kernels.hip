@@ -179,6 +179,93 @@ __global__ __launch_bounds__(kMd5Block) void md5_chunks_kernel(const unsigned ch
   digests[c] = u32x4{st[0], st[1], st[2], st[3]};
 }
 
+// ------------------------------------------------------------------------------------------
+// Coalesced form for full chunks whose size is a multiple of 128 B (the default 1 KiB):
+// one wave owns 64 consecutive chunks. Per step it pulls the next 128 B of all 64 chunks with
+// 8 wave-instructions (lane l of instruction i loads 16 B of chunk 8i + l/8), i.e. every
+// instruction reads 8 whole 128-B lines instead of 64 scattered 16-B pieces (the one-lane-
+// per-chunk loads above), stages them in a wave-private LDS tile and each lane reads its own
+// chunk's 32 words back. Rows are padded to 144 B (36 dwords): the 16 lanes of a ds_read_b128
+// phase then start on banks 36*l mod 64, all distinct, so the read-back is conflict-free.
+// The next step's global loads are issued before the current step's two compressions, so
+// HBM latency hides under 128 MD5 steps. LDS: 4 waves x 9 KiB per block -> 4 blocks (16 waves)
+// per CU.
+// ------------------------------------------------------------------------------------------
+constexpr int kWaveChunks = 64;
+constexpr int kRowVec = 9;  // u32x4 per LDS row: 8 of data + 1 of padding
+
+__device__ __forceinline__ void wave_sync_lds() {
+  // LDS ops of one wave complete in issue order; this only stops the compiler from moving the
+  // staging stores across the read-back (and vice versa).
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kMd5Block) void md5_chunks_coalesced_kernel(const unsigned char* __restrict__ src,
+                                                                        unsigned chunk_bytes,
+                                                                        unsigned long long ngroups,
+                                                                        u32x4* __restrict__ digests) {
+  __shared__ u32x4 tile[kMd5Block / 64][kWaveChunks * kRowVec];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long group = static_cast<unsigned long long>(blockIdx.x) * (kMd5Block / 64) + w;
+  if (group >= ngroups) return;  // wave-uniform
+  u32x4* my = tile[w];
+  const unsigned char* gbase = src + group * kWaveChunks * chunk_bytes;
+  const int sub = lane >> 3, piece = lane & 7;
+  const unsigned steps = chunk_bytes / 128;
+  u32x4 r[8];
+  auto load = [&](unsigned step) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      r[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+          gbase + static_cast<size_t>(8 * i + sub) * chunk_bytes + step * 128u + piece * 16u));
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) my[(8 * i + sub) * kRowVec + piece] = r[i];
+  };
+  unsigned st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  load(0);
+  stage();
+  for (unsigned step = 0; step < steps; ++step) {
+    if (step + 1 < steps) load(step + 1);
+    wave_sync_lds();
+    u32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = my[lane * kRowVec + k];
+    unsigned m[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      m[4 * q + 0] = v[q].x;
+      m[4 * q + 1] = v[q].y;
+      m[4 * q + 2] = v[q].z;
+      m[4 * q + 3] = v[q].w;
+    }
+    md5_compress(st, m);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      m[4 * q + 0] = v[4 + q].x;
+      m[4 * q + 1] = v[4 + q].y;
+      m[4 * q + 2] = v[4 + q].z;
+      m[4 * q + 3] = v[4 + q].w;
+    }
+    md5_compress(st, m);
+    wave_sync_lds();
+    if (step + 1 < steps) stage();
+  }
+  // RFC 1321 padding of a full chunk: 0x80, zeros, 64-bit bit length.
+  unsigned m[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) m[q] = 0;
+  m[0] = 0x80u;
+  const unsigned long long bits = static_cast<unsigned long long>(chunk_bytes) * 8ull;
+  m[14] = static_cast<unsigned>(bits);
+  m[15] = static_cast<unsigned>(bits >> 32);
+  md5_compress(st, m);
+  digests[group * kWaveChunks + lane] = u32x4{st[0], st[1], st[2], st[3]};
+}
+
 static unsigned long long n_chunks(size_t nbytes, uint32_t chunk_bytes) {
   return nbytes == 0 ? 1ull : (nbytes + chunk_bytes - 1) / chunk_bytes;
 }
@@ -190,10 +277,25 @@ void md5_chunks(const void* src, size_t nbytes, uint32_t chunk_bytes, void* dige
   if (reinterpret_cast<uintptr_t>(src) % 16)
     throw std::invalid_argument("md5_chunks: src must be 16-byte aligned");
   const unsigned long long nchunks = n_chunks(nbytes, chunk_bytes);
-  const unsigned grid = static_cast<unsigned>((nchunks + kMd5Block - 1) / kMd5Block);
+  // Whole groups of 64 full chunks take the coalesced kernel; the rest (and other chunk sizes)
+  // the one-lane-per-chunk kernel on the remaining bytes.
+  unsigned long long ngroups = 0;
+  if (chunk_bytes % 128 == 0) ngroups = (nbytes / chunk_bytes) / kWaveChunks;
+  if (ngroups) {
+    const unsigned waves_per_block = kMd5Block / 64;
+    const unsigned grid = static_cast<unsigned>((ngroups + waves_per_block - 1) / waves_per_block);
+    hipLaunchKernelGGL(md5_chunks_coalesced_kernel, dim3(grid), dim3(kMd5Block), 0, stream,
+                       static_cast<const unsigned char*>(src), chunk_bytes, ngroups, static_cast<u32x4*>(digests));
+    TK8S_HIP_CHECK(hipGetLastError());
+  }
+  const unsigned long long done = ngroups * kWaveChunks;
+  if (done >= nchunks && nbytes) return;
+  const size_t off = static_cast<size_t>(done) * chunk_bytes;
+  const unsigned long long rest = nchunks - done;
+  const unsigned grid = static_cast<unsigned>((rest + kMd5Block - 1) / kMd5Block);
   hipLaunchKernelGGL(md5_chunks_kernel, dim3(grid), dim3(kMd5Block), 0, stream,
-                     static_cast<const unsigned char*>(src), static_cast<unsigned long long>(nbytes),
-                     chunk_bytes, nchunks, static_cast<u32x4*>(digests));
+                     static_cast<const unsigned char*>(src) + off, static_cast<unsigned long long>(nbytes - off),
+                     chunk_bytes, rest, static_cast<u32x4*>(digests) + done);
   TK8S_HIP_CHECK(hipGetLastError());
 }
 
