@@ -300,3 +300,36 @@ def test_rerunning_the_playbook_is_idempotent(ws):
     assert (ws / "ansible" / "tmp" / "kubernetes_environment.id").read_text().strip() == s["project"]
     out = subprocess.run(["./kubectl", "get", "nodes", "-o", "json"], cwd=ws, env=_env(), capture_output=True, text=True)
     assert len(json.loads(out.stdout)["items"]) == 2
+
+
+def test_guestbook_loadbalancer_service(ws):
+    """docs/detailed.md acceptance demo: a Deployment behind a LoadBalancer Service, reached
+    through the external IP and through the ClusterIP, round-robin over both replicas."""
+    import urllib.request
+
+    _summary(_setup(ws, "--nodes", "2", "--rccl", "off"))
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=_env(), capture_output=True, text=True, timeout=60)
+    r = kc("apply", "-f", str(REPO / "manifests" / "examples" / "guestbook.yaml"))
+    assert r.returncode == 0, r.stderr
+    svc = json.loads(kc("get", "svc", "frontend", "-o", "json").stdout)
+    ext = svc["status"]["loadBalancer"]["ingress"][0]["ip"]
+    cip = svc["spec"]["clusterIP"]
+    assert cip.startswith("127.96.") and svc["spec"]["ports"][0]["nodePort"] >= 30000
+    assert "LoadBalancer" in kc("get", "svc").stdout
+    deadline = time.monotonic() + 30
+    seen = set()
+    while time.monotonic() < deadline and len(seen) < 2:
+        try:
+            body = urllib.request.urlopen(f"http://{ext}:8000/", timeout=5).read().decode()
+            seen.add(body.split()[2])
+        except OSError:
+            time.sleep(0.1)
+    assert len(seen) == 2, seen  # both replicas answered
+    assert urllib.request.urlopen(f"http://{cip}:8000/", timeout=5).read().decode().startswith("guestbook frontend")
+    pods = json.loads(kc("get", "pods", "-l", "app=guestbook", "-o", "json").stdout)["items"]
+    ips = {p["status"]["podIP"] for p in pods}
+    assert len(ips) == 2 and all(ip.startswith("127.1") for ip in ips)
+    assert kc("delete", "-f", str(REPO / "manifests" / "examples" / "guestbook.yaml")).returncode == 0
+    time.sleep(0.3)
+    with pytest.raises(OSError):
+        urllib.request.urlopen(f"http://{ext}:8000/", timeout=2).read()

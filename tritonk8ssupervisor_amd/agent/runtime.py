@@ -62,6 +62,7 @@ class PodProc:
     env: dict
     restart_policy: str
     gpu_ids: list[str] = field(default_factory=list)
+    ip: str = ""                  # the pod's own loopback IP (from the node's podCIDR)
     proc: subprocess.Popen | None = None
     restarts: int = 0
     started: float = 0.0

@@ -75,7 +75,7 @@ def fmt_nodes(items: list[dict], wide: bool) -> str:
 
 
 def fmt_pods(items: list[dict], wide: bool, all_ns: bool) -> str:
-    head = (["NAMESPACE"] if all_ns else []) + ["NAME", "READY", "STATUS", "RESTARTS", "AGE"] + (["NODE", "GPUS"] if wide else [])
+    head = (["NAMESPACE"] if all_ns else []) + ["NAME", "READY", "STATUS", "RESTARTS", "AGE"] + (["IP", "NODE", "GPUS"] if wide else [])
     rows = [head]
     for p in items:
         st = p.get("status", {})
@@ -86,7 +86,8 @@ def fmt_pods(items: list[dict], wide: bool, all_ns: bool) -> str:
         row = ([p["metadata"].get("namespace", "")] if all_ns else []) + [
             p["metadata"]["name"], "1/1" if phase == "Running" else "0/1", phase, str(cs.get("restartCount", 0)), _age(p)]
         if wide:
-            row += [p["spec"].get("nodeName") or "<none>", p["metadata"].get("annotations", {}).get("amd.com/gpu-ids", "")]
+            row += [st.get("podIP") or "<none>", p["spec"].get("nodeName") or "<none>",
+                    p["metadata"].get("annotations", {}).get("amd.com/gpu-ids", "")]
         rows.append(row)
     return _table(rows)
 
@@ -104,6 +105,18 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
     elif k == "deployment":
         rows = [["NAME", "READY", "AGE"]] + [[o["metadata"]["name"],
                 f"{o.get('status', {}).get('readyReplicas', 0)}/{o['spec'].get('replicas', 1)}", _age(o)] for o in items]
+    elif k == "service":
+        def ports(o):
+            return ",".join(f"{p['port']}" + (f":{p['nodePort']}" if p.get("nodePort") else "") + f"/{p.get('protocol', 'TCP')}"
+                            for p in o["spec"].get("ports", []))
+
+        def ext(o):
+            ing = o.get("status", {}).get("loadBalancer", {}).get("ingress") or []
+            return ",".join(i.get("ip", "") for i in ing) or ("<pending>" if o["spec"].get("type") == "LoadBalancer" else "<none>")
+
+        rows = [["NAME", "TYPE", "CLUSTER-IP", "EXTERNAL-IP", "PORT(S)", "AGE"]] + [[
+            o["metadata"]["name"], o["spec"].get("type", "ClusterIP"), o["spec"].get("clusterIP", ""), ext(o), ports(o), _age(o)]
+            for o in items]
     elif k == "event":
         rows = [["TYPE", "REASON", "OBJECT", "MESSAGE"]] + [[o.get("type", ""), o.get("reason", ""),
                 f"{o.get('involvedObject', {}).get('kind', '').lower()}/{o.get('involvedObject', {}).get('name', '')}",

@@ -113,6 +113,9 @@ class ControlPlane:
         self._seq = 0
         self._reconciling = False
         self._again = False
+        from .proxy import ServiceProxy
+
+        self.proxy = ServiceProxy(self._endpoints, log=lambda m: self._log_error(m + "\n"))
         self._routes()
 
     # ---- utilities --------------------------------------------------------------------
@@ -346,13 +349,15 @@ class ControlPlane:
         cap[GPU] = str(len(gpus))
         alloc = dict(cap)
         alloc[GPU] = str(healthy)
+        old = self.store.get("nodes", key)
+        cidr = (old or {}).get("spec", {}).get("podCIDR") or self._next_pod_cidr()
         node = {
             "kind": "Node", "apiVersion": "v1", "_project": pid,
             "metadata": {"name": name, "labels": {"kubernetes.io/hostname": name, "kubernetes.io/os": "linux",
                                                   **({"amd.com/gpu.family": "gfx950"} if gpus else {}),
                                                   **body.get("labels", {})},
                          "annotations": body.get("annotations", {})},
-            "spec": {"unschedulable": False},
+            "spec": {"unschedulable": False, "podCIDR": cidr},
             "status": {"capacity": cap, "allocatable": alloc, "devices": gpus,
                        "addresses": [{"type": "InternalIP", "address": body.get("ip", "")},
                                      {"type": "Hostname", "address": name}],
@@ -366,7 +371,7 @@ class ControlPlane:
         self.leases[key] = time.monotonic()
         self._event(pid, "default", {"kind": "Node", "name": name}, "RegisteredNode", f"Node {name} registered ({len(gpus)} GPU)")
         self.reconcile()
-        return Response(201, {"node": name, "nodeToken": ntok, "projectId": pid,
+        return Response(201, {"node": name, "nodeToken": ntok, "projectId": pid, "podCIDR": cidr,
                               "apiPrefix": f"/r/projects/{pid}/kubernetes",
                               "heartbeatSeconds": max(0.2, self.node_grace / 5)})
 
@@ -654,6 +659,8 @@ class ControlPlane:
             o = self.store.delete(kind, _key(p, ns, name))
             if o is None:
                 raise HttpError(404, f'{kind} "{name}" not found')
+            if kind == "services":
+                self._sync_proxy()
             if kind != "pods":
                 for pod in self.store.list("pods", lambda x: self._in(p, x) and any(
                         r.get("uid") == o["metadata"]["uid"] for r in x["metadata"].get("ownerReferences", []))):
@@ -661,6 +668,89 @@ class ControlPlane:
             self.reconcile()
             return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
         return h
+
+    # ---- networking: pod CIDRs, Service IPs / ports, endpoints --------------------------
+    def _next_pod_cidr(self) -> str:
+        """One /24 of 127.128.0.0/9 per registered node: pods bind their own loopback IP."""
+        used = {n.get("spec", {}).get("podCIDR") for n in self.store.list("nodes")}
+        for k in range(1 << 15):
+            c = f"127.{128 + (k >> 8)}.{k & 255}.0/24"
+            if c not in used:
+                return c
+        raise HttpError(507, "pod CIDR space exhausted")
+
+    def _alloc_service(self, body: dict) -> None:
+        spec = body.setdefault("spec", {})
+        stype = spec.setdefault("type", "ClusterIP")
+        if stype not in ("ClusterIP", "NodePort", "LoadBalancer"):
+            raise HttpError(422, f"service type {stype!r} is not supported")
+        ports = spec.get("ports") or []
+        if not ports:
+            raise HttpError(422, "spec.ports is required")
+        svcs = self.store.list("services")
+        used_ips = {o["spec"].get("clusterIP") for o in svcs}
+        used_np = {p.get("nodePort") for o in svcs for p in o["spec"].get("ports", [])}
+        used_lb = {(p.get("port")) for o in svcs if o["spec"].get("type") == "LoadBalancer" for p in o["spec"].get("ports", [])}
+        if not spec.get("clusterIP"):
+            spec["clusterIP"] = next(f"127.96.{k >> 8}.{k & 255}" for k in range(1, 1 << 16)
+                                     if f"127.96.{k >> 8}.{k & 255}" not in used_ips)
+        for i, port in enumerate(ports):
+            if "port" not in port:
+                raise HttpError(422, f"spec.ports[{i}].port is required")
+            port.setdefault("name", str(port["port"]))
+            port.setdefault("protocol", "TCP")
+            port.setdefault("targetPort", port["port"])
+            if stype in ("NodePort", "LoadBalancer") and not port.get("nodePort"):
+                port["nodePort"] = next(n for n in range(30000, 32768) if n not in used_np)
+                used_np.add(port["nodePort"])
+            if stype == "LoadBalancer" and port["port"] in used_lb:
+                raise HttpError(409, f"load balancer port {port['port']} is taken")
+        if stype == "LoadBalancer":
+            body["status"] = {"loadBalancer": {"ingress": [{"ip": self.advertise or self.host}]}}
+
+    def _endpoints(self, svc_key: str, port_key: str) -> list[tuple[str, int]]:
+        svc = self.store.get("services", svc_key)
+        if svc is None:
+            return []
+        pid, ns = svc["_project"], svc["metadata"]["namespace"]
+        sel = svc["spec"].get("selector") or {}
+        port = next((p for p in svc["spec"]["ports"] if p["name"] == port_key), None)
+        if port is None or not sel:
+            return []
+        out = []
+        for o in self.store.list("pods", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns):
+            if o.get("status", {}).get("phase") != "Running" or not labels_match(sel, o["metadata"].get("labels")):
+                continue
+            ip = o.get("status", {}).get("podIP")
+            tp = port["targetPort"]
+            if isinstance(tp, str):  # named container port
+                tp = next((cp.get("containerPort") for c in o["spec"].get("containers", [])
+                           for cp in c.get("ports", []) if cp.get("name") == tp), None)
+            if ip and tp:
+                out.append((ip, int(tp)))
+        return sorted(out)
+
+    def _proxy_wanted(self) -> dict:
+        wanted = {}
+        lb_host = self.advertise or self.host
+        for svc in self.store.list("services"):
+            key = _key(svc["_project"], svc["metadata"]["namespace"], svc["metadata"]["name"])
+            spec = svc["spec"]
+            for p in spec.get("ports", []):
+                wanted[(key, spec["clusterIP"], int(p["port"]))] = p["name"]
+                if spec.get("type") in ("NodePort", "LoadBalancer") and p.get("nodePort"):
+                    for h in {lb_host, "127.0.0.1"}:
+                        wanted[(key, h, int(p["nodePort"]))] = p["name"]
+                if spec.get("type") == "LoadBalancer":
+                    wanted[(key, lb_host, int(p["port"]))] = p["name"]
+        return wanted
+
+    def _sync_proxy(self) -> None:
+        try:
+            loop = asyncio.get_running_loop()
+        except RuntimeError:
+            return
+        loop.create_task(self.proxy.sync(self._proxy_wanted()))
 
     def create(self, pid: str, kind: str, ns: str, body: dict) -> dict:
         md = body.setdefault("metadata", {})
@@ -688,7 +778,11 @@ class ControlPlane:
             if not tmpl.get("spec", {}).get("containers"):
                 raise HttpError(422, "spec.template.spec.containers is required")
             body.setdefault("status", {})
+        elif kind == "services":
+            self._alloc_service(body)
         o = self.store.put(kind, key, body)
+        if kind == "services":
+            self._sync_proxy()
         self.reconcile()
         return o
 
@@ -991,6 +1085,8 @@ class ControlPlane:
         self._ensure_templates()
         host, port = await self.http.start(self.host, self.port)
         self.port = port
+        if self.store.keys("services"):
+            await self.proxy.sync(self._proxy_wanted())  # services restored from a snapshot
         tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop())]
         # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
         print(f"Listening on {host}:{port}", flush=True)
@@ -1005,6 +1101,7 @@ class ControlPlane:
         await self._stop.wait()
         for t in tasks:
             t.cancel()
+        await self.proxy.close()
         if self.state_dir:
             self.store.snapshot(self.state_dir / "controlplane.json")
         await self.http.close()
