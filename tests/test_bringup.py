@@ -227,7 +227,7 @@ def test_kubectl_workload_on_the_cluster(ws, tmp_path_factory):
     (d / "job.yaml").write_text(
         "apiVersion: batch/v1\nkind: Job\nmetadata:\n  name: hello\nspec:\n  completions: 2\n  parallelism: 2\n"
         "  completionMode: Indexed\n  template:\n    spec:\n      restartPolicy: Never\n      containers:\n"
-        "        - name: c\n          command: [\"sh\", \"-c\", \"echo rank=$JOB_COMPLETION_INDEX gpus=$HIP_VISIBLE_DEVICES\"]\n"
+        "        - name: c\n          command: [\"sh\", \"-c\", \"echo rank=$JOB_COMPLETION_INDEX gpus=$ROCR_VISIBLE_DEVICES\"]\n"
         "          resources:\n            limits:\n              amd.com/gpu: 1\n")
     kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=_env(), capture_output=True, text=True, timeout=60)
     r = kc("apply", "-f", str(d / "job.yaml"))

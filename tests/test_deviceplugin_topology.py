@@ -107,6 +107,7 @@ def test_discover_reads_kfd_sysfs(tmp_path, monkeypatch):
     monkeypatch.delenv("TK8S_FAKE_GPUS", raising=False)
     monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
     monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
     links = {(a, b): (11 if (a <= 2) == (b <= 2) else 2) for a in range(1, 5) for b in range(1, 5) if a != b}
     _fake_kfd(tmp_path, 4, links)
     inv = discover(tmp_path)
@@ -118,6 +119,9 @@ def test_discover_reads_kfd_sysfs(tmp_path, monkeypatch):
     inv = discover(tmp_path)
     assert inv.count == 2 and [g.kfd_node for g in inv.gpus] == [3, 4] and [g.ordinal for g in inv.gpus] == [0, 1]
     assert inv.links[0][1]["type"] == "xgmi"
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1,2,3")  # ROCr first: host 1,2,3; then HIP 2,3 -> host 3 only
+    inv = discover(tmp_path)
+    assert [g.kfd_node for g in inv.gpus] == [4]
 
 
 def test_discover_fake_and_empty(tmp_path, monkeypatch):
@@ -129,9 +133,17 @@ def test_discover_fake_and_empty(tmp_path, monkeypatch):
 
 
 def test_compose_visible_devices_nests_views():
-    assert compose_visible_devices([1, 3], {}) == {"HIP_VISIBLE_DEVICES": "1,3", "CUDA_VISIBLE_DEVICES": "1,3"}
-    # an agent that itself only sees physical GPUs 4-7 hands out physical ids
-    assert compose_visible_devices([0, 2], {"HIP_VISIBLE_DEVICES": "4,5,6,7"})["HIP_VISIBLE_DEVICES"] == "4,6"
+    # restriction at the ROCr level (the child initialises only its own GPUs), HIP = identity
+    assert compose_visible_devices([1, 3], {}) == {"ROCR_VISIBLE_DEVICES": "1,3", "HIP_VISIBLE_DEVICES": "0,1",
+                                                   "CUDA_VISIBLE_DEVICES": "0,1"}
+    # an agent that itself only sees host GPUs 4-7 (through HIP) hands out host indices
+    assert compose_visible_devices([0, 2], {"HIP_VISIBLE_DEVICES": "4,5,6,7"})["ROCR_VISIBLE_DEVICES"] == "4,6"
+    # ... and through ROCr then HIP: ROCR 2,3,5,7 -> HIP 1,3 -> host 3,7 -> ordinal 1 -> host 7
+    env = {"ROCR_VISIBLE_DEVICES": "2,3,5,7", "HIP_VISIBLE_DEVICES": "1,3"}
+    assert compose_visible_devices([1], env)["ROCR_VISIBLE_DEVICES"] == "7"
+    # nesting a child's own view again is stable
+    child = compose_visible_devices([1, 3], {})
+    assert compose_visible_devices([1], child)["ROCR_VISIBLE_DEVICES"] == "3"
 
 
 # ---- plugin ------------------------------------------------------------------------------
@@ -144,7 +156,8 @@ def test_plugin_list_allocate_and_probe_feedback(monkeypatch, native_build):
     assert [d["id"] for d in devs] == ["gpu2", "gpu3", "gpu9"]
     assert [d["health"] for d in devs] == ["Healthy", "Healthy", "Unhealthy"]  # gpu9 is not on the host
     a = p.allocate(["gpu3"])
-    assert a["env"]["HIP_VISIBLE_DEVICES"] == "3" and a["devices"][0] == "/dev/kfd"
+    assert a["env"]["ROCR_VISIBLE_DEVICES"] == "3" and a["env"]["HIP_VISIBLE_DEVICES"] == "0"
+    assert a["devices"][0] == "/dev/kfd"
     assert a["annotations"]["amd.com/gpu-ids"] == "gpu3"
     assert p.preferred(["gpu2", "gpu3"], [], 2) == ["gpu2", "gpu3"]
     assert p.preferred(["gpu2", "gpu3"], ["gpu3"], 1) == ["gpu3"]

@@ -3,7 +3,8 @@
 Reads the KFD topology in sysfs (``/sys/class/kfd/kfd/topology/nodes/*``): GPU nodes carry a
 non-zero ``gfx_target_version`` (90500 = gfx950) and ``io_links`` whose ``type`` 11 is xGMI.
 Only render nodes this process may open count (a container may see all GPUs in sysfs but be
-granted a subset), and ``HIP_VISIBLE_DEVICES``/``CUDA_VISIBLE_DEVICES`` are honoured.
+granted a subset), and ``ROCR_VISIBLE_DEVICES`` then ``HIP_VISIBLE_DEVICES``/``CUDA_VISIBLE_DEVICES``
+are honoured.
 ``TK8S_FAKE_GPUS=N`` replaces the inventory with N virtual fully-xGMI-connected gfx950 GPUs so
 the allocation logic runs on CPU-only hosts.
 
@@ -72,17 +73,25 @@ def _gfx_name(v: int) -> str:
     return f"gfx{major}{minor:x}{step:x}" if v else "cpu"
 
 
-def _visible_filter(n: int) -> list[int] | None:
-    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        val = os.environ.get(var)
-        if val is not None and val.strip() != "":
-            idx = []
-            for tok in val.split(","):
-                tok = tok.strip()
-                if tok.isdigit() and int(tok) < n:
-                    idx.append(int(tok))
-            return idx
-    return None
+def _idx_list(val: str | None) -> list[int] | None:
+    if val is None or val.strip() == "":
+        return None
+    return [int(t) for t in (x.strip() for x in val.split(",")) if t.isdigit()]
+
+
+def _visible_filter(n: int, environ=None) -> list[int] | None:
+    """Indices (into the host's KFD GPU order) this process may use: ROCR_VISIBLE_DEVICES picks
+    from the host's GPUs first, then HIP_/CUDA_VISIBLE_DEVICES from what ROCr left (the order
+    the ROCm runtime applies them in)."""
+    env = os.environ if environ is None else environ
+    view = list(range(n))
+    rocr = _idx_list(env.get("ROCR_VISIBLE_DEVICES"))
+    if rocr is not None:
+        view = [view[i] for i in rocr if i < len(view)]
+    hip = _idx_list(env.get("HIP_VISIBLE_DEVICES")) or _idx_list(env.get("CUDA_VISIBLE_DEVICES"))
+    if hip is not None:
+        view = [view[i] for i in hip if i < len(view)]
+    return None if rocr is None and hip is None else view
 
 
 def fake_inventory(n: int) -> HostInventory:
@@ -99,8 +108,8 @@ def discover(root: Path = KFD_ROOT, cache: bool = True) -> HostInventory:
     """Host inventory; memoised per process for the same root and visibility environment
     (provisioning asks once per machine, the playbook once per host: on an 8-GPU host each
     sysfs walk reads ~100 property files). The result is shared: treat it as read-only."""
-    key = (str(root), os.environ.get("TK8S_FAKE_GPUS"), os.environ.get("HIP_VISIBLE_DEVICES"),
-           os.environ.get("CUDA_VISIBLE_DEVICES"))
+    key = (str(root), os.environ.get("TK8S_FAKE_GPUS"), os.environ.get("ROCR_VISIBLE_DEVICES"),
+           os.environ.get("HIP_VISIBLE_DEVICES"), os.environ.get("CUDA_VISIBLE_DEVICES"))
     if cache and key in _CACHE:
         return _CACHE[key]
     inv = _discover(root)
@@ -161,16 +170,16 @@ def _discover(root: Path) -> HostInventory:
 
 
 def compose_visible_devices(ordinals: list[int], environ: dict | None = None) -> dict[str, str]:
-    """Env for a child that must see exactly ``ordinals`` of this process's visible GPUs."""
+    """Env for a child that must see exactly ``ordinals`` of this process's visible GPUs.
+
+    The restriction is applied at the ROCr level (``ROCR_VISIBLE_DEVICES`` = host GPU indices),
+    so the child's runtime only initialises its own GPUs -- on an 8-GPU node a HIP start that
+    brings up all eight agents in every pod and burn-in would multiply start-up cost. The HIP /
+    CUDA variables are reset to the identity over that list."""
     env = os.environ if environ is None else environ
-    out = {}
-    parent = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
-    if parent:
-        plist = [t.strip() for t in parent.split(",") if t.strip()]
-        phys = [plist[i] for i in ordinals if i < len(plist)]
-    else:
-        phys = [str(i) for i in ordinals]
-    val = ",".join(phys)
-    out["HIP_VISIBLE_DEVICES"] = val
-    out["CUDA_VISIBLE_DEVICES"] = val
-    return out
+    n_hint = max(ordinals, default=-1) + 1
+    view = _visible_filter(max(n_hint, 64), env)
+    phys = [(view[i] if view is not None else i) for i in ordinals if view is None or i < len(view)]
+    ident = ",".join(str(i) for i in range(len(phys)))
+    return {"ROCR_VISIBLE_DEVICES": ",".join(map(str, phys)), "HIP_VISIBLE_DEVICES": ident,
+            "CUDA_VISIBLE_DEVICES": ident}

@@ -78,7 +78,7 @@ def main():
         return 139  # the burn-in dies without a result; the validation pod must probe by itself
     if os.environ.get("TK8S_FAKE_PROBE_HANG", "") == node:
         time.sleep(3600)  # a wedged validation (the analogue of the reference's stuck dashboard)
-    n = len([x for x in os.environ.get("HIP_VISIBLE_DEVICES", "").split(",") if x])
+    n = len([x for x in (os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES", "")).split(",") if x])
     fail = os.environ.get("TK8S_FAKE_PROBE_FAIL", "") == node
     dev = {"ok": not fail, "hbm": {"ok": True, "gbps": 6200.0}, "md5": {"ok": True, "mbps": 2.3e6}}
     out = {"ok": not fail, "fake": True, "device_count": n, "probed": n, "devices": [dict(dev, device=i) for i in range(n)],

@@ -322,7 +322,7 @@ def m_tk8s_burnin(args, *, ctx, target, local, env, check, **_):
     command: the validation command (list); out: result file relative to the machine dir.
     Creates ``<out>.pending`` first (the validation pod's ``--reuse`` waits on it), then starts
     ``command --out <out>`` as a one-shot daemon (pidfile under run/, killed on teardown)
-    with HIP_VISIBLE_DEVICES = the machine's GPUs composed onto this process's view.
+    with ROCR_VISIBLE_DEVICES = the machine's GPUs composed onto this process's view.
     """
     ex = ctx.executor
     if ex is None or local:
@@ -380,7 +380,7 @@ def m_tk8s_gpu_facts(args, *, ctx, target, local, **_):
         facts["tk8s_machine_gpus"] = ctx.executor.machine_gpus(target.name)
     from .models.hostinfo import compose_visible_devices
 
-    facts["tk8s_machine_visible_devices"] = compose_visible_devices(facts["tk8s_machine_gpus"])["HIP_VISIBLE_DEVICES"]
+    facts["tk8s_machine_visible_devices"] = compose_visible_devices(facts["tk8s_machine_gpus"])["ROCR_VISIBLE_DEVICES"]
     from .ops import BIN
 
     facts["tk8s_native_built"] = all((BIN / t).exists() for t in ("tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl"))
