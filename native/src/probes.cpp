@@ -50,12 +50,6 @@ struct DeviceGuard {
   ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
 
-struct Stream {
-  hipStream_t s{};
-  Stream() { TK8S_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
-  ~Stream() { (void)hipStreamDestroy(s); }
-};
-
 // Per-device scratch arena for the local probes. The validation payload runs HBM, MD5 and copy
 // probes back to back; giving each its own hipMalloc/hipFree of 0.25-1 GiB cost ~70 ms per
 // device on MI355X (more than all the kernels together), so they share one allocation that
@@ -77,12 +71,38 @@ char* scratch(int device, size_t bytes) {
   return static_cast<char*>(slot.first);
 }
 
+// One non-blocking stream per device, created on first use and kept: a ROCm stream is backed
+// by a hardware queue, and creating one per probe (plus the legacy null stream for the copy's
+// source fill) cost milliseconds each on the validation's critical path.
+std::mutex g_stream_mu;
+std::map<int, hipStream_t> g_streams;
+
+hipStream_t probe_stream(int device) {
+  std::lock_guard<std::mutex> lock(g_stream_mu);
+  auto it = g_streams.find(device);
+  if (it != g_streams.end()) return it->second;
+  hipStream_t s{};
+  TK8S_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  g_streams[device] = s;
+  return s;
+}
+
+struct CachedStream {
+  hipStream_t s;
+  explicit CachedStream(int device) : s(probe_stream(device)) {}
+};
+
 constexpr size_t kAlign = 4096;
 size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 }  // namespace
 
 void release_probe_scratch() {
+  {
+    std::lock_guard<std::mutex> lock(g_stream_mu);
+    for (auto& kv : g_streams) (void)hipStreamDestroy(kv.second);
+    g_streams.clear();
+  }
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   for (auto& kv : g_scratch) {
     if (!kv.second.first) continue;
@@ -176,7 +196,7 @@ std::string hbm_write_probe(size_t bytes, int iters, StoreMode mode, int device,
     if (bytes % 16 || bytes == 0) return error_json("bytes must be a positive multiple of 16");
     iters = std::max(iters, 1);
     DeviceGuard g(device);
-    Stream st;
+    CachedStream st(device);
     char* base = scratch(device, align_up(bytes) + kAlign);
     void* buf = base;
     auto* bad = reinterpret_cast<unsigned long long*>(base + align_up(bytes));
@@ -218,7 +238,7 @@ std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int ite
     if (chunk_bytes == 0 || chunk_bytes % 64) return error_json("chunk must be a multiple of 64");
     iters = std::max(iters, 1);
     DeviceGuard g(device);
-    Stream st;
+    CachedStream st(device);
     const size_t ws = md5_tree_workspace(bytes, chunk_bytes);
     const size_t o_wa = align_up(std::max<size_t>(bytes, 16)), o_wb = o_wa + align_up(ws), o_out = o_wb + align_up(ws);
     char* base = scratch(device, o_out + kAlign);
@@ -288,8 +308,9 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters) 
     }
     {
       DeviceGuard g(src_device);
-      hbm_fill(src, bytes, 0xA5A5A5A5u, StoreMode::kPlain, nullptr);
-      TK8S_HIP_CHECK(hipStreamSynchronize(nullptr));
+      const hipStream_t ss = probe_stream(src_device);
+      hbm_fill(src, bytes, 0xA5A5A5A5u, StoreMode::kPlain, ss);
+      TK8S_HIP_CHECK(hipStreamSynchronize(ss));
     }
     DeviceGuard g(dst_device);
     if (peer) {
@@ -301,7 +322,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters) 
       dst = dst_own->get();
       bad = bad_own->as<unsigned long long>();
     }
-    Stream st;
+    CachedStream st(dst_device);
     stream_copy(dst, src, bytes, st.s);  // warm-up
     EventTimer kt, dt;
     kt.start(st.s);
