@@ -1,0 +1,9 @@
+set -euo pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/init_costs
+/opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 -o /tmp/init_costs native/bench/init_costs.hip
+for i in 1 2 3 4; do timeout -k 5 60 /tmp/init_costs; done > gpurun_out/init_costs/plain.jsonl
+for i in 1 2 3; do ROCR_VISIBLE_DEVICES=0 timeout -k 5 60 /tmp/init_costs; done > gpurun_out/init_costs/rocr0.jsonl
+for i in 1 2 3; do HSA_ENABLE_SDMA=0 timeout -k 5 60 /tmp/init_costs; done > gpurun_out/init_costs/nosdma.jsonl
+ls /dev/dri/ > gpurun_out/init_costs/dri.txt; ls /sys/class/kfd/kfd/topology/nodes | wc -l >> gpurun_out/init_costs/dri.txt
+nproc >> gpurun_out/init_costs/dri.txt

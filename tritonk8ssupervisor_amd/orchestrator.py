@@ -283,7 +283,7 @@ class Setup:
         rocmsetup's burn-in task then finds it running and does nothing."""
         if not (self.validate and m.gpus and hasattr(self.provider, "machine_env")):
             return
-        from .playbook_modules import start_burnin
+        from .burnin import start_burnin
 
         ex = MachineExecutor(self.provider, {m.name: m})
         r = start_burnin(ex, m.name, self._validation_command(), "run/gpu-burnin.json")

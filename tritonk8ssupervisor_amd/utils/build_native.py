@@ -191,7 +191,7 @@ def precompile_python() -> None:
     env["PYTHONPATH"] = os.pathsep.join([str(REPO)] + [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p])
     mods = ["tritonk8ssupervisor_amd.cli.main", "tritonk8ssupervisor_amd.cli.kubectl", "tritonk8ssupervisor_amd.orchestrator",
             "tritonk8ssupervisor_amd.playbook", "tritonk8ssupervisor_amd.playbook_modules", "tritonk8ssupervisor_amd.kube",
-            "tritonk8ssupervisor_amd.wizard", "tritonk8ssupervisor_amd.controlplane.server",
+            "tritonk8ssupervisor_amd.wizard", "tritonk8ssupervisor_amd.controlplane.server", "tritonk8ssupervisor_amd.burnin",
             "tritonk8ssupervisor_amd.agent.agent", "tritonk8ssupervisor_amd.ops.fakeprobe", "yaml", "argparse", "asyncio",
             "tritonk8ssupervisor_amd.controlplane.client", "tritonk8ssupervisor_amd.parallel.dist_allreduce"]
     code = "import importlib\nfor m in %r:\n    importlib.import_module(m)\n" % (mods[:-1] + ["tritonk8ssupervisor_amd.provision"],)
