@@ -174,16 +174,26 @@ __device__ __forceinline__ u32x4 philox4x32_10(unsigned long long idx, unsigned 
 
 __global__ __launch_bounds__(kBlock) void philox_fill_kernel(u32x4* __restrict__ dst, size_t n16,
                                                              unsigned k0, unsigned k1) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += stride)
-    dst[i] = philox4x32_10(i, k0, k1);
+  // Same slab walk as the HBM fill (block-contiguous, 4 stores in flight per lane); the 10
+  // Philox rounds per 16 B (~40 VALU ops) hide under the store stream.
+  size_t lo, hi;
+  slab_bounds(n16, &lo, &hi);
+  size_t i = lo + threadIdx.x;
+  for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = philox4x32_10(i + u * kBlock, k0, k1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dst[i + u * kBlock] = v[u];
+  }
+  for (; i < hi; i += kBlock) dst[i] = philox4x32_10(i, k0, k1);
 }
 
 void philox_fill(void* dst, size_t nbytes, uint64_t seed, hipStream_t stream) {
   if (nbytes % 16) throw std::invalid_argument("philox_fill: nbytes must be a multiple of 16");
   const size_t n16 = nbytes / 16;
   if (!n16) return;
-  hipLaunchKernelGGL(philox_fill_kernel, dim3(grid_for(n16)), dim3(kBlock), 0, stream,
+  hipLaunchKernelGGL(philox_fill_kernel, dim3(grid_for(n16 / 4, 16)), dim3(kBlock), 0, stream,
                      static_cast<u32x4*>(dst), n16, static_cast<unsigned>(seed),
                      static_cast<unsigned>(seed >> 32));
   TK8S_HIP_CHECK(hipGetLastError());
