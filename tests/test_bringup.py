@@ -105,6 +105,7 @@ def test_setup_ready_and_clean_teardown(ws, n):
         assert burn["ok"] and burn["probed"] == 1
     # teardown: machines gone, every artefact removed -- including the env-id file the
     # reference never cleans (setup.sh:513 removes ./tmp/* instead of ansible/tmp/*)
+    (ws / "ansible" / "tmp" / ".keep").touch()  # the repository's tracked placeholder
     r = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=_env(), capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "All clear!" in r.stdout
     for rel in ("config", "terraform/rancher.tf", "terraform/masters.ip", "terraform/hosts.ip", "terraform/terraform.tfstate",
@@ -112,6 +113,7 @@ def test_setup_ready_and_clean_teardown(ws, n):
                 "terraform/.terraform"):
         assert not (ws / rel).exists(), rel
     assert (ws / "ansible" / "ansible.cfg").read_text().count("private_key_file = \n") == 1
+    assert (ws / "ansible" / "tmp" / ".keep").exists()  # tracked placeholder survives the teardown
     deadline = time.monotonic() + 10
     while any(_alive(p) for p in pids) and time.monotonic() < deadline:
         time.sleep(0.05)
