@@ -39,7 +39,7 @@ import time
 from pathlib import Path
 
 from .httpserver import HttpError, HttpServer, Request, Response, Router
-from .store import Conflict, Store, now_iso
+from .store import Store, now_iso
 
 GPU = "amd.com/gpu"
 VALIDATION_LABEL = "tk8s.amd.com/validation"
