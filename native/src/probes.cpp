@@ -210,13 +210,19 @@ std::string hbm_write_probe(size_t bytes, int iters, StoreMode mode, int device,
     warm.stop(st.s);
     const float ms = warm.elapsed_ms() / iters;
     TK8S_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), st.s));
+    EventTimer rd;  // the verify pass is also the HBM read measurement (every word compared)
+    rd.start(st.s);
     verify_fill(buf, bytes, value, bad, st.s);
+    rd.stop(st.s);
+    const float read_ms = rd.elapsed_ms();
     unsigned long long nbad = 0;
     TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad, sizeof nbad, hipMemcpyDeviceToHost, st.s));
     TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
     return Json()
         .kv("ok", nbad == 0)
         .kv("probe", "hbm_write")
+        .kv("read_ms", static_cast<double>(read_ms))
+        .kv("read_gbps", bytes / (read_ms * 1e-3) / 1e9)
         .kv("device", device)
         .kv("bytes", static_cast<uint64_t>(bytes))
         .kv("iters", iters)
