@@ -916,7 +916,8 @@ class ControlPlane:
                     _set_cond(node, "AMDGPUValidated", want[0], want[1],
                               pod.get("status", {}).get("message", "")[:500])
                     ann = node["metadata"].setdefault("annotations", {})
-                    for k, path in (("hbm-write-gbps", ("hbm", "gbps")), ("md5-mbps", ("md5", "mbps")),
+                    for k, path in (("hbm-write-gbps", ("hbm", "gbps")), ("hbm-read-gbps", ("hbm", "read_gbps")),
+                                    ("md5-mbps", ("md5", "mbps")),
                                     ("copy-gbps", ("copy", "kernel_gbps")), ("probe-ms", ("timings_ms", "total")),
                                     ("hip-init-ms", ("timings_ms", "hip_init"))):
                         v = result.get(path[0], {}).get(path[1]) if isinstance(result.get(path[0]), dict) else None
