@@ -242,8 +242,9 @@ __device__ __forceinline__ unsigned short f32_to_bf16_bits(float f) {
 template <class T>
 __global__ __launch_bounds__(kBlock) void ar_fill_kernel(T* __restrict__ buf, size_t count,
                                                          float base) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
+  size_t lo, hi;
+  slab_bounds(count, &lo, &hi);
+  for (size_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     const float v = base + static_cast<float>(i % 7);
     if constexpr (sizeof(T) == 4) buf[i] = v;
     else buf[i] = f32_to_bf16_bits(v);
@@ -268,10 +269,11 @@ __global__ __launch_bounds__(kBlock) void ar_check_kernel(const T* __restrict__ 
                                                           float base, float per_mod, float tol,
                                                           unsigned* max_err_bits,
                                                           unsigned long long* bad_count) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+  size_t lo, hi;
+  slab_bounds(count, &lo, &hi);
   float emax = 0.f;
   unsigned long long bad = 0;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < count; i += stride) {
+  for (size_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     float v;
     if constexpr (sizeof(T) == 4) v = buf[i];
     else v = bf16_bits_to_f32(buf[i]);
