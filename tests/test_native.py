@@ -22,6 +22,19 @@ def test_build_produces_gfx950_code_objects(native_build):
     assert b"gfx942" not in lib and b"gfx90a" not in lib
 
 
+def _needed(path) -> list[str]:
+    out = subprocess.run(["readelf", "-d", str(path)], capture_output=True, text=True, check=True).stdout
+    return [line.split("[", 1)[1].split("]", 1)[0] for line in out.splitlines() if "(NEEDED)" in line]
+
+
+def test_only_rccl_artefacts_link_librccl(native_build):
+    # librccl is ~0.5 GB: the probe and gpuinfo payloads on the bring-up critical path must not map it
+    for name in ("libtk8s", "tk8s-probe", "tk8s-gpuinfo"):
+        assert not any(n.startswith("librccl") for n in _needed(native_build[name])), name
+    for name in ("libtk8s_rccl", "tk8s-rccl", "native_module"):
+        assert any(n.startswith("librccl") for n in _needed(native_build[name])), name
+
+
 def test_build_is_incremental(native_build):
     from tritonk8ssupervisor_amd.utils.build_native import build
 

@@ -2,9 +2,12 @@
 
 Outputs (all in-tree so they travel to the GPU box with the repo snapshot):
 
-* ``tritonk8ssupervisor_amd/lib/libtk8s.so`` — HIP kernels (N4-N7), probes (N1) and the RCCL
-  validator (N3); links ``libamdhip64`` and ``librccl``.
-* ``tritonk8ssupervisor_amd/_tk8s_native*.so`` — pybind11 module over ``libtk8s.so``.
+* ``tritonk8ssupervisor_amd/lib/libtk8s.so`` — HIP kernels (N4-N7) and probes (N1); links only
+  ``libamdhip64``.
+* ``tritonk8ssupervisor_amd/lib/libtk8s_rccl.so`` — the RCCL validator (N3); the only artefact
+  that links ``librccl`` (573 MB on ROCm 7.2), so the probe and gpuinfo payloads on the
+  bring-up's critical path never map it.
+* ``tritonk8ssupervisor_amd/_tk8s_native*.so`` — pybind11 module over both libraries.
 * ``tritonk8ssupervisor_amd/_tk8s_topo*.so`` — pybind11 module of the CPU-only xGMI-aware
   allocator (N2 core); no HIP dependency so the node agent can load it safely.
 * ``tritonk8ssupervisor_amd/bin/tk8s-{gpuinfo,probe,rccl}`` — the validation pod payloads.
@@ -41,8 +44,10 @@ LIB_SOURCES = [
     "src/stream_kernels.hip",
     "src/md5_kernels.hip",
     "src/probes.cpp",
-    "src/rccl_bench.cpp",
 ]
+RCCL_SOURCES = ["src/rccl_bench.cpp"]
+# tools that need RCCL; every other tool links libtk8s.so only
+RCCL_TOOLS = {"tk8s-rccl"}
 TOOLS = {
     "tk8s-gpuinfo": "tools/tk8s_gpuinfo.cpp",
     "tk8s-probe": "tools/tk8s_probe.cpp",
@@ -64,6 +69,15 @@ def topo_module_path() -> Path:
 
 def lib_path() -> Path:
     return LIBDIR / "libtk8s.so"
+
+
+def rccl_lib_path() -> Path:
+    return LIBDIR / "libtk8s_rccl.so"
+
+
+def _obj(rel: str) -> Path:
+    src = Path(rel)
+    return OBJ / (src.stem + src.suffix.replace(".", "_") + ".o")
 
 
 def tool_path(name: str) -> Path:
@@ -104,9 +118,9 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
     # 1. objects of libtk8s.so (hipcc, gfx950 device code)
     objs: list[tuple[Path, list[str]]] = []
-    for rel in LIB_SOURCES:
+    for rel in LIB_SOURCES + RCCL_SOURCES:
         src = NATIVE / rel
-        obj = OBJ / (src.stem + src.suffix.replace(".", "_") + ".o")
+        obj = _obj(rel)
         if force or _stale(obj, [src]):
             objs.append((obj, [HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)]))
     # tool objects and module objects compile in the same pool
@@ -131,26 +145,34 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda oc: _run(oc[1], verbose), objs))
 
-    lib_objs = [OBJ / (Path(r).stem + Path(r).suffix.replace(".", "_") + ".o") for r in LIB_SOURCES]
-    hip_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"]
+    lib_objs = [_obj(r) for r in LIB_SOURCES]
+    rccl_objs = [_obj(r) for r in RCCL_SOURCES]
+    hip_libs = [f"-L{ROCM / 'lib'}", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}"]
     lib = lib_path()
     if force or _stale(lib, lib_objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *[str(o) for o in lib_objs],
               "-o", str(lib), *hip_libs], verbose)
+    rlib = rccl_lib_path()
+    if force or _stale(rlib, rccl_objs + [lib]):
+        _run([HIPCC, "-shared", "-fPIC", *[str(o) for o in rccl_objs], "-o", str(rlib),
+              f"-L{LIBDIR}", "-ltk8s", "-Wl,-rpath,$ORIGIN", *hip_libs, "-lrccl"], verbose)
 
     links = []
     nat = native_module_path()
-    if force or _stale(nat, [nat_obj, lib]):
-        links.append([HIPCC, "-shared", "-fPIC", str(nat_obj), "-o", str(nat), f"-L{LIBDIR}", "-ltk8s",
-                      "-Wl,-rpath,$ORIGIN/lib", *hip_libs])
+    if force or _stale(nat, [nat_obj, lib, rlib]):
+        links.append([HIPCC, "-shared", "-fPIC", str(nat_obj), "-o", str(nat), f"-L{LIBDIR}",
+                      "-ltk8s_rccl", "-ltk8s", "-Wl,-rpath,$ORIGIN/lib", *hip_libs, "-lrccl"])
     topo = topo_module_path()
     if force or _stale(topo, topo_objs):
         links.append([CXX, "-shared", "-fPIC", *[str(o) for o in topo_objs], "-o", str(topo)])
     for name, obj in tool_objs.items():
         out = tool_path(name)
-        if force or _stale(out, [obj, lib]):
-            links.append([HIPCC, str(obj), "-o", str(out), f"-L{LIBDIR}", "-ltk8s",
-                          "-Wl,-rpath,$ORIGIN/../lib", *hip_libs, "-lpthread"])
+        rccl = ["-ltk8s_rccl"] if name in RCCL_TOOLS else []
+        deps = [obj, lib] + ([rlib] if rccl else [])
+        if force or _stale(out, deps):
+            links.append([HIPCC, str(obj), "-o", str(out), f"-L{LIBDIR}", *rccl, "-ltk8s",
+                          "-Wl,-rpath,$ORIGIN/../lib", *hip_libs, *(["-lrccl"] if rccl else []),
+                          "-lpthread"])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), links))
 
@@ -160,7 +182,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         _run([CXX, "-O2", "-std=c++17", "-Wall", str(sup_src), "-o", str(sup)], verbose)
 
     precompile_python()
-    out = {"libtk8s": lib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup}
+    out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup}
     out.update({n: tool_path(n) for n in TOOLS})
     return out
 
