@@ -195,16 +195,31 @@ std::string hbm_write_probe(size_t bytes, int iters, StoreMode mode, int device,
   try {
     if (bytes % 16 || bytes == 0) return error_json("bytes must be a positive multiple of 16");
     iters = std::max(iters, 1);
+    // Host-side costs of the first probe on a device (stream = a hardware queue, the arena
+    // allocation, event creation, the first launch = code-object load): they, not the kernels,
+    // dominate a cold validation run, so they are reported separately.
+    const auto h0 = std::chrono::steady_clock::now();
+    auto lap = [last = h0]() mutable {
+      const auto now = std::chrono::steady_clock::now();
+      const double ms = std::chrono::duration<double, std::milli>(now - last).count();
+      last = now;
+      return ms;
+    };
     DeviceGuard g(device);
     CachedStream st(device);
+    const double stream_ms = lap();
     char* base = scratch(device, align_up(bytes) + kAlign);
     void* buf = base;
     auto* bad = reinterpret_cast<unsigned long long*>(base + align_up(bytes));
+    const double alloc_ms = lap();
     EventTimer cold, warm;
+    const double events_ms = lap();
     cold.start(st.s);
     hbm_fill(buf, bytes, value ^ 0xFFFFFFFFu, mode, st.s);  // cold write (first touch)
     cold.stop(st.s);
+    const double launch_ms = lap();
     const float cold_ms = cold.elapsed_ms();
+    const double cold_wait_ms = lap();
     warm.start(st.s);
     for (int i = 0; i < iters; ++i) hbm_fill(buf, bytes, value, mode, st.s);
     warm.stop(st.s);
@@ -232,6 +247,13 @@ std::string hbm_write_probe(size_t bytes, int iters, StoreMode mode, int device,
         .kv("seconds", ms * 1e-3)
         .kv("gbps", bytes / (ms * 1e-3) / 1e9)
         .kv("bad_words", static_cast<uint64_t>(nbad))
+        .raw("host_ms", Json()
+                            .kv("stream", stream_ms)
+                            .kv("alloc", alloc_ms)
+                            .kv("events", events_ms)
+                            .kv("first_launch", launch_ms)
+                            .kv("first_wait", cold_wait_ms)
+                            .str())
         .str();
   } catch (const std::exception& ex) {
     return error_json(ex.what());
