@@ -11,7 +11,35 @@ static double ms(clk::time_point a, clk::time_point b) { return std::chrono::dur
 
 __global__ void touch(unsigned* p) { p[threadIdx.x] = threadIdx.x; }
 
-int main() {
+// `init_costs null`: first launch on the legacy null stream, before any stream is created —
+// does the runtime's own queue come for free, or does it cost what a created stream costs?
+static int null_first() {
+  auto t0 = clk::now();
+  int n = 0;
+  (void)hipGetDeviceCount(&n);
+  auto t1 = clk::now();
+  (void)hipSetDevice(0);
+  auto t2 = clk::now();
+  void* a = nullptr;
+  (void)hipMalloc(&a, 1ull << 30);
+  auto t3 = clk::now();
+  hipLaunchKernelGGL(touch, dim3(1), dim3(64), 0, nullptr, static_cast<unsigned*>(a));
+  (void)hipStreamSynchronize(nullptr);
+  auto t4 = clk::now();
+  hipStream_t s;
+  (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  auto t5 = clk::now();
+  hipLaunchKernelGGL(touch, dim3(1), dim3(64), 0, s, static_cast<unsigned*>(a));
+  (void)hipStreamSynchronize(s);
+  auto t6 = clk::now();
+  std::printf("{\"mode\": \"null\", \"get_device_count_ms\": %.3f, \"set_device_ms\": %.3f, \"malloc_1g_ms\": %.3f, "
+              "\"null_first_launch_ms\": %.3f, \"stream_after_null_ms\": %.3f, \"stream_launch_ms\": %.3f, \"total_ms\": %.3f}\n",
+              ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5), ms(t5, t6), ms(t0, t6));
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && argv[1][0] == 'n') return null_first();
   auto t0 = clk::now();
   int n = 0;
   (void)hipGetDeviceCount(&n);

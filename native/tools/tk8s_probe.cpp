@@ -218,6 +218,11 @@ int main(int argc, char** argv) {
     if (!info.empty()) out.raw("gpuinfo", info);
     out.raw("timings_ms", tk8s::Json().kv("hip_init", init_ms).kv("gpuinfo", gpuinfo_ms).kv("total", ms_since(t0)).str());
     emit(out.str(), out_file);
+    if (a.has("release-after")) {  // free the arena + streams before exit (experiment knob)
+      const auto tr = std::chrono::steady_clock::now();
+      tk8s::release_probe_scratch();
+      std::fprintf(stderr, "{\"release_ms\": %.3f}\n", ms_since(tr));
+    }
     return ok ? 0 : 1;
   } catch (const std::exception& e) {
     emit(std::string("{\"ok\":false,\"error\":\"") + e.what() + "\"}", out_file);
