@@ -1,4 +1,5 @@
-// Shared helpers for the tk8s native layer (HIP runtime error handling, tiny JSON writer).
+// Shared helpers for the tk8s native layer (HIP runtime error handling, RAII buffers/timers;
+// the JSON writer lives in tk8s/json.h so HIP-free code can use it).
 //
 // The reference (cheapRoc/tritonK8ssupervisor) has no native code at all;
 // every native component here is new and exists to validate MI355X workers during bring-up.
@@ -12,6 +13,8 @@
 #include <vector>
 
 #include <hip/hip_runtime.h>
+
+#include "tk8s/json.h"
 
 namespace tk8s {
 
@@ -75,62 +78,6 @@ class EventTimer {
 
  private:
   hipEvent_t start_{}, stop_{};
-};
-
-// Minimal JSON object writer: enough for flat records and arrays of records.
-class Json {
- public:
-  Json& kv(const std::string& k, const std::string& v) { key(k); str(v); return *this; }
-  Json& kv(const std::string& k, const char* v) { return kv(k, std::string(v)); }
-  Json& kv(const std::string& k, double v) { key(k); num(v); return *this; }
-  Json& kv(const std::string& k, int64_t v) { key(k); os_ << v; return *this; }
-  Json& kv(const std::string& k, uint64_t v) { key(k); os_ << v; return *this; }
-  Json& kv(const std::string& k, int v) { return kv(k, static_cast<int64_t>(v)); }
-  Json& kv(const std::string& k, unsigned v) { return kv(k, static_cast<uint64_t>(v)); }
-  Json& kv(const std::string& k, bool v) { key(k); os_ << (v ? "true" : "false"); return *this; }
-  Json& raw(const std::string& k, const std::string& json) { key(k); os_ << json; return *this; }
-  std::string str() const { return "{" + os_.str() + "}"; }
-
-  static std::string escape(const std::string& s) {
-    std::string o = "\"";
-    for (char c : s) {
-      switch (c) {
-        case '"': o += "\\\""; break;
-        case '\\': o += "\\\\"; break;
-        case '\n': o += "\\n"; break;
-        case '\t': o += "\\t"; break;
-        default:
-          if (static_cast<unsigned char>(c) < 0x20) {
-            char buf[8];
-            std::snprintf(buf, sizeof buf, "\\u%04x", c);
-            o += buf;
-          } else {
-            o += c;
-          }
-      }
-    }
-    return o + "\"";
-  }
-  static std::string array(const std::vector<std::string>& items) {
-    std::string o = "[";
-    for (size_t i = 0; i < items.size(); ++i) o += (i ? "," : "") + items[i];
-    return o + "]";
-  }
-
- private:
-  void key(const std::string& k) {
-    if (!first_) os_ << ",";
-    first_ = false;
-    os_ << escape(k) << ":";
-  }
-  void str(const std::string& v) { os_ << escape(v); }
-  void num(double v) {
-    char buf[64];
-    std::snprintf(buf, sizeof buf, "%.9g", v);
-    os_ << buf;
-  }
-  std::ostringstream os_;
-  bool first_ = true;
 };
 
 }  // namespace tk8s

@@ -335,3 +335,40 @@ def test_guestbook_loadbalancer_service(ws):
     time.sleep(0.3)
     with pytest.raises(OSError):
         urllib.request.urlopen(f"http://{ext}:8000/", timeout=2).read()
+
+
+def test_ecc_errors_take_a_gpu_out_of_allocatable(ws, tmp_path_factory):
+    """AMD SMI health (tk8s-smi; here its fake twin): a GPU reporting uncorrectable ECC errors
+    goes Unhealthy and leaves allocatable; it comes back when the errors clear."""
+    faults = tmp_path_factory.mktemp("smi") / "ue"
+    faults.write_text("")
+    env = _env(TK8S_SMI_DELAY="0.05", TK8S_SMI_INTERVAL="0.1", TK8S_FAKE_SMI_FILE=faults)
+    s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=env))
+    assert s["gpus_allocatable"] == 2
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
+
+    def node(name):
+        return json.loads(kc("get", "node", name, "-o", "json").stdout)
+
+    def wait_for(pred, what):
+        deadline = time.monotonic() + 15
+        while time.monotonic() < deadline:
+            n = node("kubenode2")
+            if pred(n):
+                return n
+            time.sleep(0.05)
+        raise AssertionError(f"timed out waiting for {what}: {json.dumps(n)[:2000]}")
+
+    n = wait_for(lambda n: n["metadata"].get("annotations", {}).get("amd.com/gpu-health-source") == "amdsmi",
+                 "first AMD SMI sample")
+    gpu = n["status"]["devices"][0]
+    host_ordinal = gpu["ordinal"]
+    assert gpu["health"] == "Healthy" and "telemetry" in gpu and gpu["pciBusId"]
+    faults.write_text(f"{host_ordinal}:2")
+    n = wait_for(lambda n: n["status"]["allocatable"].get("amd.com/gpu") == "0", "ECC -> Unhealthy")
+    assert n["status"]["devices"][0]["health"] == "Unhealthy"
+    assert n["status"]["devices"][0]["reason"].startswith("ECC: 2 uncorrectable")
+    assert node("kubenode1")["status"]["allocatable"]["amd.com/gpu"] == "1"  # the other GPU is untouched
+    assert "ECC: 2 uncorrectable" in kc("describe", "node", "kubenode2").stdout
+    faults.write_text("")
+    wait_for(lambda n: n["status"]["allocatable"].get("amd.com/gpu") == "1", "errors cleared -> Healthy")

@@ -166,3 +166,34 @@ def test_plugin_list_allocate_and_probe_feedback(monkeypatch, native_build):
     assert p.devices()[0]["pciBusId"] == "0000:23:00.0"
     p.update_from_probe({"ok": False, "_allocated_ids": ["gpu3"]})
     assert p.devices()[1]["health"] == "Unhealthy" and p.devices()[1]["reason"] == "probe failed"
+
+
+def test_smi_health_marks_ecc_devices_unhealthy_by_pci_id(monkeypatch):
+    monkeypatch.setenv("TK8S_FAKE_GPUS", "4")
+    from tritonk8ssupervisor_amd.agent.deviceplugin import DevicePlugin
+    from tritonk8ssupervisor_amd.models.hostinfo import fake_inventory
+    from tritonk8ssupervisor_amd.ops import fakesmi
+
+    plugin = DevicePlugin([2, 3], inventory=fake_inventory(4))
+    assert [d["pciBusId"] for d in plugin.devices()] == ["0000:12:00.0", "0000:13:00.0"]
+    monkeypatch.setenv("TK8S_FAKE_SMI_UE", "3:5,0:1")  # host GPU 0 is not this node's: ignored
+    assert plugin.update_from_smi(fakesmi.report(4)) is True
+    health = {d["id"]: (d["health"], d["reason"]) for d in plugin.devices()}
+    assert health == {"gpu2": ("Healthy", ""), "gpu3": ("Unhealthy", "ECC: 5 uncorrectable, 0 deferred")}
+    ann = plugin.telemetry_annotations()
+    assert ann["amd.com/gpu-ecc-uncorrectable"] == "5" and ann["amd.com/gpu-temp-hotspot-max-c"] == "43"
+    assert plugin.update_from_smi(fakesmi.report(4)) is False  # same sample: no change
+    monkeypatch.setenv("TK8S_FAKE_SMI_UE", "")
+    assert plugin.update_from_smi(fakesmi.report(4)) is True
+    assert all(d["health"] == "Healthy" for d in plugin.devices())
+    # a failed validation probe is sticky: SMI health never overrides it
+    plugin.update_from_probe({"ok": False, "_allocated_ids": ["gpu2"]})
+    assert plugin.update_from_smi(fakesmi.report(4)) is False
+    assert plugin.devices()[0]["reason"] == "probe failed"
+    assert plugin.update_from_smi({"ok": False, "error": "AMD SMI found no GPU"}) is False
+
+
+def test_pci_bus_id_from_kfd_location():
+    from tritonk8ssupervisor_amd.models.hostinfo import HostGpu
+
+    assert HostGpu(ordinal=0, location_id=(0xa4 << 8) | (1 << 3) | 2, domain=1).pci_bus_id == "0001:a4:01.2"

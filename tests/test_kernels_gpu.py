@@ -173,6 +173,27 @@ def test_probe_cli_out_and_reuse(nat, tmp_path):
     assert rc2 == 0 and again == out  # the pod reports the burn-in's result verbatim
 
 
+def test_smi_health_matches_kfd_and_hip_views(nat):
+    """tk8s-smi (AMD SMI, no HIP) sees the GPU HIP sees, under the same PCI bus id the agent's
+    KFD sysfs discovery computes — the join key of device health."""
+    import subprocess
+
+    from tritonk8ssupervisor_amd.models.hostinfo import discover
+    from tritonk8ssupervisor_amd.ops import tool
+
+    r = subprocess.run([str(tool("tk8s-smi"))], capture_output=True, text=True, timeout=60)
+    out = json.loads(r.stdout)
+    assert out["ok"] and out["gpu_count"] >= 1, out
+    assert r.returncode in (0, 1)
+    smi_ids = {g["pci_bus_id"].lower() for g in out["gpus"]}
+    kfd_ids = {g.pci_bus_id.lower() for g in discover(cache=False).gpus}
+    assert kfd_ids and kfd_ids <= smi_ids, (kfd_ids, smi_ids)
+    hip_ids = {d["pci_bus_id"].lower() for d in json.loads(nat.gpuinfo_json(False))["devices"]}
+    assert hip_ids <= smi_ids, (hip_ids, smi_ids)
+    g = out["gpus"][0]
+    assert g["vram_total_bytes"] > 250 * 2**30 and "ecc" in g and "hotspot" in g["temp_c"]
+
+
 def test_setup_on_a_real_gpu(tmp_path):
     """./setup.sh with one MI355X worker: the real tk8s-probe validates the GPU before Ready."""
     import os
@@ -190,7 +211,7 @@ def test_setup_on_a_real_gpu(tmp_path):
     for f in ("setup.sh", "tk8s", "kubectl"):
         shutil.copy2(repo / f, tmp_path / f)
     env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
-    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable)
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, TK8S_SMI_DELAY="0.1", TK8S_SMI_INTERVAL="1")
     try:
         r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120"],
                            cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
@@ -202,6 +223,20 @@ def test_setup_on_a_real_gpu(tmp_path):
         node = json.loads(k.stdout)
         assert float(node["metadata"]["annotations"]["tk8s.amd.com/hbm-write-gbps"]) > 3000
         assert node["status"]["devices"][0]["gfx"] == "gfx950"
+        # the agent's AMD SMI health sample reaches the node (device joined by PCI bus id)
+        import time
+
+        deadline = time.monotonic() + 20
+        while time.monotonic() < deadline:
+            node = json.loads(subprocess.run(["./kubectl", "get", "node", "kubenode1", "-o", "json"], cwd=tmp_path,
+                                             env=env, capture_output=True, text=True, timeout=60).stdout)
+            if "telemetry" in node["status"]["devices"][0]:
+                break
+            time.sleep(0.2)
+        dev = node["status"]["devices"][0]
+        assert "telemetry" in dev, node
+        assert dev["health"] == "Healthy" and dev["telemetry"]["ecc"]["uncorrectable"] == 0
+        assert node["metadata"]["annotations"]["amd.com/gpu-health-source"] == "amdsmi"
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 

@@ -15,7 +15,8 @@ BIN = Path(__file__).resolve().parents[1] / "tritonk8ssupervisor_amd" / "bin"
 
 
 def test_build_produces_gfx950_code_objects(native_build):
-    for name in ("libtk8s", "native_module", "topo_module", "tk8s-supervise", "tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl"):
+    for name in ("libtk8s", "libtk8s_rccl", "native_module", "topo_module", "tk8s-supervise", "tk8s-smi",
+                 "tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl"):
         assert Path(native_build[name]).exists(), name
     lib = Path(native_build["libtk8s"]).read_bytes()
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in lib  # device code is built for MI355X only
@@ -33,6 +34,19 @@ def test_only_rccl_artefacts_link_librccl(native_build):
         assert not any(n.startswith("librccl") for n in _needed(native_build[name])), name
     for name in ("libtk8s_rccl", "tk8s-rccl", "native_module"):
         assert any(n.startswith("librccl") for n in _needed(native_build[name])), name
+
+
+def test_smi_tool_is_hip_free_and_fails_loudly_without_a_gpu(native_build):
+    smi = native_build["tk8s-smi"]
+    needed = _needed(smi)
+    assert any(n.startswith("libamd_smi") for n in needed)
+    assert not any(n.startswith(("libamdhip64", "librccl", "libhsa")) for n in needed)  # agent-safe: no KFD process
+    if Path("/dev/kfd").exists():
+        pytest.skip("a GPU host: covered by the GPU suite")
+    r = subprocess.run([str(smi), "--no-links"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3
+    out = json.loads(r.stdout)
+    assert out["ok"] is False and out["error"]
 
 
 def test_build_is_incremental(native_build):

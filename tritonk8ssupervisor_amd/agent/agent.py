@@ -18,7 +18,9 @@ stops heartbeats (lease expiry -> NotReady).
 from __future__ import annotations
 
 import argparse
+import json
 import os
+import subprocess
 import sys
 import threading
 import time
@@ -45,7 +47,8 @@ def pod_gpus(p: dict) -> int:
 
 class Agent:
     def __init__(self, url: str | None, name: str, ip: str, sandbox: str, gpus: list[int],
-                 labels: dict | None = None, tool_dirs: list[str] | None = None, timeout: float = 60.0):
+                 labels: dict | None = None, tool_dirs: list[str] | None = None, timeout: float = 60.0,
+                 smi_interval: float = 30.0, smi_delay: float = 5.0):
         self.reg_url = url
         self.name = name
         self.ip = ip
@@ -61,6 +64,9 @@ class Agent:
         self._pods_meta: dict[str, dict] = {}
         self.pod_cidr = ""
         self._pod_ips: dict[str, str] = {}   # pod key -> IP
+        self.smi_interval = smi_interval     # AMD SMI health period (0: off)
+        self.smi_delay = smi_delay           # first sample after join, off the bring-up path
+        self._annotations: dict[str, str] = {}
         if url:
             self.set_url(url)
 
@@ -145,6 +151,8 @@ class Agent:
                 if self._devices_dirty:
                     self._devices_dirty = False
                     body["devices"] = self.plugin.devices()
+                if self._annotations:
+                    body["annotations"], self._annotations = self._annotations, {}
                 try:
                     api.put(api.k8s(f"/api/v1/nodes/{self.name}/status"), body)
                 except ApiError as e:
@@ -154,6 +162,27 @@ class Agent:
                 except OSError:
                     pass
             self.stop.wait(self.hb_period)
+
+    # ---- GPU health (AMD SMI) ------------------------------------------------------------
+    def smi_loop(self) -> None:
+        """Sample AMD SMI every ``smi_interval`` s through ``tk8s-smi`` (a separate process: the
+        agent stays GPU-clean and a driver hiccup cannot take it down). A device with
+        uncorrectable/deferred ECC errors goes Unhealthy -> leaves ``allocatable``."""
+        if self.smi_interval <= 0 or not self.plugin.devices_:
+            return
+        if self.stop.wait(self.smi_delay):
+            return
+        while True:
+            res = read_smi()
+            if res is not None:
+                changed = self.plugin.update_from_smi(res)
+                self._devices_dirty = True  # telemetry rides along with the device list
+                if changed:
+                    bad = [d.id for d in self.plugin.devices_ if d.reason.startswith("ECC:")]
+                    print(f"{self.name}: AMD SMI health changed; unhealthy: {bad or 'none'}", flush=True)
+                self._annotations.update(self.plugin.telemetry_annotations())
+            if self.stop.wait(self.smi_interval):
+                return
 
     # ---- pods -------------------------------------------------------------------------
     def _pod_ip(self, key: str) -> str:
@@ -295,6 +324,7 @@ class Agent:
         print(f"{self.name}: registered in {time.monotonic() - t0:.3f}s "
               f"({len(self.plugin.devices())} GPU, inventory={self.plugin.inventory.source})", flush=True)
         threads = [threading.Thread(target=self.heartbeat_loop, name="heartbeat", daemon=True),
+                   threading.Thread(target=self.smi_loop, name="smi", daemon=True),
                    threading.Thread(target=self.watch_loop, name="pods", daemon=True)]
         for t in threads:
             t.start()
@@ -307,6 +337,22 @@ class Agent:
             self.stop.set()
             self.runtime.stop_all()
         return 0
+
+
+def read_smi(timeout: float = 20.0) -> dict | None:
+    """One AMD SMI sample (tk8s-smi, or the fake twin under TK8S_FAKE_GPUS); None if unavailable."""
+    if os.environ.get("TK8S_FAKE_GPUS"):
+        cmd = [sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.ops.fakesmi", "--no-links"]
+    else:
+        tool = Path(__file__).resolve().parents[1] / "bin" / "tk8s-smi"
+        if not tool.exists():
+            return None
+        cmd = [str(tool), "--no-links"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+        return json.loads(r.stdout) if r.stdout.strip() else None
+    except (OSError, subprocess.TimeoutExpired, ValueError):
+        return None
 
 
 def _os_image() -> str:
@@ -337,6 +383,10 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--labels", default="")
     ap.add_argument("--tool-dir", action="append", default=[])
     ap.add_argument("--timeout", type=float, default=60.0)
+    ap.add_argument("--smi-interval", type=float, default=float(os.environ.get("TK8S_SMI_INTERVAL", "30")),
+                    help="AMD SMI health sampling period in s (0 disables)")
+    ap.add_argument("--smi-delay", type=float, default=float(os.environ.get("TK8S_SMI_DELAY", "5")),
+                    help="first AMD SMI sample this many s after joining")
     ap.add_argument("--await-url", default=None,
                     help="standby: wait for a file holding the registration URL (relative to --sandbox)")
     a = ap.parse_args(argv)
@@ -347,7 +397,8 @@ def main(argv: list[str] | None = None) -> int:
     labels = dict(kv.split("=", 1) for kv in a.labels.split(",") if "=" in kv)
     tools = a.tool_dir or [str(Path(__file__).resolve().parents[1] / "bin")]
     wait = Path(a.sandbox) / a.await_url if a.await_url else None
-    return Agent(url, a.name, a.ip, a.sandbox, gpus, labels, tools, a.timeout).run(wait)
+    return Agent(url, a.name, a.ip, a.sandbox, gpus, labels, tools, a.timeout,
+                 smi_interval=a.smi_interval, smi_delay=a.smi_delay).run(wait)
 
 
 if __name__ == "__main__":

@@ -10,6 +10,8 @@ K8s device-plugin v1beta1 semantics without a kubelet in between:
 Discovery reads the KFD sysfs topology (models/hostinfo.py) and never initialises HIP: the
 agent spawns pods, so it must stay GPU-clean. The validation pod (tk8s-probe, HIP) is the
 authoritative check; its gpuinfo output refreshes PCI ids / UUIDs via ``update_from_probe``.
+Runtime health comes from AMD SMI (``tk8s-smi``, no HIP): ``update_from_smi`` marks a device
+Unhealthy while it reports uncorrectable or deferred ECC errors, and keeps its telemetry.
 """
 from __future__ import annotations
 
@@ -45,11 +47,15 @@ class Device:
     pci_bus_id: str = ""
     uuid: str = ""
     reason: str = ""
+    telemetry: dict = field(default_factory=dict)   # last AMD SMI sample (temp, power, ECC, VRAM)
 
     def to_dict(self) -> dict:
-        return {"id": self.id, "ordinal": self.ordinal, "health": self.health, "gfx": self.gfx,
-                "renderMinor": self.render_minor, "pciBusId": self.pci_bus_id, "uuid": self.uuid,
-                "reason": self.reason}
+        d = {"id": self.id, "ordinal": self.ordinal, "health": self.health, "gfx": self.gfx,
+             "renderMinor": self.render_minor, "pciBusId": self.pci_bus_id, "uuid": self.uuid,
+             "reason": self.reason}
+        if self.telemetry:
+            d["telemetry"] = self.telemetry
+        return d
 
 
 @dataclass
@@ -65,7 +71,8 @@ class DevicePlugin:
             if g is None:
                 self.devices_.append(Device(f"gpu{o}", o, "Unhealthy", reason="not visible on this host"))
             else:
-                self.devices_.append(Device(f"gpu{o}", o, "Healthy", g.render_minor, g.gfx))
+                self.devices_.append(Device(f"gpu{o}", o, "Healthy", g.render_minor, g.gfx,
+                                            pci_bus_id=g.pci_bus_id if g.location_id else ""))
 
     # ---- ListAndWatch -----------------------------------------------------------------
     def devices(self) -> list[dict]:
@@ -98,6 +105,45 @@ class DevicePlugin:
             for d in self.devices_:
                 if d.id in ids:
                     d.health, d.reason = "Unhealthy", "probe failed"
+
+    def update_from_smi(self, result: dict) -> bool:
+        """Fold one AMD SMI sample (tk8s-smi JSON, every GPU of the host, keyed by PCI bus id).
+        Returns True if any device's health changed."""
+        if not result.get("ok"):
+            return False
+        by_pci = {g.get("pci_bus_id", "").lower(): g for g in result.get("gpus", [])}
+        changed = False
+        for d in self.devices_:
+            g = by_pci.get(d.pci_bus_id.lower()) if d.pci_bus_id else None
+            if g is None:
+                continue
+            ecc = g.get("ecc") or {}
+            ue, deferred = int(ecc.get("uncorrectable", 0) or 0), int(ecc.get("deferred", 0) or 0)
+            d.telemetry = {k: g[k] for k in ("temp_c", "power", "vram_used_bytes", "ecc", "activity") if k in g}
+            if d.reason == "probe failed":
+                continue
+            if ue or deferred:
+                reason = f"ECC: {ue} uncorrectable, {deferred} deferred"
+                if d.health != "Unhealthy" or d.reason != reason:
+                    d.health, d.reason, changed = "Unhealthy", reason, True
+            elif d.reason.startswith("ECC:"):
+                d.health, d.reason, changed = "Healthy", "", True
+        return changed
+
+    def telemetry_annotations(self) -> dict[str, str]:
+        """Node-level summary of the last AMD SMI sample (hottest GPU, total power, ECC)."""
+        tel = [d.telemetry for d in self.devices_ if d.telemetry]
+        if not tel:
+            return {}
+        hot = [t["temp_c"]["hotspot"] for t in tel if "hotspot" in t.get("temp_c", {})]
+        watts = [t["power"]["current_w"] for t in tel if "current_w" in t.get("power", {})]
+        ue = sum(int(t.get("ecc", {}).get("uncorrectable", 0) or 0) for t in tel)
+        out = {"amd.com/gpu-health-source": "amdsmi", "amd.com/gpu-ecc-uncorrectable": str(ue)}
+        if hot:
+            out["amd.com/gpu-temp-hotspot-max-c"] = str(max(hot))
+        if watts:
+            out["amd.com/gpu-power-w"] = str(sum(watts))
+        return out
 
     # ---- GetPreferredAllocation ---------------------------------------------------------
     def preferred(self, available: list[str], must_include: list[str], size: int) -> list[str]:

@@ -135,6 +135,21 @@ def _print(obj, output: str | None) -> None:
         print(yaml.safe_dump(obj, sort_keys=False).rstrip())
 
 
+def _device_line(d: dict) -> str:
+    line = f"  {d['id']}: {d['health']} {d.get('gfx', '')} {d.get('pciBusId', '')}".rstrip()
+    if d.get("reason"):
+        line += f" ({d['reason']})"
+    t = d.get("telemetry") or {}
+    if t:
+        hot = t.get("temp_c", {}).get("hotspot")
+        watts = t.get("power", {}).get("current_w")
+        ecc = t.get("ecc", {})
+        line += (f"  hotspot={hot}C" if hot is not None else "") + (f" power={watts}W" if watts is not None else "")
+        if ecc:
+            line += f" ecc(ue/ce)={ecc.get('uncorrectable', 0)}/{ecc.get('correctable', 0)}"
+    return line
+
+
 def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap = argparse.ArgumentParser(prog="kubectl")
     ap.add_argument("--kubeconfig")
@@ -195,7 +210,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             if what == "node":
                 print("Capacity:\n" + "\n".join(f"  {x}: {y}" for x, y in st.get("capacity", {}).items()))
                 print("Allocatable:\n" + "\n".join(f"  {x}: {y}" for x, y in st.get("allocatable", {}).items()))
-                print("Devices:\n" + "\n".join(f"  {d['id']}: {d['health']} {d.get('gfx', '')} {d.get('pciBusId', '')}" for d in st.get("devices", [])))
+                print("Devices:\n" + "\n".join(_device_line(d) for d in st.get("devices", [])))
             print("Conditions:\n" + "\n".join(f"  {c['type']:<18} {c['status']:<8} {c.get('reason', '')}  {c.get('message', '')}"
                                               for c in st.get("conditions", [])))
             if what == "pod":

@@ -130,6 +130,31 @@ def cmd_env(args) -> int:
     return 0
 
 
+def cmd_gpu_health(args) -> int:
+    """AMD SMI health of every GPU of this host (what the node agents sample)."""
+    from ..agent.agent import read_smi
+
+    r = read_smi()
+    if r is None:
+        print("tk8s-smi is not available (build the native layer first)", file=sys.stderr)
+        return 3
+    if args.json:
+        print(json.dumps(r, indent=1))
+    else:
+        print(f"{'GPU':<4} {'PCI':<13} {'HEALTHY':<8} {'HOTSPOT':>7} {'POWER':>6} {'VRAM USED':>10} {'ECC UE/CE':>10}")
+        for g in r.get("gpus", []):
+            ecc = g.get("ecc", {})
+            used = g.get("vram_used_bytes")
+            print(f"{g.get('index', '?'):<4} {g.get('pci_bus_id', '?'):<13} {str(g.get('healthy')):<8} "
+                  f"{str(g.get('temp_c', {}).get('hotspot', '-')) + 'C':>7} "
+                  f"{str(g.get('power', {}).get('current_w', '-')) + 'W':>6} "
+                  f"{(f'{used / 2**30:.1f}GiB' if used is not None else '-'):>10} "
+                  f"{str(ecc.get('uncorrectable', '-')) + '/' + str(ecc.get('correctable', '-')):>10}")
+        if not r.get("ok"):
+            print(r.get("error", "no GPU"), file=sys.stderr)
+    return 0 if r.get("ok") and r.get("healthy") else (3 if not r.get("ok") else 1)
+
+
 def cmd_terraform(args) -> int:
     from ..provision import Engine
 
@@ -225,6 +250,9 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("-l", action="store_true")
         p.set_defaults(fn=fn)
     sub.add_parser("env").set_defaults(fn=cmd_env)
+    gh = sub.add_parser("gpu-health", help="AMD SMI health/telemetry of this host's GPUs (tk8s-smi)")
+    gh.add_argument("--json", action="store_true")
+    gh.set_defaults(fn=cmd_gpu_health)
     sub.add_parser("debug-vars", help="print the exported configuration (debugVars)").set_defaults(fn=cmd_debug_vars)
 
     t = sub.add_parser("terraform")

@@ -32,10 +32,18 @@ class HostGpu:
     cu_count: int = 0
     mem_bytes: int = 0
     location_id: int = 0
+    domain: int = 0
     fake: bool = False
 
+    @property
+    def pci_bus_id(self) -> str:
+        """dddd:bb:dd.f from the KFD node's PCI domain and location_id (bus<<8 | dev<<3 | fn) —
+        the key that joins this view to AMD SMI's and HIP's."""
+        loc = self.location_id
+        return f"{self.domain:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+
     def to_dict(self) -> dict:
-        return asdict(self)
+        return {**asdict(self), "pci_bus_id": self.pci_bus_id}
 
 
 @dataclass
@@ -96,7 +104,7 @@ def _visible_filter(n: int, environ=None) -> list[int] | None:
 
 def fake_inventory(n: int) -> HostInventory:
     gpus = [HostGpu(ordinal=i, kfd_node=i + 1, render_minor=128 + i, simd_count=1024, cu_count=256,
-                    mem_bytes=288 * 10**9, fake=True) for i in range(n)]
+                    mem_bytes=288 * 10**9, location_id=(0x10 + i) << 8, fake=True) for i in range(n)]
     links = [[{"type": "self" if i == j else "xgmi", "hops": 0 if i == j else 1} for j in range(n)] for i in range(n)]
     return HostInventory(gpus=gpus, links=links, source="fake")
 
@@ -141,7 +149,7 @@ def _discover(root: Path) -> HostInventory:
             ordinal=len(gpus), kfd_node=kfd_node, gfx=_gfx_name(p.get("gfx_target_version", 0)),
             render_minor=minor, simd_count=p.get("simd_count", 0),
             cu_count=p.get("simd_count", 0) // max(p.get("simd_per_cu", 4), 1),
-            location_id=p.get("location_id", 0),
+            location_id=p.get("location_id", 0), domain=p.get("domain", 0),
         ))
     vis = _visible_filter(len(gpus))
     if vis is not None:

@@ -371,7 +371,7 @@ def m_tk8s_build(args, *, check, **_):
 
 def _artefacts(bn) -> dict:
     out = {"lib": bn.lib_path(), "rccl_lib": bn.rccl_lib_path(), "native": bn.native_module_path(), "topo": bn.topo_module_path()}
-    out.update({n: bn.tool_path(n) for n in list(bn.TOOLS) + ["tk8s-supervise"]})
+    out.update({n: bn.tool_path(n) for n in list(bn.TOOLS) + ["tk8s-supervise", "tk8s-smi"]})
     return out
 
 

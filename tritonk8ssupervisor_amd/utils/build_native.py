@@ -11,6 +11,8 @@ Outputs (all in-tree so they travel to the GPU box with the repo snapshot):
 * ``tritonk8ssupervisor_amd/_tk8s_topo*.so`` — pybind11 module of the CPU-only xGMI-aware
   allocator (N2 core); no HIP dependency so the node agent can load it safely.
 * ``tritonk8ssupervisor_amd/bin/tk8s-{gpuinfo,probe,rccl}`` — the validation pod payloads.
+* ``tritonk8ssupervisor_amd/bin/tk8s-smi`` — AMD SMI health/telemetry (links ``libamd_smi`` only,
+  no HIP), run periodically by the node agent.
 
 The reference has no native code at all; this build replaces nothing there.
 Incremental: an output is rebuilt when any of its inputs or any header is newer.
@@ -176,13 +178,21 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), links))
 
+    smi_srcs = [NATIVE / "src" / "smi_health.cpp", NATIVE / "tools" / "tk8s_smi.cpp"]
+    smi = tool_path("tk8s-smi")
+    if force or _stale(smi, smi_srcs):
+        _run([CXX, "-O2", "-std=c++17", "-Wall", f"-I{NATIVE / 'include'}", f"-I{ROCM / 'include'}",
+              *[str(x) for x in smi_srcs], "-o", str(smi), f"-L{ROCM / 'lib'}", "-lamd_smi",
+              f"-Wl,-rpath,{ROCM / 'lib'}"], verbose)
+
     sup_src = NATIVE / "tools" / "tk8s_supervise.cpp"
     sup = tool_path("tk8s-supervise")
     if force or _stale(sup, [sup_src]):
         _run([CXX, "-O2", "-std=c++17", "-Wall", str(sup_src), "-o", str(sup)], verbose)
 
     precompile_python()
-    out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup}
+    out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,
+           "tk8s-smi": smi}
     out.update({n: tool_path(n) for n in TOOLS})
     return out
 
