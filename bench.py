@@ -21,7 +21,12 @@ start-up, provisioning, the playbook, the control plane, agent joins and per-GPU
 are all inside. The step brackets (``ms_per_step``) cover the whole ``./setup.sh`` process,
 which after Ready also runs the RCCL all-reduce Job over all N GPUs (N >= 2), reported as
 ``rccl_check_s`` / ``rccl_peak_busbw_gbps``. The teardown (``./setup.sh -c``) after each
-step runs outside the timed brackets. The reference publishes no
+step runs outside the timed brackets, followed by a ``--settle`` pause (default 1 s on a GPU
+host): the amdgpu driver releases an exited GPU process asynchronously, and a new process that
+starts the HIP runtime within ~0.1-0.2 s of that exit waits for it (``hsa_init`` 45-65 ms on a
+settled host vs 100-230 ms right after one; profiles/r1_init_costs/init_costs3.json). Without the
+pause every step after the first would also time the previous step's GPU teardown, which a real
+``./setup.sh`` never sees. The per-step runtime start is reported (``hip_init_ms_steps``). The reference publishes no
 bring-up time (BASELINE.json ``published: {}``); ``vs_baseline`` is quoted against the
 51 s of fixed sleeps in the reference's bring-up path, a floor the
 reference can never go below (setup.sh:36,41,46; terraform/*/main.tf:22;
@@ -213,6 +218,9 @@ def main(argv=None) -> int:
     ap.add_argument("--workdir", default=None, help="parent of the per-step workspaces (default: a tempdir)")
     ap.add_argument("--log", default=None, help="append setup.sh output here")
     ap.add_argument("--keep-events", default=None, help="copy each step's .tk8s/events.jsonl into this directory")
+    ap.add_argument("--settle", type=float, default=None,
+                    help="pause after each teardown, outside the timed region, so the driver has released the "
+                         "previous step's GPU processes (default: 1.0 s with real GPUs, 0 with fake ones)")
     args = ap.parse_args(argv)
 
     d = Dist()
@@ -220,6 +228,7 @@ def main(argv=None) -> int:
     fake = args.fake_gpus
     if fake is None and not d.cuda and not _has_kfd_gpus():
         fake = max(8, n)
+    settle = args.settle if args.settle is not None else (0.0 if fake else 1.0)
     root = Path(args.workdir) if args.workdir else Path(tempfile.mkdtemp(prefix="tk8s-bench-", dir=os.environ.get("TMPDIR", "/tmp")))
     root.mkdir(parents=True, exist_ok=True)
     times: list[float] = []
@@ -260,6 +269,8 @@ def main(argv=None) -> int:
                     if err is None:
                         err = str(e)
                 shutil.rmtree(ws, ignore_errors=True)
+                if settle > 0 and i + 1 < args.warmup + args.steps:
+                    time.sleep(settle)
             err = d.bcast_obj(err)
             if err is not None:
                 break
@@ -288,6 +299,10 @@ def main(argv=None) -> int:
         for k, v in s.get("phases", {}).items():
             phases[k] = phases.get(k, 0.0) + v / len(summaries)
     last = summaries[-1] if summaries else {}
+    hip_init = []
+    for s in summaries:
+        v = [float(a["hip-init-ms"]) for a in (s.get("validation") or {}).values() if a.get("hip-init-ms")]
+        hip_init.append(max(v) if v else None)
     out = {
         "metric": METRIC,
         "value": round(mean, 4),
@@ -322,6 +337,8 @@ def main(argv=None) -> int:
         "nodes_validated": last.get("nodes_validated"),
         "rccl_peak_busbw_gbps": (last.get("rccl") or {}).get("peak_busbw_gbps"),
         "validation_last_step": last.get("validation"),
+        "hip_init_ms_steps": hip_init,
+        "settle_s": settle,
     }
     errs = [s["post_ready_error"] for s in summaries if s.get("post_ready_error")]
     if errs:
