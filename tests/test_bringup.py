@@ -372,3 +372,23 @@ def test_ecc_errors_take_a_gpu_out_of_allocatable(ws, tmp_path_factory):
     assert "ECC: 2 uncorrectable" in kc("describe", "node", "kubenode2").stdout
     faults.write_text("")
     wait_for(lambda n: n["status"]["allocatable"].get("amd.com/gpu") == "1", "errors cleared -> Healthy")
+
+
+def test_setup_with_the_kubelet_grpc_device_plugin(ws):
+    """TK8S_DEVICE_PLUGIN=grpc: every agent serves the amd.com/gpu plugin on the kubelet
+    device-plugin API (v1beta1, Unix sockets) and allocates through it; the RCCL Job's ranks get
+    their GPUs from gRPC Allocate and see the node (tk8s.amd.com/gpu-visibility: node)."""
+    s = _summary(_setup(ws, "--nodes", "2", env=_env(TK8S_DEVICE_PLUGIN="grpc")))
+    assert s["gpus_allocatable"] == 2 and s["nodes_validated"] == 2 and s["rccl"]["ok"]
+    for i in (1, 2):
+        log = (ws / ".tk8s" / "machines" / f"kubenode{i}" / "logs" / "agent.log").read_text()
+        assert "via gRPC v1beta1" in log and "registered with the kubelet" in log
+
+
+def test_pod_gpu_env_visibility_modes():
+    from tritonk8ssupervisor_amd.agent.agent import pod_gpu_env
+
+    alloc = {"ROCR_VISIBLE_DEVICES": "5", "HIP_VISIBLE_DEVICES": "0", "CUDA_VISIBLE_DEVICES": "0"}
+    assert pod_gpu_env(alloc, [5]) == alloc
+    node = pod_gpu_env(alloc, [5, 6], "node")
+    assert node == {"TK8S_GPU_DEVICES": "5,6", "TK8S_GPU_DEVICE": "5"}

@@ -33,6 +33,7 @@ from .runtime import PodProc, PodRuntime, install_sigterm
 
 GPU = "amd.com/gpu"
 ALL_GPUS = "tk8s.amd.com/all-gpus"
+GPU_VISIBILITY = "tk8s.amd.com/gpu-visibility"
 VALIDATION_LABEL = "tk8s.amd.com/validation"
 TERMINAL = ("Succeeded", "Failed")
 
@@ -48,7 +49,7 @@ def pod_gpus(p: dict) -> int:
 class Agent:
     def __init__(self, url: str | None, name: str, ip: str, sandbox: str, gpus: list[int],
                  labels: dict | None = None, tool_dirs: list[str] | None = None, timeout: float = 60.0,
-                 smi_interval: float = 30.0, smi_delay: float = 5.0):
+                 smi_interval: float = 30.0, smi_delay: float = 5.0, device_plugin: str = "builtin"):
         self.reg_url = url
         self.name = name
         self.ip = ip
@@ -67,6 +68,10 @@ class Agent:
         self.smi_interval = smi_interval     # AMD SMI health period (0: off)
         self.smi_delay = smi_delay           # first sample after join, off the bring-up path
         self._annotations: dict[str, str] = {}
+        self.device_plugin = device_plugin    # "builtin" (in-process core) or "grpc" (kubelet API)
+        self.dp_client = None                 # kubelet-side handle on the gRPC plugin
+        self.dp_servicer = None
+        self.kubelet = None
         if url:
             self.set_url(url)
 
@@ -92,6 +97,32 @@ class Agent:
             time.sleep(delay)
             delay = min(delay * 2, 0.005)
         raise SystemExit(0)
+
+    # ---- device plugin over the kubelet API ----------------------------------------------
+    def start_grpc_plugin(self) -> None:
+        """``--device-plugin grpc``: serve the plugin core on the kubelet device-plugin API
+        (agent/dp_grpc.py) and drive it from here the way the kubelet's device manager does
+        (Register, ListAndWatch, GetPreferredAllocation, Allocate), over the Unix sockets."""
+        from .dp_grpc import RESOURCE, GpuDevicePluginServicer, KubeletRegistry, PluginServer, socket_dir
+
+        d = socket_dir(self.sandbox / "device-plugins")
+        self.kubelet = KubeletRegistry(d).start()
+        self.kubelet.on_update = lambda _c: setattr(self, "_devices_dirty", True)
+        self.dp_servicer = GpuDevicePluginServicer(self.plugin, env_mode="process")
+        server = PluginServer(self.dp_servicer, d, log=lambda m: print(f"{self.name}: {m}", flush=True))
+        threading.Thread(target=server.serve_forever, args=(self.stop,), kwargs={"poll": 0.5},
+                         name="device-plugin", daemon=True).start()
+        c = self.kubelet.wait_plugin(RESOURCE, 10.0)
+        if c is None or not c.wait(lambda c: c.updates > 0, 10.0):
+            raise RuntimeError(f"{self.name}: the {RESOURCE} device plugin did not register over gRPC")
+        self.dp_client = c
+        print(f"{self.name}: kubelet device manager: {RESOURCE} via gRPC v1beta1, "
+              f"{len(c.healthy())} healthy device(s)", flush=True)
+
+    def _plugin_changed(self) -> None:
+        self._devices_dirty = True
+        if self.dp_servicer is not None:
+            self.dp_servicer.notify()
 
     # ---- join -------------------------------------------------------------------------
     def join(self) -> None:
@@ -178,6 +209,7 @@ class Agent:
                 changed = self.plugin.update_from_smi(res)
                 self._devices_dirty = True  # telemetry rides along with the device list
                 if changed:
+                    self._plugin_changed()
                     bad = [d.id for d in self.plugin.devices_ if d.reason.startswith("ECC:")]
                     print(f"{self.name}: AMD SMI health changed; unhealthy: {bad or 'none'}", flush=True)
                 self._annotations.update(self.plugin.telemetry_annotations())
@@ -206,7 +238,11 @@ class Agent:
         for pp in self.runtime.running().values():
             if not pp.done.is_set():
                 used.update(pp.gpu_ids)
-        return [d["id"] for d in self.plugin.devices() if d["health"] == "Healthy" and d["id"] not in used]
+        if self.dp_client is not None:  # what the plugin's ListAndWatch last reported
+            healthy = self.dp_client.healthy()
+        else:
+            healthy = [d["id"] for d in self.plugin.devices() if d["health"] == "Healthy"]
+        return [i for i in healthy if i not in used]
 
     def _start_pod(self, pod: dict) -> None:
         md, spec = pod["metadata"], pod["spec"]
@@ -223,10 +259,20 @@ class Agent:
                          {"reason": "UnexpectedAdmissionError",
                           "message": f"Allocate failed: requested {need} {GPU}, {len(free)} free"}, None)
             return
-        ids = self.plugin.preferred(free, [], need) if need else []
-        alloc = self.plugin.allocate(ids) if ids else {"env": {}, "devices": [], "annotations": {}}
+        try:
+            if need and self.dp_client is not None:
+                ids = self.dp_client.preferred(free, [], need)
+                alloc = self.dp_client.allocate(ids)
+            else:
+                ids = self.plugin.preferred(free, [], need) if need else []
+                alloc = self.plugin.allocate(ids) if ids else {"env": {}, "devices": [], "annotations": {}}
+        except Exception as e:  # noqa: BLE001 - grpc.RpcError / allocator errors fail the pod
+            self._report(key, md["name"], md["namespace"], "Failed",
+                         {"reason": "UnexpectedAdmissionError", "message": f"Allocate failed: {e}"}, None)
+            return
         env = {k: v for k, v in os.environ.items() if not k.startswith("TK8S_FAULT")}
-        env.update(alloc["env"])
+        visibility = md.get("annotations", {}).get(GPU_VISIBILITY, "allocated")
+        env.update(pod_gpu_env(alloc["env"], [self._ordinal(i) for i in ids], visibility))
         pod_ip = self._pod_ip(key)
         env.update({"POD_NAME": md["name"], "POD_NAMESPACE": md["namespace"], "POD_UID": md.get("uid", ""),
                     "POD_IP": pod_ip, "NODE_NAME": self.name, "NODE_IP": self.ip, "TK8S_API_URL": self.base,
@@ -252,7 +298,7 @@ class Agent:
         if meta.get("validation") and phase in TERMINAL and isinstance(result, dict):
             result["_allocated_ids"] = pp.gpu_ids
             self.plugin.update_from_probe(result)
-            self._devices_dirty = True
+            self._plugin_changed()
         self._report(pp.key, meta.get("name", pp.key.split("/")[1]), meta.get("namespace", "default"), phase, extra,
                      pp, meta.get("annotations"))
 
@@ -317,6 +363,8 @@ class Agent:
     # ---- lifecycle --------------------------------------------------------------------
     def run(self, await_url: Path | None = None) -> int:
         install_sigterm()
+        if self.device_plugin == "grpc":  # before the URL wait: off the join's critical path
+            self.start_grpc_plugin()
         if not self.reg_url and await_url is not None:
             self.await_url(await_url)
         t0 = time.monotonic()
@@ -336,7 +384,24 @@ class Agent:
         finally:
             self.stop.set()
             self.runtime.stop_all()
+            if self.kubelet is not None:
+                self.kubelet.stop()
         return 0
+
+    def _ordinal(self, dev_id: str) -> int:
+        return next(d.ordinal for d in self.plugin.devices_ if d.id == dev_id)
+
+
+def pod_gpu_env(alloc_env: dict, ordinals: list[int], visibility: str = "allocated") -> dict:
+    """GPU env of a pod. ``allocated`` (default): the device plugin's Allocate env, so the pod's
+    runtime initialises only its own GPUs. ``node``: the pod still owns exactly its allocated GPUs
+    but sees the agent's whole view, with its devices named in TK8S_GPU_DEVICE(S) -- what
+    rccl-tests style ranks need, since RCCL's peer-to-peer transport over xGMI only connects
+    GPUs that are visible to each rank's runtime."""
+    if visibility == "node":
+        return {"TK8S_GPU_DEVICES": ",".join(map(str, ordinals)),
+                "TK8S_GPU_DEVICE": str(ordinals[0]) if ordinals else ""}
+    return dict(alloc_env)
 
 
 def read_smi(timeout: float = 20.0) -> dict | None:
@@ -387,6 +452,9 @@ def main(argv: list[str] | None = None) -> int:
                     help="AMD SMI health sampling period in s (0 disables)")
     ap.add_argument("--smi-delay", type=float, default=float(os.environ.get("TK8S_SMI_DELAY", "5")),
                     help="first AMD SMI sample this many s after joining")
+    ap.add_argument("--device-plugin", choices=["builtin", "grpc"],
+                    default=os.environ.get("TK8S_DEVICE_PLUGIN", "builtin"),
+                    help="builtin: in-process plugin core; grpc: the kubelet device-plugin API over Unix sockets")
     ap.add_argument("--await-url", default=None,
                     help="standby: wait for a file holding the registration URL (relative to --sandbox)")
     a = ap.parse_args(argv)
@@ -398,7 +466,7 @@ def main(argv: list[str] | None = None) -> int:
     tools = a.tool_dir or [str(Path(__file__).resolve().parents[1] / "bin")]
     wait = Path(a.sandbox) / a.await_url if a.await_url else None
     return Agent(url, a.name, a.ip, a.sandbox, gpus, labels, tools, a.timeout,
-                 smi_interval=a.smi_interval, smi_delay=a.smi_delay).run(wait)
+                 smi_interval=a.smi_interval, smi_delay=a.smi_delay, device_plugin=a.device_plugin).run(wait)
 
 
 if __name__ == "__main__":

@@ -408,7 +408,7 @@ class Setup:
         else:
             from .ops import BIN
 
-            cmd = [str(BIN / "tk8s-rccl"), "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "0",
+            cmd = [str(BIN / "tk8s-rccl"), "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "$(TK8S_GPU_DEVICE)",
                    "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
                    "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
         prof_dir = None
