@@ -1,0 +1,284 @@
+"""The reference's acceptance demos on a tk8s cluster (docs/detailed.md:255-370) and the
+Kubernetes workload API they lean on: the three-tier Guestbook (redis leader + followers +
+frontend, images mapped to built-in apps) through kubectl, Ghost through the dashboard's deploy
+form, Service env vars, ConfigMaps/Secrets, rolling updates, scale, Ingress, cluster DNS, drain."""
+import asyncio
+import json
+import os
+import shutil
+import socket
+import subprocess
+import sys
+import threading
+import time
+import urllib.request
+from pathlib import Path
+
+import pytest
+
+from tritonk8ssupervisor_amd.apps import image_name, resolve
+from tritonk8ssupervisor_amd.apps.redis import Redis
+from tritonk8ssupervisor_amd.apps.resp import RespError, call
+from tritonk8ssupervisor_amd.controlplane.ingress import match_route
+from tritonk8ssupervisor_amd.utils.k8senv import field_path, service_env
+from tritonk8ssupervisor_amd.utils.net import host_port
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+# ---- units ----------------------------------------------------------------------------------
+def test_image_catalogue():
+    assert image_name("gcr.io/google-samples/gb-frontend:v4") == "gb-frontend"
+    assert image_name("registry.k8s.io/redis:e2e@sha256:abc") == "redis"
+    assert resolve("ghost:5")[-1] == "tritonk8ssupervisor_amd.apps.ghost"
+    assert resolve("gcr.io/google_samples/gb-redisslave:v1")[-2:] == ["--follow", "redis-master,redis-leader"]
+    assert resolve("busybox") is None and resolve(None) is None
+
+
+def test_host_port_remap(monkeypatch):
+    monkeypatch.setenv("TK8S_REMAP_PRIVILEGED_PORTS", "1")
+    assert host_port(80) == 20080 and host_port(6379) == 6379
+    monkeypatch.setenv("TK8S_REMAP_PRIVILEGED_PORTS", "0")
+    assert host_port(80) == 80
+
+
+def test_service_env_matches_the_kubelet(monkeypatch):
+    monkeypatch.setenv("TK8S_REMAP_PRIVILEGED_PORTS", "0")
+    svcs = [{"metadata": {"name": "redis-master"}, "spec": {"clusterIP": "127.96.0.5", "ports": [
+        {"name": "redis", "port": 6379, "protocol": "TCP"}]}},
+        {"metadata": {"name": "headless"}, "spec": {"clusterIP": "None", "ports": [{"port": 1}]}}]
+    env = service_env(svcs, "http://127.0.1.1:8080")
+    assert env["REDIS_MASTER_SERVICE_HOST"] == "127.96.0.5" and env["REDIS_MASTER_SERVICE_PORT"] == "6379"
+    assert env["REDIS_MASTER_SERVICE_PORT_REDIS"] == "6379"
+    assert env["REDIS_MASTER_PORT"] == "tcp://127.96.0.5:6379"
+    assert env["REDIS_MASTER_PORT_6379_TCP_ADDR"] == "127.96.0.5"
+    assert env["KUBERNETES_SERVICE_HOST"] == "127.0.1.1" and env["KUBERNETES_SERVICE_PORT"] == "8080"
+    assert not any(k.startswith("HEADLESS") for k in env)
+    pod = {"metadata": {"name": "p", "namespace": "ns", "labels": {"app": "x"}}, "spec": {"nodeName": "n1"}}
+    assert field_path(pod, "metadata.labels['app']") == "x" and field_path(pod, "spec.nodeName") == "n1"
+    assert field_path(pod, "status.podIP", "127.128.0.2") == "127.128.0.2"
+    with pytest.raises(ValueError):
+        field_path(pod, "spec.bogus")
+
+
+def test_ingress_rule_matching():
+    routes = [("", "/", "Prefix", "svc-default", "80"), ("shop.local", "/api", "Prefix", "svc-api", "80"),
+              ("shop.local", "/api/v2", "Exact", "svc-v2", "80"), ("", "/static", "Prefix", "svc-static", "80")]
+    assert match_route(routes, "shop.local:80", "/api/cart") == ("svc-api", "80")
+    assert match_route(routes, "shop.local", "/api/v2") == ("svc-v2", "80")
+    assert match_route(routes, "other", "/static/x.css") == ("svc-static", "80")
+    assert match_route(routes, "other", "/staticky") == ("svc-default", "80")
+    assert match_route(routes[1:3], "other", "/api") is None
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture
+def redis_pair():
+    """A leader and a follower on one private event loop thread."""
+    loop = asyncio.new_event_loop()
+    leader, follower = Redis(), Redis(sync_interval=0.02)
+    ports = (_free_port(), _free_port())
+    follower.leader = ("127.0.0.1", ports[0])
+
+    async def start():
+        servers = [await asyncio.start_server(db.handle, "127.0.0.1", p) for db, p in zip((leader, follower), ports)]
+        tasks = [asyncio.ensure_future(follower.follow_loop())]
+        return servers, tasks
+
+    servers, tasks = loop.run_until_complete(start())
+    t = threading.Thread(target=loop.run_forever, daemon=True)
+    t.start()
+    yield ports
+
+    async def stop():
+        for task in tasks:
+            task.cancel()
+        await asyncio.gather(*tasks, return_exceptions=True)
+        for srv in servers:
+            srv.close()
+
+    asyncio.run_coroutine_threadsafe(stop(), loop).result(5)
+    loop.call_soon_threadsafe(loop.stop)
+    t.join(5)
+
+
+def test_redis_commands_and_replication(redis_pair):
+    lp, fp = redis_pair
+    assert call("127.0.0.1", lp, "PING") == "PONG"
+    assert call("127.0.0.1", lp, "SET", "messages", "hello,world") == "OK"
+    assert call("127.0.0.1", lp, "GET", "messages") == b"hello,world"
+    assert call("127.0.0.1", lp, "RPUSH", "l", "a", "b", "c") == 3
+    assert call("127.0.0.1", lp, "LRANGE", "l", "0", "-1") == [b"a", b"b", b"c"]
+    assert call("127.0.0.1", lp, "INCR", "n") == 1 and call("127.0.0.1", lp, "INCRBY", "n", "41") == 42
+    with pytest.raises(RespError, match="WRONGTYPE"):
+        call("127.0.0.1", lp, "GET", "l")
+    with pytest.raises(RespError, match="unknown command"):
+        call("127.0.0.1", lp, "NOPE")
+    assert call("127.0.0.1", lp, "ROLE")[0] == b"master"
+    deadline = time.monotonic() + 5
+    while call("127.0.0.1", fp, "GET", "messages") != b"hello,world":
+        assert time.monotonic() < deadline
+        time.sleep(0.02)
+    assert call("127.0.0.1", fp, "LRANGE", "l", "0", "-1") == [b"a", b"b", b"c"]
+    with pytest.raises(RespError, match="READONLY"):
+        call("127.0.0.1", fp, "SET", "x", "1")
+    assert b"role:slave" in call("127.0.0.1", fp, "INFO")
+    assert call("127.0.0.1", fp, "REPLICAOF", "NO", "ONE") == "OK"  # promote
+    assert call("127.0.0.1", fp, "SET", "x", "1") == "OK"
+
+
+# ---- end to end on a local cluster ------------------------------------------------------------
+
+
+@pytest.fixture
+def cluster(tmp_path, monkeypatch):
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    monkeypatch.setenv("TK8S_REMAP_PRIVILEGED_PORTS", "1")  # the test's view of the shifted ports too
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, tmp_path / f)
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_FAKE_GPUS="8",
+               TK8S_REMAP_PRIVILEGED_PORTS="1")  # exercise the non-root port shift even as root
+    env.pop("TK8S_FAULTS", None)
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "2", "--rccl", "off"], cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    summary = json.loads(r.stdout.strip().splitlines()[-1])
+
+    def kc(*a, check=True):
+        p = subprocess.run(["./kubectl", *a], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+        if check:
+            assert p.returncode == 0, f"kubectl {' '.join(a)}: {p.stdout}{p.stderr}"
+        return p
+
+    yield tmp_path, env, kc, summary
+    subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+def _get(url, timeout=5.0):
+    return urllib.request.urlopen(url, timeout=timeout).read().decode()
+
+
+def _until(fn, timeout=20.0):
+    deadline = time.monotonic() + timeout
+    while True:
+        try:
+            v = fn()
+            if v:
+                return v
+        except OSError:
+            pass
+        assert time.monotonic() < deadline, "condition not met in time"
+        time.sleep(0.05)
+
+
+@pytest.mark.slow
+def test_guestbook_all_in_one_through_kubectl(cluster):
+    ws, env, kc, _ = cluster
+    out = kc("apply", "-f", str(REPO / "manifests" / "examples" / "guestbook-all-in-one.yaml")).stdout
+    assert "deployment/frontend created" in out and "service/redis-master created" in out
+    for d in ("redis-master", "redis-slave", "frontend"):
+        assert "successfully rolled out" in kc("rollout", "status", f"deploy/{d}", "--timeout", "60s").stdout
+    svc = json.loads(kc("get", "svc", "frontend", "-o", "json").stdout)
+    url = f"http://{svc['status']['loadBalancer']['ingress'][0]['ip']}:{host_port(80)}"
+    assert "(host 20080)" in kc("get", "svc").stdout
+    assert "<title>Guestbook</title>" in _until(lambda: _get(url + "/"))
+    assert json.loads(_get(url + "/guestbook.php?cmd=set&key=messages&value=hello,tk8s")) == {"message": "Updated"}
+    # reads go to a follower, which replicates the leader
+    _until(lambda: json.loads(_get(url + "/guestbook.php?cmd=get&key=messages"))["data"] == "hello,tk8s")
+    # apply again: unchanged; scale; a template change rolls out pod by pod
+    assert "deployment/frontend unchanged" in kc("apply", "-f", str(REPO / "manifests" / "examples" / "guestbook-all-in-one.yaml")).stdout
+    kc("scale", "deploy/frontend", "--replicas", "1")
+    kc("rollout", "status", "deploy/frontend", "--timeout", "60s")
+    pods = json.loads(kc("get", "pods", "-l", "tier=frontend", "-o", "json").stdout)["items"]
+    assert len([p for p in pods if p["status"].get("phase") == "Running"]) == 1
+    old_hash = pods[0]["metadata"]["labels"]["pod-template-hash"]
+    kc("rollout", "restart", "deploy/frontend")
+    kc("rollout", "status", "deploy/frontend", "--timeout", "60s")
+    pods = json.loads(kc("get", "pods", "-l", "tier=frontend", "-o", "json").stdout)["items"]
+    assert {p["metadata"]["labels"]["pod-template-hash"] for p in pods} != {old_hash}
+    _until(lambda: json.loads(_get(url + "/guestbook.php?cmd=get&key=messages"))["data"] == "hello,tk8s")
+
+
+@pytest.mark.slow
+def test_config_env_ingress_dns_and_drain(cluster, tmp_path_factory):
+    ws, env, kc, summary = cluster
+    from tritonk8ssupervisor_amd.controlplane import dns
+
+    d = tmp_path_factory.mktemp("m")
+    kc("create", "configmap", "app-config", "--from-literal", "GREETING=hello", "--from-literal", "COLOR=blue")
+    kc("create", "secret", "generic", "app-secret", "--from-literal", "password=s3cr3t")
+    assert "app-config" in kc("get", "cm").stdout and "Opaque" in kc("get", "secrets").stdout
+    (d / "env.yaml").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "envpod", "labels": {"app": "envpod"}},
+        "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "command": ["sh", "-c", "env | sort"],
+                 "envFrom": [{"configMapRef": {"name": "app-config"}, "prefix": "CFG_"}],
+                 "env": [{"name": "PW", "valueFrom": {"secretKeyRef": {"name": "app-secret", "key": "password"}}},
+                         {"name": "ME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.labels['app']"}}},
+                         {"name": "LATE", "valueFrom": {"configMapKeyRef": {"name": "late-config", "key": "v"}}}]}]}}))
+    kc("apply", "-f", str(d / "env.yaml"))
+    pod = _until(lambda: json.loads(kc("get", "pod", "envpod", "-o", "json").stdout))
+    _until(lambda: json.loads(kc("get", "pod", "envpod", "-o", "json").stdout)["status"].get("reason") == "CreateContainerConfigError")
+    kc("create", "configmap", "late-config", "--from-literal", "v=arrived")  # the kubelet retries
+    _until(lambda: json.loads(kc("get", "pod", "envpod", "-o", "json").stdout)["status"].get("phase") == "Succeeded")
+    log = kc("logs", "envpod").stdout
+    for line in ("CFG_GREETING=hello", "CFG_COLOR=blue", "PW=s3cr3t", "ME=envpod", "LATE=arrived", "KUBERNETES_SERVICE_HOST="):
+        assert line in log, line
+    # a web app behind a Service, reached through an Ingress rule and cluster DNS
+    kc("apply", "-f", str(REPO / "manifests" / "examples" / "ingress-nginx.yaml"))
+    kc("rollout", "status", "deploy/web", "--timeout", "60s")
+    ing = json.loads(kc("get", "ingress", "web", "-o", "json").stdout)
+    ip = ing["status"]["loadBalancer"]["ingress"][0]["ip"]
+    req = urllib.request.Request(f"http://{ip}:{host_port(80)}/", headers={"Host": "web.local"})
+    assert "Welcome to nginx!" in _until(lambda: urllib.request.urlopen(req, timeout=5).read().decode())
+    req = urllib.request.Request(f"http://{ip}:{host_port(80)}/", headers={"Host": "elsewhere"})
+    with pytest.raises(urllib.error.HTTPError) as e:
+        urllib.request.urlopen(req, timeout=5)
+    assert e.value.code == 404
+    svc = json.loads(kc("get", "svc", "web", "-o", "json").stdout)
+    with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+        s.settimeout(5)
+        s.sendto(dns.query("web.default.svc.cluster.local"), (ip, host_port(53)))
+        assert dns.parse_reply(s.recv(512)) == (0, [svc["spec"]["clusterIP"]])
+        s.sendto(dns.query("nope.default.svc.cluster.local"), (ip, host_port(53)))
+        assert dns.parse_reply(s.recv(512))[0] == dns.NXDOMAIN
+    # drain: pods leave the node, the Deployment re-creates them on the other node
+    node = json.loads(kc("get", "pods", "-l", "app=web", "-o", "json").stdout)["items"][0]["spec"]["nodeName"]
+    out = kc("drain", node).stdout
+    assert "drained" in out and "evicting pod default/web-" in out
+    kc("rollout", "status", "deploy/web", "--timeout", "60s")
+    pods = json.loads(kc("get", "pods", "-l", "app=web", "-o", "json").stdout)["items"]
+    assert pods and all(p["spec"]["nodeName"] != node for p in pods if p["status"].get("phase") == "Running")
+    assert "SchedulingDisabled" in kc("get", "nodes").stdout
+    top = kc("top", "nodes").stdout
+    assert "GPU(USED/ALLOC)" in top and "kubenode1" in top
+    kc("label", "node", node, "pool=mi355x")
+    assert json.loads(kc("get", "node", node, "-o", "json").stdout)["metadata"]["labels"]["pool"] == "mi355x"
+    kc("label", "node", node, "pool-")
+    assert "pool" not in json.loads(kc("get", "node", node, "-o", "json").stdout)["metadata"]["labels"]
+
+
+@pytest.mark.slow
+def test_ghost_from_the_dashboard_deploy_form(cluster):
+    ws, env, kc, summary = cluster
+    dash = summary["dashboard"]
+    body = json.dumps({"name": "ghost", "containerImage": "ghost", "replicas": 1, "isExternal": True,
+                       "portMappings": [{"port": 2368, "targetPort": 2368, "protocol": "TCP"}]}).encode()
+    r = urllib.request.urlopen(urllib.request.Request(dash + "api/v1/appdeployment", data=body, method="POST",
+                                                      headers={"Content-Type": "application/json"}), timeout=10)
+    assert r.status == 201
+    kc("rollout", "status", "deploy/ghost", "--timeout", "60s")
+    svc = json.loads(kc("get", "svc", "ghost", "-o", "json").stdout)
+    url = f"http://{svc['status']['loadBalancer']['ingress'][0]['ip']}:2368"
+    assert "<title>Ghost</title>" in _until(lambda: _get(url + "/"))
+    post = json.dumps({"posts": [{"title": "MI355X is Ready", "html": "all 8 GPUs allocatable"}]}).encode()
+    urllib.request.urlopen(urllib.request.Request(url + "/ghost/api/v0.1/posts", data=post, method="POST",
+                                                  headers={"Content-Type": "application/json"}), timeout=5)
+    assert "MI355X is Ready" in _get(url + "/")
+    page = _get(dash)
+    assert "Deploy a containerized app" in page and "ghost" in page

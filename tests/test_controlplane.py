@@ -292,3 +292,98 @@ def test_metrics_and_version(cp):
     text = cp.get("/metrics", raw=True)
     assert "tk8s_nodes" in text
     assert "version" in json.dumps(cp.get("/version")).lower()
+
+
+def test_put_patch_scale_and_rolling_update(cp):
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    nc, _ = _join(cp, proj["id"], "kubenode1", ngpu=0)
+    base = "/apis/apps/v1/namespaces/default/deployments"
+    dep = {"metadata": {"name": "web"}, "spec": {"replicas": 2, "selector": {"matchLabels": {"app": "web"}},
+           "template": {"metadata": {"labels": {"app": "web"}}, "spec": {"containers": [{"name": "c", "command": ["v1"]}]}}}}
+    d = k.post(k.k8s(base), dep)
+    assert d["metadata"]["generation"] == 1
+    pods = lambda: k.get(k.k8s("/api/v1/namespaces/default/pods"), query={"labelSelector": "app=web"})["items"]
+    v1 = pods()
+    assert len(v1) == 2 and len({p["metadata"]["labels"]["pod-template-hash"] for p in v1}) == 1
+    for p in v1:
+        _set_pod(nc, "default", p["metadata"]["name"], "Running")
+    # stale resourceVersion -> 409; clusterIP-style immutability for Jobs -> 422
+    stale = dict(dep, metadata={"name": "web", "resourceVersion": "1"})
+    with pytest.raises(ApiError) as ei:
+        k.put(k.k8s(base + "/web"), stale)
+    assert ei.value.status == 409
+    # a new template: maxSurge 1, maxUnavailable 0 -> one extra pod, no old pod gone yet
+    k.request("PATCH", k.k8s(base + "/web"), body={"spec": {"template": {"spec": {"containers": [{"name": "c", "command": ["v2"]}]}}}})
+    d = k.get(k.k8s(base + "/web"))
+    assert d["metadata"]["generation"] == 2
+    now = pods()
+    new = [p for p in now if p["spec"]["containers"][0]["command"] == ["v2"]]
+    assert len(now) == 3 and len(new) == 1
+    # each new pod that runs releases one old pod, until the rollout is complete
+    for _ in range(4):
+        for p in pods():
+            if p["spec"]["containers"][0]["command"] == ["v2"] and p["status"].get("phase") != "Running":
+                _set_pod(nc, "default", p["metadata"]["name"], "Running")
+    final = pods()
+    assert len(final) == 2 and all(p["spec"]["containers"][0]["command"] == ["v2"] for p in final)
+    st = k.get(k.k8s(base + "/web"))["status"]
+    assert st["updatedReplicas"] == 2 and st["readyReplicas"] == 2 and st["observedGeneration"] == 2
+    # scale subresource
+    sc = k.request("PATCH", k.k8s(base + "/web/scale"), body={"spec": {"replicas": 1}})
+    assert sc["kind"] == "Scale" and sc["spec"]["replicas"] == 1 and len(pods()) == 1
+    with pytest.raises(ApiError) as ei:
+        k.request("PATCH", k.k8s(base + "/web/scale"), body={"spec": {"replicas": -1}})
+    assert ei.value.status == 422
+    # labels: merge patch adds and (null) removes
+    k.request("PATCH", k.k8s(base + "/web"), body={"metadata": {"labels": {"tier": "fe"}}})
+    k.request("PATCH", k.k8s(base + "/web"), body={"metadata": {"labels": {"tier": None}}})
+    assert "tier" not in k.get(k.k8s(base + "/web"))["metadata"]["labels"]
+
+
+def test_configmaps_secrets_and_service_update(cp):
+    import base64
+
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    s = k.post(k.k8s("/api/v1/namespaces/default/secrets"), {"metadata": {"name": "s"}, "stringData": {"pw": "x"}})
+    assert s["data"] == {"pw": base64.b64encode(b"x").decode()} and s["type"] == "Opaque" and "stringData" not in s
+    with pytest.raises(ApiError) as ei:
+        k.post(k.k8s("/api/v1/namespaces/default/secrets"), {"metadata": {"name": "bad"}, "data": {"k": "%%%"}})
+    assert ei.value.status == 422
+    with pytest.raises(ApiError) as ei:
+        k.post(k.k8s("/api/v1/namespaces/default/configmaps"), {"metadata": {"name": "c"}, "data": {"n": 1}})
+    assert ei.value.status == 422
+    k.post(k.k8s("/api/v1/namespaces/default/configmaps"), {"metadata": {"name": "c"}, "data": {"n": "1"}})
+    assert k.get(k.k8s("/api/v1/configmaps"))["items"][0]["data"] == {"n": "1"}
+    svc = k.post(k.k8s("/api/v1/namespaces/default/services"), {"metadata": {"name": "web"}, "spec": {
+        "type": "NodePort", "selector": {"app": "web"}, "ports": [{"port": 8000}]}})
+    cip, np = svc["spec"]["clusterIP"], svc["spec"]["ports"][0]["nodePort"]
+    upd = k.put(k.k8s("/api/v1/namespaces/default/services/web"), {"metadata": {"name": "web"}, "spec": {
+        "type": "NodePort", "selector": {"app": "web2"}, "ports": [{"port": 8000}]}})
+    assert upd["spec"]["clusterIP"] == cip and upd["spec"]["ports"][0]["nodePort"] == np
+    assert upd["spec"]["selector"] == {"app": "web2"}
+    with pytest.raises(ApiError) as ei:
+        k.put(k.k8s("/api/v1/namespaces/default/services/web"), {"metadata": {"name": "web"}, "spec": {
+            "clusterIP": "127.96.9.9", "ports": [{"port": 8000}]}})
+    assert ei.value.status == 422
+
+
+def test_cluster_dns_names():
+    from tritonk8ssupervisor_amd.controlplane import dns
+    from tritonk8ssupervisor_amd.controlplane.server import ControlPlane
+
+    cpl = ControlPlane("127.0.0.1", 0)
+    cpl.store.put("projects", "1a1", {"id": "1a1", "created_seq": 1, "metadata": {"name": "1a1"}})
+    cpl.store.put("services", "1a1/shop/cart", {"_project": "1a1", "metadata": {"name": "cart", "namespace": "shop"},
+                                                "spec": {"clusterIP": "127.96.0.9", "ports": [{"port": 80}]}})
+    assert cpl.dns_resolve("cart.shop.svc.cluster.local") == ["127.96.0.9"]
+    assert cpl.dns_resolve("cart.shop.svc") == ["127.96.0.9"] == cpl.dns_resolve("cart.shop")
+    assert cpl.dns_resolve("127-128-0-7.shop.pod.cluster.local") == ["127.128.0.7"]
+    assert cpl.dns_resolve("nope.shop.svc.cluster.local") is None
+    assert cpl.dns_resolve("example.com") is False
+    q = dns.query("cart.shop.svc.cluster.local")
+    qid, flags, labels, qtype, qclass, question = dns.parse_query(q)
+    assert labels == ["cart", "shop", "svc", "cluster", "local"] and qtype == 1
+    assert dns.parse_reply(dns.build_reply(qid, flags, question, 0, ["127.96.0.9"])) == (0, ["127.96.0.9"])
+    assert dns.parse_reply(dns.build_reply(qid, flags, question, dns.NXDOMAIN, [])) == (dns.NXDOMAIN, [])

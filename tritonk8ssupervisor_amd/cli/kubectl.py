@@ -1,9 +1,14 @@
 """Minimal kubectl for the tk8s control plane (the CLI half of docs/detailed.md:285-370).
 
-  kubectl get nodes|pods|ds|jobs|deploy|svc|events [-n NS | -A] [-l k=v] [-o wide|json|yaml]
+  kubectl get nodes|pods|ds|jobs|deploy|svc|cm|secrets|ing|events [-n NS | -A] [-l k=v] [-o wide|json|yaml]
   kubectl describe node NAME | pod NAME
   kubectl create|apply -f FILE        kubectl delete -f FILE | KIND NAME
-  kubectl logs POD [--tail N]         kubectl cordon|uncordon NODE
+  kubectl create configmap|secret generic NAME --from-literal k=v --from-file [k=]PATH
+  kubectl scale deploy/NAME --replicas N
+  kubectl rollout status|restart deploy/NAME
+  kubectl label|annotate KIND NAME k=v k-
+  kubectl logs POD [--tail N]         kubectl cordon|uncordon|drain NODE
+  kubectl top nodes                   (amd.com/gpu in use, hotspot temperature, power, VRAM)
   kubectl wait job/NAME [--timeout S] kubectl cluster-info | version
 
 The kubeconfig comes from --kubeconfig, $KUBECONFIG, or <workdir>/.tk8s/kubeconfig.json (written
@@ -12,6 +17,7 @@ by setup; the same document the control plane serves at /env/<env>/kubernetes/ku
 from __future__ import annotations
 
 import argparse
+import base64
 import json
 import os
 import sys
@@ -22,7 +28,8 @@ import yaml
 
 from ..controlplane.client import ApiError, client_from_kubeconfig
 from ..kube import (apply_objects, collection_path, delete_objects, job_state, kind_key, load_manifests,
-                    object_path, wait_job)
+                    object_path, wait_job, wait_rollout)
+from ..utils.net import host_port
 
 GPU = "amd.com/gpu"
 
@@ -107,7 +114,8 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
                 f"{o.get('status', {}).get('readyReplicas', 0)}/{o['spec'].get('replicas', 1)}", _age(o)] for o in items]
     elif k == "service":
         def ports(o):
-            return ",".join(f"{p['port']}" + (f":{p['nodePort']}" if p.get("nodePort") else "") + f"/{p.get('protocol', 'TCP')}"
+            return ",".join(f"{p['port']}" + (f"(host {host_port(p['port'])})" if host_port(p["port"]) != p["port"] else "")
+                            + (f":{p['nodePort']}" if p.get("nodePort") else "") + f"/{p.get('protocol', 'TCP')}"
                             for p in o["spec"].get("ports", []))
 
         def ext(o):
@@ -117,6 +125,15 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
         rows = [["NAME", "TYPE", "CLUSTER-IP", "EXTERNAL-IP", "PORT(S)", "AGE"]] + [[
             o["metadata"]["name"], o["spec"].get("type", "ClusterIP"), o["spec"].get("clusterIP", ""), ext(o), ports(o), _age(o)]
             for o in items]
+    elif k in ("configmap", "secret"):
+        rows = [["NAME"] + (["TYPE"] if k == "secret" else []) + ["DATA", "AGE"]] + [
+            [o["metadata"]["name"]] + ([o.get("type", "Opaque")] if k == "secret" else [])
+            + [str(len(o.get("data") or {})), _age(o)] for o in items]
+    elif k == "ingress":
+        rows = [["NAME", "HOSTS", "ADDRESS", "AGE"]] + [[
+            o["metadata"]["name"], ",".join(r.get("host", "*") or "*" for r in o.get("spec", {}).get("rules") or []) or "*",
+            ",".join(i.get("ip", "") for i in o.get("status", {}).get("loadBalancer", {}).get("ingress", [])), _age(o)]
+            for o in items]
     elif k == "event":
         rows = [["TYPE", "REASON", "OBJECT", "MESSAGE"]] + [[o.get("type", ""), o.get("reason", ""),
                 f"{o.get('involvedObject', {}).get('kind', '').lower()}/{o.get('involvedObject', {}).get('name', '')}",
@@ -125,6 +142,64 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
         rows = [["NAME", "AGE"]] + [[o["metadata"]["name"], _age(o)] for o in items]
     if all_ns and len(rows) > 1:
         rows = [["NAMESPACE"] + rows[0]] + [[o["metadata"].get("namespace", "")] + r for o, r in zip(items, rows[1:])]
+    return _table(rows)
+
+
+def _target(args: list[str]) -> tuple[str, str]:
+    """KIND/NAME or KIND NAME."""
+    if not args:
+        raise SystemExit("error: a resource (KIND/NAME or KIND NAME) is required")
+    if "/" in args[0]:
+        what, name = args[0].split("/", 1)
+        return what, name
+    if len(args) < 2:
+        raise SystemExit("error: a resource name is required")
+    return args[0], args[1]
+
+
+def _create_data(k, a, ns: str) -> int:
+    """kubectl create configmap NAME / create secret generic NAME (--from-literal, --from-file)."""
+    secret = a.args[0] == "secret"
+    rest = a.args[1:]
+    if secret and rest and rest[0] == "generic":
+        rest = rest[1:]
+    if not rest:
+        raise SystemExit("usage: kubectl create configmap|secret generic NAME --from-literal k=v --from-file [k=]PATH")
+    data: dict[str, str] = {}
+    for kv in a.from_literal:
+        key, _, val = kv.partition("=")
+        data[key] = val
+    for spec in a.from_file:
+        key, _, path = spec.partition("=") if "=" in spec else (Path(spec).name, "", spec)
+        data[key] = Path(path).read_text()
+    body = {"apiVersion": "v1", "kind": "Secret" if secret else "ConfigMap", "metadata": {"name": rest[0]}}
+    if secret:
+        body.update(type="Opaque", data={key: base64.b64encode(v.encode()).decode() for key, v in data.items()})
+    else:
+        body["data"] = data
+    k.post(k.k8s(collection_path("secret" if secret else "configmap", ns)), body)
+    print(f"{'secret' if secret else 'configmap'}/{rest[0]} created")
+    return 0
+
+
+def fmt_top(nodes: list[dict], pods: list[dict]) -> str:
+    """Per node: amd.com/gpu in use / allocatable and the last AMD SMI sample of its GPUs."""
+    used: dict[str, int] = {}
+    for p in pods:
+        nn = p["spec"].get("nodeName")
+        if nn and p.get("status", {}).get("phase") not in ("Succeeded", "Failed"):
+            used[nn] = used.get(nn, 0) + sum(int(c.get("resources", {}).get("limits", {}).get(GPU, 0) or 0)
+                                             for c in p["spec"].get("containers", []))
+    rows = [["NAME", "GPU(USED/ALLOC)", "HOTSPOT-MAX", "POWER", "VRAM-USED"]]
+    for n in nodes:
+        tel = [d.get("telemetry") or {} for d in n["status"].get("devices", [])]
+        hot = [t["temp_c"]["hotspot"] for t in tel if "hotspot" in t.get("temp_c", {})]
+        watts = [t["power"]["current_w"] for t in tel if "current_w" in t.get("power", {})]
+        vram = [t["vram_used_bytes"] for t in tel if "vram_used_bytes" in t]
+        name = n["metadata"]["name"]
+        rows.append([name, f"{used.get(name, 0)}/{n['status']['allocatable'].get(GPU, '0')}",
+                     f"{max(hot)}C" if hot else "-", f"{sum(watts):.0f}W" if watts else "-",
+                     f"{sum(vram) / 2**30:.1f}GiB" if vram else "-"])
     return _table(rows)
 
 
@@ -160,6 +235,10 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("-f", "--filename")
     ap.add_argument("--tail", type=int, default=0)
     ap.add_argument("--timeout", default="300s")
+    ap.add_argument("--replicas", type=int)
+    ap.add_argument("--from-literal", action="append", default=[])
+    ap.add_argument("--from-file", action="append", default=[])
+    ap.add_argument("--ignore-daemonsets", action="store_true")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     a = ap.parse_args(argv)
@@ -187,9 +266,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             if what == "node":
                 items = k.get(k.k8s("/api/v1/nodes"), query=q)["items"]
             elif a.all_namespaces:
-                path = {"pod": "/api/v1/pods", "event": "/api/v1/events", "daemonset": "/apis/apps/v1/daemonsets",
-                        "job": "/apis/batch/v1/jobs"}.get(what)
-                items = k.get(k.k8s(path), query=q)["items"] if path else []
+                path = "/api/v1/pods" if what == "pod" else collection_path(what).replace("/namespaces/default", "")
+                items = k.get(k.k8s(path), query=q)["items"]
             else:
                 items = k.get(k.k8s(collection_path(what, ns)), query=q)["items"]
             if a.output in ("json", "yaml"):
@@ -215,10 +293,67 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                                               for c in st.get("conditions", [])))
             if what == "pod":
                 print(f"Node:         {o['spec'].get('nodeName')}\nStatus:       {st.get('phase')}")
+        elif a.verb == "create" and a.args and a.args[0] in ("configmap", "cm", "secret"):
+            return _create_data(k, a, ns)
         elif a.verb in ("create", "apply"):
+            if not a.filename:
+                raise SystemExit("error: must specify -f FILE")
             res = apply_objects(k, load_manifests(a.filename))
             for r in res:
-                print(f"{r['kind'].lower()}/{r['name']} {'created' if r['created'] else 'unchanged'}")
+                print(f"{r['kind'].lower()}/{r['name']} {r['action'] if a.verb == 'apply' else ('created' if r['created'] else 'unchanged')}")
+        elif a.verb == "scale":
+            what, name = _target(a.args)
+            if a.replicas is None or kind_key(what) != "deployment":
+                raise SystemExit("usage: kubectl scale deploy/NAME --replicas N")
+            k.request("PATCH", k.k8s(object_path("deployment", name, ns) + "/scale"), body={"spec": {"replicas": a.replicas}})
+            print(f"deployment.apps/{name} scaled")
+        elif a.verb == "rollout":
+            sub = a.args[0] if a.args else ""
+            what, name = _target(a.args[1:])
+            if kind_key(what) != "deployment" or sub not in ("status", "restart"):
+                raise SystemExit("usage: kubectl rollout status|restart deploy/NAME")
+            if sub == "restart":  # a new template annotation = a new pod-template-hash = a rolling update
+                k.request("PATCH", k.k8s(object_path("deployment", name, ns)), body={"spec": {"template": {"metadata": {
+                    "annotations": {"kubectl.kubernetes.io/restartedAt": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}}}}})
+                print(f"deployment.apps/{name} restarted")
+                return 0
+
+            def progress(d):
+                st, want = d.get("status", {}), d["spec"].get("replicas", 1)
+                print(f'Waiting for deployment "{name}" rollout to finish: {st.get("updatedReplicas", 0)} of {want} '
+                      f'updated replicas are available...', flush=True)
+
+            wait_rollout(k, name, ns, timeout=float(a.timeout.rstrip("s")), progress=progress)
+            print(f'deployment "{name}" successfully rolled out')
+        elif a.verb in ("label", "annotate"):
+            what, name = _target(a.args)
+            pairs = a.args[1:] if "/" in a.args[0] else a.args[2:]
+            field = "labels" if a.verb == "label" else "annotations"
+            patch = {}
+            for kv in pairs:
+                if kv.endswith("-") and "=" not in kv:
+                    patch[kv[:-1]] = None
+                else:
+                    key, _, val = kv.partition("=")
+                    patch[key] = val
+            path = f"/api/v1/nodes/{name}" if kind_key(what) == "node" else object_path(what, name, ns)
+            k.request("PATCH", k.k8s(path), body={"metadata": {field: patch}})
+            print(f"{kind_key(what)}/{name} {'labeled' if a.verb == 'label' else 'annotated'}")
+        elif a.verb == "drain":
+            node = a.args[0]
+            k.request("PATCH", k.k8s(f"/api/v1/nodes/{node}"), body={"spec": {"unschedulable": True}})
+            print(f"node/{node} cordoned")
+            for p in k.get(k.k8s("/api/v1/pods"), query={"fieldSelector": f"spec.nodeName={node}"})["items"]:
+                owners = {r.get("kind") for r in p["metadata"].get("ownerReferences", [])}
+                if "DaemonSet" in owners or p.get("status", {}).get("phase") in ("Succeeded", "Failed"):
+                    continue
+                k.delete(k.k8s(object_path("pod", p["metadata"]["name"], p["metadata"]["namespace"])))
+                print(f"evicting pod {p['metadata']['namespace']}/{p['metadata']['name']}")
+            print(f"node/{node} drained")
+        elif a.verb == "top":
+            if not a.args or kind_key(a.args[0]) != "node":
+                raise SystemExit("usage: kubectl top nodes")
+            print(fmt_top(k.get(k.k8s("/api/v1/nodes"))["items"], k.get(k.k8s("/api/v1/pods"))["items"]))
         elif a.verb == "delete":
             if a.filename:
                 n = delete_objects(k, load_manifests(a.filename))

@@ -28,7 +28,10 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import base64
+import binascii
 import copy
+import hashlib
 import html
 import json
 import os
@@ -38,12 +41,16 @@ import sys
 import time
 from pathlib import Path
 
+from ..utils.net import host_port
 from .httpserver import HttpError, HttpServer, Request, Response, Router
 from .store import Store, now_iso
 
 GPU = "amd.com/gpu"
 VALIDATION_LABEL = "tk8s.amd.com/validation"
 TERMINAL = ("Succeeded", "Failed")
+KIND_GROUPS = (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1"), ("configmaps", "/api/v1"),
+               ("secrets", "/api/v1"), ("daemonsets", "/apis/apps/v1"), ("deployments", "/apis/apps/v1"),
+               ("jobs", "/apis/batch/v1"), ("ingresses", "/apis/networking.k8s.io/v1"))
 
 
 def _key(*parts: str) -> str:
@@ -90,6 +97,45 @@ def pod_gpus(p: dict) -> int:
     return total
 
 
+def merge_patch(target, patch):
+    """RFC 7386 JSON merge patch (what kubectl's merge and strategic-merge patches reduce to here:
+    maps merge key by key, ``null`` deletes, lists are replaced whole)."""
+    if not isinstance(patch, dict):
+        return copy.deepcopy(patch)
+    out = copy.deepcopy(target) if isinstance(target, dict) else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch(out.get(k), v)
+    return out
+
+
+def template_hash(template: dict) -> str:
+    """``pod-template-hash`` of a Deployment's pod template (names its ReplicaSet generation)."""
+    return hashlib.sha1(json.dumps(template, sort_keys=True, separators=(",", ":")).encode()).hexdigest()[:10]
+
+
+def _normalize_data(kind: str, body: dict) -> None:
+    """ConfigMap data must be strings; Secret ``stringData`` folds into base64 ``data``."""
+    if kind == "configmaps":
+        data = body.get("data") or {}
+        if not isinstance(data, dict) or not all(isinstance(v, str) for v in data.values()):
+            raise HttpError(422, "ConfigMap data must map keys to strings")
+        body["data"] = data
+    elif kind == "secrets":
+        data = dict(body.get("data") or {})
+        for k, v in (body.pop("stringData", None) or {}).items():
+            data[k] = base64.b64encode(str(v).encode()).decode()
+        for k, v in data.items():
+            try:
+                base64.b64decode(str(v), validate=True)
+            except (binascii.Error, ValueError) as e:
+                raise HttpError(422, f"Secret data[{k!r}] is not valid base64: {e}") from e
+        body["data"] = data
+        body.setdefault("type", "Opaque")
+
+
 def labels_match(selector: dict | None, labels: dict | None) -> bool:
     if not selector:
         return True
@@ -99,7 +145,7 @@ def labels_match(selector: dict | None, labels: dict | None) -> bool:
 
 class ControlPlane:
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
-                 advertise: str | None = None):
+                 advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port
         self.advertise = advertise
         self.state_dir = Path(state_dir) if state_dir else None
@@ -115,7 +161,12 @@ class ControlPlane:
         self._again = False
         from .proxy import ServiceProxy
 
+        from .ingress import IngressController
+
         self.proxy = ServiceProxy(self._endpoints, log=lambda m: self._log_error(m + "\n"))
+        self.ingress = IngressController(self._ingress_routes, self._endpoints, log=lambda m: self._log_error(m + "\n"))
+        self.dns_port = host_port(53) if dns_port is None else dns_port          # 0 disables
+        self.ingress_port = host_port(80) if ingress_port is None else ingress_port
         self._routes()
 
     # ---- utilities --------------------------------------------------------------------
@@ -184,6 +235,7 @@ class ControlPlane:
         r.add("GET", r"/v1/scripts/(?P<token>[^/]+)", self.h_script)
         r.add("POST", r"/v1/scripts/(?P<token>[^/]+)", self.h_register)
         r.add("GET", r"/r/projects/(?P<pid>[^/]+)/kubernetes-dashboard:9090/?", self.h_dashboard)
+        r.add("POST", r"/r/projects/(?P<pid>[^/]+)/kubernetes-dashboard:9090/api/v1/appdeployment", self.h_app_deploy)
         r.add("GET", r"/env/(?P<pid>[^/]+)/kubernetes/kubectl", self.h_kubeconfig)
         r.add("GET", r"/env/(?P<pid>[^/]+)/infra/containers", self.h_containers)
         # KV + cluster readiness
@@ -205,16 +257,16 @@ class ControlPlane:
             add("DELETE", r"/api/v1/nodes/(?P<name>[^/]+)", self.h_node_delete)
             add("GET", r"/api/v1/namespaces", self.h_namespaces)
             add("GET", r"/api/v1/pods", self.h_pods)
-            for kind, grp in (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1"),
-                              ("daemonsets", "/apis/apps/v1"), ("deployments", "/apis/apps/v1"),
-                              ("jobs", "/apis/batch/v1")):
+            for kind, grp in KIND_GROUPS:
                 add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._lister(kind))
                 add("POST", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._creator(kind))
                 add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._getter(kind))
+                add("PUT", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._replacer(kind, False))
+                add("PATCH", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._replacer(kind, True))
                 add("DELETE", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._deleter(kind))
-            add("GET", r"/api/v1/events", self._lister("events", all_ns=True))
-            add("GET", r"/apis/apps/v1/daemonsets", self._lister("daemonsets", all_ns=True))
-            add("GET", r"/apis/batch/v1/jobs", self._lister("jobs", all_ns=True))
+                add("GET", grp + rf"/{kind}", self._lister(kind, all_ns=True))
+            for method in ("GET", "PUT", "PATCH"):
+                add(method, r"/apis/apps/v1/namespaces/(?P<ns>[^/]+)/deployments/(?P<name>[^/]+)/scale", self.h_scale)
             add("PUT", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/status", self.h_pod_status)
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/log", self.h_pod_log)
 
@@ -380,15 +432,82 @@ class ControlPlane:
         s = self.summary(p["id"])
         if s["nodes_ready"] == 0:
             return Response(503, "Service Unavailable", content_type="text/plain")
+        esc = html.escape
         rows = "".join(
-            f"<tr><td>{html.escape(n['metadata']['name'])}</td><td>{'Ready' if node_ready(n) else 'NotReady'}</td>"
+            f"<tr><td>{esc(n['metadata']['name'])}</td><td>{'Ready' if node_ready(n) else 'NotReady'}</td>"
             f"<td>{n['status']['allocatable'].get(GPU, '0')}</td><td>{'yes' if node_validated(n) else 'no'}</td></tr>"
             for n in self.store.list("nodes", lambda n: self._in(p['id'], n)))
-        body = (f"<html><head><title>Kubernetes Dashboard - {html.escape(p['name'])}</title></head><body>"
-                f"<h1>kubernetes dashboard</h1><p>environment {html.escape(p['name'])} ({p['id']})</p>"
-                f"<table><tr><th>node</th><th>status</th><th>{GPU}</th><th>validated</th></tr>{rows}</table>"
-                f"<pre>{html.escape(json.dumps(s, indent=1))}</pre></body></html>")
+        deps = "".join(
+            f"<tr><td>{esc(d['metadata']['namespace'])}</td><td>{esc(d['metadata']['name'])}</td>"
+            f"<td>{d.get('status', {}).get('readyReplicas', 0)}/{d['spec'].get('replicas', 1)}</td>"
+            f"<td>{esc(', '.join(c.get('image', '') or ' '.join(c.get('command', [])) for c in d['spec']['template']['spec']['containers']))}</td></tr>"
+            for d in self.store.list("deployments", lambda o: self._in(p['id'], o)))
+        svcs = "".join(
+            f"<tr><td>{esc(o['metadata']['name'])}</td><td>{o['spec'].get('type')}</td><td>{o['spec'].get('clusterIP')}</td>"
+            f"<td>{esc(','.join(i.get('ip', '') for i in o.get('status', {}).get('loadBalancer', {}).get('ingress', [])))}</td>"
+            f"<td>{esc(','.join(str(x['port']) for x in o['spec'].get('ports', [])))}</td></tr>"
+            for o in self.store.list("services", lambda o: self._in(p['id'], o)))
+        body = (f"<html><head><title>Kubernetes Dashboard - {esc(p['name'])}</title></head><body>"
+                f"<h1>kubernetes dashboard</h1><p>environment {esc(p['name'])} ({p['id']})</p>"
+                f"<h2>Nodes</h2><table><tr><th>node</th><th>status</th><th>{GPU}</th><th>validated</th></tr>{rows}</table>"
+                f"<h2>Deployments</h2><table><tr><th>namespace</th><th>name</th><th>ready</th><th>image</th></tr>{deps}</table>"
+                f"<h2>Services</h2><table><tr><th>name</th><th>type</th><th>cluster IP</th><th>external IP</th>"
+                f"<th>ports</th></tr>{svcs}</table>"
+                "<h2>Deploy a containerized app</h2><form id='deploy'>"
+                "<input name='name' placeholder='App name'> <input name='containerImage' placeholder='Container image'> "
+                "<input name='replicas' value='1' size='3'> <input name='port' placeholder='Port'> "
+                "<label><input type='checkbox' name='isExternal'> external</label> "
+                f"<input name='gpus' value='0' size='3'> {GPU} <button>Deploy</button></form>"
+                "<script>document.getElementById('deploy').addEventListener('submit', async (e) => {"
+                "e.preventDefault(); const f = new FormData(e.target); const port = f.get('port');"
+                "const body = {name: f.get('name'), containerImage: f.get('containerImage'),"
+                " replicas: parseInt(f.get('replicas') || '1'), isExternal: f.get('isExternal') === 'on',"
+                " gpuRequirement: parseInt(f.get('gpus') || '0'), namespace: 'default',"
+                " portMappings: port ? [{port: parseInt(port), targetPort: parseInt(port), protocol: 'TCP'}] : []};"
+                "await fetch('api/v1/appdeployment', {method: 'POST', headers: {'Content-Type': 'application/json'},"
+                " body: JSON.stringify(body)}); location.reload(); });</script>"
+                f"<pre>{esc(json.dumps(s, indent=1))}</pre></body></html>")
         return Response(200, body, content_type="text/html; charset=utf-8")
+
+    async def h_app_deploy(self, req: Request, pid: str):
+        """The dashboard's "Deploy a containerized app" form (kubernetes-dashboard
+        ``POST api/v1/appdeployment``): a Deployment plus, with port mappings, a Service --
+        how the reference's walkthrough launched Ghost (docs/detailed.md:261-283). Like the
+        Rancher 1.x UI the reference used, the dashboard needs no API token."""
+        import shlex
+
+        p = self.project(pid)
+        b = req.json()
+        name = str(b.get("name") or "").strip()
+        image = str(b.get("containerImage") or "").strip()
+        if not name or not image:
+            raise HttpError(422, "name and containerImage are required")
+        ns = b.get("namespace") or "default"
+        labels = {"app": name, **{str(lb["key"]): str(lb["value"]) for lb in b.get("labels") or []}}
+        c = {"name": name, "image": image}
+        if b.get("containerCommand"):
+            c["command"] = shlex.split(str(b["containerCommand"]))
+        if b.get("containerCommandArgs"):
+            c["args"] = shlex.split(str(b["containerCommandArgs"]))
+        if b.get("variables"):
+            c["env"] = [{"name": str(v["name"]), "value": str(v.get("value", ""))} for v in b["variables"]]
+        if int(b.get("gpuRequirement") or 0):
+            c["resources"] = {"limits": {GPU: int(b["gpuRequirement"])}}
+        ports = b.get("portMappings") or []
+        if ports:
+            c["ports"] = [{"containerPort": int(m["targetPort"]), "protocol": m.get("protocol", "TCP")} for m in ports]
+        dep = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": name, "labels": dict(labels)},
+               "spec": {"replicas": int(b.get("replicas", 1)), "selector": {"matchLabels": {"app": name}},
+                        "template": {"metadata": {"labels": labels}, "spec": {"containers": [c]}}}}
+        out = {"deployment": self._strip(self.create(p["id"], "deployments", ns, dep))}
+        if ports:
+            svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": {"app": name}},
+                   "spec": {"type": "LoadBalancer" if b.get("isExternal") else "ClusterIP", "selector": {"app": name},
+                            "ports": [{"name": f"{m.get('protocol', 'TCP').lower()}-{m['port']}-{m['targetPort']}",
+                                       "port": int(m["port"]), "targetPort": int(m["targetPort"]),
+                                       "protocol": m.get("protocol", "TCP")} for m in ports]}}
+            out["service"] = self._strip(self.create(p["id"], "services", ns, svc))
+        return Response(201, out)
 
     async def h_kubeconfig(self, req: Request, pid: str):
         p = self.project(pid)
@@ -584,10 +703,11 @@ class ControlPlane:
 
         def fn(n):
             md = body.get("metadata", {})
-            n["metadata"].setdefault("labels", {}).update(md.get("labels", {}))
-            n["metadata"].setdefault("annotations", {}).update(md.get("annotations", {}))
+            for f in ("labels", "annotations"):
+                if f in md:
+                    n["metadata"][f] = merge_patch(n["metadata"].get(f, {}), md[f] or {})
             if "spec" in body:
-                n["spec"].update(body["spec"])
+                n["spec"] = merge_patch(n["spec"], body["spec"])
 
         n = self.store.patch("nodes", _key(p, name), fn)
         if n is None:
@@ -612,7 +732,7 @@ class ControlPlane:
     async def h_namespaces(self, req: Request, pid: str | None = None):
         self._pid(pid, req)
         names = {"default", "kube-system", "amd-gpu"}
-        for kind in ("pods", "daemonsets", "jobs", "deployments", "services"):
+        for kind in ("pods", "daemonsets", "jobs", "deployments", "services", "configmaps", "secrets", "ingresses"):
             names |= {o["metadata"].get("namespace", "default") for o in self.store.list(kind)}
         return {"kind": "NamespaceList", "items": [{"metadata": {"name": n}} for n in sorted(names)]}
 
@@ -652,6 +772,35 @@ class ControlPlane:
             return Response(201, self._strip(self.create(p, kind, ns, body)))
         return h
 
+    def _replacer(self, kind: str, merge: bool):
+        async def h(req: Request, ns: str, name: str, pid: str | None = None):
+            p = self._pid(pid, req)
+            self._auth(req, self.project(p))
+            body = req.json()
+            if not isinstance(body, dict):
+                raise HttpError(422, "the body must be a JSON object")
+            return self._strip(self.replace(p, kind, ns, name, body, merge=merge))
+        return h
+
+    async def h_scale(self, req: Request, ns: str, name: str, pid: str | None = None):
+        """The Deployment ``scale`` subresource (autoscaling/v1 Scale): kubectl scale."""
+        p = self._pid(pid, req)
+        d = self.store.get("deployments", _key(p, ns, name))
+        if d is None:
+            raise HttpError(404, f'deployments.apps "{name}" not found')
+        if req.method in ("PUT", "PATCH"):
+            self._auth(req, self.project(p))
+            n = (req.json().get("spec") or {}).get("replicas")
+            if not isinstance(n, int) or isinstance(n, bool) or n < 0:
+                raise HttpError(422, "spec.replicas must be a non-negative integer")
+            d = self.replace(p, "deployments", ns, name, {"spec": {"replicas": n}}, merge=True)
+        sel = (d["spec"].get("selector") or {}).get("matchLabels") or {}
+        return {"kind": "Scale", "apiVersion": "autoscaling/v1",
+                "metadata": {"name": name, "namespace": ns, "resourceVersion": d["metadata"]["resourceVersion"]},
+                "spec": {"replicas": int(d["spec"].get("replicas", 1))},
+                "status": {"replicas": int(d.get("status", {}).get("replicas", 0)),
+                           "selector": ",".join(f"{k}={v}" for k, v in sel.items())}}
+
     def _deleter(self, kind: str):
         async def h(req: Request, ns: str, name: str, pid: str | None = None):
             p = self._pid(pid, req)
@@ -659,7 +808,7 @@ class ControlPlane:
             o = self.store.delete(kind, _key(p, ns, name))
             if o is None:
                 raise HttpError(404, f'{kind} "{name}" not found')
-            if kind == "services":
+            if kind in ("services", "ingresses"):
                 self._sync_proxy()
             if kind != "pods":
                 for pod in self.store.list("pods", lambda x: self._in(p, x) and any(
@@ -679,7 +828,7 @@ class ControlPlane:
                 return c
         raise HttpError(507, "pod CIDR space exhausted")
 
-    def _alloc_service(self, body: dict) -> None:
+    def _alloc_service(self, body: dict, exclude: str | None = None) -> None:
         spec = body.setdefault("spec", {})
         stype = spec.setdefault("type", "ClusterIP")
         if stype not in ("ClusterIP", "NodePort", "LoadBalancer"):
@@ -687,7 +836,8 @@ class ControlPlane:
         ports = spec.get("ports") or []
         if not ports:
             raise HttpError(422, "spec.ports is required")
-        svcs = self.store.list("services")
+        svcs = [o for o in self.store.list("services")
+                if _key(o["_project"], o["metadata"]["namespace"], o["metadata"]["name"]) != exclude]
         used_ips = {o["spec"].get("clusterIP") for o in svcs}
         used_np = {p.get("nodePort") for o in svcs for p in o["spec"].get("ports", [])}
         used_lb = {(p.get("port")) for o in svcs if o["spec"].get("type") == "LoadBalancer" for p in o["spec"].get("ports", [])}
@@ -727,7 +877,7 @@ class ControlPlane:
                 tp = next((cp.get("containerPort") for c in o["spec"].get("containers", [])
                            for cp in c.get("ports", []) if cp.get("name") == tp), None)
             if ip and tp:
-                out.append((ip, int(tp)))
+                out.append((ip, host_port(int(tp))))
         return sorted(out)
 
     def _proxy_wanted(self) -> dict:
@@ -737,12 +887,12 @@ class ControlPlane:
             key = _key(svc["_project"], svc["metadata"]["namespace"], svc["metadata"]["name"])
             spec = svc["spec"]
             for p in spec.get("ports", []):
-                wanted[(key, spec["clusterIP"], int(p["port"]))] = p["name"]
+                wanted[(key, spec["clusterIP"], host_port(p["port"]))] = p["name"]
                 if spec.get("type") in ("NodePort", "LoadBalancer") and p.get("nodePort"):
                     for h in {lb_host, "127.0.0.1"}:
                         wanted[(key, h, int(p["nodePort"]))] = p["name"]
                 if spec.get("type") == "LoadBalancer":
-                    wanted[(key, lb_host, int(p["port"]))] = p["name"]
+                    wanted[(key, lb_host, host_port(p["port"]))] = p["name"]
         return wanted
 
     def _sync_proxy(self) -> None:
@@ -751,6 +901,71 @@ class ControlPlane:
         except RuntimeError:
             return
         loop.create_task(self.proxy.sync(self._proxy_wanted()))
+        if self.ingress_port:
+            loop.create_task(self.ingress.ensure(self.advertise or self.host, self.ingress_port,
+                                                 bool(self.store.keys("ingresses"))))
+
+    def _ingress_routes(self) -> list[tuple[str, str, str, str, str]]:
+        """(host, path, pathType, service key, service port key) of every Ingress rule."""
+        routes = []
+        for ing in self.store.list("ingresses"):
+            pid, ns = ing["_project"], ing["metadata"]["namespace"]
+
+            def backend(b):
+                svc = (b or {}).get("service") or {}
+                key = _key(pid, ns, svc.get("name", ""))
+                o = self.store.get("services", key)
+                port = svc.get("port") or {}
+                for sp in (o or {}).get("spec", {}).get("ports", []):
+                    if sp.get("name") == port.get("name") or sp.get("port") == port.get("number"):
+                        return key, sp["name"]
+                return None
+
+            spec = ing.get("spec", {})
+            for rule in spec.get("rules") or []:
+                for path in (rule.get("http") or {}).get("paths") or []:
+                    b = backend(path.get("backend"))
+                    if b:
+                        routes.append((rule.get("host", ""), path.get("path", "/"), path.get("pathType", "Prefix"), *b))
+            b = backend(spec.get("defaultBackend"))
+            if b:
+                routes.append(("", "/", "Prefix", *b))
+        return routes
+
+    def dns_resolve(self, name: str):
+        """Cluster DNS answer for ``name``: [ips], None (NXDOMAIN) or False (REFUSED)."""
+        from .dns import DOMAIN
+
+        name = name.rstrip(".").lower()
+        if name.endswith("." + DOMAIN):
+            parts = name[: -len(DOMAIN) - 1].split(".")
+        elif name.endswith(".svc"):
+            parts = name.split(".")
+        elif name.count(".") == 1 and any(o["metadata"].get("namespace") == name.split(".")[1]
+                                          for kind in ("services", "pods") for o in self.store.list(kind)):
+            parts = name.split(".")  # <svc>.<ns> short form, for namespaces the cluster has
+        else:
+            return False
+        if len(parts) == 3 and parts[2] == "pod":
+            ip = parts[0].replace("-", ".")
+            try:
+                import ipaddress
+
+                ipaddress.IPv4Address(ip)
+                return [ip]
+            except ValueError:
+                return None
+        if parts and parts[-1] == "svc":
+            parts = parts[:-1]
+        if len(parts) != 2:
+            return None
+        svc, ns = parts
+        projects = sorted(self.store.list("projects"), key=lambda p: p["created_seq"])
+        for p in projects:
+            o = self.store.get("services", _key(p["id"], ns, svc))
+            if o and o["spec"].get("clusterIP"):
+                return [o["spec"]["clusterIP"]]
+        return None
 
     def create(self, pid: str, kind: str, ns: str, body: dict) -> dict:
         md = body.setdefault("metadata", {})
@@ -778,10 +993,70 @@ class ControlPlane:
             if not tmpl.get("spec", {}).get("containers"):
                 raise HttpError(422, "spec.template.spec.containers is required")
             body.setdefault("status", {})
+            md["generation"] = 1
         elif kind == "services":
             self._alloc_service(body)
+        elif kind in ("configmaps", "secrets"):
+            _normalize_data(kind, body)
+        elif kind == "ingresses":
+            body["status"] = {"loadBalancer": {"ingress": [{"ip": self.advertise or self.host}]}}
         o = self.store.put(kind, key, body)
+        if kind in ("services", "ingresses"):
+            self._sync_proxy()
+        self.reconcile()
+        return o
+
+    def replace(self, pid: str, kind: str, ns: str, name: str, body: dict, merge: bool = False) -> dict:
+        """PUT (``merge=False``: the whole object, optimistic concurrency on resourceVersion) or
+        PATCH (``merge=True``: RFC 7386 merge patch). Status stays server-owned; identity fields,
+        a Service's clusterIP and a Job's / Pod's spec are immutable, as in Kubernetes."""
+        key = _key(pid, ns, name)
+        cur = self.store.get(kind, key)
+        if cur is None:
+            raise HttpError(404, f'{kind} "{name}" not found')
+        if merge:
+            new = merge_patch(self._strip(cur), body)
+        else:
+            rv = (body.get("metadata") or {}).get("resourceVersion")
+            if rv and rv != cur["metadata"].get("resourceVersion"):
+                raise HttpError(409, f'Operation cannot be fulfilled on {kind} "{name}": the object has been '
+                                     "modified; please apply your changes to the latest version and try again")
+            new = copy.deepcopy(body)
+        if "status" in cur:
+            new["status"] = copy.deepcopy(cur["status"])
+        md = new.setdefault("metadata", {})
+        md.update(name=name, namespace=ns, uid=cur["metadata"]["uid"],
+                  creationTimestamp=cur["metadata"].get("creationTimestamp"))
+        md.pop("resourceVersion", None)
+        md.setdefault("labels", {})
+        md.setdefault("annotations", {})
+        spec_changed = new.get("spec") != cur.get("spec")
+        if kind == "pods" and spec_changed:
+            raise HttpError(422, f'Pod "{name}" is invalid: spec: Forbidden: pod updates may not change '
+                                 "fields other than metadata")
+        if kind == "jobs" and new.get("spec", {}).get("template") != cur.get("spec", {}).get("template"):
+            raise HttpError(422, f'Job.batch "{name}" is invalid: spec.template: field is immutable')
+        if kind in ("daemonsets", "deployments", "jobs"):
+            if not new.get("spec", {}).get("template", {}).get("spec", {}).get("containers"):
+                raise HttpError(422, "spec.template.spec.containers is required")
+            gen = int(cur["metadata"].get("generation", 1))
+            md["generation"] = gen + 1 if spec_changed else gen
         if kind == "services":
+            spec = new.setdefault("spec", {})
+            cip = cur["spec"].get("clusterIP")
+            if spec.get("clusterIP") and spec["clusterIP"] != cip:
+                raise HttpError(422, f'Service "{name}" is invalid: spec.clusterIP: field is immutable')
+            spec["clusterIP"] = cip
+            old_np = {(p.get("port"), p.get("protocol", "TCP")): p.get("nodePort") for p in cur["spec"].get("ports", [])}
+            for port in spec.get("ports") or []:
+                if not port.get("nodePort") and old_np.get((port.get("port"), port.get("protocol", "TCP"))):
+                    port["nodePort"] = old_np[(port.get("port"), port.get("protocol", "TCP"))]
+            self._alloc_service(new, exclude=key)
+        if kind in ("configmaps", "secrets"):
+            _normalize_data(kind, new)
+        new["_project"] = pid
+        o = self.store.put(kind, key, new)
+        if kind in ("services", "ingresses"):
             self._sync_proxy()
         self.reconcile()
         return o
@@ -978,19 +1253,46 @@ class ControlPlane:
                 self.store.patch("jobs", _key(pid, ns, jname), lambda o, s=status: o.__setitem__("status", s))
 
     def _ctl_deployments(self, pid: str) -> None:
+        """Deployment controller with ReplicaSet-style generations: pods carry the
+        ``pod-template-hash`` of the template they came from. A changed template rolls out with
+        the RollingUpdate defaults (maxSurge 25 % rounded up, maxUnavailable 25 % rounded down;
+        an old pod goes only when a new one runs), ``strategy: Recreate`` drops the old pods first."""
         for d in self.store.list("deployments", lambda o: self._in(pid, o)):
             ns, dname = d["metadata"]["namespace"], d["metadata"]["name"]
-            want = int(d["spec"].get("replicas", 1))
-            pods = [o for o in self._owned(pid, d) if o.get("status", {}).get("phase") not in TERMINAL]
-            for _ in range(want - len(pods)):
-                self._seq += 1
-                self._new_pod(pid, ns, f"{dname}-{self._seq:x}", d, "Deployment", d["spec"]["template"],
-                              labels=d["spec"].get("selector", {}).get("matchLabels"))
-            for o in sorted(pods, key=lambda o: o["metadata"]["name"])[want:]:
-                self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
-            pods = self._owned(pid, d)
-            status = {"replicas": want, "readyReplicas": sum(1 for o in pods if o.get("status", {}).get("phase") == "Running"),
-                      "availableReplicas": sum(1 for o in pods if o.get("status", {}).get("phase") == "Running")}
+            spec = d["spec"]
+            want = int(spec.get("replicas", 1))
+            h = template_hash(spec["template"])
+            match = (spec.get("selector") or {}).get("matchLabels") or {}
+
+            def live():
+                return [o for o in self._owned(pid, d) if o.get("status", {}).get("phase") not in TERMINAL]
+
+            unavailable = want // 4
+            for _ in range(2):  # scale down old -> room to surge again, in the same pass
+                pods = live()
+                new = [o for o in pods if o["metadata"].get("labels", {}).get("pod-template-hash") == h]
+                old = [o for o in pods if o not in new]
+                if (spec.get("strategy") or {}).get("type") == "Recreate" and old:
+                    for o in old:
+                        self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                    pods, old = new, []
+                surge = max(1, -(-want // 4)) if old else 0
+                for _ in range(max(0, min(want - len(new), want + surge - len(pods)))):
+                    self._seq += 1
+                    new.append(self._new_pod(pid, ns, f"{dname}-{h[:8]}-{self._seq:x}", d, "Deployment",
+                                             spec["template"], labels={**match, "pod-template-hash": h}))
+                ready_new = sum(1 for o in new if o.get("status", {}).get("phase") == "Running")
+                keep_old = max(0, want - unavailable - ready_new)
+                for o in sorted(old, key=lambda o: o["metadata"]["name"])[keep_old:]:
+                    self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                for o in sorted(new, key=lambda o: o["metadata"]["name"])[want:]:
+                    self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+            pods = live()
+            running = sum(1 for o in pods if o.get("status", {}).get("phase") == "Running")
+            status = {"observedGeneration": int(d["metadata"].get("generation", 1)), "replicas": len(pods),
+                      "updatedReplicas": sum(1 for o in pods if o["metadata"].get("labels", {}).get("pod-template-hash") == h),
+                      "readyReplicas": running, "availableReplicas": running,
+                      "unavailableReplicas": max(0, want - running)}
             if d.get("status") != status:
                 self.store.patch("deployments", _key(pid, ns, dname), lambda o, s=status: o.__setitem__("status", s))
 
@@ -1088,6 +1390,17 @@ class ControlPlane:
         self.port = port
         if self.store.keys("services"):
             await self.proxy.sync(self._proxy_wanted())  # services restored from a snapshot
+        if self.store.keys("ingresses") and self.ingress_port:
+            await self.ingress.ensure(self.advertise or self.host, self.ingress_port, True)
+        dns_transport = None
+        if self.dns_port:
+            from .dns import DnsProtocol
+
+            try:
+                dns_transport, _ = await asyncio.get_running_loop().create_datagram_endpoint(
+                    lambda: DnsProtocol(self.dns_resolve), local_addr=(self.advertise or self.host, self.dns_port))
+            except OSError as e:
+                self._log_error(f"cluster DNS: cannot listen on udp {self.advertise or self.host}:{self.dns_port}: {e}\n")
         tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop())]
         # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
         print(f"Listening on {host}:{port}", flush=True)
@@ -1103,6 +1416,9 @@ class ControlPlane:
         for t in tasks:
             t.cancel()
         await self.proxy.close()
+        await self.ingress.close()
+        if dns_transport is not None:
+            dns_transport.close()
         if self.state_dir:
             self.store.snapshot(self.state_dir / "controlplane.json")
         await self.http.close()
@@ -1127,8 +1443,12 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--state-dir", default=None)
     ap.add_argument("--node-grace", type=float, default=float(os.environ.get("TK8S_NODE_GRACE", "5")))
     ap.add_argument("--ready-file", default=None)
+    ap.add_argument("--dns-port", type=int, default=None, help="cluster DNS (UDP) port; 0 disables (default 53, "
+                    "shifted when not root)")
+    ap.add_argument("--ingress-port", type=int, default=None, help="ingress controller port; 0 disables (default 80, "
+                    "shifted when not root)")
     a = ap.parse_args(argv)
-    cp = ControlPlane(a.host, a.port, a.state_dir, a.node_grace, a.advertise)
+    cp = ControlPlane(a.host, a.port, a.state_dir, a.node_grace, a.advertise, a.dns_port, a.ingress_port)
     asyncio.run(cp.run(a.ready_file))
     return 0
 

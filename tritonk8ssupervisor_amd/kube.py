@@ -5,6 +5,7 @@ waits for conditions with the control plane's long-poll watch (no sleep loops).
 """
 from __future__ import annotations
 
+import copy
 import time
 from pathlib import Path
 
@@ -19,10 +20,14 @@ KINDS = {
     "daemonset": ("DaemonSet", "/apis/apps/v1", "daemonsets"),
     "deployment": ("Deployment", "/apis/apps/v1", "deployments"),
     "job": ("Job", "/apis/batch/v1", "jobs"),
+    "configmap": ("ConfigMap", "/api/v1", "configmaps"),
+    "secret": ("Secret", "/api/v1", "secrets"),
+    "ingress": ("Ingress", "/apis/networking.k8s.io/v1", "ingresses"),
 }
 ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", "ds": "daemonset",
            "daemonsets": "daemonset", "deploy": "deployment", "deployments": "deployment", "jobs": "job",
-           "ev": "event", "events": "event", "no": "node", "nodes": "node"}
+           "ev": "event", "events": "event", "no": "node", "nodes": "node", "cm": "configmap",
+           "configmaps": "configmap", "secrets": "secret", "ing": "ingress", "ingresses": "ingress"}
 
 
 def kind_key(kind: str) -> str:
@@ -57,21 +62,48 @@ def load_manifests(path: str | Path, variables: dict | None = None) -> list[dict
     return out
 
 
+def is_subset(want, have) -> bool:
+    """Does the live object already carry every field the manifest sets? (server-side defaults
+    such as a Service's clusterIP or nodePorts do not count as a difference)."""
+    if isinstance(want, dict):
+        return isinstance(have, dict) and all(is_subset(v, have.get(k)) for k, v in want.items())
+    if isinstance(want, list):
+        return isinstance(have, list) and len(want) == len(have) and all(is_subset(a, b) for a, b in zip(want, have))
+    return want == have or (want is not None and have is not None and str(want) == str(have))
+
+
 def apply_objects(k: Client, objs: list[dict]) -> list[dict]:
+    """``kubectl apply``: create, or update an existing object to the manifest (PUT with the live
+    resourceVersion; status and server-allocated fields are kept by the control plane)."""
     res = []
     for o in objs:
         kind = o.get("kind", "")
         if kind.lower() == "namespace":
-            res.append({"kind": kind, "name": o["metadata"]["name"], "created": False})
+            res.append({"kind": kind, "name": o["metadata"]["name"], "created": False, "action": "unchanged"})
             continue
         ns = o.get("metadata", {}).get("namespace", "default")
+        name = o["metadata"].get("name")
         try:
             k.post(k.k8s(collection_path(kind, ns)), o)
-            res.append({"kind": kind, "name": o["metadata"].get("name"), "created": True})
+            res.append({"kind": kind, "name": name, "created": True, "action": "created"})
+            continue
         except ApiError as e:
             if e.status != 409:
                 raise
-            res.append({"kind": kind, "name": o["metadata"].get("name"), "created": False})
+        path = k.k8s(object_path(kind, name, ns))
+        cur = k.get(path)
+        want = {key: v for key, v in o.items() if key not in ("apiVersion", "kind", "status")}
+        if is_subset(want, cur):
+            action = "unchanged"
+        else:
+            body = copy.deepcopy(o)
+            md = body.setdefault("metadata", {})
+            md["resourceVersion"] = cur["metadata"]["resourceVersion"]
+            for f in ("labels", "annotations"):  # apply merges map fields it does not mention
+                md[f] = {**cur["metadata"].get(f, {}), **(md.get(f) or {})}
+            k.put(path, body)
+            action = "configured"
+        res.append({"kind": kind, "name": name, "created": False, "action": action})
     return res
 
 
@@ -112,6 +144,33 @@ def wait_job(k: Client, name: str, ns: str = "default", timeout: float = 300.0) 
             raise TimeoutError(f"job {ns}/{name} not finished after {timeout}s")
         rv = max(rv, int(job["metadata"]["resourceVersion"]))
         rv, _ = k.watch(path, rv, timeout=min(left, 20.0))
+
+
+def rollout_complete(d: dict) -> bool:
+    st, want = d.get("status", {}), int(d["spec"].get("replicas", 1))
+    return (int(st.get("observedGeneration", 0)) >= int(d["metadata"].get("generation", 1))
+            and st.get("updatedReplicas", 0) == want and st.get("replicas", 0) == want
+            and st.get("readyReplicas", 0) == want)
+
+
+def wait_rollout(k: Client, name: str, ns: str = "default", timeout: float = 300.0, progress=None) -> dict:
+    """Block (long-poll watch) until every replica of the Deployment runs the current template."""
+    deadline = time.monotonic() + timeout
+    path = k.k8s(collection_path("deployment", ns))
+    last = None
+    while True:
+        d = k.get(k.k8s(object_path("deployment", name, ns)))
+        if rollout_complete(d):
+            return d
+        st = d.get("status", {})
+        msg = (st.get("updatedReplicas", 0), st.get("readyReplicas", 0), st.get("replicas", 0))
+        if progress is not None and msg != last:
+            progress(d)
+        last = msg
+        left = deadline - time.monotonic()
+        if left <= 0:
+            raise TimeoutError(f"deployment {ns}/{name} not rolled out after {timeout}s")
+        k.watch(path, int(d["metadata"]["resourceVersion"]), timeout=min(left, 20.0))
 
 
 def pods_of(k: Client, label_selector: str, ns: str = "default") -> list[dict]:
