@@ -28,10 +28,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
-import base64
-import binascii
 import copy
-import hashlib
 import html
 import json
 import os
@@ -113,11 +110,16 @@ def merge_patch(target, patch):
 
 def template_hash(template: dict) -> str:
     """``pod-template-hash`` of a Deployment's pod template (names its ReplicaSet generation)."""
+    import hashlib  # off the control plane's start-up path (it is on the bring-up's)
+
     return hashlib.sha1(json.dumps(template, sort_keys=True, separators=(",", ":")).encode()).hexdigest()[:10]
 
 
 def _normalize_data(kind: str, body: dict) -> None:
     """ConfigMap data must be strings; Secret ``stringData`` folds into base64 ``data``."""
+    import base64
+    import binascii
+
     if kind == "configmaps":
         data = body.get("data") or {}
         if not isinstance(data, dict) or not all(isinstance(v, str) for v in data.values()):
@@ -1392,7 +1394,15 @@ class ControlPlane:
             await self.proxy.sync(self._proxy_wanted())  # services restored from a snapshot
         if self.store.keys("ingresses") and self.ingress_port:
             await self.ingress.ensure(self.advertise or self.host, self.ingress_port, True)
-        dns_transport = None
+
+        tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop())]
+        # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
+        print(f"Listening on {host}:{port}", flush=True)
+        if ready_file:
+            from ..utils.fsutil import atomic_write_json
+
+            atomic_write_json(ready_file, {"host": host, "port": port, "pid": os.getpid(), "base": self.base})
+        dns_transport = None  # after "Listening on": not on the bring-up's critical path
         if self.dns_port:
             from .dns import DnsProtocol
 
@@ -1401,13 +1411,6 @@ class ControlPlane:
                     lambda: DnsProtocol(self.dns_resolve), local_addr=(self.advertise or self.host, self.dns_port))
             except OSError as e:
                 self._log_error(f"cluster DNS: cannot listen on udp {self.advertise or self.host}:{self.dns_port}: {e}\n")
-        tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop())]
-        # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
-        print(f"Listening on {host}:{port}", flush=True)
-        if ready_file:
-            from ..utils.fsutil import atomic_write_json
-
-            atomic_write_json(ready_file, {"host": host, "port": port, "pid": os.getpid(), "base": self.base})
         self._stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         for sig in (signal.SIGTERM, signal.SIGINT):
