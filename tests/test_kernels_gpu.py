@@ -241,6 +241,39 @@ def test_setup_on_a_real_gpu(tmp_path):
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
 
+def test_setup_with_grpc_device_plugin_and_rccl_on_a_real_gpu(tmp_path):
+    """The kubelet device-plugin API path on real hardware: the agent serves amd.com/gpu over gRPC
+    v1beta1 (real KFD inventory, NUMA topology from sysfs), allocates the validation pod and the
+    RCCL rank through it, and the rank finds its GPU as --device $(TK8S_GPU_DEVICE)."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, TK8S_DEVICE_PLUGIN="grpc")
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120",
+                            "--rccl", "on", "--rccl-max-bytes", str(4 << 20)],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1 and s["rccl"]["ok"]
+        log = (tmp_path / ".tk8s" / "machines" / "kubenode1" / "logs" / "agent.log").read_text()
+        assert "via gRPC v1beta1" in log, log[-2000:]
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
 def test_torch_rccl_allreduce_single_rank(tmp_path):
     """The PyTorch (RCCL) twin of tk8s-rccl, rendezvous through a real control-plane KV."""
     import subprocess
