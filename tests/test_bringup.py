@@ -103,6 +103,8 @@ def test_setup_ready_and_clean_teardown(ws, n):
     for i in range(1, n + 1):
         burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
         assert burn["ok"] and burn["probed"] == 1
+        # >= 2 GPUs: one host-level burn-in (the runtime starts once) split per machine
+        assert burn.get("host_burnin", False) == (n >= 2)
     # teardown: machines gone, every artefact removed -- including the env-id file the
     # reference never cleans (setup.sh:513 removes ./tmp/* instead of ansible/tmp/*)
     (ws / "ansible" / "tmp" / ".keep").touch()  # the repository's tracked placeholder
@@ -392,3 +394,21 @@ def test_pod_gpu_env_visibility_modes():
     assert pod_gpu_env(alloc, [5]) == alloc
     node = pod_gpu_env(alloc, [5, 6], "node")
     assert node == {"TK8S_GPU_DEVICES": "5,6", "TK8S_GPU_DEVICE": "5"}
+
+
+def test_host_burnin_split_per_machine():
+    from tritonk8ssupervisor_amd.burnin import split_host_result
+
+    res = {"ok": False, "md5_expected": "x", "timings_ms": {"hip_init": 50.0},
+           "devices": [{"device": i, "ok": i != 2, "hbm": {"gbps": 6000.0 + i}} for i in range(3)],
+           "gpuinfo": {"ok": True, "devices": [{"index": i, "pci_bus_id": f"0000:{i:02x}:00.0"} for i in range(3)],
+                       "links": [[{"type": "self" if a == b else "xgmi", "ab": (a, b)} for b in range(3)] for a in range(3)]}}
+    gpus = [1, 4, 6]  # host indices the burn-in process saw as its devices 0, 1, 2
+    one = split_host_result(res, gpus, [4])
+    assert one["ok"] and one["probed"] == 1 and one["devices"][0]["host_index"] == 4 and one["devices"][0]["device"] == 0
+    assert one["hbm"]["gbps"] == 6001.0 and one["gpuinfo"]["devices"][0]["pci_bus_id"] == "0000:01:00.0"
+    assert one["gpuinfo"]["links"] == [[{"type": "self", "ab": (1, 1)}]] and one["host_burnin"]
+    two = split_host_result(res, gpus, [6, 1])
+    assert not two["ok"] and [d["host_index"] for d in two["devices"]] == [6, 1]
+    assert two["gpuinfo"]["links"][0][1]["ab"] == (2, 0)
+    assert split_host_result(res, gpus, [5]) is None and split_host_result({}, gpus, [1]) is None

@@ -274,6 +274,38 @@ def test_setup_with_grpc_device_plugin_and_rccl_on_a_real_gpu(tmp_path):
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
 
+def test_setup_with_host_burnin_on_a_real_gpu(tmp_path):
+    """The host-level burn-in (one tk8s-probe for every worker GPU, split per machine) on real
+    hardware; TK8S_HOST_BURNIN=force uses it for a single GPU too."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, TK8S_HOST_BURNIN="force")
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120"],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1
+        burn = json.loads((tmp_path / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json").read_text())
+        assert burn["ok"] and burn["host_burnin"] and burn["devices"][0]["host_index"] == 0
+        assert burn["md5"]["digest"] == burn["md5_expected"] and burn["gpuinfo"]["devices"][0]["gfx"] == "gfx950"
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
 def test_torch_rccl_allreduce_single_rank(tmp_path):
     """The PyTorch (RCCL) twin of tk8s-rccl, rendezvous through a real control-plane KV."""
     import subprocess

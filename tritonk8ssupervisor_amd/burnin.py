@@ -22,6 +22,8 @@ def start_burnin(ex, host: str, command: list, out: str = "run/gpu-burnin.json",
     pending = mdir / (out + ".pending")
     if (mdir / out).exists() or ex.daemon_status(host, name).get("running"):
         return {"changed": False, "msg": "GPU burn-in already started", "gpus": gpus, "out": out}
+    if pending.exists() and _pid_alive(pending):
+        return {"changed": False, "msg": "GPU burn-in pending (host-level burn-in)", "gpus": gpus, "out": out}
     pending.parent.mkdir(parents=True, exist_ok=True)
     pending.touch()
     denv = dict(compose_visible_devices(gpus))
@@ -39,3 +41,177 @@ def start_burnin(ex, host: str, command: list, out: str = "run/gpu-burnin.json",
         # the pid lets `--reuse` stop waiting if the burn-in dies without a result
         pending.write_text(f"{info.get('pid', 0)}\n")
     return {"changed": True, "pid": info.get("pid"), "gpus": gpus, "out": out}
+
+
+def _pid_alive(pidfile: Path) -> bool:
+    try:
+        pid = int(pidfile.read_text().split()[0])
+    except (OSError, ValueError, IndexError):
+        return False
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except (OSError, IndexError):
+        return True
+
+
+def split_host_result(result: dict, burnin_gpus: list[int], machine_gpus: list[int]) -> dict | None:
+    """One machine's share of a host burn-in: the entries of its GPUs, renumbered in the order
+    the machine sees them (its pods' device i = machine_gpus[i]). None if any GPU is missing."""
+    pos = {g: i for i, g in enumerate(burnin_gpus)}
+    if not machine_gpus or any(g not in pos for g in machine_gpus):
+        return None
+    devs = {d.get("device"): d for d in result.get("devices", [])}
+    info = result.get("gpuinfo") or {}
+    infos = {d.get("index"): d for d in info.get("devices", [])}
+    links = info.get("links") or []
+    sub_devs, sub_info = [], []
+    for i, g in enumerate(machine_gpus):
+        d = devs.get(pos[g])
+        if d is None:
+            return None
+        sub_devs.append({**d, "device": i, "host_index": g})
+        if pos[g] in infos:
+            sub_info.append({**infos[pos[g]], "index": i, "host_index": g})
+    idx = [pos[g] for g in machine_gpus]
+    sub_links = [[links[a][b] for b in idx] for a in idx] if links and max(idx) < len(links) else []
+    first = sub_devs[0]
+    out = {"ok": all(d.get("ok") for d in sub_devs), "device": 0, "device_count": len(sub_devs),
+           "probed": len(sub_devs), "devices": sub_devs, "host_burnin": True, "host_burnin_gpus": burnin_gpus,
+           "timings_ms": result.get("timings_ms", {}),
+           "gpuinfo": {**{k: v for k, v in info.items() if k not in ("devices", "links")}, "device_count": len(sub_info),
+                       "devices": sub_info, "links": sub_links}}
+    for key in ("hbm", "md5", "copy"):
+        if key in first:
+            out[key] = first[key]
+    if "md5_expected" in result:
+        out["md5_expected"] = result["md5_expected"]
+    return out
+
+
+class HostBurnin:
+    """One burn-in process for every GPU the workers of a bring-up are about to receive.
+
+    A GPU process's runtime start is host-wide work serialised across processes: on the MI355X
+    box hsa_init takes ~50 ms alone, ~90 / ~130-150 / ~200-240 ms when 2 / 4 / 8 processes start
+    together, and the same with no GPU visible at all (profiles/r1_conc/): so N per-machine
+    burn-ins at N workers would cost N-fold start-up contention on the bring-up's critical path.
+    This launcher starts ONE ``tk8s-probe --all-devices`` over the predicted GPU set (the runtime
+    starts once; one host thread per GPU), and when it exits hands every machine its own share:
+    ``<sandbox>/run/gpu-burnin.json`` with exactly that machine's GPUs, which the machine's
+    validation pod then reuses (``--reuse``). Until then the machine's ``.pending`` marker names
+    this (the setup) process, so a pod waits while the split is outstanding and probes by itself
+    if the setup dies. A machine whose GPUs the burn-in did not cover gets no file and probes
+    itself -- nothing is ever skipped, only shared.
+    """
+
+    def __init__(self, command: list, gpus: list[int], state_dir: Path, env: dict | None = None,
+                 out: str = "run/gpu-burnin.json", log=None):
+        self.command = [str(a) for a in command]
+        self.gpus = list(gpus)
+        self.state_dir = Path(state_dir)
+        self.env = env or {}
+        self.out = out
+        self.log = log or (lambda *_a, **_k: None)
+        self.result_path = self.state_dir / "run" / "host-burnin.json"
+        self.pidfile = self.state_dir / "run" / "host-burnin.pid"
+        self.proc = None
+        self.done = False
+        self.result: dict | None = None
+        self.machines: dict[str, tuple[Path, list[int]]] = {}
+        import threading
+
+        self.lock = threading.Lock()
+        self.finished = threading.Event()
+
+    def start(self) -> bool:
+        import subprocess
+        import threading
+
+        from .models.hostinfo import compose_visible_devices
+
+        if os.sep in self.command[0] and not os.access(self.command[0], os.X_OK):
+            return False
+        self.result_path.parent.mkdir(parents=True, exist_ok=True)
+        self.result_path.unlink(missing_ok=True)
+        env = dict(os.environ)
+        env.update(compose_visible_devices(self.gpus))
+        env["NODE_NAME"] = "host"
+        env.update({str(k): str(v) for k, v in self.env.items()})
+        log = open(self.state_dir / "run" / "host-burnin.log", "ab")
+        try:
+            self.proc = subprocess.Popen(self.command + ["--out", str(self.result_path)], env=env, stdin=subprocess.DEVNULL,
+                                         stdout=subprocess.DEVNULL, stderr=log, start_new_session=True)
+        except OSError:
+            return False
+        finally:
+            log.close()
+        self.pidfile.write_text(f"{self.proc.pid}\n")
+        threading.Thread(target=self._wait, name="host-burnin", daemon=True).start()
+        return True
+
+    def register(self, name: str, sandbox: str, gpus: list[int]) -> bool:
+        """A machine just booted: take its share when ready. False: not covered (probe yourself)."""
+        if not gpus or any(g not in self.gpus for g in gpus):
+            return False
+        mdir = Path(sandbox)
+        pending = mdir / (self.out + ".pending")
+        pending.parent.mkdir(parents=True, exist_ok=True)
+        with self.lock:
+            if self.done:
+                self._deliver(name, mdir, gpus)
+                return True
+            pending.write_text(f"{os.getpid()}\n")  # alive until the share is delivered
+            self.machines[name] = (mdir, list(gpus))
+        return True
+
+    def _deliver(self, name: str, mdir: Path, gpus: list[int]) -> None:
+        from .utils.fsutil import atomic_write_json
+
+        share = split_host_result(self.result, self.gpus, gpus) if self.result else None
+        if share is not None and not (os.environ.get("TK8S_FAKE_GPUS") and
+                                      os.environ.get("TK8S_FAKE_BURNIN_CRASH") == name):
+            atomic_write_json(mdir / self.out, share)
+            self.log("gpu_burnin_shared", name=name, gpus=gpus, ok=share["ok"])
+        (mdir / (self.out + ".pending")).unlink(missing_ok=True)
+
+    def _wait(self) -> None:
+        import json
+
+        rc = self.proc.wait()
+        result = None
+        try:
+            result = json.loads(self.result_path.read_text())
+        except (OSError, ValueError):
+            pass
+        with self.lock:
+            self.result, self.done = result, True
+            for name, (mdir, gpus) in self.machines.items():
+                self._deliver(name, mdir, gpus)
+        self.log("gpu_burnin_host_done", rc=rc, ok=bool(result and result.get("ok")), gpus=self.gpus)
+        self.pidfile.unlink(missing_ok=True)
+        self.finished.set()
+
+    def stop(self) -> None:
+        if self.proc is not None and self.proc.poll() is None:
+            try:
+                os.killpg(self.proc.pid, 15)
+            except OSError:
+                pass
+
+
+def stop_host_burnin(state_dir: Path) -> None:
+    """Teardown: kill a host burn-in a failed or interrupted bring-up left running."""
+    pidfile = Path(state_dir) / "run" / "host-burnin.pid"
+    if _pid_alive(pidfile):
+        try:
+            os.killpg(int(pidfile.read_text().split()[0]), 15)
+        except (OSError, ValueError):
+            pass
+    pidfile.unlink(missing_ok=True)

@@ -69,11 +69,12 @@ def _emit(out, path):
 
 
 def main():
-    if "--reuse" in sys.argv:
+    node = os.environ.get("NODE_NAME") or os.environ.get("TK8S_MACHINE", "-")
+    # a failing node's GPU fails its own validation even when a (host-level) burn-in result exists
+    if "--reuse" in sys.argv and os.environ.get("TK8S_FAKE_PROBE_FAIL", "") != node:
         rc = _reuse(_arg("--reuse"), float(_arg("--reuse-wait", "120")))
         if rc is not None:
             return rc
-    node = os.environ.get("NODE_NAME") or os.environ.get("TK8S_MACHINE", "-")
     if "--out" in sys.argv and os.environ.get("TK8S_FAKE_BURNIN_CRASH", "") == node:
         return 139  # the burn-in dies without a result; the validation pod must probe by itself
     if os.environ.get("TK8S_FAKE_PROBE_HANG", "") == node:

@@ -229,6 +229,7 @@ class Setup:
         self.engine = Engine(ws.tf, self.provider, self.events, on_created=self._machine_booted)
         self.cfg: ClusterConfig | None = None
         self.summary: dict = {}
+        self.host_burnin = None
 
     def banner(self, text: str) -> None:
         self.out("#" * 80)
@@ -283,6 +284,9 @@ class Setup:
         rocmsetup's burn-in task then finds it running and does nothing."""
         if not (self.validate and m.gpus and hasattr(self.provider, "machine_env")):
             return
+        if self.host_burnin is not None and self.host_burnin.register(m.name, m.sandbox, list(m.gpus)):
+            self.events.emit("gpu_burnin_shared_pending", name=m.name, gpus=list(m.gpus))
+            return
         from .burnin import start_burnin
 
         ex = MachineExecutor(self.provider, {m.name: m})
@@ -299,6 +303,7 @@ class Setup:
                                cfg.node_networks(), cfg.HOST_PACKAGE)
         if not (ws.tf / "rancher.tf").exists() or not self.resume:
             atomic_write(ws.tf / "rancher.tf", text)
+        self._start_host_burnin()
         self.out("Generating terraform configs for environment...")
         self.out(f"    Master hostname: {cfg.RANCHER_MASTER_HOSTNAME}")
         for i, n in enumerate(cfg.node_names(), 1):
@@ -311,6 +316,26 @@ class Setup:
             for a, e in res.failed.items():
                 self.out(f"    {a}: {e}")
             raise SetupError("Terraform had too many errors. Make sure you haven't reached your provisioning limit.")
+
+    def _start_host_burnin(self) -> None:
+        """>= 2 GPUs about to be handed out: one burn-in process for all of them (burnin.HostBurnin:
+        the runtime start is host-wide and serialised across processes, so N per-machine burn-ins
+        would stack N starts on the critical path). Machines not covered fall back to their own."""
+        if not (self.validate and hasattr(self.provider, "predict_gpus")) or os.environ.get("TK8S_HOST_BURNIN", "1") == "0":
+            return
+        try:
+            pkg = self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE)
+            gpus = self.provider.predict_gpus(int(pkg.gpus or 0), int(self.cfg.KUBERNETES_NUMBER_OF_NODES))
+        except Exception:  # noqa: BLE001 - prediction is an optimisation only
+            return
+        if len(gpus) < (1 if os.environ.get("TK8S_HOST_BURNIN") == "force" else 2):
+            return
+        from .burnin import HostBurnin
+
+        hb = HostBurnin(self._validation_command(), gpus, self.ws.state_dir, log=self.events.emit)
+        if hb.start():
+            self.host_burnin = hb
+            self.events.emit("gpu_burnin_host_started", gpus=gpus, pid=hb.proc.pid)
 
     def ansible_config(self) -> None:
         """createAnsibleConfigs (setup.sh:116-137)."""
@@ -610,6 +635,9 @@ def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out: Callable[[s
         out("Please answer yes or no.")
     backend = backend or (read_config(ws.config).TK8S_BACKEND if ws.config.exists() else os.environ.get("TK8S_BACKEND", "local"))
     provider = get_provider(backend, ws.state_dir)
+    from .burnin import stop_host_burnin
+
+    stop_host_burnin(ws.state_dir)
     if (ws.tf / "rancher.tf").exists() or (ws.tf / "terraform.tfstate").exists():
         out("    destroying machines...")
         try:

@@ -151,6 +151,31 @@ class LocalProvider(Provider):
             alloc["gpus"][str(g)] = name
         return pick
 
+    def predict_gpus(self, per_machine: int, machines: int) -> list[int]:
+        """The GPUs ``machines`` creates of ``per_machine`` GPUs each will take from what is free
+        now (the same topology-aware picks as _alloc_gpus, made one after another)."""
+        if per_machine <= 0 or machines <= 0:
+            return []
+        alloc = read_json(self.alloc_file, {}) or {}
+        taken = {int(k) for k in alloc.get("gpus", {})}
+        inv = discover()
+        free = [g.ordinal for g in inv.gpus if g.ordinal not in taken]
+        out: list[int] = []
+        try:
+            from ..agent.deviceplugin import link_matrix
+            from ..ops import topo
+
+            w = link_matrix(inv.links)
+            for _ in range(machines):
+                if len(free) < per_machine:
+                    break
+                pick = list(topo().preferred_allocation(inv.count, w, free, [], per_machine)["devices"])
+                out += pick
+                free = [g for g in free if g not in pick]
+        except Exception:  # noqa: BLE001 - allocator module optional
+            out = free[: per_machine * machines]
+        return sorted(out)
+
     # ---- lifecycle ----------------------------------------------------------------
     def create_machine(self, name: str, package: str, networks: list[str], image: str = "",
                        root_authorized_keys: str = "", tags: dict | None = None) -> Machine:
