@@ -42,7 +42,15 @@ namespace {
 
 constexpr const char* kKnownDigest256M = "55af80380d572d36cc8cc7d50edd90ab";
 
-bool ok_of(const std::string& j) { return j.find("\"ok\":true") != std::string::npos; }
+// The result's own "ok" is its first key (every writer puts it first); whitespace-tolerant.
+bool ok_of(const std::string& j) {
+  auto p = j.find("\"ok\"");
+  if (p == std::string::npos) return false;
+  p = j.find(':', p + 4);
+  if (p == std::string::npos) return false;
+  p = j.find_first_not_of(" \t\r\n", p + 1);
+  return p != std::string::npos && j.compare(p, 4, "true") == 0;
+}
 
 std::string field(const std::string& j, const std::string& key) {
   const std::string pat = "\"" + key + "\":\"";

@@ -94,6 +94,8 @@ def test_setup_ready_and_clean_teardown(ws, n):
     items = json.loads(r.stdout)["items"]
     assert sorted(i["metadata"]["name"] for i in items) == [f"kubenode{i}" for i in range(1, n + 1)]
     assert all(i["status"]["allocatable"]["amd.com/gpu"] == "1" for i in items)
+    # the validation pods' results (shared from the host burn-in for n >= 2) reach the nodes
+    assert all(i["metadata"]["annotations"].get("tk8s.amd.com/hbm-write-gbps") == "6200.0" for i in items)
     # distinct GPUs per worker
     ids = [i["status"]["devices"][0]["id"] for i in items]
     assert len(set(ids)) == n

@@ -172,12 +172,16 @@ class HostBurnin:
         return True
 
     def _deliver(self, name: str, mdir: Path, gpus: list[int]) -> None:
-        from .utils.fsutil import atomic_write_json
+        import json
+
+        from .utils.fsutil import atomic_write
 
         share = split_host_result(self.result, self.gpus, gpus) if self.result else None
         if share is not None and not (os.environ.get("TK8S_FAKE_GPUS") and
                                       os.environ.get("TK8S_FAKE_BURNIN_CRASH") == name):
-            atomic_write_json(mdir / self.out, share)
+            # the probe's own format: one compact line, "ok" first (what --reuse prints and the
+            # agent parses as the pod's result)
+            atomic_write(mdir / self.out, json.dumps(share, separators=(",", ":")) + "\n")
             self.log("gpu_burnin_shared", name=name, gpus=gpus, ok=share["ok"])
         (mdir / (self.out + ".pending")).unlink(missing_ok=True)
 
