@@ -137,6 +137,7 @@ class HostBurnin:
         from .models.hostinfo import compose_visible_devices
 
         if os.sep in self.command[0] and not os.access(self.command[0], os.X_OK):
+            self._finish(None, -1)
             return False
         self.result_path.parent.mkdir(parents=True, exist_ok=True)
         self.result_path.unlink(missing_ok=True)
@@ -149,6 +150,7 @@ class HostBurnin:
             self.proc = subprocess.Popen(self.command + ["--out", str(self.result_path)], env=env, stdin=subprocess.DEVNULL,
                                          stdout=subprocess.DEVNULL, stderr=log, start_new_session=True)
         except OSError:
+            self._finish(None, -1)
             return False
         finally:
             log.close()
@@ -194,6 +196,10 @@ class HostBurnin:
             result = json.loads(self.result_path.read_text())
         except (OSError, ValueError):
             pass
+        self._finish(result, rc)
+
+    def _finish(self, result: dict | None, rc: int) -> None:
+        """Hand every registered machine its share (or release it to probe by itself)."""
         with self.lock:
             self.result, self.done = result, True
             for name, (mdir, gpus) in self.machines.items():

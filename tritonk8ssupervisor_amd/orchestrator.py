@@ -330,12 +330,18 @@ class Setup:
             return
         if len(gpus) < (1 if os.environ.get("TK8S_HOST_BURNIN") == "force" else 2):
             return
+        import threading
+
         from .burnin import HostBurnin
 
         hb = HostBurnin(self._validation_command(), gpus, self.ws.state_dir, log=self.events.emit)
-        if hb.start():
-            self.host_burnin = hb
-            self.events.emit("gpu_burnin_host_started", gpus=gpus, pid=hb.proc.pid)
+        self.host_burnin = hb  # machines register from now on; the process starts off this thread
+
+        def launch():
+            if hb.start():
+                self.events.emit("gpu_burnin_host_started", gpus=gpus, pid=hb.proc.pid)
+
+        threading.Thread(target=launch, name="host-burnin-start", daemon=True).start()
 
     def ansible_config(self) -> None:
         """createAnsibleConfigs (setup.sh:116-137)."""
