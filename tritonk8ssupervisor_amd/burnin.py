@@ -190,13 +190,25 @@ class HostBurnin:
     def _wait(self) -> None:
         import json
 
-        rc = self.proc.wait()
+        import time
+
+        # The probe writes its result (atomic rename) before it exits, and a GPU process's exit
+        # (runtime teardown, the driver releasing its queues and memory) takes tens of ms more:
+        # hand the shares out the moment the file appears, not when the process is gone.
+        rc = None
+        while not self.result_path.exists():
+            rc = self.proc.poll()
+            if rc is not None:
+                break
+            time.sleep(0.001)
         result = None
         try:
             result = json.loads(self.result_path.read_text())
         except (OSError, ValueError):
             pass
-        self._finish(result, rc)
+        self._finish(result, rc if rc is not None else 0)
+        self.proc.wait()
+        self.pidfile.unlink(missing_ok=True)
 
     def _finish(self, result: dict | None, rc: int) -> None:
         """Hand every registered machine its share (or release it to probe by itself)."""
@@ -205,7 +217,6 @@ class HostBurnin:
             for name, (mdir, gpus) in self.machines.items():
                 self._deliver(name, mdir, gpus)
         self.log("gpu_burnin_host_done", rc=rc, ok=bool(result and result.get("ok")), gpus=self.gpus)
-        self.pidfile.unlink(missing_ok=True)
         self.finished.set()
 
     def stop(self) -> None:
