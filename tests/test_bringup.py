@@ -414,3 +414,8 @@ def test_host_burnin_split_per_machine():
     assert not two["ok"] and [d["host_index"] for d in two["devices"]] == [6, 1]
     assert two["gpuinfo"]["links"][0][1]["ab"] == (2, 0)
     assert split_host_result(res, gpus, [5]) is None and split_host_result({}, gpus, [1]) is None
+    # a failed pull from another machine's GPU does not fail this machine; one inside it does
+    res["devices"][0].update(ok=False, peers=[{"src_device": 1, "dst_device": 0, "ok": False}])
+    assert split_host_result(res, gpus, [1])["ok"]
+    assert split_host_result(res, gpus, [1])["devices"][0]["host_peers"][0]["ok"] is False
+    assert not split_host_result(res, gpus, [1, 4])["ok"]

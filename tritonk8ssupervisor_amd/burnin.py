@@ -72,11 +72,20 @@ def split_host_result(result: dict, burnin_gpus: list[int], machine_gpus: list[i
     infos = {d.get("index"): d for d in info.get("devices", [])}
     links = info.get("links") or []
     sub_devs, sub_info = [], []
+    mine = {pos[g] for g in machine_gpus}
     for i, g in enumerate(machine_gpus):
         d = devs.get(pos[g])
         if d is None:
             return None
-        sub_devs.append({**d, "device": i, "host_index": g})
+        # The machine is judged on its own GPUs: their HBM/MD5/copy checks and the xGMI pulls
+        # between them. Pulls from other machines' GPUs are the fabric's business (the RCCL Job
+        # validates it cluster-wide once every node is Ready); they are kept for the record.
+        peers = [p for p in d.get("peers") or [] if p.get("src_device") in mine]
+        own = all((d.get(k) or {}).get("ok", True) for k in ("hbm", "md5", "copy")) and d.get("digest_ok", True)
+        foreign_bad = any(not p.get("ok") for p in d.get("peers") or [] if p.get("src_device") not in mine)
+        ok = bool(d.get("ok")) or bool(foreign_bad and own and all(p.get("ok") for p in peers) and "error" not in d)
+        sub_devs.append({**d, "device": i, "host_index": g, "ok": ok, "peers": peers,
+                         "host_peers": d.get("peers") or []})
         if pos[g] in infos:
             sub_info.append({**infos[pos[g]], "index": i, "host_index": g})
     idx = [pos[g] for g in machine_gpus]

@@ -334,7 +334,10 @@ class Setup:
 
         from .burnin import HostBurnin
 
-        hb = HostBurnin(self._validation_command(), gpus, self.ws.state_dir, log=self.events.emit)
+        cmd = self._validation_command()
+        if int(pkg.gpus or 0) <= 1:  # no xGMI link inside any machine: the RCCL Job checks the fabric
+            cmd = [a for a in cmd if a != "--peers"]
+        hb = HostBurnin(cmd, gpus, self.ws.state_dir, log=self.events.emit)
         self.host_burnin = hb  # machines register from now on; the process starts off this thread
 
         def launch():
