@@ -221,3 +221,15 @@ def test_triton_provider_without_cli_is_a_clear_error(tmp_path, monkeypatch):
     monkeypatch.setenv("PATH", str(tmp_path))
     with pytest.raises(ProvisionError, match="CLI not found"):
         TritonProvider(tmp_path).networks()
+
+
+def test_pmc_counter_pass_limits():
+    """--rocprof-counters: one --pmc pass holds at most 8 SQ_, 4 TCC_ (FETCH_SIZE = 3), 2 GRBM_
+    ... counters; asking for more makes rocprofv3 hang, so setup refuses before launching."""
+    from tritonk8ssupervisor_amd.orchestrator import SetupError, check_pmc_counters
+
+    check_pmc_counters(["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "GRBM_GUI_ACTIVE", "FETCH_SIZE",
+                        "TCC_HIT_sum", "TCC_HIT_avr"])
+    for bad in ([f"SQ_C{i}" for i in range(9)], ["FETCH_SIZE", "WRITE_SIZE"], ["GRBM_A", "GRBM_B", "GRBM_C"], ["XYZ_A"]):
+        with pytest.raises(SetupError):
+            check_pmc_counters(bad)

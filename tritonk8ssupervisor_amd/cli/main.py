@@ -41,7 +41,8 @@ def cmd_setup(args) -> int:
               validate=not args.no_validate, rccl=(None if args.rccl is None else args.rccl == "on"),
               quiet_ansible=not args.verbose, backend=args.backend, master_port=args.port,
               hbm_bytes=args.hbm_bytes, md5_bytes=args.md5_bytes, probe_iters=args.probe_iters,
-              node_grace=args.node_grace, rocprof=args.rocprof, rccl_max_bytes=args.rccl_max_bytes,
+              node_grace=args.node_grace, rocprof=args.rocprof, rocprof_counters=args.rocprof_counters,
+              rccl_max_bytes=args.rccl_max_bytes,
               rccl_timeout=args.rccl_timeout)
     try:
         summary = s.run()
@@ -231,6 +232,10 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--node-grace", type=float, default=5.0)
     s.add_argument("--rocprof", action="store_true",
                    help="run the RCCL Job's ranks under rocprofv3 --kernel-trace --stats (.tk8s/profiles/)")
+    s.add_argument("--rocprof-counters", default=None, metavar="C1,C2,...",
+                   help="with --rocprof: also collect these PMC counters per kernel (their own --pmc pass "
+                        "with --kernel-trace/--stats only; at most 8 SQ_ and 2 GRBM_ counters), e.g. "
+                        "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE")
     s.add_argument("--rccl-max-bytes", type=int, default=64 << 20)
     s.add_argument("--rccl-timeout", type=float, default=None, help="bound on the RCCL Job (default: --timeout)")
     s.add_argument("--json", action="store_true")

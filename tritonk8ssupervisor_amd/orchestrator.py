@@ -206,7 +206,7 @@ class Setup:
                  out: Callable[[str], None] = None, quiet_ansible: bool = True, hbm_bytes: int = 1 << 30,
                  md5_bytes: int = 256 << 20, probe_iters: int = 3, rccl_max_bytes: int = 64 << 20,
                  node_grace: float = 5.0, backend: str | None = None, master_port: int | None = None,
-                 rocprof: bool = False, rccl_timeout: float | None = None):
+                 rocprof: bool = False, rccl_timeout: float | None = None, rocprof_counters: str | None = None):
         self.ws = ws
         self.answers = answers
         self.assume_yes = assume_yes
@@ -222,6 +222,7 @@ class Setup:
         self.backend = backend or os.environ.get("TK8S_BACKEND", "local")
         self.master_port = master_port
         self.rocprof = rocprof
+        self.rocprof_counters = [c for c in (rocprof_counters or "").replace(" ", ",").split(",") if c]
         self.rccl_timeout = rccl_timeout
         ws.state_dir.mkdir(parents=True, exist_ok=True)
         self.events = EventLog(ws.events, echo=False)
@@ -455,7 +456,11 @@ class Setup:
                 # collection (--pmc) is a separate run by design: never mixed with tracing.
                 prof_dir = self.ws.state_dir / "profiles" / job
                 prof_dir.mkdir(parents=True, exist_ok=True)
-                cmd = [rp, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
+                pmc = []
+                if self.rocprof_counters:  # a counter pass: --pmc with --kernel-trace/--stats only
+                    check_pmc_counters(self.rocprof_counters)
+                    pmc = ["--pmc", *self.rocprof_counters]
+                cmd = [rp, *pmc, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
                        "--output-format", "csv", "--", *cmd]
         objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
                               {"job_name": job, "nranks": g, "rccl_command": cmd})
@@ -554,11 +559,51 @@ class Setup:
         atomic_write_json(self.ws.state_dir / "kubeconfig.json", kc)
 
 
+# Hardware counters one rocprofv3 --pmc pass can hold per block on gfx950 (asking for more makes
+# it fail with "error code 38" and hang). FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2.
+PMC_BLOCK_LIMITS = {"SQ": 8, "TCC": 4, "TCP": 4, "TA": 2, "TD": 2, "GRBM": 2}
+PMC_WEIGHT = {"FETCH_SIZE": ("TCC", 3), "WRITE_SIZE": ("TCC", 2)}
+
+
+def check_pmc_counters(counters: list[str]) -> None:
+    used: dict[str, int] = {}
+    seen = set()
+    for c in counters:
+        base = c.rsplit("_", 1)[0] if c.endswith(("_sum", "_avr", "_min", "_max")) else c
+        if base in seen:  # _sum/_avr/_min/_max of one counter count once
+            continue
+        seen.add(base)
+        block, weight = PMC_WEIGHT.get(base, (base.split("_", 1)[0], 1))
+        if block not in PMC_BLOCK_LIMITS:
+            raise SetupError(f"--rocprof-counters: unknown counter block of {c!r} "
+                             f"(supported: {', '.join(sorted(PMC_BLOCK_LIMITS))})")
+        used[block] = used.get(block, 0) + weight
+        if used[block] > PMC_BLOCK_LIMITS[block]:
+            raise SetupError(f"--rocprof-counters: more than {PMC_BLOCK_LIMITS[block]} {block} counter slots in one "
+                             "pass; split them over several runs")
+
+
 def summarize_rocprof(prof_dir: Path, top: int = 5) -> dict:
-    """Top kernels per rank from rocprofv3 `*_kernel_stats.csv` files under prof_dir."""
+    """Top kernels per rank from rocprofv3 `*_kernel_stats.csv` files under prof_dir, plus the
+    per-kernel counter totals of a --pmc pass (`*_counter_collection.csv`)."""
     import csv
 
     out = {"dir": str(prof_dir), "ranks": {}}
+    counters: dict[str, dict[str, dict[str, float]]] = {}
+    for f in sorted(prof_dir.rglob("*counter_collection.csv")):
+        rank = f.name.split("_counter_collection")[0]
+        with open(f, newline="") as fh:
+            for r in csv.DictReader(fh):
+                k = (r.get("Kernel_Name") or "")[:120]
+                name = r.get("Counter_Name") or ""
+                try:
+                    v = float(r.get("Counter_Value") or 0)
+                except ValueError:
+                    continue
+                per = counters.setdefault(rank, {}).setdefault(k, {})
+                per[name] = per.get(name, 0.0) + v
+    if counters:
+        out["counters"] = counters
     for f in sorted(prof_dir.rglob("*kernel_stats.csv")):
         with open(f, newline="") as fh:
             rows = list(csv.DictReader(fh))
