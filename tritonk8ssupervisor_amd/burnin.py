@@ -116,8 +116,8 @@ class HostBurnin:
     ``<sandbox>/run/gpu-burnin.json`` with exactly that machine's GPUs, which the machine's
     validation pod then reuses (``--reuse``). Until then the machine's ``.pending`` marker names
     this (the setup) process, so a pod waits while the split is outstanding and probes by itself
-    if the setup dies. A machine whose GPUs the burn-in did not cover gets no file and probes
-    itself -- nothing is ever skipped, only shared.
+    if the setup dies. A machine whose GPUs the burn-in did not cover, or whose share did not
+    pass, gets no file and probes itself -- nothing is ever skipped, only shared.
     """
 
     def __init__(self, command: list, gpus: list[int], state_dir: Path, env: dict | None = None,
@@ -188,6 +188,11 @@ class HostBurnin:
         from .utils.fsutil import atomic_write
 
         share = split_host_result(self.result, self.gpus, gpus) if self.result else None
+        if share is not None and not share["ok"]:
+            # Only a passing share is handed out: a failure (or a fault of the shared run itself)
+            # makes the machine's validation pod probe its GPUs on its own, which then decides.
+            self.log("gpu_burnin_share_failed", name=name, gpus=gpus)
+            share = None
         if share is not None and not (os.environ.get("TK8S_FAKE_GPUS") and
                                       os.environ.get("TK8S_FAKE_BURNIN_CRASH") == name):
             # the probe's own format: one compact line, "ok" first (what --reuse prints and the
