@@ -419,3 +419,14 @@ def test_host_burnin_split_per_machine():
     assert split_host_result(res, gpus, [1])["ok"]
     assert split_host_result(res, gpus, [1])["devices"][0]["host_peers"][0]["ok"] is False
     assert not split_host_result(res, gpus, [1, 4])["ok"]
+
+
+def test_failed_host_burnin_falls_back_to_per_machine_probes(ws):
+    """The shared (host-level) burn-in fails as a whole: no machine gets a share, every
+    validation pod probes its own GPU, and the bring-up still completes validated."""
+    s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=_env(TK8S_FAKE_PROBE_FAIL="host")))
+    assert s["nodes_validated"] == 2 and s["gpus_allocatable"] == 2
+    for i in (1, 2):
+        assert not (ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").exists()
+    events = (ws / ".tk8s" / "events.jsonl").read_text()
+    assert "gpu_burnin_share_failed" in events and "gpu_burnin_host_done" in events
