@@ -426,7 +426,8 @@ def test_failed_host_burnin_falls_back_to_per_machine_probes(ws):
     validation pod probes its own GPU, and the bring-up still completes validated."""
     s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=_env(TK8S_FAKE_PROBE_FAIL="host")))
     assert s["nodes_validated"] == 2 and s["gpus_allocatable"] == 2
-    for i in (1, 2):
-        assert not (ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").exists()
+    for i in (1, 2):  # no shared result; at most the machine's own burn-in (rocmsetup) ran
+        f = ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json"
+        assert not f.exists() or not json.loads(f.read_text()).get("host_burnin")
     events = (ws / ".tk8s" / "events.jsonl").read_text()
     assert "gpu_burnin_share_failed" in events and "gpu_burnin_host_done" in events
