@@ -35,22 +35,17 @@
 #include <vector>
 
 #include "args.h"
+#include "reuse.h"
 #include "tk8s/common.h"
 #include "tk8s/probes.h"
+
+using tk8s::exists;
+using tk8s::ok_of;
+using tk8s::reuse;
 
 namespace {
 
 constexpr const char* kKnownDigest256M = "55af80380d572d36cc8cc7d50edd90ab";
-
-// The result's own "ok" is its first key (every writer puts it first); whitespace-tolerant.
-bool ok_of(const std::string& j) {
-  auto p = j.find("\"ok\"");
-  if (p == std::string::npos) return false;
-  p = j.find(':', p + 4);
-  if (p == std::string::npos) return false;
-  p = j.find_first_not_of(" \t\r\n", p + 1);
-  return p != std::string::npos && j.compare(p, 4, "true") == 0;
-}
 
 std::string field(const std::string& j, const std::string& key) {
   const std::string pat = "\"" + key + "\":\"";
@@ -70,41 +65,6 @@ struct DeviceResult {
   double wall_ms = 0, hbm_ms = 0, md5_ms = 0, copy_ms = 0, peers_ms = 0;  // host wall clock per phase
   bool ok = true;
 };
-
-bool exists(const std::string& p) { return access(p.c_str(), F_OK) == 0; }
-
-// pid written into FILE.pending by the launcher (0 / absent: unknown, assume alive).
-bool burnin_alive(const std::string& pending) {
-  std::ifstream f(pending);
-  long pid = 0;
-  if (!(f >> pid) || pid <= 0) return true;
-  if (kill(static_cast<pid_t>(pid), 0) != 0 && errno != EPERM) return false;
-  // An exited burn-in its launcher has not reaped yet is a zombie: dead for our purpose.
-  std::ifstream st("/proc/" + std::to_string(pid) + "/stat");
-  std::string line;
-  if (!std::getline(st, line)) return true;
-  const auto rp = line.rfind(')');
-  return rp == std::string::npos || rp + 2 >= line.size() || line[rp + 2] != 'Z';
-}
-
-// --reuse: print a finished (or still running) burn-in's result. Returns -1 when there is none
-// (no burn-in, or it died without writing a result): the caller then probes itself.
-int reuse(const std::string& file, double wait_s) {
-  const auto t = std::chrono::steady_clock::now();
-  while (!exists(file) && exists(file + ".pending") && ms_since(t) < wait_s * 1e3) {
-    if (!burnin_alive(file + ".pending") && !exists(file)) break;
-    std::this_thread::sleep_for(std::chrono::milliseconds(2));
-  }
-  std::ifstream f(file);
-  if (!f) return -1;
-  std::stringstream ss;
-  ss << f.rdbuf();
-  std::string j = ss.str();
-  while (!j.empty() && (j.back() == '\n' || j.back() == '\r')) j.pop_back();
-  if (j.empty() || j.front() != '{') return -1;
-  std::printf("%s\n", j.c_str());
-  return ok_of(j) ? 0 : 1;
-}
 
 void emit(const std::string& json, const std::string& out_file) {
   if (!out_file.empty()) {

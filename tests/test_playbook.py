@@ -207,7 +207,9 @@ def test_check_mode_on_shipped_cluster_playbook(tmp_path):
     (a / "roles" / "ranchermaster" / "vars" / "vars.yml").write_text("master: 127.0.0.1\nkubernetes_name: k\nkubernetes_description: k\n")
     extra = {"tk8s_python": "python3", "tk8s_pythonpath": str(REPO), "tk8s_master_port": 1, "tk8s_bind_host": "127.0.0.1",
              "tk8s_cp_state_dir": str(tmp_path / "cp"), "tk8s_node_grace": 5, "tk8s_manifests": str(REPO / "manifests"),
-             "tk8s_validation_command": ["true"], "tk8s_validate": True, "tk8s_fake_gpus": "1"}
+             "tk8s_validation_command": ["true"], "tk8s_validation_pod_command": ["true", "--reuse", "x"],
+             "tk8s_controlplane_argv": ["python3", "-m", "tritonk8ssupervisor_amd.controlplane"],
+             "tk8s_validate": True, "tk8s_fake_gpus": "1"}
     lines = []
     res = Playbook(a / "clusterUp.yml", a / "hosts", extra_vars=extra, check=True, out=lines.append).run()
     assert res.ok, res.failures

@@ -165,6 +165,24 @@ class MachineExecutor:
             return {"ok": False, "msg": f"{name} on {host} did not log {wait_for_log!r} within {timeout}s: {tail}"}
         return info
 
+    def wait_log(self, host: str, name: str, text: str, timeout: float) -> dict:
+        """A daemon that is already running: wait until its log has the ready line."""
+        _, log = self._paths(host, name)
+        t = time.monotonic()
+        deadline = t + timeout
+        while time.monotonic() < deadline:
+            try:
+                with open(log, "rb") as f:
+                    if text.encode() in f.read():
+                        return {"ok": True, "wait_seconds": round(time.monotonic() - t, 6)}
+            except OSError:
+                pass
+            if not self.daemon_status(host, name).get("running"):
+                break
+            time.sleep(0.002)
+        tail = log.read_text(errors="replace")[-600:] if log.exists() else ""
+        return {"ok": False, "msg": f"{name} on {host} did not log {text!r} within {timeout}s: {tail}"}
+
     def stop_daemon(self, host: str, name: str) -> bool:
         pidfile, _ = self._paths(host, name)
         return kill_pidfile(pidfile)
@@ -185,6 +203,7 @@ def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, M
     """Variables the roles need beyond inventory + vars.yml (shared by setup and
     `./tk8s ansible-playbook`, so a by-hand run of clusterUp.yml behaves like setup's)."""
     m = machines[cfg.RANCHER_MASTER_HOSTNAME]
+    vcmd = validation_command or default_validation_command()
     return {
         "tk8s_python": sys.executable,
         "tk8s_pythonpath": os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]),
@@ -192,11 +211,32 @@ def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, M
         "tk8s_bind_host": m.primaryip,
         "tk8s_cp_state_dir": str(Path(m.sandbox) / "controlplane"),
         "tk8s_node_grace": node_grace,
+        "tk8s_controlplane_argv": controlplane_argv(m.primaryip, int(cfg.TK8S_MASTER_PORT), m.primaryip,
+                                                    str(Path(m.sandbox) / "controlplane"), node_grace),
         "tk8s_manifests": str(ws.manifests),
-        "tk8s_validation_command": validation_command or default_validation_command(),
+        "tk8s_validation_command": vcmd,
+        "tk8s_validation_pod_command": validation_pod_command(vcmd),
         "tk8s_validate": validate,
         "tk8s_fake_gpus": os.environ.get("TK8S_FAKE_GPUS", ""),
     }
+
+
+def controlplane_argv(bind: str, port: int, advertise: str, state_dir: str, node_grace: float) -> list[str]:
+    """The control plane daemon (the ranchermaster role's rancher/server), one definition for the
+    role and the master's boot hook."""
+    return [sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.controlplane", "--host", bind, "--port", str(port),
+            "--advertise", advertise, "--state-dir", state_dir, "--node-grace", str(node_grace)]
+
+
+def validation_pod_command(command: list[str], result: str = "$(TK8S_MACHINE_DIR)/run/gpu-burnin.json") -> list[str]:
+    """The validation DaemonSet pod: reuse the node's burn-in result, probe only without one.
+    With the real probe the reuse runs in tk8s-reuse, which loads no ROCm library."""
+    from .ops import BIN
+
+    reuse = BIN / "tk8s-reuse"
+    if not os.environ.get("TK8S_FAKE_GPUS") and reuse.exists():
+        return [str(reuse), result, "--", *command]
+    return [*command, "--reuse", result]
 
 
 # ---- setup ---------------------------------------------------------------------------------
@@ -283,6 +323,8 @@ class Setup:
         """Boot hook: a GPU machine starts its GPU burn-in the moment it exists (like a node
         image's boot-time GPU health check), overlapping the other machines' creation and play 1.
         rocmsetup's burn-in task then finds it running and does nothing."""
+        if self.cfg is not None and m.name == self.cfg.RANCHER_MASTER_HOSTNAME and hasattr(self.provider, "machine_env"):
+            self._boot_controlplane(m)
         if not (self.validate and m.gpus and hasattr(self.provider, "machine_env")):
             return
         if self.host_burnin is not None and self.host_burnin.register(m.name, m.sandbox, list(m.gpus)):
@@ -293,6 +335,20 @@ class Setup:
         ex = MachineExecutor(self.provider, {m.name: m})
         r = start_burnin(ex, m.name, self._validation_command(), "run/gpu-burnin.json")
         self.events.emit("gpu_burnin_started", name=m.name, **{k: v for k, v in r.items() if k in ("pid", "gpus", "msg")})
+
+    def _boot_controlplane(self, m: Machine) -> None:
+        """Master boot hook: the control plane service starts with its machine (the way a master
+        image would start rancher/server at boot), overlapping the workers' creation and play 1;
+        the ranchermaster role then finds it running and waits for its "Listening on"."""
+        if os.environ.get("TK8S_BOOT_CONTROLPLANE", "1") == "0":
+            return
+        argv = controlplane_argv(m.primaryip, int(self.cfg.TK8S_MASTER_PORT), m.primaryip,
+                                 str(Path(m.sandbox) / "controlplane"), self.node_grace)
+        pythonpath = os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+        ex = MachineExecutor(self.provider, {m.name: m})
+        info = ex.start_daemon(m.name, "controlplane", argv, env={"PYTHONPATH": pythonpath}, restart="unless-stopped",
+                               wait_for_log=None, timeout=0)
+        self.events.emit("controlplane_boot_started", name=m.name, pid=info.get("pid"))
 
     def provision(self) -> None:
         cfg = self.cfg

@@ -302,6 +302,11 @@ def m_tk8s_daemon(args, *, ctx, target, local, env, check, **_):
         ex.stop_daemon(target.name, name)
         return {"changed": True, "running": False}
     if status["running"]:
+        if args.get("wait_for_log") and not check and hasattr(ex, "wait_log"):
+            info = ex.wait_log(target.name, name, str(args["wait_for_log"]), float(args.get("timeout", 300)))
+            if not info.get("ok"):
+                return {"failed": True, **info}
+            return {"changed": False, "running": True, "pid": status.get("pid"), **info}
         return {"changed": False, "running": True, "pid": status.get("pid")}
     if check:
         return {"changed": True, "running": False, "msg": "would start"}

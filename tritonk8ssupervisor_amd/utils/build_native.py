@@ -185,6 +185,11 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
               *[str(x) for x in smi_srcs], "-o", str(smi), f"-L{ROCM / 'lib'}", "-lamd_smi",
               f"-Wl,-rpath,{ROCM / 'lib'}"], verbose)
 
+    reuse_src = NATIVE / "tools" / "tk8s_reuse.cpp"
+    reuse_bin = tool_path("tk8s-reuse")
+    if force or _stale(reuse_bin, [reuse_src]):
+        _run([CXX, "-O2", "-std=c++17", "-Wall", str(reuse_src), "-o", str(reuse_bin)], verbose)
+
     sup_src = NATIVE / "tools" / "tk8s_supervise.cpp"
     sup = tool_path("tk8s-supervise")
     if force or _stale(sup, [sup_src]):
@@ -192,7 +197,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
     precompile_python()
     out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,
-           "tk8s-smi": smi}
+           "tk8s-smi": smi, "tk8s-reuse": reuse_bin}
     out.update({n: tool_path(n) for n in TOOLS})
     return out
 
@@ -225,7 +230,9 @@ def precompile_python() -> None:
             "tritonk8ssupervisor_amd.playbook", "tritonk8ssupervisor_amd.playbook_modules", "tritonk8ssupervisor_amd.kube",
             "tritonk8ssupervisor_amd.wizard", "tritonk8ssupervisor_amd.controlplane.server", "tritonk8ssupervisor_amd.burnin",
             "tritonk8ssupervisor_amd.agent.agent", "tritonk8ssupervisor_amd.ops.fakeprobe", "yaml", "argparse", "asyncio",
-            "tritonk8ssupervisor_amd.controlplane.client", "tritonk8ssupervisor_amd.parallel.dist_allreduce"]
+            "tritonk8ssupervisor_amd.controlplane.client", "tritonk8ssupervisor_amd.controlplane.ingress",
+            "tritonk8ssupervisor_amd.controlplane.dns", "tritonk8ssupervisor_amd.utils.k8senv",
+            "tritonk8ssupervisor_amd.parallel.dist_allreduce"]
     code = "import importlib\nfor m in %r:\n    importlib.import_module(m)\n" % (mods[:-1] + ["tritonk8ssupervisor_amd.provision"],)
     for flag in (["-S"], []):
         subprocess.run([sys.executable, *flag, "-c", code], env=env, cwd=str(REPO), capture_output=True, timeout=120)
