@@ -105,8 +105,8 @@ def test_setup_ready_and_clean_teardown(ws, n):
     for i in range(1, n + 1):
         burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
         assert burn["ok"] and burn["probed"] == 1
-        # >= 2 GPUs: one host-level burn-in (the runtime starts once) split per machine
-        assert burn.get("host_burnin", False) == (n >= 2)
+        # one host-level burn-in (the runtime starts once, before the machines exist), split per machine
+        assert burn["host_burnin"] and burn["devices"][0]["host_index"] == int(items[i - 1]["status"]["devices"][0]["id"][3:])
     # teardown: machines gone, every artefact removed -- including the env-id file the
     # reference never cleans (setup.sh:513 removes ./tmp/* instead of ansible/tmp/*)
     (ws / "ansible" / "tmp" / ".keep").touch()  # the repository's tracked placeholder

@@ -113,17 +113,27 @@ def test_plugin_registers_again_after_a_kubelet_restart(tmp_path, fake8):
     _, srv, stop, t = _plugin(reg)
     try:
         assert reg.wait_plugin(RESOURCE, 10) is not None
-        n0 = srv.registrations
+        _until(lambda: srv.registrations == 1)  # the plugin counts once its Register RPC returned
         reg.stop()  # the kubelet exits and wipes the socket directory
         reg = KubeletRegistry(d).start()
         c = reg.wait_plugin(RESOURCE, 10)
-        assert c is not None and srv.registrations == n0 + 1
+        assert c is not None
+        _until(lambda: srv.registrations == 2)
         assert c.wait(lambda c: len(c.healthy()) == 4, 10)
     finally:
         stop.set()
         t.join(5)
         reg.stop()
     assert not srv.socket.exists()
+
+
+def _until(pred, timeout=10.0):
+    import time
+
+    deadline = time.monotonic() + timeout
+    while not pred():
+        assert time.monotonic() < deadline, "condition not met in time"
+        time.sleep(0.01)
 
 
 def test_registry_rejects_a_wrong_api_version(kubelet):

@@ -276,7 +276,7 @@ def test_setup_with_grpc_device_plugin_and_rccl_on_a_real_gpu(tmp_path):
 
 def test_setup_with_host_burnin_on_a_real_gpu(tmp_path):
     """The host-level burn-in (one tk8s-probe for every worker GPU, split per machine) on real
-    hardware; TK8S_HOST_BURNIN=force uses it for a single GPU too."""
+    hardware (the default for every GPU count)."""
     import os
     import shutil
     import subprocess
@@ -292,7 +292,7 @@ def test_setup_with_host_burnin_on_a_real_gpu(tmp_path):
     for f in ("setup.sh", "tk8s", "kubectl"):
         shutil.copy2(repo / f, tmp_path / f)
     env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
-    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, TK8S_HOST_BURNIN="force")
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable)
     try:
         r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120"],
                            cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)

@@ -70,7 +70,10 @@ def _emit(out, path):
 
 def main():
     node = os.environ.get("NODE_NAME") or os.environ.get("TK8S_MACHINE", "-")
-    # a failing node's GPU fails its own validation even when a (host-level) burn-in result exists
+    # a failing (or wedged) node's GPU fails its own validation even when a (host-level) burn-in
+    # result exists
+    if os.environ.get("TK8S_FAKE_PROBE_HANG", "") == node:
+        time.sleep(3600)  # a wedged validation (the analogue of the reference's stuck dashboard)
     if "--reuse" in sys.argv and os.environ.get("TK8S_FAKE_PROBE_FAIL", "") != node:
         rc = _reuse(_arg("--reuse"), float(_arg("--reuse-wait", "120")))
         if rc is not None:

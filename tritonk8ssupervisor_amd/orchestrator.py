@@ -360,7 +360,6 @@ class Setup:
                                cfg.node_networks(), cfg.HOST_PACKAGE)
         if not (ws.tf / "rancher.tf").exists() or not self.resume:
             atomic_write(ws.tf / "rancher.tf", text)
-        self._start_host_burnin()
         self.out("Generating terraform configs for environment...")
         self.out(f"    Master hostname: {cfg.RANCHER_MASTER_HOSTNAME}")
         for i, n in enumerate(cfg.node_names(), 1):
@@ -375,9 +374,10 @@ class Setup:
             raise SetupError("Terraform had too many errors. Make sure you haven't reached your provisioning limit.")
 
     def _start_host_burnin(self) -> None:
-        """>= 2 GPUs about to be handed out: one burn-in process for all of them (burnin.HostBurnin:
-        the runtime start is host-wide and serialised across processes, so N per-machine burn-ins
-        would stack N starts on the critical path). Machines not covered fall back to their own."""
+        """One burn-in process for every GPU about to be handed out (burnin.HostBurnin: the runtime
+        start is host-wide and serialised across processes, so N per-machine burn-ins would stack
+        N starts on the critical path), started as soon as the configuration says which GPUs the
+        workers will get -- before the machines exist. Machines not covered probe on their own."""
         if not (self.validate and hasattr(self.provider, "predict_gpus")) or os.environ.get("TK8S_HOST_BURNIN", "1") == "0":
             return
         try:
@@ -385,7 +385,7 @@ class Setup:
             gpus = self.provider.predict_gpus(int(pkg.gpus or 0), int(self.cfg.KUBERNETES_NUMBER_OF_NODES))
         except Exception:  # noqa: BLE001 - prediction is an optimisation only
             return
-        if len(gpus) < (1 if os.environ.get("TK8S_HOST_BURNIN") == "force" else 2):
+        if not gpus:
             return
         import threading
 
@@ -560,6 +560,8 @@ class Setup:
                 with self.events.phase(name):
                     fn()
                 self.mark(name)
+            if name == "configure" and not self.done("provision"):
+                self._start_host_burnin()  # the GPUs are known now: validate them while machines are made
         with self.events.phase("ready"):
             ready = self.wait_ready()
         self.mark("ready")
