@@ -282,3 +282,26 @@ def test_ghost_from_the_dashboard_deploy_form(cluster):
     assert "MI355X is Ready" in _get(url + "/")
     page = _get(dash)
     assert "Deploy a containerized app" in page and "ghost" in page
+
+
+@pytest.mark.slow
+def test_kubectl_exec_and_logs_follow(cluster, tmp_path_factory):
+    ws, env, kc, _ = cluster
+    d = tmp_path_factory.mktemp("x")
+    (d / "p.yaml").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "sleeper"},
+        "spec": {"containers": [{"name": "c", "command": ["sh", "-c", "echo started; sleep 30"],
+                                 "env": [{"name": "GREETING", "value": "hi-from-pod"}]}]}}))
+    kc("apply", "-f", str(d / "p.yaml"))
+    _until(lambda: json.loads(kc("get", "pod", "sleeper", "-o", "json").stdout)["status"].get("phase") == "Running")
+    r = kc("exec", "sleeper", "--", "sh", "-c", "echo $GREETING $POD_NAME; pwd; echo oops >&2; exit 3", check=False)
+    assert r.returncode == 3 and "hi-from-pod sleeper" in r.stdout and "oops" in r.stderr
+    assert r.stdout.splitlines()[1].endswith("/pods/sleeper")
+    r = kc("exec", "sleeper", "--", "no-such-binary", check=False)
+    assert r.returncode == 127
+    (d / "j.yaml").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "talker"},
+        "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "command": [
+            "sh", "-c", "for i in 1 2 3; do echo line$i; sleep 0.3; done"]}]}}))
+    kc("apply", "-f", str(d / "j.yaml"))
+    _until(lambda: json.loads(kc("get", "pod", "talker", "-o", "json").stdout)["status"].get("phase") in ("Running", "Succeeded"))
+    out = kc("logs", "talker", "-f").stdout
+    assert out.split() == ["line1", "line2", "line3"]

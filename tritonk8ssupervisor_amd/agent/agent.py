@@ -80,6 +80,7 @@ class Agent:
         self.kubelet = None
         self._config_wait: dict[str, dict] = {}   # pods held in CreateContainerConfigError
         self._start_lock = threading.Lock()
+        self._execs_seen: set[str] = set()
         if url:
             self.set_url(url)
 
@@ -446,6 +447,46 @@ class Agent:
                 first = True
                 self.stop.wait(0.2)
 
+    def exec_loop(self) -> None:
+        """Exec requests for this node's pods (kubectl exec): run the command with the pod's env
+        in the pod's directory, post stdout/stderr/exit code back."""
+        api = Client(self.api.base, token=self.api.token, prefix=self.api.prefix, timeout=40.0)
+        path = api.k8s(f"/api/v1/nodes/{self.name}/execs")
+        while not self.stop.is_set():
+            try:
+                items = api.get(path, query={"timeoutSeconds": "20"})["items"]
+            except (ApiError, OSError):
+                if self.stop.wait(0.5):
+                    return
+                continue
+            for x in items:
+                threading.Thread(target=self._run_exec, args=(x,), name="exec", daemon=True).start()
+
+    def _run_exec(self, x: dict) -> None:
+        xid = x["metadata"]["name"]
+        if xid in self._execs_seen:
+            return
+        self._execs_seen.add(xid)
+        pp = self.runtime.running().get(f"{x['namespace']}/{x['pod']}")
+        if pp is None or pp.done.is_set():
+            res = {"stdout": "", "stderr": f"pod {x['pod']} is not running on {self.name}\n", "exitCode": 1}
+        else:
+            env = dict(pp.env)
+            if self.runtime.tool_dirs:
+                env["PATH"] = os.pathsep.join(self.runtime.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
+            try:
+                r = subprocess.run(x["command"], input=x.get("stdin", ""), env=env, cwd=pp.dir, capture_output=True,
+                                   text=True, timeout=float(x.get("timeoutSeconds", 60)))
+                res = {"stdout": r.stdout, "stderr": r.stderr, "exitCode": r.returncode}
+            except FileNotFoundError as e:
+                res = {"stdout": "", "stderr": f"exec: {e}\n", "exitCode": 127}
+            except subprocess.TimeoutExpired as e:
+                res = {"stdout": e.stdout or "", "stderr": f"exec: timed out after {e.timeout}s\n", "exitCode": 124}
+        try:
+            self.api.put(self.api.k8s(f"/api/v1/nodes/{self.name}/execs/{xid}"), res)
+        except (ApiError, OSError) as e:
+            print(f"{self.name}: exec {xid} result not delivered: {e}", flush=True)
+
     def _handle(self, etype: str, pod: dict) -> None:
         md = pod["metadata"]
         key = f"{md['namespace']}/{md['name']}"
@@ -474,7 +515,8 @@ class Agent:
               f"({len(self.plugin.devices())} GPU, inventory={self.plugin.inventory.source})", flush=True)
         threads = [threading.Thread(target=self.heartbeat_loop, name="heartbeat", daemon=True),
                    threading.Thread(target=self.smi_loop, name="smi", daemon=True),
-                   threading.Thread(target=self.watch_loop, name="pods", daemon=True)]
+                   threading.Thread(target=self.watch_loop, name="pods", daemon=True),
+                   threading.Thread(target=self.exec_loop, name="exec", daemon=True)]
         for t in threads:
             t.start()
         try:

@@ -7,7 +7,8 @@
   kubectl scale deploy/NAME --replicas N
   kubectl rollout status|restart deploy/NAME
   kubectl label|annotate KIND NAME k=v k-
-  kubectl logs POD [--tail N]         kubectl cordon|uncordon|drain NODE
+  kubectl logs POD [--tail N] [-f]    kubectl cordon|uncordon|drain NODE
+  kubectl exec POD -- CMD [ARGS...]   (non-interactive: stdout/stderr/exit code)
   kubectl top nodes                   (amd.com/gpu in use, hotspot temperature, power, VRAM)
   kubectl wait job/NAME [--timeout S] kubectl cluster-info | version
 
@@ -239,9 +240,18 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--from-literal", action="append", default=[])
     ap.add_argument("--from-file", action="append", default=[])
     ap.add_argument("--ignore-daemonsets", action="store_true")
+    ap.add_argument("--follow", dest="follow", action="store_true")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
+    argv = list(sys.argv[1:] if argv is None else argv)
+    command: list[str] = []
+    if "--" in argv:  # kubectl exec POD -- CMD ARGS...
+        command = argv[argv.index("--") + 1:]
+        argv = argv[:argv.index("--")]
+    if argv[:1] == ["logs"] and "-f" in argv:  # `-f` means --filename everywhere but logs
+        argv = [x if x != "-f" else "--follow" for x in argv]
     a = ap.parse_args(argv)
+    a.command = command
     workdir = workdir or os.environ.get("TK8S_WORKDIR", os.getcwd())
     try:
         k = client_from_kubeconfig(_load_kubeconfig(a.kubeconfig, workdir))
@@ -363,7 +373,28 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 n = 1
             print(f"{n} object(s) deleted")
         elif a.verb == "logs":
-            print(k.get(k.k8s(object_path("pod", a.args[0], ns) + "/log"), query={"tailLines": a.tail or None}, raw=True), end="")
+            path = k.k8s(object_path("pod", a.args[0], ns) + "/log")
+            text = k.get(path, query={"tailLines": a.tail or None}, raw=True)
+            print(text, end="", flush=True)
+            if a.follow:  # -f: print what the pod appends until it terminates
+                seen = len(k.get(path, raw=True))
+                while True:
+                    phase = k.get(k.k8s(object_path("pod", a.args[0], ns))).get("status", {}).get("phase")
+                    full = k.get(path, raw=True)
+                    print(full[seen:], end="", flush=True)
+                    seen = len(full)
+                    if phase in ("Succeeded", "Failed"):
+                        break
+                    time.sleep(0.2)
+        elif a.verb == "exec":
+            if not a.command:
+                raise SystemExit("usage: kubectl exec POD -- COMMAND [ARGS...]")
+            r = k.post(k.k8s(object_path("pod", a.args[0], ns) + "/exec"),
+                       {"command": a.command, "timeoutSeconds": float(a.timeout.rstrip("s"))},
+                       timeout=float(a.timeout.rstrip("s")) + 30)
+            sys.stdout.write(r.get("stdout", ""))
+            sys.stderr.write(r.get("stderr", ""))
+            return int(r.get("exitCode", 1))
         elif a.verb in ("cordon", "uncordon"):
             k.request("PATCH", k.k8s(f"/api/v1/nodes/{a.args[0]}"), body={"spec": {"unschedulable": a.verb == "cordon"}})
             print(f"node/{a.args[0]} {a.verb}ed")

@@ -271,6 +271,9 @@ class ControlPlane:
                 add(method, r"/apis/apps/v1/namespaces/(?P<ns>[^/]+)/deployments/(?P<name>[^/]+)/scale", self.h_scale)
             add("PUT", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/status", self.h_pod_status)
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/log", self.h_pod_log)
+            add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/exec", self.h_pod_exec)
+            add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs", self.h_node_execs)
+            add("PUT", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)", self.h_exec_result)
 
     # ---- misc handlers ---------------------------------------------------------------
     async def h_ping(self, req: Request, **_):
@@ -1103,6 +1106,66 @@ class ControlPlane:
         if tail:
             text = "\n".join(text.splitlines()[-tail:]) + "\n"
         return Response(200, text, content_type="text/plain")
+
+    # ---- exec: a command in a running pod's environment (the kubelet's exec, request/response) --
+    async def h_pod_exec(self, req: Request, ns: str, name: str, pid: str | None = None):
+        """``kubectl exec POD -- CMD``: queued for the pod's node agent, which runs CMD with the
+        pod's env in its directory and posts stdout/stderr/exit code back; this request waits for
+        that (non-interactive; the API server's SPDY/websocket streams have no equivalent here)."""
+        p = self._pid(pid, req)
+        self._auth(req, self.project(p))
+        pod = self.store.get("pods", _key(p, ns, name))
+        if pod is None:
+            raise HttpError(404, f'pod "{name}" not found')
+        if pod.get("status", {}).get("phase") != "Running" or not pod["spec"].get("nodeName"):
+            raise HttpError(400, f'pod "{name}" is not running')
+        body = req.json()
+        cmd = body.get("command")
+        if not isinstance(cmd, list) or not cmd:
+            raise HttpError(422, "command must be a non-empty list")
+        timeout = min(float(body.get("timeoutSeconds", 60)), 600.0)
+        self._seq += 1
+        xid = f"x{self._seq:x}"
+        node = pod["spec"]["nodeName"]
+        key = _key(p, node, xid)
+        self.store.put("execs", key, {"metadata": {"name": xid}, "_project": p, "node": node, "pod": name,
+                                      "namespace": ns, "command": [str(c) for c in cmd],
+                                      "stdin": str(body.get("stdin", "")), "timeoutSeconds": timeout,
+                                      "status": {"phase": "Pending"}})
+        done = await self.store.wait_until(
+            lambda: (self.store.get("execs", key) or {}).get("status", {}).get("phase") == "Done", timeout + 10)
+        x = self.store.delete("execs", key) or {}
+        if not done:
+            raise HttpError(504, f"exec in {name}: no result from node {node} within {timeout:.0f}s")
+        st = x.get("status", {})
+        return {"stdout": st.get("stdout", ""), "stderr": st.get("stderr", ""), "exitCode": st.get("exitCode", 1)}
+
+    async def h_node_execs(self, req: Request, node: str, pid: str | None = None):
+        """The node agent's long-poll for exec requests of its pods."""
+        p = self._pid(pid, req)
+        self._node_secret_ok(req, _key(p, node))
+
+        def pending():
+            return [self._strip(x) for x in self.store.list("execs", lambda x: x.get("_project") == p and
+                    x.get("node") == node and x.get("status", {}).get("phase") == "Pending")]
+
+        wait = min(float(req.q("timeoutSeconds", "20") or 20), 60.0)
+        items = await self.store.wait_until(pending, wait) or []
+        for x in items:  # handed out: not returned again
+            self.store.patch("execs", _key(p, node, x["metadata"]["name"]),
+                             lambda o: o["status"].update(phase="Running"))
+        return {"items": items}
+
+    async def h_exec_result(self, req: Request, node: str, xid: str, pid: str | None = None):
+        p = self._pid(pid, req)
+        self._node_secret_ok(req, _key(p, node))
+        body = req.json()
+        x = self.store.patch("execs", _key(p, node, xid), lambda o: o["status"].update(
+            phase="Done", stdout=str(body.get("stdout", ""))[-1 << 20:], stderr=str(body.get("stderr", ""))[-1 << 20:],
+            exitCode=int(body.get("exitCode", 1))))
+        if x is None:
+            raise HttpError(404, f"exec {xid} not found (timed out?)")
+        return {"ok": True}
 
     # ---- controllers ------------------------------------------------------------------
     def reconcile(self) -> None:
