@@ -431,3 +431,18 @@ def test_failed_host_burnin_falls_back_to_per_machine_probes(ws):
         assert not f.exists() or not json.loads(f.read_text()).get("host_burnin")
     events = (ws / ".tk8s" / "events.jsonl").read_text()
     assert "gpu_burnin_share_failed" in events and "gpu_burnin_host_done" in events
+
+
+def test_two_gpu_workers_share_one_host_burnin(ws):
+    """mi355x-2gpu workers: one burn-in over all 4 GPUs, each machine gets exactly its two
+    (renumbered as it sees them), and every node advertises 2 validated amd.com/gpu."""
+    s = _summary(_setup(ws, "--nodes", "2", "--package", "mi355x-2gpu", "--rccl", "off"))
+    assert s["gpus_allocatable"] == 4 and s["nodes_validated"] == 2
+    seen = []
+    for i in (1, 2):
+        m = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "machine.json").read_text())
+        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
+        assert burn["host_burnin"] and burn["probed"] == 2
+        assert [d["host_index"] for d in burn["devices"]] == m["gpus"] and [d["device"] for d in burn["devices"]] == [0, 1]
+        seen += m["gpus"]
+    assert sorted(seen) == [0, 1, 2, 3]
