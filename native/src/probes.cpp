@@ -55,36 +55,51 @@ struct DeviceGuard {
 // device on MI355X (more than all the kernels together), so they share one allocation that
 // grows on demand and lives until release_probe_scratch() / process exit. Peer copies keep
 // their own buffers (another device's thread may be using its arena concurrently).
-std::mutex g_scratch_mu;
-std::map<int, std::pair<void*, size_t>> g_scratch;
+struct ScratchSlot {
+  std::mutex mu;  // per device: growing one GPU's arena never waits on another's
+  void* p = nullptr;
+  size_t n = 0;
+};
+std::mutex g_scratch_mu;                 // guards the map only (node-based: slots never move)
+std::map<int, ScratchSlot> g_scratch;
 
 char* scratch(int device, size_t bytes) {
-  std::lock_guard<std::mutex> lock(g_scratch_mu);
-  auto& slot = g_scratch[device];
-  if (slot.second < bytes) {
-    if (slot.first) TK8S_HIP_CHECK(hipFree(slot.first));
-    slot.first = nullptr;
-    slot.second = 0;
-    TK8S_HIP_CHECK(hipMalloc(&slot.first, bytes));
-    slot.second = bytes;
+  ScratchSlot* slot;
+  {
+    std::lock_guard<std::mutex> lock(g_scratch_mu);
+    slot = &g_scratch[device];
   }
-  return static_cast<char*>(slot.first);
+  std::lock_guard<std::mutex> lock(slot->mu);
+  if (slot->n < bytes) {
+    if (slot->p) TK8S_HIP_CHECK(hipFree(slot->p));
+    slot->p = nullptr;
+    slot->n = 0;
+    TK8S_HIP_CHECK(hipMalloc(&slot->p, bytes));
+    slot->n = bytes;
+  }
+  return static_cast<char*>(slot->p);
 }
 
 // One non-blocking stream per device, created on first use and kept: a ROCm stream is backed
 // by a hardware queue, and creating one per probe (plus the legacy null stream for the copy's
-// source fill) cost milliseconds each on the validation's critical path.
+// source fill) cost milliseconds each on the validation's critical path. Created outside the
+// lock: a first queue costs ~20 ms (profiles/r1_init_costs), and the per-device threads of a
+// multi-GPU burn-in must not serialise behind each other's creation.
 std::mutex g_stream_mu;
 std::map<int, hipStream_t> g_streams;
 
 hipStream_t probe_stream(int device) {
-  std::lock_guard<std::mutex> lock(g_stream_mu);
-  auto it = g_streams.find(device);
-  if (it != g_streams.end()) return it->second;
+  {
+    std::lock_guard<std::mutex> lock(g_stream_mu);
+    auto it = g_streams.find(device);
+    if (it != g_streams.end()) return it->second;
+  }
   hipStream_t s{};
   TK8S_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  g_streams[device] = s;
-  return s;
+  std::lock_guard<std::mutex> lock(g_stream_mu);
+  const auto ins = g_streams.emplace(device, s);
+  if (!ins.second) (void)hipStreamDestroy(s);  // another thread of this device won the race
+  return ins.first->second;
 }
 
 struct CachedStream {
@@ -105,12 +120,15 @@ void release_probe_scratch() {
   }
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   for (auto& kv : g_scratch) {
-    if (!kv.second.first) continue;
+    std::lock_guard<std::mutex> slot_lock(kv.second.mu);
+    if (!kv.second.p) continue;
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(kv.first);
-    (void)hipFree(kv.second.first);
+    (void)hipFree(kv.second.p);
     (void)hipSetDevice(prev);
+    kv.second.p = nullptr;
+    kv.second.n = 0;
   }
   g_scratch.clear();
 }
