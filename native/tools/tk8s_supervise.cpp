@@ -100,10 +100,20 @@ int main(int argc, char** argv) {
 
   int restarts = 0, status = 0;
   long delay = backoff_ms;
+  // SIGTERM/SIGINT stay blocked across fork(): a signal landing before the child has reset its
+  // handlers would otherwise run on_signal in the child and be lost, and the program then exec'd
+  // would never see the stop. Pending signals are delivered after the unblock (in the child:
+  // with the default action; in the parent: once g_child names the child).
+  sigset_t term_set, old_set;
+  sigemptyset(&term_set);
+  sigaddset(&term_set, SIGTERM);
+  sigaddset(&term_set, SIGINT);
   while (!g_stop) {
     const double started = now_s();
+    sigprocmask(SIG_BLOCK, &term_set, &old_set);
     const pid_t pid = fork();
     if (pid < 0) {
+      sigprocmask(SIG_SETMASK, &old_set, nullptr);
       std::perror("tk8s-supervise: fork");
       return 1;
     }
@@ -111,12 +121,14 @@ int main(int argc, char** argv) {
       signal(SIGTERM, SIG_DFL);
       signal(SIGINT, SIG_DFL);
       signal(SIGHUP, SIG_DFL);
+      sigprocmask(SIG_SETMASK, &old_set, nullptr);
       execvp(child_argv[0], child_argv.data());
       std::fprintf(stderr, "tk8s-supervise: exec %s: %s\n", child_argv[0], std::strerror(errno));
       _exit(127);
     }
     g_child = pid;
-    if (g_stop) kill(pid, SIGTERM);  // a signal that landed between fork() and the store above
+    sigprocmask(SIG_SETMASK, &old_set, nullptr);
+    if (g_stop) kill(pid, SIGTERM);  // stopped before this fork: do not leave the child running
     write_pidfile(pidfile, pid, restarts);
     while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
     }

@@ -238,3 +238,33 @@ def test_engine_rejects_unknown_module_argument(ws):
     (ws.tf / "rancher.tf").write_text('module "x" {\n source = "host"\n hostname = "x"\n networks = []\n bogus = 1\n}\n')
     with pytest.raises(Exception, match="unknown arguments"):
         Engine(ws.tf, prov).specs()
+
+
+def test_clusters_on_one_host_never_share_an_ip_or_a_gpu(tmp_path, monkeypatch):
+    """Two workspaces on one host: the host registry keeps their loopback IPs (and so their DNS,
+    ingress and NodePort sockets) and their GPUs disjoint, and frees them on delete or when the
+    owner is gone."""
+    monkeypatch.setenv("TK8S_HOST_REGISTRY", str(tmp_path / "hostreg"))
+    monkeypatch.setenv("TK8S_FAKE_GPUS", "8")
+    monkeypatch.setattr(LocalProvider, "_host_gpus", staticmethod(lambda: True))  # as on a real host
+    a, b = LocalProvider(tmp_path / "a"), LocalProvider(tmp_path / "b")
+    ma = a.create_machine("kubemaster", "cpu-only", ["local-public"], tags={"role": "master"})
+    wa = a.create_machine("kubenode1", "mi355x-4gpu", ["local-public"])
+    mb = b.create_machine("kubemaster", "cpu-only", ["local-public"], tags={"role": "master"})
+    wb = b.create_machine("kubenode1", "mi355x-4gpu", ["local-public"])
+    assert len({ma.primaryip, wa.primaryip, mb.primaryip, wb.primaryip}) == 4
+    assert not set(wa.gpus) & set(wb.gpus) and len(wa.gpus + wb.gpus) == 8
+    assert b.predict_gpus(1, 1) == []
+    with pytest.raises(Exception, match="free"):
+        b.create_machine("kubenode2", "mi355x-1gpu", ["local-public"])
+    a.delete_machine(wa)  # released explicitly
+    assert len(b.predict_gpus(4, 1)) == 4
+    w2 = b.create_machine("kubenode2", "mi355x-4gpu", ["local-public"])
+    assert sorted(w2.gpus) == sorted(wa.gpus)
+    # a workspace deleted without teardown: its claims are reaped on the next allocation
+    import shutil
+
+    shutil.rmtree(tmp_path / "b")
+    c = LocalProvider(tmp_path / "c")
+    assert len(c.predict_gpus(4, 2)) == 8
+    assert c.create_machine("kubemaster", "cpu-only", ["local-public"], tags={"role": "master"}).primaryip != ma.primaryip

@@ -12,7 +12,8 @@ Replaces the Triton KVM of terraform/master/main.tf:1-11 / terraform/host/main.t
   group recorded under the sandbox and frees its IPs and GPUs.
 
 IP/GPU allocation is serialised by an flock on ``<state>/alloc.lock`` so concurrent creates
-(the Terraform fan-out) are race-free.
+(the Terraform fan-out) are race-free, and claimed host-wide (``hostreg.py``) so clusters that
+share the host never share an address or a GPU.
 """
 from __future__ import annotations
 
@@ -30,6 +31,7 @@ from ..utils.fsutil import atomic_write_json, file_lock, read_json
 from ..utils.procs import kill_pidfile
 from . import keys
 from .base import Machine, Network, Package, Provider, ProvisionError
+from .hostreg import HostRegistry
 
 _NS = uuid.UUID("5f1c0d3e-8a4b-4c6e-9b1a-7e2f3d4c5b6a")
 
@@ -71,6 +73,7 @@ class LocalProvider(Provider):
         self.key_dir = Path(key_dir) if key_dir else self.state_dir / "keys"
         self.alloc_file = self.state_dir / "alloc.json"
         self.lock_file = self.state_dir / "alloc.lock"
+        self.host = HostRegistry()
         self._multi_ip = None
 
     # ---- inventory ----------------------------------------------------------------
@@ -109,29 +112,38 @@ class LocalProvider(Provider):
             self._multi_ip = _loopback_multi_ok()
         return self._multi_ip
 
-    def _alloc_ips(self, alloc: dict, name: str, nets: list[Network]) -> list[str]:
+    @staticmethod
+    def _host_gpus() -> bool:
+        """Real GPUs are claimed host-wide; a fake inventory is private to each cluster."""
+        return not os.environ.get("TK8S_FAKE_GPUS")
+
+    def _alloc_ips(self, alloc: dict, name: str, nets: list[Network], host: dict) -> list[str]:
         used = alloc.setdefault("ips", {})
+        host_used = HostRegistry.taken(host, "ips")
         out = []
         for net in nets:
             if not self._multi():
                 out.append("127.0.0.1")
                 continue
             subnet = ipaddress.ip_network(net.subnet)
-            for host in subnet.hosts():
-                ip = str(host)
-                if ip not in used:
+            for addr in subnet.hosts():
+                ip = str(addr)
+                if ip not in used and ip not in host_used:
                     used[ip] = name
+                    HostRegistry.claim(host, "ips", ip, self.alloc_file, name)
                     out.append(ip)
                     break
             else:
                 raise ProvisionError(f"network {net.name} exhausted")
         return out
 
-    def _alloc_gpus(self, alloc: dict, name: str, count: int) -> list[int]:
+    def _alloc_gpus(self, alloc: dict, name: str, count: int, host: dict) -> list[int]:
         if count == 0:
             return []
         inv = discover()
         taken = {int(k) for k in alloc.setdefault("gpus", {})}
+        if self._host_gpus():
+            taken |= {int(k) for k in HostRegistry.taken(host, "gpus")}
         free = [g.ordinal for g in inv.gpus if g.ordinal not in taken]
         if len(free) < count:
             raise ProvisionError(
@@ -149,6 +161,8 @@ class LocalProvider(Provider):
             pick = free[:count]
         for g in pick:
             alloc["gpus"][str(g)] = name
+            if self._host_gpus():
+                HostRegistry.claim(host, "gpus", g, self.alloc_file, name)
         return pick
 
     def predict_gpus(self, per_machine: int, machines: int) -> list[int]:
@@ -158,6 +172,9 @@ class LocalProvider(Provider):
             return []
         alloc = read_json(self.alloc_file, {}) or {}
         taken = {int(k) for k in alloc.get("gpus", {})}
+        if self._host_gpus():
+            with self.host.locked() as host:
+                taken |= {int(k) for k in HostRegistry.taken(host, "gpus")}
         inv = discover()
         free = [g.ordinal for g in inv.gpus if g.ordinal not in taken]
         out: list[int] = []
@@ -187,10 +204,13 @@ class LocalProvider(Provider):
             alloc = read_json(self.alloc_file, {}) or {}
             if name in alloc.get("machines", {}):
                 raise ProvisionError(f"machine {name} already exists")
-            ips = self._alloc_ips(alloc, name, nets)
-            gpus = self._alloc_gpus(alloc, name, 0 if role == "master" else pkg.gpus)
-            alloc.setdefault("machines", {})[name] = {"ips": ips, "gpus": gpus}
-            atomic_write_json(self.alloc_file, alloc)
+            # the owner's alloc.json is written under the host lock too: a concurrent reaper
+            # must never see a claim whose machine its owner does not list yet
+            with self.host.locked() as host:
+                ips = self._alloc_ips(alloc, name, nets, host)
+                gpus = self._alloc_gpus(alloc, name, 0 if role == "master" else pkg.gpus, host)
+                alloc.setdefault("machines", {})[name] = {"ips": ips, "gpus": gpus}
+                atomic_write_json(self.alloc_file, alloc)
         for sub in ("run", "logs", "pods", "etc"):
             (sandbox / sub).mkdir(parents=True, exist_ok=True)
         if root_authorized_keys:
@@ -253,4 +273,6 @@ class LocalProvider(Provider):
                 for key in [key for key, owner in table.items() if owner == machine.name]:
                     del table[key]
             atomic_write_json(self.alloc_file, alloc)
+            with self.host.locked() as host:
+                HostRegistry.release(host, self.alloc_file, machine.name)
         shutil.rmtree(sandbox, ignore_errors=True)
