@@ -154,6 +154,12 @@ def child_env(fake_gpus: int | None) -> dict:
     return env
 
 
+def private_registry(env: dict, root: Path) -> None:
+    """The bench measures one cluster: claims left on the host by other clusters (say, a test run
+    that leaked one) must not keep its GPUs from it."""
+    env.setdefault("TK8S_HOST_REGISTRY", str(root / "hostreg"))
+
+
 def one_bringup(ws: Path, n: int, args, env: dict, log) -> dict:
     answers = {"nodes": n, "package": args.package, "name": "k8s bench", "confirm": "yes"}
     (ws / "answers.json").write_text(json.dumps(answers))
@@ -241,6 +247,7 @@ def main(argv=None) -> int:
 
         build()  # incremental; no-op when the in-tree build is current
     env = child_env(fake)
+    private_registry(env, root)
     log = open(args.log, "a") if (args.log and d.rank == 0) else open(os.devnull, "w")
     try:
         for i in range(args.warmup + args.steps):

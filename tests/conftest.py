@@ -10,6 +10,10 @@ if str(REPO) not in sys.path:
 
 # Keep CPU tests off any GPU and hermetic.
 os.environ.setdefault("TK8S_TEST", "1")
+# One host registry per test run (shared by its xdist workers, whose clusters must stay disjoint),
+# so a cluster an earlier run leaked cannot hold this run's GPU.
+os.environ.setdefault("TK8S_HOST_REGISTRY", os.path.join(
+    os.environ.get("TMPDIR", "/tmp"), f"tk8s-hostreg-{os.environ.get('PYTEST_XDIST_TESTRUNUID') or os.getpid()}"))
 
 
 def pytest_configure(config):
@@ -23,3 +27,10 @@ def native_build():
     from tritonk8ssupervisor_amd.utils.build_native import build
 
     return build()
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not hasattr(session.config, "workerinput"):  # the controller, after every worker is done
+        import shutil
+
+        shutil.rmtree(os.environ["TK8S_HOST_REGISTRY"], ignore_errors=True)
