@@ -6,6 +6,7 @@
 #include "tk8s/rccl_bench.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -130,9 +131,23 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
                        .kv("bad", static_cast<uint64_t>(bad))
                        .str());
   }
+  // What shaped the collective: RCCL's algorithm / protocol / channel overrides (unset = RCCL's
+  // own tuning), and the peak against one xGMI link, i.e. how many links' worth of traffic the
+  // channels spread the ring over.
+  auto env_or = [](const char* k) {
+    const char* v = std::getenv(k);
+    return std::string(v && *v ? v : "auto");
+  };
+  constexpr double kXgmiLinkGBps = 153.0;
   return Json()
       .kv("ok", all_ok)
       .kv("mode", mode)
+      .kv("nccl_algo", env_or("NCCL_ALGO"))
+      .kv("nccl_proto", env_or("NCCL_PROTO"))
+      .kv("nccl_min_nchannels", env_or("NCCL_MIN_NCHANNELS"))
+      .kv("nccl_max_nchannels", env_or("NCCL_MAX_NCHANNELS"))
+      .kv("xgmi_link_gbps", kXgmiLinkGBps)
+      .kv("peak_links_equivalent", all_ranks > 1 ? peak_bus / kXgmiLinkGBps : 0.0)
       .kv("nranks", all_ranks)
       .kv("local_ranks", static_cast<int>(ranks.size()))
       .kv("rccl_version", rccl_version())

@@ -531,7 +531,10 @@ class Setup:
         results = [p.get("status", {}).get("result") or {} for p in pods]
         peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)
         ok = j["status"].get("succeeded", 0) >= g and all(r.get("ok") for r in results)
+        first = next((r for r in results if r), {})
         rep = {"job": job, "ok": ok, "nranks": g, "peak_busbw_gbps": peak,
+               "tuning": {k: first.get(k) for k in ("nccl_algo", "nccl_proto", "nccl_min_nchannels",
+                                                    "nccl_max_nchannels", "peak_links_equivalent") if k in first},
                "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),
                                  "ok": (p.get("status", {}).get("result") or {}).get("ok")} for p in pods]}
         if prof_dir is not None:

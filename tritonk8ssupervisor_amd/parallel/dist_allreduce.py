@@ -129,6 +129,10 @@ def main(argv=None) -> int:
     out = {"ok": res["ok"], "backend": a.backend, "mode": "multi_process", "nranks": a.nranks, "rank": a.rank,
            "dtype": a.dtype, "init_seconds": round(init_s, 4), "peak_busbw_gbps": res["peak_busbw_gbps"],
            "results": res["results"]}
+    if a.backend == "nccl":  # same tuning report as tk8s-rccl
+        for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS"):
+            out[k.lower()] = os.environ.get(k) or "auto"
+        out["peak_links_equivalent"] = res["peak_busbw_gbps"] / 153.0 if a.nranks > 1 else 0.0
     print(json.dumps(out))
     return 0 if res["ok"] else 1
 
