@@ -446,3 +446,18 @@ def test_two_gpu_workers_share_one_host_burnin(ws):
         assert [d["host_index"] for d in burn["devices"]] == m["gpus"] and [d["device"] for d in burn["devices"]] == [0, 1]
         seen += m["gpus"]
     assert sorted(seen) == [0, 1, 2, 3]
+
+
+def test_answers_file_bring_up_starts_the_burnin_before_the_cli_imports(ws):
+    """``./setup.sh --answers FILE``: the burn-in is spawned first thing (earlyburn.py) and the
+    orchestrator adopts it; the workers get its GPUs and reuse its result."""
+    (ws / "answers.json").write_text(json.dumps({"nodes": 2, "package": "mi355x-1gpu", "confirm": "yes"}))
+    s = _summary(_setup(ws, "--answers", "answers.json", "--rccl", "off"))
+    assert s["nodes_validated"] == 2 and s["gpus_allocatable"] == 2
+    events = [json.loads(line) for line in (ws / ".tk8s" / "events.jsonl").read_text().splitlines()]
+    started = [e for e in events if e["event"] == "gpu_burnin_host_started"]
+    assert len(started) == 1 and started[0].get("early") and started[0]["gpus"] == [0, 1]
+    assert not any(e["event"] == "gpu_burnin_early_discarded" for e in events)
+    for i in (1, 2):
+        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
+        assert burn["host_burnin"] and burn["ok"]

@@ -1,0 +1,119 @@
+"""The early host burn-in (earlyburn.py): started by ``cli/__main__.py`` before the CLI imports
+anything, then adopted by the orchestrator -- or discarded when its plan is not exactly the run's."""
+import json
+import os
+
+from tritonk8ssupervisor_amd import earlyburn
+from tritonk8ssupervisor_amd.models.hostinfo import discover
+
+
+def _ws(tmp_path, answers=None):
+    (tmp_path / "answers.json").write_text(json.dumps(answers or {"nodes": 2, "package": "mi355x-1gpu"}))
+    return str(tmp_path)
+
+
+def test_plan_for_a_plain_non_interactive_bring_up(tmp_path):
+    env = {"TK8S_FAKE_GPUS": "8"}
+    ws = _ws(tmp_path)
+    p = earlyburn.plan(["--answers", "answers.json", "--yes", "--json", "--port", "0"], env, ws)
+    assert p["gpus"] == [0, 1] and p["result"] == os.path.join(ws, ".tk8s", "run", "host-burnin.json")
+    assert earlyburn.plan(["--answers=answers.json", "--nodes", "3"], env, ws)["gpus"] == [0, 1, 2]
+    four = earlyburn.plan(["--answers", "answers.json", "--package", "mi355x-4gpu"], env, ws)
+    assert four["gpus"] == list(range(8))
+    assert earlyburn.plan(["--answers", "answers.json", "--nodes", "3", "--package", "mi355x-4gpu"], env, ws) is None
+
+
+def test_anything_unusual_is_left_to_the_orchestrator(tmp_path):
+    env = {"TK8S_FAKE_GPUS": "8"}
+    ws = _ws(tmp_path)
+    for argv in (["--yes"],                                          # interactive: no answers file
+                 ["--answers", "answers.json", "--resume"],
+                 ["--answers", "answers.json", "--no-validate"],
+                 ["--answers", "answers.json", "--hbm-bytes", "1024"],
+                 ["--answers", "answers.json", "--rocprof"],
+                 ["--answers", "answers.json", "--package", "cpu-only"],
+                 ["--answers", "answers.json", "--package", "2"]):  # a menu index: the wizard maps it
+        assert earlyburn.plan(argv, env, ws) is None, argv
+    assert earlyburn.plan(["--answers", "answers.json"], dict(env, TK8S_HOST_BURNIN="0"), ws) is None
+    assert earlyburn.plan(["--answers", "answers.json"], dict(env, TK8S_BACKEND="triton"), ws) is None
+    (tmp_path / "config").write_text("KUBERNETES_NAME=x\n")  # the wizard refuses an old configuration
+    assert earlyburn.plan(["--answers", "answers.json"], env, ws) is None
+
+
+def test_real_host_view_skips_claimed_gpus_and_matches_hostinfo(tmp_path, monkeypatch):
+    root = tmp_path / "kfd"
+    for node, gfx in ((0, 0), (1, 90500), (2, 90500), (3, 90500)):  # node 0: the CPU
+        d = root / str(node)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"gfx_target_version {gfx}\nsimd_count {1024 if gfx else 0}\n")
+    monkeypatch.delenv("TK8S_FAKE_GPUS", raising=False)
+    assert len(earlyburn.kfd_gpu_nodes(str(root))) == discover(root, cache=False).count == 3
+    reg = tmp_path / "reg"
+    reg.mkdir()
+    (reg / "claims.json").write_text(json.dumps({"gpus": {"0": {}}, "ips": {}}))
+    env = {"TK8S_HOST_REGISTRY": str(reg)}
+    ws = _ws(tmp_path)
+    assert earlyburn.plan(["--answers", "answers.json"], env, ws, kfd_root=str(root))["gpus"] == [1, 2]
+    assert earlyburn.plan(["--answers", "answers.json", "--nodes", "3"], env, ws, kfd_root=str(root)) is None
+
+
+def _setup_obj(tmp_path, events):
+    import types
+
+    from tritonk8ssupervisor_amd import orchestrator
+    from tritonk8ssupervisor_amd.config import ClusterConfig
+    from tritonk8ssupervisor_amd.provider.local import LocalProvider
+
+    s = orchestrator.Setup.__new__(orchestrator.Setup)
+    s.ws, s.validate = orchestrator.Workspace(tmp_path), True
+    s.hbm_bytes, s.md5_bytes, s.probe_iters = 1 << 30, 256 << 20, 3
+    s.provider = LocalProvider(tmp_path / ".tk8s")
+    s.cfg = ClusterConfig(HOST_PACKAGE="mi355x-1gpu", KUBERNETES_NUMBER_OF_NODES=2)
+    s.events = types.SimpleNamespace(emit=lambda ev, **kw: events.append((ev, kw)))
+    s.host_burnin = None
+    return s
+
+
+def _spawn_early(tmp_path, gpus, cmd):
+    import sys
+
+    result = tmp_path / ".tk8s" / "run" / "host-burnin.json"
+    result.parent.mkdir(parents=True, exist_ok=True)
+    env = dict(os.environ, **earlyburn.compose_visible_devices(gpus), NODE_NAME="host")
+    argv = cmd + ["--out", str(result)]
+    pid = os.posix_spawn(sys.executable if cmd[0] == sys.executable else cmd[0], argv, env, setsid=True)
+    earlyburn._LAUNCHED = earlyburn.Early(earlyburn.Spawned(pid), gpus, cmd, str(result))
+    return earlyburn._LAUNCHED
+
+
+def test_orchestrator_adopts_a_matching_early_burnin(tmp_path, monkeypatch):
+    monkeypatch.setenv("TK8S_FAKE_GPUS", "8")
+    cmd = [a for a in earlyburn.default_validation_command() if a != "--peers"]
+    early = _spawn_early(tmp_path, [5, 6], cmd)  # not the allocator's own first choice
+    events = []
+    s = _setup_obj(tmp_path, events)
+    s._start_host_burnin()
+    hb = s.host_burnin
+    assert hb is not None and hb.proc is early.proc and hb.gpus == [5, 6]
+    assert ("gpu_burnin_host_started", {"gpus": [5, 6], "pid": early.proc.pid, "early": True}) in events
+    assert hb.finished.wait(30) and hb.result["ok"]
+    # the workers then get exactly the GPUs the early run validated
+    m1 = s.provider.create_machine("kubenode1", "mi355x-1gpu", ["local-public"])
+    m2 = s.provider.create_machine("kubenode2", "mi355x-1gpu", ["local-public"])
+    assert sorted(m1.gpus + m2.gpus) == [5, 6]
+    assert earlyburn.take() is None
+
+
+def test_orchestrator_discards_an_early_burnin_planned_differently(tmp_path, monkeypatch):
+    monkeypatch.setenv("TK8S_FAKE_GPUS", "8")
+    cmd = [a for a in earlyburn.default_validation_command() if a != "--peers"] + ["--iters", "9"]
+    early = _spawn_early(tmp_path, [5, 6], ["/bin/sleep", "30"])
+    early.command = cmd
+    events = []
+    s = _setup_obj(tmp_path, events)
+    s._start_host_burnin()
+    assert early.proc.returncode is not None  # killed and reaped before the right one started
+    assert any(ev == "gpu_burnin_early_discarded" for ev, _ in events)
+    hb = s.host_burnin
+    assert hb is not None and hb.proc is not early.proc and hb.gpus == [0, 1]
+    assert hb.finished.wait(30) and hb.result["ok"]

@@ -30,6 +30,7 @@ from pathlib import Path
 from ..controlplane.client import ApiError, Client
 from ..utils.faults import fault
 from ..utils.k8senv import field_path, service_env
+from ..utils.trace import trace
 from .deviceplugin import DevicePlugin
 from .runtime import PodProc, PodRuntime, install_sigterm
 
@@ -400,6 +401,7 @@ class Agent:
             result["_allocated_ids"] = pp.gpu_ids
             self.plugin.update_from_probe(result)
             self._plugin_changed()
+        trace(self.name, f"report {pp.key} {phase}")
         self._report(pp.key, meta.get("name", pp.key.split("/")[1]), meta.get("namespace", "default"), phase, extra,
                      pp, meta.get("annotations"))
 
@@ -420,6 +422,7 @@ class Agent:
             body["annotations"] = annotations
         try:
             self.api.put(self.api.k8s(f"/api/v1/namespaces/{ns}/pods/{name}/status"), body)
+            trace(self.name, f"reported {key} {phase}")
         except (ApiError, OSError) as e:
             print(f"{self.name}: status report for {key} failed: {e}", flush=True)
 
@@ -500,6 +503,7 @@ class Agent:
         if phase in TERMINAL:
             return
         if key not in self.runtime.running():
+            trace(self.name, f"watch {etype} {key}")
             self._start_pod(pod)
 
     # ---- lifecycle --------------------------------------------------------------------

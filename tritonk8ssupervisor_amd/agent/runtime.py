@@ -20,6 +20,7 @@ from pathlib import Path
 
 from ..utils.fsutil import atomic_write_json
 from ..utils.procs import kill_group
+from ..utils.trace import trace
 
 _VAR = re.compile(r"\$\(([A-Za-z_][A-Za-z0-9_]*)\)")
 
@@ -108,8 +109,10 @@ class PodRuntime:
                 pp.exit_code = 127
                 self.on_status(pp, "Failed", {"message": f"failed to start {pp.argv[0]!r}: {e}", "reason": "StartError"})
                 break
+            trace("runtime", f"spawned {pp.key}")
             self.on_status(pp, "Running", {})
             rc = pp.proc.wait()
+            trace("runtime", f"exited {pp.key} rc={rc}")
             pp.exit_code = rc
             (pp.dir / "pod.pid").unlink(missing_ok=True)
             if pp.stopping:

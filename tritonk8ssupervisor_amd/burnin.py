@@ -167,6 +167,16 @@ class HostBurnin:
         threading.Thread(target=self._wait, name="host-burnin", daemon=True).start()
         return True
 
+    def adopt(self, proc) -> None:
+        """Take over a burn-in already running this exact command over these GPUs into
+        ``result_path`` (earlyburn.py started it before the CLI imported anything)."""
+        import threading
+
+        self.proc = proc
+        self.pidfile.parent.mkdir(parents=True, exist_ok=True)
+        self.pidfile.write_text(f"{proc.pid}\n")
+        threading.Thread(target=self._wait, name="host-burnin", daemon=True).start()
+
     def register(self, name: str, sandbox: str, gpus: list[int]) -> bool:
         """A machine just booted: take its share when ready. False: not covered (probe yourself)."""
         if not gpus or any(g not in self.gpus for g in gpus):

@@ -39,6 +39,7 @@ import time
 from pathlib import Path
 
 from ..utils.net import host_port
+from ..utils.trace import trace
 from .httpserver import HttpError, HttpServer, Request, Response, Router
 from .store import Store, now_iso
 
@@ -621,6 +622,7 @@ class ControlPlane:
 
         res = await self.store.wait_until(check, timeout)
         if res:
+            trace("cp", f"cluster wait -> ready={res.get('ready')}")
             return res
         p = self.project(pid)
         s = self.summary(p["id"])
@@ -1084,6 +1086,7 @@ class ControlPlane:
             if ann:
                 o["metadata"].setdefault("annotations", {}).update(ann)
 
+        trace("cp", f"pod status {ns}/{name} {st.get('phase')}")
         o = self.store.patch("pods", key, fn)
         phase = st.get("phase")
         if phase in ("Running", "Succeeded", "Failed"):
@@ -1091,6 +1094,7 @@ class ControlPlane:
                                                                "Failed": "Failed"}[phase],
                         f"pod {name} {phase.lower()} on {node}", "Warning" if phase == "Failed" else "Normal")
         self.reconcile()
+        trace("cp", f"pod status {ns}/{name} reconciled")
         return self._strip(o)
 
     async def h_pod_log(self, req: Request, ns: str, name: str, pid: str | None = None):

@@ -1,0 +1,277 @@
+"""Start the host GPU burn-in before the setup CLI has imported anything.
+
+The bring-up's critical path is the GPU burn-in (burnin.HostBurnin): ~50 ms of host-wide HIP
+runtime start, a first hardware queue, a few ms of kernels (profiles/r1_init_costs,
+profiles/r1_bench21/events). Everything else -- provisioning, the three plays, the joins --
+finishes inside it. The orchestrator can only start it once it has imported its modules and
+run the wizard (~30 ms after ``./setup.sh`` started), so a non-interactive ``./setup.sh --answers
+FILE`` starts it here instead, straight from ``cli/__main__.py``, with nothing but ``os``/``json``
+loaded: the answers file says how many workers of which package, the KFD sysfs (no GPU runtime
+in this process) and the host registry say which GPUs are free, and ``os.posix_spawn`` runs the
+same ``tk8s-probe`` command the orchestrator would. The orchestrator then *adopts* the process
+(``take()``): the provider prefers exactly these GPUs for the workers, and if its own plan
+differs in any way (command, GPU set, result path) it kills the early run and starts its own,
+so the early start can only save time, never change what is validated.
+
+This module is import-light on purpose (it also holds the helpers the heavy modules share with
+it: visibility env composition, the KFD GPU walk, the validation command, the registry path).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+BIN = os.path.join(PKG, "bin")
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+# ---- shared helpers (re-exported by models/hostinfo.py, provider/hostreg.py, orchestrator.py) ----
+def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 << 20, iters: int = 3) -> list[str]:
+    """The validation DaemonSet payload (and the burn-in): every GPU of a worker."""
+    if os.environ.get("TK8S_FAKE_GPUS"):
+        return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
+    return [os.path.join(BIN, "tk8s-probe"), "--all-devices", "--gpuinfo", "--peers", "--hbm-bytes", str(hbm_bytes),
+            "--md5-bytes", str(md5_bytes), "--iters", str(iters)]
+
+
+def registry_dir(environ=None) -> str:
+    """Where the host-wide IP/GPU claims live (provider/hostreg.py)."""
+    env = os.environ if environ is None else environ
+    d = env.get("TK8S_HOST_REGISTRY")
+    if d:
+        return d
+    return os.path.join(env.get("TMPDIR") or "/tmp", f"tk8s-host-{os.getuid()}")
+
+
+def idx_list(val: str | None) -> list[int] | None:
+    if val is None or val.strip() == "":
+        return None
+    return [int(t) for t in (x.strip() for x in val.split(",")) if t.isdigit()]
+
+
+def visible_filter(n: int, environ=None) -> list[int] | None:
+    """Indices (into the host's KFD GPU order) this process may use: ROCR_VISIBLE_DEVICES picks
+    from the host's GPUs first, then HIP_/CUDA_VISIBLE_DEVICES from what ROCr left (the order
+    the ROCm runtime applies them in)."""
+    env = os.environ if environ is None else environ
+    view = list(range(n))
+    rocr = idx_list(env.get("ROCR_VISIBLE_DEVICES"))
+    if rocr is not None:
+        view = [view[i] for i in rocr if i < len(view)]
+    hip = idx_list(env.get("HIP_VISIBLE_DEVICES")) or idx_list(env.get("CUDA_VISIBLE_DEVICES"))
+    if hip is not None:
+        view = [view[i] for i in hip if i < len(view)]
+    return None if rocr is None and hip is None else view
+
+
+def compose_visible_devices(ordinals: list[int], environ: dict | None = None) -> dict[str, str]:
+    """Env for a child that must see exactly ``ordinals`` of this process's visible GPUs.
+
+    The restriction is applied at the ROCr level (``ROCR_VISIBLE_DEVICES`` = host GPU indices),
+    so the child's runtime only initialises its own GPUs -- on an 8-GPU node a HIP start that
+    brings up all eight agents in every pod and burn-in would multiply start-up cost. The HIP /
+    CUDA variables are reset to the identity over that list."""
+    env = os.environ if environ is None else environ
+    n_hint = max(ordinals, default=-1) + 1
+    view = visible_filter(max(n_hint, 64), env)
+    phys = [(view[i] if view is not None else i) for i in ordinals if view is None or i < len(view)]
+    ident = ",".join(str(i) for i in range(len(phys)))
+    return {"ROCR_VISIBLE_DEVICES": ",".join(map(str, phys)), "HIP_VISIBLE_DEVICES": ident,
+            "CUDA_VISIBLE_DEVICES": ident}
+
+
+def read_props(path: str) -> dict[str, int]:
+    out = {}
+    try:
+        with open(path) as f:
+            for line in f.read().splitlines():
+                parts = line.split()
+                if len(parts) == 2:
+                    try:
+                        out[parts[0]] = int(parts[1])
+                    except ValueError:
+                        pass
+    except OSError:
+        pass
+    return out
+
+
+def kfd_gpu_nodes(root: str = KFD_NODES) -> list[tuple[int, dict, str]]:
+    """(kfd node id, properties, node dir) of every GPU node this process may open, in KFD
+    order: a non-zero ``gfx_target_version`` and SIMDs, and a render node we can read and write
+    (a container may see all GPUs in sysfs but be granted a subset)."""
+    try:
+        names = [n for n in os.listdir(root) if n.isdigit()]
+    except OSError:
+        return []
+    out = []
+    for name in sorted(names, key=int):
+        d = os.path.join(root, name)
+        p = read_props(os.path.join(d, "properties"))
+        if not (p.get("gfx_target_version", 0) and p.get("simd_count", 0)):
+            continue
+        minor = p.get("drm_render_minor", -1)
+        if minor >= 0:
+            dev = f"/dev/dri/renderD{minor}"
+            if not os.path.exists(dev) or not os.access(dev, os.R_OK | os.W_OK):
+                continue
+        out.append((int(name), p, d))
+    return out
+
+
+# ---- the early start ----------------------------------------------------------------------------
+_VALUE_FLAGS = {"--answers", "--port", "--timeout", "--rccl-timeout", "--rccl", "--nodes", "--package", "--name",
+                "--master-hostname", "--node-prefix", "--node-grace", "--rccl-max-bytes"}
+_BOOL_FLAGS = {"--yes", "--json", "-v", "--verbose"}
+
+
+def package_gpus(name) -> int | None:
+    """GPUs per machine of a local package given by name (``mi355x-<k>gpu`` / ``cpu-only``)."""
+    s = str(name)
+    if s == "cpu-only":
+        return 0
+    if s.startswith("mi355x-") and s.endswith("gpu") and s[7:-3].isdigit():
+        return int(s[7:-3])
+    return None
+
+
+def _host_claimed_gpus(environ=None) -> set[int]:
+    try:
+        with open(os.path.join(registry_dir(environ), "claims.json")) as f:
+            return {int(k) for k in (json.load(f) or {}).get("gpus", {})}
+    except (OSError, ValueError, AttributeError):
+        return set()
+
+
+def plan(argv: list[str], environ=None, cwd: str | None = None, kfd_root: str = KFD_NODES) -> dict | None:
+    """What to burn in for ``tk8s setup <argv>``, or None when this run is not a plain fresh
+    non-interactive local bring-up (anything unusual is left to the orchestrator)."""
+    env = os.environ if environ is None else environ
+    if env.get("TK8S_HOST_BURNIN", "1") == "0" or env.get("TK8S_BACKEND", "local") != "local":
+        return None
+    opts: dict[str, str] = {}
+    i = 0
+    while i < len(argv):
+        a = argv[i]
+        if "=" in a and a.split("=", 1)[0] in _VALUE_FLAGS:
+            k, v = a.split("=", 1)
+            opts[k] = v
+        elif a in _VALUE_FLAGS and i + 1 < len(argv):
+            opts[a] = argv[i + 1]
+            i += 1
+        elif a not in _BOOL_FLAGS:
+            return None  # --resume, --no-validate, probe sizes, rocprof, ...: the orchestrator decides
+        i += 1
+    answers_file = opts.get("--answers")
+    if not answers_file:
+        return None
+    cwd = cwd or os.getcwd()
+    ws = env.get("TK8S_WORKDIR") or cwd
+    answers_path = os.path.join(cwd, answers_file)  # as the CLI opens it: relative to the cwd
+    if (os.path.exists(os.path.join(ws, "config")) or os.path.exists(os.path.join(ws, "terraform", "rancher.tf"))
+            or not answers_path.endswith(".json")):
+        return None
+    try:
+        with open(answers_path) as f:
+            answers = {str(k).lower(): v for k, v in json.load(f).items()}
+    except (OSError, ValueError, AttributeError):
+        return None
+    nodes = str(opts.get("--nodes", answers.get("nodes", 1)) or 1)
+    per = package_gpus(opts.get("--package", answers.get("package") or "mi355x-1gpu"))
+    if not (len(nodes) == 1 and nodes in "123456789") or not per:
+        return None
+    count = int(nodes) * per
+    fake = env.get("TK8S_FAKE_GPUS")
+    if fake:
+        free = list(range(int(fake)))
+    else:
+        n = len(kfd_gpu_nodes(kfd_root))
+        vis = visible_filter(n, env)
+        claimed = _host_claimed_gpus(env)
+        free = [i for i in range(len(vis) if vis is not None else n) if i not in claimed]
+    if len(free) < count:
+        return None
+    cmd = default_validation_command()
+    if per <= 1:  # no xGMI link inside any machine: the RCCL Job checks the fabric
+        cmd = [a for a in cmd if a != "--peers"]
+    state = os.path.join(ws, ".tk8s")
+    return {"gpus": free[:count], "command": cmd, "state_dir": state,
+            "result": os.path.join(state, "run", "host-burnin.json")}
+
+
+class Spawned:
+    """The early burn-in process (a child of this process, its own session): Popen's poll/wait."""
+
+    def __init__(self, pid: int):
+        self.pid = pid
+        self.returncode: int | None = None
+
+    def _status(self, flags: int) -> int | None:
+        if self.returncode is None:
+            try:
+                pid, status = os.waitpid(self.pid, flags)
+            except ChildProcessError:  # reaped elsewhere: its result file is what counts
+                self.returncode = -1
+                return self.returncode
+            if pid:
+                self.returncode = os.waitstatus_to_exitcode(status)
+        return self.returncode
+
+    def poll(self) -> int | None:
+        return self._status(os.WNOHANG)
+
+    def wait(self) -> int:
+        return self._status(0)
+
+
+class Early:
+    def __init__(self, proc: Spawned, gpus: list[int], command: list[str], result: str):
+        self.proc, self.gpus, self.command, self.result = proc, gpus, command, result
+
+    def kill(self) -> None:
+        try:
+            os.killpg(self.proc.pid, 15)
+        except OSError:
+            pass
+
+
+_LAUNCHED: Early | None = None
+
+
+def launch(argv: list[str]) -> Early | None:
+    """Called first thing by ``python -m tritonk8ssupervisor_amd.cli setup ...``."""
+    global _LAUNCHED
+    try:
+        p = plan(argv)
+        if p is None:
+            return None
+        run = os.path.join(p["state_dir"], "run")
+        os.makedirs(run, exist_ok=True)
+        try:
+            os.unlink(p["result"])
+        except FileNotFoundError:
+            pass
+        env = dict(os.environ)
+        env.update(compose_visible_devices(p["gpus"]))
+        env["NODE_NAME"] = "host"
+        cmd = p["command"] + ["--out", p["result"]]
+        pid = os.posix_spawn(cmd[0], cmd, env, setsid=True, file_actions=[
+            (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
+            (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
+            (os.POSIX_SPAWN_OPEN, 2, os.path.join(run, "host-burnin.log"), os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644),
+        ])
+        with open(os.path.join(run, "host-burnin.pid"), "w") as f:
+            f.write(f"{pid}\n")
+    except Exception:  # noqa: BLE001 - an optimisation only: the orchestrator starts its own
+        return None
+    _LAUNCHED = Early(Spawned(pid), p["gpus"], p["command"], p["result"])
+    return _LAUNCHED
+
+
+def take() -> Early | None:
+    """Hand the early burn-in (if any) to the orchestrator, once."""
+    global _LAUNCHED
+    e, _LAUNCHED = _LAUNCHED, None
+    return e

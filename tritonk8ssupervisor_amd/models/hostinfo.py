@@ -17,6 +17,8 @@ import os
 from dataclasses import asdict, dataclass, field
 from pathlib import Path
 
+from ..earlyburn import compose_visible_devices, idx_list, kfd_gpu_nodes, read_props, visible_filter  # noqa: F401
+
 KFD_ROOT = Path("/sys/class/kfd/kfd/topology/nodes")
 IOLINK_XGMI = 11
 IOLINK_PCIE = 2
@@ -81,25 +83,8 @@ def _gfx_name(v: int) -> str:
     return f"gfx{major}{minor:x}{step:x}" if v else "cpu"
 
 
-def _idx_list(val: str | None) -> list[int] | None:
-    if val is None or val.strip() == "":
-        return None
-    return [int(t) for t in (x.strip() for x in val.split(",")) if t.isdigit()]
-
-
-def _visible_filter(n: int, environ=None) -> list[int] | None:
-    """Indices (into the host's KFD GPU order) this process may use: ROCR_VISIBLE_DEVICES picks
-    from the host's GPUs first, then HIP_/CUDA_VISIBLE_DEVICES from what ROCr left (the order
-    the ROCm runtime applies them in)."""
-    env = os.environ if environ is None else environ
-    view = list(range(n))
-    rocr = _idx_list(env.get("ROCR_VISIBLE_DEVICES"))
-    if rocr is not None:
-        view = [view[i] for i in rocr if i < len(view)]
-    hip = _idx_list(env.get("HIP_VISIBLE_DEVICES")) or _idx_list(env.get("CUDA_VISIBLE_DEVICES"))
-    if hip is not None:
-        view = [view[i] for i in hip if i < len(view)]
-    return None if rocr is None and hip is None else view
+_idx_list = idx_list
+_visible_filter = visible_filter
 
 
 def fake_inventory(n: int) -> HostInventory:
@@ -130,21 +115,10 @@ def _discover(root: Path) -> HostInventory:
     fake = os.environ.get("TK8S_FAKE_GPUS")
     if fake is not None and fake.strip() != "":
         return fake_inventory(int(fake))
-    nodes = []
-    if root.is_dir():
-        for d in sorted(root.iterdir(), key=lambda p: int(p.name) if p.name.isdigit() else 1 << 30):
-            if not d.name.isdigit():
-                continue
-            p = _props(d / "properties")
-            if p.get("gfx_target_version", 0) and p.get("simd_count", 0):
-                nodes.append((int(d.name), p, d))
+    nodes = [(n, p, Path(d)) for n, p, d in kfd_gpu_nodes(str(root))]
     gpus: list[HostGpu] = []
     for kfd_node, p, _ in nodes:
         minor = p.get("drm_render_minor", -1)
-        if minor >= 0:
-            dev = Path(f"/dev/dri/renderD{minor}")
-            if not dev.exists() or not os.access(dev, os.R_OK | os.W_OK):
-                continue
         gpus.append(HostGpu(
             ordinal=len(gpus), kfd_node=kfd_node, gfx=_gfx_name(p.get("gfx_target_version", 0)),
             render_minor=minor, simd_count=p.get("simd_count", 0),
@@ -175,19 +149,3 @@ def _discover(root: Path) -> HostInventory:
             links[i][j] = {"type": "xgmi" if t == IOLINK_XGMI else "pcie" if t == IOLINK_PCIE else "unknown",
                            "hops": 1}
     return HostInventory(gpus=gpus, links=links, source="kfd-sysfs" if n else "none")
-
-
-def compose_visible_devices(ordinals: list[int], environ: dict | None = None) -> dict[str, str]:
-    """Env for a child that must see exactly ``ordinals`` of this process's visible GPUs.
-
-    The restriction is applied at the ROCr level (``ROCR_VISIBLE_DEVICES`` = host GPU indices),
-    so the child's runtime only initialises its own GPUs -- on an 8-GPU node a HIP start that
-    brings up all eight agents in every pod and burn-in would multiply start-up cost. The HIP /
-    CUDA variables are reset to the identity over that list."""
-    env = os.environ if environ is None else environ
-    n_hint = max(ordinals, default=-1) + 1
-    view = _visible_filter(max(n_hint, 64), env)
-    phys = [(view[i] if view is not None else i) for i in ordinals if view is None or i < len(view)]
-    ident = ",".join(str(i) for i in range(len(phys)))
-    return {"ROCR_VISIBLE_DEVICES": ",".join(map(str, phys)), "HIP_VISIBLE_DEVICES": ident,
-            "CUDA_VISIBLE_DEVICES": ident}

@@ -26,6 +26,7 @@ from typing import Callable
 
 from . import hcl
 from .config import ClusterConfig, export_vars, read_config, write_config
+from .earlyburn import default_validation_command  # noqa: F401 - shared with the early burn-in
 from .provider import get_provider
 from .provider.base import Machine, ProvisionError
 from .provision import Engine
@@ -186,16 +187,6 @@ class MachineExecutor:
     def stop_daemon(self, host: str, name: str) -> bool:
         pidfile, _ = self._paths(host, name)
         return kill_pidfile(pidfile)
-
-
-def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 << 20, iters: int = 3) -> list[str]:
-    """The validation DaemonSet payload (and the early burn-in): every GPU of a worker."""
-    if os.environ.get("TK8S_FAKE_GPUS"):
-        return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
-    from .ops import BIN
-
-    return [str(BIN / "tk8s-probe"), "--all-devices", "--gpuinfo", "--peers", "--hbm-bytes", str(hbm_bytes),
-            "--md5-bytes", str(md5_bytes), "--iters", str(iters)]
 
 
 def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, Machine], *, node_grace: float = 5.0,
@@ -378,23 +369,40 @@ class Setup:
         start is host-wide and serialised across processes, so N per-machine burn-ins would stack
         N starts on the critical path), started as soon as the configuration says which GPUs the
         workers will get -- before the machines exist. Machines not covered probe on their own."""
+        from . import earlyburn
+
+        early = earlyburn.take()  # started by cli/__main__.py before any import (earlyburn.py)
         if not (self.validate and hasattr(self.provider, "predict_gpus")) or os.environ.get("TK8S_HOST_BURNIN", "1") == "0":
+            if early is not None:
+                early.kill()
             return
         try:
             pkg = self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE)
+            cmd = self._validation_command()
+            if int(pkg.gpus or 0) <= 1:  # no xGMI link inside any machine: the RCCL Job checks the fabric
+                cmd = [a for a in cmd if a != "--peers"]
+            if early is not None and early.command == cmd and hasattr(self.provider, "prefer_gpus"):
+                self.provider.prefer_gpus(early.gpus)
             gpus = self.provider.predict_gpus(int(pkg.gpus or 0), int(self.cfg.KUBERNETES_NUMBER_OF_NODES))
         except Exception:  # noqa: BLE001 - prediction is an optimisation only
-            return
-        if not gpus:
-            return
+            gpus, cmd = [], None
         import threading
 
         from .burnin import HostBurnin
 
-        cmd = self._validation_command()
-        if int(pkg.gpus or 0) <= 1:  # no xGMI link inside any machine: the RCCL Job checks the fabric
-            cmd = [a for a in cmd if a != "--peers"]
-        hb = HostBurnin(cmd, gpus, self.ws.state_dir, log=self.events.emit)
+        hb = HostBurnin(cmd, gpus, self.ws.state_dir, log=self.events.emit) if gpus else None
+        if early is not None:
+            if (hb is not None and early.command == cmd and sorted(early.gpus) == sorted(gpus)
+                    and Path(early.result) == hb.result_path):
+                hb.adopt(early.proc)
+                self.host_burnin = hb
+                self.events.emit("gpu_burnin_host_started", gpus=gpus, pid=early.proc.pid, early=True)
+                return
+            early.kill()  # planned differently from what the run needs: start the right one,
+            early.proc.wait()  # once this one can no longer write the shared result file
+            self.events.emit("gpu_burnin_early_discarded", gpus=early.gpus, wanted=gpus)
+        if hb is None:
+            return
         self.host_burnin = hb  # machines register from now on; the process starts off this thread
 
         def launch():

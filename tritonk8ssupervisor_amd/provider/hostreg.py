@@ -5,7 +5,7 @@ host the local provider plays that cloud for every cluster the host runs, so eac
 own ``alloc.json`` is not enough: two clusters brought up side by side (two users, or parallel
 test workers) would both take 127.0.1.1 for their master -- and with it the same DNS, ingress
 and NodePort sockets -- and both claim GPU 0. This registry is the host's view: one JSON file
-under a per-user directory (``$TK8S_HOST_REGISTRY``, default ``$TMPDIR/tk8s-host-<uid>``),
+under a per-user directory (``$TK8S_HOST_REGISTRY``, default ``${TMPDIR:-/tmp}/tk8s-host-<uid>``),
 guarded by an flock and always taken *inside* the workspace lock (workspace, then host: no
 lock-order inversion).
 
@@ -18,7 +18,6 @@ from __future__ import annotations
 
 import contextlib
 import os
-import tempfile
 from pathlib import Path
 from typing import Iterator
 
@@ -27,8 +26,9 @@ from ..utils.procs import pid_alive, read_pidfile
 
 
 def registry_dir() -> Path:
-    d = os.environ.get("TK8S_HOST_REGISTRY")
-    return Path(d) if d else Path(tempfile.gettempdir()) / f"tk8s-host-{os.getuid()}"
+    from ..earlyburn import registry_dir as path  # one definition: the early burn-in reads it too
+
+    return Path(path())
 
 
 def _sandbox_alive(sandbox: Path) -> bool:
@@ -65,6 +65,7 @@ class HostRegistry:
         self.dir.mkdir(parents=True, exist_ok=True, mode=0o700)
         with file_lock(self.lock_file):
             table = read_json(self.file, {}) or {}
+            before = repr(table)
             for kind in ("ips", "gpus"):
                 claims = table.setdefault(kind, {})
                 owners: dict[tuple, bool] = {}
@@ -75,7 +76,6 @@ class HostRegistry:
                         owners[k] = _stale(c)
                     if owners[k]:
                         del claims[key]
-            before = repr(table)
             yield table
             if repr(table) != before or not self.file.exists():
                 atomic_write_json(self.file, table)

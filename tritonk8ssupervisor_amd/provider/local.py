@@ -75,6 +75,16 @@ class LocalProvider(Provider):
         self.lock_file = self.state_dir / "alloc.lock"
         self.host = HostRegistry()
         self._multi_ip = None
+        self.preferred_gpus: list[int] = []  # an early burn-in is already validating these
+
+    def prefer_gpus(self, gpus: list[int]) -> None:
+        """Hand workers these GPUs first (when enough of them are free): the early burn-in
+        (earlyburn.py) picked them before the allocator ran."""
+        self.preferred_gpus = list(gpus)
+
+    def _candidates(self, free: list[int], count: int) -> list[int]:
+        pref = [g for g in free if g in self.preferred_gpus]
+        return pref if len(pref) >= count else free
 
     # ---- inventory ----------------------------------------------------------------
     def env(self) -> dict[str, str]:
@@ -145,6 +155,8 @@ class LocalProvider(Provider):
         if self._host_gpus():
             taken |= {int(k) for k in HostRegistry.taken(host, "gpus")}
         free = [g.ordinal for g in inv.gpus if g.ordinal not in taken]
+        if len(free) >= count:
+            free = self._candidates(free, count)
         if len(free) < count:
             raise ProvisionError(
                 f"{name}: package needs {count} GPU(s) but only {len(free)} of {inv.count} are free "
@@ -186,11 +198,12 @@ class LocalProvider(Provider):
             for _ in range(machines):
                 if len(free) < per_machine:
                     break
-                pick = list(topo().preferred_allocation(inv.count, w, free, [], per_machine)["devices"])
+                pick = list(topo().preferred_allocation(inv.count, w, self._candidates(free, per_machine), [],
+                                                        per_machine)["devices"])
                 out += pick
                 free = [g for g in free if g not in pick]
         except Exception:  # noqa: BLE001 - allocator module optional
-            out = free[: per_machine * machines]
+            out = self._candidates(free, per_machine * machines)[: per_machine * machines]
         return sorted(out)
 
     # ---- lifecycle ----------------------------------------------------------------
