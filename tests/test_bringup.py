@@ -458,6 +458,27 @@ def test_answers_file_bring_up_starts_the_burnin_before_the_cli_imports(ws):
     started = [e for e in events if e["event"] == "gpu_burnin_host_started"]
     assert len(started) == 1 and started[0].get("early") and started[0]["gpus"] == [0, 1]
     assert not any(e["event"] == "gpu_burnin_early_discarded" for e in events)
+    # the control plane's interpreter started with the CLI and got its arguments at master boot
+    boot = [e for e in events if e["event"] == "controlplane_boot_started"]
+    assert len(boot) == 1 and boot[0].get("zygote")
+    assert json.loads((ws / ".tk8s" / "machines" / "kubemaster" / "run" / "controlplane.args").read_text())[0] == "--host"
+    # the agents started with their machines; rocmsetup's standby task found them running
+    assert sorted(e["name"] for e in events if e["event"] == "agent_boot_started") == ["kubenode1", "kubenode2"]
+    standby = [e for e in events if e.get("task", "").endswith("Start the node agent in standby on every host")]
+    assert standby and all(v in ("ok", "skipped") for v in standby[0]["results"].values()), standby
     for i in (1, 2):
         burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
         assert burn["host_burnin"] and burn["ok"]
+
+
+def test_agent_boot_hook_uses_the_roles_standby_argv():
+    """The worker boot hook pre-starts the agent the rocmsetup role would start: same argv, so
+    the role's task finds it running instead of starting a second one."""
+    import yaml
+
+    from tritonk8ssupervisor_amd.orchestrator import agent_standby_argv
+
+    tasks = yaml.safe_load((REPO / "ansible" / "roles" / "rocmsetup" / "tasks" / "main.yml").read_text())
+    t = next(t for t in tasks if t.get("name") == "Start the node agent in standby on every host")
+    subst = {"{{ tk8s_python }}": sys.executable, "{{ inventory_hostname }}": "kubenode1", "{{ ansible_host }}": "127.0.1.2"}
+    assert [subst.get(a, a) for a in t["tk8s_daemon"]["argv"]] == agent_standby_argv("kubenode1", "127.0.1.2")

@@ -117,3 +117,47 @@ def test_orchestrator_discards_an_early_burnin_planned_differently(tmp_path, mon
     hb = s.host_burnin
     assert hb is not None and hb.proc is not early.proc and hb.gpus == [0, 1]
     assert hb.finished.wait(30) and hb.result["ok"]
+
+
+def test_controlplane_zygote_nobody_hands_arguments_to_stops_with_its_supervisor(tmp_path, native_build):
+    """A bring-up that dies before its master exists must not leave a control plane (or a
+    supervisor restarting it) behind."""
+    import subprocess
+    import sys
+    import time
+
+    from tritonk8ssupervisor_amd.ops import BIN
+
+    pidfile = tmp_path / "cp.pid"
+    env = dict(os.environ, TK8S_ZYGOTE_TIMEOUT="0.3", PYTHONPATH=str(earlyburn.PKG.rsplit(os.sep, 1)[0]))
+    p = subprocess.Popen([str(BIN / "tk8s-supervise"), "--pidfile", str(pidfile), "--restart", "unless-stopped", "--",
+                          sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.controlplane", "--await-args",
+                          str(tmp_path / "never.args")], env=env, start_new_session=True)
+    assert p.wait(30) in (0, 143, -15)
+    time.sleep(0.05)
+    assert not pidfile.exists()
+
+
+def test_controlplane_zygote_serves_once_its_arguments_arrive(tmp_path):
+    import socket
+    import subprocess
+    import sys
+    import urllib.request
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    args = tmp_path / "cp.args"
+    env = dict(os.environ, PYTHONPATH=str(earlyburn.PKG.rsplit(os.sep, 1)[0]))
+    p = subprocess.Popen([sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.controlplane", "--await-args", str(args)],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    try:
+        args.write_text(json.dumps(["--host", "127.0.0.1", "--port", str(port), "--dns-port", "0", "--ingress-port", "0"]))
+        line = p.stdout.readline()
+        assert "Listening on" in line, line
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/v2-beta/projectTemplates?name=kubernetes", timeout=5) as r:
+            assert r.status == 200
+    finally:
+        p.terminate()
+        p.wait(10)

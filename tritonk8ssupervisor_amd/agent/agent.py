@@ -102,10 +102,11 @@ class Agent:
             except OSError:
                 url = ""
             if url:
+                trace(self.name, "registration url seen")
                 self.set_url(url)
                 return
             time.sleep(delay)
-            delay = min(delay * 2, 0.005)
+            delay = min(delay * 2, 0.001)  # one stat per ms while idle; the join starts <= 1 ms late
         raise SystemExit(0)
 
     # ---- device plugin over the kubelet API ----------------------------------------------
@@ -515,6 +516,7 @@ class Agent:
             self.await_url(await_url)
         t0 = time.monotonic()
         self.join()
+        trace(self.name, "joined")
         print(f"{self.name}: registered in {time.monotonic() - t0:.3f}s "
               f"({len(self.plugin.devices())} GPU, inventory={self.plugin.inventory.source})", flush=True)
         threads = [threading.Thread(target=self.heartbeat_loop, name="heartbeat", daemon=True),

@@ -429,6 +429,7 @@ class ControlPlane:
         self.leases[key] = time.monotonic()
         self._event(pid, "default", {"kind": "Node", "name": name}, "RegisteredNode", f"Node {name} registered ({len(gpus)} GPU)")
         self.reconcile()
+        trace("cp", f"node {name} registered")
         return Response(201, {"node": name, "nodeToken": ntok, "projectId": pid, "podCIDR": cidr,
                               "apiPrefix": f"/r/projects/{pid}/kubernetes",
                               "heartbeatSeconds": max(0.2, self.node_grace / 5)})
@@ -1503,6 +1504,33 @@ def _parse_selector(s: str | None) -> dict | None:
             k, v = part.split("=", 1)
             out[k.strip().rstrip("=")] = v.strip()
     return out
+
+
+def await_args(path: str, timeout: float | None = None) -> list[str]:
+    """Zygote mode: wait for the JSON argument list (orchestrator._boot_controlplane writes it
+    atomically). A zygote nobody hands arguments to -- the bring-up failed before its master
+    existed -- stops its supervisor and exits, so it never lingers or restarts."""
+    if timeout is None:
+        timeout = float(os.environ.get("TK8S_ZYGOTE_TIMEOUT", "120"))
+    deadline = time.monotonic() + timeout
+    while True:
+        try:
+            with open(path) as f:
+                argv = json.load(f)
+            if isinstance(argv, list):
+                return [str(a) for a in argv]
+        except (OSError, ValueError):
+            pass
+        if time.monotonic() > deadline:
+            parent = os.getppid()
+            try:
+                with open(f"/proc/{parent}/comm") as f:
+                    if f.read().strip() == "tk8s-supervise":
+                        os.kill(parent, signal.SIGTERM)
+            except OSError:
+                pass
+            raise SystemExit(0)
+        time.sleep(0.001)
 
 
 def main(argv: list[str] | None = None) -> int:

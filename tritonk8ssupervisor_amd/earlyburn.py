@@ -197,8 +197,11 @@ def plan(argv: list[str], environ=None, cwd: str | None = None, kfd_root: str = 
     if per <= 1:  # no xGMI link inside any machine: the RCCL Job checks the fabric
         cmd = [a for a in cmd if a != "--peers"]
     state = os.path.join(ws, ".tk8s")
+    master = str(opts.get("--master-hostname", answers.get("master_hostname") or "kubemaster"))
     return {"gpus": free[:count], "command": cmd, "state_dir": state,
-            "result": os.path.join(state, "run", "host-burnin.json")}
+            "result": os.path.join(state, "run", "host-burnin.json"),
+            # the wizard's hostname rule (^[a-zA-Z][0-9a-zA-Z]+$); anything else: no zygote
+            "master": master if len(master) >= 2 and master.isascii() and master.isalnum() and master[0].isalpha() else None}
 
 
 class Spawned:
@@ -238,11 +241,56 @@ class Early:
 
 
 _LAUNCHED: Early | None = None
+_ZYGOTE: dict | None = None
+
+
+def controlplane_zygote(p: dict) -> dict | None:
+    """Start the control plane's interpreter now, under its supervisor, in the master's future
+    sandbox: it imports everything (asyncio alone is ~40-60 ms of interpreter work) while the
+    orchestrator starts, provisions and runs play 1, then waits for its arguments -- the master's
+    address and port, known only once the machine exists -- in ``run/controlplane.args``
+    (``orchestrator._boot_controlplane`` writes them). Same pidfile and log as a control plane
+    started by the boot hook or the ranchermaster role, so both find it running; a restart
+    re-reads the same arguments. It gives up (and stops its supervisor) if no arguments come."""
+    if not p.get("master") or os.environ.get("TK8S_BOOT_CONTROLPLANE", "1") == "0" \
+            or os.environ.get("TK8S_CP_ZYGOTE", "1") == "0":
+        return None
+    sup = os.path.join(BIN, "tk8s-supervise")
+    if not os.access(sup, os.X_OK):
+        return None
+    sb = os.path.join(p["state_dir"], "machines", p["master"])
+    pidfile = os.path.join(sb, "run", "controlplane.pid")
+    if os.path.exists(pidfile):  # something of an earlier run: leave it to the orchestrator
+        return None
+    os.makedirs(os.path.join(sb, "run"), exist_ok=True)
+    os.makedirs(os.path.join(sb, "logs"), exist_ok=True)
+    args = os.path.join(sb, "run", "controlplane.args")
+    argv = [sup, "--pidfile", pidfile, "--log", os.path.join(sb, "logs", "controlplane.log"), "--restart",
+            "unless-stopped", "--", sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.controlplane",
+            "--await-args", args]
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(PKG)] + [x for x in env.get("PYTHONPATH", "").split(os.pathsep) if x])
+    pid = os.posix_spawn(sup, argv, env, setsid=True, file_actions=[
+        (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
+        (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
+        (os.POSIX_SPAWN_OPEN, 2, os.devnull, os.O_WRONLY, 0),
+    ])
+    return {"pid": pid, "sandbox": sb, "args": args, "pidfile": pidfile}
+
+
+def zygote_for(sandbox: str) -> dict | None:
+    """The control plane zygote started for this master sandbox, if any (once)."""
+    global _ZYGOTE
+    z = _ZYGOTE
+    if z is not None and os.path.realpath(z["sandbox"]) == os.path.realpath(sandbox):
+        _ZYGOTE = None
+        return z
+    return None
 
 
 def launch(argv: list[str]) -> Early | None:
     """Called first thing by ``python -m tritonk8ssupervisor_amd.cli setup ...``."""
-    global _LAUNCHED
+    global _LAUNCHED, _ZYGOTE
     try:
         p = plan(argv)
         if p is None:
@@ -267,6 +315,10 @@ def launch(argv: list[str]) -> Early | None:
     except Exception:  # noqa: BLE001 - an optimisation only: the orchestrator starts its own
         return None
     _LAUNCHED = Early(Spawned(pid), p["gpus"], p["command"], p["result"])
+    try:
+        _ZYGOTE = controlplane_zygote(p)
+    except Exception:  # noqa: BLE001 - the boot hook starts the control plane the usual way
+        _ZYGOTE = None
     return _LAUNCHED
 
 

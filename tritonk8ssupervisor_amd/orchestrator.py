@@ -219,6 +219,13 @@ def controlplane_argv(bind: str, port: int, advertise: str, state_dir: str, node
             "--advertise", advertise, "--state-dir", state_dir, "--node-grace", str(node_grace)]
 
 
+def agent_standby_argv(name: str, ip: str) -> list[str]:
+    """The node agent in standby (rocmsetup's "Start the node agent in standby" task spells out
+    the same argv), waiting for play 3's registration URL."""
+    return [sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.agent", "--await-url", "run/registration-url",
+            "--name", name, "--ip", ip]
+
+
 def validation_pod_command(command: list[str], result: str = "$(TK8S_MACHINE_DIR)/run/gpu-burnin.json") -> list[str]:
     """The validation DaemonSet pod: reuse the node's burn-in result, probe only without one.
     With the real probe the reuse runs in tk8s-reuse, which loads no ROCm library."""
@@ -316,6 +323,8 @@ class Setup:
         rocmsetup's burn-in task then finds it running and does nothing."""
         if self.cfg is not None and m.name == self.cfg.RANCHER_MASTER_HOSTNAME and hasattr(self.provider, "machine_env"):
             self._boot_controlplane(m)
+        elif self.cfg is not None and hasattr(self.provider, "machine_env"):
+            self._boot_agent(m)
         if not (self.validate and m.gpus and hasattr(self.provider, "machine_env")):
             return
         if self.host_burnin is not None and self.host_burnin.register(m.name, m.sandbox, list(m.gpus)):
@@ -327,6 +336,20 @@ class Setup:
         r = start_burnin(ex, m.name, self._validation_command(), "run/gpu-burnin.json")
         self.events.emit("gpu_burnin_started", name=m.name, **{k: v for k, v in r.items() if k in ("pid", "gpus", "msg")})
 
+    def _boot_agent(self, m: Machine) -> None:
+        """Worker boot hook: the node agent (kubelet role) starts in standby with its machine, the
+        way a node image starts its kubelet at boot. Its interpreter start and imports (~30 ms on
+        the MI355X box, profiles/r1_trace2) then overlap provisioning and play 1 instead of
+        delaying the join after play 3 hands it the registration URL; rocmsetup's standby task
+        finds it running (same argv: agent_standby_argv)."""
+        if os.environ.get("TK8S_BOOT_AGENT", "1") == "0":
+            return
+        pythonpath = os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+        ex = MachineExecutor(self.provider, {m.name: m})
+        info = ex.start_daemon(m.name, "agent", agent_standby_argv(m.name, m.primaryip), env={"PYTHONPATH": pythonpath},
+                               restart="unless-stopped", wait_for_log=None, timeout=0)
+        self.events.emit("agent_boot_started", name=m.name, pid=info.get("pid"))
+
     def _boot_controlplane(self, m: Machine) -> None:
         """Master boot hook: the control plane service starts with its machine (the way a master
         image would start rancher/server at boot), overlapping the workers' creation and play 1;
@@ -335,6 +358,18 @@ class Setup:
             return
         argv = controlplane_argv(m.primaryip, int(self.cfg.TK8S_MASTER_PORT), m.primaryip,
                                  str(Path(m.sandbox) / "controlplane"), self.node_grace)
+        from . import earlyburn
+
+        z = earlyburn.zygote_for(m.sandbox)  # its interpreter started with the CLI: hand it the arguments
+        if z is not None:
+            if pid_alive(z["pid"]):  # its supervisor (a child of this process)
+                atomic_write(z["args"], json.dumps(argv[4:]))
+                self.events.emit("controlplane_boot_started", name=m.name, pid=z["pid"], zygote=True)
+                return
+            try:  # gone or going: make sure no part of it outlives the regular start below
+                os.killpg(z["pid"], 15)
+            except OSError:
+                pass
         pythonpath = os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
         ex = MachineExecutor(self.provider, {m.name: m})
         info = ex.start_daemon(m.name, "controlplane", argv, env={"PYTHONPATH": pythonpath}, restart="unless-stopped",
