@@ -5,8 +5,8 @@ runtime start, a first hardware queue, a few ms of kernels (profiles/r1_init_cos
 profiles/r1_bench21/events). Everything else -- provisioning, the three plays, the joins --
 finishes inside it. The orchestrator can only start it once it has imported its modules and
 run the wizard (~30 ms after ``./setup.sh`` started), so a non-interactive ``./setup.sh --answers
-FILE`` starts it here instead, straight from ``cli/__main__.py``, with nothing but ``os``/``json``
-loaded: the answers file says how many workers of which package, the KFD sysfs (no GPU runtime
+FILE`` starts it here instead, straight from ``cli/__main__.py``, with nothing but ``os``
+loaded (JSON through the C scanner): the answers file says how many workers of which package, the KFD sysfs (no GPU runtime
 in this process) and the host registry say which GPUs are free, and ``os.posix_spawn`` runs the
 same ``tk8s-probe`` command the orchestrator would. The orchestrator then *adopts* the process
 (``take()``): the provider prefers exactly these GPUs for the workers, and if its own plan
@@ -18,13 +18,36 @@ it: visibility env composition, the KFD GPU walk, the validation command, the re
 """
 from __future__ import annotations
 
-import json
 import os
 import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 BIN = os.path.join(PKG, "bin")
 KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _loads(text: str):
+    """json.loads through the C scanner alone: ``import json`` pulls in ``re`` (~4-8 ms of
+    interpreter work, the largest import on this path); ``_json`` is ~0.5 ms."""
+    try:
+        import _json
+    except ImportError:  # pragma: no cover - CPython always has it
+        import json
+
+        return json.loads(text)
+
+    class _Ctx:
+        strict = True
+        object_hook = object_pairs_hook = None
+        parse_float, parse_int, parse_constant = float, int, float
+
+    s = text.strip()
+    if not s:
+        raise ValueError("empty document")
+    obj, end = _json.make_scanner(_Ctx())(s, 0)
+    if end != len(s):
+        raise ValueError("extra data")
+    return obj
 
 
 # ---- shared helpers (re-exported by models/hostinfo.py, provider/hostreg.py, orchestrator.py) ----
@@ -140,8 +163,8 @@ def package_gpus(name) -> int | None:
 def _host_claimed_gpus(environ=None) -> set[int]:
     try:
         with open(os.path.join(registry_dir(environ), "claims.json")) as f:
-            return {int(k) for k in (json.load(f) or {}).get("gpus", {})}
-    except (OSError, ValueError, AttributeError):
+            return {int(k) for k in (_loads(f.read()) or {}).get("gpus", {})}
+    except (OSError, ValueError, AttributeError, StopIteration):
         return set()
 
 
@@ -175,8 +198,8 @@ def plan(argv: list[str], environ=None, cwd: str | None = None, kfd_root: str = 
         return None
     try:
         with open(answers_path) as f:
-            answers = {str(k).lower(): v for k, v in json.load(f).items()}
-    except (OSError, ValueError, AttributeError):
+            answers = {str(k).lower(): v for k, v in _loads(f.read()).items()}
+    except (OSError, ValueError, AttributeError, StopIteration):
         return None
     nodes = str(opts.get("--nodes", answers.get("nodes", 1)) or 1)
     per = package_gpus(opts.get("--package", answers.get("package") or "mi355x-1gpu"))

@@ -232,6 +232,7 @@ def precompile_python() -> None:
             "tritonk8ssupervisor_amd.agent.agent", "tritonk8ssupervisor_amd.ops.fakeprobe", "yaml", "argparse", "asyncio",
             "tritonk8ssupervisor_amd.controlplane.client", "tritonk8ssupervisor_amd.controlplane.ingress",
             "tritonk8ssupervisor_amd.controlplane.dns", "tritonk8ssupervisor_amd.utils.k8senv",
+            "tritonk8ssupervisor_amd.earlyburn", "tritonk8ssupervisor_amd.provider.hostreg",
             "tritonk8ssupervisor_amd.parallel.dist_allreduce"]
     code = "import importlib\nfor m in %r:\n    importlib.import_module(m)\n" % (mods[:-1] + ["tritonk8ssupervisor_amd.provision"],)
     for flag in (["-S"], []):
