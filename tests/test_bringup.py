@@ -469,6 +469,16 @@ def test_answers_file_bring_up_starts_the_burnin_before_the_cli_imports(ws):
     for i in (1, 2):
         burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
         assert burn["host_burnin"] and burn["ok"]
+    # teardown stops the adopted processes too (the zygote's supervisor holds the master's pidfile)
+    sup = json.loads((ws / ".tk8s" / "machines" / "kubemaster" / "run" / "controlplane.pid").read_text())["pid"]
+    pids = _pids(ws) + [sup]
+    assert all(_alive(p) for p in pids)
+    r = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=_env(), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0
+    deadline = time.monotonic() + 10
+    while any(_alive(p) for p in pids) and time.monotonic() < deadline:
+        time.sleep(0.05)
+    assert not any(_alive(p) for p in pids)
 
 
 def test_agent_boot_hook_uses_the_roles_standby_argv():
