@@ -305,3 +305,18 @@ def test_kubectl_exec_and_logs_follow(cluster, tmp_path_factory):
     _until(lambda: json.loads(kc("get", "pod", "talker", "-o", "json").stdout)["status"].get("phase") in ("Running", "Succeeded"))
     out = kc("logs", "talker", "-f").stdout
     assert out.split() == ["line1", "line2", "line3"]
+
+
+@pytest.mark.slow
+def test_imperative_create_deployment_and_expose(cluster):
+    """kubectl create deployment / expose: nginx behind a LoadBalancer Service, no manifest."""
+    ws, env, kc, _ = cluster
+    assert "deployment.apps/hello created" in kc("create", "deployment", "hello", "--image", "nginx:1.25",
+                                                 "--replicas", "2", "--port", "80").stdout
+    kc("rollout", "status", "deploy/hello", "--timeout", "60s")
+    assert "service/hello exposed" in kc("expose", "deployment", "hello", "--port", "80", "--type", "LoadBalancer").stdout
+    svc = json.loads(kc("get", "svc", "hello", "-o", "json").stdout)
+    assert svc["spec"]["selector"] == {"app": "hello"} and svc["spec"]["type"] == "LoadBalancer"
+    url = f"http://{_until(lambda: json.loads(kc('get', 'svc', 'hello', '-o', 'json').stdout)['status']['loadBalancer']['ingress'])[0]['ip']}:{host_port(80)}/"
+    assert "Welcome to nginx!" in _until(lambda: _get(url))
+    assert kc("create", "deployment", "broken", check=False).returncode != 0  # --image is required

@@ -492,3 +492,38 @@ def test_agent_boot_hook_uses_the_roles_standby_argv():
     t = next(t for t in tasks if t.get("name") == "Start the node agent in standby on every host")
     subst = {"{{ tk8s_python }}": sys.executable, "{{ inventory_hostname }}": "kubenode1", "{{ ansible_host }}": "127.0.1.2"}
     assert [subst.get(a, a) for a in t["tk8s_daemon"]["argv"]] == agent_standby_argv("kubenode1", "127.0.1.2")
+
+
+def test_scale_workers_up_and_down(ws):
+    """Elastic node count: 2 -> 3 joins a new validated worker; 3 -> 1 drains (the Deployment's
+    pods move), deletes the removed nodes and destroys their machines."""
+    _summary(_setup(ws, "--nodes", "2", "--rccl", "off"))
+    tk = lambda *a: subprocess.run(["./tk8s", *a], cwd=ws, env=_env(), capture_output=True, text=True, timeout=180)
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=_env(), capture_output=True, text=True, timeout=60)
+    r = tk("scale", "3", "--json")
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and out["nodes"] == 3 and out["nodes_validated"] == 3 and out["gpus_allocatable"] == 3
+    nodes = json.loads(kc("get", "nodes", "-o", "json").stdout)["items"]
+    assert sorted(n["metadata"]["name"] for n in nodes) == ["kubenode1", "kubenode2", "kubenode3"]
+    assert len((ws / "terraform" / "hosts.ip").read_text().split()) == 3
+    assert "KUBERNETES_NUMBER_OF_NODES=3" in (ws / "config").read_text()
+    # a workload on the node that goes away moves
+    kc("create", "deployment", "web", "--image", "nginx", "--replicas", "2")
+    kc("rollout", "status", "deploy/web", "--timeout", "60s")
+    gone = [ws / ".tk8s" / "machines" / f"kubenode{i}" for i in (2, 3)]
+    agent_pids = [json.loads((d / "run" / "agent.pid").read_text())["pid"] for d in gone]
+    r = tk("scale", "1", "--json")
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0 and out["removed"] == ["kubenode2", "kubenode3"] and out["nodes_validated"] == 1, r.stdout[-2000:]
+    nodes = json.loads(kc("get", "nodes", "-o", "json").stdout)["items"]
+    assert [n["metadata"]["name"] for n in nodes] == ["kubenode1"]
+    kc("rollout", "status", "deploy/web", "--timeout", "60s")
+    pods = json.loads(kc("get", "pods", "-l", "app=web", "-o", "json").stdout)["items"]
+    assert pods and all(p["spec"]["nodeName"] == "kubenode1" for p in pods if p["status"].get("phase") == "Running")
+    assert not any(d.exists() for d in gone)
+    deadline = time.monotonic() + 10
+    while any(_alive(p) for p in agent_pids) and time.monotonic() < deadline:
+        time.sleep(0.05)
+    assert not any(_alive(p) for p in agent_pids)
+    assert len((ws / "terraform" / "hosts.ip").read_text().split()) == 1
+    assert tk("scale", "0").returncode != 0

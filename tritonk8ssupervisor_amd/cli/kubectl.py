@@ -158,6 +158,38 @@ def _target(args: list[str]) -> tuple[str, str]:
     return args[0], args[1]
 
 
+def _create_deployment(k, a, ns: str) -> int:
+    """kubectl create deployment NAME --image IMAGE [--replicas N] [--port P]: labels app=NAME."""
+    if len(a.args) < 2 or not a.image:
+        raise SystemExit("usage: kubectl create deployment NAME --image IMAGE [--replicas N] [--port P]")
+    name = a.args[1]
+    container = {"name": a.image.rsplit("/", 1)[-1].split(":", 1)[0].split("@", 1)[0] or name, "image": a.image}
+    if a.port:
+        container["ports"] = [{"containerPort": a.port}]
+    body = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": name, "labels": {"app": name}},
+            "spec": {"replicas": 1 if a.replicas is None else a.replicas, "selector": {"matchLabels": {"app": name}},
+                     "template": {"metadata": {"labels": {"app": name}}, "spec": {"containers": [container]}}}}
+    k.post(k.k8s(collection_path("deployment", ns)), body)
+    print(f"deployment.apps/{name} created")
+    return 0
+
+
+def _expose(k, a, ns: str) -> int:
+    """kubectl expose deployment NAME --port P [--target-port T] [--type T] [--name SVC]: a Service
+    selecting the Deployment's pods."""
+    if len(a.args) < 2 or kind_key(a.args[0]) != "deployment" or not a.port:
+        raise SystemExit("usage: kubectl expose deployment NAME --port P [--target-port T] [--type TYPE] [--name SVC]")
+    d = k.get(k.k8s(object_path("deployment", a.args[1], ns)))
+    sel = d["spec"].get("selector", {}).get("matchLabels") or d["spec"]["template"]["metadata"].get("labels", {})
+    name = a.name or a.args[1]
+    body = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": dict(sel)},
+            "spec": {"type": a.type, "selector": sel,
+                     "ports": [{"port": a.port, "targetPort": a.target_port or a.port, "protocol": "TCP"}]}}
+    k.post(k.k8s(collection_path("service", ns)), body)
+    print(f"service/{name} exposed")
+    return 0
+
+
 def _create_data(k, a, ns: str) -> int:
     """kubectl create configmap NAME / create secret generic NAME (--from-literal, --from-file)."""
     secret = a.args[0] == "secret"
@@ -241,6 +273,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--from-file", action="append", default=[])
     ap.add_argument("--ignore-daemonsets", action="store_true")
     ap.add_argument("--follow", dest="follow", action="store_true")
+    ap.add_argument("--image")
+    ap.add_argument("--port", type=int)
+    ap.add_argument("--target-port", type=int)
+    ap.add_argument("--type", default="ClusterIP", choices=["ClusterIP", "NodePort", "LoadBalancer"])
+    ap.add_argument("--name")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -305,6 +342,10 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 print(f"Node:         {o['spec'].get('nodeName')}\nStatus:       {st.get('phase')}")
         elif a.verb == "create" and a.args and a.args[0] in ("configmap", "cm", "secret"):
             return _create_data(k, a, ns)
+        elif a.verb == "create" and a.args and kind_key(a.args[0]) == "deployment":
+            return _create_deployment(k, a, ns)
+        elif a.verb == "expose":
+            return _expose(k, a, ns)
         elif a.verb in ("create", "apply"):
             if not a.filename:
                 raise SystemExit("error: must specify -f FILE")

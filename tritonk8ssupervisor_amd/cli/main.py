@@ -8,6 +8,7 @@
   ./tk8s terraform get|plan|apply|destroy     (provisioning engine, in terraform/)
   ./tk8s ansible-playbook [--check] [-i hosts] clusterUp.yml           (playbook engine)
   ./tk8s status [--json]            (phases, nodes, GPUs, last RCCL busbw)
+  ./tk8s scale N [--json]           (add / drain and remove workers of the running cluster)
   ./kubectl ...                     (see cli/kubectl.py)
 """
 from __future__ import annotations
@@ -53,6 +54,21 @@ def cmd_setup(args) -> int:
         return e.code
     if args.json:
         print(json.dumps(summary))
+    return 0
+
+
+def cmd_scale(args) -> int:
+    from ..orchestrator import Setup, SetupError
+
+    s = Setup(_ws(args), resume=False, timeout=args.timeout, rccl=(None if args.rccl is None else args.rccl == "on"),
+              quiet_ansible=not args.verbose, backend=args.backend)
+    try:
+        out = s.scale(args.nodes)
+    except SetupError as e:
+        print(str(e), file=sys.stderr)
+        return e.code
+    if args.json:
+        print(json.dumps(out))
     return 0
 
 
@@ -241,6 +257,14 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--json", action="store_true")
     s.add_argument("-v", "--verbose", action="store_true")
     s.set_defaults(fn=cmd_setup)
+
+    sc = sub.add_parser("scale", help="change the number of workers of the running cluster (1-9)")
+    sc.add_argument("nodes", type=int)
+    sc.add_argument("--timeout", type=float, default=600.0, help="bound on the readiness wait (s)")
+    sc.add_argument("--rccl", choices=["on", "off"], default=None, help="re-run the RCCL all-reduce Job afterwards")
+    sc.add_argument("--json", action="store_true")
+    sc.add_argument("-v", "--verbose", action="store_true")
+    sc.set_defaults(fn=cmd_scale)
 
     c = sub.add_parser("clean", help="destroy machines and reset configuration (./setup.sh -c)")
     c.add_argument("--yes", action="store_true")

@@ -656,6 +656,83 @@ class Setup:
         self.out("    CONGRATULATIONS, YOU HAVE CONFIGURED YOUR KUBERNETES ENVIRONMENT!")
         return self.summary
 
+    def scale(self, n: int) -> dict:
+        """Change the number of workers of a running cluster (the reference fixes it at creation,
+        setup.sh:297-307, and could only be torn down and rebuilt). Shrinking drains the removed
+        workers (cordon, evict every non-DaemonSet pod so its controller re-creates it elsewhere)
+        and deletes their nodes before their machines go; then the same phases as a bring-up run
+        against the new configuration: Terraform apply (creates the new machines / destroys the
+        removed ones; new machines boot their agent and GPU burn-in), the playbook (idempotent on
+        the existing hosts, joins the new ones), and the bounded readiness wait for exactly n
+        validated workers."""
+        ws = self.ws
+        if not ws.config.exists() or "ready" not in ws.state().get("completed", []):
+            raise SetupError("error: no running cluster in this directory (./setup.sh first)")
+        if not 1 <= int(n) <= 9:
+            raise SetupError("error: the number of nodes must be 1-9 (the wizard's limit)")
+        cfg = read_config(ws.config)
+        export_vars(cfg)
+        self.cfg = cfg
+        old = int(cfg.KUBERNETES_NUMBER_OF_NODES)
+        if int(n) == old:
+            self.out(f"{old} node(s) already; nothing to do")
+            return {"nodes": old, "changed": False}
+        t0 = time.monotonic()
+        self.events.emit("scale_start", nodes=int(n), previous=old)
+        removed = cfg.node_names()[int(n):]
+        if removed:
+            self.banner(f"Draining {', '.join(removed)}...")
+            with self.events.phase("drain"):
+                self._drain_and_delete(removed)
+        cfg.KUBERNETES_NUMBER_OF_NODES = int(n)
+        write_config(ws.config, cfg)
+        export_vars(cfg)
+        for name, fn, title in (("provision", self.provision, "Starting terraform tasks..."),
+                                ("ansible-config", self.ansible_config, "Creating ansible configs..."),
+                                ("ansible", self.ansible, "Running ansible tasks...")):
+            self.banner(title)
+            with self.events.phase(name):
+                fn()
+        with self.events.phase("ready"):
+            ready = self.wait_ready()
+        self.out(f"ALL NODES READY: {ready.get('nodes_ready', 0)} node(s), "
+                 f"{ready.get('gpus_allocatable', 0)} x amd.com/gpu allocatable after {time.monotonic() - t0:.3f}s")
+        rccl = None
+        if self.rccl:
+            with self.events.phase("rccl"):
+                rccl = self.run_rccl()
+        summary = dict(ws.state().get("summary") or {})
+        summary.update(nodes=int(n), gpus_allocatable=ready.get("gpus_allocatable", 0),
+                       nodes_validated=ready.get("nodes_validated", 0))
+        if rccl is not None:
+            summary["rccl"] = rccl
+        ws.save_state(summary=summary)
+        out = {"nodes": int(n), "previous": old, "changed": True, "removed": removed,
+               "seconds": round(time.monotonic() - t0, 4), "gpus_allocatable": ready.get("gpus_allocatable", 0),
+               "nodes_validated": ready.get("nodes_validated", 0), "rccl": rccl}
+        self.events.emit("scale_done", **out)
+        return out
+
+    def _drain_and_delete(self, names: list[str]) -> None:
+        from .controlplane.client import ApiError, client_from_kubeconfig
+
+        c = self._client()
+        pid = self.project_id()
+        k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
+        for node in names:
+            try:
+                k.request("PATCH", k.k8s(f"/api/v1/nodes/{node}"), body={"spec": {"unschedulable": True}})
+            except ApiError as e:
+                if e.status != 404:
+                    raise
+                continue
+            for p in k.get(k.k8s("/api/v1/pods"), query={"fieldSelector": f"spec.nodeName={node}"})["items"]:
+                md = p["metadata"]
+                k.delete(k.k8s(f"/api/v1/namespaces/{md['namespace']}/pods/{md['name']}"))
+                self.out(f"    evicted pod {md['namespace']}/{md['name']}")
+            k.delete(k.k8s(f"/api/v1/nodes/{node}"))
+            self.out(f"    node/{node} drained and deleted")
+
     def _write_kubeconfig(self, base: str, pid: str) -> None:
         from .controlplane.client import Client
 

@@ -57,6 +57,7 @@ class PlanAction:
 class ApplyResult:
     created: list[str] = field(default_factory=list)
     unchanged: list[str] = field(default_factory=list)
+    destroyed: list[str] = field(default_factory=list)
     failed: dict[str, str] = field(default_factory=dict)
     seconds: float = 0.0
 
@@ -233,6 +234,15 @@ class Engine:
         res = ApplyResult()
         specs = self.specs()
         st = self.state()["resources"]
+        # Terraform semantics: a resource in the state whose module left the configuration (the
+        # node count went down) is destroyed by apply, as `plan` announced.
+        wanted = {s.address for s in specs}
+        for addr, rec in list(st.items()):
+            if addr not in wanted:
+                self.provider.delete_machine(Machine.from_dict(rec["machine"]))
+                self._save_resource(addr, None)
+                res.destroyed.append(addr)
+                self.events.emit("machine_destroyed", address=addr, name=rec["machine"].get("name"))
         todo = []
         for s in specs:
             cur = st.get(s.address)
