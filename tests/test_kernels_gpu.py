@@ -416,3 +416,40 @@ def test_multi_gpu_setup_with_rccl_job(tmp_path):
         assert s["gpus_allocatable"] == 2 and s["rccl"]["ok"] and s["rccl"]["nranks"] == 2
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+@pytest.mark.gpu
+def test_setup_from_an_answers_file_adopts_the_early_burnin_on_a_real_gpu(tmp_path):
+    """``./setup.sh --answers FILE`` (the bench's path): the real tk8s-probe is spawned before the
+    CLI imports anything, the orchestrator adopts it, and the control plane zygote serves."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    (tmp_path / "answers.json").write_text(json.dumps({"nodes": 1, "package": "mi355x-1gpu", "confirm": "yes"}))
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, TK8S_HOST_REGISTRY=str(tmp_path / "hostreg"))
+    try:
+        r = subprocess.run(["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", "0", "--timeout", "120"],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1
+        events = [json.loads(x) for x in (tmp_path / ".tk8s" / "events.jsonl").read_text().splitlines()]
+        started = [e for e in events if e["event"] == "gpu_burnin_host_started"]
+        assert len(started) == 1 and started[0].get("early"), started
+        assert any(e["event"] == "controlplane_boot_started" and e.get("zygote") for e in events)
+        burn = json.loads((tmp_path / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json").read_text())
+        assert burn["ok"] and burn["host_burnin"] and burn["gpuinfo"]["devices"][0]["gfx"] == "gfx950"
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
