@@ -370,6 +370,11 @@ class Setup:
                 os.killpg(z["pid"], 15)
             except OSError:
                 pass
+        # The machine was just created: whatever still runs under its pidfile is a zygote an earlier,
+        # failed start left waiting; stop it, or its exit would later remove this start's pidfile.
+        stale = Path(m.sandbox) / "run" / "controlplane.pid"
+        if stale.exists():
+            kill_pidfile(stale, grace=1.0)
         pythonpath = os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
         ex = MachineExecutor(self.provider, {m.name: m})
         info = ex.start_daemon(m.name, "controlplane", argv, env={"PYTHONPATH": pythonpath}, restart="unless-stopped",
