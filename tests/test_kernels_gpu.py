@@ -453,3 +453,44 @@ def test_setup_from_an_answers_file_adopts_the_early_burnin_on_a_real_gpu(tmp_pa
         assert burn["ok"] and burn["host_burnin"] and burn["gpuinfo"]["devices"][0]["gfx"] == "gfx950"
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+def _hsaprobe(*args, timeout=120):
+    import subprocess
+
+    from tritonk8ssupervisor_amd.ops import BIN
+
+    r = subprocess.run([str(BIN / "tk8s-hsaprobe"), *args], capture_output=True, text=True, timeout=timeout)
+    return r.returncode, json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_hsaprobe_digests_match_the_host_oracle(nat):
+    """tk8s-hsaprobe dispatches the same kernels on ROCr with hand-built AQL packets: the MD5 tree
+    of the Philox stream must match the host oracle, bit for bit, at a ragged and a full size."""
+    from tritonk8ssupervisor_amd.ops import reference as ref
+
+    for nbytes in (1 << 20, 3 * (1 << 20) + 4096):
+        rc, out = _hsaprobe("--hbm-bytes", str(16 << 20), "--md5-bytes", str(nbytes), "--copy-bytes", str(1 << 20),
+                            "--iters", "1")
+        assert rc == 0 and out["ok"] and out["runtime"] == "hsa", out
+        assert out["md5"]["digest"] == ref.md5_tree(ref.philox_bytes(nbytes, 0), 1024).hex()
+        assert out["hbm"]["bad_words"] == 0 and out["copy"]["bad_words"] == 0
+
+
+def test_hsaprobe_known_answer_and_gpuinfo_agree_with_the_hip_probe(nat):
+    rc, hsa = _hsaprobe("--all-devices", "--gpuinfo", "--iters", "2")
+    assert rc == 0 and hsa["ok"], hsa
+    assert hsa["md5_expected"] == "55af80380d572d36cc8cc7d50edd90ab" and hsa["md5"]["digest"] == hsa["md5_expected"]
+    for d in hsa["devices"]:
+        assert d["ok"] and d["digest_ok"] and d["hbm"]["gbps"] > 3000 and d["copy"]["kernel_gbps"] > 1500
+    rc, hip = _probe("--all-devices", "--gpuinfo", "--iters", "1", "--hbm-bytes", str(64 << 20))
+    assert rc == 0
+    for a, b in zip(hsa["gpuinfo"]["devices"], hip["gpuinfo"]["devices"]):
+        assert a["gfx"] == b["gfx"] == "gfx950"
+        assert a["pci_bus_id"] == b["pci_bus_id"] and a["cu_count"] == b["cu_count"]
+    # peer pulls stay with tk8s-probe: asked for them, the HSA tool refuses before touching the GPU
+    import subprocess
+
+    from tritonk8ssupervisor_amd.ops import BIN
+
+    assert subprocess.run([str(BIN / "tk8s-hsaprobe"), "--peers"], capture_output=True, timeout=30).returncode == 4

@@ -51,12 +51,27 @@ def _loads(text: str):
 
 
 # ---- shared helpers (re-exported by models/hostinfo.py, provider/hostreg.py, orchestrator.py) ----
-def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 << 20, iters: int = 3) -> list[str]:
-    """The validation DaemonSet payload (and the burn-in): every GPU of a worker."""
+def probe_tool(peers: bool) -> str:
+    """The validation payload binary: ``tk8s-hsaprobe`` (the same kernels and checks dispatched on
+    ROCr directly, ~20 ms less start-up than HIP, native/tools/tk8s_hsaprobe.cpp) unless xGMI
+    peer pulls are wanted (HIP peer access: ``tk8s-probe``), ``TK8S_PROBE_RUNTIME=hip`` says so,
+    or its code objects are missing."""
+    hsa = os.path.join(BIN, "tk8s-hsaprobe")
+    lib = os.path.join(PKG, "lib")
+    if (not peers and os.environ.get("TK8S_PROBE_RUNTIME", "hsa") != "hip" and os.access(hsa, os.X_OK)
+            and os.path.exists(os.path.join(lib, "tk8s_stream.co")) and os.path.exists(os.path.join(lib, "tk8s_md5.co"))):
+        return hsa
+    return os.path.join(BIN, "tk8s-probe")
+
+
+def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 << 20, iters: int = 3,
+                               peers: bool = True) -> list[str]:
+    """The validation DaemonSet payload (and the burn-in): every GPU of a worker; ``peers``: also
+    the xGMI pulls between them (workers of more than one GPU)."""
     if os.environ.get("TK8S_FAKE_GPUS"):
         return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
-    return [os.path.join(BIN, "tk8s-probe"), "--all-devices", "--gpuinfo", "--peers", "--hbm-bytes", str(hbm_bytes),
-            "--md5-bytes", str(md5_bytes), "--iters", str(iters)]
+    return [probe_tool(peers), "--all-devices", "--gpuinfo", *(["--peers"] if peers else []), "--hbm-bytes",
+            str(hbm_bytes), "--md5-bytes", str(md5_bytes), "--iters", str(iters)]
 
 
 def registry_dir(environ=None) -> str:
@@ -216,9 +231,8 @@ def plan(argv: list[str], environ=None, cwd: str | None = None, kfd_root: str = 
         free = [i for i in range(len(vis) if vis is not None else n) if i not in claimed]
     if len(free) < count:
         return None
-    cmd = default_validation_command()
-    if per <= 1:  # no xGMI link inside any machine: the RCCL Job checks the fabric
-        cmd = [a for a in cmd if a != "--peers"]
+    # no xGMI link inside a 1-GPU machine: the RCCL Job checks the fabric
+    cmd = default_validation_command(peers=per > 1)
     state = os.path.join(ws, ".tk8s")
     master = str(opts.get("--master-hostname", answers.get("master_hostname") or "kubemaster"))
     return {"gpus": free[:count], "command": cmd, "state_dir": state,

@@ -419,8 +419,6 @@ class Setup:
         try:
             pkg = self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE)
             cmd = self._validation_command()
-            if int(pkg.gpus or 0) <= 1:  # no xGMI link inside any machine: the RCCL Job checks the fabric
-                cmd = [a for a in cmd if a != "--peers"]
             if early is not None and early.command == cmd and hasattr(self.provider, "prefer_gpus"):
                 self.provider.prefer_gpus(early.gpus)
             gpus = self.provider.predict_gpus(int(pkg.gpus or 0), int(self.cfg.KUBERNETES_NUMBER_OF_NODES))
@@ -474,7 +472,14 @@ class Setup:
         self.out("    created: ansible/roles/ranchermaster/vars/vars.yml")
 
     def _validation_command(self) -> list[str]:
-        return default_validation_command(self.hbm_bytes, self.md5_bytes, self.probe_iters)
+        # xGMI pulls only inside multi-GPU machines (a 1-GPU machine has none; the RCCL Job checks
+        # the fabric between machines)
+        peers = True
+        try:
+            peers = int(self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE).gpus or 0) > 1
+        except Exception:  # noqa: BLE001 - no configuration yet: the full check
+            pass
+        return default_validation_command(self.hbm_bytes, self.md5_bytes, self.probe_iters, peers=peers)
 
     def ansible(self) -> None:
         from .playbook import Playbook

@@ -195,9 +195,25 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if force or _stale(sup, [sup_src]):
         _run([CXX, "-O2", "-std=c++17", "-Wall", str(sup_src), "-o", str(sup)], verbose)
 
+    # Device-only code objects of the validation kernels (the same sources as libtk8s.so) for
+    # tk8s-hsaprobe, which dispatches them on ROCr directly, and that tool itself (no HIP).
+    cos = {}
+    for rel, name in (("src/stream_kernels.hip", "tk8s_stream.co"), ("src/md5_kernels.hip", "tk8s_md5.co")):
+        co = LIBDIR / name
+        cos[name] = co
+        if force or _stale(co, [NATIVE / rel]):
+            _run([HIPCC, *HIP_FLAGS, "--cuda-device-only", "--no-gpu-bundle-output", "-c", str(NATIVE / rel),
+                  "-o", str(co)], verbose)
+    hsa_src = NATIVE / "tools" / "tk8s_hsaprobe.cpp"
+    hsa_bin = tool_path("tk8s-hsaprobe")
+    if force or _stale(hsa_bin, [hsa_src]):
+        _run([CXX, "-O2", "-std=c++17", "-Wall", f"-I{NATIVE / 'include'}", f"-I{NATIVE / 'tools'}",
+              f"-I{ROCM / 'include'}", str(hsa_src), "-o", str(hsa_bin), f"-L{ROCM / 'lib'}", "-lhsa-runtime64",
+              f"-Wl,-rpath,{ROCM / 'lib'}", "-lpthread"], verbose)
+
     precompile_python()
     out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,
-           "tk8s-smi": smi, "tk8s-reuse": reuse_bin}
+           "tk8s-smi": smi, "tk8s-reuse": reuse_bin, "tk8s-hsaprobe": hsa_bin, **cos}
     out.update({n: tool_path(n) for n in TOOLS})
     return out
 
