@@ -1,0 +1,74 @@
+"""bench.py driver contract on the CPU (fake gfx950 devices): one JSON line from rank 0 with the
+BASELINE.json metric, the K timed steps, and MAX-over-ranks timing under torch.distributed.run
+(gloo, world_size 2), the way the driver launches the N-GPU scaling runs."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config")
+
+
+def _env(tmp_path: Path) -> dict:
+    env = dict(os.environ)
+    env["TMPDIR"] = str(tmp_path)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_line(stdout: str) -> dict:
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def _check(out: dict, n: int, steps: int, warmup: int) -> None:
+    for k in REQUIRED:
+        assert k in out, k
+    assert out["metric"] == json.loads((REPO / "BASELINE.json").read_text())["metric"]
+    assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
+    assert out["higher_is_better"] is False and out["scaling"] == "weak" and out["unit"] == "s"
+    assert out["value"] > 0 and out["min_s"] <= out["value"] <= out["max_s"]
+    # the step brackets hold the whole ./setup.sh process, which prints Ready before it exits
+    assert out["ms_per_step"] >= out["min_s"] * 1000.0
+    assert "fake GPUs" in out["data"]
+    assert out["gpus_allocatable"] == n and out["nodes_validated"] == n
+    assert out["config"]["parallelism"] == f"workers{n}"
+
+
+@pytest.mark.timeout(300)
+def test_bench_single_process(tmp_path):
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "2", "--warmup", "1",
+                        "--fake-gpus", "2"], cwd=REPO, env=_env(tmp_path), capture_output=True, text=True,
+                       timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
+    _check(_json_line(p.stdout), 1, 2, 1)
+    assert p.stderr.count("(timed)") == 2 and p.stderr.count("(warmup)") == 1
+
+
+@pytest.mark.timeout(400)
+def test_bench_torchrun_two_ranks(tmp_path):
+    """Only rank 0 prints; both ranks take part in the barriers and the MAX reduction."""
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
+                        "--gpus", "2", "--steps", "1", "--warmup", "1", "--fake-gpus", "2", "--rccl", "off"],
+                       cwd=REPO, env=_env(tmp_path), capture_output=True, text=True, timeout=380)
+    assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
+    _check(_json_line(p.stdout), 2, 1, 1)
