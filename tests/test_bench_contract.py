@@ -72,3 +72,20 @@ def test_bench_torchrun_two_ranks(tmp_path):
                        cwd=REPO, env=_env(tmp_path), capture_output=True, text=True, timeout=380)
     assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
     _check(_json_line(p.stdout), 2, 1, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_bench_real_gpu(tmp_path):
+    """On an MI355X: one real bring-up through bench.py, validated by the native probe on the GPU."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "0"], cwd=REPO,
+                       env=_env(tmp_path), capture_output=True, text=True, timeout=220)
+    assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
+    out = _json_line(p.stdout)
+    assert out["n_gpus"] == 1 and out["gpus_allocatable"] == 1 and out["nodes_validated"] == 1
+    assert "fake" not in out["data"] and out["value"] < 5.0
+    v = next(iter(out["validation_last_step"].values()))
+    assert float(v["hbm-write-gbps"]) > 1000.0 and float(v["md5-mbps"]) > 1000.0
