@@ -334,6 +334,8 @@ def main(argv=None) -> int:
                            "barrier + device sync on every rank on both sides, MAX over ranks",
         "min_s": round(min(ready_times), 4),
         "max_s": round(max(ready_times), 4),
+        "median_s": round(sorted(ready_times)[len(ready_times) // 2] if len(ready_times) % 2
+                          else sum(sorted(ready_times)[len(ready_times) // 2 - 1:len(ready_times) // 2 + 1]) / 2, 4),
         "setup_process_s": round(step_mean, 4),
         "rccl_check_s": round(sum(s.get("phases", {}).get("rccl", 0.0) for s in summaries) / len(summaries), 4)
         if summaries else None,

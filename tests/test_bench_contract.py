@@ -46,6 +46,7 @@ def _check(out: dict, n: int, steps: int, warmup: int) -> None:
     assert out["n_gpus"] == n and out["steps"] == steps and out["warmup"] == warmup
     assert out["higher_is_better"] is False and out["scaling"] == "weak" and out["unit"] == "s"
     assert out["value"] > 0 and out["min_s"] <= out["value"] <= out["max_s"]
+    assert out["min_s"] <= out["median_s"] <= out["max_s"]
     # the step brackets hold the whole ./setup.sh process, which prints Ready before it exits
     assert out["ms_per_step"] >= out["min_s"] * 1000.0
     assert "fake GPUs" in out["data"]
