@@ -19,10 +19,19 @@
 //
 //   tk8s-hsaprobe [--all-devices | --device D] [--gpuinfo] [--hbm-bytes B] [--md5-bytes B]
 //                 [--chunk C] [--seed S] [--copy-bytes B] [--iters K] [--mode plain|nontemporal]
+//                 [--peers [--peer-bytes B] [--peer-iters K]] [--peers-host]
 //                 [--out FILE] [--reuse FILE [--reuse-wait S]]
 //
-// xGMI peer pulls (--peers) stay with tk8s-probe (HIP peer access); asked for them, this tool
-// exits 4 without touching the GPU so the caller can fall back.
+// --peers (N7, the xGMI link check before Ready): once every device has passed its own probes,
+// each one fills a source buffer with a pattern naming it, grants every other GPU access to it
+// (hsa_amd_agents_allow_access, after checking the pool is not NEVER_ALLOWED for that agent),
+// and then in round r = 1..n-1 every GPU i pulls from GPU (i + r) mod n with the stream copy
+// kernel and verifies the pattern. A round is a permutation, so each directed link carries one
+// pull at a time and its GB/s is that link's. Each pull lands in the destination device's JSON
+// under "peers" (src_device/dst_device/kernel_gbps/bad_words), the shape tk8s-probe uses; the
+// bring-up judges the link matrix (tritonk8ssupervisor_amd/xgmi.py). With one GPU there is no
+// pair and the phase costs nothing. --peers-host runs the same pull path from a host-memory
+// source (granted the same way): the part of the mechanism a 1-GPU box can exercise.
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <unistd.h>
@@ -376,11 +385,11 @@ class KernArgs {
 
 // ---- one device ---------------------------------------------------------------------------
 struct Config {
-  size_t hbm = 1ull << 30, md5 = 256ull << 20, copy = 256ull << 20;
+  size_t hbm = 1ull << 30, md5 = 256ull << 20, copy = 256ull << 20, peer = 32ull << 20;
   uint32_t chunk = 1024;
   uint64_t seed = 0;
-  int iters = 5;
-  bool nontemporal = false;
+  int iters = 5, peer_iters = 2;
+  bool nontemporal = false, peers = false, peers_host = false;
 };
 
 struct Dispatch {
@@ -388,7 +397,8 @@ struct Dispatch {
   unsigned blocks = 1;
   uint16_t block = 1;
   size_t slot = 0;  // offset of its kernel arguments in the (host staging / VRAM) arena
-  bool system = false;
+  bool system = false;       // release at system scope: the host (or a peer GPU) reads the result
+  bool sys_acquire = false;  // acquire at system scope: it reads memory another agent wrote
   hsa_signal_t sig{};
 };
 
@@ -471,7 +481,8 @@ class Device {
   // Stage one kernel of the current batch; returns its index (for its GPU timestamps).
   // system: the kernel's results are read by the host (system-scope release).
   template <class Fill>
-  size_t launch(const Kernel& k, unsigned blocks, uint16_t block, Fill fill, bool system = false) {
+  size_t launch(const Kernel& k, unsigned blocks, uint16_t block, Fill fill, bool system = false,
+                bool sys_acquire = false) {
     const size_t slot = align_up(std::max<uint32_t>(k.kernarg_size, 64), 64);
     if (stage_off_ + slot > kKernargArena) sync();  // the arenas are reused after a sync
     KernArgs args(stage_ + stage_off_, static_cast<uint32_t>(slot));
@@ -483,6 +494,7 @@ class Device {
     d.block = block;
     d.slot = stage_off_;
     d.system = system;
+    d.sys_acquire = sys_acquire;
     stage_off_ += slot;
     batch_.push_back(d);
     return count_++;
@@ -512,7 +524,7 @@ class Device {
       // Agent scope between kernels, as HIP does on one stream (L2s of the XCDs written back
       // and invalidated; with no fence the next kernel read stale lines and the MD5 tree came
       // out wrong); system-scope release for results the host reads.
-      enqueue(*d.k, d.blocks, d.block, dev_args_ + d.slot, HSA_FENCE_SCOPE_AGENT,
+      enqueue(*d.k, d.blocks, d.block, dev_args_ + d.slot, d.sys_acquire ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT,
               d.system ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT, d.sig);
     }
     const hsa_signal_t last = batch_.back().sig;
@@ -538,11 +550,11 @@ class Device {
   double span_ms(size_t a, size_t b) const { return (times_[b].second - times_[a].first) * 1e-6; }
 
   // ---- the kernels, with the same launch shapes as the HIP wrappers ----
-  size_t fill(void* dst, size_t bytes, uint32_t value, bool nt) {
+  size_t fill(void* dst, size_t bytes, uint32_t value, bool nt, bool system = false) {
     const size_t n16 = bytes / 16;
     const unsigned grid = grid_for(n16 / 4, 16);
     return launch(nt ? ks_.fill_nt : ks_.fill_plain, grid, kBlock,
-                           [&](KernArgs& a) { a.ptr(dst).u64(n16).u32(value); });
+                  [&](KernArgs& a) { a.ptr(dst).u64(n16).u32(value); }, system);
   }
   size_t verify(const void* src, size_t bytes, uint32_t value, void* bad) {
     const size_t n16 = bytes / 16;
@@ -555,10 +567,10 @@ class Device {
              a.ptr(dst).u64(n16).u32(static_cast<uint32_t>(seed)).u32(static_cast<uint32_t>(seed >> 32));
            });
   }
-  size_t copy(void* dst, const void* src, size_t bytes, bool to_host = false) {
+  size_t copy(void* dst, const void* src, size_t bytes, bool to_host = false, bool from_remote = false) {
     const size_t n16 = bytes / 16;
     return launch(ks_.copy, grid_for(n16 / 4, 32), kBlock,
-                  [&](KernArgs& a) { a.ptr(dst).ptr(src).u64(n16); }, to_host);
+                  [&](KernArgs& a) { a.ptr(dst).ptr(src).u64(n16); }, to_host, from_remote);
   }
   // md5_kernels.hip md5_tree: level by level until one digest; returns (first, last) dispatch.
   std::pair<size_t, size_t> md5_tree(const void* src, size_t nbytes, uint32_t chunk, void* wa, void* wb, void* out) {
@@ -597,6 +609,7 @@ class Device {
     }
   }
   uint8_t* host() { return host_; }
+  const Gpu& gpu() const { return g_; }
 
   double code_ms = 0, queue_ms = 0, host_alloc_ms = 0;
 
@@ -651,9 +664,13 @@ class Device {
 
 // ---- the probes (same semantics and JSON as native/src/probes.cpp) --------------------------
 struct DeviceResult {
-  std::string hbm, md5, copy, digest, error;
+  std::string hbm, md5, copy, digest, error, host_pull;
+  std::vector<std::string> peers;  // pulls INTO this device, one per source GPU
+  bool peers_ok = true;
   double wall_ms = 0, hbm_ms = 0, md5_ms = 0, copy_ms = 0, setup_ms = 0;
   bool ok = true;
+  Device* dev = nullptr;  // kept for the peer phase (never freed, see run_device)
+  char* base = nullptr;   // start of its VRAM allocation (what peers are granted access to)
 };
 
 void run_device(const Gpu& g, const Host& h, const std::vector<std::string>& cos, double freq, const Config& c,
@@ -665,8 +682,10 @@ void run_device(const Gpu& g, const Host& h, const std::vector<std::string>& cos
   const size_t ws = c.md5 ? (c.md5 + c.chunk - 1) / c.chunk * 16 : 0;
   const size_t md5_need = c.md5 ? align_up(std::max<size_t>(c.md5, 16)) + 2 * align_up(ws) + kAlign : 0;
   const size_t need = std::max({c.hbm ? align_up(c.hbm) + kAlign : 0, md5_need, c.copy ? 2 * align_up(c.copy) + kAlign : 0,
-                                kAlign});
+                                (c.peers || c.peers_host) ? 2 * align_up(c.peer) + kAlign : 0, kAlign});
   char* base = dev->vram(need);
+  r.dev = dev;
+  r.base = base;
   r.setup_ms = ms_since(td);
   uint8_t* host = dev->host();
   const int it = std::max(c.iters, 1);
@@ -792,6 +811,141 @@ void run_device(const Gpu& g, const Host& h, const std::vector<std::string>& cos
   r.wall_ms = ms_since(td);
 }
 
+// ---- N7: xGMI peer pulls --------------------------------------------------------------------
+// The source pattern names the GPU it came from, so a pull that read the wrong device (or a
+// stale line) fails verification, not just one that read garbage.
+uint32_t peer_pattern(int src) { return 0x5EE00000u | static_cast<uint32_t>(src & 0xFFFF); }
+
+std::string pull_json(const char* probe, int src, int dst, const Config& c, const std::string& access, double ms,
+                      uint64_t nbad, const std::string& error) {
+  Json j;
+  j.kv("ok", error.empty() && nbad == 0).kv("probe", probe).kv("src_device", src).kv("dst_device", dst)
+      .kv("bytes", static_cast<uint64_t>(c.peer)).kv("iters", std::max(c.peer_iters, 1)).kv("access", access);
+  if (error.empty()) j.kv("kernel_ms", ms).kv("kernel_gbps", ms > 0 ? c.peer / (ms * 1e-3) / 1e9 : 0.0).kv("bad_words", nbad);
+  else j.kv("error", error);
+  return j.str();
+}
+
+// One pull of c.peer bytes from `src` (memory of another agent, already granted to this device)
+// into this device's scratch: a warm-up, peer_iters timed copies, then a pattern check.
+// Returns (GPU ms per copy, bad words).
+std::pair<double, uint64_t> pull(DeviceResult& r, const void* src, uint32_t pattern, const Config& c) {
+  Device* d = r.dev;
+  char* dst = r.base + align_up(c.peer);
+  char* bad = dst + align_up(c.peer);
+  const int it = std::max(c.peer_iters, 1);
+  d->copy(dst, src, c.peer, false, /*from_remote=*/true);  // warm-up (and the system-scope acquire)
+  size_t first = 0, last = 0;
+  for (int i = 0; i < it; ++i) {
+    const size_t k = d->copy(dst, src, c.peer);
+    if (i == 0) first = k;
+    last = k;
+  }
+  d->fill(bad, 16, 0, false);
+  d->verify(dst, c.peer, pattern, bad);
+  d->copy(d->host() + 192, bad, 16, true);
+  d->sync();
+  uint64_t nbad = 0;
+  std::memcpy(&nbad, d->host() + 192, 8);
+  return {d->span_ms(first, last) / it, nbad};
+}
+
+void run_peers(const std::vector<int>& devices, const Config& c, std::vector<DeviceResult>& res) {
+  const size_t m = devices.size();
+  // 1. every source buffer gets its pattern, released at system scope (peers read it next).
+  for (size_t k = 0; k < m; ++k) {
+    if (!res[k].dev) continue;
+    try {
+      res[k].dev->fill(res[k].base, c.peer, peer_pattern(devices[k]), false, /*system=*/true);
+      res[k].dev->sync();
+    } catch (const std::exception& e) {
+      res[k].error = std::string("peer source fill: ") + e.what();
+      res[k].ok = false;
+    }
+  }
+  // 2. grants: who may read whose VRAM. A pool the runtime reports NEVER_ALLOWED for an agent is
+  // not granted and not touched (a kernel reading memory it has no mapping for faults the GPU).
+  std::vector<std::vector<std::string>> access(m, std::vector<std::string>(m, "self"));
+  for (size_t j = 0; j < m; ++j) {
+    std::vector<hsa_agent_t> readers;
+    std::vector<size_t> idx;
+    for (size_t k = 0; k < m; ++k) {
+      if (k == j) continue;
+      if (!res[j].dev || !res[k].dev || !res[j].error.empty() || !res[k].error.empty()) {
+        access[k][j] = "unavailable";
+        continue;
+      }
+      hsa_amd_memory_pool_access_t a = HSA_AMD_MEMORY_POOL_ACCESS_NEVER_ALLOWED;
+      hsa_amd_agent_memory_pool_get_info(res[k].dev->gpu().agent, res[j].dev->gpu().vram,
+                                         HSA_AMD_AGENT_MEMORY_POOL_INFO_ACCESS, &a);
+      if (a == HSA_AMD_MEMORY_POOL_ACCESS_NEVER_ALLOWED) {
+        access[k][j] = "never_allowed";
+        continue;
+      }
+      readers.push_back(res[k].dev->gpu().agent);
+      idx.push_back(k);
+    }
+    if (readers.empty()) continue;
+    const hsa_status_t st = hsa_amd_agents_allow_access(static_cast<uint32_t>(readers.size()), readers.data(), nullptr,
+                                                        res[j].base);
+    for (size_t k : idx) access[k][j] = st == HSA_STATUS_SUCCESS ? "allowed" : "denied";
+  }
+  // 3. rounds: in round r every GPU i pulls from GPU (i + r) mod m, all at once.
+  for (size_t r = 1; r < m; ++r) {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < m; ++k) {
+      th.emplace_back([&, k, r] {
+        const size_t j = (k + r) % m;
+        const std::string& acc = access[k][j];
+        DeviceResult& rk = res[k];  // only this thread touches it in this round
+        if (acc != "allowed") {
+          rk.peers.push_back(pull_json("xgmi_peer_pull", devices[j], devices[k], c, acc, 0, 0, "no access: " + acc));
+          rk.peers_ok = false;
+          return;
+        }
+        try {
+          const auto p = pull(rk, res[j].base, peer_pattern(devices[j]), c);
+          rk.peers.push_back(pull_json("xgmi_peer_pull", devices[j], devices[k], c, acc, p.first, p.second, ""));
+          rk.peers_ok = rk.peers_ok && p.second == 0;
+        } catch (const std::exception& e) {
+          rk.peers.push_back(pull_json("xgmi_peer_pull", devices[j], devices[k], c, acc, 0, 0, e.what()));
+          rk.peers_ok = false;
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+  }
+}
+
+// --peers-host: the pull path from a host-memory source (the runtime's fine-grained system pool,
+// filled by the CPU, granted to the GPU the way peers are).
+void run_host_pull(const Host& h, int device, const Config& c, DeviceResult& r) {
+  if (!r.dev) return;
+  void* src = nullptr;
+  std::string acc = "allowed", err;
+  double ms = 0;
+  uint64_t nbad = 0;
+  try {
+    HSA_OK(hsa_amd_memory_pool_allocate(h.kernarg, c.peer, 0, &src));
+    const uint32_t pat = peer_pattern(-1);
+    auto* w = static_cast<uint32_t*>(src);
+    for (size_t i = 0; i < c.peer / 4; ++i) w[i] = pat;
+    const hsa_agent_t agent = r.dev->gpu().agent;
+    if (hsa_amd_agents_allow_access(1, &agent, nullptr, src) != HSA_STATUS_SUCCESS) acc = "denied";
+    if (acc == "allowed") {
+      const auto p = pull(r, src, pat, c);
+      ms = p.first;
+      nbad = p.second;
+    } else {
+      err = "no access: denied";
+    }
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  r.host_pull = pull_json("host_pull", -1, device, c, acc, ms, nbad, err);
+  if (src) hsa_amd_memory_pool_free(src);
+}
+
 void emit(const std::string& json, const std::string& out_file) {
   if (!out_file.empty()) {
     const std::string tmp = out_file + ".tmp";
@@ -826,10 +980,6 @@ int main(int argc, char** argv) {
       const int rc = tk8s::reuse(a.str("reuse"), static_cast<double>(a.num("reuse-wait", 120)));
       if (rc >= 0) return rc;
     }
-    if (a.has("peers")) {
-      std::fprintf(stderr, "tk8s-hsaprobe: --peers needs tk8s-probe (HIP peer access)\n");
-      return 4;
-    }
     Config c;
     c.hbm = static_cast<size_t>(a.num("hbm-bytes", 1LL << 30));
     c.md5 = a.has("skip-md5") ? 0 : static_cast<size_t>(a.num("md5-bytes", 256LL << 20));
@@ -838,7 +988,11 @@ int main(int argc, char** argv) {
     c.seed = static_cast<uint64_t>(a.num("seed", 0));
     c.iters = static_cast<int>(a.num("iters", 5));
     c.nontemporal = a.str("mode", "plain") == "nontemporal";
-    if (c.hbm % 16 || c.md5 % 16 || c.copy % 16 || c.chunk == 0 || c.chunk % 64)
+    c.peers = a.has("peers");
+    c.peers_host = a.has("peers-host");
+    c.peer = static_cast<size_t>(a.num("peer-bytes", 32LL << 20));
+    c.peer_iters = static_cast<int>(a.num("peer-iters", std::min<long long>(c.iters, 2)));
+    if (c.hbm % 16 || c.md5 % 16 || c.copy % 16 || c.peer % 16 || c.peer == 0 || c.chunk == 0 || c.chunk % 64)
       throw std::invalid_argument("sizes must be multiples of 16 and --chunk a positive multiple of 64");
     const std::string dir = exe_dir() + "/../lib/";
     const std::vector<std::string> cos = {read_file(dir + "tk8s_stream.co"), read_file(dir + "tk8s_md5.co")};
@@ -885,9 +1039,16 @@ int main(int argc, char** argv) {
     for (size_t k = 1; k < devices.size(); ++k) threads.emplace_back(run_one, k);
     run_one(0);
     for (auto& th : threads) th.join();
+    const auto tp = std::chrono::steady_clock::now();
+    if (c.peers && devices.size() > 1) run_peers(devices, c, res);
+    if (c.peers_host) run_host_pull(t.host, devices[0], c, res[0]);
+    const double peers_ms = ms_since(tp);
 
+    // The known answer is pinned for the default input only; any other configuration can only be
+    // checked for agreement across devices, and says so ("md5_pinned": false).
     std::string want;
-    if (c.md5 == (256u << 20) && c.chunk == 1024 && c.seed == 0) want = kKnownDigest256M;
+    const bool pinned = c.md5 == (256u << 20) && c.chunk == 1024 && c.seed == 0;
+    if (pinned) want = kKnownDigest256M;
     else if (c.md5) want = res[0].digest;
     bool ok = true;
     std::vector<std::string> per_dev;
@@ -903,18 +1064,22 @@ int main(int argc, char** argv) {
       if (!r.hbm.empty()) d.raw("hbm", with_device(r.hbm, devices[k]));
       if (c.md5 && !r.md5.empty()) d.raw("md5", with_device(r.md5, devices[k])).kv("digest_ok", digest_ok);
       if (c.copy && !r.copy.empty()) d.raw("copy", r.copy);
+      // Data integrity of its incoming pulls; their bandwidth is judged host-wide (xgmi.py).
+      if (c.peers) d.raw("peers", Json::array(r.peers)).kv("peers_ok", r.peers_ok);
+      if (!r.host_pull.empty()) d.raw("host_pull", r.host_pull);
       per_dev.push_back(d.str());
     }
     Json out;
     out.kv("ok", ok).kv("runtime", "hsa").kv("device", devices[0]).kv("device_count", n)
         .kv("probed", static_cast<int>(devices.size()));
     if (!res[0].hbm.empty()) out.raw("hbm", res[0].hbm);
-    if (c.md5 && !res[0].md5.empty()) out.raw("md5", res[0].md5).kv("md5_expected", want);
+    if (c.md5 && !res[0].md5.empty()) out.raw("md5", res[0].md5).kv("md5_expected", want).kv("md5_pinned", pinned);
     if (c.copy && !res[0].copy.empty()) out.raw("copy", res[0].copy);
     out.raw("devices", Json::array(per_dev));
     if (!info.empty()) out.raw("gpuinfo", info);
+    if (c.peers) out.kv("peer_bytes", static_cast<uint64_t>(c.peer)).kv("peer_rounds", static_cast<int>(devices.size()) - 1);
     out.raw("timings_ms", Json().kv("hip_init", init_ms).kv("runtime_init", init_ms).kv("gpuinfo", gpuinfo_ms)
-                              .kv("total", ms_since(t0)).str());
+                              .kv("peers", peers_ms).kv("total", ms_since(t0)).str());
     emit(out.str(), out_file);
     std::fflush(stdout);
     // No runtime teardown on the way out (see run_device) -- unless a tool that finalises in

@@ -527,3 +527,65 @@ def test_scale_workers_up_and_down(ws):
     assert not any(_alive(p) for p in agent_pids)
     assert len((ws / "terraform" / "hosts.ip").read_text().split()) == 1
     assert tk("scale", "0").returncode != 0
+
+
+def test_xgmi_link_report_judges_the_pull_matrix(monkeypatch):
+    from tritonk8ssupervisor_amd import xgmi
+    from tritonk8ssupervisor_amd.burnin import split_host_result
+
+    def pull(s, d, g, ok=True):
+        return {"ok": ok, "src_device": s, "dst_device": d, "kernel_gbps": g}
+
+    n = 4
+    res = {"ok": True, "devices": [{"device": d, "ok": True, "peers": [pull(s, d, 60.0) for s in range(n) if s != d]}
+                                   for d in range(n)]}
+    res["devices"][2]["peers"][0] = pull(0, 2, 12.0)           # 0 -> 2 runs at a fifth of the rest
+    res["devices"][3]["peers"][1] = pull(1, 3, None, ok=False)  # 1 -> 3 failed outright
+    gpus = [2, 3, 5, 7]  # host ordinals of the probe's devices 0..3
+    rep = xgmi.link_report(res, gpus, fraction=0.5)
+    assert rep["pulls"] == 12 and rep["median_gbps"] == 60.0 and rep["floor_gbps"] == 30.0
+    assert {(e["src"], e["dst"]) for e in rep["degraded"]} == {(2, 5), (3, 7)}
+    v = xgmi.node_view(rep, [7])
+    assert not v["healthy"] and v["pulls"] == 6 and [(e["src"], e["dst"]) for e in v["degraded"]] == [(3, 7)]
+    ann = xgmi.annotations(v)
+    assert ann["tk8s.amd.com/xgmi-healthy"] == "false" and "3->7:failed" in ann["tk8s.amd.com/xgmi-links"]
+    share = split_host_result(res, gpus, [3])
+    assert share["ok"] and not share["xgmi"]["healthy"]  # its own GPU is fine; a link is not
+    # the fault point scales one directed link (host ordinals)
+    monkeypatch.setenv("TK8S_FAULTS", "xgmi.degrade@5-7:0.25")
+    rep = xgmi.link_report(res, gpus, fraction=0.5)
+    assert {(e["src"], e["dst"]) for e in rep["degraded"]} == {(2, 5), (3, 7), (5, 7)}
+
+
+def test_host_burnin_pulls_every_link_only_with_two_or_more_gpus():
+    from tritonk8ssupervisor_amd.earlyburn import default_validation_command, host_burnin_command
+
+    base = default_validation_command(peers=False)
+    assert "--peers" not in host_burnin_command(base, [0])       # N=1: a no-op by construction
+    assert host_burnin_command(base, [0, 1]).count("--peers") == 1
+    assert host_burnin_command(host_burnin_command(base, [0, 1]), [0, 1]).count("--peers") == 1
+
+
+def test_setup_checks_xgmi_links_before_ready(ws):
+    s = _summary(_setup(ws, "--nodes", "3", "--rccl", "off"))
+    assert s["xgmi"]["pulls"] == 6 and not s["xgmi"]["degraded"]
+    for i in (1, 2, 3):
+        ann = s["validation"][f"kubenode{i}"]
+        assert ann["xgmi-healthy"] == "true" and len(ann["xgmi-links"].split(",")) == 4  # 2 in + 2 out
+    r = subprocess.run(["./kubectl", "get", "node", "kubenode1", "-o", "json"], cwd=ws, env=_env(),
+                       capture_output=True, text=True)
+    conds = {c["type"]: c for c in json.loads(r.stdout)["status"]["conditions"]}
+    assert conds["XGMILinksHealthy"]["status"] == "True" and conds["Ready"]["status"] == "True"
+
+
+def test_degraded_xgmi_link_marks_its_nodes_not_ready(ws):
+    t = time.monotonic()
+    r = _setup(ws, "--nodes", "3", "--rccl", "off", env=_env(TK8S_FAULTS="xgmi.degrade@0-1:0.1"))
+    assert r.returncode == 2 and "XGMILinkDegraded" in r.stderr, r.stdout[-2000:] + r.stderr[-2000:]
+    assert time.monotonic() - t < 60
+    out = subprocess.run(["./kubectl", "get", "nodes"], cwd=ws, env=_env(), capture_output=True, text=True).stdout
+    state = {l.split()[0]: l.split()[1] for l in out.splitlines()[1:] if l.strip()}
+    assert state["kubenode1"] == "NotReady" and state["kubenode2"] == "NotReady" and state["kubenode3"] == "Ready", out
+    d = subprocess.run(["./kubectl", "describe", "node", "kubenode2"], cwd=ws, env=_env(), capture_output=True,
+                       text=True).stdout
+    assert "XGMILinkDegraded" in d and "0->1" in d

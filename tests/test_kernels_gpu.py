@@ -488,9 +488,54 @@ def test_hsaprobe_known_answer_and_gpuinfo_agree_with_the_hip_probe(nat):
     for a, b in zip(hsa["gpuinfo"]["devices"], hip["gpuinfo"]["devices"]):
         assert a["gfx"] == b["gfx"] == "gfx950"
         assert a["pci_bus_id"] == b["pci_bus_id"] and a["cu_count"] == b["cu_count"]
-    # peer pulls stay with tk8s-probe: asked for them, the HSA tool refuses before touching the GPU
-    import subprocess
 
-    from tritonk8ssupervisor_amd.ops import BIN
 
-    assert subprocess.run([str(BIN / "tk8s-hsaprobe"), "--peers"], capture_output=True, timeout=30).returncode == 4
+def test_hsaprobe_peers_on_one_gpu_is_a_no_op(nat):
+    """--peers with a single GPU: no pair to pull over, nothing dispatched for it, result unchanged."""
+    n = _gpu_count()
+    rc, out = _hsaprobe("--all-devices", "--peers", "--hbm-bytes", str(64 << 20), "--md5-bytes", str(1 << 20),
+                        "--copy-bytes", str(16 << 20), "--iters", "1")
+    assert rc == 0 and out["ok"], out
+    assert out["peer_rounds"] == n - 1
+    for d in out["devices"]:
+        assert d["peers_ok"] and len(d["peers"]) == n - 1
+    if n == 1:
+        assert out["timings_ms"]["peers"] < 1.0, out["timings_ms"]
+
+
+def test_hsaprobe_pull_from_granted_non_local_memory(nat):
+    """The peer-pull mechanism from a source the GPU does not own: host memory granted with
+    hsa_amd_agents_allow_access, pulled by the stream copy kernel at system-scope acquire and
+    checked against the source's pattern (the part of N7 a one-GPU box can run)."""
+    rc, out = _hsaprobe("--peers-host", "--peer-bytes", str(8 << 20), "--hbm-bytes", str(16 << 20),
+                        "--md5-bytes", str(1 << 20), "--copy-bytes", str(1 << 20), "--iters", "1")
+    assert rc == 0 and out["ok"], out
+    hp = out["devices"][0]["host_pull"]
+    assert hp["ok"] and hp["access"] == "allowed" and hp["bad_words"] == 0 and hp["src_device"] == -1, hp
+    assert 1.0 < hp["kernel_gbps"] < 1000.0, hp  # PCIe/host-link rate, not a local-HBM copy
+
+
+def test_hsaprobe_md5_unpinned_for_other_inputs(nat):
+    rc, out = _hsaprobe("--md5-bytes", str(1 << 20), "--hbm-bytes", str(16 << 20), "--copy-bytes", str(1 << 20),
+                        "--iters", "1")
+    assert rc == 0 and out["md5_pinned"] is False
+    rc, out = _hsaprobe("--hbm-bytes", str(16 << 20), "--copy-bytes", str(1 << 20), "--iters", "1")
+    assert rc == 0 and out["md5_pinned"] is True and out["md5"]["digest"] == out["md5_expected"]
+
+
+@pytest.mark.skipif(_gpu_count() < 2, reason="needs >= 2 MI355X (xGMI)")
+def test_multi_gpu_hsaprobe_peer_matrix(nat):
+    """Every ordered pair pulled once over its own link, pattern-checked, at xGMI rates."""
+    n = _gpu_count()
+    rc, out = _hsaprobe("--all-devices", "--peers", "--hbm-bytes", str(64 << 20), "--md5-bytes", str(1 << 20),
+                        "--copy-bytes", str(16 << 20), "--iters", "2")
+    assert rc == 0 and out["ok"], out
+    pairs = {(p["src_device"], p["dst_device"]) for d in out["devices"] for p in d["peers"]}
+    assert pairs == {(a, b) for a in range(n) for b in range(n) if a != b}
+    for d in out["devices"]:
+        assert d["peers_ok"]
+        assert all(p["ok"] and p["access"] == "allowed" and p["kernel_gbps"] > 20 for p in d["peers"]), d["peers"]
+    from tritonk8ssupervisor_amd import xgmi
+
+    rep = xgmi.link_report(out)
+    assert rep["pulls"] == n * (n - 1) and not rep["degraded"], rep

@@ -61,9 +61,12 @@ def _pid_alive(pidfile: Path) -> bool:
         return True
 
 
-def split_host_result(result: dict, burnin_gpus: list[int], machine_gpus: list[int]) -> dict | None:
+def split_host_result(result: dict, burnin_gpus: list[int], machine_gpus: list[int],
+                      report: dict | None = None) -> dict | None:
     """One machine's share of a host burn-in: the entries of its GPUs, renumbered in the order
-    the machine sees them (its pods' device i = machine_gpus[i]). None if any GPU is missing."""
+    the machine sees them (its pods' device i = machine_gpus[i]). None if any GPU is missing.
+    With peer pulls in the result, the share also carries ``xgmi``: the host-wide link verdict
+    (xgmi.link_report) for the links into and out of this machine's GPUs."""
     pos = {g: i for i, g in enumerate(burnin_gpus)}
     if not machine_gpus or any(g not in pos for g in machine_gpus):
         return None
@@ -101,6 +104,14 @@ def split_host_result(result: dict, burnin_gpus: list[int], machine_gpus: list[i
             out[key] = first[key]
     if "md5_expected" in result:
         out["md5_expected"] = result["md5_expected"]
+    if report is None and any(d.get("peers") for d in result.get("devices", [])):
+        from .xgmi import link_report
+
+        report = link_report(result, burnin_gpus)
+    if report is not None and report.get("pulls"):
+        from .xgmi import node_view
+
+        out["xgmi"] = node_view(report, machine_gpus)
     return out
 
 
@@ -133,6 +144,7 @@ class HostBurnin:
         self.proc = None
         self.done = False
         self.result: dict | None = None
+        self.xgmi: dict | None = None  # host-wide link verdict (xgmi.link_report), with peer pulls
         self.machines: dict[str, tuple[Path, list[int]]] = {}
         import threading
 
@@ -197,7 +209,7 @@ class HostBurnin:
 
         from .utils.fsutil import atomic_write
 
-        share = split_host_result(self.result, self.gpus, gpus) if self.result else None
+        share = split_host_result(self.result, self.gpus, gpus, self.xgmi) if self.result else None
         if share is not None and not share["ok"]:
             # Only a passing share is handed out: a failure (or a fault of the shared run itself)
             # makes the machine's validation pod probe its GPUs on its own, which then decides.
@@ -236,11 +248,23 @@ class HostBurnin:
 
     def _finish(self, result: dict | None, rc: int) -> None:
         """Hand every registered machine its share (or release it to probe by itself)."""
+        xg = None
+        if result and any(d.get("peers") for d in result.get("devices", [])):
+            from .xgmi import link_report
+
+            xg = link_report(result, self.gpus)
         with self.lock:
-            self.result, self.done = result, True
+            self.result, self.xgmi, self.done = result, xg, True
             for name, (mdir, gpus) in self.machines.items():
                 self._deliver(name, mdir, gpus)
-        self.log("gpu_burnin_host_done", rc=rc, ok=bool(result and result.get("ok")), gpus=self.gpus)
+        extra = {}
+        if xg is not None:
+            extra = {"xgmi_pulls": xg["pulls"], "xgmi_median_gbps": xg["median_gbps"], "xgmi_min_gbps": xg["min_gbps"],
+                     "xgmi_degraded": [f"{e['src']}->{e['dst']}" for e in xg["degraded"]]}
+        timings = (result or {}).get("timings_ms") or {}
+        self.log("gpu_burnin_host_done", rc=rc, ok=bool(result and result.get("ok")), gpus=self.gpus,
+                 runtime_init_ms=timings.get("runtime_init", timings.get("hip_init")), peers_ms=timings.get("peers"),
+                 **extra)
         self.finished.set()
 
     def stop(self) -> None:

@@ -81,6 +81,15 @@ def node_ready(n: dict) -> bool:
     return bool(c and c["status"] == "True")
 
 
+def _set_ready(node: dict, message: str = "tk8s agent heartbeating") -> bool:
+    """Ready follows the heartbeat, unless the node's xGMI links failed the pre-Ready check
+    (xgmi.py): then it stays NotReady with that reason while the agent is alive."""
+    x = _cond(node, "XGMILinksHealthy")
+    if x and x["status"] == "False":
+        return _set_cond(node, "Ready", "False", "XGMILinkDegraded", x.get("message", ""))
+    return _set_cond(node, "Ready", "True", "AgentReady", message)
+
+
 def node_validated(n: dict) -> bool:
     c = _cond(n, "AMDGPUValidated")
     return bool(c and c["status"] == "True")
@@ -93,6 +102,21 @@ def pod_gpus(p: dict) -> int:
         v = r.get("limits", {}).get(GPU, r.get("requests", {}).get(GPU, 0))
         total += int(v or 0)
     return total
+
+
+def _xgmi_view(result: dict) -> dict | None:
+    """The xGMI link verdict of a validation result: the host burn-in's share carries it
+    (``xgmi``); a machine's own multi-GPU probe carries raw pulls, judged here."""
+    if not isinstance(result, dict):
+        return None
+    if isinstance(result.get("xgmi"), dict):
+        return result["xgmi"]
+    if any(d.get("peers") for d in result.get("devices") or []):
+        from .. import xgmi
+
+        rep = xgmi.link_report(result)
+        return xgmi.node_view(rep, sorted({e["src"] for e in rep["links"]} | {e["dst"] for e in rep["links"]}))
+    return None
 
 
 def merge_patch(target, patch):
@@ -421,7 +445,9 @@ class ControlPlane:
                                      {"type": "Hostname", "address": name}],
                        "nodeInfo": body.get("nodeInfo", {}), "conditions": []},
         }
-        _set_cond(node, "Ready", "True", "AgentReady", "tk8s agent registered and heartbeating")
+        if old is not None and _cond(old, "XGMILinksHealthy"):  # a re-join keeps the link verdict
+            node["status"]["conditions"].append(copy.deepcopy(_cond(old, "XGMILinksHealthy")))
+        _set_ready(node, "tk8s agent registered and heartbeating")
         _set_cond(node, "AMDGPUValidated", "Unknown" if gpus else "True",
                   "Pending" if gpus else "NoGPUs", "validation pod not finished" if gpus else "")
         self.store.put("nodes", key, node)
@@ -573,6 +599,9 @@ class ControlPlane:
             "project": pid, "nodes": len(nodes), "nodes_ready": len(ready),
             "nodes_validated": sum(1 for n in ready if node_validated(n)),
             "nodes_validation_failed": sum(1 for n in nodes if (_cond(n, "AMDGPUValidated") or {}).get("status") == "False"),
+            "validation_failures": [{"node": n["metadata"]["name"], "reason": c.get("reason"),
+                                     "message": (c.get("message") or "")[:300]}
+                                    for n in nodes for c in [_cond(n, "AMDGPUValidated") or {}] if c.get("status") == "False"],
             "gpus_capacity": sum(int(n["status"]["capacity"].get(GPU, 0)) for n in nodes),
             "gpus_allocatable": sum(int(n["status"]["allocatable"].get(GPU, 0)) for n in ready),
             "gpus_in_use": in_use, "pods_by_phase": by_phase, "resourceVersion": self.store.rv,
@@ -698,7 +727,7 @@ class ControlPlane:
         if "annotations" in body:
             new["metadata"].setdefault("annotations", {}).update(body["annotations"])
             changed = True
-        changed |= _set_cond(new, "Ready", "True", "AgentReady", "tk8s agent heartbeating")
+        changed |= _set_ready(new)
         if changed:
             self.store.put("nodes", key, new)
             self.reconcile()
@@ -1251,16 +1280,29 @@ class ControlPlane:
                 n = self.store.get("nodes", key)
                 if n is None:
                     continue
+                result = pod.get("status", {}).get("result") or {}
+                view = _xgmi_view(result)
                 want = ("True", "ProbesPassed") if phase == "Succeeded" else ("False", "ProbesFailed")
+                if want[0] == "True" and view is not None and not view["healthy"]:
+                    want = ("False", "XGMILinkDegraded")
                 c = _cond(n, "AMDGPUValidated")
                 if c and (c["status"], c["reason"]) == want:
                     continue
-                result = pod.get("status", {}).get("result") or {}
 
-                def fn(node, want=want, result=result, pod=pod):
-                    _set_cond(node, "AMDGPUValidated", want[0], want[1],
-                              pod.get("status", {}).get("message", "")[:500])
+                def fn(node, want=want, result=result, pod=pod, view=view):
+                    from .. import xgmi
+
+                    msg = xgmi.message(view) if want[1] == "XGMILinkDegraded" else pod.get("status", {}).get("message", "")
+                    _set_cond(node, "AMDGPUValidated", want[0], want[1], msg[:500])
                     ann = node["metadata"].setdefault("annotations", {})
+                    if view is not None:
+                        ann.update(xgmi.annotations(view))
+                        if view["healthy"]:
+                            _set_cond(node, "XGMILinksHealthy", "True", "LinksHealthy",
+                                      f"{view['pulls']} pulls >= {view.get('min_fraction')} x median {view.get('median_gbps')} GB/s")
+                        else:
+                            _set_cond(node, "XGMILinksHealthy", "False", "XGMILinkDegraded", xgmi.message(view))
+                        _set_ready(node)
                     for k, path in (("hbm-write-gbps", ("hbm", "gbps")), ("hbm-read-gbps", ("hbm", "read_gbps")),
                                     ("md5-mbps", ("md5", "mbps")),
                                     ("copy-gbps", ("copy", "kernel_gbps")), ("probe-ms", ("timings_ms", "total")),
@@ -1270,6 +1312,11 @@ class ControlPlane:
                             ann[f"tk8s.amd.com/{k}"] = f"{v:.1f}"
 
                 self.store.patch("nodes", key, fn)
+                if want[1] == "XGMILinkDegraded":
+                    from .. import xgmi
+
+                    self._event(pid, "default", {"kind": "Node", "name": nn}, "XGMILinkDegraded", xgmi.message(view),
+                                "Warning")
 
     def _ctl_jobs(self, pid: str) -> None:
         for job in self.store.list("jobs", lambda o: self._in(pid, o)):

@@ -51,14 +51,14 @@ def _loads(text: str):
 
 
 # ---- shared helpers (re-exported by models/hostinfo.py, provider/hostreg.py, orchestrator.py) ----
-def probe_tool(peers: bool) -> str:
+def probe_tool(peers: bool = False) -> str:
     """The validation payload binary: ``tk8s-hsaprobe`` (the same kernels and checks dispatched on
-    ROCr directly, ~20 ms less start-up than HIP, native/tools/tk8s_hsaprobe.cpp) unless xGMI
-    peer pulls are wanted (HIP peer access: ``tk8s-probe``), ``TK8S_PROBE_RUNTIME=hip`` says so,
-    or its code objects are missing."""
+    ROCr directly, ~20 ms less start-up than HIP, native/tools/tk8s_hsaprobe.cpp; its --peers
+    pulls every ordered GPU pair over xGMI) unless ``TK8S_PROBE_RUNTIME=hip`` says otherwise or
+    its code objects are missing: then ``tk8s-probe`` (HIP, the same checks and JSON)."""
     hsa = os.path.join(BIN, "tk8s-hsaprobe")
     lib = os.path.join(PKG, "lib")
-    if (not peers and os.environ.get("TK8S_PROBE_RUNTIME", "hsa") != "hip" and os.access(hsa, os.X_OK)
+    if (os.environ.get("TK8S_PROBE_RUNTIME", "hsa") != "hip" and os.access(hsa, os.X_OK)
             and os.path.exists(os.path.join(lib, "tk8s_stream.co")) and os.path.exists(os.path.join(lib, "tk8s_md5.co"))):
         return hsa
     return os.path.join(BIN, "tk8s-probe")
@@ -72,6 +72,17 @@ def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 <<
         return [sys.executable, "-m", "tritonk8ssupervisor_amd.ops.fakeprobe"]
     return [probe_tool(peers), "--all-devices", "--gpuinfo", *(["--peers"] if peers else []), "--hbm-bytes",
             str(hbm_bytes), "--md5-bytes", str(md5_bytes), "--iters", str(iters)]
+
+
+def host_burnin_command(command: list[str], gpus: list[int]) -> list[str]:
+    """The host burn-in runs the validation command over every worker GPU at once, so it is the
+    one place that owns both ends of every xGMI link: with two or more GPUs it also pulls every
+    ordered pair (``--peers``, N7) before any node can be Ready -- also when each worker has a
+    single GPU, where no per-machine probe could see a link. One GPU: nothing to pull, no flag."""
+    cmd = [str(a) for a in command]
+    if len(gpus) > 1 and "--peers" not in cmd:
+        cmd.append("--peers")
+    return cmd
 
 
 def registry_dir(environ=None) -> str:
@@ -231,8 +242,8 @@ def plan(argv: list[str], environ=None, cwd: str | None = None, kfd_root: str = 
         free = [i for i in range(len(vis) if vis is not None else n) if i not in claimed]
     if len(free) < count:
         return None
-    # no xGMI link inside a 1-GPU machine: the RCCL Job checks the fabric
-    cmd = default_validation_command(peers=per > 1)
+    # the per-machine command (peers inside a multi-GPU machine), with the host-wide pulls added
+    cmd = host_burnin_command(default_validation_command(peers=per > 1), free[:count])
     state = os.path.join(ws, ".tk8s")
     master = str(opts.get("--master-hostname", answers.get("master_hostname") or "kubemaster"))
     return {"gpus": free[:count], "command": cmd, "state_dir": state,

@@ -85,7 +85,14 @@ def main():
     n = len([x for x in (os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES", "")).split(",") if x])
     fail = os.environ.get("TK8S_FAKE_PROBE_FAIL", "") == node
     dev = {"ok": not fail, "hbm": {"ok": True, "gbps": 6200.0}, "md5": {"ok": True, "mbps": 2.3e6}}
-    out = {"ok": not fail, "fake": True, "device_count": n, "probed": n, "devices": [dict(dev, device=i) for i in range(n)],
+    devices = [dict(dev, device=i) for i in range(n)]
+    if "--peers" in sys.argv:  # every ordered pair, the shape of tk8s-hsaprobe --peers
+        for i, d in enumerate(devices):
+            d["peers"] = [{"ok": True, "probe": "xgmi_peer_pull", "src_device": j, "dst_device": i, "bytes": 32 << 20,
+                           "iters": 2, "access": "allowed", "kernel_ms": 0.6, "kernel_gbps": 55.0 + 0.1 * ((i + j) % 5),
+                           "bad_words": 0} for j in range(n) if j != i]
+            d["peers_ok"] = True
+    out = {"ok": not fail, "fake": True, "device_count": n, "probed": n, "devices": devices,
            "hbm": dev["hbm"], "md5": dev["md5"],
            "gpuinfo": {"ok": True, "device_count": n, "devices": [{"index": i, "gfx": "gfx950", "pci_bus_id": f"0000:{i:02x}:00.0",
                                                                     "uuid": f"fake-{i}"} for i in range(n)]}}

@@ -19,6 +19,7 @@ import json
 import os
 import shutil
 import sys
+import threading
 import time
 from dataclasses import dataclass
 from pathlib import Path
@@ -416,12 +417,16 @@ class Setup:
             if early is not None:
                 early.kill()
             return
+        from .earlyburn import host_burnin_command
+
         try:
             pkg = self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE)
-            cmd = self._validation_command()
-            if early is not None and early.command == cmd and hasattr(self.provider, "prefer_gpus"):
+            base = self._validation_command()
+            if (early is not None and hasattr(self.provider, "prefer_gpus")
+                    and early.command == host_burnin_command(base, early.gpus)):
                 self.provider.prefer_gpus(early.gpus)
             gpus = self.provider.predict_gpus(int(pkg.gpus or 0), int(self.cfg.KUBERNETES_NUMBER_OF_NODES))
+            cmd = host_burnin_command(base, gpus)
         except Exception:  # noqa: BLE001 - prediction is an optimisation only
             gpus, cmd = [], None
         import threading
@@ -518,12 +523,16 @@ class Setup:
         pid = self.project_id()
         n = int(self.cfg.KUBERNETES_NUMBER_OF_NODES)
         g = self.expected_gpus()
+        # kubectl works from here on, also when the wait below fails (its message points at it)
+        kc = threading.Thread(target=self._write_kubeconfig, args=(c.base, pid), name="kubeconfig", daemon=True)
+        kc.start()
         self.out("Waiting on the cluster: all nodes Ready" + (f", {g} x amd.com/gpu validated" if g else ""))
         deadline = time.monotonic() + self.timeout
         last = {}
         while True:
             left = deadline - time.monotonic()
             if left <= 0:
+                kc.join(5.0)
                 raise SetupError(f"cluster not ready after {self.timeout:.0f}s: {json.dumps(last)}", code=124)
             last = c.get("/v1/cluster/wait", query={"project": pid, "nodes": n, "gpus": g,
                                                     "validated": int(self.validate), "timeout": min(left, 30.0)},
@@ -531,8 +540,12 @@ class Setup:
             if last.get("ready"):
                 return last
             if last.get("failed"):
-                raise SetupError(f"GPU validation failed on {last.get('nodes_validation_failed')} node(s): "
-                                 f"see `./kubectl get pods -n kube-system` and pod logs", code=2)
+                kc.join(5.0)
+                why = "; ".join(f"{f['node']}: {f['reason']}" + (f" ({f['message']})" if f.get("message") else "")
+                                for f in last.get("validation_failures") or [])
+                raise SetupError(f"GPU validation failed on {last.get('nodes_validation_failed')} node(s)"
+                                 + (f": {why}" if why else "")
+                                 + "\n    see `./kubectl describe nodes` and `./kubectl get pods -n kube-system`", code=2)
 
     def run_rccl(self) -> dict | None:
         from .controlplane.client import client_from_kubeconfig
@@ -652,6 +665,16 @@ class Setup:
             "dashboard": f"{base}/r/projects/{pid}/kubernetes-dashboard:9090/",
             "kubectl_config": f"{base}/env/{pid}/kubernetes/kubectl", "project": pid, "api": base,
         }
+        hb = self.host_burnin
+        if hb is not None and hb.done:
+            t = (hb.result or {}).get("timings_ms") or {}
+            self.summary["host_burnin"] = {"gpus": hb.gpus, "ok": bool(hb.result and hb.result.get("ok")),
+                                           "runtime_init_ms": t.get("runtime_init", t.get("hip_init")),
+                                           "peers_ms": t.get("peers"), "total_ms": t.get("total")}
+            if hb.xgmi is not None:
+                self.summary["xgmi"] = {k: hb.xgmi[k] for k in ("pulls", "median_gbps", "min_gbps", "floor_gbps",
+                                                                 "min_fraction")}
+                self.summary["xgmi"]["degraded"] = [f"{e['src']}->{e['dst']}" for e in hb.xgmi["degraded"]]
         ws.save_state(summary=self.summary, finished=time.time())
         self.events.emit("setup_done", **{k: v for k, v in self.summary.items() if k != "phases"})
         self.out("")

@@ -1,0 +1,113 @@
+"""xGMI link health from a GPU burn-in's peer pulls (N7).
+
+The reference checks every host during its readiness loop, before it declares success
+(/root/reference/setup.sh:69-82: it ssh-counts the dashboard containers on every host and
+restarts a stuck one). The MI355X analogue of "is this host healthy enough to be Ready" is the
+fabric: every ordered GPU pair is pulled once by ``tk8s-hsaprobe --peers`` (one round per
+offset, so each directed link carries exactly one pull at a time and its GB/s is that link's),
+and this module judges the matrix:
+
+* a pull that failed (no access, a kernel error, a wrong word) is a dead link;
+* a pull below ``fraction`` x the median of the good pulls is a degraded link (the 8 GPUs of
+  an MI355X node are fully connected by identical links, so the median is the healthy rate).
+
+A node whose GPU sits at either end of a bad link is marked ``XGMILinksHealthy=False``
+(reason ``XGMILinkDegraded``), which the control plane turns into NotReady and a failed
+validation, so the bring-up stops with a reason instead of handing out a GPU whose collectives
+would crawl. Per-link GB/s are published as node annotations.
+
+Fault point (utils/faults.py): ``xgmi.degrade@<src>-<dst>:<factor>`` scales the measured rate
+of that directed link (host GPU ordinals) by ``factor`` (default 0.1), on real pulls or the
+fake probe's alike, to exercise the NotReady path.
+"""
+from __future__ import annotations
+
+import os
+
+from .utils.faults import _parse
+
+DEFAULT_FRACTION = 0.5
+
+
+def min_fraction() -> float:
+    try:
+        return float(os.environ.get("TK8S_XGMI_MIN_FRACTION", DEFAULT_FRACTION))
+    except ValueError:
+        return DEFAULT_FRACTION
+
+
+def _injected() -> dict[tuple[int, int], float]:
+    out = {}
+    for point, target, arg in _parse(os.environ.get("TK8S_FAULTS", "")):
+        if point != "xgmi.degrade" or not target or "-" not in target:
+            continue
+        a, b = target.split("-", 1)
+        if a.isdigit() and b.isdigit():
+            out[(int(a), int(b))] = float(arg) if arg else 0.1
+    return out
+
+
+def link_report(result: dict, gpus: list[int] | None = None, fraction: float | None = None) -> dict:
+    """Judge the peer pulls of one probe result. ``gpus`` maps the probe's device index to host
+    GPU ordinals (a burn-in over ROCR_VISIBLE_DEVICES=gpus sees them as 0..n-1)."""
+    fraction = min_fraction() if fraction is None else fraction
+    host = (lambda i: gpus[i] if gpus is not None and 0 <= i < len(gpus) else i)
+    faults = _injected()
+    links = []
+    for d in result.get("devices") or []:
+        for p in d.get("peers") or []:
+            src, dst = host(int(p.get("src_device", -1))), host(int(p.get("dst_device", d.get("device", -1))))
+            gbps = p.get("kernel_gbps")
+            ok = bool(p.get("ok")) and gbps is not None
+            if ok and (src, dst) in faults:
+                gbps = gbps * faults[(src, dst)]
+            links.append({"src": src, "dst": dst, "gbps": round(float(gbps), 2) if gbps is not None else None,
+                          "ok": ok, **({"error": p["error"]} if p.get("error") else {})})
+    links.sort(key=lambda e: (e["src"], e["dst"]))
+    good = sorted(e["gbps"] for e in links if e["ok"])
+    median = 0.0
+    if good:
+        mid = len(good) // 2
+        median = good[mid] if len(good) % 2 else (good[mid - 1] + good[mid]) / 2
+    floor = fraction * median
+    degraded = []
+    for e in links:
+        if not e["ok"]:
+            degraded.append({**e, "reason": e.get("error") or "pull failed"})
+        elif e["gbps"] < floor:
+            degraded.append({**e, "reason": f"{e['gbps']:.1f} GB/s < {fraction:g} x median {median:.1f} GB/s"})
+    return {"pulls": len(links), "median_gbps": round(median, 2), "min_fraction": fraction,
+            "floor_gbps": round(floor, 2), "min_gbps": min(good) if good else None, "links": links,
+            "degraded": degraded}
+
+
+def node_view(report: dict, gpus: list[int]) -> dict:
+    """The part of a host-wide report that concerns a machine owning host GPUs ``gpus``: the
+    links into and out of them, and the bad ones among those."""
+    mine = set(gpus)
+    links = [e for e in report.get("links", []) if e["src"] in mine or e["dst"] in mine]
+    bad = [e for e in report.get("degraded", []) if e["src"] in mine or e["dst"] in mine]
+    good = [e["gbps"] for e in links if e["ok"]]
+    return {"gpus": sorted(mine), "pulls": len(links), "median_gbps": report.get("median_gbps"),
+            "floor_gbps": report.get("floor_gbps"), "min_fraction": report.get("min_fraction"),
+            "min_gbps": min(good) if good else None, "links": links, "degraded": bad, "healthy": not bad}
+
+
+def annotations(view: dict) -> dict[str, str]:
+    """Node annotations for a node_view: per-link GB/s (host ordinals), the min and the verdict."""
+    if not view or not view.get("pulls"):
+        return {}
+    out = {"tk8s.amd.com/xgmi-links": ",".join(
+        f"{e['src']}->{e['dst']}:{e['gbps']:.1f}" if e["ok"] else f"{e['src']}->{e['dst']}:failed" for e in view["links"]),
+        "tk8s.amd.com/xgmi-median-gbps": f"{view.get('median_gbps') or 0:.1f}",
+        "tk8s.amd.com/xgmi-healthy": "true" if view.get("healthy") else "false"}
+    if view.get("min_gbps") is not None:
+        out["tk8s.amd.com/xgmi-min-gbps"] = f"{view['min_gbps']:.1f}"
+    if view.get("degraded"):
+        out["tk8s.amd.com/xgmi-degraded"] = ",".join(f"{e['src']}->{e['dst']}" for e in view["degraded"])
+    return out
+
+
+def message(view: dict) -> str:
+    bad = view.get("degraded") or []
+    return "; ".join(f"GPU {e['src']}->{e['dst']}: {e['reason']}" for e in bad)[:500]
