@@ -88,7 +88,8 @@ def _spawn_early(tmp_path, gpus, cmd):
 
 def test_orchestrator_adopts_a_matching_early_burnin(tmp_path, monkeypatch):
     monkeypatch.setenv("TK8S_FAKE_GPUS", "8")
-    cmd = [a for a in earlyburn.default_validation_command() if a != "--peers"]
+    # the host burn-in of two 1-GPU workers: the per-machine command plus the xGMI pulls
+    cmd = earlyburn.host_burnin_command(earlyburn.default_validation_command(peers=False), [5, 6])
     early = _spawn_early(tmp_path, [5, 6], cmd)  # not the allocator's own first choice
     events = []
     s = _setup_obj(tmp_path, events)
