@@ -196,6 +196,12 @@ def test_triton_provider_with_fake_cli(tmp_path, monkeypatch):
     monkeypatch.setenv("HOME", str(home))
     monkeypatch.setenv("FAKE_TRITON_LOG", str(tmp_path / "calls"))
     monkeypatch.setenv("FAKE_KEY_ID", md5)
+    # the VMs are configured over ssh with the discovered key (fake ssh: tests/fakessh.py)
+    (tmp_path / "hosts" / "10.0.0.9" / ".ssh").mkdir(parents=True)
+    (tmp_path / "hosts" / "10.0.0.9" / ".ssh" / "authorized_keys").write_text((home / ".ssh" / "id_ed25519.pub").read_text())
+    monkeypatch.setenv("TK8S_SSH", f"{sys.executable} {Path(__file__).parent / 'fakessh.py'}")
+    monkeypatch.setenv("FAKESSH_ROOT", str(tmp_path / "hosts"))
+    monkeypatch.setenv("SDC_KEY", str(home / ".ssh" / "id_ed25519"))
     p = TritonProvider(tmp_path / "state")
     env = p.env()
     assert env == {"SDC_URL": "https://us-east-1.api.joyent.com", "SDC_ACCOUNT": "me", "SDC_KEY_ID": md5}
@@ -208,6 +214,14 @@ def test_triton_provider_with_fake_cli(tmp_path, monkeypatch):
     assert [x.name for x in pk] == ["k4-highcpu-kvm-1.75G", "k4-highcpu-kvm-7.75G"]  # -kvm- only (setup.sh:259)
     m = p.create_machine("kubenode1", "3333", ["1111-aaaa"], tags={"role": "host"})
     assert m.primaryip == "10.0.0.9" and m.id == "id-kubenode1"
+    # node runtime installed on the VM, work dir made there; exec runs in it with the machine env
+    assert Path(m.home, "tritonk8ssupervisor_amd", "executor.py").exists()
+    assert m.sandbox == str(tmp_path / "hosts" / "10.0.0.9" / "tk8s" / "machine")
+    rc, out = p.exec(m, "pwd; echo $TK8S_MACHINE")
+    assert rc == 0 and out.split() == [m.sandbox, "kubenode1"]
+    calls = [json.loads(x) for x in (tmp_path / "hosts" / "calls.jsonl").read_text().splitlines()]
+    assert all(c["key"] == str(home / ".ssh" / "id_ed25519") and c["user"] == "root" for c in calls)
+    assert all(c["opts"]["StrictHostKeyChecking"] == "accept-new" and c["opts"]["UserKnownHostsFile"] for c in calls)
     p.delete_machine(m)
     calls = (tmp_path / "calls").read_text().splitlines()
     assert any(c.startswith("instance create --wait --json --name=kubenode1 -N 1111-aaaa -t role=host") for c in calls)

@@ -39,6 +39,33 @@ ALL_GPUS = "tk8s.amd.com/all-gpus"
 GPU_VISIBILITY = "tk8s.amd.com/gpu-visibility"
 VALIDATION_LABEL = "tk8s.amd.com/validation"
 TERMINAL = ("Succeeded", "Failed")
+TK8S_HOME = str(Path(__file__).resolve().parents[2])  # this node's tk8s install root
+
+# What of the agent's own environment a pod inherits (the rest of a pod's env is the pod spec, the
+# downward API and the device plugin's Allocate()). A container starts from its image's env, not
+# from the kubelet's: agent internals (TK8S_MACHINE*, TK8S_FAULTS, PYTHONPATH, credentials) never
+# reach a pod. Kept: the login basics, the ROCm/HIP/HSA runtime knobs and the GPU view the node
+# was given, RCCL tuning, and the tk8s fake-GPU/diagnostic switches the test tier relies on.
+POD_ENV_KEEP = {"PATH", "HOME", "USER", "LOGNAME", "SHELL", "LANG", "LANGUAGE", "TZ", "TMPDIR", "TERM",
+                "ROCM_PATH", "LD_LIBRARY_PATH", "CUDA_VISIBLE_DEVICES", "GPU_MAX_HW_QUEUES", "OMP_NUM_THREADS",
+                "PYTORCH_ROCM_ARCH", "TK8S_TRACE", "TK8S_REMAP_PRIVILEGED_PORTS"}
+POD_ENV_KEEP_PREFIXES = ("LC_", "HSA_", "HIP_", "ROCR_", "AMD_", "NCCL_", "RCCL_", "TK8S_FAKE_", "TK8S_PROBE_")
+
+
+def pod_base_env(environ=None) -> dict:
+    env = os.environ if environ is None else environ
+    out = {k: v for k, v in env.items() if k in POD_ENV_KEEP or k.startswith(POD_ENV_KEEP_PREFIXES)}
+    out["TK8S_HOME"] = TK8S_HOME
+    out["TK8S_PYTHON"] = sys.executable
+    return out
+
+
+def node_visibility_allowed(pod: dict) -> bool:
+    """``gpu-visibility: node`` (a rank sees every GPU of the node, rccl-tests style) is for the
+    cluster's own fabric Jobs only: kube-system pods owned by a Job."""
+    md = pod.get("metadata", {})
+    return md.get("namespace") == "kube-system" and any(
+        r.get("kind") == "Job" for r in md.get("ownerReferences") or [])
 
 
 def pod_gpus(p: dict) -> int:
@@ -272,7 +299,10 @@ class Agent:
         need = len(self.plugin.devices()) if all_gpus else pod_gpus(pod)
         pp_dir = self.sandbox / "pods" / md["name"]
         pod_ip = self._pod_ip(key)
-        base = {"POD_NAME": md["name"], "POD_NAMESPACE": md["namespace"], "POD_UID": md.get("uid", ""),
+        # TK8S_MACHINE_DIR: the node's state dir (the hostPath the validation pod reads its
+        # machine's burn-in result from)
+        base = {"TK8S_HOME": TK8S_HOME, "TK8S_PYTHON": sys.executable, "TK8S_MACHINE_DIR": str(self.sandbox),
+                "POD_NAME": md["name"], "POD_NAMESPACE": md["namespace"], "POD_UID": md.get("uid", ""),
                 "POD_IP": pod_ip, "NODE_NAME": self.name, "NODE_IP": self.ip, "TK8S_API_URL": self.base,
                 "TK8S_K8S_API": f"{self.base}{self.api.prefix}", "TK8S_KV_URL": f"{self.base}/v1/kv"}
         try:  # config first: a pod waiting for a ConfigMap must not hold GPUs
@@ -284,6 +314,12 @@ class Agent:
             self._config_wait[key] = pod
             return
         self._config_wait.pop(key, None)
+        visibility = md.get("annotations", {}).get(GPU_VISIBILITY, "allocated")
+        if visibility == "node" and not node_visibility_allowed(pod):
+            self._report(key, md["name"], md["namespace"], "Failed",
+                         {"reason": "Forbidden", "message": f"{GPU_VISIBILITY}: node is reserved for kube-system "
+                                                            "Jobs (the cluster's RCCL fabric check)"}, None)
+            return
         free = self._free_devices()
         if need > len(free):
             self._report(key, md["name"], md["namespace"], "Failed",
@@ -301,8 +337,7 @@ class Agent:
             self._report(key, md["name"], md["namespace"], "Failed",
                          {"reason": "UnexpectedAdmissionError", "message": f"Allocate failed: {e}"}, None)
             return
-        env = {k: v for k, v in os.environ.items() if not k.startswith("TK8S_FAULT")}
-        visibility = md.get("annotations", {}).get(GPU_VISIBILITY, "allocated")
+        env = pod_base_env()
         env.update(pod_gpu_env(alloc["env"], [self._ordinal(i) for i in ids], visibility))
         env.update(base)
         env.update({"TK8S_GPU_IDS": ",".join(ids), "TK8S_GPU_COUNT": str(len(ids))})
@@ -312,7 +347,8 @@ class Agent:
             from ..apps import resolve
 
             entry = resolve(c.get("image"))
-            if entry:  # the image's entrypoint: a built-in app (apps/__init__.py)
+            if entry:  # the image's entrypoint: a built-in app (apps/__init__.py), the image's own env
+                env.setdefault("PYTHONPATH", TK8S_HOME)
                 argv = entry + [_expand(str(x), env) for x in (c.get("args") or [])]
         if not argv:
             self._report(key, md["name"], md["namespace"], "Failed", {
@@ -344,7 +380,7 @@ class Agent:
                 if ref:
                     for k, v in (self._config_data(kind, ns, ref["name"], ref.get("optional", False)) or {}).items():
                         out[prefix + k] = v
-        merged = {**os.environ, **base, **out}
+        merged = {**pod_base_env(), **base, **out}
         for e in c.get("env") or []:
             if "valueFrom" in e:
                 v = self._value_from(e["valueFrom"], pod, ns, pod_ip)

@@ -12,35 +12,44 @@ from pathlib import Path
 def start_burnin(ex, host: str, command: list, out: str = "run/gpu-burnin.json", name: str = "gpu-burnin",
                  env: dict | None = None) -> dict:
     """Start `command --out <out>` on a machine's GPUs as a one-shot daemon; idempotent (a burn-in
-    that is running or has finished is left alone)."""
+    that is running or has finished is left alone). Every file and process action goes through
+    the machine's executor, so on a remote machine the burn-in, its markers and its result all
+    live on that machine."""
     gpus = ex.machine_gpus(host)
     if not gpus:
         return {"changed": False, "skipped": True, "msg": "machine has no GPUs"}
     from .models.hostinfo import compose_visible_devices
 
-    mdir = Path(ex.machine_dir(host))
-    pending = mdir / (out + ".pending")
-    if (mdir / out).exists() or ex.daemon_status(host, name).get("running"):
+    fs = ex.fs(host)
+    pending = out + ".pending"
+    if fs.stat(out)["exists"] or ex.daemon_status(host, name).get("running"):
         return {"changed": False, "msg": "GPU burn-in already started", "gpus": gpus, "out": out}
-    if pending.exists() and _pid_alive(pending):
+    marker = fs.read(pending)
+    if marker is not None and _marker_pid(marker) and ex.pid_alive(host, _marker_pid(marker)):
         return {"changed": False, "msg": "GPU burn-in pending (host-level burn-in)", "gpus": gpus, "out": out}
-    pending.parent.mkdir(parents=True, exist_ok=True)
-    pending.touch()
     denv = dict(compose_visible_devices(gpus))
     denv["NODE_NAME"] = host
     denv.update({str(k): str(v) for k, v in (env or {}).items()})
     argv = [str(a) for a in command] + ["--out", out]
-    if os.sep in argv[0] and not os.access(argv[0], os.X_OK):
-        pending.unlink(missing_ok=True)  # not built yet: the validation pod will probe itself
-        return {"changed": False, "skipped": True, "msg": f"{argv[0]} is not built yet"}
+    tool = ex.localize(host, argv[0])
+    if os.sep in tool and not fs.stat(tool)["exists"]:
+        return {"changed": False, "skipped": True, "msg": f"{tool} is not built yet"}  # the pod probes itself
+    fs.write(pending, b"")
     info = ex.start_daemon(host, name, argv, env=denv, restart="no", wait_for_log=None, timeout=0)
     if not info.get("ok"):
-        pending.unlink(missing_ok=True)
+        fs.remove(pending)
         return {"failed": True, "msg": info.get("msg", "burn-in failed to start")}
-    if not (mdir / out).exists():
+    if not fs.stat(out)["exists"]:
         # the pid lets `--reuse` stop waiting if the burn-in dies without a result
-        pending.write_text(f"{info.get('pid', 0)}\n")
+        fs.write(pending, f"{info.get('pid', 0)}\n".encode())
     return {"changed": True, "pid": info.get("pid"), "gpus": gpus, "out": out}
+
+
+def _marker_pid(data: bytes) -> int:
+    try:
+        return int(data.split()[0])
+    except (ValueError, IndexError):
+        return 0
 
 
 def _pid_alive(pidfile: Path) -> bool:

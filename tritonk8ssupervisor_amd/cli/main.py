@@ -223,10 +223,17 @@ def cmd_playbook(args) -> int:
     return 0 if res.ok else 2
 
 
+def _backend_flags(p: argparse.ArgumentParser) -> None:
+    """--backend/--inventory also after the subcommand (``./setup.sh --backend baremetal ...``)."""
+    p.add_argument("--backend", default=argparse.SUPPRESS, help="local (default), baremetal or triton")
+    p.add_argument("--inventory", default=argparse.SUPPRESS, help="baremetal: the SSH inventory file")
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser(prog="tk8s", description="MI355X-native cluster bring-up")
     ap.add_argument("--workdir", default=os.environ.get("TK8S_WORKDIR", os.getcwd()))
-    ap.add_argument("--backend", default=None, help="local (default) or triton")
+    ap.add_argument("--backend", default=None, help="local (default), baremetal (ssh inventory) or triton")
+    ap.add_argument("--inventory", default=None, help="baremetal: the SSH inventory file (TK8S_INVENTORY)")
     sub = ap.add_subparsers(dest="cmd", required=True)
 
     s = sub.add_parser("setup", help="create the cluster (./setup.sh)")
@@ -256,6 +263,7 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--rccl-timeout", type=float, default=None, help="bound on the RCCL Job (default: --timeout)")
     s.add_argument("--json", action="store_true")
     s.add_argument("-v", "--verbose", action="store_true")
+    _backend_flags(s)
     s.set_defaults(fn=cmd_setup)
 
     sc = sub.add_parser("scale", help="change the number of workers of the running cluster (1-9)")
@@ -264,10 +272,12 @@ def build_parser() -> argparse.ArgumentParser:
     sc.add_argument("--rccl", choices=["on", "off"], default=None, help="re-run the RCCL all-reduce Job afterwards")
     sc.add_argument("--json", action="store_true")
     sc.add_argument("-v", "--verbose", action="store_true")
+    _backend_flags(sc)
     sc.set_defaults(fn=cmd_scale)
 
     c = sub.add_parser("clean", help="destroy machines and reset configuration (./setup.sh -c)")
     c.add_argument("--yes", action="store_true")
+    _backend_flags(c)
     c.set_defaults(fn=cmd_clean)
 
     st = sub.add_parser("status")
@@ -303,6 +313,10 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv: list[str] | None = None) -> int:
     args = build_parser().parse_args(argv)
+    if getattr(args, "inventory", None):
+        os.environ["TK8S_INVENTORY"] = str(Path(args.inventory).resolve())
+    if getattr(args, "backend", None):
+        os.environ["TK8S_BACKEND"] = args.backend  # the same backend for every later step of this run
     prof = os.environ.get("TK8S_PROFILE")
     if not prof:
         return args.fn(args)

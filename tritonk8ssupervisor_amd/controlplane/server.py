@@ -140,6 +140,25 @@ def template_hash(template: dict) -> str:
     return hashlib.sha1(json.dumps(template, sort_keys=True, separators=(",", ":")).encode()).hexdigest()[:10]
 
 
+GPU_VISIBILITY = "tk8s.amd.com/gpu-visibility"
+
+
+def _admit_gpu_visibility(kind: str, ns: str, body: dict) -> None:
+    """Admission: ``gpu-visibility: node`` lets a pod's runtime see every GPU of its node (the RCCL
+    fabric Job's ranks need it for xGMI peer-to-peer). Only kube-system Jobs may ask for it; a pod
+    cannot ask for it directly (the agent re-checks: kube-system pods owned by a Job)."""
+    if kind == "pods":
+        ann = (body.get("metadata") or {}).get("annotations") or {}
+        if ann.get(GPU_VISIBILITY) == "node":
+            raise HttpError(403, f'pods is forbidden: annotation {GPU_VISIBILITY}: node is reserved for '
+                                 'kube-system Jobs')
+    elif kind in ("jobs", "daemonsets", "deployments"):
+        ann = ((body.get("spec") or {}).get("template") or {}).get("metadata", {}).get("annotations") or {}
+        if ann.get(GPU_VISIBILITY) == "node" and (kind != "jobs" or ns != "kube-system"):
+            raise HttpError(403, f'{kind} is forbidden: annotation {GPU_VISIBILITY}: node is reserved for '
+                                 'kube-system Jobs')
+
+
 def _normalize_data(kind: str, body: dict) -> None:
     """ConfigMap data must be strings; Secret ``stringData`` folds into base64 ``data``."""
     import base64
@@ -1019,6 +1038,7 @@ class ControlPlane:
         key = _key(pid, ns, name)
         if self.store.get(kind, key) is not None:
             raise HttpError(409, f'{kind} "{name}" already exists')
+        _admit_gpu_visibility(kind, ns, body)
         if kind == "pods":
             spec = body.setdefault("spec", {})
             if not spec.get("containers"):

@@ -1,0 +1,42 @@
+"""Node runtime facts of the machine this runs on (the rocmsetup role's ``tk8s_gpu_facts``).
+
+Replaces the reference's ``docker --version | grep 1.12.6`` idempotency probe
+(ansible/roles/dockersetup/tasks/main.yml:2-4): what ROCm userspace is installed, whether the
+KFD device is usable, how many GPUs the kernel exposes (sysfs only, the GPU is never
+initialised), and whether the tk8s native validation tools are present. Runs in-process for the
+local provider and as ``python3 -S -m tritonk8ssupervisor_amd.nodefacts`` on a remote machine
+(one JSON line on stdout).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+NATIVE_TOOLS = ("tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl")
+
+
+def node_facts() -> dict:
+    from .models.hostinfo import discover
+
+    ver = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / ".info" / "version"
+    try:
+        rocm = ver.read_text().strip()
+    except OSError:
+        rocm = ""
+    inv = discover()
+    return {
+        "tk8s_rocm_version": rocm,
+        "tk8s_kfd": os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK | os.W_OK),
+        "tk8s_host_gpus": inv.count,
+        "tk8s_inventory_source": inv.source,
+        "tk8s_native_built": all((PKG / "bin" / t).exists() for t in NATIVE_TOOLS),
+        "tk8s_node_python": sys.version.split()[0],
+        "tk8s_node_kernel": os.uname().release,
+    }
+
+
+if __name__ == "__main__":
+    print(json.dumps(node_facts(), separators=(",", ":")))

@@ -33,7 +33,7 @@ from .provider.base import Machine, ProvisionError
 from .provision import Engine
 from .utils.events import EventLog
 from .utils.fsutil import atomic_write, atomic_write_json, read_json, remove_paths
-from .utils.procs import kill_pidfile, pid_alive, read_pidfile, spawn_daemon, wait_for_file_text
+from .utils.procs import kill_pidfile, pid_alive
 
 REPO = Path(__file__).resolve().parents[1]
 TEMPLATE_DIRS = ["terraform/master", "terraform/host", "ansible/roles", "manifests"]
@@ -96,98 +96,8 @@ def init_workspace(dst: str | os.PathLike, src: Path = REPO) -> Workspace:
 
 
 # ---- machine executor for the playbook engine ---------------------------------------------
-class MachineExecutor:
-    """Runs playbook commands / daemons "on" provisioned machines through the provider."""
-
-    def __init__(self, provider, machines: dict[str, Machine]):
-        self.provider = provider
-        self.machines = machines  # inventory host name -> Machine
-        sup = REPO / "tritonk8ssupervisor_amd" / "bin" / "tk8s-supervise"
-        self.supervise = str(sup) if sup.exists() else None
-
-    def _m(self, host: str) -> Machine:
-        if host not in self.machines:
-            raise ProvisionError(f"unknown machine {host}")
-        return self.machines[host]
-
-    def exec(self, host: str, cmd: str, env: dict | None = None, timeout: float = 600) -> tuple[int, str]:
-        return self.provider.exec(self._m(host), cmd, timeout=timeout, env=env)
-
-    def machine_dir(self, host: str) -> str:
-        return self._m(host).sandbox
-
-    def machine_gpus(self, host: str) -> list[int]:
-        return list(self._m(host).gpus)
-
-    def _paths(self, host: str, name: str) -> tuple[Path, Path]:
-        sb = Path(self._m(host).sandbox)
-        return sb / "run" / f"{name}.pid", sb / "logs" / f"{name}.log"
-
-    def daemon_status(self, host: str, name: str) -> dict:
-        pidfile, _ = self._paths(host, name)
-        info = read_pidfile(pidfile)
-        if not info:
-            return {"running": False}
-        return {"running": pid_alive(int(info["pid"])), "pid": info["pid"]}
-
-    def start_daemon(self, host: str, name: str, argv: list[str], env: dict, restart: str,
-                     wait_for_log: str | None, timeout: float) -> dict:
-        m = self._m(host)
-        pidfile, log = self._paths(host, name)
-        full_env = dict(os.environ)
-        full_env.update(getattr(self.provider, "machine_env", lambda _m: {})(m))
-        full_env.update(env)
-        log.parent.mkdir(parents=True, exist_ok=True)
-        offset = log.stat().st_size if log.exists() else 0
-        if self.supervise and restart != "no":
-            cmd = [self.supervise, "--pidfile", str(pidfile), "--log", str(log), "--restart", restart, "--", *argv]
-            p = spawn_daemon(cmd, env=full_env, cwd=m.sandbox)
-            deadline = time.monotonic() + 5
-            while not pidfile.exists() and time.monotonic() < deadline and p.poll() is None:
-                time.sleep(0.001)
-        else:
-            p = spawn_daemon(argv, env=full_env, cwd=m.sandbox, log_path=str(log), pidfile=str(pidfile))
-        info = {"ok": True, "pid": p.pid, "log": str(log)}
-        if wait_for_log:
-            t = time.monotonic()
-            deadline = t + timeout
-            while time.monotonic() < deadline:
-                try:
-                    with open(log, "rb") as f:
-                        f.seek(offset)
-                        if wait_for_log.encode() in f.read():
-                            info["wait_seconds"] = round(time.monotonic() - t, 6)
-                            return info
-                except OSError:
-                    pass
-                if p.poll() is not None:
-                    break
-                time.sleep(0.002)
-            tail = log.read_text(errors="replace")[-600:] if log.exists() else ""
-            return {"ok": False, "msg": f"{name} on {host} did not log {wait_for_log!r} within {timeout}s: {tail}"}
-        return info
-
-    def wait_log(self, host: str, name: str, text: str, timeout: float) -> dict:
-        """A daemon that is already running: wait until its log has the ready line."""
-        _, log = self._paths(host, name)
-        t = time.monotonic()
-        deadline = t + timeout
-        while time.monotonic() < deadline:
-            try:
-                with open(log, "rb") as f:
-                    if text.encode() in f.read():
-                        return {"ok": True, "wait_seconds": round(time.monotonic() - t, 6)}
-            except OSError:
-                pass
-            if not self.daemon_status(host, name).get("running"):
-                break
-            time.sleep(0.002)
-        tail = log.read_text(errors="replace")[-600:] if log.exists() else ""
-        return {"ok": False, "msg": f"{name} on {host} did not log {text!r} within {timeout}s: {tail}"}
-
-    def stop_daemon(self, host: str, name: str) -> bool:
-        pidfile, _ = self._paths(host, name)
-        return kill_pidfile(pidfile)
+# executor.py: LocalExecutor for colocated sandboxes, RemoteExecutor (ssh) for everything else.
+from .executor import MachineExecutor  # noqa: E402,F401 - re-exported (./tk8s ansible-playbook)
 
 
 def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, Machine], *, node_grace: float = 5.0,
@@ -234,8 +144,22 @@ def validation_pod_command(command: list[str], result: str = "$(TK8S_MACHINE_DIR
 
     reuse = BIN / "tk8s-reuse"
     if not os.environ.get("TK8S_FAKE_GPUS") and reuse.exists():
-        return [str(reuse), result, "--", *command]
-    return [*command, "--reuse", result]
+        return pod_portable([str(reuse), result, "--", *command])
+    return pod_portable([*command, "--reuse", result])
+
+
+def pod_portable(argv: list[str]) -> list[str]:
+    """A pod command in terms of the NODE's tk8s install: the agent expands $(TK8S_HOME) and
+    $(TK8S_PYTHON) (Kubernetes $(VAR) syntax) to its own install root and interpreter, so one
+    DaemonSet/Job spec runs on colocated sandboxes and on remote machines alike."""
+    out = []
+    for a in argv:
+        a = str(a)
+        if a == sys.executable:
+            out.append("$(TK8S_PYTHON)")
+        else:
+            out.append(a.replace(str(REPO), "$(TK8S_HOME)"))
+    return out
 
 
 # ---- setup ---------------------------------------------------------------------------------
@@ -322,11 +246,13 @@ class Setup:
         """Boot hook: a GPU machine starts its GPU burn-in the moment it exists (like a node
         image's boot-time GPU health check), overlapping the other machines' creation and play 1.
         rocmsetup's burn-in task then finds it running and does nothing."""
-        if self.cfg is not None and m.name == self.cfg.RANCHER_MASTER_HOSTNAME and hasattr(self.provider, "machine_env"):
+        if not self.provider.colocated:  # remote machines: the playbook does everything, over ssh
+            return
+        if self.cfg is not None and m.name == self.cfg.RANCHER_MASTER_HOSTNAME:
             self._boot_controlplane(m)
-        elif self.cfg is not None and hasattr(self.provider, "machine_env"):
+        elif self.cfg is not None:
             self._boot_agent(m)
-        if not (self.validate and m.gpus and hasattr(self.provider, "machine_env")):
+        if not (self.validate and m.gpus):
             return
         if self.host_burnin is not None and self.host_burnin.register(m.name, m.sandbox, list(m.gpus)):
             self.events.emit("gpu_burnin_shared_pending", name=m.name, gpus=list(m.gpus))
@@ -413,7 +339,8 @@ class Setup:
         from . import earlyburn
 
         early = earlyburn.take()  # started by cli/__main__.py before any import (earlyburn.py)
-        if not (self.validate and hasattr(self.provider, "predict_gpus")) or os.environ.get("TK8S_HOST_BURNIN", "1") == "0":
+        if (not (self.validate and self.provider.colocated and hasattr(self.provider, "predict_gpus"))
+                or os.environ.get("TK8S_HOST_BURNIN", "1") == "0"):
             if early is not None:
                 early.kill()
             return
@@ -560,12 +487,12 @@ class Setup:
         k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
         job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
         if os.environ.get("TK8S_FAKE_GPUS"):
-            cmd = [sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", "$(JOB_COMPLETION_INDEX)",
+            cmd = ["$(TK8S_PYTHON)", "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", "$(JOB_COMPLETION_INDEX)",
                    "--nranks", str(g), "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
         else:
             from .ops import BIN
 
-            cmd = [str(BIN / "tk8s-rccl"), "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "$(TK8S_GPU_DEVICE)",
+            cmd = [pod_portable([str(BIN / "tk8s-rccl")])[0], "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "$(TK8S_GPU_DEVICE)",
                    "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
                    "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
         prof_dir = None

@@ -15,7 +15,6 @@ from __future__ import annotations
 import base64
 import json
 import os
-import re
 import shlex
 import socket
 import subprocess
@@ -134,71 +133,71 @@ def m_uri(args, *, check, **_):
 
 
 # ---- files ----------------------------------------------------------------------------------
-def _path(p: str, ctx, target, local) -> Path:
-    pp = Path(os.path.expanduser(str(p)))
-    if pp.is_absolute():
-        return pp
+def _fs(ctx, target, local):
+    """Where a file task acts: the controller (local_action / delegate_to localhost / no
+    machines; relative to the playbook dir) or the target machine through its executor (relative
+    to the machine's work dir; over ssh for remote machines)."""
     if local or ctx.executor is None:
-        return ctx.dir / pp
-    return Path(ctx.executor.machine_dir(target.name)) / pp
+        from .executor import LocalFS
+
+        return LocalFS(ctx.dir)
+    return ctx.executor.fs(target.name)
+
+
+def _path(p: str, ctx, target, local) -> Path:
+    """Controller-side path (the task runs locally)."""
+    from .executor import LocalFS
+
+    return LocalFS(ctx.dir).path(p)
 
 
 def m_slurp(args, *, ctx, target, local, check, **_):
-    p = _path(args.get("src") or args.get("path"), ctx, target, local)
-    if check and not p.exists():  # produced by a task that check mode did not run
-        return {"skipped": True, "changed": False, "msg": f"check mode: {p} does not exist yet"}
-    data = p.read_bytes()
-    return {"content": base64.b64encode(data).decode(), "encoding": "base64", "source": str(p), "changed": False}
+    fs = _fs(ctx, target, local)
+    src = args.get("src") or args.get("path")
+    data = fs.read(src)
+    if data is None:
+        if check:  # produced by a task that check mode did not run
+            return {"skipped": True, "changed": False, "msg": f"check mode: {src} does not exist yet"}
+        return {"failed": True, "msg": f"file not found: {fs.path(src)}"}
+    return {"content": base64.b64encode(data).decode(), "encoding": "base64", "source": str(fs.path(src)), "changed": False}
 
 
 def m_copy(args, *, ctx, target, local, check, **_):
-    dest = _path(args["dest"], ctx, target, local)
+    fs = _fs(ctx, target, local)
     if "content" in args:
         data = str(args["content"]).encode()
     else:
         data = _path(args["src"], ctx, target, True).read_bytes()
-    old = dest.read_bytes() if dest.exists() else None
-    changed = old != data
-    if changed and not check:
-        from .utils.fsutil import atomic_write
-
-        atomic_write(dest, data)
-        if "mode" in args:
-            os.chmod(dest, int(str(args["mode"]), 8))
-    return {"changed": changed, "dest": str(dest)}
+    mode = int(str(args["mode"]), 8) if "mode" in args else None
+    changed = fs.write(args["dest"], data, mode=mode, check=check)
+    return {"changed": changed, "dest": str(fs.path(args["dest"]))}
 
 
 def m_file(args, *, ctx, target, local, check, **_):
-    p = _path(args.get("path") or args.get("dest"), ctx, target, local)
+    fs = _fs(ctx, target, local)
+    p = args.get("path") or args.get("dest")
     state = args.get("state", "file")
+    st = fs.stat(p)
     changed = False
     if state == "directory":
-        changed = not p.is_dir()
+        changed = not (st["exists"] and st.get("isdir"))
         if changed and not check:
-            p.mkdir(parents=True, exist_ok=True)
+            fs.mkdir(p)
     elif state == "absent":
-        changed = p.exists()
+        changed = st["exists"]
         if changed and not check:
-            from .utils.fsutil import remove_paths
-
-            remove_paths([p])
+            fs.remove(p)
     elif state == "touch":
         changed = True
         if not check:
-            p.parent.mkdir(parents=True, exist_ok=True)
-            p.touch()
-    elif not p.exists():
-        return {"failed": True, "msg": f"file {p} does not exist"}
-    return {"changed": changed, "path": str(p), "state": state}
+            fs.touch(p)
+    elif not st["exists"]:
+        return {"failed": True, "msg": f"file {fs.path(p)} does not exist"}
+    return {"changed": changed, "path": str(fs.path(p)), "state": state}
 
 
 def m_stat(args, *, ctx, target, local, **_):
-    p = _path(args["path"], ctx, target, local)
-    if not p.exists():
-        return {"stat": {"exists": False}, "changed": False}
-    st = p.stat()
-    return {"stat": {"exists": True, "isdir": p.is_dir(), "size": st.st_size, "mtime": st.st_mtime, "path": str(p)},
-            "changed": False}
+    return {"stat": _fs(ctx, target, local).stat(args["path"]), "changed": False}
 
 
 def m_include_vars(args, *, ctx, target, local, **_):
@@ -261,14 +260,12 @@ def m_wait_for(args, *, ctx, target, local, check, **_):
             if up == (state in ("started", "present")):
                 return {"changed": False, "elapsed": round(timeout - (deadline - time.monotonic()), 3)}
         elif "path" in args:
-            p = _path(args["path"], ctx, target, local)
+            fs = _fs(ctx, target, local)
             if state == "absent":
-                if not p.exists():
+                if not fs.stat(args["path"])["exists"]:
                     return {"changed": False}
-            elif p.exists():
-                rx = args.get("search_regex")
-                if not rx or re.search(rx, p.read_text(errors="replace")):
-                    return {"changed": False}
+            elif fs.search(args["path"], args.get("search_regex")):
+                return {"changed": False}
         else:
             return {"changed": False}
         time.sleep(0.02)
@@ -341,24 +338,19 @@ def m_tk8s_burnin(args, *, ctx, target, local, env, check, **_):
 
 
 def m_tk8s_gpu_facts(args, *, ctx, target, local, **_):
-    from .models.hostinfo import discover
-
-    facts = {}
-    ver = Path("/opt/rocm/.info/version")
-    facts["tk8s_rocm_version"] = ver.read_text().strip() if ver.exists() else ""
-    facts["tk8s_kfd"] = os.path.exists("/dev/kfd")
-    inv = discover()
-    facts["tk8s_host_gpus"] = inv.count
-    facts["tk8s_inventory_source"] = inv.source
-    facts["tk8s_machine_gpus"] = []
-    if ctx.executor is not None and not local:
-        facts["tk8s_machine_gpus"] = ctx.executor.machine_gpus(target.name)
+    """Node runtime facts (nodefacts.py) of the target machine -- gathered ON it (over ssh for a
+    remote machine) -- plus the GPU slice the provider gave it."""
     from .models.hostinfo import compose_visible_devices
 
-    facts["tk8s_machine_visible_devices"] = compose_visible_devices(facts["tk8s_machine_gpus"])["ROCR_VISIBLE_DEVICES"]
-    from .ops import BIN
+    if ctx.executor is not None and not local:
+        facts = dict(ctx.executor.facts(target.name))
+        facts["tk8s_machine_gpus"] = ctx.executor.machine_gpus(target.name)
+    else:
+        from .nodefacts import node_facts
 
-    facts["tk8s_native_built"] = all((BIN / t).exists() for t in ("tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl"))
+        facts = dict(node_facts())
+        facts["tk8s_machine_gpus"] = []
+    facts["tk8s_machine_visible_devices"] = compose_visible_devices(facts["tk8s_machine_gpus"])["ROCR_VISIBLE_DEVICES"]
     return {"ansible_facts": facts, "changed": False}
 
 

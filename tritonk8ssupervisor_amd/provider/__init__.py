@@ -9,8 +9,9 @@ same four things behind one interface:
 * ``packages()``  — machine shapes with ids (``triton packages -oname,id | grep -kvm-``)
 * machine lifecycle: ``create_machine``/``exec``/``delete_machine`` (``triton_machine``)
 
-``local`` (default) provisions worker sandboxes on this MI355X host; ``triton`` shells out to
-the real CLI for parity with the reference (untestable offline).
+``local`` (default) provisions worker sandboxes on this MI355X host; ``baremetal`` claims slices
+of real hosts from an SSH inventory and configures them over SSH; ``triton`` shells out to the
+real CLI for parity with the reference (untestable offline) and configures its VMs over SSH.
 """
 from __future__ import annotations
 
@@ -22,8 +23,12 @@ def get_provider(name: str, state_dir, **kw) -> "Provider":
         from .local import LocalProvider
 
         return LocalProvider(state_dir, **kw)
+    if name == "baremetal":
+        from .baremetal import BareMetalProvider
+
+        return BareMetalProvider(state_dir, **kw)
     if name == "triton":
         from .triton import TritonProvider
 
         return TritonProvider(state_dir, **kw)
-    raise ValueError(f"unknown backend {name!r} (expected 'local' or 'triton')")
+    raise ValueError(f"unknown backend {name!r} (expected 'local', 'baremetal' or 'triton')")

@@ -34,8 +34,10 @@ class Machine:
     gpus: list[int] = field(default_factory=list)  # host GPU ordinals owned by this machine
     image: str = ""
     tags: dict = field(default_factory=dict)
-    sandbox: str = ""
+    sandbox: str = ""      # the machine's work dir (on the machine: remote path for remote providers)
     state: str = "running"
+    home: str = ""         # tk8s install root on the machine ("" = the controller's own checkout)
+    python: str = ""       # interpreter on the machine ("" = the controller's sys.executable)
 
     def to_dict(self) -> dict:
         return asdict(self)
@@ -53,6 +55,10 @@ class Provider(abc.ABC):
     name = "abstract"
     default_network = ""
     default_package = ""
+    # True when machines are sandboxes of the controller host (local provider): the orchestrator
+    # may then spawn their daemons directly and run its boot hooks; otherwise every action goes
+    # through exec() (ssh) -- executor.RemoteExecutor.
+    colocated = False
 
     @abc.abstractmethod
     def env(self) -> dict[str, str]:
@@ -76,8 +82,10 @@ class Provider(abc.ABC):
         ...
 
     @abc.abstractmethod
-    def exec(self, machine: Machine, command: str, timeout: float = 300, env: dict | None = None) -> tuple[int, str]:
-        """Run a shell command "on" the machine (remote-exec); returns (rc, output)."""
+    def exec(self, machine: Machine, command: str, timeout: float = 300, env: dict | None = None,
+             stdin: bytes | None = None) -> tuple[int, str]:
+        """Run a shell command on the machine (remote-exec), in its work dir with its machine
+        environment (TK8S_MACHINE*) plus ``env``; returns (rc, stdout+stderr)."""
 
     @abc.abstractmethod
     def delete_machine(self, machine: Machine) -> None:

@@ -66,6 +66,7 @@ class LocalProvider(Provider):
     name = "local"
     default_network = "local-public"
     default_package = "mi355x-1gpu"
+    colocated = True
 
     def __init__(self, state_dir: str | os.PathLike, key_dir: str | os.PathLike | None = None):
         self.state_dir = Path(state_dir).resolve()
@@ -256,16 +257,17 @@ class LocalProvider(Provider):
             "TK8S_MACHINE_PACKAGE": m.package,
         }
 
-    def exec(self, machine: Machine, command: str, timeout: float = 300, env: dict | None = None) -> tuple[int, str]:
+    def exec(self, machine: Machine, command: str, timeout: float = 300, env: dict | None = None,
+             stdin: bytes | None = None) -> tuple[int, str]:
         e = dict(os.environ)
         e.update(self.machine_env(machine))
         e.update(env or {})
         try:
             r = subprocess.run(["bash", "-c", command], cwd=machine.sandbox, env=e, capture_output=True,
-                               text=True, timeout=timeout)
+                               input=stdin if stdin is not None else b"", timeout=timeout)
         except subprocess.TimeoutExpired as ex:
             return 124, f"timeout after {timeout}s: {ex}"
-        return r.returncode, (r.stdout or "") + (r.stderr or "")
+        return r.returncode, (r.stdout or b"").decode(errors="replace") + (r.stderr or b"").decode(errors="replace")
 
     def delete_machine(self, machine: Machine) -> None:
         sandbox = Path(machine.sandbox or self.machines_dir / machine.name)

@@ -6,7 +6,12 @@ Mirrors setup.sh exactly where the reference talks to Triton:
   * packages()  : `triton packages -oname,id | grep -- -kvm- | sort` (setup.sh:259, 541)
   * find_key()  : MD5 fingerprint scan of ~/.ssh (setup.sh:215-230)
   * machines    : `triton instance create/delete` (docs/manual-setup.md:10-23)
-Not exercised offline (no CLI, no network); the local provider is the tested backend.
+  * exec        : ssh as root with the discovered key (SDC_KEY) and a per-cluster known-hosts
+                  file -- the reference's `ssh -o StrictHostKeyChecking=no root@ip` (setup.sh:72)
+                  used no key and trusted any host key (utils/ssh.py); machines are configured
+                  remotely by executor.RemoteExecutor, exactly like the baremetal backend.
+The CLI half is not exercised offline (no CLI, no network); the SSH half is shared with the
+baremetal provider, which the fake-ssh bring-up test covers.
 """
 from __future__ import annotations
 
@@ -15,6 +20,8 @@ import os
 import shutil
 import subprocess
 from pathlib import Path
+
+from ..utils import ssh
 
 from .base import Machine, Network, Package, Provider, ProvisionError
 
@@ -42,8 +49,15 @@ class TritonProvider(Provider):
     default_network = "Joyent-SDC-Public"
     default_package = "k4-highcpu-kvm-7.75G"
 
+    colocated = False
+
     def __init__(self, state_dir, **_):
         self.state_dir = Path(state_dir)
+
+    def target(self, ip: str) -> ssh.SSHTarget:
+        ctl = ssh.control_dir_for(self.state_dir)
+        return ssh.SSHTarget(host=ip, user="root", key=os.environ.get("SDC_KEY", ""),
+                             known_hosts=str(self.state_dir / "known_hosts"), control_dir=str(ctl))
 
     def env(self) -> dict[str, str]:
         out = {}
@@ -83,16 +97,31 @@ class TritonProvider(Provider):
             argv += ["-t", f"{k}={v}"]
         argv += [image or "ubuntu-certified-16.04", package]
         d = json.loads(_run(argv, timeout=1800).splitlines()[-1])
-        return Machine(name=name, id=d.get("id", ""), package=package, networks=list(networks),
-                       primaryip=d.get("primaryIp", ""), ips=d.get("ips", []), image=image, tags=dict(tags or {}))
+        ip = d.get("primaryIp", "")
+        # The VM's node runtime: the tk8s distribution (tar over ssh, once) and the machine's work
+        # dir, like the baremetal backend. ssh retries while the VM is still booting.
+        t = self.target(ip)
+        rc, home, out = ssh.push_dist(t, Path(__file__).resolve().parents[2])
+        if rc != 0:
+            raise ProvisionError(f"{name}: installing tk8s over ssh failed (rc={rc}): {out.strip()[-400:]}")
+        rc, out = ssh.run(t, "mkdir -p tk8s/machine && cd tk8s/machine && mkdir -p run logs pods etc && pwd "
+                             "&& command -v python3")
+        if rc != 0:
+            raise ProvisionError(f"{name}: preparing the machine failed: {out.strip()[-400:]}")
+        sandbox, py = out.strip().splitlines()[-2:]
+        return Machine(name=name, id=d.get("id", ""), package=package, networks=list(networks), primaryip=ip,
+                       ips=d.get("ips", []), image=image, tags=dict(tags or {}), sandbox=sandbox, home=home, python=py)
 
-    def exec(self, machine, command, timeout=300, env=None):
-        argv = ["ssh", "-o", "StrictHostKeyChecking=no", f"root@{machine.primaryip}", command]
-        try:
-            r = subprocess.run(argv, capture_output=True, text=True, timeout=timeout, env={**os.environ, **(env or {})})
-        except subprocess.TimeoutExpired:
-            return 124, "timeout"
-        return r.returncode, r.stdout + r.stderr
+    def machine_env(self, m: Machine) -> dict[str, str]:
+        return {"TK8S_MACHINE": m.name, "TK8S_MACHINE_DIR": m.sandbox, "TK8S_MACHINE_IP": m.primaryip,
+                "TK8S_MACHINE_GPUS": ",".join(map(str, m.gpus)), "TK8S_MACHINE_PACKAGE": m.package,
+                "TK8S_HOME": m.home}
+
+    def exec(self, machine, command, timeout=300, env=None, stdin=None):
+        script = ssh.remote_script(command, cwd=machine.sandbox or None, env={**self.machine_env(machine), **(env or {})})
+        return ssh.run(self.target(machine.primaryip), script, timeout=timeout, stdin=stdin, retries_on_connect=5)
 
     def delete_machine(self, machine) -> None:
         _run(["triton", "instance", "delete", "--wait", machine.id or machine.name], timeout=1800)
+        subprocess.run(["ssh-keygen", "-R", machine.primaryip, "-f", str(self.state_dir / "known_hosts")],
+                       capture_output=True, timeout=30)  # the reference's `ssh-keygen -R` (setup.sh:504-508)
