@@ -589,3 +589,64 @@ def test_degraded_xgmi_link_marks_its_nodes_not_ready(ws):
     d = subprocess.run(["./kubectl", "describe", "node", "kubenode2"], cwd=ws, env=_env(), capture_output=True,
                        text=True).stdout
     assert "XGMILinkDegraded" in d and "0->1" in d
+
+
+def _kube(ws):
+    from tritonk8ssupervisor_amd.controlplane.client import client_from_kubeconfig
+
+    return client_from_kubeconfig(json.loads((ws / ".tk8s" / "kubeconfig.json").read_text()))
+
+
+def _wait_pod(k, ns, name, timeout=30):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        p = k.get(k.k8s(f"/api/v1/namespaces/{ns}/pods/{name}"))
+        if p.get("status", {}).get("phase") in ("Succeeded", "Failed"):
+            return p
+        time.sleep(0.05)
+    raise AssertionError(f"pod {ns}/{name} did not finish: {p.get('status')}")
+
+
+def test_pods_are_isolated_from_the_agent(ws):
+    """P4: a pod's env is its spec + downward API + the device plugin's, not the agent's; node-wide
+    GPU visibility is refused outside the cluster's own kube-system Jobs; CPU pods get their own
+    PID namespace when the kernel allows it (and say so either way)."""
+    from tritonk8ssupervisor_amd.controlplane.client import ApiError
+
+    _summary(_setup(ws, "--nodes", "1", "--rccl", "off", env=_env(TK8S_FAULTS="agent.never@nowhere")))
+    k = _kube(ws)
+    script = "env; echo PIDNS_PID=$$"
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "envdump", "namespace": "default"},
+           "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "command": ["sh", "-c", script],
+                                                              "env": [{"name": "MINE", "value": "x-$(POD_NAME)"}]}]}}
+    k.post(k.k8s("/api/v1/namespaces/default/pods"), pod)
+    p = _wait_pod(k, "default", "envdump")
+    assert p["status"]["phase"] == "Succeeded"
+    log = Path(p["metadata"]["annotations"]["tk8s.amd.com/log-path"]).read_text()
+    env = dict(line.split("=", 1) for line in log.splitlines() if "=" in line)
+    assert env["MINE"] == "x-envdump" and env["POD_NAME"] == "envdump" and env["NODE_NAME"] == "kubenode1"
+    for leaked in ("PYTHONPATH", "TK8S_FAULTS", "TK8S_MACHINE", "TK8S_MACHINE_GPUS", "TK8S_PYTHON_PATH"):
+        assert leaked not in env, leaked
+    assert "TK8S_FAKE_GPUS" in env  # the fake-GPU switch of the test tier passes (POD_ENV_KEEP_PREFIXES)
+    how = p["metadata"]["annotations"]["tk8s.amd.com/isolation"]
+    assert how == "user,pid,mount" or how.startswith("none: ")
+    if how == "user,pid,mount":
+        assert env["PIDNS_PID"] in ("1", "2")  # init of its own PID namespace (or its first child)
+    # node-wide GPU visibility: refused at admission for a user pod / a user Job ...
+    vis = {"tk8s.amd.com/gpu-visibility": "node"}
+    bad = json.loads(json.dumps(pod))
+    bad["metadata"].update(name="peek", annotations=vis)
+    with pytest.raises(ApiError) as e:
+        k.post(k.k8s("/api/v1/namespaces/default/pods"), bad)
+    assert e.value.status == 403
+    job = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "peekjob", "namespace": "default"},
+           "spec": {"template": {"metadata": {"annotations": vis}, "spec": pod["spec"]}}}
+    with pytest.raises(ApiError) as e:
+        k.post(k.k8s("/apis/batch/v1/namespaces/default/jobs"), job)
+    assert e.value.status == 403
+    # ... and by the agent for a kube-system pod that no Job owns
+    from tritonk8ssupervisor_amd.agent.agent import node_visibility_allowed
+
+    assert not node_visibility_allowed({"metadata": {"namespace": "kube-system"}})
+    assert node_visibility_allowed({"metadata": {"namespace": "kube-system", "ownerReferences": [{"kind": "Job"}]}})
+    assert not node_visibility_allowed({"metadata": {"namespace": "default", "ownerReferences": [{"kind": "Job"}]}})

@@ -247,3 +247,21 @@ def test_pmc_counter_pass_limits():
     for bad in ([f"SQ_C{i}" for i in range(9)], ["FETCH_SIZE", "WRITE_SIZE"], ["GRBM_A", "GRBM_B", "GRBM_C"], ["XYZ_A"]):
         with pytest.raises(SetupError):
             check_pmc_counters(bad)
+
+
+def test_pod_in_its_own_pid_namespace(tmp_path, monkeypatch):
+    """P4: with unprivileged user namespaces, a CPU pod runs as init of its own PID namespace with
+    its own /proc (it cannot see or signal the node's processes)."""
+    from tritonk8ssupervisor_amd.agent import runtime
+
+    monkeypatch.setattr(runtime, "_ISOLATION", None)
+    avail, how = runtime.namespace_isolation("", str(tmp_path))
+    if not avail:
+        pytest.skip(f"no unprivileged namespaces here: {how}")
+    rt, events, wait_for = _runtime(tmp_path)
+    pp = _pod(tmp_path, "iso", ["sh", "-c", "echo pid=$$; ls /proc | grep -c '^[0-9]'"], "Never")
+    pp.isolate = True
+    rt.start(pp)
+    wait_for(lambda ev: any(p == "Succeeded" for _, p, _ in ev))
+    out = (tmp_path / "pods" / "iso" / "log").read_text().split()
+    assert out[0] in ("pid=1", "pid=2") and int(out[1]) <= 4  # only the pod's own processes are visible

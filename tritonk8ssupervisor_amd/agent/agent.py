@@ -32,7 +32,7 @@ from ..utils.faults import fault
 from ..utils.k8senv import field_path, service_env
 from ..utils.trace import trace
 from .deviceplugin import DevicePlugin
-from .runtime import PodProc, PodRuntime, install_sigterm
+from .runtime import PodProc, PodRuntime, install_sigterm, namespace_isolation
 
 GPU = "amd.com/gpu"
 ALL_GPUS = "tk8s.amd.com/all-gpus"
@@ -355,11 +355,20 @@ class Agent:
                 "reason": "NoCommand", "message": f"container has no command and image {c.get('image')!r} is not "
                                                   "in the tk8s app catalogue (tritonk8ssupervisor_amd/apps)"}, None)
             return
+        # GPU pods stay in the host PID namespace: HIP/RCCL inter-process sharing (dmabuf handles
+        # passed by pid, RCCL's pid-keyed shared memory) needs the peers' real pids.
+        gpu_pod = bool(ids) or all_gpus or visibility == "node"
+        avail, how = namespace_isolation(str(Path(TK8S_HOME) / "tritonk8ssupervisor_amd" / "__init__.py"),
+                                         str(self.sandbox / "pods"))
+        isolation = "none: GPU pod (shares the host PID namespace for HIP/RCCL IPC)" if gpu_pod else how if avail \
+            else f"none: {how}"
         pp = PodProc(key=key, uid=md.get("uid", ""), dir=pp_dir, argv=argv, env=env,
-                     restart_policy=spec.get("restartPolicy", "Always"), gpu_ids=ids, ip=pod_ip)
+                     restart_policy=spec.get("restartPolicy", "Always"), gpu_ids=ids, ip=pod_ip,
+                     isolate=avail and not gpu_pod)
         self._pods_meta[key] = {"name": md["name"], "namespace": md["namespace"],
                                 "validation": md.get("labels", {}).get(VALIDATION_LABEL) == "true",
-                                "annotations": {**alloc["annotations"], "tk8s.amd.com/log-path": str(pp_dir / "log")}}
+                                "annotations": {**alloc["annotations"], "tk8s.amd.com/log-path": str(pp_dir / "log"),
+                                                "tk8s.amd.com/isolation": isolation}}
         self.runtime.start(pp)
 
     # ---- container env (kubelet semantics) ------------------------------------------------

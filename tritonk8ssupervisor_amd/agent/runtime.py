@@ -64,6 +64,7 @@ class PodProc:
     restart_policy: str
     gpu_ids: list[str] = field(default_factory=list)
     ip: str = ""                  # the pod's own loopback IP (from the node's podCIDR)
+    isolate: bool = False         # own user/pid/mount namespaces (see namespace_isolation())
     proc: subprocess.Popen | None = None
     restarts: int = 0
     started: float = 0.0
@@ -90,9 +91,12 @@ class PodRuntime:
         env = dict(pp.env)
         if self.tool_dirs:
             env["PATH"] = os.pathsep.join(self.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
+        argv = list(pp.argv)
+        if pp.isolate and namespace_isolation()[0]:
+            argv = [*UNSHARE, "--", *argv]
         log = open(pp.dir / "log", "ab", buffering=0)
         try:
-            p = subprocess.Popen(pp.argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
+            p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
                                  stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
         finally:
             log.close()
@@ -152,6 +156,40 @@ class PodRuntime:
     def running(self) -> dict[str, PodProc]:
         with self.lock:
             return dict(self.pods)
+
+
+# A pod's own namespaces, when the kernel lets an unprivileged user create them: a user namespace
+# mapping the agent's uid to itself, a PID namespace (the pod's processes see only each other;
+# --kill-child: the pod dies with its init) and a mount namespace with its own /proc. The network
+# namespace stays the host's: pods bind their own loopback IPs and Services/DNS answer there.
+UNSHARE = ["unshare", "--user", "--map-current-user", "--pid", "--fork", "--mount-proc", "--kill-child"]
+_ISOLATION: tuple[bool, str] | None = None
+
+
+def namespace_isolation(readable: str = "", writable: str = "") -> tuple[bool, str]:
+    """(available, description), probed once: ``unshare`` with the flags above must start, and
+    inside it the tk8s install (``readable``) and the pods dir (``writable``) must still be
+    usable -- a user namespace drops capabilities such as root's DAC override, which a node
+    running as root may rely on to reach them."""
+    global _ISOLATION
+    if _ISOLATION is None:
+        if os.environ.get("TK8S_POD_ISOLATION", "auto") == "none":
+            _ISOLATION = (False, "disabled (TK8S_POD_ISOLATION=none)")
+        else:
+            check = "true"
+            if readable:
+                check += f" && test -r '{readable}'"
+            if writable:
+                check += f" && test -w '{writable}'"
+            try:
+                r = subprocess.run([*UNSHARE, "--", "sh", "-c", check], capture_output=True, text=True, timeout=10)
+                ok = r.returncode == 0
+                why = (r.stderr or "").strip().splitlines()[-1:] or [
+                    f"the tk8s install or the pods dir is not accessible inside a user namespace (rc={r.returncode})"]
+                _ISOLATION = (ok, "user,pid,mount" if ok else f"unavailable: {why[0]}")
+            except (OSError, subprocess.TimeoutExpired) as e:
+                _ISOLATION = (False, f"unavailable: {e}")
+    return _ISOLATION
 
 
 def _sigterm_to_exit(*_):
