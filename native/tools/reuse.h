@@ -44,6 +44,9 @@ inline bool burnin_alive(const std::string& pending) {
 
 // Print a finished (or still running) burn-in's result. Returns -1 when there is none (no
 // burn-in, or it died without writing a result): the caller then probes itself.
+// A result is single-use: it is renamed to FILE.consumed before it is read (rename is atomic, so
+// of two readers exactly one gets it), and a re-created validation pod -- agent restart,
+// --resume, a re-join -- finds nothing and probes the GPU again instead of re-reporting an old pass.
 inline int reuse(const std::string& file, double wait_s) {
   const auto t = std::chrono::steady_clock::now();
   auto waited_ms = [&] {
@@ -53,7 +56,9 @@ inline int reuse(const std::string& file, double wait_s) {
     if (!burnin_alive(file + ".pending") && !exists(file)) break;
     std::this_thread::sleep_for(std::chrono::microseconds(500));  // a stat + /proc read: cheap
   }
-  std::ifstream f(file);
+  const std::string taken = file + ".consumed";
+  if (std::rename(file.c_str(), taken.c_str()) != 0) return -1;
+  std::ifstream f(taken);
   if (!f) return -1;
   std::stringstream ss;
   ss << f.rdbuf();

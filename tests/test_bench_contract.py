@@ -90,3 +90,62 @@ def test_bench_real_gpu(tmp_path):
     assert "fake" not in out["data"] and out["value"] < 5.0
     v = next(iter(out["validation_last_step"].values()))
     assert float(v["hbm-write-gbps"]) > 1000.0 and float(v["md5-mbps"]) > 1000.0
+
+
+def test_bench_reports_post_ready_failures(monkeypatch, capsys, tmp_path):
+    """ADVICE r1: a step that reached Ready and then failed (the RCCL check) keeps its Ready time
+    and the JSON line reports the failure instead of the bench dying on a missing key."""
+    sys.path.insert(0, str(REPO))
+    import bench
+
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    calls = {"n": 0}
+
+    def fake_bringup(ws, n, args, env, log):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            return {"wall_seconds": 0.3, "ready_wall_seconds": 0.2, "phases": {}, "post_ready_error": "exit 2: RCCL"}
+        return {"wall_seconds": 0.3, "ready_wall_seconds": 0.25, "ready_seconds": 0.24, "phases": {"ready": 0.1},
+                "gpus_allocatable": 1, "nodes_validated": 1}
+
+    monkeypatch.setattr(bench, "one_bringup", fake_bringup)
+    monkeypatch.setattr(bench, "teardown", lambda ws, env, log: 0.01)
+    monkeypatch.setattr(bench, "make_workspace", lambda root: root)
+    monkeypatch.setattr("tritonk8ssupervisor_amd.utils.build_native.build", lambda: {})
+    assert bench.main(["--gpus", "1", "--steps", "3", "--warmup", "0", "--fake-gpus", "1"]) == 0
+    out = _json_line(capsys.readouterr().out)
+    assert out["post_ready_errors"]["count"] == 1 and "RCCL" in out["post_ready_errors"]["last"]
+    assert out["min_s"] == 0.2 and out["ready_s_inside_setup"] == 0.24
+    assert "not like-for-like" in out["vs_baseline_note"].replace("NOT", "not")
+
+
+def test_bench_kills_a_silent_hang(tmp_path):
+    """ADVICE r1: the per-step bound fires even when ./setup.sh hangs without printing."""
+    sys.path.insert(0, str(REPO))
+    import time as _t
+    import types
+
+    import bench
+
+    ws = tmp_path / "ws"
+    ws.mkdir()
+    (ws / "setup.sh").write_text("#!/bin/sh\nsleep 600\n")
+    (ws / "setup.sh").chmod(0o755)
+    args = types.SimpleNamespace(package="mi355x-1gpu", timeout=-118.0, rccl_timeout=1, no_validate=False, rccl=None)
+    t = _t.monotonic()
+    with pytest.raises(RuntimeError, match="killed"):
+        bench.one_bringup(ws, 1, args, dict(os.environ), open(os.devnull, "w"))
+    assert _t.monotonic() - t < 30
+
+
+@pytest.mark.timeout(600)
+def test_bench_torchrun_eight_ranks(tmp_path):
+    """VERDICT r1 #4: the N=8 launch shape the driver uses, rehearsed on CPU (gloo, fake GPUs)."""
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
+                        "--gpus", "8", "--steps", "1", "--warmup", "0", "--fake-gpus", "8"],
+                       cwd=REPO, env=_env(tmp_path), capture_output=True, text=True, timeout=580)
+    assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
+    out = _json_line(p.stdout)
+    _check(out, 8, 1, 0)
+    assert out["config"]["rccl"] == "on"

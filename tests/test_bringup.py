@@ -103,7 +103,7 @@ def test_setup_ready_and_clean_teardown(ws, n):
     assert len(pids) == n + 1 and all(_alive(p) for p in pids)
     # the early GPU burn-in ran on every worker and the validation pods reused its result
     for i in range(1, n + 1):
-        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
+        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json.consumed").read_text())
         assert burn["ok"] and burn["probed"] == 1
         # one host-level burn-in (the runtime starts once, before the machines exist), split per machine
         assert burn["host_burnin"] and burn["devices"][0]["host_index"] == int(items[i - 1]["status"]["devices"][0]["id"][3:])
@@ -173,8 +173,8 @@ def test_crashed_burnin_falls_back_to_probing_in_the_pod(ws):
     t = time.monotonic()
     s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=_env(TK8S_FAKE_BURNIN_CRASH="kubenode2")))
     assert s["nodes_validated"] == 2 and time.monotonic() - t < 30  # no 120 s --reuse wait
-    assert not (ws / ".tk8s" / "machines" / "kubenode2" / "run" / "gpu-burnin.json").exists()
-    assert (ws / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json").exists()
+    assert not (ws / ".tk8s" / "machines" / "kubenode2" / "run" / "gpu-burnin.json.consumed").exists()
+    assert (ws / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json.consumed").exists()
 
 
 def test_stalled_node_hits_the_bounded_timeout(ws):
@@ -427,7 +427,7 @@ def test_failed_host_burnin_falls_back_to_per_machine_probes(ws):
     s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=_env(TK8S_FAKE_PROBE_FAIL="host")))
     assert s["nodes_validated"] == 2 and s["gpus_allocatable"] == 2
     for i in (1, 2):  # no shared result; at most the machine's own burn-in (rocmsetup) ran
-        f = ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json"
+        f = ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json.consumed"
         assert not f.exists() or not json.loads(f.read_text()).get("host_burnin")
     events = (ws / ".tk8s" / "events.jsonl").read_text()
     assert "gpu_burnin_share_failed" in events and "gpu_burnin_host_done" in events
@@ -441,7 +441,7 @@ def test_two_gpu_workers_share_one_host_burnin(ws):
     seen = []
     for i in (1, 2):
         m = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "machine.json").read_text())
-        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
+        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json.consumed").read_text())
         assert burn["host_burnin"] and burn["probed"] == 2
         assert [d["host_index"] for d in burn["devices"]] == m["gpus"] and [d["device"] for d in burn["devices"]] == [0, 1]
         seen += m["gpus"]
@@ -467,7 +467,7 @@ def test_answers_file_bring_up_starts_the_burnin_before_the_cli_imports(ws):
     standby = [e for e in events if e.get("task", "").endswith("Start the node agent in standby on every host")]
     assert standby and all(v in ("ok", "skipped") for v in standby[0]["results"].values()), standby
     for i in (1, 2):
-        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json").read_text())
+        burn = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "gpu-burnin.json.consumed").read_text())
         assert burn["host_burnin"] and burn["ok"]
     # teardown stops the adopted processes too (the zygote's supervisor holds the master's pidfile)
     sup = json.loads((ws / ".tk8s" / "machines" / "kubemaster" / "run" / "controlplane.pid").read_text())["pid"]
@@ -650,3 +650,25 @@ def test_pods_are_isolated_from_the_agent(ws):
     assert not node_visibility_allowed({"metadata": {"namespace": "kube-system"}})
     assert node_visibility_allowed({"metadata": {"namespace": "kube-system", "ownerReferences": [{"kind": "Job"}]}})
     assert not node_visibility_allowed({"metadata": {"namespace": "default", "ownerReferences": [{"kind": "Job"}]}})
+
+
+def test_shared_burnin_result_is_single_use(ws):
+    """a re-created validation pod (agent restart, --resume, re-join) must probe the GPU
+    again, never re-report a burn-in result an earlier pod already consumed."""
+    _summary(_setup(ws, "--nodes", "1", "--rccl", "off"))
+    run = ws / ".tk8s" / "machines" / "kubenode1" / "run"
+    assert (run / "gpu-burnin.json.consumed").exists() and not (run / "gpu-burnin.json").exists()
+    k = _kube(ws)
+    k.delete(k.k8s("/api/v1/namespaces/kube-system/pods/amd-gpu-validation-kubenode1"))
+    deadline = time.monotonic() + 30
+    while True:  # the DaemonSet re-creates the pod; it finds no result and probes by itself
+        try:
+            p = k.get(k.k8s("/api/v1/namespaces/kube-system/pods/amd-gpu-validation-kubenode1"))
+            if p.get("status", {}).get("phase") == "Succeeded":
+                break
+        except Exception:  # noqa: BLE001 - not re-created yet
+            pass
+        assert time.monotonic() < deadline
+        time.sleep(0.05)
+    res = p["status"]["result"]
+    assert res["ok"] and not res.get("host_burnin")  # its own probe, not the shared burn-in

@@ -147,6 +147,12 @@ def test_registry_rejects_a_wrong_api_version(kubelet):
 
 
 def test_socket_dir_falls_back_when_the_path_is_too_long(tmp_path):
+    from tritonk8ssupervisor_amd.agent.dp_grpc import KubeletRegistry
+
     long = tmp_path / ("d" * 120)
-    assert socket_dir(long) != long
+    d = socket_dir(long)
+    assert d != long and socket_dir(long) == d  # the same stand-in every time: nothing piles up
     assert socket_dir(tmp_path / "dp") == (tmp_path / "dp").absolute()
+    reg = KubeletRegistry(d).start()
+    reg.stop()
+    assert not d.exists()  # the stand-in is removed with the kubelet side

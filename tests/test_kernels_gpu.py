@@ -299,7 +299,7 @@ def test_setup_with_host_burnin_on_a_real_gpu(tmp_path):
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
         s = json.loads(r.stdout.strip().splitlines()[-1])
         assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1
-        burn = json.loads((tmp_path / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json").read_text())
+        burn = json.loads((tmp_path / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json.consumed").read_text())
         assert burn["ok"] and burn["host_burnin"] and burn["devices"][0]["host_index"] == 0
         assert burn["md5"]["digest"] == burn["md5_expected"] and burn["gpuinfo"]["devices"][0]["gfx"] == "gfx950"
     finally:
@@ -449,7 +449,7 @@ def test_setup_from_an_answers_file_adopts_the_early_burnin_on_a_real_gpu(tmp_pa
         started = [e for e in events if e["event"] == "gpu_burnin_host_started"]
         assert len(started) == 1 and started[0].get("early"), started
         assert any(e["event"] == "controlplane_boot_started" and e.get("zygote") for e in events)
-        burn = json.loads((tmp_path / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json").read_text())
+        burn = json.loads((tmp_path / ".tk8s" / "machines" / "kubenode1" / "run" / "gpu-burnin.json.consumed").read_text())
         assert burn["ok"] and burn["host_burnin"] and burn["gpuinfo"]["devices"][0]["gfx"] == "gfx950"
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)

@@ -141,7 +141,7 @@ def test_baremetal_bringup_over_ssh(bm):
     # the GPU burn-in ran ON the host (its result file is in the machine's dir there)
     for i in range(1, 6):
         m = machines[f"kubenode{i}"]
-        burn = json.loads(Path(m.sandbox, "run", "gpu-burnin.json").read_text())
+        burn = json.loads(Path(m.sandbox, "run", "gpu-burnin.json.consumed").read_text())
         assert burn["ok"]
 
     # kubectl sees 5 Ready nodes with one GPU each

@@ -60,12 +60,25 @@ def numa_node(render_minor: int) -> int:
 
 
 def socket_dir(path: str | os.PathLike) -> Path:
-    """``path`` if the kubelet and plugin sockets fit in sun_path there, else a private /tmp dir."""
+    """``path`` if the kubelet and plugin sockets fit in sun_path there, else a short private dir
+    named after it (``/tmp/tk8s-dp-<uid>/<hash>``: the same one on every restart, so nothing piles
+    up; ``KubeletRegistry.stop`` removes it)."""
+    import hashlib
+
     p = Path(path).absolute()
     if len(str(p)) + 1 + max(len(ENDPOINT), len(KUBELET_SOCKET)) <= _SUN_PATH_MAX:
         p.mkdir(parents=True, exist_ok=True)
         return p
-    return Path(tempfile.mkdtemp(prefix="tk8s-dp-"))
+    base = Path(tempfile.gettempdir())
+    if len(str(base)) > 40:
+        base = Path("/tmp")
+    d = base / f"tk8s-dp-{os.getuid()}" / hashlib.sha1(str(p).encode()).hexdigest()[:12]
+    d.mkdir(parents=True, exist_ok=True, mode=0o700)
+    return d
+
+
+def _is_private_socket_dir(d: Path) -> bool:
+    return d.parent.name == f"tk8s-dp-{os.getuid()}"
 
 
 def _unix(path: Path) -> str:
@@ -394,6 +407,10 @@ class KubeletRegistry:
         if wipe:
             for s in self.dir.glob("*.sock"):
                 s.unlink(missing_ok=True)
+            if _is_private_socket_dir(self.dir):  # the short /tmp stand-in for a too-long path
+                import shutil
+
+                shutil.rmtree(self.dir, ignore_errors=True)
 
 
 # ---- CLI: the DaemonSet payload on a kubelet-managed MI355X node ------------------------------

@@ -1580,6 +1580,7 @@ def await_args(path: str, timeout: float | None = None) -> list[str]:
     if timeout is None:
         timeout = float(os.environ.get("TK8S_ZYGOTE_TIMEOUT", "120"))
     deadline = time.monotonic() + timeout
+    t_fast = time.monotonic() + 2.0
     while True:
         try:
             with open(path) as f:
@@ -1597,7 +1598,9 @@ def await_args(path: str, timeout: float | None = None) -> list[str]:
             except OSError:
                 pass
             raise SystemExit(0)
-        time.sleep(0.001)
+        # 1 ms while a bring-up is on its way (the arguments normally arrive within ~0.1 s, on the
+        # critical path), 50 ms once it is clearly not coming (a failed bring-up's leftover)
+        time.sleep(0.001 if time.monotonic() < t_fast else 0.05)
 
 
 def main(argv: list[str] | None = None) -> int:

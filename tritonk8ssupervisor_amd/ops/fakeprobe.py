@@ -44,8 +44,9 @@ def _reuse(path, wait):
         if not _alive(path + ".pending") and not os.path.exists(path):
             break
         time.sleep(0.002)
-    try:
-        with open(path) as f:
+    try:  # single-use (native/tools/reuse.h): take it atomically, then read it
+        os.rename(path, path + ".consumed")
+        with open(path + ".consumed") as f:
             text = f.read().strip()
     except OSError:
         return None

@@ -842,6 +842,10 @@ def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out: Callable[[s
     if hasattr(provider, "list_machines"):  # leftovers of an interrupted apply
         for m in provider.list_machines():
             provider.delete_machine(m)
+    # A machine sandbox no allocation lists any more can still hold a live process: the control
+    # plane zygote started with the CLI of a bring-up that failed before its master existed.
+    for pidfile in sorted((ws.state_dir / "machines").glob("*/run/*.pid")):
+        kill_pidfile(pidfile, grace=1.0)
     remove_paths([ws.tf / n for n in ("hosts.ip", "masters.ip", "rancher.tf", "terraform.tfstate", ".tfstate.lock",
                                       "hosts.ip.lock", "masters.ip.lock", ".terraform")]
                  + list(ws.tf.glob("terraform.tfstate*")))
