@@ -217,3 +217,64 @@ def test_check_mode_on_shipped_cluster_playbook(tmp_path):
     assert not list((a / "tmp").glob("*.id"))
     plays = [l for l in lines if l.startswith("PLAY [")]
     assert len(plays) == 3
+
+
+# ---- the fast subset agrees with real Jinja2 -----------------------------------------------------
+CORPUS_VARS = {
+    "project_id": {"content": "MWE3Cg=="}, "rancher_token_url": {"json": {"links": {"self": "http://m:8080/v1/t/1"}}},
+    "joined": {"stat": {"exists": False}}, "agent": {"running": True}, "tk8s_validate": "yes", "group_names": ["HOST"],
+    "tk8s_rocm_version": "7.0.0", "tk8s_fake_gpus": "", "tk8s_kfd": True, "tk8s_machine_gpus": [3],
+    "kubernetes_template_id": {"json": {"data": [{"id": "1t5"}]}}, "env_id_file": {"stat": {"exists": True}},
+    "master": "10.0.0.1", "tk8s_master_port": 8080, "inventory_hostname": "kubenode1", "xs": [1, 2, 3],
+    "containerd_cfg": {"changed": True}, "k8s_sysctl": {"changed": False}, "n": "4", "name": "k8s dev",
+    "cni": {"stdout": "daemonset.apps/kube-flannel-ds created"}, "groups": {"MASTER": ["kubemaster"]},
+}
+CORPUS = [
+    "project_id['content'] | b64decode | replace('\\n', '')", "not joined.stat.exists",
+    "not joined.stat.exists and not agent.running", "tk8s_validate | bool", "'HOST' in group_names",
+    "tk8s_rocm_version != '' or tk8s_fake_gpus != ''", "tk8s_kfd or tk8s_fake_gpus != '' or (tk8s_machine_gpus | length) == 0",
+    "kubernetes_template_id.json.data[0].id", "rancher_token_url.json['links']['self']", "xs | length > 2",
+    "'restarted' if containerd_cfg is changed else 'started'", "k8s_sysctl is changed", "n | int + 1",
+    "name ~ '!'", "missing | default('d')", "xs | join(',')", "name | upper", "groups['MASTER'][0]",
+    "'created' in cni.stdout or 'configured' in cni.stdout", "master + ':' + tk8s_master_port | string",
+    "tk8s_machine_gpus | first", "xs | last", "{'a': 1} | to_json", "true and not false", "none is none",
+]
+
+
+@pytest.mark.parametrize("expr", CORPUS)
+def test_subset_agrees_with_jinja2(expr):
+    fast = T._evaluate_subset(expr, CORPUS_VARS)
+    assert fast == T.jinja_evaluate(expr, CORPUS_VARS), expr
+
+
+def test_every_template_in_the_roles_parses():
+    """Every {{ }} in the shipped playbooks and roles is either in the fast subset or valid Jinja2."""
+    import re
+
+    exprs = set()
+    for f in [*(REPO / "ansible").glob("*.yml"), *(REPO / "ansible" / "roles").rglob("*.yml")]:
+        exprs.update(m.strip() for m in re.findall(r"\{\{(.*?)\}\}", f.read_text(), re.S))
+        for doc in yaml.safe_load(f.read_text()) or []:  # bare when/until/changed_when/failed_when
+            for t in (doc.get("tasks") or [doc]) if isinstance(doc, dict) else []:
+                for k in ("when", "until", "changed_when", "failed_when"):
+                    if isinstance(t.get(k), str) and "{{" not in t[k]:
+                        exprs.add(t[k].strip())
+    assert len(exprs) > 45
+    env = T._jinja_env(True)  # real Jinja2 + the Ansible filters/tests tk8s registers
+    for e in exprs:
+        try:
+            T._rewrite(T._pyify(e))
+        except T.TemplateError:
+            pass
+        env.compile_expression(e)  # raises on anything Jinja2 itself would reject
+
+
+def test_outside_the_subset_goes_to_jinja2(tmp_path):
+    v = {"xs": ["1", "2", "3"], "nodes": [{"a": {"g": "1"}}, {"a": {"g": "2"}}]}
+    assert T.evaluate("xs | map('int') | sum", v) == 6  # map/sum: not in the subset
+    assert T.evaluate("nodes | map(attribute='a') | map(attribute='g') | list", v) == ["1", "2"]
+    (tmp_path / "t.yaml").write_text("image: {{ img }}\n")
+    assert T.render("{{ lookup('template', p) }}", {"p": str(tmp_path / "t.yaml"), "img": "rocm/x"}) == "image: rocm/x\n"
+    assert T.render("{% for x in xs %}{{ x }}{% endfor %}", v) == "123"
+    with pytest.raises(T.Undefined):
+        T.evaluate("nope | map('int') | list", {})

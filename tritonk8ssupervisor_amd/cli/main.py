@@ -44,7 +44,7 @@ def cmd_setup(args) -> int:
               hbm_bytes=args.hbm_bytes, md5_bytes=args.md5_bytes, probe_iters=args.probe_iters,
               node_grace=args.node_grace, rocprof=args.rocprof, rocprof_counters=args.rocprof_counters,
               rccl_max_bytes=args.rccl_max_bytes,
-              rccl_timeout=args.rccl_timeout)
+              rccl_timeout=args.rccl_timeout, platform=args.platform)
     try:
         summary = s.run()
     except WizardAbort:
@@ -261,6 +261,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE")
     s.add_argument("--rccl-max-bytes", type=int, default=64 << 20)
     s.add_argument("--rccl-timeout", type=float, default=None, help="bound on the RCCL Job (default: --timeout)")
+    s.add_argument("--platform", choices=["tk8s", "kubeadm"], default=None,
+                   help="tk8s (default): the in-repo control plane and node agents; kubeadm: install ROCm, "
+                        "amdgpu-dkms, containerd and a real Kubernetes on the machines (needs root + network)")
     s.add_argument("--json", action="store_true")
     s.add_argument("-v", "--verbose", action="store_true")
     _backend_flags(s)

@@ -40,6 +40,7 @@ KEY_ORDER = [
     "HOST_PACKAGE",
     "TK8S_BACKEND",
     "TK8S_MASTER_PORT",
+    "TK8S_PLATFORM",
 ]
 QUOTED = {
     "SDC_URL", "SDC_ACCOUNT", "SDC_KEY_ID", "SDC_KEY", "KUBERNETES_NAME", "KUBERNETES_DESCRIPTION",
@@ -64,6 +65,7 @@ class ClusterConfig:
     HOST_PACKAGE: str = ""
     TK8S_BACKEND: str = "local"
     TK8S_MASTER_PORT: int = 8080
+    TK8S_PLATFORM: str = "tk8s"   # tk8s (in-repo control plane + node agents) | kubeadm (real Kubernetes)
     extra: dict = field(default_factory=dict)
 
     # ---- derived ---------------------------------------------------------------------

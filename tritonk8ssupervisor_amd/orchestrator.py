@@ -36,9 +36,11 @@ from .utils.fsutil import atomic_write, atomic_write_json, read_json, remove_pat
 from .utils.procs import kill_pidfile, pid_alive
 
 REPO = Path(__file__).resolve().parents[1]
-TEMPLATE_DIRS = ["terraform/master", "terraform/host", "ansible/roles", "manifests"]
-TEMPLATE_FILES = ["ansible/ansible.cfg", "ansible/clusterUp.yml"]
+TEMPLATE_DIRS = ["terraform/master", "terraform/host", "ansible/roles", "ansible/group_vars", "manifests"]
+TEMPLATE_FILES = ["ansible/ansible.cfg", "ansible/clusterUp.yml", "ansible/clusterUp-kubeadm.yml"]
 PHASES = ["configure", "provision", "ansible-config", "ansible", "ready", "rccl"]
+PLATFORMS = ("tk8s", "kubeadm")
+PLAYBOOKS = {"tk8s": "clusterUp.yml", "kubeadm": "clusterUp-kubeadm.yml"}
 
 
 class SetupError(RuntimeError):
@@ -123,6 +125,17 @@ def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, M
     }
 
 
+def kubeadm_extra_vars(setup: "Setup", cfg: ClusterConfig) -> dict:
+    """What the kubeadm roles need beyond the inventory and the role defaults."""
+    per_node = 0
+    try:
+        per_node = int(setup.provider.package_by_id_or_name(cfg.HOST_PACKAGE).gpus or 0)
+    except Exception:  # noqa: BLE001
+        pass
+    return {"tk8s_expected_gpus": per_node * int(cfg.KUBERNETES_NUMBER_OF_NODES), "tk8s_gpus_per_node": per_node,
+            "tk8s_ready_timeout": int(setup.timeout)}
+
+
 def controlplane_argv(bind: str, port: int, advertise: str, state_dir: str, node_grace: float) -> list[str]:
     """The control plane daemon (the ranchermaster role's rancher/server), one definition for the
     role and the master's boot hook."""
@@ -169,7 +182,8 @@ class Setup:
                  out: Callable[[str], None] = None, quiet_ansible: bool = True, hbm_bytes: int = 1 << 30,
                  md5_bytes: int = 256 << 20, probe_iters: int = 3, rccl_max_bytes: int = 64 << 20,
                  node_grace: float = 5.0, backend: str | None = None, master_port: int | None = None,
-                 rocprof: bool = False, rccl_timeout: float | None = None, rocprof_counters: str | None = None):
+                 rocprof: bool = False, rccl_timeout: float | None = None, rocprof_counters: str | None = None,
+                 platform: str | None = None):
         self.ws = ws
         self.answers = answers
         self.assume_yes = assume_yes
@@ -183,6 +197,9 @@ class Setup:
         self.rccl_max_bytes = rccl_max_bytes
         self.node_grace = node_grace
         self.backend = backend or os.environ.get("TK8S_BACKEND", "local")
+        self.platform = platform or os.environ.get("TK8S_PLATFORM", "tk8s")
+        if self.platform not in PLATFORMS:
+            raise SetupError(f"error: unknown platform {self.platform!r} (expected one of {', '.join(PLATFORMS)})")
         self.master_port = master_port
         self.rocprof = rocprof
         self.rocprof_counters = [c for c in (rocprof_counters or "").replace(" ", ",").split(",") if c]
@@ -220,7 +237,7 @@ class Setup:
         else:
             if ws.config.exists():
                 raise SetupError("error: old configuration found\n    clean the configuration (./setup.sh -c)")
-            cfg = ClusterConfig(TK8S_BACKEND=self.backend)
+            cfg = ClusterConfig(TK8S_BACKEND=self.backend, TK8S_PLATFORM=self.platform)
             if self.master_port == 0:  # any free port (benchmarks / tests run clusters side by side)
                 cfg.TK8S_MASTER_PORT = _free_port()
             elif self.master_port:
@@ -240,6 +257,10 @@ class Setup:
             write_config(ws.config, cfg)
         export_vars(cfg)
         self.cfg = cfg
+        self.platform = cfg.TK8S_PLATFORM or "tk8s"
+        if self.platform == "kubeadm" and self.provider.colocated:
+            raise SetupError("error: the kubeadm platform installs ROCm, amdgpu-dkms, containerd and Kubernetes as root on "
+                             "its machines: use machines you own (--backend baremetal with an SSH inventory, or triton)")
         return cfg
 
     def _machine_booted(self, address: str, m: Machine) -> None:
@@ -389,11 +410,14 @@ class Setup:
         if not masters or not hosts_:
             raise SetupError("Terraform had too many errors. Make sure you haven't reached your provisioning limit.")
         machines = self.engine.machines()
-        lines = ["[MASTER]"]
-        lines.append(f"{cfg.RANCHER_MASTER_HOSTNAME} ansible_host={machines[cfg.RANCHER_MASTER_HOSTNAME].primaryip}")
-        lines.append("[HOST]")
-        for n in cfg.node_names():
-            lines.append(f"{n} ansible_host={machines[n].primaryip}")
+        def host_line(name: str) -> str:
+            m = machines[name]
+            hv = {"ansible_host": m.primaryip}
+            hv.update(getattr(self.provider, "ansible_host_vars", lambda _m: {})(m))
+            return name + "".join(f" {k}={_ini_quote(v)}" for k, v in hv.items())
+
+        lines = ["[MASTER]", host_line(cfg.RANCHER_MASTER_HOSTNAME), "[HOST]"]
+        lines += [host_line(n) for n in cfg.node_names()]
         atomic_write(ws.ansible / "hosts", "\n".join(lines) + "\n")
         self.out("Creating ansible hosts file and variable files")
         self.out("    created: ansible/hosts")
@@ -420,10 +444,14 @@ class Setup:
         machines = self.engine.machines()
         extra = playbook_extra_vars(ws, cfg, machines, node_grace=self.node_grace, validate=self.validate,
                                     validation_command=self._validation_command())
+        if self.platform == "kubeadm":
+            extra.update(kubeadm_extra_vars(self, cfg))
         lines: list[str] = []
-        pb = Playbook(ws.ansible / "clusterUp.yml", ws.ansible / "hosts", executor=MachineExecutor(self.provider, machines),
-                      extra_vars=extra, events=self.events, out=(lines.append if self.quiet_ansible else self.out))
+        pb = Playbook(ws.ansible / PLAYBOOKS[self.platform], ws.ansible / "hosts",
+                      executor=MachineExecutor(self.provider, machines), extra_vars=extra, events=self.events,
+                      out=(lines.append if self.quiet_ansible else self.out))
         res = pb.run()
+        self.playbook_result = res
         atomic_write(ws.state_dir / "ansible.log", "\n".join(lines) + "\n")
         if not res.ok:
             if self.quiet_ansible:
@@ -444,8 +472,61 @@ class Setup:
         pkg = self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE)
         return int(self.cfg.KUBERNETES_NUMBER_OF_NODES) * int(getattr(pkg, "gpus", 0) or 0)
 
+    # -- kubeadm platform -------------------------------------------------------------------
+    def _master_exec(self, cmd: str, timeout: float = 120) -> tuple[int, str]:
+        ex = MachineExecutor(self.provider, self.engine.machines())
+        return ex.exec(self.cfg.RANCHER_MASTER_HOSTNAME, cmd, timeout=timeout)
+
+    def _kubeadm_nodes(self) -> list[dict]:
+        hv = getattr(self, "playbook_result", None)
+        reg = ((hv.hostvars if hv else {}).get(self.cfg.RANCHER_MASTER_HOSTNAME) or {}).get("tk8s_nodes") or {}
+        text = reg.get("stdout") or ""
+        if not text:  # --resume past the playbook: ask the API server
+            rc, text = self._master_exec("kubectl --kubeconfig /etc/kubernetes/admin.conf get nodes -o json")
+            if rc != 0:
+                raise SetupError(f"kubectl get nodes failed on the master: {text.strip()[-400:]}")
+        return json.loads(text)["items"]
+
+    def _kubeadm_ready(self) -> dict:
+        """Readiness on the kubeadm platform: the kubeadmvalidate role already waited (bounded) for
+        every node Ready and the expected amd.com/gpu; this reads back what the API server said."""
+        items = self._kubeadm_nodes()
+        workers = set(self.cfg.node_names())
+        ready = [n for n in items if n["metadata"]["name"] in workers and any(
+            c.get("type") == "Ready" and c.get("status") == "True" for c in n.get("status", {}).get("conditions", []))]
+        gpus = sum(int((n.get("status", {}).get("allocatable") or {}).get("amd.com/gpu", "0") or 0) for n in ready)
+        out = {"ready": len(ready) == len(workers) and gpus >= self.expected_gpus(), "nodes_ready": len(ready),
+               "gpus_allocatable": gpus, "nodes_validated": len(ready)}
+        if not out["ready"]:
+            raise SetupError(f"cluster not ready: {len(ready)}/{len(workers)} workers Ready, {gpus} amd.com/gpu "
+                             f"(expected {self.expected_gpus()})", code=124)
+        return out
+
+    def _kubeadm_finish(self, ready: dict, rccl, t_ready: float, total: float) -> dict:
+        m = self.engine.machines()[self.cfg.RANCHER_MASTER_HOSTNAME]
+        kubeconfig = self.ws.ansible / "tmp" / "kubeconfig"
+        self.summary = {
+            "platform": "kubeadm", "ready_seconds": round(t_ready, 4), "total_seconds": round(total, 4),
+            "nodes": int(self.cfg.KUBERNETES_NUMBER_OF_NODES), "gpus_allocatable": ready.get("gpus_allocatable", 0),
+            "nodes_validated": ready.get("nodes_validated", 0), "rccl": rccl,
+            "phases": {k: round(v, 4) for k, v in self.events.phases.items()},
+            "api": f"https://{m.primaryip}:6443", "kubectl_config": str(kubeconfig),
+            "project": self.project_id() if self.ws.env_id_file.exists() else "",
+        }
+        self.ws.save_state(summary=self.summary, finished=time.time())
+        self.events.emit("setup_done", **{k: v for k, v in self.summary.items() if k != "phases"})
+        self.out("")
+        self.out("Congratulations, your Kubernetes cluster setup has been complete.")
+        self.out(f"----> Kubernetes API server is at {self.summary['api']}")
+        self.out(f"----> kubectl: KUBECONFIG={kubeconfig} kubectl get nodes")
+        self.out(f"----> {self.summary['nodes']} node(s) Ready, {self.summary['gpus_allocatable']} x amd.com/gpu allocatable")
+        self.out(f"----> bring-up: {t_ready:.3f}s to all nodes Ready ({total:.3f}s including fabric validation)")
+        return self.summary
+
     def wait_ready(self) -> dict:
         """Event-driven, bounded replacement of the readiness loop (setup.sh:56-85)."""
+        if self.platform == "kubeadm":
+            return self._kubeadm_ready()
         c = self._client()
         pid = self.project_id()
         n = int(self.cfg.KUBERNETES_NUMBER_OF_NODES)
@@ -477,6 +558,13 @@ class Setup:
     def run_rccl(self) -> dict | None:
         from .controlplane.client import client_from_kubeconfig
         from .kube import apply_objects, load_manifests, pods_of, wait_job
+
+        if self.platform == "kubeadm":  # the RCCL-tests DaemonSet ran in the kubeadmvalidate role
+            pr = getattr(self, "playbook_result", None)
+            reg = ((pr.hostvars if pr else {}).get(self.cfg.RANCHER_MASTER_HOSTNAME) or {}).get("rccl_pods") or {}
+            lines = reg.get("stdout_lines") or []
+            return {"ok": bool(lines) and all(ln.split()[-1] == "true" for ln in lines if ln.strip()),
+                    "daemonset": "kube-system/tk8s-rccl-tests", "pods": lines} if lines else None
 
         g = self.expected_gpus()
         enabled = self.rccl if self.rccl is not None else g >= 2
@@ -571,6 +659,8 @@ class Setup:
             rccl = self.run_rccl()
         self.mark("rccl")
         total = time.monotonic() - t0
+        if self.platform == "kubeadm":
+            return self._kubeadm_finish(ready, rccl, t_ready, total)
         m = self.engine.machines()[self.cfg.RANCHER_MASTER_HOSTNAME]
         base = f"http://{m.primaryip}:{self.cfg.TK8S_MASTER_PORT}"
         pid = self.project_id()
@@ -785,6 +875,11 @@ class _Sink:
         pass
 
 
+def _ini_quote(v) -> str:
+    v = str(v)
+    return v if v and not any(c in v for c in " \t'\"#=") else "'" + v.replace("'", "'\"'\"'") + "'"
+
+
 def _set_ini_value(path: Path, key: str, value: str) -> None:
     """Replace `key = ...` in an ini file without sed (the reference's sed uses `;` as the
     delimiter on a user path, setup.sh:133)."""
@@ -802,6 +897,21 @@ def _set_ini_value(path: Path, key: str, value: str) -> None:
 
 
 # ---- teardown --------------------------------------------------------------------------------
+KUBEADM_RESET = ("kubeadm reset -f --cri-socket unix:///run/containerd/containerd.sock; "
+                 "rm -rf /etc/cni/net.d /root/.kube /etc/kubernetes/tk8s; systemctl restart containerd || true")
+
+
+def _kubeadm_reset(ws: "Workspace", provider, out) -> None:
+    """Undo kubeadm init/join on every machine before the machines go (best effort: a machine
+    that is gone already needs nothing)."""
+    if not (ws.tf / "terraform.tfstate").exists():
+        return
+    import concurrent.futures as cf
+
+    machines = list(Engine(ws.tf, provider).machines().values())
+    with cf.ThreadPoolExecutor(max_workers=max(1, len(machines))) as pool:
+        for m, (rc, text) in zip(machines, pool.map(lambda m: provider.exec(m, KUBEADM_RESET, timeout=300), machines)):
+            out(f"    kubeadm reset on {m.name}: {'ok' if rc == 0 else 'failed: ' + text.strip()[-200:]}")
 def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out: Callable[[str], None] = print,
           backend: str | None = None) -> int:
     """cleanRunner (setup.sh:484-521), non-destructive unless confirmed."""
@@ -833,6 +943,8 @@ def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out: Callable[[s
     from .burnin import stop_host_burnin
 
     stop_host_burnin(ws.state_dir)
+    if ws.config.exists() and read_config(ws.config).TK8S_PLATFORM == "kubeadm":
+        _kubeadm_reset(ws, provider, out)
     if (ws.tf / "rancher.tf").exists() or (ws.tf / "terraform.tfstate").exists():
         out("    destroying machines...")
         try:

@@ -34,12 +34,10 @@ from .templating import TemplateError, Undefined
 from .utils import yamlio
 from .utils.events import EventLog
 
-MODULE_ALIASES = {"command", "shell", "uri", "slurp", "pause", "debug", "set_fact", "wait_for", "fail",
-                  "assert", "copy", "file", "stat", "tk8s_daemon", "tk8s_gpu_facts", "tk8s_burnin", "tk8s_build", "tk8s_kube",
-                  "include_vars", "meta", "ping"}
 TASK_KEYS = {"name", "register", "when", "until", "retries", "delay", "with_items", "loop", "run_once",
              "delegate_to", "local_action", "action", "ignore_errors", "failed_when", "changed_when",
-             "environment", "no_log", "tags", "vars", "check_mode", "loop_control", "become", "args"}
+             "environment", "no_log", "tags", "vars", "check_mode", "loop_control", "become", "become_user", "args",
+             "notify", "delegate_facts", "any_errors_fatal", "timeout"}
 
 
 class PlaybookError(RuntimeError):
@@ -127,6 +125,12 @@ class Playbook:
         self.stats = {h: {"ok": 0, "changed": 0, "failed": 0, "skipped": 0, "unreachable": 0} for h in self.hosts}
         self._print_lock = threading.Lock()
         self._pool: cf.ThreadPoolExecutor | None = None
+        # every module invocation as rendered (play, host, task, module, args): what --check
+        # reports and the golden tests pin
+        self.trace: list[dict] = []
+        self._trace_lock = threading.Lock()
+        self._play = ""
+        self._defaults: dict = {}
 
     def _read_cfg(self) -> dict:
         p = self.dir / "ansible.cfg"
@@ -151,6 +155,8 @@ class Playbook:
         v = {"inventory_hostname": host.name, "ansible_host": host.address, "playbook_dir": str(self.dir),
              "groups": self._groups(), "group_names": host.groups, "ansible_check_mode": self.check,
              "ansible_default_ipv4": {"address": host.address}, "hostvars": self.hostvars}
+        v.update(self._defaults)  # role defaults: the lowest precedence of all
+        v.update(self._group_vars(host))  # group_vars/ next to the playbook (all, then the host's groups)
         v.update(host.vars)
         v.update(play_vars)
         v.update(self.hostvars.get(host.name, {}))
@@ -194,6 +200,9 @@ class Playbook:
 
     @staticmethod
     def _args(mod: str, raw: Any, extra: dict | None = None) -> dict:
+        from .playbook_modules import module_name
+
+        mod = module_name(mod)
         if isinstance(raw, dict):
             args = dict(raw)
         elif raw is None:
@@ -255,9 +264,17 @@ class Playbook:
                 elif not self.check:
                     raise PlaybookError(f"vars_files entry {fp} not found")
             tasks: list[dict] = []
+            self._defaults = {}
             for role in play.get("roles") or []:
-                tasks += self._role_tasks(role if isinstance(role, str) else role["role"])
+                rname = role if isinstance(role, str) else role["role"]
+                dfile = self.dir / "roles" / rname / "defaults" / "main.yml"
+                if dfile.exists():
+                    self._defaults.update(yamlio.load(dfile.read_text()) or {})
+                tasks += self._role_tasks(rname)
             tasks += play.get("tasks") or []
+            self._play = str(name)
+            if play.get("gather_facts", True) and not self._facts_done(hosts):
+                tasks = [{"name": "Gathering Facts", "setup": {}}] + tasks
             alive = list(hosts)
             failures: list[str] = []
             for task in tasks:
@@ -337,6 +354,22 @@ class Playbook:
         r = TaskResult(host.name, status, result, time.monotonic() - t0)
         return self._record(task, host, r)
 
+    def _group_vars(self, host: Host) -> dict:
+        cache = self.__dict__.setdefault("_gv_cache", {})
+        out: dict = {}
+        for g in ["all", *host.groups]:
+            if g not in cache:
+                cache[g] = {}
+                for f in (self.dir / "group_vars" / f"{g}.yml", self.dir / "group_vars" / f"{g}.yaml"):
+                    if f.exists():
+                        cache[g] = yamlio.load(f.read_text()) or {}
+                        break
+            out.update(cache[g])
+        return out
+
+    def _facts_done(self, hosts: list[Host]) -> bool:
+        return all("ansible_kernel" in self.hostvars.get(h.name, {}) for h in hosts)
+
     def _executor(self) -> cf.ThreadPoolExecutor:
         """One pool for the whole run (``forks`` workers; 0 = every host): starting fresh threads
         for every task cost ~2.5 ms per thread start under GIL contention at 9 hosts."""
@@ -357,6 +390,9 @@ class Playbook:
         extra = task.get("args")
         args = templating.render(self._args(mod, raw, extra), v)
         env = templating.render(task.get("environment") or {}, v)
+        with self._trace_lock:
+            self.trace.append({"play": self._play, "host": host.name, "task": task.get("name", ""),
+                               "module": mod, "args": args, "local": bool(local), "delegate": deleg.name if deleg else None})
         retries = int(task.get("retries", 3)) if "until" in task else 0
         delay = float(task.get("delay", 5))
         attempt = 0

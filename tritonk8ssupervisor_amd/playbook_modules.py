@@ -15,6 +15,7 @@ from __future__ import annotations
 import base64
 import json
 import os
+import re
 import shlex
 import socket
 import subprocess
@@ -39,7 +40,7 @@ def _bool(v: Any, default: bool = False) -> bool:
 
 def run_module(mod: str, args: dict, *, ctx, host, target, local: bool, env: dict, check: bool,
                variables: dict) -> dict:
-    fn = MODULES.get(mod)
+    fn = MODULES.get(module_name(mod))
     if fn is None:
         return {"failed": True, "msg": f"module {mod!r} is not supported by the tk8s playbook engine"}
     try:
@@ -51,14 +52,18 @@ def run_module(mod: str, args: dict, *, ctx, host, target, local: bool, env: dic
 
 
 # ---- command / shell ---------------------------------------------------------------------
-def _run_cmd(cmd: str | list[str], *, ctx, target, local, env, shell: bool, timeout: float = 600) -> dict:
+def _run_cmd(cmd: str | list[str], *, ctx, target, local, env, shell: bool, timeout: float = 600,
+             chdir: str | None = None) -> dict:
     t = time.monotonic()
     if local or ctx.executor is None:
         argv = ["bash", "-c", cmd] if shell else (cmd if isinstance(cmd, list) else shlex.split(cmd))
-        r = subprocess.run(argv, cwd=ctx.dir, env={**os.environ, **env}, capture_output=True, text=True, timeout=timeout)
+        cwd = ctx.dir / chdir if chdir else ctx.dir
+        r = subprocess.run(argv, cwd=cwd, env={**os.environ, **env}, capture_output=True, text=True, timeout=timeout)
         rc, out, err = r.returncode, r.stdout, r.stderr
     else:
         line = cmd if shell else " ".join(shlex.quote(a) for a in (cmd if isinstance(cmd, list) else shlex.split(cmd)))
+        if chdir:
+            line = f"cd {shlex.quote(chdir)} && {line}"
         rc, out = ctx.executor.exec(target.name, line, env=env, timeout=timeout)
         err = ""
     out = out or ""
@@ -67,18 +72,243 @@ def _run_cmd(cmd: str | list[str], *, ctx, target, local, env, shell: bool, time
             "msg": "" if rc == 0 else f"non-zero return code {rc}: {(err or out).strip()[-300:]}"}
 
 
-def m_command(args, *, ctx, target, local, env, check, **_):
-    if check:
-        return {"skipped": True, "changed": False, "msg": "command skipped in check mode"}
+_CMD_KEYS = ("creates", "removes", "chdir")
+
+
+def _cmd_args(args: dict) -> tuple[str | list, dict]:
+    """The command and its ``creates``/``removes``/``chdir`` options, from args or free form."""
+    opts = {k: args[k] for k in _CMD_KEYS if k in args}
     cmd = args.get("_raw_params") or args.get("cmd") or args.get("argv")
-    return _run_cmd(cmd, ctx=ctx, target=target, local=local, env=env, shell=False)
+    if isinstance(cmd, str):
+        words = shlex.split(cmd)
+        keep = []
+        for w in words:
+            k, eq, v = w.partition("=")
+            if eq and k in _CMD_KEYS:
+                opts[k] = v
+            else:
+                keep.append(w)
+        if len(keep) != len(words):
+            cmd = " ".join(shlex.quote(w) for w in keep)
+    return cmd, opts
+
+
+def _command(args, *, ctx, target, local, env, check, shell: bool) -> dict:
+    cmd, opts = _cmd_args(args)
+    fs = _fs(ctx, target, local)
+    if opts.get("creates") and fs.stat(opts["creates"])["exists"]:
+        return {"changed": False, "cmd": cmd, "rc": 0, "stdout": f"skipped, since {opts['creates']} exists",
+                "stdout_lines": []}
+    if opts.get("removes") and not fs.stat(opts["removes"])["exists"]:
+        return {"changed": False, "cmd": cmd, "rc": 0, "stdout": f"skipped, since {opts['removes']} does not exist",
+                "stdout_lines": []}
+    if check:
+        return {"skipped": True, "changed": False, "cmd": cmd, "msg": f"{'shell' if shell else 'command'} "
+                                                                      "skipped in check mode"}
+    res = _run_cmd(cmd, ctx=ctx, target=target, local=local, env=env, shell=shell, chdir=opts.get("chdir"))
+    res["cmd"] = cmd
+    return res
+
+
+def m_command(args, *, ctx, target, local, env, check, **_):
+    return _command(args, ctx=ctx, target=target, local=local, env=env, check=check, shell=False)
 
 
 def m_shell(args, *, ctx, target, local, env, check, **_):
+    return _command(args, ctx=ctx, target=target, local=local, env=env, check=check, shell=True)
+
+
+# ---- node runtime installation (ansible.builtin apt / apt_repository / get_url / systemd_service /
+# replace / lineinfile / fetch / setup): what the kubeadm platform's roles use --------------------
+def _sh(ctx, target, local, script: str, env: dict | None = None, timeout: float = 1800) -> tuple[int, str]:
+    if local or ctx.executor is None:
+        r = subprocess.run(["bash", "-c", script], cwd=ctx.dir, env={**os.environ, **(env or {})},
+                           capture_output=True, text=True, timeout=timeout)
+        return r.returncode, (r.stdout or "") + (r.stderr or "")
+    return ctx.executor.exec(target.name, script, env=env, timeout=timeout)
+
+
+def _as_list(v) -> list[str]:
+    if v is None:
+        return []
+    if isinstance(v, str):
+        return [x.strip() for x in v.split(",") if x.strip()]
+    return [str(x) for x in v]
+
+
+def apt_script(args: dict) -> str:
+    """The shell the apt module runs (also what --check reports): idempotent via dpkg-query."""
+    names = _as_list(args.get("name") or args.get("pkg"))
+    state = str(args.get("state", "present"))
+    parts = ["export DEBIAN_FRONTEND=noninteractive"]
+    if _bool(args.get("update_cache")):
+        valid = int(args.get("cache_valid_time", 0) or 0)
+        if valid:
+            parts.append(f"if [ -z \"$(find /var/lib/apt/lists -maxdepth 1 -newermt '-{valid} seconds' -name '*Packages' "
+                         "2>/dev/null | head -n1)\" ]; then apt-get update -q; fi")
+        else:
+            parts.append("apt-get update -q")
+    if _bool(args.get("upgrade")) or args.get("upgrade") == "dist":
+        parts.append("apt-get dist-upgrade -y -q")
+    if names:
+        q = " ".join(shlex.quote(n) for n in names)
+        if state == "absent":
+            parts.append(f"pkgs=$(for p in {q}; do dpkg-query -W -f='${{Status}}' \"$p\" 2>/dev/null | grep -q 'ok installed' "
+                         f"&& echo \"$p\"; done); [ -z \"$pkgs\" ] || {{ apt-get remove -y -q $pkgs && echo TK8S_CHANGED; }}")
+        else:
+            flag = " --only-upgrade" if state == "latest" else ""
+            miss = (f"pkgs=$(for p in {q}; do dpkg-query -W -f='${{Status}}' \"$p\" 2>/dev/null | grep -q 'ok installed' "
+                    f"|| echo \"$p\"; done)")
+            parts.append(miss)
+            if state == "latest":
+                parts.append(f"apt-get install -y -q --no-install-recommends{flag} {q} | grep -q 'newly installed' "
+                             "&& echo TK8S_CHANGED || true")
+            parts.append("[ -z \"$pkgs\" ] || { apt-get install -y -q --no-install-recommends $pkgs && echo TK8S_CHANGED; }")
+    return "\n".join(parts)
+
+
+def m_apt(args, *, ctx, target, local, env, check, **_):
+    script = apt_script(args)
     if check:
-        return {"skipped": True, "changed": False, "msg": "shell skipped in check mode"}
-    cmd = args.get("_raw_params") or args.get("cmd")
-    return _run_cmd(cmd, ctx=ctx, target=target, local=local, env=env, shell=True)
+        return {"changed": True, "cmd": script, "msg": "check mode: apt not run"}
+    rc, out = _sh(ctx, target, local, script, env)
+    return {"changed": "TK8S_CHANGED" in out, "failed": rc != 0, "rc": rc, "stdout": out[-2000:],
+            "msg": "" if rc == 0 else f"apt failed rc={rc}: {out.strip()[-500:]}"}
+
+
+def m_apt_repository(args, *, ctx, target, local, check, **_):
+    repo = str(args["repo"])
+    name = str(args.get("filename") or re.sub(r"[^A-Za-z0-9]+", "_", repo.split("//", 1)[-1]).strip("_")[:60])
+    dest = f"/etc/apt/sources.list.d/{name}.list"
+    fs = _fs(ctx, target, local)
+    if str(args.get("state", "present")) == "absent":
+        changed = fs.stat(dest)["exists"]
+        if changed and not check:
+            fs.remove(dest)
+        return {"changed": changed, "dest": dest}
+    changed = fs.write(dest, (repo + "\n").encode(), mode=0o644, check=check)
+    if changed and not check and _bool(args.get("update_cache", True)):
+        rc, out = _sh(ctx, target, local, "DEBIAN_FRONTEND=noninteractive apt-get update -q")
+        if rc != 0:
+            return {"failed": True, "msg": f"apt-get update failed: {out.strip()[-500:]}"}
+    return {"changed": changed, "dest": dest, "repo": repo}
+
+
+def m_get_url(args, *, ctx, target, local, check, **_):
+    url, dest = str(args["url"]), str(args["dest"])
+    fs = _fs(ctx, target, local)
+    if fs.stat(dest)["exists"] and not _bool(args.get("force")):
+        return {"changed": False, "dest": dest, "url": url}
+    cmd = f"curl -fsSL --retry 3 -o {shlex.quote(dest)} {shlex.quote(url)}"
+    if "mode" in args:
+        cmd += f" && chmod {str(args['mode'])} {shlex.quote(dest)}"
+    if check:
+        return {"changed": True, "cmd": cmd, "dest": dest}
+    rc, out = _sh(ctx, target, local, cmd, timeout=float(args.get("timeout", 120)) + 60)
+    return {"changed": rc == 0, "failed": rc != 0, "dest": dest, "url": url,
+            "msg": "" if rc == 0 else f"download of {url} failed: {out.strip()[-300:]}"}
+
+
+def m_systemd_service(args, *, ctx, target, local, check, **_):
+    name = args.get("name")
+    cmds = []
+    if _bool(args.get("daemon_reload")):
+        cmds.append("systemctl daemon-reload")
+    if name is not None and "enabled" in args:
+        cmds.append(f"systemctl {'enable' if _bool(args['enabled']) else 'disable'} {shlex.quote(str(name))}")
+    verb = {"started": "start", "stopped": "stop", "restarted": "restart", "reloaded": "reload"}.get(
+        str(args.get("state", "")))
+    if name is not None and verb:
+        cmds.append(f"systemctl {verb} {shlex.quote(str(name))}")
+    script = " && ".join(cmds) or "true"
+    if check:
+        return {"changed": bool(cmds), "cmd": script}
+    rc, out = _sh(ctx, target, local, script)
+    return {"changed": bool(cmds), "failed": rc != 0, "name": name,
+            "msg": "" if rc == 0 else f"systemctl failed: {out.strip()[-300:]}"}
+
+
+def m_replace(args, *, ctx, target, local, check, **_):
+    fs = _fs(ctx, target, local)
+    path = args.get("path") or args.get("dest")
+    data = fs.read(path)
+    if data is None:
+        if check:
+            return {"skipped": True, "changed": False, "msg": f"check mode: {path} does not exist yet"}
+        return {"failed": True, "msg": f"Path {path} does not exist !"}
+    text = data.decode()
+    new, n = re.subn(str(args["regexp"]), str(args.get("replace", "")), text, flags=re.MULTILINE)
+    changed = new != text
+    if changed:
+        fs.write(path, new.encode(), check=check)
+    return {"changed": changed, "msg": f"{n} replacements made" if changed else ""}
+
+
+def m_lineinfile(args, *, ctx, target, local, check, **_):
+    fs = _fs(ctx, target, local)
+    path = args.get("path") or args.get("dest")
+    data = fs.read(path)
+    if data is None and not _bool(args.get("create")):
+        return {"failed": True, "msg": f"Destination {path} does not exist !"}
+    lines = (data or b"").decode().splitlines()
+    line, rx = args.get("line"), args.get("regexp")
+    state = str(args.get("state", "present"))
+    out = list(lines)
+    if state == "absent":
+        out = [ln for ln in lines if not ((rx and re.search(rx, ln)) or (line is not None and ln == line))]
+    else:
+        idx = [i for i, ln in enumerate(lines) if rx and re.search(rx, ln)]
+        if idx:
+            out[idx[-1]] = str(line)
+        elif str(line) not in lines:
+            out.append(str(line))
+    changed = out != lines
+    if changed:
+        fs.write(path, ("\n".join(out) + "\n").encode(), check=check)
+    return {"changed": changed}
+
+
+def m_fetch(args, *, ctx, target, local, check, **_):
+    """Copy a file FROM the machine to the controller (``flat: yes``: exactly ``dest``)."""
+    src, dest = str(args["src"]), str(args["dest"])
+    data = _fs(ctx, target, local).read(src)
+    if data is None:
+        if check or _bool(args.get("fail_on_missing", True)) is False:
+            return {"skipped": True, "changed": False, "msg": f"{src} not found"}
+        return {"failed": True, "msg": f"the remote file does not exist: {src}"}
+    from .executor import LocalFS
+
+    d = dest if _bool(args.get("flat")) else os.path.join(dest, target.name, src.lstrip("/"))
+    changed = LocalFS(ctx.dir).write(d, data, check=check)
+    return {"changed": changed, "dest": str(LocalFS(ctx.dir).path(d))}
+
+
+FACTS_SCRIPT = r"""
+. /etc/os-release 2>/dev/null
+echo "distribution=${NAME%% *}"
+echo "release=${VERSION_CODENAME:-$UBUNTU_CODENAME}"
+echo "version=$VERSION_ID"
+echo "kernel=$(uname -r)"
+echo "arch=$(uname -m)"
+echo "hostname=$(hostname -s 2>/dev/null || uname -n)"
+echo "ipv4=$(ip -4 route get 1.1.1.1 2>/dev/null | sed -n 's/.* src \([0-9.]*\).*//p' | head -n1)"
+echo "processor_vcpus=$(nproc 2>/dev/null)"
+echo "memtotal_mb=$(awk '/MemTotal/ {print int($2/1024)}' /proc/meminfo 2>/dev/null)"
+"""
+
+
+def m_setup(args, *, ctx, target, local, **_):
+    """Fact gathering (the subset the roles read), run ON the machine."""
+    rc, out = _sh(ctx, target, local, FACTS_SCRIPT, timeout=60)
+    kv = dict(line.split("=", 1) for line in out.splitlines() if "=" in line)
+    facts = {"ansible_distribution": kv.get("distribution", ""), "ansible_distribution_release": kv.get("release", ""),
+             "ansible_distribution_version": kv.get("version", ""), "ansible_kernel": kv.get("kernel", ""),
+             "ansible_architecture": kv.get("arch", ""), "ansible_hostname": kv.get("hostname", ""),
+             "ansible_processor_vcpus": int(kv.get("processor_vcpus") or 0),
+             "ansible_memtotal_mb": int(kv.get("memtotal_mb") or 0)}
+    ip = kv.get("ipv4") or target.address
+    facts["ansible_default_ipv4"] = {"address": ip}
+    return {"ansible_facts": facts, "changed": False, "failed": rc != 0 and not out.strip()}
 
 
 # ---- uri ----------------------------------------------------------------------------------
@@ -191,6 +421,16 @@ def m_file(args, *, ctx, target, local, check, **_):
         changed = True
         if not check:
             fs.touch(p)
+    elif state == "link":
+        src = str(args["src"])
+        cmd = f"ln -sfn {shlex.quote(src)} {shlex.quote(str(fs.path(p)))}"
+        rc, cur = _sh(ctx, target, local, f"readlink -- {shlex.quote(str(fs.path(p)))}")
+        changed = cur.strip() != src
+        if changed and not check:
+            rc, out = _sh(ctx, target, local, cmd)
+            if rc != 0:
+                return {"failed": True, "msg": f"{cmd}: {out.strip()[-300:]}"}
+        return {"changed": changed, "path": str(fs.path(p)), "state": state, "src": src}
     elif not st["exists"]:
         return {"failed": True, "msg": f"file {fs.path(p)} does not exist"}
     return {"changed": changed, "path": str(fs.path(p)), "state": state}
@@ -406,4 +646,15 @@ MODULES = {
     "fail": m_fail, "assert": m_assert, "wait_for": m_wait_for, "meta": m_meta, "ping": m_ping,
     "tk8s_daemon": m_tk8s_daemon, "tk8s_gpu_facts": m_tk8s_gpu_facts, "tk8s_burnin": m_tk8s_burnin, "tk8s_build": m_tk8s_build,
     "tk8s_kube": m_tk8s_kube,
+    "apt": m_apt, "apt_repository": m_apt_repository, "get_url": m_get_url, "systemd_service": m_systemd_service,
+    "systemd": m_systemd_service, "service": m_systemd_service, "replace": m_replace, "lineinfile": m_lineinfile,
+    "fetch": m_fetch, "setup": m_setup, "gather_facts": m_setup,
 }
+
+
+def module_name(mod: str) -> str:
+    """``ansible.builtin.apt`` / ``ansible.legacy.apt`` -> ``apt`` (FQCNs as real Ansible writes them)."""
+    for prefix in ("ansible.builtin.", "ansible.legacy."):
+        if mod.startswith(prefix):
+            return mod[len(prefix):]
+    return mod

@@ -291,6 +291,18 @@ class BareMetalProvider(Provider):
             raise ProvisionError(f"machine {m.name}: no host recorded")
         return self.target(self._host(host))
 
+    def ansible_host_vars(self, m: Machine) -> dict:
+        """Inventory variables that let a stock ansible-playbook reach and use this machine the way
+        the in-repo engine does (ssh user/port/key, known-hosts policy, the node's tk8s install)."""
+        t = self._target_of(m)
+        hv = {"ansible_user": t.user, "ansible_port": t.port, "tk8s_home": m.home, "tk8s_machine_dir": m.sandbox,
+              "ansible_python_interpreter": m.python or "python3"}
+        if t.key:
+            hv["ansible_ssh_private_key_file"] = os.path.expanduser(t.key)
+        if t.known_hosts:
+            hv["ansible_ssh_common_args"] = f"-o UserKnownHostsFile={t.known_hosts} -o StrictHostKeyChecking=accept-new"
+        return hv
+
     def exec(self, machine: Machine, command: str, timeout: float = 300, env: dict | None = None,
              stdin: bytes | None = None) -> tuple[int, str]:
         script = ssh.remote_script(command, cwd=machine.sandbox, env={**self.machine_env(machine), **(env or {})})

@@ -117,6 +117,18 @@ class TritonProvider(Provider):
                 "TK8S_MACHINE_GPUS": ",".join(map(str, m.gpus)), "TK8S_MACHINE_PACKAGE": m.package,
                 "TK8S_HOME": m.home}
 
+    def ansible_host_vars(self, m: Machine) -> dict:
+        """Inventory variables that let a stock ansible-playbook reach and use this machine the way
+        the in-repo engine does (ssh user/port/key, known-hosts policy, the node's tk8s install)."""
+        t = self.target(m.primaryip)
+        hv = {"ansible_user": t.user, "ansible_port": t.port, "tk8s_home": m.home, "tk8s_machine_dir": m.sandbox,
+              "ansible_python_interpreter": m.python or "python3"}
+        if t.key:
+            hv["ansible_ssh_private_key_file"] = os.path.expanduser(t.key)
+        if t.known_hosts:
+            hv["ansible_ssh_common_args"] = f"-o UserKnownHostsFile={t.known_hosts} -o StrictHostKeyChecking=accept-new"
+        return hv
+
     def exec(self, machine, command, timeout=300, env=None, stdin=None):
         script = ssh.remote_script(command, cwd=machine.sandbox or None, env={**self.machine_env(machine), **(env or {})})
         return ssh.run(self.target(machine.primaryip), script, timeout=timeout, stdin=stdin, retries_on_connect=5)
