@@ -16,6 +16,16 @@ os.environ.setdefault("TK8S_HOST_REGISTRY", os.path.join(
     os.environ.get("TMPDIR", "/tmp"), f"tk8s-hostreg-{os.environ.get('PYTEST_XDIST_TESTRUNUID') or os.getpid()}"))
 
 
+@pytest.fixture(autouse=True)
+def _restore_environ():
+    """Setup.configure exports the cluster config into os.environ (the reference's exportVars,
+    setup.sh:543-549): never let one test's TK8S_BACKEND/TK8S_PLATFORM leak into the next."""
+    saved = dict(os.environ)
+    yield
+    os.environ.clear()
+    os.environ.update(saved)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: multi-second integration test")

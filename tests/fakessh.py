@@ -97,6 +97,14 @@ def main(argv: list[str]) -> int:
     if not command:
         print("fakessh: interactive sessions are not supported", file=sys.stderr)
         return 255
+    # The "hosts" are directories of THIS machine: anything that would change the machine itself
+    # (package managers, kernel modules, services, kubeadm) is refused, never run.
+    for word in ("apt-get", "dpkg ", "modprobe", "systemctl", "kubeadm", "swapoff", "sysctl ", "apt-mark",
+                 "/etc/apt", "/etc/kubernetes", "/etc/containerd", "/etc/modules-load.d", "/etc/sysctl.d",
+                 "/etc/fstab", "/opt/tk8s", "/root/.kube"):
+        if word in command:
+            print(f"fakessh: refusing a system-changing command on a fake host ({word.strip()})", file=sys.stderr)
+            return 126
     r = subprocess.run(["bash", "-c", command], cwd=hd, env=env)
     return r.returncode
 

@@ -68,7 +68,7 @@ def bm(tmp_path):
     env = dict(os.environ)
     env.update(PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_BACKEND="baremetal",
                TK8S_SSH=f"{sys.executable} {REPO / 'tests' / 'fakessh.py'}", FAKESSH_ROOT=str(root),
-               TK8S_FAKE_GPUS="4", TK8S_CONTROLLER_ONLY="leak-check", TK8S_SSH_CONNECT_RETRIES="0")
+               TK8S_FAKE_GPUS="4", TK8S_CONTROLLER_ONLY="leak-check", TK8S_SSH_CONNECT_RETRIES="0", TK8S_PLATFORM="tk8s")
     env.pop("TK8S_FAULTS", None)
     yield ws, root, env
     subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, timeout=120)

@@ -419,6 +419,13 @@ class Setup:
         lines = ["[MASTER]", host_line(cfg.RANCHER_MASTER_HOSTNAME), "[HOST]"]
         lines += [host_line(n) for n in cfg.node_names()]
         atomic_write(ws.ansible / "hosts", "\n".join(lines) + "\n")
+        # the variables the in-repo engine passes, for a by-hand stock run:
+        #   cd ansible && ansible-playbook -i hosts clusterUp.yml -e @tmp/tk8s_extra_vars.json
+        extra = playbook_extra_vars(ws, cfg, machines, node_grace=self.node_grace, validate=self.validate,
+                                    validation_command=self._validation_command())
+        if self.platform == "kubeadm":
+            extra.update(kubeadm_extra_vars(self, cfg))
+        atomic_write_json(ws.ansible / "tmp" / "tk8s_extra_vars.json", extra)
         self.out("Creating ansible hosts file and variable files")
         self.out("    created: ansible/hosts")
         master = masters[-1]

@@ -131,6 +131,7 @@ class Playbook:
         self._trace_lock = threading.Lock()
         self._play = ""
         self._defaults: dict = {}
+        self._play_env: dict = {}
 
     def _read_cfg(self) -> dict:
         p = self.dir / "ansible.cfg"
@@ -157,7 +158,8 @@ class Playbook:
              "ansible_default_ipv4": {"address": host.address}, "hostvars": self.hostvars}
         v.update(self._defaults)  # role defaults: the lowest precedence of all
         v.update(self._group_vars(host))  # group_vars/ next to the playbook (all, then the host's groups)
-        v.update(host.vars)
+        v.update(self._machine_vars(host))  # what the provider knows of the machine (a hand-written
+        v.update(host.vars)                 # inventory need not repeat it; the inventory wins)
         v.update(play_vars)
         v.update(self.hostvars.get(host.name, {}))
         v.update(self.extra_vars)
@@ -273,6 +275,7 @@ class Playbook:
                 tasks += self._role_tasks(rname)
             tasks += play.get("tasks") or []
             self._play = str(name)
+            self._play_env = play.get("environment") or {}
             if play.get("gather_facts", True) and not self._facts_done(hosts):
                 tasks = [{"name": "Gathering Facts", "setup": {}}] + tasks
             alive = list(hosts)
@@ -354,6 +357,14 @@ class Playbook:
         r = TaskResult(host.name, status, result, time.monotonic() - t0)
         return self._record(task, host, r)
 
+    def _machine_vars(self, host: Host) -> dict:
+        ex = self.executor
+        m = getattr(ex, "machines", {}).get(host.name) if ex is not None else None
+        if m is None:
+            return {}
+        return {"tk8s_machine_dir": m.sandbox, "tk8s_gpus": ",".join(map(str, m.gpus)),
+                "tk8s_home": m.home or str(Path(__file__).resolve().parents[1])}
+
     def _group_vars(self, host: Host) -> dict:
         cache = self.__dict__.setdefault("_gv_cache", {})
         out: dict = {}
@@ -389,7 +400,7 @@ class Playbook:
 
         extra = task.get("args")
         args = templating.render(self._args(mod, raw, extra), v)
-        env = templating.render(task.get("environment") or {}, v)
+        env = {**templating.render(self._play_env, v), **templating.render(task.get("environment") or {}, v)}
         with self._trace_lock:
             self.trace.append({"play": self._play, "host": host.name, "task": task.get("name", ""),
                                "module": mod, "args": args, "local": bool(local), "delegate": deleg.name if deleg else None})

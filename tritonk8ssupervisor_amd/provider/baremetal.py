@@ -296,6 +296,7 @@ class BareMetalProvider(Provider):
         the in-repo engine does (ssh user/port/key, known-hosts policy, the node's tk8s install)."""
         t = self._target_of(m)
         hv = {"ansible_user": t.user, "ansible_port": t.port, "tk8s_home": m.home, "tk8s_machine_dir": m.sandbox,
+              "tk8s_gpus": ",".join(map(str, m.gpus)),
               "ansible_python_interpreter": m.python or "python3"}
         if t.key:
             hv["ansible_ssh_private_key_file"] = os.path.expanduser(t.key)

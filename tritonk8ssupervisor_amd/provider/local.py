@@ -257,6 +257,14 @@ class LocalProvider(Provider):
             "TK8S_MACHINE_PACKAGE": m.package,
         }
 
+    def ansible_host_vars(self, m: Machine) -> dict:
+        """Inventory variables for stock ansible-playbook: the machines are sandboxes of this host,
+        so it connects locally; the tk8s modules find the sandbox and the install from these."""
+        from pathlib import Path as _P
+
+        return {"ansible_connection": "local", "tk8s_machine_dir": m.sandbox, "tk8s_gpus": ",".join(map(str, m.gpus)),
+                "tk8s_home": str(_P(__file__).resolve().parents[2])}
+
     def exec(self, machine: Machine, command: str, timeout: float = 300, env: dict | None = None,
              stdin: bytes | None = None) -> tuple[int, str]:
         e = dict(os.environ)
