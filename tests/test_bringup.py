@@ -672,3 +672,13 @@ def test_shared_burnin_result_is_single_use(ws):
         time.sleep(0.05)
     res = p["status"]["result"]
     assert res["ok"] and not res.get("host_burnin")  # its own probe, not the shared burn-in
+
+
+def test_bringup_with_the_stock_terraform_modules(ws):
+    """TK8S_TERRAFORM_FORM=compat: rancher.tf points at terraform/compat (terraform_data modules a
+    stock `terraform plan` loads); the engine brings the same cluster up from them."""
+    s = _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=_env(TK8S_TERRAFORM_FORM="compat")))
+    assert s["nodes"] == 2 and s["nodes_validated"] == 2
+    assert 'source = "compat/host"' in (ws / "terraform" / "rancher.tf").read_text()
+    st = json.loads((ws / "terraform" / "terraform.tfstate").read_text())
+    assert all(".terraform_data." in a for a in st["resources"])

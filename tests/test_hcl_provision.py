@@ -268,3 +268,73 @@ def test_clusters_on_one_host_never_share_an_ip_or_a_gpu(tmp_path, monkeypatch):
     c = LocalProvider(tmp_path / "c")
     assert len(c.predict_gpus(4, 2)) == 8
     assert c.create_machine("kubemaster", "cpu-only", ["local-public"], tags={"role": "master"}).primaryip != ma.primaryip
+
+
+# ---- the stock-Terraform form (terraform/compat: terraform_data + `tk8s machine`) ----------------
+def _rancher_tf_form(ws, prov, nodes, form):
+    env = prov.env()
+    key = prov.find_key(env["SDC_KEY_ID"])
+    pub = prov.network_by_id_or_name("local-public").id
+    (ws.tf / "rancher.tf").write_text(hcl.render_root(
+        "local", env["SDC_ACCOUNT"], key, key + ".pub", env["SDC_KEY_ID"], env["SDC_URL"], "kubemaster", [pub],
+        [f"kubenode{i}" for i in range(1, nodes + 1)], [pub], prov.package_by_id_or_name("mi355x-1gpu").id, form=form))
+
+
+def test_both_terraform_forms_plan_identically(ws):
+    """the modules stock Terraform can load (terraform_data + local-exec calling
+    `./tk8s machine create|delete`) plan exactly like the engine's tk8s_machine modules. Real
+    terraform is not installed here: that it accepts the files is unpinned beyond the HCL2
+    constructs they use (built-in terraform_data, list(string), join(), when = destroy)."""
+    prov = LocalProvider(ws.state_dir)
+    plans = {}
+    for form in ("tk8s", "compat"):
+        _rancher_tf_form(ws, prov, 2, form)
+        eng = Engine(ws.tf, prov)
+        eng.get()
+        plans[form] = [(a.address.split(".")[1], a.action, a.attrs) for a in eng.plan()]
+    assert plans["tk8s"] == plans["compat"]
+    assert [p[0] for p in plans["compat"]] == ["kubemaster", "kubenode1", "kubenode2"]
+    text = (ws.tf / "rancher.tf").read_text()
+    assert 'source = "compat/host"' in text and 'provider "local"' not in text  # no provider to download
+    compat = (hcl.parse_dir(ws.tf / "compat" / "host")).children("resource")[0]
+    assert compat.labels == ["terraform_data", "host"]
+    cmds = [p.attrs["command"] for p in compat.children("provisioner")]
+    assert any("machine create" in c for c in cmds) and any("machine delete" in c for c in cmds)
+
+
+def test_compat_form_applies_through_the_engine(ws):
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf_form(ws, prov, 2, "compat")
+    eng = Engine(ws.tf, prov)
+    eng.get()
+    res = eng.apply()
+    assert res.ok and len(res.created) == 3
+    ms = eng.machines()
+    assert (ws.tf / "hosts.ip").read_text().split() == [ms["kubenode1"].primaryip, ms["kubenode2"].primaryip]
+    assert len(eng.destroy()) == 3 and prov.list_machines() == []
+
+
+def test_machine_cli_is_what_the_compat_provisioners_run(ws):
+    """The exact commands terraform/compat/host/main.tf's provisioners run, from terraform/."""
+    import subprocess
+    import sys
+
+    repo = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable)
+    import shutil
+
+    shutil.copy2(repo / "tk8s", ws.root / "tk8s")
+    prov = LocalProvider(ws.state_dir)
+    pub = prov.network_by_id_or_name("local-public").id
+    pkg = prov.package_by_id_or_name("mi355x-1gpu").id
+    run = lambda *a: subprocess.run(["../tk8s", "--workdir", "..", "machine", *a], cwd=ws.tf, env=env,
+                                    capture_output=True, text=True, timeout=60)
+    r = run("create", "--name", "kubenode1", "--package", pkg, "--networks", pub, "--role", "host", "--ip-file", "hosts.ip")
+    assert r.returncode == 0, r.stderr
+    m = json.loads(r.stdout)
+    assert m["name"] == "kubenode1" and len(m["gpus"]) == 1
+    assert (ws.tf / "hosts.ip").read_text().split() == [m["primaryip"]]
+    assert [json.loads(x)["name"] for x in run("list").stdout.splitlines()] == ["kubenode1"]
+    assert run("delete", "--name", "kubenode1").returncode == 0
+    assert prov.list_machines() == []
+    assert "already deleted" in run("delete", "--name", "kubenode1").stdout  # destroy is idempotent

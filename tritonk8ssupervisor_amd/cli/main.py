@@ -172,6 +172,51 @@ def cmd_gpu_health(args) -> int:
     return 0 if r.get("ok") and r.get("healthy") else (3 if not r.get("ok") else 1)
 
 
+def cmd_machine(args) -> int:
+    """``./tk8s machine create|delete|list``: the provider's machine lifecycle as a CLI -- what the
+    stock-Terraform modules' local-exec provisioners call (terraform/compat/*/main.tf)."""
+    import fcntl
+
+    from ..provider.base import ProvisionError
+    from ..provision import BOOTSTRAP
+
+    ws = _ws(args)
+    prov = _provider(args)
+    if args.action == "list":
+        for m in getattr(prov, "list_machines", lambda: [])():
+            print(json.dumps(m.to_dict()))
+        return 0
+    if args.action == "create":
+        key = ""
+        if args.authorized_keys and Path(args.authorized_keys).exists():
+            key = Path(args.authorized_keys).read_text()
+        try:
+            m = prov.create_machine(args.name, args.package, [n for n in args.networks.split(",") if n],
+                                    image=args.image or "", root_authorized_keys=key,
+                                    tags={"name": args.name, "role": args.role})
+        except ProvisionError as e:
+            print(f"Error: {e}", file=sys.stderr)
+            return 1
+        rc, out = prov.exec(m, "set -e\n" + "\n".join(BOOTSTRAP))
+        if rc != 0:
+            prov.delete_machine(m)
+            print(f"Error: {args.name}: bootstrap failed: {out.strip()[-400:]}", file=sys.stderr)
+            return 1
+        if args.ip_file:  # the masters.ip / hosts.ip hand-off, appended under a lock
+            with open(ws.tf / args.ip_file if not Path(args.ip_file).is_absolute() else args.ip_file, "a") as f:
+                fcntl.flock(f, fcntl.LOCK_EX)
+                f.write(m.primaryip + "\n")
+        print(json.dumps(m.to_dict()))
+        return 0
+    m = prov.get_machine(args.name)
+    if m is None:
+        print(f"machine {args.name} not found (already deleted)")
+        return 0
+    prov.delete_machine(m)
+    print(f"machine {args.name} deleted")
+    return 0
+
+
 def cmd_terraform(args) -> int:
     from ..provision import Engine
 
@@ -202,6 +247,8 @@ def cmd_playbook(args) -> int:
     machines = {}
     if (ws.tf / "terraform.tfstate").exists():
         machines = Engine(ws.tf, prov).machines()
+    elif hasattr(prov, "list_machines"):  # machines made by stock Terraform (terraform/compat)
+        machines = {m.name: m for m in prov.list_machines()}
     pb = Path(args.playbook)
     if not pb.is_absolute():
         pb = ws.ansible / pb
@@ -296,6 +343,17 @@ def build_parser() -> argparse.ArgumentParser:
     gh.add_argument("--json", action="store_true")
     gh.set_defaults(fn=cmd_gpu_health)
     sub.add_parser("debug-vars", help="print the exported configuration (debugVars)").set_defaults(fn=cmd_debug_vars)
+
+    mc = sub.add_parser("machine", help="create/delete/list machines (what the stock-Terraform modules call)")
+    mc.add_argument("action", choices=["create", "delete", "list"])
+    mc.add_argument("--name")
+    mc.add_argument("--package", default="")
+    mc.add_argument("--networks", default="")
+    mc.add_argument("--role", default="host", choices=["master", "host"])
+    mc.add_argument("--image", default="")
+    mc.add_argument("--authorized-keys", default=None, help="public key file to authorise on the machine")
+    mc.add_argument("--ip-file", default=None, help="append the machine's IP here (relative to terraform/)")
+    mc.set_defaults(fn=cmd_machine)
 
     t = sub.add_parser("terraform")
     t.add_argument("action", choices=["get", "plan", "apply", "destroy"])

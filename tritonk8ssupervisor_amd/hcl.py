@@ -7,7 +7,8 @@ vars.tf:1-23) and the generated root config ``terraform/rancher.tf`` (setup.sh:1
 
 Supported: blocks with string labels, ``key = value`` attributes, strings with ``${...}``
 interpolation (nested quotes inside, e.g. ``"${file("x")}"``), numbers, booleans, lists,
-maps, ``#``/``//``/``/* */`` comments. Interpolation functions: ``file(path)``; references
+maps, ``#``/``//``/``/* */`` comments, HCL2 bare expressions (``list(string)``,
+``when = destroy``). Interpolation functions: ``file(path)``, ``join(sep, list)``; references
 ``var.X``, ``TYPE.NAME.ATTR``, ``self.ATTR``. Duplicate attributes keep the LAST value and are
 reported (the reference declares ``tags`` twice, terraform/master/main.tf:6-8 and 33-35).
 """
@@ -37,7 +38,7 @@ class Block:
 
 
 # ---- tokenizer ---------------------------------------------------------------------------
-_PUNCT = set("{}[]=,:")
+_PUNCT = set("{}[]=,:()")
 
 
 def _tokens(text: str) -> list[tuple[str, Any, int]]:
@@ -174,6 +175,19 @@ class _Parser:
         tok = self.peek()
         if tok[0] in ("str", "num", "bool"):
             return self.take()[1]
+        if tok[0] == "ident" and self.peek(1)[0] == "(":  # function call / type constraint, e.g.
+            name = self.take()[1]                           # list(string), join(",", x): kept as an
+            depth, parts = 0, [name]                        # interpolation
+            while True:
+                t = self.take()
+                if t[0] == "eof":
+                    raise HclError(f"line {tok[2]}: unterminated call of {name}")
+                depth += t[0] == "("
+                depth -= t[0] == ")"
+                parts.append(f'"{t[1]}"' if t[0] == "str" else str(t[1]).lower() if t[0] == "bool" else str(t[1]))
+                if depth == 0:
+                    break
+            return "${" + "".join(parts) + "}"
         if tok[0] == "ident":  # bare reference (HCL2 style), kept as an interpolation
             return "${" + self.take()[1] + "}"
         if tok[0] == "[":
@@ -249,6 +263,10 @@ def _split_interps(s: str) -> list[tuple[bool, str]]:
 
 def eval_expr(expr: str, ctx: dict) -> Any:
     expr = expr.strip()
+    m = re.fullmatch(r'join\(\s*"([^"]*)"\s*,\s*(.+)\)', expr, re.S)
+    if m:
+        v = eval_expr(m.group(2), ctx)
+        return m.group(1).join(map(str, v if isinstance(v, list) else [v]))
     m = re.fullmatch(r'file\(\s*"(.*)"\s*\)', expr, re.S)
     if m:
         p = Path(interpolate(m.group(1), ctx)).expanduser()
@@ -330,9 +348,13 @@ def render_module(name: str, source: str, networks: list[str], pub_key_path: str
 
 def render_root(provider_kind: str, account: str, key_path: str, pub_key_path: str, key_id: str, url: str,
                 master: str, master_networks: list[str], hosts: list[str], host_networks: list[str],
-                package: str) -> str:
-    out = render_provider(provider_kind, account, key_path, key_id, url)
-    out += render_module(master, "master", master_networks, pub_key_path, package)
+                package: str, form: str = "tk8s") -> str:
+    """``form`` "tk8s": modules terraform/{master,host} (resource tk8s_machine, the engine's own
+    type); "compat": terraform/compat/{master,host} (terraform_data + the tk8s CLI), which stock
+    Terraform plans and applies as well."""
+    prefix = "compat/" if form == "compat" else ""
+    out = render_provider(provider_kind, account, key_path, key_id, url) if form != "compat" else ""
+    out += render_module(master, prefix + "master", master_networks, pub_key_path, package)
     for h in hosts:
-        out += render_module(h, "host", host_networks, pub_key_path, package)
+        out += render_module(h, prefix + "host", host_networks, pub_key_path, package)
     return out

@@ -36,7 +36,8 @@ from .utils.fsutil import atomic_write, atomic_write_json, read_json, remove_pat
 from .utils.procs import kill_pidfile, pid_alive
 
 REPO = Path(__file__).resolve().parents[1]
-TEMPLATE_DIRS = ["terraform/master", "terraform/host", "ansible/roles", "ansible/group_vars", "manifests"]
+TEMPLATE_DIRS = ["terraform/master", "terraform/host", "terraform/compat", "ansible/roles", "ansible/group_vars",
+                 "manifests"]
 TEMPLATE_FILES = ["ansible/ansible.cfg", "ansible/clusterUp.yml", "ansible/clusterUp-kubeadm.yml"]
 PHASES = ["configure", "provision", "ansible-config", "ansible", "ready", "rccl"]
 PLATFORMS = ("tk8s", "kubeadm")
@@ -336,7 +337,8 @@ class Setup:
         pub = key + ".pub" if Path(key + ".pub").exists() else key
         text = hcl.render_root(self.provider.name, cfg.SDC_ACCOUNT, key, pub, cfg.SDC_KEY_ID, cfg.SDC_URL,
                                cfg.RANCHER_MASTER_HOSTNAME, cfg.master_networks(), cfg.node_names(),
-                               cfg.node_networks(), cfg.HOST_PACKAGE)
+                               cfg.node_networks(), cfg.HOST_PACKAGE,
+                               form=os.environ.get("TK8S_TERRAFORM_FORM", "tk8s"))
         if not (ws.tf / "rancher.tf").exists() or not self.resume:
             atomic_write(ws.tf / "rancher.tf", text)
         self.out("Generating terraform configs for environment...")

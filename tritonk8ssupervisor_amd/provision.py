@@ -33,6 +33,12 @@ from .utils.faults import fault
 
 STATE_FILE = "terraform.tfstate"
 RESOURCE_TYPE = "tk8s_machine"
+# Stock-Terraform form of the same machine (terraform/compat/*): terraform_data whose ``input``
+# carries the tk8s_machine attributes and whose local-exec provisioners call `tk8s machine ...`.
+# The engine plans it identically and creates it through the same provider fast path.
+COMPAT_TYPE = "terraform_data"
+BOOTSTRAP = ["test -d run && test -d logs && test -d pods",
+             "python3 -S -E -c 'import sys; sys.exit(0 if sys.version_info >= (3, 8) else 1)'"]
 
 
 @dataclass
@@ -123,6 +129,17 @@ class Engine:
             ctx = {"var": variables, "__dir__": str(src)}
             for r in mod.children("resource"):
                 rtype, rname = r.labels
+                if rtype == COMPAT_TYPE:
+                    attrs = {k: hcl.interpolate(v, ctx) for k, v in (r.attrs.get("input") or {}).items()}
+                    # its local-exec provisioners ARE the machine lifecycle (`tk8s machine create|delete`):
+                    # the engine does that itself, then runs the standard bootstrap check
+                    provs = [p for p in r.children("provisioner") if "machine " not in str(p.attrs.get("command", ""))]
+                    provs.append(hcl.Block("provisioner", ["remote-exec"], {"inline": list(BOOTSTRAP)}))
+                    if isinstance(attrs.get("networks"), str):
+                        attrs["networks"] = [x for x in attrs["networks"].split(",") if x]
+                    out.append(ResourceSpec(f"module.{name}.{rtype}.{rname}", name, str(m.attrs["source"]),
+                                            rname, attrs, provs, src))
+                    continue
                 if rtype != RESOURCE_TYPE:
                     raise ProvisionError(f"module {name}: unsupported resource type {rtype}")
                 attrs = {k: hcl.interpolate(v, ctx) for k, v in r.attrs.items()}
