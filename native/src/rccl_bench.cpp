@@ -6,6 +6,7 @@
 #include "tk8s/rccl_bench.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -55,8 +56,15 @@ std::vector<size_t> sweep_sizes(const AllReduceConfig& cfg, DType dtype) {
 }
 
 // Runs the sweep on the given ranks (all driven by this process). `all_ranks` = communicator size.
+double unix_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+// init_ms: the communicator set-up (ncclCommInitAll / ncclCommInitRank) this process waited for;
+// init_done: wall clock when it returned -- across ranks, the spread of init_done is how unevenly
+// the ranks' runtimes came up (the fabric check's start-up cost at 8 processes per node).
 std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceConfig& cfg,
-                      const char* mode) {
+                      const char* mode, double init_ms, double init_done) {
   const size_t es = elem_size(cfg.dtype);
   const auto sizes = sweep_sizes(cfg, cfg.dtype);
   const size_t maxb = sizes.back();
@@ -154,6 +162,8 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
       .kv("dtype", cfg.dtype == DType::kF32 ? "float32" : "bfloat16")
       .kv("iters", cfg.iters)
       .kv("peak_busbw_gbps", peak_bus)
+      .kv("comm_init_ms", init_ms)
+      .kv("init_done_unix_ms", init_done)
       .raw("results", Json::array(rows))
       .str();
 }
@@ -214,7 +224,10 @@ std::string allreduce_single_process(const std::vector<int>& devices, const AllR
   try {
     if (devices.empty()) return error_json("no devices");
     std::vector<ncclComm_t> comms(devices.size());
+    const auto t0 = std::chrono::steady_clock::now();
     TK8S_NCCL_CHECK(ncclCommInitAll(comms.data(), static_cast<int>(devices.size()), devices.data()));
+    const double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double init_done = unix_ms();
     for (size_t i = 0; i < devices.size(); ++i) {
       ranks[i].device = devices[i];
       ranks[i].rank = static_cast<int>(i);
@@ -222,7 +235,7 @@ std::string allreduce_single_process(const std::vector<int>& devices, const AllR
       TK8S_HIP_CHECK(hipSetDevice(devices[i]));
       TK8S_HIP_CHECK(hipStreamCreateWithFlags(&ranks[i].stream, hipStreamNonBlocking));
     }
-    std::string out = run_sweep(ranks, static_cast<int>(devices.size()), cfg, "single_process");
+    std::string out = run_sweep(ranks, static_cast<int>(devices.size()), cfg, "single_process", init_ms, init_done);
     release(ranks);
     return out;
   } catch (const std::exception& ex) {
@@ -239,8 +252,10 @@ std::string allreduce_rank(int rank, int nranks, int device, const ncclUniqueId&
     ranks[0].rank = rank;
     TK8S_HIP_CHECK(hipSetDevice(device));
     TK8S_HIP_CHECK(hipStreamCreateWithFlags(&ranks[0].stream, hipStreamNonBlocking));
+    const auto t0 = std::chrono::steady_clock::now();
     TK8S_NCCL_CHECK(ncclCommInitRank(&ranks[0].comm, nranks, id, rank));
-    std::string out = run_sweep(ranks, nranks, cfg, "multi_process");
+    const double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    std::string out = run_sweep(ranks, nranks, cfg, "multi_process", init_ms, unix_ms());
     release(ranks);
     return out;
   } catch (const std::exception& ex) {

@@ -406,14 +406,20 @@ def test_multi_gpu_setup_with_rccl_job(tmp_path):
     for f in ("setup.sh", "tk8s", "kubectl"):
         shutil.copy2(repo / f, tmp_path / f)
     env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
-    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable)
+    # the ranks log their transports: every channel must be P2P over xGMI
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P")
     try:
         r = subprocess.run(["./setup.sh", "--nodes", "2", "--yes", "--json", "--port", "0", "--timeout", "240",
                             "--rccl-max-bytes", str(64 << 20)], cwd=tmp_path, env=env, capture_output=True, text=True,
                            timeout=400)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
         s = json.loads(r.stdout.strip().splitlines()[-1])
-        assert s["gpus_allocatable"] == 2 and s["rccl"]["ok"] and s["rccl"]["nranks"] == 2
+        rc = s["rccl"]
+        assert s["gpus_allocatable"] == 2 and rc["ok"] and rc["nranks"] == 2
+        assert rc["transport"]["logged"] and rc["transport"]["p2p"] > 0, rc["transport"]
+        assert rc["transport"]["shm"] == 0 and rc["transport"]["net"] == 0, rc["transport"]  # no host fallback
+        assert rc["peak_busbw_gbps"] > 40, rc  # one xGMI link at 64 MiB, not PCIe / host memory
+        assert rc["init_spread_ms"] < 5000, rc  # the ranks' runtimes came up together
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 

@@ -627,6 +627,12 @@ class Setup:
                                                     "nccl_max_nchannels", "peak_links_equivalent") if k in first},
                "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),
                                  "ok": (p.get("status", {}).get("result") or {}).get("ok")} for p in pods]}
+        done = [r["init_done_unix_ms"] for r in results if r.get("init_done_unix_ms")]
+        if done:  # how unevenly the ranks' runtimes + communicators came up
+            rep["init_spread_ms"] = round(max(done) - min(done), 3)
+            rep["comm_init_ms_max"] = round(max(r.get("comm_init_ms", 0.0) for r in results), 3)
+        rep["transport"] = rccl_transports([(p.get("metadata", {}).get("annotations") or {}).get("tk8s.amd.com/log-path")
+                                            for p in pods])
         if prof_dir is not None:
             rep["rocprof"] = summarize_rocprof(prof_dir)
         if not ok:
@@ -797,6 +803,26 @@ class Setup:
 
         kc = Client(base).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
         atomic_write_json(self.ws.state_dir / "kubeconfig.json", kc)
+
+
+def rccl_transports(log_paths: list) -> dict:
+    """Which transports the RCCL ranks' channels used, from their NCCL_DEBUG=INFO lines
+    ("... via P2P/IPC", "via SHM/...", "via NET/..."): on one MI355X node every channel must be
+    P2P over xGMI; SHM or NET means a host-memory or network fallback."""
+    import re
+
+    counts = {"p2p": 0, "shm": 0, "net": 0, "collnet": 0}
+    seen = False
+    for p in log_paths:
+        try:
+            text = Path(p).read_text(errors="replace") if p else ""
+        except OSError:
+            continue
+        for m in re.finditer(r" via (P2P|SHM|NET|COLLNET)\b", text):
+            counts[m.group(1).lower()] += 1
+            seen = True
+    counts["logged"] = seen  # False: NCCL_DEBUG=INFO was not set, nothing to judge
+    return counts
 
 
 # Hardware counters one rocprofv3 --pmc pass can hold per block on gfx950 (asking for more makes
