@@ -1,0 +1,227 @@
+"""Controllers of the control plane: DaemonSets, the GPU validation gate, Indexed Jobs,
+Deployments (rolling updates), run by reconcile() after every change. A mixin of
+server.ControlPlane.
+"""
+from __future__ import annotations
+
+import copy
+
+from .store import now_iso
+from .objects import (
+    VALIDATION_LABEL, TERMINAL, _key, _cond, _set_cond, _set_ready, _xgmi_view, template_hash, labels_match,
+)
+
+
+class Controllers:
+    # ---- controllers ------------------------------------------------------------------
+    def reconcile(self) -> None:
+        """Run every controller once (cheap at this scale; called after each mutation)."""
+        if getattr(self, "_reconciling", False):
+            self._again = True
+            return
+        self._reconciling = True
+        try:
+            for _ in range(8):
+                self._again = False
+                for p in self.store.list("projects"):
+                    pid = p["id"]
+                    self._ctl_daemonsets(pid)
+                    self._ctl_jobs(pid)
+                    self._ctl_deployments(pid)
+                    self._ctl_validation(pid)
+                    self._scheduler(pid)
+                if not self._again:
+                    break
+        finally:
+            self._reconciling = False
+
+    def _new_pod(self, pid: str, ns: str, name: str, owner: dict, owner_kind: str, template: dict,
+                 node: str | None = None, extra_env: dict | None = None, labels: dict | None = None,
+                 annotations: dict | None = None) -> dict:
+        spec = copy.deepcopy(template.get("spec", {}))
+        if extra_env:
+            for c in spec.get("containers", []):
+                c.setdefault("env", []).extend({"name": k, "value": str(v)} for k, v in extra_env.items())
+        if node:
+            spec["nodeName"] = node
+        md = copy.deepcopy(template.get("metadata", {}))
+        md.update(name=name, namespace=ns)
+        md.setdefault("labels", {}).update(labels or {})
+        md.setdefault("annotations", {}).update(annotations or {})
+        md["ownerReferences"] = [{"kind": owner_kind, "name": owner["metadata"]["name"], "uid": owner["metadata"]["uid"]}]
+        pod = {"kind": "Pod", "apiVersion": "v1", "metadata": md, "spec": spec, "_project": pid,
+               "status": {"phase": "Pending", "conditions": []}}
+        spec.setdefault("restartPolicy", "Always")
+        return self.store.put("pods", _key(pid, ns, name), pod)
+
+    def _owned(self, pid: str, owner: dict) -> list[dict]:
+        uid = owner["metadata"]["uid"]
+        return self.store.list("pods", lambda o: self._in(pid, o) and any(
+            r.get("uid") == uid for r in o["metadata"].get("ownerReferences", [])))
+
+    def _ctl_daemonsets(self, pid: str) -> None:
+        nodes = self.store.list("nodes", lambda n: self._in(pid, n))
+        for ds in self.store.list("daemonsets", lambda o: self._in(pid, o)):
+            ns = ds["metadata"]["namespace"]
+            tmpl = ds["spec"]["template"]
+            sel = tmpl.get("spec", {}).get("nodeSelector")
+            pods = {o["spec"].get("nodeName"): o for o in self._owned(pid, ds)}
+            eligible = [n for n in nodes if labels_match(sel, n["metadata"].get("labels"))
+                        and not n["spec"].get("unschedulable")]
+            for n in eligible:
+                nn = n["metadata"]["name"]
+                if nn not in pods:
+                    pods[nn] = self._new_pod(pid, ns, f"{ds['metadata']['name']}-{nn}", ds, "DaemonSet", tmpl, node=nn,
+                                             labels=ds["spec"].get("selector", {}).get("matchLabels"))
+            phases = [o.get("status", {}).get("phase") for o in pods.values()]
+            status = {"desiredNumberScheduled": len(eligible), "currentNumberScheduled": len(pods),
+                      "numberReady": phases.count("Running") + phases.count("Succeeded"),
+                      "numberSucceeded": phases.count("Succeeded"), "numberFailed": phases.count("Failed")}
+            if ds.get("status") != status:
+                self.store.patch("daemonsets", _key(pid, ns, ds["metadata"]["name"]), lambda o, s=status: o.__setitem__("status", s))
+
+    def _ctl_validation(self, pid: str) -> None:
+        """Node condition AMDGPUValidated from the validation DaemonSet's pod on that node."""
+        for ds in self.store.list("daemonsets", lambda o: self._in(pid, o) and o["metadata"].get("labels", {}).get(VALIDATION_LABEL) == "true"):
+            for pod in self._owned(pid, ds):
+                nn = pod["spec"].get("nodeName")
+                phase = pod.get("status", {}).get("phase")
+                if not nn or phase not in TERMINAL:
+                    continue
+                key = _key(pid, nn)
+                n = self.store.get("nodes", key)
+                if n is None:
+                    continue
+                result = pod.get("status", {}).get("result") or {}
+                view = _xgmi_view(result)
+                want = ("True", "ProbesPassed") if phase == "Succeeded" else ("False", "ProbesFailed")
+                if want[0] == "True" and view is not None and not view["healthy"]:
+                    want = ("False", "XGMILinkDegraded")
+                c = _cond(n, "AMDGPUValidated")
+                if c and (c["status"], c["reason"]) == want:
+                    continue
+
+                def fn(node, want=want, result=result, pod=pod, view=view):
+                    from .. import xgmi
+
+                    msg = xgmi.message(view) if want[1] == "XGMILinkDegraded" else pod.get("status", {}).get("message", "")
+                    _set_cond(node, "AMDGPUValidated", want[0], want[1], msg[:500])
+                    ann = node["metadata"].setdefault("annotations", {})
+                    if view is not None:
+                        ann.update(xgmi.annotations(view))
+                        if view["healthy"]:
+                            _set_cond(node, "XGMILinksHealthy", "True", "LinksHealthy",
+                                      f"{view['pulls']} pulls >= {view.get('min_fraction')} x median {view.get('median_gbps')} GB/s")
+                        else:
+                            _set_cond(node, "XGMILinksHealthy", "False", "XGMILinkDegraded", xgmi.message(view))
+                        _set_ready(node)
+                    for k, path in (("hbm-write-gbps", ("hbm", "gbps")), ("hbm-read-gbps", ("hbm", "read_gbps")),
+                                    ("md5-mbps", ("md5", "mbps")),
+                                    ("copy-gbps", ("copy", "kernel_gbps")), ("probe-ms", ("timings_ms", "total")),
+                                    ("hip-init-ms", ("timings_ms", "hip_init"))):
+                        v = result.get(path[0], {}).get(path[1]) if isinstance(result.get(path[0]), dict) else None
+                        if v is not None:
+                            ann[f"tk8s.amd.com/{k}"] = f"{v:.1f}"
+
+                self.store.patch("nodes", key, fn)
+                if want[1] == "XGMILinkDegraded":
+                    from .. import xgmi
+
+                    self._event(pid, "default", {"kind": "Node", "name": nn}, "XGMILinkDegraded", xgmi.message(view),
+                                "Warning")
+
+    def _ctl_jobs(self, pid: str) -> None:
+        for job in self.store.list("jobs", lambda o: self._in(pid, o)):
+            ns, jname = job["metadata"]["namespace"], job["metadata"]["name"]
+            spec = job["spec"]
+            completions = int(spec.get("completions", 1))
+            parallelism = int(spec.get("parallelism", completions))
+            backoff = int(spec.get("backoffLimit", 6))
+            indexed = spec.get("completionMode") == "Indexed"
+            pods = self._owned(pid, job)
+            succeeded_idx, active, failed = set(), 0, 0
+            for o in pods:
+                ph = o.get("status", {}).get("phase")
+                idx = int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
+                if ph == "Succeeded":
+                    succeeded_idx.add(idx if indexed else o["metadata"]["name"])
+                elif ph == "Failed":
+                    failed += 1
+                else:
+                    active += 1
+            done = any(c["type"] in ("Complete", "Failed") and c["status"] == "True" for c in job.get("status", {}).get("conditions", []))
+            if not done and failed > backoff:
+                for o in pods:  # stop the rest (a gang job cannot finish without all ranks)
+                    if o.get("status", {}).get("phase") not in TERMINAL:
+                        self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+            elif not done:
+                running_idx = {int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
+                               for o in pods if o.get("status", {}).get("phase") not in TERMINAL}
+                need = [i for i in range(completions) if i not in succeeded_idx and i not in running_idx] if indexed \
+                    else list(range(max(0, completions - len(succeeded_idx) - active)))
+                for i in need[: max(0, parallelism - active)]:
+                    self._seq += 1
+                    name = f"{jname}-{i}-{self._seq:x}" if indexed else f"{jname}-{self._seq:x}"
+                    env = {"JOB_COMPLETION_INDEX": i, "JOB_COMPLETIONS": completions, "JOB_NAME": jname} if indexed else {"JOB_NAME": jname}
+                    self._new_pod(pid, ns, name, job, "Job", spec["template"], extra_env=env,
+                                  labels={"job-name": jname},
+                                  annotations={"batch.kubernetes.io/job-completion-index": str(i)} if indexed else None)
+                    active += 1
+            status = dict(job.get("status", {}))
+            status.update(active=active, succeeded=len(succeeded_idx), failed=failed)
+            conds = [c for c in status.get("conditions", [])]
+            if not done:
+                if len(succeeded_idx) >= completions:
+                    conds.append({"type": "Complete", "status": "True", "lastTransitionTime": now_iso()})
+                    status["completionTime"] = now_iso()
+                elif failed > backoff:
+                    conds.append({"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded",
+                                  "lastTransitionTime": now_iso()})
+            status["conditions"] = conds
+            if status != job.get("status"):
+                self.store.patch("jobs", _key(pid, ns, jname), lambda o, s=status: o.__setitem__("status", s))
+
+    def _ctl_deployments(self, pid: str) -> None:
+        """Deployment controller with ReplicaSet-style generations: pods carry the
+        ``pod-template-hash`` of the template they came from. A changed template rolls out with
+        the RollingUpdate defaults (maxSurge 25 % rounded up, maxUnavailable 25 % rounded down;
+        an old pod goes only when a new one runs), ``strategy: Recreate`` drops the old pods first."""
+        for d in self.store.list("deployments", lambda o: self._in(pid, o)):
+            ns, dname = d["metadata"]["namespace"], d["metadata"]["name"]
+            spec = d["spec"]
+            want = int(spec.get("replicas", 1))
+            h = template_hash(spec["template"])
+            match = (spec.get("selector") or {}).get("matchLabels") or {}
+
+            def live():
+                return [o for o in self._owned(pid, d) if o.get("status", {}).get("phase") not in TERMINAL]
+
+            unavailable = want // 4
+            for _ in range(2):  # scale down old -> room to surge again, in the same pass
+                pods = live()
+                new = [o for o in pods if o["metadata"].get("labels", {}).get("pod-template-hash") == h]
+                old = [o for o in pods if o not in new]
+                if (spec.get("strategy") or {}).get("type") == "Recreate" and old:
+                    for o in old:
+                        self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                    pods, old = new, []
+                surge = max(1, -(-want // 4)) if old else 0
+                for _ in range(max(0, min(want - len(new), want + surge - len(pods)))):
+                    self._seq += 1
+                    new.append(self._new_pod(pid, ns, f"{dname}-{h[:8]}-{self._seq:x}", d, "Deployment",
+                                             spec["template"], labels={**match, "pod-template-hash": h}))
+                ready_new = sum(1 for o in new if o.get("status", {}).get("phase") == "Running")
+                keep_old = max(0, want - unavailable - ready_new)
+                for o in sorted(old, key=lambda o: o["metadata"]["name"])[keep_old:]:
+                    self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                for o in sorted(new, key=lambda o: o["metadata"]["name"])[want:]:
+                    self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+            pods = live()
+            running = sum(1 for o in pods if o.get("status", {}).get("phase") == "Running")
+            status = {"observedGeneration": int(d["metadata"].get("generation", 1)), "replicas": len(pods),
+                      "updatedReplicas": sum(1 for o in pods if o["metadata"].get("labels", {}).get("pod-template-hash") == h),
+                      "readyReplicas": running, "availableReplicas": running,
+                      "unavailableReplicas": max(0, want - running)}
+            if d.get("status") != status:
+                self.store.patch("deployments", _key(pid, ns, dname), lambda o, s=status: o.__setitem__("status", s))
+

@@ -1,0 +1,169 @@
+"""Object helpers of the control plane (split out of server.py): store keys, node conditions and
+readiness, GPU counts, merge patches, template hashes, admission, label selectors.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import secrets
+
+from .httpserver import HttpError
+from .store import now_iso
+
+GPU = "amd.com/gpu"
+VALIDATION_LABEL = "tk8s.amd.com/validation"
+TERMINAL = ("Succeeded", "Failed")
+KIND_GROUPS = (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1"), ("configmaps", "/api/v1"),
+               ("secrets", "/api/v1"), ("daemonsets", "/apis/apps/v1"), ("deployments", "/apis/apps/v1"),
+               ("jobs", "/apis/batch/v1"), ("ingresses", "/apis/networking.k8s.io/v1"))
+
+
+def _key(*parts: str) -> str:
+    return "/".join(parts)
+
+
+def _cond(obj: dict, ctype: str) -> dict | None:
+    for c in obj.get("status", {}).get("conditions", []):
+        if c.get("type") == ctype:
+            return c
+    return None
+
+
+def _set_cond(obj: dict, ctype: str, status: str, reason: str = "", message: str = "") -> bool:
+    conds = obj.setdefault("status", {}).setdefault("conditions", [])
+    for c in conds:
+        if c["type"] == ctype:
+            changed = c.get("status") != status or c.get("reason") != reason
+            if changed:
+                c["lastTransitionTime"] = now_iso()
+            c.update(status=status, reason=reason, message=message)
+            return changed
+    conds.append({"type": ctype, "status": status, "reason": reason, "message": message,
+                  "lastTransitionTime": now_iso()})
+    return True
+
+
+def node_ready(n: dict) -> bool:
+    c = _cond(n, "Ready")
+    return bool(c and c["status"] == "True")
+
+
+def _set_ready(node: dict, message: str = "tk8s agent heartbeating") -> bool:
+    """Ready follows the heartbeat, unless the node's xGMI links failed the pre-Ready check
+    (xgmi.py): then it stays NotReady with that reason while the agent is alive."""
+    x = _cond(node, "XGMILinksHealthy")
+    if x and x["status"] == "False":
+        return _set_cond(node, "Ready", "False", "XGMILinkDegraded", x.get("message", ""))
+    return _set_cond(node, "Ready", "True", "AgentReady", message)
+
+
+def node_validated(n: dict) -> bool:
+    c = _cond(n, "AMDGPUValidated")
+    return bool(c and c["status"] == "True")
+
+
+def pod_gpus(p: dict) -> int:
+    total = 0
+    for c in p.get("spec", {}).get("containers", []):
+        r = c.get("resources", {})
+        v = r.get("limits", {}).get(GPU, r.get("requests", {}).get(GPU, 0))
+        total += int(v or 0)
+    return total
+
+
+def _xgmi_view(result: dict) -> dict | None:
+    """The xGMI link verdict of a validation result: the host burn-in's share carries it
+    (``xgmi``); a machine's own multi-GPU probe carries raw pulls, judged here."""
+    if not isinstance(result, dict):
+        return None
+    if isinstance(result.get("xgmi"), dict):
+        return result["xgmi"]
+    if any(d.get("peers") for d in result.get("devices") or []):
+        from .. import xgmi
+
+        rep = xgmi.link_report(result)
+        return xgmi.node_view(rep, sorted({e["src"] for e in rep["links"]} | {e["dst"] for e in rep["links"]}))
+    return None
+
+
+def merge_patch(target, patch):
+    """RFC 7386 JSON merge patch (what kubectl's merge and strategic-merge patches reduce to here:
+    maps merge key by key, ``null`` deletes, lists are replaced whole)."""
+    if not isinstance(patch, dict):
+        return copy.deepcopy(patch)
+    out = copy.deepcopy(target) if isinstance(target, dict) else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch(out.get(k), v)
+    return out
+
+
+def template_hash(template: dict) -> str:
+    """``pod-template-hash`` of a Deployment's pod template (names its ReplicaSet generation)."""
+    import hashlib  # off the control plane's start-up path (it is on the bring-up's)
+
+    return hashlib.sha1(json.dumps(template, sort_keys=True, separators=(",", ":")).encode()).hexdigest()[:10]
+
+
+GPU_VISIBILITY = "tk8s.amd.com/gpu-visibility"
+
+
+def _admit_gpu_visibility(kind: str, ns: str, body: dict) -> None:
+    """Admission: ``gpu-visibility: node`` lets a pod's runtime see every GPU of its node (the RCCL
+    fabric Job's ranks need it for xGMI peer-to-peer). Only kube-system Jobs may ask for it; a pod
+    cannot ask for it directly (the agent re-checks: kube-system pods owned by a Job)."""
+    if kind == "pods":
+        ann = (body.get("metadata") or {}).get("annotations") or {}
+        if ann.get(GPU_VISIBILITY) == "node":
+            raise HttpError(403, f'pods is forbidden: annotation {GPU_VISIBILITY}: node is reserved for '
+                                 'kube-system Jobs')
+    elif kind in ("jobs", "daemonsets", "deployments"):
+        ann = ((body.get("spec") or {}).get("template") or {}).get("metadata", {}).get("annotations") or {}
+        if ann.get(GPU_VISIBILITY) == "node" and (kind != "jobs" or ns != "kube-system"):
+            raise HttpError(403, f'{kind} is forbidden: annotation {GPU_VISIBILITY}: node is reserved for '
+                                 'kube-system Jobs')
+
+
+def _normalize_data(kind: str, body: dict) -> None:
+    """ConfigMap data must be strings; Secret ``stringData`` folds into base64 ``data``."""
+    import base64
+    import binascii
+
+    if kind == "configmaps":
+        data = body.get("data") or {}
+        if not isinstance(data, dict) or not all(isinstance(v, str) for v in data.values()):
+            raise HttpError(422, "ConfigMap data must map keys to strings")
+        body["data"] = data
+    elif kind == "secrets":
+        data = dict(body.get("data") or {})
+        for k, v in (body.pop("stringData", None) or {}).items():
+            data[k] = base64.b64encode(str(v).encode()).decode()
+        for k, v in data.items():
+            try:
+                base64.b64decode(str(v), validate=True)
+            except (binascii.Error, ValueError) as e:
+                raise HttpError(422, f"Secret data[{k!r}] is not valid base64: {e}") from e
+        body["data"] = data
+        body.setdefault("type", "Opaque")
+
+
+def labels_match(selector: dict | None, labels: dict | None) -> bool:
+    if not selector:
+        return True
+    labels = labels or {}
+    return all(labels.get(k) == v for k, v in selector.items())
+
+
+def _parse_selector(s: str | None) -> dict | None:
+    if not s:
+        return None
+    out = {}
+    for part in s.split(","):
+        if "=" in part:
+            k, v = part.split("=", 1)
+            out[k.strip().rstrip("=")] = v.strip()
+    return out
+
+

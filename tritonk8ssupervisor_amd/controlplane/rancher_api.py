@@ -1,0 +1,359 @@
+"""Rancher 1.x environment API of the control plane (what the reference's roles call:
+ansible/roles/ranchermaster/tasks/main.yml:29-52, rancherhost/tasks/main.yml:11-34), the KV
+rendezvous store and the readiness summary / long-poll (setup.sh:56-85). A mixin of
+server.ControlPlane: it uses the store, the routes and the helpers the server sets up.
+"""
+from __future__ import annotations
+
+import copy
+import html
+import json
+import os
+import secrets
+import time
+
+from ..utils.trace import trace
+from .httpserver import HttpError, Request, Response
+from .store import now_iso
+from .objects import GPU, TERMINAL, _key, _cond, _set_cond, node_ready, _set_ready, node_validated, pod_gpus
+
+
+class RancherAPI:
+    # ---- Rancher API -----------------------------------------------------------------
+    def _ensure_templates(self) -> None:
+        if not self.store.list("projecttemplates"):
+            for i, (name, desc) in enumerate([("cattle", "Default Cattle template"),
+                                              ("kubernetes", "Kubernetes on MI355X (tk8s control plane)")], 1):
+                tid = f"1pt{i}"
+                self.store.put("projecttemplates", tid, {"id": tid, "type": "projectTemplate", "name": name,
+                                                          "description": desc, "isPublic": True,
+                                                          "metadata": {"name": name}})
+
+    async def h_templates(self, req: Request):
+        self._ensure_templates()
+        name = req.q("name")
+        data = [t for t in self.store.list("projecttemplates") if name is None or t["name"] == name]
+        return {"type": "collection", "resourceType": "projectTemplate", "data": data}
+
+    async def h_projects(self, req: Request):
+        return {"type": "collection", "resourceType": "project", "data": [self._public_project(p) for p in self.store.list("projects")]}
+
+    def _public_project(self, p: dict) -> dict:
+        return {k: v for k, v in p.items() if k not in ("apiToken",)}
+
+    async def h_project_create(self, req: Request):
+        self._ensure_templates()
+        body = req.json()
+        name = str(body.get("name") or "").strip()
+        tid = body.get("projectTemplateId")
+        if not name:
+            raise HttpError(422, "name is required")
+        tmpl = self.store.get("projecttemplates", str(tid))
+        if tmpl is None:
+            raise HttpError(422, f"projectTemplateId {tid!r} does not exist")
+        pid = self._next_id("1a")
+        self._seq += 1
+        p = {"id": pid, "type": "project", "name": name, "description": body.get("description", ""),
+             "projectTemplateId": tid, "orchestration": tmpl["name"], "state": "active",
+             "allowSystemRole": bool(body.get("allowSystemRole", False)), "members": body.get("members", []),
+             "virtualMachine": bool(body.get("virtualMachine", False)),
+             "servicesPortRange": body.get("servicesPortRange"), "projectLinks": body.get("projectLinks", []),
+             "created": now_iso(), "created_seq": self._seq, "apiToken": secrets.token_hex(16),
+             "links": {"self": f"{self.base}/v2-beta/projects/{pid}"},
+             "metadata": {"name": pid}}
+        self.store.put("projects", pid, p)
+        return Response(201, self._public_project(p))
+
+    async def h_project_get(self, req: Request, pid: str):
+        return self._public_project(self.project(pid))
+
+    async def h_project_delete(self, req: Request, pid: str):
+        p = self.project(pid)
+        for kind in list(self.store.objs):
+            for k in self.store.keys(kind):
+                if k.startswith(pid + "/"):
+                    self.store.delete(kind, k)
+        self.store.delete("projects", p["id"])
+        return {"id": pid, "state": "removed"}
+
+    async def h_token_create(self, req: Request):
+        pid = req.q("projectId") or req.json().get("projectId")
+        p = self.project(pid)
+        tid = self._next_id("1c")
+        token = secrets.token_hex(20)
+        t = {"id": tid, "type": "registrationToken", "projectId": p["id"], "token": token, "state": "active",
+             "registrationUrl": f"{self.base}/v1/scripts/{token}",
+             "command": f"python3 -m tritonk8ssupervisor_amd.agent --url {self.base}/v1/scripts/{token}",
+             "links": {"self": f"{self.base}/v1/registrationtokens/{tid}"}, "metadata": {"name": tid}}
+        self.store.put("registrationtokens", tid, t)
+        return Response(201, {k: v for k, v in t.items() if k not in ("token", "registrationUrl", "command")})
+
+    async def h_token_get(self, req: Request, tid: str):
+        t = self.store.get("registrationtokens", tid)
+        if t is None:
+            raise HttpError(404, f"registration token {tid} not found")
+        return t
+
+    def _token(self, token: str) -> dict:
+        for t in self.store.list("registrationtokens"):
+            if t["token"] == token and t["state"] == "active":
+                return t
+        raise HttpError(403, "invalid registration token")
+
+    async def h_script(self, req: Request, token: str):
+        t = self._token(token)
+        pid = t["projectId"]
+        return {"projectId": pid, "apiUrl": self.base, "apiPrefix": f"/r/projects/{pid}/kubernetes",
+                "heartbeatSeconds": max(0.2, self.node_grace / 5), "nodeGraceSeconds": self.node_grace}
+
+    async def h_register(self, req: Request, token: str):
+        t = self._token(token)
+        pid = t["projectId"]
+        body = req.json()
+        name = str(body.get("name") or "").strip()
+        if not name:
+            raise HttpError(422, "node name is required")
+        key = _key(pid, name)
+        ntok = secrets.token_hex(16)
+        gpus = body.get("devices", [])
+        healthy = sum(1 for d in gpus if d.get("health", "Healthy") == "Healthy")
+        cap = dict(body.get("capacity", {}))
+        cap[GPU] = str(len(gpus))
+        alloc = dict(cap)
+        alloc[GPU] = str(healthy)
+        old = self.store.get("nodes", key)
+        cidr = (old or {}).get("spec", {}).get("podCIDR") or self._next_pod_cidr()
+        node = {
+            "kind": "Node", "apiVersion": "v1", "_project": pid,
+            "metadata": {"name": name, "labels": {"kubernetes.io/hostname": name, "kubernetes.io/os": "linux",
+                                                  **({"amd.com/gpu.family": "gfx950"} if gpus else {}),
+                                                  **body.get("labels", {})},
+                         "annotations": body.get("annotations", {})},
+            "spec": {"unschedulable": False, "podCIDR": cidr},
+            "status": {"capacity": cap, "allocatable": alloc, "devices": gpus,
+                       "addresses": [{"type": "InternalIP", "address": body.get("ip", "")},
+                                     {"type": "Hostname", "address": name}],
+                       "nodeInfo": body.get("nodeInfo", {}), "conditions": []},
+        }
+        if old is not None and _cond(old, "XGMILinksHealthy"):  # a re-join keeps the link verdict
+            node["status"]["conditions"].append(copy.deepcopy(_cond(old, "XGMILinksHealthy")))
+        _set_ready(node, "tk8s agent registered and heartbeating")
+        _set_cond(node, "AMDGPUValidated", "Unknown" if gpus else "True",
+                  "Pending" if gpus else "NoGPUs", "validation pod not finished" if gpus else "")
+        self.store.put("nodes", key, node)
+        self.store.put("nodesecrets", key, {"metadata": {"name": name}, "nodeToken": ntok, "_project": pid})
+        self.leases[key] = time.monotonic()
+        self._event(pid, "default", {"kind": "Node", "name": name}, "RegisteredNode", f"Node {name} registered ({len(gpus)} GPU)")
+        self.reconcile()
+        trace("cp", f"node {name} registered")
+        return Response(201, {"node": name, "nodeToken": ntok, "projectId": pid, "podCIDR": cidr,
+                              "apiPrefix": f"/r/projects/{pid}/kubernetes",
+                              "heartbeatSeconds": max(0.2, self.node_grace / 5)})
+
+    async def h_dashboard(self, req: Request, pid: str):
+        p = self.project(pid)
+        s = self.summary(p["id"])
+        if s["nodes_ready"] == 0:
+            return Response(503, "Service Unavailable", content_type="text/plain")
+        esc = html.escape
+        rows = "".join(
+            f"<tr><td>{esc(n['metadata']['name'])}</td><td>{'Ready' if node_ready(n) else 'NotReady'}</td>"
+            f"<td>{n['status']['allocatable'].get(GPU, '0')}</td><td>{'yes' if node_validated(n) else 'no'}</td></tr>"
+            for n in self.store.list("nodes", lambda n: self._in(p['id'], n)))
+        deps = "".join(
+            f"<tr><td>{esc(d['metadata']['namespace'])}</td><td>{esc(d['metadata']['name'])}</td>"
+            f"<td>{d.get('status', {}).get('readyReplicas', 0)}/{d['spec'].get('replicas', 1)}</td>"
+            f"<td>{esc(', '.join(c.get('image', '') or ' '.join(c.get('command', [])) for c in d['spec']['template']['spec']['containers']))}</td></tr>"
+            for d in self.store.list("deployments", lambda o: self._in(p['id'], o)))
+        svcs = "".join(
+            f"<tr><td>{esc(o['metadata']['name'])}</td><td>{o['spec'].get('type')}</td><td>{o['spec'].get('clusterIP')}</td>"
+            f"<td>{esc(','.join(i.get('ip', '') for i in o.get('status', {}).get('loadBalancer', {}).get('ingress', [])))}</td>"
+            f"<td>{esc(','.join(str(x['port']) for x in o['spec'].get('ports', [])))}</td></tr>"
+            for o in self.store.list("services", lambda o: self._in(p['id'], o)))
+        body = (f"<html><head><title>Kubernetes Dashboard - {esc(p['name'])}</title></head><body>"
+                f"<h1>kubernetes dashboard</h1><p>environment {esc(p['name'])} ({p['id']})</p>"
+                f"<h2>Nodes</h2><table><tr><th>node</th><th>status</th><th>{GPU}</th><th>validated</th></tr>{rows}</table>"
+                f"<h2>Deployments</h2><table><tr><th>namespace</th><th>name</th><th>ready</th><th>image</th></tr>{deps}</table>"
+                f"<h2>Services</h2><table><tr><th>name</th><th>type</th><th>cluster IP</th><th>external IP</th>"
+                f"<th>ports</th></tr>{svcs}</table>"
+                "<h2>Deploy a containerized app</h2><form id='deploy'>"
+                "<input name='name' placeholder='App name'> <input name='containerImage' placeholder='Container image'> "
+                "<input name='replicas' value='1' size='3'> <input name='port' placeholder='Port'> "
+                "<label><input type='checkbox' name='isExternal'> external</label> "
+                f"<input name='gpus' value='0' size='3'> {GPU} <button>Deploy</button></form>"
+                "<script>document.getElementById('deploy').addEventListener('submit', async (e) => {"
+                "e.preventDefault(); const f = new FormData(e.target); const port = f.get('port');"
+                "const body = {name: f.get('name'), containerImage: f.get('containerImage'),"
+                " replicas: parseInt(f.get('replicas') || '1'), isExternal: f.get('isExternal') === 'on',"
+                " gpuRequirement: parseInt(f.get('gpus') || '0'), namespace: 'default',"
+                " portMappings: port ? [{port: parseInt(port), targetPort: parseInt(port), protocol: 'TCP'}] : []};"
+                "await fetch('api/v1/appdeployment', {method: 'POST', headers: {'Content-Type': 'application/json'},"
+                " body: JSON.stringify(body)}); location.reload(); });</script>"
+                f"<pre>{esc(json.dumps(s, indent=1))}</pre></body></html>")
+        return Response(200, body, content_type="text/html; charset=utf-8")
+
+    async def h_app_deploy(self, req: Request, pid: str):
+        """The dashboard's "Deploy a containerized app" form (kubernetes-dashboard
+        ``POST api/v1/appdeployment``): a Deployment plus, with port mappings, a Service --
+        how the reference's walkthrough launched Ghost (docs/detailed.md:261-283). Like the
+        Rancher 1.x UI the reference used, the dashboard needs no API token."""
+        import shlex
+
+        p = self.project(pid)
+        b = req.json()
+        name = str(b.get("name") or "").strip()
+        image = str(b.get("containerImage") or "").strip()
+        if not name or not image:
+            raise HttpError(422, "name and containerImage are required")
+        ns = b.get("namespace") or "default"
+        labels = {"app": name, **{str(lb["key"]): str(lb["value"]) for lb in b.get("labels") or []}}
+        c = {"name": name, "image": image}
+        if b.get("containerCommand"):
+            c["command"] = shlex.split(str(b["containerCommand"]))
+        if b.get("containerCommandArgs"):
+            c["args"] = shlex.split(str(b["containerCommandArgs"]))
+        if b.get("variables"):
+            c["env"] = [{"name": str(v["name"]), "value": str(v.get("value", ""))} for v in b["variables"]]
+        if int(b.get("gpuRequirement") or 0):
+            c["resources"] = {"limits": {GPU: int(b["gpuRequirement"])}}
+        ports = b.get("portMappings") or []
+        if ports:
+            c["ports"] = [{"containerPort": int(m["targetPort"]), "protocol": m.get("protocol", "TCP")} for m in ports]
+        dep = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": name, "labels": dict(labels)},
+               "spec": {"replicas": int(b.get("replicas", 1)), "selector": {"matchLabels": {"app": name}},
+                        "template": {"metadata": {"labels": labels}, "spec": {"containers": [c]}}}}
+        out = {"deployment": self._strip(self.create(p["id"], "deployments", ns, dep))}
+        if ports:
+            svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": {"app": name}},
+                   "spec": {"type": "LoadBalancer" if b.get("isExternal") else "ClusterIP", "selector": {"app": name},
+                            "ports": [{"name": f"{m.get('protocol', 'TCP').lower()}-{m['port']}-{m['targetPort']}",
+                                       "port": int(m["port"]), "targetPort": int(m["targetPort"]),
+                                       "protocol": m.get("protocol", "TCP")} for m in ports]}}
+            out["service"] = self._strip(self.create(p["id"], "services", ns, svc))
+        return Response(201, out)
+
+    async def h_kubeconfig(self, req: Request, pid: str):
+        p = self.project(pid)
+        server = f"{self.base}/r/projects/{p['id']}/kubernetes"
+        cfg = {"apiVersion": "v1", "kind": "Config", "current-context": p["name"].replace(" ", "-"),
+               "clusters": [{"name": p["name"].replace(" ", "-"), "cluster": {"server": server}}],
+               "users": [{"name": p["name"].replace(" ", "-"), "user": {"token": p["apiToken"]}}],
+               "contexts": [{"name": p["name"].replace(" ", "-"),
+                             "context": {"cluster": p["name"].replace(" ", "-"), "user": p["name"].replace(" ", "-")}}]}
+        if req.q("format") == "json":
+            return cfg
+        import yaml  # local import: only this endpoint needs it
+
+        return Response(200, yaml.safe_dump(cfg, sort_keys=False), content_type="text/yaml")
+
+    async def h_containers(self, req: Request, pid: str):
+        p = self.project(pid)
+        pods = self.store.list("pods", lambda o: self._in(p["id"], o))
+        return {"project": p["id"], "containers": [
+            {"name": o["metadata"]["name"], "namespace": o["metadata"].get("namespace"),
+             "node": o["spec"].get("nodeName"), "phase": o.get("status", {}).get("phase"),
+             "gpus": o["metadata"].get("annotations", {}).get(GPU + "-ids")} for o in pods]}
+
+    # ---- KV -------------------------------------------------------------------------
+    async def h_kv_get(self, req: Request, key: str):
+        wait = float(req.q("wait", "0") or 0)
+        v = await self.store.wait_until(lambda: self.store.get("kv", key), min(wait, 120.0))
+        if not v:
+            raise HttpError(404, f"key {key} not found")
+        return Response(200, v["value"], content_type="text/plain")
+
+    async def h_kv_put(self, req: Request, key: str):
+        self.store.put("kv", key, {"metadata": {"name": key}, "value": req.body.decode()})
+        return Response(201, {"key": key})
+
+    async def h_kv_delete(self, req: Request, key: str):
+        self.store.delete("kv", key)
+        return Response(200, {"key": key, "deleted": True})
+
+    # ---- readiness -----------------------------------------------------------------------
+    @staticmethod
+    def _in(pid: str, obj: dict) -> bool:
+        return obj.get("_project") == pid
+
+    def summary(self, pid: str) -> dict:
+        nodes = self.store.list("nodes", lambda n: self._in(pid, n))
+        pods = self.store.list("pods", lambda o: self._in(pid, o))
+        by_phase: dict[str, int] = {}
+        for o in pods:
+            ph = o.get("status", {}).get("phase", "Pending")
+            by_phase[ph] = by_phase.get(ph, 0) + 1
+        in_use = sum(pod_gpus(o) for o in pods if o.get("spec", {}).get("nodeName")
+                     and o.get("status", {}).get("phase") not in TERMINAL)
+        ready = [n for n in nodes if node_ready(n)]
+        return {
+            "project": pid, "nodes": len(nodes), "nodes_ready": len(ready),
+            "nodes_validated": sum(1 for n in ready if node_validated(n)),
+            "nodes_validation_failed": sum(1 for n in nodes if (_cond(n, "AMDGPUValidated") or {}).get("status") == "False"),
+            "validation_failures": [{"node": n["metadata"]["name"], "reason": c.get("reason"),
+                                     "message": (c.get("message") or "")[:300]}
+                                    for n in nodes for c in [_cond(n, "AMDGPUValidated") or {}] if c.get("status") == "False"],
+            "gpus_capacity": sum(int(n["status"]["capacity"].get(GPU, 0)) for n in nodes),
+            "gpus_allocatable": sum(int(n["status"]["allocatable"].get(GPU, 0)) for n in ready),
+            "gpus_in_use": in_use, "pods_by_phase": by_phase, "resourceVersion": self.store.rv,
+            "node_names": sorted(n["metadata"]["name"] for n in nodes),
+        }
+
+    def _job_state(self, pid: str, ref: str | None) -> str | None:
+        if not ref:
+            return None
+        ns, _, name = ref.rpartition("/")
+        j = self.store.get("jobs", _key(pid, ns or "default", name))
+        if j is None:
+            return "Missing"
+        for c in j.get("status", {}).get("conditions", []):
+            if c["type"] in ("Complete", "Failed") and c["status"] == "True":
+                return c["type"]
+        return "Running"
+
+    async def h_cluster_status(self, req: Request):
+        p = self.project(req.q("project"))
+        s = self.summary(p["id"])
+        s["job"] = self._job_state(p["id"], req.q("job"))
+        return s
+
+    async def h_cluster_wait(self, req: Request):
+        """Long-poll until `nodes` Ready (+validated) with >= `gpus` allocatable (+ job done)."""
+        pid = req.q("project")
+        want_nodes = int(req.q("nodes", "1"))
+        want_gpus = int(req.q("gpus", "0"))
+        validated = req.q("validated", "1") not in ("0", "false")
+        job = req.q("job")
+        timeout = min(float(req.q("timeout", "30")), 300.0)
+
+        def check():
+            try:
+                p = self.project(pid)
+            except HttpError:
+                return None
+            s = self.summary(p["id"])
+            js = self._job_state(p["id"], job)
+            failed = s["nodes_validation_failed"] > 0 or js in ("Failed", "Missing")
+            ok = (s["nodes_ready"] >= want_nodes and (not validated or s["nodes_validated"] >= want_nodes)
+                  and s["gpus_allocatable"] >= want_gpus and (js in (None, "Complete")))
+            if ok or failed:
+                s.update(ready=ok, failed=failed and not ok, job=js)
+                return s
+            return None
+
+        res = await self.store.wait_until(check, timeout)
+        if res:
+            trace("cp", f"cluster wait -> ready={res.get('ready')}")
+            return res
+        p = self.project(pid)
+        s = self.summary(p["id"])
+        s.update(ready=False, failed=False, timed_out=True, job=self._job_state(p["id"], job))
+        return Response(200, s)
+
+    async def h_cp_events(self, req: Request):
+        since = int(req.q("resourceVersion", "0") or 0)
+        wait = min(float(req.q("timeoutSeconds", "0") or 0), 60.0)
+        ev = await self.store.wait_events(since, None, wait)
+        return {"resourceVersion": self.store.rv,
+                "events": [{"type": e["type"], "kind": e["kind"], "name": e["object"].get("metadata", {}).get("name"),
+                            "resourceVersion": e["resourceVersion"]} for e in ev]}
+
