@@ -176,3 +176,53 @@ def test_baremetal_wrong_key_is_refused(bm, tmp_path):
     r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"],
                        cwd=ws, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "Permission denied" in (r.stdout + r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_baremetal_bringup_over_ssh_on_a_real_gpu(tmp_path):
+    """The remote path with the real validation payload: one inventory host (this GPU box behind
+    the fake ssh) with its real MI355X(s); the tk8s distribution is pushed, the burn-in
+    (tk8s-hsaprobe) and the agent run through ssh sessions, the validation pod reuses the
+    burn-in's result with tk8s-reuse, and the node is Ready with its GPU validated."""
+    from tritonk8ssupervisor_amd.models.hostinfo import discover
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    n = discover().count
+    if n < 1:
+        pytest.skip("no GPU")
+    ws = tmp_path / "ws"
+    ws.mkdir()
+    init_workspace(ws)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, ws / f)
+    keydir = tmp_path / "keys"
+    keydir.mkdir()
+    subprocess.run(["ssh-keygen", "-q", "-t", "ed25519", "-N", "", "-f", str(keydir / "id_ed25519")], check=True)
+    root = tmp_path / "hosts"
+    h = root / "127.0.7.20"
+    (h / ".ssh").mkdir(parents=True)
+    (h / ".ssh" / "authorized_keys").write_text((keydir / "id_ed25519.pub").read_text())
+    keep = {k: v for k, v in os.environ.items() if k.startswith(("HSA_", "ROCM", "HIP_", "LD_LIBRARY_PATH"))}
+    (h / ".env").write_text("".join(f"{k}={v}\n" for k, v in keep.items()))
+    inv = {"ssh": {"user": "root", "key": str(keydir / "id_ed25519")}, "python": sys.executable,
+           "hosts": [{"name": "box", "address": "127.0.7.20", "gpus": n}]}
+    (ws / "inventory.yml").write_text(json.dumps(inv))
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_BACKEND="baremetal", TK8S_PLATFORM="tk8s",
+               TK8S_SSH=f"{sys.executable} {REPO / 'tests' / 'fakessh.py'}", FAKESSH_ROOT=str(root),
+               TK8S_SSH_CONNECT_RETRIES="0")
+    try:
+        r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--timeout", "120"],
+                           cwd=ws, env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1
+        v = s["validation"]["kubenode1"]
+        assert float(v["hbm-write-gbps"]) > 1000.0
+        burn = next(root.glob("*/tk8s/machines/kubenode1/run/gpu-burnin.json.consumed"))
+        res = json.loads(burn.read_text())
+        assert res["ok"] and res["md5"]["digest"] == res["md5_expected"]
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, timeout=120)
+    assert not list(root.glob("*/tk8s/machines/*"))
