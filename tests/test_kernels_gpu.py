@@ -545,3 +545,34 @@ def test_multi_gpu_hsaprobe_peer_matrix(nat):
 
     rep = xgmi.link_report(out)
     assert rep["pulls"] == n * (n - 1) and not rep["degraded"], rep
+
+
+@pytest.mark.skipif(_gpu_count() < 2, reason="needs >= 2 MI355X (xGMI)")
+def test_multi_gpu_degraded_link_keeps_its_nodes_not_ready(tmp_path):
+    """N7 before Ready on real links: the host burn-in pulls every ordered pair; a link reported at
+    a tenth of its measured rate (TK8S_FAULTS=xgmi.degrade@0-1:0.1, applied to the measurement)
+    keeps both of its nodes NotReady with XGMILinkDegraded, and setup fails fast."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable)
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "2", "--yes", "--json", "--port", "0", "--timeout", "120",
+                            "--rccl", "off"], cwd=tmp_path, env={**env, "TK8S_FAULTS": "xgmi.degrade@0-1:0.1"},
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 2 and "XGMILinkDegraded" in r.stderr, r.stdout[-2000:] + r.stderr[-2000:]
+        out = subprocess.run(["./kubectl", "get", "nodes"], cwd=tmp_path, env=env, capture_output=True,
+                             text=True).stdout
+        assert out.count("NotReady") == 2, out
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
