@@ -87,11 +87,14 @@ def _daemon_pids(root: Path) -> list[int]:
 def test_baremetal_bringup_over_ssh(bm):
     ws, root, env = bm
     t = time.monotonic()
-    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "5", "--rccl", "off"],
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "5"],
                        cwd=ws, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     s = json.loads(r.stdout.strip().splitlines()[-1])
     assert s["nodes"] == 5 and s["gpus_allocatable"] == 5 and s["nodes_validated"] == 5
+    # the fabric check ran across both hosts: one rank per GPU, on the machines' own installs
+    assert s["rccl"]["ok"] and s["rccl"]["nranks"] == 5
+    assert len({r["node"] for r in s["rccl"]["rank_results"]}) == 5
     assert time.monotonic() - t < 180
     cfg = (ws / "config").read_text()
     assert "TK8S_BACKEND=baremetal" in cfg and "HOST_PACKAGE=" in cfg
