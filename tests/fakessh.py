@@ -18,6 +18,7 @@ appended to ``<FAKESSH_ROOT>/calls.jsonl`` (host, user, options, whether a key w
 """
 import json
 import os
+import re
 import subprocess
 import sys
 import zlib
@@ -97,12 +98,27 @@ def main(argv: list[str]) -> int:
     if not command:
         print("fakessh: interactive sessions are not supported", file=sys.stderr)
         return 255
+    # A "fake root" host (a .fakeroot file; tests/fakeroot/) runs with a PATH of ONLY its own bin/
+    # -- stand-ins for apt-get, kubeadm, systemctl ... and safe coreutils -- and $TK8S_SYSROOT
+    # pointing into the host directory: the kubeadm roles run for real against simulated tools.
+    fakeroot = (hd / ".fakeroot").exists()
+    if fakeroot:
+        env["PATH"] = str(hd / "bin")
+        env["TK8S_SYSROOT"] = str(hd / "sysroot")
+        # paths under the staging root (literal, or through $TK8S_SYSROOT) are the fake host's own
+        sysroot_free = re.sub(r"\$\{?TK8S_SYSROOT(:-)?\}?/[^\s'\"]*", "",
+                              re.sub(re.escape(str(hd / "sysroot")) + r"/[^\s'\"]*", "", command))
+    else:
+        sysroot_free = command
     # The "hosts" are directories of THIS machine: anything that would change the machine itself
-    # (package managers, kernel modules, services, kubeadm) is refused, never run.
+    # (package managers, kernel modules, services, kubeadm) is refused, never run -- on a fake
+    # root only system PATHS are checked (the tools there are the stand-ins).
     for word in ("apt-get", "dpkg ", "modprobe", "systemctl", "kubeadm", "swapoff", "sysctl ", "apt-mark",
                  "/etc/apt", "/etc/kubernetes", "/etc/containerd", "/etc/modules-load.d", "/etc/sysctl.d",
                  "/etc/fstab", "/opt/tk8s", "/root/.kube"):
-        if word in command:
+        if fakeroot and not word.startswith("/"):
+            continue
+        if word in sysroot_free:
             print(f"fakessh: refusing a system-changing command on a fake host ({word.strip()})", file=sys.stderr)
             return 126
     r = subprocess.run(["bash", "-c", command], cwd=hd, env=env)

@@ -153,3 +153,104 @@ def test_kubeadm_readiness_from_kubectl(tmp_path, monkeypatch):
     s.playbook_result.hostvars["kubemaster"]["tk8s_nodes"]["stdout"] = json.dumps({"items": items})
     with pytest.raises(SetupError, match="1/2 workers Ready"):
         s.wait_ready()
+
+
+# ---- the kubeadm platform for real, against simulated system tools ----------------------------------
+SAFE_TOOLS = ("bash", "sh", "tar", "gzip", "mkdir", "cat", "mv", "rm", "ln", "chmod", "install", "grep", "sed", "cut",
+              "md5sum", "base64", "stat", "readlink", "head", "tail", "find", "sleep", "date", "setsid", "kill", "env",
+              "dirname", "basename", "id", "hostname", "uname", "nproc", "ip", "awk", "touch", "wc", "sort", "xargs",
+              "tr", "cp", "ls", "pwd", "test", "true", "false", "printf", "echo")
+FAKE_TOOLS = ("apt-get", "apt-mark", "dpkg-query", "modprobe", "sysctl", "swapoff", "systemctl", "containerd", "curl",
+              "kubeadm", "kubectl")
+
+
+def _fake_root_host(root: Path, addr: str, pubkey: str, state: Path) -> Path:
+    import sys
+
+    h = root / addr
+    (h / ".ssh").mkdir(parents=True)
+    (h / ".ssh" / "authorized_keys").write_text(pubkey)
+    (h / ".fakeroot").touch()
+    (h / ".env").write_text(f"FAKE_K8S_STATE={state}\n")
+    (h / "sysroot" / "etc").mkdir(parents=True)
+    (h / "sysroot" / "etc" / "fstab").write_text("/dev/sda1 / ext4 defaults 0 1\n/swap.img none swap sw 0 0\n")
+    b = h / "bin"
+    b.mkdir()
+    for t in SAFE_TOOLS:
+        real = shutil.which(t)
+        if real:
+            (b / t).symlink_to(real)
+    (b / "python3").symlink_to(sys.executable)
+    tool = REPO / "tests" / "fakeroot" / "faketool.py"
+    for t in FAKE_TOOLS:  # one wrapper per tool name; the stand-in dispatches on FAKETOOL_NAME
+        (b / t).write_text(f"#!/bin/sh\nFAKETOOL_NAME={t} exec {sys.executable} {tool} \"$@\"\n")
+        (b / t).chmod(0o755)
+    return h
+
+
+def test_kubeadm_platform_end_to_end_against_simulated_tools(tmp_path):
+    """./setup.sh --backend baremetal --platform kubeadm for real: every task of the four plays runs
+    over ssh on two fake-root hosts whose apt-get/kubeadm/kubectl/systemctl/... are stand-ins
+    (tests/fakeroot/faketool.py) and whose system paths live under a staging root -- so the roles'
+    control flow (facts, registered results, the join command handed from master to hosts, the
+    readiness waits, the RCCL-tests DaemonSet check) is exercised end to end, then torn down with
+    kubeadm reset."""
+    import subprocess
+    import sys
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    ws = tmp_path / "ws"
+    ws.mkdir()
+    init_workspace(ws)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, ws / f)
+    # the staging root of each host, from its login HOME (ansible_env, gathered in play 1)
+    gv = ws / "ansible" / "group_vars" / "all.yml"
+    gv.write_text(gv.read_text().replace('tk8s_sysroot: ""', 'tk8s_sysroot: "{{ ansible_env.HOME }}/sysroot"'))
+    keydir = tmp_path / "keys"
+    keydir.mkdir()
+    subprocess.run(["ssh-keygen", "-q", "-t", "ed25519", "-N", "", "-f", str(keydir / "id_ed25519")], check=True)
+    root = tmp_path / "hosts"
+    state = tmp_path / "cluster.json"
+    hosts = {"mi355x-a": "127.0.7.30", "mi355x-b": "127.0.7.31", "mi355x-c": "127.0.7.32"}
+    for addr in hosts.values():
+        _fake_root_host(root, addr, (keydir / "id_ed25519.pub").read_text(), state)
+    inv = {"ssh": {"user": "root", "key": str(keydir / "id_ed25519")}, "python": sys.executable,
+           "hosts": [{"name": "mi355x-a", "address": hosts["mi355x-a"], "gpus": 0, "role": "master"},
+                     {"name": "mi355x-b", "address": hosts["mi355x-b"], "gpus": 1},
+                     {"name": "mi355x-c", "address": hosts["mi355x-c"], "gpus": 1}]}
+    (ws / "inventory.yml").write_text(json.dumps(inv))
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_BACKEND="baremetal",
+               TK8S_SSH=f"{sys.executable} {REPO / 'tests' / 'fakessh.py'}", FAKESSH_ROOT=str(root),
+               TK8S_SSH_CONNECT_RETRIES="0")
+    env.pop("TK8S_FAKE_GPUS", None)
+    r = subprocess.run(["./setup.sh", "--platform", "kubeadm", "--yes", "--json", "--nodes", "2", "--timeout", "60"],
+                       cwd=ws, env=env, capture_output=True, text=True, timeout=300)
+    try:
+        assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["platform"] == "kubeadm" and s["nodes"] == 2 and s["gpus_allocatable"] == 2
+        assert s["rccl"]["ok"] and len(s["rccl"]["pods"]) == 2
+        assert s["api"] == f"https://{hosts['mi355x-a']}:6443"
+        assert (ws / "ansible" / "tmp" / "kubeconfig").read_text().startswith("apiVersion: v1")
+        assert (ws / "ansible" / "tmp" / "kubernetes_environment.id").read_text() == json.loads(state.read_text())["uid"]
+        log_a = (root / hosts["mi355x-a"] / "sysroot" / "var" / "log" / "fake-tools.log").read_text()
+        log_b = (root / hosts["mi355x-b"] / "sysroot" / "var" / "log" / "fake-tools.log").read_text()
+        log_c = (root / hosts["mi355x-c"] / "sysroot" / "var" / "log" / "fake-tools.log").read_text()
+        assert "kubeadm init --apiserver-advertise-address 127.0.7.30" in log_a
+        assert "amdgpu-dkms" in log_b and "amdgpu-dkms" not in log_a  # the GPU driver on GPU hosts only
+        for log in (log_b, log_c):  # every worker on its own host joined with the master's token
+            assert log.count("kubeadm join 127.0.7.30:6443 --token abcdef.0123456789abcdef") == 1
+        assert (root / hosts["mi355x-b"] / "sysroot" / "dev" / "kfd").exists()
+        cfg = (root / hosts["mi355x-b"] / "sysroot" / "etc" / "containerd" / "config.toml").read_text()
+        assert "SystemdCgroup = true" in cfg
+        assert "# /swap.img none swap" in (root / hosts["mi355x-b"] / "sysroot" / "etc" / "fstab").read_text()
+        assert (root / hosts["mi355x-b"] / "sysroot" / "etc" / "apt" / "sources.list.d" / "rocm.list").exists()
+        nodes = json.loads(state.read_text())["nodes"]
+        assert nodes["kubenode1"]["gpus"] + nodes["kubenode2"]["gpus"] == 2
+        assert nodes["kubenode1"]["labels"]["amd.com/gpu.family"] == "gfx950"
+    finally:
+        c = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, text=True, timeout=120)
+    assert c.returncode == 0 and "kubeadm reset on kubenode1: ok" in c.stdout, c.stdout + c.stderr
+    assert not (root / hosts["mi355x-b"] / "sysroot" / "etc" / "kubernetes" / "kubelet.conf").exists()

@@ -262,6 +262,8 @@ class Setup:
         if self.platform == "kubeadm" and self.provider.colocated:
             raise SetupError("error: the kubeadm platform installs ROCm, amdgpu-dkms, containerd and Kubernetes as root on "
                              "its machines: use machines you own (--backend baremetal with an SSH inventory, or triton)")
+        if self.platform == "kubeadm" and hasattr(self.provider, "whole_hosts"):
+            self.provider.whole_hosts = True  # a kubelet per host: machines are whole hosts, not slices
         return cfg
 
     def _machine_booted(self, address: str, m: Machine) -> None:
@@ -933,7 +935,8 @@ def _set_ini_value(path: Path, key: str, value: str) -> None:
 
 # ---- teardown --------------------------------------------------------------------------------
 KUBEADM_RESET = ("kubeadm reset -f --cri-socket unix:///run/containerd/containerd.sock; "
-                 "rm -rf /etc/cni/net.d /root/.kube /etc/kubernetes/tk8s; systemctl restart containerd || true")
+                 'rm -rf "${TK8S_SYSROOT:-}/etc/cni/net.d" "${TK8S_SYSROOT:-}/root/.kube" '
+                 '"${TK8S_SYSROOT:-}/etc/kubernetes/tk8s"; systemctl restart containerd || true')
 
 
 def _kubeadm_reset(ws: "Workspace", provider, out) -> None:

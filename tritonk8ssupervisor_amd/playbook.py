@@ -132,6 +132,7 @@ class Playbook:
         self._play = ""
         self._defaults: dict = {}
         self._play_env: dict = {}
+        self._gv_cache: dict[str, dict] = {}
 
     def _read_cfg(self) -> dict:
         p = self.dir / "ansible.cfg"
@@ -277,7 +278,7 @@ class Playbook:
             self._play = str(name)
             self._play_env = play.get("environment") or {}
             if play.get("gather_facts", True) and not self._facts_done(hosts):
-                tasks = [{"name": "Gathering Facts", "setup": {}}] + tasks
+                tasks = [{"name": "Gathering Facts", "setup": {}, "_facts": True}] + tasks
             alive = list(hosts)
             failures: list[str] = []
             for task in tasks:
@@ -366,16 +367,17 @@ class Playbook:
                 "tk8s_home": m.home or str(Path(__file__).resolve().parents[1])}
 
     def _group_vars(self, host: Host) -> dict:
-        cache = self.__dict__.setdefault("_gv_cache", {})
         out: dict = {}
-        for g in ["all", *host.groups]:
-            if g not in cache:
-                cache[g] = {}
-                for f in (self.dir / "group_vars" / f"{g}.yml", self.dir / "group_vars" / f"{g}.yaml"):
-                    if f.exists():
-                        cache[g] = yamlio.load(f.read_text()) or {}
-                        break
-            out.update(cache[g])
+        with self._trace_lock:  # hosts run in parallel: load each group's file exactly once
+            for g in ["all", *host.groups]:
+                if g not in self._gv_cache:
+                    data = {}
+                    for f in (self.dir / "group_vars" / f"{g}.yml", self.dir / "group_vars" / f"{g}.yaml"):
+                        if f.exists():
+                            data = yamlio.load(f.read_text()) or {}
+                            break
+                    self._gv_cache[g] = data
+                out.update(self._gv_cache[g])
         return out
 
     def _facts_done(self, hosts: list[Host]) -> bool:
@@ -400,7 +402,8 @@ class Playbook:
 
         extra = task.get("args")
         args = templating.render(self._args(mod, raw, extra), v)
-        env = {**templating.render(self._play_env, v), **templating.render(task.get("environment") or {}, v)}
+        play_env = self._play_env if not task.get("_facts") else {}  # facts come first: nothing to render yet
+        env = {**templating.render(play_env, v), **templating.render(task.get("environment") or {}, v)}
         with self._trace_lock:
             self.trace.append({"play": self._play, "host": host.name, "task": task.get("name", ""),
                                "module": mod, "args": args, "local": bool(local), "delegate": deleg.name if deleg else None})

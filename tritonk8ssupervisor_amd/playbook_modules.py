@@ -176,10 +176,11 @@ def m_apt(args, *, ctx, target, local, env, check, **_):
             "msg": "" if rc == 0 else f"apt failed rc={rc}: {out.strip()[-500:]}"}
 
 
-def m_apt_repository(args, *, ctx, target, local, check, **_):
+def m_apt_repository(args, *, ctx, target, local, env, check, **_):
     repo = str(args["repo"])
     name = str(args.get("filename") or re.sub(r"[^A-Za-z0-9]+", "_", repo.split("//", 1)[-1]).strip("_")[:60])
-    dest = f"/etc/apt/sources.list.d/{name}.list"
+    # TK8S_SYSROOT (the plays' environment): the staging root the fake hosts of the tests use
+    dest = f"{(env or {}).get('TK8S_SYSROOT', '')}/etc/apt/sources.list.d/{name}.list"
     fs = _fs(ctx, target, local)
     if str(args.get("state", "present")) == "absent":
         changed = fs.stat(dest)["exists"]
@@ -294,6 +295,9 @@ echo "hostname=$(hostname -s 2>/dev/null || uname -n)"
 echo "ipv4=$(ip -4 route get 1.1.1.1 2>/dev/null | sed -n 's/.* src \([0-9.]*\).*//p' | head -n1)"
 echo "processor_vcpus=$(nproc 2>/dev/null)"
 echo "memtotal_mb=$(awk '/MemTotal/ {print int($2/1024)}' /proc/meminfo 2>/dev/null)"
+echo "env_HOME=$HOME"
+echo "env_USER=${USER:-$(id -un 2>/dev/null)}"
+echo "env_PATH=$PATH"
 """
 
 
@@ -308,6 +312,7 @@ def m_setup(args, *, ctx, target, local, **_):
              "ansible_memtotal_mb": int(kv.get("memtotal_mb") or 0)}
     ip = kv.get("ipv4") or target.address
     facts["ansible_default_ipv4"] = {"address": ip}
+    facts["ansible_env"] = {k[4:]: v for k, v in kv.items() if k.startswith("env_")}
     return {"ansible_facts": facts, "changed": False, "failed": rc != 0 and not out.strip()}
 
 
@@ -423,7 +428,8 @@ def m_file(args, *, ctx, target, local, check, **_):
             fs.touch(p)
     elif state == "link":
         src = str(args["src"])
-        cmd = f"ln -sfn {shlex.quote(src)} {shlex.quote(str(fs.path(p)))}"
+        q = shlex.quote(str(fs.path(p)))
+        cmd = f'mkdir -p "$(dirname -- {q})" && ln -sfn {shlex.quote(src)} {q}'
         rc, cur = _sh(ctx, target, local, f"readlink -- {shlex.quote(str(fs.path(p)))}")
         changed = cur.strip() != src
         if changed and not check:

@@ -192,6 +192,10 @@ class BareMetalProvider(Provider):
         return "bm-1gpu" if any(h["gpus"] for h in self.inventory()["hosts"]) else "bm-cpu"
 
     # ---- placement --------------------------------------------------------------------------
+    # One machine per host (the kubeadm platform: one kubelet per OS, which owns all the host's
+    # GPUs); False = machines are slices of hosts (the tk8s platform's node agents).
+    whole_hosts = False
+
     def _place(self, alloc: dict, name: str, role: str, ngpus: int) -> tuple[dict, list[int]]:
         hosts = self.inventory()["hosts"]
         used: dict[str, set] = {h["name"]: set() for h in hosts}
@@ -199,6 +203,15 @@ class BareMetalProvider(Provider):
         for rec in alloc.get("machines", {}).values():
             used.setdefault(rec["host"], set()).update(rec.get("gpus", []))
             load[rec["host"]] = load.get(rec["host"], 0) + 1
+        if self.whole_hosts:
+            free = [h for h in hosts if load[h["name"]] == 0 and len(h["gpus"]) >= ngpus]
+            if role == "master":
+                free.sort(key=lambda h: (h["role"] != "master", len(h["gpus"])))  # the master host, else the smallest
+            if not free:
+                raise ProvisionError(f"{name}: every machine needs a host of its own here (one kubelet per host) and no "
+                                     f"free host has {ngpus} GPU(s); add hosts to the inventory")
+            h = free[0]
+            return h, ([] if role == "master" else list(h["gpus"]))
         if role == "master":
             h = next((h for h in hosts if h["role"] == "master"), hosts[0])
             return h, []

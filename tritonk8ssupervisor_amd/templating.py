@@ -403,6 +403,16 @@ def _evaluate_subset(expr: str, variables: dict, strict: bool = True) -> Any:
 _JINJA = {}
 
 
+def _flatten(xs, levels=None):
+    out = []
+    for x in xs:
+        if isinstance(x, (list, tuple)) and (levels is None or levels > 0):
+            out.extend(_flatten(x, None if levels is None else levels - 1))
+        else:
+            out.append(x)
+    return out
+
+
 def _jinja_env(strict: bool):
     env = _JINJA.get(strict)
     if env is not None:
@@ -423,6 +433,7 @@ def _jinja_env(strict: bool):
         "to_yaml": lambda v: __import__("yaml").safe_dump(v, default_flow_style=False),
         "from_yaml": lambda s: __import__("yaml").safe_load(s),
         "quote": lambda s: __import__("shlex").quote(str(s)),
+        "flatten": _flatten,
     })
     for name in ("changed", "failed", "failure", "succeeded", "success", "skipped"):
         env.tests[name] = (lambda n: (lambda v: _jinja_test(n, v)))(name)
@@ -486,6 +497,13 @@ def render_text(text: str, variables: dict, strict: bool = True) -> str:
 _TPL = re.compile(r"\{\{(.*?)\}\}", re.S)
 
 
+def _single(text: str):
+    """The match when ``text`` is exactly ONE ``{{ expr }}`` (then the value keeps its type);
+    ``{{ a }}{{ b }}`` is two templates concatenated, not one expression."""
+    m = _TPL.fullmatch(text.strip())
+    return m if m and "{{" not in m.group(1) and "}}" not in m.group(1) else None
+
+
 def render(value: Any, variables: dict, strict: bool = True) -> Any:
     """Render `{{ }}` templates in strings (recursively in lists/dicts). A string that is a single
     template returns the native value (so lists/dicts survive)."""
@@ -497,10 +515,20 @@ def render(value: Any, variables: dict, strict: bool = True) -> Any:
         return value
     if "{%" in value:  # statements: real Jinja2
         return render_text(value, variables, strict)
-    m = _TPL.fullmatch(value.strip())
+    m = _single(value)
     if m:
-        return evaluate(m.group(1), variables, strict)
-    return _TPL.sub(lambda mm: _to_str(evaluate(mm.group(1), variables, strict)), value)
+        out = evaluate(m.group(1), variables, strict)
+    else:
+        out = _TPL.sub(lambda mm: _to_str(evaluate(mm.group(1), variables, strict)), value)
+    # a variable whose value is itself a template (group_vars: `x: "{{ y }}/z"`) renders in turn,
+    # as Ansible's lazy templating does (bounded: a self-reference cannot loop)
+    for _ in range(8):
+        if not (isinstance(out, str) and "{{" in out):
+            break
+        m = _single(out)
+        out = evaluate(m.group(1), variables, strict) if m else \
+            _TPL.sub(lambda mm: _to_str(evaluate(mm.group(1), variables, strict)), out)
+    return out
 
 
 def _to_str(v: Any) -> str:
@@ -516,7 +544,7 @@ def test(expr: Any, variables: dict) -> bool:
     if isinstance(expr, list):
         return all(test(e, variables) for e in expr)
     s = str(expr).strip()
-    m = _TPL.fullmatch(s)
+    m = _single(s)
     if m:
         s = m.group(1)
     v = evaluate(s, variables)
