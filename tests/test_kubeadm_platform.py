@@ -250,6 +250,12 @@ def test_kubeadm_platform_end_to_end_against_simulated_tools(tmp_path):
         nodes = json.loads(state.read_text())["nodes"]
         assert nodes["kubenode1"]["gpus"] + nodes["kubenode2"]["gpus"] == 2
         assert nodes["kubenode1"]["labels"]["amd.com/gpu.family"] == "gfx950"
+        st = json.loads(subprocess.run(["./tk8s", "status", "--json"], cwd=ws, env=env, capture_output=True,
+                                       text=True, timeout=60).stdout)
+        assert st["cluster"]["nodes_ready"] == 3 and st["cluster"]["gpus_allocatable"] == 2, st
+        k = subprocess.run(["./kubectl", "get", "nodes"], cwd=ws, env={**env, "PATH": "/usr/bin:/bin"},
+                           capture_output=True, text=True, timeout=60)
+        assert k.returncode == 1 and "KUBECONFIG=" in k.stderr and "ansible/tmp/kubeconfig" in k.stderr
     finally:
         c = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, text=True, timeout=120)
     assert c.returncode == 0 and "kubeadm reset on kubenode1: ok" in c.stdout, c.stdout + c.stderr

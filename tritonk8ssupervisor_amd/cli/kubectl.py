@@ -258,6 +258,32 @@ def _device_line(d: dict) -> str:
     return line
 
 
+def _platform(workdir: str) -> str:
+    try:
+        for line in (Path(workdir) / "config").read_text().splitlines():
+            if line.startswith("TK8S_PLATFORM="):
+                return line.split("=", 1)[1].strip().strip('"')
+    except OSError:
+        pass
+    return "tk8s"
+
+
+def _real_kubectl(argv: list[str], kubeconfig: Path) -> int:
+    """The kubeadm platform is a real Kubernetes: hand the command to the real kubectl with the
+    kubeconfig the kubeadmmaster role fetched (ansible/tmp/kubeconfig)."""
+    import shutil
+    import subprocess
+
+    here = Path(__file__).resolve().parents[2]
+    exe = next((c for c in (shutil.which("kubectl", path=p) for p in os.environ.get("PATH", "").split(os.pathsep))
+                if c and Path(c).resolve().parent != here), None)
+    if exe is None:
+        print(f"this cluster runs real Kubernetes (--platform kubeadm): install kubectl and run\n"
+              f"    KUBECONFIG={kubeconfig} kubectl {' '.join(argv)}", file=sys.stderr)
+        return 1
+    return subprocess.run([exe, *argv], env={**os.environ, "KUBECONFIG": str(kubeconfig)}).returncode
+
+
 def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap = argparse.ArgumentParser(prog="kubectl")
     ap.add_argument("--kubeconfig")
@@ -281,6 +307,9 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
+    wd = workdir or os.environ.get("TK8S_WORKDIR", os.getcwd())
+    if "--kubeconfig" not in argv and not os.environ.get("KUBECONFIG") and _platform(wd) == "kubeadm":
+        return _real_kubectl(argv, Path(wd) / "ansible" / "tmp" / "kubeconfig")
     command: list[str] = []
     if "--" in argv:  # kubectl exec POD -- CMD ARGS...
         command = argv[argv.index("--") + 1:]

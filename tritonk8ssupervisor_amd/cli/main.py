@@ -83,7 +83,27 @@ def cmd_status(args) -> int:
     st = ws.state()
     out = {"completed": st.get("completed", []), "timings": st.get("timings", {}), "summary": st.get("summary")}
     summ = st.get("summary") or {}
-    if summ.get("api"):
+    if summ.get("platform") == "kubeadm":  # a real Kubernetes: ask its API server through the master
+        from ..config import read_config
+        from ..orchestrator import MachineExecutor
+        from ..provision import Engine
+
+        try:
+            cfg = read_config(ws.config)
+            prov = _provider(args)
+            machines = Engine(ws.tf, prov).machines()
+            rc, text = MachineExecutor(prov, machines).exec(
+                cfg.RANCHER_MASTER_HOSTNAME, "kubectl --kubeconfig ${TK8S_SYSROOT:-}/etc/kubernetes/admin.conf get nodes -o json",
+                timeout=60)
+            items = json.loads(text)["items"] if rc == 0 else []
+            ready = [n for n in items if any(c.get("type") == "Ready" and c.get("status") == "True"
+                                             for c in n["status"].get("conditions", []))]
+            out["cluster"] = {"nodes": len(items), "nodes_ready": len(ready), "nodes_validated": len(ready),
+                              "gpus_allocatable": sum(int(n["status"].get("allocatable", {}).get("amd.com/gpu", 0) or 0)
+                                                      for n in ready), "gpus_in_use": None}
+        except Exception as e:  # noqa: BLE001 - reporting only
+            out["cluster"] = {"error": str(e)}
+    elif summ.get("api"):
         from ..controlplane.client import Client
 
         try:
@@ -100,8 +120,11 @@ def cmd_status(args) -> int:
         if c and "error" not in c:
             print(f"nodes: {c['nodes_ready']}/{c['nodes']} Ready, {c['nodes_validated']} validated; "
                   f"amd.com/gpu allocatable {c['gpus_allocatable']} (in use {c['gpus_in_use']})")
-        if summ.get("rccl"):
-            print(f"last RCCL all-reduce: peak busbw {summ['rccl']['peak_busbw_gbps']:.1f} GB/s over {summ['rccl']['nranks']} GPU(s)")
+        r = summ.get("rccl") or {}
+        if r.get("peak_busbw_gbps") is not None:
+            print(f"last RCCL all-reduce: peak busbw {r['peak_busbw_gbps']:.1f} GB/s over {r['nranks']} GPU(s)")
+        elif r:
+            print(f"RCCL-tests DaemonSet: {'ok' if r.get('ok') else 'FAILED'} on {len(r.get('pods', []))} node(s)")
     return 0
 
 

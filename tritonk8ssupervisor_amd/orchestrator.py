@@ -740,6 +740,9 @@ class Setup:
         cfg = read_config(ws.config)
         export_vars(cfg)
         self.cfg = cfg
+        self.platform = cfg.TK8S_PLATFORM or "tk8s"
+        if self.platform == "kubeadm" and hasattr(self.provider, "whole_hosts"):
+            self.provider.whole_hosts = True
         old = int(cfg.KUBERNETES_NUMBER_OF_NODES)
         if int(n) == old:
             self.out(f"{old} node(s) already; nothing to do")
@@ -782,6 +785,18 @@ class Setup:
 
     def _drain_and_delete(self, names: list[str]) -> None:
         from .controlplane.client import ApiError, client_from_kubeconfig
+
+        if self.platform == "kubeadm":  # a real Kubernetes: kubectl drain on the master, kubeadm reset on the node
+            machines = self.engine.machines()
+            for node in names:
+                rc, text = self._master_exec(
+                    f"kubectl --kubeconfig ${{TK8S_SYSROOT:-}}/etc/kubernetes/admin.conf drain {node} --ignore-daemonsets "
+                    f"--delete-emptydir-data --force --timeout=120s && kubectl --kubeconfig "
+                    f"${{TK8S_SYSROOT:-}}/etc/kubernetes/admin.conf delete node {node}", timeout=300)
+                self.out(f"    node/{node} {'drained and deleted' if rc == 0 else 'drain failed: ' + text.strip()[-200:]}")
+                if node in machines:
+                    self.provider.exec(machines[node], KUBEADM_RESET, timeout=300)
+            return
 
         c = self._client()
         pid = self.project_id()
