@@ -151,6 +151,13 @@ def kubectl(args):
             d["nodes"][a[2]]["labels"][k] = v
             print(f"node/{a[2]} labeled")
             return 0
+        if a[:1] == ["drain"]:
+            print(f"node/{a[1]} drained")
+            return 0
+        if a[:2] == ["delete", "node"]:
+            d["nodes"].pop(a[2], None)
+            print(f'node "{a[2]}" deleted')
+            return 0
         if a[:1] == ["wait"]:
             for n in d["nodes"]:
                 print(f"node/{n} condition met")

@@ -256,7 +256,17 @@ def test_kubeadm_platform_end_to_end_against_simulated_tools(tmp_path):
         k = subprocess.run(["./kubectl", "get", "nodes"], cwd=ws, env={**env, "PATH": "/usr/bin:/bin"},
                            capture_output=True, text=True, timeout=60)
         assert k.returncode == 1 and "KUBECONFIG=" in k.stderr and "ansible/tmp/kubeconfig" in k.stderr
+        # shrink: kubenode2 is drained and deleted on the master, reset on its host, its machine destroyed
+        sc = subprocess.run(["./tk8s", "scale", "1", "--json"], cwd=ws, env=env, capture_output=True, text=True,
+                            timeout=300)
+        assert sc.returncode == 0, sc.stdout[-3000:] + sc.stderr[-2000:]
+        assert json.loads(sc.stdout.strip().splitlines()[-1])["nodes"] == 1
+        assert "kubenode2" not in json.loads(state.read_text())["nodes"]
+        gone = next(h for h in ("mi355x-b", "mi355x-c")
+                    if not list((root / hosts[h]).glob("tk8s/machines/kubenode*")))
+        assert "kubeadm reset -f" in (root / hosts[gone] / "sysroot" / "var" / "log" / "fake-tools.log").read_text()
     finally:
         c = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, text=True, timeout=120)
     assert c.returncode == 0 and "kubeadm reset on kubenode1: ok" in c.stdout, c.stdout + c.stderr
-    assert not (root / hosts["mi355x-b"] / "sysroot" / "etc" / "kubernetes" / "kubelet.conf").exists()
+    for h in ("mi355x-b", "mi355x-c"):
+        assert not (root / hosts[h] / "sysroot" / "etc" / "kubernetes" / "kubelet.conf").exists()
