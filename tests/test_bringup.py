@@ -682,3 +682,28 @@ def test_bringup_with_the_stock_terraform_modules(ws):
     assert 'source = "compat/host"' in (ws / "terraform" / "rancher.tf").read_text()
     st = json.loads((ws / "terraform" / "terraform.tfstate").read_text())
     assert all(".terraform_data." in a for a in st["resources"])
+
+
+def test_dry_run_plans_and_checks_without_changing_anything(ws):
+    """BASELINE.json config 1 in one command: `terraform plan` + `ansible-playbook --check`."""
+    r = _setup(ws, "--dry-run", "--nodes", "2")
+    s = _summary(r)
+    assert s["dry_run"] and s["check_ok"] and [p["action"] for p in s["plan"]] == ["create"] * 3
+    assert "Plan: 3 to add, 0 to change, 0 to destroy." in r.stdout and "PLAY RECAP" in r.stdout
+    for rel in ("config", "terraform/rancher.tf", "terraform/terraform.tfstate", "ansible/hosts",
+                "ansible/tmp/kubernetes_environment.id"):
+        assert not (ws / rel).exists(), rel
+    assert not (ws / ".tk8s" / "machines").exists() and not _pids(ws)
+    _summary(_setup(ws, "--nodes", "1", "--rccl", "off"))  # and a real run after it is unaffected
+
+
+def test_dry_run_of_the_kubeadm_platform_on_an_inventory(ws):
+    inv = {"ssh": {"user": "root", "key": str(ws / "nokey")}, "hosts": [
+        {"name": "a", "address": "10.1.0.1", "gpus": 0, "role": "master"}, {"name": "b", "address": "10.1.0.2", "gpus": 8}]}
+    subprocess.run(["ssh-keygen", "-q", "-t", "ed25519", "-N", "", "-f", str(ws / "nokey")], check=True)
+    (ws / "inventory.yml").write_text(json.dumps(inv))
+    r = _setup(ws, "--dry-run", "--nodes", "1", "--backend", "baremetal", "--platform", "kubeadm", "--package", "bm-8gpu")
+    s = _summary(r)
+    assert s["platform"] == "kubeadm" and s["check_ok"], r.stdout[-3000:]
+    assert "kubeadm init" in r.stdout or "TASK [kubeadmmaster : kubeadm init" in r.stdout
+    assert not (ws / "config").exists()

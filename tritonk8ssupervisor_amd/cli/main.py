@@ -28,6 +28,7 @@ def _ws(args):
 
 def cmd_setup(args) -> int:
     from ..orchestrator import Setup, SetupError
+    from ..provider.base import ProvisionError
     from ..wizard import WizardAbort, load_answers
 
     answers = load_answers(args.answers) if args.answers else None
@@ -46,12 +47,15 @@ def cmd_setup(args) -> int:
               rccl_max_bytes=args.rccl_max_bytes,
               rccl_timeout=args.rccl_timeout, platform=args.platform)
     try:
-        summary = s.run()
+        summary = s.dry_run() if args.dry_run else s.run()
     except WizardAbort:
         return 0
     except SetupError as e:
         print(str(e), file=sys.stderr)
         return e.code
+    except ProvisionError as e:  # a provider refusing before any phase could (inventory, credentials)
+        print(f"error: {e}", file=sys.stderr)
+        return 1
     if args.json:
         print(json.dumps(summary))
     return 0
@@ -331,6 +335,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE")
     s.add_argument("--rccl-max-bytes", type=int, default=64 << 20)
     s.add_argument("--rccl-timeout", type=float, default=None, help="bound on the RCCL Job (default: --timeout)")
+    s.add_argument("--dry-run", action="store_true",
+                   help="terraform plan + ansible-playbook --check of what setup would do; changes nothing "
+                        "(BASELINE.json config 1)")
     s.add_argument("--platform", choices=["tk8s", "kubeadm"], default=None,
                    help="tk8s (default): the in-repo control plane and node agents; kubeadm: install ROCm, "
                         "amdgpu-dkms, containerd and a real Kubernetes on the machines (needs root + network)")

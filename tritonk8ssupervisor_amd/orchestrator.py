@@ -641,6 +641,58 @@ class Setup:
             raise SetupError(f"RCCL all-reduce validation failed: {json.dumps(rep)[:800]}", code=2)
         return rep
 
+    # -- dry run (BASELINE.json config 1: `terraform plan` + `ansible-playbook --check`) -------
+    def dry_run(self) -> dict:
+        """What ``./setup.sh`` would do, changing nothing: the wizard's answers, the Terraform plan
+        of the rendered rancher.tf, and the playbook in check mode against the planned machines.
+        Everything is rendered in a scratch copy of the workspace, which is removed afterwards;
+        no machine is created, no process started, no file of this workspace written."""
+        import tempfile
+
+        from .playbook import Playbook
+
+        scratch = Path(tempfile.mkdtemp(prefix="tk8s-dry-"))
+        try:
+            sws = init_workspace(scratch, self.ws.root if (self.ws.root / "ansible" / "roles").is_dir() else REPO)
+            twin = Setup(sws, answers=self.answers, assume_yes=self.assume_yes, validate=self.validate,
+                         out=self.out, backend=self.backend, master_port=self.master_port, platform=self.platform,
+                         quiet_ansible=self.quiet_ansible)
+            twin.provider = self.provider if not self.provider.colocated else get_provider(self.backend, sws.state_dir)
+            twin.engine = Engine(sws.tf, twin.provider, twin.events)
+            cfg = twin.configure()
+            key = cfg.SDC_KEY
+            pub = key + ".pub" if Path(key + ".pub").exists() else key
+            atomic_write(sws.tf / "rancher.tf", hcl.render_root(
+                twin.provider.name, cfg.SDC_ACCOUNT, key, pub, cfg.SDC_KEY_ID, cfg.SDC_URL, cfg.RANCHER_MASTER_HOSTNAME,
+                cfg.master_networks(), cfg.node_names(), cfg.node_networks(), cfg.HOST_PACKAGE,
+                form=os.environ.get("TK8S_TERRAFORM_FORM", "tk8s")))
+            twin.engine.get()
+            plan = twin.engine.plan()
+            self.banner("terraform plan")
+            self.out(Engine.plan_summary(plan))
+            lines = ["[MASTER]", f"{cfg.RANCHER_MASTER_HOSTNAME} ansible_host=planned-{cfg.RANCHER_MASTER_HOSTNAME}", "[HOST]"]
+            lines += [f"{n} ansible_host=planned-{n}" for n in cfg.node_names()]
+            atomic_write(sws.ansible / "hosts", "\n".join(lines) + "\n")
+            atomic_write(sws.vars_file, f"master: planned-{cfg.RANCHER_MASTER_HOSTNAME}\n"
+                                        f"kubernetes_name: {json.dumps(cfg.KUBERNETES_NAME)}\n"
+                                        f"kubernetes_description: {json.dumps(cfg.KUBERNETES_DESCRIPTION)}\n")
+            self.banner(f"ansible-playbook --check {PLAYBOOKS[twin.platform]}")
+            extra = {"tk8s_master_port": int(cfg.TK8S_MASTER_PORT), "tk8s_validate": self.validate,
+                     "tk8s_manifests": str(sws.manifests), "tk8s_python": sys.executable,
+                     "tk8s_pythonpath": str(REPO), "tk8s_fake_gpus": os.environ.get("TK8S_FAKE_GPUS", ""),
+                     "tk8s_validation_command": [], "tk8s_validation_pod_command": [],
+                     "tk8s_controlplane_argv": [], "tk8s_machine_dir": "(known after apply)", "tk8s_gpus": "",
+                     "tk8s_home": str(REPO)}
+            if twin.platform == "kubeadm":
+                extra.update(kubeadm_extra_vars(twin, cfg))
+            res = Playbook(sws.ansible / PLAYBOOKS[twin.platform], sws.ansible / "hosts", check=True,
+                           extra_vars=extra, out=self.out).run()
+            return {"dry_run": True, "platform": twin.platform, "backend": self.backend,
+                    "plan": [{"address": a.address, "action": a.action} for a in plan],
+                    "check_ok": res.ok, "check_failures": res.failures, "check_stats": res.stats}
+        finally:
+            shutil.rmtree(scratch, ignore_errors=True)
+
     # -- main ------------------------------------------------------------------------------
     def run(self) -> dict:
         ws = self.ws
