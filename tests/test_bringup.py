@@ -710,3 +710,13 @@ def test_dry_run_of_the_kubeadm_platform_on_an_inventory(ws):
     assert s["platform"] == "kubeadm" and s["check_ok"], r.stdout[-3000:]
     assert "kubeadm init" in r.stdout or "TASK [kubeadmmaster : kubeadm init" in r.stdout
     assert not (ws / "config").exists()
+
+
+def test_dry_run_exits_nonzero_when_the_check_fails(ws):
+    tasks = ws / "ansible" / "roles" / "rocmsetup" / "tasks" / "main.yml"
+    tasks.write_text(tasks.read_text() + "\n- name: refuse this machine\n  fail:\n    msg: not today\n")
+    r = _setup(ws, "--dry-run", "--nodes", "1")
+    assert r.returncode == 2, r.stdout[-2000:] + r.stderr[-2000:]
+    s = json.loads(r.stdout.strip().splitlines()[-1])
+    assert not s["check_ok"] and s["check_failures"] and "--check playbook failed" in r.stderr
+    assert not (ws / "config").exists() and not (ws / "terraform" / "rancher.tf").exists()

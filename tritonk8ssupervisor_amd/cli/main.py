@@ -58,6 +58,10 @@ def cmd_setup(args) -> int:
         return 1
     if args.json:
         print(json.dumps(summary))
+    if args.dry_run and not summary.get("check_ok"):
+        print(f"dry run: the --check playbook failed on {', '.join(summary.get('check_failures') or ['?'])}",
+              file=sys.stderr)
+        return 2
     return 0
 
 
