@@ -6,8 +6,12 @@
 //
 // Two launch shapes:
 //  * allreduce_single_process: one process drives n GPUs (ncclCommInitAll + group calls).
-//  * allreduce_rank: one process per GPU (ncclCommInitRank); rank 0 creates the unique id and
-//    the caller ships it to the other ranks (file or control-plane KV, see tools/tk8s_rccl.cpp).
+//  * allreduce_rank_group: one process per NODE, driving all of that node's GPUs as consecutive
+//    ranks of one multi-process communicator (ncclCommInitRank per device inside one group).
+//    On an 8-GPU node that is one runtime start instead of eight concurrent ones, each of which
+//    would initialise all eight agents (the fabric Job's start-up cost).
+//    allreduce_rank is the one-device case. Rank 0 creates the unique id and the caller ships it
+//    to the other processes (file or control-plane KV, see tools/tk8s_rccl.cpp).
 #pragma once
 
 #include <cstddef>
@@ -37,7 +41,12 @@ bool nccl_unique_id_from_hex(const std::string& hex, ncclUniqueId* id);
 // time_us,algbw_gbps,busbw_gbps,max_err,bad}...],"peak_busbw_gbps":..}
 std::string allreduce_single_process(const std::vector<int>& devices, const AllReduceConfig& cfg);
 
-// Same record for one rank of a multi-process communicator (times are this rank's).
+// Same record for ranks first_rank .. first_rank+devices.size()-1 of an nranks communicator,
+// all driven by this process ("mode":"rank_group"; times are the slowest local rank's).
+std::string allreduce_rank_group(int first_rank, int nranks, const std::vector<int>& devices,
+                                 const ncclUniqueId& id, const AllReduceConfig& cfg);
+
+// One rank of a multi-process communicator ("mode":"multi_process").
 std::string allreduce_rank(int rank, int nranks, int device, const ncclUniqueId& id,
                            const AllReduceConfig& cfg);
 

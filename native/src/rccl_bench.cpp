@@ -158,6 +158,7 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
       .kv("peak_links_equivalent", all_ranks > 1 ? peak_bus / kXgmiLinkGBps : 0.0)
       .kv("nranks", all_ranks)
       .kv("local_ranks", static_cast<int>(ranks.size()))
+      .kv("first_rank", ranks.empty() ? 0 : ranks.front().rank)
       .kv("rccl_version", rccl_version())
       .kv("dtype", cfg.dtype == DType::kF32 ? "float32" : "bfloat16")
       .kv("iters", cfg.iters)
@@ -244,24 +245,44 @@ std::string allreduce_single_process(const std::vector<int>& devices, const AllR
   }
 }
 
-std::string allreduce_rank(int rank, int nranks, int device, const ncclUniqueId& id,
-                           const AllReduceConfig& cfg) {
-  std::vector<Rank> ranks(1);
+std::string allreduce_rank_group(int first_rank, int nranks, const std::vector<int>& devices,
+                                 const ncclUniqueId& id, const AllReduceConfig& cfg) {
+  std::vector<Rank> ranks(devices.size());
   try {
-    ranks[0].device = device;
-    ranks[0].rank = rank;
-    TK8S_HIP_CHECK(hipSetDevice(device));
-    TK8S_HIP_CHECK(hipStreamCreateWithFlags(&ranks[0].stream, hipStreamNonBlocking));
+    if (devices.empty()) return error_json("no devices");
+    if (first_rank < 0 || first_rank + static_cast<int>(devices.size()) > nranks)
+      return error_json("ranks " + std::to_string(first_rank) + ".." +
+                        std::to_string(first_rank + static_cast<int>(devices.size()) - 1) +
+                        " do not fit a communicator of " + std::to_string(nranks));
+    for (size_t i = 0; i < devices.size(); ++i) {
+      ranks[i].device = devices[i];
+      ranks[i].rank = first_rank + static_cast<int>(i);
+      TK8S_HIP_CHECK(hipSetDevice(devices[i]));
+      TK8S_HIP_CHECK(hipStreamCreateWithFlags(&ranks[i].stream, hipStreamNonBlocking));
+    }
     const auto t0 = std::chrono::steady_clock::now();
-    TK8S_NCCL_CHECK(ncclCommInitRank(&ranks[0].comm, nranks, id, rank));
+    // Several ranks of one communicator in one thread: the inits must be one group, or the first
+    // would wait forever for its local peers.
+    TK8S_NCCL_CHECK(ncclGroupStart());
+    for (auto& r : ranks) {
+      TK8S_HIP_CHECK(hipSetDevice(r.device));
+      TK8S_NCCL_CHECK(ncclCommInitRank(&r.comm, nranks, id, r.rank));
+    }
+    TK8S_NCCL_CHECK(ncclGroupEnd());
     const double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    std::string out = run_sweep(ranks, nranks, cfg, "multi_process", init_ms, unix_ms());
+    std::string out = run_sweep(ranks, nranks, cfg, ranks.size() > 1 ? "rank_group" : "multi_process", init_ms,
+                                unix_ms());
     release(ranks);
     return out;
   } catch (const std::exception& ex) {
     release(ranks);
     return error_json(ex.what());
   }
+}
+
+std::string allreduce_rank(int rank, int nranks, int device, const ncclUniqueId& id,
+                           const AllReduceConfig& cfg) {
+  return allreduce_rank_group(rank, nranks, std::vector<int>{device}, id, cfg);
 }
 
 }  // namespace tk8s

@@ -2,12 +2,15 @@
 //
 // Single process, n GPUs:   tk8s-rccl --ngpus N
 // One process per GPU:      tk8s-rccl --rank R --nranks N [--device D]
-//                                     (--uid-file PATH | --kv-url http://host:port/v1/kv/KEY)
-//   Rank 0 creates the RCCL unique id and publishes it (atomic file rename, or HTTP PUT to the
-//   control-plane KV); the other ranks wait for it (file poll, or HTTP long-poll GET).
+// One process per node:     tk8s-rccl --group-index I --devices D0,D1,.. --nranks N
+//                             (ranks I*k .. I*k+k-1 for k devices; or --rank R --devices ..)
+//                           ... (--uid-file PATH | --kv-url http://host:port/v1/kv/KEY)
+//   The process holding rank 0 creates the RCCL unique id and publishes it (atomic file rename,
+//   or HTTP PUT to the control-plane KV); the others wait for it (file poll, or HTTP long-poll).
 // Sweep: --min-bytes B --max-bytes B --factor F --iters K --warmup W --dtype float32|bfloat16
 // Prints one JSON object; exit 0 iff every size reduced exactly.
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <fstream>
 #include <sstream>
@@ -63,6 +66,20 @@ bool fetch_uid(const tk8s::Args& a, std::string* hex, int timeout_s) {
   return false;
 }
 
+// "3,5,7" -> {3,5,7}; empty on any malformed entry.
+std::vector<int> parse_devices(const std::string& s) {
+  std::vector<int> out;
+  std::stringstream ss(s);
+  std::string tok;
+  while (std::getline(ss, tok, ',')) {
+    char* end = nullptr;
+    const long v = std::strtol(tok.c_str(), &end, 10);
+    if (tok.empty() || *end != '\0' || v < 0) return {};
+    out.push_back(static_cast<int>(v));
+  }
+  return out;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -77,17 +94,23 @@ int main(int argc, char** argv) {
     cfg.dtype = a.str("dtype", "float32") == "bfloat16" ? tk8s::DType::kBF16 : tk8s::DType::kF32;
     cfg.check = !a.has("no-check");
     std::string out;
-    if (a.has("rank")) {
-      const int rank = static_cast<int>(a.num("rank", 0));
+    if (a.has("rank") || a.has("group-index")) {
       const int nranks = static_cast<int>(a.num("nranks", 1));
-      const int device = static_cast<int>(a.num("device", 0));
+      std::vector<int> devices = a.has("devices") ? parse_devices(a.str("devices"))
+                                                  : std::vector<int>{static_cast<int>(a.num("device", 0))};
+      if (devices.empty()) {
+        std::fprintf(stderr, "tk8s-rccl: bad --devices '%s'\n", a.str("devices").c_str());
+        return 2;
+      }
+      const int first = a.has("rank") ? static_cast<int>(a.num("rank", 0))
+                                      : static_cast<int>(a.num("group-index", 0)) * static_cast<int>(devices.size());
       if (!a.has("uid-file") && !a.has("kv-url")) {
-        std::fprintf(stderr, "tk8s-rccl: --rank needs --uid-file or --kv-url\n");
+        std::fprintf(stderr, "tk8s-rccl: --rank/--group-index needs --uid-file or --kv-url\n");
         return 2;
       }
       ncclUniqueId id;
       std::string hex;
-      if (rank == 0) {
+      if (first == 0) {
         if (ncclGetUniqueId(&id) != ncclSuccess) {
           std::fprintf(stderr, "tk8s-rccl: ncclGetUniqueId failed\n");
           return 2;
@@ -104,7 +127,7 @@ int main(int argc, char** argv) {
           return 2;
         }
       }
-      out = tk8s::allreduce_rank(rank, nranks, device, id, cfg);
+      out = tk8s::allreduce_rank_group(first, nranks, devices, id, cfg);
     } else {
       int n = 0;
       if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {

@@ -720,3 +720,17 @@ def test_dry_run_exits_nonzero_when_the_check_fails(ws):
     s = json.loads(r.stdout.strip().splitlines()[-1])
     assert not s["check_ok"] and s["check_failures"] and "--check playbook failed" in r.stderr
     assert not (ws / "config").exists() and not (ws / "terraform" / "rancher.tf").exists()
+
+
+def test_rccl_job_runs_one_pod_per_multi_gpu_node(ws):
+    """mi355x-2gpu workers: the fabric Job is one pod per node holding both of its GPUs, one
+    process driving them as consecutive ranks (not one process per GPU)."""
+    s = _summary(_setup(ws, "--nodes", "2", "--package", "mi355x-2gpu", "--rccl", "on"))
+    rc = s["rccl"]
+    assert rc["ok"] and rc["nranks"] == 4 and rc["pods"] == 2 and rc["gpus_per_pod"] == 2, rc
+    assert sorted(r["node"] for r in rc["rank_results"]) == ["kubenode1", "kubenode2"]
+    r = subprocess.run(["./kubectl", "get", "pods", "-n", "kube-system", "-l", f"job-name={rc['job']}", "-o", "json"],
+                       cwd=ws, env=_env(), capture_output=True, text=True)
+    res = sorted((p["status"]["result"] for p in json.loads(r.stdout)["items"]), key=lambda x: x["first_rank"])
+    assert [(x["first_rank"], x["local_ranks"], x["mode"]) for x in res] == [(0, 2, "rank_group"), (2, 2, "rank_group")]
+    assert all(x["nranks"] == 4 for x in res)

@@ -424,6 +424,58 @@ def test_multi_gpu_setup_with_rccl_job(tmp_path):
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
 
+@pytest.mark.skipif(_gpu_count() < 2, reason="needs >= 2 MI355X (xGMI)")
+def test_multi_gpu_node_fabric_job_is_one_process_per_node(tmp_path):
+    """A 2-GPU worker: the RCCL Job is one pod holding both GPUs, its one process driving them as
+    ranks 0 and 1 (tk8s-rccl --group-index/--devices), P2P over xGMI."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable, NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P")
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--package", "mi355x-2gpu", "--rccl", "on", "--yes", "--json",
+                            "--port", "0", "--timeout", "240", "--rccl-max-bytes", str(64 << 20)], cwd=tmp_path, env=env,
+                           capture_output=True, text=True, timeout=400)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+        rc = json.loads(r.stdout.strip().splitlines()[-1])["rccl"]
+        assert rc["ok"] and rc["nranks"] == 2 and rc["pods"] == 1 and rc["gpus_per_pod"] == 2, rc
+        assert rc["transport"]["p2p"] > 0 and rc["transport"]["shm"] == 0, rc["transport"]
+        assert rc["peak_busbw_gbps"] > 40, rc
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+def test_rccl_rank_group_cli_on_one_gpu(tmp_path):
+    """tk8s-rccl's per-node shape with one device (what the fabric Job runs on 1-GPU nodes)."""
+    import subprocess
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tritonk8ssupervisor_amd.ops import BIN
+
+    r = subprocess.run([str(BIN / "tk8s-rccl"), "--group-index", "0", "--devices", "0", "--nranks", "1",
+                        "--uid-file", str(tmp_path / "uid"), "--max-bytes", str(4 << 20), "--iters", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"] and out["nranks"] == 1 and out["first_rank"] == 0 and out["local_ranks"] == 1
+    assert all(x["bad"] == 0 for x in out["results"])
+    bad = subprocess.run([str(BIN / "tk8s-rccl"), "--group-index", "1", "--devices", "0", "--nranks", "1",
+                          "--uid-file", str(tmp_path / "uid"), "--uid-timeout", "5"], capture_output=True, text=True,
+                         timeout=60)
+    assert bad.returncode != 0  # rank 1 of a 1-rank communicator is refused, not a hang
+
+
 @pytest.mark.gpu
 def test_setup_from_an_answers_file_adopts_the_early_burnin_on_a_real_gpu(tmp_path):
     """``./setup.sh --answers FILE`` (the bench's path): the real tk8s-probe is spawned before the

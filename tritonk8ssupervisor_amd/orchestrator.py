@@ -566,6 +566,20 @@ class Setup:
                                  + (f": {why}" if why else "")
                                  + "\n    see `./kubectl describe nodes` and `./kubectl get pods -n kube-system`", code=2)
 
+    @staticmethod
+    def rccl_gpus_per_pod(k, g: int) -> int:
+        """GPUs per fabric-Job pod: every GPU of its node when the GPU nodes are uniform (one
+        process -- one runtime start -- per node, its GPUs as consecutive ranks), else 1."""
+        try:
+            nodes = k.get("/api/v1/nodes").get("items", [])
+        except Exception:  # noqa: BLE001 - the per-GPU shape works whatever the nodes say
+            return 1
+        counts = [int((n.get("status", {}).get("allocatable") or {}).get("amd.com/gpu", 0) or 0) for n in nodes]
+        counts = [c for c in counts if c > 0]
+        if counts and len(set(counts)) == 1 and counts[0] * len(counts) == g:
+            return counts[0]
+        return 1
+
     def run_rccl(self) -> dict | None:
         from .controlplane.client import client_from_kubeconfig
         from .kube import apply_objects, load_manifests, pods_of, wait_job
@@ -585,13 +599,17 @@ class Setup:
         pid = self.project_id()
         k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
         job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
+        per_pod = self.rccl_gpus_per_pod(k, g)
+        npods = g // per_pod
+        # one process per node drives all of that node's GPUs (ranks index*k .. index*k+k-1)
+        group = ["--group-index", "$(JOB_COMPLETION_INDEX)", "--devices", "$(TK8S_GPU_DEVICES)", "--nranks", str(g)]
         if os.environ.get("TK8S_FAKE_GPUS"):
-            cmd = ["$(TK8S_PYTHON)", "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", "$(JOB_COMPLETION_INDEX)",
-                   "--nranks", str(g), "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
+            cmd = ["$(TK8S_PYTHON)", "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", *group,
+                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
         else:
             from .ops import BIN
 
-            cmd = [pod_portable([str(BIN / "tk8s-rccl")])[0], "--rank", "$(JOB_COMPLETION_INDEX)", "--nranks", str(g), "--device", "$(TK8S_GPU_DEVICE)",
+            cmd = [pod_portable([str(BIN / "tk8s-rccl")])[0], *group,
                    "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
                    "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
         prof_dir = None
@@ -611,9 +629,9 @@ class Setup:
                 cmd = [rp, *pmc, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
                        "--output-format", "csv", "--", *cmd]
         objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
-                              {"job_name": job, "nranks": g, "rccl_command": cmd})
+                              {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd})
         apply_objects(k, objs)
-        self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job})")
+        self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job}, {npods} pod(s) x {per_pod} GPU(s))")
         left = max(10.0, self.rccl_timeout or self.timeout)
         try:
             j = wait_job(k, job, "kube-system", timeout=left)
@@ -622,9 +640,9 @@ class Setup:
         pods = pods_of(k, f"job-name={job}", "kube-system")
         results = [p.get("status", {}).get("result") or {} for p in pods]
         peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)
-        ok = j["status"].get("succeeded", 0) >= g and all(r.get("ok") for r in results)
+        ok = j["status"].get("succeeded", 0) >= npods and all(r.get("ok") for r in results)
         first = next((r for r in results if r), {})
-        rep = {"job": job, "ok": ok, "nranks": g, "peak_busbw_gbps": peak,
+        rep = {"job": job, "ok": ok, "nranks": g, "pods": npods, "gpus_per_pod": per_pod, "peak_busbw_gbps": peak,
                "tuning": {k: first.get(k) for k in ("nccl_algo", "nccl_proto", "nccl_min_nchannels",
                                                     "nccl_max_nchannels", "peak_links_equivalent") if k in first},
                "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),

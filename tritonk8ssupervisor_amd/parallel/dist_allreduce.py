@@ -9,6 +9,10 @@ step so the control-plane path is exercised unchanged: rank 0 publishes its rend
 RCCL-tests-style sweep with an exact result check and prints ONE JSON line with the same keys
 as native/tools/tk8s_rccl.cpp (``ok``, ``nranks``, ``rank``, ``peak_busbw_gbps``, ``results``).
 
+``--group-index I --devices d0,..,dk-1`` is the fabric Job's one-pod-per-node shape (ranks
+I*k .. I*k+k-1, like ``tk8s-rccl --group-index``): torch.distributed has one default group per
+process, so the pod runs its k ranks as child processes and prints ONE merged line for the pod.
+
 Check (N6 semantics): rank r contributes ``(r + 1) * p[i]`` with ``p[i] = (i % m) + 1``;
 every element must equal ``n (n + 1) / 2 * p[i]`` exactly. ``m`` keeps every partial sum an
 exactly representable integer: 251 for fp32 (< 2^24), 4 for bf16 (sums <= 256 up to n = 8).
@@ -86,9 +90,49 @@ def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters:
     return {"ok": ok, "results": results, "peak_busbw_gbps": peak}
 
 
+def _rank_group(a, argv: list[str], k: int) -> int:
+    """Run ranks group_index*k .. +k-1 as child processes; one merged JSON line for the pod."""
+    import subprocess
+
+    rest, skip = [], False
+    for i, tok in enumerate(argv):  # drop --group-index/--devices (and their values), keep the rest
+        if skip:
+            skip = False
+            continue
+        if tok in ("--group-index", "--devices"):
+            skip = True
+            continue
+        if tok.startswith(("--group-index=", "--devices=")):
+            continue
+        rest.append(tok)
+    first = a.group_index * k
+    procs = [subprocess.Popen([sys.executable, "-m", __spec__.name if __spec__ else "tritonk8ssupervisor_amd.parallel.dist_allreduce",
+                               "--rank", str(first + j), *rest], stdout=subprocess.PIPE, text=True)
+             for j in range(k)]
+    outs = []
+    for pr in procs:
+        out, _ = pr.communicate()
+        line = (out or "").strip().splitlines()
+        try:
+            outs.append(json.loads(line[-1]) if line else {"ok": False, "error": f"rank exited {pr.returncode}"})
+        except ValueError:
+            outs.append({"ok": False, "error": line[-1][:200]})
+    merged = dict(outs[0])
+    merged.update(ok=all(o.get("ok") for o in outs), mode="rank_group", rank=first, first_rank=first, local_ranks=k,
+                  peak_busbw_gbps=min((o.get("peak_busbw_gbps", 0.0) for o in outs), default=0.0),
+                  init_seconds=max((o.get("init_seconds", 0.0) for o in outs), default=0.0))
+    errs = [o["error"] for o in outs if o.get("error")]
+    if errs:
+        merged["error"] = "; ".join(errs)
+    print(json.dumps(merged))
+    return 0 if merged["ok"] else 1
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--rank", type=int)
+    ap.add_argument("--group-index", type=int, help="the pod's index: ranks group-index*k .. +k-1")
+    ap.add_argument("--devices", default="", help="the pod's GPUs, comma separated (k = their count)")
     ap.add_argument("--nranks", type=int, required=True)
     ap.add_argument("--kv-url", required=True)
     ap.add_argument("--min-bytes", type=int, default=1024)
@@ -100,6 +144,13 @@ def main(argv=None) -> int:
     ap.add_argument("--timeout", type=float, default=60.0)
     ap.add_argument("--backend", choices=["gloo", "nccl"], default="gloo", help="nccl = RCCL on ROCm (GPU tensors)")
     a = ap.parse_args(argv)
+    if a.rank is None:
+        if a.group_index is None:
+            ap.error("one of --rank / --group-index is required")
+        devs = [d for d in a.devices.split(",") if d.strip()] or ["0"]
+        if len(devs) > 1:
+            return _rank_group(a, argv if argv is not None else sys.argv[1:], len(devs))
+        a.rank = a.group_index
     t0 = time.monotonic()
     host = os.environ.get("NODE_IP", "127.0.0.1")
     try:
