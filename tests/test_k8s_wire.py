@@ -1,0 +1,239 @@
+"""The control plane speaks the Kubernetes wire conventions a stock client relies on
+(controlplane/k8s_wire.py): discovery, typed lists, Status errors, field selectors, the three
+patch types, server-side Tables and the chunked watch stream.
+
+No kubectl / client-go / kubernetes Python client is installed here, so these tests play the
+client's part at the HTTP level, request by request, the way kubectl issues them (discovery
+first, then e.g. GET -> 404 -> POST -> PATCH application/strategic-merge-patch+json for
+``kubectl apply``). Parity with a real kubectl binary is unpinned."""
+import http.client
+import json
+import threading
+import time
+
+import pytest
+
+from tritonk8ssupervisor_amd.controlplane import k8s_wire
+from tritonk8ssupervisor_amd.controlplane.client import client_from_kubeconfig
+
+from test_controlplane import _env, _join, _start, _stop
+
+
+@pytest.fixture
+def kube(tmp_path):
+    p, c = _start(tmp_path)
+    proj = _env(c)
+    _join(c, proj["id"], "kubenode1", ngpu=2)
+    k = client_from_kubeconfig(c.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    yield k
+    _stop(p)
+
+
+def _raw(k, method, path, body=None, ctype="application/json", accept="application/json", timeout=10):
+    conn = http.client.HTTPConnection(k.host, k.port, timeout=timeout)
+    headers = {"Accept": accept, "Authorization": f"Bearer {k.token}"}
+    data = None
+    if body is not None:
+        data = json.dumps(body).encode()
+        headers["Content-Type"] = ctype
+    conn.request(method, k.k8s(path), body=data, headers=headers)
+    r = conn.getresponse()
+    out = r.status, r.getheader("Content-Type"), r.read()
+    conn.close()
+    return out[0], out[1], (json.loads(out[2]) if out[2] and "json" in (out[1] or "") else out[2])
+
+
+# ---- discovery ------------------------------------------------------------------------------
+def test_discovery_documents(kube):
+    st, _, v = _raw(kube, "GET", "/api")
+    assert st == 200 and v["kind"] == "APIVersions" and v["versions"] == ["v1"]
+    _, _, groups = _raw(kube, "GET", "/apis")
+    names = {g["name"]: g["preferredVersion"]["groupVersion"] for g in groups["groups"]}
+    assert names == {"apps": "apps/v1", "batch": "batch/v1", "networking.k8s.io": "networking.k8s.io/v1"}
+    _, _, core = _raw(kube, "GET", "/api/v1")
+    res = {r["name"]: r for r in core["resources"]}
+    assert core["kind"] == "APIResourceList" and core["groupVersion"] == "v1"
+    assert res["pods"]["kind"] == "Pod" and res["pods"]["namespaced"] and "po" in res["pods"]["shortNames"]
+    assert not res["nodes"]["namespaced"] and "watch" in res["nodes"]["verbs"] and "pods/log" in res
+    _, _, apps = _raw(kube, "GET", "/apis/apps/v1")
+    scale = next(r for r in apps["resources"] if r["name"] == "deployments/scale")
+    assert scale["kind"] == "Scale" and scale["group"] == "autoscaling"
+    assert _raw(kube, "GET", "/apis/nope/v1")[0] == 404
+    _, _, grp = _raw(kube, "GET", "/apis/batch")
+    assert grp["kind"] == "APIGroup" and grp["preferredVersion"]["version"] == "v1"
+
+
+# ---- typed objects, lists and Status errors --------------------------------------------------
+def test_typed_lists_and_objects(kube):
+    cm = {"metadata": {"name": "a"}, "data": {"k": "v"}}
+    _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", cm)
+    _, _, lst = _raw(kube, "GET", "/api/v1/namespaces/default/configmaps")
+    assert lst["kind"] == "ConfigMapList" and lst["apiVersion"] == "v1" and lst["metadata"]["resourceVersion"]
+    assert lst["items"][0]["kind"] == "ConfigMap" and lst["items"][0]["apiVersion"] == "v1"
+    _, _, nodes = _raw(kube, "GET", "/api/v1/nodes")
+    assert nodes["kind"] == "NodeList" and nodes["items"][0]["kind"] == "Node"
+    _, _, deps = _raw(kube, "GET", "/apis/apps/v1/deployments")
+    assert deps["kind"] == "DeploymentList" and deps["apiVersion"] == "apps/v1"
+    _, _, ns = _raw(kube, "GET", "/api/v1/namespaces")
+    assert ns["kind"] == "NamespaceList" and all(i["kind"] == "Namespace" for i in ns["items"])
+
+
+def test_errors_are_kubernetes_status_objects(kube):
+    st, _, body = _raw(kube, "GET", "/api/v1/namespaces/default/pods/missing")
+    assert st == 404 and body["kind"] == "Status" and body["reason"] == "NotFound" and body["code"] == 404
+    cm = {"metadata": {"name": "dup"}, "data": {}}
+    _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", cm)
+    st, _, body = _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", cm)
+    assert st == 409 and body["reason"] == "AlreadyExists"
+    stale = dict(cm, metadata={"name": "dup", "resourceVersion": "1"})
+    st, _, body = _raw(kube, "PUT", "/api/v1/namespaces/default/configmaps/dup", stale)
+    assert st == 409 and body["reason"] == "Conflict"
+    st, _, body = _raw(kube, "POST", "/api/v1/namespaces/default/pods", {"metadata": {"name": "x"}, "spec": {}})
+    assert st == 422 and body["reason"] == "Invalid"
+
+
+# ---- selectors and tables -------------------------------------------------------------------
+def test_field_selectors(kube):
+    for n in ("one", "two"):
+        _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", {"metadata": {"name": n}, "data": {}})
+    _, _, one = _raw(kube, "GET", "/api/v1/namespaces/default/configmaps?fieldSelector=metadata.name%3Done")
+    assert [i["metadata"]["name"] for i in one["items"]] == ["one"]
+    _, _, rest = _raw(kube, "GET", "/api/v1/namespaces/default/configmaps?fieldSelector=metadata.name!%3Done")
+    assert [i["metadata"]["name"] for i in rest["items"]] == ["two"]
+    _, _, nodes = _raw(kube, "GET", "/api/v1/nodes?fieldSelector=metadata.name%3Dkubenode1")
+    assert len(nodes["items"]) == 1
+
+
+def test_server_side_table_for_kubectl_get(kube):
+    acc = "application/json;as=Table;v=v1;g=meta.k8s.io,application/json;as=Table;v=v1beta1;g=meta.k8s.io,application/json"
+    _, _, t = _raw(kube, "GET", "/api/v1/nodes", accept=acc)
+    assert t["kind"] == "Table" and t["apiVersion"] == "meta.k8s.io/v1"
+    cols = [c["name"] for c in t["columnDefinitions"]]
+    assert cols[:2] == ["Name", "Status"] and "GPU" in cols
+    row = t["rows"][0]
+    assert row["cells"][0] == "kubenode1" and row["cells"][cols.index("GPU")] == "2/2"
+    assert row["object"]["kind"] == "PartialObjectMetadata" and row["object"]["metadata"]["name"] == "kubenode1"
+    _, _, t = _raw(kube, "GET", "/api/v1/namespaces", accept=acc)
+    assert t["kind"] == "Table" and any(r["cells"][0] == "default" for r in t["rows"])
+
+
+# ---- patches --------------------------------------------------------------------------------
+DEPLOY = {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "web"},
+          "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "web"}},
+                   "template": {"metadata": {"labels": {"app": "web"}},
+                                "spec": {"containers": [
+                                    {"name": "a", "image": "img:1", "command": ["sleep", "60"],
+                                     "env": [{"name": "X", "value": "1"}, {"name": "Y", "value": "2"}]},
+                                    {"name": "b", "image": "side:1", "command": ["sleep", "60"]}]}}}}
+
+
+def test_kubectl_apply_flow_with_a_strategic_merge_patch(kube):
+    """kubectl apply: GET (404) -> POST with last-applied; change -> PATCH strategic-merge-patch."""
+    path = "/apis/apps/v1/namespaces/default/deployments/web"
+    assert _raw(kube, "GET", path)[0] == 404
+    st, _, created = _raw(kube, "POST", "/apis/apps/v1/namespaces/default/deployments", DEPLOY)
+    assert st == 201 and created["kind"] == "Deployment"
+    patch = {"metadata": {"annotations": {"kubectl.kubernetes.io/last-applied-configuration": "{}"}},
+             "spec": {"template": {"spec": {
+                 "$setElementOrder/containers": [{"name": "a"}, {"name": "b"}],
+                 "containers": [{"name": "a", "image": "img:2",
+                                 "$setElementOrder/env": [{"name": "X"}, {"name": "Y"}],
+                                 "env": [{"name": "Y", "value": "3"}]}]}}}}
+    st, _, d = _raw(kube, "PATCH", path, patch, ctype=k8s_wire.STRATEGIC_PATCH)
+    assert st == 200, d
+    a, b = d["spec"]["template"]["spec"]["containers"]
+    assert a["image"] == "img:2" and a["command"] == ["sleep", "60"]          # merged by name, not replaced
+    assert a["env"] == [{"name": "X", "value": "1"}, {"name": "Y", "value": "3"}]
+    assert b == DEPLOY["spec"]["template"]["spec"]["containers"][1]
+    assert "$setElementOrder" not in json.dumps(d)  # directives are applied, never stored
+    assert d["metadata"]["generation"] == 2
+    # $patch: delete removes one element of a merge-keyed list
+    st, _, d = _raw(kube, "PATCH", path, {"spec": {"template": {"spec": {"containers": [{"name": "b", "$patch": "delete"}]}}}},
+                    ctype=k8s_wire.STRATEGIC_PATCH)
+    assert [c["name"] for c in d["spec"]["template"]["spec"]["containers"]] == ["a"]
+
+
+def test_json_patch_and_merge_patch(kube):
+    _raw(kube, "POST", "/apis/apps/v1/namespaces/default/deployments", DEPLOY)
+    path = "/apis/apps/v1/namespaces/default/deployments/web"
+    st, _, d = _raw(kube, "PATCH", path, [{"op": "replace", "path": "/spec/replicas", "value": 3},
+                                          {"op": "add", "path": "/metadata/labels/tier", "value": "front"}],
+                    ctype=k8s_wire.JSON_PATCH)
+    assert st == 200 and d["spec"]["replicas"] == 3 and d["metadata"]["labels"]["tier"] == "front"
+    st, _, body = _raw(kube, "PATCH", path, [{"op": "test", "path": "/spec/replicas", "value": 9}],
+                       ctype=k8s_wire.JSON_PATCH)
+    assert st == 422 and body["reason"] == "Invalid"
+    st, _, d = _raw(kube, "PATCH", path, {"spec": {"replicas": 2}}, ctype=k8s_wire.MERGE_PATCH)
+    assert st == 200 and d["spec"]["replicas"] == 2
+    assert _raw(kube, "PATCH", path, {"spec": {}}, ctype=k8s_wire.APPLY_PATCH)[0] == 415
+
+
+def test_strategic_merge_directives_unit():
+    cur = {"spec": {"ports": [{"port": 80, "name": "http"}, {"port": 443, "name": "https"}],
+                    "finalizers": ["a"], "keep": 1, "drop": 2}}
+    out = k8s_wire.strategic_merge(cur, {"spec": {"ports": [{"port": 443, "targetPort": 8443}],
+                                                  "finalizers": ["b"], "drop": None}})
+    assert out["spec"]["ports"] == [{"port": 80, "name": "http"}, {"port": 443, "name": "https", "targetPort": 8443}]
+    assert out["spec"]["finalizers"] == ["a", "b"] and "drop" not in out["spec"]
+    assert k8s_wire.strategic_merge(cur, {"spec": {"$patch": "replace", "x": 1}}) == {"spec": {"x": 1}}
+    assert k8s_wire.strategic_merge(cur, {"spec": {"$retainKeys": ["keep"], "keep": 5}}) == {"spec": {"keep": 5}}
+    out = k8s_wire.strategic_merge(cur, {"spec": {"$deleteFromPrimitiveList/finalizers": ["a"]}})
+    assert out["spec"]["finalizers"] == []
+    with pytest.raises(k8s_wire.PatchError):
+        k8s_wire.json_patch({"a": 1}, [{"op": "remove", "path": "/b"}])
+    assert k8s_wire.json_patch({"a": [1, 2]}, [{"op": "add", "path": "/a/-", "value": 3},
+                                               {"op": "move", "from": "/a/0", "path": "/b"}]) == {"a": [2, 3], "b": 1}
+
+
+# ---- watch stream ---------------------------------------------------------------------------
+def _stream(k, path, timeout=10):
+    conn = http.client.HTTPConnection(k.host, k.port, timeout=timeout)
+    conn.request("GET", k.k8s(path), headers={"Accept": "application/json"})
+    r = conn.getresponse()
+    return conn, r
+
+
+def test_watch_is_a_chunked_stream_of_events(kube):
+    _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", {"metadata": {"name": "before"}, "data": {}})
+    conn, r = _stream(kube, "/api/v1/namespaces/default/configmaps?watch=true&timeoutSeconds=3")
+    assert r.status == 200 and r.getheader("Transfer-Encoding") == "chunked"
+    first = json.loads(r.readline())
+    assert first["type"] == "ADDED" and first["object"]["metadata"]["name"] == "before"
+    assert first["object"]["kind"] == "ConfigMap"
+
+    def later():
+        time.sleep(0.2)
+        _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", {"metadata": {"name": "after"}, "data": {}})
+        _raw(kube, "DELETE", "/api/v1/namespaces/default/configmaps/before")
+
+    threading.Thread(target=later).start()
+    ev = [json.loads(r.readline()) for _ in range(2)]
+    assert [(e["type"], e["object"]["metadata"]["name"]) for e in ev] == [("ADDED", "after"), ("DELETED", "before")]
+    t = time.monotonic()
+    assert r.read() == b""  # the stream ends at timeoutSeconds (chunked terminator)
+    assert time.monotonic() - t < 5
+    conn.close()
+
+
+def test_watch_from_a_resource_version_and_with_a_field_selector(kube):
+    _, _, cm = _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", {"metadata": {"name": "w"}, "data": {}})
+    rv = cm["metadata"]["resourceVersion"]
+    _raw(kube, "POST", "/api/v1/namespaces/default/configmaps", {"metadata": {"name": "other"}, "data": {}})
+    _raw(kube, "PATCH", "/api/v1/namespaces/default/configmaps/w", {"data": {"k": "v"}}, ctype=k8s_wire.MERGE_PATCH)
+    conn, r = _stream(kube, f"/api/v1/namespaces/default/configmaps?watch=true&resourceVersion={rv}"
+                            "&fieldSelector=metadata.name%3Dw&timeoutSeconds=1")
+    ev = [json.loads(ln) for ln in r.read().splitlines() if ln.strip()]
+    assert [(e["type"], e["object"]["data"]) for e in ev] == [("MODIFIED", {"k": "v"})]
+    conn.close()
+    conn, r = _stream(kube, "/api/v1/namespaces/default/configmaps?watch=true&resourceVersion=abc&timeoutSeconds=1")
+    e = json.loads(r.readline())
+    assert e["type"] == "ERROR" and e["object"]["code"] == 400
+    conn.close()
+
+
+def test_tk8s_clients_keep_the_batch_long_poll(kube):
+    rv = int(kube.get(kube.k8s("/api/v1/namespaces/default/configmaps"))["metadata"]["resourceVersion"])
+    threading.Timer(0.2, lambda: _raw(kube, "POST", "/api/v1/namespaces/default/configmaps",
+                                      {"metadata": {"name": "lp"}, "data": {}})).start()
+    new_rv, events = kube.watch(kube.k8s("/api/v1/namespaces/default/configmaps"), rv, timeout=5)
+    assert new_rv > rv and [e["object"]["metadata"]["name"] for e in events] == ["lp"]

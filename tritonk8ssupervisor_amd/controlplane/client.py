@@ -120,7 +120,8 @@ class Client:
         return False
 
     def watch(self, path: str, since: int, timeout: float = 30.0, query: dict | None = None) -> tuple[int, list[dict]]:
-        q = {"watch": "1", "resourceVersion": str(since), "timeoutSeconds": str(timeout)}
+        # batch=1: the long-poll form (one JSON batch per request), not the Kubernetes stream
+        q = {"watch": "1", "batch": "1", "resourceVersion": str(since), "timeoutSeconds": str(timeout)}
         q.update(query or {})
         r = self.get(path, query=q, timeout=timeout + 10)
         return int(r["resourceVersion"]), r["events"]

@@ -11,7 +11,7 @@ import json
 import re
 import traceback
 from dataclasses import dataclass, field
-from typing import Any, Awaitable, Callable
+from typing import Any, AsyncIterator, Awaitable, Callable
 from urllib.parse import parse_qs, unquote, urlsplit
 
 REASONS = {200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
@@ -64,10 +64,21 @@ class Response:
                 self.content_type or "application/json")
 
 
+@dataclass
+class StreamResponse:
+    """A chunked response whose body is produced over time (a Kubernetes watch stream)."""
+    chunks: AsyncIterator[bytes]
+    status: int = 200
+    content_type: str = "application/json"
+    headers: dict[str, str] = field(default_factory=dict)
+
+
 class HttpError(Exception):
     def __init__(self, status: int, message: str, body: Any = None):
         super().__init__(message)
         self.status = status
+        self.message = message
+        self.custom_body = body is not None
         self.body = body if body is not None else {"type": "error", "status": status, "message": message}
 
 
@@ -127,10 +138,18 @@ async def _read_request(reader: asyncio.StreamReader, peer: str) -> Request | No
 
 
 class HttpServer:
-    def __init__(self, router: Router, on_error: Callable[[str], None] | None = None):
+    def __init__(self, router: Router, on_error: Callable[[str], None] | None = None,
+                 error_body: Callable[[str, HttpError], Any] | None = None):
         self.router = router
         self.on_error = on_error
+        self.error_body = error_body  # path, error -> body (e.g. a Kubernetes Status on API paths)
         self.server: asyncio.base_events.Server | None = None
+
+    def _error(self, path: str, e: HttpError) -> Response:
+        body = e.body
+        if self.error_body is not None and not e.custom_body:
+            body = self.error_body(path, e)
+        return Response(e.status, body)
 
     async def _handle(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter) -> None:
         peer = "%s:%s" % (writer.get_extra_info("peername") or ("?", 0))[:2]
@@ -146,16 +165,19 @@ class HttpServer:
                 try:
                     handler, params = self.router.match(req.method, req.path)
                     res = await handler(req, **params)
-                    if not isinstance(res, Response):
+                    if not isinstance(res, (Response, StreamResponse)):
                         res = Response(200, res)
                 except HttpError as e:
-                    res = Response(e.status, e.body)
+                    res = self._error(req.path, e)
                 except Exception as e:  # noqa: BLE001 - keep the server alive
                     if self.on_error:
                         self.on_error(traceback.format_exc())
-                    res = Response(500, {"type": "error", "status": 500, "message": repr(e)})
+                    res = self._error(req.path, HttpError(500, repr(e)))
                 keep = req.headers.get("connection", "").lower() != "close"
-                await self._send(writer, res, keep=keep, head=req.method == "HEAD")
+                if isinstance(res, StreamResponse):
+                    await self._stream(writer, res, keep=keep)
+                else:
+                    await self._send(writer, res, keep=keep, head=req.method == "HEAD")
                 if not keep:
                     return
         except (ConnectionError, asyncio.IncompleteReadError):
@@ -174,6 +196,26 @@ class HttpServer:
                f"Connection: {'keep-alive' if keep else 'close'}"]
         hdr += [f"{k}: {v}" for k, v in res.headers.items()]
         writer.write(("\r\n".join(hdr) + "\r\n\r\n").encode("latin-1") + (b"" if head else body))
+        await writer.drain()
+
+    @staticmethod
+    async def _stream(writer: asyncio.StreamWriter, res: StreamResponse, keep: bool) -> None:
+        hdr = [f"HTTP/1.1 {res.status} {REASONS.get(res.status, 'Status')}", f"Content-Type: {res.content_type}",
+               "Transfer-Encoding: chunked", "Cache-Control: no-cache, private",
+               f"Connection: {'keep-alive' if keep else 'close'}"]
+        hdr += [f"{k}: {v}" for k, v in res.headers.items()]
+        writer.write(("\r\n".join(hdr) + "\r\n\r\n").encode("latin-1"))
+        await writer.drain()
+        try:
+            async for chunk in res.chunks:
+                if chunk:
+                    writer.write(b"%x\r\n%s\r\n" % (len(chunk), chunk))
+                    await writer.drain()
+        finally:
+            aclose = getattr(res.chunks, "aclose", None)
+            if aclose is not None:
+                await aclose()
+        writer.write(b"0\r\n\r\n")
         await writer.drain()
 
     async def start(self, host: str, port: int) -> tuple[str, int]:

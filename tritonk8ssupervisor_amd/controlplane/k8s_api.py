@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import asyncio
 import copy
+import json
 import os
 import secrets
 import time
@@ -13,7 +14,8 @@ from pathlib import Path
 
 from ..utils.net import host_port
 from ..utils.trace import trace
-from .httpserver import HttpError, Request, Response
+from . import k8s_wire
+from .httpserver import HttpError, Request, Response, StreamResponse
 from .objects import (
     GPU, _key, _set_ready, merge_patch, _admit_gpu_visibility, _normalize_data, labels_match, _parse_selector,
 )
@@ -27,8 +29,13 @@ class KubernetesAPI:
     def _strip(self, obj: dict) -> dict:
         return {k: v for k, v in obj.items() if not k.startswith("_")}
 
-    async def _list_or_watch(self, req: Request, kind: str, pred) -> dict:
+    async def _list_or_watch(self, req: Request, kind: str, pred):
+        fsel = k8s_wire.parse_field_selector(req.q("fieldSelector"))
+        if fsel:
+            base, pred = pred, (lambda o: base(o) and k8s_wire.fields_match(fsel, o))
         if req.q("watch") in ("1", "true"):
+            if req.q("batch") != "1":  # a stock client: a Kubernetes watch stream
+                return StreamResponse(self._watch_stream(req, kind, pred))
             since = int(req.q("resourceVersion", "0") or 0)
             timeout = min(float(req.q("timeoutSeconds", "30") or 30), 300.0)
             ev = await self.store.wait_events(since, kind, timeout, pred)
@@ -36,7 +43,49 @@ class KubernetesAPI:
                     "events": [{"type": e["type"], "object": self._strip(e["object"])} for e in ev]}
         items = [self._strip(o) for o in self.store.list(kind, pred)]
         items.sort(key=lambda o: (o["metadata"].get("namespace", ""), o["metadata"]["name"]))
-        return {"kind": "List", "apiVersion": "v1", "metadata": {"resourceVersion": str(self.store.rv)}, "items": items}
+        if k8s_wire.wants_table(req.headers.get("accept", "")):
+            return k8s_wire.table(kind, items, str(self.store.rv))
+        api, lk = k8s_wire.list_kind(kind) if kind in k8s_wire.RESOURCES else ("v1", "List")
+        return {"kind": lk, "apiVersion": api, "metadata": {"resourceVersion": str(self.store.rv)}, "items": items}
+
+    async def _watch_stream(self, req: Request, kind: str, pred):
+        """Kubernetes watch: newline-delimited ``{"type", "object"}`` events until timeoutSeconds.
+        No resourceVersion (or "0"): the current objects first, as ADDED; a resourceVersion older
+        than the kept history: one ERROR event with a 410 Expired Status (the client relists)."""
+        rv = req.q("resourceVersion") or ""
+        timeout = min(float(req.q("timeoutSeconds") or 1800), 3600.0)
+        deadline = time.monotonic() + timeout
+
+        def line(etype: str, obj: dict) -> bytes:
+            return (json.dumps({"type": etype, "object": obj}, separators=(",", ":"), default=str) + "\n").encode()
+
+        if rv in ("", "0"):
+            since = self.store.rv
+            for o in sorted(self.store.list(kind, pred), key=lambda o: o["metadata"].get("name", "")):
+                yield line("ADDED", self._strip(o))
+        else:
+            try:
+                since = int(rv)
+            except ValueError:
+                yield line("ERROR", k8s_wire.status_body(400, f"invalid resourceVersion {rv!r}"))
+                return
+            hist = self.store.history
+            oldest = hist[0][0] if hist else self.store.rv + 1
+            if since < self.store.rv and since < oldest - 1:
+                yield line("ERROR", k8s_wire.status_body(410, f"too old resource version: {since} ({oldest - 1})"))
+                return
+        if req.q("sendInitialEvents") == "true" and req.q("allowWatchBookmarks") == "true":
+            yield line("BOOKMARK", {"kind": k8s_wire.RESOURCES.get(kind, ("", "", "Status"))[2],
+                                    "apiVersion": k8s_wire.group_version(kind) if kind in k8s_wire.RESOURCES else "v1",
+                                    "metadata": {"resourceVersion": str(since),
+                                                 "annotations": {"k8s.io/initial-events-end": "true"}}})
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                return
+            for e in await self.store.wait_events(since, kind, left, pred):
+                since = e["resourceVersion"]
+                yield line(e["type"], self._strip(e["object"]))
 
     async def h_nodes(self, req: Request, pid: str | None = None):
         p = self._pid(pid, req)
@@ -124,18 +173,18 @@ class KubernetesAPI:
         names = {"default", "kube-system", "amd-gpu"}
         for kind in ("pods", "daemonsets", "jobs", "deployments", "services", "configmaps", "secrets", "ingresses"):
             names |= {o["metadata"].get("namespace", "default") for o in self.store.list(kind)}
-        return {"kind": "NamespaceList", "items": [{"metadata": {"name": n}} for n in sorted(names)]}
+        items = [{"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": n}, "spec": {"finalizers": ["kubernetes"]},
+                  "status": {"phase": "Active"}} for n in sorted(names)]
+        if k8s_wire.wants_table(req.headers.get("accept", "")):
+            return k8s_wire.table("namespaces", items, str(self.store.rv))
+        return {"kind": "NamespaceList", "apiVersion": "v1", "metadata": {"resourceVersion": str(self.store.rv)},
+                "items": items}
 
     # ---- k8s: generic namespaced kinds ------------------------------------------------
     async def h_pods(self, req: Request, pid: str | None = None):
         p = self._pid(pid, req)
-        node = None
-        fs = req.q("fieldSelector") or ""
-        if fs.startswith("spec.nodeName="):
-            node = fs.split("=", 1)[1]
         sel = _parse_selector(req.q("labelSelector"))
-        return await self._list_or_watch(req, "pods", lambda o: self._in(p, o) and (node is None or o["spec"].get("nodeName") == node)
-                                         and labels_match(sel, o["metadata"].get("labels")))
+        return await self._list_or_watch(req, "pods", lambda o: self._in(p, o) and labels_match(sel, o["metadata"].get("labels")))
 
     def _lister(self, kind: str, all_ns: bool = False):
         async def h(req: Request, pid: str | None = None, ns: str | None = None):
@@ -167,6 +216,22 @@ class KubernetesAPI:
             p = self._pid(pid, req)
             self._auth(req, self.project(p))
             body = req.json()
+            ctype = (req.headers.get("content-type") or "").split(";")[0].strip()
+            if merge and ctype in (k8s_wire.JSON_PATCH, k8s_wire.STRATEGIC_PATCH):
+                cur = self.store.get(kind, _key(p, ns, name))
+                if cur is None:
+                    raise HttpError(404, f'{kind} "{name}" not found')
+                try:
+                    full = (k8s_wire.json_patch(self._strip(cur), body) if ctype == k8s_wire.JSON_PATCH
+                            else k8s_wire.strategic_merge(self._strip(cur), body))
+                except k8s_wire.PatchError as e:
+                    raise HttpError(422, str(e)) from e
+                if not isinstance(full, dict):
+                    raise HttpError(422, "the patched object is not an object")
+                full.setdefault("metadata", {})["resourceVersion"] = cur["metadata"].get("resourceVersion")
+                return self._strip(self.replace(p, kind, ns, name, full, merge=False))
+            if merge and ctype == k8s_wire.APPLY_PATCH:
+                raise HttpError(415, "server-side apply is not supported; use client-side kubectl apply")
             if not isinstance(body, dict):
                 raise HttpError(422, "the body must be a JSON object")
             return self._strip(self.replace(p, kind, ns, name, body, merge=merge))

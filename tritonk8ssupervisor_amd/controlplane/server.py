@@ -16,7 +16,11 @@ Rancher-compatible REST (what the reference's Ansible roles call):
 
 Kubernetes subset under /r/projects/ENV/kubernetes and /api, /apis (default project):
   nodes (leases, Ready/NotReady), pods, daemonsets, jobs (Indexed), deployments, services,
-  events; watch = long-poll batches (?watch=1&resourceVersion=N&timeoutSeconds=T).
+  events; watch = a Kubernetes watch stream (chunked JSON lines, ?watch=true), or long-poll
+  batches for tk8s's own clients (?watch=1&batch=1&resourceVersion=N&timeoutSeconds=T).
+  Discovery, typed lists, Status errors, field selectors, merge/JSON/strategic patches and
+  server-side Tables follow the Kubernetes wire conventions (k8s_wire.py), so a stock kubectl
+  works against the kubeconfig.
   Extended resource ``amd.com/gpu`` is scheduled like the AMD k8s-device-plugin exposes it.
 
 Extras: /v1/kv/KEY (rendezvous store, e.g. RCCL unique ids), /v1/cluster/wait (event-driven
@@ -40,6 +44,7 @@ import time
 from pathlib import Path
 
 from ..utils.net import host_port
+from . import k8s_wire
 from .controllers import Controllers
 from .httpserver import HttpError, HttpServer, Request, Response, Router
 from .k8s_api import KubernetesAPI
@@ -57,8 +62,9 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
         self.state_dir = Path(state_dir) if state_dir else None
         self.node_grace = node_grace
         self.store = Store()
+        self.store.type_meta = k8s_wire.type_meta()
         self.router = Router()
-        self.http = HttpServer(self.router, on_error=self._log_error)
+        self.http = HttpServer(self.router, on_error=self._log_error, error_body=self._error_body)
         self.leases: dict[str, float] = {}   # node key -> monotonic time of last heartbeat
         self.started = time.time()
         self._stop = None
@@ -156,6 +162,11 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
         for pre in (r"/r/projects/(?P<pid>[^/]+)/kubernetes", r""):
             def add(method, path, h, pre=pre):
                 r.add(method, pre + path, h)
+            add("GET", r"/api/?", self.h_api_versions)
+            add("GET", r"/apis/?", self.h_api_groups)
+            add("GET", r"/api/v1/?", self.h_api_resources)
+            add("GET", r"/apis/(?P<group>[^/]+)/?", self.h_api_group)
+            add("GET", r"/apis/(?P<group>[^/]+)/(?P<version>[^/]+)/?", self.h_api_resources)
             add("GET", r"/api/v1/nodes", self.h_nodes)
             add("GET", r"/api/v1/nodes/(?P<name>[^/]+)", self.h_node_get)
             add("PUT", r"/api/v1/nodes/(?P<name>[^/]+)/status", self.h_node_status)
@@ -178,6 +189,31 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
             add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/exec", self.h_pod_exec)
             add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs", self.h_node_execs)
             add("PUT", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)", self.h_exec_result)
+
+    # ---- Kubernetes discovery (k8s_wire.py) ----------------------------------------------
+    @staticmethod
+    def _error_body(path: str, e: HttpError):
+        if k8s_wire.is_k8s_path(path):
+            return k8s_wire.status_body(e.status, e.message)
+        return e.body
+
+    async def h_api_versions(self, req: Request, pid: str | None = None):
+        return k8s_wire.api_versions(req.headers.get("host") or f"{self.host}:{self.port}")
+
+    async def h_api_groups(self, req: Request, pid: str | None = None):
+        return k8s_wire.api_group_list()
+
+    async def h_api_group(self, req: Request, group: str, pid: str | None = None):
+        g = k8s_wire.api_group(group)
+        if g is None:
+            raise HttpError(404, f"the server could not find the requested resource (group {group})")
+        return g
+
+    async def h_api_resources(self, req: Request, group: str = "", version: str = "v1", pid: str | None = None):
+        r = k8s_wire.api_resource_list(group, version)
+        if r is None:
+            raise HttpError(404, f"the server could not find the requested resource ({group}/{version})")
+        return r
 
     # ---- misc handlers ---------------------------------------------------------------
     async def h_ping(self, req: Request, **_):

@@ -33,6 +33,7 @@ class Store:
         self.history: deque[tuple[int, str, str, dict]] = deque(maxlen=HISTORY)
         self._waiters: list[asyncio.Future] = []
         self.listeners: list[Callable[[str, str, dict], None]] = []
+        self.type_meta: dict[str, tuple[str, str]] = {}  # kind -> (apiVersion, Kind) stamped on put
 
     # ---- reads ------------------------------------------------------------------------
     def get(self, kind: str, key: str) -> dict | None:
@@ -72,6 +73,10 @@ class Store:
         if expect_rv is not None and old is not None and old["metadata"].get("resourceVersion") != expect_rv:
             raise Conflict(f"{kind}/{key}: resourceVersion {expect_rv} is stale")
         self.rv += 1
+        tm = self.type_meta.get(kind)
+        if tm is not None:
+            obj.setdefault("apiVersion", tm[0])
+            obj.setdefault("kind", tm[1])
         md = obj.setdefault("metadata", {})
         md["resourceVersion"] = str(self.rv)
         md.setdefault("uid", old["metadata"]["uid"] if old else str(uuid.uuid4()))
