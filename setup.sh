@@ -9,8 +9,9 @@ cd "$(dirname "$0")"
 PY="${TK8S_PYTHON:-python3}"
 if [[ "${1:-}" == "-c" ]]; then
     shift
-    exec "$PY" -S -m tritonk8ssupervisor_amd.cli clean "$@"
+    exec "$PY" -S -c 'from tritonk8ssupervisor_amd.cli.fast import run; run()' clean "$@"
 fi
 # -S: skip site-packages .pth processing at start-up (tritonk8ssupervisor_amd/__init__.py adds
-# the site directories back); the CLI's start-up is part of the bring-up time.
-exec "$PY" -S -m tritonk8ssupervisor_amd.cli setup "$@"
+# the site directories back); -c instead of -m: no runpy. The CLI's start-up is part of the
+# bring-up time.
+exec "$PY" -S -c 'from tritonk8ssupervisor_amd.cli.fast import run; run()' setup "$@"

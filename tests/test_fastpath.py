@@ -1,0 +1,214 @@
+"""The import-light replacements on the bring-up path behave like the stdlib pieces they stand
+in for: utils/record.py (dataclasses), utils/pool.py (concurrent.futures), utils/http1.py
+(http.client), utils/ids.py (uuid.uuid5), utils/yamlio.py's parse cache (PyYAML) -- and
+./setup.sh's interpreter does not import the heavy modules at all."""
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+import uuid
+from pathlib import Path
+
+import pytest
+import yaml
+
+from tritonk8ssupervisor_amd.utils import yamlio
+from tritonk8ssupervisor_amd.utils.http1 import Connection, ProtocolError
+from tritonk8ssupervisor_amd.utils.ids import uuid5
+from tritonk8ssupervisor_amd.utils.pool import Pool, as_completed
+from tritonk8ssupervisor_amd.utils.record import asdict, field, fields, record
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+# ---- record ---------------------------------------------------------------------------------
+@record
+class Point:
+    x: int
+    y: int = 0
+    tags: list = field(default_factory=list)
+
+
+@record(frozen=True)
+class Key:
+    name: str
+    n: int = 1
+
+
+@record
+class Outer:
+    p: Point
+    ps: list = field(default_factory=list)
+
+
+def test_record_init_repr_eq():
+    a = Point(1)
+    assert (a.x, a.y, a.tags) == (1, 0, [])
+    assert Point(1, 2, ["t"]) == Point(x=1, y=2, tags=["t"]) and Point(1) != Point(2)
+    assert repr(Point(1, 2)) == "Point(x=1, y=2, tags=[])"
+    assert Point(1).tags is not Point(1).tags  # fresh default per instance
+    assert [f.name for f in fields(Point)] == ["x", "y", "tags"]
+    with pytest.raises(TypeError):
+        Point()
+    with pytest.raises(TypeError):
+        Point(1, 2, [], 4)
+    with pytest.raises(TypeError):
+        Point(1, x=2)
+    with pytest.raises(TypeError):
+        Point(1, z=3)
+    with pytest.raises(TypeError):
+        hash(Point(1))  # eq without frozen: unhashable, as with dataclasses
+
+
+def test_record_frozen_and_asdict():
+    k = Key("a")
+    assert {k: 1}[Key("a", 1)] == 1
+    with pytest.raises(AttributeError):
+        k.name = "b"
+    o = Outer(Point(1, tags=["x"]), [Point(2)])
+    d = asdict(o)
+    assert d == {"p": {"x": 1, "y": 0, "tags": ["x"]}, "ps": [{"x": 2, "y": 0, "tags": []}]}
+    d["p"]["tags"].append("y")
+    assert o.p.tags == ["x"]  # deep copy
+
+
+# ---- pool -----------------------------------------------------------------------------------
+def test_pool_map_order_errors_and_as_completed():
+    with Pool(4) as p:
+        assert p.map(lambda v: v * v, range(10)) == [v * v for v in range(10)]
+
+        def boom(v):
+            if v == 3:
+                raise ValueError("three")
+            return v
+
+        with pytest.raises(ValueError):
+            p.map(boom, range(5))
+        futs = [p.submit(time.sleep, d) for d in (0.15, 0.01, 0.08)]
+        order = [futs.index(f) for f in as_completed(futs)]
+        assert order == [1, 2, 0]
+        assert len(p._threads) <= 4
+    with pytest.raises(RuntimeError):
+        p.submit(lambda: 1)
+
+
+def test_pool_reuses_idle_workers():
+    p = Pool(8)
+    for _ in range(20):
+        p.submit(lambda: None).result()
+    assert len(p._threads) == 1
+    p.shutdown()
+
+
+# ---- http1 ----------------------------------------------------------------------------------
+def _serve(responses):
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    seen = []
+
+    def run():
+        c, _ = srv.accept()
+        f = c.makefile("rb")
+        for resp in responses:
+            req = b""
+            while not req.endswith(b"\r\n\r\n"):
+                line = f.readline()
+                if not line:
+                    return
+                req += line
+            n = next((int(ln.split(b":")[1]) for ln in req.split(b"\r\n") if ln.lower().startswith(b"content-length")), 0)
+            seen.append(req + f.read(n))
+            c.sendall(resp)
+        c.close()
+        srv.close()
+
+    threading.Thread(target=run, daemon=True).start()
+    return srv.getsockname()[1], seen
+
+
+def test_http1_content_length_chunked_and_keepalive():
+    port, seen = _serve([b"HTTP/1.1 100 Continue\r\n\r\nHTTP/1.1 200 OK\r\nContent-Length: 5\r\nX-A: 1\r\n\r\nhello",
+                         b"HTTP/1.1 201 Created\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n2;ext=1\r\nde\r\n0\r\n\r\n",
+                         b"HTTP/1.1 204 No Content\r\n\r\n",
+                         b"HTTP/1.0 200 OK\r\n\r\nuntil close"])
+    c = Connection("127.0.0.1", port, timeout=5)
+    r = c.request("GET", "/a")
+    assert (r.status, r.body, r.header("x-a")) == (200, b"hello", "1")
+    r = c.request("POST", "/b", body=b'{"k":1}', headers={"Content-Type": "application/json"})
+    assert (r.status, r.body) == (201, b"abcde")
+    assert c.request("DELETE", "/c").status == 204
+    r = c.request("GET", "/d")
+    assert r.body == b"until close" and not c.connected
+    assert seen[0].startswith(b"GET /a HTTP/1.1\r\n") and b"Host: 127.0.0.1:" in seen[0]
+    assert seen[1].endswith(b'\r\n\r\n{"k":1}') and b"Content-Length: 7" in seen[1]
+
+
+def test_http1_truncated_response_is_an_error():
+    port, _ = _serve([b"HTTP/1.1 200 OK\r\nContent-Length: 10\r\n\r\nshort"])
+    c = Connection("127.0.0.1", port, timeout=5)
+    with pytest.raises(ProtocolError):
+        c.request("GET", "/")
+    assert not c.connected
+
+
+# ---- ids ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["tk8s/machine/kubenode1", "", "ünïcode/名"])
+def test_uuid5_matches_the_stdlib(name):
+    ns = "5f1c0d3e-8a4b-4c6e-9b1a-7e2f3d4c5b6a"
+    assert uuid5(ns, name) == str(uuid.uuid5(uuid.UUID(ns), name))
+
+
+# ---- yaml parse cache ------------------------------------------------------------------------
+def test_yaml_cache_returns_exactly_the_parse(tmp_path, monkeypatch):
+    monkeypatch.setenv("TK8S_YAML_CACHE", str(tmp_path / "c"))
+    text = "a: 1\nb: [yes, no, on, '0x1f', 0x1f, 1e3, 1.5e3, ~]\nc: {d: e}\n0: zero\n"
+    want = yaml.safe_load(text)
+    assert yamlio.load(text) == want                # miss: parsed and stored
+    assert len(os.listdir(tmp_path / "c")) == 1
+    first = yamlio.load(text)
+    assert first == want and yamlio.load(text) is not first   # hit: a fresh copy each time
+    first["a"] = 2
+    assert yamlio.load(text)["a"] == 1
+    assert yamlio.load_all("---\nx: 1\n---\ny: 2\n") == [{"x": 1}, {"y": 2}]
+    stamp = "when: 2024-01-02 03:04:05\n"       # a timestamp marshal cannot hold: not cached
+    assert yamlio.load(stamp) == yaml.safe_load(stamp)
+    assert len(os.listdir(tmp_path / "c")) == 2
+
+
+def test_yaml_cache_entry_must_match_the_text(tmp_path, monkeypatch):
+    import marshal
+
+    monkeypatch.setenv("TK8S_YAML_CACHE", str(tmp_path))
+    text = "k: v\n"
+    yamlio.load(text)
+    (entry,) = tmp_path.iterdir()
+    entry.write_bytes(marshal.dumps(("k: other\n", {"k": "forged"})))  # same key, different text
+    assert yamlio.load(text) == {"k": "v"}
+
+
+def test_flat_mapping_is_what_yaml_reads(tmp_path, monkeypatch):
+    monkeypatch.setenv("TK8S_YAML_CACHE", str(tmp_path))
+    data = {"master": "127.0.1.2", "kubernetes_name": 'k8s "dev"\tü', "n": 3, "b": True, "z": None}
+    text = yamlio.flat_mapping(data)
+    assert yaml.safe_load(text) == data
+    assert yamlio.load(text) == data
+    with pytest.raises(ValueError):
+        yamlio.flat_mapping({"a": [1]})
+
+
+def test_setup_cli_does_not_import_the_heavy_modules(tmp_path):
+    """What ./setup.sh's interpreter loads before the bring-up starts (cli/fast.py, cli/main.py,
+    orchestrator.py): none of the modules the fast path replaced."""
+    code = ("import sys; from tritonk8ssupervisor_amd.cli import main; from tritonk8ssupervisor_amd import orchestrator, "
+            "playbook, playbook_modules, provision; from tritonk8ssupervisor_amd.provider import local; "
+            "from tritonk8ssupervisor_amd.controlplane import client; "
+            "bad = {'yaml', 'dataclasses', 'inspect', 'concurrent.futures', 'logging', 'uuid', 'http.client', "
+            "'urllib.request', 'email.parser', 'ssl', 'tempfile', 'hashlib', 'typing', 'runpy'} & set(sys.modules); "
+            "print(sorted(bad))")
+    r = subprocess.run([sys.executable, "-S", "-c", code], cwd=REPO, capture_output=True, text=True, timeout=60,
+                       env={**os.environ, "PYTHONPATH": str(REPO)})
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "[]", r.stdout

@@ -16,7 +16,7 @@ Unhealthy while it reports uncorrectable or deferred ECC errors, and keeps its t
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass, field
+from ..utils.record import field, record as dataclass
 from pathlib import Path
 
 from ..models.hostinfo import HostInventory, compose_visible_devices, discover

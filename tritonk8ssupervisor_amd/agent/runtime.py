@@ -15,7 +15,7 @@ import signal
 import subprocess
 import threading
 import time
-from dataclasses import dataclass, field
+from ..utils.record import field, record as dataclass
 from pathlib import Path
 
 from ..utils.fsutil import atomic_write_json

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import os
 import shlex
-from dataclasses import asdict, dataclass, field, fields
+from .utils.record import asdict, field, fields, record as dataclass
 from pathlib import Path
 
 from .utils.fsutil import atomic_write

@@ -1,12 +1,13 @@
-"""Keep-alive HTTP/JSON client for the tk8s control plane (stdlib only, import-light)."""
+"""Keep-alive HTTP/JSON client for the tk8s control plane (stdlib only, import-light: the
+connection is utils/http1.py, not http.client)."""
 from __future__ import annotations
 
-import http.client
 import json
 import threading
 import time
-from typing import Any
 from urllib.parse import urlencode, urlsplit
+
+from ..utils.http1 import Connection
 
 
 class ApiError(RuntimeError):
@@ -27,16 +28,14 @@ class Client:
         self.prefix = prefix.rstrip("/")
         self.token = token
         self.timeout = timeout
-        self._conn: http.client.HTTPConnection | None = None
+        self._conn: Connection | None = None
         self._lock = threading.Lock()
 
-    def _connection(self, timeout: float) -> http.client.HTTPConnection:
+    def _connection(self, timeout: float) -> Connection:
         if self._conn is None:
-            self._conn = http.client.HTTPConnection(self.host, self.port, timeout=timeout)
+            self._conn = Connection(self.host, self.port, timeout=timeout)
         else:
-            self._conn.timeout = timeout
-            if self._conn.sock is not None:
-                self._conn.sock.settimeout(timeout)
+            self._conn.set_timeout(timeout)
         return self._conn
 
     def close(self) -> None:
@@ -65,20 +64,19 @@ class Client:
         with self._lock:
             for attempt in range(2):  # one transparent reconnect for a dropped keep-alive
                 conn = self._connection(t)
+                reused = conn.connected
                 try:
-                    conn.request(method, url, body=data, headers=headers)
-                    resp = conn.getresponse()
-                    payload = resp.read()
-                    status = resp.status
-                    ctype = resp.getheader("Content-Type", "")
-                    if resp.getheader("Connection", "").lower() == "close":
-                        conn.close()
+                    resp = conn.request(method, url, body=data, headers=headers)
+                    payload, status, ctype = resp.body, resp.status, resp.header("content-type")
+                    if not conn.connected:  # the server closed it (Connection: close)
                         self._conn = None
                     break
-                except (http.client.HTTPException, ConnectionError, OSError):
+                except OSError as e:
                     conn.close()
                     self._conn = None
-                    if attempt:
+                    # only a keep-alive connection the server dropped while idle is retried: a
+                    # fresh connection's failure or a timeout is the caller's to see
+                    if attempt or not reused or isinstance(e, TimeoutError):
                         raise
         if raw:
             if status not in ok:
@@ -114,7 +112,7 @@ class Client:
             try:
                 if self.request("GET", "/ping", raw=True, timeout=2.0) == "pong":
                     return True
-            except (ApiError, OSError, http.client.HTTPException):
+            except (ApiError, OSError):
                 pass
             time.sleep(interval)
         return False

@@ -10,7 +10,7 @@ import asyncio
 import json
 import re
 import traceback
-from dataclasses import dataclass, field
+from ..utils.record import field, record as dataclass
 from typing import Any, AsyncIterator, Awaitable, Callable
 from urllib.parse import parse_qs, unquote, urlsplit
 

@@ -337,7 +337,7 @@ def zygote_for(sandbox: str) -> dict | None:
 
 
 def launch(argv: list[str]) -> Early | None:
-    """Called first thing by ``python -m tritonk8ssupervisor_amd.cli setup ...``."""
+    """Called first thing by ``./setup.sh`` (cli/fast.py) for ``setup ...``."""
     global _LAUNCHED, _ZYGOTE
     try:
         p = plan(argv)

@@ -16,9 +16,8 @@ from __future__ import annotations
 
 import os
 import re
-from dataclasses import dataclass, field
+from .utils.record import field, record as dataclass
 from pathlib import Path
-from typing import Any
 
 
 class HclError(ValueError):

@@ -14,7 +14,7 @@ GPU runtime; only leaf validation pods do (tools/tk8s_gpuinfo.cpp is the authori
 from __future__ import annotations
 
 import os
-from dataclasses import asdict, dataclass, field
+from ..utils.record import asdict, field, record as dataclass
 from pathlib import Path
 
 from ..earlyburn import compose_visible_devices, idx_list, kfd_gpu_nodes, read_props, visible_filter  # noqa: F401

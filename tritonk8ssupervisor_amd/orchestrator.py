@@ -21,9 +21,8 @@ import shutil
 import sys
 import threading
 import time
-from dataclasses import dataclass
+from .utils.record import record as dataclass
 from pathlib import Path
-from typing import Callable
 
 from . import hcl
 from .config import ClusterConfig, export_vars, read_config, write_config
@@ -433,8 +432,10 @@ class Setup:
         self.out("Creating ansible hosts file and variable files")
         self.out("    created: ansible/hosts")
         master = masters[-1]
-        atomic_write(ws.vars_file, f"master: {master}\nkubernetes_name: {json.dumps(cfg.KUBERNETES_NAME)}\n"
-                                   f"kubernetes_description: {json.dumps(cfg.KUBERNETES_DESCRIPTION)}\n")
+        from .utils.yamlio import flat_mapping
+
+        atomic_write(ws.vars_file, flat_mapping({"master": master, "kubernetes_name": cfg.KUBERNETES_NAME,
+                                                 "kubernetes_description": cfg.KUBERNETES_DESCRIPTION}))
         _set_ini_value(ws.ansible / "ansible.cfg", "private_key_file", cfg.SDC_KEY)
         self.out("    created: ansible/roles/ranchermaster/vars/vars.yml")
 
@@ -1035,6 +1036,8 @@ def _kubeadm_reset(ws: "Workspace", provider, out) -> None:
     with cf.ThreadPoolExecutor(max_workers=max(1, len(machines))) as pool:
         for m, (rc, text) in zip(machines, pool.map(lambda m: provider.exec(m, KUBEADM_RESET, timeout=300), machines)):
             out(f"    kubeadm reset on {m.name}: {'ok' if rc == 0 else 'failed: ' + text.strip()[-200:]}")
+
+
 def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out: Callable[[str], None] = print,
           backend: str | None = None) -> int:
     """cleanRunner (setup.sh:484-521), non-destructive unless confirmed."""

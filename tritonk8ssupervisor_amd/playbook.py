@@ -18,16 +18,15 @@ our role uses explicit tests), ``playbook_dir: $(pwd)`` (clusterUp.yml:12 — th
 """
 from __future__ import annotations
 
-import concurrent.futures as cf
 import configparser
 import copy
 import os
 import shlex
 import threading
 import time
-from dataclasses import dataclass, field
+from .utils.pool import Pool
+from .utils.record import field, record as dataclass
 from pathlib import Path
-from typing import Any, Callable
 
 from . import templating
 from .templating import TemplateError, Undefined
@@ -124,7 +123,7 @@ class Playbook:
         self.hostvars: dict[str, dict] = {h: {} for h in self.hosts}
         self.stats = {h: {"ok": 0, "changed": 0, "failed": 0, "skipped": 0, "unreachable": 0} for h in self.hosts}
         self._print_lock = threading.Lock()
-        self._pool: cf.ThreadPoolExecutor | None = None
+        self._pool: Pool | None = None
         # every module invocation as rendered (play, host, task, module, args): what --check
         # reports and the golden tests pin
         self.trace: list[dict] = []
@@ -383,12 +382,11 @@ class Playbook:
     def _facts_done(self, hosts: list[Host]) -> bool:
         return all("ansible_kernel" in self.hostvars.get(h.name, {}) for h in hosts)
 
-    def _executor(self) -> cf.ThreadPoolExecutor:
+    def _executor(self) -> Pool:
         """One pool for the whole run (``forks`` workers; 0 = every host): starting fresh threads
         for every task cost ~2.5 ms per thread start under GIL contention at 9 hosts."""
         if self._pool is None:
-            self._pool = cf.ThreadPoolExecutor(max_workers=max(1, self.forks or len(self.hosts)),
-                                               thread_name_prefix="play")
+            self._pool = Pool(max(1, self.forks or len(self.hosts)), "play")
         return self._pool
 
     def _host_by_addr(self, target: str) -> Host | None:

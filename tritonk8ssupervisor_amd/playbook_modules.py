@@ -20,12 +20,8 @@ import shlex
 import socket
 import subprocess
 import time
-import urllib.error
-import urllib.request
 from pathlib import Path
-from typing import Any
 
-import yaml
 
 from . import templating
 
@@ -317,6 +313,45 @@ def m_setup(args, *, ctx, target, local, **_):
 
 
 # ---- uri ----------------------------------------------------------------------------------
+def _http(method: str, url: str, data: bytes | None, headers: dict, timeout: float,
+          redirects: int = 5) -> tuple[int, bytes]:
+    """One HTTP(S) request: plain HTTP over utils/http1.py (the connection the control-plane
+    client uses; urllib.request would add its import cost to the bring-up), HTTPS over
+    http.client. Follows redirects for GET/HEAD like the uri module's ``follow_redirects: safe``."""
+    from urllib.parse import urljoin, urlsplit
+
+    for _ in range(redirects + 1):
+        u = urlsplit(url)
+        if u.scheme not in ("http", "https") or not u.hostname:
+            raise ValueError(f"unsupported URL {url!r}")
+        target = (u.path or "/") + (f"?{u.query}" if u.query else "")
+        hdrs = {"Connection": "close", "User-Agent": "tk8s-uri", **headers}
+        if u.scheme == "http":
+            from .utils.http1 import Connection
+
+            conn = Connection(u.hostname, u.port or 80, timeout=timeout)
+            try:
+                r = conn.request(method, target, body=data, headers=hdrs)
+            finally:
+                conn.close()
+            status, content, loc = r.status, r.body, r.header("location")
+        else:
+            import http.client
+
+            hc = http.client.HTTPSConnection(u.hostname, u.port, timeout=timeout)
+            try:
+                hc.request(method, target, body=data, headers=hdrs)
+                hr = hc.getresponse()
+                status, content, loc = hr.status, hr.read(), hr.getheader("Location")
+            finally:
+                hc.close()
+        if status in (301, 302, 303, 307, 308) and loc and method in ("GET", "HEAD"):
+            url = urljoin(url, loc)
+            continue
+        return status, content
+    raise ValueError(f"too many redirects from {url}")
+
+
 def m_uri(args, *, check, **_):
     method = str(args.get("method", "GET")).upper()
     if check and method != "GET":
@@ -343,14 +378,10 @@ def m_uri(args, *, check, **_):
             data = body.encode() if isinstance(body, str) else json.dumps(body).encode()
     if method in ("POST", "PUT", "PATCH") and data is None:
         data = b""
-    req = urllib.request.Request(url, data=data, method=method, headers=headers)
     timeout = float(args.get("timeout", 30))
     try:
-        with urllib.request.urlopen(req, timeout=timeout) as r:
-            status, content = r.status, r.read()
-    except urllib.error.HTTPError as e:
-        status, content = e.code, e.read()
-    except (urllib.error.URLError, OSError) as e:
+        status, content = _http(method, url, data, headers, timeout)
+    except (OSError, ValueError) as e:
         if check:  # dry run: the service this GET targets is not up yet
             return {"skipped": True, "changed": False, "status": -1, "msg": f"check mode: {url} unreachable: {e}"}
         return {"failed": True, "status": -1, "msg": f"request to {url} failed: {e}", "url": url}
@@ -448,7 +479,9 @@ def m_stat(args, *, ctx, target, local, **_):
 
 def m_include_vars(args, *, ctx, target, local, **_):
     p = _path(args.get("file") or args.get("_raw_params"), ctx, target, True)
-    return {"ansible_facts": yaml.safe_load(p.read_text()) or {}, "changed": False}
+    from .utils import yamlio
+
+    return {"ansible_facts": yamlio.load(p.read_text()) or {}, "changed": False}
 
 
 # ---- control flow ---------------------------------------------------------------------------

@@ -37,7 +37,6 @@ import json
 import os
 import shlex
 import threading
-import uuid
 from pathlib import Path
 
 from ..utils import ssh
@@ -45,7 +44,7 @@ from ..utils.fsutil import atomic_write_json, file_lock, read_json
 from . import keys
 from .base import Machine, Network, Package, Provider, ProvisionError
 
-_NS = uuid.UUID("7b0e2c4a-1f3d-4e5b-8a6c-9d0e1f2a3b4c")
+_NS = "7b0e2c4a-1f3d-4e5b-8a6c-9d0e1f2a3b4c"
 DEFAULT_NETWORK = "baremetal-default"
 SHAPES = [1, 2, 4, 8]
 REPO = Path(__file__).resolve().parents[2]
@@ -54,7 +53,9 @@ _install_guard = threading.Lock()
 
 
 def _uid(kind: str, name: str) -> str:
-    return str(uuid.uuid5(_NS, f"tk8s/baremetal/{kind}/{name}"))
+    from ..utils.ids import uuid5
+
+    return uuid5(_NS, f"tk8s/baremetal/{kind}/{name}")
 
 
 def load_inventory(path: str | os.PathLike) -> dict:

@@ -2,7 +2,7 @@
 from __future__ import annotations
 
 import abc
-from dataclasses import asdict, dataclass, field
+from ..utils.record import asdict, field, record as dataclass
 
 
 @dataclass(frozen=True)
@@ -44,7 +44,7 @@ class Machine:
 
     @classmethod
     def from_dict(cls, d: dict) -> "Machine":
-        return cls(**{k: d[k] for k in cls.__dataclass_fields__ if k in d})
+        return cls(**{k: d[k] for k in (f.name for f in cls.__record_fields__) if k in d})
 
 
 class ProvisionError(RuntimeError):

@@ -19,7 +19,6 @@ from __future__ import annotations
 import contextlib
 import os
 from pathlib import Path
-from typing import Iterator
 
 from ..utils.fsutil import atomic_write_json, file_lock, read_json
 from ..utils.procs import pid_alive, read_pidfile

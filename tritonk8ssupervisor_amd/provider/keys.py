@@ -7,11 +7,15 @@ passes the private key path as root_authorized_keys, SURVEY.md §2.2 quirk — n
 """
 from __future__ import annotations
 
-import base64
-import hashlib
+import binascii
 import os
-import secrets
 from pathlib import Path
+
+try:  # the builtin hash modules: hashlib (OpenSSL) costs more to import than the bring-up hashes
+    from _md5 import md5
+    from _sha256 import sha256
+except ImportError:
+    from hashlib import md5, sha256
 
 from ..utils.fsutil import atomic_write
 
@@ -19,13 +23,13 @@ KEY_NAME = "tk8s_cluster_key"
 
 
 def fingerprint_md5(public_blob: bytes) -> str:
-    h = hashlib.md5(public_blob).hexdigest()
+    h = md5(public_blob).hexdigest()
     return ":".join(h[i : i + 2] for i in range(0, 32, 2))
 
 
 def public_line(private: bytes) -> str:
-    pub = hashlib.sha256(b"tk8s-public:" + private).digest()
-    return f"tk8s-key {base64.b64encode(pub).decode()} tk8s"
+    pub = sha256(b"tk8s-public:" + private).digest()
+    return f"tk8s-key {binascii.b2a_base64(pub, newline=False).decode()} tk8s"
 
 
 def ensure_cluster_key(key_dir: str | os.PathLike) -> tuple[Path, Path, str]:
@@ -34,17 +38,17 @@ def ensure_cluster_key(key_dir: str | os.PathLike) -> tuple[Path, Path, str]:
     d.mkdir(parents=True, exist_ok=True)
     priv, pub = d / KEY_NAME, d / f"{KEY_NAME}.pub"
     if not priv.exists():
-        atomic_write(priv, secrets.token_hex(32) + "\n", mode=0o600)
+        atomic_write(priv, os.urandom(32).hex() + "\n", mode=0o600)
     line = public_line(priv.read_bytes().strip())
     if not pub.exists() or pub.read_text().strip() != line:
         atomic_write(pub, line + "\n", mode=0o644)
-    return priv, pub, fingerprint_md5(base64.b64decode(line.split()[1]))
+    return priv, pub, fingerprint_md5(binascii.a2b_base64(line.split()[1]))
 
 
 def key_fingerprint(pub_path: str | os.PathLike) -> str | None:
     try:
         parts = Path(pub_path).read_text().split()
-        return fingerprint_md5(base64.b64decode(parts[1]))
+        return fingerprint_md5(binascii.a2b_base64(parts[1]))
     except (OSError, IndexError, ValueError):
         return None
 

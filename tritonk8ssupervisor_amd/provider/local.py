@@ -23,17 +23,17 @@ import os
 import shutil
 import socket
 import subprocess
-import uuid
 from pathlib import Path
 
 from ..models.hostinfo import discover
 from ..utils.fsutil import atomic_write_json, file_lock, read_json
+from ..utils.ids import uuid5
 from ..utils.procs import kill_pidfile
 from . import keys
 from .base import Machine, Network, Package, Provider, ProvisionError
 from .hostreg import HostRegistry
 
-_NS = uuid.UUID("5f1c0d3e-8a4b-4c6e-9b1a-7e2f3d4c5b6a")
+_NS = "5f1c0d3e-8a4b-4c6e-9b1a-7e2f3d4c5b6a"
 
 NETWORKS = [
     ("local-fabric", "127.0.2.0/24", False),
@@ -45,7 +45,7 @@ SHAPES = [("cpu-only", 0), ("mi355x-1gpu", 1), ("mi355x-2gpu", 2), ("mi355x-4gpu
 
 
 def _uid(kind: str, name: str) -> str:
-    return str(uuid.uuid5(_NS, f"tk8s/{kind}/{name}"))
+    return uuid5(_NS, f"tk8s/{kind}/{name}")
 
 
 def _loopback_multi_ok() -> bool:

@@ -17,12 +17,12 @@ Differences from the reference's Terraform usage:
 """
 from __future__ import annotations
 
-import concurrent.futures as cf
 import os
 import subprocess
 import threading
 import time
-from dataclasses import dataclass, field
+from .utils.pool import Pool, as_completed
+from .utils.record import field, record as dataclass
 from pathlib import Path
 
 from . import hcl
@@ -271,9 +271,9 @@ class Engine:
                 self._save_resource(s.address, None)
             todo.append(s)
         workers = self.parallelism or max(1, len(todo))
-        with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+        with Pool(workers, "provision") as ex:
             futs = {ex.submit(self._create, s): s for s in todo}
-            for f in cf.as_completed(futs):
+            for f in as_completed(futs):
                 s = futs[f]
                 try:
                     f.result()
@@ -321,7 +321,7 @@ class Engine:
             self._save_resource(addr, None)
             return addr
 
-        with cf.ThreadPoolExecutor(max_workers=max(1, len(st))) as ex:
-            for f in cf.as_completed([ex.submit(one, a, r) for a, r in st.items()]):
+        with Pool(max(1, len(st)), "destroy") as ex:
+            for f in as_completed([ex.submit(one, a, r) for a, r in st.items()]):
                 gone.append(f.result())
         return gone

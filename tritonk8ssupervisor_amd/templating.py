@@ -29,7 +29,6 @@ import tokenize
 import json
 import os
 import re
-from typing import Any
 
 
 class TemplateError(ValueError):

@@ -11,7 +11,6 @@ import os
 import threading
 import time
 from pathlib import Path
-from typing import Any, Iterator
 
 _lock = threading.Lock()
 

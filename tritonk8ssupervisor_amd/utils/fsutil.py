@@ -10,9 +10,18 @@ import contextlib
 import fcntl
 import json
 import os
-import tempfile
 from pathlib import Path
-from typing import Any, Iterator
+
+
+def _mkstemp(p: Path) -> tuple[int, str]:
+    """tempfile.mkstemp's contract (a new 0600 file, exclusive create) without importing
+    tempfile (random, bisect, weakref ...) on the bring-up path."""
+    while True:
+        tmp = str(p.parent / f".{p.name}.{os.urandom(6).hex()}.tmp")
+        try:
+            return os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_EXCL | os.O_CLOEXEC, 0o600), tmp
+        except FileExistsError:
+            continue
 
 
 def atomic_write(path: str | os.PathLike, data: str | bytes, mode: int | None = None, durable: bool = False) -> None:
@@ -23,7 +32,7 @@ def atomic_write(path: str | os.PathLike, data: str | bytes, mode: int | None = 
     guarantees that no reader ever sees a torn file."""
     p = Path(path)
     p.parent.mkdir(parents=True, exist_ok=True)
-    fd, tmp = tempfile.mkstemp(prefix=f".{p.name}.", suffix=".tmp", dir=p.parent)
+    fd, tmp = _mkstemp(p)
     try:
         with os.fdopen(fd, "wb") as f:
             f.write(data.encode() if isinstance(data, str) else data)

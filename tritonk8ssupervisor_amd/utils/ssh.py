@@ -25,7 +25,7 @@ import shlex
 import io
 import subprocess
 import tarfile
-from dataclasses import dataclass, field
+from .record import field, record as dataclass
 from pathlib import Path
 
 

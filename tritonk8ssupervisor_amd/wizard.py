@@ -14,7 +14,6 @@ import json
 import re
 import sys
 from pathlib import Path
-from typing import Iterable, TextIO
 
 from .config import ClusterConfig
 from .provider.base import Provider
