@@ -43,4 +43,25 @@ def pytest_sessionfinish(session, exitstatus):
     if not hasattr(session.config, "workerinput"):  # the controller, after every worker is done
         import shutil
 
+        _teardown_leaked_clusters(Path(os.environ["TK8S_HOST_REGISTRY"]))
         shutil.rmtree(os.environ["TK8S_HOST_REGISTRY"], ignore_errors=True)
+
+
+def _teardown_leaked_clusters(registry: Path) -> None:
+    """A run interrupted by ``-x`` (xdist stops the other workers mid-test) skips fixture
+    teardowns: every workspace still holding claims in this run's registry is torn down here,
+    so no control plane or agent outlives the run (and keeps serving on an address the next
+    run hands out again)."""
+    import json
+    import subprocess
+
+    try:
+        table = json.loads((registry / "claims.json").read_text())
+    except (OSError, ValueError):
+        return
+    workspaces = {Path(c.get("alloc", "")).parent.parent for kind in ("ips", "gpus")
+                  for c in (table.get(kind) or {}).values() if c.get("alloc")}
+    for ws in sorted(workspaces):
+        if (ws / "setup.sh").exists():
+            subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, capture_output=True, timeout=120,
+                           env={**os.environ, "PYTHONPATH": str(REPO)})

@@ -7,7 +7,6 @@ import socket
 import subprocess
 import sys
 import threading
-import time
 import uuid
 from pathlib import Path
 
@@ -86,9 +85,12 @@ def test_pool_map_order_errors_and_as_completed():
 
         with pytest.raises(ValueError):
             p.map(boom, range(5))
-        futs = [p.submit(time.sleep, d) for d in (0.15, 0.01, 0.08)]
-        order = [futs.index(f) for f in as_completed(futs)]
-        assert order == [1, 2, 0]
+        gates = [threading.Event() for _ in range(3)]
+        futs = [p.submit(g.wait, 30) for g in gates]
+        done = as_completed(futs)
+        for i in (1, 2, 0):  # finish them in this order; as_completed yields them the same way
+            gates[i].set()
+            assert futs.index(next(done)) == i
         assert len(p._threads) <= 4
     with pytest.raises(RuntimeError):
         p.submit(lambda: 1)

@@ -265,3 +265,25 @@ def test_pod_in_its_own_pid_namespace(tmp_path, monkeypatch):
     wait_for(lambda ev: any(p == "Succeeded" for _, p, _ in ev))
     out = (tmp_path / "pods" / "iso" / "log").read_text().split()
     assert out[0] in ("pid=1", "pid=2") and int(out[1]) <= 4  # only the pod's own processes are visible
+
+
+def test_local_provider_skips_addresses_something_already_serves_on():
+    """A loopback address with a TCP listener or a bound UDP socket on it (a cluster this host's
+    registry does not know about, e.g. one an interrupted run leaked) is never handed out."""
+    import socket
+
+    from tritonk8ssupervisor_amd.provider.local import LocalProvider
+
+    u = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    t = socket.socket()
+    c = socket.socket()
+    try:
+        u.bind(("127.0.9.77", 0))
+        t.bind(("127.0.9.78", 0))
+        t.listen(1)
+        c.bind(("127.0.9.79", 0))  # bound but not listening: not serving
+        seen = LocalProvider._bound_ips()
+        assert {"127.0.9.77", "127.0.9.78"} <= seen and "127.0.9.79" not in seen
+    finally:
+        for s in (u, t, c):
+            s.close()

@@ -128,9 +128,31 @@ class LocalProvider(Provider):
         """Real GPUs are claimed host-wide; a fake inventory is private to each cluster."""
         return not os.environ.get("TK8S_FAKE_GPUS")
 
+    @staticmethod
+    def _bound_ips() -> set[str]:
+        """Loopback addresses something on this host already serves on (a TCP listener or a
+        UDP socket bound to that address): a cluster the registry does not know about -- another
+        user's, or one whose registry is gone -- still owns its master's DNS / ingress / API
+        sockets there, and a new machine on the same address would answer for neither."""
+        out: set[str] = set()
+        for table, listen_only in (("/proc/net/tcp", True), ("/proc/net/udp", False)):
+            try:
+                with open(table) as f:
+                    next(f, None)
+                    for line in f:
+                        cols = line.split()
+                        if len(cols) < 4 or (listen_only and cols[3] != "0A"):
+                            continue
+                        ip = socket.inet_ntoa(bytes.fromhex(cols[1].split(":")[0])[::-1])
+                        if ip.startswith("127.") and ip != "127.0.0.1":
+                            out.add(ip)
+            except (OSError, ValueError):
+                continue
+        return out
+
     def _alloc_ips(self, alloc: dict, name: str, nets: list[Network], host: dict) -> list[str]:
         used = alloc.setdefault("ips", {})
-        host_used = HostRegistry.taken(host, "ips")
+        host_used = HostRegistry.taken(host, "ips") | (self._bound_ips() if self._multi() else set())
         out = []
         for net in nets:
             if not self._multi():
