@@ -172,6 +172,7 @@ def one_bringup(ws: Path, n: int, args, env: dict, log) -> dict:
     import threading
 
     t0 = time.perf_counter()
+    launched_unix = time.time()
     p = subprocess.Popen(cmd, cwd=ws, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, bufsize=1,
                          start_new_session=True)
     lines: list[str] = []
@@ -210,6 +211,9 @@ def one_bringup(ws: Path, n: int, args, env: dict, log) -> dict:
     summary = json.loads(out.strip().splitlines()[-1])
     summary["wall_seconds"] = wall
     summary["ready_wall_seconds"] = t_ready
+    spawned = (summary.get("host_burnin") or {}).get("spawned_unix")
+    if spawned:  # how long after the launch of ./setup.sh the GPU burn-in process started
+        summary["burnin_spawn_ms"] = round((spawned - launched_unix) * 1e3, 2)
     return summary
 
 
@@ -380,6 +384,7 @@ def main(argv=None) -> int:
         "settle_s": settle,
         "burnin_runtime_init_ms_steps": [(s.get("host_burnin") or {}).get("runtime_init_ms") for s in summaries],
         "burnin_total_ms_steps": [(s.get("host_burnin") or {}).get("total_ms") for s in summaries],
+        "burnin_spawn_ms_steps": [s.get("burnin_spawn_ms") for s in summaries],
     }
     if b2b_ready:
         out["back_to_back"] = {"steps": len(b2b_ready), "mean_s": round(sum(b2b_ready) / len(b2b_ready), 4),

@@ -86,11 +86,15 @@ def test_pool_map_order_errors_and_as_completed():
         with pytest.raises(ValueError):
             p.map(boom, range(5))
         gates = [threading.Event() for _ in range(3)]
-        futs = [p.submit(g.wait, 30) for g in gates]
+        futs = [p.submit(g.wait) for g in gates]
         done = as_completed(futs)
-        for i in (1, 2, 0):  # finish them in this order; as_completed yields them the same way
-            gates[i].set()
-            assert futs.index(next(done)) == i
+        try:
+            for i in (1, 2, 0):  # finish them in this order; as_completed yields them the same way
+                gates[i].set()
+                assert futs.index(next(done)) == i
+        finally:
+            for g in gates:
+                g.set()
         assert len(p._threads) <= 4
     with pytest.raises(RuntimeError):
         p.submit(lambda: 1)
@@ -214,3 +218,21 @@ def test_setup_cli_does_not_import_the_heavy_modules(tmp_path):
                        env={**os.environ, "PYTHONPATH": str(REPO)})
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "[]", r.stdout
+
+
+def test_pool_never_strands_a_task_behind_a_waiting_worker():
+    """Tasks that wait on tasks submitted after them (each needs a worker of its own): with
+    enough workers allowed, every one of them runs, however the workers happen to be idle."""
+    for _ in range(200):
+        p = Pool(3)
+        p.submit(lambda: None).result()  # one worker, idle
+        gates = [threading.Event() for _ in range(3)]
+        futs = [p.submit(gates[0].wait), p.submit(lambda: (gates[0].set(), gates[1].wait())),
+                p.submit(lambda: gates[1].set())]
+        try:
+            for f in futs:
+                f.result(timeout=10)
+        finally:
+            for g in gates:
+                g.set()
+            p.shutdown()

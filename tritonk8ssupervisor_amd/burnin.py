@@ -151,6 +151,7 @@ class HostBurnin:
         self.result_path = self.state_dir / "run" / "host-burnin.json"
         self.pidfile = self.state_dir / "run" / "host-burnin.pid"
         self.proc = None
+        self.spawned_unix = 0.0  # wall clock of the burn-in's spawn
         self.done = False
         self.result: dict | None = None
         self.xgmi: dict | None = None  # host-wide link verdict (xgmi.link_report), with peer pulls
@@ -163,6 +164,7 @@ class HostBurnin:
     def start(self) -> bool:
         import subprocess
         import threading
+        import time
 
         from .models.hostinfo import compose_visible_devices
 
@@ -184,16 +186,18 @@ class HostBurnin:
             return False
         finally:
             log.close()
+        self.spawned_unix = time.time()
         self.pidfile.write_text(f"{self.proc.pid}\n")
         threading.Thread(target=self._wait, name="host-burnin", daemon=True).start()
         return True
 
-    def adopt(self, proc) -> None:
+    def adopt(self, proc, spawned_unix: float = 0.0) -> None:
         """Take over a burn-in already running this exact command over these GPUs into
         ``result_path`` (earlyburn.py started it before the CLI imported anything)."""
         import threading
 
         self.proc = proc
+        self.spawned_unix = spawned_unix
         self.pidfile.parent.mkdir(parents=True, exist_ok=True)
         self.pidfile.write_text(f"{proc.pid}\n")
         threading.Thread(target=self._wait, name="host-burnin", daemon=True).start()

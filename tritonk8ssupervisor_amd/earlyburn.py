@@ -278,8 +278,9 @@ class Spawned:
 
 
 class Early:
-    def __init__(self, proc: Spawned, gpus: list[int], command: list[str], result: str):
+    def __init__(self, proc: Spawned, gpus: list[int], command: list[str], result: str, spawned_unix: float = 0.0):
         self.proc, self.gpus, self.command, self.result = proc, gpus, command, result
+        self.spawned_unix = spawned_unix  # wall clock of the spawn (bench: launch -> burn-in start)
 
     def kill(self) -> None:
         try:
@@ -353,16 +354,19 @@ def launch(argv: list[str]) -> Early | None:
         env.update(compose_visible_devices(p["gpus"]))
         env["NODE_NAME"] = "host"
         cmd = p["command"] + ["--out", p["result"]]
+        import time
+
         pid = os.posix_spawn(cmd[0], cmd, env, setsid=True, file_actions=[
             (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
             (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
             (os.POSIX_SPAWN_OPEN, 2, os.path.join(run, "host-burnin.log"), os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644),
         ])
+        spawned = time.time()
         with open(os.path.join(run, "host-burnin.pid"), "w") as f:
             f.write(f"{pid}\n")
     except Exception:  # noqa: BLE001 - an optimisation only: the orchestrator starts its own
         return None
-    _LAUNCHED = Early(Spawned(pid), p["gpus"], p["command"], p["result"])
+    _LAUNCHED = Early(Spawned(pid), p["gpus"], p["command"], p["result"], spawned)
     try:
         _ZYGOTE = controlplane_zygote(p)
     except Exception:  # noqa: BLE001 - the boot hook starts the control plane the usual way

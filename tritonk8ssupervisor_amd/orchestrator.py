@@ -388,7 +388,7 @@ class Setup:
         if early is not None:
             if (hb is not None and early.command == cmd and sorted(early.gpus) == sorted(gpus)
                     and Path(early.result) == hb.result_path):
-                hb.adopt(early.proc)
+                hb.adopt(early.proc, early.spawned_unix)
                 self.host_burnin = hb
                 self.events.emit("gpu_burnin_host_started", gpus=gpus, pid=early.proc.pid, early=True)
                 return
@@ -775,7 +775,8 @@ class Setup:
             t = (hb.result or {}).get("timings_ms") or {}
             self.summary["host_burnin"] = {"gpus": hb.gpus, "ok": bool(hb.result and hb.result.get("ok")),
                                            "runtime_init_ms": t.get("runtime_init", t.get("hip_init")),
-                                           "peers_ms": t.get("peers"), "total_ms": t.get("total")}
+                                           "peers_ms": t.get("peers"), "total_ms": t.get("total"),
+                                           "spawned_unix": hb.spawned_unix or None}
             if hb.xgmi is not None:
                 self.summary["xgmi"] = {k: hb.xgmi[k] for k in ("pulls", "median_gbps", "min_gbps", "floor_gbps",
                                                                  "min_fraction")}

@@ -69,12 +69,17 @@ class Pool:
             if self._shutdown:
                 raise RuntimeError("cannot submit to a pool that was shut down")
             self._queue.append((fut, fn, args, kwargs))
-            if self._idle == 0 and len(self._threads) < self.max_workers:
+            if self._idle > 0:
+                # claim one waiting worker now: counting it as idle until it has woken up would
+                # let the next submit skip spawning while this worker is taken (a lost task when
+                # every running task waits on a later one)
+                self._idle -= 1
+                self._cv.notify()
+            elif len(self._threads) < self.max_workers:
                 t = threading.Thread(target=self._work, name=f"{self.name}_{len(self._threads)}", daemon=True)
                 self._threads.append(t)
                 t.start()
-            else:
-                self._cv.notify()
+            # else: every worker is busy and at the limit; the next one to finish takes it
         return fut
 
     def _work(self) -> None:
@@ -82,8 +87,7 @@ class Pool:
             with self._cv:
                 while not self._queue and not self._shutdown:
                     self._idle += 1
-                    self._cv.wait()
-                    self._idle -= 1
+                    self._cv.wait()  # whoever notified took this worker off the idle count
                 if not self._queue:
                     return
                 fut, fn, args, kwargs = self._queue.popleft()
