@@ -211,9 +211,15 @@ def one_bringup(ws: Path, n: int, args, env: dict, log) -> dict:
     summary = json.loads(out.strip().splitlines()[-1])
     summary["wall_seconds"] = wall
     summary["ready_wall_seconds"] = t_ready
-    spawned = (summary.get("host_burnin") or {}).get("spawned_unix")
+    hb = summary.get("host_burnin") or {}
+    spawned = hb.get("spawned_unix")
     if spawned:  # how long after the launch of ./setup.sh the GPU burn-in process started
         summary["burnin_spawn_ms"] = round((spawned - launched_unix) * 1e3, 2)
+        if hb.get("main_unix_ms"):  # exec + dynamic loading until the probe's main()
+            summary["burnin_exec_ms"] = round(hb["main_unix_ms"] - spawned * 1e3, 2)
+        if hb.get("seen_unix") and hb.get("main_unix_ms") and hb.get("total_ms") is not None:
+            # from the probe's result to setup noticing it
+            summary["burnin_notice_ms"] = round(hb["seen_unix"] * 1e3 - hb["main_unix_ms"] - hb["total_ms"], 2)
     return summary
 
 
@@ -385,6 +391,8 @@ def main(argv=None) -> int:
         "burnin_runtime_init_ms_steps": [(s.get("host_burnin") or {}).get("runtime_init_ms") for s in summaries],
         "burnin_total_ms_steps": [(s.get("host_burnin") or {}).get("total_ms") for s in summaries],
         "burnin_spawn_ms_steps": [s.get("burnin_spawn_ms") for s in summaries],
+        "burnin_exec_ms_steps": [s.get("burnin_exec_ms") for s in summaries],
+        "burnin_notice_ms_steps": [s.get("burnin_notice_ms") for s in summaries],
     }
     if b2b_ready:
         out["back_to_back"] = {"steps": len(b2b_ready), "mean_s": round(sum(b2b_ready) / len(b2b_ready), 4),

@@ -59,7 +59,10 @@ class Json {
   void str(const std::string& v) { os_ << escape(v); }
   void num(double v) {
     char buf[64];
-    std::snprintf(buf, sizeof buf, "%.9g", v);
+    // 9 significant digits, except for large magnitudes (wall-clock timestamps in ms, ~1.8e12):
+    // those keep three decimals, or "%.9g" would round them to whole seconds
+    if (v >= 1e6 || v <= -1e6) std::snprintf(buf, sizeof buf, "%.3f", v);
+    else std::snprintf(buf, sizeof buf, "%.9g", v);
     os_ << buf;
   }
   std::ostringstream os_;

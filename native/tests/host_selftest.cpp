@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../tools/args.h"
+#include "tk8s/json.h"
 #include "tk8s/topology.h"
 
 namespace {
@@ -74,7 +75,17 @@ int main() {
     ++bad;
   }
   check(bad == 1, "stray argument rejected");
-  if (failures) return 1;
+
+  // JSON writer: escaping, and doubles that keep their precision -- a wall-clock timestamp in ms
+  // (~1.8e12) must not be rounded to whole seconds (the RCCL ranks' init spread is a difference
+  // of two of them)
+  const std::string j = tk8s::Json().kv("s", std::string("a\"b\\c\n")).kv("t", 1760000000123.456).kv("x", 0.174566)
+                            .kv("n", static_cast<int64_t>(-3)).str();
+  check(j == "{\"s\":\"a\\\"b\\\\c\\n\",\"t\":1760000000123.456,\"x\":0.174566,\"n\":-3}", "json writer");
+  if (failures) {
+    std::fprintf(stderr, "json: %s\n", j.c_str());
+    return 1;
+  }
   std::printf("host selftest ok\n");
   return 0;
 }

@@ -960,6 +960,9 @@ std::string with_device(const std::string& j, int d) {
 
 int main(int argc, char** argv) {
   const auto t0 = std::chrono::steady_clock::now();
+  // wall clock at main(): against the launcher's spawn time it shows the exec + loader cost
+  const double main_unix_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::system_clock::now().time_since_epoch()).count();
   std::string out_file;
   try {
     tk8s::Args a(argc, argv);
@@ -1082,7 +1085,8 @@ int main(int argc, char** argv) {
     if (!info.empty()) out.raw("gpuinfo", info);
     if (c.peers) out.kv("peer_bytes", static_cast<uint64_t>(c.peer)).kv("peer_rounds", static_cast<int>(devices.size()) - 1);
     out.raw("timings_ms", Json().kv("hip_init", init_ms).kv("runtime_init", init_ms).kv("gpuinfo", gpuinfo_ms)
-                              .kv("peers", peers_ms).kv("total", ms_since(t0)).str());
+                              .kv("peers", peers_ms).kv("total", ms_since(t0))
+                              .kv("main_unix_ms", main_unix_ms).str());
     emit(out.str(), out_file);
     std::fflush(stdout);
     // No runtime teardown on the way out (see run_device) -- unless a tool that finalises in

@@ -245,11 +245,13 @@ class HostBurnin:
         # (runtime teardown, the driver releasing its queues and memory) takes tens of ms more:
         # hand the shares out the moment the file appears, not when the process is gone.
         rc = None
+        self.seen_unix = 0.0
         while not self.result_path.exists():
             rc = self.proc.poll()
             if rc is not None:
                 break
             time.sleep(0.001)
+        self.seen_unix = time.time()
         result = None
         try:
             result = json.loads(self.result_path.read_text())

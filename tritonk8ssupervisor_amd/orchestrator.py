@@ -776,7 +776,9 @@ class Setup:
             self.summary["host_burnin"] = {"gpus": hb.gpus, "ok": bool(hb.result and hb.result.get("ok")),
                                            "runtime_init_ms": t.get("runtime_init", t.get("hip_init")),
                                            "peers_ms": t.get("peers"), "total_ms": t.get("total"),
-                                           "spawned_unix": hb.spawned_unix or None}
+                                           "spawned_unix": hb.spawned_unix or None,
+                                           "main_unix_ms": t.get("main_unix_ms"),
+                                           "seen_unix": getattr(hb, "seen_unix", 0.0) or None}
             if hb.xgmi is not None:
                 self.summary["xgmi"] = {k: hb.xgmi[k] for k in ("pulls", "median_gbps", "min_gbps", "floor_gbps",
                                                                  "min_fraction")}
