@@ -11,6 +11,20 @@ if [[ "${1:-}" == "-c" ]]; then
     shift
     exec "$PY" -S -c 'from tritonk8ssupervisor_amd.cli.fast import run; run()' clean "$@"
 fi
+# A non-interactive bring-up (--answers) preloads the GPU burn-in: tk8s-hsaprobe starts now, maps
+# the ROCr runtime (~11 ms before its main()) while the CLI's interpreter starts, and waits on
+# fd 7 for the plan (which GPUs, where the result goes) that earlyburn.py writes -- or for EOF
+# when this run has no early burn-in (see tk8s_hsaprobe.cpp, --plan-stdin).
+if [[ -z "${TK8S_FAKE_GPUS:-}" && "${TK8S_PRELOAD_BURNIN:-1}" != 0 && " $* " == *" --answers"* ]]; then
+    for d in "${TK8S_HOME:-}" "${PYTHONPATH%%:*}" "$(pwd)"; do
+        probe="$d/tritonk8ssupervisor_amd/bin/tk8s-hsaprobe"
+        if [[ -n "$d" && -x "$probe" ]]; then
+            exec 7> >(exec "$probe" --plan-stdin > /dev/null 2>&1)
+            export TK8S_EARLY_PROBE_FD=7 TK8S_EARLY_PROBE_PID=$! TK8S_EARLY_PROBE_BIN="$probe"
+            break
+        fi
+    done
+fi
 # -S: skip site-packages .pth processing at start-up (tritonk8ssupervisor_amd/__init__.py adds
 # the site directories back); -c instead of -m: no runpy. The CLI's start-up is part of the
 # bring-up time.
