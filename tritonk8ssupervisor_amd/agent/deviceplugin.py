@@ -16,10 +16,10 @@ Unhealthy while it reports uncorrectable or deferred ECC errors, and keeps its t
 from __future__ import annotations
 
 import os
-from ..utils.record import field, record as dataclass
 from pathlib import Path
 
 from ..models.hostinfo import HostInventory, compose_visible_devices, discover
+from ..utils.record import field, record as dataclass
 
 _LINK_WEIGHT = {"self": 1000, "xgmi": 100, "pcie": 10}
 

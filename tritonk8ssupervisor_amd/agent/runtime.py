@@ -15,11 +15,11 @@ import signal
 import subprocess
 import threading
 import time
-from ..utils.record import field, record as dataclass
 from pathlib import Path
 
 from ..utils.fsutil import atomic_write_json
 from ..utils.procs import kill_group
+from ..utils.record import field, record as dataclass
 from ..utils.trace import trace
 
 _VAR = re.compile(r"\$\(([A-Za-z_][A-Za-z0-9_]*)\)")

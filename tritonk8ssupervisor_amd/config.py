@@ -11,10 +11,10 @@ from __future__ import annotations
 
 import os
 import shlex
-from .utils.record import asdict, field, fields, record as dataclass
 from pathlib import Path
 
 from .utils.fsutil import atomic_write
+from .utils.record import asdict, field, fields, record as dataclass
 
 # Reference defaults (setup.sh:245-252); package/network defaults are provider-resolved.
 DEFAULT_NAME = "k8s dev"

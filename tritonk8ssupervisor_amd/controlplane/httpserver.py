@@ -10,9 +10,10 @@ import asyncio
 import json
 import re
 import traceback
-from ..utils.record import field, record as dataclass
 from typing import Any, AsyncIterator, Awaitable, Callable
 from urllib.parse import parse_qs, unquote, urlsplit
+
+from ..utils.record import field, record as dataclass
 
 REASONS = {200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
            401: "Unauthorized", 403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed",

@@ -16,8 +16,9 @@ from __future__ import annotations
 
 import os
 import re
-from .utils.record import field, record as dataclass
 from pathlib import Path
+
+from .utils.record import field, record as dataclass
 
 
 class HclError(ValueError):

@@ -14,10 +14,10 @@ GPU runtime; only leaf validation pods do (tools/tk8s_gpuinfo.cpp is the authori
 from __future__ import annotations
 
 import os
-from ..utils.record import asdict, field, record as dataclass
 from pathlib import Path
 
 from ..earlyburn import compose_visible_devices, idx_list, kfd_gpu_nodes, read_props, visible_filter  # noqa: F401
+from ..utils.record import asdict, field, record as dataclass
 
 KFD_ROOT = Path("/sys/class/kfd/kfd/topology/nodes")
 IOLINK_XGMI = 11

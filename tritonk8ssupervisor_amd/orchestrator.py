@@ -21,7 +21,6 @@ import shutil
 import sys
 import threading
 import time
-from .utils.record import record as dataclass
 from pathlib import Path
 
 from . import hcl
@@ -33,6 +32,7 @@ from .provision import Engine
 from .utils.events import EventLog
 from .utils.fsutil import atomic_write, atomic_write_json, read_json, remove_paths
 from .utils.procs import kill_pidfile, pid_alive
+from .utils.record import record as dataclass
 
 REPO = Path(__file__).resolve().parents[1]
 TEMPLATE_DIRS = ["terraform/master", "terraform/host", "terraform/compat", "ansible/roles", "ansible/group_vars",

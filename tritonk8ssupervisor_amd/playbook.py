@@ -24,14 +24,14 @@ import os
 import shlex
 import threading
 import time
-from .utils.pool import Pool
-from .utils.record import field, record as dataclass
 from pathlib import Path
 
 from . import templating
 from .templating import TemplateError, Undefined
 from .utils import yamlio
 from .utils.events import EventLog
+from .utils.pool import Pool
+from .utils.record import field, record as dataclass
 
 TASK_KEYS = {"name", "register", "when", "until", "retries", "delay", "with_items", "loop", "run_once",
              "delegate_to", "local_action", "action", "ignore_errors", "failed_when", "changed_when",

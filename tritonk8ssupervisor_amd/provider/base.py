@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import abc
+
 from ..utils.record import asdict, field, record as dataclass
 
 

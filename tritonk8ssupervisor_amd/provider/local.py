@@ -128,6 +128,20 @@ class LocalProvider(Provider):
         """Real GPUs are claimed host-wide; a fake inventory is private to each cluster."""
         return not os.environ.get("TK8S_FAKE_GPUS")
 
+    _bound_cache: tuple[float, set[str]] | None = None
+
+    @classmethod
+    def _bound_ips_cached(cls, max_age: float = 2.0) -> set[str]:
+        """_bound_ips() shared by the machines of one provisioning run: reading /proc/net costs
+        ~1-4 ms and the allocations run one after another under the workspace lock."""
+        import time
+
+        c = cls._bound_cache
+        now = time.monotonic()
+        if c is None or now - c[0] > max_age:
+            c = cls._bound_cache = (now, cls._bound_ips())
+        return c[1]
+
     @staticmethod
     def _bound_ips() -> set[str]:
         """Loopback addresses something on this host already serves on (a TCP listener or a
@@ -152,7 +166,7 @@ class LocalProvider(Provider):
 
     def _alloc_ips(self, alloc: dict, name: str, nets: list[Network], host: dict) -> list[str]:
         used = alloc.setdefault("ips", {})
-        host_used = HostRegistry.taken(host, "ips") | (self._bound_ips() if self._multi() else set())
+        host_used = HostRegistry.taken(host, "ips") | (self._bound_ips_cached() if self._multi() else set())
         out = []
         for net in nets:
             if not self._multi():

@@ -25,8 +25,9 @@ import shlex
 import io
 import subprocess
 import tarfile
-from .record import field, record as dataclass
 from pathlib import Path
+
+from .record import field, record as dataclass
 
 
 @dataclass(frozen=True)
