@@ -33,6 +33,8 @@ from .utils.events import EventLog
 from .utils.pool import Pool
 from .utils.record import field, record as dataclass
 
+_HOME = str(Path(__file__).resolve().parents[1])  # this checkout: the tk8s install of colocated machines
+
 TASK_KEYS = {"name", "register", "when", "until", "retries", "delay", "with_items", "loop", "run_once",
              "delegate_to", "local_action", "action", "ignore_errors", "failed_when", "changed_when",
              "environment", "no_log", "tags", "vars", "check_mode", "loop_control", "become", "become_user", "args",
@@ -305,7 +307,13 @@ class Playbook:
         elif len(hosts) == 1:
             res = [self._run_on_host(task, hosts[0], play_vars)]
         else:
+            start = len(self.trace)
             res = list(self._executor().map(lambda h: self._run_on_host(task, h, play_vars), hosts))
+            # hosts ran in parallel: the trace of this task in host order (each host's own
+            # entries keep their order), so --check plans read the same on every run
+            order = {h.name: i for i, h in enumerate(hosts)}
+            with self._trace_lock:
+                self.trace[start:] = sorted(self.trace[start:], key=lambda e: order.get(e["host"], len(order)))
         self.events.emit("task", task=f"{prefix}{title}", seconds=round(time.monotonic() - t, 6),
                          results={r.host: r.status for r in res})
         return res
@@ -362,8 +370,7 @@ class Playbook:
         m = getattr(ex, "machines", {}).get(host.name) if ex is not None else None
         if m is None:
             return {}
-        return {"tk8s_machine_dir": m.sandbox, "tk8s_gpus": ",".join(map(str, m.gpus)),
-                "tk8s_home": m.home or str(Path(__file__).resolve().parents[1])}
+        return {"tk8s_machine_dir": m.sandbox, "tk8s_gpus": ",".join(map(str, m.gpus)), "tk8s_home": m.home or _HOME}
 
     def _group_vars(self, host: Host) -> dict:
         out: dict = {}

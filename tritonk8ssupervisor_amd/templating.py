@@ -383,15 +383,50 @@ def evaluate(expr: str, variables: dict, strict: bool = True) -> Any:
         return jinja_evaluate(expr, variables, strict)
 
 
-def _evaluate_subset(expr: str, variables: dict, strict: bool = True) -> Any:
-    try:
+_REWRITE_VERSION = 1  # bump when _rewrite / _pyify change what they produce
+_PARSED: dict[str, Any] = {}  # expression text -> its parsed tree (or the _Unsupported it raised)
+
+
+_REWRITES = None  # expression text -> rewritten Python source, kept across processes
+
+
+def _rewritten(expr: str) -> str:
+    """_rewrite(_pyify(expr)), remembered across bring-ups (utils/pcache.py): the rewrite needs
+    the stdlib tokenizer, whose first use in a process compiles a large regex."""
+    global _REWRITES
+    if _REWRITES is None:
+        from .utils.pcache import PersistentCache
+
+        _REWRITES = PersistentCache(f"jinja-rewrite-{_REWRITE_VERSION}")
+    src = _REWRITES.get(expr)
+    if src is None:
         src = _rewrite(_pyify(expr.strip()))
-    except TemplateError as e:
-        raise _Unsupported(str(e)) from e
-    try:
-        tree = ast.parse(src or "None", mode="eval")
-    except SyntaxError as e:
-        raise _Unsupported(f"cannot parse {expr!r}: {e}") from e
+        _REWRITES.put(expr, src)
+    return src
+
+
+def _parse(expr: str):
+    """The rewritten, parsed form of an expression, computed once per distinct text: a play
+    evaluates the same few expressions for every host (the tokenizer is most of the cost)."""
+    hit = _PARSED.get(expr)
+    if hit is None:
+        try:
+            src = _rewritten(expr)
+            hit = ast.parse(src or "None", mode="eval")
+        except TemplateError as e:
+            hit = _Unsupported(str(e))
+        except SyntaxError as e:
+            hit = _Unsupported(f"cannot parse {expr!r}: {e}")
+        if len(_PARSED) >= 4096:
+            _PARSED.clear()
+        _PARSED[expr] = hit
+    if isinstance(hit, _Unsupported):
+        raise _Unsupported(str(hit))
+    return hit
+
+
+def _evaluate_subset(expr: str, variables: dict, strict: bool = True) -> Any:
+    tree = _parse(expr)
     val = _Eval(variables, strict)(tree)
     if isinstance(val, _UndefinedValue) and strict:
         raise Undefined(f"'{val.name}' is undefined")
