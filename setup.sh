@@ -1,11 +1,13 @@
-#!/usr/bin/env bash
+#!/bin/bash
 # MI355X cluster bring-up wizard (same surface as the reference's setup.sh):
 #   ./setup.sh            create: prompts, provisioning, configuration, readiness wait
 #   ./setup.sh -c         teardown: destroy machines and reset configuration
 # Non-interactive: ./setup.sh --answers answers.yaml --yes   (see docs/usage.md)
 set -o errexit
 set -o pipefail
-cd "$(dirname "$0")"
+# (no subshells or extra execs before the burn-in preload below: the shebang is bash itself and
+# the script's directory comes from a parameter expansion, not $(dirname))
+case "$0" in */*) cd "${0%/*}" ;; esac
 PY="${TK8S_PYTHON:-python3}"
 if [[ "${1:-}" == "-c" ]]; then
     shift
@@ -16,7 +18,7 @@ fi
 # fd 7 for the plan (which GPUs, where the result goes) that earlyburn.py writes -- or for EOF
 # when this run has no early burn-in (see tk8s_hsaprobe.cpp, --plan-stdin).
 if [[ -z "${TK8S_FAKE_GPUS:-}" && "${TK8S_PRELOAD_BURNIN:-1}" != 0 && " $* " == *" --answers"* ]]; then
-    for d in "${TK8S_HOME:-}" "${PYTHONPATH%%:*}" "$(pwd)"; do
+    for d in "${TK8S_HOME:-}" "${PYTHONPATH%%:*}" "$PWD"; do
         probe="$d/tritonk8ssupervisor_amd/bin/tk8s-hsaprobe"
         if [[ -n "$d" && -x "$probe" ]]; then
             exec 7> >(exec "$probe" --plan-stdin > /dev/null 2>&1)
