@@ -151,6 +151,10 @@ def child_env(fake_gpus: int | None) -> dict:
         env.pop(k, None)
     if fake_gpus is not None:
         env["TK8S_FAKE_GPUS"] = str(fake_gpus)
+    # the RCCL fabric Job (after Ready, N >= 2) logs its init and P2P channel setup, so the JSON's
+    # rccl_last_step.transport says what the channels ran over (P2P/IPC vs SHM/NET)
+    env.setdefault("NCCL_DEBUG", "INFO")
+    env.setdefault("NCCL_DEBUG_SUBSYS", "INIT,P2P")
     return env
 
 
@@ -385,6 +389,12 @@ def main(argv=None) -> int:
         "gpus_allocatable": last.get("gpus_allocatable"),
         "nodes_validated": last.get("nodes_validated"),
         "rccl_peak_busbw_gbps": (last.get("rccl") or {}).get("peak_busbw_gbps"),
+        # the fabric check of the last step, for the multi-GPU runs: communicator start-up, how
+        # unevenly the ranks came up, the channel transports RCCL logged, the Job's shape
+        "rccl_last_step": {k: (last.get("rccl") or {}).get(k) for k in (
+            "ok", "nranks", "pods", "gpus_per_pod", "comm_init_ms_max", "init_spread_ms", "transport")}
+        if last.get("rccl") else None,
+        "xgmi_last_step": last.get("xgmi"),
         "validation_last_step": last.get("validation"),
         "hip_init_ms_steps": hip_init,
         "settle_s": settle,
