@@ -67,7 +67,13 @@ def _free_port() -> int:
 
 
 class Dist:
-    """Barrier + device sync across the torchrun ranks (RCCL on GPU, gloo on CPU)."""
+    """Barrier + device sync across the torchrun ranks.
+
+    The barrier runs over gloo (host sockets) even on GPUs: an RCCL barrier would leave ranks
+    1..N-1 spinning a kernel on their GPUs -- and a proxy thread on the CPU -- for the whole timed
+    bring-up, on the very GPUs the bring-up is validating (and, after Ready, next to the
+    cluster's own RCCL fabric check). Each side of a step is still bracketed by
+    torch.cuda.synchronize() on every rank's device."""
 
     def __init__(self):
         self.rank = int(os.environ.get("RANK", "0"))
@@ -89,7 +95,7 @@ class Dist:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if self.cuda:
                 self.torch.cuda.set_device(self.local_rank)
-            dist.init_process_group("nccl" if self.cuda else "gloo")
+            dist.init_process_group("gloo")
             self.pg = True
 
     def sync(self) -> None:
@@ -98,10 +104,7 @@ class Dist:
         if self.pg:
             import torch.distributed as dist
 
-            if self.cuda:
-                dist.barrier(device_ids=[self.local_rank])
-            else:
-                dist.barrier()
+            dist.barrier()
         if self.cuda:
             self.torch.cuda.synchronize()
 
@@ -110,7 +113,7 @@ class Dist:
             return v
         import torch.distributed as dist
 
-        t = self.torch.tensor([v], dtype=self.torch.float64, device=f"cuda:{self.local_rank}" if self.cuda else "cpu")
+        t = self.torch.tensor([v], dtype=self.torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
