@@ -55,8 +55,8 @@ def test_build_is_incremental(native_build):
     before = {k: Path(v).stat().st_mtime for k, v in native_build.items()}
     t = time.monotonic()
     out = build()
-    assert time.monotonic() - t < 5
-    assert {k: Path(v).stat().st_mtime for k, v in out.items()} == before
+    assert {k: Path(v).stat().st_mtime for k, v in out.items()} == before  # nothing rebuilt
+    assert time.monotonic() - t < 20  # a rebuild of the HIP layer takes minutes; the checks, seconds
 
 
 def test_native_module_imports_without_a_gpu(native_build):

@@ -188,7 +188,7 @@ def test_forks_bound_parallelism(tmp_path):
     t = time.monotonic()
     _, res, _ = _play(tmp_path, plays, inventory=inv)  # forks=0 -> all 6 hosts at once
     all_at_once = time.monotonic() - t
-    assert res.ok and all_at_once < 1.2
+    assert res.ok and all_at_once < 1.6  # one after another would be >= 1.8 s
     d = tmp_path / "f2"
     d.mkdir()
     t = time.monotonic()

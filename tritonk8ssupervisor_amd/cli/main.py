@@ -4,6 +4,7 @@
   ./setup.sh -c [--yes]                                               -> tk8s clean
   ./tk8s networks|packages [-l]     (triton networks / triton packages)
   ./tk8s env                        (triton env)
+  ./tk8s doctor [--platform P] [--json]   (preflight checks for the backend / platform)
   ./tk8s debug-vars                 (debugVars: the exported ./config)
   ./tk8s terraform get|plan|apply|destroy     (provisioning engine, in terraform/)
   ./tk8s ansible-playbook [--check] [-i hosts] clusterUp.yml           (playbook engine)
@@ -63,6 +64,12 @@ def cmd_setup(args) -> int:
               file=sys.stderr)
         return 2
     return 0
+
+
+def cmd_doctor(args) -> int:
+    from ..doctor import main as doctor
+
+    return doctor(args.workdir, getattr(args, "backend", None), args.platform, args.json)
 
 
 def cmd_scale(args) -> int:
@@ -373,6 +380,11 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("-l", action="store_true")
         p.set_defaults(fn=fn)
     sub.add_parser("env").set_defaults(fn=cmd_env)
+    dr = sub.add_parser("doctor", help="preflight: check what a bring-up on this backend/platform needs")
+    dr.add_argument("--platform", choices=["tk8s", "kubeadm"], default=None)
+    dr.add_argument("--json", action="store_true")
+    _backend_flags(dr)
+    dr.set_defaults(fn=cmd_doctor)
     gh = sub.add_parser("gpu-health", help="AMD SMI health/telemetry of this host's GPUs (tk8s-smi)")
     gh.add_argument("--json", action="store_true")
     gh.set_defaults(fn=cmd_gpu_health)
