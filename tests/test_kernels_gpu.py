@@ -628,3 +628,23 @@ def test_multi_gpu_degraded_link_keeps_its_nodes_not_ready(tmp_path):
         assert out.count("NotReady") == 2, out
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+def test_doctor_passes_on_the_mi355x_host():
+    """./tk8s doctor on the GPU box: the KFD is usable and exposes gfx950 GPUs, the build is there."""
+    import os
+    import subprocess
+    from pathlib import Path
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env["PYTHONPATH"] = str(repo)
+    r = subprocess.run([str(repo / "tk8s"), "doctor", "--json"], cwd=repo, env=env, capture_output=True, text=True,
+                       timeout=120)
+    checks = {c["check"]: c for c in json.loads(r.stdout)}
+    assert checks["/dev/kfd"]["status"] == "OK" and checks["rocm"]["status"] == "OK", checks
+    assert checks["gpus"]["status"] == "OK" and "gfx950" in checks["gpus"]["detail"], checks["gpus"]
+    assert checks["native build"]["status"] == "OK"
+    assert r.returncode == 0 or any(c["status"] == "FAIL" and c["check"] == "free gpus" for c in checks.values()), checks
