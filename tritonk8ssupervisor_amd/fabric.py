@@ -1,0 +1,189 @@
+"""The cluster's RCCL fabric check (BASELINE.json configs 4-5): after every node is Ready, an
+Indexed Job all-reduces over every GPU -- one pod per GPU node, its process driving the node's
+GPUs as consecutive ranks -- and checks the result exactly; ``--rocprof`` runs the ranks under
+rocprofv3 (kernel trace + stats, or one counter pass). The reference's readiness oracle was a
+curl of the dashboard (setup.sh:56-85); this is the data-plane check that replaces it.
+
+``FabricCheck`` is a mixin of orchestrator.Setup; the helpers below parse the ranks' logs and
+the profiler's output.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import time
+from pathlib import Path
+
+from .workspace import SetupError, pod_portable
+
+
+class FabricCheck:
+    @staticmethod
+    def rccl_gpus_per_pod(k, g: int) -> int:
+        """GPUs per fabric-Job pod: every GPU of its node when the GPU nodes are uniform (one
+        process -- one runtime start -- per node, its GPUs as consecutive ranks), else 1."""
+        try:
+            nodes = k.get("/api/v1/nodes").get("items", [])
+        except Exception:  # noqa: BLE001 - the per-GPU shape works whatever the nodes say
+            return 1
+        counts = [int((n.get("status", {}).get("allocatable") or {}).get("amd.com/gpu", 0) or 0) for n in nodes]
+        counts = [c for c in counts if c > 0]
+        if counts and len(set(counts)) == 1 and counts[0] * len(counts) == g:
+            return counts[0]
+        return 1
+
+    def run_rccl(self) -> dict | None:
+        from .controlplane.client import client_from_kubeconfig
+        from .kube import apply_objects, load_manifests, pods_of, wait_job
+
+        if self.platform == "kubeadm":  # the RCCL-tests DaemonSet ran in the kubeadmvalidate role
+            pr = getattr(self, "playbook_result", None)
+            reg = ((pr.hostvars if pr else {}).get(self.cfg.RANCHER_MASTER_HOSTNAME) or {}).get("rccl_pods") or {}
+            lines = reg.get("stdout_lines") or []
+            return {"ok": bool(lines) and all(ln.split()[-1] == "true" for ln in lines if ln.strip()),
+                    "daemonset": "kube-system/tk8s-rccl-tests", "pods": lines} if lines else None
+
+        g = self.expected_gpus()
+        enabled = self.rccl if self.rccl is not None else g >= 2
+        if not enabled or g < 1:
+            return None
+        c = self._client()
+        pid = self.project_id()
+        k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
+        job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
+        per_pod = self.rccl_gpus_per_pod(k, g)
+        npods = g // per_pod
+        # one process per node drives all of that node's GPUs (ranks index*k .. index*k+k-1)
+        group = ["--group-index", "$(JOB_COMPLETION_INDEX)", "--devices", "$(TK8S_GPU_DEVICES)", "--nranks", str(g)]
+        if os.environ.get("TK8S_FAKE_GPUS"):
+            cmd = ["$(TK8S_PYTHON)", "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", *group,
+                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
+        else:
+            from .ops import BIN
+
+            cmd = [pod_portable([str(BIN / "tk8s-rccl")])[0], *group,
+                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
+                   "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
+        prof_dir = None
+        if self.rocprof:
+            rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+            if os.environ.get("TK8S_FAKE_GPUS") or not os.path.exists(rp):
+                self.out("    --rocprof: rocprofv3 unavailable here (or GPUs are faked); profiling skipped")
+            else:
+                # N8 (BASELINE.json config 5): kernel trace + per-kernel stats of every rank. Counter
+                # collection (--pmc) is a separate run by design: never mixed with tracing.
+                prof_dir = self.ws.state_dir / "profiles" / job
+                prof_dir.mkdir(parents=True, exist_ok=True)
+                pmc = []
+                if self.rocprof_counters:  # a counter pass: --pmc with --kernel-trace/--stats only
+                    check_pmc_counters(self.rocprof_counters)
+                    pmc = ["--pmc", *self.rocprof_counters]
+                cmd = [rp, *pmc, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
+                       "--output-format", "csv", "--", *cmd]
+        objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
+                              {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd})
+        apply_objects(k, objs)
+        self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job}, {npods} pod(s) x {per_pod} GPU(s))")
+        left = max(10.0, self.rccl_timeout or self.timeout)
+        try:
+            j = wait_job(k, job, "kube-system", timeout=left)
+        except TimeoutError as e:
+            raise SetupError(f"RCCL all-reduce Job {job} did not finish within {left:.0f}s: {e}", code=124) from e
+        pods = pods_of(k, f"job-name={job}", "kube-system")
+        results = [p.get("status", {}).get("result") or {} for p in pods]
+        peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)
+        ok = j["status"].get("succeeded", 0) >= npods and all(r.get("ok") for r in results)
+        first = next((r for r in results if r), {})
+        rep = {"job": job, "ok": ok, "nranks": g, "pods": npods, "gpus_per_pod": per_pod, "peak_busbw_gbps": peak,
+               "tuning": {k: first.get(k) for k in ("nccl_algo", "nccl_proto", "nccl_min_nchannels",
+                                                    "nccl_max_nchannels", "peak_links_equivalent") if k in first},
+               "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),
+                                 "ok": (p.get("status", {}).get("result") or {}).get("ok")} for p in pods]}
+        done = [r["init_done_unix_ms"] for r in results if r.get("init_done_unix_ms")]
+        if done:  # how unevenly the ranks' runtimes + communicators came up
+            rep["init_spread_ms"] = round(max(done) - min(done), 3)
+            rep["comm_init_ms_max"] = round(max(r.get("comm_init_ms", 0.0) for r in results), 3)
+        rep["transport"] = rccl_transports([(p.get("metadata", {}).get("annotations") or {}).get("tk8s.amd.com/log-path")
+                                            for p in pods])
+        if prof_dir is not None:
+            rep["rocprof"] = summarize_rocprof(prof_dir)
+        if not ok:
+            raise SetupError(f"RCCL all-reduce validation failed: {json.dumps(rep)[:800]}", code=2)
+        return rep
+
+
+def rccl_transports(log_paths: list) -> dict:
+    """Which transports the RCCL ranks' channels used, from their NCCL_DEBUG=INFO lines
+    ("... via P2P/IPC", "via SHM/...", "via NET/..."): on one MI355X node every channel must be
+    P2P over xGMI; SHM or NET means a host-memory or network fallback."""
+    import re
+
+    counts = {"p2p": 0, "shm": 0, "net": 0, "collnet": 0}
+    seen = False
+    for p in log_paths:
+        try:
+            text = Path(p).read_text(errors="replace") if p else ""
+        except OSError:
+            continue
+        for m in re.finditer(r" via (P2P|SHM|NET|COLLNET)\b", text):
+            counts[m.group(1).lower()] += 1
+            seen = True
+    counts["logged"] = seen  # False: NCCL_DEBUG=INFO was not set, nothing to judge
+    return counts
+
+
+# Hardware counters one rocprofv3 --pmc pass can hold per block on gfx950 (asking for more makes
+# it fail with "error code 38" and hang). FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2.
+PMC_BLOCK_LIMITS = {"SQ": 8, "TCC": 4, "TCP": 4, "TA": 2, "TD": 2, "GRBM": 2}
+PMC_WEIGHT = {"FETCH_SIZE": ("TCC", 3), "WRITE_SIZE": ("TCC", 2)}
+
+
+def check_pmc_counters(counters: list[str]) -> None:
+    used: dict[str, int] = {}
+    seen = set()
+    for c in counters:
+        base = c.rsplit("_", 1)[0] if c.endswith(("_sum", "_avr", "_min", "_max")) else c
+        if base in seen:  # _sum/_avr/_min/_max of one counter count once
+            continue
+        seen.add(base)
+        block, weight = PMC_WEIGHT.get(base, (base.split("_", 1)[0], 1))
+        if block not in PMC_BLOCK_LIMITS:
+            raise SetupError(f"--rocprof-counters: unknown counter block of {c!r} "
+                             f"(supported: {', '.join(sorted(PMC_BLOCK_LIMITS))})")
+        used[block] = used.get(block, 0) + weight
+        if used[block] > PMC_BLOCK_LIMITS[block]:
+            raise SetupError(f"--rocprof-counters: more than {PMC_BLOCK_LIMITS[block]} {block} counter slots in one "
+                             "pass; split them over several runs")
+
+
+def summarize_rocprof(prof_dir: Path, top: int = 5) -> dict:
+    """Top kernels per rank from rocprofv3 `*_kernel_stats.csv` files under prof_dir, plus the
+    per-kernel counter totals of a --pmc pass (`*_counter_collection.csv`)."""
+    import csv
+
+    out = {"dir": str(prof_dir), "ranks": {}}
+    counters: dict[str, dict[str, dict[str, float]]] = {}
+    for f in sorted(prof_dir.rglob("*counter_collection.csv")):
+        rank = f.name.split("_counter_collection")[0]
+        with open(f, newline="") as fh:
+            for r in csv.DictReader(fh):
+                k = (r.get("Kernel_Name") or "")[:120]
+                name = r.get("Counter_Name") or ""
+                try:
+                    v = float(r.get("Counter_Value") or 0)
+                except ValueError:
+                    continue
+                per = counters.setdefault(rank, {}).setdefault(k, {})
+                per[name] = per.get(name, 0.0) + v
+    if counters:
+        out["counters"] = counters
+    for f in sorted(prof_dir.rglob("*kernel_stats.csv")):
+        with open(f, newline="") as fh:
+            rows = list(csv.DictReader(fh))
+        rows.sort(key=lambda r: -float(r.get("TotalDurationNs", 0) or 0))
+        out["ranks"][f.name.split("_kernel_stats")[0]] = [
+            {"kernel": r.get("Name", "")[:120], "calls": int(r.get("Calls", 0) or 0),
+             "total_us": round(float(r.get("TotalDurationNs", 0) or 0) / 1e3, 2),
+             "avg_us": round(float(r.get("AverageNs", 0) or 0) / 1e3, 3)} for r in rows[:top]]
+    return out

@@ -26,75 +26,18 @@ from pathlib import Path
 from . import hcl
 from .config import ClusterConfig, export_vars, read_config, write_config
 from .earlyburn import default_validation_command  # noqa: F401 - shared with the early burn-in
+from .fabric import FabricCheck, check_pmc_counters, rccl_transports, summarize_rocprof  # noqa: F401
+from .kubeadm_platform import KUBEADM_RESET, KubeadmPlatform, kubeadm_extra_vars
 from .provider import get_provider
 from .provider.base import Machine, ProvisionError
 from .provision import Engine
 from .utils.events import EventLog
-from .utils.fsutil import atomic_write, atomic_write_json, read_json, remove_paths
+from .utils.fsutil import atomic_write, atomic_write_json, read_json
 from .utils.procs import kill_pidfile, pid_alive
-from .utils.record import record as dataclass
-
-REPO = Path(__file__).resolve().parents[1]
-TEMPLATE_DIRS = ["terraform/master", "terraform/host", "terraform/compat", "ansible/roles", "ansible/group_vars",
-                 "manifests"]
-TEMPLATE_FILES = ["ansible/ansible.cfg", "ansible/clusterUp.yml", "ansible/clusterUp-kubeadm.yml"]
-PHASES = ["configure", "provision", "ansible-config", "ansible", "ready", "rccl"]
-PLATFORMS = ("tk8s", "kubeadm")
-PLAYBOOKS = {"tk8s": "clusterUp.yml", "kubeadm": "clusterUp-kubeadm.yml"}
-
-
-class SetupError(RuntimeError):
-    def __init__(self, msg: str, code: int = 1):
-        super().__init__(msg)
-        self.code = code
-
-
-@dataclass
-class Workspace:
-    root: Path
-
-    @property
-    def config(self) -> Path: return self.root / "config"
-    @property
-    def tf(self) -> Path: return self.root / "terraform"
-    @property
-    def ansible(self) -> Path: return self.root / "ansible"
-    @property
-    def manifests(self) -> Path: return self.root / "manifests"
-    @property
-    def state_dir(self) -> Path: return self.root / ".tk8s"
-    @property
-    def state_file(self) -> Path: return self.state_dir / "state.json"
-    @property
-    def events(self) -> Path: return self.state_dir / "events.jsonl"
-    @property
-    def env_id_file(self) -> Path: return self.ansible / "tmp" / "kubernetes_environment.id"
-    @property
-    def vars_file(self) -> Path: return self.ansible / "roles" / "ranchermaster" / "vars" / "vars.yml"
-
-    def state(self) -> dict:
-        return read_json(self.state_file, {}) or {}
-
-    def save_state(self, **kw) -> dict:
-        st = self.state()
-        st.update(kw)
-        atomic_write_json(self.state_file, st)
-        return st
-
-
-def init_workspace(dst: str | os.PathLike, src: Path = REPO) -> Workspace:
-    """Copy the module/role/manifest templates into a fresh workspace directory."""
-    d = Path(dst)
-    for rel in TEMPLATE_DIRS:
-        if (d / rel).exists():
-            shutil.rmtree(d / rel)
-        shutil.copytree(src / rel, d / rel, ignore=shutil.ignore_patterns("vars.yml", "__pycache__"))
-    for rel in TEMPLATE_FILES:
-        (d / rel).parent.mkdir(parents=True, exist_ok=True)
-        shutil.copy2(src / rel, d / rel)
-    (d / "ansible" / "tmp").mkdir(parents=True, exist_ok=True)
-    (d / "ansible" / "roles" / "ranchermaster" / "vars").mkdir(parents=True, exist_ok=True)
-    return Workspace(d)
+from .workspace import (  # noqa: F401 - the orchestrator's public names, re-exported
+    PHASES, PLATFORMS, PLAYBOOKS, REPO, TEMPLATE_DIRS, TEMPLATE_FILES, SetupError, Workspace, agent_standby_argv,
+    controlplane_argv, init_workspace, pod_portable, validation_pod_command,
+)
 
 
 # ---- machine executor for the playbook engine ---------------------------------------------
@@ -125,58 +68,8 @@ def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, M
     }
 
 
-def kubeadm_extra_vars(setup: "Setup", cfg: ClusterConfig) -> dict:
-    """What the kubeadm roles need beyond the inventory and the role defaults."""
-    per_node = 0
-    try:
-        per_node = int(setup.provider.package_by_id_or_name(cfg.HOST_PACKAGE).gpus or 0)
-    except Exception:  # noqa: BLE001
-        pass
-    return {"tk8s_expected_gpus": per_node * int(cfg.KUBERNETES_NUMBER_OF_NODES), "tk8s_gpus_per_node": per_node,
-            "tk8s_ready_timeout": int(setup.timeout)}
-
-
-def controlplane_argv(bind: str, port: int, advertise: str, state_dir: str, node_grace: float) -> list[str]:
-    """The control plane daemon (the ranchermaster role's rancher/server), one definition for the
-    role and the master's boot hook."""
-    return [sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.controlplane", "--host", bind, "--port", str(port),
-            "--advertise", advertise, "--state-dir", state_dir, "--node-grace", str(node_grace)]
-
-
-def agent_standby_argv(name: str, ip: str) -> list[str]:
-    """The node agent in standby (rocmsetup's "Start the node agent in standby" task spells out
-    the same argv), waiting for play 3's registration URL."""
-    return [sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.agent", "--await-url", "run/registration-url",
-            "--name", name, "--ip", ip]
-
-
-def validation_pod_command(command: list[str], result: str = "$(TK8S_MACHINE_DIR)/run/gpu-burnin.json") -> list[str]:
-    """The validation DaemonSet pod: reuse the node's burn-in result, probe only without one.
-    With the real probe the reuse runs in tk8s-reuse, which loads no ROCm library."""
-    from .ops import BIN
-
-    reuse = BIN / "tk8s-reuse"
-    if not os.environ.get("TK8S_FAKE_GPUS") and reuse.exists():
-        return pod_portable([str(reuse), result, "--", *command])
-    return pod_portable([*command, "--reuse", result])
-
-
-def pod_portable(argv: list[str]) -> list[str]:
-    """A pod command in terms of the NODE's tk8s install: the agent expands $(TK8S_HOME) and
-    $(TK8S_PYTHON) (Kubernetes $(VAR) syntax) to its own install root and interpreter, so one
-    DaemonSet/Job spec runs on colocated sandboxes and on remote machines alike."""
-    out = []
-    for a in argv:
-        a = str(a)
-        if a == sys.executable:
-            out.append("$(TK8S_PYTHON)")
-        else:
-            out.append(a.replace(str(REPO), "$(TK8S_HOME)"))
-    return out
-
-
 # ---- setup ---------------------------------------------------------------------------------
-class Setup:
+class Setup(KubeadmPlatform, FabricCheck):
     def __init__(self, ws: Workspace, *, answers: dict | None = None, assume_yes: bool = False,
                  resume: bool = False, timeout: float = 600.0, validate: bool = True, rccl: bool | None = None,
                  out: Callable[[str], None] = None, quiet_ansible: bool = True, hbm_bytes: int = 1 << 30,
@@ -483,58 +376,6 @@ class Setup:
     def expected_gpus(self) -> int:
         pkg = self.provider.package_by_id_or_name(self.cfg.HOST_PACKAGE)
         return int(self.cfg.KUBERNETES_NUMBER_OF_NODES) * int(getattr(pkg, "gpus", 0) or 0)
-
-    # -- kubeadm platform -------------------------------------------------------------------
-    def _master_exec(self, cmd: str, timeout: float = 120) -> tuple[int, str]:
-        ex = MachineExecutor(self.provider, self.engine.machines())
-        return ex.exec(self.cfg.RANCHER_MASTER_HOSTNAME, cmd, timeout=timeout)
-
-    def _kubeadm_nodes(self) -> list[dict]:
-        hv = getattr(self, "playbook_result", None)
-        reg = ((hv.hostvars if hv else {}).get(self.cfg.RANCHER_MASTER_HOSTNAME) or {}).get("tk8s_nodes") or {}
-        text = reg.get("stdout") or ""
-        if not text:  # --resume past the playbook: ask the API server
-            rc, text = self._master_exec("kubectl --kubeconfig /etc/kubernetes/admin.conf get nodes -o json")
-            if rc != 0:
-                raise SetupError(f"kubectl get nodes failed on the master: {text.strip()[-400:]}")
-        return json.loads(text)["items"]
-
-    def _kubeadm_ready(self) -> dict:
-        """Readiness on the kubeadm platform: the kubeadmvalidate role already waited (bounded) for
-        every node Ready and the expected amd.com/gpu; this reads back what the API server said."""
-        items = self._kubeadm_nodes()
-        workers = set(self.cfg.node_names())
-        ready = [n for n in items if n["metadata"]["name"] in workers and any(
-            c.get("type") == "Ready" and c.get("status") == "True" for c in n.get("status", {}).get("conditions", []))]
-        gpus = sum(int((n.get("status", {}).get("allocatable") or {}).get("amd.com/gpu", "0") or 0) for n in ready)
-        out = {"ready": len(ready) == len(workers) and gpus >= self.expected_gpus(), "nodes_ready": len(ready),
-               "gpus_allocatable": gpus, "nodes_validated": len(ready)}
-        if not out["ready"]:
-            raise SetupError(f"cluster not ready: {len(ready)}/{len(workers)} workers Ready, {gpus} amd.com/gpu "
-                             f"(expected {self.expected_gpus()})", code=124)
-        return out
-
-    def _kubeadm_finish(self, ready: dict, rccl, t_ready: float, total: float) -> dict:
-        m = self.engine.machines()[self.cfg.RANCHER_MASTER_HOSTNAME]
-        kubeconfig = self.ws.ansible / "tmp" / "kubeconfig"
-        self.summary = {
-            "platform": "kubeadm", "ready_seconds": round(t_ready, 4), "total_seconds": round(total, 4),
-            "nodes": int(self.cfg.KUBERNETES_NUMBER_OF_NODES), "gpus_allocatable": ready.get("gpus_allocatable", 0),
-            "nodes_validated": ready.get("nodes_validated", 0), "rccl": rccl,
-            "phases": {k: round(v, 4) for k, v in self.events.phases.items()},
-            "api": f"https://{m.primaryip}:6443", "kubectl_config": str(kubeconfig),
-            "project": self.project_id() if self.ws.env_id_file.exists() else "",
-        }
-        self.ws.save_state(summary=self.summary, finished=time.time())
-        self.events.emit("setup_done", **{k: v for k, v in self.summary.items() if k != "phases"})
-        self.out("")
-        self.out("Congratulations, your Kubernetes cluster setup has been complete.")
-        self.out(f"----> Kubernetes API server is at {self.summary['api']}")
-        self.out(f"----> kubectl: KUBECONFIG={kubeconfig} kubectl get nodes")
-        self.out(f"----> {self.summary['nodes']} node(s) Ready, {self.summary['gpus_allocatable']} x amd.com/gpu allocatable")
-        self.out(f"----> bring-up: {t_ready:.3f}s to all nodes Ready ({total:.3f}s including fabric validation)")
-        return self.summary
-
     def wait_ready(self) -> dict:
         """Event-driven, bounded replacement of the readiness loop (setup.sh:56-85)."""
         if self.platform == "kubeadm":
@@ -566,99 +407,6 @@ class Setup:
                 raise SetupError(f"GPU validation failed on {last.get('nodes_validation_failed')} node(s)"
                                  + (f": {why}" if why else "")
                                  + "\n    see `./kubectl describe nodes` and `./kubectl get pods -n kube-system`", code=2)
-
-    @staticmethod
-    def rccl_gpus_per_pod(k, g: int) -> int:
-        """GPUs per fabric-Job pod: every GPU of its node when the GPU nodes are uniform (one
-        process -- one runtime start -- per node, its GPUs as consecutive ranks), else 1."""
-        try:
-            nodes = k.get("/api/v1/nodes").get("items", [])
-        except Exception:  # noqa: BLE001 - the per-GPU shape works whatever the nodes say
-            return 1
-        counts = [int((n.get("status", {}).get("allocatable") or {}).get("amd.com/gpu", 0) or 0) for n in nodes]
-        counts = [c for c in counts if c > 0]
-        if counts and len(set(counts)) == 1 and counts[0] * len(counts) == g:
-            return counts[0]
-        return 1
-
-    def run_rccl(self) -> dict | None:
-        from .controlplane.client import client_from_kubeconfig
-        from .kube import apply_objects, load_manifests, pods_of, wait_job
-
-        if self.platform == "kubeadm":  # the RCCL-tests DaemonSet ran in the kubeadmvalidate role
-            pr = getattr(self, "playbook_result", None)
-            reg = ((pr.hostvars if pr else {}).get(self.cfg.RANCHER_MASTER_HOSTNAME) or {}).get("rccl_pods") or {}
-            lines = reg.get("stdout_lines") or []
-            return {"ok": bool(lines) and all(ln.split()[-1] == "true" for ln in lines if ln.strip()),
-                    "daemonset": "kube-system/tk8s-rccl-tests", "pods": lines} if lines else None
-
-        g = self.expected_gpus()
-        enabled = self.rccl if self.rccl is not None else g >= 2
-        if not enabled or g < 1:
-            return None
-        c = self._client()
-        pid = self.project_id()
-        k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
-        job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
-        per_pod = self.rccl_gpus_per_pod(k, g)
-        npods = g // per_pod
-        # one process per node drives all of that node's GPUs (ranks index*k .. index*k+k-1)
-        group = ["--group-index", "$(JOB_COMPLETION_INDEX)", "--devices", "$(TK8S_GPU_DEVICES)", "--nranks", str(g)]
-        if os.environ.get("TK8S_FAKE_GPUS"):
-            cmd = ["$(TK8S_PYTHON)", "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", *group,
-                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
-        else:
-            from .ops import BIN
-
-            cmd = [pod_portable([str(BIN / "tk8s-rccl")])[0], *group,
-                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
-                   "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
-        prof_dir = None
-        if self.rocprof:
-            rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
-            if os.environ.get("TK8S_FAKE_GPUS") or not os.path.exists(rp):
-                self.out("    --rocprof: rocprofv3 unavailable here (or GPUs are faked); profiling skipped")
-            else:
-                # N8 (BASELINE.json config 5): kernel trace + per-kernel stats of every rank. Counter
-                # collection (--pmc) is a separate run by design: never mixed with tracing.
-                prof_dir = self.ws.state_dir / "profiles" / job
-                prof_dir.mkdir(parents=True, exist_ok=True)
-                pmc = []
-                if self.rocprof_counters:  # a counter pass: --pmc with --kernel-trace/--stats only
-                    check_pmc_counters(self.rocprof_counters)
-                    pmc = ["--pmc", *self.rocprof_counters]
-                cmd = [rp, *pmc, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
-                       "--output-format", "csv", "--", *cmd]
-        objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
-                              {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd})
-        apply_objects(k, objs)
-        self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job}, {npods} pod(s) x {per_pod} GPU(s))")
-        left = max(10.0, self.rccl_timeout or self.timeout)
-        try:
-            j = wait_job(k, job, "kube-system", timeout=left)
-        except TimeoutError as e:
-            raise SetupError(f"RCCL all-reduce Job {job} did not finish within {left:.0f}s: {e}", code=124) from e
-        pods = pods_of(k, f"job-name={job}", "kube-system")
-        results = [p.get("status", {}).get("result") or {} for p in pods]
-        peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)
-        ok = j["status"].get("succeeded", 0) >= npods and all(r.get("ok") for r in results)
-        first = next((r for r in results if r), {})
-        rep = {"job": job, "ok": ok, "nranks": g, "pods": npods, "gpus_per_pod": per_pod, "peak_busbw_gbps": peak,
-               "tuning": {k: first.get(k) for k in ("nccl_algo", "nccl_proto", "nccl_min_nchannels",
-                                                    "nccl_max_nchannels", "peak_links_equivalent") if k in first},
-               "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),
-                                 "ok": (p.get("status", {}).get("result") or {}).get("ok")} for p in pods]}
-        done = [r["init_done_unix_ms"] for r in results if r.get("init_done_unix_ms")]
-        if done:  # how unevenly the ranks' runtimes + communicators came up
-            rep["init_spread_ms"] = round(max(done) - min(done), 3)
-            rep["comm_init_ms_max"] = round(max(r.get("comm_init_ms", 0.0) for r in results), 3)
-        rep["transport"] = rccl_transports([(p.get("metadata", {}).get("annotations") or {}).get("tk8s.amd.com/log-path")
-                                            for p in pods])
-        if prof_dir is not None:
-            rep["rocprof"] = summarize_rocprof(prof_dir)
-        if not ok:
-            raise SetupError(f"RCCL all-reduce validation failed: {json.dumps(rep)[:800]}", code=2)
-        return rep
 
     # -- dry run (BASELINE.json config 1: `terraform plan` + `ansible-playbook --check`) -------
     def dry_run(self) -> dict:
@@ -896,82 +644,6 @@ class Setup:
         atomic_write_json(self.ws.state_dir / "kubeconfig.json", kc)
 
 
-def rccl_transports(log_paths: list) -> dict:
-    """Which transports the RCCL ranks' channels used, from their NCCL_DEBUG=INFO lines
-    ("... via P2P/IPC", "via SHM/...", "via NET/..."): on one MI355X node every channel must be
-    P2P over xGMI; SHM or NET means a host-memory or network fallback."""
-    import re
-
-    counts = {"p2p": 0, "shm": 0, "net": 0, "collnet": 0}
-    seen = False
-    for p in log_paths:
-        try:
-            text = Path(p).read_text(errors="replace") if p else ""
-        except OSError:
-            continue
-        for m in re.finditer(r" via (P2P|SHM|NET|COLLNET)\b", text):
-            counts[m.group(1).lower()] += 1
-            seen = True
-    counts["logged"] = seen  # False: NCCL_DEBUG=INFO was not set, nothing to judge
-    return counts
-
-
-# Hardware counters one rocprofv3 --pmc pass can hold per block on gfx950 (asking for more makes
-# it fail with "error code 38" and hang). FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2.
-PMC_BLOCK_LIMITS = {"SQ": 8, "TCC": 4, "TCP": 4, "TA": 2, "TD": 2, "GRBM": 2}
-PMC_WEIGHT = {"FETCH_SIZE": ("TCC", 3), "WRITE_SIZE": ("TCC", 2)}
-
-
-def check_pmc_counters(counters: list[str]) -> None:
-    used: dict[str, int] = {}
-    seen = set()
-    for c in counters:
-        base = c.rsplit("_", 1)[0] if c.endswith(("_sum", "_avr", "_min", "_max")) else c
-        if base in seen:  # _sum/_avr/_min/_max of one counter count once
-            continue
-        seen.add(base)
-        block, weight = PMC_WEIGHT.get(base, (base.split("_", 1)[0], 1))
-        if block not in PMC_BLOCK_LIMITS:
-            raise SetupError(f"--rocprof-counters: unknown counter block of {c!r} "
-                             f"(supported: {', '.join(sorted(PMC_BLOCK_LIMITS))})")
-        used[block] = used.get(block, 0) + weight
-        if used[block] > PMC_BLOCK_LIMITS[block]:
-            raise SetupError(f"--rocprof-counters: more than {PMC_BLOCK_LIMITS[block]} {block} counter slots in one "
-                             "pass; split them over several runs")
-
-
-def summarize_rocprof(prof_dir: Path, top: int = 5) -> dict:
-    """Top kernels per rank from rocprofv3 `*_kernel_stats.csv` files under prof_dir, plus the
-    per-kernel counter totals of a --pmc pass (`*_counter_collection.csv`)."""
-    import csv
-
-    out = {"dir": str(prof_dir), "ranks": {}}
-    counters: dict[str, dict[str, dict[str, float]]] = {}
-    for f in sorted(prof_dir.rglob("*counter_collection.csv")):
-        rank = f.name.split("_counter_collection")[0]
-        with open(f, newline="") as fh:
-            for r in csv.DictReader(fh):
-                k = (r.get("Kernel_Name") or "")[:120]
-                name = r.get("Counter_Name") or ""
-                try:
-                    v = float(r.get("Counter_Value") or 0)
-                except ValueError:
-                    continue
-                per = counters.setdefault(rank, {}).setdefault(k, {})
-                per[name] = per.get(name, 0.0) + v
-    if counters:
-        out["counters"] = counters
-    for f in sorted(prof_dir.rglob("*kernel_stats.csv")):
-        with open(f, newline="") as fh:
-            rows = list(csv.DictReader(fh))
-        rows.sort(key=lambda r: -float(r.get("TotalDurationNs", 0) or 0))
-        out["ranks"][f.name.split("_kernel_stats")[0]] = [
-            {"kernel": r.get("Name", "")[:120], "calls": int(r.get("Calls", 0) or 0),
-             "total_us": round(float(r.get("TotalDurationNs", 0) or 0) / 1e3, 2),
-             "avg_us": round(float(r.get("AverageNs", 0) or 0) / 1e3, 3)} for r in rows[:top]]
-    return out
-
-
 def _free_port() -> int:
     import socket
 
@@ -1022,78 +694,4 @@ def _set_ini_value(path: Path, key: str, value: str) -> None:
     atomic_write(path, "\n".join(out) + "\n")
 
 
-# ---- teardown --------------------------------------------------------------------------------
-KUBEADM_RESET = ("kubeadm reset -f --cri-socket unix:///run/containerd/containerd.sock; "
-                 'rm -rf "${TK8S_SYSROOT:-}/etc/cni/net.d" "${TK8S_SYSROOT:-}/root/.kube" '
-                 '"${TK8S_SYSROOT:-}/etc/kubernetes/tk8s"; systemctl restart containerd || true')
-
-
-def _kubeadm_reset(ws: "Workspace", provider, out) -> None:
-    """Undo kubeadm init/join on every machine before the machines go (best effort: a machine
-    that is gone already needs nothing)."""
-    if not (ws.tf / "terraform.tfstate").exists():
-        return
-    import concurrent.futures as cf
-
-    machines = list(Engine(ws.tf, provider).machines().values())
-    with cf.ThreadPoolExecutor(max_workers=max(1, len(machines))) as pool:
-        for m, (rc, text) in zip(machines, pool.map(lambda m: provider.exec(m, KUBEADM_RESET, timeout=300), machines)):
-            out(f"    kubeadm reset on {m.name}: {'ok' if rc == 0 else 'failed: ' + text.strip()[-200:]}")
-
-
-def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out: Callable[[str], None] = print,
-          backend: str | None = None) -> int:
-    """cleanRunner (setup.sh:484-521), non-destructive unless confirmed."""
-    inp = inp or sys.stdin
-    out("Clearing settings....")
-    masters, hosts_ = ws.tf / "masters.ip", ws.tf / "hosts.ip"
-    while True:
-        if masters.exists():
-            out("WARNING: You are about to destroy the following machines associated with the cluster:")
-            for f in (masters, hosts_):
-                if f.exists():
-                    out(f.read_text().rstrip())
-            q = "Do you wish to destroy the machines and reset configuration (yes | no)? "
-        else:
-            q = "Do you wish to reset configuration (yes | no)? "
-        if assume_yes:
-            yn = "yes"
-        else:
-            sys.stdout.write(q)
-            sys.stdout.flush()
-            yn = (inp.readline() or "no").strip()
-        if yn == "no":
-            return 0
-        if yn == "yes":
-            break
-        out("Please answer yes or no.")
-    backend = backend or (read_config(ws.config).TK8S_BACKEND if ws.config.exists() else os.environ.get("TK8S_BACKEND", "local"))
-    provider = get_provider(backend, ws.state_dir)
-    from .burnin import stop_host_burnin
-
-    stop_host_burnin(ws.state_dir)
-    if ws.config.exists() and read_config(ws.config).TK8S_PLATFORM == "kubeadm":
-        _kubeadm_reset(ws, provider, out)
-    if (ws.tf / "rancher.tf").exists() or (ws.tf / "terraform.tfstate").exists():
-        out("    destroying machines...")
-        try:
-            Engine(ws.tf, provider).destroy()
-        except Exception as e:  # noqa: BLE001 - keep cleaning
-            out(f"    warning: destroy: {e}")
-    if hasattr(provider, "list_machines"):  # leftovers of an interrupted apply
-        for m in provider.list_machines():
-            provider.delete_machine(m)
-    # A machine sandbox no allocation lists any more can still hold a live process: the control
-    # plane zygote started with the CLI of a bring-up that failed before its master existed.
-    for pidfile in sorted((ws.state_dir / "machines").glob("*/run/*.pid")):
-        kill_pidfile(pidfile, grace=1.0)
-    remove_paths([ws.tf / n for n in ("hosts.ip", "masters.ip", "rancher.tf", "terraform.tfstate", ".tfstate.lock",
-                                      "hosts.ip.lock", "masters.ip.lock", ".terraform")]
-                 + list(ws.tf.glob("terraform.tfstate*")))
-    if (ws.ansible / "ansible.cfg").exists():
-        _set_ini_value(ws.ansible / "ansible.cfg", "private_key_file", "")
-    remove_paths([ws.ansible / "hosts", ws.vars_file, *ws.ansible.glob("*.retry"), *(p for p in (ws.ansible / "tmp").glob("*") if not p.name.startswith(".")),
-                  ws.config, ws.state_dir / "machines", ws.state_dir / "alloc.json", ws.state_dir / "alloc.lock",
-                  ws.state_dir / "state.json", ws.state_dir / "kubeconfig.json", ws.state_dir / "ansible.log"])
-    out("    All clear!")
-    return 0
+from .teardown import clean  # noqa: E402,F401 - ./setup.sh -c (re-exported)
