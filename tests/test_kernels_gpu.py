@@ -513,12 +513,14 @@ def test_setup_from_an_answers_file_adopts_the_early_burnin_on_a_real_gpu(tmp_pa
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
 
-def _hsaprobe(*args, timeout=120):
+def _hsaprobe(*args, timeout=120, env=None):
+    import os
     import subprocess
 
     from tritonk8ssupervisor_amd.ops import BIN
 
-    r = subprocess.run([str(BIN / "tk8s-hsaprobe"), *args], capture_output=True, text=True, timeout=timeout)
+    r = subprocess.run([str(BIN / "tk8s-hsaprobe"), *args], capture_output=True, text=True, timeout=timeout,
+                       env=None if env is None else {**os.environ, **env})
     return r.returncode, json.loads(r.stdout.strip().splitlines()[-1])
 
 
@@ -546,6 +548,26 @@ def test_hsaprobe_known_answer_and_gpuinfo_agree_with_the_hip_probe(nat):
     for a, b in zip(hsa["gpuinfo"]["devices"], hip["gpuinfo"]["devices"]):
         assert a["gfx"] == b["gfx"] == "gfx950"
         assert a["pci_bus_id"] == b["pci_bus_id"] and a["cu_count"] == b["cu_count"]
+
+
+def test_hsaprobe_skips_the_cpu_cache_walk_and_still_passes(nat):
+    """The probe hides the per-CPU sysfs cache directories from the thunk's hsa_init walk
+    (profiles/r2_hsainit/); the runtime must come up with the same agents and the burn-in must
+    give the same answers as with the walk kept (TK8S_HSA_CPU_CACHES=1)."""
+    import os
+
+    args = ("--all-devices", "--gpuinfo", "--hbm-bytes", str(64 << 20), "--md5-bytes", str(256 << 20), "--iters", "1")
+    rc, fast = _hsaprobe(*args)
+    assert rc == 0 and fast["ok"], fast
+    assert fast["timings_ms"]["cpu_cache_walk"] == "skipped"
+    if os.path.isdir("/sys/devices/system/cpu/cpu0/cache"):
+        assert fast["timings_ms"]["cpu_cache_dirs_hidden"] > 0
+    rc, kept = _hsaprobe(*args, env={"TK8S_HSA_CPU_CACHES": "1"})
+    assert rc == 0 and kept["ok"], kept
+    assert kept["timings_ms"]["cpu_cache_walk"] == "kept" and kept["timings_ms"]["cpu_cache_dirs_hidden"] == 0
+    assert fast["device_count"] == kept["device_count"]
+    assert fast["md5"]["digest"] == kept["md5"]["digest"] == fast["md5_expected"]
+    assert [d["pci_bus_id"] for d in fast["gpuinfo"]["devices"]] == [d["pci_bus_id"] for d in kept["gpuinfo"]["devices"]]
 
 
 def test_hsaprobe_peers_on_one_gpu_is_a_no_op(nat):

@@ -36,6 +36,14 @@ def test_only_rccl_artefacts_link_librccl(native_build):
         assert any(n.startswith("librccl") for n in _needed(native_build[name])), name
 
 
+def test_hsaprobe_exports_its_opendir_for_the_thunk(native_build):
+    # the per-CPU cache walk of hsa_init is skipped by the probe's own opendir (profiles/r2_hsainit/):
+    # it only takes effect if the dynamic symbol table carries it ahead of libc's
+    out = subprocess.run(["nm", "-D", "--defined-only", str(native_build["tk8s-hsaprobe"])],
+                         capture_output=True, text=True, check=True).stdout
+    assert any(line.split()[-1] == "opendir" and line.split()[-2] == "T" for line in out.splitlines() if line.strip())
+
+
 def test_smi_tool_is_hip_free_and_fails_loudly_without_a_gpu(native_build):
     smi = native_build["tk8s-smi"]
     needed = _needed(smi)
