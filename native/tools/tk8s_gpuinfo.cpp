@@ -3,9 +3,11 @@
 #include <cstdio>
 
 #include "args.h"
+#include "cachewalk.h"
 #include "tk8s/probes.h"
 
 int main(int argc, char** argv) {
+  tk8s::cachewalk::configure();  // before the HIP runtime starts (cachewalk.h)
   try {
     tk8s::Args a(argc, argv);
     const std::string j = tk8s::gpuinfo_json(!a.has("no-links"));

@@ -40,8 +40,6 @@
 // above, in order), "ENV <NAME>=<value>" (the GPU visibility, set before hsa_init), "LOG <path>"
 // (stderr) -- and "GO". EOF before "GO" (no early burn-in for this run) exits 0 silently; so
 // does no plan within 60 s. The probe makes itself a session leader (teardown kills its group).
-#include <dirent.h>
-#include <dlfcn.h>
 #include <fcntl.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -49,7 +47,6 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <cerrno>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -63,6 +60,7 @@
 #include <vector>
 
 #include "args.h"
+#include "cachewalk.h"
 #include "reuse.h"
 #include "tk8s/json.h"
 
@@ -969,46 +967,7 @@ std::string with_device(const std::string& j, int d) {
   return j.substr(0, p) + "\"device\":" + std::to_string(d) + j.substr(p + pat.size());
 }
 
-// See opendir() below. Decided in main() before hsa_init, after the plan's environment.
-bool g_skip_cpu_caches = true;
-int g_cpu_cache_dirs_hidden = 0;
-
-// "/sys/devices/system/<...>/cpu<N>/cache": one CPU's cache directory, under either the NUMA node
-// (node/node<K>/cpu<N>) or the flat cpu list (cpu/cpu<N>), the two places the thunk looks.
-bool cpu_cache_dir(const char* p) {
-  static const char kSys[] = "/sys/devices/system/";
-  static const char kTail[] = "/cache";
-  if (!p || std::strncmp(p, kSys, sizeof kSys - 1) != 0) return false;
-  const size_t n = std::strlen(p);
-  if (n < sizeof kSys + sizeof kTail || std::strcmp(p + n - (sizeof kTail - 1), kTail) != 0) return false;
-  const size_t end = n - (sizeof kTail - 1);
-  size_t i = end;
-  while (i > 0 && p[i - 1] >= '0' && p[i - 1] <= '9') --i;
-  return i < end && i >= 4 && std::strncmp(p + i - 4, "/cpu", 4) == 0;
-}
-
 }  // namespace
-
-// The HSA thunk inside libhsa-runtime64 walks every CPU's cache hierarchy in sysfs during
-// hsa_init: for each CPU it lists .../cpu<M>/cache and then reads index<K>/{shared_cpu_list,level,
-// type,size,...}. On the 2-socket MI355X hosts (256 CPUs) that is ~7,600 sysfs files and about
-// half of hsa_init's ~47 ms, all of it kernel time (profiles/r2_hsainit/). The probe never asks the
-// CPU agent for its caches, so it tells the thunk a CPU has none: this definition preempts libc's
-// opendir for libhsa (the executable comes first in symbol lookup; it is exported with
-// --export-dynamic-symbol) and answers ENOENT for per-CPU cache directories only -- what the
-// thunk sees on kernels or VMs that publish no cache information. Every other directory,
-// including the NUMA node and cpu lists, is libc's. (Hiding the node directory is not enough: the
-// thunk then walks /sys/devices/system/cpu instead, profiles/r2_numa2/.) glibc's own internal
-// directory reads do not come through here. TK8S_HSA_CPU_CACHES=1 keeps the walk.
-extern "C" DIR* opendir(const char* name) {
-  static auto real = reinterpret_cast<DIR* (*)(const char*)>(dlsym(RTLD_NEXT, "opendir"));
-  if (g_skip_cpu_caches && cpu_cache_dir(name)) {
-    ++g_cpu_cache_dirs_hidden;
-    errno = ENOENT;
-    return nullptr;
-  }
-  return real(name);
-}
 
 // --plan-stdin: read "ARG"/"ENV"/"LOG" lines until "GO" (see the header). False: no plan.
 bool read_plan(std::vector<std::string>* args) {
@@ -1096,8 +1055,7 @@ int main(int argc, char** argv) {
     const std::string dir = exe_dir() + "/../lib/";
     const std::vector<std::string> cos = {read_file(dir + "tk8s_stream.co"), read_file(dir + "tk8s_md5.co")};
 
-    const char* caches = std::getenv("TK8S_HSA_CPU_CACHES");
-    g_skip_cpu_caches = !(caches && std::strcmp(caches, "1") == 0);
+    tk8s::cachewalk::configure();  // the plan's environment is in place (cachewalk.h)
     HSA_OK(hsa_init());
     const double init_ms = ms_since(t0);
     Topology t;
@@ -1198,8 +1156,8 @@ int main(int argc, char** argv) {
                               .kv("peers", peers_ms).kv("total", ms_since(t0))
                               .kv("main_unix_ms", plan_unix_ms > 0 ? plan_unix_ms : main_unix_ms)
                               .kv("preloaded", plan_unix_ms > 0).kv("exec_unix_ms", main_unix_ms)
-                              .kv("cpu_cache_walk", g_skip_cpu_caches ? "skipped" : "kept")
-                              .kv("cpu_cache_dirs_hidden", g_cpu_cache_dirs_hidden).str());
+                              .kv("cpu_cache_walk", tk8s::cachewalk::mode())
+                              .kv("cpu_cache_dirs_hidden", tk8s::cachewalk::g_hidden).str());
     emit(out.str(), out_file);
     std::fflush(stdout);
     // No runtime teardown on the way out (see run_device) -- unless a tool that finalises in

@@ -38,6 +38,7 @@
 #include "reuse.h"
 #include "tk8s/common.h"
 #include "tk8s/probes.h"
+#include "cachewalk.h"
 
 using tk8s::exists;
 using tk8s::ok_of;
@@ -82,6 +83,7 @@ void emit(const std::string& json, const std::string& out_file) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  tk8s::cachewalk::configure();  // before the HIP runtime starts (cachewalk.h)
   const auto t0 = std::chrono::steady_clock::now();
   std::string out_file;
   try {
@@ -199,7 +201,8 @@ int main(int argc, char** argv) {
     if (copy) out.raw("copy", res[0].copy);
     out.raw("devices", tk8s::Json::array(per_dev));
     if (!info.empty()) out.raw("gpuinfo", info);
-    out.raw("timings_ms", tk8s::Json().kv("hip_init", init_ms).kv("gpuinfo", gpuinfo_ms).kv("total", ms_since(t0)).str());
+    out.raw("timings_ms", tk8s::Json().kv("hip_init", init_ms).kv("gpuinfo", gpuinfo_ms).kv("total", ms_since(t0))
+                              .kv("cpu_cache_walk", tk8s::cachewalk::mode()).str());
     emit(out.str(), out_file);
     if (a.has("release-after")) {  // free the arena + streams before exit (experiment knob)
       const auto tr = std::chrono::steady_clock::now();

@@ -22,6 +22,7 @@
 #include "httpkv.h"
 #include "tk8s/common.h"
 #include "tk8s/rccl_bench.h"
+#include "cachewalk.h"
 
 namespace {
 
@@ -83,6 +84,7 @@ std::vector<int> parse_devices(const std::string& s) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  tk8s::cachewalk::configure();  // before the HIP runtime starts (cachewalk.h)
   try {
     tk8s::Args a(argc, argv);
     tk8s::AllReduceConfig cfg;

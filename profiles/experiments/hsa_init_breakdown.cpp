@@ -33,6 +33,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -69,6 +70,7 @@ std::mutex g_slow_mu;
 std::vector<Slow> g_slow;
 std::vector<Slow> g_other;
 std::vector<Slow> g_dirs;
+std::map<std::string, std::pair<long, double>> g_topo;
 std::atomic<long> g_fopen_fail{0};
 std::atomic<bool> g_on{false};
 
@@ -103,6 +105,20 @@ void account_path(Kind k, double t0, const char* path) {
   g_path_count[c]++;
   g_path_ns[c] += (long)(ms * 1e6);
   note_slow(ms, std::string(kKindName[k]) + " " + (path ? path : "?"));
+  if (c == kSysTopo && path) {
+    std::string pat;
+    for (const char* q = path; *q; ++q) {
+      if (*q >= '0' && *q <= '9') {
+        if (pat.empty() || pat.back() != 'N') pat += 'N';
+      } else {
+        pat += *q;
+      }
+    }
+    std::lock_guard<std::mutex> l(g_slow_mu);
+    auto& e = g_topo[pat];
+    e.first++;
+    e.second += ms;
+  }
   if (c == kOtherPath || c == kProc || c == kSysOther) {
     std::lock_guard<std::mutex> l(g_slow_mu);
     if (g_other.size() < 200) g_other.push_back({ms, path ? path : "?"});
@@ -178,8 +194,15 @@ int openat(int dirfd, const char* path, int flags, ...) {
   return r;
 }
 
+// SKIP_GPU_CACHES=1: an empty file (/dev/null) for the KFD topology's per-node cache property files
+static bool gpu_cache_props(const char* p) {
+  static const bool skip = getenv("SKIP_GPU_CACHES") && !strcmp(getenv("SKIP_GPU_CACHES"), "1");
+  return skip && p && !strncmp(p, "/sys/devices/virtual/kfd/kfd/topology/nodes/", 44) && strstr(p, "/caches/");
+}
+
 FILE* fopen(const char* path, const char* mode) {
   static auto f = real<FILE* (*)(const char*, const char*)>("fopen");
+  if (gpu_cache_props(path)) return f("/dev/null", mode);  // an empty property file
   double t0 = now_ms();
   FILE* r = f(path, mode);
   account_path(kFopen, t0, path);
@@ -393,10 +416,18 @@ int main() {
   if (st == HSA_STATUS_SUCCESS) {
     hsa_agent_t gpu{};
     hsa_iterate_agents(first_gpu, &gpu);
+    for (int k = 0; k < kNKinds; k++) g_count[k] = 0, g_ns[k] = 0;
+    for (unsigned i = 0; i < 65536; i++) g_ioctl_count[i] = 0, g_ioctl_ns[i] = 0;
+    {
+      std::lock_guard<std::mutex> l(g_slow_mu);
+      g_slow.clear();
+    }
+    g_on = true;  // from here on the accounting is the queue creation's
     double tq = now_ms();
     hsa_queue_t* q = nullptr;
     hsa_status_t qs = hsa_queue_create(gpu, 64, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, UINT32_MAX, UINT32_MAX, &q);
     t_queue = now_ms() - tq;
+    g_on = false;
     if (qs == HSA_STATUS_SUCCESS) hsa_queue_destroy(q);
     double ts = now_ms();
     hsa_shut_down();
@@ -425,7 +456,15 @@ int main() {
   std::sort(g_slow.begin(), g_slow.end(), [](const Slow& a, const Slow& b) { return a.ms > b.ms; });
   for (size_t j = 0; j < g_slow.size() && j < 20; j++)
     printf("%s[%.3f, \"%s\"]", j ? ", " : "", g_slow[j].ms, g_slow[j].what.c_str());
-  printf("], \"fopen_failed\": %ld, \"opendir\": [", g_fopen_fail.load());
+  printf("], \"topology_patterns\": {");
+  {
+    bool first = true;
+    for (auto& kv : g_topo) {
+      printf("%s\"%s\": [%ld, %.3f]", first ? "" : ", ", kv.first.c_str(), kv.second.first, kv.second.second);
+      first = false;
+    }
+  }
+  printf("}, \"fopen_failed\": %ld, \"opendir\": [", g_fopen_fail.load());
   for (size_t j = 0; j < g_dirs.size() && j < 100; j++) printf("%s[%d, \"%s\"]", j ? ", " : "", (int)g_dirs[j].ms, g_dirs[j].what.c_str());
   printf("], \"other_paths\": [");
   for (size_t j = 0; j < g_other.size(); j++) printf("%s[%.3f, \"%s\"]", j ? ", " : "", g_other[j].ms, g_other[j].what.c_str());

@@ -212,7 +212,8 @@ def test_setup_cli_does_not_import_the_heavy_modules(tmp_path):
             "playbook, playbook_modules, provision; from tritonk8ssupervisor_amd.provider import local; "
             "from tritonk8ssupervisor_amd.controlplane import client; "
             "bad = {'yaml', 'dataclasses', 'inspect', 'concurrent.futures', 'logging', 'uuid', 'http.client', "
-            "'urllib.request', 'email.parser', 'ssl', 'tempfile', 'hashlib', 'typing', 'runpy'} & set(sys.modules); "
+            "'urllib.request', 'email.parser', 'ssl', 'tempfile', 'hashlib', 'typing', 'runpy', 'argparse', 'gettext', "
+            "'configparser', 'copy', 'shutil', 'ast', 'tokenize', 'base64'} & set(sys.modules); "
             "print(sorted(bad))")
     r = subprocess.run([sys.executable, "-S", "-c", code], cwd=REPO, capture_output=True, text=True, timeout=60,
                        env={**os.environ, "PYTHONPATH": str(REPO)})
@@ -236,3 +237,62 @@ def test_pool_never_strands_a_task_behind_a_waiting_worker():
             for g in gates:
                 g.set()
             p.shutdown()
+
+
+@pytest.mark.parametrize("argv", [
+    ["setup"],
+    ["setup", "--answers", "a.json", "--yes", "--json", "--port", "18080", "--timeout", "300", "--rccl-timeout", "120"],
+    ["setup", "--answers=a.yml", "--no-validate", "--rccl", "off", "-v", "--backend", "baremetal", "--inventory", "i.yml"],
+    ["setup", "--nodes", "4", "--package", "mi355x-2gpu", "--name", "x y", "--dry-run", "--platform", "kubeadm",
+     "--hbm-bytes", "4096", "--md5-bytes", "1024", "--probe-iters", "1", "--node-grace", "2.5", "--rocprof",
+     "--rocprof-counters", "SQ_WAVES", "--rccl-max-bytes", "1024", "--resume", "--master-hostname", "m",
+     "--node-prefix", "n", "--verbose"],
+])
+def test_fast_setup_parser_builds_what_argparse_builds(argv):
+    from tritonk8ssupervisor_amd.cli import main as cli
+
+    fast = cli._fast_setup_args(argv)
+    assert fast is not None
+    slow = cli.build_parser().parse_args(argv)
+    assert vars(fast) == vars(slow)
+
+
+@pytest.mark.parametrize("argv", [
+    ["setup", "--help"], ["setup", "--ans", "a.json"], ["setup", "--rccl", "maybe"], ["setup", "--nodes", "two"],
+    ["setup", "--timeout", "-1"], ["setup", "--yes=1"], ["setup", "--answers"], ["setup", "-vv"], ["status"],
+])
+def test_fast_setup_parser_leaves_the_rest_to_argparse(argv):
+    from tritonk8ssupervisor_amd.cli import main as cli
+
+    assert cli._fast_setup_args(argv) is None
+
+
+def test_ini_reader_matches_configparser():
+    import configparser
+
+    from tritonk8ssupervisor_amd.playbook import read_ini_section
+
+    texts = ["[defaults]\nhost_key_checking = False\nforks=0\n# comment\n; other\nRetry_Files_Enabled: no\n[ssh]\nx = 1\n",
+             "", "[other]\na = 1\n", "[defaults]\nlong = a\n  continued\n", "[defaults]\nx = %(y)s\ny = 2\n"]
+    for t in texts:
+        cp = configparser.ConfigParser()
+        cp.read_string(t)
+        assert read_ini_section(t, "defaults") == (dict(cp["defaults"]) if cp.has_section("defaults") else {}), t
+
+
+@pytest.mark.parametrize("cidr", ["127.0.1.0/24", "10.0.0.0/30", "192.168.4.0/22", "10.9.0.0/31", "10.9.0.7/32"])
+def test_ipv4_hosts_match_ipaddress(cidr):
+    import ipaddress
+
+    from tritonk8ssupervisor_amd.provider.local import _ipv4_hosts
+
+    assert list(_ipv4_hosts(cidr)) == [str(a) for a in ipaddress.ip_network(cidr).hosts()]
+
+
+def test_late_site_finder_only_adds_site_dirs_for_third_party_imports():
+    code = ("import sys; import tritonk8ssupervisor_amd; n = len(sys.path); import ntpath, pathlib; "
+            "assert len(sys.path) == n, 'a stdlib probe added the site dirs'; import yaml; "
+            "assert len(sys.path) > n; print('ok')")
+    r = subprocess.run([sys.executable, "-S", "-c", code], cwd=REPO, capture_output=True, text=True, timeout=60,
+                       env={**os.environ, "PYTHONPATH": str(REPO)})
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr

@@ -570,6 +570,11 @@ def test_hsaprobe_skips_the_cpu_cache_walk_and_still_passes(nat):
     assert [d["pci_bus_id"] for d in fast["gpuinfo"]["devices"]] == [d["pci_bus_id"] for d in kept["gpuinfo"]["devices"]]
 
 
+def test_hip_probe_skips_the_cpu_cache_walk(nat):
+    rc, out = _probe("--iters", "1", "--hbm-bytes", str(64 << 20))
+    assert rc == 0 and out["ok"] and out["timings_ms"]["cpu_cache_walk"] == "skipped", out
+
+
 def test_hsaprobe_peers_on_one_gpu_is_a_no_op(nat):
     """--peers with a single GPU: no pair to pull over, nothing dispatched for it, result unchanged."""
     n = _gpu_count()

@@ -36,10 +36,12 @@ def test_only_rccl_artefacts_link_librccl(native_build):
         assert any(n.startswith("librccl") for n in _needed(native_build[name])), name
 
 
-def test_hsaprobe_exports_its_opendir_for_the_thunk(native_build):
-    # the per-CPU cache walk of hsa_init is skipped by the probe's own opendir (profiles/r2_hsainit/):
-    # it only takes effect if the dynamic symbol table carries it ahead of libc's
-    out = subprocess.run(["nm", "-D", "--defined-only", str(native_build["tk8s-hsaprobe"])],
+@pytest.mark.parametrize("tool", ["tk8s-hsaprobe", "tk8s-probe", "tk8s-gpuinfo", "tk8s-rccl"])
+def test_gpu_tools_export_their_opendir_for_the_thunk(native_build, tool):
+    # the per-CPU cache walk of the runtime start is skipped by the tool's own opendir
+    # (native/tools/cachewalk.h, profiles/r2_hsainit/): it only takes effect if the dynamic symbol
+    # table carries it ahead of libc's
+    out = subprocess.run(["nm", "-D", "--defined-only", str(native_build[tool])],
                          capture_output=True, text=True, check=True).stdout
     assert any(line.split()[-1] == "opendir" and line.split()[-2] == "T" for line in out.splitlines() if line.strip())
 

@@ -17,17 +17,34 @@ __version__ = "0.1.0"
 def _fast_site() -> None:
     """Our daemons and the CLI start with ``python3 -S`` (no ``site`` processing: ~30 ms less
     per interpreter on the bring-up's critical path, where three start one after another).
-    Append the site-packages directories ourselves -- without executing their ``.pth`` hooks --
-    so third-party packages (PyYAML) stay importable."""
+    Third-party packages (PyYAML, jinja2, grpc) must stay importable, so the site-packages
+    directories are appended -- without executing their ``.pth`` hooks -- but only when an import
+    first needs them: a finder placed last on ``sys.meta_path`` sees only imports nothing else
+    could satisfy, and when the module is in one of those directories it adds them all (once) and
+    returns its spec. A bring-up whose caches are warm never loads a third-party package."""
     import sys
 
-    if not sys.flags.no_site:
+    if not sys.flags.no_site or any(getattr(f, "_tk8s_late_site", False) for f in sys.meta_path):
         return
-    import site
 
-    for d in site.getsitepackages() + [site.getusersitepackages()]:
-        if d not in sys.path:
-            sys.path.append(d)
+    class _LateSite:
+        _tk8s_late_site = True
+
+        @classmethod
+        def find_spec(cls, name, path=None, target=None):
+            if path is not None:  # a submodule: its package was found, so nothing is missing
+                return None
+            import site
+            from importlib.machinery import PathFinder
+
+            dirs = [d for d in site.getsitepackages() + [site.getusersitepackages()] if d not in sys.path]
+            spec = PathFinder.find_spec(name, dirs)
+            if spec is not None:  # a third-party package: from now on the directories are on sys.path
+                sys.meta_path.remove(cls)
+                sys.path.extend(dirs)
+            return spec  # None: a probe for an optional module (ntpath's _winapi, ...) stays a miss
+
+    sys.meta_path.append(_LateSite)
 
 
 def _pycache_prefix() -> None:

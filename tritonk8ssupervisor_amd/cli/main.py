@@ -14,7 +14,6 @@
 """
 from __future__ import annotations
 
-import argparse
 import json
 import os
 import sys
@@ -308,13 +307,101 @@ def cmd_playbook(args) -> int:
     return 0 if res.ok else 2
 
 
+# `tk8s setup` options: argparse builds the parser from this table, and _fast_setup_args parses
+# the same table by hand on the bring-up path (argparse + gettext + locale cost ~5 ms there).
+SETUP_OPTIONS: list[tuple[tuple[str, ...], dict]] = [
+    (("--answers",), {"help": "YAML/JSON answers file (non-interactive)"}),
+    (("--yes",), {"action": "store_true", "help": "answer yes to the confirmation"}),
+    (("--resume",), {"action": "store_true", "help": "continue a partial run"}),
+    (("--timeout",), {"type": float, "default": 600.0, "help": "bound on the readiness wait (s)"}),
+    (("--nodes",), {"type": int}),
+    (("--package",), {}),
+    (("--name",), {}),
+    (("--master-hostname",), {}),
+    (("--node-prefix",), {}),
+    (("--port",), {"type": int, "default": None}),
+    (("--no-validate",), {"action": "store_true", "help": "skip the GPU validation DaemonSet"}),
+    (("--rccl",), {"choices": ["on", "off"], "default": None,
+                   "help": "cluster RCCL all-reduce (default: on if >= 2 GPUs)"}),
+    (("--hbm-bytes",), {"type": int, "default": 1 << 30}),
+    (("--md5-bytes",), {"type": int, "default": 256 << 20}),
+    (("--probe-iters",), {"type": int, "default": 3}),
+    (("--node-grace",), {"type": float, "default": 5.0}),
+    (("--rocprof",), {"action": "store_true",
+                      "help": "run the RCCL Job's ranks under rocprofv3 --kernel-trace --stats (.tk8s/profiles/)"}),
+    (("--rocprof-counters",), {"default": None, "metavar": "C1,C2,...",
+                               "help": "with --rocprof: also collect these PMC counters per kernel (their own --pmc "
+                                       "pass with --kernel-trace/--stats only; at most 8 SQ_ and 2 GRBM_ counters), "
+                                       "e.g. SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE"}),
+    (("--rccl-max-bytes",), {"type": int, "default": 64 << 20}),
+    (("--rccl-timeout",), {"type": float, "default": None, "help": "bound on the RCCL Job (default: --timeout)"}),
+    (("--dry-run",), {"action": "store_true",
+                      "help": "terraform plan + ansible-playbook --check of what setup would do; changes nothing "
+                              "(BASELINE.json config 1)"}),
+    (("--platform",), {"choices": ["tk8s", "kubeadm"], "default": None,
+                       "help": "tk8s (default): the in-repo control plane and node agents; kubeadm: install ROCm, "
+                               "amdgpu-dkms, containerd and a real Kubernetes on the machines (needs root + network)"}),
+    (("--json",), {"action": "store_true"}),
+    (("-v", "--verbose"), {"action": "store_true"}),
+]
+
+
+def _fast_setup_args(argv: list[str]):
+    """``setup`` arguments parsed from SETUP_OPTIONS without argparse -- the same Namespace
+    argparse would build -- or None for anything it does not handle exactly like argparse (help,
+    an unknown or abbreviated option, a bad value), which then goes to argparse."""
+    if not argv or argv[0] != "setup":
+        return None
+    from types import SimpleNamespace
+
+    opts = {}
+    ns = {"workdir": os.environ.get("TK8S_WORKDIR", os.getcwd()), "backend": None, "inventory": None,
+          "cmd": "setup", "fn": cmd_setup}
+    for flags, kw in SETUP_OPTIONS:
+        dest = flags[-1].lstrip("-").replace("-", "_")
+        ns[dest] = False if kw.get("action") == "store_true" else kw.get("default")
+        for f in flags:
+            opts[f] = (dest, kw)
+    for f in ("--backend", "--inventory"):
+        opts[f] = (f[2:], {})
+    i, rest = 0, argv[1:]
+    while i < len(rest):
+        a = rest[i]
+        name, eq, val = a.partition("=") if a.startswith("--") else (a, "", "")
+        if name not in opts:
+            return None
+        dest, kw = opts[name]
+        if kw.get("action") == "store_true":
+            if eq:
+                return None
+            ns[dest] = True
+            i += 1
+            continue
+        if not eq:
+            if i + 1 >= len(rest) or rest[i + 1].startswith("-"):
+                return None
+            val = rest[i + 1]
+            i += 1
+        i += 1
+        try:
+            val = kw.get("type", str)(val)
+        except ValueError:
+            return None
+        if "choices" in kw and val not in kw["choices"]:
+            return None
+        ns[dest] = val
+    return SimpleNamespace(**ns)
+
+
 def _backend_flags(p: argparse.ArgumentParser) -> None:
     """--backend/--inventory also after the subcommand (``./setup.sh --backend baremetal ...``)."""
+    import argparse
     p.add_argument("--backend", default=argparse.SUPPRESS, help="local (default), baremetal or triton")
     p.add_argument("--inventory", default=argparse.SUPPRESS, help="baremetal: the SSH inventory file")
 
 
 def build_parser() -> argparse.ArgumentParser:
+    import argparse
     ap = argparse.ArgumentParser(prog="tk8s", description="MI355X-native cluster bring-up")
     ap.add_argument("--workdir", default=os.environ.get("TK8S_WORKDIR", os.getcwd()))
     ap.add_argument("--backend", default=None, help="local (default), baremetal (ssh inventory) or triton")
@@ -322,38 +409,8 @@ def build_parser() -> argparse.ArgumentParser:
     sub = ap.add_subparsers(dest="cmd", required=True)
 
     s = sub.add_parser("setup", help="create the cluster (./setup.sh)")
-    s.add_argument("--answers", help="YAML/JSON answers file (non-interactive)")
-    s.add_argument("--yes", action="store_true", help="answer yes to the confirmation")
-    s.add_argument("--resume", action="store_true", help="continue a partial run")
-    s.add_argument("--timeout", type=float, default=600.0, help="bound on the readiness wait (s)")
-    s.add_argument("--nodes", type=int)
-    s.add_argument("--package")
-    s.add_argument("--name")
-    s.add_argument("--master-hostname")
-    s.add_argument("--node-prefix")
-    s.add_argument("--port", type=int, default=None)
-    s.add_argument("--no-validate", action="store_true", help="skip the GPU validation DaemonSet")
-    s.add_argument("--rccl", choices=["on", "off"], default=None, help="cluster RCCL all-reduce (default: on if >= 2 GPUs)")
-    s.add_argument("--hbm-bytes", type=int, default=1 << 30)
-    s.add_argument("--md5-bytes", type=int, default=256 << 20)
-    s.add_argument("--probe-iters", type=int, default=3)
-    s.add_argument("--node-grace", type=float, default=5.0)
-    s.add_argument("--rocprof", action="store_true",
-                   help="run the RCCL Job's ranks under rocprofv3 --kernel-trace --stats (.tk8s/profiles/)")
-    s.add_argument("--rocprof-counters", default=None, metavar="C1,C2,...",
-                   help="with --rocprof: also collect these PMC counters per kernel (their own --pmc pass "
-                        "with --kernel-trace/--stats only; at most 8 SQ_ and 2 GRBM_ counters), e.g. "
-                        "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE")
-    s.add_argument("--rccl-max-bytes", type=int, default=64 << 20)
-    s.add_argument("--rccl-timeout", type=float, default=None, help="bound on the RCCL Job (default: --timeout)")
-    s.add_argument("--dry-run", action="store_true",
-                   help="terraform plan + ansible-playbook --check of what setup would do; changes nothing "
-                        "(BASELINE.json config 1)")
-    s.add_argument("--platform", choices=["tk8s", "kubeadm"], default=None,
-                   help="tk8s (default): the in-repo control plane and node agents; kubeadm: install ROCm, "
-                        "amdgpu-dkms, containerd and a real Kubernetes on the machines (needs root + network)")
-    s.add_argument("--json", action="store_true")
-    s.add_argument("-v", "--verbose", action="store_true")
+    for flags, kw in SETUP_OPTIONS:
+        s.add_argument(*flags, **kw)
     _backend_flags(s)
     s.set_defaults(fn=cmd_setup)
 
@@ -419,7 +476,8 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 def main(argv: list[str] | None = None) -> int:
-    args = build_parser().parse_args(argv)
+    argv = sys.argv[1:] if argv is None else argv
+    args = _fast_setup_args(argv) or build_parser().parse_args(argv)
     if getattr(args, "inventory", None):
         os.environ["TK8S_INVENTORY"] = str(Path(args.inventory).resolve())
     if getattr(args, "backend", None):

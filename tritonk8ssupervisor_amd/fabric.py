@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import json
 import os
-import shutil
 import time
 from pathlib import Path
 
@@ -67,6 +66,8 @@ class FabricCheck:
                    "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
         prof_dir = None
         if self.rocprof:
+            import shutil
+
             rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
             if os.environ.get("TK8S_FAKE_GPUS") or not os.path.exists(rp):
                 self.out("    --rocprof: rocprofv3 unavailable here (or GPUs are faked); profiling skipped")

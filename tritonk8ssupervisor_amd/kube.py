@@ -5,7 +5,6 @@ waits for conditions with the control plane's long-poll watch (no sleep loops).
 """
 from __future__ import annotations
 
-import copy
 import time
 from pathlib import Path
 
@@ -96,6 +95,8 @@ def apply_objects(k: Client, objs: list[dict]) -> list[dict]:
         if is_subset(want, cur):
             action = "unchanged"
         else:
+            import copy
+
             body = copy.deepcopy(o)
             md = body.setdefault("metadata", {})
             md["resourceVersion"] = cur["metadata"]["resourceVersion"]

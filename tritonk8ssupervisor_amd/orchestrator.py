@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import json
 import os
-import shutil
 import sys
 import threading
 import time
@@ -414,6 +413,7 @@ class Setup(KubeadmPlatform, FabricCheck):
         of the rendered rancher.tf, and the playbook in check mode against the planned machines.
         Everything is rendered in a scratch copy of the workspace, which is removed afterwards;
         no machine is created, no process started, no file of this workspace written."""
+        import shutil
         import tempfile
 
         from .playbook import Playbook

@@ -18,8 +18,6 @@ our role uses explicit tests), ``playbook_dir: $(pwd)`` (clusterUp.yml:12 — th
 """
 from __future__ import annotations
 
-import configparser
-import copy
 import os
 import shlex
 import threading
@@ -136,11 +134,11 @@ class Playbook:
         self._gv_cache: dict[str, dict] = {}
 
     def _read_cfg(self) -> dict:
-        p = self.dir / "ansible.cfg"
-        cp = configparser.ConfigParser()
-        if p.exists():
-            cp.read(p)
-        return dict(cp["defaults"]) if cp.has_section("defaults") else {}
+        try:
+            text = (self.dir / "ansible.cfg").read_text()
+        except OSError:
+            return {}
+        return read_ini_section(text, "defaults")
 
     def say(self, s: str) -> None:
         with self._print_lock:
@@ -457,4 +455,46 @@ class Playbook:
 
 
 def copy_vars(d: dict) -> dict:
+    import copy
+
     return copy.deepcopy(d)
+
+
+def read_ini_section(text: str, section: str) -> dict:
+    """``dict(ConfigParser()[section])`` of an INI text (ansible.cfg) without importing configparser
+    on the bring-up path: ``key = value`` / ``key: value`` lines, keys lower-cased, ``#``/``;``
+    comment lines. Anything beyond that (continuation lines, ``%(..)s`` interpolation, a
+    DEFAULT section) goes to configparser itself."""
+    if "%(" in text or "[DEFAULT]" in text:
+        return _configparser_section(text, section)
+    out: dict = {}
+    cur = None
+    for raw in text.splitlines():
+        line = raw.strip()
+        if not line or line[0] in "#;":
+            continue
+        if raw[:1] in " \t":
+            return _configparser_section(text, section)  # a continuation line
+        if line.startswith("[") and line.endswith("]"):
+            cur = line[1:-1]
+            continue
+        if cur != section:
+            continue
+        k, sep, v = _split_ini(line)
+        if not sep:
+            return _configparser_section(text, section)
+        out[k.strip().lower()] = v.strip()
+    return out
+
+
+def _split_ini(line: str):
+    i = min([j for j in (line.find("="), line.find(":")) if j >= 0], default=-1)
+    return (line, "", "") if i < 0 else (line[:i], line[i], line[i + 1:])
+
+
+def _configparser_section(text: str, section: str) -> dict:
+    import configparser
+
+    cp = configparser.ConfigParser()
+    cp.read_string(text)
+    return dict(cp[section]) if cp.has_section(section) else {}

@@ -12,7 +12,6 @@ include_vars, meta, ping. tk8s modules replace the Docker ones:
 """
 from __future__ import annotations
 
-import base64
 import json
 import os
 import re
@@ -425,6 +424,8 @@ def m_slurp(args, *, ctx, target, local, check, **_):
         if check:  # produced by a task that check mode did not run
             return {"skipped": True, "changed": False, "msg": f"check mode: {src} does not exist yet"}
         return {"failed": True, "msg": f"file not found: {fs.path(src)}"}
+    import base64
+
     return {"content": base64.b64encode(data).decode(), "encoding": "base64", "source": str(fs.path(src)), "changed": False}
 
 

@@ -18,9 +18,7 @@ share the host never share an address or a GPU.
 from __future__ import annotations
 
 import getpass
-import ipaddress
 import os
-import shutil
 import socket
 import subprocess
 from pathlib import Path
@@ -61,6 +59,26 @@ def _loopback_multi_ok() -> bool:
     finally:
         s.close()
 
+
+
+def _ipv4_hosts(cidr: str):
+    """The host addresses of an IPv4 network, in order -- ``ipaddress.ip_network(cidr).hosts()``
+    as strings, without importing ipaddress on the bring-up path (prefixes /31 and /32, and
+    anything that is not dotted-quad IPv4, go to ipaddress itself)."""
+    addr, _, plen = cidr.partition("/")
+    parts = addr.split(".")
+    if len(parts) != 4 or not all(p.isdigit() and int(p) < 256 for p in parts) or not plen.isdigit() or int(plen) > 30:
+        import ipaddress
+
+        yield from (str(a) for a in ipaddress.ip_network(cidr).hosts())
+        return
+    n = int(plen)
+    base = (int(parts[0]) << 24) | (int(parts[1]) << 16) | (int(parts[2]) << 8) | int(parts[3])
+    mask = (0xFFFFFFFF << (32 - n)) & 0xFFFFFFFF
+    if base & ~mask & 0xFFFFFFFF:
+        raise ValueError(f"{cidr} has host bits set")
+    for a in range(base + 1, base + (1 << (32 - n)) - 1):
+        yield f"{a >> 24}.{(a >> 16) & 255}.{(a >> 8) & 255}.{a & 255}"
 
 class LocalProvider(Provider):
     name = "local"
@@ -172,9 +190,7 @@ class LocalProvider(Provider):
             if not self._multi():
                 out.append("127.0.0.1")
                 continue
-            subnet = ipaddress.ip_network(net.subnet)
-            for addr in subnet.hosts():
-                ip = str(addr)
+            for ip in _ipv4_hosts(net.subnet):
                 if ip not in used and ip not in host_used:
                     used[ip] = name
                     HostRegistry.claim(host, "ips", ip, self.alloc_file, name)
@@ -334,4 +350,6 @@ class LocalProvider(Provider):
             atomic_write_json(self.alloc_file, alloc)
             with self.host.locked() as host:
                 HostRegistry.release(host, self.alloc_file, machine.name)
+        import shutil
+
         shutil.rmtree(sandbox, ignore_errors=True)

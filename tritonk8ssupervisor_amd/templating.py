@@ -22,10 +22,7 @@ Reference playbooks rely on e.g. ``project_id['content'] | b64decode | replace('
 """
 from __future__ import annotations
 
-import ast
-import base64
-import io
-import tokenize
+import _ast  # the node classes and the parse flag; the ``ast`` module (unparse) only for messages
 import json
 import os
 import re
@@ -48,7 +45,21 @@ _ALLOWED_METHODS = {
 
 
 def _b64decode(s):
+    import base64
+
     return base64.b64decode(s).decode(errors="replace")
+
+
+def _b64encode(s):
+    import base64
+
+    return base64.b64encode(str(s).encode()).decode()
+
+
+def _unparse(node) -> str:
+    import ast
+
+    return ast.unparse(node)
 
 
 def _default(v, d="", boolean=False):
@@ -59,7 +70,7 @@ def _default(v, d="", boolean=False):
 
 FILTERS = {
     "b64decode": _b64decode,
-    "b64encode": lambda s: base64.b64encode(str(s).encode()).decode(),
+    "b64encode": _b64encode,
     "replace": lambda s, a, b: str(s).replace(a, b),
     "default": _default,
     "d": _default,
@@ -156,7 +167,7 @@ class _Eval:
     def v_Dict(self, n):
         return {self(k): self(v) for k, v in zip(n.keys, n.values)}
 
-    def _get(self, base, key, label):
+    def _get(self, base, key, node):
         if isinstance(base, _UndefinedValue):
             if self.strict:
                 raise Undefined(f"'{base.name}' is undefined")
@@ -170,20 +181,20 @@ class _Eval:
             except IndexError:
                 pass
         if self.strict:
-            raise Undefined(f"{label} has no attribute/key {key!r}")
-        return _UndefinedValue(f"{label}.{key}")
+            raise Undefined(f"{_unparse(node)} has no attribute/key {key!r}")
+        return _UndefinedValue(f"{_unparse(node)}.{key}")
 
     def v_Attribute(self, n):
         base = self(n.value)
         if isinstance(base, (str, dict, list)) and n.attr in _ALLOWED_METHODS.get(type(base), ()):
             if not (isinstance(base, dict) and n.attr in base):
                 return getattr(base, n.attr)
-        return self._get(base, n.attr, ast.unparse(n.value))
+        return self._get(base, n.attr, n.value)
 
     def v_Subscript(self, n):
         base = self(n.value)
         key = self(n.slice)
-        return self._get(base, key, ast.unparse(n.value))
+        return self._get(base, key, n.value)
 
     def _lenient(self, node):
         saved, self.strict = self.strict, False
@@ -193,7 +204,7 @@ class _Eval:
             self.strict = saved
 
     def v_Call(self, n):
-        if isinstance(n.func, ast.Name) and n.func.id == "__filter__":
+        if isinstance(n.func, _ast.Name) and n.func.id == "__filter__":
             name = n.args[0].value
             if name not in FILTERS:
                 raise _Unsupported(f"unknown filter {name!r}")
@@ -203,25 +214,25 @@ class _Eval:
                     raise Undefined(f"'{val.name}' is undefined")
                 return val  # propagate to the enclosing (strict) expression
             return FILTERS[name](val, *[self(a) for a in n.args[2:]])
-        if isinstance(n.func, ast.Name) and n.func.id == "__test__":
+        if isinstance(n.func, _ast.Name) and n.func.id == "__test__":
             return _jinja_test(n.args[0].value, self._lenient(n.args[1]))
-        if isinstance(n.func, ast.Name) and n.func.id not in self.vars:
+        if isinstance(n.func, _ast.Name) and n.func.id not in self.vars:
             raise _Unsupported(f"function {n.func.id}()")  # lookup(), query(), range() ...
         fn = self(n.func)
         if not callable(fn) or getattr(fn, "__self__", None) is None:
-            raise TemplateError(f"call of {ast.unparse(n.func)} not allowed")
+            raise TemplateError(f"call of {_unparse(n.func)} not allowed")
         return fn(*[self(a) for a in n.args])
 
     def v_UnaryOp(self, n):
         v = self(n.operand)
-        if isinstance(n.op, ast.Not):
+        if isinstance(n.op, _ast.Not):
             return not v
-        if isinstance(n.op, ast.USub):
+        if isinstance(n.op, _ast.USub):
             return -v
         raise TemplateError("unsupported unary op")
 
     def v_BoolOp(self, n):
-        if isinstance(n.op, ast.And):
+        if isinstance(n.op, _ast.And):
             v = True
             for e in n.values:
                 v = self(e)
@@ -237,8 +248,8 @@ class _Eval:
 
     def v_BinOp(self, n):
         a, b = self(n.left), self(n.right)
-        ops = {ast.Add: lambda: a + b, ast.Sub: lambda: a - b, ast.Mult: lambda: a * b,
-               ast.Div: lambda: a / b, ast.Mod: lambda: a % b, ast.FloorDiv: lambda: a // b}
+        ops = {_ast.Add: lambda: a + b, _ast.Sub: lambda: a - b, _ast.Mult: lambda: a * b,
+               _ast.Div: lambda: a / b, _ast.Mod: lambda: a % b, _ast.FloorDiv: lambda: a // b}
         f = ops.get(type(n.op))
         if f is None:
             raise TemplateError("unsupported operator")
@@ -248,10 +259,10 @@ class _Eval:
         left = self(n.left)
         for op, comp in zip(n.ops, n.comparators):
             right = self(comp)
-            ok = {ast.Eq: lambda: left == right, ast.NotEq: lambda: left != right, ast.Lt: lambda: left < right,
-                  ast.LtE: lambda: left <= right, ast.Gt: lambda: left > right, ast.GtE: lambda: left >= right,
-                  ast.In: lambda: left in right, ast.NotIn: lambda: left not in right,
-                  ast.Is: lambda: left is right, ast.IsNot: lambda: left is not right}[type(op)]()
+            ok = {_ast.Eq: lambda: left == right, _ast.NotEq: lambda: left != right, _ast.Lt: lambda: left < right,
+                  _ast.LtE: lambda: left <= right, _ast.Gt: lambda: left > right, _ast.GtE: lambda: left >= right,
+                  _ast.In: lambda: left in right, _ast.NotIn: lambda: left not in right,
+                  _ast.Is: lambda: left is right, _ast.IsNot: lambda: left is not right}[type(op)]()
             if not ok:
                 return False
             left = right
@@ -301,6 +312,9 @@ def _operand_start(out: list[str]) -> int:
 def _rewrite(expr: str) -> str:
     """Jinja filters/tests -> calls the evaluator understands, with Jinja precedence:
     ``x | f(a) + 1`` -> ``__filter__('f', x, a) + 1``; ``x is not defined`` -> ``not __test__('defined', x)``."""
+    import io
+    import tokenize  # only on a rewrite-cache miss (_rewritten)
+
     try:
         toks = [t for t in tokenize.generate_tokens(io.StringIO(expr).readline)
                 if t.type not in (tokenize.NEWLINE, tokenize.NL, tokenize.ENDMARKER, tokenize.INDENT, tokenize.DEDENT)]
@@ -412,7 +426,7 @@ def _parse(expr: str):
     if hit is None:
         try:
             src = _rewritten(expr)
-            hit = ast.parse(src or "None", mode="eval")
+            hit = compile(src or "None", "<template>", "eval", _ast.PyCF_ONLY_AST)  # = ast.parse(mode="eval")
         except TemplateError as e:
             hit = _Unsupported(str(e))
         except SyntaxError as e:

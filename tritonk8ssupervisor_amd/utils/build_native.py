@@ -174,7 +174,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if force or _stale(out, deps):
             links.append([HIPCC, str(obj), "-o", str(out), f"-L{LIBDIR}", *rccl, "-ltk8s",
                           "-Wl,-rpath,$ORIGIN/../lib", *hip_libs, *(["-lrccl"] if rccl else []),
-                          "-lpthread"])
+                          "-Wl,--export-dynamic-symbol=opendir", "-ldl", "-lpthread"])  # cachewalk.h
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(lambda c: _run(c, verbose), links))
 
@@ -209,7 +209,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if force or _stale(hsa_bin, [hsa_src]):
         _run([CXX, "-O2", "-std=c++17", "-Wall", f"-I{NATIVE / 'include'}", f"-I{NATIVE / 'tools'}",
               f"-I{ROCM / 'include'}", str(hsa_src), "-o", str(hsa_bin), f"-L{ROCM / 'lib'}", "-lhsa-runtime64",
-              f"-Wl,-rpath,{ROCM / 'lib'}", "-Wl,--export-dynamic-symbol=opendir", "-ldl", "-lpthread"], verbose)
+              f"-Wl,-rpath,{ROCM / 'lib'}", "-Wl,--export-dynamic-symbol=opendir", "-ldl", "-lpthread"], verbose)  # cachewalk.h
 
     precompile_python()
     out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,

@@ -84,8 +84,6 @@ def locked_append_line(path: str | os.PathLike, line: str) -> None:
 
 def remove_paths(paths: list[str | os.PathLike]) -> list[str]:
     """rm -rf each path; returns the ones that existed."""
-    import shutil
-
     removed = []
     for p in paths:
         p = Path(p)
@@ -93,6 +91,8 @@ def remove_paths(paths: list[str | os.PathLike]) -> list[str]:
             p.unlink()
             removed.append(str(p))
         elif p.is_dir():
+            import shutil  # only for directories: not on the bring-up path
+
             shutil.rmtree(p, ignore_errors=True)
             removed.append(str(p))
     return removed

@@ -8,7 +8,6 @@ into a fresh one; orchestrator.Setup, the fabric check and the kubeadm platform 
 from __future__ import annotations
 
 import os
-import shutil
 import sys
 from pathlib import Path
 
@@ -65,6 +64,8 @@ class Workspace:
 
 def init_workspace(dst: str | os.PathLike, src: Path = REPO) -> Workspace:
     """Copy the module/role/manifest templates into a fresh workspace directory."""
+    import shutil
+
     d = Path(dst)
     for rel in TEMPLATE_DIRS:
         if (d / rel).exists():
