@@ -296,3 +296,61 @@ def test_late_site_finder_only_adds_site_dirs_for_third_party_imports():
     r = subprocess.run([sys.executable, "-S", "-c", code], cwd=REPO, capture_output=True, text=True, timeout=60,
                        env={**os.environ, "PYTHONPATH": str(REPO)})
     assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr
+
+
+@pytest.mark.parametrize("argv", [
+    ["--await-url", "run/registration-url", "--name", "kubenode1", "--ip", "127.0.1.3"],
+    ["http://127.0.0.1:1/v1/scripts/T", "--name", "n", "--tool-dir", "/a", "--tool-dir", "/b", "--gpus", "0,1",
+     "--timeout", "5", "--smi-interval", "0", "--smi-delay", "1.5", "--labels", "a=b,c=d", "--sandbox", "/s"],
+    ["--device-plugin", "grpc", "--url", "http://u"],
+])
+def test_agent_fast_parser_matches_argparse(argv):
+    from tritonk8ssupervisor_amd.agent import agent as ag
+
+    assert ag._parse_fast(argv) == ag._parse_argparse(argv)
+
+
+@pytest.mark.parametrize("argv", [["--help"], ["--name=x"], ["--device-plugin", "other", "--url", "u"], ["a", "b"],
+                                  ["--timeout", "soon", "--url", "u"], ["--name"]])
+def test_agent_fast_parser_defers_the_rest(argv):
+    from tritonk8ssupervisor_amd.agent import agent as ag
+
+    assert ag._parse_fast(argv) is None
+
+
+def test_controlplane_fast_parser():
+    from tritonk8ssupervisor_amd.controlplane import server
+
+    a = server._parse_fast(["--host", "127.0.1.1", "--port", "0", "--advertise", "127.0.1.1", "--state-dir", "/s",
+                            "--node-grace", "2.5", "--dns-port", "0", "--ingress-port", "0", "--ready-file", "/r"])
+    assert a == {"host": "127.0.1.1", "port": 0, "advertise": "127.0.1.1", "state_dir": "/s", "node_grace": 2.5,
+                 "dns_port": 0, "ingress_port": 0, "ready_file": "/r"}
+    assert server._parse_fast(["--help"]) is None and server._parse_fast(["--port=1"]) is None
+    assert server._parse_fast(["--port", "x"]) is None
+
+
+def test_daemon_entries_skip_runpy_and_ssl():
+    """The control plane and agent start with -c '<pkg>.__main__' imports: no runpy, and the control
+    plane (plain HTTP) keeps ssl out of asyncio."""
+    code = ("import sys; sys.argv = ['-c', '--help']; "
+            "import tritonk8ssupervisor_amd.controlplane.__main__")
+    r = subprocess.run([sys.executable, "-S", "-c", code], cwd=REPO, capture_output=True, text=True, timeout=60,
+                       env={**os.environ, "PYTHONPATH": str(REPO)})
+    assert r.returncode == 0 and "tk8s-controlplane" in r.stdout, r.stderr
+    code = ("import sys; sys.modules.setdefault('ssl', None); import asyncio, tritonk8ssupervisor_amd.controlplane.server; "
+            "print(sorted({'runpy', 'argparse', 'uuid', 'secrets', 'html'} & set(sys.modules)), sys.modules['ssl'])")
+    r = subprocess.run([sys.executable, "-S", "-c", code], cwd=REPO, capture_output=True, text=True, timeout=60,
+                       env={**os.environ, "PYTHONPATH": str(REPO)})
+    assert r.returncode == 0 and r.stdout.strip() == "[] None", (r.stdout, r.stderr)
+
+
+def test_uuid4_and_token_hex_shapes():
+    import re
+    import uuid
+
+    from tritonk8ssupervisor_amd.utils.ids import token_hex, uuid4
+
+    u = uuid4()
+    assert uuid.UUID(u).version == 4 and str(uuid.UUID(u)) == u and uuid.UUID(u).variant == uuid.RFC_4122
+    assert uuid4() != u
+    assert re.fullmatch(r"[0-9a-f]{40}", token_hex(20))

@@ -14,6 +14,11 @@ and their start-up time is part of the bring-up metric.
 __version__ = "0.1.0"
 
 
+# optional modules the stdlib probes for on Linux (subprocess: msvcrt, _winapi; ntpath: nt, ...)
+_PLATFORM_PROBES = frozenset({"msvcrt", "_winapi", "nt", "winreg", "_winreg", "_overlapped", "_scproxy", "vms_lib",
+                              "java", "_wmi"})
+
+
 def _fast_site() -> None:
     """Our daemons and the CLI start with ``python3 -S`` (no ``site`` processing: ~30 ms less
     per interpreter on the bring-up's critical path, where three start one after another).
@@ -32,8 +37,8 @@ def _fast_site() -> None:
 
         @classmethod
         def find_spec(cls, name, path=None, target=None):
-            if path is not None:  # a submodule: its package was found, so nothing is missing
-                return None
+            if path is not None or name in _PLATFORM_PROBES:  # a submodule, or the stdlib probing
+                return None                                       # for another OS: nothing to add
             import site
             from importlib.machinery import PathFinder
 

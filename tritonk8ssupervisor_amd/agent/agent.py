@@ -17,8 +17,6 @@ stops heartbeats (lease expiry -> NotReady).
 """
 from __future__ import annotations
 
-import argparse
-import base64
 import json
 import os
 import subprocess
@@ -413,6 +411,8 @@ class Agent:
             raise ConfigError(f"{kind[:-1]} {name}: {e}") from e
         data = dict(o.get("data") or {})
         if kind == "secrets":
+            import base64
+
             data = {k: base64.b64decode(v).decode(errors="replace") for k, v in data.items()}
         return data
 
@@ -631,36 +631,95 @@ def _expand(s: str, env: dict) -> str:
     return expand(s, env)
 
 
-def main(argv: list[str] | None = None) -> int:
+_STR_OPTS = {"--url": "url_opt", "--name": "name", "--ip": "ip", "--sandbox": "sandbox", "--gpus": "gpus",
+             "--labels": "labels", "--device-plugin": "device_plugin", "--await-url": "await_url"}
+_FLOAT_OPTS = {"--timeout": "timeout", "--smi-interval": "smi_interval", "--smi-delay": "smi_delay"}
+
+
+def _defaults() -> dict:
+    return {"url": None, "url_opt": None, "name": os.environ.get("TK8S_MACHINE", os.uname().nodename),
+            "ip": os.environ.get("TK8S_MACHINE_IP", "127.0.0.1"), "sandbox": os.environ.get("TK8S_MACHINE_DIR", "."),
+            "gpus": os.environ.get("TK8S_MACHINE_GPUS", ""), "labels": "", "tool_dir": [], "timeout": 60.0,
+            "smi_interval": float(os.environ.get("TK8S_SMI_INTERVAL", "30")),
+            "smi_delay": float(os.environ.get("TK8S_SMI_DELAY", "5")),
+            "device_plugin": os.environ.get("TK8S_DEVICE_PLUGIN", "builtin"), "await_url": None}
+
+
+def _parse_fast(argv: list[str]) -> dict | None:
+    """The agent's arguments without argparse (~2 ms of its start, which the bring-up waits for):
+    ``--opt value`` pairs and one optional positional URL; None for anything else (``--help``,
+    ``--opt=value``, unknown options, bad values), which argparse then handles."""
+    a = _defaults()
+    i = 0
+    while i < len(argv):
+        tok = argv[i]
+        if not tok.startswith("-"):
+            if a["url"] is not None:
+                return None
+            a["url"] = tok
+            i += 1
+            continue
+        if i + 1 >= len(argv) or argv[i + 1].startswith("-"):
+            return None
+        val = argv[i + 1]
+        if tok in _STR_OPTS:
+            a[_STR_OPTS[tok]] = val
+        elif tok in _FLOAT_OPTS:
+            try:
+                a[_FLOAT_OPTS[tok]] = float(val)
+            except ValueError:
+                return None
+        elif tok == "--tool-dir":
+            a["tool_dir"].append(val)
+        else:
+            return None
+        i += 2
+    if a["device_plugin"] not in ("builtin", "grpc"):
+        return None
+    return a
+
+
+def _parse_argparse(argv: list[str] | None) -> dict:
+    import argparse
+
+    d = _defaults()
     ap = argparse.ArgumentParser(prog="tk8s-agent", description="tk8s node agent")
     ap.add_argument("url", nargs="?", help="registration URL (http://master:port/v1/scripts/TOKEN)")
     ap.add_argument("--url", dest="url_opt")
-    ap.add_argument("--name", default=os.environ.get("TK8S_MACHINE", os.uname().nodename))
-    ap.add_argument("--ip", default=os.environ.get("TK8S_MACHINE_IP", "127.0.0.1"))
-    ap.add_argument("--sandbox", default=os.environ.get("TK8S_MACHINE_DIR", "."))
-    ap.add_argument("--gpus", default=os.environ.get("TK8S_MACHINE_GPUS", ""))
+    ap.add_argument("--name", default=d["name"])
+    ap.add_argument("--ip", default=d["ip"])
+    ap.add_argument("--sandbox", default=d["sandbox"])
+    ap.add_argument("--gpus", default=d["gpus"])
     ap.add_argument("--labels", default="")
     ap.add_argument("--tool-dir", action="append", default=[])
     ap.add_argument("--timeout", type=float, default=60.0)
-    ap.add_argument("--smi-interval", type=float, default=float(os.environ.get("TK8S_SMI_INTERVAL", "30")),
+    ap.add_argument("--smi-interval", type=float, default=d["smi_interval"],
                     help="AMD SMI health sampling period in s (0 disables)")
-    ap.add_argument("--smi-delay", type=float, default=float(os.environ.get("TK8S_SMI_DELAY", "5")),
+    ap.add_argument("--smi-delay", type=float, default=d["smi_delay"],
                     help="first AMD SMI sample this many s after joining")
-    ap.add_argument("--device-plugin", choices=["builtin", "grpc"],
-                    default=os.environ.get("TK8S_DEVICE_PLUGIN", "builtin"),
+    ap.add_argument("--device-plugin", choices=["builtin", "grpc"], default=d["device_plugin"],
                     help="builtin: in-process plugin core; grpc: the kubelet device-plugin API over Unix sockets")
     ap.add_argument("--await-url", default=None,
                     help="standby: wait for a file holding the registration URL (relative to --sandbox)")
-    a = ap.parse_args(argv)
-    url = a.url_opt or a.url
-    if not url and not a.await_url:
+    a = vars(ap.parse_args(argv))
+    if not (a["url_opt"] or a["url"]) and not a["await_url"]:
         ap.error("registration URL (or --await-url FILE) is required")
-    gpus = [int(x) for x in a.gpus.split(",") if x.strip() != ""]
-    labels = dict(kv.split("=", 1) for kv in a.labels.split(",") if "=" in kv)
-    tools = a.tool_dir or [str(Path(__file__).resolve().parents[1] / "bin")]
-    wait = Path(a.sandbox) / a.await_url if a.await_url else None
-    return Agent(url, a.name, a.ip, a.sandbox, gpus, labels, tools, a.timeout,
-                 smi_interval=a.smi_interval, smi_delay=a.smi_delay, device_plugin=a.device_plugin).run(wait)
+    return a
+
+
+def main(argv: list[str] | None = None) -> int:
+    trace("agent", "imported")
+    argv = sys.argv[1:] if argv is None else argv
+    a = _parse_fast(argv)
+    if a is None or not (a["url_opt"] or a["url"] or a["await_url"]):
+        a = _parse_argparse(argv)
+    url = a["url_opt"] or a["url"]
+    gpus = [int(x) for x in a["gpus"].split(",") if x.strip() != ""]
+    labels = dict(kv.split("=", 1) for kv in a["labels"].split(",") if "=" in kv)
+    tools = a["tool_dir"] or [str(Path(__file__).resolve().parents[1] / "bin")]
+    wait = Path(a["sandbox"]) / a["await_url"] if a["await_url"] else None
+    return Agent(url, a["name"], a["ip"], a["sandbox"], gpus, labels, tools, a["timeout"],
+                 smi_interval=a["smi_interval"], smi_delay=a["smi_delay"], device_plugin=a["device_plugin"]).run(wait)
 
 
 if __name__ == "__main__":

@@ -8,10 +8,10 @@ import asyncio
 import copy
 import json
 import os
-import secrets
 import time
 from pathlib import Path
 
+from ..utils.ids import token_hex
 from ..utils.net import host_port
 from ..utils.trace import trace
 from . import k8s_wire
@@ -426,7 +426,7 @@ class KubernetesAPI:
         md = body.setdefault("metadata", {})
         name = md.get("name")
         if not name and md.get("generateName"):
-            name = md["generateName"] + secrets.token_hex(3)
+            name = md["generateName"] + token_hex(3)
         if not name:
             raise HttpError(422, "metadata.name is required")
         md["name"] = name

@@ -5,7 +5,6 @@ from __future__ import annotations
 
 import copy
 import json
-import secrets
 
 from .httpserver import HttpError
 from .store import now_iso

@@ -6,12 +6,11 @@ server.ControlPlane: it uses the store, the routes and the helpers the server se
 from __future__ import annotations
 
 import copy
-import html
 import json
 import os
-import secrets
 import time
 
+from ..utils.ids import token_hex
 from ..utils.trace import trace
 from .httpserver import HttpError, Request, Response
 from .store import now_iso
@@ -58,7 +57,7 @@ class RancherAPI:
              "allowSystemRole": bool(body.get("allowSystemRole", False)), "members": body.get("members", []),
              "virtualMachine": bool(body.get("virtualMachine", False)),
              "servicesPortRange": body.get("servicesPortRange"), "projectLinks": body.get("projectLinks", []),
-             "created": now_iso(), "created_seq": self._seq, "apiToken": secrets.token_hex(16),
+             "created": now_iso(), "created_seq": self._seq, "apiToken": token_hex(16),
              "links": {"self": f"{self.base}/v2-beta/projects/{pid}"},
              "metadata": {"name": pid}}
         self.store.put("projects", pid, p)
@@ -80,7 +79,7 @@ class RancherAPI:
         pid = req.q("projectId") or req.json().get("projectId")
         p = self.project(pid)
         tid = self._next_id("1c")
-        token = secrets.token_hex(20)
+        token = token_hex(20)
         t = {"id": tid, "type": "registrationToken", "projectId": p["id"], "token": token, "state": "active",
              "registrationUrl": f"{self.base}/v1/scripts/{token}",
              "command": f"python3 -m tritonk8ssupervisor_amd.agent --url {self.base}/v1/scripts/{token}",
@@ -114,7 +113,7 @@ class RancherAPI:
         if not name:
             raise HttpError(422, "node name is required")
         key = _key(pid, name)
-        ntok = secrets.token_hex(16)
+        ntok = token_hex(16)
         gpus = body.get("devices", [])
         healthy = sum(1 for d in gpus if d.get("health", "Healthy") == "Healthy")
         cap = dict(body.get("capacity", {}))
@@ -155,6 +154,8 @@ class RancherAPI:
         s = self.summary(p["id"])
         if s["nodes_ready"] == 0:
             return Response(503, "Service Unavailable", content_type="text/plain")
+        import html
+
         esc = html.escape
         rows = "".join(
             f"<tr><td>{esc(n['metadata']['name'])}</td><td>{'Ready' if node_ready(n) else 'NotReady'}</td>"

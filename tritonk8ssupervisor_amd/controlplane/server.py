@@ -34,7 +34,6 @@ This module keeps the process: routes, leases, snapshots, the asyncio run loop a
 """
 from __future__ import annotations
 
-import argparse
 import asyncio
 import json
 import os
@@ -44,6 +43,7 @@ import time
 from pathlib import Path
 
 from ..utils.net import host_port
+from ..utils.trace import trace
 from . import k8s_wire
 from .controllers import Controllers
 from .httpserver import HttpError, HttpServer, Request, Response, Router
@@ -297,6 +297,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
         tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop())]
         # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
         print(f"Listening on {host}:{port}", flush=True)
+        trace("cp", "listening")
         if ready_file:
             from ..utils.fsutil import atomic_write_json
 
@@ -356,21 +357,51 @@ def await_args(path: str, timeout: float | None = None) -> list[str]:
         time.sleep(0.001 if time.monotonic() < t_fast else 0.05)
 
 
+_OPTS = {"--host": ("host", str, "127.0.0.1"), "--port": ("port", int, 8080), "--advertise": ("advertise", str, None),
+         "--state-dir": ("state_dir", str, None), "--ready-file": ("ready_file", str, None),
+         "--node-grace": ("node_grace", float, None), "--dns-port": ("dns_port", int, None),
+         "--ingress-port": ("ingress_port", int, None)}
+
+
+def _parse_fast(argv: list[str]) -> dict | None:
+    """The daemon's ``--opt value`` arguments without argparse (~2 ms of its start); None for
+    anything else (``--help``, ``--opt=value``, an unknown option), which argparse then handles."""
+    out = {dest: default for dest, _, default in _OPTS.values()}
+    out["node_grace"] = float(os.environ.get("TK8S_NODE_GRACE", "5"))
+    if len(argv) % 2:
+        return None
+    for flag, val in zip(argv[::2], argv[1::2]):
+        if flag not in _OPTS:
+            return None
+        dest, typ, _ = _OPTS[flag]
+        try:
+            out[dest] = typ(val)
+        except ValueError:
+            return None
+    return out
+
+
 def main(argv: list[str] | None = None) -> int:
-    ap = argparse.ArgumentParser(prog="tk8s-controlplane", description=__doc__.splitlines()[0])
-    ap.add_argument("--host", default="127.0.0.1")
-    ap.add_argument("--port", type=int, default=8080)
-    ap.add_argument("--advertise", default=None, help="address put into URLs handed to agents")
-    ap.add_argument("--state-dir", default=None)
-    ap.add_argument("--node-grace", type=float, default=float(os.environ.get("TK8S_NODE_GRACE", "5")))
-    ap.add_argument("--ready-file", default=None)
-    ap.add_argument("--dns-port", type=int, default=None, help="cluster DNS (UDP) port; 0 disables (default 53, "
-                    "shifted when not root)")
-    ap.add_argument("--ingress-port", type=int, default=None, help="ingress controller port; 0 disables (default 80, "
-                    "shifted when not root)")
-    a = ap.parse_args(argv)
-    cp = ControlPlane(a.host, a.port, a.state_dir, a.node_grace, a.advertise, a.dns_port, a.ingress_port)
-    asyncio.run(cp.run(a.ready_file))
+    argv = sys.argv[1:] if argv is None else argv
+    a = _parse_fast(argv)
+    if a is None:
+        import argparse
+
+        ap = argparse.ArgumentParser(prog="tk8s-controlplane", description=__doc__.splitlines()[0])
+        ap.add_argument("--host", default="127.0.0.1")
+        ap.add_argument("--port", type=int, default=8080)
+        ap.add_argument("--advertise", default=None, help="address put into URLs handed to agents")
+        ap.add_argument("--state-dir", default=None)
+        ap.add_argument("--node-grace", type=float, default=float(os.environ.get("TK8S_NODE_GRACE", "5")))
+        ap.add_argument("--ready-file", default=None)
+        ap.add_argument("--dns-port", type=int, default=None, help="cluster DNS (UDP) port; 0 disables (default 53, "
+                        "shifted when not root)")
+        ap.add_argument("--ingress-port", type=int, default=None, help="ingress controller port; 0 disables (default "
+                        "80, shifted when not root)")
+        a = vars(ap.parse_args(argv))
+    cp = ControlPlane(a["host"], a["port"], a["state_dir"], a["node_grace"], a["advertise"], a["dns_port"],
+                      a["ingress_port"])
+    asyncio.run(cp.run(a["ready_file"]))
     return 0
 
 

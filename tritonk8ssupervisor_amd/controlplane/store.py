@@ -9,11 +9,11 @@ from __future__ import annotations
 import asyncio
 import copy
 import time
-import uuid
 from collections import deque
 from typing import Any, Callable, Iterable
 
 from ..utils.fsutil import atomic_write_json, read_json
+from ..utils.ids import uuid4
 
 HISTORY = 50_000
 
@@ -79,7 +79,7 @@ class Store:
             obj.setdefault("kind", tm[1])
         md = obj.setdefault("metadata", {})
         md["resourceVersion"] = str(self.rv)
-        md.setdefault("uid", old["metadata"]["uid"] if old else str(uuid.uuid4()))
+        md.setdefault("uid", old["metadata"]["uid"] if old else uuid4())
         md.setdefault("creationTimestamp", old["metadata"].get("creationTimestamp") if old else now_iso())
         table[key] = obj
         self._notify(kind, "MODIFIED" if old else "ADDED", obj)

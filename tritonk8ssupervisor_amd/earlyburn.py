@@ -315,7 +315,7 @@ def controlplane_zygote(p: dict) -> dict | None:
     os.makedirs(os.path.join(sb, "logs"), exist_ok=True)
     args = os.path.join(sb, "run", "controlplane.args")
     argv = [sup, "--pidfile", pidfile, "--log", os.path.join(sb, "logs", "controlplane.log"), "--restart",
-            "unless-stopped", "--", sys.executable, "-S", "-m", "tritonk8ssupervisor_amd.controlplane",
+            "unless-stopped", "--", sys.executable, "-S", "-c", "import tritonk8ssupervisor_amd.controlplane.__main__",
             "--await-args", args]
     env = dict(os.environ)
     env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(PKG)] + [x for x in env.get("PYTHONPATH", "").split(os.pathsep) if x])
