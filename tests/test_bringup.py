@@ -462,8 +462,14 @@ def test_answers_file_bring_up_starts_the_burnin_before_the_cli_imports(ws):
     boot = [e for e in events if e["event"] == "controlplane_boot_started"]
     assert len(boot) == 1 and boot[0].get("zygote")
     assert json.loads((ws / ".tk8s" / "machines" / "kubemaster" / "run" / "controlplane.args").read_text())[0] == "--host"
-    # the agents started with their machines; rocmsetup's standby task found them running
-    assert sorted(e["name"] for e in events if e["event"] == "agent_boot_started") == ["kubenode1", "kubenode2"]
+    # the agents' interpreters started with the CLI too (one zygote per planned worker) and got
+    # their argv and machine environment at worker boot; rocmsetup's standby task found them running
+    agents = [e for e in events if e["event"] == "agent_boot_started"]
+    assert sorted(e["name"] for e in agents) == ["kubenode1", "kubenode2"] and all(e.get("zygote") for e in agents)
+    for i in (1, 2):
+        spec = json.loads((ws / ".tk8s" / "machines" / f"kubenode{i}" / "run" / "agent.args").read_text())
+        assert spec["argv"][:2] == ["--await-url", "run/registration-url"] and spec["env"]["TK8S_MACHINE"] == f"kubenode{i}"
+        assert spec["cwd"].endswith(f"kubenode{i}")
     standby = [e for e in events if e.get("task", "").endswith("Start the node agent in standby on every host")]
     assert standby and all(v in ("ok", "skipped") for v in standby[0]["results"].values()), standby
     for i in (1, 2):

@@ -331,30 +331,9 @@ def await_args(path: str, timeout: float | None = None) -> list[str]:
     """Zygote mode: wait for the JSON argument list (orchestrator._boot_controlplane writes it
     atomically). A zygote nobody hands arguments to -- the bring-up failed before its master
     existed -- stops its supervisor and exits, so it never lingers or restarts."""
-    if timeout is None:
-        timeout = float(os.environ.get("TK8S_ZYGOTE_TIMEOUT", "120"))
-    deadline = time.monotonic() + timeout
-    t_fast = time.monotonic() + 2.0
-    while True:
-        try:
-            with open(path) as f:
-                argv = json.load(f)
-            if isinstance(argv, list):
-                return [str(a) for a in argv]
-        except (OSError, ValueError):
-            pass
-        if time.monotonic() > deadline:
-            parent = os.getppid()
-            try:
-                with open(f"/proc/{parent}/comm") as f:
-                    if f.read().strip() == "tk8s-supervise":
-                        os.kill(parent, signal.SIGTERM)
-            except OSError:
-                pass
-            raise SystemExit(0)
-        # 1 ms while a bring-up is on its way (the arguments normally arrive within ~0.1 s, on the
-        # critical path), 50 ms once it is clearly not coming (a failed bring-up's leftover)
-        time.sleep(0.001 if time.monotonic() < t_fast else 0.05)
+    from ..utils.zygote import await_json
+
+    return [str(a) for a in await_json(path, timeout, want=list)]
 
 
 _OPTS = {"--host": ("host", str, "127.0.0.1"), "--port": ("port", int, 8080), "--advertise": ("advertise", str, None),

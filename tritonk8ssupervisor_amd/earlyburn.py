@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import os
 import sys
+import threading
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 BIN = os.path.join(PKG, "bin")
@@ -246,10 +247,17 @@ def plan(argv: list[str], environ=None, cwd: str | None = None, kfd_root: str = 
     cmd = host_burnin_command(default_validation_command(peers=per > 1), free[:count])
     state = os.path.join(ws, ".tk8s")
     master = str(opts.get("--master-hostname", answers.get("master_hostname") or "kubemaster"))
+    prefix = str(opts.get("--node-prefix", answers.get("node_prefix") or "kubenode"))
     return {"gpus": free[:count], "command": cmd, "state_dir": state,
+            "workers": [f"{prefix}{i}" for i in range(1, int(nodes) + 1)] if _hostname_ok(prefix) else [],
             "result": os.path.join(state, "run", "host-burnin.json"),
             # the wizard's hostname rule (^[a-zA-Z][0-9a-zA-Z]+$); anything else: no zygote
-            "master": master if len(master) >= 2 and master.isascii() and master.isalnum() and master[0].isalpha() else None}
+            "master": master if _hostname_ok(master) else None}
+
+
+def _hostname_ok(name: str) -> bool:
+    """The wizard's hostname rule (^[a-zA-Z][0-9a-zA-Z]+$): only such names get a zygote."""
+    return len(name) >= 2 and name.isascii() and name.isalnum() and name[0].isalpha()
 
 
 class Spawned:
@@ -325,6 +333,58 @@ def controlplane_zygote(p: dict) -> dict | None:
         (os.POSIX_SPAWN_OPEN, 2, os.devnull, os.O_WRONLY, 0),
     ])
     return {"pid": pid, "sandbox": sb, "args": args, "pidfile": pidfile}
+
+
+AGENT_ENTRY = "import tritonk8ssupervisor_amd.agent.__main__"  # = workspace.AGENT_ENTRY
+_AGENTS: dict[str, dict] = {}
+_AGENTS_STARTED: threading.Thread | None = None
+
+
+def agent_zygotes(p: dict) -> None:
+    """Start each planned worker's node agent interpreter now (in a thread: a spawn per worker),
+    under its supervisor, in the worker's future sandbox: it imports everything while the
+    orchestrator provisions, then waits in ``run/agent.args`` for what only the created machine
+    knows -- its argv (name, address) and environment (sandbox, GPUs) -- which the worker's boot
+    hook (orchestrator._boot_agent) writes. The agent then runs exactly as if started then."""
+    global _AGENTS_STARTED
+    if os.environ.get("TK8S_AGENT_ZYGOTE", "1") == "0" or not p.get("workers"):
+        return
+    sup = os.path.join(BIN, "tk8s-supervise")
+    if not os.access(sup, os.X_OK):
+        return
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(PKG)] + [x for x in env.get("PYTHONPATH", "").split(os.pathsep) if x])
+
+    def spawn_all():
+        for name in p["workers"]:
+            sb = os.path.join(p["state_dir"], "machines", name)
+            pidfile = os.path.join(sb, "run", "agent.pid")
+            try:
+                if os.path.exists(pidfile):  # something of an earlier run: leave it to the orchestrator
+                    continue
+                os.makedirs(os.path.join(sb, "run"), exist_ok=True)
+                os.makedirs(os.path.join(sb, "logs"), exist_ok=True)
+                args = os.path.join(sb, "run", "agent.args")
+                argv = [sup, "--pidfile", pidfile, "--log", os.path.join(sb, "logs", "agent.log"), "--restart",
+                        "unless-stopped", "--", sys.executable, "-S", "-c", AGENT_ENTRY, "--await-args", args]
+                pid = os.posix_spawn(sup, argv, env, setsid=True, file_actions=[
+                    (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
+                    (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
+                    (os.POSIX_SPAWN_OPEN, 2, os.devnull, os.O_WRONLY, 0),
+                ])
+            except OSError:
+                continue
+            _AGENTS[os.path.realpath(sb)] = {"pid": pid, "sandbox": sb, "args": args, "pidfile": pidfile}
+
+    _AGENTS_STARTED = threading.Thread(target=spawn_all, name="agent-zygotes", daemon=True)
+    _AGENTS_STARTED.start()
+
+
+def agent_zygote_for(sandbox: str) -> dict | None:
+    """The node agent zygote started for this worker sandbox, if any (once)."""
+    if _AGENTS_STARTED is not None:
+        _AGENTS_STARTED.join()
+    return _AGENTS.pop(os.path.realpath(sandbox), None)
 
 
 def zygote_for(sandbox: str) -> dict | None:
@@ -427,6 +487,10 @@ def launch(argv: list[str]) -> Early | None:
         _ZYGOTE = controlplane_zygote(p)
     except Exception:  # noqa: BLE001 - the boot hook starts the control plane the usual way
         _ZYGOTE = None
+    try:
+        agent_zygotes(p)
+    except Exception:  # noqa: BLE001 - the boot hooks start the agents the usual way
+        pass
     return _LAUNCHED
 
 

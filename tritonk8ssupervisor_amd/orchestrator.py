@@ -187,8 +187,22 @@ class Setup(KubeadmPlatform, FabricCheck):
         if os.environ.get("TK8S_BOOT_AGENT", "1") == "0":
             return
         pythonpath = os.pathsep.join([str(REPO)] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+        argv = agent_standby_argv(m.name, m.primaryip)
+        from . import earlyburn
+
+        z = earlyburn.agent_zygote_for(m.sandbox)  # its interpreter started with the CLI: hand it the arguments
+        if z is not None:
+            if pid_alive(z["pid"]):
+                env = {**getattr(self.provider, "machine_env", lambda _m: {})(m), "PYTHONPATH": pythonpath}
+                atomic_write(z["args"], json.dumps({"argv": argv[4:], "env": env, "cwd": m.sandbox}))
+                self.events.emit("agent_boot_started", name=m.name, pid=z["pid"], zygote=True)
+                return
+            try:
+                os.killpg(z["pid"], 15)
+            except OSError:
+                pass
         ex = MachineExecutor(self.provider, {m.name: m})
-        info = ex.start_daemon(m.name, "agent", agent_standby_argv(m.name, m.primaryip), env={"PYTHONPATH": pythonpath},
+        info = ex.start_daemon(m.name, "agent", argv, env={"PYTHONPATH": pythonpath},
                                restart="unless-stopped", wait_for_log=None, timeout=0)
         self.events.emit("agent_boot_started", name=m.name, pid=info.get("pid"))
 
