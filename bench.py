@@ -167,7 +167,104 @@ def private_registry(env: dict, root: Path) -> None:
     env.setdefault("TK8S_HOST_REGISTRY", str(root / "hostreg"))
 
 
-def one_bringup(ws: Path, n: int, args, env: dict, log) -> dict:
+KFD_PROC = Path("/sys/class/kfd/kfd/proc")
+
+
+class KfdCensus:
+    """Which processes hold the KFD (``/sys/class/kfd/kfd/proc/<pid>``: every process of the
+    host with the GPU driver open, this box's other tenants included) during one bring-up,
+    sampled every ``period`` s from before ./setup.sh starts (the previous step's settle pause,
+    outside the timed brackets) until its Ready line.
+    A slow runtime start (``hsa_init``) of the burn-in is then attributed to what changed in
+    the KFD process set just before it: a process exiting (the driver
+    tears its GPU state down; a runtime starting meanwhile waits for it), one starting, or
+    nothing visible (a driver-internal cause)."""
+
+    def __init__(self, period: float = 0.005):
+        self.period = period
+        self.events: list[tuple[float, str, str]] = []   # (unix time, "start"|"exit", pid)
+        self.initial: set[str] = set()
+        self._stop = None
+        self._th = None
+
+    @staticmethod
+    def snapshot() -> set[str] | None:
+        try:
+            return {e for e in os.listdir(KFD_PROC) if e.isdigit()}
+        except OSError:
+            return None
+
+    def start(self) -> "KfdCensus":
+        import threading
+
+        first = self.snapshot()
+        if first is None:
+            return self
+        self.initial = first
+        self._stop = threading.Event()
+
+        def loop():
+            prev = first
+            while not self._stop.is_set():
+                cur = self.snapshot() or set()
+                t = time.time()
+                self.events += [(t, "start", p) for p in sorted(cur - prev)]
+                self.events += [(t, "exit", p) for p in sorted(prev - cur)]
+                prev = cur
+                self._stop.wait(self.period)
+
+        self._th = threading.Thread(target=loop, name="kfd-census", daemon=True)
+        self._th.start()
+        return self
+
+    def stop(self) -> None:
+        if self._stop is not None:
+            self._stop.set()
+            self._th.join(1.0)
+
+    def report(self, spawned_unix: float | None, own_pids: set[str], window: float = 0.3) -> dict:
+        """KFD process changes in the ``window`` s before the burn-in was spawned and during its
+        runtime start; own_pids: the KFD pids this bring-up's own processes are known by."""
+        if self._stop is None:
+            return {"available": False}
+        out = {"available": True, "present_at_launch": len(self.initial)}
+        if spawned_unix is None:
+            return out
+        lo = spawned_unix - window
+        near = [{"dt_ms": round((t - spawned_unix) * 1e3, 1), "what": what, "pid": int(p),
+                 "own": p in own_pids} for t, what, p in self.events if t >= lo]
+        out["changes"] = near[:40]
+        return out
+
+
+def slow_start_cause(census: dict, runtime_init_ms: float | None, limit_ms: float = 50.0) -> str | None:
+    """One line naming what most likely delayed a runtime start over ``limit_ms``."""
+    if runtime_init_ms is None or runtime_init_ms <= limit_ms:
+        return None
+    if not census.get("available"):
+        return "unknown: /sys/class/kfd/kfd/proc not readable here"
+    window = runtime_init_ms + 1.0  # changes up to the end of the runtime start count
+    ch = [c for c in census.get("changes", []) if c["dt_ms"] <= window]
+    exits = [c for c in ch if c["what"] == "exit" and c["dt_ms"] <= 0]
+    foreign_exit = [c for c in exits if not c["own"]]
+    if foreign_exit:
+        c = foreign_exit[-1]
+        return f"foreign KFD process {c['pid']} exited {-c['dt_ms']:.0f} ms before the burn-in spawned"
+    if exits:
+        c = exits[-1]
+        return f"this bring-up's KFD process {c['pid']} exited {-c['dt_ms']:.0f} ms before the burn-in spawned"
+    starts = [c for c in ch if c["what"] == "start" and not c["own"]]
+    if starts:
+        c = starts[0]
+        return f"foreign KFD process {c['pid']} started {c['dt_ms']:+.0f} ms around the burn-in spawn"
+    late_exits = [c for c in ch if c["what"] == "exit"]
+    if late_exits:
+        c = late_exits[0]
+        return f"KFD process {c['pid']} exited {c['dt_ms']:.0f} ms into the burn-in's runtime start"
+    return "no KFD process change within 0.3 s before or during the start (driver-internal)"
+
+
+def one_bringup(ws: Path, n: int, args, env: dict, log, census: KfdCensus | None = None) -> dict:
     answers = {"nodes": n, "package": args.package, "name": "k8s bench", "confirm": "yes"}
     (ws / "answers.json").write_text(json.dumps(answers))
     cmd = ["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", str(_free_port()),
@@ -178,46 +275,68 @@ def one_bringup(ws: Path, n: int, args, env: dict, log) -> dict:
         cmd += ["--rccl", args.rccl]
     import threading
 
+    census = census or KfdCensus()
     t0 = time.perf_counter()
     launched_unix = time.time()
     p = subprocess.Popen(cmd, cwd=ws, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, bufsize=1,
                          start_new_session=True)
     lines: list[str] = []
     ready_at: list[float] = []
+    eof_at: list[float] = []
 
     def reader():  # stream: the READY line is timestamped as it is printed
         for line in p.stdout:
             if not ready_at and line.startswith("ALL NODES READY"):
                 ready_at.append(time.perf_counter() - t0)
+                census.stop()
             lines.append(line)
+        eof_at.append(time.perf_counter() - t0)
 
     th = threading.Thread(target=reader, name="setup-stdout", daemon=True)
     th.start()
-    try:  # the bound holds even when setup.sh hangs without printing anything
-        rc = p.wait(timeout=args.timeout + 120)
-    except subprocess.TimeoutExpired:
+    killed: list[bool] = []
+
+    def watchdog():  # the bound holds even when setup.sh hangs without printing anything
+        killed.append(True)
         try:
             os.killpg(p.pid, 9)
         except OSError:
             pass
+
+    # a blocking wait (waitpid), with the bound on a timer: Popen.wait(timeout=...) polls with a
+    # backoff capped at 50 ms, which quantised every step's time
+    dog = threading.Timer(args.timeout + 120, watchdog)
+    dog.daemon = True
+    dog.start()
+    try:
         rc = p.wait()
-        lines.append(f"\n[bench] ./setup.sh killed after {args.timeout + 120:.0f}s\n")
-    th.join(10)
-    t_ready = ready_at[0] if ready_at else None
+    finally:
+        dog.cancel()
     wall = time.perf_counter() - t0
+    census.stop()
+    th.join(10)
+    if killed:
+        lines.append(f"\n[bench] ./setup.sh killed after {args.timeout + 120:.0f}s\n")
+    t_ready = ready_at[0] if ready_at else None
     out = "".join(lines)
     log.write(out)
     log.flush()
     if t_ready is None:
         raise RuntimeError(f"./setup.sh exited {rc} before every node was Ready:\n{out[-3000:]}")
+    post_ready = (eof_at[0] if eof_at else wall) - t_ready
     if rc != 0:
         # Ready was reached (the metric); what failed afterwards is the RCCL fabric check. Keep
         # the measurement and report the failure instead of dropping the whole step.
-        return {"wall_seconds": wall, "ready_wall_seconds": t_ready, "phases": {},
+        return {"wall_seconds": wall, "ready_wall_seconds": t_ready, "post_ready_seconds": post_ready, "phases": {},
                 "post_ready_error": f"exit {rc}: " + out.strip()[-1500:]}
     summary = json.loads(out.strip().splitlines()[-1])
     summary["wall_seconds"] = wall
     summary["ready_wall_seconds"] = t_ready
+    summary["post_ready_seconds"] = post_ready
+    hb = summary.get("host_burnin") or {}
+    own = {str(x) for x in (hb.get("pid"), hb.get("kfd_pid")) if x}
+    summary["kfd_census"] = census.report(hb.get("spawned_unix"), own)
+    summary["slow_start_cause"] = slow_start_cause(summary["kfd_census"], hb.get("runtime_init_ms"))
     hb = summary.get("host_burnin") or {}
     spawned = hb.get("spawned_unix")
     if spawned:  # how long after the launch of ./setup.sh the GPU burn-in process started
@@ -286,7 +405,9 @@ def main(argv=None) -> int:
     log = open(args.log, "a") if (args.log and d.rank == 0) else open(os.devnull, "w")
     b2b = args.back_to_back if args.back_to_back is not None else (0 if fake else 2)
     b2b_ready: list[float] = []
+    cold: dict | None = None
     total = args.warmup + args.steps
+    census = KfdCensus().start() if d.rank == 0 else None
     try:
         for i in range(total + b2b):
             timed = args.warmup <= i < total
@@ -298,8 +419,16 @@ def main(argv=None) -> int:
             t0 = time.perf_counter()
             s = None
             if d.rank == 0 and err is None:
+                step_env = env
+                if i == 0 and args.warmup > 0:
+                    # the first step runs cold: empty byte-code and parse caches, i.e. a user's
+                    # first ./setup.sh on a fresh install
+                    step_env = dict(env, PYTHONPYCACHEPREFIX=str(root / "cold-pycache"),
+                                    TK8S_YAML_CACHE=str(root / "cold-cache"))
                 try:
-                    s = one_bringup(ws, n, args, env, log)
+                    s = one_bringup(ws, n, args, step_env, log, census)
+                    if i == 0 and args.warmup > 0:
+                        cold = s
                 except Exception as e:  # noqa: BLE001 - reported after the collective
                     err = str(e)
             d.sync()
@@ -315,6 +444,9 @@ def main(argv=None) -> int:
                     if err is None:
                         err = str(e)
                 shutil.rmtree(ws, ignore_errors=True)
+                if census is not None:
+                    census.stop()
+                census = KfdCensus().start()  # the next step's census starts before its settle pause
                 if settle > 0 and i + 1 < total:  # no pause before the back-to-back steps / between them
                     time.sleep(settle)
             err = d.bcast_obj(err)
@@ -333,6 +465,8 @@ def main(argv=None) -> int:
                 kind = "timed" if timed else "back-to-back" if extra else "warmup"
                 print(f"[bench] step {i} ({kind}): {dt:.3f}s", file=sys.stderr, flush=True)
     finally:
+        if census is not None:
+            census.stop()
         log.close()
         if d.rank == 0 and not args.workdir:
             shutil.rmtree(root, ignore_errors=True)
@@ -389,6 +523,13 @@ def main(argv=None) -> int:
         "median_s": round(sorted(ready_times)[len(ready_times) // 2] if len(ready_times) % 2
                           else sum(sorted(ready_times)[len(ready_times) // 2 - 1:len(ready_times) // 2 + 1]) / 2, 4),
         "setup_process_s": round(step_mean, 4),
+        # from the Ready line to ./setup.sh's exit (the RCCL fabric check, the summary): with
+        # value, what ms_per_step is made of
+        "post_ready_s": round(sum(s.get("post_ready_seconds", 0.0) for s in summaries) / len(summaries), 4)
+        if summaries else None,
+        "cold_first_run_s": round(cold["ready_wall_seconds"], 4) if cold else None,
+        "cold_first_run_what": "step 0 (a warmup step) with empty byte-code and parse caches: a first "
+                               "./setup.sh on a fresh install" if cold else None,
         "rccl_check_s": round(sum(s.get("phases", {}).get("rccl", 0.0) for s in summaries) / len(summaries), 4)
         if summaries else None,
         "ready_s_inside_setup": round(sum(ready) / len(ready), 4) if ready else None,
@@ -411,6 +552,10 @@ def main(argv=None) -> int:
         "burnin_spawn_ms_steps": [s.get("burnin_spawn_ms") for s in summaries],
         "burnin_exec_ms_steps": [s.get("burnin_exec_ms") for s in summaries],
         "burnin_notice_ms_steps": [s.get("burnin_notice_ms") for s in summaries],
+        # every timed step whose runtime start took > 50 ms, with what the KFD process census saw
+        "slow_start_cause": {str(args.warmup + i): s["slow_start_cause"] for i, s in enumerate(summaries)
+                             if s.get("slow_start_cause")},
+        "kfd_census_available": any((s.get("kfd_census") or {}).get("available") for s in summaries),
     }
     if b2b_ready:
         out["back_to_back"] = {"steps": len(b2b_ready), "mean_s": round(sum(b2b_ready) / len(b2b_ready), 4),

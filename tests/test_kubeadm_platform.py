@@ -25,11 +25,13 @@ from tritonk8ssupervisor_amd.playbook import Playbook
 
 REPO = Path(__file__).resolve().parents[1]
 GOLDEN = REPO / "tests" / "golden" / "kubeadm_check.jsonl"
+GOLDEN_SINGLE = REPO / "tests" / "golden" / "kubeadm_check_single.jsonl"
 ROLES = ("k8sruntime", "kubeadmmaster", "kubeadmhost", "kubeadmvalidate")
 BUILTIN = {"apt", "apt_repository", "get_url", "file", "copy", "command", "shell", "stat", "assert", "replace",
            "systemd_service", "fetch", "lineinfile", "uri", "wait_for", "set_fact", "debug", "slurp"}
 TASK_KEYS = {"name", "register", "when", "until", "retries", "delay", "run_once", "delegate_to", "changed_when",
-             "failed_when", "args", "local_action", "become", "notify", "ignore_errors", "loop", "with_items"}
+             "failed_when", "args", "local_action", "become", "notify", "ignore_errors", "loop", "with_items",
+             "no_log"}
 
 
 def _tasks(role):
@@ -38,7 +40,7 @@ def _tasks(role):
 
 def test_every_task_is_a_core_ansible_module():
     plays = yaml.safe_load((REPO / "ansible" / "clusterUp-kubeadm.yml").read_text())
-    assert [p["roles"] for p in plays] == [[r] for r in ROLES]
+    assert [[r if isinstance(r, str) else r["role"] for r in p["roles"]] for p in plays] == [[r] for r in ROLES]
     for role in ROLES:
         for t in _tasks(role):
             mods = [k for k in t if k not in TASK_KEYS]
@@ -51,24 +53,29 @@ def test_every_task_is_a_core_ansible_module():
             assert t.get("name"), t  # every task says what it does
 
 
-def _inventory(tmp: Path) -> Path:
+def _inventory(tmp: Path, single: bool = False) -> Path:
     inv = tmp / "hosts"
-    inv.write_text("[MASTER]\nkubemaster ansible_host=10.20.0.1 tk8s_home=/home/ops/.tk8s/dist/0123456789abcdef\n"
-                   "[HOST]\nkubenode1 ansible_host=10.20.0.2 tk8s_home=/home/ops/.tk8s/dist/0123456789abcdef\n"
-                   "kubenode2 ansible_host=10.20.0.3 tk8s_home=/home/ops/.tk8s/dist/0123456789abcdef\n")
+    home = "tk8s_home=/home/ops/.tk8s/dist/0123456789abcdef"
+    if single:  # one host: the master machine and the GPU slots share its address
+        inv.write_text(f"[MASTER]\nkubemaster ansible_host=10.20.0.1 {home}\n"
+                       + "[HOST]\n" + "".join(f"kubenode{i} ansible_host=10.20.0.1 {home}\n" for i in range(1, 9)))
+        return inv
+    inv.write_text(f"[MASTER]\nkubemaster ansible_host=10.20.0.1 {home}\n"
+                   f"[HOST]\nkubenode1 ansible_host=10.20.0.2 {home}\n"
+                   f"kubenode2 ansible_host=10.20.0.3 {home}\n")
     return inv
 
 
-def _check_run(tmp_path: Path) -> Playbook:
+def _check_run(tmp_path: Path, single: bool = False) -> Playbook:
     from tritonk8ssupervisor_amd.orchestrator import init_workspace
 
     ws = init_workspace(tmp_path / "ws")
     ws.vars_file.write_text('master: 10.20.0.1\nkubernetes_name: "k8s dev"\nkubernetes_description: "k8s dev"\n')
     facts = {"ansible_kernel": "6.8.0-45-generic", "ansible_distribution_release": "jammy",
              "ansible_distribution": "Ubuntu", "ansible_architecture": "x86_64"}
-    pb = Playbook(ws.ansible / "clusterUp-kubeadm.yml", _inventory(tmp_path), check=True, out=None,
-                  extra_vars={**facts, "tk8s_manifests": "MANIFESTS", "tk8s_expected_gpus": 2, "tk8s_gpus_per_node": 1,
-                              "tk8s_ready_timeout": 900})
+    pb = Playbook(ws.ansible / "clusterUp-kubeadm.yml", _inventory(tmp_path, single), check=True, out=None,
+                  extra_vars={**facts, "tk8s_manifests": "MANIFESTS", "tk8s_expected_gpus": 8 if single else 2,
+                              "tk8s_gpus_per_node": 1, "tk8s_ready_timeout": 900, "tk8s_single_node": single})
     # the manifests are rendered from the repository's copy, their path is not part of the golden
     pb.extra_vars["tk8s_manifests"] = str(ws.manifests)
     res = pb.run()
@@ -86,13 +93,15 @@ def _normal(pb: Playbook, tmp_path: Path) -> list[dict]:
     return out
 
 
-def test_check_mode_renders_the_golden_plan(tmp_path):
-    pb = _check_run(tmp_path)
+@pytest.mark.parametrize("single", [False, True], ids=["multi-host", "single-node"])
+def test_check_mode_renders_the_golden_plan(tmp_path, single):
+    pb = _check_run(tmp_path, single)
     got = _normal(pb, tmp_path)
+    golden = GOLDEN_SINGLE if single else GOLDEN
     if os.environ.get("TK8S_REGOLDEN") == "1":
-        GOLDEN.parent.mkdir(parents=True, exist_ok=True)
-        GOLDEN.write_text("".join(json.dumps(t, sort_keys=True) + "\n" for t in got))
-    want = [json.loads(x) for x in GOLDEN.read_text().splitlines()]
+        golden.parent.mkdir(parents=True, exist_ok=True)
+        golden.write_text("".join(json.dumps(t, sort_keys=True) + "\n" for t in got))
+    want = [json.loads(x) for x in golden.read_text().splitlines()]
     assert len(got) == len(want)
     for g, w in zip(got, want):
         assert g == w, (g["task"], g["host"])
@@ -112,13 +121,37 @@ def test_check_mode_plan_content(tmp_path):
                                                           "(amdgpu-dkms builds against them)")]["args"]["name"]
     assert ("kubemaster", "GPU hosts - amdgpu-dkms, the HIP runtime, RCCL and AMD SMI") not in by  # no GPU driver
     repo = by[("kubenode1", "ROCm repository")]["args"]["repo"]
-    assert repo.endswith("https://repo.radeon.com/rocm/apt/7.0 jammy main")
+    assert repo.endswith("https://repo.radeon.com/rocm/apt/7.2 jammy main")
     init = by[("kubemaster", "kubeadm init (etcd, kube-apiserver, kube-scheduler, kube-controller-manager)")]["args"]
     assert "--apiserver-advertise-address 10.20.0.1" in init["cmd"] and init["creates"] == "/etc/kubernetes/admin.conf"
     dp = by[("kubemaster", "AMD GPU device plugin manifest (amd.com/gpu on every MI355X node)")]["args"]["content"]
-    assert "image: docker.io/rocm/k8s-device-plugin:latest" in dp and "/var/lib/kubelet/device-plugins" in dp
-    assert by[("kubenode1", "The node's tk8s tools at a fixed path (hostPath of the RCCL-tests DaemonSet)")][
+    assert "image: docker.io/rocm/k8s-device-plugin:1.31.0.6" in dp and "/var/lib/kubelet/device-plugins" in dp
+    # the dashboard is deployed and every image / manifest is pinned
+    assert by[("kubemaster", "Kubernetes dashboard")]["args"]["_raw_params"].endswith(
+        "kubernetes/dashboard/v2.7.0/aio/deploy/recommended.yaml")
+    access = by[("kubemaster", "Dashboard access objects manifest (NodePort service, admin service account)")]
+    assert "nodePort: 30443" in access["args"]["content"] and "name: cluster-admin" in access["args"]["content"]
+    assert not [x for x in t if ":latest" in json.dumps(x["args"]) or "releases/latest" in json.dumps(x["args"])]
+    # Ready stops at the nodes and their GPUs: the RCCL-tests Job runs after ALL NODES READY (fabric.py)
+    assert not [x for x in t if "rccl" in json.dumps(x["args"]).lower() and x["play"].startswith("Every node")]
+    assert by[("kubenode1", "The node's tk8s tools at a fixed path (hostPath of the RCCL-tests Job)")][
         "args"]["src"] == "/home/ops/.tk8s/dist/0123456789abcdef"
+
+
+def test_single_node_check_plan(tmp_path):
+    """one host carries the control plane and the GPU worker. Only the master machine
+    installs the runtime; its taint is removed; no machine joins; the master's node is the GPU node."""
+    t = _normal(_check_run(tmp_path, single=True), tmp_path)
+    hosts = {x["host"] for x in t}
+    assert hosts == {"kubemaster"}, hosts  # the GPU slots run nothing
+    names = [x["task"] for x in t]
+    assert "GPU hosts - amdgpu-dkms, the HIP runtime, RCCL and AMD SMI" in names
+    untaint = next(x for x in t if x["task"].startswith("Single-node cluster"))
+    assert untaint["args"]["_raw_params"].endswith("taint nodes kubemaster node-role.kubernetes.io/control-plane:NoSchedule-")
+    assert not any(x["task"].startswith("kubeadm join") for x in t)
+    assert not any(x["task"].startswith("Join command") for x in t)
+    label = next(x for x in t if x["task"].startswith("Label the GPU nodes"))
+    assert "label node kubemaster amd.com/gpu.family=gfx950" in label["args"]["_raw_params"]
 
 
 def test_kubeadm_refused_on_colocated_sandboxes(tmp_path, monkeypatch):
@@ -164,14 +197,14 @@ FAKE_TOOLS = ("apt-get", "apt-mark", "dpkg-query", "modprobe", "sysctl", "swapof
               "kubeadm", "kubectl")
 
 
-def _fake_root_host(root: Path, addr: str, pubkey: str, state: Path) -> Path:
+def _fake_root_host(root: Path, addr: str, pubkey: str, state: Path, gpus: int = 0) -> Path:
     import sys
 
     h = root / addr
     (h / ".ssh").mkdir(parents=True)
     (h / ".ssh" / "authorized_keys").write_text(pubkey)
     (h / ".fakeroot").touch()
-    (h / ".env").write_text(f"FAKE_K8S_STATE={state}\n")
+    (h / ".env").write_text(f"FAKE_K8S_STATE={state}\nFAKE_HOST_GPUS={gpus}\n")
     (h / "sysroot" / "etc").mkdir(parents=True)
     (h / "sysroot" / "etc" / "fstab").write_text("/dev/sda1 / ext4 defaults 0 1\n/swap.img none swap sw 0 0\n")
     b = h / "bin"
@@ -214,8 +247,8 @@ def test_kubeadm_platform_end_to_end_against_simulated_tools(tmp_path):
     root = tmp_path / "hosts"
     state = tmp_path / "cluster.json"
     hosts = {"mi355x-a": "127.0.7.30", "mi355x-b": "127.0.7.31", "mi355x-c": "127.0.7.32"}
-    for addr in hosts.values():
-        _fake_root_host(root, addr, (keydir / "id_ed25519.pub").read_text(), state)
+    for h, addr in hosts.items():
+        _fake_root_host(root, addr, (keydir / "id_ed25519.pub").read_text(), state, gpus=0 if h == "mi355x-a" else 1)
     inv = {"ssh": {"user": "root", "key": str(keydir / "id_ed25519")}, "python": sys.executable,
            "hosts": [{"name": "mi355x-a", "address": hosts["mi355x-a"], "gpus": 0, "role": "master"},
                      {"name": "mi355x-b", "address": hosts["mi355x-b"], "gpus": 1},
@@ -223,7 +256,7 @@ def test_kubeadm_platform_end_to_end_against_simulated_tools(tmp_path):
     (ws / "inventory.yml").write_text(json.dumps(inv))
     env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_BACKEND="baremetal",
                TK8S_SSH=f"{sys.executable} {REPO / 'tests' / 'fakessh.py'}", FAKESSH_ROOT=str(root),
-               TK8S_SSH_CONNECT_RETRIES="0")
+               TK8S_SSH_CONNECT_RETRIES="0", TK8S_RCCL_POLL="0.05")
     env.pop("TK8S_FAKE_GPUS", None)
     r = subprocess.run(["./setup.sh", "--platform", "kubeadm", "--yes", "--json", "--nodes", "2", "--timeout", "60"],
                        cwd=ws, env=env, capture_output=True, text=True, timeout=300)
@@ -231,7 +264,7 @@ def test_kubeadm_platform_end_to_end_against_simulated_tools(tmp_path):
         assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
         s = json.loads(r.stdout.strip().splitlines()[-1])
         assert s["platform"] == "kubeadm" and s["nodes"] == 2 and s["gpus_allocatable"] == 2
-        assert s["rccl"]["ok"] and len(s["rccl"]["pods"]) == 2
+        assert s["rccl"]["ok"] and s["rccl"]["pods"] == 2 and s["rccl"]["platform"] == "kubeadm"
         assert s["api"] == f"https://{hosts['mi355x-a']}:6443"
         assert (ws / "ansible" / "tmp" / "kubeconfig").read_text().startswith("apiVersion: v1")
         assert (ws / "ansible" / "tmp" / "kubernetes_environment.id").read_text() == json.loads(state.read_text())["uid"]
@@ -270,3 +303,158 @@ def test_kubeadm_platform_end_to_end_against_simulated_tools(tmp_path):
     assert c.returncode == 0 and "kubeadm reset on kubenode1: ok" in c.stdout, c.stdout + c.stderr
     for h in ("mi355x-b", "mi355x-c"):
         assert not (root / hosts[h] / "sysroot" / "etc" / "kubernetes" / "kubelet.conf").exists()
+
+
+def _kubeadm_env(tmp_path: Path, hosts: dict[str, tuple[str, int]], state: Path, scenario: dict | None = None):
+    """A workspace, fake-root hosts ({name: (address, gpus)}) and the env to run ./setup.sh
+    --backend baremetal --platform kubeadm against them."""
+    import subprocess
+    import sys
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    ws = tmp_path / "ws"
+    ws.mkdir()
+    init_workspace(ws)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, ws / f)
+    gv = ws / "ansible" / "group_vars" / "all.yml"
+    gv.write_text(gv.read_text().replace('tk8s_sysroot: ""', 'tk8s_sysroot: "{{ ansible_env.HOME }}/sysroot"'))
+    keydir = tmp_path / "keys"
+    keydir.mkdir()
+    subprocess.run(["ssh-keygen", "-q", "-t", "ed25519", "-N", "", "-f", str(keydir / "id_ed25519")], check=True)
+    root = tmp_path / "hosts"
+    for addr, gpus in hosts.values():
+        _fake_root_host(root, addr, (keydir / "id_ed25519.pub").read_text(), state, gpus=gpus)
+    if scenario is not None:
+        state.write_text(json.dumps({"nodes": {}, "objects": [], "uid": "", "master": "", "rccl_scenario": scenario}))
+    inv = {"ssh": {"user": "root", "key": str(keydir / "id_ed25519")}, "python": sys.executable,
+           "hosts": [{"name": n, "address": a, "gpus": g, **({"role": "master"} if i == 0 else {})}
+                     for i, (n, (a, g)) in enumerate(hosts.items())]}
+    (ws / "inventory.yml").write_text(json.dumps(inv))
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_BACKEND="baremetal",
+               TK8S_SSH=f"{sys.executable} {REPO / 'tests' / 'fakessh.py'}", FAKESSH_ROOT=str(root),
+               TK8S_SSH_CONNECT_RETRIES="0", TK8S_RCCL_POLL="0.05")
+    env.pop("TK8S_FAKE_GPUS", None)
+    return ws, root, env
+
+
+def _fake_kubectl(host_dir: Path, state: Path, *args) -> "subprocess.CompletedProcess":
+    import subprocess
+    import sys
+
+    env = dict(os.environ, TK8S_SYSROOT=str(host_dir / "sysroot"), FAKE_K8S_STATE=str(state), FAKETOOL_NAME="kubectl")
+    return subprocess.run([sys.executable, str(REPO / "tests" / "fakeroot" / "faketool.py"), *args], env=env,
+                          capture_output=True, text=True, timeout=60)
+
+
+def test_kubeadm_single_node_on_one_8gpu_host(tmp_path):
+    """VERDICT r2 #1: ./setup.sh --platform kubeadm with a ONE-host inventory (the 8x MI355X box):
+    kubeadm init on that host, its control-plane taint removed, 8 amd.com/gpu on its one node, the
+    8 workers are GPU slots of it; the RCCL-tests Job leaves every GPU schedulable; -c resets it."""
+    import subprocess
+
+    state = tmp_path / "cluster.json"
+    ws, root, env = _kubeadm_env(tmp_path, {"mi355x": ("127.0.7.40", 8)}, state)
+    r = subprocess.run(["./setup.sh", "--platform", "kubeadm", "--yes", "--json", "--nodes", "8", "--timeout", "60"],
+                       cwd=ws, env=env, capture_output=True, text=True, timeout=300)
+    host = root / "127.0.7.40"
+    try:
+        assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["single_node"] is True and s["nodes"] == 8 and s["kubernetes_nodes"] == 1
+        assert s["gpus_allocatable"] == 8 and s["nodes_validated"] == 1
+        assert "ALL NODES READY: 1 node(s) (single-node: kubemaster is control plane and GPU worker, 8 worker slot(s)), " \
+               "8 x amd.com/gpu allocatable" in r.stdout
+        nodes = json.loads(state.read_text())["nodes"]
+        assert list(nodes) == ["kubemaster"] and nodes["kubemaster"]["gpus"] == 8
+        assert nodes["kubemaster"]["taints"] == [] and nodes["kubemaster"]["labels"]["amd.com/gpu.family"] == "gfx950"
+        # the fabric check ran after Ready: one Job, one pod, all 8 GPUs, then the GPUs are free again
+        assert s["rccl"]["ok"] and s["rccl"]["pods"] == 1 and s["rccl"]["nranks"] == 8 and s["rccl"]["gpus_per_pod"] == 8
+        assert r.stdout.index("ALL NODES READY") < r.stdout.index("Running RCCL all-reduce on 1 GPU node(s)")
+        assert s["rccl_check_s"] > 0 and s["ready_seconds"] < s["total_seconds"]
+        pod = tmp_path / "gpu-pod.yaml"
+        pod.write_text(yaml.safe_dump({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "hello-gpu"},
+                                       "spec": {"containers": [{"name": "c", "image": "rocm/dev-ubuntu-22.04:7.2",
+                                                                "resources": {"limits": {"amd.com/gpu": 1}}}]}}))
+        assert _fake_kubectl(host, state, "apply", "-f", str(pod)).returncode == 0
+        got = json.loads(_fake_kubectl(host, state, "get", "pod", "hello-gpu", "-o", "json").stdout)
+        assert got["status"]["phase"] == "Running" and got["spec"]["nodeName"] == "kubemaster"
+        # the reference's deliverables: dashboard URL + kubectl config
+        assert s["dashboard"] == "https://127.0.7.40:30443/" and "Kubernetes dashboard is at https://127.0.7.40:30443/" in r.stdout
+        assert (ws / "ansible" / "tmp" / "dashboard-token").read_text().startswith("eyJ")
+        assert f"Kubernetes CLI config is at {ws / 'ansible' / 'tmp' / 'kubeconfig'}" in r.stdout
+        log = (host / "sysroot" / "var" / "log" / "fake-tools.log").read_text()
+        assert log.count("kubeadm init") == 1 and "kubeadm join" not in log
+        # the node runtime went in once (play 1 on the master machine only), not once per GPU slot
+        assert sum(ln.startswith("apt-get") and "amdgpu-dkms" in ln for ln in log.splitlines()) == 1, log
+        assert "taint nodes kubemaster node-role.kubernetes.io/control-plane:NoSchedule-" in log
+        # the GPU slots are machines of the one host, each with one of its GPUs
+        alloc = json.loads((ws / ".tk8s" / "baremetal-alloc.json").read_text())["machines"]
+        assert sorted(g for m, rec in alloc.items() if m != "kubemaster" for g in rec["gpus"]) == list(range(8))
+    finally:
+        c = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, text=True, timeout=120)
+    assert c.returncode == 0, c.stdout + c.stderr
+    assert c.stdout.count("kubeadm reset on ") == 1 and "kubeadm reset on kubemaster: ok" in c.stdout
+    assert not (host / "sysroot" / "etc" / "kubernetes" / "admin.conf").exists()
+
+
+def test_rccl_job_verdict_states():
+    """VERDICT r2 #2: the wait needs exactly one successfully terminated pod per GPU node."""
+    from tritonk8ssupervisor_amd.kubeadm_platform import rccl_job_verdict
+
+    jobs = {"n1": "j-0", "n2": "j-1"}
+
+    def pod(job, phase, code=None, name=None):
+        st = {"phase": phase}
+        if code is not None:
+            st["containerStatuses"] = [{"state": {"terminated": {"exitCode": code, "reason": "Error" if code else "Completed"}}}]
+        return {"metadata": {"name": name or f"{job}-x", "labels": {"job-name": job}}, "status": st}
+
+    assert rccl_job_verdict([], jobs)["state"] == "waiting"  # no pods yet: still waiting
+    v = rccl_job_verdict([pod("j-0", "Pending"), pod("j-1", "Pending")], jobs)
+    assert v["state"] == "waiting" and "n1: pod j-0-x Pending" in v["reason"]
+    assert rccl_job_verdict([pod("j-0", "Succeeded", 0)], jobs)["state"] == "waiting"  # n2 has none
+    v = rccl_job_verdict([pod("j-0", "Succeeded", 0), pod("j-1", "Failed", 1)], jobs)
+    assert v["state"] == "failed" and "n2: pod j-1-x failed (Error, exit code 1)" in v["reason"]
+    v = rccl_job_verdict([pod("j-0", "Succeeded", 0), pod("j-1", "Succeeded", 0)], jobs)
+    assert v["state"] == "done" and v["pods"] == {"n1": "j-0-x", "n2": "j-1-x"}
+    v = rccl_job_verdict([pod("j-0", "Succeeded", 0), pod("j-0", "Running", name="j-0-y"), pod("j-1", "Succeeded", 0)], jobs)
+    assert v["state"] == "failed" and "2 pods" in v["reason"]
+
+
+def test_kubeadm_rccl_failure_fails_setup(tmp_path):
+    """VERDICT r2 #2: one node's RCCL pod failing fails ./setup.sh (exit != 0, with the reason), after
+    the ALL NODES READY line -- and no Congratulations."""
+    import subprocess
+
+    state = tmp_path / "cluster.json"
+    ws, root, env = _kubeadm_env(tmp_path, {"mi355x-a": ("127.0.7.50", 0), "mi355x-b": ("127.0.7.51", 1),
+                                            "mi355x-c": ("127.0.7.52", 1)}, state,
+                                 scenario={"pending_polls": 2, "fail": ["kubenode2"]})
+    r = subprocess.run(["./setup.sh", "--platform", "kubeadm", "--yes", "--json", "--nodes", "2", "--timeout", "60"],
+                       cwd=ws, env=env, capture_output=True, text=True, timeout=300)
+    try:
+        assert r.returncode == 2, r.stdout[-3000:] + r.stderr[-2000:]
+        assert "ALL NODES READY: 2 node(s), 2 x amd.com/gpu allocatable" in r.stdout
+        assert "RCCL all-reduce validation failed: kubenode2: pod" in r.stderr and "exit code 1" in r.stderr
+        assert "Congratulations" not in r.stdout
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, text=True, timeout=120)
+
+
+def test_both_platforms_report_ready_and_rccl_alike():
+    """VERDICT r2 #7: 'Ready' means the same on both platforms -- the summaries carry ready_seconds
+    (to the ALL NODES READY line, before the fabric check) and rccl / rccl_check_s (after it)."""
+    import inspect
+
+    from tritonk8ssupervisor_amd import kubeadm_platform, orchestrator
+
+    for src in (inspect.getsource(orchestrator.Setup.run), inspect.getsource(kubeadm_platform.KubeadmPlatform._kubeadm_finish)):
+        for key in ('"ready_seconds"', '"rccl_check_s"', '"rccl"', '"total_seconds"'):
+            assert key in src, key
+    run = inspect.getsource(orchestrator.Setup.run)
+    assert run.index("self.ready_line(") < run.index("self.run_rccl()") < run.index("_kubeadm_finish")
+    # the kubeadm playbook's last play waits for nodes + GPUs only; no RCCL object is created in it
+    role = (REPO / "ansible" / "roles" / "kubeadmvalidate" / "tasks" / "main.yml").read_text()
+    assert "rccl-tests" not in role.split("\n- name:", 1)[1].lower().replace("rccl-tests select", "")

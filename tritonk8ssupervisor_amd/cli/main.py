@@ -138,7 +138,7 @@ def cmd_status(args) -> int:
         if r.get("peak_busbw_gbps") is not None:
             print(f"last RCCL all-reduce: peak busbw {r['peak_busbw_gbps']:.1f} GB/s over {r['nranks']} GPU(s)")
         elif r:
-            print(f"RCCL-tests DaemonSet: {'ok' if r.get('ok') else 'FAILED'} on {len(r.get('pods', []))} node(s)")
+            print(f"RCCL all-reduce: {'ok' if r.get('ok') else 'FAILED'} on {r.get('pods')} pod(s)")
     return 0
 
 

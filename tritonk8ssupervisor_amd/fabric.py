@@ -36,12 +36,8 @@ class FabricCheck:
         from .controlplane.client import client_from_kubeconfig
         from .kube import apply_objects, load_manifests, pods_of, wait_job
 
-        if self.platform == "kubeadm":  # the RCCL-tests DaemonSet ran in the kubeadmvalidate role
-            pr = getattr(self, "playbook_result", None)
-            reg = ((pr.hostvars if pr else {}).get(self.cfg.RANCHER_MASTER_HOSTNAME) or {}).get("rccl_pods") or {}
-            lines = reg.get("stdout_lines") or []
-            return {"ok": bool(lines) and all(ln.split()[-1] == "true" for ln in lines if ln.strip()),
-                    "daemonset": "kube-system/tk8s-rccl-tests", "pods": lines} if lines else None
+        if self.platform == "kubeadm":  # one RCCL-tests Job per GPU node (kubeadm_platform.py)
+            return self.kubeadm_rccl()
 
         g = self.expected_gpus()
         enabled = self.rccl if self.rccl is not None else g >= 2

@@ -154,7 +154,9 @@ class Setup(KubeadmPlatform, FabricCheck):
             raise SetupError("error: the kubeadm platform installs ROCm, amdgpu-dkms, containerd and Kubernetes as root on "
                              "its machines: use machines you own (--backend baremetal with an SSH inventory, or triton)")
         if self.platform == "kubeadm" and hasattr(self.provider, "whole_hosts"):
-            self.provider.whole_hosts = True  # a kubelet per host: machines are whole hosts, not slices
+            # a kubelet per host: machines are whole hosts, not slices -- except on a one-host
+            # inventory (single-node mode), where the workers are GPU slots of the master's node
+            self.provider.whole_hosts = not self.kubeadm_single_node
         return cfg
 
     def _machine_booted(self, address: str, m: Machine) -> None:
@@ -502,8 +504,7 @@ class Setup(KubeadmPlatform, FabricCheck):
         t_ready = time.monotonic() - t0
         # One greppable line the moment every node is Ready (bench.py timestamps it): the RCCL
         # fabric check that follows is reported on its own, it is not part of "all nodes Ready".
-        self.out(f"ALL NODES READY: {ready.get('nodes_ready', 0)} node(s), "
-                 f"{ready.get('gpus_allocatable', 0)} x amd.com/gpu allocatable after {t_ready:.3f}s")
+        self.out(self.ready_line(ready, t_ready))
         rccl = None
         with self.events.phase("rccl"):
             rccl = self.run_rccl()
@@ -525,7 +526,8 @@ class Setup(KubeadmPlatform, FabricCheck):
         except Exception:  # noqa: BLE001 - reporting only
             pass
         self.summary = {
-            "ready_seconds": round(t_ready, 4), "total_seconds": round(total, 4), "validation": validation,
+            "platform": "tk8s", "ready_seconds": round(t_ready, 4), "total_seconds": round(total, 4),
+            "rccl_check_s": round(self.events.phases.get("rccl", 0.0), 4), "validation": validation,
             "nodes": int(self.cfg.KUBERNETES_NUMBER_OF_NODES), "gpus_allocatable": ready.get("gpus_allocatable", 0),
             "nodes_validated": ready.get("nodes_validated", 0), "rccl": rccl,
             "phases": {k: round(v, 4) for k, v in self.events.phases.items()},
@@ -536,6 +538,7 @@ class Setup(KubeadmPlatform, FabricCheck):
         if hb is not None and hb.done:
             t = (hb.result or {}).get("timings_ms") or {}
             self.summary["host_burnin"] = {"gpus": hb.gpus, "ok": bool(hb.result and hb.result.get("ok")),
+                                           "pid": getattr(getattr(hb, "proc", None), "pid", None),
                                            "runtime_init_ms": t.get("runtime_init", t.get("hip_init")),
                                            "peers_ms": t.get("peers"), "total_ms": t.get("total"),
                                            "spawned_unix": hb.spawned_unix or None,
@@ -578,7 +581,7 @@ class Setup(KubeadmPlatform, FabricCheck):
         self.cfg = cfg
         self.platform = cfg.TK8S_PLATFORM or "tk8s"
         if self.platform == "kubeadm" and hasattr(self.provider, "whole_hosts"):
-            self.provider.whole_hosts = True
+            self.provider.whole_hosts = not self.kubeadm_single_node
         old = int(cfg.KUBERNETES_NUMBER_OF_NODES)
         if int(n) == old:
             self.out(f"{old} node(s) already; nothing to do")
@@ -601,8 +604,7 @@ class Setup(KubeadmPlatform, FabricCheck):
                 fn()
         with self.events.phase("ready"):
             ready = self.wait_ready()
-        self.out(f"ALL NODES READY: {ready.get('nodes_ready', 0)} node(s), "
-                 f"{ready.get('gpus_allocatable', 0)} x amd.com/gpu allocatable after {time.monotonic() - t0:.3f}s")
+        self.out(self.ready_line(ready, time.monotonic() - t0))
         rccl = None
         if self.rccl:
             with self.events.phase("rccl"):
@@ -622,6 +624,10 @@ class Setup(KubeadmPlatform, FabricCheck):
     def _drain_and_delete(self, names: list[str]) -> None:
         from .controlplane.client import ApiError, client_from_kubeconfig
 
+        if self.kubeadm_single_node:  # GPU slots of the master's node: no Kubernetes node to drain
+            for node in names:
+                self.out(f"    slot {node} released (single-node: its GPUs stay on {self.cfg.RANCHER_MASTER_HOSTNAME})")
+            return
         if self.platform == "kubeadm":  # a real Kubernetes: kubectl drain on the master, kubeadm reset on the node
             machines = self.engine.machines()
             for node in names:

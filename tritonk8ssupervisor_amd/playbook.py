@@ -272,7 +272,14 @@ class Playbook:
                 dfile = self.dir / "roles" / rname / "defaults" / "main.yml"
                 if dfile.exists():
                     self._defaults.update(yamlio.load(dfile.read_text()) or {})
-                tasks += self._role_tasks(rname)
+                rtasks = self._role_tasks(rname)
+                rwhen = None if isinstance(role, str) else role.get("when")
+                if rwhen is not None:  # a role's `when:` applies to every task of it (and-ed with theirs)
+                    for t in rtasks:
+                        own = t.get("when")
+                        t["when"] = [*(rwhen if isinstance(rwhen, list) else [rwhen]),
+                                     *([] if own is None else own if isinstance(own, list) else [own])]
+                tasks += rtasks
             tasks += play.get("tasks") or []
             self._play = str(name)
             self._play_env = play.get("environment") or {}

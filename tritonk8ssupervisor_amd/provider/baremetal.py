@@ -194,8 +194,14 @@ class BareMetalProvider(Provider):
 
     # ---- placement --------------------------------------------------------------------------
     # One machine per host (the kubeadm platform: one kubelet per OS, which owns all the host's
-    # GPUs); False = machines are slices of hosts (the tk8s platform's node agents).
+    # GPUs); False = machines are slices of hosts (the tk8s platform's node agents, and the
+    # kubeadm platform's single-node mode, whose workers are GPU slots of the one host).
     whole_hosts = False
+
+    def single_host(self) -> bool:
+        """The inventory holds one host: the kubeadm platform then runs single-node (control plane
+        and GPU worker on that host, kubeadm_platform.py) instead of one kubelet per machine."""
+        return len(self.inventory()["hosts"]) == 1
 
     def _place(self, alloc: dict, name: str, role: str, ngpus: int) -> tuple[dict, list[int]]:
         hosts = self.inventory()["hosts"]
@@ -210,7 +216,8 @@ class BareMetalProvider(Provider):
                 free.sort(key=lambda h: (h["role"] != "master", len(h["gpus"])))  # the master host, else the smallest
             if not free:
                 raise ProvisionError(f"{name}: every machine needs a host of its own here (one kubelet per host) and no "
-                                     f"free host has {ngpus} GPU(s); add hosts to the inventory")
+                                     f"free host has {ngpus} GPU(s); add hosts to the inventory, or use a one-host "
+                                     "inventory (single-node mode: control plane and GPU worker on that host)")
             h = free[0]
             return h, ([] if role == "master" else list(h["gpus"]))
         if role == "master":
