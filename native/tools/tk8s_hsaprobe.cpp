@@ -666,6 +666,7 @@ struct DeviceResult {
   std::string hbm, md5, copy, digest, error, host_pull;
   std::vector<std::string> peers;  // pulls INTO this device, one per source GPU
   bool peers_ok = true;
+  std::string peer_source_error;  // filling its buffer for the peers failed: a link verdict, not a device one
   double wall_ms = 0, hbm_ms = 0, md5_ms = 0, copy_ms = 0, setup_ms = 0;
   bool ok = true;
   Device* dev = nullptr;  // kept for the peer phase (never freed, see run_device)
@@ -858,8 +859,11 @@ void run_peers(const std::vector<int>& devices, const Config& c, std::vector<Dev
       res[k].dev->fill(res[k].base, c.peer, peer_pattern(devices[k]), false, /*system=*/true);
       res[k].dev->sync();
     } catch (const std::exception& e) {
-      res[k].error = std::string("peer source fill: ") + e.what();
-      res[k].ok = false;
+      // The device itself passed its own checks: this fails the links that read from it (their
+      // pulls report "unavailable", peers_ok goes false on both ends), so the machines still get
+      // their share of the result and the xGMI verdict keeps the node NotReady.
+      res[k].peer_source_error = std::string("peer source fill: ") + e.what();
+      res[k].peers_ok = false;
     }
   }
   // 2. grants: who may read whose VRAM. A pool the runtime reports NEVER_ALLOWED for an agent is
@@ -870,7 +874,8 @@ void run_peers(const std::vector<int>& devices, const Config& c, std::vector<Dev
     std::vector<size_t> idx;
     for (size_t k = 0; k < m; ++k) {
       if (k == j) continue;
-      if (!res[j].dev || !res[k].dev || !res[j].error.empty() || !res[k].error.empty()) {
+      if (!res[j].dev || !res[k].dev || !res[j].error.empty() || !res[k].error.empty() ||
+          !res[j].peer_source_error.empty()) {
         access[k][j] = "unavailable";
         continue;
       }
@@ -1140,6 +1145,7 @@ int main(int argc, char** argv) {
       if (c.copy && !r.copy.empty()) d.raw("copy", r.copy);
       // Data integrity of its incoming pulls; their bandwidth is judged host-wide (xgmi.py).
       if (c.peers) d.raw("peers", Json::array(r.peers)).kv("peers_ok", r.peers_ok);
+      if (!r.peer_source_error.empty()) d.kv("peer_source_error", r.peer_source_error);
       if (!r.host_pull.empty()) d.raw("host_pull", r.host_pull);
       per_dev.push_back(d.str());
     }

@@ -41,13 +41,40 @@ double now_s() {
   return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
+// Field 22 of /proc/self/stat (start time, clock ticks since boot): with the pid, the identity
+// teardown checks before it signals the group (utils/procs.py pidfile_owner_alive).
+long long start_ticks() {
+  FILE* f = std::fopen("/proc/self/stat", "r");
+  if (!f) return -1;
+  char buf[1024];
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* p = std::strrchr(buf, ')');
+  if (!p) return -1;
+  long long v = -1;
+  for (int field = 2; p && *p; ++field) {  // field 2 ends at ')'; fields are space separated after it
+    p = std::strchr(p, ' ');
+    if (!p) break;
+    ++p;
+    if (field + 1 == 22) {
+      v = std::atoll(p);
+      break;
+    }
+  }
+  return v;
+}
+
 void write_pidfile(const std::string& path, pid_t child, int restarts) {
   if (path.empty()) return;
   const std::string tmp = path + ".tmp";
   FILE* f = std::fopen(tmp.c_str(), "w");
   if (!f) return;
-  std::fprintf(f, "{\"pid\": %d, \"pgid\": %d, \"child\": %d, \"restarts\": %d, \"supervisor\": \"tk8s-supervise\"}\n",
+  static const long long start = start_ticks();
+  std::fprintf(f, "{\"pid\": %d, \"pgid\": %d, \"child\": %d, \"restarts\": %d, \"supervisor\": \"tk8s-supervise\"",
                static_cast<int>(getpid()), static_cast<int>(getpgrp()), static_cast<int>(child), restarts);
+  if (start >= 0) std::fprintf(f, ", \"start\": %lld", start);
+  std::fprintf(f, "}\n");
   std::fclose(f);
   std::rename(tmp.c_str(), path.c_str());
 }

@@ -79,8 +79,18 @@ def test_setup_ready_and_clean_teardown(ws, n):
     wall = time.monotonic() - t
     assert s["nodes"] == n and s["gpus_allocatable"] == n and s["nodes_validated"] == n
     if n >= 2:  # the RCCL fabric check ran across all GPUs, one rank per GPU
-        assert s["rccl"]["ok"] and s["rccl"]["nranks"] == n
-        assert len({r["node"] for r in s["rccl"]["rank_results"]}) == n
+        rc = s["rccl"]
+        assert rc["ok"] and rc["nranks"] == n
+        # every worker is a one-GPU slice of this one host: ONE pod, ONE process driving all n GPUs
+        # as ranks 0..n-1, its GPUs claimed on every node of the host meanwhile
+        assert rc["pods"] == 1 and rc["gpus_per_pod"] == n and rc["scope"] == "host", rc
+        r = subprocess.run(["./kubectl", "get", "pods", "-n", "kube-system", "-l", f"job-name={rc['job']}", "-o",
+                            "json"], cwd=ws, env=_env(), capture_output=True, text=True)
+        (pod,) = json.loads(r.stdout)["items"]
+        res = pod["status"]["result"]
+        assert (res["first_rank"], res["local_ranks"], res["nranks"]) == (0, n, n), res
+        claims = json.loads(pod["metadata"]["annotations"]["tk8s.amd.com/host-claims"])
+        assert claims == {f"kubenode{i}": 1 for i in range(1, n + 1)}
     assert wall < 60  # the reference's fixed sleeps alone are 51 s
     # reference artefacts exist, with reference names
     for rel in ("config", "terraform/rancher.tf", "terraform/masters.ip", "terraform/hosts.ip", "ansible/hosts",
@@ -728,15 +738,86 @@ def test_dry_run_exits_nonzero_when_the_check_fails(ws):
     assert not (ws / "config").exists() and not (ws / "terraform" / "rancher.tf").exists()
 
 
-def test_rccl_job_runs_one_pod_per_multi_gpu_node(ws):
-    """mi355x-2gpu workers: the fabric Job is one pod per node holding both of its GPUs, one
-    process driving them as consecutive ranks (not one process per GPU)."""
-    s = _summary(_setup(ws, "--nodes", "2", "--package", "mi355x-2gpu", "--rccl", "on"))
+def test_rccl_job_runs_one_pod_per_host(ws):
+    """mi355x-2gpu workers on two (simulated) hosts: the fabric Job is one pod per host holding
+    both of its GPUs, one process driving them as consecutive ranks (not one process per GPU),
+    the two pods joined by one communicator (ncclCommInitRank groups)."""
+    s = _summary(_setup(ws, "--nodes", "2", "--package", "mi355x-2gpu", "--rccl", "on", env=_env(TK8S_FAKE_HOSTS="2")))
     rc = s["rccl"]
     assert rc["ok"] and rc["nranks"] == 4 and rc["pods"] == 2 and rc["gpus_per_pod"] == 2, rc
+    assert rc["scope"] == "node"  # one node per host: no claims on other nodes needed
     assert sorted(r["node"] for r in rc["rank_results"]) == ["kubenode1", "kubenode2"]
     r = subprocess.run(["./kubectl", "get", "pods", "-n", "kube-system", "-l", f"job-name={rc['job']}", "-o", "json"],
                        cwd=ws, env=_env(), capture_output=True, text=True)
     res = sorted((p["status"]["result"] for p in json.loads(r.stdout)["items"]), key=lambda x: x["first_rank"])
     assert [(x["first_rank"], x["local_ranks"], x["mode"]) for x in res] == [(0, 2, "rank_group"), (2, 2, "rank_group")]
     assert all(x["nranks"] == 4 for x in res)
+
+
+def _fake_gpu_tree(root: Path, n: int) -> tuple[Path, Path]:
+    """A KFD topology + /dev/dri twin of TK8S_FAKE_GPUS=n (models/hostinfo.fake_inventory: KFD node
+    i+1, render minor 128+i; node 0 the CPU) for the GPU jail to act on."""
+    kfd, dri = root / "kfd" / "nodes", root / "dri"
+    (kfd / "0").mkdir(parents=True)
+    (kfd / "0" / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+    dri.mkdir(parents=True)
+    for i in range(n):
+        (kfd / str(i + 1)).mkdir()
+        (kfd / str(i + 1) / "properties").write_text(f"simd_count 1024\ndrm_render_minor {128 + i}\n")
+        (dri / f"renderD{128 + i}").write_text(f"gpu{i}\n")
+        (dri / f"card{i}").write_text(f"card{i}\n")
+    return kfd, dri
+
+
+def test_pods_can_open_only_their_gpus(ws, tmp_path_factory):
+    """GPU isolation that does not depend on the pod's env. Every pod runs in the GPU
+    jail (Landlock, native/tools/tk8s_gpujail.cpp): a pod holding one GPU can read that GPU's KFD node
+    and render node and nothing of the other GPU -- even after clearing HIP_VISIBLE_DEVICES -- and a pod
+    with no amd.com/gpu request can open none; `kubectl describe pod` names the isolation."""
+    from tritonk8ssupervisor_amd.agent.runtime import gpu_jail
+
+    if not gpu_jail()[0]:
+        pytest.skip(f"GPU jail unavailable here: {gpu_jail()[1]}")
+    d = tmp_path_factory.mktemp("jail")
+    kfd, dri = _fake_gpu_tree(d, 2)
+    env = _env(TK8S_FAKE_GPUS="2", TK8S_GPU_JAIL_KFD_ROOT=str(kfd), TK8S_GPU_JAIL_DRI_ROOT=str(dri))
+    _summary(_setup(ws, "--nodes", "2", "--rccl", "off", env=env))
+    probe = (f"unset HIP_VISIBLE_DEVICES ROCR_VISIBLE_DEVICES CUDA_VISIBLE_DEVICES; "
+             f"for i in 1 2; do cat {kfd}/$i/properties >/dev/null 2>&1 && echo node$i=open || echo node$i=denied; done; "
+             f"for m in 128 129; do cat {dri}/renderD$m >/dev/null 2>&1 && echo render$m=open || echo render$m=denied; done; "
+             f"cat {kfd}/0/properties >/dev/null && echo cpu=open; echo iso=$TK8S_GPU_ISOLATION")
+    for name, gpus in (("with-gpu", 1), ("no-gpu", 0)):
+        res = {"limits": {"amd.com/gpu": gpus}} if gpus else {}
+        (d / f"{name}.yaml").write_text(json.dumps({
+            "apiVersion": "v1", "kind": "Pod", "metadata": {"name": name},
+            "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "command": ["sh", "-c", probe],
+                                                               "resources": res}]}}))
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
+    for name in ("with-gpu", "no-gpu"):
+        assert kc("apply", "-f", str(d / f"{name}.yaml")).returncode == 0
+    deadline = time.monotonic() + 30
+    pods = {}
+    while time.monotonic() < deadline:
+        pods = {p["metadata"]["name"]: p for p in json.loads(kc("get", "pods", "-o", "json").stdout)["items"]}
+        if all(pods.get(n, {}).get("status", {}).get("phase") == "Succeeded" for n in ("with-gpu", "no-gpu")):
+            break
+        time.sleep(0.2)
+    logs = {n: dict(x.split("=", 1) for x in kc("logs", n).stdout.split() if "=" in x) for n in ("with-gpu", "no-gpu")}
+    mine = pods["with-gpu"]["metadata"]["annotations"]["amd.com/gpu-ids"]  # gpu0 or gpu1
+    i = int(mine[-1])
+    other = 1 - i
+    assert logs["with-gpu"][f"node{i + 1}"] == "open" and logs["with-gpu"][f"render{128 + i}"] == "open", logs
+    assert logs["with-gpu"][f"node{other + 1}"] == "denied" and logs["with-gpu"][f"render{128 + other}"] == "denied", logs
+    assert logs["no-gpu"] == {"node1": "denied", "node2": "denied", "render128": "denied", "render129": "denied",
+                              "cpu": "open", "iso": logs["no-gpu"]["iso"]}, logs
+    assert logs["no-gpu"]["iso"].startswith("landlock:abi")
+    r = kc("describe", "pod", "no-gpu")
+    assert "Isolation:" in r.stdout and "may open no GPU" in r.stdout, r.stdout
+    assert f"may open gpu{i}" in kc("describe", "pod", "with-gpu").stdout
+
+
+def test_rccl_job_one_process_for_multi_gpu_nodes_on_one_host(ws):
+    """Two 2-GPU workers on ONE host: one host-scoped pod, one process, 4 ranks."""
+    s = _summary(_setup(ws, "--nodes", "2", "--package", "mi355x-2gpu", "--rccl", "on"))
+    rc = s["rccl"]
+    assert rc["ok"] and rc["nranks"] == 4 and rc["pods"] == 1 and rc["gpus_per_pod"] == 4 and rc["scope"] == "host", rc

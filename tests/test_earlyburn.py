@@ -236,3 +236,20 @@ def test_launch_hands_the_plan_to_the_preloaded_probe(tmp_path, monkeypatch):
     finally:
         earlyburn.take()
     del ws
+
+
+def test_multi_gpu_pulls_take_the_hip_peer_path_unless_asked(monkeypatch):
+    """the HSA probe's peer grants have not run on a multi-GPU box, so the
+    host burn-in's xGMI pulls go through the HIP probe (hipDeviceEnablePeerAccess, RCCL's own P2P
+    path) unless TK8S_PEERS_RUNTIME=hsa; one-GPU burn-ins keep the faster HSA start."""
+    monkeypatch.delenv("TK8S_FAKE_GPUS", raising=False)
+    monkeypatch.delenv("TK8S_PEERS_RUNTIME", raising=False)
+    base = earlyburn.default_validation_command(peers=False)
+    one = earlyburn.host_burnin_command(base, [0])
+    many = earlyburn.host_burnin_command(base, [0, 1])
+    assert "--peers" not in one and "--peers" in many
+    assert os.path.basename(many[0]) == "tk8s-probe"
+    if os.path.basename(base[0]) == "tk8s-hsaprobe":
+        assert os.path.basename(one[0]) == "tk8s-hsaprobe"
+    monkeypatch.setenv("TK8S_PEERS_RUNTIME", "hsa")
+    assert os.path.basename(earlyburn.probe_tool(peers=True)) == os.path.basename(earlyburn.probe_tool())

@@ -287,3 +287,43 @@ def test_local_provider_skips_addresses_something_already_serves_on():
     finally:
         for s in (u, t, c):
             s.close()
+
+
+def test_kill_pidfile_never_signals_a_stranger(tmp_path):
+    """a pidfile whose process is gone (or whose pid now belongs to another process)
+    is removed without signalling anything; the recorded start time is the identity."""
+    import subprocess
+    import sys
+
+    from tritonk8ssupervisor_amd.utils.procs import kill_pidfile, proc_start_ticks, spawn_daemon
+
+    pf = tmp_path / "d.pid"
+    p = spawn_daemon([sys.executable, "-c", "import time; time.sleep(30)"], pidfile=str(pf))
+    info = json.loads(pf.read_text())
+    assert info["start"] == proc_start_ticks(p.pid)
+    # the same pid with another start time: a reused pid -- left alone, the pidfile removed
+    pf.write_text(json.dumps(dict(info, start=info["start"] - 1)))
+    assert kill_pidfile(pf, grace=0.5) is False and not pf.exists() and p.poll() is None
+    # a legacy pidfile (no start time) naming a process that is not tk8s's: left alone too
+    stranger = subprocess.Popen(["sleep", "30"], start_new_session=True)
+    pf.write_text(json.dumps({"pid": stranger.pid, "pgid": stranger.pid}))
+    assert kill_pidfile(pf, grace=0.5) is False and stranger.poll() is None
+    stranger.kill()
+    stranger.wait()
+    # the real owner is stopped
+    pf.write_text(json.dumps(info))
+    assert kill_pidfile(pf, grace=2.0) is True
+    p.wait(5)
+
+
+def test_fabric_visibility_needs_a_real_owner_job():
+    """the agent checks a pod's Job ownerReference against the Job the control plane
+    has (same uid), so a client-written ownerReference does not unlock node / host GPU views."""
+    from tritonk8ssupervisor_amd.agent.agent import node_visibility_allowed
+
+    pod = {"metadata": {"namespace": "kube-system", "ownerReferences": [{"kind": "Job", "name": "j", "uid": "u1"}]}}
+    assert node_visibility_allowed(pod, lambda ns, name: "u1" if (ns, name) == ("kube-system", "j") else None)
+    assert not node_visibility_allowed(pod, lambda ns, name: None)       # no such Job
+    assert not node_visibility_allowed(pod, lambda ns, name: "u2")       # another Job of that name
+    other_ns = {"metadata": {**pod["metadata"], "namespace": "default"}}
+    assert not node_visibility_allowed(other_ns, lambda ns, name: "u1")

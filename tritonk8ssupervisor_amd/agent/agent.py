@@ -30,11 +30,15 @@ from ..utils.faults import fault
 from ..utils.k8senv import field_path, service_env
 from ..utils.trace import trace
 from .deviceplugin import DevicePlugin
-from .runtime import PodProc, PodRuntime, install_sigterm, namespace_isolation
+from .runtime import PodProc, PodRuntime, gpu_jail, gpu_jail_argv, install_sigterm, namespace_isolation
 
 GPU = "amd.com/gpu"
 ALL_GPUS = "tk8s.amd.com/all-gpus"
 GPU_VISIBILITY = "tk8s.amd.com/gpu-visibility"
+GPU_SCOPE = "tk8s.amd.com/gpu-scope"            # "host": the fabric Job's one process per host
+HOST_LABEL = "tk8s.amd.com/host"                # which physical host a node's machine lives on
+HOST_CLAIMS = "tk8s.amd.com/host-claims"        # set by the scheduler on host-scoped pods
+HOST_DEVICES = "tk8s.amd.com/host-devices"
 VALIDATION_LABEL = "tk8s.amd.com/validation"
 TERMINAL = ("Succeeded", "Failed")
 TK8S_HOME = str(Path(__file__).resolve().parents[2])  # this node's tk8s install root
@@ -58,12 +62,30 @@ def pod_base_env(environ=None) -> dict:
     return out
 
 
-def node_visibility_allowed(pod: dict) -> bool:
-    """``gpu-visibility: node`` (a rank sees every GPU of the node, rccl-tests style) is for the
-    cluster's own fabric Jobs only: kube-system pods owned by a Job."""
+def node_visibility_allowed(pod: dict, job_uid=None) -> bool:
+    """``gpu-visibility: node`` (a rank sees every GPU of the node, rccl-tests style) and
+    ``gpu-scope: host`` are for the cluster's own fabric Jobs only: kube-system pods owned by a
+    Job. ``job_uid(ns, name)`` looks the owner up (None: no such Job): an ownerReference a client
+    wrote itself names no real Job, or one with another uid."""
     md = pod.get("metadata", {})
-    return md.get("namespace") == "kube-system" and any(
-        r.get("kind") == "Job" for r in md.get("ownerReferences") or [])
+    if md.get("namespace") != "kube-system":
+        return False
+    owners = [r for r in md.get("ownerReferences") or [] if r.get("kind") == "Job"]
+    if not owners:
+        return False
+    if job_uid is None:
+        return True
+    return any(r.get("uid") and job_uid("kube-system", r.get("name", "")) == r["uid"] for r in owners)
+
+
+def host_id() -> str:
+    """This host's identity for the ``tk8s.amd.com/host`` node label (a label value: at most 63
+    characters of [A-Za-z0-9._-]): ``TK8S_HOST_ID`` if the provider set it, else the host name."""
+    import re
+
+    raw = os.environ.get("TK8S_HOST_ID") or os.uname().nodename or "localhost"
+    v = re.sub(r"[^A-Za-z0-9._-]", "-", raw).strip("-._")[:63].strip("-._")
+    return v or "localhost"
 
 
 def pod_gpus(p: dict) -> int:
@@ -86,7 +108,8 @@ class Agent:
         self.name = name
         self.ip = ip
         self.sandbox = Path(sandbox)
-        self.labels = labels or {}
+        self.labels = dict(labels or {})
+        self.labels.setdefault(HOST_LABEL, host_id())
         self.timeout = timeout
         self.plugin = DevicePlugin(gpus)
         self.runtime = PodRuntime(self.sandbox / "pods", self._on_status, tool_dirs)
@@ -312,12 +335,25 @@ class Agent:
             self._config_wait[key] = pod
             return
         self._config_wait.pop(key, None)
-        visibility = md.get("annotations", {}).get(GPU_VISIBILITY, "allocated")
-        if visibility == "node" and not node_visibility_allowed(pod):
+        ann = md.get("annotations", {})
+        visibility = ann.get(GPU_VISIBILITY, "allocated")
+        scope = ann.get(GPU_SCOPE, "node")
+        if (visibility == "node" or scope == "host") and not node_visibility_allowed(pod, self._job_uid):
+            what = f"{GPU_SCOPE}: host" if scope == "host" else f"{GPU_VISIBILITY}: node"
             self._report(key, md["name"], md["namespace"], "Failed",
-                         {"reason": "Forbidden", "message": f"{GPU_VISIBILITY}: node is reserved for kube-system "
-                                                            "Jobs (the cluster's RCCL fabric check)"}, None)
+                         {"reason": "Forbidden", "message": f"{what} is reserved for kube-system Jobs (the cluster's "
+                                                            "RCCL fabric check)"}, None)
             return
+        others: list[dict] = []
+        if scope == "host":  # one process over GPUs of several nodes of this host (scheduler.py)
+            try:
+                claims = json.loads(ann.get(HOST_CLAIMS) or "{}")
+                others = [d for d in json.loads(ann.get(HOST_DEVICES) or "[]") if d.get("node") != self.name]
+                need = int(claims.get(self.name, 0))
+            except (ValueError, AttributeError, TypeError):
+                self._report(key, md["name"], md["namespace"], "Failed",
+                             {"reason": "UnexpectedAdmissionError", "message": f"unreadable {HOST_CLAIMS}"}, None)
+                return
         free = self._free_devices()
         if need > len(free):
             self._report(key, md["name"], md["namespace"], "Failed",
@@ -336,9 +372,15 @@ class Agent:
                          {"reason": "UnexpectedAdmissionError", "message": f"Allocate failed: {e}"}, None)
             return
         env = pod_base_env()
-        env.update(pod_gpu_env(alloc["env"], [self._ordinal(i) for i in ids], visibility))
+        ordinals = [self._ordinal(i) for i in ids]
+        if scope == "host":
+            ordinals += [int(d["ordinal"]) for d in others]
+            env.update(host_scope_env(ordinals))
+        else:
+            env.update(pod_gpu_env(alloc["env"], ordinals, visibility))
         env.update(base)
-        env.update({"TK8S_GPU_IDS": ",".join(ids), "TK8S_GPU_COUNT": str(len(ids))})
+        env.update({"TK8S_GPU_IDS": ",".join(ids + [f"{d['node']}/{d['id']}" for d in others]),
+                    "TK8S_GPU_COUNT": str(len(ordinals))})
         env.update(cenv)
         argv = [_expand(str(x), env) for x in (c.get("command") or []) + (c.get("args") or [])]
         if not c.get("command"):
@@ -355,18 +397,29 @@ class Agent:
             return
         # GPU pods stay in the host PID namespace: HIP/RCCL inter-process sharing (dmabuf handles
         # passed by pid, RCCL's pid-keyed shared memory) needs the peers' real pids.
-        gpu_pod = bool(ids) or all_gpus or visibility == "node"
+        gpu_pod = bool(ids) or all_gpus or visibility == "node" or bool(others)
         avail, how = namespace_isolation(str(Path(TK8S_HOME) / "tritonk8ssupervisor_amd" / "__init__.py"),
                                          str(self.sandbox / "pods"))
         isolation = "none: GPU pod (shares the host PID namespace for HIP/RCCL IPC)" if gpu_pod else how if avail \
             else f"none: {how}"
+        # GPU isolation, whatever the pod does with *_VISIBLE_DEVICES: it can open exactly the
+        # GPUs it holds (none for a pod without an amd.com/gpu request)
+        jail_ok, jail_how = gpu_jail()
+        by_ord = {g.ordinal: g for g in self.plugin.inventory.gpus}
+        # node visibility (rccl-tests style ranks): the pod's runtime sees the node's GPUs
+        view = [d.ordinal for d in self.plugin.devices_] if visibility == "node" and scope != "host" else ordinals
+        mine = [by_ord[o] for o in view if o in by_ord]
+        jail = gpu_jail_argv(mine) if jail_ok else []
+        gpu_isolation = (f"{jail_how}: may open {', '.join(f'gpu{g.ordinal}' for g in mine) or 'no GPU'}" if jail_ok
+                         else f"none: {jail_how}")
         pp = PodProc(key=key, uid=md.get("uid", ""), dir=pp_dir, argv=argv, env=env,
                      restart_policy=spec.get("restartPolicy", "Always"), gpu_ids=ids, ip=pod_ip,
-                     isolate=avail and not gpu_pod)
+                     isolate=avail and not gpu_pod, jail=jail)
         self._pods_meta[key] = {"name": md["name"], "namespace": md["namespace"],
                                 "validation": md.get("labels", {}).get(VALIDATION_LABEL) == "true",
                                 "annotations": {**alloc["annotations"], "tk8s.amd.com/log-path": str(pp_dir / "log"),
-                                                "tk8s.amd.com/isolation": isolation}}
+                                                "tk8s.amd.com/isolation": isolation,
+                                                "tk8s.amd.com/gpu-isolation": gpu_isolation}}
         self.runtime.start(pp)
 
     # ---- container env (kubelet semantics) ------------------------------------------------
@@ -582,8 +635,26 @@ class Agent:
                 self.kubelet.stop()
         return 0
 
+    def _job_uid(self, ns: str, name: str) -> str | None:
+        """uid of the Job ns/name as the control plane has it (None: there is none)."""
+        try:
+            return self.api.get(self.api.k8s(f"/apis/batch/v1/namespaces/{ns}/jobs/{name}"))["metadata"].get("uid")
+        except (ApiError, OSError, KeyError):
+            return None
+
     def _ordinal(self, dev_id: str) -> int:
         return next(d.ordinal for d in self.plugin.devices_ if d.id == dev_id)
+
+
+def host_scope_env(ordinals: list[int]) -> dict:
+    """GPU env of a host-scoped pod: its runtime sees exactly the claimed GPUs of the host (its
+    own node's and the other claimed nodes', host ordinals), named 0..n-1 in TK8S_GPU_DEVICES."""
+    from ..earlyburn import compose_visible_devices
+
+    env = compose_visible_devices(ordinals)
+    env["TK8S_GPU_DEVICES"] = ",".join(str(i) for i in range(len(ordinals)))
+    env["TK8S_GPU_DEVICE"] = "0" if ordinals else ""
+    return env
 
 
 def pod_gpu_env(alloc_env: dict, ordinals: list[int], visibility: str = "allocated") -> dict:

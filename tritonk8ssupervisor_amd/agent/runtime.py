@@ -18,7 +18,7 @@ import time
 from pathlib import Path
 
 from ..utils.fsutil import atomic_write_json
-from ..utils.procs import kill_group
+from ..utils.procs import kill_group, proc_start_ticks
 from ..utils.record import field, record as dataclass
 from ..utils.trace import trace
 
@@ -65,6 +65,7 @@ class PodProc:
     gpu_ids: list[str] = field(default_factory=list)
     ip: str = ""                  # the pod's own loopback IP (from the node's podCIDR)
     isolate: bool = False         # own user/pid/mount namespaces (see namespace_isolation())
+    jail: list[str] = field(default_factory=list)  # GPU jail argv prefix (gpu_jail_argv), [] = none
     proc: subprocess.Popen | None = None
     restarts: int = 0
     started: float = 0.0
@@ -91,8 +92,8 @@ class PodRuntime:
         env = dict(pp.env)
         if self.tool_dirs:
             env["PATH"] = os.pathsep.join(self.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
-        argv = list(pp.argv)
-        if pp.isolate and namespace_isolation()[0]:
+        argv = [*pp.jail, *pp.argv]  # nothing the pod runs can leave the jail
+        if pp.isolate and namespace_isolation()[0]:  # outside the jail: a Landlocked process may not mount /proc
             argv = [*UNSHARE, "--", *argv]
         log = open(pp.dir / "log", "ab", buffering=0)
         try:
@@ -100,7 +101,8 @@ class PodRuntime:
                                  stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
         finally:
             log.close()
-        atomic_write_json(pp.dir / "pod.pid", {"pid": p.pid, "pgid": p.pid, "argv": pp.argv})
+        atomic_write_json(pp.dir / "pod.pid", {"pid": p.pid, "pgid": p.pid, "argv": pp.argv,
+                                               "start": proc_start_ticks(p.pid)})
         return p
 
     def _run(self, pp: PodProc) -> None:
@@ -190,6 +192,49 @@ def namespace_isolation(readable: str = "", writable: str = "") -> tuple[bool, s
             except (OSError, subprocess.TimeoutExpired) as e:
                 _ISOLATION = (False, f"unavailable: {e}")
     return _ISOLATION
+
+
+# The GPU jail (native/tools/tk8s_gpujail.cpp): Landlock keeps a pod from opening the KFD
+# topology nodes and DRM render nodes of GPUs it was not allocated, so its runtime enumerates
+# exactly its GPUs whatever *_VISIBLE_DEVICES it sets -- the device-cgroup part of a container,
+# with no privileges and no namespaces (both unavailable to the GPU tier's user).
+JAIL = Path(__file__).resolve().parents[1] / "bin" / "tk8s-gpujail"
+_JAIL: tuple[bool, str] | None = None
+
+
+def gpu_jail() -> tuple[bool, str]:
+    """(available, description), probed once (``tk8s-gpujail --probe``); TK8S_GPU_JAIL=0 disables."""
+    global _JAIL
+    if _JAIL is None:
+        if os.environ.get("TK8S_GPU_JAIL", "1") == "0":
+            _JAIL = (False, "disabled (TK8S_GPU_JAIL=0)")
+        elif not JAIL.exists():
+            _JAIL = (False, "unavailable: tk8s-gpujail is not built")
+        else:
+            try:
+                r = subprocess.run([str(JAIL), "--probe"], capture_output=True, text=True, timeout=10)
+                info = json.loads(r.stdout or "{}")
+                _JAIL = ((True, f"landlock (abi {info.get('landlock_abi')})") if r.returncode == 0 and info.get("usable")
+                         else (False, f"unavailable: Landlock {info.get('error') or 'not usable'}"))
+            except (OSError, ValueError, subprocess.TimeoutExpired) as e:
+                _JAIL = (False, f"unavailable: {e}")
+    return _JAIL
+
+
+def gpu_jail_argv(gpus: list) -> list[str]:
+    """argv prefix that runs a command allowed to open only ``gpus`` (HostGpu records: KFD node +
+    render minor). TK8S_GPU_JAIL_KFD_ROOT / TK8S_GPU_JAIL_DRI_ROOT point it at another tree (the
+    CPU tests' fake GPUs)."""
+    argv = [str(JAIL)]
+    for g in gpus:
+        if getattr(g, "kfd_node", -1) >= 0:
+            argv += ["--allow-node", str(g.kfd_node)]
+        if getattr(g, "render_minor", -1) >= 0:
+            argv += ["--allow-render", str(g.render_minor)]
+    for opt, env in (("--kfd-root", "TK8S_GPU_JAIL_KFD_ROOT"), ("--dri-root", "TK8S_GPU_JAIL_DRI_ROOT")):
+        if os.environ.get(env):
+            argv += [opt, os.environ[env]]
+    return argv + ["--"]
 
 
 def _sigterm_to_exit(*_):

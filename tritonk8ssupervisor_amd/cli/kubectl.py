@@ -369,6 +369,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                                               for c in st.get("conditions", [])))
             if what == "pod":
                 print(f"Node:         {o['spec'].get('nodeName')}\nStatus:       {st.get('phase')}")
+                ann = o["metadata"].get("annotations", {})
+                if "tk8s.amd.com/gpu-isolation" in ann or "tk8s.amd.com/isolation" in ann:
+                    print("Isolation:\n"
+                          f"  GPU:        {ann.get('tk8s.amd.com/gpu-isolation', '-')}\n"
+                          f"  Namespaces: {ann.get('tk8s.amd.com/isolation', '-')}")
         elif a.verb == "create" and a.args and a.args[0] in ("configmap", "cm", "secret"):
             return _create_data(k, a, ns)
         elif a.verb == "create" and a.args and kind_key(a.args[0]) == "deployment":

@@ -245,7 +245,17 @@ class KubernetesAPI:
             raise HttpError(404, f'deployments.apps "{name}" not found')
         if req.method in ("PUT", "PATCH"):
             self._auth(req, self.project(p))
-            n = (req.json().get("spec") or {}).get("replicas")
+            body = req.json()
+            ctype = (req.headers.get("content-type") or "").split(";")[0].strip()
+            if ctype == k8s_wire.JSON_PATCH:  # kubectl patch --type json on the Scale object
+                cur = {"spec": {"replicas": int(d["spec"].get("replicas", 1))}}
+                try:
+                    body = k8s_wire.json_patch(cur, body)
+                except k8s_wire.PatchError as e:
+                    raise HttpError(422, str(e)) from e
+            if not isinstance(body, dict):  # a 4xx, not a 500
+                raise HttpError(422, "the body must be a JSON object (a Scale)")
+            n = (body.get("spec") or {}).get("replicas")
             if not isinstance(n, int) or isinstance(n, bool) or n < 0:
                 raise HttpError(422, "spec.replicas must be a non-negative integer")
             d = self.replace(p, "deployments", ns, name, {"spec": {"replicas": n}}, merge=True)
@@ -486,6 +496,7 @@ class KubernetesAPI:
         md.pop("resourceVersion", None)
         md.setdefault("labels", {})
         md.setdefault("annotations", {})
+        _admit_gpu_visibility(kind, ns, new, cur)  # PUT and every patch type, not only create
         spec_changed = new.get("spec") != cur.get("spec")
         if kind == "pods" and spec_changed:
             raise HttpError(422, f'Pod "{name}" is invalid: spec: Forbidden: pod updates may not change '

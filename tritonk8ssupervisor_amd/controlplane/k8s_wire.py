@@ -281,12 +281,12 @@ def json_patch(doc, ops: list):
 
     def parent(d, parts):
         for p in parts[:-1]:
-            d = d[int(p)] if isinstance(d, list) else d[p]
+            d = d[_index(p)] if isinstance(d, list) else d[p]
         return d
 
     def get(d, parts):
         for p in parts:
-            d = d[int(p)] if isinstance(d, list) else d[p]
+            d = d[_index(p)] if isinstance(d, list) else d[p]
         return d
 
     def add(d, parts, value):
@@ -294,15 +294,26 @@ def json_patch(doc, ops: list):
             return value
         par, last = parent(d, parts), parts[-1]
         if isinstance(par, list):
-            par.insert(len(par) if last == "-" else int(last), value)
+            if last == "-":
+                par.append(value)
+                return d
+            idx = _index(last)
+            if idx > len(par):  # RFC 6902 4.1: an index past the end is an error, not an append
+                raise PatchError(f"index {last} out of bounds (array of {len(par)})")
+            par.insert(idx, value)
         else:
             par[last] = value
         return d
 
+    def _index(tok: str) -> int:
+        if not tok.isdigit() or (len(tok) > 1 and tok[0] == "0"):  # RFC 6901: no sign, no leading zero
+            raise PatchError(f"invalid array index {tok!r}")
+        return int(tok)
+
     def remove(d, parts):
         par, last = parent(d, parts), parts[-1]
         if isinstance(par, list):
-            return par.pop(int(last))
+            return par.pop(_index(last))
         return par.pop(last)
 
     for i, op in enumerate(ops):
@@ -318,7 +329,7 @@ def json_patch(doc, ops: list):
                     doc = copy.deepcopy(op["value"])
                 else:
                     par = parent(doc, parts)
-                    par[int(parts[-1]) if isinstance(par, list) else parts[-1]] = copy.deepcopy(op["value"])
+                    par[_index(parts[-1]) if isinstance(par, list) else parts[-1]] = copy.deepcopy(op["value"])
             elif kind in ("move", "copy"):
                 src = _pointer(op["from"])
                 val = remove(doc, src) if kind == "move" else copy.deepcopy(get(doc, src))

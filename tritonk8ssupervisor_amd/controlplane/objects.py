@@ -107,22 +107,42 @@ def template_hash(template: dict) -> str:
 
 
 GPU_VISIBILITY = "tk8s.amd.com/gpu-visibility"
+GPU_SCOPE = "tk8s.amd.com/gpu-scope"
+# annotations only the cluster's own fabric Jobs may carry: the pod's runtime sees every GPU of its
+# node (xGMI peer-to-peer between ranks), or one process drives GPUs of several nodes of a host
+_RESERVED = ((GPU_VISIBILITY, "node"), (GPU_SCOPE, "host"))
+# set by the scheduler on host-scoped pods (scheduler.py): never by a client
+_SCHEDULER_OWNED = ("tk8s.amd.com/host-claims", "tk8s.amd.com/host-devices")
 
 
-def _admit_gpu_visibility(kind: str, ns: str, body: dict) -> None:
-    """Admission: ``gpu-visibility: node`` lets a pod's runtime see every GPU of its node (the RCCL
-    fabric Job's ranks need it for xGMI peer-to-peer). Only kube-system Jobs may ask for it; a pod
-    cannot ask for it directly (the agent re-checks: kube-system pods owned by a Job)."""
+def _reserved(ann: dict) -> str | None:
+    for k, v in _RESERVED:
+        if ann.get(k) == v:
+            return f"{k}: {v}"
+    return None
+
+
+def _admit_gpu_visibility(kind: str, ns: str, body: dict, cur: dict | None = None) -> None:
+    """Admission for the fabric-only GPU annotations (``gpu-visibility: node``, ``gpu-scope: host``):
+    only kube-system Jobs may carry them in their pod template; a pod cannot ask for them itself --
+    not at create, and not later through PUT / merge / JSON / strategic patches (``cur``: the
+    object being replaced; a pod may keep what its Job gave it, never add or change it). The
+    agent re-checks the owner against the real Job's uid (agent.node_visibility_allowed)."""
     if kind == "pods":
         ann = (body.get("metadata") or {}).get("annotations") or {}
-        if ann.get(GPU_VISIBILITY) == "node":
-            raise HttpError(403, f'pods is forbidden: annotation {GPU_VISIBILITY}: node is reserved for '
-                                 'kube-system Jobs')
+        old = ((cur or {}).get("metadata") or {}).get("annotations") or {}
+        for k, _v in _RESERVED:
+            if ann.get(k) != old.get(k) and _reserved({k: ann.get(k)}):
+                raise HttpError(403, f'pods is forbidden: annotation {_reserved({k: ann.get(k)})} is reserved for '
+                                     'kube-system Jobs')
+        for k in _SCHEDULER_OWNED:
+            if ann.get(k) != old.get(k):
+                raise HttpError(403, f"pods is forbidden: annotation {k} is set by the scheduler")
     elif kind in ("jobs", "daemonsets", "deployments"):
         ann = ((body.get("spec") or {}).get("template") or {}).get("metadata", {}).get("annotations") or {}
-        if ann.get(GPU_VISIBILITY) == "node" and (kind != "jobs" or ns != "kube-system"):
-            raise HttpError(403, f'{kind} is forbidden: annotation {GPU_VISIBILITY}: node is reserved for '
-                                 'kube-system Jobs')
+        what = _reserved(ann)
+        if what and (kind != "jobs" or ns != "kube-system"):
+            raise HttpError(403, f"{kind} is forbidden: annotation {what} is reserved for kube-system Jobs")
 
 
 def _normalize_data(kind: str, body: dict) -> None:

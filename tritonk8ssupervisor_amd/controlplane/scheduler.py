@@ -1,10 +1,39 @@
 """The pod scheduler of the control plane: binds pending pods to Ready nodes with room, counting
 the extended resource amd.com/gpu (validated nodes only), the way the AMD k8s-device-plugin
 exposes it. A mixin of server.ControlPlane.
+
+Host-scoped GPU pods (``tk8s.amd.com/gpu-scope: host``, the cluster's own RCCL fabric Job only,
+objects._admit_gpu_visibility): in the default layout every worker is a one-GPU slice of the same
+8x MI355X host, and an all-reduce over them wants ONE process driving all of the host's GPUs
+(one runtime start, one ncclCommInitAll) rather than one rank process per node. Such a pod asks
+for N amd.com/gpu; the scheduler finds a host (node label ``tk8s.amd.com/host``) whose whole,
+idle GPU nodes add up to exactly N, binds the pod to one of them (the leader, whose agent runs it)
+and records the claim on the others in the pod's annotations -- ``host-claims`` (GPUs counted
+against each node, so nothing else lands there meanwhile) and ``host-devices`` (which devices of
+the other nodes the leader's process may open).
 """
 from __future__ import annotations
 
+import json
+
 from .objects import GPU, TERMINAL, _key, _cond, _set_cond, node_ready, node_validated, pod_gpus, labels_match
+
+GPU_SCOPE = "tk8s.amd.com/gpu-scope"
+HOST_LABEL = "tk8s.amd.com/host"
+HOST_CLAIMS = "tk8s.amd.com/host-claims"
+HOST_DEVICES = "tk8s.amd.com/host-devices"
+
+
+def pod_claims(o: dict) -> dict[str, int]:
+    """amd.com/gpu a bound pod holds per node: its node's share, or a host-scoped pod's claims."""
+    ann = o["metadata"].get("annotations") or {}
+    if ann.get(HOST_CLAIMS):
+        try:
+            return {k: int(v) for k, v in json.loads(ann[HOST_CLAIMS]).items()}
+        except (ValueError, AttributeError):
+            pass
+    nn = o["spec"].get("nodeName")
+    return {nn: pod_gpus(o)} if nn else {}
 
 
 class Scheduler:
@@ -20,11 +49,16 @@ class Scheduler:
         for o in self.store.list("pods", lambda o: self._in(pid, o)):
             nn = o["spec"].get("nodeName")
             if nn and o.get("status", {}).get("phase") not in TERMINAL:
-                used[nn] = used.get(nn, 0) + pod_gpus(o)
-                count[nn] = count.get(nn, 0) + 1
+                for cn, g in pod_claims(o).items():
+                    used[cn] = used.get(cn, 0) + g
+                    count[cn] = count.get(cn, 0) + 1
         for pod in sorted(pending, key=lambda o: o["metadata"]["name"]):
             need = pod_gpus(pod)
             sel = pod["spec"].get("nodeSelector")
+            key = _key(pid, pod["metadata"]["namespace"], pod["metadata"]["name"])
+            if (pod["metadata"].get("annotations") or {}).get(GPU_SCOPE) == "host" and need > 0:
+                self._schedule_host_scoped(pid, pod, key, need, sel, nodes, used, count)
+                continue
             best = None
             for n in nodes:
                 nn = n["metadata"]["name"]
@@ -36,22 +70,64 @@ class Scheduler:
                 score = (count.get(nn, 0), -free, nn)
                 if best is None or score < best[0]:
                     best = (score, nn, free)
-            key = _key(pid, pod["metadata"]["namespace"], pod["metadata"]["name"])
             if best is None:
-                c = _cond(pod, "PodScheduled")
-                if not c or c["status"] != "False":
-                    self.store.patch("pods", key, lambda o, need=need: _set_cond(
-                        o, "PodScheduled", "False", "Unschedulable", f"0/{len(nodes)} nodes available: need {need} {GPU}"))
+                self._unschedulable(pod, key, f"0/{len(nodes)} nodes available: need {need} {GPU}")
                 continue
             nn = best[1]
             used[nn] = used.get(nn, 0) + need
             count[nn] = count.get(nn, 0) + 1
+            self._bind(pid, pod, key, nn)
 
-            def bind(o, nn=nn):
-                o["spec"]["nodeName"] = nn
-                _set_cond(o, "PodScheduled", "True", "Scheduled", f"assigned to {nn}")
+    def _unschedulable(self, pod: dict, key: str, msg: str) -> None:
+        c = _cond(pod, "PodScheduled")
+        if not c or c["status"] != "False" or c.get("message") != msg:
+            self.store.patch("pods", key, lambda o: _set_cond(o, "PodScheduled", "False", "Unschedulable", msg))
 
-            self.store.patch("pods", key, bind)
-            self._event(pid, pod["metadata"]["namespace"], {"kind": "Pod", "name": pod["metadata"]["name"]},
-                        "Scheduled", f"Successfully assigned {pod['metadata']['name']} to {nn}")
+    def _bind(self, pid: str, pod: dict, key: str, nn: str, annotations: dict | None = None) -> None:
+        def bind(o, nn=nn):
+            o["spec"]["nodeName"] = nn
+            if annotations:
+                o["metadata"].setdefault("annotations", {}).update(annotations)
+            _set_cond(o, "PodScheduled", "True", "Scheduled", f"assigned to {nn}")
 
+        self.store.patch("pods", key, bind)
+        self._event(pid, pod["metadata"]["namespace"], {"kind": "Pod", "name": pod["metadata"]["name"]},
+                    "Scheduled", f"Successfully assigned {pod['metadata']['name']} to {nn}")
+
+    def _schedule_host_scoped(self, pid: str, pod: dict, key: str, need: int, sel, nodes: list[dict],
+                              used: dict, count: dict) -> None:
+        hosts: dict[str, list[dict]] = {}
+        for n in nodes:
+            nn = n["metadata"]["name"]
+            alloc = int(n["status"]["allocatable"].get(GPU, 0))
+            # whole idle validated GPU nodes only: the leader's process opens every device of each
+            if (alloc > 0 and used.get(nn, 0) == 0 and node_validated(n)
+                    and labels_match(sel, n["metadata"].get("labels"))):
+                hosts.setdefault((n["metadata"].get("labels") or {}).get(HOST_LABEL, f"node:{nn}"), []).append(n)
+        for host in sorted(hosts):
+            members = sorted(hosts[host], key=lambda n: (-int(n["status"]["allocatable"].get(GPU, 0)), n["metadata"]["name"]))
+            chosen, total = [], 0
+            for n in members:
+                g = int(n["status"]["allocatable"].get(GPU, 0))
+                if total + g <= need:
+                    chosen.append(n)
+                    total += g
+                if total == need:
+                    break
+            if total != need:
+                continue
+            leader = chosen[0]["metadata"]["name"]
+            claims = {n["metadata"]["name"]: int(n["status"]["allocatable"].get(GPU, 0)) for n in chosen}
+            devices = [{"node": n["metadata"]["name"], "id": d["id"], "ordinal": d.get("ordinal"),
+                        "renderMinor": d.get("renderMinor", -1)}
+                       for n in chosen[1:] for d in (n.get("status", {}).get("devices") or [])
+                       if d.get("health") == "Healthy"]
+            for cn, g in claims.items():
+                used[cn] = used.get(cn, 0) + g
+                count[cn] = count.get(cn, 0) + 1
+            self._bind(pid, pod, key, leader, {HOST_CLAIMS: json.dumps(claims, sort_keys=True),
+                                               HOST_DEVICES: json.dumps(devices, sort_keys=True),
+                                               HOST_LABEL: host})
+            return
+        self._unschedulable(pod, key, f"no host has idle GPU nodes adding up to {need} {GPU} "
+                                      f"({GPU_SCOPE}: host)")

@@ -54,11 +54,20 @@ def _loads(text: str):
 # ---- shared helpers (re-exported by models/hostinfo.py, provider/hostreg.py, orchestrator.py) ----
 def probe_tool(peers: bool = False) -> str:
     """The validation payload binary: ``tk8s-hsaprobe`` (the same kernels and checks dispatched on
-    ROCr directly, ~20 ms less start-up than HIP, native/tools/tk8s_hsaprobe.cpp; its --peers
-    pulls every ordered GPU pair over xGMI) unless ``TK8S_PROBE_RUNTIME=hip`` says otherwise or
-    its code objects are missing: then ``tk8s-probe`` (HIP, the same checks and JSON)."""
+    ROCr directly, ~20 ms less start-up than HIP, native/tools/tk8s_hsaprobe.cpp) unless
+    ``TK8S_PROBE_RUNTIME=hip`` says otherwise or its code objects are missing: then ``tk8s-probe``
+    (HIP, the same checks and JSON).
+
+    With xGMI pulls (``peers``: two or more GPUs) the HIP probe runs unless
+    ``TK8S_PEERS_RUNTIME=hsa``: peer access through ``hipDeviceEnablePeerAccess`` is the path
+    RCCL's own P2P transport takes, while the HSA probe's peer grants
+    (``hsa_amd_agents_allow_access`` on another GPU's VRAM) have not yet run on a multi-GPU box --
+    a fault there would stop every multi-GPU bring-up. One-GPU bring-ups keep the
+    faster HSA start."""
     hsa = os.path.join(BIN, "tk8s-hsaprobe")
     lib = os.path.join(PKG, "lib")
+    if peers and os.environ.get("TK8S_PEERS_RUNTIME", "hip") != "hsa":
+        return os.path.join(BIN, "tk8s-probe")
     if (os.environ.get("TK8S_PROBE_RUNTIME", "hsa") != "hip" and os.access(hsa, os.X_OK)
             and os.path.exists(os.path.join(lib, "tk8s_stream.co")) and os.path.exists(os.path.join(lib, "tk8s_md5.co"))):
         return hsa
@@ -83,6 +92,9 @@ def host_burnin_command(command: list[str], gpus: list[int]) -> list[str]:
     cmd = [str(a) for a in command]
     if len(gpus) > 1 and "--peers" not in cmd:
         cmd.append("--peers")
+        hip = probe_tool(peers=True)
+        if cmd and os.path.basename(cmd[0]) == "tk8s-hsaprobe" and os.path.basename(hip) != "tk8s-hsaprobe":
+            cmd[0] = hip  # the pulls take the HIP peer path (probe_tool)
     return cmd
 
 

@@ -1,6 +1,6 @@
 """The cluster's RCCL fabric check (BASELINE.json configs 4-5): after every node is Ready, an
-Indexed Job all-reduces over every GPU -- one pod per GPU node, its process driving the node's
-GPUs as consecutive ranks -- and checks the result exactly; ``--rocprof`` runs the ranks under
+Indexed Job all-reduces over every GPU -- one pod per physical host, its process driving all of
+the host's GPUs as consecutive ranks (rccl_layout) -- and checks the result exactly; ``--rocprof`` runs the ranks under
 rocprofv3 (kernel trace + stats, or one counter pass). The reference's readiness oracle was a
 curl of the dashboard (setup.sh:56-85); this is the data-plane check that replaces it.
 
@@ -19,18 +19,35 @@ from .workspace import SetupError, pod_portable
 
 class FabricCheck:
     @staticmethod
-    def rccl_gpus_per_pod(k, g: int) -> int:
-        """GPUs per fabric-Job pod: every GPU of its node when the GPU nodes are uniform (one
-        process -- one runtime start -- per node, its GPUs as consecutive ranks), else 1."""
+    def rccl_layout(k, g: int) -> dict:
+        """Shape of the fabric Job: ONE pod per physical host (node label ``tk8s.amd.com/host``),
+        its one process driving every GPU of the host as consecutive ranks -- one runtime start
+        and one communicator init per host instead of one per node (8 one-GPU
+        workers on one host were 8 rank processes). Several nodes on a host: the pod is
+        host-scoped (``tk8s.amd.com/gpu-scope: host``, scheduler.py claims the other nodes' GPUs).
+        Hosts must carry equal GPU counts (one Indexed Job, equal shares); else one pod per node
+        when nodes are uniform, else one per GPU."""
         try:
             nodes = k.get("/api/v1/nodes").get("items", [])
         except Exception:  # noqa: BLE001 - the per-GPU shape works whatever the nodes say
-            return 1
-        counts = [int((n.get("status", {}).get("allocatable") or {}).get("amd.com/gpu", 0) or 0) for n in nodes]
-        counts = [c for c in counts if c > 0]
+            return {"per_pod": 1, "scope": "node"}
+        per_node = {n["metadata"]["name"]: int((n.get("status", {}).get("allocatable") or {}).get("amd.com/gpu", 0) or 0)
+                    for n in nodes}
+        per_node = {nn: c for nn, c in per_node.items() if c > 0}
+        hosts: dict[str, int] = {}
+        for n in nodes:
+            nn = n["metadata"]["name"]
+            if nn in per_node:
+                h = (n["metadata"].get("labels") or {}).get("tk8s.amd.com/host") or f"node:{nn}"
+                hosts[h] = hosts.get(h, 0) + per_node[nn]
+        if hosts and len(set(hosts.values())) == 1 and sum(hosts.values()) == g:
+            nodes_per_host = len(per_node) // len(hosts)
+            return {"per_pod": next(iter(hosts.values())), "scope": "host" if nodes_per_host > 1 else "node",
+                    "hosts": len(hosts)}
+        counts = list(per_node.values())
         if counts and len(set(counts)) == 1 and counts[0] * len(counts) == g:
-            return counts[0]
-        return 1
+            return {"per_pod": counts[0], "scope": "node"}
+        return {"per_pod": 1, "scope": "node"}
 
     def run_rccl(self) -> dict | None:
         from .controlplane.client import client_from_kubeconfig
@@ -47,7 +64,8 @@ class FabricCheck:
         pid = self.project_id()
         k = client_from_kubeconfig(c.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"}))
         job = f"rccl-allreduce-{int(time.time() * 1000) % 10**9:x}"
-        per_pod = self.rccl_gpus_per_pod(k, g)
+        layout = self.rccl_layout(k, g)
+        per_pod = layout["per_pod"]
         npods = g // per_pod
         # one process per node drives all of that node's GPUs (ranks index*k .. index*k+k-1)
         group = ["--group-index", "$(JOB_COMPLETION_INDEX)", "--devices", "$(TK8S_GPU_DEVICES)", "--nranks", str(g)]
@@ -79,9 +97,11 @@ class FabricCheck:
                 cmd = [rp, *pmc, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
                        "--output-format", "csv", "--", *cmd]
         objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
-                              {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd})
+                              {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd,
+                               "gpu_scope": layout["scope"]})
         apply_objects(k, objs)
-        self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job}, {npods} pod(s) x {per_pod} GPU(s))")
+        self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job}, {npods} pod(s) x {per_pod} GPU(s)"
+                 + (", one process per host" if layout["scope"] == "host" else "") + ")")
         left = max(10.0, self.rccl_timeout or self.timeout)
         try:
             j = wait_job(k, job, "kube-system", timeout=left)
@@ -92,7 +112,8 @@ class FabricCheck:
         peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)
         ok = j["status"].get("succeeded", 0) >= npods and all(r.get("ok") for r in results)
         first = next((r for r in results if r), {})
-        rep = {"job": job, "ok": ok, "nranks": g, "pods": npods, "gpus_per_pod": per_pod, "peak_busbw_gbps": peak,
+        rep = {"job": job, "ok": ok, "nranks": g, "pods": npods, "gpus_per_pod": per_pod, "scope": layout["scope"],
+               "peak_busbw_gbps": peak,
                "tuning": {k: first.get(k) for k in ("nccl_algo", "nccl_proto", "nccl_min_nchannels",
                                                     "nccl_max_nchannels", "peak_links_equivalent") if k in first},
                "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),

@@ -301,13 +301,18 @@ class LocalProvider(Provider):
         return out
 
     def machine_env(self, m: Machine) -> dict[str, str]:
-        return {
+        env = {
             "TK8S_MACHINE": m.name,
             "TK8S_MACHINE_DIR": m.sandbox,
             "TK8S_MACHINE_IP": m.primaryip,
             "TK8S_MACHINE_GPUS": ",".join(map(str, m.gpus)),
             "TK8S_MACHINE_PACKAGE": m.package,
         }
+        fake_hosts = int(os.environ.get("TK8S_FAKE_HOSTS", "0") or 0)
+        if fake_hosts > 1:  # CPU tests: pretend the machines are spread over that many hosts
+            digits = "".join(ch for ch in m.name if ch.isdigit()) or "0"
+            env["TK8S_HOST_ID"] = f"fakehost{(int(digits) - 1) % fake_hosts}"
+        return env
 
     def ansible_host_vars(self, m: Machine) -> dict:
         """Inventory variables for stock ansible-playbook: the machines are sandboxes of this host,

@@ -190,6 +190,11 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if force or _stale(reuse_bin, [reuse_src]):
         _run([CXX, "-O2", "-std=c++17", "-Wall", str(reuse_src), "-o", str(reuse_bin)], verbose)
 
+    jail_src = NATIVE / "tools" / "tk8s_gpujail.cpp"
+    jail = tool_path("tk8s-gpujail")
+    if force or _stale(jail, [jail_src]):
+        _run([CXX, "-O2", "-std=c++17", "-Wall", "-Wextra", str(jail_src), "-o", str(jail)], verbose)
+
     sup_src = NATIVE / "tools" / "tk8s_supervise.cpp"
     sup = tool_path("tk8s-supervise")
     if force or _stale(sup, [sup_src]):
@@ -213,6 +218,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
     precompile_python()
     out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,
+           "tk8s-gpujail": jail,
            "tk8s-smi": smi, "tk8s-reuse": reuse_bin, "tk8s-hsaprobe": hsa_bin, **cos}
     out.update({n: tool_path(n) for n in TOOLS})
     return out

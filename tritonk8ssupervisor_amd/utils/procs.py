@@ -30,8 +30,38 @@ def spawn_daemon(argv: list[str], *, env: dict | None = None, cwd: str | None = 
         Path(pidfile).parent.mkdir(parents=True, exist_ok=True)
         from .fsutil import atomic_write_json
 
-        atomic_write_json(pidfile, {"pid": p.pid, "pgid": p.pid, "argv": argv, "started": time.time()})
+        atomic_write_json(pidfile, {"pid": p.pid, "pgid": p.pid, "argv": argv, "started": time.time(),
+                                    "start": proc_start_ticks(p.pid)})
     return p
+
+
+def proc_start_ticks(pid: int) -> int | None:
+    """When the process started (``/proc/<pid>/stat`` field 22, clock ticks since boot): with the
+    pid, an identity that a reused pid does not share. None if there is no such process."""
+    try:
+        with open(f"/proc/{int(pid)}/stat") as f:
+            return int(f.read().rsplit(")", 1)[1].split()[19])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def pidfile_owner_alive(info: dict) -> bool:
+    """Is the process a pidfile names still the one that wrote it? Its recorded start time must
+    match; a pidfile without one (written by an older tk8s) must name a tk8s process. A pidfile
+    that outlived a reboot or a failed run must never get an unrelated process group signalled
+    (ADVICE r2)."""
+    pid = int(info.get("pid") or 0)
+    now = proc_start_ticks(pid) if pid > 0 else None
+    if now is None:
+        return False
+    if info.get("start") is not None:
+        return int(info["start"]) == now
+    try:
+        with open(f"/proc/{pid}/cmdline", "rb") as f:
+            cmd = f.read().replace(b"\0", b" ")
+    except OSError:
+        return False
+    return any(k in cmd for k in (b"tk8s", b"tritonk8ssupervisor"))
 
 
 def pid_alive(pid: int) -> bool:
@@ -107,8 +137,16 @@ def kill_group(pgid: int, grace: float = 3.0) -> bool:
 
 
 def kill_pidfile(pidfile: str | os.PathLike, grace: float = 3.0) -> bool:
+    """Stop the process group a pidfile names -- only if its process is still the one that wrote
+    the pidfile (pidfile_owner_alive); a stale pidfile is just removed."""
     info = read_pidfile(pidfile)
-    if not info:
+    if isinstance(info, int):  # a bare pid (the burn-in's)
+        info = {"pid": info}
+    if not isinstance(info, dict) or not info.get("pid"):
+        return False
+    if not pidfile_owner_alive(info):
+        with contextlib.suppress(FileNotFoundError):
+            Path(pidfile).unlink()
         return False
     alive = kill_group(int(info.get("pgid") or info["pid"]), grace)
     with contextlib.suppress(FileNotFoundError):
