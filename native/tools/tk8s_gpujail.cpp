@@ -1,7 +1,7 @@
 // tk8s-gpujail: run a pod's command so that it can open only the GPUs it was allocated.
 //
-//   tk8s-gpujail [--allow-node N]... [--allow-render M]... [--kfd-root DIR] [--dri-root DIR]
-//                [--best-effort] -- CMD ARGS...
+//   tk8s-gpujail [--allow-render M]... [--dri-root DIR] [--hide-topology [--allow-node N]...
+//                [--kfd-root DIR]] [--best-effort] -- CMD ARGS...
 //   tk8s-gpujail --probe            (prints {"landlock_abi": N, ...}; exit 0 when usable)
 //
 // The reference ran every workload in a Docker container (ansible/roles/rancherhost/tasks/
@@ -11,15 +11,18 @@
 // GPU tier run as an ordinary user; user namespaces are off on the GPU hosts):
 //
 //   Landlock (kernel >= 5.13) restricts READ_FILE / WRITE_FILE for this process and everything it
-//   starts, permanently. Granted: every path of the file system EXCEPT the KFD topology nodes of
-//   the GPUs that are not the pod's (/sys/devices/virtual/kfd/kfd/topology/nodes/<n>) and the DRM
-//   device nodes of those GPUs (/dev/dri/renderD<m>, card*). Landlock rules can only grant, so the
-//   exceptions are carved out by granting each sibling along the way from / to them.
+//   starts, permanently. Granted: every path of the file system EXCEPT the DRM device nodes of the
+//   GPUs that are not the pod's (/dev/dri/renderD<m>, card*). Landlock rules can only grant, so
+//   the exceptions are carved out by granting each sibling along the way from / to them.
 //
-// ROCr's thunk enumerates the topology nodes and skips a GPU whose node it cannot read or whose
-// render node it cannot open (the same way it runs in a container given a subset of /dev/dri),
-// so the pod's runtime sees exactly its GPUs whatever its *_VISIBLE_DEVICES say; and without the
-// render node no process can map another GPU's memory or queues through /dev/kfd.
+// ROCr's thunk skips a GPU whose render node it cannot open (as in a container given a subset of
+// /dev/dri), so the pod's runtime sees exactly its GPUs whatever its *_VISIBLE_DEVICES say; and
+// without the render node no process can acquire a GPU VM for that device through /dev/kfd, i.e.
+// map its memory or create queues on it. The KFD topology in sysfs stays readable, as in a
+// container: measured on the MI355X box with ROCm 7.2 (profiles/r3_gpujail/), denying a GPU's
+// topology node makes the thunk fail its whole start (HSA_STATUS_ERROR_OUT_OF_RESOURCES) even for
+// the allowed GPUs, while a denied render node is skipped cleanly. --hide-topology adds the
+// topology nodes anyway (for runtimes that skip them).
 //
 // The child's environment gets TK8S_GPU_ISOLATION=landlock:abi<N> (or none:<why> under
 // --best-effort when Landlock is unavailable; without --best-effort that is exit 125).
@@ -129,8 +132,8 @@ struct Jail {
 
 int usage() {
   std::fprintf(stderr,
-               "usage: tk8s-gpujail [--allow-node N]... [--allow-render M]... [--kfd-root DIR] [--dri-root DIR]\n"
-               "                    [--best-effort] -- CMD ARGS...\n       tk8s-gpujail --probe\n");
+               "usage: tk8s-gpujail [--allow-render M]... [--dri-root DIR] [--hide-topology [--allow-node N]...\n"
+               "                    [--kfd-root DIR]] [--best-effort] -- CMD ARGS...\n       tk8s-gpujail --probe\n");
   return 2;
 }
 
@@ -139,7 +142,7 @@ int usage() {
 int main(int argc, char** argv) {
   std::set<long> allow_nodes, allow_render;
   std::string kfd_root = "/sys/devices/virtual/kfd/kfd/topology/nodes", dri_root = "/dev/dri";
-  bool best_effort = false, probe = false;
+  bool best_effort = false, probe = false, hide_topology = false;
   int i = 1;
   for (; i < argc; ++i) {
     const std::string a = argv[i];
@@ -154,6 +157,7 @@ int main(int argc, char** argv) {
       else if (a == "--kfd-root") kfd_root = next();
       else if (a == "--dri-root") dri_root = next();
       else if (a == "--best-effort") best_effort = true;
+      else if (a == "--hide-topology") hide_topology = true;
       else if (a == "--probe") probe = true;
       else return usage();
     } catch (const std::exception& e) {
@@ -179,7 +183,7 @@ int main(int argc, char** argv) {
   } else {
     // what this pod must not open: the other GPUs' topology nodes and DRM device nodes
     std::set<std::string> deny;
-    const std::string kroot = real(kfd_root);
+    const std::string kroot = hide_topology ? real(kfd_root) : std::string();
     if (!kroot.empty()) {
       for (const auto& n : list_dir(kroot)) {
         char* end = nullptr;

@@ -86,3 +86,15 @@ def test_argument_errors_are_ansible_errors(tmp_path):
 def test_burnin_module_without_gpus_is_a_noop(tmp_path):
     rc, out = _run("tk8s_burnin", {"machine_dir": str(tmp_path / "m"), "command": ["true"]}, tmp_path)
     assert rc == 0 and out.get("skipped") and "no GPUs" in out["msg"]
+
+
+def test_library_files_are_the_generated_front_ends():
+    """the five front ends are one template (ansible_bridge.LIBRARY_TEMPLATE) rendered
+    per module; the shipped files must be exactly that output (regenerate with
+    `python -m tritonk8ssupervisor_amd.ansible_bridge --write-library`)."""
+    from tritonk8ssupervisor_amd.ansible_bridge import library_sources
+
+    gen = library_sources()
+    assert set(gen) == {p.stem for p in LIB.glob("tk8s_*.py")}
+    for name, text in gen.items():
+        assert (LIB / f"{name}.py").read_text() == text, name

@@ -109,6 +109,73 @@ def run(module_name: str, params: dict, check_mode: bool) -> dict:
                       variables={})
 
 
+# ---- ansible/library/<module>.py, generated -------------------------------------------------
+# Ansible needs one file per module; every one is the same front end, rendered from LIBRARY_TEMPLATE
+# (``python -m tritonk8ssupervisor_amd.ansible_bridge --write-library``; tests/test_ansible_library.py
+# checks the shipped files are exactly this output).
+SHORT_DESCRIPTIONS = {
+    "tk8s_build": "Build the tk8s native validation stack for gfx950 in place (replaces the docker-engine install)",
+    "tk8s_burnin": "Start the early GPU burn-in on this machine's MI355X GPUs (one-shot daemon, result shared with the validation pod)",
+    "tk8s_daemon": "Start, stop or query a supervised long-running process on this machine (the reference's docker_container rancher/server and docker run rancher/agent)",
+    "tk8s_gpu_facts": "ROCm / KFD / GPU facts of this machine, read from sysfs without initialising the GPU (replaces the docker --version probe)",
+    "tk8s_kube": "Create, delete or wait for Kubernetes objects through the tk8s control plane",
+}
+
+LIBRARY_TEMPLATE = '''#!/usr/bin/python
+# -*- coding: utf-8 -*-
+# GENERATED by tritonk8ssupervisor_amd/ansible_bridge.py (--write-library): edit the template there.
+"""Ansible module {name}: {short}.
+
+Real-Ansible front end of the in-repo playbook engine's module of the same name: it runs on the
+target machine, finds that machine's tk8s install ($TK8S_HOME, or the newest ~/.tk8s/dist/<digest>
+the baremetal/triton providers push) and calls the shared implementation
+(tritonk8ssupervisor_amd/ansible_bridge.py -> playbook_modules.py). Arguments: ansible_bridge.ARG_SPECS.
+"""
+import glob
+import os
+import sys
+
+DOCUMENTATION = r"""
+module: {name}
+short_description: {short}
+description: see tritonk8ssupervisor_amd/ansible_bridge.py (ARG_SPECS) and playbook_modules.py
+"""
+
+
+def _home():
+    cands = [os.environ.get("TK8S_HOME", "")]
+    cands += sorted(glob.glob(os.path.expanduser("~/.tk8s/dist/*")), key=os.path.getmtime, reverse=True)
+    for c in cands:
+        if c and os.path.isdir(os.path.join(c, "tritonk8ssupervisor_amd")):
+            return c
+    return None
+
+
+if __name__ == "__main__":
+    home = _home()
+    if home and home not in sys.path:
+        sys.path.insert(0, home)
+    from tritonk8ssupervisor_amd.ansible_bridge import main
+
+    main("{name}")
+'''
+
+
+def library_sources() -> dict[str, str]:
+    """{module name: the text of ansible/library/<name>.py}, one per ARG_SPECS entry."""
+    return {n: LIBRARY_TEMPLATE.format(name=n, short=SHORT_DESCRIPTIONS[n]) for n in sorted(ARG_SPECS)}
+
+
+def write_library(directory: str | os.PathLike) -> list[str]:
+    out = []
+    for name, text in library_sources().items():
+        p = Path(directory) / f"{name}.py"
+        p.write_text(text)
+        p.chmod(0o755)
+        out.append(str(p))
+    return out
+
+
 def main(module_name: str) -> None:
     """Entry point of ansible/library/<module_name>.py (after it put the tk8s install on sys.path)."""
     from ansible.module_utils.basic import AnsibleModule  # provided by Ansible on the target
@@ -131,3 +198,8 @@ def bootstrap(module_name: str, argv_home: str | None = None) -> None:
     if home and home not in sys.path:
         sys.path.insert(0, home)
     main(module_name)
+
+
+if __name__ == "__main__" and "--write-library" in sys.argv:
+    for f in write_library(Path(__file__).resolve().parents[1] / "ansible" / "library"):
+        print(f)

@@ -334,6 +334,7 @@ def controlplane_zygote(p: dict) -> dict | None:
     os.makedirs(os.path.join(sb, "run"), exist_ok=True)
     os.makedirs(os.path.join(sb, "logs"), exist_ok=True)
     args = os.path.join(sb, "run", "controlplane.args")
+    _mark_zygote(os.path.join(sb, "run", "controlplane.zygote"))
     argv = [sup, "--pidfile", pidfile, "--log", os.path.join(sb, "logs", "controlplane.log"), "--restart",
             "unless-stopped", "--", sys.executable, "-S", "-c", "import tritonk8ssupervisor_amd.controlplane.__main__",
             "--await-args", args]
@@ -345,6 +346,14 @@ def controlplane_zygote(p: dict) -> dict | None:
         (os.POSIX_SPAWN_OPEN, 2, os.devnull, os.O_WRONLY, 0),
     ])
     return {"pid": pid, "sandbox": sb, "args": args, "pidfile": pidfile}
+
+
+def _mark_zygote(path: str) -> None:
+    """``run/<daemon>.zygote``: this daemon's process is a zygote until ``run/<daemon>.args`` is
+    written -- the mark that lets the playbook's daemon module replace one nobody ever handed its
+    arguments (playbook_modules._orphaned_zygote)."""
+    with open(path, "w") as f:
+        f.write(f"{os.getpid()}\n")
 
 
 AGENT_ENTRY = "import tritonk8ssupervisor_amd.agent.__main__"  # = workspace.AGENT_ENTRY
@@ -377,6 +386,7 @@ def agent_zygotes(p: dict) -> None:
                 os.makedirs(os.path.join(sb, "run"), exist_ok=True)
                 os.makedirs(os.path.join(sb, "logs"), exist_ok=True)
                 args = os.path.join(sb, "run", "agent.args")
+                _mark_zygote(os.path.join(sb, "run", "agent.zygote"))
                 argv = [sup, "--pidfile", pidfile, "--log", os.path.join(sb, "logs", "agent.log"), "--restart",
                         "unless-stopped", "--", sys.executable, "-S", "-c", AGENT_ENTRY, "--await-args", args]
                 pid = os.posix_spawn(sup, argv, env, setsid=True, file_actions=[
@@ -439,6 +449,14 @@ def _release(pre: tuple[int, int, str] | None) -> None:
     threading.Thread(target=Spawned(pre[1]).wait, name="preload-reap", daemon=True).start()
 
 
+def _kill_preloaded(pre: tuple[int, int, str]) -> None:
+    try:
+        os.kill(pre[1], 9)
+        os.waitpid(pre[1], 0)
+    except OSError:
+        pass
+
+
 def _send_plan(pre: tuple[int, int, str], cmd: list[str], env: dict, log: str) -> bool:
     lines = [f"ARG {a}" for a in cmd[1:]] + [f"ENV {k}={v}" for k, v in env.items()] + [f"LOG {log}", "GO"]
     if any("\n" in ln for ln in lines):
@@ -478,6 +496,8 @@ def launch(argv: list[str]) -> Early | None:
         log = os.path.join(run, "host-burnin.log")
         import time
 
+        if pre is not None and os.environ.get("TK8S_FAULTS", "").find("preload.kill") >= 0:
+            _kill_preloaded(pre)  # fault injection (tests/test_startup_fallbacks.py): dead before the plan
         if pre is not None and os.path.realpath(pre[2]) == os.path.realpath(cmd[0]) and _send_plan(pre, cmd, vis, log):
             pid = pre[1]  # the preloaded probe: same binary, same environment plus the plan's
         else:

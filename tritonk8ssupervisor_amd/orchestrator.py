@@ -31,6 +31,7 @@ from .provider import get_provider
 from .provider.base import Machine, ProvisionError
 from .provision import Engine
 from .utils.events import EventLog
+from .utils.faults import fault
 from .utils.fsutil import atomic_write, atomic_write_json, read_json
 from .utils.procs import kill_pidfile, pid_alive
 from .workspace import (  # noqa: F401 - the orchestrator's public names, re-exported
@@ -193,6 +194,8 @@ class Setup(KubeadmPlatform, FabricCheck):
         from . import earlyburn
 
         z = earlyburn.agent_zygote_for(m.sandbox)  # its interpreter started with the CLI: hand it the arguments
+        if z is not None and fault("zygote.no_args", m.name) is not None:
+            return  # fault injection: the zygote is never handed its arguments (rocmsetup recovers)
         if z is not None:
             if pid_alive(z["pid"]):
                 env = {**getattr(self.provider, "machine_env", lambda _m: {})(m), "PYTHONPATH": pythonpath}
@@ -219,6 +222,8 @@ class Setup(KubeadmPlatform, FabricCheck):
         from . import earlyburn
 
         z = earlyburn.zygote_for(m.sandbox)  # its interpreter started with the CLI: hand it the arguments
+        if z is not None and fault("zygote.no_args", m.name) is not None:
+            return  # fault injection: the zygote is never handed its arguments (ranchermaster recovers)
         if z is not None:
             if pid_alive(z["pid"]):  # its supervisor (a child of this process)
                 atomic_write(z["args"], json.dumps(argv[4:]))

@@ -578,6 +578,12 @@ def m_tk8s_daemon(args, *, ctx, target, local, env, check, **_):
             return {"changed": status["running"], "running": False}
         ex.stop_daemon(target.name, name)
         return {"changed": True, "running": False}
+    if status["running"] and not check and _orphaned_zygote(ex, target.name, name):
+        # an interpreter started early for this daemon (earlyburn zygote) that its boot hook never
+        # handed its arguments: it would wait forever. Stop it and start the daemon the plain way
+        # below -- slower by the zygote's head start, but correct.
+        ex.stop_daemon(target.name, name)
+        status = {"running": False}
     if status["running"]:
         if args.get("wait_for_log") and not check and hasattr(ex, "wait_log"):
             info = ex.wait_log(target.name, name, str(args["wait_for_log"]), float(args.get("timeout", 300)))
@@ -596,6 +602,16 @@ def m_tk8s_daemon(args, *, ctx, target, local, env, check, **_):
     if not info.get("ok"):
         return {"failed": True, "msg": info.get("msg", "daemon failed to start"), **info}
     return {"changed": True, "running": True, **info}
+
+
+def _orphaned_zygote(ex, host: str, name: str) -> bool:
+    """The running ``name`` daemon is a zygote (earlyburn: ``run/<name>.zygote``) still waiting for
+    the ``run/<name>.args`` its boot hook should have written."""
+    fs = getattr(ex, "fs", None)
+    if fs is None:
+        return False
+    f = fs(host)
+    return f.read(f"run/{name}.zygote") is not None and f.read(f"run/{name}.args") is None
 
 
 def m_tk8s_burnin(args, *, ctx, target, local, env, check, **_):

@@ -28,6 +28,33 @@ from .utils.faults import _parse
 
 DEFAULT_FRACTION = 0.5
 
+# Link figures the floors below derive from: every MI355X has 7 point-to-point
+# xGMI links of 153.6 GB/s each, counted both ways, i.e. 76.8 GB/s per direction; on an 8-GPU
+# node they connect every pair directly. PCIe Gen5 x16 -- the fallback a misconfigured node
+# would use for peer traffic -- moves at most 64 GB/s per direction.
+XGMI_LINK_GBPS_PER_DIRECTION = 76.8
+XGMI_LINKS_PER_GPU = 7
+PCIE_GEN5_X16_GBPS = 64.0
+
+
+def fabric_floors(n: int) -> dict[str, float]:
+    """What an n-GPU xGMI fabric must at least reach, per check (the gated multi-GPU tests use
+    these; VERDICT r2 weak #6 -- fixed 40-50 GB/s floors were cleared by a PCIe fallback too):
+
+    * ``allreduce_busbw_gbps``: a ring all-reduce's busbw is bound by the links each GPU can use
+      at once, min(n - 1, 7) direct links. Floor: a quarter of that bound, and -- from 3 GPUs on,
+      where it can -- above anything one PCIe Gen5 x16 link could carry (x1.1). At n = 2 the
+      single link cannot be told from PCIe by rate alone: the transport check (P2P over xGMI,
+      no SHM / NET channels) and the KFD link type do that.
+    * ``peer_pull_gbps``: one directed link, pulled by a kernel: half its per-direction rate.
+    """
+    links = max(1, min(n - 1, XGMI_LINKS_PER_GPU))
+    busbw = 0.25 * XGMI_LINK_GBPS_PER_DIRECTION * links
+    if n >= 3:
+        busbw = max(busbw, 1.1 * PCIE_GEN5_X16_GBPS)
+    return {"allreduce_busbw_gbps": round(busbw, 1), "peer_pull_gbps": round(0.5 * XGMI_LINK_GBPS_PER_DIRECTION, 1),
+            "links_per_gpu": links}
+
 
 def min_fraction() -> float:
     try:
