@@ -51,7 +51,7 @@ PYBIND11_MODULE(_tk8s_native, m) {
   m.def("md5_probe", &tk8s::md5_probe, py::arg("bytes"), py::arg("chunk_bytes") = 1024,
         py::arg("seed") = 0, py::arg("iters") = 10, py::arg("device") = 0, G());
   m.def("copy_probe", &tk8s::copy_probe, py::arg("src_device"), py::arg("dst_device"),
-        py::arg("bytes"), py::arg("iters") = 10, G());
+        py::arg("bytes"), py::arg("iters") = 10, py::arg("dma") = true, G());
   m.def(
       "rccl_allreduce",
       [](const std::vector<int>& devices, size_t min_bytes, size_t max_bytes, int factor,

@@ -27,7 +27,8 @@ std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int ite
 
 // N7: copy bandwidth from device src to device dst (src == dst: local D2D copy). Kernel pull
 // over xGMI (peer access enabled) and the SDMA engine path (hipMemcpyPeerAsync).
-std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters);
+// dma: also time the SDMA-engine path (hipMemcpyPeerAsync) for a peer copy.
+std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, bool dma = true);
 
 // The local probes share one grow-on-demand device allocation per device (see probes.cpp);
 // free them (e.g. from a long-lived process once validation is done).

@@ -326,7 +326,7 @@ std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int ite
   }
 }
 
-std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters) {
+std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, bool dma) {
   try {
     if (bytes % 16 || bytes == 0) return error_json("bytes must be a positive multiple of 16");
     iters = std::max(iters, 1);
@@ -383,7 +383,8 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters) 
     // checking); locally it measured nothing the kernel copy does not, and bringing up the
     // copy engine cost ~10 ms of the validation's critical path.
     float dma_ms = 0.f;
-    if (peer) {
+    dma = dma && peer;
+    if (dma) {
       dt.start(st.s);
       for (int i = 0; i < iters; ++i)
         TK8S_HIP_CHECK(hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, st.s));
@@ -400,7 +401,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters) 
         .kv("iters", iters)
         .kv("kernel_ms", static_cast<double>(kernel_ms))
         .kv("kernel_gbps", bytes / (kernel_ms * 1e-3) / 1e9);
-    if (peer) j.kv("dma_ms", static_cast<double>(dma_ms)).kv("dma_gbps", bytes / (dma_ms * 1e-3) / 1e9);
+    if (dma) j.kv("dma_ms", static_cast<double>(dma_ms)).kv("dma_gbps", bytes / (dma_ms * 1e-3) / 1e9);
     return j.kv("bad_words", static_cast<uint64_t>(nbad)).str();
   } catch (const std::exception& ex) {
     return error_json(ex.what());

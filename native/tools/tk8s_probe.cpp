@@ -3,7 +3,7 @@
 // (local copy, and xGMI peer pulls with --peers) and prints ONE JSON object.
 //
 //   tk8s-probe [--device D | --all-devices] [--gpuinfo] [--peers] [--hbm-bytes B]
-//              [--md5-bytes B] [--chunk C] [--seed S] [--copy-bytes B] [--peer-bytes B]
+//              [--md5-bytes B] [--chunk C] [--seed S] [--copy-bytes B] [--peer-bytes B] [--no-peer-dma]
 //              [--iters K] [--mode plain|nontemporal] [--skip-md5]
 //              [--out FILE] [--reuse FILE [--reuse-wait S]]
 //
@@ -145,14 +145,16 @@ int main(int argc, char** argv) {
       r.ok = ok_of(r.hbm) && (r.md5.empty() || ok_of(r.md5)) && (r.copy.empty() || ok_of(r.copy));
       t = std::chrono::steady_clock::now();
       if (a.has("peers"))
-        for (int s : devices)
-          if (s != dev) {
-            // A failed pull is a link verdict (xgmi.link_report: dead link -> the nodes at both
-            // ends NotReady), not a device one: the device keeps its own result, so every
-            // machine still gets its share of the burn-in.
-            r.peers.push_back(tk8s::copy_probe(s, dev, peer_bytes, iters));
-            r.peers_ok = r.peers_ok && ok_of(r.peers.back());
-          }
+        // Offset order: device k pulls from k+1, k+2, ... (mod m), so at any moment the devices
+        // read from different sources over different links instead of all from device 0 first.
+        for (size_t off = 1; off < devices.size(); ++off) {
+          const int s = devices[(k + off) % devices.size()];
+          // A failed pull is a link verdict (xgmi.link_report: dead link -> the nodes at both
+          // ends NotReady), not a device one: the device keeps its own result, so every machine
+          // still gets its share of the burn-in.
+          r.peers.push_back(tk8s::copy_probe(s, dev, peer_bytes, iters, !a.has("no-peer-dma")));
+          r.peers_ok = r.peers_ok && ok_of(r.peers.back());
+        }
       r.peers_ms = ms_since(t);
       r.wall_ms = ms_since(td);
     };

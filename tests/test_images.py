@@ -1,0 +1,155 @@
+"""Container images on an offline node (agent/images.py + native/tools/tk8s_container.cpp):
+``./tk8s image load`` of a docker-save archive, the layers applied with their whiteouts, and a pod
+naming the image running in its root file system with the image's entrypoint, env and working
+directory -- the reference's Docker workloads (ansible/roles/rancherhost/tasks/main.yml:26-34),
+without a registry. The test image is built here from this host's /bin/sh and its libraries."""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import pytest
+
+from tritonk8ssupervisor_amd.agent.images import ImageStore, normalize, write_docker_archive
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def test_reference_normalisation():
+    assert normalize("nginx") == "docker.io/library/nginx:latest"
+    assert normalize("nginx:1.27") == "docker.io/library/nginx:1.27"
+    assert normalize("rocm/k8s-device-plugin:1.31.0.6") == "docker.io/rocm/k8s-device-plugin:1.31.0.6"
+    assert normalize("registry.local:5000/team/app") == "registry.local:5000/team/app:latest"
+    assert normalize("localhost/x:2") == "localhost/x:2"
+    assert normalize("busybox@sha256:abc") == "docker.io/library/busybox@sha256:abc"
+
+
+def _host_files(*binaries: str) -> dict[str, bytes]:
+    """The binaries and every library they load, at their own paths (a minimal root file system)."""
+    files: dict[str, bytes] = {}
+    for b in binaries:
+        real = shutil.which(b)
+        files[f"bin/{Path(b).name}"] = Path(real).read_bytes()
+        out = subprocess.run(["ldd", real], capture_output=True, text=True).stdout
+        for tok in out.split():
+            if tok.startswith("/") and Path(tok).exists():
+                files[tok.lstrip("/")] = Path(tok).resolve().read_bytes()
+    return files
+
+
+def _hello_archive(path: Path) -> str:
+    base = _host_files("sh", "cat")
+    base.update({"etc/hello-release": b"tk8s hello 1\n", "etc/removed": b"gone in layer 1\n", "app/": b""})
+    top = {"etc/.wh.removed": b"", "app/run.sh": (
+        b"#!/bin/sh\necho greeting=$GREETING\necho cwd=$(pwd)\necho pid=$$\ncat /etc/hello-release\n"
+        b"cat /etc/removed 2>/dev/null || echo removed=yes\necho args=$*\necho iso=$TK8S_GPU_ISOLATION\n"
+        b"echo container=$TK8S_CONTAINER\necho written > /app/out.txt\n")}
+    write_docker_archive(path, "hello:1", [base, top], {
+        "Entrypoint": ["/bin/sh", "/app/run.sh"], "Cmd": ["default-arg"], "Env": ["GREETING=hi", "PATH=/bin"],
+        "WorkingDir": "/app"})
+    return "docker.io/library/hello:1"
+
+
+def test_load_apply_whiteouts_and_kubernetes_command_rules(tmp_path):
+    store = ImageStore(tmp_path / "store")
+    ref = _hello_archive(tmp_path / "hello.tar")
+    assert store.load(tmp_path / "hello.tar") == [ref]
+    assert [i["ref"] for i in store.list()] == [ref] and store.get("hello:1") is not None
+    root = store.rootfs("hello:1")
+    assert (root / "etc" / "hello-release").read_text() == "tk8s hello 1\n"
+    assert not (root / "etc" / "removed").exists() and (root / "app" / "run.sh").exists()
+    assert store.rootfs("hello:1") == root  # built once
+    # Kubernetes: command replaces ENTRYPOINT (and drops CMD), args replace CMD
+    assert store.container_argv(ref, None, None) == (["/bin/sh", "/app/run.sh", "default-arg"],
+                                                     {"GREETING": "hi", "PATH": "/bin"}, "/app")
+    assert store.container_argv(ref, None, ["x"])[0] == ["/bin/sh", "/app/run.sh", "x"]
+    assert store.container_argv(ref, ["/bin/cat"], ["/etc/hello-release"])[0] == ["/bin/cat", "/etc/hello-release"]
+    assert store.remove("hello:1") and store.get(ref) is None
+
+
+def test_layers_cannot_escape_the_root(tmp_path):
+    import io
+    import tarfile
+
+    from tritonk8ssupervisor_amd.agent.images import apply_layer
+
+    layer = tmp_path / "evil.tar"
+    with tarfile.open(layer, "w") as t:
+        for name, data in (("../escape.txt", b"x"), ("ok.txt", b"y")):
+            ti = tarfile.TarInfo(name)
+            ti.size = len(data)
+            t.addfile(ti, io.BytesIO(data))
+        ti = tarfile.TarInfo("link")
+        ti.type, ti.linkname = tarfile.SYMTYPE, "/"
+        t.addfile(ti)
+        ti = tarfile.TarInfo("link/etc-escape")
+        ti.size = 1
+        t.addfile(ti, io.BytesIO(b"z"))
+    root = tmp_path / "root"
+    root.mkdir()
+    apply_layer(layer, root)
+    assert (root / "ok.txt").read_bytes() == b"y"
+    assert not (tmp_path / "escape.txt").exists() and not Path("/etc-escape").exists()
+
+
+@pytest.fixture
+def ws(tmp_path):
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, tmp_path / f)
+    yield tmp_path
+    subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=_env(tmp_path), capture_output=True, timeout=120)
+
+
+def _env(ws: Path) -> dict:
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_FAKE_GPUS="2",
+               TK8S_IMAGE_STORE=str(ws / "images"))
+    env.pop("TK8S_FAULTS", None)
+    return env
+
+
+def test_a_pod_runs_in_its_image(ws, native_build):
+    """./tk8s image load, then a pod naming the image (no command): it runs the image's entrypoint
+    in the image's root file system, with the image's env and working dir, as pid 1 of its own PID
+    namespace, writes into its own overlay layer, and is GPU-jailed; describe pod says so."""
+    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
+
+    if not container_runtime()[0]:
+        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+    env = _env(ws)
+    ref = _hello_archive(ws / "hello.tar")
+    r = subprocess.run(["./tk8s", "image", "load", "hello.tar"], cwd=ws, env=env, capture_output=True, text=True)
+    assert r.returncode == 0 and f"Loaded image: {ref}" in r.stdout, r.stderr
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"], cwd=ws,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    (ws / "pod.json").write_text(json.dumps({
+        "apiVersion": "v1", "kind": "Pod", "metadata": {"name": "hello"},
+        "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "image": "hello:1", "args": ["from-k8s"],
+                                                           "env": [{"name": "GREETING", "value": "hello"}]}]}}))
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
+    assert kc("apply", "-f", "pod.json").returncode == 0
+    deadline = time.monotonic() + 60
+    phase = None
+    while time.monotonic() < deadline:
+        phase = json.loads(kc("get", "pod", "hello", "-o", "json").stdout)["status"].get("phase")
+        if phase in ("Succeeded", "Failed"):
+            break
+        time.sleep(0.2)
+    log = kc("logs", "hello").stdout
+    assert phase == "Succeeded", (phase, log, kc("describe", "pod", "hello").stdout)
+    lines = dict(x.split("=", 1) for x in log.split() if "=" in x)
+    assert lines["greeting"] == "hello" and lines["cwd"] == "/app" and lines["pid"] == "1", log
+    assert "tk8s hello 1" in log and lines["removed"] == "yes" and lines["args"] == "from-k8s", log
+    assert lines["iso"].startswith("landlock:abi") and "rootfs:overlay" in lines["container"], log
+    # the write went to the pod's own layer, never into the shared image
+    store = ImageStore(ws / "images")
+    assert not (store.rootfs(ref) / "app" / "out.txt").exists()
+    d = kc("describe", "pod", "hello").stdout
+    assert "container: namespaces (root)" in d or "container: namespaces (userns)" in d, d
+    assert "image hello:1" in d and "own PID namespace" in d, d

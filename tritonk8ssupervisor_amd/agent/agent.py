@@ -30,7 +30,9 @@ from ..utils.faults import fault
 from ..utils.k8senv import field_path, service_env
 from ..utils.trace import trace
 from .deviceplugin import DevicePlugin
-from .runtime import PodProc, PodRuntime, gpu_jail, gpu_jail_argv, install_sigterm, namespace_isolation
+from .runtime import (
+    PodProc, PodRuntime, container_argv, container_runtime, gpu_jail, gpu_jail_argv, install_sigterm, namespace_isolation,
+)
 
 GPU = "amd.com/gpu"
 ALL_GPUS = "tk8s.amd.com/all-gpus"
@@ -383,7 +385,21 @@ class Agent:
                     "TK8S_GPU_COUNT": str(len(ordinals))})
         env.update(cenv)
         argv = [_expand(str(x), env) for x in (c.get("command") or []) + (c.get("args") or [])]
-        if not c.get("command"):
+        image = self._image(c.get("image"))
+        if image is not None:  # a loaded image (agent/images.py): its root file system, entrypoint, env
+            ok, why = container_runtime()
+            if not ok:
+                self._report(key, md["name"], md["namespace"], "Failed", {
+                    "reason": "ContainerCannotRun", "message": f"image {c.get('image')!r} needs a mount namespace on "
+                                                              f"this node: {why}"}, None)
+                return
+            store, ref = image
+            img_argv, img_env, img_wd = store.container_argv(ref, c.get("command"), c.get("args"))
+            for k, v in img_env.items():  # the image's env, under what the pod spec sets itself
+                if k not in cenv:
+                    env[k] = v
+            argv = [_expand(str(x), env) for x in img_argv]
+        elif not c.get("command"):
             from ..apps import resolve
 
             entry = resolve(c.get("image"))
@@ -392,8 +408,9 @@ class Agent:
                 argv = entry + [_expand(str(x), env) for x in (c.get("args") or [])]
         if not argv:
             self._report(key, md["name"], md["namespace"], "Failed", {
-                "reason": "NoCommand", "message": f"container has no command and image {c.get('image')!r} is not "
-                                                  "in the tk8s app catalogue (tritonk8ssupervisor_amd/apps)"}, None)
+                "reason": "ErrImageNeverPull", "message": f"container has no command and image {c.get('image')!r} is "
+                                                          "neither loaded on this node (./tk8s image load) nor in the "
+                                                          "tk8s app catalogue (tritonk8ssupervisor_amd/apps)"}, None)
             return
         # GPU pods stay in the host PID namespace: HIP/RCCL inter-process sharing (dmabuf handles
         # passed by pid, RCCL's pid-keyed shared memory) needs the peers' real pids.
@@ -412,6 +429,19 @@ class Agent:
         jail = gpu_jail_argv(mine) if jail_ok else []
         gpu_isolation = (f"{jail_how}: may open {', '.join(f'gpu{g.ordinal}' for g in mine) or 'no GPU'}" if jail_ok
                          else f"none: {jail_how}")
+        if image is not None:  # tk8s-container: namespaces, the image's root, the same GPU jail inside
+            store, ref = image
+            try:
+                rootfs = store.rootfs(ref)
+            except Exception as e:  # noqa: BLE001 - an unreadable image fails the pod, not the agent
+                self._report(key, md["name"], md["namespace"], "Failed",
+                             {"reason": "ErrImageUnpack", "message": str(e)[:500]}, None)
+                return
+            workdir = c.get("workingDir") or store.container_argv(ref, None, None)[2]
+            jail = container_argv(str(rootfs), str(pp_dir / "rootfs"), workdir, pid_ns=not gpu_pod, gpus=mine,
+                                  binds=_host_path_binds(spec, c))
+            isolation = f"container: {container_runtime()[1]}, image {ref}" + ("" if gpu_pod else ", own PID namespace")
+            avail = False
         pp = PodProc(key=key, uid=md.get("uid", ""), dir=pp_dir, argv=argv, env=env,
                      restart_policy=spec.get("restartPolicy", "Always"), gpu_ids=ids, ip=pod_ip,
                      isolate=avail and not gpu_pod, jail=jail)
@@ -635,6 +665,15 @@ class Agent:
                 self.kubelet.stop()
         return 0
 
+    def _image(self, ref: str | None):
+        """(store, ref) when ``ref`` is an image loaded on this node, else None."""
+        if not ref:
+            return None
+        from .images import ImageStore
+
+        store = ImageStore()
+        return (store, ref) if store.get(ref) is not None else None
+
     def _job_uid(self, ns: str, name: str) -> str | None:
         """uid of the Job ns/name as the control plane has it (None: there is none)."""
         try:
@@ -644,6 +683,13 @@ class Agent:
 
     def _ordinal(self, dev_id: str) -> int:
         return next(d.ordinal for d in self.plugin.devices_ if d.id == dev_id)
+
+
+def _host_path_binds(spec: dict, c: dict) -> list[tuple[str, str]]:
+    """The container's hostPath volumeMounts as (host path, path in the container)."""
+    vols = {v.get("name"): (v.get("hostPath") or {}).get("path") for v in spec.get("volumes") or []}
+    return [(vols[m["name"]], m["mountPath"]) for m in c.get("volumeMounts") or []
+            if vols.get(m.get("name")) and m.get("mountPath")]
 
 
 def host_scope_env(ordinals: list[int]) -> dict:

@@ -10,6 +10,7 @@
   ./tk8s ansible-playbook [--check] [-i hosts] clusterUp.yml           (playbook engine)
   ./tk8s status [--json]            (phases, nodes, GPUs, last RCCL busbw)
   ./tk8s scale N [--json]           (add / drain and remove workers of the running cluster)
+  ./tk8s image load FILE | ls | rm REF   (this host's container images, loaded from files)
   ./kubectl ...                     (see cli/kubectl.py)
 """
 from __future__ import annotations
@@ -139,6 +140,36 @@ def cmd_status(args) -> int:
             print(f"last RCCL all-reduce: peak busbw {r['peak_busbw_gbps']:.1f} GB/s over {r['nranks']} GPU(s)")
         elif r:
             print(f"RCCL all-reduce: {'ok' if r.get('ok') else 'FAILED'} on {r.get('pods')} pod(s)")
+    return 0
+
+
+def cmd_image(args) -> int:
+    """``./tk8s image load FILE | ls | rm REF``: the node's image store (agent/images.py), the
+    reference's ``docker pull`` for an offline host: pods naming a loaded image run in it."""
+    from ..agent.images import ImageError, ImageStore
+
+    store = ImageStore()
+    try:
+        if args.action == "load":
+            if not args.source:
+                raise ImageError("image load needs a file or directory")
+            out = {"loaded": store.load(args.source, tag=args.tag)}
+            text = "\n".join(f"Loaded image: {r}" for r in out["loaded"])
+        elif args.action == "ls":
+            out = {"images": store.list()}
+            text = "\n".join([f"{'IMAGE':<60} {'LAYERS':>6} {'SIZE':>12}"] +
+                              [f"{i['ref']:<60} {i['layers']:>6} {i['size']:>12}" for i in out["images"]])
+        else:
+            if not args.source:
+                raise ImageError("image rm needs a reference")
+            if not store.remove(args.source):
+                raise ImageError(f"no such image: {args.source}")
+            out = {"removed": args.source}
+            text = f"Untagged: {args.source}"
+    except (ImageError, OSError) as e:
+        print(f"error: {e}", file=sys.stderr)
+        return 1
+    print(json.dumps(out) if args.json else text)
     return 0
 
 
@@ -468,6 +499,13 @@ def build_parser() -> argparse.ArgumentParser:
     pb.add_argument("--check", "-C", action="store_true")
     pb.add_argument("-e", "--extra-vars", action="append")
     pb.set_defaults(fn=cmd_playbook)
+
+    im = sub.add_parser("image", help="this host's container images (air-gapped: loaded from files)")
+    im.add_argument("action", choices=["load", "ls", "rm"])
+    im.add_argument("source", nargs="?", help="load: a docker save archive or an OCI layout; rm: a reference")
+    im.add_argument("--tag", default=None, help="load: the name for an image the file does not name")
+    im.add_argument("--json", action="store_true")
+    im.set_defaults(fn=cmd_image)
 
     k = sub.add_parser("kubectl", add_help=False)
     k.add_argument("rest", nargs=argparse.REMAINDER)

@@ -95,6 +95,10 @@ def host_burnin_command(command: list[str], gpus: list[int]) -> list[str]:
         hip = probe_tool(peers=True)
         if cmd and os.path.basename(cmd[0]) == "tk8s-hsaprobe" and os.path.basename(hip) != "tk8s-hsaprobe":
             cmd[0] = hip  # the pulls take the HIP peer path (probe_tool)
+    if "--peers" in cmd and os.path.basename(cmd[0]) == "tk8s-probe" and "--peer-bytes" not in cmd:
+        # a link check, on the Ready path: 16 MiB kernel pulls (~0.25 ms per link at xGMI rates),
+        # not the standalone probe's 64 MiB kernel + SDMA timing per pair
+        cmd += ["--peer-bytes", str(16 << 20), "--no-peer-dma"]
     return cmd
 
 

@@ -132,12 +132,13 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         obj = OBJ / (src.stem + ".o")
         tool_objs[name] = obj
         if force or _stale(obj, [src]):
-            objs.append((obj, [HIPCC, *COMMON, "-c", str(src), "-o", str(obj)]))
+            objs.append((obj, [HIPCC, *COMMON, f"--offload-arch={ARCH}", "-c", str(src), "-o", str(obj)]))
     py_inc = _pybind_includes()
     nat_obj = OBJ / "native_module.o"
     nat_src = NATIVE / "bindings" / "native_module.cpp"
     if force or _stale(nat_obj, [nat_src]):
-        objs.append((nat_obj, [HIPCC, *COMMON, *py_inc, "-fvisibility=hidden", "-c", str(nat_src), "-o", str(nat_obj)]))
+        objs.append((nat_obj, [HIPCC, *COMMON, f"--offload-arch={ARCH}", *py_inc, "-fvisibility=hidden", "-c",
+                               str(nat_src), "-o", str(nat_obj)]))
     topo_srcs = [NATIVE / "src" / "topology.cpp", NATIVE / "bindings" / "topo_module.cpp"]
     topo_objs = [OBJ / (s.stem + "_topo.o") for s in topo_srcs]
     for s, o in zip(topo_srcs, topo_objs):
@@ -190,10 +191,13 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if force or _stale(reuse_bin, [reuse_src]):
         _run([CXX, "-O2", "-std=c++17", "-Wall", str(reuse_src), "-o", str(reuse_bin)], verbose)
 
-    jail_src = NATIVE / "tools" / "tk8s_gpujail.cpp"
+    # pod isolation: the GPU jail (process pods) and the container runtime (image pods), no HIP
+    jail_hdr = NATIVE / "tools" / "gpujail.h"
+    for tname, tsrc in (("tk8s-gpujail", "tk8s_gpujail.cpp"), ("tk8s-container", "tk8s_container.cpp")):
+        src = NATIVE / "tools" / tsrc
+        if force or _stale(tool_path(tname), [src, jail_hdr]):
+            _run([CXX, "-O2", "-std=c++17", "-Wall", "-Wextra", str(src), "-o", str(tool_path(tname))], verbose)
     jail = tool_path("tk8s-gpujail")
-    if force or _stale(jail, [jail_src]):
-        _run([CXX, "-O2", "-std=c++17", "-Wall", "-Wextra", str(jail_src), "-o", str(jail)], verbose)
 
     sup_src = NATIVE / "tools" / "tk8s_supervise.cpp"
     sup = tool_path("tk8s-supervise")
@@ -218,7 +222,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
     precompile_python()
     out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,
-           "tk8s-gpujail": jail,
+           "tk8s-gpujail": jail, "tk8s-container": tool_path("tk8s-container"),
            "tk8s-smi": smi, "tk8s-reuse": reuse_bin, "tk8s-hsaprobe": hsa_bin, **cos}
     out.update({n: tool_path(n) for n in TOOLS})
     return out
