@@ -327,6 +327,11 @@ std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int ite
 }
 
 std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, bool dma) {
+  // a failed pull still names its link: xgmi.py counts it as a dead link between the two GPUs
+  auto link_error = [&](const std::string& what) {
+    return Json().kv("ok", false).kv("probe", src_device != dst_device ? "xgmi_peer_copy" : "local_copy")
+        .kv("src_device", src_device).kv("dst_device", dst_device).kv("error", what).str();
+  };
   try {
     if (bytes % 16 || bytes == 0) return error_json("bytes must be a positive multiple of 16");
     iters = std::max(iters, 1);
@@ -334,7 +339,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
     int can = 1;
     if (peer) {
       TK8S_HIP_CHECK(hipDeviceCanAccessPeer(&can, dst_device, src_device));
-      if (!can) return error_json("no peer access from dst to src");
+      if (!can) return link_error("no peer access from dst to src");
     }
     // Local: src, dst and the error counter are carved from this device's scratch arena.
     // Peer: own buffers (the source device's arena may be busy in another thread).
@@ -404,7 +409,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
     if (dma) j.kv("dma_ms", static_cast<double>(dma_ms)).kv("dma_gbps", bytes / (dma_ms * 1e-3) / 1e9);
     return j.kv("bad_words", static_cast<uint64_t>(nbad)).str();
   } catch (const std::exception& ex) {
-    return error_json(ex.what());
+    return link_error(ex.what());
   }
 }
 

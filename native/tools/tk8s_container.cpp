@@ -2,6 +2,7 @@
 //
 //   tk8s-container --rootfs DIR [--upper DIR] [--workdir D] [--hostname H] [--pid-ns]
 //                  [--bind SRC:DST]... [jail options, gpujail.h] [--no-gpu-jail] -- ARGV...
+//   tk8s-container --exec-in PID [--workdir D] [jail options] -- ARGV...   (kubectl exec)
 //   tk8s-container --probe      {"usable": bool, "how": "root"|"userns", "error": ...}
 //
 // The reference's workloads ran in Docker containers (ansible/roles/rancherhost/tasks/main.yml:
@@ -33,6 +34,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -111,10 +113,70 @@ int probe() {
   return ok ? 0 : 1;
 }
 
+// --exec-in PID: run a command inside a running image pod (kubectl exec): its user, mount and
+// PID namespaces, its root, the same GPU jail. PID is the pod's tk8s-container process; with a
+// PID namespace that process only waits, and the container is its child.
+int exec_in(pid_t pid, const std::string& workdir, const tk8s::jail::Policy& policy, bool jail, char** argv) {
+  auto root_of = [](pid_t p) {
+    char buf[PATH_MAX];
+    const ssize_t n = readlink(("/proc/" + std::to_string(p) + "/root").c_str(), buf, sizeof(buf) - 1);
+    return n > 0 ? std::string(buf, n) : std::string();
+  };
+  if (root_of(pid) == "/") {  // the relaying parent: the container is its first child
+    std::ifstream kids("/proc/" + std::to_string(pid) + "/task/" + std::to_string(pid) + "/children");
+    pid_t child = 0;
+    if (!(kids >> child) || child <= 0) {
+      errno = ESRCH;
+      die("no container process under pid " + std::to_string(pid));
+    }
+    pid = child;
+  }
+  const std::string proc = "/proc/" + std::to_string(pid);
+  const int rootfd = open((proc + "/root").c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+  if (rootfd < 0) die("open " + proc + "/root");
+  auto join = [&](const char* ns, int type) {
+    struct stat mine {}, theirs {};
+    if (stat((proc + "/ns/" + ns).c_str(), &theirs) != 0) die(std::string("stat ns ") + ns);
+    if (stat((std::string("/proc/self/ns/") + ns).c_str(), &mine) == 0 && mine.st_ino == theirs.st_ino) return;
+    const int fd = open((proc + "/ns/" + ns).c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0 || setns(fd, type) != 0) die(std::string("setns ") + ns);
+    close(fd);
+  };
+  join("user", CLONE_NEWUSER);
+  join("mnt", CLONE_NEWNS);
+  join("pid", CLONE_NEWPID);
+  if (fchdir(rootfd) != 0 || chroot(".") != 0 || chdir("/") != 0) die("enter the container's root");
+  close(rootfd);
+  const pid_t child = fork();  // a joined PID namespace takes effect for children only
+  if (child < 0) die("fork");
+  if (child > 0) {
+    for (int s : {SIGTERM, SIGINT, SIGHUP}) signal(s, [](int) {});
+    int st = 0;
+    while (waitpid(child, &st, 0) < 0 && errno == EINTR) {
+    }
+    return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSIG(st);
+  }
+  prctl(PR_SET_PDEATHSIG, SIGKILL);
+  std::string mode = "none:--no-gpu-jail";
+  if (jail) {
+    mode = tk8s::jail::apply(policy);
+    if (mode.rfind("none:", 0) == 0) {
+      std::fprintf(stderr, "tk8s-container: GPU jail: %s\n", mode.c_str());
+      _exit(125);
+    }
+  }
+  if (chdir(workdir.c_str()) != 0) die("chdir " + workdir);
+  setenv("TK8S_GPU_ISOLATION", mode.c_str(), 1);
+  execvp(argv[0], argv);
+  std::fprintf(stderr, "tk8s-container: exec %s: %s\n", argv[0], std::strerror(errno));
+  _exit(127);
+}
+
 int usage() {
   std::fprintf(stderr,
                "usage: tk8s-container --rootfs DIR [--upper DIR] [--workdir D] [--hostname H] [--pid-ns]\n"
                "                      [--bind SRC:DST]... [--allow-render M]... [--no-gpu-jail] -- ARGV...\n"
+               "       tk8s-container --exec-in PID [--workdir D] [--allow-render M]... -- ARGV...\n"
                "       tk8s-container --probe\n");
   return 2;
 }
@@ -125,6 +187,7 @@ int main(int argc, char** argv) {
   std::string rootfs, upper, workdir = "/", hostname;
   std::vector<std::pair<std::string, std::string>> binds;
   bool pid_ns = false, jail = true;
+  pid_t exec_pid = 0;
   tk8s::jail::Policy policy;
   int i = 1;
   for (; i < argc; ++i) {
@@ -146,6 +209,7 @@ int main(int argc, char** argv) {
       else if (a == "--hostname") hostname = next();
       else if (a == "--pid-ns") pid_ns = true;
       else if (a == "--no-gpu-jail") jail = false;
+      else if (a == "--exec-in") exec_pid = static_cast<pid_t>(std::stol(next()));
       else if (a == "--bind") {
         const std::string v = next();
         const auto c = v.find(':');
@@ -159,6 +223,7 @@ int main(int argc, char** argv) {
       return usage();
     }
   }
+  if (exec_pid > 0 && i < argc) return exec_in(exec_pid, workdir, policy, jail, argv + i);
   if (rootfs.empty() || i >= argc) return usage();
   rootfs = tk8s::jail::real(rootfs);
   if (rootfs.empty()) die("--rootfs");

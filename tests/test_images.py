@@ -41,7 +41,7 @@ def _host_files(*binaries: str) -> dict[str, bytes]:
 
 
 def _hello_archive(path: Path) -> str:
-    base = _host_files("sh", "cat")
+    base = _host_files("sh", "cat", "sleep")
     base.update({"etc/hello-release": b"tk8s hello 1\n", "etc/removed": b"gone in layer 1\n", "app/": b""})
     top = {"etc/.wh.removed": b"", "app/run.sh": (
         b"#!/bin/sh\necho greeting=$GREETING\necho cwd=$(pwd)\necho pid=$$\ncat /etc/hello-release\n"
@@ -153,3 +153,34 @@ def test_a_pod_runs_in_its_image(ws, native_build):
     d = kc("describe", "pod", "hello").stdout
     assert "container: namespaces (root)" in d or "container: namespaces (userns)" in d, d
     assert "image hello:1" in d and "own PID namespace" in d, d
+
+
+def test_kubectl_exec_enters_the_container(ws, native_build):
+    """kubectl exec into an image pod runs inside its container (its root, its PID namespace, the
+    same GPU jail), not on the host."""
+    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
+
+    if not container_runtime()[0]:
+        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+    env = _env(ws)
+    _hello_archive(ws / "hello.tar")
+    assert subprocess.run(["./tk8s", "image", "load", "hello.tar"], cwd=ws, env=env, capture_output=True).returncode == 0
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"], cwd=ws,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    (ws / "pod.json").write_text(json.dumps({
+        "apiVersion": "v1", "kind": "Pod", "metadata": {"name": "sleeper"},
+        "spec": {"containers": [{"name": "c", "image": "hello:1", "command": ["/bin/sleep", "60"]}]}}))
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
+    assert kc("apply", "-f", "pod.json").returncode == 0
+    deadline = time.monotonic() + 30
+    while time.monotonic() < deadline:
+        if json.loads(kc("get", "pod", "sleeper", "-o", "json").stdout)["status"].get("phase") == "Running":
+            break
+        time.sleep(0.2)
+    time.sleep(0.5)  # the container's pid 1 has started
+    r = kc("exec", "sleeper", "--", "/bin/sh", "-c", "cat /etc/hello-release; echo pid=$$; echo iso=$TK8S_GPU_ISOLATION")
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = dict(x.split("=", 1) for x in r.stdout.split() if "=" in x)
+    assert "tk8s hello 1" in r.stdout and int(out["pid"]) < 100 and out["iso"].startswith("landlock"), r.stdout
+    assert kc("exec", "sleeper", "--", "/bin/cat", "/etc/removed").returncode != 0  # the image's view, not the host's
