@@ -113,10 +113,18 @@ def local_checks(workdir: str) -> list[dict]:
         out.append(_check("loopback addresses", OK, "127.0.1.0/24 bindable (machine addresses)"))
     except OSError as e:
         out.append(_check("loopback addresses", WARN, f"127.0.1.x not bindable ({e}): machines share 127.0.0.1"))
-    from .agent.runtime import namespace_isolation
+    from .agent.runtime import container_runtime, gpu_jail, namespace_isolation
 
     iso, why = namespace_isolation()
     out.append(_check("pod isolation", OK if iso else WARN, "user/PID/mount namespaces for CPU pods" if iso else why))
+    jail, jhow = gpu_jail()
+    out.append(_check("gpu jail", OK if jail else WARN,
+                      f"{jhow}: a pod can open only its own GPUs' render nodes" if jail else
+                      f"{jhow}: a pod's GPU view is its *_VISIBLE_DEVICES only"))
+    cont, chow = container_runtime()
+    out.append(_check("image pods", OK if cont else WARN,
+                      f"{chow}: pods can run loaded images (./tk8s image load)" if cont else
+                      f"{chow}: pods run as processes; images not in the app catalogue fail"))
     try:
         free_gb = shutil.disk_usage(workdir).free / 2**30
         out.append(_check("disk", OK if free_gb >= 1 else WARN, f"{free_gb:.1f} GiB free in {workdir}"))
@@ -192,11 +200,22 @@ def triton_checks() -> list[dict]:
     return out
 
 
-def kubeadm_checks(backend: str) -> list[dict]:
+def kubeadm_checks(backend: str, workdir: str = ".") -> list[dict]:
     if backend == "local":
-        return [_check("kubeadm platform", FAIL, "needs machines it owns: --backend baremetal or triton")]
+        return [_check("kubeadm platform", FAIL, "needs machines it owns: --backend baremetal or triton "
+                                                 "(one host in the inventory: single-node mode)")]
+    layout = ""
+    if backend == "baremetal":
+        try:
+            from .provider.baremetal import BareMetalProvider
+
+            p = BareMetalProvider(Path(workdir) / ".tk8s")
+            layout = (" -- single-node: control plane and every GPU on the one host" if p.single_host()
+                      else " -- a kubelet per host")
+        except Exception:  # noqa: BLE001 - the inventory check reports it
+            pass
     return [_check("kubeadm platform", OK, "installs ROCm, amdgpu-dkms, containerd and kubeadm as root over ssh "
-                                          "(the machines need apt and network access)")]
+                                          "(the machines need apt and network access)" + layout)]
 
 
 def run_checks(workdir: str, backend: str | None = None, platform: str | None = None) -> list[dict]:
@@ -212,7 +231,7 @@ def run_checks(workdir: str, backend: str | None = None, platform: str | None = 
     else:
         out.append(_check("backend", FAIL, f"unknown backend {backend!r}"))
     if platform == "kubeadm":
-        out += kubeadm_checks(backend)
+        out += kubeadm_checks(backend, workdir)
     return out
 
 
