@@ -823,3 +823,87 @@ def test_rccl_job_one_process_for_multi_gpu_nodes_on_one_host(ws):
     s = _summary(_setup(ws, "--nodes", "2", "--package", "mi355x-2gpu", "--rccl", "on"))
     rc = s["rccl"]
     assert rc["ok"] and rc["nranks"] == 4 and rc["pods"] == 1 and rc["gpus_per_pod"] == 4 and rc["scope"] == "host", rc
+
+
+def _ws_exec(host: str, port: int, path: str, token: str, proto: str = "v5.channel.k8s.io", stdin: bytes | None = None):
+    """A stock kubectl's exec, at the wire level: GET upgraded to a WebSocket, channel-prefixed
+    frames back (kubectl >= 1.29 talks exactly this; no kubectl binary is installed here)."""
+    import base64
+    import socket as _s
+
+    sock = _s.create_connection((host, port), timeout=30)
+    key = base64.b64encode(os.urandom(16)).decode()
+    sock.sendall((f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+                  f"Sec-WebSocket-Key: {key}\r\nSec-WebSocket-Version: 13\r\nSec-WebSocket-Protocol: {proto}\r\n"
+                  f"Authorization: Bearer {token}\r\n\r\n").encode())
+    f = sock.makefile("rb")
+    status = f.readline().decode()
+    headers = {}
+    while True:
+        line = f.readline().decode().strip()
+        if not line:
+            break
+        k, _, v = line.partition(":")
+        headers[k.strip().lower()] = v.strip()
+
+    def send(payload: bytes, opcode=0x2):
+        mask = os.urandom(4)
+        n = len(payload)
+        head = bytes([0x80 | opcode, 0x80 | n]) if n < 126 else bytes([0x80 | opcode, 0x80 | 126]) + n.to_bytes(2, "big")
+        sock.sendall(head + mask + bytes(b ^ mask[i & 3] for i, b in enumerate(payload)))
+
+    if stdin is not None and status.startswith("HTTP/1.1 101"):
+        send(b"\x00" + stdin)
+        send(b"\xff\x00")  # v5: close stdin
+    frames = []
+    while status.startswith("HTTP/1.1 101"):
+        h = f.read(2)
+        if len(h) < 2:
+            break
+        n = h[1] & 0x7F
+        if n == 126:
+            n = int.from_bytes(f.read(2), "big")
+        elif n == 127:
+            n = int.from_bytes(f.read(8), "big")
+        data = f.read(n)
+        if h[0] & 0x0F == 0x8:
+            break
+        frames.append((data[0], data[1:]))
+    sock.close()
+    return status, headers, frames
+
+
+def test_stock_kubectl_exec_over_websocket(ws, tmp_path_factory):
+    """`kubectl exec` of a stock client (v5.channel.k8s.io WebSocket; v4 without
+    stdin) runs the command in the pod and returns stdout / stderr / the exit Status."""
+    from urllib.parse import urlsplit
+
+    _summary(_setup(ws, "--nodes", "1", "--rccl", "off"))
+    d = tmp_path_factory.mktemp("wsx")
+    (d / "pod.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "box"},
+                                            "spec": {"containers": [{"name": "c", "command": ["sleep", "60"]}]}}))
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=_env(), capture_output=True, text=True, timeout=60)
+    assert kc("apply", "-f", str(d / "pod.json")).returncode == 0
+    deadline = time.monotonic() + 30
+    while time.monotonic() < deadline and json.loads(kc("get", "pod", "box", "-o", "json").stdout)["status"].get("phase") != "Running":
+        time.sleep(0.1)
+    cfg = json.loads((ws / ".tk8s" / "kubeconfig.json").read_text())
+    server = urlsplit(cfg["clusters"][0]["cluster"]["server"])
+    token = cfg["users"][0]["user"]["token"]
+    base = f"{server.path}/api/v1/namespaces/default/pods/box/exec"
+    q = "?command=sh&command=-c&command=echo+out%3B+echo+err+%3E%262%3B+exit+3&stdout=true&stderr=true"
+    status, headers, frames = _ws_exec(server.hostname, server.port, base + q, token)
+    assert status.startswith("HTTP/1.1 101") and headers["sec-websocket-protocol"] == "v5.channel.k8s.io", status
+    by = {}
+    for ch, data in frames:
+        by[ch] = by.get(ch, b"") + data
+    assert by[1] == b"out\n" and by[2] == b"err\n", frames
+    st = json.loads(by[3])
+    assert st["status"] == "Failure" and st["details"]["causes"][0]["message"] == "3", st
+    # stdin (v5 closes it with [255, 0])
+    q = "?command=cat&stdin=true&stdout=true"
+    status, _, frames = _ws_exec(server.hostname, server.port, base + q, token, stdin=b"hello from stdin")
+    assert (1, b"hello from stdin") in frames and json.loads(dict(frames)[3])["status"] == "Success", frames
+    # no token, no exec
+    status, _, _ = _ws_exec(server.hostname, server.port, base + q, "wrong")
+    assert status.startswith("HTTP/1.1 401"), status

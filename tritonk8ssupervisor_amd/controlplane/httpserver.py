@@ -15,7 +15,7 @@ from urllib.parse import parse_qs, unquote, urlsplit
 
 from ..utils.record import field, record as dataclass
 
-REASONS = {200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
+REASONS = {101: "Switching Protocols", 200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
            401: "Unauthorized", 403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed",
            409: "Conflict", 422: "Unprocessable Entity", 500: "Internal Server Error",
            503: "Service Unavailable", 504: "Gateway Timeout"}
@@ -29,6 +29,11 @@ class Request:
     headers: dict[str, str]
     body: bytes
     peer: str = ""
+    raw_query: str = ""
+
+    def q_all(self, key: str) -> list[str]:
+        """Every value of a repeated query parameter (``?command=ls&command=-l``)."""
+        return parse_qs(self.raw_query, keep_blank_values=True).get(key, [])
 
     def json(self) -> Any:
         if not self.body:
@@ -72,6 +77,79 @@ class StreamResponse:
     status: int = 200
     content_type: str = "application/json"
     headers: dict[str, str] = field(default_factory=dict)
+
+
+@dataclass
+class WebSocketResponse:
+    """Switch the connection to a WebSocket (RFC 6455) and hand it to ``session(ws)``: what
+    ``kubectl exec`` speaks since Kubernetes 1.29 (subprotocol v5.channel.k8s.io / v4.channel.k8s.io)."""
+    session: Callable[["WebSocket"], Awaitable[None]]
+    protocol: str = ""
+
+
+class WebSocket:
+    """Server side of an RFC 6455 connection: binary/text frames, client masking, ping/pong,
+    close. Messages only (no fragments sent; incoming fragments are reassembled)."""
+
+    def __init__(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
+        self.reader, self.writer = reader, writer
+        self.closed = False
+
+    async def send(self, data: bytes, opcode: int = 0x2) -> None:
+        n = len(data)
+        head = bytes([0x80 | opcode])
+        if n < 126:
+            head += bytes([n])
+        elif n < 1 << 16:
+            head += bytes([126]) + n.to_bytes(2, "big")
+        else:
+            head += bytes([127]) + n.to_bytes(8, "big")
+        self.writer.write(head + data)
+        await self.writer.drain()
+
+    async def recv(self) -> bytes | None:
+        """The next message's payload; None once the client closed."""
+        buf = b""
+        while True:
+            h = await self.reader.readexactly(2)
+            fin, opcode = h[0] & 0x80, h[0] & 0x0F
+            n = h[1] & 0x7F
+            if n == 126:
+                n = int.from_bytes(await self.reader.readexactly(2), "big")
+            elif n == 127:
+                n = int.from_bytes(await self.reader.readexactly(8), "big")
+            if n > 64 << 20:
+                raise HttpError(413, "websocket frame too large")
+            mask = await self.reader.readexactly(4) if h[1] & 0x80 else b""
+            data = await self.reader.readexactly(n)
+            if mask:
+                data = bytes(b ^ mask[i & 3] for i, b in enumerate(data))
+            if opcode == 0x8:
+                self.closed = True
+                return None
+            if opcode == 0x9:
+                await self.send(data, 0xA)
+                continue
+            if opcode == 0xA:
+                continue
+            buf += data
+            if fin:
+                return buf
+
+    async def close(self, code: int = 1000) -> None:
+        if not self.closed:
+            self.closed = True
+            try:
+                await self.send(code.to_bytes(2, "big"), 0x8)
+            except (ConnectionError, RuntimeError):
+                pass
+
+
+def websocket_accept(key: str) -> str:
+    import base64
+    import hashlib
+
+    return base64.b64encode(hashlib.sha1((key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11").encode()).digest()).decode()
 
 
 class HttpError(Exception):
@@ -135,7 +213,7 @@ async def _read_request(reader: asyncio.StreamReader, peer: str) -> Request | No
         body = await reader.readexactly(n)
     u = urlsplit(target)
     query = {k: v[-1] for k, v in parse_qs(u.query, keep_blank_values=True).items()}
-    return Request(method.upper(), u.path or "/", query, headers, body, peer)
+    return Request(method.upper(), u.path or "/", query, headers, body, peer, u.query)
 
 
 class HttpServer:
@@ -166,7 +244,7 @@ class HttpServer:
                 try:
                     handler, params = self.router.match(req.method, req.path)
                     res = await handler(req, **params)
-                    if not isinstance(res, (Response, StreamResponse)):
+                    if not isinstance(res, (Response, StreamResponse, WebSocketResponse)):
                         res = Response(200, res)
                 except HttpError as e:
                     res = self._error(req.path, e)
@@ -175,6 +253,19 @@ class HttpServer:
                         self.on_error(traceback.format_exc())
                     res = self._error(req.path, HttpError(500, repr(e)))
                 keep = req.headers.get("connection", "").lower() != "close"
+                if isinstance(res, WebSocketResponse):
+                    hdr = ["HTTP/1.1 101 Switching Protocols", "Upgrade: websocket", "Connection: Upgrade",
+                           f"Sec-WebSocket-Accept: {websocket_accept(req.headers.get('sec-websocket-key', ''))}"]
+                    if res.protocol:
+                        hdr.append(f"Sec-WebSocket-Protocol: {res.protocol}")
+                    writer.write(("\r\n".join(hdr) + "\r\n\r\n").encode("latin-1"))
+                    await writer.drain()
+                    ws = WebSocket(reader, writer)
+                    try:
+                        await res.session(ws)
+                    finally:
+                        await ws.close()
+                    return
                 if isinstance(res, StreamResponse):
                     await self._stream(writer, res, keep=keep)
                 else:

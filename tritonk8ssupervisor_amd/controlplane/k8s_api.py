@@ -588,14 +588,21 @@ class KubernetesAPI:
         if not isinstance(cmd, list) or not cmd:
             raise HttpError(422, "command must be a non-empty list")
         timeout = min(float(body.get("timeoutSeconds", 60)), 600.0)
+        return await self._run_exec(p, ns, name, cmd, str(body.get("stdin", "")), timeout)
+
+    async def _run_exec(self, p: str, ns: str, name: str, cmd: list[str], stdin: str, timeout: float) -> dict:
+        pod = self.store.get("pods", _key(p, ns, name))
+        if pod is None:
+            raise HttpError(404, f'pod "{name}" not found')
+        if pod.get("status", {}).get("phase") != "Running" or not pod["spec"].get("nodeName"):
+            raise HttpError(400, f'pod "{name}" is not running')
         self._seq += 1
         xid = f"x{self._seq:x}"
         node = pod["spec"]["nodeName"]
         key = _key(p, node, xid)
         self.store.put("execs", key, {"metadata": {"name": xid}, "_project": p, "node": node, "pod": name,
-                                      "namespace": ns, "command": [str(c) for c in cmd],
-                                      "stdin": str(body.get("stdin", "")), "timeoutSeconds": timeout,
-                                      "status": {"phase": "Pending"}})
+                                      "namespace": ns, "command": [str(c) for c in cmd], "stdin": stdin,
+                                      "timeoutSeconds": timeout, "status": {"phase": "Pending"}})
         done = await self.store.wait_until(
             lambda: (self.store.get("execs", key) or {}).get("status", {}).get("phase") == "Done", timeout + 10)
         x = self.store.delete("execs", key) or {}
@@ -603,6 +610,59 @@ class KubernetesAPI:
             raise HttpError(504, f"exec in {name}: no result from node {node} within {timeout:.0f}s")
         st = x.get("status", {})
         return {"stdout": st.get("stdout", ""), "stderr": st.get("stderr", ""), "exitCode": st.get("exitCode", 1)}
+
+    async def h_pod_exec_ws(self, req: Request, ns: str, name: str, pid: str | None = None):
+        """A stock ``kubectl exec`` (Kubernetes >= 1.29 clients): GET .../pods/NAME/exec?command=..
+        upgraded to a WebSocket with subprotocol v5.channel.k8s.io (or v4). Frames carry a channel
+        byte: 0 stdin, 1 stdout, 2 stderr, 3 the final Status, 255 (v5) closes a stream. The command
+        runs like the request/response exec (non-interactive: no TTY, output after it exits)."""
+        from .httpserver import WebSocketResponse
+
+        p = self._pid(pid, req)
+        tok = req.bearer
+        if not (tok and (tok == self.project(p).get("apiToken") or any(
+                n.get("nodeToken") == tok for n in self.store.list("nodesecrets")))):
+            raise HttpError(401, "exec needs a bearer token")
+        offered = [x.strip() for x in (req.headers.get("sec-websocket-protocol") or "").split(",")]
+        proto = next((x for x in ("v5.channel.k8s.io", "v4.channel.k8s.io") if x in offered), None)
+        if "websocket" not in (req.headers.get("upgrade") or "").lower() or proto is None:
+            raise HttpError(400, "exec needs a WebSocket upgrade with subprotocol v5.channel.k8s.io or v4.channel.k8s.io")
+        cmd = req.q_all("command")
+        if not cmd:
+            raise HttpError(422, "command must be given (?command=...)")
+        if req.q("tty") == "true":
+            raise HttpError(400, "exec with a TTY is not supported (non-interactive exec only)")
+        want_stdin = req.q("stdin") == "true"
+
+        async def session(ws):
+            data = b""
+            if want_stdin:  # v5: until the client closes stdin ([255, 0]); v4 has no such signal
+                while proto == "v5.channel.k8s.io":
+                    msg = await ws.recv()
+                    if msg is None or msg[:2] == b"\xff\x00":
+                        break
+                    if msg[:1] == b"\x00":
+                        data += msg[1:]
+            try:
+                r = await self._run_exec(p, ns, name, cmd, data.decode(errors="replace"), 600.0)
+            except HttpError as e:
+                status = {"metadata": {}, "status": "Failure", "message": e.message, "reason": "InternalError",
+                          "code": e.status}
+                await ws.send(b"\x03" + json.dumps(status).encode())
+                return
+            if r["stdout"] and req.q("stdout", "true") != "false":
+                await ws.send(b"\x01" + r["stdout"].encode())
+            if r["stderr"] and req.q("stderr", "true") != "false":
+                await ws.send(b"\x02" + r["stderr"].encode())
+            if r["exitCode"] == 0:
+                status = {"metadata": {}, "status": "Success"}
+            else:
+                status = {"metadata": {}, "status": "Failure", "reason": "NonZeroExitCode",
+                          "message": f"command terminated with non-zero exit code: {r['exitCode']}",
+                          "details": {"causes": [{"reason": "ExitCode", "message": str(r["exitCode"])}]}}
+            await ws.send(b"\x03" + json.dumps(status).encode())
+
+        return WebSocketResponse(session, proto)
 
     async def h_node_execs(self, req: Request, node: str, pid: str | None = None):
         """The node agent's long-poll for exec requests of its pods."""
