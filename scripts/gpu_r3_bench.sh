@@ -11,7 +11,7 @@ BIN="$ROOT/tritonk8ssupervisor_amd/bin"
 echo "[r3bench] bench" &&
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --keep-events "$OUT/events" --log "$OUT/bench_setup.log" \
   > "$OUT/bench.json" 2> "$OUT/bench.err" &&
-echo "[r3bench] rocprofv3 hsaprobe" && cd /tmp &&
+echo "[r3bench] rocprofv3 hsaprobe" && cd /tmp && export TK8S_PROBE_CLEAN_EXIT=1 &&
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$OUT/prof_hsaprobe" -o hsaprobe --output-format csv -- \
   "$BIN/tk8s-hsaprobe" --all-devices --gpuinfo --hbm-bytes 1073741824 --md5-bytes 268435456 --iters 3 \
   > "$OUT/rocprof_hsaprobe.log" 2>&1 &&

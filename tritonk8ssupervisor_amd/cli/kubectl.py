@@ -29,7 +29,7 @@ import yaml
 
 from ..controlplane.client import ApiError, client_from_kubeconfig
 from ..kube import (apply_objects, collection_path, delete_objects, job_state, kind_key, load_manifests,
-                    object_path, wait_job, wait_rollout)
+                    object_path, server_apply_objects, wait_job, wait_rollout)
 from ..utils.net import host_port
 
 GPU = "amd.com/gpu"
@@ -236,7 +236,19 @@ def fmt_top(nodes: list[dict], pods: list[dict]) -> str:
     return _table(rows)
 
 
-def _print(obj, output: str | None) -> None:
+def _hide_managed_fields(obj):
+    """What kubectl does unless --show-managed-fields: managedFields are noise in -o yaml/json."""
+    if isinstance(obj, dict):
+        if isinstance(obj.get("metadata"), dict) and "managedFields" in obj["metadata"]:
+            obj = {**obj, "metadata": {k: v for k, v in obj["metadata"].items() if k != "managedFields"}}
+        if isinstance(obj.get("items"), list):
+            obj = {**obj, "items": [_hide_managed_fields(i) for i in obj["items"]]}
+    return obj
+
+
+def _print(obj, output: str | None, show_managed: bool = False) -> None:
+    if not show_managed:
+        obj = _hide_managed_fields(obj)
     if output == "json":
         print(json.dumps(obj, indent=2))
     else:
@@ -304,6 +316,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--target-port", type=int)
     ap.add_argument("--type", default="ClusterIP", choices=["ClusterIP", "NodePort", "LoadBalancer"])
     ap.add_argument("--name")
+    ap.add_argument("--server-side", action="store_true")
+    ap.add_argument("--force-conflicts", action="store_true")
+    ap.add_argument("--field-manager", default="kubectl")
+    ap.add_argument("--dry-run", choices=["none", "client", "server"], default="none")
+    ap.add_argument("--show-managed-fields", action="store_true")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -337,7 +354,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 what, name = kind_key(a.args[0].split("/")[0]), a.args[0].split("/")[1]
             q = {"labelSelector": a.selector} if a.selector else None
             if name:
-                _print(k.get(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns))), a.output or "yaml")
+                _print(k.get(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns))), a.output or "yaml",
+                       a.show_managed_fields)
                 return 0
             if what == "node":
                 items = k.get(k.k8s("/api/v1/nodes"), query=q)["items"]
@@ -347,7 +365,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             else:
                 items = k.get(k.k8s(collection_path(what, ns)), query=q)["items"]
             if a.output in ("json", "yaml"):
-                _print({"apiVersion": "v1", "kind": "List", "items": items}, a.output)
+                _print({"apiVersion": "v1", "kind": "List", "items": items}, a.output, a.show_managed_fields)
             elif what == "node":
                 print(fmt_nodes(items, a.output == "wide"))
             elif what == "pod":
@@ -380,6 +398,12 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             return _create_deployment(k, a, ns)
         elif a.verb == "expose":
             return _expose(k, a, ns)
+        elif a.verb == "apply" and a.server_side:
+            if not a.filename:
+                raise SystemExit("error: must specify -f FILE")
+            for r in server_apply_objects(k, load_manifests(a.filename), a.field_manager, a.force_conflicts,
+                                          dry_run=a.dry_run == "server"):
+                print(f"{r['kind'].lower()}/{r['name']} {r['action']}" + (" (server dry run)" if a.dry_run == "server" else ""))
         elif a.verb in ("create", "apply"):
             if not a.filename:
                 raise SystemExit("error: must specify -f FILE")

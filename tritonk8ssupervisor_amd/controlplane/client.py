@@ -45,7 +45,8 @@ class Client:
                 self._conn = None
 
     def request(self, method: str, path: str, body: Any = None, query: dict | None = None,
-                timeout: float | None = None, raw: bool = False, ok=(200, 201, 202, 204)) -> Any:
+                timeout: float | None = None, raw: bool = False, ok=(200, 201, 202, 204),
+                content_type: str | None = None) -> Any:
         url = path if path.startswith("/") else "/" + path
         if query:
             url += ("&" if "?" in url else "?") + urlencode({k: v for k, v in query.items() if v is not None})
@@ -57,7 +58,7 @@ class Client:
                 headers["Content-Type"] = "text/plain"
             else:
                 data = json.dumps(body).encode()
-                headers["Content-Type"] = "application/json"
+                headers["Content-Type"] = content_type or "application/json"
         if self.token:
             headers["Authorization"] = f"Bearer {self.token}"
         t = self.timeout if timeout is None else timeout

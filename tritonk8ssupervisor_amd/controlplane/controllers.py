@@ -120,6 +120,9 @@ class Controllers:
                                     ("copy-gbps", ("copy", "kernel_gbps")), ("probe-ms", ("timings_ms", "total")),
                                     ("hip-init-ms", ("timings_ms", "hip_init"))):
                         v = result.get(path[0], {}).get(path[1]) if isinstance(result.get(path[0]), dict) else None
+                        if k.endswith(("gbps", "mbps")) and (result.get("hbm") or {}).get("timing") == "implausible":
+                            ann["tk8s.amd.com/probe-timing"] = "implausible (GPU timestamps above the HBM peak)"
+                            continue
                         if v is not None:
                             ann[f"tk8s.amd.com/{k}"] = f"{v:.1f}"
 

@@ -14,8 +14,9 @@ from pathlib import Path
 from ..utils.ids import token_hex
 from ..utils.net import host_port
 from ..utils.trace import trace
-from . import k8s_wire
+from . import k8s_openapi, k8s_wire, ssa
 from .httpserver import HttpError, Request, Response, StreamResponse
+from .store import now_iso
 from .objects import (
     GPU, _key, _set_ready, merge_patch, _admit_gpu_visibility, _normalize_data, labels_match, _parse_selector,
 )
@@ -203,20 +204,54 @@ class KubernetesAPI:
             return self._strip(o)
         return h
 
+    @staticmethod
+    def _manager(req: Request) -> str:
+        """The field manager of a write: ``?fieldManager=``, else the client's User-Agent name
+        (what the API server does: ``kubectl/v1.31.0 (linux/amd64) ...`` -> ``kubectl``)."""
+        m = req.q("fieldManager")
+        if m:
+            return m[:128]
+        ua = (req.headers.get("user-agent") or "unknown").split("/", 1)[0].strip()
+        return (ua or "unknown")[:128]
+
+    @staticmethod
+    def _dry_run(req: Request) -> bool:
+        d = req.q_all("dryRun")
+        if any(x not in ("All", "") for x in d):
+            raise HttpError(400, f"unsupported dryRun value {d}; the only one is All")
+        return bool(d)
+
+    @staticmethod
+    def _field_warnings(req: Request, kind: str, body) -> dict[str, str]:
+        """``?fieldValidation=Strict`` -> 400 on unknown fields; ``Warn`` -> Warning headers."""
+        mode = req.q("fieldValidation")
+        bad = k8s_openapi.check_fields(kind, body, mode)
+        if not bad:
+            return {}
+        if mode.lower() == "strict":
+            raise HttpError(400, "strict decoding error: " + ", ".join(bad))
+        return {"Warning": ", ".join('299 - "%s"' % b.replace('"', "'") for b in bad)}
+
     def _creator(self, kind: str):
         async def h(req: Request, ns: str, pid: str | None = None):
             p = self._pid(pid, req)
             self._auth(req, self.project(p))
             body = req.json()
-            return Response(201, self._strip(self.create(p, kind, ns, body)))
+            if not isinstance(body, dict):
+                raise HttpError(400, "the body must be a JSON object")
+            warn = self._field_warnings(req, kind, body)
+            o = self.create(p, kind, ns, body, manager=self._manager(req), dry_run=self._dry_run(req))
+            return Response(201, self._strip(o), headers=warn)
         return h
 
     def _replacer(self, kind: str, merge: bool):
         async def h(req: Request, ns: str, name: str, pid: str | None = None):
             p = self._pid(pid, req)
             self._auth(req, self.project(p))
-            body = req.json()
             ctype = (req.headers.get("content-type") or "").split(";")[0].strip()
+            if merge and ctype == k8s_wire.APPLY_PATCH:
+                return await self._apply(req, p, kind, ns, name)
+            body = req.json()
             if merge and ctype in (k8s_wire.JSON_PATCH, k8s_wire.STRATEGIC_PATCH):
                 cur = self.store.get(kind, _key(p, ns, name))
                 if cur is None:
@@ -229,13 +264,58 @@ class KubernetesAPI:
                 if not isinstance(full, dict):
                     raise HttpError(422, "the patched object is not an object")
                 full.setdefault("metadata", {})["resourceVersion"] = cur["metadata"].get("resourceVersion")
-                return self._strip(self.replace(p, kind, ns, name, full, merge=False))
-            if merge and ctype == k8s_wire.APPLY_PATCH:
-                raise HttpError(415, "server-side apply is not supported; use client-side kubectl apply")
+                return self._strip(self.replace(p, kind, ns, name, full, merge=False, manager=self._manager(req),
+                                                dry_run=self._dry_run(req)))
             if not isinstance(body, dict):
                 raise HttpError(422, "the body must be a JSON object")
-            return self._strip(self.replace(p, kind, ns, name, body, merge=merge))
+            warn = self._field_warnings(req, kind, body)
+            o = self.replace(p, kind, ns, name, body, merge=merge, manager=self._manager(req), dry_run=self._dry_run(req))
+            return Response(200, self._strip(o), headers=warn)
         return h
+
+    async def _apply(self, req: Request, p: str, kind: str, ns: str, name: str):
+        """Server-side apply (``PATCH`` + ``application/apply-patch+yaml``, ssa.py): create or merge
+        the manager's configuration; 409 with one cause per conflicting field unless force=true."""
+        try:
+            body = json.loads(req.body or b"{}")
+        except ValueError:
+            import yaml  # local import: only apply bodies sent as YAML need it
+
+            try:
+                body = yaml.safe_load(req.body)
+            except yaml.YAMLError as e:
+                raise HttpError(400, f"invalid apply body: {e}") from e
+        if not isinstance(body, dict):
+            raise HttpError(400, "the apply body must be an object")
+        manager = req.q("fieldManager")
+        if not manager:
+            raise HttpError(400, "PATCH, application/apply-patch+yaml: fieldManager is required for apply requests")
+        api_version, kind_name = k8s_wire.type_meta()[kind]
+        if body.get("apiVersion") != api_version or body.get("kind") != kind_name:
+            raise HttpError(400, f"apply: apiVersion/kind must be {api_version}/{kind_name}, "
+                                 f"got {body.get('apiVersion')}/{body.get('kind')}")
+        md = body.get("metadata") or {}
+        if md.get("name") not in (None, name):
+            raise HttpError(400, f"the name of the object ({md.get('name')}) does not match the name on the URL ({name})")
+        if md.get("namespace") not in (None, ns):
+            raise HttpError(400, f"the namespace of the object ({md.get('namespace')}) does not match the namespace "
+                                 f"on the URL ({ns})")
+        warn = self._field_warnings(req, kind, body)
+        dry = self._dry_run(req)
+        cur = self.store.get(kind, _key(p, ns, name))
+        try:
+            out = ssa.apply(self._strip(cur) if cur else None, body, manager, req.q("force") in ("true", "1"),
+                            api_version)
+        except ssa.Conflict as e:
+            st = e.status()
+            raise HttpError(409, st["message"], body=st) from e
+        out.setdefault("metadata", {})["name"] = name
+        if cur is None:
+            return Response(201, self._strip(self.create(p, kind, ns, out, dry_run=dry, keep_managed=True)),
+                            headers=warn)
+        out["metadata"]["resourceVersion"] = cur["metadata"].get("resourceVersion")
+        return Response(200, self._strip(self.replace(p, kind, ns, name, out, keep_managed=True, dry_run=dry)),
+                        headers=warn)
 
     async def h_scale(self, req: Request, ns: str, name: str, pid: str | None = None):
         """The Deployment ``scale`` subresource (autoscaling/v1 Scale): kubectl scale."""
@@ -258,7 +338,8 @@ class KubernetesAPI:
             n = (body.get("spec") or {}).get("replicas")
             if not isinstance(n, int) or isinstance(n, bool) or n < 0:
                 raise HttpError(422, "spec.replicas must be a non-negative integer")
-            d = self.replace(p, "deployments", ns, name, {"spec": {"replicas": n}}, merge=True)
+            d = self.replace(p, "deployments", ns, name, {"spec": {"replicas": n}}, merge=True,
+                             manager=self._manager(req), subresource="scale", dry_run=self._dry_run(req))
         sel = (d["spec"].get("selector") or {}).get("matchLabels") or {}
         return {"kind": "Scale", "apiVersion": "autoscaling/v1",
                 "metadata": {"name": name, "namespace": ns, "resourceVersion": d["metadata"]["resourceVersion"]},
@@ -270,6 +351,10 @@ class KubernetesAPI:
         async def h(req: Request, ns: str, name: str, pid: str | None = None):
             p = self._pid(pid, req)
             self._auth(req, self.project(p))
+            if self._dry_run(req):
+                if self.store.get(kind, _key(p, ns, name)) is None:
+                    raise HttpError(404, f'{kind} "{name}" not found')
+                return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
             o = self.store.delete(kind, _key(p, ns, name))
             if o is None:
                 raise HttpError(404, f'{kind} "{name}" not found')
@@ -432,8 +517,14 @@ class KubernetesAPI:
                 return [o["spec"]["clusterIP"]]
         return None
 
-    def create(self, pid: str, kind: str, ns: str, body: dict) -> dict:
+    def create(self, pid: str, kind: str, ns: str, body: dict, manager: str | None = None, dry_run: bool = False,
+               keep_managed: bool = False) -> dict:
+        """Create an object. ``manager``: the client's field manager, recorded in
+        ``metadata.managedFields`` (ssa.py); ``keep_managed``: the body already carries them (a
+        server-side apply); ``dry_run``: everything but the write."""
         md = body.setdefault("metadata", {})
+        if not keep_managed:
+            md.pop("managedFields", None)
         name = md.get("name")
         if not name and md.get("generateName"):
             name = md["generateName"] + token_hex(3)
@@ -466,16 +557,27 @@ class KubernetesAPI:
             _normalize_data(kind, body)
         elif kind == "ingresses":
             body["status"] = {"loadBalancer": {"ingress": [{"ip": self.advertise or self.host}]}}
+        if manager and not keep_managed:
+            m = ssa.Managed(None, k8s_wire.type_meta()[kind][0])
+            m.update(None, body, manager)
+            md["managedFields"] = m.entries()
+        if dry_run:
+            return {**copy.deepcopy(body), "metadata": {**copy.deepcopy(md), "uid": "dry-run",
+                                                        "creationTimestamp": now_iso()}}
         o = self.store.put(kind, key, body)
         if kind in ("services", "ingresses"):
             self._sync_proxy()
         self.reconcile()
         return o
 
-    def replace(self, pid: str, kind: str, ns: str, name: str, body: dict, merge: bool = False) -> dict:
+    def replace(self, pid: str, kind: str, ns: str, name: str, body: dict, merge: bool = False,
+                manager: str | None = None, subresource: str = "", keep_managed: bool = False,
+                dry_run: bool = False) -> dict:
         """PUT (``merge=False``: the whole object, optimistic concurrency on resourceVersion) or
         PATCH (``merge=True``: RFC 7386 merge patch). Status stays server-owned; identity fields,
-        a Service's clusterIP and a Job's / Pod's spec are immutable, as in Kubernetes."""
+        a Service's clusterIP and a Job's / Pod's spec are immutable, as in Kubernetes.
+        ``manager`` takes the fields it changed (``metadata.managedFields``, ssa.py) -- clients
+        cannot rewrite those entries, except a server-side apply (``keep_managed``)."""
         key = _key(pid, ns, name)
         cur = self.store.get(kind, key)
         if cur is None:
@@ -521,6 +623,20 @@ class KubernetesAPI:
             self._alloc_service(new, exclude=key)
         if kind in ("configmaps", "secrets"):
             _normalize_data(kind, new)
+        old_mf = cur["metadata"].get("managedFields")
+        if not keep_managed:
+            md.pop("managedFields", None)
+            if old_mf:
+                md["managedFields"] = copy.deepcopy(old_mf)
+            if manager:
+                m = ssa.Managed(old_mf, k8s_wire.type_meta()[kind][0])
+                m.update(self._strip(cur), new, manager, subresource)
+                md["managedFields"] = m.entries()
+        if not md.get("managedFields"):
+            md.pop("managedFields", None)
+        if dry_run:
+            return {**copy.deepcopy(new), "metadata": {**copy.deepcopy(md),
+                                                       "resourceVersion": cur["metadata"].get("resourceVersion")}}
         new["_project"] = pid
         o = self.store.put(kind, key, new)
         if kind in ("services", "ingresses"):

@@ -128,7 +128,7 @@ def is_k8s_path(path: str) -> bool:
     if path.startswith("/r/projects/"):
         parts = path.split("/", 5)  # '', r, projects, pid, kubernetes, rest
         path = "/" + parts[5] if len(parts) > 5 and parts[4] == "kubernetes" else ""
-    return path == "/api" or path.startswith(("/api/", "/apis"))
+    return path == "/api" or path.startswith(("/api/", "/apis", "/openapi/"))
 
 
 # ---- field selectors ----------------------------------------------------------------------

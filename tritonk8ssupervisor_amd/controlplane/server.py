@@ -44,7 +44,7 @@ from pathlib import Path
 
 from ..utils.net import host_port
 from ..utils.trace import trace
-from . import k8s_wire
+from . import k8s_openapi, k8s_wire
 from .controllers import Controllers
 from .httpserver import HttpError, HttpServer, Request, Response, Router
 from .k8s_api import KubernetesAPI
@@ -162,6 +162,8 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
         for pre in (r"/r/projects/(?P<pid>[^/]+)/kubernetes", r""):
             def add(method, path, h, pre=pre):
                 r.add(method, pre + path, h)
+            add("GET", r"/openapi/v3/?", self.h_openapi_root)
+            add("GET", r"/openapi/v3/(?P<gv>api/[^/]+|apis/[^/]+/[^/]+)", self.h_openapi_gv)
             add("GET", r"/api/?", self.h_api_versions)
             add("GET", r"/apis/?", self.h_api_groups)
             add("GET", r"/api/v1/?", self.h_api_resources)
@@ -195,11 +197,25 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
     @staticmethod
     def _error_body(path: str, e: HttpError):
         if k8s_wire.is_k8s_path(path):
+            if e.custom_body and isinstance(e.body, dict) and e.body.get("kind") == "Status":
+                return e.body  # e.g. a server-side apply conflict with its causes
             return k8s_wire.status_body(e.status, e.message)
         return e.body
 
     async def h_api_versions(self, req: Request, pid: str | None = None):
         return k8s_wire.api_versions(req.headers.get("host") or f"{self.host}:{self.port}")
+
+    async def h_openapi_root(self, req: Request, pid: str | None = None):
+        return k8s_openapi.root(f"/r/projects/{pid}/kubernetes" if pid else "")
+
+    async def h_openapi_gv(self, req: Request, gv: str, pid: str | None = None):
+        d = k8s_openapi.document(gv)
+        if d is None:
+            raise HttpError(404, f"no OpenAPI document for {gv}")
+        doc, h = d
+        # a hash-addressed document never changes: clients may cache it for good
+        return Response(200, doc, headers={"Cache-Control": "public, immutable" if req.q("hash") == h else "no-cache",
+                                           "Etag": f'"{h}"'})
 
     async def h_api_groups(self, req: Request, pid: str | None = None):
         return k8s_wire.api_group_list()

@@ -10,6 +10,7 @@ from pathlib import Path
 
 from . import templating
 from .controlplane.client import ApiError, Client
+from .controlplane.k8s_wire import APPLY_PATCH
 from .utils import yamlio
 
 KINDS = {
@@ -105,6 +106,25 @@ def apply_objects(k: Client, objs: list[dict]) -> list[dict]:
             k.put(path, body)
             action = "configured"
         res.append({"kind": kind, "name": name, "created": False, "action": action})
+    return res
+
+
+def server_apply_objects(k: Client, objs: list[dict], manager: str = "kubectl", force: bool = False,
+                         dry_run: bool = False) -> list[dict]:
+    """``kubectl apply --server-side``: one ``PATCH application/apply-patch+yaml`` per object; the
+    control plane merges it and tracks field ownership (controlplane/ssa.py). A conflict with
+    another manager raises ApiError 409 unless ``force`` (``--force-conflicts``)."""
+    res = []
+    for o in objs:
+        kind = o.get("kind", "")
+        if kind.lower() == "namespace":
+            res.append({"kind": kind, "name": o["metadata"]["name"], "created": False, "action": "unchanged"})
+            continue
+        ns = o.get("metadata", {}).get("namespace", "default")
+        name = o["metadata"]["name"]
+        q = {"fieldManager": manager, "force": "true" if force else None, "dryRun": "All" if dry_run else None}
+        k.request("PATCH", k.k8s(object_path(kind, name, ns)), body=o, query=q, content_type=APPLY_PATCH)
+        res.append({"kind": kind, "name": name, "action": "serverside-applied"})
     return res
 
 
