@@ -321,6 +321,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--field-manager", default="kubectl")
     ap.add_argument("--dry-run", choices=["none", "client", "server"], default="none")
     ap.add_argument("--show-managed-fields", action="store_true")
+    ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -494,6 +495,17 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             sys.stdout.write(r.get("stdout", ""))
             sys.stderr.write(r.get("stderr", ""))
             return int(r.get("exitCode", 1))
+        elif a.verb == "port-forward":
+            from .kubectl_streams import port_forward
+
+            if not a.args:
+                raise SystemExit("usage: kubectl port-forward TYPE/NAME [LOCAL_PORT:]REMOTE_PORT ...")
+            return port_forward(k, ns, a.args[0], a.args[1:], a.address)
+        elif a.verb == "attach":
+            from .kubectl_streams import attach
+
+            what, name = _target(a.args) if "/" in (a.args[0] if a.args else "") else ("pod", (a.args or [""])[0])
+            return attach(k, ns, name)
         elif a.verb in ("cordon", "uncordon"):
             k.request("PATCH", k.k8s(f"/api/v1/nodes/{a.args[0]}"), body={"spec": {"unschedulable": a.verb == "cordon"}})
             print(f"node/{a.args[0]} {a.verb}ed")

@@ -1,0 +1,168 @@
+"""The bundled kubectl's stream commands over the control plane's WebSocket channel endpoints:
+
+* ``port-forward TARGET [LOCAL:]REMOTE ...`` -- TARGET is ``pod/NAME`` (or ``NAME``),
+  ``deployment/NAME`` or ``service/NAME`` (a running pod the selector matches; a Service's port is
+  mapped to its targetPort, as kubectl does). Every accepted local connection gets its own
+  WebSocket (``v4.channel.k8s.io``, data channel 0, error channel 1).
+* ``attach POD`` -- the pod's output from now on until it stops (output only).
+
+What kubectl prints ("Forwarding from 127.0.0.1:8080 -> 80", "Handling connection for 8080") is
+kept, so scripts that wait for that line work unchanged.
+"""
+from __future__ import annotations
+
+import json
+import socket
+import sys
+import threading
+import time
+
+from ..controlplane.wsclient import WSClient, WSClosed
+from ..kube import kind_key, object_path
+
+
+def _labels_match(sel: dict, labels: dict) -> bool:
+    return all(labels.get(k) == v for k, v in (sel or {}).items())
+
+
+def resolve_pod(k, target: str, ns: str, ports: list[int]) -> tuple[str, list[int]]:
+    """TARGET -> (running pod name, remote ports after Service port -> targetPort mapping)."""
+    what, name = target.split("/", 1) if "/" in target else ("pod", target)
+    kind = kind_key(what)
+    if kind == "pod":
+        return name, ports
+    obj = k.get(k.k8s(object_path(kind, name, ns)))
+    if kind == "service":
+        sel = obj["spec"].get("selector") or {}
+        mapped = []
+        for p in ports:
+            sp = next((x for x in obj["spec"].get("ports", []) if x.get("port") == p), None)
+            if sp is None:
+                raise SystemExit(f"error: Service {name} does not have a service port {p}")
+            tp = sp.get("targetPort", p)
+            mapped.append(int(tp) if str(tp).isdigit() else p)
+        ports = mapped
+    elif kind in ("deployment", "daemonset", "job"):
+        sel = (obj["spec"].get("selector") or {}).get("matchLabels") or {}
+    else:
+        raise SystemExit(f"error: cannot port-forward to {what}")
+    pods = k.get(k.k8s(f"/api/v1/namespaces/{ns}/pods"))["items"]
+    for p in sorted(pods, key=lambda p: p["metadata"]["name"]):
+        if p.get("status", {}).get("phase") == "Running" and _labels_match(sel, p["metadata"].get("labels", {})):
+            return p["metadata"]["name"], ports
+    raise SystemExit(f"error: no running pod for {target}")
+
+
+def _pump_ws_to_sock(ws: WSClient, conn: socket.socket, port: int, last: list[float]) -> None:
+    headers = 0
+    try:
+        while (msg := ws.recv()) is not None:
+            last[0] = time.monotonic()
+            if not msg:
+                continue
+            ch, data = msg[0], msg[1:]
+            if headers < 2 and len(data) == 2:  # the two port frames that open the stream
+                headers += 1
+                continue
+            if ch == 0:
+                conn.sendall(data)
+            elif ch == 1 and data:
+                print(f"E port-forward {port}: {data.decode(errors='replace')}", file=sys.stderr, flush=True)
+    except OSError:
+        pass
+    finally:
+        try:
+            conn.shutdown(socket.SHUT_WR)
+        except OSError:
+            pass
+
+
+def _forward_one(k, pod: str, ns: str, remote: int, conn: socket.socket) -> None:
+    try:
+        ws = WSClient.connect(k.host, k.port, k.k8s(object_path("pod", pod, ns) + "/portforward"),
+                              [("ports", str(remote))], k.token, ("v4.channel.k8s.io",))
+    except (OSError, WSClosed) as e:
+        print(f"E port-forward {remote}: {e}", file=sys.stderr, flush=True)
+        conn.close()
+        return
+    last = [time.monotonic()]
+    t = threading.Thread(target=_pump_ws_to_sock, args=(ws, conn, remote, last), daemon=True)
+    t.start()
+    try:
+        while chunk := conn.recv(1 << 16):
+            ws.send(b"\x00" + chunk)
+    except OSError:
+        pass
+    # The local side is done sending. The channel protocol has no half-close, so keep relaying
+    # the pod's answer while it still comes (0.5 s without data ends it), then close the stream.
+    deadline = time.monotonic() + 30
+    while t.is_alive() and time.monotonic() < deadline and time.monotonic() - last[0] < 0.5:
+        t.join(0.1)
+    ws.close()
+    conn.close()
+
+
+def port_forward(k, ns: str, target: str, specs: list[str], address: str = "127.0.0.1") -> int:
+    if not specs:
+        raise SystemExit("usage: kubectl port-forward TYPE/NAME [LOCAL_PORT:]REMOTE_PORT ...")
+    pairs = []
+    for sp in specs:
+        local, _, remote = sp.rpartition(":")
+        pairs.append((int(local) if local else (0 if ":" in sp else int(remote)), int(remote)))
+    pod, remotes = resolve_pod(k, target, ns, [r for _l, r in pairs])
+    listeners = []
+    for (local, _r), remote in zip(pairs, remotes):
+        s = socket.socket(socket.AF_INET6 if ":" in address else socket.AF_INET)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        s.bind((address, local))
+        s.listen(64)
+        print(f"Forwarding from {address}:{s.getsockname()[1]} -> {remote}", flush=True)
+        listeners.append((s, remote))
+
+    def serve(s: socket.socket, remote: int):
+        while True:
+            try:
+                conn, _ = s.accept()
+            except OSError:
+                return
+            print(f"Handling connection for {s.getsockname()[1]}", flush=True)
+            threading.Thread(target=_forward_one, args=(k, pod, ns, remote, conn), daemon=True).start()
+
+    threads = [threading.Thread(target=serve, args=ls, daemon=True) for ls in listeners]
+    for t in threads:
+        t.start()
+    try:
+        for t in threads:
+            t.join()
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
+def attach(k, ns: str, pod: str) -> int:
+    """Stream the pod's output (channel 1) until its Status (channel 3)."""
+    try:
+        ws = WSClient.connect(k.host, k.port, k.k8s(object_path("pod", pod, ns) + "/attach"),
+                              [("stdout", "true"), ("stderr", "true")], k.token,
+                              ("v5.channel.k8s.io", "v4.channel.k8s.io"))
+    except (OSError, WSClosed) as e:
+        print(f"error: {e}", file=sys.stderr)
+        return 1
+    code = 0
+    try:
+        while (msg := ws.recv()) is not None:
+            if msg[:1] == b"\x01":
+                sys.stdout.buffer.write(msg[1:])
+                sys.stdout.flush()
+            elif msg[:1] == b"\x02":
+                sys.stderr.buffer.write(msg[1:])
+            elif msg[:1] == b"\x03":
+                st = json.loads(msg[1:] or b"{}")
+                code = 0 if st.get("status") == "Success" else 1
+                if code:
+                    print(f"error: {st.get('message', 'attach ended')}", file=sys.stderr)
+                break
+    except KeyboardInterrupt:
+        pass
+    ws.close()
+    return code

@@ -94,6 +94,7 @@ class WebSocket:
     def __init__(self, reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
         self.reader, self.writer = reader, writer
         self.closed = False
+        self._send_lock = asyncio.Lock()  # several tasks send (port-forward: one per port)
 
     async def send(self, data: bytes, opcode: int = 0x2) -> None:
         n = len(data)
@@ -104,8 +105,9 @@ class WebSocket:
             head += bytes([126]) + n.to_bytes(2, "big")
         else:
             head += bytes([127]) + n.to_bytes(8, "big")
-        self.writer.write(head + data)
-        await self.writer.drain()
+        async with self._send_lock:
+            self.writer.write(head + data)
+            await self.writer.drain()
 
     async def recv(self) -> bytes | None:
         """The next message's payload; None once the client closed."""
@@ -122,8 +124,9 @@ class WebSocket:
                 raise HttpError(413, "websocket frame too large")
             mask = await self.reader.readexactly(4) if h[1] & 0x80 else b""
             data = await self.reader.readexactly(n)
-            if mask:
-                data = bytes(b ^ mask[i & 3] for i, b in enumerate(data))
+            if mask and n:  # unmask as one big-integer XOR (port-forward moves MBs through here)
+                m = (mask * (n // 4 + 1))[:n]
+                data = (int.from_bytes(data, "little") ^ int.from_bytes(m, "little")).to_bytes(n, "little")
             if opcode == 0x8:
                 self.closed = True
                 return None

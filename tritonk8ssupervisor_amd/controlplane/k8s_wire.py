@@ -25,7 +25,7 @@ import time
 
 # plural -> (group, version, Kind, singular, namespaced, short names, subresources)
 RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str, ...]]] = {
-    "pods": ("", "v1", "Pod", "pod", True, ("po",), ("log", "status", "exec")),
+    "pods": ("", "v1", "Pod", "pod", True, ("po",), ("log", "status", "exec", "portforward", "attach")),
     "services": ("", "v1", "Service", "service", True, ("svc",), ()),
     "events": ("", "v1", "Event", "event", True, ("ev",), ()),
     "configmaps": ("", "v1", "ConfigMap", "configmap", True, ("cm",), ()),
@@ -98,7 +98,8 @@ def api_resource_list(group: str, version: str) -> dict | None:
         res.append(r)
         for s in subs:
             sub = {"name": f"{plural}/{s}", "singularName": "", "namespaced": namespaced, "kind": kind,
-                   "verbs": ["get"] if s == "log" else ["create"] if s == "exec" else ["get", "patch", "update"]}
+                   "verbs": ["get"] if s == "log" else ["create", "get"] if s in ("exec", "portforward", "attach")
+                   else ["get", "patch", "update"]}
             if s == "scale":
                 sub.update(kind="Scale", group="autoscaling", version="v1")
             res.append(sub)
