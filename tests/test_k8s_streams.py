@@ -90,6 +90,12 @@ def test_portforward_wire_protocol(cluster, echo):
     closed.bind(("127.0.0.1", 0))
     dead = closed.getsockname()[1]
     closed.close()
+    # a pod IP the node did not register (or outside its pod CIDR) is refused
+    _set(nc, "Running")
+    nc.put(nc.k8s("/api/v1/namespaces/default/pods/srv/status"), {"status": {"podIP": "10.9.9.9"}})
+    with pytest.raises(WSClosed, match="403"):
+        _ws(k, "portforward", [("ports", str(echo))], ("v4.channel.k8s.io",))
+    _set(nc, "Running")
     ws = _ws(k, "portforward", [("ports", f"{echo},{dead}")], ("v4.channel.k8s.io",))
     assert ws.protocol == "v4.channel.k8s.io"
     first = [ws.recv() for _ in range(4)]
