@@ -320,3 +320,53 @@ def test_imperative_create_deployment_and_expose(cluster):
     url = f"http://{_until(lambda: json.loads(kc('get', 'svc', 'hello', '-o', 'json').stdout)['status']['loadBalancer']['ingress'])[0]['ip']}:{host_port(80)}/"
     assert "Welcome to nginx!" in _until(lambda: _get(url))
     assert kc("create", "deployment", "broken", check=False).returncode != 0  # --image is required
+
+
+def test_statefulset_cronjob_and_port_forward_on_a_real_cluster(cluster):
+    """A StatefulSet behind a headless Service (stable names, DNS per pod, HOSTNAME), a CronJob
+    whose Jobs run, and ./kubectl port-forward to a pod's own IP -- with real node agents."""
+    from tritonk8ssupervisor_amd.controlplane import dns
+
+    ws, env, kc, summary = cluster
+    (ws / "sts.json").write_text(json.dumps({"apiVersion": "v1", "kind": "List", "items": [
+        {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "web"},
+         "spec": {"clusterIP": "None", "selector": {"app": "web"}, "ports": [{"port": 8000}]}},
+        {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "web"},
+         "spec": {"replicas": 2, "serviceName": "web", "selector": {"matchLabels": {"app": "web"}},
+                  "template": {"metadata": {"labels": {"app": "web"}}, "spec": {"containers": [{
+                      "name": "c", "image": "python",
+                      "command": ["sh", "-c", "echo host=$HOSTNAME; exec python3 -m http.server 8000 --bind $(POD_IP)"]}]}}}},
+        {"apiVersion": "batch/v1", "kind": "CronJob", "metadata": {"name": "tick"},
+         "spec": {"schedule": "@every 2s", "jobTemplate": {"spec": {"template": {"spec": {
+             "restartPolicy": "Never", "containers": [{"name": "c", "image": "busybox", "command": ["echo", "tick"]}]}}}}}}]}))
+    kc("apply", "-f", "sts.json")
+
+    def pods():
+        return {p["metadata"]["name"]: p for p in json.loads(kc("get", "pods", "-o", "json").stdout)["items"]}
+
+    _until(lambda: all(pods().get(n, {}).get("status", {}).get("phase") == "Running" for n in ("web-0", "web-1")), 60)
+    assert "host=web-1" in kc("logs", "web-1").stdout
+    ip = kc("cluster-info").stdout.split("://", 1)[1].split(":", 1)[0]  # the master's address
+    p0 = pods()["web-0"]["status"]["podIP"]
+    with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+        s.settimeout(5)
+        s.sendto(dns.query("web-0.web.default.svc.cluster.local"), (ip, host_port(53)))
+        assert dns.parse_reply(s.recv(512)) == (0, [p0])
+    assert "web" in kc("get", "sts").stdout
+    # a CronJob's Jobs run to completion
+    _until(lambda: any(j.get("status", {}).get("succeeded") for j in json.loads(kc("get", "jobs", "-o", "json").stdout)["items"]
+                       if j["metadata"]["name"].startswith("tick-")), 30)
+    assert "@every 2s" in kc("get", "cronjobs").stdout
+    # port-forward to web-0's own address
+    pf = subprocess.Popen(["./kubectl", "port-forward", "pod/web-0", ":8000"], cwd=ws, env=env,
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        line = pf.stdout.readline()
+        local = int(line.split(":")[1].split()[0])
+        assert "Directory listing" in _get(f"http://127.0.0.1:{local}/")
+    finally:
+        pf.terminate()
+        pf.wait(10)
+    kc("scale", "sts/web", "--replicas", "1")
+    _until(lambda: "web-1" not in pods(), 30)
+    kc("delete", "cronjob", "tick")

@@ -1,0 +1,242 @@
+"""StatefulSets, ReplicaSets, CronJobs and headless Services (controlplane/workloads.py,
+controlplane/cron.py), driven in-process: objects go through the API's create/replace, pod phases
+are reported the way a node agent does, and reconcile() runs as after every change."""
+import json
+import socket
+from datetime import datetime, timedelta, timezone
+
+import pytest
+
+from tritonk8ssupervisor_amd.controlplane import cron
+from tritonk8ssupervisor_amd.controlplane.httpserver import HttpError
+from tritonk8ssupervisor_amd.controlplane.objects import _key
+from tritonk8ssupervisor_amd.controlplane.server import ControlPlane
+
+UTC = timezone.utc
+
+
+# ---- cron -----------------------------------------------------------------------------------
+def _t(s: str) -> datetime:
+    return datetime.strptime(s, "%Y-%m-%d %H:%M").replace(tzinfo=UTC)
+
+
+@pytest.mark.parametrize("expr,after,want", [
+    ("*/15 * * * *", "2026-03-01 10:07", "2026-03-01 10:15"),
+    ("0 3 * * *", "2026-03-01 10:07", "2026-03-02 03:00"),
+    ("30 9 * * mon-fri", "2026-10-16 10:00", "2026-10-19 09:30"),   # Friday after 9:30 -> Monday
+    ("0 0 1 jan,jul *", "2026-03-01 00:00", "2026-07-01 00:00"),
+    ("0 12 13 * 5", "2026-10-01 00:00", "2026-10-02 12:00"),        # dom OR dow: Friday the 2nd first
+    ("5 4 * * 7", "2026-10-17 00:00", "2026-10-18 04:05"),          # 7 is Sunday
+    ("@hourly", "2026-03-01 10:07", "2026-03-01 11:00"),
+    ("@weekly", "2026-10-14 10:00", "2026-10-18 00:00"),
+    ("0 0 29 2 *", "2026-03-01 00:00", "2028-02-29 00:00"),
+])
+def test_cron_next(expr, after, want):
+    assert cron.parse(expr, "UTC").next_after(_t(after)) == _t(want)
+
+
+@pytest.mark.parametrize("bad", ["* * * *", "61 * * * *", "* * * 13 *", "*/0 * * * *", "5-1 * * * *", "x * * * *",
+                                 "@every", "@every 5q", "* * * * * *"])
+def test_cron_rejects(bad):
+    with pytest.raises(cron.CronError):
+        cron.parse(bad, "UTC")
+
+
+def test_cron_every_timezones_and_missed_runs():
+    s = cron.parse("@every 1m30s")
+    assert s.every == 90.0
+    t0 = _t("2026-03-01 10:00")
+    assert cron.most_recent(s, t0, t0 + timedelta(seconds=89)) == (None, 0)
+    assert cron.most_recent(s, t0, t0 + timedelta(seconds=200)) == (t0 + timedelta(seconds=180), 2)
+    hourly = cron.parse("0 * * * *", "UTC")
+    last, n = cron.most_recent(hourly, t0, t0 + timedelta(hours=5, minutes=10))
+    assert last == t0 + timedelta(hours=5) and n == 5
+    # a time zone moves the wall clock the schedule is read in
+    tokyo = cron.parse("CRON_TZ=Asia/Tokyo 0 9 * * *")
+    assert tokyo.next_after(_t("2026-03-01 00:30")) == _t("2026-03-02 00:00")  # 09:00 JST = 00:00 UTC
+
+
+# ---- in-process control plane -------------------------------------------------------------------
+@pytest.fixture
+def cp():
+    c = ControlPlane("127.0.0.1", 0)
+    c.store.put("projects", "1a1", {"id": "1a1", "created_seq": 1, "metadata": {"name": "1a1"}})
+    return c
+
+
+def _pods(c, prefix=""):
+    return sorted(o["metadata"]["name"] for o in c.store.list("pods") if o["metadata"]["name"].startswith(prefix))
+
+
+def _run(c, name, ip="127.128.0.{}"):
+    def fn(o):
+        o.setdefault("status", {}).update(phase="Running", podIP=ip.format(2 + int(name.rsplit("-", 1)[1], 16) % 200))
+    c.store.patch("pods", _key("1a1", "default", name), fn)
+    c.reconcile()
+
+
+def _sts(replicas=3, **spec):
+    return {"apiVersion": "apps/v1", "kind": "StatefulSet", "metadata": {"name": "web"},
+            "spec": {"replicas": replicas, "serviceName": "web", "selector": {"matchLabels": {"app": "web"}},
+                     "template": {"metadata": {"labels": {"app": "web"}},
+                                  "spec": {"containers": [{"name": "c", "image": "python", "command": ["sleep", "60"]}]}},
+                     **spec}}
+
+
+def test_statefulset_ordered_scaling_and_stable_names(cp):
+    cp.create("1a1", "statefulsets", "default", _sts(3))
+    assert _pods(cp, "web") == ["web-0"]  # OrderedReady: one at a time
+    p0 = cp.store.get("pods", _key("1a1", "default", "web-0"))
+    assert p0["spec"]["hostname"] == "web-0" and p0["spec"]["subdomain"] == "web"
+    assert p0["metadata"]["labels"]["apps.kubernetes.io/pod-index"] == "0"
+    _run(cp, "web-0")
+    assert _pods(cp, "web") == ["web-0", "web-1"]
+    _run(cp, "web-1")
+    _run(cp, "web-2")
+    st = cp.store.get("statefulsets", _key("1a1", "default", "web"))["status"]
+    assert st["readyReplicas"] == 3 and st["updatedReplicas"] == 3 and st["currentRevision"] == st["updateRevision"]
+    # a deleted pod comes back under its own name
+    cp.store.delete("pods", _key("1a1", "default", "web-1"))
+    cp.reconcile()
+    assert "web-1" in _pods(cp, "web")
+    _run(cp, "web-1")
+    # scale down: the highest ordinal first, one at a time
+    cur = cp.store.get("statefulsets", _key("1a1", "default", "web"))
+    body = json.loads(json.dumps(cp._strip(cur)))
+    body["spec"]["replicas"] = 1
+    cp.replace("1a1", "statefulsets", "default", "web", body)
+    assert _pods(cp, "web") == ["web-0", "web-1"]
+    cp.reconcile()
+    assert _pods(cp, "web") == ["web-0"]
+    # identity fields are immutable
+    body = json.loads(json.dumps(cp._strip(cp.store.get("statefulsets", _key("1a1", "default", "web")))))
+    body["spec"]["serviceName"] = "other"
+    with pytest.raises(HttpError) as e:
+        cp.replace("1a1", "statefulsets", "default", "web", body)
+    assert e.value.status == 422
+
+
+def test_statefulset_rolling_update_and_parallel(cp):
+    cp.create("1a1", "statefulsets", "default", _sts(3, podManagementPolicy="Parallel"))
+    assert _pods(cp, "web") == ["web-0", "web-1", "web-2"]
+    for n in ("web-0", "web-1", "web-2"):
+        _run(cp, n)
+    old = {n: cp.store.get("pods", _key("1a1", "default", n))["metadata"]["uid"] for n in _pods(cp, "web")}
+    body = json.loads(json.dumps(cp._strip(cp.store.get("statefulsets", _key("1a1", "default", "web")))))
+    body["spec"]["template"]["spec"]["containers"][0]["command"] = ["sleep", "61"]
+    cp.replace("1a1", "statefulsets", "default", "web", body)
+
+    def uid(n):
+        return cp.store.get("pods", _key("1a1", "default", n))["metadata"]["uid"]
+
+    assert uid("web-2") != old["web-2"] and uid("web-1") == old["web-1"]  # highest ordinal first
+    _run(cp, "web-2")
+    assert uid("web-1") != old["web-1"] and uid("web-0") == old["web-0"]
+    _run(cp, "web-1")
+    _run(cp, "web-0")
+    st = cp.store.get("statefulsets", _key("1a1", "default", "web"))["status"]
+    assert st["updatedReplicas"] == 3 and st["currentRevision"] == st["updateRevision"]
+
+
+def test_headless_service_dns_for_statefulset_pods(cp):
+    cp.create("1a1", "services", "default", {"metadata": {"name": "web"}, "spec": {
+        "clusterIP": "None", "selector": {"app": "web"}, "ports": [{"port": 29500}]}})
+    assert cp.store.get("services", _key("1a1", "default", "web"))["spec"]["clusterIP"] == "None"
+    assert not any(k[1] == "None" for k in cp._proxy_wanted())  # no proxy listener for a headless Service
+    cp.create("1a1", "statefulsets", "default", _sts(2))
+    assert cp.dns_resolve("web-0.web.default.svc.cluster.local") is None  # not running yet
+    _run(cp, "web-0")
+    _run(cp, "web-1")
+    ip0 = cp.store.get("pods", _key("1a1", "default", "web-0"))["status"]["podIP"]
+    ip1 = cp.store.get("pods", _key("1a1", "default", "web-1"))["status"]["podIP"]
+    assert cp.dns_resolve("web-0.web.default.svc.cluster.local") == [ip0]
+    assert cp.dns_resolve("web-1.web.default.svc") == [ip1]
+    assert cp.dns_resolve("web.default.svc.cluster.local") == sorted([ip0, ip1])
+    assert cp.dns_resolve("web-7.web.default.svc.cluster.local") is None
+    with pytest.raises(HttpError):
+        cp.create("1a1", "services", "default", {"metadata": {"name": "bad"}, "spec": {
+            "clusterIP": "None", "type": "NodePort", "ports": [{"port": 80}]}})
+
+
+def test_replicaset(cp):
+    with pytest.raises(HttpError):  # the selector must match the template's labels
+        cp.create("1a1", "replicasets", "default", {"metadata": {"name": "rs"}, "spec": {
+            "selector": {"matchLabels": {"app": "x"}}, "template": {"metadata": {"labels": {"app": "y"}},
+                                                                 "spec": {"containers": [{"name": "c"}]}}}})
+    cp.create("1a1", "replicasets", "default", {"metadata": {"name": "rs"}, "spec": {
+        "replicas": 3, "selector": {"matchLabels": {"app": "rs"}},
+        "template": {"metadata": {"labels": {"app": "rs"}}, "spec": {"containers": [{"name": "c", "command": ["true"]}]}}}})
+    names = _pods(cp, "rs-")
+    assert len(names) == 3
+    _run(cp, names[0])
+    body = json.loads(json.dumps(cp._strip(cp.store.get("replicasets", _key("1a1", "default", "rs")))))
+    body["spec"]["replicas"] = 1
+    cp.replace("1a1", "replicasets", "default", "rs", body)
+    assert _pods(cp, "rs-") == [names[0]]  # the pods not yet running go first
+
+
+def _cronjob(**spec):
+    return {"apiVersion": "batch/v1", "kind": "CronJob", "metadata": {"name": "tick"},
+            "spec": {"schedule": "@every 10s", "jobTemplate": {"spec": {"template": {"spec": {
+                "restartPolicy": "Never", "containers": [{"name": "c", "command": ["true"]}]}}}}, **spec}}
+
+
+def _jobs(c):
+    return sorted(o["metadata"]["name"] for o in c.store.list("jobs"))
+
+
+def _finish(c, name, kind="Complete"):
+    c.store.patch("jobs", _key("1a1", "default", name), lambda o: o.setdefault("status", {}).update(
+        conditions=[{"type": kind, "status": "True"}], completionTime="2026-01-01T00:00:00Z"))
+
+
+def test_cronjob_schedules_policies_and_history(cp):
+    with pytest.raises(HttpError) as e:
+        cp.create("1a1", "cronjobs", "default", _cronjob(schedule="61 * * * *"))
+    assert e.value.status == 422
+    cj = cp.create("1a1", "cronjobs", "default", _cronjob(concurrencyPolicy="Forbid"))
+    t0 = datetime.strptime(cj["metadata"]["creationTimestamp"], "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=UTC)
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=5))
+    assert _jobs(cp) == []
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=11))
+    assert len(_jobs(cp)) == 1
+    job = cp.store.get("jobs", _key("1a1", "default", _jobs(cp)[0]))
+    assert job["metadata"]["ownerReferences"][0]["kind"] == "CronJob"
+    assert job["metadata"]["annotations"]["batch.kubernetes.io/cronjob-scheduled-timestamp"]
+    assert cp.store.list("pods", lambda o: o["metadata"]["name"].startswith(job["metadata"]["name"]))  # the Job ran
+    st = cp.store.get("cronjobs", _key("1a1", "default", "tick"))["status"]
+    assert len(st["active"]) == 1 and st["lastScheduleTime"]
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=21))  # Forbid: the first is still active
+    assert len(_jobs(cp)) == 1
+    _finish(cp, _jobs(cp)[0])
+    for k in range(3, 8):  # more runs than the history keeps
+        cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=10 * k + 1))
+        for j in _jobs(cp):
+            _finish(cp, j)
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=81))
+    st = cp.store.get("cronjobs", _key("1a1", "default", "tick"))["status"]
+    done = [j for j in _jobs(cp) if j != (st.get("active") or [{}])[0].get("name")]
+    assert len(done) <= 3 and st.get("lastSuccessfulTime")
+    # Replace: a new run replaces the active one; suspend: nothing runs
+    body = json.loads(json.dumps(cp._strip(cp.store.get("cronjobs", _key("1a1", "default", "tick")))))
+    body["spec"]["concurrencyPolicy"] = "Replace"
+    cp.replace("1a1", "cronjobs", "default", "tick", body)
+    before = set(_jobs(cp))
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=91))
+    active = cp.store.get("cronjobs", _key("1a1", "default", "tick"))["status"]["active"]
+    assert len(active) == 1 and active[0]["name"] not in before
+    body = json.loads(json.dumps(cp._strip(cp.store.get("cronjobs", _key("1a1", "default", "tick")))))
+    body["spec"]["suspend"] = True
+    cp.replace("1a1", "cronjobs", "default", "tick", body)
+    n = len(_jobs(cp))
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=200))
+    assert len(_jobs(cp)) == n
+
+
+def test_cronjob_starting_deadline_skips_a_late_run(cp):
+    cj = cp.create("1a1", "cronjobs", "default", _cronjob(startingDeadlineSeconds=5))
+    t0 = datetime.strptime(cj["metadata"]["creationTimestamp"], "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=UTC)
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=18))  # due at +10, 8 s late > 5 s
+    assert _jobs(cp) == []
+    cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=21))  # due at +20, 1 s late
+    assert len(_jobs(cp)) == 1

@@ -321,12 +321,14 @@ class Agent:
         c = spec["containers"][0]
         all_gpus = md.get("annotations", {}).get(ALL_GPUS) == "true"
         need = len(self.plugin.devices()) if all_gpus else pod_gpus(pod)
-        pp_dir = self.sandbox / "pods" / md["name"]
+        # (namespaces are DNS labels, so "<ns>_<name>" cannot collide with a default-namespace pod)
+        pp_dir = self.sandbox / "pods" / (md["name"] if md["namespace"] == "default" else f"{md['namespace']}_{md['name']}")
         pod_ip = self._pod_ip(key)
         # TK8S_MACHINE_DIR: the node's state dir (the hostPath the validation pod reads its
         # machine's burn-in result from)
         base = {"TK8S_HOME": TK8S_HOME, "TK8S_PYTHON": sys.executable, "TK8S_MACHINE_DIR": str(self.sandbox),
                 "POD_NAME": md["name"], "POD_NAMESPACE": md["namespace"], "POD_UID": md.get("uid", ""),
+                "HOSTNAME": spec.get("hostname") or md["name"],
                 "POD_IP": pod_ip, "NODE_NAME": self.name, "NODE_IP": self.ip, "TK8S_API_URL": self.base,
                 "TK8S_K8S_API": f"{self.base}{self.api.prefix}", "TK8S_KV_URL": f"{self.base}/v1/kv"}
         try:  # config first: a pod waiting for a ConfigMap must not hold GPUs
@@ -634,6 +636,12 @@ class Agent:
         phase = pod.get("status", {}).get("phase", "Pending")
         if phase in TERMINAL:
             return
+        cur = self.runtime.running().get(key)
+        if cur is not None and md.get("uid") and cur.uid and cur.uid != md["uid"]:
+            # the same name, a new pod (a StatefulSet's replacement) whose deletion event this
+            # watch did not see: the old process goes first
+            self.runtime.stop(key)
+            self._pod_ips.pop(key, None)
         if key not in self.runtime.running():
             trace(self.name, f"watch {etype} {key}")
             self._start_pod(pod)

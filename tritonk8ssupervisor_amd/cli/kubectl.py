@@ -110,9 +110,18 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
     elif k == "job":
         rows = [["NAME", "COMPLETIONS", "STATUS", "AGE"]] + [[o["metadata"]["name"],
                 f"{o.get('status', {}).get('succeeded', 0)}/{o['spec'].get('completions', 1)}", job_state(o), _age(o)] for o in items]
-    elif k == "deployment":
+    elif k in ("deployment", "statefulset"):
         rows = [["NAME", "READY", "AGE"]] + [[o["metadata"]["name"],
                 f"{o.get('status', {}).get('readyReplicas', 0)}/{o['spec'].get('replicas', 1)}", _age(o)] for o in items]
+    elif k == "replicaset":
+        rows = [["NAME", "DESIRED", "CURRENT", "READY", "AGE"]] + [[o["metadata"]["name"], str(o["spec"].get("replicas", 1)),
+                str(o.get("status", {}).get("replicas", 0)), str(o.get("status", {}).get("readyReplicas", 0)), _age(o)]
+                for o in items]
+    elif k == "cronjob":
+        rows = [["NAME", "SCHEDULE", "SUSPEND", "ACTIVE", "LAST SCHEDULE", "AGE"]] + [[
+            o["metadata"]["name"], o["spec"].get("schedule", ""), str(bool(o["spec"].get("suspend", False))),
+            str(len(o.get("status", {}).get("active") or [])), o.get("status", {}).get("lastScheduleTime", "<none>"), _age(o)]
+            for o in items]
     elif k == "service":
         def ports(o):
             return ",".join(f"{p['port']}" + (f"(host {host_port(p['port'])})" if host_port(p["port"]) != p["port"] else "")
@@ -413,10 +422,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 print(f"{r['kind'].lower()}/{r['name']} {r['action'] if a.verb == 'apply' else ('created' if r['created'] else 'unchanged')}")
         elif a.verb == "scale":
             what, name = _target(a.args)
-            if a.replicas is None or kind_key(what) != "deployment":
-                raise SystemExit("usage: kubectl scale deploy/NAME --replicas N")
-            k.request("PATCH", k.k8s(object_path("deployment", name, ns) + "/scale"), body={"spec": {"replicas": a.replicas}})
-            print(f"deployment.apps/{name} scaled")
+            if a.replicas is None or kind_key(what) not in ("deployment", "statefulset", "replicaset"):
+                raise SystemExit("usage: kubectl scale deploy|sts|rs/NAME --replicas N")
+            k.request("PATCH", k.k8s(object_path(kind_key(what), name, ns) + "/scale"), body={"spec": {"replicas": a.replicas}},
+                      query={"fieldManager": "kubectl-scale"})
+            print(f"{kind_key(what)}.apps/{name} scaled")
         elif a.verb == "rollout":
             sub = a.args[0] if a.args else ""
             what, name = _target(a.args[1:])

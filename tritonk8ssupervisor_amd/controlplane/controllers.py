@@ -28,6 +28,8 @@ class Controllers:
                     self._ctl_daemonsets(pid)
                     self._ctl_jobs(pid)
                     self._ctl_deployments(pid)
+                    self._ctl_statefulsets(pid)
+                    self._ctl_replicasets(pid)
                     self._ctl_validation(pid)
                     self._scheduler(pid)
                 if not self._again:

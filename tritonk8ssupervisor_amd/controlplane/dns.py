@@ -2,6 +2,9 @@
 docs/img/infrastructure-containers.png): authoritative A records under ``cluster.local``.
 
   <svc>.<ns>.svc.cluster.local   (also <svc>.<ns>.svc and <svc>.<ns>)   -> the Service's clusterIP
+                                 (a headless Service, clusterIP None: its running pods' IPs)
+  <host>.<svc>.<ns>.svc.cluster.local                                  -> the pod with that hostname
+                                 and subdomain (a StatefulSet's <name>-<ordinal> under its Service)
   <a-b-c-d>.<ns>.pod.cluster.local                                     -> a.b.c.d
   any other name under cluster.local                                   -> NXDOMAIN
   names outside the cluster domain                                     -> REFUSED (not a recursor)

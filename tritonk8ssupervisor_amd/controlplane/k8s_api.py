@@ -317,12 +317,13 @@ class KubernetesAPI:
         return Response(200, self._strip(self.replace(p, kind, ns, name, out, keep_managed=True, dry_run=dry)),
                         headers=warn)
 
-    async def h_scale(self, req: Request, ns: str, name: str, pid: str | None = None):
-        """The Deployment ``scale`` subresource (autoscaling/v1 Scale): kubectl scale."""
+    async def h_scale(self, req: Request, ns: str, name: str, kind: str = "deployments", pid: str | None = None):
+        """The ``scale`` subresource of Deployments, StatefulSets and ReplicaSets (autoscaling/v1
+        Scale): kubectl scale."""
         p = self._pid(pid, req)
-        d = self.store.get("deployments", _key(p, ns, name))
+        d = self.store.get(kind, _key(p, ns, name))
         if d is None:
-            raise HttpError(404, f'deployments.apps "{name}" not found')
+            raise HttpError(404, f'{kind}.apps "{name}" not found')
         if req.method in ("PUT", "PATCH"):
             self._auth(req, self.project(p))
             body = req.json()
@@ -338,7 +339,7 @@ class KubernetesAPI:
             n = (body.get("spec") or {}).get("replicas")
             if not isinstance(n, int) or isinstance(n, bool) or n < 0:
                 raise HttpError(422, "spec.replicas must be a non-negative integer")
-            d = self.replace(p, "deployments", ns, name, {"spec": {"replicas": n}}, merge=True,
+            d = self.replace(p, kind, ns, name, {"spec": {"replicas": n}}, merge=True,
                              manager=self._manager(req), subresource="scale", dry_run=self._dry_run(req))
         sel = (d["spec"].get("selector") or {}).get("matchLabels") or {}
         return {"kind": "Scale", "apiVersion": "autoscaling/v1",
@@ -369,10 +370,22 @@ class KubernetesAPI:
         return h
 
     # ---- networking: pod CIDRs, Service IPs / ports, endpoints --------------------------
+    def _pod_cidr_block(self) -> int:
+        """This control plane's share of 127.128.0.0/9: 32 /24s picked by its own address. Two
+        clusters on one host have different master addresses (the local provider claims them
+        host-wide, provider/hostreg.py), so their pods never get the same IP -- the same IP would
+        let one cluster's Service reach the other cluster's pod, or fail to bind."""
+        parts = (self.advertise or self.host or "").split(".")
+        if len(parts) == 4 and parts[0] == "127" and all(p.isdigit() for p in parts):
+            return ((int(parts[2]) & 3) << 8 | int(parts[3])) & 1023
+        return 0
+
     def _next_pod_cidr(self) -> str:
-        """One /24 of 127.128.0.0/9 per registered node: pods bind their own loopback IP."""
+        """One /24 of 127.128.0.0/9 per registered node, from this control plane's block (then
+        anywhere free): pods bind their own loopback IP."""
         used = {n.get("spec", {}).get("podCIDR") for n in self.store.list("nodes")}
-        for k in range(1 << 15):
+        base = self._pod_cidr_block() * 32
+        for k in [*range(base, base + 32), *range(1 << 15)]:
             c = f"127.{128 + (k >> 8)}.{k & 255}.0/24"
             if c not in used:
                 return c
@@ -384,6 +397,16 @@ class KubernetesAPI:
         if stype not in ("ClusterIP", "NodePort", "LoadBalancer"):
             raise HttpError(422, f"service type {stype!r} is not supported")
         ports = spec.get("ports") or []
+        if spec.get("clusterIP") == "None":  # headless: DNS answers with the pods, no proxy
+            if stype != "ClusterIP":
+                raise HttpError(422, f"spec.clusterIP: a headless service must be of type ClusterIP, not {stype}")
+            for i, port in enumerate(ports):
+                if "port" not in port:
+                    raise HttpError(422, f"spec.ports[{i}].port is required")
+                port.setdefault("name", str(port["port"]))
+                port.setdefault("protocol", "TCP")
+                port.setdefault("targetPort", port["port"])
+            return
         if not ports:
             raise HttpError(422, "spec.ports is required")
         svcs = [o for o in self.store.list("services")
@@ -436,6 +459,8 @@ class KubernetesAPI:
         for svc in self.store.list("services"):
             key = _key(svc["_project"], svc["metadata"]["namespace"], svc["metadata"]["name"])
             spec = svc["spec"]
+            if spec.get("clusterIP") == "None":
+                continue
             for p in spec.get("ports", []):
                 wanted[(key, spec["clusterIP"], host_port(p["port"]))] = p["name"]
                 if spec.get("type") in ("NodePort", "LoadBalancer") and p.get("nodePort"):
@@ -507,15 +532,51 @@ class KubernetesAPI:
                 return None
         if parts and parts[-1] == "svc":
             parts = parts[:-1]
-        if len(parts) != 2:
+        if len(parts) not in (2, 3):
             return None
-        svc, ns = parts
+        host, (svc, ns) = (parts[0] if len(parts) == 3 else None), parts[-2:]
         projects = sorted(self.store.list("projects"), key=lambda p: p["created_seq"])
         for p in projects:
             o = self.store.get("services", _key(p["id"], ns, svc))
-            if o and o["spec"].get("clusterIP"):
+            if o is None:
+                continue
+            if host is None and o["spec"].get("clusterIP") not in (None, "", "None"):
                 return [o["spec"]["clusterIP"]]
+            # headless Service: its running pods; <host>.<svc>: the pod with that hostname and
+            # subdomain (a StatefulSet's <name>-<ordinal>)
+            sel = o["spec"].get("selector") or {}
+            ips = sorted({x["status"]["podIP"] for x in self.store.list("pods", lambda x, pid=p["id"]: self._in(pid, x)
+                          and x["metadata"].get("namespace") == ns and x.get("status", {}).get("phase") == "Running"
+                          and x.get("status", {}).get("podIP")
+                          and (labels_match(sel, x["metadata"].get("labels")) if host is None else
+                               (x["spec"].get("hostname") == host and x["spec"].get("subdomain") == svc)))})
+            if host is None and o["spec"].get("clusterIP") != "None":
+                return None
+            return ips or None
         return None
+
+    @staticmethod
+    def _check_selector(kind: str, name: str, spec: dict) -> None:
+        sel = (spec.get("selector") or {}).get("matchLabels") or {}
+        labels = ((spec.get("template") or {}).get("metadata") or {}).get("labels") or {}
+        if not sel or any(labels.get(k) != v for k, v in sel.items()):
+            raise HttpError(422, f'{kind} "{name}" is invalid: spec.template.metadata.labels: Invalid value: '
+                                 "`selector` does not match template `labels`")
+
+    @staticmethod
+    def _check_cronjob(name: str, spec: dict) -> None:
+        from . import cron
+
+        try:
+            cron.parse(str(spec.get("schedule", "")), spec.get("timeZone"))
+        except cron.CronError as e:
+            raise HttpError(422, f'CronJob.batch "{name}" is invalid: spec.schedule: Invalid value: '
+                                 f'"{spec.get("schedule", "")}": {e}') from e
+        tmpl = ((spec.get("jobTemplate") or {}).get("spec") or {}).get("template") or {}
+        if not (tmpl.get("spec") or {}).get("containers"):
+            raise HttpError(422, "spec.jobTemplate.spec.template.spec.containers is required")
+        if spec.get("concurrencyPolicy", "Allow") not in ("Allow", "Forbid", "Replace"):
+            raise HttpError(422, "spec.concurrencyPolicy must be Allow, Forbid or Replace")
 
     def create(self, pid: str, kind: str, ns: str, body: dict, manager: str | None = None, dry_run: bool = False,
                keep_managed: bool = False) -> dict:
@@ -545,10 +606,16 @@ class KubernetesAPI:
                 raise HttpError(422, "spec.containers is required")
             spec.setdefault("restartPolicy", "Always")
             body["status"] = {"phase": "Pending", "conditions": []}
-        elif kind in ("daemonsets", "deployments", "jobs"):
+        elif kind in ("daemonsets", "deployments", "jobs", "statefulsets", "replicasets"):
             tmpl = body.get("spec", {}).get("template", {})
             if not tmpl.get("spec", {}).get("containers"):
                 raise HttpError(422, "spec.template.spec.containers is required")
+            if kind in ("statefulsets", "replicasets"):
+                self._check_selector(kind, name, body["spec"])
+            body.setdefault("status", {})
+            md["generation"] = 1
+        elif kind == "cronjobs":
+            self._check_cronjob(name, body.get("spec") or {})
             body.setdefault("status", {})
             md["generation"] = 1
         elif kind == "services":
@@ -605,7 +672,16 @@ class KubernetesAPI:
                                  "fields other than metadata")
         if kind == "jobs" and new.get("spec", {}).get("template") != cur.get("spec", {}).get("template"):
             raise HttpError(422, f'Job.batch "{name}" is invalid: spec.template: field is immutable')
-        if kind in ("daemonsets", "deployments", "jobs"):
+        if kind == "statefulsets":
+            for f in ("serviceName", "selector", "volumeClaimTemplates", "podManagementPolicy"):
+                if (new.get("spec") or {}).get(f) != (cur.get("spec") or {}).get(f):
+                    raise HttpError(422, f'StatefulSet.apps "{name}" is invalid: spec: Forbidden: updates to statefulset '
+                                         f"spec for fields other than 'replicas', 'template', 'updateStrategy', "
+                                         f"'persistentVolumeClaimRetentionPolicy' and 'minReadySeconds' are forbidden")
+        if kind == "cronjobs":
+            self._check_cronjob(name, new.get("spec") or {})
+            md["generation"] = int(cur["metadata"].get("generation", 1)) + (1 if spec_changed else 0)
+        if kind in ("daemonsets", "deployments", "jobs", "statefulsets", "replicasets"):
             if not new.get("spec", {}).get("template", {}).get("spec", {}).get("containers"):
                 raise HttpError(422, "spec.template.spec.containers is required")
             gen = int(cur["metadata"].get("generation", 1))

@@ -34,7 +34,10 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "nodes": ("", "v1", "Node", "node", False, ("no",), ("status",)),
     "daemonsets": ("apps", "v1", "DaemonSet", "daemonset", True, ("ds",), ()),
     "deployments": ("apps", "v1", "Deployment", "deployment", True, ("deploy",), ("scale",)),
+    "statefulsets": ("apps", "v1", "StatefulSet", "statefulset", True, ("sts",), ("scale",)),
+    "replicasets": ("apps", "v1", "ReplicaSet", "replicaset", True, ("rs",), ("scale",)),
     "jobs": ("batch", "v1", "Job", "job", True, (), ()),
+    "cronjobs": ("batch", "v1", "CronJob", "cronjob", True, ("cj",), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
 }
 READ_ONLY = {"namespaces": ("get", "list", "watch"), "events": ("get", "list", "watch", "create", "delete")}
@@ -93,7 +96,7 @@ def api_resource_list(group: str, version: str) -> dict | None:
              "verbs": list(READ_ONLY.get(plural, VERBS))}
         if short:
             r["shortNames"] = list(short)
-        if plural in ("pods", "deployments", "daemonsets", "jobs", "services"):
+        if plural in ("pods", "deployments", "daemonsets", "jobs", "services", "statefulsets", "replicasets", "cronjobs"):
             r["categories"] = ["all"]
         res.append(r)
         for s in subs:
@@ -414,6 +417,25 @@ def _svc_row(o: dict) -> list:
             ",".join(i.get("ip", "") for i in lb) or "<none>", ports or "<none>", _age(o)]
 
 
+def _sts_row(o: dict) -> list:
+    s = o.get("status") or {}
+    return [o["metadata"]["name"], f"{s.get('readyReplicas', 0)}/{(o.get('spec') or {}).get('replicas', 1)}", _age(o)]
+
+
+def _rs_row(o: dict) -> list:
+    s = o.get("status") or {}
+    return [o["metadata"]["name"], (o.get("spec") or {}).get("replicas", 1), s.get("replicas", 0),
+            s.get("readyReplicas", 0), _age(o)]
+
+
+def _cj_row(o: dict) -> list:
+    spec, s = o.get("spec") or {}, o.get("status") or {}
+    return [o["metadata"]["name"], spec.get("schedule", ""), spec.get("timeZone") or "<none>",
+            str(bool(spec.get("suspend", False))), len(s.get("active") or []),
+            _age({"metadata": {"creationTimestamp": s["lastScheduleTime"]}}) if s.get("lastScheduleTime") else "<none>",
+            _age(o)]
+
+
 def _ds_row(o: dict) -> list:
     s = o.get("status") or {}
     return [o["metadata"]["name"], s.get("desiredNumberScheduled", 0), s.get("currentNumberScheduled", 0),
@@ -431,6 +453,10 @@ TABLES = {
     "services": ([("Name", _S), ("Type", _S), ("Cluster-IP", _S), ("External-IP", _S), ("Port(s)", _S), ("Age", _S)],
                  _svc_row),
     "daemonsets": ([("Name", _S), ("Desired", _I), ("Current", _I), ("Ready", _I), ("Age", _S)], _ds_row),
+    "statefulsets": ([("Name", _S), ("Ready", _S), ("Age", _S)], _sts_row),
+    "replicasets": ([("Name", _S), ("Desired", _I), ("Current", _I), ("Ready", _I), ("Age", _S)], _rs_row),
+    "cronjobs": ([("Name", _S), ("Schedule", _S), ("Timezone", _S), ("Suspend", _S), ("Active", _I),
+                  ("Last Schedule", _S), ("Age", _S)], _cj_row),
 }
 
 

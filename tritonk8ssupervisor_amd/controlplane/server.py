@@ -51,10 +51,11 @@ from .k8s_api import KubernetesAPI
 from .objects import KIND_GROUPS, _cond, _key, _set_cond
 from .rancher_api import RancherAPI
 from .scheduler import Scheduler
+from .workloads import Workloads
 from .store import Store, now_iso
 
 
-class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
+class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port
@@ -185,7 +186,9 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
                 add("DELETE", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._deleter(kind))
                 add("GET", grp + rf"/{kind}", self._lister(kind, all_ns=True))
             for method in ("GET", "PUT", "PATCH"):
-                add(method, r"/apis/apps/v1/namespaces/(?P<ns>[^/]+)/deployments/(?P<name>[^/]+)/scale", self.h_scale)
+                for kind in ("deployments", "statefulsets", "replicasets"):
+                    add(method, rf"/apis/apps/v1/namespaces/(?P<ns>[^/]+)/(?P<kind>{kind})/(?P<name>[^/]+)/scale",
+                        self.h_scale)
             add("PUT", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/status", self.h_pod_status)
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/log", self.h_pod_log)
             add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/exec", self.h_pod_exec)
@@ -313,7 +316,8 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Scheduler):
         if self.store.keys("ingresses") and self.ingress_port:
             await self.ingress.ensure(self.advertise or self.host, self.ingress_port, True)
 
-        tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop())]
+        tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop()),
+                 asyncio.create_task(self.cron_loop())]
         # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
         print(f"Listening on {host}:{port}", flush=True)
         trace("cp", "listening")

@@ -20,6 +20,9 @@ KINDS = {
     "daemonset": ("DaemonSet", "/apis/apps/v1", "daemonsets"),
     "deployment": ("Deployment", "/apis/apps/v1", "deployments"),
     "job": ("Job", "/apis/batch/v1", "jobs"),
+    "statefulset": ("StatefulSet", "/apis/apps/v1", "statefulsets"),
+    "replicaset": ("ReplicaSet", "/apis/apps/v1", "replicasets"),
+    "cronjob": ("CronJob", "/apis/batch/v1", "cronjobs"),
     "configmap": ("ConfigMap", "/api/v1", "configmaps"),
     "secret": ("Secret", "/api/v1", "secrets"),
     "ingress": ("Ingress", "/apis/networking.k8s.io/v1", "ingresses"),
@@ -27,7 +30,9 @@ KINDS = {
 ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", "ds": "daemonset",
            "daemonsets": "daemonset", "deploy": "deployment", "deployments": "deployment", "jobs": "job",
            "ev": "event", "events": "event", "no": "node", "nodes": "node", "cm": "configmap",
-           "configmaps": "configmap", "secrets": "secret", "ing": "ingress", "ingresses": "ingress"}
+           "configmaps": "configmap", "secrets": "secret", "ing": "ingress", "ingresses": "ingress",
+           "sts": "statefulset", "statefulsets": "statefulset", "rs": "replicaset", "replicasets": "replicaset",
+           "cj": "cronjob", "cronjobs": "cronjob"}
 
 
 def kind_key(kind: str) -> str:

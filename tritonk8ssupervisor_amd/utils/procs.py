@@ -133,6 +133,12 @@ def kill_group(pgid: int, grace: float = 3.0) -> bool:
         delay = min(delay * 2, 0.02)
     with contextlib.suppress(ProcessLookupError, PermissionError):
         os.killpg(pgid, signal.SIGKILL)
+    # until the kernel has torn it down (its sockets and addresses are free for the next owner)
+    deadline = time.monotonic() + 2.0
+    while time.monotonic() < deadline and group_alive(pgid):
+        with contextlib.suppress(ChildProcessError, OSError):
+            os.waitpid(-pgid, os.WNOHANG)
+        time.sleep(0.005)
     return True
 
 
