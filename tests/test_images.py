@@ -184,3 +184,67 @@ def test_kubectl_exec_enters_the_container(ws, native_build):
     out = dict(x.split("=", 1) for x in r.stdout.split() if "=" in x)
     assert "tk8s hello 1" in r.stdout and int(out["pid"]) < 100 and out["iso"].startswith("landlock"), r.stdout
     assert kc("exec", "sleeper", "--", "/bin/cat", "/etc/removed").returncode != 0  # the image's view, not the host's
+
+
+def test_image_pod_volumes(ws, native_build):
+    """An image pod mounts its volumes where the spec says: a ConfigMap (read-only), a Secret, an
+    emptyDir, a PersistentVolumeClaim (data kept for the next pod), the downward API; and gets
+    its own hostname (UTS namespace)."""
+    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
+
+    if not container_runtime()[0]:
+        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+    env = _env(ws)
+    _hello_archive(ws / "hello.tar")
+    assert subprocess.run(["./tk8s", "image", "load", "hello.tar"], cwd=ws, env=env, capture_output=True).returncode == 0
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"], cwd=ws,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
+    script = ("cat /etc/app/app.conf; cat /etc/pw/password; echo; cat /info/name; echo; "
+              "echo hostname=$(cat /proc/sys/kernel/hostname); cat /data/count 2>/dev/null || echo count=none; "
+              "echo count=again > /data/count; echo x > /scratch/f && echo scratch=ok; "
+              "echo y > /etc/app/new 2>/dev/null || echo cfg=readonly")
+
+    def pod(name):
+        return {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name},
+                "spec": {"restartPolicy": "Never", "hostname": "box",
+                         "containers": [{"name": "c", "image": "hello:1", "command": ["/bin/sh", "-c", script],
+                                         "volumeMounts": [{"name": "cfg", "mountPath": "/etc/app"},
+                                                          {"name": "pw", "mountPath": "/etc/pw"},
+                                                          {"name": "info", "mountPath": "/info"},
+                                                          {"name": "data", "mountPath": "/data"},
+                                                          {"name": "scratch", "mountPath": "/scratch"}]}],
+                         "volumes": [{"name": "cfg", "configMap": {"name": "cfg"}},
+                                     {"name": "pw", "secret": {"secretName": "pw"}},
+                                     {"name": "info", "downwardAPI": {"items": [
+                                         {"path": "name", "fieldRef": {"fieldPath": "metadata.name"}}]}},
+                                     {"name": "data", "persistentVolumeClaim": {"claimName": "data"}},
+                                     {"name": "scratch", "emptyDir": {}}]}}
+
+    (ws / "objs.json").write_text(json.dumps({"apiVersion": "v1", "kind": "List", "items": [
+        {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cfg"}, "data": {"app.conf": "greeting=hi"}},
+        {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "pw"}, "stringData": {"password": "s3cr3t"}},
+        {"apiVersion": "v1", "kind": "PersistentVolumeClaim", "metadata": {"name": "data"},
+         "spec": {"resources": {"requests": {"storage": "1Gi"}}}},
+        pod("first")]}))
+    assert kc("apply", "-f", "objs.json").returncode == 0
+
+    def wait(name):
+        deadline = time.monotonic() + 60
+        while time.monotonic() < deadline:
+            phase = json.loads(kc("get", "pod", name, "-o", "json").stdout)["status"].get("phase")
+            if phase in ("Succeeded", "Failed"):
+                return phase
+            time.sleep(0.2)
+        return None
+
+    assert wait("first") == "Succeeded", kc("describe", "pod", "first").stdout
+    log = kc("logs", "first").stdout
+    assert "greeting=hi" in log and "s3cr3t" in log and "first" in log and "hostname=box" in log, log
+    assert "count=none" in log and "scratch=ok" in log and "cfg=readonly" in log, log
+    (ws / "second.json").write_text(json.dumps(pod("second")))
+    assert kc("apply", "-f", "second.json").returncode == 0
+    assert wait("second") == "Succeeded"
+    assert "count=again" in kc("logs", "second").stdout  # the claim kept the first pod's data
+    assert "data" in kc("get", "pvc").stdout

@@ -240,3 +240,96 @@ def test_cronjob_starting_deadline_skips_a_late_run(cp):
     assert _jobs(cp) == []
     cp._ctl_cronjobs("1a1", now=t0 + timedelta(seconds=21))  # due at +20, 1 s late
     assert len(_jobs(cp)) == 1
+
+
+def test_pvc_binds_on_first_use_and_pins_later_pods(cp):
+    for n in ("kubenode1", "kubenode2"):
+        cp.store.put("nodes", _key("1a1", n), {"_project": "1a1", "metadata": {"name": n, "labels": {
+            "kubernetes.io/hostname": n}}, "spec": {}, "status": {"allocatable": {"amd.com/gpu": "0"}, "conditions": [
+                {"type": "Ready", "status": "True"}, {"type": "AMDGPUValidated", "status": "True"}]}})
+    with pytest.raises(HttpError):
+        cp.create("1a1", "persistentvolumeclaims", "default", {"metadata": {"name": "nosize"}, "spec": {}})
+    pvc = cp.create("1a1", "persistentvolumeclaims", "default", {"metadata": {"name": "data"}, "spec": {
+        "resources": {"requests": {"storage": "10Gi"}}}})
+    assert pvc["status"]["phase"] == "Bound" and pvc["spec"]["storageClassName"] == "tk8s-local"
+    pod = {"metadata": {"name": "{}"}, "spec": {"containers": [{"name": "c", "command": ["true"]}],
+                                                 "volumes": [{"name": "d", "persistentVolumeClaim": {"claimName": "data"}}]}}
+    first = json.loads(json.dumps(pod).replace("{}", "user-a"))
+    cp.create("1a1", "pods", "default", first)
+    node = cp.store.get("pods", _key("1a1", "default", "user-a"))["spec"]["nodeName"]
+    assert cp.store.get("persistentvolumeclaims", _key("1a1", "default", "data"))["metadata"]["annotations"][
+        "volume.kubernetes.io/selected-node"] == node
+    for k in range(4):  # every later user of the claim lands on the same node
+        cp.create("1a1", "pods", "default", json.loads(json.dumps(pod).replace("{}", f"user-{k}b")))
+        assert cp.store.get("pods", _key("1a1", "default", f"user-{k}b"))["spec"]["nodeName"] == node
+    lost = json.loads(json.dumps(pod).replace("{}", "lost").replace('"data"', '"missing"'))
+    cp.create("1a1", "pods", "default", lost)
+    p = cp.store.get("pods", _key("1a1", "default", "lost"))
+    assert not p["spec"].get("nodeName") and "not found" in p["status"]["conditions"][0]["message"]
+    # the claim's spec is immutable but for its size
+    body = json.loads(json.dumps(cp._strip(cp.store.get("persistentvolumeclaims", _key("1a1", "default", "data")))))
+    body["spec"]["accessModes"] = ["ReadWriteMany"]
+    with pytest.raises(HttpError):
+        cp.replace("1a1", "persistentvolumeclaims", "default", "data", body)
+
+
+def test_statefulset_volume_claim_templates(cp):
+    cp.create("1a1", "statefulsets", "default", _sts(2, podManagementPolicy="Parallel", volumeClaimTemplates=[
+        {"metadata": {"name": "data"}, "spec": {"resources": {"requests": {"storage": "1Gi"}}}}]))
+    claims = sorted(o["metadata"]["name"] for o in cp.store.list("persistentvolumeclaims"))
+    assert claims == ["data-web-0", "data-web-1"]
+    p1 = cp.store.get("pods", _key("1a1", "default", "web-1"))
+    assert {"name": "data", "persistentVolumeClaim": {"claimName": "data-web-1"}} in p1["spec"]["volumes"]
+    # the ordinal's replacement gets the same claim; scaling down keeps the claims
+    cp.store.delete("pods", _key("1a1", "default", "web-1"))
+    cp.reconcile()
+    assert cp.store.get("pods", _key("1a1", "default", "web-1"))["spec"]["volumes"][-1]["persistentVolumeClaim"][
+        "claimName"] == "data-web-1"
+    body = json.loads(json.dumps(cp._strip(cp.store.get("statefulsets", _key("1a1", "default", "web")))))
+    body["spec"]["replicas"] = 1
+    cp.replace("1a1", "statefulsets", "default", "web", body)
+    assert len(cp.store.list("persistentvolumeclaims")) == 2
+
+
+def test_volume_materialisation_unit(tmp_path):
+    import base64
+    import os
+    import stat
+
+    from tritonk8ssupervisor_amd.agent.volumes import VolumeError, mounts, volume_dirs
+
+    objs = {("configmaps", "cfg"): {"data": {"app.conf": "x=1\n", "other": "y"},
+                                   "binaryData": {"blob": base64.b64encode(b"\x00\x01").decode()}},
+            ("secrets", "pw"): {"data": {"password": base64.b64encode(b"s3cr3t").decode()}},
+            ("persistentvolumeclaims", "data"): {"metadata": {"uid": "0123456789abcdef"}}}
+    fetch = lambda kind, ns, name: objs.get((kind, name))  # noqa: E731
+    pod = {"metadata": {"name": "p", "namespace": "default", "labels": {"app": "x"}},
+           "spec": {"volumes": [
+               {"name": "cfg", "configMap": {"name": "cfg", "items": [{"key": "app.conf", "path": "conf/app.conf", "mode": 0o600}]}},
+               {"name": "bin", "configMap": {"name": "cfg"}},
+               {"name": "pw", "secret": {"secretName": "pw", "defaultMode": 0o400}},
+               {"name": "scratch", "emptyDir": {}},
+               {"name": "info", "downwardAPI": {"items": [{"path": "labels", "fieldRef": {"fieldPath": "metadata.labels"}},
+                                                        {"path": "name", "fieldRef": {"fieldPath": "metadata.name"}}]}},
+               {"name": "data", "persistentVolumeClaim": {"claimName": "data"}},
+               {"name": "opt", "configMap": {"name": "absent", "optional": True}}]}}
+    dirs = volume_dirs(pod, tmp_path / "pod", tmp_path / "node", fetch)
+    assert (dirs["cfg"][0] / "conf" / "app.conf").read_text() == "x=1\n"
+    assert stat.S_IMODE(os.stat(dirs["cfg"][0] / "conf" / "app.conf").st_mode) == 0o600
+    assert (dirs["bin"][0] / "blob").read_bytes() == b"\x00\x01" and (dirs["bin"][0] / "other").read_text() == "y"
+    assert (dirs["pw"][0] / "password").read_bytes() == b"s3cr3t"
+    assert stat.S_IMODE(os.stat(dirs["pw"][0] / "password").st_mode) == 0o400
+    assert (dirs["info"][0] / "labels").read_text() == 'app="x"\n' and (dirs["info"][0] / "name").read_text() == "p"
+    assert dirs["data"][0] == tmp_path / "node" / "volumes" / "default_data-01234567"
+    assert dirs["cfg"][1] and not dirs["scratch"][1]  # configMaps are read-only, emptyDirs are not
+    m = mounts({"volumeMounts": [{"name": "scratch", "mountPath": "/work", "subPath": "a/b"},
+                                 {"name": "data", "mountPath": "/data", "readOnly": True}]}, dirs)
+    assert m == [(str(dirs["scratch"][0] / "a" / "b"), "/work", False), (str(dirs["data"][0]), "/data", True)]
+    with pytest.raises(VolumeError, match="not found"):
+        volume_dirs({"metadata": pod["metadata"], "spec": {"volumes": [{"name": "c", "configMap": {"name": "absent"}}]}},
+                    tmp_path / "p2", tmp_path / "node", fetch)
+    with pytest.raises(VolumeError):  # item paths cannot leave the volume
+        volume_dirs({"metadata": pod["metadata"], "spec": {"volumes": [{"name": "c", "configMap": {
+            "name": "cfg", "items": [{"key": "other", "path": "../../etc/x"}]}}]}}, tmp_path / "p3", tmp_path / "node", fetch)
+    with pytest.raises(VolumeError):
+        mounts({"volumeMounts": [{"name": "scratch", "mountPath": "/w", "subPath": "../x"}]}, dirs)

@@ -30,6 +30,7 @@ from ..utils.faults import fault
 from ..utils.k8senv import field_path, service_env
 from ..utils.trace import trace
 from .deviceplugin import DevicePlugin
+from .volumes import VolumeError, env_name as volume_env_name, mounts as volume_mounts, volume_dirs
 from .runtime import (
     PodProc, PodRuntime, container_argv, container_exec_argv, container_runtime, gpu_jail, gpu_jail_argv,
     install_sigterm, namespace_isolation,
@@ -333,7 +334,9 @@ class Agent:
                 "TK8S_K8S_API": f"{self.base}{self.api.prefix}", "TK8S_KV_URL": f"{self.base}/v1/kv"}
         try:  # config first: a pod waiting for a ConfigMap must not hold GPUs
             cenv = self._container_env(pod, c, base, pod_ip)
-        except ConfigError as e:
+            vol_dirs = volume_dirs(pod, pp_dir, self.sandbox, self._fetch_object, pod_ip, self.ip)
+            vol_mounts = volume_mounts(c, vol_dirs)
+        except (ConfigError, VolumeError) as e:
             if key not in self._config_wait:
                 self._report(key, md["name"], md["namespace"], "Pending",
                              {"reason": "CreateContainerConfigError", "message": str(e)}, None)
@@ -384,6 +387,7 @@ class Agent:
         else:
             env.update(pod_gpu_env(alloc["env"], ordinals, visibility))
         env.update(base)
+        env.update({volume_env_name(n): str(d) for n, (d, _ro) in vol_dirs.items()})
         env.update({"TK8S_GPU_IDS": ",".join(ids + [f"{d['node']}/{d['id']}" for d in others]),
                     "TK8S_GPU_COUNT": str(len(ordinals))})
         env.update(cenv)
@@ -443,7 +447,7 @@ class Agent:
                 return
             workdir = c.get("workingDir") or store.container_argv(ref, None, None)[2]
             jail = container_argv(str(rootfs), str(pp_dir / "rootfs"), workdir, pid_ns=not gpu_pod, gpus=mine,
-                                  binds=_host_path_binds(spec, c))
+                                  binds=vol_mounts, hostname=spec.get("hostname") or md["name"])
             exec_prefix = ["--workdir", workdir, *gpu_jail_argv(mine)[1:-1], "--"]
             isolation = f"container: {container_runtime()[1]}, image {ref}" + ("" if gpu_pod else ", own PID namespace")
             avail = False
@@ -485,6 +489,17 @@ class Agent:
                 v = _expand(str(e.get("value", "")), merged)
             out[e["name"]] = merged[e["name"]] = v
         return out
+
+    def _fetch_object(self, kind: str, ns: str, name: str) -> dict | None:
+        """A namespaced object the pod's volumes need (None: it does not exist)."""
+        try:
+            return self.api.get(self.api.k8s(f"/api/v1/namespaces/{ns}/{kind}/{name}"))
+        except ApiError as e:
+            if e.status == 404:
+                return None
+            raise VolumeError(f"{kind[:-1]} {name}: {e}") from e
+        except OSError as e:
+            raise VolumeError(f"{kind[:-1]} {name}: {e}") from e
 
     def _config_data(self, kind: str, ns: str, name: str, optional: bool) -> dict | None:
         try:
@@ -694,13 +709,6 @@ class Agent:
 
     def _ordinal(self, dev_id: str) -> int:
         return next(d.ordinal for d in self.plugin.devices_ if d.id == dev_id)
-
-
-def _host_path_binds(spec: dict, c: dict) -> list[tuple[str, str]]:
-    """The container's hostPath volumeMounts as (host path, path in the container)."""
-    vols = {v.get("name"): (v.get("hostPath") or {}).get("path") for v in spec.get("volumes") or []}
-    return [(vols[m["name"]], m["mountPath"]) for m in c.get("volumeMounts") or []
-            if vols.get(m.get("name")) and m.get("mountPath")]
 
 
 def host_scope_env(ordinals: list[int]) -> dict:

@@ -267,14 +267,18 @@ def container_runtime() -> tuple[bool, str]:
 
 
 def container_argv(rootfs: str, upper: str, workdir: str, *, pid_ns: bool, gpus: list,
-                   binds: list[tuple[str, str]] = ()) -> list[str]:
-    """argv prefix that runs a command as an image pod (see CONTAINER above)."""
+                   binds: list[tuple] = (), hostname: str = "") -> list[str]:
+    """argv prefix that runs a command as an image pod (see CONTAINER above). ``binds``:
+    (source, path in the container[, read-only]) -- the pod's volume mounts (agent/volumes.py)."""
     jail = gpu_jail_argv(gpus)[1:-1]  # the jail options without the binary and "--"
     argv = [str(CONTAINER), "--rootfs", str(rootfs), "--upper", str(upper), "--workdir", workdir or "/"]
     if pid_ns:
         argv.append("--pid-ns")
-    for src, dst in binds:
-        argv += ["--bind", f"{src}:{dst}"]
+    if hostname:
+        argv += ["--hostname", hostname]
+    for b in binds:
+        src, dst, ro = (*b, False)[:3]
+        argv += ["--bind-ro" if ro else "--bind", f"{src}:{dst}"]
     return argv + jail + ["--"]
 
 

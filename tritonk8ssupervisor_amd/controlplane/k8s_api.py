@@ -564,6 +564,21 @@ class KubernetesAPI:
                                  "`selector` does not match template `labels`")
 
     @staticmethod
+    def _admit_pvc(name: str, body: dict) -> None:
+        """A claim is bound at once to a node-local volume of the ``tk8s-local`` class; the node is
+        chosen with the first pod that uses it (WaitForFirstConsumer, scheduler.py), and the data
+        lives in that node's state directory (agent/volumes.py) until the node goes."""
+        spec = body.setdefault("spec", {})
+        storage = ((spec.get("resources") or {}).get("requests") or {}).get("storage")
+        if not storage:
+            raise HttpError(422, f'PersistentVolumeClaim "{name}" is invalid: spec.resources[storage]: Required value')
+        spec.setdefault("accessModes", ["ReadWriteOnce"])
+        spec.setdefault("storageClassName", "tk8s-local")
+        spec.setdefault("volumeMode", "Filesystem")
+        spec.setdefault("volumeName", f"pvc-{token_hex(8)}")
+        body["status"] = {"phase": "Bound", "accessModes": list(spec["accessModes"]), "capacity": {"storage": storage}}
+
+    @staticmethod
     def _check_cronjob(name: str, spec: dict) -> None:
         from . import cron
 
@@ -618,6 +633,8 @@ class KubernetesAPI:
             self._check_cronjob(name, body.get("spec") or {})
             body.setdefault("status", {})
             md["generation"] = 1
+        elif kind == "persistentvolumeclaims":
+            self._admit_pvc(name, body)
         elif kind == "services":
             self._alloc_service(body)
         elif kind in ("configmaps", "secrets"):
@@ -678,6 +695,13 @@ class KubernetesAPI:
                     raise HttpError(422, f'StatefulSet.apps "{name}" is invalid: spec: Forbidden: updates to statefulset '
                                          f"spec for fields other than 'replicas', 'template', 'updateStrategy', "
                                          f"'persistentVolumeClaimRetentionPolicy' and 'minReadySeconds' are forbidden")
+        if kind == "persistentvolumeclaims":
+            keep = {k: v for k, v in (cur.get("spec") or {}).items() if k != "resources"}
+            if {k: v for k, v in (new.get("spec") or {}).items() if k != "resources"} != keep:
+                raise HttpError(422, f'PersistentVolumeClaim "{name}" is invalid: spec: Forbidden: spec is immutable '
+                                     "after creation except resources.requests")
+            new["status"] = {**cur.get("status", {}), "capacity": {"storage": (((new.get("spec") or {}).get("resources")
+                                                                                  or {}).get("requests") or {}).get("storage", "")}}
         if kind == "cronjobs":
             self._check_cronjob(name, new.get("spec") or {})
             md["generation"] = int(cur["metadata"].get("generation", 1)) + (1 if spec_changed else 0)

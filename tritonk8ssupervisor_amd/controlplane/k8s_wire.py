@@ -30,6 +30,7 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "events": ("", "v1", "Event", "event", True, ("ev",), ()),
     "configmaps": ("", "v1", "ConfigMap", "configmap", True, ("cm",), ()),
     "secrets": ("", "v1", "Secret", "secret", True, (), ()),
+    "persistentvolumeclaims": ("", "v1", "PersistentVolumeClaim", "persistentvolumeclaim", True, ("pvc",), ()),
     "namespaces": ("", "v1", "Namespace", "namespace", False, ("ns",), ()),
     "nodes": ("", "v1", "Node", "node", False, ("no",), ("status",)),
     "daemonsets": ("apps", "v1", "DaemonSet", "daemonset", True, ("ds",), ()),
@@ -436,6 +437,16 @@ def _cj_row(o: dict) -> list:
             _age(o)]
 
 
+def _pvc_row(o: dict) -> list:
+    spec, s = o.get("spec") or {}, o.get("status") or {}
+    return [o["metadata"]["name"], s.get("phase", "Pending"), spec.get("volumeName", ""),
+            (s.get("capacity") or {}).get("storage", ""), ",".join(_ACCESS.get(m, m) for m in spec.get("accessModes") or []),
+            spec.get("storageClassName", ""), _age(o)]
+
+
+_ACCESS = {"ReadWriteOnce": "RWO", "ReadOnlyMany": "ROX", "ReadWriteMany": "RWX", "ReadWriteOncePod": "RWOP"}
+
+
 def _ds_row(o: dict) -> list:
     s = o.get("status") or {}
     return [o["metadata"]["name"], s.get("desiredNumberScheduled", 0), s.get("currentNumberScheduled", 0),
@@ -454,6 +465,8 @@ TABLES = {
                  _svc_row),
     "daemonsets": ([("Name", _S), ("Desired", _I), ("Current", _I), ("Ready", _I), ("Age", _S)], _ds_row),
     "statefulsets": ([("Name", _S), ("Ready", _S), ("Age", _S)], _sts_row),
+    "persistentvolumeclaims": ([("Name", _S), ("Status", _S), ("Volume", _S), ("Capacity", _S), ("Access Modes", _S),
+                                ("StorageClass", _S), ("Age", _S)], _pvc_row),
     "replicasets": ([("Name", _S), ("Desired", _I), ("Current", _I), ("Ready", _I), ("Age", _S)], _rs_row),
     "cronjobs": ([("Name", _S), ("Schedule", _S), ("Timezone", _S), ("Suspend", _S), ("Active", _I),
                   ("Last Schedule", _S), ("Age", _S)], _cj_row),

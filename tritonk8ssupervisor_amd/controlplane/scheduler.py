@@ -22,6 +22,7 @@ GPU_SCOPE = "tk8s.amd.com/gpu-scope"
 HOST_LABEL = "tk8s.amd.com/host"
 HOST_CLAIMS = "tk8s.amd.com/host-claims"
 HOST_DEVICES = "tk8s.amd.com/host-devices"
+SELECTED_NODE = "volume.kubernetes.io/selected-node"
 
 
 def pod_claims(o: dict) -> dict[str, int]:
@@ -56,6 +57,12 @@ class Scheduler:
             need = pod_gpus(pod)
             sel = pod["spec"].get("nodeSelector")
             key = _key(pid, pod["metadata"]["namespace"], pod["metadata"]["name"])
+            claims, pinned, missing = self._pod_claims_nodes(pid, pod)
+            if missing:
+                self._unschedulable(pod, key, f'persistentvolumeclaim "{missing}" not found')
+                continue
+            if pinned:  # a claim's data lives on one node
+                sel = {**(sel or {}), "kubernetes.io/hostname": pinned}
             if (pod["metadata"].get("annotations") or {}).get(GPU_SCOPE) == "host" and need > 0:
                 self._schedule_host_scoped(pid, pod, key, need, sel, nodes, used, count)
                 continue
@@ -76,7 +83,25 @@ class Scheduler:
             nn = best[1]
             used[nn] = used.get(nn, 0) + need
             count[nn] = count.get(nn, 0) + 1
+            for c in claims:  # WaitForFirstConsumer: the first pod's node holds the claim's data
+                self.store.patch("persistentvolumeclaims", _key(pid, pod["metadata"]["namespace"], c),
+                                 lambda o, nn=nn: o["metadata"].setdefault("annotations", {}).setdefault(SELECTED_NODE, nn))
             self._bind(pid, pod, key, nn)
+
+    def _pod_claims_nodes(self, pid: str, pod: dict) -> tuple[list[str], str | None, str | None]:
+        """(claims the pod mounts, the node they pin it to, a claim that does not exist)."""
+        ns = pod["metadata"]["namespace"]
+        claims, pinned = [], None
+        for v in pod["spec"].get("volumes") or []:
+            c = (v.get("persistentVolumeClaim") or {}).get("claimName")
+            if not c:
+                continue
+            pvc = self.store.get("persistentvolumeclaims", _key(pid, ns, c))
+            if pvc is None:
+                return claims, pinned, c
+            claims.append(c)
+            pinned = pinned or (pvc["metadata"].get("annotations") or {}).get(SELECTED_NODE)
+        return claims, pinned, None
 
     def _unschedulable(self, pod: dict, key: str, msg: str) -> None:
         c = _cond(pod, "PodScheduled")

@@ -10,6 +10,8 @@ ReplicaSets and CronJobs. A mixin of server.ControlPlane, run by reconcile().
   after the others run (``partition`` keeps ordinals below it); ``OnDelete`` replaces only pods
   the user deletes. A stable name is what a multi-node GPU job keys its ranks on (rank = ordinal,
   ``MASTER_ADDR`` = ``<name>-0.<service>``).
+  ``volumeClaimTemplates`` give each ordinal its own claim ``<template>-<name>-<ordinal>``,
+  which outlives the pod (and the StatefulSet), as in Kubernetes.
 * **ReplicaSet** -- ``replicas`` pods from the template (no rollout: that is the Deployment's).
 * **CronJob** -- a Job from ``jobTemplate`` at each scheduled time (cron.py), named
   ``<name>-<scheduled minute>``; ``concurrencyPolicy`` Allow/Forbid/Replace, ``suspend``,
@@ -95,6 +97,17 @@ class Workloads:
                 tspec["hostname"] = f"{name}-{i}"
                 if spec.get("serviceName"):
                     tspec["subdomain"] = spec["serviceName"]
+                # volumeClaimTemplates: one claim per ordinal, kept when the pod goes, so the
+                # ordinal's replacement mounts the same data
+                for vct in spec.get("volumeClaimTemplates") or []:
+                    vname = (vct.get("metadata") or {}).get("name", "data")
+                    claim = f"{vname}-{name}-{i}"
+                    if self.store.get("persistentvolumeclaims", _key(pid, ns, claim)) is None:
+                        self.create(pid, "persistentvolumeclaims", ns, {
+                            "apiVersion": "v1", "kind": "PersistentVolumeClaim",
+                            "metadata": {"name": claim, "labels": dict(match)}, "spec": copy.deepcopy(vct.get("spec") or {})})
+                    vols = [v for v in tspec.get("volumes") or [] if v.get("name") != vname]
+                    tspec["volumes"] = vols + [{"name": vname, "persistentVolumeClaim": {"claimName": claim}}]
                 # (no ControllerRevision history here: a pod is always created from the current
                 # template, below a rolling-update partition too)
                 pods[i] = self._new_pod(pid, ns, f"{name}-{i}", s, "StatefulSet", tmpl,

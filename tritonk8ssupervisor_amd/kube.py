@@ -25,6 +25,7 @@ KINDS = {
     "cronjob": ("CronJob", "/apis/batch/v1", "cronjobs"),
     "configmap": ("ConfigMap", "/api/v1", "configmaps"),
     "secret": ("Secret", "/api/v1", "secrets"),
+    "persistentvolumeclaim": ("PersistentVolumeClaim", "/api/v1", "persistentvolumeclaims"),
     "ingress": ("Ingress", "/apis/networking.k8s.io/v1", "ingresses"),
 }
 ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", "ds": "daemonset",
@@ -32,7 +33,8 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "ev": "event", "events": "event", "no": "node", "nodes": "node", "cm": "configmap",
            "configmaps": "configmap", "secrets": "secret", "ing": "ingress", "ingresses": "ingress",
            "sts": "statefulset", "statefulsets": "statefulset", "rs": "replicaset", "replicasets": "replicaset",
-           "cj": "cronjob", "cronjobs": "cronjob"}
+           "cj": "cronjob", "cronjobs": "cronjob", "pvc": "persistentvolumeclaim",
+           "persistentvolumeclaims": "persistentvolumeclaim"}
 
 
 def kind_key(kind: str) -> str:
