@@ -289,3 +289,15 @@ def test_fabric_only_annotations_cannot_be_added_by_update(kube):
                     {"spec": {"template": {"metadata": {"annotations": {"tk8s.amd.com/gpu-scope": "host"}}}}},
                     ctype=k8s_wire.MERGE_PATCH)
     assert st == 403
+
+
+def test_events_select_by_uid_as_kubectl_describe_does(kube):
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "ev"},
+           "spec": {"containers": [{"name": "c", "image": "x", "command": ["true"]}]}}
+    st, _, p = _raw(kube, "POST", "/api/v1/namespaces/default/pods", pod)
+    assert st == 201
+    sel = f"involvedObject.kind=Pod,involvedObject.name=ev,involvedObject.namespace=default,involvedObject.uid={p['metadata']['uid']}"
+    _, _, evs = _raw(kube, "GET", "/api/v1/namespaces/default/events?fieldSelector=" + sel.replace(",", "%2C"))
+    assert any(e["reason"] == "Scheduled" for e in evs["items"]), evs
+    e = evs["items"][0]
+    assert e["involvedObject"]["apiVersion"] == "v1" and e["lastTimestamp"] and e["source"]["component"]

@@ -397,11 +397,27 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                                               for c in st.get("conditions", [])))
             if what == "pod":
                 print(f"Node:         {o['spec'].get('nodeName')}\nStatus:       {st.get('phase')}")
+                vols = o["spec"].get("volumes") or []
+                if vols:
+                    print("Volumes:\n" + "\n".join(f"  {v.get('name')}: {next((k for k in v if k != 'name'), '?')}"
+                                                   for v in vols))
                 ann = o["metadata"].get("annotations", {})
                 if "tk8s.amd.com/gpu-isolation" in ann or "tk8s.amd.com/isolation" in ann:
                     print("Isolation:\n"
                           f"  GPU:        {ann.get('tk8s.amd.com/gpu-isolation', '-')}\n"
                           f"  Namespaces: {ann.get('tk8s.amd.com/isolation', '-')}")
+            # the object's events, selected as kubectl describe does (kind, name, namespace, uid)
+            sel = f"involvedObject.kind={o.get('kind', '')},involvedObject.name={o['metadata']['name']}"
+            if o["metadata"].get("uid"):
+                sel += f",involvedObject.uid={o['metadata']['uid']}"
+            try:
+                evs = k.get(k.k8s(f"/api/v1/namespaces/{ns if what != 'node' else 'default'}/events"),
+                            query={"fieldSelector": sel})["items"]
+            except ApiError:
+                evs = []
+            print("Events:" + ("  <none>" if not evs else ""))
+            for e in evs[-20:]:
+                print(f"  {e.get('type', ''):<8} {e.get('reason', ''):<20} {e.get('message', '')}")
         elif a.verb == "create" and a.args and a.args[0] in ("configmap", "cm", "secret"):
             return _create_data(k, a, ns)
         elif a.verb == "create" and a.args and kind_key(a.args[0]) == "deployment":

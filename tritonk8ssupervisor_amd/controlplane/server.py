@@ -55,6 +55,9 @@ from .workloads import Workloads
 from .store import Store, now_iso
 
 
+_KIND_PLURAL = {r[2]: plural for plural, r in k8s_wire.RESOURCES.items()}
+
+
 class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
@@ -98,10 +101,22 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler)
     def _event(self, project: str, ns: str, involved: dict, reason: str, message: str, etype: str = "Normal") -> None:
         self._seq += 1
         name = f"{involved.get('name', 'x')}.{self._seq:x}"
+        involved = dict(involved)
+        plural = _KIND_PLURAL.get(involved.get("kind", ""))
+        if plural:  # what kubectl describe selects an object's events by: kind, name, namespace, uid
+            namespaced = k8s_wire.RESOURCES[plural][4]
+            obj = self.store.get(plural, _key(project, ns, involved["name"]) if namespaced else _key(project, involved["name"]))
+            involved.setdefault("apiVersion", k8s_wire.group_version(plural))
+            if namespaced:
+                involved.setdefault("namespace", ns)
+            if obj is not None:
+                involved.setdefault("uid", obj["metadata"].get("uid", ""))
+        now = now_iso()
         self.store.put("events", _key(project, ns, name), {
             "kind": "Event", "metadata": {"name": name, "namespace": ns}, "_project": project,
             "involvedObject": involved, "reason": reason, "message": message, "type": etype,
-            "firstTimestamp": now_iso(), "count": 1,
+            "firstTimestamp": now, "lastTimestamp": now, "count": 1,
+            "source": {"component": "tk8s-controlplane"}, "reportingComponent": "tk8s-controlplane",
         })
         evs = self.store.keys("events")
         if len(evs) > 5000:
