@@ -159,3 +159,38 @@ def test_attach_streams_new_output_until_the_pod_ends(cluster, tmp_path):
     out, err = p.communicate(timeout=20)
     assert p.returncode == 0, err
     assert out == "new line\n"
+
+
+def test_pod_conditions_and_log_follow(cluster, tmp_path):
+    """Ready conditions from the reported phase (kubectl wait --for=condition=Ready), and a
+    stock kubectl's ``logs -f``: one chunked response that ends when the pod does."""
+    import http.client
+
+    k, nc, _ = cluster
+    log = tmp_path / "srv.log"
+    log.write_text("one\n")
+    _set(nc, "Running", annotations={"tk8s.amd.com/log-path": str(log)})
+    p = k.get(k.k8s("/api/v1/namespaces/default/pods/srv"))
+    conds = {c["type"]: c["status"] for c in p["status"]["conditions"]}
+    assert conds["Ready"] == "True" and conds["ContainersReady"] == "True" and conds["Initialized"] == "True"
+    conn = http.client.HTTPConnection(k.host, k.port, timeout=20)
+    conn.request("GET", k.k8s("/api/v1/namespaces/default/pods/srv/log?follow=true"),
+                 headers={"Authorization": f"Bearer {k.token}"})
+    r = conn.getresponse()
+    assert r.status == 200 and r.getheader("Transfer-Encoding") == "chunked"
+
+    def later():
+        time.sleep(0.5)
+        with log.open("a") as f:
+            f.write("two\n")
+        time.sleep(0.5)
+        _set(nc, "Succeeded")
+
+    threading.Thread(target=later, daemon=True).start()
+    assert r.read() == b"one\ntwo\n"  # returns once the pod has stopped
+    conn.close()
+    p = k.get(k.k8s("/api/v1/namespaces/default/pods/srv"))
+    ready = next(c for c in p["status"]["conditions"] if c["type"] == "Ready")
+    assert ready["status"] == "False" and ready["reason"] == "PodCompleted"
+    assert k.get(k.k8s("/api/v1/namespaces/default/pods/srv/log"), query={"tailLines": "1"}, raw=True) == "two\n"
+    assert k.get(k.k8s("/api/v1/namespaces/default/pods/srv/log"), query={"limitBytes": "2"}, raw=True) == "on"

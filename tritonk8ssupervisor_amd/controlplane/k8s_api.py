@@ -761,6 +761,7 @@ class KubernetesAPI:
             o.setdefault("status", {}).update(st)
             if ann:
                 o["metadata"].setdefault("annotations", {}).update(ann)
+            _pod_conditions(o)
 
         trace("cp", f"pod status {ns}/{name} {st.get('phase')}")
         o = self.store.patch("pods", key, fn)
@@ -774,18 +775,55 @@ class KubernetesAPI:
         return self._strip(o)
 
     async def h_pod_log(self, req: Request, ns: str, name: str, pid: str | None = None):
+        """``kubectl logs``: ``tailLines``, ``limitBytes``, ``sinceSeconds`` (whole file when it
+        changed since), ``follow=true`` (a chunked stream of what the pod appends, until it stops)."""
         p = self._pid(pid, req)
-        o = self.store.get("pods", _key(p, ns, name))
+        key = _key(p, ns, name)
+        o = self.store.get("pods", key)
         if o is None:
             raise HttpError(404, f'pod "{name}" not found')
+        c = req.q("container")
+        names = [x.get("name") for x in o["spec"].get("containers") or []]
+        if c and c not in names:
+            raise HttpError(400, f"container {c} is not valid for pod {name}")
         path = o["metadata"].get("annotations", {}).get("tk8s.amd.com/log-path")
+        follow = req.q("follow") in ("true", "1")
         if not path or not os.path.exists(path):
-            return Response(200, "", content_type="text/plain")
+            if not follow:
+                return Response(200, "", content_type="text/plain")
         tail = int(req.q("tailLines", "0") or 0)
-        text = Path(path).read_text(errors="replace")
+        limit = int(req.q("limitBytes", "0") or 0)
+        since = float(req.q("sinceSeconds", "0") or 0)
+        text = Path(path).read_text(errors="replace") if path and os.path.exists(path) else ""
+        if since and path and os.path.exists(path) and time.time() - os.path.getmtime(path) > since:
+            text = ""
         if tail:
-            text = "\n".join(text.splitlines()[-tail:]) + "\n"
+            text = "\n".join(text.splitlines()[-tail:]) + "\n" if text else ""
+        if limit:
+            text = text.encode()[:limit].decode(errors="ignore")
+        if follow:
+            return StreamResponse(self._follow_log(key, path, text), content_type="text/plain")
         return Response(200, text, content_type="text/plain")
+
+    async def _follow_log(self, key: str, path: str | None, first: str):
+        """The text so far, then what the pod appends, until it has stopped and the file is read."""
+        if first:
+            yield first.encode()
+        pos = os.path.getsize(path) if path and os.path.exists(path) else 0
+        while True:
+            cur = self.store.get("pods", key)
+            path = path or ((cur or {}).get("metadata", {}).get("annotations", {}).get("tk8s.amd.com/log-path"))
+            size = os.path.getsize(path) if path and os.path.exists(path) else 0
+            if size > pos:
+                with open(path, "rb") as f:
+                    f.seek(pos)
+                    chunk = f.read(min(size - pos, 1 << 20))
+                pos += len(chunk)
+                yield chunk
+                continue
+            if cur is None or cur.get("status", {}).get("phase") in ("Succeeded", "Failed"):
+                return
+            await asyncio.sleep(0.1)
 
     # ---- exec: a command in a running pod's environment (the kubelet's exec, request/response) --
     async def h_pod_exec(self, req: Request, ns: str, name: str, pid: str | None = None):
@@ -1063,3 +1101,17 @@ class KubernetesAPI:
             raise HttpError(404, f"exec {xid} not found (timed out?)")
         return {"ok": True}
 
+
+def _pod_conditions(pod: dict) -> None:
+    """The kubelet's pod conditions from the phase the node reported: Initialized, ContainersReady
+    and Ready (``kubectl wait --for=condition=Ready``); PodScheduled is the scheduler's."""
+    from .objects import _set_cond
+
+    phase = pod.get("status", {}).get("phase")
+    if phase not in ("Running", "Succeeded", "Failed"):
+        return
+    ready = phase == "Running" and all(c.get("ready") for c in pod["status"].get("containerStatuses") or [{"ready": True}])
+    reason = "" if ready else ("PodCompleted" if phase == "Succeeded" else "ContainersNotReady")
+    _set_cond(pod, "Initialized", "True", "", "")
+    for t in ("ContainersReady", "Ready"):
+        _set_cond(pod, t, "True" if ready else "False", reason, "")
