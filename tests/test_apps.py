@@ -370,3 +370,23 @@ def test_statefulset_cronjob_and_port_forward_on_a_real_cluster(cluster):
     kc("scale", "sts/web", "--replicas", "1")
     _until(lambda: "web-1" not in pods(), 30)
     kc("delete", "cronjob", "tick")
+
+
+def test_init_and_multi_container_pod_on_a_real_cluster(cluster):
+    ws, env, kc, summary = cluster
+    (ws / "multi.json").write_text(json.dumps({
+        "apiVersion": "v1", "kind": "Pod", "metadata": {"name": "multi"},
+        "spec": {"restartPolicy": "Never",
+                 "initContainers": [{"name": "prep", "image": "busybox",
+                                     "command": ["sh", "-c", "echo prepared > $(TK8S_VOLUME_SHARED)/ready"]}],
+                 "containers": [{"name": "app", "image": "busybox", "command": ["sh", "-c", "cat $(TK8S_VOLUME_SHARED)/ready"]},
+                                {"name": "helper", "image": "busybox", "command": ["sh", "-c", "echo helper ran"]}],
+                 "volumes": [{"name": "shared", "emptyDir": {}}]}}))
+    kc("apply", "-f", "multi.json")
+    _until(lambda: json.loads(kc("get", "pod", "multi", "-o", "json").stdout)["status"].get("phase") == "Succeeded", 30)
+    assert kc("logs", "multi").stdout.strip() == "prepared"
+    st = json.loads(kc("get", "pod", "multi", "-o", "json").stdout)["status"]
+    assert [c["name"] for c in st["containerStatuses"]] == ["app", "helper"]
+    assert [c["name"] for c in st["initContainerStatuses"]] == ["prep"]
+    assert kc("logs", "multi", "-c", "helper").stdout.strip() == "helper ran"
+    assert kc("logs", "multi", "-c", "nope", check=False).returncode != 0

@@ -327,3 +327,45 @@ def test_fabric_visibility_needs_a_real_owner_job():
     assert not node_visibility_allowed(pod, lambda ns, name: "u2")       # another Job of that name
     other_ns = {"metadata": {**pod["metadata"], "namespace": "default"}}
     assert not node_visibility_allowed(other_ns, lambda ns, name: "u1")
+
+
+def test_init_containers_then_all_app_containers(tmp_path):
+    """Init containers run in order to a zero exit before the app containers; every app container
+    runs (each with its own log); the pod ends Succeeded once all of them exit 0, Failed if one
+    does not; an init container that fails under restartPolicy Never fails the pod."""
+    from tritonk8ssupervisor_amd.agent.runtime import PodProc, PodRuntime
+
+    events = []
+    rt = PodRuntime(tmp_path / "pods", lambda pp, phase, extra: events.append((phase, extra.get("reason"))))
+    d = tmp_path / "pods" / "p"
+
+    def proc(name, script, log="log"):
+        return PodProc(key="default/p" if log == "log" else f"default/p/{name}", uid="u", dir=d, argv=["sh", "-c", script],
+                       env={"PATH": "/usr/bin:/bin"}, restart_policy="Never", name=name, log_name=log)
+
+    main = proc("main", "cat order.txt; echo main >> order.txt")
+    main.init = [proc("i1", "echo i1 > order.txt", "log.i1"), proc("i2", "echo i2 >> order.txt", "log.i2")]
+    main.sidecars = [proc("side", "sleep 0.3; echo side-done", "log.side")]
+    rt.start(main)
+    assert main.done.wait(20)
+    assert events[-1] == ("Succeeded", None), events
+    assert (d / "log").read_text() == "i1\ni2\n" and (d / "log.side").read_text() == "side-done\n"
+    assert ("Pending", "PodInitializing") in events
+
+    events.clear()
+    d2 = tmp_path / "pods" / "q"
+    bad = PodProc(key="default/q", uid="u", dir=d2, argv=["true"], env={"PATH": "/usr/bin:/bin"}, restart_policy="Never",
+                  name="main")
+    bad.sidecars = [PodProc(key="default/q/s", uid="u", dir=d2, argv=["sh", "-c", "exit 3"], env={"PATH": "/usr/bin:/bin"},
+                            restart_policy="Never", name="s", log_name="log.s")]
+    rt.start(bad)
+    assert bad.done.wait(20) and events[-1][0] == "Failed"
+
+    events.clear()
+    d3 = tmp_path / "pods" / "r"
+    never = PodProc(key="default/r", uid="u", dir=d3, argv=["true"], env={"PATH": "/usr/bin:/bin"}, restart_policy="Never",
+                    name="main")
+    never.init = [PodProc(key="default/r/i", uid="u", dir=d3, argv=["false"], env={"PATH": "/usr/bin:/bin"},
+                          restart_policy="Never", name="i", log_name="log.i")]
+    rt.start(never)
+    assert never.done.wait(20) and events[-1] == ("Failed", "Init:Error")

@@ -100,6 +100,14 @@ def pod_gpus(p: dict) -> int:
     return total
 
 
+class _PodFail(Exception):
+    """A container of the pod cannot run: the pod fails with this reason."""
+
+    def __init__(self, reason: str, message: str):
+        super().__init__(message)
+        self.reason, self.message = reason, message
+
+
 class ConfigError(Exception):
     """A pod's env refers to a ConfigMap/Secret (key) that does not exist (yet)."""
 
@@ -332,10 +340,11 @@ class Agent:
                 "HOSTNAME": spec.get("hostname") or md["name"],
                 "POD_IP": pod_ip, "NODE_NAME": self.name, "NODE_IP": self.ip, "TK8S_API_URL": self.base,
                 "TK8S_K8S_API": f"{self.base}{self.api.prefix}", "TK8S_KV_URL": f"{self.base}/v1/kv"}
+        inits = list(spec.get("initContainers") or [])
+        apps = list(spec["containers"])
         try:  # config first: a pod waiting for a ConfigMap must not hold GPUs
-            cenv = self._container_env(pod, c, base, pod_ip)
             vol_dirs = volume_dirs(pod, pp_dir, self.sandbox, self._fetch_object, pod_ip, self.ip)
-            vol_mounts = volume_mounts(c, vol_dirs)
+            cfg = {id(x): (self._container_env(pod, x, base, pod_ip), volume_mounts(x, vol_dirs)) for x in inits + apps}
         except (ConfigError, VolumeError) as e:
             if key not in self._config_wait:
                 self._report(key, md["name"], md["namespace"], "Pending",
@@ -390,35 +399,6 @@ class Agent:
         env.update({volume_env_name(n): str(d) for n, (d, _ro) in vol_dirs.items()})
         env.update({"TK8S_GPU_IDS": ",".join(ids + [f"{d['node']}/{d['id']}" for d in others]),
                     "TK8S_GPU_COUNT": str(len(ordinals))})
-        env.update(cenv)
-        argv = [_expand(str(x), env) for x in (c.get("command") or []) + (c.get("args") or [])]
-        image = self._image(c.get("image"))
-        if image is not None:  # a loaded image (agent/images.py): its root file system, entrypoint, env
-            ok, why = container_runtime()
-            if not ok:
-                self._report(key, md["name"], md["namespace"], "Failed", {
-                    "reason": "ContainerCannotRun", "message": f"image {c.get('image')!r} needs a mount namespace on "
-                                                              f"this node: {why}"}, None)
-                return
-            store, ref = image
-            img_argv, img_env, img_wd = store.container_argv(ref, c.get("command"), c.get("args"))
-            for k, v in img_env.items():  # the image's env, under what the pod spec sets itself
-                if k not in cenv:
-                    env[k] = v
-            argv = [_expand(str(x), env) for x in img_argv]
-        elif not c.get("command"):
-            from ..apps import resolve
-
-            entry = resolve(c.get("image"))
-            if entry:  # the image's entrypoint: a built-in app (apps/__init__.py), the image's own env
-                env.setdefault("PYTHONPATH", TK8S_HOME)
-                argv = entry + [_expand(str(x), env) for x in (c.get("args") or [])]
-        if not argv:
-            self._report(key, md["name"], md["namespace"], "Failed", {
-                "reason": "ErrImageNeverPull", "message": f"container has no command and image {c.get('image')!r} is "
-                                                          "neither loaded on this node (./tk8s image load) nor in the "
-                                                          "tk8s app catalogue (tritonk8ssupervisor_amd/apps)"}, None)
-            return
         # GPU pods stay in the host PID namespace: HIP/RCCL inter-process sharing (dmabuf handles
         # passed by pid, RCCL's pid-keyed shared memory) needs the peers' real pids.
         gpu_pod = bool(ids) or all_gpus or visibility == "node" or bool(others)
@@ -433,34 +413,81 @@ class Agent:
         # node visibility (rccl-tests style ranks): the pod's runtime sees the node's GPUs
         view = [d.ordinal for d in self.plugin.devices_] if visibility == "node" and scope != "host" else ordinals
         mine = [by_ord[o] for o in view if o in by_ord]
-        jail = gpu_jail_argv(mine) if jail_ok else []
-        exec_prefix: list[str] = []
         gpu_isolation = (f"{jail_how}: may open {', '.join(f'gpu{g.ordinal}' for g in mine) or 'no GPU'}" if jail_ok
                          else f"none: {jail_how}")
-        if image is not None:  # tk8s-container: namespaces, the image's root, the same GPU jail inside
-            store, ref = image
+        procs = []
+        for n, cont in enumerate(inits + apps):
+            first_app = cont is apps[0]
             try:
-                rootfs = store.rootfs(ref)
-            except Exception as e:  # noqa: BLE001 - an unreadable image fails the pod, not the agent
-                self._report(key, md["name"], md["namespace"], "Failed",
-                             {"reason": "ErrImageUnpack", "message": str(e)[:500]}, None)
+                built = self._container_cmd(pod, cont, env, cfg[id(cont)], mine, gpu_pod, jail_ok, pp_dir, first_app)
+            except _PodFail as e:
+                self._report(key, md["name"], md["namespace"], "Failed", {"reason": e.reason, "message": e.message}, None)
                 return
-            workdir = c.get("workingDir") or store.container_argv(ref, None, None)[2]
-            jail = container_argv(str(rootfs), str(pp_dir / "rootfs"), workdir, pid_ns=not gpu_pod, gpus=mine,
-                                  binds=vol_mounts, hostname=spec.get("hostname") or md["name"])
-            exec_prefix = ["--workdir", workdir, *gpu_jail_argv(mine)[1:-1], "--"]
-            isolation = f"container: {container_runtime()[1]}, image {ref}" + ("" if gpu_pod else ", own PID namespace")
-            avail = False
-        pp = PodProc(key=key, uid=md.get("uid", ""), dir=pp_dir, argv=argv, env=env,
-                     restart_policy=spec.get("restartPolicy", "Always"), gpu_ids=ids, ip=pod_ip,
-                     isolate=avail and not gpu_pod, jail=jail, exec_prefix=exec_prefix)
+            if built["image"] is not None and first_app:
+                isolation = f"container: {container_runtime()[1]}, image {built['image']}" + (
+                    "" if gpu_pod else ", own PID namespace")
+            procs.append(PodProc(key=key if first_app else f"{key}/{cont.get('name')}", uid=md.get("uid", ""), dir=pp_dir,
+                                 argv=built["argv"], env=built["env"], restart_policy=spec.get("restartPolicy", "Always"),
+                                 gpu_ids=ids if first_app else [], ip=pod_ip,
+                                 isolate=avail and not gpu_pod and built["image"] is None, jail=built["jail"],
+                                 exec_prefix=built["exec_prefix"], name=cont.get("name") or f"c{n}",
+                                 log_name="log" if first_app else f"log.{cont.get('name') or n}"))
+        pp = procs[len(inits)]
+        pp.init, pp.sidecars = procs[:len(inits)], procs[len(inits) + 1:]
+        c = apps[0]
         self._pods_meta[key] = {"name": md["name"], "namespace": md["namespace"],
-                                "container": {"name": c.get("name"), "image": c.get("image")},
+                                "images": {x.get("name"): x.get("image") or "" for x in inits + apps},
                                 "validation": md.get("labels", {}).get(VALIDATION_LABEL) == "true",
                                 "annotations": {**alloc["annotations"], "tk8s.amd.com/log-path": str(pp_dir / "log"),
                                                 "tk8s.amd.com/isolation": isolation,
                                                 "tk8s.amd.com/gpu-isolation": gpu_isolation}}
         self.runtime.start(pp)
+
+    def _container_cmd(self, pod: dict, c: dict, pod_env: dict, cfg: tuple, mine: list, gpu_pod: bool, jail_ok: bool,
+                       pp_dir: Path, first_app: bool) -> dict:
+        """One container's process: argv, env, and the prefix it runs under (GPU jail, or
+        tk8s-container for a loaded image); raises _PodFail with the pod's failure reason."""
+        md, spec = pod["metadata"], pod["spec"]
+        cenv, mounts = cfg
+        env = {**pod_env, **cenv}
+        argv = [_expand(str(x), env) for x in (c.get("command") or []) + (c.get("args") or [])]
+        image = self._image(c.get("image"))
+        if image is not None:  # a loaded image (agent/images.py): its root file system, entrypoint, env
+            ok, why = container_runtime()
+            if not ok:
+                raise _PodFail("ContainerCannotRun", f"image {c.get('image')!r} needs a mount namespace on this node: {why}")
+            store, ref = image
+            img_argv, img_env, _wd = store.container_argv(ref, c.get("command"), c.get("args"))
+            for k, v in img_env.items():  # the image's env, under what the pod spec sets itself
+                if k not in cenv:
+                    env[k] = v
+            argv = [_expand(str(x), env) for x in img_argv]
+        elif not c.get("command"):
+            from ..apps import resolve
+
+            entry = resolve(c.get("image"))
+            if entry:  # the image's entrypoint: a built-in app (apps/__init__.py), the image's own env
+                env.setdefault("PYTHONPATH", TK8S_HOME)
+                argv = entry + [_expand(str(x), env) for x in (c.get("args") or [])]
+        if not argv:
+            raise _PodFail("ErrImageNeverPull", f"container {c.get('name')!r} has no command and image {c.get('image')!r} "
+                                                "is neither loaded on this node (./tk8s image load) nor in the tk8s app "
+                                                "catalogue (tritonk8ssupervisor_amd/apps)")
+        jail = gpu_jail_argv(mine) if jail_ok else []
+        exec_prefix: list[str] = []
+        if image is not None:  # tk8s-container: namespaces, the image's root, the same GPU jail inside
+            store, ref = image
+            try:
+                rootfs = store.rootfs(ref)
+            except Exception as e:  # noqa: BLE001 - an unreadable image fails the pod, not the agent
+                raise _PodFail("ErrImageUnpack", str(e)[:500]) from e
+            workdir = c.get("workingDir") or store.container_argv(ref, None, None)[2]
+            upper = pp_dir / ("rootfs" if first_app else f"rootfs-{c.get('name')}")
+            jail = container_argv(str(rootfs), str(upper), workdir, pid_ns=not gpu_pod, gpus=mine,
+                                  binds=mounts, hostname=spec.get("hostname") or md["name"])
+            exec_prefix = ["--workdir", workdir, *gpu_jail_argv(mine)[1:-1], "--"]
+        return {"argv": argv, "env": env, "jail": jail, "exec_prefix": exec_prefix,
+                "image": image[1] if image is not None else None}
 
     # ---- container env (kubelet semantics) ------------------------------------------------
     def _container_env(self, pod: dict, c: dict, base: dict, pod_ip: str) -> dict:
@@ -559,12 +586,27 @@ class Agent:
                 annotations: dict | None = None) -> None:
         st = {"phase": phase, "hostIP": self.ip, "podIP": (pp.ip if pp is not None and pp.ip else self.ip)}
         if pp is not None:
-            state = {"running": {"startedAt": pp.started}} if phase == "Running" else \
-                {"terminated": {"exitCode": extra.get("exitCode", pp.exit_code), "reason": "Completed" if phase == "Succeeded" else "Error"}}
-            c0 = self._pods_meta.get(key, {}).get("container") or {}
-            st["containerStatuses"] = [{"name": c0.get("name") or "main", "image": c0.get("image") or "",
-                                        "restartCount": pp.restarts, "state": state, "ready": phase == "Running",
-                                        "started": phase == "Running"}]
+            def cstatus(cp: PodProc, image: str = "") -> dict:
+                alive = cp.proc is not None and cp.proc.poll() is None
+                if alive:
+                    state = {"running": {"startedAt": cp.started}}
+                elif cp.exit_code is not None:
+                    state = {"terminated": {"exitCode": cp.exit_code, "reason": "Completed" if cp.exit_code == 0 else "Error"}}
+                else:
+                    state = {"waiting": {"reason": "PodInitializing" if phase == "Pending" else "ContainerCreating"}}
+                return {"name": cp.name or "main", "image": image, "restartCount": cp.restarts, "state": state,
+                        "ready": alive, "started": alive}
+
+            images = self._pods_meta.get(key, {}).get("images") or {}
+            main = cstatus(pp, images.get(pp.name, ""))
+            if phase in ("Succeeded", "Failed") and "terminated" not in main["state"]:
+                main["state"] = {"terminated": {"exitCode": extra.get("exitCode", pp.exit_code),
+                                                "reason": "Completed" if phase == "Succeeded" else "Error"}}
+            if phase == "Running" and "running" not in main["state"] and pp.proc is not None:
+                main.update(state={"running": {"startedAt": pp.started}}, ready=True, started=True)
+            st["containerStatuses"] = [main] + [cstatus(sc, images.get(sc.name, "")) for sc in pp.sidecars]
+            if pp.init:
+                st["initContainerStatuses"] = [cstatus(ic, images.get(ic.name, "")) for ic in pp.init]
             st["startTime"] = pp.started
         for k in ("message", "reason", "result"):
             if extra.get(k) is not None:

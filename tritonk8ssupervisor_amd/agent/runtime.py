@@ -5,6 +5,12 @@ ansible/roles/rancherhost/tasks/main.yml:26-34). Here a pod is a process group: 
 device plugin's Allocate() result and the downward-API values, ``$(VAR)`` references in
 command/args are expanded like Kubernetes does, stdout/stderr go to ``pods/<pod>/log``, and
 restartPolicy Always/OnFailure/Never is honoured with capped exponential back-off.
+
+A pod's containers: ``initContainers`` run one after the other, each to a zero exit (retried
+with back-off, or the pod fails with ``Init:Error`` under ``restartPolicy: Never``), then every
+app container runs as its own process group. The first is the pod's ``PodProc`` (log ``log``);
+the others are its ``sidecars`` (log ``log.<name>``), restarted under the same policy. The pod
+ends once every app container has ended, Succeeded if all exited 0.
 """
 from __future__ import annotations
 
@@ -67,6 +73,10 @@ class PodProc:
     isolate: bool = False         # own user/pid/mount namespaces (see namespace_isolation())
     jail: list[str] = field(default_factory=list)  # GPU jail argv prefix (gpu_jail_argv), [] = none
     exec_prefix: list[str] = field(default_factory=list)  # image pods: `tk8s-container --exec-in` options
+    name: str = ""                # the container's name
+    log_name: str = "log"         # its log file in the pod dir (the first app container: "log")
+    init: list = field(default_factory=list)      # init containers (PodProc each), run in order first
+    sidecars: list = field(default_factory=list)  # the pod's other app containers (PodProc each)
     proc: subprocess.Popen | None = None
     restarts: int = 0
     started: float = 0.0
@@ -96,17 +106,71 @@ class PodRuntime:
         argv = [*pp.jail, *pp.argv]  # nothing the pod runs can leave the jail
         if pp.isolate and namespace_isolation()[0]:  # outside the jail: a Landlocked process may not mount /proc
             argv = [*UNSHARE, "--", *argv]
-        log = open(pp.dir / "log", "ab", buffering=0)
+        log = open(pp.dir / pp.log_name, "ab", buffering=0)
         try:
             p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
                                  stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
         finally:
             log.close()
-        atomic_write_json(pp.dir / "pod.pid", {"pid": p.pid, "pgid": p.pid, "argv": pp.argv,
-                                               "start": proc_start_ticks(p.pid)})
+        atomic_write_json(pp.dir / _pidfile(pp), {"pid": p.pid, "pgid": p.pid, "argv": pp.argv,
+                                                  "start": proc_start_ticks(p.pid)})
         return p
 
+    def _init(self, pp: PodProc) -> bool:
+        """Run the init containers in order; False when the pod stops or fails on one."""
+        for i, ic in enumerate(pp.init):
+            backoff = 0.1
+            while True:
+                if pp.stopping:
+                    return False
+                try:
+                    ic.proc = self._spawn(ic)
+                except OSError as e:
+                    self.on_status(pp, "Failed", {"message": f"init container {ic.name}: {e}", "reason": "Init:StartError"})
+                    return False
+                self.on_status(pp, "Pending", {"reason": "PodInitializing", "message": f"Init:{i}/{len(pp.init)}"})
+                rc = ic.proc.wait()
+                ic.exit_code = rc
+                (pp.dir / _pidfile(ic)).unlink(missing_ok=True)
+                if rc == 0 or pp.stopping:
+                    break
+                if pp.restart_policy == "Never":
+                    self.on_status(pp, "Failed", {"reason": "Init:Error", "exitCode": rc,
+                                                  "message": f"init container {ic.name} exited {rc}"})
+                    return False
+                ic.restarts += 1
+                time.sleep(backoff)
+                backoff = min(backoff * 2, 10.0)
+        return not pp.stopping
+
+    def _run_sidecar(self, sc: PodProc, pp: PodProc) -> None:
+        backoff = 0.1
+        while not pp.stopping:
+            sc.started = time.time()
+            try:
+                sc.proc = self._spawn(sc)
+            except OSError:
+                sc.exit_code = 127
+                break
+            if pp.proc is not None and pp.proc.poll() is None:
+                self.on_status(pp, "Running", {})  # its container statuses now include this one
+            rc = sc.proc.wait()
+            sc.exit_code = rc
+            (pp.dir / _pidfile(sc)).unlink(missing_ok=True)
+            if pp.stopping or not (pp.restart_policy == "Always" or (pp.restart_policy == "OnFailure" and rc != 0)):
+                break
+            sc.restarts += 1
+            self.on_status(pp, "Running", {})
+            time.sleep(backoff)
+            backoff = min(backoff * 2, 10.0)
+        sc.done.set()
+
     def _run(self, pp: PodProc) -> None:
+        if pp.init and not self._init(pp):
+            pp.done.set()
+            return
+        for sc in pp.sidecars:
+            threading.Thread(target=self._run_sidecar, args=(sc, pp), name=f"pod-{pp.key}-{sc.name}", daemon=True).start()
         backoff = 0.1
         while not pp.stopping:
             pp.started = time.time()
@@ -121,12 +185,21 @@ class PodRuntime:
             rc = pp.proc.wait()
             trace("runtime", f"exited {pp.key} rc={rc}")
             pp.exit_code = rc
-            (pp.dir / "pod.pid").unlink(missing_ok=True)
+            (pp.dir / _pidfile(pp)).unlink(missing_ok=True)
             if pp.stopping:
                 break
             ok = rc == 0
             again = pp.restart_policy == "Always" or (pp.restart_policy == "OnFailure" and not ok)
             if not again:
+                for sc in pp.sidecars:  # the pod ends with its last container
+                    while not sc.done.wait(0.5):
+                        if pp.stopping:
+                            break
+                if pp.stopping:
+                    break
+                bad = [sc for sc in pp.sidecars if sc.exit_code not in (0, None)]
+                if bad and ok:
+                    ok, rc = False, bad[0].exit_code
                 text = ""
                 try:
                     text = (pp.dir / "log").read_text(errors="replace")
@@ -148,8 +221,9 @@ class PodRuntime:
         if pp is None:
             return None
         pp.stopping = True
-        if pp.proc is not None and pp.proc.poll() is None:
-            kill_group(pp.proc.pid, grace)
+        for c in (pp, *pp.sidecars, *pp.init):
+            if c.proc is not None and c.proc.poll() is None:
+                kill_group(c.proc.pid, grace)
         return pp
 
     def stop_all(self) -> None:
@@ -159,6 +233,10 @@ class PodRuntime:
     def running(self) -> dict[str, PodProc]:
         with self.lock:
             return dict(self.pods)
+
+
+def _pidfile(pp: PodProc) -> str:
+    return "pod.pid" if pp.log_name == "log" else f"pod-{pp.name}.pid"
 
 
 # A pod's own namespaces, when the kernel lets an unprivileged user create them: a user namespace

@@ -331,6 +331,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--dry-run", choices=["none", "client", "server"], default="none")
     ap.add_argument("--show-managed-fields", action="store_true")
     ap.add_argument("--address", default="127.0.0.1")
+    ap.add_argument("-c", "--container")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -500,13 +501,13 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             print(f"{n} object(s) deleted")
         elif a.verb == "logs":
             path = k.k8s(object_path("pod", a.args[0], ns) + "/log")
-            text = k.get(path, query={"tailLines": a.tail or None}, raw=True)
+            text = k.get(path, query={"tailLines": a.tail or None, "container": a.container}, raw=True)
             print(text, end="", flush=True)
             if a.follow:  # -f: print what the pod appends until it terminates
-                seen = len(k.get(path, raw=True))
+                seen = len(k.get(path, query={"container": a.container}, raw=True))
                 while True:
                     phase = k.get(k.k8s(object_path("pod", a.args[0], ns))).get("status", {}).get("phase")
-                    full = k.get(path, raw=True)
+                    full = k.get(path, query={"container": a.container}, raw=True)
                     print(full[seen:], end="", flush=True)
                     seen = len(full)
                     if phase in ("Succeeded", "Failed"):
