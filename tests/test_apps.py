@@ -390,3 +390,31 @@ def test_init_and_multi_container_pod_on_a_real_cluster(cluster):
     assert [c["name"] for c in st["initContainerStatuses"]] == ["prep"]
     assert kc("logs", "multi", "-c", "helper").stdout.strip() == "helper ran"
     assert kc("logs", "multi", "-c", "nope", check=False).returncode != 0
+
+
+def test_readiness_and_liveness_probes_on_a_real_cluster(cluster):
+    """A pod is Ready only once its readiness probe passes (and only then a Service endpoint); a
+    failing liveness probe restarts it."""
+    ws, env, kc, summary = cluster
+    (ws / "probes.json").write_text(json.dumps({"apiVersion": "v1", "kind": "List", "items": [
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "slow", "labels": {"app": "slow"}},
+         "spec": {"containers": [{"name": "c", "image": "busybox",
+                                  "command": ["sh", "-c", "sleep 1.5; touch marker; sleep 60"],
+                                  "readinessProbe": {"exec": {"command": ["test", "-f", "marker"]}, "periodSeconds": 0.2,
+                                                     "failureThreshold": 1}}]}},
+        {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "sick"},
+         "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"],
+                                  "livenessProbe": {"exec": {"command": ["false"]}, "periodSeconds": 0.2,
+                                                    "failureThreshold": 2}}]}}]}))
+    kc("apply", "-f", "probes.json")
+
+    def pod(n):
+        return json.loads(kc("get", "pod", n, "-o", "json").stdout)
+
+    def ready(n):
+        return next((c["status"] for c in pod(n)["status"].get("conditions", []) if c["type"] == "Ready"), None)
+
+    _until(lambda: pod("slow")["status"].get("phase") == "Running", 20)
+    assert ready("slow") == "False"
+    _until(lambda: ready("slow") == "True", 20)
+    _until(lambda: pod("sick")["status"]["containerStatuses"][0]["restartCount"] >= 1, 30)

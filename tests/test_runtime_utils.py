@@ -369,3 +369,62 @@ def test_init_containers_then_all_app_containers(tmp_path):
                           restart_policy="Never", name="i", log_name="log.i")]
     rt.start(never)
     assert never.done.wait(20) and events[-1] == ("Failed", "Init:Error")
+
+
+def test_probe_handlers_and_prober(tmp_path):
+    """httpGet / tcpSocket / exec handlers; readiness flips ready after its thresholds; a failing
+    liveness probe kills the process."""
+    import http.server
+    import socketserver
+    import threading as th
+    import time as tm
+
+    from tritonk8ssupervisor_amd.agent.probes import Prober, run_probe
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            self.send_response(200 if self.path == "/ok" else 503)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = socketserver.TCPServer(("127.0.0.1", 0), H)
+    th.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    c = {"ports": [{"name": "web", "containerPort": port}]}
+    try:
+        assert run_probe({"httpGet": {"path": "/ok", "port": "web"}}, c, "127.0.0.1")[0]
+        ok, msg = run_probe({"httpGet": {"path": "/bad", "port": port}}, c, "127.0.0.1")
+        assert not ok and "503" in msg
+        assert run_probe({"tcpSocket": {"port": port}}, c, "127.0.0.1")[0]
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    assert not run_probe({"tcpSocket": {"port": port}}, c, "127.0.0.1")[0]
+    assert run_probe({"exec": {"command": ["true"]}}, c, "127.0.0.1")[0]
+    assert not run_probe({"exec": {"command": ["false"]}}, c, "127.0.0.1")[0]
+
+    marker = tmp_path / "ready"
+    changes, killed = [], []
+    spec = {"readinessProbe": {"exec": {"command": ["test", "-f", str(marker)]}, "periodSeconds": 0.05,
+                               "failureThreshold": 1},
+            "livenessProbe": {"exec": {"command": ["test", "!", "-f", str(tmp_path / "dead")]}, "periodSeconds": 0.05,
+                              "failureThreshold": 2}}
+    alive = [True]
+    p = Prober(spec, "127.0.0.1", lambda: alive[0], lambda: (killed.append(1), alive.__setitem__(0, False)),
+               lambda: changes.append(1))
+    assert not p.ready
+    p.start()
+    tm.sleep(0.2)
+    assert not p.ready
+    marker.touch()
+    deadline = tm.monotonic() + 5
+    while not p.ready and tm.monotonic() < deadline:
+        tm.sleep(0.02)
+    assert p.ready and changes
+    (tmp_path / "dead").touch()
+    deadline = tm.monotonic() + 5
+    while not killed and tm.monotonic() < deadline:
+        tm.sleep(0.02)
+    assert killed and "livenessProbe failed 2 times" in p.last_message

@@ -430,7 +430,7 @@ class Agent:
                                  argv=built["argv"], env=built["env"], restart_policy=spec.get("restartPolicy", "Always"),
                                  gpu_ids=ids if first_app else [], ip=pod_ip,
                                  isolate=avail and not gpu_pod and built["image"] is None, jail=built["jail"],
-                                 exec_prefix=built["exec_prefix"], name=cont.get("name") or f"c{n}",
+                                 exec_prefix=built["exec_prefix"], name=cont.get("name") or f"c{n}", container=cont,
                                  log_name="log" if first_app else f"log.{cont.get('name') or n}"))
         pp = procs[len(inits)]
         pp.init, pp.sidecars = procs[:len(inits)], procs[len(inits) + 1:]
@@ -588,14 +588,18 @@ class Agent:
         if pp is not None:
             def cstatus(cp: PodProc, image: str = "") -> dict:
                 alive = cp.proc is not None and cp.proc.poll() is None
+                ready = alive and (cp.prober is None or cp.prober.ready)
                 if alive:
                     state = {"running": {"startedAt": cp.started}}
                 elif cp.exit_code is not None:
                     state = {"terminated": {"exitCode": cp.exit_code, "reason": "Completed" if cp.exit_code == 0 else "Error"}}
                 else:
                     state = {"waiting": {"reason": "PodInitializing" if phase == "Pending" else "ContainerCreating"}}
-                return {"name": cp.name or "main", "image": image, "restartCount": cp.restarts, "state": state,
-                        "ready": alive, "started": alive}
+                out = {"name": cp.name or "main", "image": image, "restartCount": cp.restarts, "state": state,
+                       "ready": ready, "started": alive and (cp.prober is None or cp.prober.started)}
+                if cp.prober is not None and cp.prober.last_message and not ready:
+                    out["lastProbeMessage"] = cp.prober.last_message[-300:]
+                return out
 
             images = self._pods_meta.get(key, {}).get("images") or {}
             main = cstatus(pp, images.get(pp.name, ""))
@@ -603,7 +607,8 @@ class Agent:
                 main["state"] = {"terminated": {"exitCode": extra.get("exitCode", pp.exit_code),
                                                 "reason": "Completed" if phase == "Succeeded" else "Error"}}
             if phase == "Running" and "running" not in main["state"] and pp.proc is not None:
-                main.update(state={"running": {"startedAt": pp.started}}, ready=True, started=True)
+                main.update(state={"running": {"startedAt": pp.started}}, ready=pp.prober is None or pp.prober.ready,
+                            started=True)
             st["containerStatuses"] = [main] + [cstatus(sc, images.get(sc.name, "")) for sc in pp.sidecars]
             if pp.init:
                 st["initContainerStatuses"] = [cstatus(ic, images.get(ic.name, "")) for ic in pp.init]

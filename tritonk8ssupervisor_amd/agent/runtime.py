@@ -77,6 +77,8 @@ class PodProc:
     log_name: str = "log"         # its log file in the pod dir (the first app container: "log")
     init: list = field(default_factory=list)      # init containers (PodProc each), run in order first
     sidecars: list = field(default_factory=list)  # the pod's other app containers (PodProc each)
+    container: dict = field(default_factory=dict)  # its spec (probes, ports)
+    prober: object = None         # agent/probes.Prober of the running process, if it has probes
     proc: subprocess.Popen | None = None
     restarts: int = 0
     started: float = 0.0
@@ -116,6 +118,19 @@ class PodRuntime:
                                                   "start": proc_start_ticks(p.pid)})
         return p
 
+    def _probe(self, cp: PodProc, pp: PodProc) -> None:
+        """Start the container's probes for the process just spawned (agent/probes.py)."""
+        if not any(k in cp.container for k in ("startupProbe", "livenessProbe", "readinessProbe")):
+            cp.prober = None
+            return
+        from .probes import Prober
+
+        proc = cp.proc
+        cp.prober = Prober(cp.container, cp.ip, lambda: proc.poll() is None, lambda: kill_group(proc.pid, 1.0),
+                           lambda: self.on_status(pp, "Running", {}), lambda cmd: container_exec_argv(cp, cmd),
+                           env=dict(cp.env), cwd=str(cp.dir))
+        cp.prober.start()
+
     def _init(self, pp: PodProc) -> bool:
         """Run the init containers in order; False when the pod stops or fails on one."""
         for i, ic in enumerate(pp.init):
@@ -152,6 +167,7 @@ class PodRuntime:
             except OSError:
                 sc.exit_code = 127
                 break
+            self._probe(sc, pp)
             if pp.proc is not None and pp.proc.poll() is None:
                 self.on_status(pp, "Running", {})  # its container statuses now include this one
             rc = sc.proc.wait()
@@ -181,6 +197,7 @@ class PodRuntime:
                 self.on_status(pp, "Failed", {"message": f"failed to start {pp.argv[0]!r}: {e}", "reason": "StartError"})
                 break
             trace("runtime", f"spawned {pp.key}")
+            self._probe(pp, pp)
             self.on_status(pp, "Running", {})
             rc = pp.proc.wait()
             trace("runtime", f"exited {pp.key} rc={rc}")
@@ -221,6 +238,9 @@ class PodRuntime:
         if pp is None:
             return None
         pp.stopping = True
+        for c in (pp, *pp.sidecars):
+            if c.prober is not None:
+                c.prober.stop.set()
         for c in (pp, *pp.sidecars, *pp.init):
             if c.proc is not None and c.proc.poll() is None:
                 kill_group(c.proc.pid, grace)

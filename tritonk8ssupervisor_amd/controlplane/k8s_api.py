@@ -444,6 +444,8 @@ class KubernetesAPI:
         for o in self.store.list("pods", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns):
             if o.get("status", {}).get("phase") != "Running" or not labels_match(sel, o["metadata"].get("labels")):
                 continue
+            if any(c.get("type") == "Ready" and c.get("status") == "False" for c in o["status"].get("conditions") or []):
+                continue  # not ready (a readiness probe): no traffic
             ip = o.get("status", {}).get("podIP")
             tp = port["targetPort"]
             if isinstance(tp, str):  # named container port
