@@ -301,3 +301,26 @@ def test_events_select_by_uid_as_kubectl_describe_does(kube):
     assert any(e["reason"] == "Scheduled" for e in evs["items"]), evs
     e = evs["items"][0]
     assert e["involvedObject"]["apiVersion"] == "v1" and e["lastTimestamp"] and e["source"]["component"]
+
+
+def test_namespaces_create_get_label_and_cascade_delete(kube):
+    st, _, ns = _raw(kube, "POST", "/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace",
+                                                          "metadata": {"name": "team-a"}})
+    assert st == 201 and ns["metadata"]["labels"]["kubernetes.io/metadata.name"] == "team-a"
+    assert _raw(kube, "POST", "/api/v1/namespaces", {"metadata": {"name": "team-a"}})[0] == 409
+    assert _raw(kube, "POST", "/api/v1/namespaces", {"metadata": {"name": "Bad_Name"}})[0] == 422
+    assert _raw(kube, "GET", "/api/v1/namespaces/team-a")[0] == 200
+    assert _raw(kube, "GET", "/api/v1/namespaces/kube-system")[0] == 200  # built in
+    assert _raw(kube, "GET", "/api/v1/namespaces/nope")[0] == 404
+    st, _, ns = _raw(kube, "PATCH", "/api/v1/namespaces/team-a", {"metadata": {"labels": {"tier": "gpu"}}},
+                     ctype=k8s_wire.MERGE_PATCH)
+    assert st == 200 and ns["metadata"]["labels"]["tier"] == "gpu"
+    cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "c"}, "data": {"a": "1"}}
+    assert _raw(kube, "POST", "/api/v1/namespaces/team-a/configmaps", cm)[0] == 201
+    names = [n["metadata"]["name"] for n in _raw(kube, "GET", "/api/v1/namespaces")[2]["items"]]
+    assert "team-a" in names and "default" in names
+    st, _, gone = _raw(kube, "DELETE", "/api/v1/namespaces/team-a")
+    assert st == 200 and gone["status"]["phase"] == "Terminating"
+    assert _raw(kube, "GET", "/api/v1/namespaces/team-a/configmaps/c")[0] == 404  # its objects went with it
+    assert _raw(kube, "GET", "/api/v1/namespaces/team-a")[0] == 404
+    assert _raw(kube, "DELETE", "/api/v1/namespaces/default")[0] == 403

@@ -135,6 +135,9 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
         rows = [["NAME", "TYPE", "CLUSTER-IP", "EXTERNAL-IP", "PORT(S)", "AGE"]] + [[
             o["metadata"]["name"], o["spec"].get("type", "ClusterIP"), o["spec"].get("clusterIP", ""), ext(o), ports(o), _age(o)]
             for o in items]
+    elif k == "namespace":
+        rows = [["NAME", "STATUS", "AGE"]] + [[o["metadata"]["name"], o.get("status", {}).get("phase", "Active"), _age(o)]
+                                             for o in items]
     elif k in ("configmap", "secret"):
         rows = [["NAME"] + (["TYPE"] if k == "secret" else []) + ["DATA", "AGE"]] + [
             [o["metadata"]["name"]] + ([o.get("type", "Opaque")] if k == "secret" else [])
@@ -421,6 +424,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 print(f"  {e.get('type', ''):<8} {e.get('reason', ''):<20} {e.get('message', '')}")
         elif a.verb == "create" and a.args and a.args[0] in ("configmap", "cm", "secret"):
             return _create_data(k, a, ns)
+        elif a.verb == "create" and a.args and kind_key(a.args[0]) == "namespace":
+            if len(a.args) < 2:
+                raise SystemExit("usage: kubectl create namespace NAME")
+            k.post(k.k8s("/api/v1/namespaces"), {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": a.args[1]}})
+            print(f"namespace/{a.args[1]} created")
         elif a.verb == "create" and a.args and kind_key(a.args[0]) == "deployment":
             return _create_deployment(k, a, ns)
         elif a.verb == "expose":

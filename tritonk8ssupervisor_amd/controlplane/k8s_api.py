@@ -8,6 +8,7 @@ import asyncio
 import copy
 import json
 import os
+import re
 import time
 from pathlib import Path
 
@@ -169,13 +170,84 @@ class KubernetesAPI:
         self.reconcile()
         return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": "nodes"}}
 
+    _BUILTIN_NS = ("default", "kube-system", "kube-public", "amd-gpu")
+
+    def _namespaces(self, p: str) -> dict[str, dict]:
+        """The project's namespaces: the ones created through the API, the built-in ones, and any
+        other that objects were created in (created implicitly, as a lenient API server would)."""
+        out = {o["metadata"]["name"]: self._strip(o) for o in self.store.list("namespaces", lambda o: self._in(p, o))}
+        implicit = set(self._BUILTIN_NS)
+        for plural, r in k8s_wire.RESOURCES.items():
+            if r[4] and plural != "events":
+                implicit |= {o["metadata"].get("namespace", "default") for o in self.store.list(plural, lambda o: self._in(p, o))}
+        for n in implicit - set(out):
+            out[n] = {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": n, "labels": {
+                "kubernetes.io/metadata.name": n}}, "spec": {"finalizers": ["kubernetes"]}, "status": {"phase": "Active"}}
+        return out
+
+    async def h_namespace_get(self, req: Request, name: str, pid: str | None = None):
+        p = self._pid(pid, req)
+        ns = self._namespaces(p).get(name)
+        if ns is None:
+            raise HttpError(404, f'namespaces "{name}" not found')
+        return ns
+
+    async def h_namespace_create(self, req: Request, pid: str | None = None):
+        p = self._pid(pid, req)
+        self._auth(req, self.project(p))
+        body = req.json()
+        name = ((body or {}).get("metadata") or {}).get("name")
+        if not name or not re.fullmatch(r"[a-z0-9]([-a-z0-9]*[a-z0-9])?", name) or len(name) > 63:
+            raise HttpError(422, f'Namespace "{name}" is invalid: metadata.name: must be a DNS label')
+        if self.store.get("namespaces", _key(p, name)) is not None:
+            raise HttpError(409, f'namespaces "{name}" already exists')
+        md = body["metadata"]
+        md.setdefault("labels", {})["kubernetes.io/metadata.name"] = name
+        md.setdefault("annotations", {})
+        obj = {"apiVersion": "v1", "kind": "Namespace", "metadata": md, "spec": {"finalizers": ["kubernetes"]},
+               "status": {"phase": "Active"}, "_project": p}
+        if self._dry_run(req):
+            return Response(201, self._strip(obj))
+        return Response(201, self._strip(self.store.put("namespaces", _key(p, name), obj)))
+
+    async def h_namespace_patch(self, req: Request, name: str, pid: str | None = None):
+        """Labels and annotations of a namespace (kubectl label/annotate ns)."""
+        p = self._pid(pid, req)
+        self._auth(req, self.project(p))
+        cur = self._namespaces(p).get(name)
+        if cur is None:
+            raise HttpError(404, f'namespaces "{name}" not found')
+        body = req.json()
+        md = (body.get("metadata") or {}) if isinstance(body, dict) else {}
+        new = merge_patch(cur, {"metadata": {k: md[k] for k in ("labels", "annotations") if k in md}})
+        new["_project"] = p
+        return self._strip(self.store.put("namespaces", _key(p, name), new))
+
+    async def h_namespace_delete(self, req: Request, name: str, pid: str | None = None):
+        """Delete a namespace and everything in it (the namespace controller's cascade)."""
+        p = self._pid(pid, req)
+        self._auth(req, self.project(p))
+        if name in ("default", "kube-system", "kube-public"):
+            raise HttpError(403, f'namespaces "{name}" is forbidden: this namespace may not be deleted')
+        cur = self._namespaces(p).get(name)
+        if cur is None:
+            raise HttpError(404, f'namespaces "{name}" not found')
+        if self._dry_run(req):
+            return {**cur, "status": {"phase": "Terminating"}}
+        for plural, r in k8s_wire.RESOURCES.items():
+            if r[4]:
+                for o in self.store.list(plural, lambda o: self._in(p, o) and o["metadata"].get("namespace") == name):
+                    self.store.delete(plural, _key(p, name, o["metadata"]["name"]))
+        self.store.delete("namespaces", _key(p, name))
+        self._sync_proxy()
+        self.reconcile()
+        return {**cur, "status": {"phase": "Terminating"}}
+
     async def h_namespaces(self, req: Request, pid: str | None = None):
-        self._pid(pid, req)
-        names = {"default", "kube-system", "amd-gpu"}
-        for kind in ("pods", "daemonsets", "jobs", "deployments", "services", "configmaps", "secrets", "ingresses"):
-            names |= {o["metadata"].get("namespace", "default") for o in self.store.list(kind)}
-        items = [{"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": n}, "spec": {"finalizers": ["kubernetes"]},
-                  "status": {"phase": "Active"}} for n in sorted(names)]
+        p = self._pid(pid, req)
+        if req.method == "POST":
+            return await self.h_namespace_create(req, pid)
+        items = sorted(self._namespaces(p).values(), key=lambda o: o["metadata"]["name"])
         if k8s_wire.wants_table(req.headers.get("accept", "")):
             return k8s_wire.table("namespaces", items, str(self.store.rv))
         return {"kind": "NamespaceList", "apiVersion": "v1", "metadata": {"resourceVersion": str(self.store.rv)},

@@ -41,7 +41,8 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "cronjobs": ("batch", "v1", "CronJob", "cronjob", True, ("cj",), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
 }
-READ_ONLY = {"namespaces": ("get", "list", "watch"), "events": ("get", "list", "watch", "create", "delete")}
+READ_ONLY = {"namespaces": ("create", "delete", "get", "list", "patch", "watch"),
+             "events": ("get", "list", "watch", "create", "delete")}
 VERBS = ("create", "delete", "get", "list", "patch", "update", "watch")
 
 

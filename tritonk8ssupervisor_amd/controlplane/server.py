@@ -191,6 +191,10 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler)
             add("PATCH", r"/api/v1/nodes/(?P<name>[^/]+)", self.h_node_patch)
             add("DELETE", r"/api/v1/nodes/(?P<name>[^/]+)", self.h_node_delete)
             add("GET", r"/api/v1/namespaces", self.h_namespaces)
+            add("POST", r"/api/v1/namespaces", self.h_namespace_create)
+            add("GET", r"/api/v1/namespaces/(?P<name>[^/]+)", self.h_namespace_get)
+            add("PATCH", r"/api/v1/namespaces/(?P<name>[^/]+)", self.h_namespace_patch)
+            add("DELETE", r"/api/v1/namespaces/(?P<name>[^/]+)", self.h_namespace_delete)
             add("GET", r"/api/v1/pods", self.h_pods)
             for kind, grp in KIND_GROUPS:
                 add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._lister(kind))

@@ -34,7 +34,7 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "configmaps": "configmap", "secrets": "secret", "ing": "ingress", "ingresses": "ingress",
            "sts": "statefulset", "statefulsets": "statefulset", "rs": "replicaset", "replicasets": "replicaset",
            "cj": "cronjob", "cronjobs": "cronjob", "pvc": "persistentvolumeclaim",
-           "persistentvolumeclaims": "persistentvolumeclaim"}
+           "persistentvolumeclaims": "persistentvolumeclaim", "ns": "namespace", "namespaces": "namespace"}
 
 
 def kind_key(kind: str) -> str:
@@ -46,6 +46,8 @@ def collection_path(kind: str, ns: str = "default") -> str:
     k = kind_key(kind)
     if k == "node":
         return "/api/v1/nodes"
+    if k == "namespace":
+        return "/api/v1/namespaces"
     if k not in KINDS:
         raise ValueError(f"unsupported kind {kind!r}")
     _, group, plural = KINDS[k]
@@ -79,6 +81,17 @@ def is_subset(want, have) -> bool:
     return want == have or (want is not None and have is not None and str(want) == str(have))
 
 
+def _ensure_namespace(k: Client, o: dict) -> dict:
+    try:
+        k.post(k.k8s("/api/v1/namespaces"), {"apiVersion": "v1", "kind": "Namespace", "metadata": {
+            "name": o["metadata"]["name"], **{f: o["metadata"][f] for f in ("labels", "annotations") if o["metadata"].get(f)}}})
+        return {"created": True, "action": "created"}
+    except ApiError as e:
+        if e.status != 409:
+            raise
+        return {"created": False, "action": "unchanged"}
+
+
 def apply_objects(k: Client, objs: list[dict]) -> list[dict]:
     """``kubectl apply``: create, or update an existing object to the manifest (PUT with the live
     resourceVersion; status and server-allocated fields are kept by the control plane)."""
@@ -86,7 +99,7 @@ def apply_objects(k: Client, objs: list[dict]) -> list[dict]:
     for o in objs:
         kind = o.get("kind", "")
         if kind.lower() == "namespace":
-            res.append({"kind": kind, "name": o["metadata"]["name"], "created": False, "action": "unchanged"})
+            res.append({"kind": kind, "name": o["metadata"]["name"], **_ensure_namespace(k, o)})
             continue
         ns = o.get("metadata", {}).get("namespace", "default")
         name = o["metadata"].get("name")
@@ -125,7 +138,8 @@ def server_apply_objects(k: Client, objs: list[dict], manager: str = "kubectl", 
     for o in objs:
         kind = o.get("kind", "")
         if kind.lower() == "namespace":
-            res.append({"kind": kind, "name": o["metadata"]["name"], "created": False, "action": "unchanged"})
+            _ensure_namespace(k, o)
+            res.append({"kind": kind, "name": o["metadata"]["name"], "action": "serverside-applied"})
             continue
         ns = o.get("metadata", {}).get("namespace", "default")
         name = o["metadata"]["name"]
@@ -136,11 +150,10 @@ def server_apply_objects(k: Client, objs: list[dict], manager: str = "kubectl", 
 
 
 def delete_objects(k: Client, objs: list[dict]) -> int:
+    """``kubectl delete -f``: the objects, then the manifest's namespaces (with what is left in them)."""
     n = 0
-    for o in objs:
+    for o in sorted(objs, key=lambda o: o.get("kind", "").lower() == "namespace"):
         kind = o.get("kind", "")
-        if kind.lower() == "namespace":
-            continue
         ns = o.get("metadata", {}).get("namespace", "default")
         try:
             k.delete(k.k8s(object_path(kind, o["metadata"]["name"], ns)))
