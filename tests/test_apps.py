@@ -144,7 +144,8 @@ def cluster(tmp_path, monkeypatch):
     for f in ("setup.sh", "tk8s", "kubectl"):
         shutil.copy2(REPO / f, tmp_path / f)
     env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_FAKE_GPUS="8",
-               TK8S_REMAP_PRIVILEGED_PORTS="1")  # exercise the non-root port shift even as root
+               TK8S_REMAP_PRIVILEGED_PORTS="1",  # exercise the non-root port shift even as root
+               TK8S_METRICS_PERIOD="0.5")
     env.pop("TK8S_FAULTS", None)
     r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "2", "--rccl", "off"], cwd=tmp_path,
                        env=env, capture_output=True, text=True, timeout=180)
@@ -418,3 +419,18 @@ def test_readiness_and_liveness_probes_on_a_real_cluster(cluster):
     assert ready("slow") == "False"
     _until(lambda: ready("slow") == "True", 20)
     _until(lambda: pod("sick")["status"]["containerStatuses"][0]["restartCount"] >= 1, 30)
+
+
+def test_kubectl_top_pods_from_the_metrics_api(cluster):
+    ws, env, kc, summary = cluster
+    (ws / "burn.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "burn"},
+        "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sh", "-c", "while :; do :; done"]}]}}))
+    kc("apply", "-f", "burn.json")
+
+    def cpu_m():
+        out = kc("top", "pods", check=False).stdout
+        row = next((line.split() for line in out.splitlines() if line.startswith("burn ")), None)
+        return int(row[1].rstrip("m")) if row else 0
+
+    assert _until(lambda: cpu_m() > 300, 30)  # a busy loop uses most of a core
+    kc("delete", "pod", "burn")

@@ -49,7 +49,8 @@ def test_discovery_documents(kube):
     assert st == 200 and v["kind"] == "APIVersions" and v["versions"] == ["v1"]
     _, _, groups = _raw(kube, "GET", "/apis")
     names = {g["name"]: g["preferredVersion"]["groupVersion"] for g in groups["groups"]}
-    assert names == {"apps": "apps/v1", "batch": "batch/v1", "networking.k8s.io": "networking.k8s.io/v1"}
+    assert names == {"apps": "apps/v1", "batch": "batch/v1", "networking.k8s.io": "networking.k8s.io/v1",
+                     "autoscaling": "autoscaling/v2", "metrics.k8s.io": "metrics.k8s.io/v1beta1"}
     _, _, core = _raw(kube, "GET", "/api/v1")
     res = {r["name"]: r for r in core["resources"]}
     assert core["kind"] == "APIResourceList" and core["groupVersion"] == "v1"

@@ -333,3 +333,51 @@ def test_volume_materialisation_unit(tmp_path):
             "name": "cfg", "items": [{"key": "other", "path": "../../etc/x"}]}}]}}, tmp_path / "p3", tmp_path / "node", fetch)
     with pytest.raises(VolumeError):
         mounts({"volumeMounts": [{"name": "scratch", "mountPath": "/w", "subPath": "../x"}]}, dirs)
+
+
+def test_metrics_api_and_hpa(cp):
+    import asyncio
+
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "web"}, "spec": {
+        "replicas": 2, "selector": {"matchLabels": {"app": "web"}},
+        "template": {"metadata": {"labels": {"app": "web"}}, "spec": {"containers": [
+            {"name": "c", "command": ["true"], "resources": {"requests": {"cpu": "500m"}}}]}}}})
+    for n in _pods(cp, "web-"):
+        cp.store.patch("pods", _key("1a1", "default", n), lambda o: o["status"].update(phase="Running"))
+
+    def usage(cores):
+        cp._ingest_metrics("1a1", "kubenode1", {"timestamp": "2026-01-01T00:00:00Z", "node": {
+            "cpu_cores": 3.0, "memory_bytes": 2 ** 30}, "pods": {
+            f"default/{n}": [{"name": "c", "cpu_cores": cores, "memory_bytes": 2 ** 20}] for n in _pods(cp, "web-")}})
+
+    usage(0.5)  # 100 % of the request
+    req = type("R", (), {"q": lambda self, k, d=None: None})()
+    cp._pid = lambda pid, r: "1a1"
+    lst = asyncio.run(cp.h_pod_metrics(req, ns="default"))
+    assert lst["kind"] == "PodMetricsList" and len(lst["items"]) == 2
+    assert lst["items"][0]["containers"][0]["usage"] == {"cpu": "500000000n", "memory": "1024Ki"}
+    nodes = asyncio.run(cp.h_node_metrics(req))
+    assert nodes["items"][0]["usage"]["cpu"] == "3000000000n"
+    cp.create("1a1", "horizontalpodautoscalers", "default", {"metadata": {"name": "web"}, "spec": {
+        "scaleTargetRef": {"apiVersion": "apps/v1", "kind": "Deployment", "name": "web"},
+        "minReplicas": 1, "maxReplicas": 3,
+        "metrics": [{"type": "Resource", "resource": {"name": "cpu", "target": {"type": "Utilization",
+                                                                               "averageUtilization": 50}}}]}})
+    cp._ctl_hpas("1a1", now=1000.0)
+    d = cp.store.get("deployments", _key("1a1", "default", "web"))
+    assert d["spec"]["replicas"] == 3  # 2 x 100/50 = 4, capped at maxReplicas
+    hpa = cp.store.get("horizontalpodautoscalers", _key("1a1", "default", "web"))
+    assert hpa["status"]["desiredReplicas"] == 3 and hpa["status"]["currentMetrics"][0]["resource"]["current"][
+        "averageUtilization"] == 100
+    # low use: the scale-down waits out the stabilization window (300 s by default)
+    for n in _pods(cp, "web-"):
+        cp.store.patch("pods", _key("1a1", "default", n), lambda o: o["status"].update(phase="Running"))
+    usage(0.05)
+    cp._ctl_hpas("1a1", now=1100.0)
+    assert cp.store.get("deployments", _key("1a1", "default", "web"))["spec"]["replicas"] == 3
+    cp._ctl_hpas("1a1", now=1500.0)
+    assert cp.store.get("deployments", _key("1a1", "default", "web"))["spec"]["replicas"] == 1
+    assert any(e["reason"] == "SuccessfulRescale" for e in cp.store.list("events"))
+    with pytest.raises(HttpError):
+        cp.create("1a1", "horizontalpodautoscalers", "default", {"metadata": {"name": "bad"}, "spec": {
+            "scaleTargetRef": {"kind": "Deployment", "name": "web"}, "minReplicas": 5, "maxReplicas": 2}})

@@ -128,6 +128,8 @@ class Agent:
         self.api: Client | None = None
         self.stop = threading.Event()
         self.hb_period = 1.0
+        self.metrics_period = float(os.environ.get("TK8S_METRICS_PERIOD", "5"))
+        self._sampler = None
         self._devices_dirty = False
         self._pods_meta: dict[str, dict] = {}
         self.pod_cidr = ""
@@ -243,6 +245,8 @@ class Agent:
     def heartbeat_loop(self) -> None:
         api = Client(self.api.base, token=self.api.token, prefix=self.api.prefix, timeout=10.0)
         last_health = time.monotonic()
+        # the first sample after one period: never on the bring-up's critical path
+        next_metrics = time.monotonic() + self.metrics_period
         while not self.stop.is_set():
             if fault("agent.no_heartbeat", self.name) is None:
                 body = {}
@@ -255,6 +259,9 @@ class Agent:
                     body["devices"] = self.plugin.devices()
                 if self._annotations:
                     body["annotations"], self._annotations = self._annotations, {}
+                if time.monotonic() >= next_metrics:  # CPU / memory for metrics.k8s.io (agent/usage.py)
+                    next_metrics = time.monotonic() + self.metrics_period
+                    body["metrics"] = self._usage_sample()
                 for key, pod in list(self._config_wait.items()):  # kubelet retries config errors
                     if key not in self.runtime.running():
                         self._start_pod(pod)
@@ -267,6 +274,20 @@ class Agent:
                 except OSError:
                     pass
             self.stop.wait(self.hb_period)
+
+    def _usage_sample(self) -> dict:
+        if self._sampler is None:
+            from .usage import UsageSampler
+
+            self._sampler = UsageSampler()
+        groups = {}
+        for key, pp in self.runtime.running().items():
+            cs = {c.name or "main": c.proc.pid for c in (pp, *pp.sidecars) if c.proc is not None and c.proc.poll() is None}
+            if cs:
+                groups[key] = cs
+        m = self._sampler.sample(groups)
+        m["window"] = f"{self.metrics_period:g}s"
+        return m
 
     # ---- GPU health (AMD SMI) ------------------------------------------------------------
     def smi_loop(self) -> None:

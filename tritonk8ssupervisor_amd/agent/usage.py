@@ -1,0 +1,89 @@
+"""CPU and memory usage of the node and of its pods, for the metrics API (``kubectl top``) and the
+HorizontalPodAutoscaler: what the kubelet's resource metrics endpoint answers.
+
+A pod's usage is the sum over the processes in its containers' process groups (every container
+runs in a session of its own, agent/runtime.py): CPU from ``utime + stime`` deltas between two
+samples, memory from the resident set. The node's comes from ``/proc/stat`` and ``/proc/meminfo``.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+_TICK = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+_PAGE = os.sysconf("SC_PAGE_SIZE") if hasattr(os, "sysconf") else 4096
+
+
+def _proc_table() -> dict[int, tuple[int, int, int]]:
+    """pid -> (process group, cpu ticks, resident bytes) for every readable process."""
+    out = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat", "rb") as f:
+                raw = f.read().decode(errors="replace")
+            rest = raw[raw.rindex(")") + 2:].split()
+            # fields after "(comm)": state ppid pgrp session ... utime(14) stime(15) ... rss(24)
+            out[int(d)] = (int(rest[2]), int(rest[11]) + int(rest[12]), int(rest[21]) * _PAGE)
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
+def _node_cpu_ticks() -> tuple[int, int]:
+    with open("/proc/stat") as f:
+        vals = [int(x) for x in f.readline().split()[1:]]
+    idle = vals[3] + (vals[4] if len(vals) > 4 else 0)
+    return sum(vals), idle
+
+
+def _node_memory() -> int:
+    info = {}
+    with open("/proc/meminfo") as f:
+        for line in f:
+            k, v = line.split(":", 1)
+            info[k] = int(v.split()[0]) * 1024
+    return info.get("MemTotal", 0) - info.get("MemAvailable", info.get("MemFree", 0))
+
+
+class UsageSampler:
+    """Call ``sample(groups)`` periodically; ``groups``: pod key -> {container name: pgid}."""
+
+    def __init__(self):
+        self.prev: dict[tuple[str, str], tuple[float, int]] = {}
+        self.prev_node: tuple[int, int] | None = None
+
+    def sample(self, groups: dict[str, dict[str, int]]) -> dict:
+        now = time.time()
+        table = _proc_table()
+        by_group: dict[int, list[tuple[int, int]]] = {}
+        for _pid, (pg, ticks, rss) in table.items():
+            by_group.setdefault(pg, []).append((ticks, rss))
+        pods = {}
+        for key, containers in groups.items():
+            cs = []
+            for name, pgid in containers.items():
+                procs = by_group.get(pgid, [])
+                ticks = sum(t for t, _ in procs)
+                rss = sum(r for _, r in procs)
+                last = self.prev.get((key, name))
+                self.prev[(key, name)] = (now, ticks)
+                cores = 0.0
+                if last is not None and now > last[0] and ticks >= last[1]:
+                    cores = (ticks - last[1]) / _TICK / (now - last[0])
+                cs.append({"name": name, "cpu_cores": cores, "memory_bytes": rss})
+            pods[key] = cs
+        live = {(k, n) for k, c in groups.items() for n in c}
+        self.prev = {k: v for k, v in self.prev.items() if k in live}
+        node = {"cpu_cores": 0.0, "memory_bytes": 0}
+        try:
+            total, idle = _node_cpu_ticks()
+            if self.prev_node is not None and total > self.prev_node[0]:
+                busy = (total - self.prev_node[0]) - (idle - self.prev_node[1])
+                node["cpu_cores"] = busy / (total - self.prev_node[0]) * (os.cpu_count() or 1)
+            self.prev_node = (total, idle)
+            node["memory_bytes"] = _node_memory()
+        except (OSError, ValueError, IndexError):
+            pass
+        return {"timestamp": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(now)), "node": node, "pods": pods}

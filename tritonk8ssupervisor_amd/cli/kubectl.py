@@ -496,9 +496,20 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 print(f"evicting pod {p['metadata']['namespace']}/{p['metadata']['name']}")
             print(f"node/{node} drained")
         elif a.verb == "top":
-            if not a.args or kind_key(a.args[0]) != "node":
-                raise SystemExit("usage: kubectl top nodes")
-            print(fmt_top(k.get(k.k8s("/api/v1/nodes"))["items"], k.get(k.k8s("/api/v1/pods"))["items"]))
+            if not a.args or kind_key(a.args[0]) not in ("node", "pod"):
+                raise SystemExit("usage: kubectl top nodes|pods")
+            if kind_key(a.args[0]) == "node":
+                print(fmt_top(k.get(k.k8s("/api/v1/nodes"))["items"], k.get(k.k8s("/api/v1/pods"))["items"]))
+            else:  # the resource metrics API (metrics.k8s.io), as a stock kubectl top pods reads it
+                from ..utils import quantity
+
+                path = "/apis/metrics.k8s.io/v1beta1/" + ("pods" if a.all_namespaces else f"namespaces/{ns}/pods")
+                items = k.get(k.k8s(path), query={"labelSelector": a.selector} if a.selector else None)["items"]
+                rows = [["NAME", "CPU(cores)", "MEMORY(bytes)"]] + [[
+                    m["metadata"]["name"],
+                    f"{int(sum(quantity.parse(c['usage']['cpu']) for c in m['containers']) * 1000)}m",
+                    f"{int(sum(quantity.parse(c['usage']['memory']) for c in m['containers']) / 2**20)}Mi"] for m in items]
+                print(_table(rows))
         elif a.verb == "delete":
             if a.filename:
                 n = delete_objects(k, load_manifests(a.filename))

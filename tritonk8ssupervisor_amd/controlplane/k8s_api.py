@@ -131,6 +131,8 @@ class KubernetesAPI:
         if "annotations" in body:
             new["metadata"].setdefault("annotations", {}).update(body["annotations"])
             changed = True
+        if "metrics" in body:  # CPU / memory samples for metrics.k8s.io (metrics_api.py), not stored
+            self._ingest_metrics(p, name, body["metrics"])
         changed |= _set_ready(new)
         if changed:
             self.store.put("nodes", key, new)
@@ -709,6 +711,16 @@ class KubernetesAPI:
             md["generation"] = 1
         elif kind == "persistentvolumeclaims":
             self._admit_pvc(name, body)
+        elif kind == "horizontalpodautoscalers":
+            spec = body.get("spec") or {}
+            ref = spec.get("scaleTargetRef") or {}
+            if not ref.get("kind") or not ref.get("name") or not spec.get("maxReplicas"):
+                raise HttpError(422, f'HorizontalPodAutoscaler.autoscaling "{name}" is invalid: spec.scaleTargetRef '
+                                     "(kind, name) and spec.maxReplicas are required")
+            if int(spec.get("minReplicas", 1)) > int(spec["maxReplicas"]):
+                raise HttpError(422, "spec.minReplicas must not exceed spec.maxReplicas")
+            body.setdefault("status", {})
+            md["generation"] = 1
         elif kind == "services":
             self._alloc_service(body)
         elif kind in ("configmaps", "secrets"):

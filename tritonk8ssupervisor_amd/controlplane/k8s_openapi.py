@@ -39,6 +39,11 @@ _DESCRIPTIONS = {
     "Deployment": "A replicated, rolling-updated set of pods.",
     "Job": "Pods that run to completion (Indexed jobs get JOB_COMPLETION_INDEX).",
     "Ingress": "HTTP routing from the node's proxy to Services.",
+    "StatefulSet": "Pods with stable names <name>-<ordinal>, their own DNS names and claims.",
+    "ReplicaSet": "A number of identical pods.",
+    "CronJob": "A Job on a schedule.",
+    "PersistentVolumeClaim": "Node-local storage that outlives pods (class tk8s-local).",
+    "HorizontalPodAutoscaler": "Scales a workload by its pods' CPU or memory use.",
 }
 # the top-level fields each kind's objects may have (fieldValidation=Strict rejects others)
 _TOP = {"Pod": ("spec", "status"), "Service": ("spec", "status"), "Node": ("spec", "status"),
@@ -59,6 +64,7 @@ def gv_key(group: str, version: str) -> str:
 
 
 def _gvs() -> list[tuple[str, str]]:
+    """The group versions with objects (metrics.k8s.io has no writable objects: no document)."""
     out: list[tuple[str, str]] = []
     for g, v, *_ in k8s_wire.RESOURCES.values():
         if (g, v) not in out:
@@ -67,7 +73,8 @@ def _gvs() -> list[tuple[str, str]]:
 
 
 def _schema_name(group: str, version: str, kind: str) -> str:
-    pkg = {"": "core", "apps": "apps", "batch": "batch", "networking.k8s.io": "networking"}.get(group, group)
+    pkg = {"": "core", "apps": "apps", "batch": "batch", "networking.k8s.io": "networking",
+           "autoscaling": "autoscaling"}.get(group, group)
     return f"io.k8s.api.{pkg}.{version}.{kind}"
 
 

@@ -39,6 +39,8 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "replicasets": ("apps", "v1", "ReplicaSet", "replicaset", True, ("rs",), ("scale",)),
     "jobs": ("batch", "v1", "Job", "job", True, (), ()),
     "cronjobs": ("batch", "v1", "CronJob", "cronjob", True, ("cj",), ()),
+    "horizontalpodautoscalers": ("autoscaling", "v2", "HorizontalPodAutoscaler", "horizontalpodautoscaler", True,
+                                 ("hpa",), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
 }
 READ_ONLY = {"namespaces": ("create", "delete", "get", "list", "patch", "watch"),
@@ -71,7 +73,7 @@ def _groups() -> list[tuple[str, str]]:
     for g, v, *_ in RESOURCES.values():
         if g and (g, v) not in seen:
             seen.append((g, v))
-    return seen
+    return seen + [("metrics.k8s.io", "v1beta1")]  # served by metrics_api.py, not objects
 
 
 def api_group_list() -> dict:

@@ -15,7 +15,8 @@ TERMINAL = ("Succeeded", "Failed")
 KIND_GROUPS = (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1"), ("configmaps", "/api/v1"),
                ("secrets", "/api/v1"), ("persistentvolumeclaims", "/api/v1"), ("daemonsets", "/apis/apps/v1"), ("deployments", "/apis/apps/v1"),
                ("statefulsets", "/apis/apps/v1"), ("replicasets", "/apis/apps/v1"),
-               ("jobs", "/apis/batch/v1"), ("cronjobs", "/apis/batch/v1"), ("ingresses", "/apis/networking.k8s.io/v1"))
+               ("jobs", "/apis/batch/v1"), ("cronjobs", "/apis/batch/v1"), ("ingresses", "/apis/networking.k8s.io/v1"),
+               ("horizontalpodautoscalers", "/apis/autoscaling/v2"))
 
 
 def _key(*parts: str) -> str:

@@ -52,13 +52,14 @@ from .objects import KIND_GROUPS, _cond, _key, _set_cond
 from .rancher_api import RancherAPI
 from .scheduler import Scheduler
 from .workloads import Workloads
+from .metrics_api import MetricsAPI
 from .store import Store, now_iso
 
 
 _KIND_PLURAL = {r[2]: plural for plural, r in k8s_wire.RESOURCES.items()}
 
 
-class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler):
+class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port
@@ -180,6 +181,12 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler)
                 r.add(method, pre + path, h)
             add("GET", r"/openapi/v3/?", self.h_openapi_root)
             add("GET", r"/openapi/v3/(?P<gv>api/[^/]+|apis/[^/]+/[^/]+)", self.h_openapi_gv)
+            add("GET", r"/apis/metrics.k8s.io/v1beta1/?", self.h_metrics_resources)
+            add("GET", r"/apis/metrics.k8s.io/v1beta1/nodes", self.h_node_metrics)
+            add("GET", r"/apis/metrics.k8s.io/v1beta1/nodes/(?P<name>[^/]+)", self.h_node_metrics)
+            add("GET", r"/apis/metrics.k8s.io/v1beta1/pods", self.h_pod_metrics)
+            add("GET", r"/apis/metrics.k8s.io/v1beta1/namespaces/(?P<ns>[^/]+)/pods", self.h_pod_metrics)
+            add("GET", r"/apis/metrics.k8s.io/v1beta1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)", self.h_pod_metrics)
             add("GET", r"/api/?", self.h_api_versions)
             add("GET", r"/apis/?", self.h_api_groups)
             add("GET", r"/api/v1/?", self.h_api_resources)
@@ -251,6 +258,8 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler)
         return g
 
     async def h_api_resources(self, req: Request, group: str = "", version: str = "v1", pid: str | None = None):
+        if (group, version) == ("metrics.k8s.io", "v1beta1"):
+            return await self.h_metrics_resources(req)
         r = k8s_wire.api_resource_list(group, version)
         if r is None:
             raise HttpError(404, f"the server could not find the requested resource ({group}/{version})")
@@ -336,7 +345,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, Scheduler)
             await self.ingress.ensure(self.advertise or self.host, self.ingress_port, True)
 
         tasks = [asyncio.create_task(self.lease_loop()), asyncio.create_task(self.snapshot_loop()),
-                 asyncio.create_task(self.cron_loop())]
+                 asyncio.create_task(self.cron_loop()), asyncio.create_task(self.hpa_loop())]
         # Mirrors the rancher/server log line the reference waits for (ranchermaster:14-20).
         print(f"Listening on {host}:{port}", flush=True)
         trace("cp", "listening")
