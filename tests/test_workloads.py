@@ -381,3 +381,25 @@ def test_metrics_api_and_hpa(cp):
     with pytest.raises(HttpError):
         cp.create("1a1", "horizontalpodautoscalers", "default", {"metadata": {"name": "bad"}, "spec": {
             "scaleTargetRef": {"kind": "Deployment", "name": "web"}, "minReplicas": 5, "maxReplicas": 2}})
+
+
+def test_hpa_on_gpu_utilisation(cp):
+    """An MI355X-aware HorizontalPodAutoscaler: resource amd.com/gpu, the pods' GPU busy %."""
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "infer"}, "spec": {
+        "replicas": 2, "selector": {"matchLabels": {"app": "infer"}},
+        "template": {"metadata": {"labels": {"app": "infer"}}, "spec": {"containers": [
+            {"name": "c", "command": ["true"], "resources": {"limits": {"amd.com/gpu": "1"}}}]}}}})
+    for n in _pods(cp, "infer-"):
+        cp.store.patch("pods", _key("1a1", "default", n), lambda o: o["status"].update(phase="Running"))
+    cp.create("1a1", "horizontalpodautoscalers", "default", {"metadata": {"name": "infer"}, "spec": {
+        "scaleTargetRef": {"kind": "Deployment", "name": "infer"}, "maxReplicas": 8,
+        "metrics": [{"type": "Resource", "resource": {"name": "amd.com/gpu", "target": {"type": "Utilization",
+                                                                                       "averageUtilization": 60}}}]}})
+    cp._ctl_hpas("1a1", now=10.0)
+    hpa = cp.store.get("horizontalpodautoscalers", _key("1a1", "default", "infer"))
+    assert hpa["status"]["conditions"][-1]["reason"] == "FailedGetResourceMetric"  # no samples yet
+    cp._ingest_metrics("1a1", "kubenode1", {"pods": {f"default/{n}": [{"name": "c", "cpu_cores": 0.1, "memory_bytes": 0,
+                                                                       "gpu_pct": 90.0, "gpus": 1}]
+                                                     for n in _pods(cp, "infer-")}})
+    cp._ctl_hpas("1a1", now=20.0)
+    assert cp.store.get("deployments", _key("1a1", "default", "infer"))["spec"]["replicas"] == 3  # ceil(2 x 90/60)

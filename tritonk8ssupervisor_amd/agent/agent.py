@@ -287,6 +287,14 @@ class Agent:
                 groups[key] = cs
         m = self._sampler.sample(groups)
         m["window"] = f"{self.metrics_period:g}s"
+        # GPU busy % of each pod's GPUs (AMD SMI gfx activity, smi_loop): what a GPU-aware
+        # HorizontalPodAutoscaler scales on (metrics_api.py, resource amd.com/gpu)
+        busy = {d.id: (d.telemetry.get("activity") or {}).get("gfx_pct") for d in self.plugin.devices_}
+        for key, pp in self.runtime.running().items():
+            vals = [busy[i] for i in pp.gpu_ids if busy.get(i) is not None]
+            if vals and key in m["pods"] and m["pods"][key]:
+                m["pods"][key][0]["gpu_pct"] = sum(vals) / len(vals)
+                m["pods"][key][0]["gpus"] = len(pp.gpu_ids)
         return m
 
     # ---- GPU health (AMD SMI) ------------------------------------------------------------

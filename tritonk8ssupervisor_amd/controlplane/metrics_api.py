@@ -9,7 +9,9 @@ the store: metrics are not objects and are not persisted, as with metrics-server
 HPA: every ``HPA_PERIOD`` seconds (15, the controller-manager's default) each autoscaler reads
 its target's pods' usage and requests, and scales the target's ``replicas`` to
 ``ceil(current * utilization / target)`` -- for ``Resource`` metrics ``cpu``/``memory`` with
-``Utilization`` (percent of requests) or ``AverageValue`` targets -- within
+``Utilization`` (percent of requests) or ``AverageValue`` targets, and ``amd.com/gpu`` with a
+``Utilization`` target: the average GFX busy percent of the pods' GPUs (AMD SMI, sampled by the
+node agents) -- within
 [minReplicas, maxReplicas], ignoring changes inside a 10 % tolerance, and keeping the highest
 recommendation of the scale-down stabilization window (``behavior.scaleDown.
 stabilizationWindowSeconds``, default 300). Pods that are not Running or have no sample yet
@@ -97,8 +99,9 @@ class MetricsAPI:
             items.append({"kind": "PodMetrics", "apiVersion": METRICS_GV,
                           "metadata": {"name": pname, "namespace": pns, "labels": pod["metadata"].get("labels", {})},
                           "timestamp": ts, "window": "10s",
-                          "containers": [{"name": c["name"], "usage": {"cpu": quantity.cpu(c.get("cpu_cores", 0)),
-                                                                       "memory": quantity.memory(c.get("memory_bytes", 0))}}
+                          "containers": [{"name": c["name"], "usage": {
+                              "cpu": quantity.cpu(c.get("cpu_cores", 0)), "memory": quantity.memory(c.get("memory_bytes", 0)),
+                              **({"amd.com/gpu-utilization": f"{c['gpu_pct']:.0f}"} if c.get("gpu_pct") is not None else {})}}
                                          for c in cs]})
         if name:
             if not items:
@@ -119,13 +122,14 @@ class MetricsAPI:
             plural = _TARGET_KIND.get(ref.get("kind", ""))
             target = self.store.get(plural, _key(pid, ns, ref.get("name", ""))) if plural else None
             st = dict(hpa.get("status") or {})
-            conds = {"conditions": list(st.get("conditions") or [])}
+            holder = {"status": {"conditions": list(st.get("conditions") or [])}}  # what _set_cond edits
+            conds = holder["status"]
             if target is None:
-                _set_cond(conds, "AbleToScale", "False", "FailedGetScale",
+                _set_cond(holder, "AbleToScale", "False", "FailedGetScale",
                           f"the HPA controller was unable to get the target's current scale: {ref.get('kind')}/{ref.get('name')}")
                 self._hpa_status(pid, ns, name, hpa, {**st, "conditions": conds["conditions"]})
                 continue
-            _set_cond(conds, "AbleToScale", "True", "SucceededGetScale", "the HPA controller was able to get the target's current scale")
+            _set_cond(holder, "AbleToScale", "True", "SucceededGetScale", "the HPA controller was able to get the target's current scale")
             current = int(target["spec"].get("replicas", 1))
             sel = (target["spec"].get("selector") or {}).get("matchLabels") or {}
             pods = [o for o in self.store.list("pods", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns
@@ -139,6 +143,19 @@ class MetricsAPI:
                     continue
                 res = metric["resource"].get("name")
                 tgt = metric["resource"].get("target") or {}
+                if res == "amd.com/gpu":  # GPU busy %, averaged over the pods that report it
+                    vals = [c["gpu_pct"] for o in pods for c in samples.get(f"{ns}/{o['metadata']['name']}", ("", []))[1]
+                            if c.get("gpu_pct") is not None]
+                    if not vals:
+                        why = "no GPU activity samples for the target's pods yet (AMD SMI)"
+                        continue
+                    util = sum(vals) / len(vals)
+                    ratio = util / float(tgt.get("averageUtilization", 80))
+                    current_metrics.append({"type": "Resource", "resource": {"name": res, "current": {
+                        "averageUtilization": int(round(util))}}})
+                    want = current if abs(ratio - 1.0) <= TOLERANCE else math.ceil(len(vals) * ratio)
+                    desired = want if desired is None else max(desired, want)
+                    continue
                 usage, requests, n = 0.0, 0.0, 0
                 for o in pods:
                     key = f"{ns}/{o['metadata']['name']}"
@@ -170,11 +187,11 @@ class MetricsAPI:
                 desired = want if desired is None else max(desired, want)
             lo, hi = int(spec.get("minReplicas", 1)), int(spec.get("maxReplicas", current))
             if desired is None:
-                _set_cond(conds, "ScalingActive", "False", "FailedGetResourceMetric", why)
+                _set_cond(holder, "ScalingActive", "False", "FailedGetResourceMetric", why)
                 self._hpa_status(pid, ns, name, hpa, {**st, "currentReplicas": current, "desiredReplicas": current,
                                                       "conditions": conds["conditions"]})
                 continue
-            _set_cond(conds, "ScalingActive", "True", "ValidMetricFound", "the HPA was able to compute the replica count")
+            _set_cond(holder, "ScalingActive", "True", "ValidMetricFound", "the HPA was able to compute the replica count")
             desired = min(hi, max(lo, desired))
             # scale-down stabilization: the highest recommendation of the window wins
             window = float((((spec.get("behavior") or {}).get("scaleDown") or {}).get("stabilizationWindowSeconds", 300)))
