@@ -817,3 +817,61 @@ def test_multi_gpu_burnin_command_runs_on_one_gpu(tmp_path):
     assert res["ok"] and res["device_count"] == 1 and res["md5"]["digest"] == res["md5_expected"], res
     rep = xgmi.link_report(res, [0])
     assert rep["pulls"] == 0 and not rep["degraded"]
+
+
+def test_gpu_busy_metric_and_hpa_on_a_real_gpu(tmp_path):
+    """A pod keeping its MI355X busy shows up in the metrics API as amd.com/gpu-utilization (AMD SMI
+    gfx activity, sampled by the node agent), and an HPA on resource amd.com/gpu scales its
+    Deployment up from it."""
+    import subprocess
+    import sys as _sys
+    import time
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tritonk8ssupervisor_amd.controlplane.client import client_from_kubeconfig
+
+    env = _real_ws(tmp_path)
+    env.update(TK8S_SMI_INTERVAL="1", TK8S_SMI_DELAY="0.5", TK8S_METRICS_PERIOD="1", TK8S_HPA_PERIOD="2")
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=60)
+    busy = ("import time, torch\n"
+            "a = torch.randn(8192, 8192, device='cuda', dtype=torch.bfloat16)\n"
+            "print('busy', flush=True)\n"
+            "t = time.time()\n"
+            "while time.time() - t < 40:\n"
+            "    for _ in range(20):\n"
+            "        a = (a @ a) * 1e-4\n"
+            "    torch.cuda.synchronize()\n")
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120"],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        (tmp_path / "busy.json").write_text(json.dumps({"apiVersion": "v1", "kind": "List", "items": [
+            {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "busy"},
+             "spec": {"replicas": 1, "selector": {"matchLabels": {"app": "busy"}},
+                      "template": {"metadata": {"labels": {"app": "busy"}}, "spec": {"containers": [{
+                          "name": "c", "command": [_sys.executable, "-c", busy],
+                          "resources": {"limits": {"amd.com/gpu": 1}}}]}}}},
+            {"apiVersion": "autoscaling/v2", "kind": "HorizontalPodAutoscaler", "metadata": {"name": "busy"},
+             "spec": {"scaleTargetRef": {"apiVersion": "apps/v1", "kind": "Deployment", "name": "busy"},
+                      "minReplicas": 1, "maxReplicas": 2,
+                      "metrics": [{"type": "Resource", "resource": {"name": "amd.com/gpu", "target": {
+                          "type": "Utilization", "averageUtilization": 20}}}]}}]}))
+        assert kc("apply", "-f", "busy.json").returncode == 0
+        k = client_from_kubeconfig(json.loads((tmp_path / ".tk8s" / "kubeconfig.json").read_text()))
+        deadline = time.monotonic() + 100
+        seen, replicas = 0.0, 1
+        while time.monotonic() < deadline:
+            for m in k.get(k.k8s("/apis/metrics.k8s.io/v1beta1/namespaces/default/pods"))["items"]:
+                for c in m["containers"]:
+                    seen = max(seen, float(c["usage"].get("amd.com/gpu-utilization", 0)))
+            replicas = json.loads(kc("get", "deploy", "busy", "-o", "json").stdout)["spec"]["replicas"]
+            if seen >= 20 and replicas == 2:
+                break
+            time.sleep(1)
+        hpa = json.loads(kc("get", "hpa", "busy", "-o", "json").stdout)
+        assert seen >= 20, (seen, hpa.get("status"), kc("logs", json.loads(kc("get", "pods", "-o", "json").stdout)[
+            "items"][-1]["metadata"]["name"]).stdout[-500:])
+        assert replicas == 2, hpa.get("status")
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)

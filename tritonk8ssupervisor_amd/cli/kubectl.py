@@ -135,6 +135,21 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
         rows = [["NAME", "TYPE", "CLUSTER-IP", "EXTERNAL-IP", "PORT(S)", "AGE"]] + [[
             o["metadata"]["name"], o["spec"].get("type", "ClusterIP"), o["spec"].get("clusterIP", ""), ext(o), ports(o), _age(o)]
             for o in items]
+    elif k == "horizontalpodautoscaler":
+        def targets(o):
+            out = []
+            for m in o.get("status", {}).get("currentMetrics") or []:
+                r = m.get("resource") or {}
+                cur = (r.get("current") or {}).get("averageUtilization")
+                want = next((((x.get("resource") or {}).get("target") or {}).get("averageUtilization")
+                            for x in o["spec"].get("metrics") or [] if (x.get("resource") or {}).get("name") == r.get("name")), None)
+                out.append(f"{r.get('name')}: {cur}%/{want}%")
+            return ", ".join(out) or "<unknown>"
+
+        rows = [["NAME", "REFERENCE", "TARGETS", "MINPODS", "MAXPODS", "REPLICAS", "AGE"]] + [[
+            o["metadata"]["name"], f"{o['spec']['scaleTargetRef'].get('kind')}/{o['spec']['scaleTargetRef'].get('name')}",
+            targets(o), str(o["spec"].get("minReplicas", 1)), str(o["spec"].get("maxReplicas")),
+            str(o.get("status", {}).get("currentReplicas", 0)), _age(o)] for o in items]
     elif k == "namespace":
         rows = [["NAME", "STATUS", "AGE"]] + [[o["metadata"]["name"], o.get("status", {}).get("phase", "Active"), _age(o)]
                                              for o in items]

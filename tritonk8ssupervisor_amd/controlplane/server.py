@@ -84,6 +84,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         self.ingress = IngressController(self._ingress_routes, self._endpoints, log=lambda m: self._log_error(m + "\n"))
         self.dns_port = host_port(53) if dns_port is None else dns_port          # 0 disables
         self.ingress_port = host_port(80) if ingress_port is None else ingress_port
+        self.hpa_period = float(os.environ.get("TK8S_HPA_PERIOD", "15"))  # the HPA controller's sync period
         self._routes()
 
     # ---- utilities --------------------------------------------------------------------

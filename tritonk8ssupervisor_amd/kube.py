@@ -23,6 +23,7 @@ KINDS = {
     "statefulset": ("StatefulSet", "/apis/apps/v1", "statefulsets"),
     "replicaset": ("ReplicaSet", "/apis/apps/v1", "replicasets"),
     "cronjob": ("CronJob", "/apis/batch/v1", "cronjobs"),
+    "horizontalpodautoscaler": ("HorizontalPodAutoscaler", "/apis/autoscaling/v2", "horizontalpodautoscalers"),
     "configmap": ("ConfigMap", "/api/v1", "configmaps"),
     "secret": ("Secret", "/api/v1", "secrets"),
     "persistentvolumeclaim": ("PersistentVolumeClaim", "/api/v1", "persistentvolumeclaims"),
@@ -34,7 +35,8 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "configmaps": "configmap", "secrets": "secret", "ing": "ingress", "ingresses": "ingress",
            "sts": "statefulset", "statefulsets": "statefulset", "rs": "replicaset", "replicasets": "replicaset",
            "cj": "cronjob", "cronjobs": "cronjob", "pvc": "persistentvolumeclaim",
-           "persistentvolumeclaims": "persistentvolumeclaim", "ns": "namespace", "namespaces": "namespace"}
+           "persistentvolumeclaims": "persistentvolumeclaim", "ns": "namespace", "namespaces": "namespace",
+           "hpa": "horizontalpodautoscaler", "horizontalpodautoscalers": "horizontalpodautoscaler"}
 
 
 def kind_key(kind: str) -> str:
