@@ -434,3 +434,22 @@ def test_kubectl_top_pods_from_the_metrics_api(cluster):
 
     assert _until(lambda: cpu_m() > 300, 30)  # a busy loop uses most of a core
     kc("delete", "pod", "burn")
+
+
+def test_rollout_history_and_undo_on_a_real_cluster(cluster):
+    ws, env, kc, summary = cluster
+    kc("create", "deployment", "hist", "--image", "nginx", "--replicas", "1")
+    kc("rollout", "status", "deploy/hist", "--timeout", "60s")
+    d = json.loads(kc("get", "deploy", "hist", "-o", "json").stdout)
+    first = json.loads(json.dumps(d["spec"]["template"]))
+    d["spec"]["template"]["metadata"].setdefault("annotations", {})["v"] = "2"
+    (ws / "hist.json").write_text(json.dumps({k: v for k, v in d.items() if k != "status"}))
+    kc("apply", "-f", "hist.json")
+    kc("rollout", "status", "deploy/hist", "--timeout", "60s")
+    hist = kc("rollout", "history", "deploy/hist").stdout
+    assert "REVISION" in hist and "\n1 " in hist and "\n2 " in hist, hist
+    assert len(json.loads(kc("get", "rs", "-o", "json").stdout)["items"]) >= 2
+    kc("rollout", "undo", "deploy/hist")
+    kc("rollout", "status", "deploy/hist", "--timeout", "60s")
+    back = json.loads(kc("get", "deploy", "hist", "-o", "json").stdout)
+    assert back["spec"]["template"] == first and back["metadata"]["annotations"]["deployment.kubernetes.io/revision"] == "3"

@@ -403,3 +403,46 @@ def test_hpa_on_gpu_utilisation(cp):
                                                      for n in _pods(cp, "infer-")}})
     cp._ctl_hpas("1a1", now=20.0)
     assert cp.store.get("deployments", _key("1a1", "default", "infer"))["spec"]["replicas"] == 3  # ceil(2 x 90/60)
+
+
+def test_deployment_revisions_as_replicasets(cp):
+    """Every template a Deployment has had is a ReplicaSet <name>-<hash> with a revision; going
+    back to an old template makes it the newest revision; deleting the Deployment removes them."""
+    tmpl = {"metadata": {"labels": {"app": "web"}}, "spec": {"containers": [{"name": "c", "command": ["sleep", "1"]}]}}
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "web"}, "spec": {
+        "replicas": 2, "selector": {"matchLabels": {"app": "web"}}, "template": json.loads(json.dumps(tmpl))}})
+
+    def rss():
+        return {o["metadata"]["name"]: o for o in cp.store.list("replicasets")}
+
+    def rev(o):
+        return int(o["metadata"]["annotations"]["deployment.kubernetes.io/revision"])
+
+    first = rss()
+    assert len(first) == 1
+    (n1, rs1), = first.items()
+    assert rev(rs1) == 1 and rs1["status"]["replicas"] == 2 and rs1["metadata"]["ownerReferences"][0]["kind"] == "Deployment"
+    assert cp.store.get("deployments", _key("1a1", "default", "web"))["metadata"]["annotations"][
+        "deployment.kubernetes.io/revision"] == "1"
+    assert len(_pods(cp, "web-")) == 2  # the ReplicaSet controller does not run a Deployment's pods again
+
+    def set_cmd(cmd):
+        body = json.loads(json.dumps(cp._strip(cp.store.get("deployments", _key("1a1", "default", "web")))))
+        body["spec"]["template"]["spec"]["containers"][0]["command"] = cmd
+        cp.replace("1a1", "deployments", "default", "web", body)
+        for n in _pods(cp, "web-"):
+            cp.store.patch("pods", _key("1a1", "default", n), lambda o: o["status"].update(phase="Running"))
+        cp.reconcile()
+
+    set_cmd(["sleep", "2"])
+    assert len(rss()) == 2 and max(rev(o) for o in rss().values()) == 2
+    set_cmd(["sleep", "1"])  # back to the first template: its ReplicaSet is revision 3 now
+    assert rev(rss()[n1]) == 3 and len(rss()) == 2
+    import asyncio
+
+    from tritonk8ssupervisor_amd.controlplane.httpserver import Request
+
+    cp._auth = lambda req, proj: None
+    cp._pid = lambda pid, req: "1a1"
+    asyncio.run(cp._deleter("deployments")(Request("DELETE", "/x", {}, {}, b""), ns="default", name="web"))
+    assert rss() == {} and _pods(cp, "web-") == []

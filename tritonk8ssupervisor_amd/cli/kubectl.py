@@ -185,6 +185,33 @@ def _target(args: list[str]) -> tuple[str, str]:
     return args[0], args[1]
 
 
+def _rollout_history(k, name: str, ns: str, sub: str, to_revision: int = 0) -> int:
+    """``rollout history`` lists the Deployment's revisions (its ReplicaSets); ``rollout undo``
+    puts the template of the previous revision (or ``--to-revision``) back, as kubectl does."""
+    d = k.get(k.k8s(object_path("deployment", name, ns)))
+    uid = d["metadata"]["uid"]
+    rss = [rs for rs in k.get(k.k8s(collection_path("replicaset", ns)))["items"]
+           if any(r.get("uid") == uid for r in rs["metadata"].get("ownerReferences", []))]
+    revs = sorted(((int(rs["metadata"].get("annotations", {}).get("deployment.kubernetes.io/revision", 0)), rs)
+                   for rs in rss), key=lambda x: x[0])
+    if sub == "history":
+        print(f"deployment.apps/{name}\nREVISION  CHANGE-CAUSE")
+        for rev, rs in revs:
+            print(f"{rev:<9} {rs['metadata'].get('annotations', {}).get('kubernetes.io/change-cause', '<none>')}")
+        return 0
+    if len(revs) < 2 and not to_revision:
+        raise SystemExit(f"error: no rollout history found for deployment {name!r}")
+    target = next((rs for rev, rs in revs if rev == to_revision), None) if to_revision else revs[-2][1]
+    if target is None:
+        raise SystemExit(f"error: unable to find specified revision {to_revision} in history")
+    tmpl = target["spec"]["template"]
+    tmpl.get("metadata", {}).get("labels", {}).pop("pod-template-hash", None)
+    k.put(k.k8s(object_path("deployment", name, ns)), {**{x: v for x, v in d.items() if x != "status"},
+                                                     "spec": {**d["spec"], "template": tmpl}})
+    print(f"deployment.apps/{name} rolled back")
+    return 0
+
+
 def _create_deployment(k, a, ns: str) -> int:
     """kubectl create deployment NAME --image IMAGE [--replicas N] [--port P]: labels app=NAME."""
     if len(a.args) < 2 or not a.image:
@@ -350,6 +377,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--show-managed-fields", action="store_true")
     ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("-c", "--container")
+    ap.add_argument("--to-revision", type=int, default=0)
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -470,8 +498,10 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
         elif a.verb == "rollout":
             sub = a.args[0] if a.args else ""
             what, name = _target(a.args[1:])
-            if kind_key(what) != "deployment" or sub not in ("status", "restart"):
-                raise SystemExit("usage: kubectl rollout status|restart deploy/NAME")
+            if kind_key(what) != "deployment" or sub not in ("status", "restart", "history", "undo"):
+                raise SystemExit("usage: kubectl rollout status|restart|history|undo deploy/NAME")
+            if sub in ("history", "undo"):
+                return _rollout_history(k, name, ns, sub, a.to_revision)
             if sub == "restart":  # a new template annotation = a new pod-template-hash = a rolling update
                 k.request("PATCH", k.k8s(object_path("deployment", name, ns)), body={"spec": {"template": {"metadata": {
                     "annotations": {"kubectl.kubernetes.io/restartedAt": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}}}}})

@@ -7,6 +7,8 @@ from __future__ import annotations
 import copy
 
 from .store import now_iso
+
+REVISION = "deployment.kubernetes.io/revision"
 from .objects import (
     VALIDATION_LABEL, TERMINAL, _key, _cond, _set_cond, _set_ready, _xgmi_view, template_hash, labels_match,
 )
@@ -222,6 +224,7 @@ class Controllers:
                 for o in sorted(new, key=lambda o: o["metadata"]["name"])[want:]:
                     self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
             pods = live()
+            self._sync_deployment_revisions(pid, d, h, pods)
             running = sum(1 for o in pods if o.get("status", {}).get("phase") == "Running")
             status = {"observedGeneration": int(d["metadata"].get("generation", 1)), "replicas": len(pods),
                       "updatedReplicas": sum(1 for o in pods if o["metadata"].get("labels", {}).get("pod-template-hash") == h),
@@ -230,3 +233,60 @@ class Controllers:
             if d.get("status") != status:
                 self.store.patch("deployments", _key(pid, ns, dname), lambda o, s=status: o.__setitem__("status", s))
 
+    def _sync_deployment_revisions(self, pid: str, d: dict, h: str, pods: list[dict]) -> None:
+        """A ReplicaSet per pod template the Deployment has had (``<name>-<pod-template-hash>``,
+        annotation ``deployment.kubernetes.io/revision``), as Kubernetes keeps them: what
+        ``kubectl get rs``, ``kubectl rollout history`` and ``kubectl rollout undo`` read. The pods
+        stay the Deployment's own (this controller runs them); the ReplicaSets are its revision
+        history, with replicas counted from the pods of their template, and only the newest
+        ``revisionHistoryLimit`` (10) empty old ones are kept. Returning to an old template makes
+        its ReplicaSet the newest revision again."""
+        ns, dname, uid = d["metadata"]["namespace"], d["metadata"]["name"], d["metadata"]["uid"]
+        match = (d["spec"].get("selector") or {}).get("matchLabels") or {}
+        owned = {rs["metadata"].get("labels", {}).get("pod-template-hash"): rs for rs in self.store.list(
+            "replicasets", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns and any(
+                r.get("uid") == uid for r in o["metadata"].get("ownerReferences", [])))}
+        revs = {k: int(rs["metadata"].get("annotations", {}).get(REVISION, "0") or 0) for k, rs in owned.items()}
+        counts: dict[str, int] = {}
+        ready: dict[str, int] = {}
+        for o in pods:
+            ph = o["metadata"].get("labels", {}).get("pod-template-hash")
+            counts[ph] = counts.get(ph, 0) + 1
+            ready[ph] = ready.get(ph, 0) + (o.get("status", {}).get("phase") == "Running")
+        top = max(revs.values(), default=0)
+        want = int(d["spec"].get("replicas", 1))
+        if h not in owned or revs[h] < top:  # a new template, or back to an old one: the newest revision
+            revs[h] = top + 1 if (h not in owned or revs[h] < top) else revs[h]
+        for ph in set(owned) | {h}:
+            rs = owned.get(ph)
+            n = counts.get(ph, 0)
+            tmpl = copy.deepcopy(d["spec"]["template"]) if ph == h else (rs or {}).get("spec", {}).get("template")
+            if tmpl is None:
+                continue
+            tmpl.setdefault("metadata", {}).setdefault("labels", {})["pod-template-hash"] = ph
+            ann = {REVISION: str(revs[ph])}
+            if ph == h:
+                ann["deployment.kubernetes.io/desired-replicas"] = str(want)
+            body = {"apiVersion": "apps/v1", "kind": "ReplicaSet",
+                    "metadata": {"name": f"{dname}-{ph}", "namespace": ns, "labels": {**match, "pod-template-hash": ph},
+                                 "annotations": {**((rs or {}).get("metadata", {}).get("annotations") or {}), **ann},
+                                 "ownerReferences": [{"apiVersion": "apps/v1", "kind": "Deployment", "name": dname,
+                                                      "uid": uid, "controller": True, "blockOwnerDeletion": True}]},
+                    "spec": {"replicas": want if ph == h else n, "selector": {"matchLabels": {**match, "pod-template-hash": ph}},
+                             "template": tmpl},
+                    "status": {"replicas": n, "readyReplicas": ready.get(ph, 0), "availableReplicas": ready.get(ph, 0),
+                               "fullyLabeledReplicas": n, "observedGeneration": 1}, "_project": pid}
+            if rs is not None:
+                body["metadata"]["uid"] = rs["metadata"]["uid"]
+                body["metadata"]["creationTimestamp"] = rs["metadata"].get("creationTimestamp")
+                if all(self._strip(rs).get(k) == body.get(k) for k in ("spec", "status")) and \
+                        rs["metadata"].get("annotations") == body["metadata"]["annotations"]:
+                    continue
+            self.store.put("replicasets", _key(pid, ns, f"{dname}-{ph}"), body)
+        limit = int(d["spec"].get("revisionHistoryLimit", 10))
+        old = sorted((revs[ph], ph) for ph in owned if ph != h and not counts.get(ph))
+        for _rev, ph in old[: max(0, len(old) - limit)]:
+            self.store.delete("replicasets", _key(pid, ns, f"{dname}-{ph}"))
+        if d["metadata"].get("annotations", {}).get(REVISION) != str(revs[h]):
+            self.store.patch("deployments", _key(pid, ns, dname),
+                             lambda o, r=str(revs[h]): o["metadata"].setdefault("annotations", {}).__setitem__(REVISION, r))

@@ -435,10 +435,11 @@ class KubernetesAPI:
                 raise HttpError(404, f'{kind} "{name}" not found')
             if kind in ("services", "ingresses"):
                 self._sync_proxy()
-            if kind != "pods":
-                for pod in self.store.list("pods", lambda x: self._in(p, x) and any(
-                        r.get("uid") == o["metadata"]["uid"] for r in x["metadata"].get("ownerReferences", []))):
-                    self.store.delete("pods", _key(p, ns, pod["metadata"]["name"]))
+            if kind != "pods":  # garbage collection: what the object owned goes with it
+                for dep_kind in ("pods", "replicasets", "jobs"):
+                    for dep in self.store.list(dep_kind, lambda x: self._in(p, x) and any(
+                            r.get("uid") == o["metadata"]["uid"] for r in x["metadata"].get("ownerReferences", []))):
+                        self.store.delete(dep_kind, _key(p, ns, dep["metadata"]["name"]))
             self.reconcile()
             return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
         return h

@@ -140,7 +140,9 @@ class Workloads:
 
     # ---- ReplicaSets ----------------------------------------------------------------------
     def _ctl_replicasets(self, pid: str) -> None:
-        for rs in self.store.list("replicasets", lambda o: self._in(pid, o)):
+        for rs in self.store.list("replicasets", lambda o: self._in(pid, o) and not any(
+                r.get("kind") == "Deployment" for r in o["metadata"].get("ownerReferences", []))):
+            # (a Deployment's ReplicaSets are its revision history: controllers.py runs those pods)
             ns, name = rs["metadata"]["namespace"], rs["metadata"]["name"]
             spec = rs["spec"]
             want = int(spec.get("replicas", 1))
