@@ -453,3 +453,34 @@ def test_rollout_history_and_undo_on_a_real_cluster(cluster):
     kc("rollout", "status", "deploy/hist", "--timeout", "60s")
     back = json.loads(kc("get", "deploy", "hist", "-o", "json").stdout)
     assert back["spec"]["template"] == first and back["metadata"]["annotations"]["deployment.kubernetes.io/revision"] == "3"
+
+
+def test_pods_call_the_api_with_their_service_account(cluster):
+    """A pod's ServiceAccount token is mounted (process pods: TK8S_SERVICEACCOUNT_TOKEN_FILE) and
+    the API authorizes it by RBAC: listing pods fails until a RoleBinding grants view."""
+    ws, env, kc, summary = cluster
+    script = ("import json, os, urllib.request, urllib.error\n"
+              "tok = open(os.environ['TK8S_SERVICEACCOUNT_TOKEN_FILE']).read()\n"
+              "for path in ('/api/v1/namespaces/default/pods', '/api/v1/namespaces/default/secrets'):\n"
+              "    req = urllib.request.Request(os.environ['TK8S_K8S_API'] + path, headers={'Authorization': 'Bearer ' + tok})\n"
+              "    try:\n"
+              "        print(path.rsplit('/', 1)[1], urllib.request.urlopen(req, timeout=5).status)\n"
+              "    except urllib.error.HTTPError as e:\n"
+              "        print(path.rsplit('/', 1)[1], e.code)\n")
+
+    def run(name):
+        (ws / f"{name}.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name},
+            "spec": {"restartPolicy": "Never", "serviceAccountName": "reader",
+                     "containers": [{"name": "c", "image": "python", "command": [sys.executable, "-c", script]}]}}))
+        kc("apply", "-f", f"{name}.json")
+        _until(lambda: json.loads(kc("get", "pod", name, "-o", "json").stdout)["status"].get("phase") == "Succeeded", 30)
+        return kc("logs", name).stdout.split()
+
+    (ws / "sa.json").write_text(json.dumps({"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "reader"}}))
+    kc("apply", "-f", "sa.json")
+    assert run("before") == ["pods", "403", "secrets", "403"]
+    (ws / "rb.json").write_text(json.dumps({"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "RoleBinding",
+        "metadata": {"name": "reader-view"}, "roleRef": {"kind": "ClusterRole", "name": "view"},
+        "subjects": [{"kind": "ServiceAccount", "name": "reader", "namespace": "default"}]}))
+    kc("apply", "-f", "rb.json")
+    assert run("after") == ["pods", "200", "secrets", "403"]

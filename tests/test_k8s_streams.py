@@ -151,14 +151,20 @@ def test_attach_streams_new_output_until_the_pod_ends(cluster, tmp_path):
     p = subprocess.Popen([sys.executable, "-m", "tritonk8ssupervisor_amd.cli.kubectl", "--kubeconfig",
                           str(tmp / "kubeconfig.json"), "attach", "srv"],
                          cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    time.sleep(1.0)
-    with log.open("a") as f:
-        f.write("new line\n")
-    time.sleep(0.5)
+    got: list[str] = []
+    reader = threading.Thread(target=lambda: got.extend(iter(p.stdout.readline, "")), daemon=True)
+    reader.start()
+    deadline = time.monotonic() + 30
+    n = 0
+    while not got and time.monotonic() < deadline:  # until the attach is streaming (it may start slowly)
+        n += 1
+        with log.open("a") as f:
+            f.write(f"new line {n}\n")
+        time.sleep(0.3)
     _set(nc, "Succeeded")
-    out, err = p.communicate(timeout=20)
-    assert p.returncode == 0, err
-    assert out == "new line\n"
+    assert p.wait(20) == 0, p.stderr.read()
+    reader.join(5)
+    assert got and all(line.startswith("new line") for line in got), got  # never what was there before
 
 
 def test_pod_conditions_and_log_follow(cluster, tmp_path):

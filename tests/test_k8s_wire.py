@@ -50,7 +50,8 @@ def test_discovery_documents(kube):
     _, _, groups = _raw(kube, "GET", "/apis")
     names = {g["name"]: g["preferredVersion"]["groupVersion"] for g in groups["groups"]}
     assert names == {"apps": "apps/v1", "batch": "batch/v1", "networking.k8s.io": "networking.k8s.io/v1",
-                     "autoscaling": "autoscaling/v2", "metrics.k8s.io": "metrics.k8s.io/v1beta1"}
+                     "autoscaling": "autoscaling/v2", "metrics.k8s.io": "metrics.k8s.io/v1beta1",
+                     "rbac.authorization.k8s.io": "rbac.authorization.k8s.io/v1"}
     _, _, core = _raw(kube, "GET", "/api/v1")
     res = {r["name"]: r for r in core["resources"]}
     assert core["kind"] == "APIResourceList" and core["groupVersion"] == "v1"
@@ -325,3 +326,59 @@ def test_namespaces_create_get_label_and_cascade_delete(kube):
     assert _raw(kube, "GET", "/api/v1/namespaces/team-a/configmaps/c")[0] == 404  # its objects went with it
     assert _raw(kube, "GET", "/api/v1/namespaces/team-a")[0] == 404
     assert _raw(kube, "DELETE", "/api/v1/namespaces/default")[0] == 403
+
+
+def test_service_accounts_and_rbac(kube):
+    import base64
+
+    def as_(tok, method, path, body=None):
+        conn = http.client.HTTPConnection(kube.host, kube.port, timeout=10)
+        headers = {"Content-Type": "application/json", **({"Authorization": f"Bearer {tok}"} if tok else {})}
+        conn.request(method, kube.k8s(path), body=json.dumps(body).encode() if body is not None else None, headers=headers)
+        r = conn.getresponse()
+        out = r.status, r.read()
+        conn.close()
+        return out[0], json.loads(out[1]) if out[1] else None
+
+    assert _raw(kube, "POST", "/api/v1/namespaces/default/serviceaccounts", {"metadata": {"name": "bot"}})[0] == 201
+    sa = _raw(kube, "GET", "/api/v1/namespaces/default/serviceaccounts/bot")[2]
+    assert sa["secrets"] == [{"name": "bot-token"}]
+    assert _raw(kube, "GET", "/api/v1/namespaces/default/serviceaccounts/default")[0] == 200  # every namespace has one
+    sec = _raw(kube, "GET", "/api/v1/namespaces/default/secrets/bot-token")[2]
+    assert sec["type"] == "kubernetes.io/service-account-token"
+    tok = base64.b64decode(sec["data"]["token"]).decode()
+    st, body = as_(tok, "GET", "/api/v1/namespaces/default/pods")
+    assert st == 403 and 'User "system:serviceaccount:default:bot" cannot list resource "pods"' in body["message"]
+    assert as_(tok, "GET", "/apis/apps/v1")[0] == 200  # discovery is open
+    # view in its namespace: read workloads, not secrets, no writes
+    assert _raw(kube, "POST", "/apis/rbac.authorization.k8s.io/v1/namespaces/default/rolebindings", {
+        "metadata": {"name": "bot-view"}, "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
+                                                     "name": "view"},
+        "subjects": [{"kind": "ServiceAccount", "name": "bot", "namespace": "default"}]})[0] == 201
+    assert as_(tok, "GET", "/api/v1/namespaces/default/pods")[0] == 200
+    assert as_(tok, "GET", "/api/v1/namespaces/kube-system/pods")[0] == 403  # a RoleBinding is namespaced
+    assert as_(tok, "GET", "/api/v1/namespaces/default/secrets")[0] == 403
+    cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "bot-cm"}, "data": {}}
+    assert as_(tok, "POST", "/api/v1/namespaces/default/configmaps", cm)[0] == 403
+    # a Role with a resourceName, then edit cluster-wide
+    assert _raw(kube, "POST", "/apis/rbac.authorization.k8s.io/v1/namespaces/default/roles", {
+        "metadata": {"name": "one-secret"}, "rules": [{"apiGroups": [""], "resources": ["secrets"], "verbs": ["get"],
+                                                      "resourceNames": ["bot-token"]}]})[0] == 201
+    assert _raw(kube, "POST", "/apis/rbac.authorization.k8s.io/v1/namespaces/default/rolebindings", {
+        "metadata": {"name": "bot-secret"}, "roleRef": {"kind": "Role", "name": "one-secret"},
+        "subjects": [{"kind": "ServiceAccount", "name": "bot", "namespace": "default"}]})[0] == 201
+    assert as_(tok, "GET", "/api/v1/namespaces/default/secrets/bot-token")[0] == 200
+    assert as_(tok, "GET", "/api/v1/namespaces/default/secrets/default-token")[0] == 403
+    st, _ = _raw(kube, "POST", "/apis/rbac.authorization.k8s.io/v1/clusterrolebindings", {
+        "metadata": {"name": "bot-edit"}, "roleRef": {"kind": "ClusterRole", "name": "edit"},
+        "subjects": [{"kind": "ServiceAccount", "name": "bot", "namespace": "default"}]})[:2]
+    assert st == 201
+    assert as_(tok, "POST", "/api/v1/namespaces/default/configmaps", cm)[0] == 201
+    assert as_(tok, "GET", "/api/v1/namespaces/kube-system/pods")[0] == 200
+    assert as_(tok, "POST", "/apis/rbac.authorization.k8s.io/v1/clusterrolebindings", {"metadata": {"name": "x"}})[0] == 403
+    names = [o["metadata"]["name"] for o in _raw(kube, "GET", "/apis/rbac.authorization.k8s.io/v1/clusterroles")[2]["items"]]
+    assert {"cluster-admin", "admin", "edit", "view"} <= set(names)
+    # anonymous: reads but Secrets, no writes
+    assert as_(None, "GET", "/api/v1/namespaces/default/pods")[0] == 200
+    assert as_(None, "GET", "/api/v1/namespaces/default/secrets")[0] == 401
+    assert as_(None, "POST", "/api/v1/namespaces/default/configmaps", cm)[0] == 401

@@ -100,6 +100,9 @@ def pod_gpus(p: dict) -> int:
     return total
 
 
+SA_PATH = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
 class _PodFail(Exception):
     """A container of the pod cannot run: the pod fails with this reason."""
 
@@ -373,7 +376,11 @@ class Agent:
         apps = list(spec["containers"])
         try:  # config first: a pod waiting for a ConfigMap must not hold GPUs
             vol_dirs = volume_dirs(pod, pp_dir, self.sandbox, self._fetch_object, pod_ip, self.ip)
-            cfg = {id(x): (self._container_env(pod, x, base, pod_ip), volume_mounts(x, vol_dirs)) for x in inits + apps}
+            sa_dir = self._service_account_dir(pod, pp_dir)
+            sa_mount = [(str(sa_dir), SA_PATH, True)] if sa_dir is not None else []
+            cfg = {id(x): (self._container_env(pod, x, base, pod_ip), volume_mounts(x, vol_dirs) + [
+                m for m in sa_mount if not any(v.get("mountPath") == SA_PATH for v in x.get("volumeMounts") or [])])
+                for x in inits + apps}
         except (ConfigError, VolumeError) as e:
             if key not in self._config_wait:
                 self._report(key, md["name"], md["namespace"], "Pending",
@@ -426,6 +433,8 @@ class Agent:
             env.update(pod_gpu_env(alloc["env"], ordinals, visibility))
         env.update(base)
         env.update({volume_env_name(n): str(d) for n, (d, _ro) in vol_dirs.items()})
+        if sa_dir is not None:  # process pods: the token where a client can find it (image pods: SA_PATH)
+            env.update(TK8S_SERVICEACCOUNT_DIR=str(sa_dir), TK8S_SERVICEACCOUNT_TOKEN_FILE=str(sa_dir / "token"))
         env.update({"TK8S_GPU_IDS": ",".join(ids + [f"{d['node']}/{d['id']}" for d in others]),
                     "TK8S_GPU_COUNT": str(len(ordinals))})
         # GPU pods stay in the host PID namespace: HIP/RCCL inter-process sharing (dmabuf handles
@@ -546,6 +555,26 @@ class Agent:
                 v = _expand(str(e.get("value", "")), merged)
             out[e["name"]] = merged[e["name"]] = v
         return out
+
+    def _service_account_dir(self, pod: dict, pp_dir: Path) -> Path | None:
+        """The pod's ServiceAccount token, namespace and CA files (kubelet's projected token
+        volume), unless ``automountServiceAccountToken: false``."""
+        spec, ns = pod["spec"], pod["metadata"]["namespace"]
+        if spec.get("automountServiceAccountToken") is False:
+            return None
+        sa = spec.get("serviceAccountName") or spec.get("serviceAccount") or "default"
+        s = self._fetch_object("secrets", ns, f"{sa}-token")
+        if s is None:
+            return None
+        import base64
+
+        d = pp_dir / "serviceaccount"
+        d.mkdir(parents=True, exist_ok=True)
+        for name, data in (("token", base64.b64decode((s.get("data") or {}).get("token", ""))), ("namespace", ns.encode()),
+                           ("ca.crt", b"")):
+            (d / name).write_bytes(data)
+            os.chmod(d / name, 0o600 if name == "token" else 0o644)
+        return d
 
     def _fetch_object(self, kind: str, ns: str, name: str) -> dict | None:
         """A namespaced object the pod's volumes need (None: it does not exist)."""

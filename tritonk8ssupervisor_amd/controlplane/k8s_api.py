@@ -28,6 +28,69 @@ class KubernetesAPI:
     def _pid(self, pid: str | None, req: Request) -> str:
         return self.project(pid or req.q("project")).get("id")
 
+    # ---- authentication / authorization (rbac.py) ------------------------------------------
+    def _identity(self, p: str | None, tok: str | None) -> str | None:
+        """``admin`` (the project's API token), ``node:<name>``, ``sa:<ns>:<name>``, or None."""
+        if not tok:
+            return None
+        try:
+            if tok == self.project(p).get("apiToken"):
+                return "admin"
+        except HttpError:
+            pass
+        for n in self.store.list("nodesecrets"):
+            if n.get("nodeToken") == tok:
+                return f"node:{n['metadata']['name']}"
+        if getattr(self, "_sa_tokens_rv", None) != self.store.rv:  # token -> ServiceAccount, rebuilt on change
+            import base64
+
+            self._sa_tokens = {}
+            for s in self.store.list("secrets", lambda o: o.get("type") == "kubernetes.io/service-account-token"):
+                t = (s.get("data") or {}).get("token")
+                sa = (s["metadata"].get("annotations") or {}).get("kubernetes.io/service-account.name")
+                if t and sa:
+                    self._sa_tokens[base64.b64decode(t).decode()] = (s["_project"], s["metadata"]["namespace"], sa)
+            self._sa_tokens_rv = self.store.rv
+        hit = self._sa_tokens.get(tok)
+        if hit and (p is None or hit[0] == p):
+            return f"sa:{hit[1]}:{hit[2]}"
+        return None
+
+    def _authorize(self, req: Request, pid: str | None) -> None:
+        """RBAC for ServiceAccounts; the admin and nodes as before; anonymous reads but Secrets."""
+        from . import rbac
+
+        try:
+            p = self.project(pid or req.q("project")).get("id")
+        except HttpError:
+            p = None
+        ident = self._identity(p, req.bearer)
+        req.identity = ident
+        info = rbac.request_info(req.method, req.path, req.query)
+        if info is None or ident == "admin" or (ident or "").startswith("node:"):
+            return
+        if ident is None:
+            if req.method in ("GET", "HEAD") and info.resource.split("/")[0] != "secrets":
+                return
+            if req.method in ("GET", "HEAD"):
+                raise HttpError(401, "Unauthorized: reading secrets needs a bearer token")
+            return  # a write: the handler's _auth answers 401
+        _sa, sns, sname = ident.split(":", 2)
+        roles = {(o["metadata"]["namespace"], o["metadata"]["name"]): o.get("rules") or []
+                 for o in self.store.list("roles", lambda o: self._in(p, o))}
+        croles = {o["metadata"]["name"]: o.get("rules") or [] for o in self.store.list("clusterroles", lambda o: self._in(p, o))}
+        binds = self.store.list("rolebindings", lambda o: self._in(p, o))
+        cbinds = self.store.list("clusterrolebindings", lambda o: self._in(p, o))
+        if not rbac.allowed(roles, croles, binds, cbinds, sns, sname, info):
+            raise HttpError(403, f'{info.resource} is forbidden: User "system:serviceaccount:{sns}:{sname}" {info.describe()}')
+
+    def _guarded(self, h):
+        async def g(req: Request, **kw):
+            self._authorize(req, kw.get("pid"))
+            return await h(req, **kw)
+        g.__name__ = getattr(h, "__name__", "handler")
+        return g
+
     def _strip(self, obj: dict) -> dict:
         return {k: v for k, v in obj.items() if not k.startswith("_")}
 
@@ -241,6 +304,7 @@ class KubernetesAPI:
                 for o in self.store.list(plural, lambda o: self._in(p, o) and o["metadata"].get("namespace") == name):
                     self.store.delete(plural, _key(p, name, o["metadata"]["name"]))
         self.store.delete("namespaces", _key(p, name))
+        self.__dict__.get("_sa_seen", set()).discard((p, name))  # a new namespace of that name gets its default SA
         self._sync_proxy()
         self.reconcile()
         return {**cur, "status": {"phase": "Terminating"}}
@@ -685,6 +749,8 @@ class KubernetesAPI:
             raise HttpError(422, "metadata.name is required")
         md["name"] = name
         md["namespace"] = ns
+        if not ns:  # a cluster-scoped kind (ClusterRole, ClusterRoleBinding)
+            md.pop("namespace")
         md.setdefault("labels", {})
         md.setdefault("annotations", {})
         body["_project"] = pid
@@ -738,8 +804,50 @@ class KubernetesAPI:
         o = self.store.put(kind, key, body)
         if kind in ("services", "ingresses"):
             self._sync_proxy()
+        if kind == "serviceaccounts":
+            self._sa_token(pid, ns, name)
+        if ns:
+            self._default_sa(pid, ns)
         self.reconcile()
         return o
+
+    def _default_sa(self, pid: str, ns: str) -> None:
+        """Every namespace has a ``default`` ServiceAccount (created with the namespace's first
+        object), and every project the built-in ClusterRoles (rbac.BUILTIN_CLUSTER_ROLES)."""
+        from . import rbac
+
+        seen = self.__dict__.setdefault("_sa_seen", set())
+        if (pid, ns) in seen:
+            return
+        seen.add((pid, ns))
+        if (pid, "") not in seen:
+            seen.add((pid, ""))
+            for name, rules in rbac.BUILTIN_CLUSTER_ROLES.items():
+                if self.store.get("clusterroles", _key(pid, "", name)) is None:
+                    self.store.put("clusterroles", _key(pid, "", name), {
+                        "metadata": {"name": name, "labels": {"kubernetes.io/bootstrapping": "rbac-defaults"}},
+                        "rules": rules, "_project": pid})
+        if self.store.get("serviceaccounts", _key(pid, ns, "default")) is None:
+            self.store.put("serviceaccounts", _key(pid, ns, "default"),
+                           {"metadata": {"name": "default", "namespace": ns}, "_project": pid})
+            self._sa_token(pid, ns, "default")
+
+    def _sa_token(self, pid: str, ns: str, sa: str) -> None:
+        """The ServiceAccount's token Secret (``<sa>-token``), listed in its ``secrets``."""
+        import base64
+
+        name = f"{sa}-token"
+        if self.store.get("secrets", _key(pid, ns, name)) is None:
+            tok = f"tk8s-sa.{token_hex(24)}"
+            self.store.put("secrets", _key(pid, ns, name), {
+                "metadata": {"name": name, "namespace": ns, "annotations": {"kubernetes.io/service-account.name": sa}},
+                "type": "kubernetes.io/service-account-token", "_project": pid,
+                "data": {"token": base64.b64encode(tok.encode()).decode(),
+                         "namespace": base64.b64encode(ns.encode()).decode()}})
+        cur = self.store.get("serviceaccounts", _key(pid, ns, sa))
+        if cur is not None and {"name": name} not in (cur.get("secrets") or []):
+            self.store.patch("serviceaccounts", _key(pid, ns, sa),
+                             lambda o: o.setdefault("secrets", []).append({"name": name}))
 
     def replace(self, pid: str, kind: str, ns: str, name: str, body: dict, merge: bool = False,
                 manager: str | None = None, subresource: str = "", keep_managed: bool = False,
@@ -766,6 +874,8 @@ class KubernetesAPI:
         md = new.setdefault("metadata", {})
         md.update(name=name, namespace=ns, uid=cur["metadata"]["uid"],
                   creationTimestamp=cur["metadata"].get("creationTimestamp"))
+        if not ns:
+            md.pop("namespace")
         md.pop("resourceVersion", None)
         md.setdefault("labels", {})
         md.setdefault("annotations", {})
@@ -1005,7 +1115,8 @@ class KubernetesAPI:
         """Authorise a WebSocket stream request (project API token or a node token) and pick the
         subprotocol: the first of ``protocols`` the client offers."""
         tok = req.bearer
-        if not (tok and (tok == self.project(p).get("apiToken") or any(
+        sa_ok = (getattr(req, "identity", None) or "").startswith("sa:")  # RBAC allowed it (_authorize)
+        if not (sa_ok or tok and (tok == self.project(p).get("apiToken") or any(
                 n.get("nodeToken") == tok for n in self.store.list("nodesecrets")))):
             raise HttpError(401, f"{what} needs a bearer token")
         offered = [x.strip() for x in (req.headers.get("sec-websocket-protocol") or "").split(",") if x.strip()]

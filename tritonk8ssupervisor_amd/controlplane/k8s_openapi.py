@@ -50,6 +50,9 @@ _TOP = {"Pod": ("spec", "status"), "Service": ("spec", "status"), "Node": ("spec
         "Namespace": ("spec", "status"), "DaemonSet": ("spec", "status"), "Deployment": ("spec", "status"),
         "Job": ("spec", "status"), "Ingress": ("spec", "status"),
         "ConfigMap": ("data", "binaryData", "immutable"),
+        "ServiceAccount": ("secrets", "imagePullSecrets", "automountServiceAccountToken"),
+        "Role": ("rules",), "ClusterRole": ("rules", "aggregationRule"),
+        "RoleBinding": ("roleRef", "subjects"), "ClusterRoleBinding": ("roleRef", "subjects"),
         "Secret": ("data", "stringData", "type", "immutable"),
         "Event": ("involvedObject", "reason", "message", "source", "firstTimestamp", "lastTimestamp", "count",
                   "type", "eventTime", "series", "action", "related", "reportingComponent",
@@ -74,7 +77,7 @@ def _gvs() -> list[tuple[str, str]]:
 
 def _schema_name(group: str, version: str, kind: str) -> str:
     pkg = {"": "core", "apps": "apps", "batch": "batch", "networking.k8s.io": "networking",
-           "autoscaling": "autoscaling"}.get(group, group)
+           "autoscaling": "autoscaling", "rbac.authorization.k8s.io": "rbac"}.get(group, group)
     return f"io.k8s.api.{pkg}.{version}.{kind}"
 
 
@@ -119,8 +122,10 @@ def gv_document(group: str, version: str) -> dict | None:
         name = _schema_name(g, v, kind)
         ref = f"#/components/schemas/{name}"
         top = {f: {"type": "object" if f in ("spec", "status", "data", "binaryData", "stringData", "involvedObject",
-                                              "source", "series", "related") else
-                   "boolean" if f == "immutable" else "integer" if f == "count" else "string",
+                                              "source", "series", "related", "roleRef", "aggregationRule") else
+                   "array" if f in ("rules", "subjects", "secrets", "imagePullSecrets") else
+                   "boolean" if f in ("immutable", "automountServiceAccountToken") else
+                   "integer" if f == "count" else "string",
                    **({"x-kubernetes-preserve-unknown-fields": True} if f in ("spec", "status") else {})}
                for f in _TOP.get(kind, ("spec", "status"))}
         schemas[name] = {"type": "object", "description": _DESCRIPTIONS.get(kind, kind), GVK: [gvk],

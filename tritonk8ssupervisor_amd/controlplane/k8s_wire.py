@@ -41,6 +41,11 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "cronjobs": ("batch", "v1", "CronJob", "cronjob", True, ("cj",), ()),
     "horizontalpodautoscalers": ("autoscaling", "v2", "HorizontalPodAutoscaler", "horizontalpodautoscaler", True,
                                  ("hpa",), ()),
+    "serviceaccounts": ("", "v1", "ServiceAccount", "serviceaccount", True, ("sa",), ()),
+    "roles": ("rbac.authorization.k8s.io", "v1", "Role", "role", True, (), ()),
+    "rolebindings": ("rbac.authorization.k8s.io", "v1", "RoleBinding", "rolebinding", True, (), ()),
+    "clusterroles": ("rbac.authorization.k8s.io", "v1", "ClusterRole", "clusterrole", False, (), ()),
+    "clusterrolebindings": ("rbac.authorization.k8s.io", "v1", "ClusterRoleBinding", "clusterrolebinding", False, (), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
 }
 READ_ONLY = {"namespaces": ("create", "delete", "get", "list", "patch", "watch"),

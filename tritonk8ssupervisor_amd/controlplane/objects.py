@@ -16,7 +16,11 @@ KIND_GROUPS = (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1
                ("secrets", "/api/v1"), ("persistentvolumeclaims", "/api/v1"), ("daemonsets", "/apis/apps/v1"), ("deployments", "/apis/apps/v1"),
                ("statefulsets", "/apis/apps/v1"), ("replicasets", "/apis/apps/v1"),
                ("jobs", "/apis/batch/v1"), ("cronjobs", "/apis/batch/v1"), ("ingresses", "/apis/networking.k8s.io/v1"),
-               ("horizontalpodautoscalers", "/apis/autoscaling/v2"))
+               ("horizontalpodautoscalers", "/apis/autoscaling/v2"), ("serviceaccounts", "/api/v1"),
+               ("roles", "/apis/rbac.authorization.k8s.io/v1"), ("rolebindings", "/apis/rbac.authorization.k8s.io/v1"))
+# cluster-scoped kinds served through the generic handlers (namespace "")
+CLUSTER_KIND_GROUPS = (("clusterroles", "/apis/rbac.authorization.k8s.io/v1"),
+                       ("clusterrolebindings", "/apis/rbac.authorization.k8s.io/v1"))
 
 
 def _key(*parts: str) -> str:
@@ -140,8 +144,11 @@ def _admit_gpu_visibility(kind: str, ns: str, body: dict, cur: dict | None = Non
         for k in _SCHEDULER_OWNED:
             if ann.get(k) != old.get(k):
                 raise HttpError(403, f"pods is forbidden: annotation {k} is set by the scheduler")
-    elif kind in ("jobs", "daemonsets", "deployments"):
-        ann = ((body.get("spec") or {}).get("template") or {}).get("metadata", {}).get("annotations") or {}
+    elif kind in ("jobs", "daemonsets", "deployments", "statefulsets", "replicasets", "cronjobs"):
+        spec = body.get("spec") or {}
+        if kind == "cronjobs":
+            spec = (spec.get("jobTemplate") or {}).get("spec") or {}
+        ann = (spec.get("template") or {}).get("metadata", {}).get("annotations") or {}
         what = _reserved(ann)
         if what and (kind != "jobs" or ns != "kube-system"):
             raise HttpError(403, f"{kind} is forbidden: annotation {what} is reserved for kube-system Jobs")

@@ -48,7 +48,7 @@ from . import k8s_openapi, k8s_wire
 from .controllers import Controllers
 from .httpserver import HttpError, HttpServer, Request, Response, Router
 from .k8s_api import KubernetesAPI
-from .objects import KIND_GROUPS, _cond, _key, _set_cond
+from .objects import CLUSTER_KIND_GROUPS, KIND_GROUPS, _cond, _key, _set_cond
 from .rancher_api import RancherAPI
 from .scheduler import Scheduler
 from .workloads import Workloads
@@ -57,6 +57,13 @@ from .store import Store, now_iso
 
 
 _KIND_PLURAL = {r[2]: plural for plural, r in k8s_wire.RESOURCES.items()}
+
+
+def _cluster_scoped(h):
+    """A namespaced handler used for a cluster-scoped kind: its objects live in namespace ""."""
+    async def g(req, pid=None, **kw):
+        return await h(req, ns="", pid=pid, **kw)
+    return g
 
 
 class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, Scheduler):
@@ -140,6 +147,8 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         tok = req.bearer
         if req.method in ("GET", "HEAD"):
             return
+        if (getattr(req, "identity", None) or "").startswith("sa:"):
+            return  # a ServiceAccount this request's RBAC check (_authorize) already allowed
         valid = {project.get("apiToken")}
         if tok in valid:
             return
@@ -179,7 +188,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         # Kubernetes subset, with and without the Rancher project prefix
         for pre in (r"/r/projects/(?P<pid>[^/]+)/kubernetes", r""):
             def add(method, path, h, pre=pre):
-                r.add(method, pre + path, h)
+                r.add(method, pre + path, self._guarded(h))
             add("GET", r"/openapi/v3/?", self.h_openapi_root)
             add("GET", r"/openapi/v3/(?P<gv>api/[^/]+|apis/[^/]+/[^/]+)", self.h_openapi_gv)
             add("GET", r"/apis/metrics.k8s.io/v1beta1/?", self.h_metrics_resources)
@@ -204,6 +213,13 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             add("PATCH", r"/api/v1/namespaces/(?P<name>[^/]+)", self.h_namespace_patch)
             add("DELETE", r"/api/v1/namespaces/(?P<name>[^/]+)", self.h_namespace_delete)
             add("GET", r"/api/v1/pods", self.h_pods)
+            for kind, grp in CLUSTER_KIND_GROUPS:
+                add("GET", grp + rf"/{kind}", self._lister(kind, all_ns=True))
+                add("POST", grp + rf"/{kind}", _cluster_scoped(self._creator(kind)))
+                add("GET", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._getter(kind)))
+                add("PUT", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._replacer(kind, False)))
+                add("PATCH", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._replacer(kind, True)))
+                add("DELETE", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._deleter(kind)))
             for kind, grp in KIND_GROUPS:
                 add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._lister(kind))
                 add("POST", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._creator(kind))

@@ -24,6 +24,11 @@ KINDS = {
     "replicaset": ("ReplicaSet", "/apis/apps/v1", "replicasets"),
     "cronjob": ("CronJob", "/apis/batch/v1", "cronjobs"),
     "horizontalpodautoscaler": ("HorizontalPodAutoscaler", "/apis/autoscaling/v2", "horizontalpodautoscalers"),
+    "serviceaccount": ("ServiceAccount", "/api/v1", "serviceaccounts"),
+    "role": ("Role", "/apis/rbac.authorization.k8s.io/v1", "roles"),
+    "rolebinding": ("RoleBinding", "/apis/rbac.authorization.k8s.io/v1", "rolebindings"),
+    "clusterrole": ("ClusterRole", "/apis/rbac.authorization.k8s.io/v1", "clusterroles"),
+    "clusterrolebinding": ("ClusterRoleBinding", "/apis/rbac.authorization.k8s.io/v1", "clusterrolebindings"),
     "configmap": ("ConfigMap", "/api/v1", "configmaps"),
     "secret": ("Secret", "/api/v1", "secrets"),
     "persistentvolumeclaim": ("PersistentVolumeClaim", "/api/v1", "persistentvolumeclaims"),
@@ -36,7 +41,9 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "sts": "statefulset", "statefulsets": "statefulset", "rs": "replicaset", "replicasets": "replicaset",
            "cj": "cronjob", "cronjobs": "cronjob", "pvc": "persistentvolumeclaim",
            "persistentvolumeclaims": "persistentvolumeclaim", "ns": "namespace", "namespaces": "namespace",
-           "hpa": "horizontalpodautoscaler", "horizontalpodautoscalers": "horizontalpodautoscaler"}
+           "hpa": "horizontalpodautoscaler", "horizontalpodautoscalers": "horizontalpodautoscaler",
+           "sa": "serviceaccount", "serviceaccounts": "serviceaccount", "roles": "role", "rolebindings": "rolebinding",
+           "clusterroles": "clusterrole", "clusterrolebindings": "clusterrolebinding"}
 
 
 def kind_key(kind: str) -> str:
@@ -50,6 +57,8 @@ def collection_path(kind: str, ns: str = "default") -> str:
         return "/api/v1/nodes"
     if k == "namespace":
         return "/api/v1/namespaces"
+    if k in ("clusterrole", "clusterrolebinding"):  # cluster-scoped
+        return f"/apis/rbac.authorization.k8s.io/v1/{KINDS[k][2]}"
     if k not in KINDS:
         raise ValueError(f"unsupported kind {kind!r}")
     _, group, plural = KINDS[k]
