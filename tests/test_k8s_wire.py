@@ -51,7 +51,8 @@ def test_discovery_documents(kube):
     names = {g["name"]: g["preferredVersion"]["groupVersion"] for g in groups["groups"]}
     assert names == {"apps": "apps/v1", "batch": "batch/v1", "networking.k8s.io": "networking.k8s.io/v1",
                      "autoscaling": "autoscaling/v2", "metrics.k8s.io": "metrics.k8s.io/v1beta1",
-                     "rbac.authorization.k8s.io": "rbac.authorization.k8s.io/v1"}
+                     "rbac.authorization.k8s.io": "rbac.authorization.k8s.io/v1",
+                     "authorization.k8s.io": "authorization.k8s.io/v1"}
     _, _, core = _raw(kube, "GET", "/api/v1")
     res = {r["name"]: r for r in core["resources"]}
     assert core["kind"] == "APIResourceList" and core["groupVersion"] == "v1"
@@ -382,3 +383,28 @@ def test_service_accounts_and_rbac(kube):
     assert as_(None, "GET", "/api/v1/namespaces/default/pods")[0] == 200
     assert as_(None, "GET", "/api/v1/namespaces/default/secrets")[0] == 401
     assert as_(None, "POST", "/api/v1/namespaces/default/configmaps", cm)[0] == 401
+
+
+def test_self_subject_access_review(kube):
+    """kubectl auth can-i: the admin may, a fresh ServiceAccount may not until bound."""
+    import base64
+
+    def review(tok, verb, resource, ns="default"):
+        conn = http.client.HTTPConnection(kube.host, kube.port, timeout=10)
+        conn.request("POST", kube.k8s("/apis/authorization.k8s.io/v1/selfsubjectaccessreviews"), body=json.dumps({
+            "apiVersion": "authorization.k8s.io/v1", "kind": "SelfSubjectAccessReview",
+            "spec": {"resourceAttributes": {"namespace": ns, "verb": verb, "resource": resource}}}).encode(),
+            headers={"Content-Type": "application/json", "Authorization": f"Bearer {tok}"})
+        r = conn.getresponse()
+        out = json.loads(r.read())
+        conn.close()
+        return out["status"]["allowed"]
+
+    assert review(kube.token, "delete", "nodes")
+    _raw(kube, "POST", "/api/v1/namespaces/default/serviceaccounts", {"metadata": {"name": "asker"}})
+    tok = base64.b64decode(_raw(kube, "GET", "/api/v1/namespaces/default/secrets/asker-token")[2]["data"]["token"]).decode()
+    assert not review(tok, "list", "pods")
+    _raw(kube, "POST", "/apis/rbac.authorization.k8s.io/v1/namespaces/default/rolebindings", {
+        "metadata": {"name": "asker"}, "roleRef": {"kind": "ClusterRole", "name": "view"},
+        "subjects": [{"kind": "ServiceAccount", "name": "asker", "namespace": "default"}]})
+    assert review(tok, "list", "pods") and not review(tok, "create", "pods") and not review(tok, "list", "pods", "other")

@@ -69,6 +69,8 @@ class KubernetesAPI:
         info = rbac.request_info(req.method, req.path, req.query)
         if info is None or ident == "admin" or (ident or "").startswith("node:"):
             return
+        if info.group == "authorization.k8s.io":  # anyone may ask what it may do (system:basic-user)
+            return
         if ident is None:
             if req.method in ("GET", "HEAD") and info.resource.split("/")[0] != "secrets":
                 return
@@ -83,6 +85,34 @@ class KubernetesAPI:
         cbinds = self.store.list("clusterrolebindings", lambda o: self._in(p, o))
         if not rbac.allowed(roles, croles, binds, cbinds, sns, sname, info):
             raise HttpError(403, f'{info.resource} is forbidden: User "system:serviceaccount:{sns}:{sname}" {info.describe()}')
+
+    async def h_access_review(self, req: Request, pid: str | None = None):
+        """``kubectl auth can-i``: a SelfSubjectAccessReview answered for the caller's identity."""
+        from . import rbac
+
+        body = req.json()
+        ra = ((body or {}).get("spec") or {}).get("resourceAttributes") or {}
+        res = ra.get("resource", "") + (f"/{ra['subresource']}" if ra.get("subresource") else "")
+        info = rbac.RequestInfo(ra.get("verb", "get"), ra.get("group", ""), res, ra.get("namespace", ""), ra.get("name", ""))
+        ident = getattr(req, "identity", None)
+        p = self._pid(pid, req)
+        if ident == "admin" or (ident or "").startswith("node:"):
+            ok, why = True, "the cluster administrator" if ident == "admin" else "a node"
+        elif ident is None:
+            ok = info.verb in ("get", "list", "watch") and info.resource.split("/")[0] != "secrets"
+            why = "anonymous: read-only, no Secrets"
+        else:
+            _sa, sns, sname = ident.split(":", 2)
+            ok = rbac.allowed({(o["metadata"]["namespace"], o["metadata"]["name"]): o.get("rules") or []
+                               for o in self.store.list("roles", lambda o: self._in(p, o))},
+                              {o["metadata"]["name"]: o.get("rules") or []
+                               for o in self.store.list("clusterroles", lambda o: self._in(p, o))},
+                              self.store.list("rolebindings", lambda o: self._in(p, o)),
+                              self.store.list("clusterrolebindings", lambda o: self._in(p, o)), sns, sname, info)
+            why = "RBAC"
+        return Response(201, {"apiVersion": "authorization.k8s.io/v1", "kind": "SelfSubjectAccessReview",
+                              "metadata": {}, "spec": body.get("spec", {}),
+                              "status": {"allowed": ok, **({"reason": why} if ok else {"reason": why, "denied": False})}})
 
     def _guarded(self, h):
         async def g(req: Request, **kw):

@@ -78,7 +78,8 @@ def _groups() -> list[tuple[str, str]]:
     for g, v, *_ in RESOURCES.values():
         if g and (g, v) not in seen:
             seen.append((g, v))
-    return seen + [("metrics.k8s.io", "v1beta1")]  # served by metrics_api.py, not objects
+    # served by metrics_api.py and rbac.py, not objects
+    return seen + [("metrics.k8s.io", "v1beta1"), ("authorization.k8s.io", "v1")]
 
 
 def api_group_list() -> dict:

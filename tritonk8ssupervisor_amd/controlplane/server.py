@@ -197,6 +197,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             add("GET", r"/apis/metrics.k8s.io/v1beta1/pods", self.h_pod_metrics)
             add("GET", r"/apis/metrics.k8s.io/v1beta1/namespaces/(?P<ns>[^/]+)/pods", self.h_pod_metrics)
             add("GET", r"/apis/metrics.k8s.io/v1beta1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)", self.h_pod_metrics)
+            add("POST", r"/apis/authorization.k8s.io/v1/selfsubjectaccessreviews", self.h_access_review)
             add("GET", r"/api/?", self.h_api_versions)
             add("GET", r"/apis/?", self.h_api_groups)
             add("GET", r"/api/v1/?", self.h_api_resources)
@@ -277,6 +278,10 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
     async def h_api_resources(self, req: Request, group: str = "", version: str = "v1", pid: str | None = None):
         if (group, version) == ("metrics.k8s.io", "v1beta1"):
             return await self.h_metrics_resources(req)
+        if (group, version) == ("authorization.k8s.io", "v1"):
+            return {"kind": "APIResourceList", "apiVersion": "v1", "groupVersion": "authorization.k8s.io/v1", "resources": [
+                {"name": "selfsubjectaccessreviews", "singularName": "", "namespaced": False,
+                 "kind": "SelfSubjectAccessReview", "verbs": ["create"]}]}
         r = k8s_wire.api_resource_list(group, version)
         if r is None:
             raise HttpError(404, f"the server could not find the requested resource ({group}/{version})")
