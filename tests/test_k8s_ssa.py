@@ -42,8 +42,8 @@ def _supports_field_validation(doc: dict, gvk: dict) -> bool:
 
 def test_openapi_v3_lets_kubectl_validate_on_the_server(kube):
     st, _, root = _raw(kube, "GET", "/openapi/v3")
-    assert st == 200 and set(root["paths"]) == {"api/v1", "apis/apps/v1", "apis/batch/v1", "apis/networking.k8s.io/v1",
-                                                "apis/autoscaling/v2", "apis/rbac.authorization.k8s.io/v1"}
+    assert st == 200 and set(root["paths"]) == {k8s_openapi.gv_key(g, v) for g, v in k8s_openapi._gvs()}
+    assert {"api/v1", "apis/apps/v1", "apis/batch/v1"} <= set(root["paths"])
     for key, ref in root["paths"].items():
         url = ref["serverRelativeURL"]
         # client-go replaces the server URL's path with this one, so it carries the project prefix

@@ -49,10 +49,11 @@ def test_discovery_documents(kube):
     assert st == 200 and v["kind"] == "APIVersions" and v["versions"] == ["v1"]
     _, _, groups = _raw(kube, "GET", "/apis")
     names = {g["name"]: g["preferredVersion"]["groupVersion"] for g in groups["groups"]}
-    assert names == {"apps": "apps/v1", "batch": "batch/v1", "networking.k8s.io": "networking.k8s.io/v1",
-                     "autoscaling": "autoscaling/v2", "metrics.k8s.io": "metrics.k8s.io/v1beta1",
-                     "rbac.authorization.k8s.io": "rbac.authorization.k8s.io/v1",
-                     "authorization.k8s.io": "authorization.k8s.io/v1"}
+    # every served group, each at its one version (the list grows with the kinds served)
+    assert {"apps": "apps/v1", "batch": "batch/v1", "networking.k8s.io": "networking.k8s.io/v1",
+            "autoscaling": "autoscaling/v2", "metrics.k8s.io": "metrics.k8s.io/v1beta1",
+            "rbac.authorization.k8s.io": "rbac.authorization.k8s.io/v1"}.items() <= names.items()
+    assert set(names) == {g for g, _v in k8s_wire._groups()}
     _, _, core = _raw(kube, "GET", "/api/v1")
     res = {r["name"]: r for r in core["resources"]}
     assert core["kind"] == "APIResourceList" and core["groupVersion"] == "v1"
@@ -408,3 +409,46 @@ def test_self_subject_access_review(kube):
         "metadata": {"name": "asker"}, "roleRef": {"kind": "ClusterRole", "name": "view"},
         "subjects": [{"kind": "ServiceAccount", "name": "asker", "namespace": "default"}]})
     assert review(tok, "list", "pods") and not review(tok, "create", "pods") and not review(tok, "list", "pods", "other")
+
+
+def test_custom_resource_definitions(kube):
+    crd = {"apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition",
+           "metadata": {"name": "trainingjobs.mi355x.example.com"},
+           "spec": {"group": "mi355x.example.com", "scope": "Namespaced",
+                    "names": {"plural": "trainingjobs", "singular": "trainingjob", "kind": "TrainingJob",
+                              "shortNames": ["tj"]},
+                    "versions": [{"name": "v1", "served": True, "storage": True, "subresources": {"status": {}},
+                                  "schema": {"openAPIV3Schema": {"type": "object", "x-kubernetes-preserve-unknown-fields": True}}}]}}
+    bad = json.loads(json.dumps(crd))
+    bad["metadata"]["name"] = "wrong"
+    assert _raw(kube, "POST", "/apis/apiextensions.k8s.io/v1/customresourcedefinitions", bad)[0] == 422
+    st, _, c = _raw(kube, "POST", "/apis/apiextensions.k8s.io/v1/customresourcedefinitions", crd)
+    assert st == 201 and {x["type"] for x in c["status"]["conditions"]} == {"NamesAccepted", "Established"}
+    groups = {g["name"] for g in _raw(kube, "GET", "/apis")[2]["groups"]}
+    assert "mi355x.example.com" in groups
+    res = _raw(kube, "GET", "/apis/mi355x.example.com/v1")[2]["resources"]
+    assert {r["name"] for r in res} == {"trainingjobs", "trainingjobs/status"} and res[0]["shortNames"] == ["tj"]
+    base = "/apis/mi355x.example.com/v1/namespaces/default/trainingjobs"
+    tj = {"apiVersion": "mi355x.example.com/v1", "kind": "TrainingJob", "metadata": {"name": "llama"},
+          "spec": {"gpus": 8, "model": "llama"}}
+    st, _, o = _raw(kube, "POST", base, tj)
+    assert st == 201 and o["kind"] == "TrainingJob" and o["metadata"]["uid"]
+    assert _raw(kube, "GET", base + "/llama")[2]["spec"]["gpus"] == 8
+    lst = _raw(kube, "GET", base)[2]
+    assert lst["kind"] == "TrainingJobList" and lst["apiVersion"] == "mi355x.example.com/v1" and len(lst["items"]) == 1
+    assert len(_raw(kube, "GET", "/apis/mi355x.example.com/v1/trainingjobs")[2]["items"]) == 1  # all namespaces
+    st, _, o = _raw(kube, "PATCH", base + "/llama", {"spec": {"gpus": 16}}, ctype=k8s_wire.MERGE_PATCH)
+    assert st == 200 and o["spec"]["gpus"] == 16
+    st, _, o = _raw(kube, "PUT", base + "/llama/status", {"status": {"phase": "Running"}})
+    assert st == 200 and o["status"] == {"phase": "Running"} and o["spec"]["gpus"] == 16
+    st, _, o = _raw(kube, "PATCH", base + "/llama?fieldManager=op", {"apiVersion": "mi355x.example.com/v1",
+                    "kind": "TrainingJob", "metadata": {"name": "llama"}, "spec": {"priority": 1}},
+                    ctype=k8s_wire.APPLY_PATCH)
+    assert st == 200 and o["spec"]["priority"] == 1  # server-side apply works on custom resources too
+    assert _raw(kube, "GET", "/apis/mi355x.example.com/v2/namespaces/default/trainingjobs")[0] == 404
+    assert _raw(kube, "GET", "/apis/nope.example.com/v1/namespaces/default/things")[0] == 404
+    # deleting the CRD deletes its objects and its API
+    assert _raw(kube, "DELETE", "/apis/apiextensions.k8s.io/v1/customresourcedefinitions/trainingjobs.mi355x.example.com")[0] == 200
+    assert _raw(kube, "GET", base)[0] == 404
+    _raw(kube, "POST", "/apis/apiextensions.k8s.io/v1/customresourcedefinitions", crd)
+    assert _raw(kube, "GET", base)[2]["items"] == []

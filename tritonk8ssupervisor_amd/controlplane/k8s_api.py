@@ -140,7 +140,8 @@ class KubernetesAPI:
         items.sort(key=lambda o: (o["metadata"].get("namespace", ""), o["metadata"]["name"]))
         if k8s_wire.wants_table(req.headers.get("accept", "")):
             return k8s_wire.table(kind, items, str(self.store.rv))
-        api, lk = k8s_wire.list_kind(kind) if kind in k8s_wire.RESOURCES else ("v1", "List")
+        api, k_name, _ns = self._kind_meta(kind)
+        lk = k_name + "List" if k_name != "Status" else "List"
         return {"kind": lk, "apiVersion": api, "metadata": {"resourceVersion": str(self.store.rv)}, "items": items}
 
     async def _watch_stream(self, req: Request, kind: str, pred):
@@ -170,8 +171,7 @@ class KubernetesAPI:
                 yield line("ERROR", k8s_wire.status_body(410, f"too old resource version: {since} ({oldest - 1})"))
                 return
         if req.q("sendInitialEvents") == "true" and req.q("allowWatchBookmarks") == "true":
-            yield line("BOOKMARK", {"kind": k8s_wire.RESOURCES.get(kind, ("", "", "Status"))[2],
-                                    "apiVersion": k8s_wire.group_version(kind) if kind in k8s_wire.RESOURCES else "v1",
+            yield line("BOOKMARK", {"kind": self._kind_meta(kind)[1], "apiVersion": self._kind_meta(kind)[0],
                                     "metadata": {"resourceVersion": str(since),
                                                  "annotations": {"k8s.io/initial-events-end": "true"}}})
         while True:
@@ -458,7 +458,7 @@ class KubernetesAPI:
         manager = req.q("fieldManager")
         if not manager:
             raise HttpError(400, "PATCH, application/apply-patch+yaml: fieldManager is required for apply requests")
-        api_version, kind_name = k8s_wire.type_meta()[kind]
+        api_version, kind_name, _ns = self._kind_meta(kind)
         if body.get("apiVersion") != api_version or body.get("kind") != kind_name:
             raise HttpError(400, f"apply: apiVersion/kind must be {api_version}/{kind_name}, "
                                  f"got {body.get('apiVersion')}/{body.get('kind')}")
@@ -529,6 +529,10 @@ class KubernetesAPI:
                 raise HttpError(404, f'{kind} "{name}" not found')
             if kind in ("services", "ingresses"):
                 self._sync_proxy()
+            if kind == "customresourcedefinitions":  # its custom resources go with it
+                cr = name  # "<plural>.<group>" is also their store kind
+                for x in self.store.list(cr, lambda x: self._in(p, x)):
+                    self.store.delete(cr, _key(p, x["metadata"].get("namespace", ""), x["metadata"]["name"]))
             if kind != "pods":  # garbage collection: what the object owned goes with it
                 for dep_kind in ("pods", "replicasets", "jobs"):
                     for dep in self.store.list(dep_kind, lambda x: self._in(p, x) and any(
@@ -808,6 +812,13 @@ class KubernetesAPI:
             md["generation"] = 1
         elif kind == "persistentvolumeclaims":
             self._admit_pvc(name, body)
+        elif kind == "customresourcedefinitions":
+            self._admit_crd(name, body)
+        elif kind not in k8s_wire.RESOURCES:  # a custom resource: its type from the CRD
+            api_version, kind_name, _ns = self._kind_meta(kind)
+            if body.get("kind") not in (None, kind_name):
+                raise HttpError(400, f"kind {body.get('kind')!r} does not match {kind_name!r}")
+            body["apiVersion"], body["kind"] = api_version, kind_name
         elif kind == "horizontalpodautoscalers":
             spec = body.get("spec") or {}
             ref = spec.get("scaleTargetRef") or {}
@@ -825,7 +836,7 @@ class KubernetesAPI:
         elif kind == "ingresses":
             body["status"] = {"loadBalancer": {"ingress": [{"ip": self.advertise or self.host}]}}
         if manager and not keep_managed:
-            m = ssa.Managed(None, k8s_wire.type_meta()[kind][0])
+            m = ssa.Managed(None, self._kind_meta(kind)[0])
             m.update(None, body, manager)
             md["managedFields"] = m.entries()
         if dry_run:
@@ -956,7 +967,7 @@ class KubernetesAPI:
             if old_mf:
                 md["managedFields"] = copy.deepcopy(old_mf)
             if manager:
-                m = ssa.Managed(old_mf, k8s_wire.type_meta()[kind][0])
+                m = ssa.Managed(old_mf, self._kind_meta(kind)[0])
                 m.update(self._strip(cur), new, manager, subresource)
                 md["managedFields"] = m.entries()
         if not md.get("managedFields"):

@@ -46,6 +46,8 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "rolebindings": ("rbac.authorization.k8s.io", "v1", "RoleBinding", "rolebinding", True, (), ()),
     "clusterroles": ("rbac.authorization.k8s.io", "v1", "ClusterRole", "clusterrole", False, (), ()),
     "clusterrolebindings": ("rbac.authorization.k8s.io", "v1", "ClusterRoleBinding", "clusterrolebinding", False, (), ()),
+    "customresourcedefinitions": ("apiextensions.k8s.io", "v1", "CustomResourceDefinition", "customresourcedefinition",
+                                  False, ("crd", "crds"), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
 }
 READ_ONLY = {"namespaces": ("create", "delete", "get", "list", "patch", "watch"),

@@ -20,7 +20,8 @@ KIND_GROUPS = (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1
                ("roles", "/apis/rbac.authorization.k8s.io/v1"), ("rolebindings", "/apis/rbac.authorization.k8s.io/v1"))
 # cluster-scoped kinds served through the generic handlers (namespace "")
 CLUSTER_KIND_GROUPS = (("clusterroles", "/apis/rbac.authorization.k8s.io/v1"),
-                       ("clusterrolebindings", "/apis/rbac.authorization.k8s.io/v1"))
+                       ("clusterrolebindings", "/apis/rbac.authorization.k8s.io/v1"),
+                       ("customresourcedefinitions", "/apis/apiextensions.k8s.io/v1"))
 
 
 def _key(*parts: str) -> str:

@@ -52,11 +52,17 @@ from .objects import CLUSTER_KIND_GROUPS, KIND_GROUPS, _cond, _key, _set_cond
 from .rancher_api import RancherAPI
 from .scheduler import Scheduler
 from .workloads import Workloads
+from .crds import CustomResources
 from .metrics_api import MetricsAPI
 from .store import Store, now_iso
 
 
 _KIND_PLURAL = {r[2]: plural for plural, r in k8s_wire.RESOURCES.items()}
+
+
+def _group_doc(group: str, versions: list[str]) -> dict:
+    return {"name": group, "versions": [{"groupVersion": f"{group}/{v}", "version": v} for v in versions],
+            "preferredVersion": {"groupVersion": f"{group}/{versions[0]}", "version": versions[0]}}
 
 
 def _cluster_scoped(h):
@@ -66,7 +72,7 @@ def _cluster_scoped(h):
     return g
 
 
-class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, Scheduler):
+class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port
@@ -241,6 +247,8 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/attach", self.h_pod_attach_ws)
             add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs", self.h_node_execs)
             add("PUT", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)", self.h_exec_result)
+            for method in ("GET", "POST", "PUT", "PATCH", "DELETE"):  # custom resources (crds.py): last
+                add(method, r"/apis/(?P<group>[^/]+)/(?P<version>[^/]+)/(?P<rest>.+)", self.h_custom)
 
     # ---- Kubernetes discovery (k8s_wire.py) ----------------------------------------------
     @staticmethod
@@ -267,10 +275,15 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
                                            "Etag": f'"{h}"'})
 
     async def h_api_groups(self, req: Request, pid: str | None = None):
-        return k8s_wire.api_group_list()
+        out = k8s_wire.api_group_list()
+        for g, versions in sorted(self._crd_groups().items()):  # custom resources' groups (crds.py)
+            out["groups"].append(_group_doc(g, versions))
+        return out
 
     async def h_api_group(self, req: Request, group: str, pid: str | None = None):
         g = k8s_wire.api_group(group)
+        if g is None and group in self._crd_groups():
+            return {"kind": "APIGroup", "apiVersion": "v1", **_group_doc(group, self._crd_groups()[group])}
         if g is None:
             raise HttpError(404, f"the server could not find the requested resource (group {group})")
         return g
@@ -282,7 +295,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             return {"kind": "APIResourceList", "apiVersion": "v1", "groupVersion": "authorization.k8s.io/v1", "resources": [
                 {"name": "selfsubjectaccessreviews", "singularName": "", "namespaced": False,
                  "kind": "SelfSubjectAccessReview", "verbs": ["create"]}]}
-        r = k8s_wire.api_resource_list(group, version)
+        r = k8s_wire.api_resource_list(group, version) or self._crd_resource_list(group, version)
         if r is None:
             raise HttpError(404, f"the server could not find the requested resource ({group}/{version})")
         return r
