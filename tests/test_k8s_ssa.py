@@ -234,3 +234,29 @@ def test_bundled_kubectl_server_side_apply(kube, tmp_path, capsys):
     assert kc("get", "deploy", "web", "-o", "json", "--show-managed-fields") == 0
     managers = {e["manager"] for e in json.loads(capsys.readouterr().out)["metadata"]["managedFields"]}
     assert managers == {"kubectl", "ci"}
+
+
+def test_bundled_kubectl_custom_resources(kube, tmp_path, capsys):
+    """./kubectl apply of a CRD and its objects, then get/delete them by plural or short name."""
+    from tritonk8ssupervisor_amd.cli import kubectl
+
+    pid = kube.prefix.split("/")[3]
+    cfg = tmp_path / "kubeconfig.json"
+    cfg.write_text(json.dumps(kube.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})))
+    kc = lambda *a: kubectl.main(["--kubeconfig", str(cfg), *a], workdir=str(tmp_path))
+    crd = {"apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition",
+           "metadata": {"name": "gpuquotas.tk8s.example.com"},
+           "spec": {"group": "tk8s.example.com", "scope": "Namespaced",
+                    "names": {"plural": "gpuquotas", "singular": "gpuquota", "kind": "GpuQuota", "shortNames": ["gq"]},
+                    "versions": [{"name": "v1alpha1", "served": True, "storage": True}]}}
+    (tmp_path / "crd.json").write_text(json.dumps(crd))
+    assert kc("apply", "-f", str(tmp_path / "crd.json")) == 0
+    (tmp_path / "q.json").write_text(json.dumps({"apiVersion": "tk8s.example.com/v1alpha1", "kind": "GpuQuota",
+                                                 "metadata": {"name": "team-a"}, "spec": {"gpus": 4}}))
+    assert kc("apply", "-f", str(tmp_path / "q.json")) == 0
+    capsys.readouterr()
+    assert kc("get", "gq") == 0 and "team-a" in capsys.readouterr().out
+    assert kc("get", "gpuquota", "team-a", "-o", "json") == 0
+    assert json.loads(capsys.readouterr().out)["spec"]["gpus"] == 4
+    assert kc("get", "crds") == 0 and "gpuquotas.tk8s.example.com" in capsys.readouterr().out
+    assert kc("delete", "gpuquotas", "team-a") == 0

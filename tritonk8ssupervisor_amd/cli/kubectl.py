@@ -400,6 +400,12 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
         return 1
     ns = a.namespace
     try:
+        from ..kube import KINDS, learn_kind
+
+        for word in ([a.args[0].split("/")[0]] if a.args and a.verb in ("get", "describe", "delete", "label", "annotate")
+                     else []):
+            if kind_key(word) not in KINDS and kind_key(word) not in ("node", "namespace"):
+                learn_kind(k, word)  # a custom resource: ask discovery where it lives
         if a.verb in ("version",):
             print(json.dumps(k.get("/version"), indent=1))
         elif a.verb == "cluster-info":

@@ -29,6 +29,7 @@ KINDS = {
     "rolebinding": ("RoleBinding", "/apis/rbac.authorization.k8s.io/v1", "rolebindings"),
     "clusterrole": ("ClusterRole", "/apis/rbac.authorization.k8s.io/v1", "clusterroles"),
     "clusterrolebinding": ("ClusterRoleBinding", "/apis/rbac.authorization.k8s.io/v1", "clusterrolebindings"),
+    "customresourcedefinition": ("CustomResourceDefinition", "/apis/apiextensions.k8s.io/v1", "customresourcedefinitions"),
     "configmap": ("ConfigMap", "/api/v1", "configmaps"),
     "secret": ("Secret", "/api/v1", "secrets"),
     "persistentvolumeclaim": ("PersistentVolumeClaim", "/api/v1", "persistentvolumeclaims"),
@@ -43,7 +44,36 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "persistentvolumeclaims": "persistentvolumeclaim", "ns": "namespace", "namespaces": "namespace",
            "hpa": "horizontalpodautoscaler", "horizontalpodautoscalers": "horizontalpodautoscaler",
            "sa": "serviceaccount", "serviceaccounts": "serviceaccount", "roles": "role", "rolebindings": "rolebinding",
-           "clusterroles": "clusterrole", "clusterrolebindings": "clusterrolebinding"}
+           "clusterroles": "clusterrole", "clusterrolebindings": "clusterrolebinding", "crd": "customresourcedefinition",
+           "crds": "customresourcedefinition", "customresourcedefinitions": "customresourcedefinition"}
+
+
+CLUSTER_SCOPED: set[str] = {"customresourcedefinition"}  # (+ kinds learnt from discovery without a namespace)
+
+
+def learn_kind(k: Client, name: str) -> str | None:
+    """A kind the bundled client does not know (a CustomResourceDefinition's): find it by plural,
+    singular, kind or short name in the server's discovery and remember where it lives."""
+    want = name.lower()
+    for g in k.get(k.k8s("/apis")).get("groups", []):
+        gv = g["preferredVersion"]["groupVersion"]
+        try:
+            res = k.get(k.k8s(f"/apis/{gv}")).get("resources", [])
+        except ApiError:
+            continue
+        for r in res:
+            if "/" in r["name"]:
+                continue
+            names = {r["name"], r.get("singularName", ""), r.get("kind", "").lower(), *r.get("shortNames", [])}
+            if want in names:
+                key = r.get("singularName") or r["kind"].lower()
+                KINDS[key] = (r["kind"], f"/apis/{gv}", r["name"])
+                for n in names - {""}:
+                    ALIASES.setdefault(n, key)
+                if not r.get("namespaced", True):
+                    CLUSTER_SCOPED.add(key)
+                return key
+    return None
 
 
 def kind_key(kind: str) -> str:
@@ -57,8 +87,8 @@ def collection_path(kind: str, ns: str = "default") -> str:
         return "/api/v1/nodes"
     if k == "namespace":
         return "/api/v1/namespaces"
-    if k in ("clusterrole", "clusterrolebinding"):  # cluster-scoped
-        return f"/apis/rbac.authorization.k8s.io/v1/{KINDS[k][2]}"
+    if k in ("clusterrole", "clusterrolebinding") or k in CLUSTER_SCOPED:  # cluster-scoped
+        return f"{KINDS[k][1]}/{KINDS[k][2]}"
     if k not in KINDS:
         raise ValueError(f"unsupported kind {kind!r}")
     _, group, plural = KINDS[k]
@@ -103,6 +133,11 @@ def _ensure_namespace(k: Client, o: dict) -> dict:
         return {"created": False, "action": "unchanged"}
 
 
+def _known(k: Client, kind: str) -> None:
+    if kind_key(kind) not in KINDS and kind_key(kind) not in ("node", "namespace"):
+        learn_kind(k, kind)
+
+
 def apply_objects(k: Client, objs: list[dict]) -> list[dict]:
     """``kubectl apply``: create, or update an existing object to the manifest (PUT with the live
     resourceVersion; status and server-allocated fields are kept by the control plane)."""
@@ -112,6 +147,7 @@ def apply_objects(k: Client, objs: list[dict]) -> list[dict]:
         if kind.lower() == "namespace":
             res.append({"kind": kind, "name": o["metadata"]["name"], **_ensure_namespace(k, o)})
             continue
+        _known(k, kind)
         ns = o.get("metadata", {}).get("namespace", "default")
         name = o["metadata"].get("name")
         try:
@@ -152,6 +188,7 @@ def server_apply_objects(k: Client, objs: list[dict], manager: str = "kubectl", 
             _ensure_namespace(k, o)
             res.append({"kind": kind, "name": o["metadata"]["name"], "action": "serverside-applied"})
             continue
+        _known(k, kind)
         ns = o.get("metadata", {}).get("namespace", "default")
         name = o["metadata"]["name"]
         q = {"fieldManager": manager, "force": "true" if force else None, "dryRun": "All" if dry_run else None}
@@ -165,6 +202,7 @@ def delete_objects(k: Client, objs: list[dict]) -> int:
     n = 0
     for o in sorted(objs, key=lambda o: o.get("kind", "").lower() == "namespace"):
         kind = o.get("kind", "")
+        _known(k, kind)
         ns = o.get("metadata", {}).get("namespace", "default")
         try:
             k.delete(k.k8s(object_path(kind, o["metadata"]["name"], ns)))
