@@ -446,3 +446,31 @@ def test_deployment_revisions_as_replicasets(cp):
     cp._pid = lambda pid, req: "1a1"
     asyncio.run(cp._deleter("deployments")(Request("DELETE", "/x", {}, {}, b""), ns="default", name="web"))
     assert rss() == {} and _pods(cp, "web-") == []
+
+
+def test_endpoints_follow_ready_pods_and_leases_are_plain_objects(cp):
+    cp.create("1a1", "services", "default", {"metadata": {"name": "web"}, "spec": {
+        "selector": {"app": "web"}, "ports": [{"name": "http", "port": 80, "targetPort": "http"}]}})
+    for n in ("a", "b"):
+        cp.create("1a1", "pods", "default", {"metadata": {"name": n, "labels": {"app": "web"}}, "spec": {
+            "containers": [{"name": "c", "command": ["true"], "ports": [{"name": "http", "containerPort": 8080}]}]}})
+    assert cp.store.get("endpoints", _key("1a1", "default", "web"))["subsets"] == []
+    cp.store.patch("pods", _key("1a1", "default", "a"), lambda o: o["status"].update(phase="Running", podIP="127.128.0.2"))
+    cp.store.patch("pods", _key("1a1", "default", "b"), lambda o: o["status"].update(
+        phase="Running", podIP="127.128.0.3", conditions=[{"type": "Ready", "status": "False"}]))
+    cp.reconcile()
+    sub = cp.store.get("endpoints", _key("1a1", "default", "web"))["subsets"][0]
+    assert [a["ip"] for a in sub["addresses"]] == ["127.128.0.2"] and sub["addresses"][0]["targetRef"]["name"] == "a"
+    assert [a["ip"] for a in sub["notReadyAddresses"]] == ["127.128.0.3"]
+    assert sub["ports"] == [{"name": "http", "port": 8080, "protocol": "TCP"}]
+    import asyncio
+
+    from tritonk8ssupervisor_amd.controlplane.httpserver import Request
+
+    cp._auth = lambda req, proj: None
+    cp._pid = lambda pid, req: "1a1"
+    asyncio.run(cp._deleter("services")(Request("DELETE", "/x", {}, {}, b""), ns="default", name="web"))
+    assert cp.store.get("endpoints", _key("1a1", "default", "web")) is None
+    lease = cp.create("1a1", "leases", "default", {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                                                   "metadata": {"name": "leader"}, "spec": {"holderIdentity": "op-1"}})
+    assert lease["kind"] == "Lease" and lease["spec"]["holderIdentity"] == "op-1"

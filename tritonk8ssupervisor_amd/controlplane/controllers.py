@@ -32,6 +32,7 @@ class Controllers:
                     self._ctl_deployments(pid)
                     self._ctl_statefulsets(pid)
                     self._ctl_replicasets(pid)
+                    self._ctl_endpoints(pid)
                     self._ctl_validation(pid)
                     self._scheduler(pid)
                 if not self._again:
@@ -290,3 +291,55 @@ class Controllers:
         if d["metadata"].get("annotations", {}).get(REVISION) != str(revs[h]):
             self.store.patch("deployments", _key(pid, ns, dname),
                              lambda o, r=str(revs[h]): o["metadata"].setdefault("annotations", {}).__setitem__(REVISION, r))
+
+    def _ctl_endpoints(self, pid: str) -> None:
+        """The Endpoints object of every Service with a selector: the Ready pods' IPs and the
+        Service's target ports (named container ports resolved per pod), Not-Ready ones apart --
+        what clients that discover backends through the API read (the proxy computes the same
+        set itself, k8s_api._endpoints)."""
+        services = self.store.list("services", lambda o: self._in(pid, o))
+        wanted = set()
+        for svc in services:
+            sel = svc["spec"].get("selector") or {}
+            if not sel:
+                continue
+            ns, name = svc["metadata"]["namespace"], svc["metadata"]["name"]
+            wanted.add((ns, name))
+            ready, not_ready, ports = [], [], {}
+            for o in self.store.list("pods", lambda o, ns=ns: self._in(pid, o) and o["metadata"].get("namespace") == ns):
+                if not labels_match(sel, o["metadata"].get("labels")) or o.get("status", {}).get("phase") != "Running":
+                    continue
+                ip = o["status"].get("podIP")
+                if not ip:
+                    continue
+                addr = {"ip": ip, "nodeName": o["spec"].get("nodeName"),
+                        "targetRef": {"kind": "Pod", "name": o["metadata"]["name"], "namespace": ns,
+                                      "uid": o["metadata"].get("uid")}}
+                is_ready = not any(c.get("type") == "Ready" and c.get("status") == "False"
+                                   for c in o["status"].get("conditions") or [])
+                (ready if is_ready else not_ready).append(addr)
+                for p in svc["spec"].get("ports") or []:
+                    tp = p.get("targetPort", p.get("port"))
+                    if isinstance(tp, str) and not tp.isdigit():
+                        tp = next((cp.get("containerPort") for c in o["spec"].get("containers", [])
+                                   for cp in c.get("ports", []) if cp.get("name") == tp), None)
+                    if tp:
+                        ports[p.get("name") or str(p.get("port"))] = {"name": p.get("name"), "port": int(tp),
+                                                                      "protocol": p.get("protocol", "TCP")}
+            subsets = []
+            if ready or not_ready:
+                sub = {"ports": sorted(ports.values(), key=lambda x: str(x["name"]))}
+                if ready:
+                    sub["addresses"] = sorted(ready, key=lambda a: a["ip"])
+                if not_ready:
+                    sub["notReadyAddresses"] = sorted(not_ready, key=lambda a: a["ip"])
+                subsets = [sub]
+            key = _key(pid, ns, name)
+            cur = self.store.get("endpoints", key)
+            if cur is None or cur.get("subsets") != subsets:
+                self.store.put("endpoints", key, {  # (the store keeps the uid and creation time)
+                    "metadata": {"name": name, "namespace": ns, "labels": dict(svc["metadata"].get("labels") or {})},
+                    "subsets": subsets, "_project": pid})
+        for ep in self.store.list("endpoints", lambda o: self._in(pid, o)):
+            if (ep["metadata"]["namespace"], ep["metadata"]["name"]) not in wanted:
+                self.store.delete("endpoints", _key(pid, ep["metadata"]["namespace"], ep["metadata"]["name"]))

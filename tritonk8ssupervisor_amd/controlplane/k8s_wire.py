@@ -42,6 +42,8 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "horizontalpodautoscalers": ("autoscaling", "v2", "HorizontalPodAutoscaler", "horizontalpodautoscaler", True,
                                  ("hpa",), ()),
     "serviceaccounts": ("", "v1", "ServiceAccount", "serviceaccount", True, ("sa",), ()),
+    "endpoints": ("", "v1", "Endpoints", "endpoints", True, ("ep",), ()),
+    "leases": ("coordination.k8s.io", "v1", "Lease", "lease", True, (), ()),
     "roles": ("rbac.authorization.k8s.io", "v1", "Role", "role", True, (), ()),
     "rolebindings": ("rbac.authorization.k8s.io", "v1", "RoleBinding", "rolebinding", True, (), ()),
     "clusterroles": ("rbac.authorization.k8s.io", "v1", "ClusterRole", "clusterrole", False, (), ()),

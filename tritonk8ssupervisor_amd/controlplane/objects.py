@@ -17,6 +17,7 @@ KIND_GROUPS = (("pods", "/api/v1"), ("services", "/api/v1"), ("events", "/api/v1
                ("statefulsets", "/apis/apps/v1"), ("replicasets", "/apis/apps/v1"),
                ("jobs", "/apis/batch/v1"), ("cronjobs", "/apis/batch/v1"), ("ingresses", "/apis/networking.k8s.io/v1"),
                ("horizontalpodautoscalers", "/apis/autoscaling/v2"), ("serviceaccounts", "/api/v1"),
+               ("endpoints", "/api/v1"), ("leases", "/apis/coordination.k8s.io/v1"),
                ("roles", "/apis/rbac.authorization.k8s.io/v1"), ("rolebindings", "/apis/rbac.authorization.k8s.io/v1"))
 # cluster-scoped kinds served through the generic handlers (namespace "")
 CLUSTER_KIND_GROUPS = (("clusterroles", "/apis/rbac.authorization.k8s.io/v1"),
