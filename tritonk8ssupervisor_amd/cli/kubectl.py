@@ -571,10 +571,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             print(f"{n} object(s) deleted")
         elif a.verb == "logs":
             path = k.k8s(object_path("pod", a.args[0], ns) + "/log")
-            text = k.get(path, query={"tailLines": a.tail or None, "container": a.container}, raw=True)
+            full = k.get(path, query={"container": a.container}, raw=True)  # one read: nothing slips between
+            text = "".join(full.splitlines(keepends=True)[-a.tail:]) if a.tail else full
             print(text, end="", flush=True)
             if a.follow:  # -f: print what the pod appends until it terminates
-                seen = len(k.get(path, query={"container": a.container}, raw=True))
+                seen = len(full)
                 while True:
                     phase = k.get(k.k8s(object_path("pod", a.args[0], ns))).get("status", {}).get("phase")
                     full = k.get(path, query={"container": a.container}, raw=True)

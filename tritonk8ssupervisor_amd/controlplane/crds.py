@@ -18,6 +18,8 @@ from .httpserver import HttpError, Request
 from .objects import _key
 
 CRD_KIND = "customresourcedefinitions"
+# built-in kinds with routes of their own (server._routes), never the generic ones
+_SPECIAL = {"nodes", "namespaces"}
 
 
 class CustomResources:
@@ -92,37 +94,60 @@ class CustomResources:
                           "conditions": [{"type": "NamesAccepted", "status": "True", "reason": "NoConflicts"},
                                          {"type": "Established", "status": "True", "reason": "InitialNamesAccepted"}]}
 
-    async def h_custom(self, req: Request, group: str, version: str, rest: str, pid: str | None = None):
-        """Every request under /apis/<group>/<version>/... that no built-in route took."""
+    def _handler(self, op: str, kind: str, flag: bool = False):
+        """The generic handler ``op`` of ``kind`` (k8s_api.py), made once."""
+        cache = self.__dict__.setdefault("_handlers", {})
+        h = cache.get((op, kind, flag))
+        if h is None:
+            h = {"list": lambda: self._lister(kind, all_ns=flag), "create": lambda: self._creator(kind),
+                 "get": lambda: self._getter(kind), "update": lambda: self._replacer(kind, flag),
+                 "delete": lambda: self._deleter(kind)}[op]()
+            cache[(op, kind, flag)] = h
+        return h
+
+    def _resolve(self, group: str, version: str, plural: str) -> tuple[str, bool, bool] | None:
+        """(store kind, namespaced, has a status subresource) of group/version/plural, or None."""
+        r = k8s_wire.RESOURCES.get(plural)
+        if r is not None and (r[0], r[1]) == (group, version) and plural not in _SPECIAL:
+            return plural, r[4], False
+        m = self._crds().get(f"{plural}.{group}") if group else None
+        if m is not None and version in m["versions"]:
+            return f"{plural}.{group}", m["namespaced"], m["status"]
+        return None
+
+    async def h_resource(self, req: Request, version: str, rest: str, group: str = "", pid: str | None = None):
+        """Every object path that no specific route took: ``[namespaces/<ns>/]<plural>[/<name>
+        [/status]]`` of a built-in kind or a custom resource."""
         parts = [x for x in rest.split("/") if x]
         ns = ""
         if len(parts) >= 3 and parts[0] == "namespaces":
             ns, parts = parts[1], parts[2:]
-        if not parts:
-            raise HttpError(404, f"the server could not find the requested resource ({group}/{version})")
-        kind = f"{parts[0]}.{group}"
-        m = self._crds().get(kind)
-        if m is None or version not in m["versions"]:
-            raise HttpError(404, f"the server could not find the requested resource ({parts[0]}.{group}/{version})")
-        if (m["namespaced"] and not ns and not (len(parts) == 1 and req.method == "GET")) or (not m["namespaced"] and ns):
-            raise HttpError(404, f"{parts[0]}.{group} is {'namespaced' if m['namespaced'] else 'cluster-scoped'}")
+        where = f"{group}/{version}" if group else version
+        if not parts or len(parts) > 3:
+            raise HttpError(404, f"the server could not find the requested resource ({where} {rest})")
+        hit = self._resolve(group, version, parts[0])
+        if hit is None:
+            raise HttpError(404, f"the server could not find the requested resource ({parts[0]} in {where})")
+        kind, namespaced, has_status = hit
+        if (namespaced and not ns and not (len(parts) == 1 and req.method == "GET")) or (not namespaced and ns):
+            raise HttpError(404, f"{parts[0]} is {'namespaced' if namespaced else 'cluster-scoped'}")
         name = parts[1] if len(parts) > 1 else None
         sub = parts[2] if len(parts) > 2 else None
-        if sub is not None and not (sub == "status" and m["status"]):
-            raise HttpError(404, f"no subresource {sub!r} on {parts[0]}.{group}")
+        if sub is not None and not (sub == "status" and has_status):
+            raise HttpError(404, f"the server could not find the requested resource ({parts[0]}/{sub})")
         if name is None:
             if req.method == "GET":
-                return await self._lister(kind, all_ns=not ns)(req, pid=pid, ns=ns or None)
+                return await self._handler("list", kind, not ns)(req, pid=pid, ns=ns or None)
             if req.method == "POST":
-                return await self._creator(kind)(req, ns=ns, pid=pid)
+                return await self._handler("create", kind)(req, ns=ns, pid=pid)
             raise HttpError(405, f"method {req.method} not allowed")
         if sub == "status":
             return await self._status_subresource(req, kind, ns, name, pid)
-        handler = {"GET": self._getter(kind), "PUT": self._replacer(kind, False), "PATCH": self._replacer(kind, True),
-                   "DELETE": self._deleter(kind)}.get(req.method)
-        if handler is None:
+        op = {"GET": ("get", False), "PUT": ("update", False), "PATCH": ("update", True), "DELETE": ("delete", False)}.get(
+            req.method)
+        if op is None:
             raise HttpError(405, f"method {req.method} not allowed")
-        return await handler(req, ns=ns, name=name, pid=pid)
+        return await self._handler(op[0], kind, op[1])(req, ns=ns, name=name, pid=pid)
 
     async def _status_subresource(self, req: Request, kind: str, ns: str, name: str, pid: str | None):
         """``/status`` of a custom resource: only ``status`` changes (a controller's update)."""

@@ -15,7 +15,7 @@ from pathlib import Path
 from ..utils.ids import token_hex
 from ..utils.net import host_port
 from ..utils.trace import trace
-from . import k8s_openapi, k8s_wire, ssa
+from . import k8s_wire
 from .httpserver import HttpError, Request, Response, StreamResponse
 from .store import now_iso
 from .objects import (
@@ -393,6 +393,9 @@ class KubernetesAPI:
     def _field_warnings(req: Request, kind: str, body) -> dict[str, str]:
         """``?fieldValidation=Strict`` -> 400 on unknown fields; ``Warn`` -> Warning headers."""
         mode = req.q("fieldValidation")
+        if not mode:
+            return {}
+        from . import k8s_openapi
         bad = k8s_openapi.check_fields(kind, body, mode)
         if not bad:
             return {}
@@ -444,6 +447,7 @@ class KubernetesAPI:
     async def _apply(self, req: Request, p: str, kind: str, ns: str, name: str):
         """Server-side apply (``PATCH`` + ``application/apply-patch+yaml``, ssa.py): create or merge
         the manager's configuration; 409 with one cause per conflicting field unless force=true."""
+        from . import ssa
         try:
             body = json.loads(req.body or b"{}")
         except ValueError:
@@ -836,6 +840,8 @@ class KubernetesAPI:
         elif kind == "ingresses":
             body["status"] = {"loadBalancer": {"ingress": [{"ip": self.advertise or self.host}]}}
         if manager and not keep_managed:
+            from . import ssa
+
             m = ssa.Managed(None, self._kind_meta(kind)[0])
             m.update(None, body, manager)
             md["managedFields"] = m.entries()
@@ -967,6 +973,8 @@ class KubernetesAPI:
             if old_mf:
                 md["managedFields"] = copy.deepcopy(old_mf)
             if manager:
+                from . import ssa
+
                 m = ssa.Managed(old_mf, self._kind_meta(kind)[0])
                 m.update(self._strip(cur), new, manager, subresource)
                 md["managedFields"] = m.entries()

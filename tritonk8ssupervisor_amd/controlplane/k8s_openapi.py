@@ -20,7 +20,6 @@ Reference: the reference's users pointed any kubectl at the cluster it printed
 """
 from __future__ import annotations
 
-import hashlib
 import json
 
 from . import k8s_wire
@@ -163,6 +162,8 @@ def gv_document(group: str, version: str) -> dict | None:
 
 
 def _hash(doc: dict) -> str:
+    import hashlib  # (the control plane's start-up path imports this module)
+
     return hashlib.sha512(json.dumps(doc, sort_keys=True).encode()).hexdigest()[:32].upper()
 
 

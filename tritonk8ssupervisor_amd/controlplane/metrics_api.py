@@ -22,7 +22,6 @@ from __future__ import annotations
 import math
 import time
 
-from ..utils import quantity
 from .httpserver import HttpError, Request
 from .objects import _key, _set_cond, labels_match
 
@@ -63,6 +62,8 @@ class MetricsAPI:
         return resource_list()
 
     async def h_node_metrics(self, req: Request, name: str | None = None, pid: str | None = None):
+        from ..utils import quantity
+
         p = self._pid(pid, req)
         items = []
         for node, m in sorted(self._node_samples(p).items()):
@@ -83,6 +84,8 @@ class MetricsAPI:
 
     async def h_pod_metrics(self, req: Request, ns: str | None = None, name: str | None = None,
                             pid: str | None = None):
+        from ..utils import quantity
+
         p = self._pid(pid, req)
         sel = req.q("labelSelector")
         from .objects import _parse_selector
@@ -111,6 +114,8 @@ class MetricsAPI:
 
     # ---- HorizontalPodAutoscaler ------------------------------------------------------------
     def _ctl_hpas(self, pid: str, now: float | None = None) -> None:
+        from ..utils import quantity
+
         now = time.time() if now is None else now
         samples = self._pod_samples(pid)
         if not hasattr(self, "_hpa_recs"):

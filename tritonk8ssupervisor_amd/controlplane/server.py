@@ -44,11 +44,11 @@ from pathlib import Path
 
 from ..utils.net import host_port
 from ..utils.trace import trace
-from . import k8s_openapi, k8s_wire
+from . import k8s_wire
 from .controllers import Controllers
 from .httpserver import HttpError, HttpServer, Request, Response, Router
 from .k8s_api import KubernetesAPI
-from .objects import CLUSTER_KIND_GROUPS, KIND_GROUPS, _cond, _key, _set_cond
+from .objects import _cond, _key, _set_cond
 from .rancher_api import RancherAPI
 from .scheduler import Scheduler
 from .workloads import Workloads
@@ -63,13 +63,6 @@ _KIND_PLURAL = {r[2]: plural for plural, r in k8s_wire.RESOURCES.items()}
 def _group_doc(group: str, versions: list[str]) -> dict:
     return {"name": group, "versions": [{"groupVersion": f"{group}/{v}", "version": v} for v in versions],
             "preferredVersion": {"groupVersion": f"{group}/{versions[0]}", "version": versions[0]}}
-
-
-def _cluster_scoped(h):
-    """A namespaced handler used for a cluster-scoped kind: its objects live in namespace ""."""
-    async def g(req, pid=None, **kw):
-        return await h(req, ns="", pid=pid, **kw)
-    return g
 
 
 class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Scheduler):
@@ -220,25 +213,9 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             add("PATCH", r"/api/v1/namespaces/(?P<name>[^/]+)", self.h_namespace_patch)
             add("DELETE", r"/api/v1/namespaces/(?P<name>[^/]+)", self.h_namespace_delete)
             add("GET", r"/api/v1/pods", self.h_pods)
-            for kind, grp in CLUSTER_KIND_GROUPS:
-                add("GET", grp + rf"/{kind}", self._lister(kind, all_ns=True))
-                add("POST", grp + rf"/{kind}", _cluster_scoped(self._creator(kind)))
-                add("GET", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._getter(kind)))
-                add("PUT", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._replacer(kind, False)))
-                add("PATCH", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._replacer(kind, True)))
-                add("DELETE", grp + rf"/{kind}/(?P<name>[^/]+)", _cluster_scoped(self._deleter(kind)))
-            for kind, grp in KIND_GROUPS:
-                add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._lister(kind))
-                add("POST", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}", self._creator(kind))
-                add("GET", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._getter(kind))
-                add("PUT", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._replacer(kind, False))
-                add("PATCH", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._replacer(kind, True))
-                add("DELETE", grp + rf"/namespaces/(?P<ns>[^/]+)/{kind}/(?P<name>[^/]+)", self._deleter(kind))
-                add("GET", grp + rf"/{kind}", self._lister(kind, all_ns=True))
             for method in ("GET", "PUT", "PATCH"):
-                for kind in ("deployments", "statefulsets", "replicasets"):
-                    add(method, rf"/apis/apps/v1/namespaces/(?P<ns>[^/]+)/(?P<kind>{kind})/(?P<name>[^/]+)/scale",
-                        self.h_scale)
+                add(method, r"/apis/apps/v1/namespaces/(?P<ns>[^/]+)/(?P<kind>deployments|statefulsets|replicasets)"
+                            r"/(?P<name>[^/]+)/scale", self.h_scale)
             add("PUT", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/status", self.h_pod_status)
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/log", self.h_pod_log)
             add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/exec", self.h_pod_exec)
@@ -247,8 +224,12 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/attach", self.h_pod_attach_ws)
             add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs", self.h_node_execs)
             add("PUT", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)", self.h_exec_result)
-            for method in ("GET", "POST", "PUT", "PATCH", "DELETE"):  # custom resources (crds.py): last
-                add(method, r"/apis/(?P<group>[^/]+)/(?P<version>[^/]+)/(?P<rest>.+)", self.h_custom)
+            # every other object path, built-in kinds (KIND_GROUPS, CLUSTER_KIND_GROUPS) and custom
+            # resources alike: two patterns resolved by plural (crds.h_resource), not a regex per
+            # kind -- fewer routes to compile at start-up and to scan per request
+            for method in ("GET", "POST", "PUT", "PATCH", "DELETE"):
+                add(method, r"/api/(?P<version>v1)/(?P<rest>.+)", self.h_resource)
+                add(method, r"/apis/(?P<group>[^/]+)/(?P<version>[^/]+)/(?P<rest>.+)", self.h_resource)
 
     # ---- Kubernetes discovery (k8s_wire.py) ----------------------------------------------
     @staticmethod
@@ -263,9 +244,13 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         return k8s_wire.api_versions(req.headers.get("host") or f"{self.host}:{self.port}")
 
     async def h_openapi_root(self, req: Request, pid: str | None = None):
+        from . import k8s_openapi
+
         return k8s_openapi.root(f"/r/projects/{pid}/kubernetes" if pid else "")
 
     async def h_openapi_gv(self, req: Request, gv: str, pid: str | None = None):
+        from . import k8s_openapi
+
         d = k8s_openapi.document(gv)
         if d is None:
             raise HttpError(404, f"no OpenAPI document for {gv}")

@@ -26,9 +26,7 @@ from __future__ import annotations
 
 import copy
 import time
-from datetime import datetime, timezone
 
-from . import cron
 from .objects import TERMINAL, _key, template_hash
 
 STS_POD_NAME = "statefulset.kubernetes.io/pod-name"
@@ -37,7 +35,9 @@ REVISION = "controller-revision-hash"
 SCHEDULED_AT = "batch.kubernetes.io/cronjob-scheduled-timestamp"
 
 
-def _ts(iso: str | None) -> datetime | None:
+def _ts(iso: str | None):
+    from datetime import datetime, timezone  # (off the control plane's start-up path)
+
     if not iso:
         return None
     try:
@@ -46,7 +46,9 @@ def _ts(iso: str | None) -> datetime | None:
         return None
 
 
-def _iso(t: datetime) -> str:
+def _iso(t) -> str:
+    from datetime import timezone
+
     return t.astimezone(timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
 
 
@@ -171,7 +173,11 @@ class Workloads:
         for pod in self._owned(pid, job):
             self.store.delete("pods", _key(pid, ns, pod["metadata"]["name"]))
 
-    def _ctl_cronjobs(self, pid: str, now: datetime | None = None) -> None:
+    def _ctl_cronjobs(self, pid: str, now=None) -> None:
+        from datetime import datetime, timezone
+
+        from . import cron
+
         now = now or datetime.now(timezone.utc)
         for cj in self.store.list("cronjobs", lambda o: self._in(pid, o)):
             ns, name = cj["metadata"]["namespace"], cj["metadata"]["name"]
