@@ -110,7 +110,8 @@ def api_resource_list(group: str, version: str) -> dict | None:
              "verbs": list(READ_ONLY.get(plural, VERBS))}
         if short:
             r["shortNames"] = list(short)
-        if plural in ("pods", "deployments", "daemonsets", "jobs", "services", "statefulsets", "replicasets", "cronjobs"):
+        if plural in ("pods", "deployments", "daemonsets", "jobs", "services", "statefulsets", "replicasets", "cronjobs",
+                      "horizontalpodautoscalers"):
             r["categories"] = ["all"]
         res.append(r)
         for s in subs:
