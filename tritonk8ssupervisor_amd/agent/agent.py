@@ -359,7 +359,6 @@ class Agent:
         key = f"{md['namespace']}/{md['name']}"
         if key in self.runtime.running():
             return
-        c = spec["containers"][0]
         all_gpus = md.get("annotations", {}).get(ALL_GPUS) == "true"
         need = len(self.plugin.devices()) if all_gpus else pod_gpus(pod)
         # (namespaces are DNS labels, so "<ns>_<name>" cannot collide with a default-namespace pod)
@@ -472,7 +471,6 @@ class Agent:
                                  log_name="log" if first_app else f"log.{cont.get('name') or n}"))
         pp = procs[len(inits)]
         pp.init, pp.sidecars = procs[:len(inits)], procs[len(inits) + 1:]
-        c = apps[0]
         self._pods_meta[key] = {"name": md["name"], "namespace": md["namespace"],
                                 "images": {x.get("name"): x.get("image") or "" for x in inits + apps},
                                 "validation": md.get("labels", {}).get(VALIDATION_LABEL) == "true",
