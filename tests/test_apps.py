@@ -484,3 +484,21 @@ def test_pods_call_the_api_with_their_service_account(cluster):
         "subjects": [{"kind": "ServiceAccount", "name": "reader", "namespace": "default"}]}))
     kc("apply", "-f", "rb.json")
     assert run("after") == ["pods", "200", "secrets", "403"]
+
+
+def test_kubectl_cp_both_ways(cluster, tmp_path_factory):
+    ws, env, kc, summary = cluster
+    (ws / "cp.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "store"},
+        "spec": {"containers": [{"name": "c", "image": "busybox", "command": ["sleep", "60"]}]}}))
+    kc("apply", "-f", "cp.json")
+    _until(lambda: json.loads(kc("get", "pod", "store", "-o", "json").stdout)["status"].get("phase") == "Running")
+    src = tmp_path_factory.mktemp("cpsrc")
+    (src / "data").mkdir()
+    (src / "data" / "weights.bin").write_bytes(bytes(range(256)) * 100)
+    (src / "data" / "cfg.txt").write_text("lr=3e-4\n")
+    kc("cp", str(src / "data"), "store:incoming")
+    r = kc("exec", "store", "--", "sh", "-c", "wc -c < incoming/weights.bin; cat incoming/cfg.txt")
+    assert r.stdout.split() == ["25600", "lr=3e-4"], r.stdout
+    back = tmp_path_factory.mktemp("cpback") / "out"
+    kc("cp", "store:incoming", str(back))
+    assert (back / "weights.bin").read_bytes() == bytes(range(256)) * 100 and (back / "cfg.txt").read_text() == "lr=3e-4\n"

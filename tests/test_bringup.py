@@ -904,6 +904,17 @@ def test_stock_kubectl_exec_over_websocket(ws, tmp_path_factory):
     q = "?command=cat&stdin=true&stdout=true"
     status, _, frames = _ws_exec(server.hostname, server.port, base + q, token, stdin=b"hello from stdin")
     assert (1, b"hello from stdin") in frames and json.loads(dict(frames)[3])["status"] == "Success", frames
+    # binary both ways, as `kubectl cp` streams tar archives: every byte value survives
+    blob = bytes(range(256)) * 4
+    status, _, frames = _ws_exec(server.hostname, server.port, base + q, token, stdin=blob)
+    assert b"".join(d for ch, d in frames if ch == 1) == blob, frames[:3]
+    q2 = "?command=sh&command=-c&command=mkdir+-p+t%3B+printf+%27%5C000%5C377%27+%3E+t%2Fb%3B+tar+cf+-+t&stdout=true"
+    status, _, frames = _ws_exec(server.hostname, server.port, base + q2, token)
+    import io
+    import tarfile
+
+    tar = tarfile.open(fileobj=io.BytesIO(b"".join(d for ch, d in frames if ch == 1)))
+    assert tar.extractfile("t/b").read() == b"\x00\xff"
     # no token, no exec
     status, _, _ = _ws_exec(server.hostname, server.port, base + q, "wrong")
     assert status.startswith("HTTP/1.1 401"), status

@@ -732,14 +732,20 @@ class Agent:
             env = dict(pp.env)
             if self.runtime.tool_dirs:
                 env["PATH"] = os.pathsep.join(self.runtime.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
+            import base64
+
+            # bytes both ways (kubectl cp streams tar archives through exec)
+            stdin = base64.b64decode(x["stdin_b64"]) if x.get("stdin_b64") else str(x.get("stdin", "")).encode()
             try:
-                r = subprocess.run(container_exec_argv(pp, list(x["command"])), input=x.get("stdin", ""), env=env,
-                                   cwd=pp.dir, capture_output=True, text=True, timeout=float(x.get("timeoutSeconds", 60)))
-                res = {"stdout": r.stdout, "stderr": r.stderr, "exitCode": r.returncode}
+                r = subprocess.run(container_exec_argv(pp, list(x["command"])), input=stdin, env=env, cwd=pp.dir,
+                                   capture_output=True, timeout=float(x.get("timeoutSeconds", 60)))
+                res = {"stdout_b64": base64.b64encode(r.stdout).decode(), "stderr_b64": base64.b64encode(r.stderr).decode(),
+                       "exitCode": r.returncode}
             except FileNotFoundError as e:
                 res = {"stdout": "", "stderr": f"exec: {e}\n", "exitCode": 127}
             except subprocess.TimeoutExpired as e:
-                res = {"stdout": e.stdout or "", "stderr": f"exec: timed out after {e.timeout}s\n", "exitCode": 124}
+                res = {"stdout_b64": base64.b64encode(e.stdout or b"").decode(),
+                       "stderr": f"exec: timed out after {e.timeout}s\n", "exitCode": 124}
         try:
             self.api.put(self.api.k8s(f"/api/v1/nodes/{self.name}/execs/{xid}"), res)
         except (ApiError, OSError) as e:

@@ -185,6 +185,58 @@ def _target(args: list[str]) -> tuple[str, str]:
     return args[0], args[1]
 
 
+def _cp(k, ns: str, args: list[str], container: str | None = None) -> int:
+    """``kubectl cp SRC DST`` with one side ``[namespace/]pod:path``: a tar archive through exec,
+    as kubectl does (the pod needs ``tar``)."""
+    import base64
+    import io
+    import posixpath
+    import tarfile
+
+    if len(args) != 2 or sum(":" in x for x in args) != 1:
+        raise SystemExit("usage: kubectl cp LOCAL POD:PATH | kubectl cp POD:PATH LOCAL")
+    src, dst = args
+
+    def pod_side(spec: str) -> tuple[str, str, str]:
+        who, path = spec.split(":", 1)
+        pns, pod = who.split("/", 1) if "/" in who else (ns, who)
+        return pns, pod, path
+
+    def run(pns: str, pod: str, cmd: list[str], stdin: bytes = b"") -> dict:
+        r = k.post(k.k8s(object_path("pod", pod, pns) + "/exec"), {
+            "command": cmd, "stdin_b64": base64.b64encode(stdin).decode(), "binary": True, "timeoutSeconds": 600},
+            timeout=660)
+        if r.get("exitCode", 1) != 0:
+            raise SystemExit(f"error: {' '.join(cmd)}: {r.get('stderr', '').strip()}")
+        return r
+
+    if ":" in dst:  # local -> pod
+        pns, pod, path = pod_side(dst)
+        buf = io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w") as t:
+            t.add(src, arcname=posixpath.basename(path.rstrip("/")) or Path(src).name)
+        run(pns, pod, ["tar", "xf", "-", "-C", posixpath.dirname(path.rstrip("/")) or "."], buf.getvalue())
+    else:  # pod -> local
+        pns, pod, path = pod_side(src)
+        r = run(pns, pod, ["tar", "cf", "-", "-C", posixpath.dirname(path.rstrip("/")) or ".",
+                           posixpath.basename(path.rstrip("/"))])
+        with tarfile.open(fileobj=io.BytesIO(base64.b64decode(r["stdout_b64"]))) as t:
+            for m in t.getmembers():  # never outside the destination
+                if m.name.startswith("/") or ".." in Path(m.name).parts or m.issym() or m.islnk():
+                    raise SystemExit(f"error: refusing archive member {m.name!r}")
+            base = posixpath.basename(path.rstrip("/"))
+            out = Path(dst)
+            for m in t.getmembers():
+                rel = Path(m.name).relative_to(base) if m.name != base else Path()
+                target = out / rel
+                if m.isdir():
+                    target.mkdir(parents=True, exist_ok=True)
+                elif m.isfile():
+                    target.parent.mkdir(parents=True, exist_ok=True)
+                    target.write_bytes(t.extractfile(m).read())
+    return 0
+
+
 def _rollout_history(k, name: str, ns: str, sub: str, to_revision: int = 0) -> int:
     """``rollout history`` lists the Deployment's revisions (its ReplicaSets); ``rollout undo``
     puts the template of the previous revision (or ``--to-revision``) back, as kubectl does."""
@@ -604,6 +656,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
 
             what, name = _target(a.args) if "/" in (a.args[0] if a.args else "") else ("pod", (a.args or [""])[0])
             return attach(k, ns, name)
+        elif a.verb == "cp":
+            return _cp(k, ns, a.args, a.container)
         elif a.verb in ("cordon", "uncordon"):
             k.request("PATCH", k.k8s(f"/api/v1/nodes/{a.args[0]}"), body={"spec": {"unschedulable": a.verb == "cordon"}})
             print(f"node/{a.args[0]} {a.verb}ed")

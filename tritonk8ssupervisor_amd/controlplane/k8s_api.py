@@ -1091,9 +1091,20 @@ class KubernetesAPI:
         if not isinstance(cmd, list) or not cmd:
             raise HttpError(422, "command must be a non-empty list")
         timeout = min(float(body.get("timeoutSeconds", 60)), 600.0)
-        return await self._run_exec(p, ns, name, cmd, str(body.get("stdin", "")), timeout)
+        import base64
 
-    async def _run_exec(self, p: str, ns: str, name: str, cmd: list[str], stdin: str, timeout: float) -> dict:
+        stdin = base64.b64decode(body["stdin_b64"]) if body.get("stdin_b64") else str(body.get("stdin", ""))
+        r = await self._run_exec(p, ns, name, cmd, stdin, timeout)
+        out = {"stdout": r["stdout"], "stderr": r["stderr"], "exitCode": r["exitCode"]}
+        if body.get("binary"):  # the exact bytes too (kubectl cp)
+            out["stdout_b64"] = base64.b64encode(r["stdout_bytes"]).decode()
+        return out
+
+    async def _run_exec(self, p: str, ns: str, name: str, cmd: list[str], stdin, timeout: float) -> dict:
+        """Run ``cmd`` in the pod through its node agent; ``stdin`` str or bytes. The result has the
+        output as text (``stdout``/``stderr``) and as bytes (``stdout_bytes``/``stderr_bytes``)."""
+        import base64
+
         pod = self.store.get("pods", _key(p, ns, name))
         if pod is None:
             raise HttpError(404, f'pod "{name}" not found')
@@ -1103,8 +1114,10 @@ class KubernetesAPI:
         xid = f"x{self._seq:x}"
         node = pod["spec"]["nodeName"]
         key = _key(p, node, xid)
+        raw = stdin if isinstance(stdin, (bytes, bytearray)) else str(stdin or "").encode()
         self.store.put("execs", key, {"metadata": {"name": xid}, "_project": p, "node": node, "pod": name,
-                                      "namespace": ns, "command": [str(c) for c in cmd], "stdin": stdin,
+                                      "namespace": ns, "command": [str(c) for c in cmd],
+                                      "stdin_b64": base64.b64encode(raw).decode(),
                                       "timeoutSeconds": timeout, "status": {"phase": "Pending"}})
         done = await self.store.wait_until(
             lambda: (self.store.get("execs", key) or {}).get("status", {}).get("phase") == "Done", timeout + 10)
@@ -1112,7 +1125,11 @@ class KubernetesAPI:
         if not done:
             raise HttpError(504, f"exec in {name}: no result from node {node} within {timeout:.0f}s")
         st = x.get("status", {})
-        return {"stdout": st.get("stdout", ""), "stderr": st.get("stderr", ""), "exitCode": st.get("exitCode", 1)}
+        out = {}
+        for f in ("stdout", "stderr"):
+            b = base64.b64decode(st[f + "_b64"]) if st.get(f + "_b64") else str(st.get(f, "")).encode()
+            out[f], out[f + "_bytes"] = b.decode(errors="replace"), b
+        return {**out, "exitCode": st.get("exitCode", 1)}
 
     async def h_pod_exec_ws(self, req: Request, ns: str, name: str, pid: str | None = None):
         """A stock ``kubectl exec`` (Kubernetes >= 1.29 clients): GET .../pods/NAME/exec?command=..
@@ -1140,16 +1157,17 @@ class KubernetesAPI:
                     if msg[:1] == b"\x00":
                         data += msg[1:]
             try:
-                r = await self._run_exec(p, ns, name, cmd, data.decode(errors="replace"), 600.0)
+                r = await self._run_exec(p, ns, name, cmd, data, 600.0)
             except HttpError as e:
                 status = {"metadata": {}, "status": "Failure", "message": e.message, "reason": "InternalError",
                           "code": e.status}
                 await ws.send(b"\x03" + json.dumps(status).encode())
                 return
-            if r["stdout"] and req.q("stdout", "true") != "false":
-                await ws.send(b"\x01" + r["stdout"].encode())
-            if r["stderr"] and req.q("stderr", "true") != "false":
-                await ws.send(b"\x02" + r["stderr"].encode())
+            for ch, f in ((b"\x01", "stdout"), (b"\x02", "stderr")):
+                data = r[f + "_bytes"]
+                if data and req.q(f, "true") != "false":
+                    for i in range(0, len(data), 1 << 20):  # frames of at most 1 MiB
+                        await ws.send(ch + data[i:i + (1 << 20)])
             if r["exitCode"] == 0:
                 status = {"metadata": {}, "status": "Success"}
             else:
@@ -1344,8 +1362,10 @@ class KubernetesAPI:
         p = self._pid(pid, req)
         self._node_secret_ok(req, _key(p, node))
         body = req.json()
+        limit = 96 << 20  # base64 of 64 MiB: a kubectl cp of a large directory still fits
         x = self.store.patch("execs", _key(p, node, xid), lambda o: o["status"].update(
             phase="Done", stdout=str(body.get("stdout", ""))[-1 << 20:], stderr=str(body.get("stderr", ""))[-1 << 20:],
+            stdout_b64=str(body.get("stdout_b64", ""))[:limit], stderr_b64=str(body.get("stderr_b64", ""))[-(1 << 22):],
             exitCode=int(body.get("exitCode", 1))))
         if x is None:
             raise HttpError(404, f"exec {xid} not found (timed out?)")
