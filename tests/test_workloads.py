@@ -474,3 +474,59 @@ def test_endpoints_follow_ready_pods_and_leases_are_plain_objects(cp):
     lease = cp.create("1a1", "leases", "default", {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
                                                    "metadata": {"name": "leader"}, "spec": {"holderIdentity": "op-1"}})
     assert lease["kind"] == "Lease" and lease["spec"]["holderIdentity"] == "op-1"
+
+
+def _nodes(cp, n=3, gpus=0):
+    for i in range(1, n + 1):
+        cp.store.put("nodes", _key("1a1", f"kubenode{i}"), {"_project": "1a1", "metadata": {
+            "name": f"kubenode{i}", "labels": {"kubernetes.io/hostname": f"kubenode{i}", "zone": "a" if i < 3 else "b"}},
+            "spec": {}, "status": {"allocatable": {"amd.com/gpu": str(gpus)}, "conditions": [
+                {"type": "Ready", "status": "True"}, {"type": "AMDGPUValidated", "status": "True"}]}})
+
+
+def _node_of(cp, name):
+    return cp.store.get("pods", _key("1a1", "default", name))["spec"].get("nodeName")
+
+
+def test_taints_tolerations_and_node_affinity(cp):
+    _nodes(cp)
+    cp.store.patch("nodes", _key("1a1", "kubenode1"), lambda o: o["spec"].update(
+        taints=[{"key": "dedicated", "value": "train", "effect": "NoSchedule"}]))
+    cp.store.patch("nodes", _key("1a1", "kubenode2"), lambda o: o["spec"].update(
+        taints=[{"key": "maint", "effect": "NoSchedule"}]))
+    pod = lambda name, **spec: {"metadata": {"name": name}, "spec": {"containers": [{"name": "c", "command": ["true"]}], **spec}}
+    cp.create("1a1", "pods", "default", pod("plain"))
+    assert _node_of(cp, "plain") == "kubenode3"  # the only untainted node
+    cp.create("1a1", "pods", "default", pod("trainer", tolerations=[{"key": "dedicated", "operator": "Equal",
+                                                                      "value": "train", "effect": "NoSchedule"}],
+                                            affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                                                "nodeSelectorTerms": [{"matchExpressions": [{"key": "zone", "operator": "In",
+                                                                                             "values": ["a"]}]}]}}}))
+    assert _node_of(cp, "trainer") == "kubenode1"  # zone a, and kubenode2's taint is not tolerated
+    cp.create("1a1", "pods", "default", pod("nowhere", affinity={"nodeAffinity": {
+        "requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [{"matchFields": [
+            {"key": "metadata.name", "operator": "In", "values": ["kubenode2"]}]}]}}}))
+    p = cp.store.get("pods", _key("1a1", "default", "nowhere"))
+    assert not p["spec"].get("nodeName") and "untolerated taint" in p["status"]["conditions"][0]["message"]
+    cp.create("1a1", "pods", "default", pod("anything", tolerations=[{"operator": "Exists"}], affinity={"nodeAffinity": {
+        "requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [{"matchFields": [
+            {"key": "metadata.name", "operator": "In", "values": ["kubenode2"]}]}]}}}))
+    assert _node_of(cp, "anything") == "kubenode2"
+
+
+def test_pod_anti_affinity_spreads_ranks_one_per_node(cp):
+    _nodes(cp)
+    cp.create("1a1", "statefulsets", "default", _sts(4, podManagementPolicy="Parallel", template={
+        "metadata": {"labels": {"app": "web"}},
+        "spec": {"containers": [{"name": "c", "command": ["sleep", "60"]}],
+                 "affinity": {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                     {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "kubernetes.io/hostname"}]}}}}))
+    placed = [_node_of(cp, f"web-{i}") for i in range(4)]
+    assert sorted(n for n in placed if n) == ["kubenode1", "kubenode2", "kubenode3"] and placed.count(None) == 1
+    # co-location: a pod that wants to be next to web-0
+    cp.create("1a1", "pods", "default", {"metadata": {"name": "sidecar"}, "spec": {
+        "containers": [{"name": "c", "command": ["true"]}],
+        "affinity": {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+            {"labelSelector": {"matchExpressions": [{"key": "statefulset.kubernetes.io/pod-name", "operator": "In",
+                                                     "values": ["web-0"]}]}, "topologyKey": "kubernetes.io/hostname"}]}}}})
+    assert _node_of(cp, "sidecar") == _node_of(cp, "web-0")

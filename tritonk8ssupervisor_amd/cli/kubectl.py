@@ -656,6 +656,22 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
 
             what, name = _target(a.args) if "/" in (a.args[0] if a.args else "") else ("pod", (a.args or [""])[0])
             return attach(k, ns, name)
+        elif a.verb == "taint":
+            # kubectl taint nodes NAME key[=value]:Effect ... (a trailing "-" removes the taint)
+            what, name = _target(a.args)
+            if kind_key(what) != "node":
+                raise SystemExit("usage: kubectl taint nodes NAME key[=value]:Effect[-] ...")
+            node = k.get(k.k8s(f"/api/v1/nodes/{name}"))
+            taints = list((node.get("spec") or {}).get("taints") or [])
+            for spec in (a.args[1:] if "/" in a.args[0] else a.args[2:]):
+                remove = spec.endswith("-")
+                kv, _, effect = spec.rstrip("-").partition(":")
+                key, _, value = kv.partition("=")
+                taints = [t for t in taints if not (t.get("key") == key and (not effect or t.get("effect") == effect))]
+                if not remove:
+                    taints.append({"key": key, **({"value": value} if value else {}), "effect": effect or "NoSchedule"})
+            k.request("PATCH", k.k8s(f"/api/v1/nodes/{name}"), body={"spec": {"taints": taints}})
+            print(f"node/{name} {'untainted' if all(s.endswith('-') for s in a.args[1:]) else 'tainted'}")
         elif a.verb == "cp":
             return _cp(k, ns, a.args, a.container)
         elif a.verb in ("cordon", "uncordon"):

@@ -53,6 +53,12 @@ class Scheduler:
                 for cn, g in pod_claims(o).items():
                     used[cn] = used.get(cn, 0) + g
                     count[cn] = count.get(cn, 0) + 1
+        # taints, node affinity, inter-pod (anti-)affinity (placement.py): only when something asks
+        rules = any((n.get("spec") or {}).get("taints") for n in nodes) or any(
+            p["spec"].get("affinity") or p["spec"].get("tolerations") for p in pending)
+        by_name = {n["metadata"]["name"]: n for n in nodes}
+        bound = [o for o in self.store.list("pods", lambda o: self._in(pid, o))
+                 if o["spec"].get("nodeName") and o.get("status", {}).get("phase") not in TERMINAL] if rules else []
         for pod in sorted(pending, key=lambda o: o["metadata"]["name"]):
             need = pod_gpus(pod)
             sel = pod["spec"].get("nodeSelector")
@@ -67,6 +73,7 @@ class Scheduler:
                 self._schedule_host_scoped(pid, pod, key, need, sel, nodes, used, count)
                 continue
             best = None
+            why: dict[str, int] = {}
             for n in nodes:
                 nn = n["metadata"]["name"]
                 free = int(n["status"]["allocatable"].get(GPU, 0)) - used.get(nn, 0)
@@ -74,15 +81,27 @@ class Scheduler:
                     continue
                 if need and not node_validated(n):
                     continue  # GPU pods only land on validated nodes
-                score = (count.get(nn, 0), -free, nn)
+                pref = 0
+                if rules:
+                    from . import placement
+
+                    no = placement.feasible(pod, n, by_name, bound)
+                    if no:
+                        why[no] = why.get(no, 0) + 1
+                        continue
+                    pref = placement.score(pod, n, by_name, bound)
+                score = (-pref, count.get(nn, 0), -free, nn)
                 if best is None or score < best[0]:
                     best = (score, nn, free)
             if best is None:
-                self._unschedulable(pod, key, f"0/{len(nodes)} nodes available: need {need} {GPU}")
+                extra = "".join(f", {c} node(s) excluded by {w}" for w, c in sorted(why.items()))
+                self._unschedulable(pod, key, f"0/{len(nodes)} nodes available: need {need} {GPU}{extra}")
                 continue
             nn = best[1]
             used[nn] = used.get(nn, 0) + need
             count[nn] = count.get(nn, 0) + 1
+            if rules:  # what the next pods of this pass see (anti-affinity spreads replicas at once)
+                bound.append({**pod, "spec": {**pod["spec"], "nodeName": nn}})
             for c in claims:  # WaitForFirstConsumer: the first pod's node holds the claim's data
                 self.store.patch("persistentvolumeclaims", _key(pid, pod["metadata"]["namespace"], c),
                                  lambda o, nn=nn: o["metadata"].setdefault("annotations", {}).setdefault(SELECTED_NODE, nn))
