@@ -530,3 +530,46 @@ def test_pod_anti_affinity_spreads_ranks_one_per_node(cp):
             {"labelSelector": {"matchExpressions": [{"key": "statefulset.kubernetes.io/pod-name", "operator": "In",
                                                      "values": ["web-0"]}]}, "topologyKey": "kubernetes.io/hostname"}]}}}})
     assert _node_of(cp, "sidecar") == _node_of(cp, "web-0")
+
+
+def test_resource_quota_caps_a_namespaces_gpus(cp):
+    _nodes(cp, 2, gpus=4)
+    cp.create("1a1", "resourcequotas", "team", {"metadata": {"name": "gpus"}, "spec": {"hard": {
+        "requests.amd.com/gpu": "3", "pods": "4", "requests.cpu": "2"}}})
+    pod = lambda name, gpus=0, cpu=None: {"metadata": {"name": name}, "spec": {"containers": [{
+        "name": "c", "command": ["true"], "resources": {"limits": {"amd.com/gpu": str(gpus), **({"cpu": cpu} if cpu else {})}}}]}}
+    cp.create("1a1", "pods", "team", pod("a", 2))
+    with pytest.raises(HttpError) as e:
+        cp.create("1a1", "pods", "team", pod("b", 2))
+    assert e.value.status == 403 and "exceeded quota: gpus" in e.value.message and "requests.amd.com/gpu" in e.value.message
+    cp.create("1a1", "pods", "team", pod("c", 1, cpu="1500m"))
+    with pytest.raises(HttpError) as e:
+        cp.create("1a1", "pods", "team", pod("d", 0, cpu="1"))  # cpu: 1.5 + 1 > 2
+    assert "requests.cpu" in e.value.message
+    cp.create("1a1", "pods", "other", pod("free", 4))  # other namespaces are not limited
+    st = cp.store.get("resourcequotas", _key("1a1", "team", "gpus"))["status"]
+    assert st["used"] == {"requests.amd.com/gpu": "3", "pods": "2", "requests.cpu": "1.5"}
+    # a finished pod no longer counts
+    cp.store.patch("pods", _key("1a1", "team", "a"), lambda o: o["status"].update(phase="Succeeded"))
+    cp.create("1a1", "pods", "team", pod("b", 2))
+
+
+def test_quota_holds_back_controller_pods_until_it_allows_them(cp):
+    _nodes(cp, 1, gpus=8)
+    cp.create("1a1", "resourcequotas", "default", {"metadata": {"name": "gpus"}, "spec": {"hard": {"requests.amd.com/gpu": "2"}}})
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "inf"}, "spec": {
+        "replicas": 3, "selector": {"matchLabels": {"app": "inf"}},
+        "template": {"metadata": {"labels": {"app": "inf"}}, "spec": {"containers": [
+            {"name": "c", "command": ["true"], "resources": {"limits": {"amd.com/gpu": "1"}}}]}}}})
+    pods = [cp.store.get("pods", _key("1a1", "default", n)) for n in _pods(cp, "inf-")]
+    assert len(pods) == 3
+    bound = [p for p in pods if p["spec"].get("nodeName")]
+    held = [p for p in pods if not p["spec"].get("nodeName")]
+    assert len(bound) == 2 and len(held) == 1 and held[0]["status"]["conditions"][0]["reason"] == "ExceededQuota"
+    assert any(e["reason"] == "FailedCreate" for e in cp.store.list("events"))
+    # raising the quota lets the held pod through
+    body = json.loads(json.dumps(cp._strip(cp.store.get("resourcequotas", _key("1a1", "default", "gpus")))))
+    body["spec"]["hard"]["requests.amd.com/gpu"] = "3"
+    cp.replace("1a1", "resourcequotas", "default", "gpus", body)
+    assert cp.store.get("pods", _key("1a1", "default", held[0]["metadata"]["name"]))["spec"].get("nodeName") == "kubenode1"
+    assert cp.store.get("resourcequotas", _key("1a1", "default", "gpus"))["status"]["used"] == {"requests.amd.com/gpu": "3"}

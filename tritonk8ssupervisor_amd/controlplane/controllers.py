@@ -33,6 +33,7 @@ class Controllers:
                     self._ctl_statefulsets(pid)
                     self._ctl_replicasets(pid)
                     self._ctl_endpoints(pid)
+                    self._ctl_quotas(pid)
                     self._ctl_validation(pid)
                     self._scheduler(pid)
                 if not self._again:
@@ -57,6 +58,14 @@ class Controllers:
         pod = {"kind": "Pod", "apiVersion": "v1", "metadata": md, "spec": spec, "_project": pid,
                "status": {"phase": "Pending", "conditions": []}}
         spec.setdefault("restartPolicy", "Always")
+        why = self._quota_block(pid, ns, name, pod)
+        if why:  # as the ReplicaSet controller's 403: the pod waits (unscheduled) until the quota allows it
+            from .objects import QUOTA_BLOCKED
+
+            md.setdefault("annotations", {})[QUOTA_BLOCKED] = "true"
+            _set_cond(pod, "PodScheduled", "False", "ExceededQuota", why)
+            self._event(pid, ns, {"kind": owner_kind, "name": owner["metadata"]["name"]}, "FailedCreate",
+                        f"Error creating: pods \"{name}\" is forbidden: {why}", "Warning")
         return self.store.put("pods", _key(pid, ns, name), pod)
 
     def _owned(self, pid: str, owner: dict) -> list[dict]:
@@ -343,3 +352,23 @@ class Controllers:
         for ep in self.store.list("endpoints", lambda o: self._in(pid, o)):
             if (ep["metadata"]["namespace"], ep["metadata"]["name"]) not in wanted:
                 self.store.delete("endpoints", _key(pid, ep["metadata"]["namespace"], ep["metadata"]["name"]))
+
+    def _ctl_quotas(self, pid: str) -> None:
+        """ResourceQuota status: ``hard`` echoed, ``used`` summed over the namespace's live pods."""
+        quotas = self.store.list("resourcequotas", lambda o: self._in(pid, o))
+        if not quotas:
+            return
+        from .objects import _fmt, pod_usage
+
+        for q in quotas:
+            ns = q["metadata"]["namespace"]
+            used: dict[str, float] = {}
+            for o in self.store.list("pods", lambda o, ns=ns: self._in(pid, o) and o["metadata"].get("namespace") == ns):
+                if o.get("status", {}).get("phase") not in TERMINAL:
+                    for k, v in pod_usage(o).items():
+                        used[k] = used.get(k, 0.0) + v
+            hard = (q.get("spec") or {}).get("hard") or {}
+            status = {"hard": dict(hard), "used": {r: _fmt(used.get("pods" if r == "count/pods" else r, 0.0)) for r in hard}}
+            if q.get("status") != status:
+                self.store.patch("resourcequotas", _key(pid, ns, q["metadata"]["name"]),
+                                 lambda o, s=status: o.__setitem__("status", s))

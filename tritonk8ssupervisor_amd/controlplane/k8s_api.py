@@ -742,6 +742,34 @@ class KubernetesAPI:
             raise HttpError(422, f'{kind} "{name}" is invalid: spec.template.metadata.labels: Invalid value: '
                                  "`selector` does not match template `labels`")
 
+    def _quota_block(self, pid: str, ns: str, name: str, pod: dict) -> str | None:
+        """Why ``pod`` would take its namespace past a ResourceQuota's ``hard`` (pods, amd.com/gpu,
+        cpu/memory requests/limits), or None. Live pods count, but not ones held back by a quota."""
+        quotas = self.store.list("resourcequotas", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns)
+        if not quotas:
+            return None
+        from .objects import QUOTA_BLOCKED, pod_usage, quota_excess
+
+        add = pod_usage(pod)
+        used: dict[str, float] = {}
+        for o in self.store.list("pods", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns):
+            if o["metadata"]["name"] == name or (o["metadata"].get("annotations") or {}).get(QUOTA_BLOCKED):
+                continue
+            if o.get("status", {}).get("phase") not in ("Succeeded", "Failed"):
+                for k2, v in pod_usage(o).items():
+                    used[k2] = used.get(k2, 0.0) + v
+        for q in quotas:
+            bad = quota_excess((q.get("spec") or {}).get("hard") or {}, used, add)
+            if bad:
+                return f'exceeded quota: {q["metadata"]["name"]}, ' + "; ".join(bad)
+        return None
+
+    def _admit_quota(self, pid: str, ns: str, name: str, pod: dict) -> None:
+        """ResourceQuota admission of a pod a client creates: refused, as the API server does."""
+        why = self._quota_block(pid, ns, name, pod)
+        if why:
+            raise HttpError(403, f'pods "{name}" is forbidden: {why}')
+
     @staticmethod
     def _admit_pvc(name: str, body: dict) -> None:
         """A claim is bound at once to a node-local volume of the ``tk8s-local`` class; the node is
@@ -800,6 +828,7 @@ class KubernetesAPI:
             spec = body.setdefault("spec", {})
             if not spec.get("containers"):
                 raise HttpError(422, "spec.containers is required")
+            self._admit_quota(pid, ns, name, body)
             spec.setdefault("restartPolicy", "Always")
             body["status"] = {"phase": "Pending", "conditions": []}
         elif kind in ("daemonsets", "deployments", "jobs", "statefulsets", "replicasets"):

@@ -43,6 +43,7 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
                                  ("hpa",), ()),
     "serviceaccounts": ("", "v1", "ServiceAccount", "serviceaccount", True, ("sa",), ()),
     "endpoints": ("", "v1", "Endpoints", "endpoints", True, ("ep",), ()),
+    "resourcequotas": ("", "v1", "ResourceQuota", "resourcequota", True, ("quota",), ()),
     "leases": ("coordination.k8s.io", "v1", "Lease", "lease", True, (), ()),
     "roles": ("rbac.authorization.k8s.io", "v1", "Role", "role", True, (), ()),
     "rolebindings": ("rbac.authorization.k8s.io", "v1", "RoleBinding", "rolebinding", True, (), ()),

@@ -16,7 +16,9 @@ from __future__ import annotations
 
 import json
 
-from .objects import GPU, TERMINAL, _key, _cond, _set_cond, node_ready, node_validated, pod_gpus, labels_match
+from .objects import (
+    GPU, QUOTA_BLOCKED, TERMINAL, _key, _cond, _set_cond, node_ready, node_validated, pod_gpus, labels_match,
+)
 
 GPU_SCOPE = "tk8s.amd.com/gpu-scope"
 HOST_LABEL = "tk8s.amd.com/host"
@@ -63,6 +65,11 @@ class Scheduler:
             need = pod_gpus(pod)
             sel = pod["spec"].get("nodeSelector")
             key = _key(pid, pod["metadata"]["namespace"], pod["metadata"]["name"])
+            if (pod["metadata"].get("annotations") or {}).get(QUOTA_BLOCKED):
+                why = self._quota_block(pid, pod["metadata"]["namespace"], pod["metadata"]["name"], pod)
+                if why:
+                    continue  # still over its namespace's quota
+                self.store.patch("pods", key, lambda o: o["metadata"]["annotations"].pop(QUOTA_BLOCKED, None))
             claims, pinned, missing = self._pod_claims_nodes(pid, pod)
             if missing:
                 self._unschedulable(pod, key, f'persistentvolumeclaim "{missing}" not found')
