@@ -288,9 +288,20 @@ def test_state_snapshot_survives_restart(tmp_path):
 
 def test_metrics_and_version(cp):
     proj = _env(cp)
-    _join(cp, proj["id"], "kubenode1", ngpu=1)
+    nc, _ = _join(cp, proj["id"], "kubenode1", ngpu=1)
+    # a heartbeat with GPU telemetry (AMD SMI) and a usage sample, as the agent sends them
+    nc.put(nc.k8s("/api/v1/nodes/kubenode1/status"), {"devices": [{"id": "gpu0", "health": "Healthy", "pciBusId": "0000:75:00.0",
+        "telemetry": {"temp_c": {"hotspot": 41}, "power": {"current_w": 212.5}, "vram_used_bytes": 1 << 30,
+                      "activity": {"gfx_pct": 87, "umc_pct": 40}, "ecc": {"uncorrectable": 0, "correctable": 2}}}],
+        "metrics": {"pods": {"default/train": [{"name": "c", "cpu_cores": 0.5, "memory_bytes": 1024, "gpu_pct": 87.0}]}}})
     text = cp.get("/metrics", raw=True)
     assert "tk8s_nodes" in text
+    for line in ('tk8s_gpu_gfx_activity_percent{node="kubenode1",gpu="gpu0",pci="0000:75:00.0"} 87',
+                 'tk8s_gpu_power_watts{node="kubenode1",gpu="gpu0",pci="0000:75:00.0"} 212.5',
+                 'tk8s_gpu_healthy{node="kubenode1",gpu="gpu0",pci="0000:75:00.0"} 1',
+                 'tk8s_gpu_ecc_correctable_total{node="kubenode1",gpu="gpu0",pci="0000:75:00.0"} 2',
+                 'tk8s_container_gpu_busy_percent{namespace="default",pod="train",container="c",node="kubenode1"} 87.0'):
+        assert line in text, line
     assert "version" in json.dumps(cp.get("/version")).lower()
 
 

@@ -311,8 +311,47 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         now = time.monotonic()
         for k, t in self.leases.items():
             lines.append(f'tk8s_node_heartbeat_age_seconds{{node="{k}"}} {now - t:.3f}')
+        lines += self._gpu_metric_lines()
         lines.append(f"tk8s_store_resource_version {self.store.rv}")
         return Response(200, "\n".join(lines) + "\n", content_type="text/plain; version=0.0.4")
+
+    def _gpu_metric_lines(self) -> list[str]:
+        """Per-GPU telemetry (AMD SMI, as the nodes report it), validation results and pod usage,
+        in the Prometheus text format -- what a device-metrics exporter would scrape."""
+        out = []
+        for n in self.store.list("nodes"):
+            node = n["metadata"]["name"]
+            ann = n["metadata"].get("annotations") or {}
+            for d in n.get("status", {}).get("devices") or []:
+                lab = f'node="{node}",gpu="{d.get("id")}",pci="{d.get("pciBusId", "")}"'
+                out.append(f"tk8s_gpu_healthy{{{lab}}} {1 if d.get('health') == 'Healthy' else 0}")
+                t = d.get("telemetry") or {}
+                for name, v in (("temperature_hotspot_celsius", (t.get("temp_c") or {}).get("hotspot")),
+                                ("power_watts", (t.get("power") or {}).get("current_w")),
+                                ("vram_used_bytes", t.get("vram_used_bytes")),
+                                ("gfx_activity_percent", (t.get("activity") or {}).get("gfx_pct")),
+                                ("umc_activity_percent", (t.get("activity") or {}).get("umc_pct")),
+                                ("ecc_uncorrectable_total", (t.get("ecc") or {}).get("uncorrectable")),
+                                ("ecc_correctable_total", (t.get("ecc") or {}).get("correctable"))):
+                    if isinstance(v, (int, float)):
+                        out.append(f"tk8s_gpu_{name}{{{lab}}} {v}")
+            for key, metric in (("tk8s.amd.com/hbm-write-gbps", "tk8s_validation_hbm_write_gbps"),
+                                ("tk8s.amd.com/md5-mbps", "tk8s_validation_md5_mbps"),
+                                ("tk8s.amd.com/copy-gbps", "tk8s_validation_copy_gbps")):
+                try:
+                    out.append(f'{metric}{{node="{node}"}} {float(ann[key])}')
+                except (KeyError, ValueError):
+                    pass
+        for (pid, node), m in sorted(getattr(self, "metrics", {}).items()):
+            for key, cs in (m.get("pods") or {}).items():
+                ns, pod = key.split("/", 1)
+                for c in cs:
+                    lab = f'namespace="{ns}",pod="{pod}",container="{c.get("name")}",node="{node}"'
+                    out.append(f"tk8s_container_cpu_cores{{{lab}}} {c.get('cpu_cores', 0):.4f}")
+                    out.append(f"tk8s_container_memory_bytes{{{lab}}} {int(c.get('memory_bytes', 0))}")
+                    if c.get("gpu_pct") is not None:
+                        out.append(f"tk8s_container_gpu_busy_percent{{{lab}}} {c['gpu_pct']:.1f}")
+        return out
 
     # ---- node lifecycle ---------------------------------------------------------------
     async def lease_loop(self) -> None:
