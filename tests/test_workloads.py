@@ -573,3 +573,42 @@ def test_quota_holds_back_controller_pods_until_it_allows_them(cp):
     cp.replace("1a1", "resourcequotas", "default", "gpus", body)
     assert cp.store.get("pods", _key("1a1", "default", held[0]["metadata"]["name"]))["spec"].get("nodeName") == "kubenode1"
     assert cp.store.get("resourcequotas", _key("1a1", "default", "gpus"))["status"]["used"] == {"requests.amd.com/gpu": "3"}
+
+
+def test_lost_node_taints_and_evicts_its_pods(cp):
+    """SURVEY §5.3 failure recovery: a node whose agent goes silent gets the unreachable taints;
+    after the pods' toleration their controller re-creates them on the nodes that are left."""
+    from tritonk8ssupervisor_amd.controlplane.objects import UNREACHABLE, _set_ready
+
+    _nodes(cp, 2)
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "srv"}, "spec": {
+        "replicas": 1, "selector": {"matchLabels": {"app": "srv"}}, "template": {
+            "metadata": {"labels": {"app": "srv"}}, "spec": {"containers": [{"name": "c", "command": ["sleep", "60"]}]}}}})
+    (first,) = _pods(cp, "srv")
+    node = _node_of(cp, first)
+    stay = lambda name, **tol: {"metadata": {"name": name}, "spec": {
+        "containers": [{"name": "c", "command": ["true"]}], "nodeName": node,
+        "tolerations": [{"key": UNREACHABLE, "operator": "Exists", "effect": "NoExecute", **tol}]}}
+    cp.create("1a1", "pods", "default", stay("forever"))
+    cp.create("1a1", "pods", "default", stay("patient", tolerationSeconds=3600))
+    cp._node_lost(_key("1a1", node), "lease expired")
+    n = cp.store.get("nodes", _key("1a1", node))
+    assert {t["effect"] for t in n["spec"]["taints"] if t["key"] == UNREACHABLE} == {"NoSchedule", "NoExecute"}
+    assert not cp._taint_manager()  # the default 300 s toleration has not run out
+    cp.pod_eviction_timeout = 0
+    assert cp._taint_manager()
+    cp.reconcile()
+    left = _pods(cp)
+    assert first not in left and {"forever", "patient"} <= set(left)
+    (again,) = _pods(cp, "srv")
+    assert _node_of(cp, again) not in (None, node)  # NoSchedule keeps the replacement off the lost node
+    ev = [e for e in cp.store.list("events") if e.get("reason") == "TaintManagerEviction"]
+    assert ev and ev[0]["involvedObject"]["name"] == first
+    # the next heartbeat lifts the taints
+    cp.store.patch("nodes", _key("1a1", node), _set_ready)
+    assert not cp.store.get("nodes", _key("1a1", node))["spec"]["taints"]
+    # a user's NoExecute taint evicts what does not tolerate it at once
+    other = _node_of(cp, again)
+    cp.store.patch("nodes", _key("1a1", other), lambda o: o["spec"].update(taints=[{"key": "drain", "effect": "NoExecute"}]))
+    assert cp._taint_manager()
+    assert again not in _pods(cp)

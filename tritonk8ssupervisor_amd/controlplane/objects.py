@@ -55,13 +55,22 @@ def node_ready(n: dict) -> bool:
     return bool(c and c["status"] == "True")
 
 
+UNREACHABLE = "node.kubernetes.io/unreachable"
+
+
 def _set_ready(node: dict, message: str = "tk8s agent heartbeating") -> bool:
     """Ready follows the heartbeat, unless the node's xGMI links failed the pre-Ready check
-    (xgmi.py): then it stays NotReady with that reason while the agent is alive."""
+    (xgmi.py): then it stays NotReady with that reason while the agent is alive. A heartbeat
+    also lifts the unreachable taints a lost lease put on the node (server.lease_loop)."""
+    spec = node.setdefault("spec", {})
+    lifted = False
+    if any(t.get("key") == UNREACHABLE for t in spec.get("taints") or []):
+        spec["taints"] = [t for t in spec["taints"] if t.get("key") != UNREACHABLE]
+        lifted = True
     x = _cond(node, "XGMILinksHealthy")
     if x and x["status"] == "False":
-        return _set_cond(node, "Ready", "False", "XGMILinkDegraded", x.get("message", ""))
-    return _set_cond(node, "Ready", "True", "AgentReady", message)
+        return _set_cond(node, "Ready", "False", "XGMILinkDegraded", x.get("message", "")) or lifted
+    return _set_cond(node, "Ready", "True", "AgentReady", message) or lifted
 
 
 def node_validated(n: dict) -> bool:

@@ -48,7 +48,7 @@ from . import k8s_wire
 from .controllers import Controllers
 from .httpserver import HttpError, HttpServer, Request, Response, Router
 from .k8s_api import KubernetesAPI
-from .objects import _cond, _key, _set_cond
+from .objects import UNREACHABLE, _cond, _key, _set_cond
 from .rancher_api import RancherAPI
 from .scheduler import Scheduler
 from .workloads import Workloads
@@ -58,6 +58,12 @@ from .store import Store, now_iso
 
 
 _KIND_PLURAL = {r[2]: plural for plural, r in k8s_wire.RESOURCES.items()}
+
+
+def _tolerates_taint(tol: dict, taint: dict) -> bool:
+    from .placement import _tolerates
+
+    return _tolerates(tol, taint)
 
 
 def _group_doc(group: str, versions: list[str]) -> dict:
@@ -91,6 +97,8 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         self.dns_port = host_port(53) if dns_port is None else dns_port          # 0 disables
         self.ingress_port = host_port(80) if ingress_port is None else ingress_port
         self.hpa_period = float(os.environ.get("TK8S_HPA_PERIOD", "15"))  # the HPA controller's sync period
+        # how long pods stay on a node whose agent went silent (Kubernetes' default tolerations: 300 s)
+        self.pod_eviction_timeout = float(os.environ.get("TK8S_POD_EVICTION_TIMEOUT", "300"))
         self._routes()
 
     # ---- utilities --------------------------------------------------------------------
@@ -367,14 +375,65 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
                         continue
                     c = _cond(n, "Ready")
                     if c and c["status"] == "True":
-                        self.store.patch("nodes", key, lambda o: _set_cond(
-                            o, "Ready", "Unknown", "NodeStatusUnknown", "tk8s agent stopped posting node status"))
-                        pid = key.split("/", 1)[0]
-                        self._event(pid, "default", {"kind": "Node", "name": n["metadata"]["name"]}, "NodeNotReady",
-                                    f"lease expired after {self.node_grace:.1f}s", "Warning")
+                        self._node_lost(key, f"lease expired after {self.node_grace:.1f}s")
                         changed = True
+            changed |= self._taint_manager()
             if changed:
                 self.reconcile()
+
+    def _node_lost(self, key: str, why: str) -> None:
+        """The node lifecycle controller's verdict on a silent agent: Ready=Unknown plus the
+        ``node.kubernetes.io/unreachable`` NoSchedule/NoExecute taints (the next heartbeat lifts
+        them, objects._set_ready); the taint manager evicts its pods after their toleration."""
+        def lost(o):
+            _set_cond(o, "Ready", "Unknown", "NodeStatusUnknown", "tk8s agent stopped posting node status")
+            kept = [x for x in o.setdefault("spec", {}).get("taints") or [] if x.get("key") != UNREACHABLE]
+            o["spec"]["taints"] = kept + [{"key": UNREACHABLE, "effect": e, "timeAdded": now_iso()}
+                                          for e in ("NoSchedule", "NoExecute")]
+
+        n = self.store.patch("nodes", key, lost)
+        self._event(key.split("/", 1)[0], "default", {"kind": "Node", "name": n["metadata"]["name"]}, "NodeNotReady",
+                    why, "Warning")
+
+    def _taint_manager(self) -> bool:
+        """Evict pods from nodes with NoExecute taints they do not tolerate: at once for a taint
+        the pod has no toleration for, after ``tolerationSeconds`` for one it tolerates for a while.
+        The unreachable taint a lost lease adds is tolerated for ``pod_eviction_timeout`` seconds
+        (300, as Kubernetes' default tolerations) unless the pod says otherwise. Their controllers
+        (Deployment, StatefulSet, Job ...) then re-create them on the nodes that are left."""
+        import calendar
+
+        tainted = [n for n in self.store.list("nodes") if any(
+            t.get("effect") == "NoExecute" for t in (n.get("spec") or {}).get("taints") or [])]
+        if not tainted:
+            return False
+        now = time.time()
+        evicted = False
+        for n in tainted:
+            pid, nn = n["_project"], n["metadata"]["name"]
+            taints = [t for t in n["spec"]["taints"] if t.get("effect") == "NoExecute"]
+            for pod in self.store.list("pods", lambda o: o.get("_project") == pid and o["spec"].get("nodeName") == nn
+                                       and o.get("status", {}).get("phase") not in ("Succeeded", "Failed")):
+                for t in taints:
+                    tols = [x for x in pod["spec"].get("tolerations") or [] if _tolerates_taint(x, t)]
+                    if not tols and t.get("key") == UNREACHABLE:
+                        tols = [{"tolerationSeconds": self.pod_eviction_timeout}]
+                    secs = [x.get("tolerationSeconds") for x in tols]
+                    if tols and any(s is None for s in secs):
+                        continue  # tolerated for good
+                    try:
+                        added = calendar.timegm(time.strptime(t.get("timeAdded") or "", "%Y-%m-%dT%H:%M:%SZ"))
+                    except ValueError:
+                        added = now
+                    if not tols or now - added >= min(float(s) for s in secs):
+                        ns, name = pod["metadata"].get("namespace", "default"), pod["metadata"]["name"]
+                        self.store.delete("pods", _key(pid, ns, name))
+                        self._event(pid, ns, {"kind": "Pod", "name": name}, "TaintManagerEviction",
+                                    f"Marking for deletion Pod {ns}/{name}: node {nn} has taint {t.get('key')}:NoExecute",
+                                    "Warning")
+                        evicted = True
+                        break
+        return evicted
 
     async def snapshot_loop(self) -> None:
         if not self.state_dir:
