@@ -612,3 +612,58 @@ def test_lost_node_taints_and_evicts_its_pods(cp):
     cp.store.patch("nodes", _key("1a1", other), lambda o: o["spec"].update(taints=[{"key": "drain", "effect": "NoExecute"}]))
     assert cp._taint_manager()
     assert again not in _pods(cp)
+
+
+def _job(**spec):
+    return {"metadata": {"name": "train"}, "spec": {"completions": 2, "parallelism": 2, "template": {
+        "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "command": ["sleep", "60"]}]}}, **spec}}
+
+
+def _age(cp, kind, name, field, seconds, cond=None):
+    """Move a job's timestamp ``seconds`` into the past."""
+    import time as _time
+
+    past = _time.strftime("%Y-%m-%dT%H:%M:%SZ", _time.gmtime(_time.time() - seconds))
+
+    def fn(o):
+        if cond:
+            next(c for c in o["status"]["conditions"] if c["type"] == cond)[field] = past
+        else:
+            o["status"][field] = past
+    cp.store.patch(kind, _key("1a1", "default", name), fn)
+
+
+def test_job_suspend_resume_deadline_and_ttl(cp):
+    cp.create("1a1", "jobs", "default", _job(suspend=True))
+    j = cp.store.get("jobs", _key("1a1", "default", "train"))
+    assert not _pods(cp, "train") and "startTime" not in j["status"]
+    assert [(c["type"], c["status"]) for c in j["status"]["conditions"]] == [("Suspended", "True")]
+    body = json.loads(json.dumps(cp._strip(j)))
+    body["spec"]["suspend"] = False
+    cp.replace("1a1", "jobs", "default", "train", body)
+    assert len(_pods(cp, "train")) == 2
+    j = cp.store.get("jobs", _key("1a1", "default", "train"))
+    assert j["status"]["startTime"] and j["status"]["conditions"][0]["reason"] == "JobResumed"
+    # suspending a running job stops its pods
+    body = json.loads(json.dumps(cp._strip(j)))
+    body["spec"]["suspend"] = True
+    cp.replace("1a1", "jobs", "default", "train", body)
+    assert not _pods(cp, "train") and cp.store.get("jobs", _key("1a1", "default", "train"))["status"]["active"] == 0
+    cp._delete_job("1a1", "default", "train")
+    # activeDeadlineSeconds
+    cp.create("1a1", "jobs", "default", _job(activeDeadlineSeconds=30, ttlSecondsAfterFinished=60))
+    assert len(_pods(cp, "train")) == 2
+    cp.reconcile()
+    assert len(_pods(cp, "train")) == 2  # not yet
+    _age(cp, "jobs", "train", "startTime", 31)
+    cp.reconcile()
+    j = cp.store.get("jobs", _key("1a1", "default", "train"))
+    assert not _pods(cp, "train")
+    failed = [c for c in j["status"]["conditions"] if c["type"] == "Failed"]
+    assert failed and failed[0]["reason"] == "DeadlineExceeded"
+    # ttlSecondsAfterFinished deletes the finished job
+    cp.reconcile()
+    assert cp.store.get("jobs", _key("1a1", "default", "train")) is not None
+    _age(cp, "jobs", "train", "lastTransitionTime", 61, cond="Failed")
+    cp.reconcile()
+    assert cp.store.get("jobs", _key("1a1", "default", "train")) is None

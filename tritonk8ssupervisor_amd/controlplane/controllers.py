@@ -5,8 +5,19 @@ server.ControlPlane.
 from __future__ import annotations
 
 import copy
+import time
 
 from .store import now_iso
+
+
+def _epoch(iso: str | None) -> float:
+    """Seconds since the epoch of an RFC 3339 ``...Z`` timestamp (now if missing or malformed)."""
+    import calendar
+
+    try:
+        return float(calendar.timegm(time.strptime(iso or "", "%Y-%m-%dT%H:%M:%SZ")))
+    except ValueError:
+        return time.time()
 
 REVISION = "deployment.kubernetes.io/revision"
 from .objects import (
@@ -148,9 +159,20 @@ class Controllers:
                                 "Warning")
 
     def _ctl_jobs(self, pid: str) -> None:
+        """Job controller: ``completions``/``parallelism``, ``completionMode: Indexed`` (ranks get
+        JOB_COMPLETION_INDEX), ``backoffLimit``; ``suspend`` stops the active pods and holds new
+        ones back; ``activeDeadlineSeconds`` fails a job that ran too long (DeadlineExceeded) and
+        ``ttlSecondsAfterFinished`` deletes a finished one with its pods (cron_loop keeps time)."""
+        now = time.time()
         for job in self.store.list("jobs", lambda o: self._in(pid, o)):
             ns, jname = job["metadata"]["namespace"], job["metadata"]["name"]
             spec = job["spec"]
+            st0 = job.get("status") or {}
+            fin = next((c for c in st0.get("conditions", []) if c["type"] in ("Complete", "Failed") and c["status"] == "True"), None)
+            ttl = spec.get("ttlSecondsAfterFinished")
+            if fin is not None and ttl is not None and now - _epoch(fin.get("lastTransitionTime")) >= float(ttl):
+                self._delete_job(pid, ns, jname)
+                continue
             completions = int(spec.get("completions", 1))
             parallelism = int(spec.get("parallelism", completions))
             backoff = int(spec.get("backoffLimit", 6))
@@ -166,11 +188,17 @@ class Controllers:
                     failed += 1
                 else:
                     active += 1
-            done = any(c["type"] in ("Complete", "Failed") and c["status"] == "True" for c in job.get("status", {}).get("conditions", []))
-            if not done and failed > backoff:
+            done = fin is not None
+            suspended = bool(spec.get("suspend"))
+            deadline = spec.get("activeDeadlineSeconds")
+            started = st0.get("startTime") if not suspended else None
+            over = (not done and not suspended and started is not None and deadline is not None
+                    and now - _epoch(started) >= float(deadline))
+            if not done and (failed > backoff or over or suspended):
                 for o in pods:  # stop the rest (a gang job cannot finish without all ranks)
                     if o.get("status", {}).get("phase") not in TERMINAL:
                         self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                        active -= 1
             elif not done:
                 running_idx = {int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
                                for o in pods if o.get("status", {}).get("phase") not in TERMINAL}
@@ -187,13 +215,28 @@ class Controllers:
             status = dict(job.get("status", {}))
             status.update(active=active, succeeded=len(succeeded_idx), failed=failed)
             conds = [c for c in status.get("conditions", [])]
+            sus = next((c for c in conds if c["type"] == "Suspended"), None)
             if not done:
+                if suspended and (sus is None or sus["status"] != "True"):
+                    conds = [c for c in conds if c is not sus] + [{"type": "Suspended", "status": "True", "reason": "JobSuspended",
+                                                                   "message": "Job suspended", "lastTransitionTime": now_iso()}]
+                    status.pop("startTime", None)
+                elif not suspended and sus is not None and sus["status"] == "True":
+                    conds = [c for c in conds if c is not sus] + [{"type": "Suspended", "status": "False", "reason": "JobResumed",
+                                                                   "message": "Job resumed", "lastTransitionTime": now_iso()}]
+                if not suspended and "startTime" not in status:
+                    status["startTime"] = now_iso()
                 if len(succeeded_idx) >= completions:
                     conds.append({"type": "Complete", "status": "True", "lastTransitionTime": now_iso()})
                     status["completionTime"] = now_iso()
                 elif failed > backoff:
                     conds.append({"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded",
                                   "lastTransitionTime": now_iso()})
+                elif over:
+                    conds.append({"type": "Failed", "status": "True", "reason": "DeadlineExceeded",
+                                  "message": "Job was active longer than specified deadline", "lastTransitionTime": now_iso()})
+                    self._event(pid, ns, {"kind": "Job", "name": jname}, "DeadlineExceeded",
+                                "Job was active longer than specified deadline", "Warning")
             status["conditions"] = conds
             if status != job.get("status"):
                 self.store.patch("jobs", _key(pid, ns, jname), lambda o, s=status: o.__setitem__("status", s))

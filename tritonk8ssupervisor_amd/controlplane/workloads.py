@@ -239,11 +239,15 @@ class Workloads:
                 self.store.patch("cronjobs", _key(pid, ns, name), lambda o, s2=st: o.__setitem__("status", s2))
 
     async def cron_loop(self) -> None:
-        """The controllers that run on the clock rather than on changes: CronJobs, every second."""
+        """The controllers that run on the clock rather than on changes, every second: CronJobs,
+        and Jobs with an ``activeDeadlineSeconds`` or ``ttlSecondsAfterFinished``."""
         import asyncio
 
         while True:
             await asyncio.sleep(1.0 - (time.time() % 1.0) + 0.01)
+            if any("activeDeadlineSeconds" in j["spec"] or "ttlSecondsAfterFinished" in j["spec"]
+                   for j in self.store.list("jobs")):
+                self.reconcile()
             if not self.store.keys("cronjobs"):
                 continue
             for p in self.store.list("projects"):
