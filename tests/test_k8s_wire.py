@@ -452,3 +452,51 @@ def test_custom_resource_definitions(kube):
     assert _raw(kube, "GET", base)[0] == 404
     _raw(kube, "POST", "/apis/apiextensions.k8s.io/v1/customresourcedefinitions", crd)
     assert _raw(kube, "GET", base)[2]["items"] == []
+
+
+def test_eviction_api_and_kubectl_drain_wait(kube, tmp_path, capsys):
+    """POST pods/<name>/eviction answers 429 while a PodDisruptionBudget allows no disruption;
+    ./kubectl drain evicts through it and retries; ./kubectl wait --for=condition/delete/jsonpath."""
+    from tritonk8ssupervisor_amd.cli import kubectl
+    from test_controlplane import Client
+
+    pid = kube.prefix.split("/")[3]
+    cfg = tmp_path / "kubeconfig.json"
+    cfg.write_text(json.dumps(kube.get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})))
+    kc = lambda *a: kubectl.main(["--kubeconfig", str(cfg), *a], workdir=str(tmp_path))
+    # the fixture's node, and its node token to post pod status as its agent would
+    ctl = Client(kube.base, token=kube.token)
+    from test_controlplane import _join
+
+    nc, _reg = _join(ctl, pid, "kubenode2", ngpu=0)
+    for i in range(2):
+        kube.post(kube.k8s("/api/v1/namespaces/default/pods"), {"metadata": {"name": f"p{i}", "labels": {"app": "x"}},
+                                                                 "spec": {"nodeName": "kubenode2", "containers": [
+                                                                     {"name": "c", "command": ["sleep", "60"]}]}})
+        nc.put(nc.k8s(f"/api/v1/namespaces/default/pods/p{i}/status"), {"status": {"phase": "Running"}})
+    assert kc("wait", "pod/p0", "pod/p1", "--for=condition=Ready", "--timeout=5s") == 0
+    assert "pod/p0 condition met" in capsys.readouterr().out
+    assert kc("wait", "pod", "-l", "app=x", "--for=jsonpath={.status.phase}=Running", "--timeout=5s") == 0
+    assert kc("wait", "pod/p0", "--for=jsonpath={.status.phase}=Failed", "--timeout=0.5s") == 1
+    assert "timed out waiting" in capsys.readouterr().err
+    kube.post(kube.k8s("/apis/policy/v1/namespaces/default/poddisruptionbudgets"), {
+        "apiVersion": "policy/v1", "kind": "PodDisruptionBudget", "metadata": {"name": "x"},
+        "spec": {"minAvailable": 2, "selector": {"matchLabels": {"app": "x"}}}})
+    code, _ct, body = _raw(kube, "POST", "/api/v1/namespaces/default/pods/p0/eviction",
+                           {"apiVersion": "policy/v1", "kind": "Eviction", "metadata": {"name": "p0"}})
+    assert code == 429 and body["reason"] == "TooManyRequests"
+    assert kc("drain", "kubenode2", "--ignore-daemonsets", "--timeout=2s") == 1
+    err = capsys.readouterr().err
+    assert "disruption budget" in err and "global timeout" in err
+    assert kube.get(kube.k8s("/api/v1/nodes/kubenode2"))["spec"]["unschedulable"] is True
+    # relax the budget: the drain goes through
+    kube.request("PATCH", kube.k8s("/apis/policy/v1/namespaces/default/poddisruptionbudgets/x"),
+                 body={"spec": {"minAvailable": 0}}, content_type="application/merge-patch+json")
+    assert kc("drain", "kubenode2", "--timeout=5s") == 0
+    out = capsys.readouterr().out
+    assert "evicting pod default/p0" in out and "node/kubenode2 drained" in out
+    assert kc("wait", "pod/p0", "--for=delete", "--timeout=5s") == 0
+    assert "pod/p0 deleted" in capsys.readouterr().out
+    assert kc("get", "pdb") == 0
+    out = capsys.readouterr().out
+    assert "ALLOWED DISRUPTIONS" in out and out.splitlines()[1].split()[:3] == ["x", "0", "N/A"]

@@ -667,3 +667,45 @@ def test_job_suspend_resume_deadline_and_ttl(cp):
     _age(cp, "jobs", "train", "lastTransitionTime", 61, cond="Failed")
     cp.reconcile()
     assert cp.store.get("jobs", _key("1a1", "default", "train")) is None
+
+
+def test_pod_disruption_budget_and_eviction(cp):
+    _nodes(cp, 2)
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "srv"}, "spec": {
+        "replicas": 3, "selector": {"matchLabels": {"app": "srv"}}, "template": {
+            "metadata": {"labels": {"app": "srv"}}, "spec": {"containers": [{"name": "c", "command": ["sleep", "60"]}]}}}})
+    for n in _pods(cp, "srv"):
+        _run(cp, n)
+    with pytest.raises(HttpError) as e:
+        cp.create("1a1", "poddisruptionbudgets", "default", {"metadata": {"name": "bad"}, "spec": {
+            "minAvailable": 1, "maxUnavailable": 1, "selector": {"matchLabels": {"app": "srv"}}}})
+    assert e.value.status == 422
+    cp.create("1a1", "poddisruptionbudgets", "default", {"metadata": {"name": "srv"}, "spec": {
+        "minAvailable": "60%", "selector": {"matchLabels": {"app": "srv"}}}})
+    st = cp.store.get("poddisruptionbudgets", _key("1a1", "default", "srv"))["status"]
+    assert (st["expectedPods"], st["currentHealthy"], st["desiredHealthy"], st["disruptionsAllowed"]) == (3, 3, 2, 1)
+    first, second, _third = _pods(cp, "srv")
+    cp.evict("1a1", "default", first)
+    assert first not in _pods(cp)
+    with pytest.raises(HttpError) as e:  # the replacement is not Running yet: 2 healthy, 2 needed
+        cp.evict("1a1", "default", second)
+    assert e.value.status == 429 and "disruption budget" in e.value.message
+    assert e.value.body["details"]["causes"][0]["reason"] == "DisruptionBudget"
+    # a pending pod may always go
+    (pending,) = [n for n in _pods(cp, "srv") if n not in (second, _third)]
+    cp.evict("1a1", "default", pending)
+    for n in _pods(cp, "srv"):
+        _run(cp, n)
+    cp.evict("1a1", "default", second)  # healthy again: 3 of 3
+    st = cp.store.get("poddisruptionbudgets", _key("1a1", "default", "srv"))["status"]
+    assert st["disruptionsAllowed"] == 0 and st["conditions"][0]["reason"] == "InsufficientPods"
+    assert any(ev.get("reason") == "Evicted" for ev in cp.store.list("events"))
+    # maxUnavailable 0: nothing may be evicted
+    cp.replace("1a1", "poddisruptionbudgets", "default", "srv", {"metadata": {"name": "srv"}, "spec": {
+        "maxUnavailable": 0, "selector": {"matchLabels": {"app": "srv"}}}})
+    for n in _pods(cp, "srv"):
+        _run(cp, n)
+    with pytest.raises(HttpError):
+        cp.evict("1a1", "default", _pods(cp, "srv")[0])
+    d = cp.store.get("deployments", _key("1a1", "default", "srv"))["status"]
+    assert {c["type"]: c["status"] for c in d["conditions"]} == {"Available": "True", "Progressing": "True"}

@@ -117,6 +117,10 @@ def fmt_generic(kind: str, items: list[dict], all_ns: bool) -> str:
         rows = [["NAME", "DESIRED", "CURRENT", "READY", "AGE"]] + [[o["metadata"]["name"], str(o["spec"].get("replicas", 1)),
                 str(o.get("status", {}).get("replicas", 0)), str(o.get("status", {}).get("readyReplicas", 0)), _age(o)]
                 for o in items]
+    elif k == "poddisruptionbudget":
+        rows = [["NAME", "MIN AVAILABLE", "MAX UNAVAILABLE", "ALLOWED DISRUPTIONS", "AGE"]] + [[
+            o["metadata"]["name"], str(o["spec"].get("minAvailable", "N/A")), str(o["spec"].get("maxUnavailable", "N/A")),
+            str(o.get("status", {}).get("disruptionsAllowed", 0)), _age(o)] for o in items]
     elif k == "cronjob":
         rows = [["NAME", "SCHEDULE", "SUSPEND", "ACTIVE", "LAST SCHEDULE", "AGE"]] + [[
             o["metadata"]["name"], o["spec"].get("schedule", ""), str(bool(o["spec"].get("suspend", False))),
@@ -234,6 +238,114 @@ def _cp(k, ns: str, args: list[str], container: str | None = None) -> int:
                 elif m.isfile():
                     target.parent.mkdir(parents=True, exist_ok=True)
                     target.write_bytes(t.extractfile(m).read())
+    return 0
+
+
+def _jsonpath(obj, expr: str):
+    """The value at a simple JSONPath (``{.status.phase}``, ``{.status.conditions[0].type}``)."""
+    import re
+
+    cur = obj
+    for name, idx in re.findall(r"\.([^.\[\]]+)|\[(\d+)\]", expr.strip().strip("{}")):
+        if cur is None:
+            return None
+        cur = (cur.get(name) if isinstance(cur, dict) else None) if name else (
+            cur[int(idx)] if isinstance(cur, list) and int(idx) < len(cur) else None)
+    return cur
+
+
+def _wait_met(obj: dict | None, cond: str) -> bool:
+    if cond == "delete":
+        return obj is None
+    if obj is None:
+        return False
+    if cond.startswith("condition="):
+        ctype, _, want = cond[len("condition="):].partition("=")
+        return any(c.get("type", "").lower() == ctype.lower() and str(c.get("status")).lower() == (want or "true").lower()
+                   for c in (obj.get("status") or {}).get("conditions") or [])
+    if cond.startswith("jsonpath="):
+        expr, _, want = cond[len("jsonpath="):].rpartition("=") if "}=" in cond else (cond[len("jsonpath="):], "", "")
+        v = _jsonpath(obj, expr)
+        return v is not None if not want else str(v) == want.strip("'\"")
+    raise SystemExit(f"error: unrecognized condition: {cond!r} (condition=TYPE[=STATUS], delete, jsonpath={{...}}=VALUE)")
+
+
+def _wait(k, ns: str, args: list[str], cond: str, selector: str | None, timeout: float) -> int:
+    """``kubectl wait TYPE/NAME... | TYPE -l SEL --for=condition=Ready|delete|jsonpath=...``."""
+    if len(args) == 1 and "/" not in args[0] and not selector:
+        raise SystemExit("error: resource name or selector required")
+    targets = [tuple(x.split("/", 1)) for x in args] if "/" in args[0] else [(args[0], n) for n in args[1:]]
+    kind = kind_key(targets[0][0] if targets else args[0])
+    if selector:
+        items = k.get(k.k8s(collection_path(kind, ns)), query={"labelSelector": selector})["items"]
+        targets += [(kind, o["metadata"]["name"]) for o in items]
+        if not targets:
+            print(f"error: no matching resources found", file=sys.stderr)
+            return 1
+    deadline = time.monotonic() + timeout
+    rc = 0
+    for what, name in targets:
+        path = k.k8s(f"/api/v1/nodes/{name}" if kind_key(what) == "node" else object_path(what, name, ns))
+        while True:
+            try:
+                obj = k.get(path)
+            except ApiError as e:
+                if e.status != 404:
+                    raise
+                obj = None
+            if _wait_met(obj, cond):
+                print(f"{kind_key(what)}/{name} {'deleted' if cond == 'delete' else 'condition met'}")
+                break
+            if obj is None:
+                print(f'Error from server (NotFound): {kind_key(what)}s "{name}" not found', file=sys.stderr)
+                rc = 1
+                break
+            if time.monotonic() >= deadline:
+                print(f"error: timed out waiting for the condition on {kind_key(what)}s/{name}", file=sys.stderr)
+                rc = 1
+                break
+            time.sleep(0.2)
+    return rc
+
+
+def _drain(k, node: str, timeout: float, disable_eviction: bool) -> int:
+    """Cordon, then evict every pod but DaemonSets' and finished ones through the Eviction API,
+    retrying those a PodDisruptionBudget holds back (429) until ``timeout``."""
+    k.request("PATCH", k.k8s(f"/api/v1/nodes/{node}"), body={"spec": {"unschedulable": True}})
+    print(f"node/{node} cordoned")
+    pods = []
+    for p in k.get(k.k8s("/api/v1/pods"), query={"fieldSelector": f"spec.nodeName={node}"})["items"]:
+        owners = {r.get("kind") for r in p["metadata"].get("ownerReferences", [])}
+        if "DaemonSet" in owners or p.get("status", {}).get("phase") in ("Succeeded", "Failed"):
+            continue
+        pods.append((p["metadata"]["namespace"], p["metadata"]["name"]))
+    deadline = time.monotonic() + timeout
+    while pods:
+        left = []
+        for pns, name in pods:
+            path = k.k8s(object_path("pod", name, pns))
+            try:
+                if disable_eviction:
+                    k.delete(path)
+                else:
+                    k.post(path + "/eviction", {"apiVersion": "policy/v1", "kind": "Eviction",
+                                                "metadata": {"name": name, "namespace": pns}})
+                print(f"{'deleting' if disable_eviction else 'evicting'} pod {pns}/{name}")
+            except ApiError as e:
+                if e.status == 404:
+                    continue
+                if e.status != 429:
+                    raise
+                print(f'error when evicting pods/"{name}" -n "{pns}" (will retry after 1s): {e}', file=sys.stderr)
+                left.append((pns, name))
+        pods = left
+        if pods:
+            if time.monotonic() >= deadline:
+                print(f"error: unable to drain node {node!r} due to error: global timeout reached: {timeout:g}s, "
+                      f"{len(pods)} pod(s) left", file=sys.stderr)
+                return 1
+            time.sleep(1.0)
+    print(f"node/{node} drained")
     return 0
 
 
@@ -430,6 +542,10 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("-c", "--container")
     ap.add_argument("--to-revision", type=int, default=0)
+    ap.add_argument("--for", dest="for_")
+    ap.add_argument("--disable-eviction", action="store_true")
+    ap.add_argument("--delete-emptydir-data", action="store_true")  # (accepted: emptyDirs go with their pod)
+    ap.add_argument("--force", action="store_true")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -588,16 +704,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             k.request("PATCH", k.k8s(path), body={"metadata": {field: patch}})
             print(f"{kind_key(what)}/{name} {'labeled' if a.verb == 'label' else 'annotated'}")
         elif a.verb == "drain":
-            node = a.args[0]
-            k.request("PATCH", k.k8s(f"/api/v1/nodes/{node}"), body={"spec": {"unschedulable": True}})
-            print(f"node/{node} cordoned")
-            for p in k.get(k.k8s("/api/v1/pods"), query={"fieldSelector": f"spec.nodeName={node}"})["items"]:
-                owners = {r.get("kind") for r in p["metadata"].get("ownerReferences", [])}
-                if "DaemonSet" in owners or p.get("status", {}).get("phase") in ("Succeeded", "Failed"):
-                    continue
-                k.delete(k.k8s(object_path("pod", p["metadata"]["name"], p["metadata"]["namespace"])))
-                print(f"evicting pod {p['metadata']['namespace']}/{p['metadata']['name']}")
-            print(f"node/{node} drained")
+            return _drain(k, a.args[0], float(a.timeout.rstrip("s")), a.disable_eviction)
         elif a.verb == "top":
             if not a.args or kind_key(a.args[0]) not in ("node", "pod"):
                 raise SystemExit("usage: kubectl top nodes|pods")
@@ -677,10 +784,12 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
         elif a.verb in ("cordon", "uncordon"):
             k.request("PATCH", k.k8s(f"/api/v1/nodes/{a.args[0]}"), body={"spec": {"unschedulable": a.verb == "cordon"}})
             print(f"node/{a.args[0]} {a.verb}ed")
+        elif a.verb == "wait" and getattr(a, "for_", None):
+            return _wait(k, ns, a.args, a.for_, a.selector, float(a.timeout.rstrip("s")))
         elif a.verb == "wait":
             what, name = a.args[0].split("/", 1)
             if kind_key(what) != "job":
-                raise SystemExit("only job/NAME is supported by wait")
+                raise SystemExit("wait without --for is job/NAME only (until Complete or Failed)")
             j = wait_job(k, name, ns, timeout=float(a.timeout.rstrip("s")))
             print(f"job.batch/{name} condition met ({job_state(j)})")
             return 0 if job_state(j) == "Complete" else 1

@@ -10,6 +10,22 @@ import time
 from .store import now_iso
 
 
+def _conditions(obj: dict, want: list[tuple[str, str, str, str]]) -> list[dict]:
+    """Status conditions (type, status, reason, message), keeping an old entry's times while its
+    status and reason hold, so an unchanged object is not rewritten."""
+    old = {c.get("type"): c for c in (obj.get("status") or {}).get("conditions") or []}
+    out = []
+    for ctype, status, reason, message in want:
+        c = old.get(ctype)
+        if c and (c.get("status"), c.get("reason"), c.get("message")) == (status, reason, message):
+            out.append(c)
+        else:
+            t = now_iso()
+            out.append({"type": ctype, "status": status, "reason": reason, "message": message,
+                        "lastUpdateTime": t, "lastTransitionTime": c["lastTransitionTime"] if c and c.get("status") == status else t})
+    return out
+
+
 def _epoch(iso: str | None) -> float:
     """Seconds since the epoch of an RFC 3339 ``...Z`` timestamp (now if missing or malformed)."""
     import calendar
@@ -45,6 +61,7 @@ class Controllers:
                     self._ctl_replicasets(pid)
                     self._ctl_endpoints(pid)
                     self._ctl_quotas(pid)
+                    self._ctl_pdbs(pid)
                     self._ctl_validation(pid)
                     self._scheduler(pid)
                 if not self._again:
@@ -283,6 +300,13 @@ class Controllers:
                       "updatedReplicas": sum(1 for o in pods if o["metadata"].get("labels", {}).get("pod-template-hash") == h),
                       "readyReplicas": running, "availableReplicas": running,
                       "unavailableReplicas": max(0, want - running)}
+            done = status["updatedReplicas"] == want == running and status["replicas"] == want
+            status["conditions"] = _conditions(d, [
+                ("Available", *(("True", "MinimumReplicasAvailable", "Deployment has minimum availability.")
+                                if running >= want - unavailable else
+                                ("False", "MinimumReplicasUnavailable", "Deployment does not have minimum availability."))),
+                ("Progressing", "True", *(("NewReplicaSetAvailable", f'ReplicaSet "{dname}-{h}" has successfully progressed.')
+                                          if done else ("ReplicaSetUpdated", f'ReplicaSet "{dname}-{h}" is progressing.')))])
             if d.get("status") != status:
                 self.store.patch("deployments", _key(pid, ns, dname), lambda o, s=status: o.__setitem__("status", s))
 

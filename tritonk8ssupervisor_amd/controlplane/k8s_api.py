@@ -845,6 +845,9 @@ class KubernetesAPI:
             md["generation"] = 1
         elif kind == "persistentvolumeclaims":
             self._admit_pvc(name, body)
+        elif kind == "poddisruptionbudgets":
+            self._admit_pdb(name, body)
+            md["generation"] = 1
         elif kind == "customresourcedefinitions":
             self._admit_crd(name, body)
         elif kind not in k8s_wire.RESOURCES:  # a custom resource: its type from the CRD
@@ -975,8 +978,8 @@ class KubernetesAPI:
                                      "after creation except resources.requests")
             new["status"] = {**cur.get("status", {}), "capacity": {"storage": (((new.get("spec") or {}).get("resources")
                                                                                   or {}).get("requests") or {}).get("storage", "")}}
-        if kind == "cronjobs":
-            self._check_cronjob(name, new.get("spec") or {})
+        if kind in ("cronjobs", "poddisruptionbudgets"):
+            (self._check_cronjob if kind == "cronjobs" else self._admit_pdb)(name, new.get("spec") if kind == "cronjobs" else new)
             md["generation"] = int(cur["metadata"].get("generation", 1)) + (1 if spec_changed else 0)
         if kind in ("daemonsets", "deployments", "jobs", "statefulsets", "replicasets"):
             if not new.get("spec", {}).get("template", {}).get("spec", {}).get("containers"):

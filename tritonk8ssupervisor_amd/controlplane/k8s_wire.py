@@ -25,7 +25,7 @@ import time
 
 # plural -> (group, version, Kind, singular, namespaced, short names, subresources)
 RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str, ...]]] = {
-    "pods": ("", "v1", "Pod", "pod", True, ("po",), ("log", "status", "exec", "portforward", "attach")),
+    "pods": ("", "v1", "Pod", "pod", True, ("po",), ("log", "status", "exec", "portforward", "attach", "eviction")),
     "services": ("", "v1", "Service", "service", True, ("svc",), ()),
     "events": ("", "v1", "Event", "event", True, ("ev",), ()),
     "configmaps": ("", "v1", "ConfigMap", "configmap", True, ("cm",), ()),
@@ -52,6 +52,7 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "customresourcedefinitions": ("apiextensions.k8s.io", "v1", "CustomResourceDefinition", "customresourcedefinition",
                                   False, ("crd", "crds"), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
+    "poddisruptionbudgets": ("policy", "v1", "PodDisruptionBudget", "poddisruptionbudget", True, ("pdb",), ("status",)),
 }
 READ_ONLY = {"namespaces": ("create", "delete", "get", "list", "patch", "watch"),
              "events": ("get", "list", "watch", "create", "delete")}
@@ -118,9 +119,12 @@ def api_resource_list(group: str, version: str) -> dict | None:
         for s in subs:
             sub = {"name": f"{plural}/{s}", "singularName": "", "namespaced": namespaced, "kind": kind,
                    "verbs": ["get"] if s == "log" else ["create", "get"] if s in ("exec", "portforward", "attach")
+                   else ["create"] if s == "eviction"
                    else ["get", "patch", "update"]}
             if s == "scale":
                 sub.update(kind="Scale", group="autoscaling", version="v1")
+            elif s == "eviction":
+                sub.update(kind="Eviction", group="policy", version="v1")
             res.append(sub)
     if not res:
         return None
@@ -130,7 +134,8 @@ def api_resource_list(group: str, version: str) -> dict | None:
 
 # ---- errors -------------------------------------------------------------------------------
 REASONS = {400: "BadRequest", 401: "Unauthorized", 403: "Forbidden", 404: "NotFound", 405: "MethodNotAllowed",
-           409: "Conflict", 410: "Expired", 415: "UnsupportedMediaType", 422: "Invalid", 500: "InternalError",
+           409: "Conflict", 410: "Expired", 415: "UnsupportedMediaType", 422: "Invalid", 429: "TooManyRequests",
+           500: "InternalError",
            503: "ServiceUnavailable", 504: "Timeout"}
 
 
@@ -468,6 +473,12 @@ def _ds_row(o: dict) -> list:
             s.get("numberReady", 0), _age(o)]
 
 
+def _pdb_row(o: dict) -> list:
+    spec, s = o.get("spec") or {}, o.get("status") or {}
+    return [o["metadata"]["name"], str(spec.get("minAvailable", "N/A")), str(spec.get("maxUnavailable", "N/A")),
+            s.get("disruptionsAllowed", 0), _age(o)]
+
+
 _S, _I = "string", "integer"
 TABLES = {
     "nodes": ([("Name", _S), ("Status", _S), ("Roles", _S), ("Age", _S), ("Version", _S), ("GPU", _S),
@@ -485,6 +496,8 @@ TABLES = {
     "replicasets": ([("Name", _S), ("Desired", _I), ("Current", _I), ("Ready", _I), ("Age", _S)], _rs_row),
     "cronjobs": ([("Name", _S), ("Schedule", _S), ("Timezone", _S), ("Suspend", _S), ("Active", _I),
                   ("Last Schedule", _S), ("Age", _S)], _cj_row),
+    "poddisruptionbudgets": ([("Name", _S), ("Min Available", _S), ("Max Unavailable", _S), ("Allowed Disruptions", _I),
+                              ("Age", _S)], _pdb_row),
 }
 
 

@@ -24,13 +24,14 @@ from dataclasses import dataclass
 
 _PREFIX = re.compile(r"^/r/projects/[^/]+/kubernetes(?=/)")
 
-WORKLOAD_RESOURCES = ["pods", "pods/log", "pods/exec", "pods/portforward", "pods/attach", "services", "configmaps",
+WORKLOAD_RESOURCES = ["pods", "pods/log", "pods/exec", "pods/portforward", "pods/attach", "pods/eviction", "services",
+                      "configmaps", "poddisruptionbudgets",
                       "secrets", "persistentvolumeclaims", "serviceaccounts", "events", "deployments",
                       "deployments/scale", "statefulsets", "statefulsets/scale", "replicasets", "replicasets/scale",
                       "daemonsets", "jobs", "cronjobs", "ingresses", "horizontalpodautoscalers"]
 READ = ["get", "list", "watch"]
 WRITE = ["create", "update", "patch", "delete", "deletecollection"]
-ALL_GROUPS = ["", "apps", "batch", "networking.k8s.io", "autoscaling", "metrics.k8s.io"]
+ALL_GROUPS = ["", "apps", "batch", "networking.k8s.io", "autoscaling", "metrics.k8s.io", "policy"]
 
 BUILTIN_CLUSTER_ROLES = {
     "cluster-admin": [{"apiGroups": ["*"], "resources": ["*"], "verbs": ["*"]}],
@@ -38,7 +39,7 @@ BUILTIN_CLUSTER_ROLES = {
               {"apiGroups": ["rbac.authorization.k8s.io"], "resources": ["roles", "rolebindings"], "verbs": READ + WRITE}],
     "edit": [{"apiGroups": ALL_GROUPS, "resources": WORKLOAD_RESOURCES, "verbs": READ + WRITE}],
     "view": [{"apiGroups": ALL_GROUPS, "resources": [r for r in WORKLOAD_RESOURCES if r not in (
-        "secrets", "pods/exec", "pods/portforward", "pods/attach")] + ["namespaces", "nodes"], "verbs": READ}],
+        "secrets", "pods/exec", "pods/portforward", "pods/attach", "pods/eviction")] + ["namespaces", "nodes"], "verbs": READ}],
 }
 
 

@@ -54,6 +54,7 @@ from .scheduler import Scheduler
 from .workloads import Workloads
 from .crds import CustomResources
 from .metrics_api import MetricsAPI
+from .disruption import Disruption
 from .store import Store, now_iso
 
 
@@ -71,7 +72,8 @@ def _group_doc(group: str, versions: list[str]) -> dict:
             "preferredVersion": {"groupVersion": f"{group}/{versions[0]}", "version": versions[0]}}
 
 
-class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Scheduler):
+class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Disruption,
+                   Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port
@@ -230,6 +232,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/exec", self.h_pod_exec_ws)
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/portforward", self.h_pod_portforward_ws)
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/attach", self.h_pod_attach_ws)
+            add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/eviction", self.h_pod_eviction)
             add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs", self.h_node_execs)
             add("PUT", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)", self.h_exec_result)
             # every other object path, built-in kinds (KIND_GROUPS, CLUSTER_KIND_GROUPS) and custom

@@ -34,6 +34,7 @@ KINDS = {
     "secret": ("Secret", "/api/v1", "secrets"),
     "persistentvolumeclaim": ("PersistentVolumeClaim", "/api/v1", "persistentvolumeclaims"),
     "ingress": ("Ingress", "/apis/networking.k8s.io/v1", "ingresses"),
+    "poddisruptionbudget": ("PodDisruptionBudget", "/apis/policy/v1", "poddisruptionbudgets"),
 }
 ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", "ds": "daemonset",
            "daemonsets": "daemonset", "deploy": "deployment", "deployments": "deployment", "jobs": "job",
@@ -45,7 +46,8 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "hpa": "horizontalpodautoscaler", "horizontalpodautoscalers": "horizontalpodautoscaler",
            "sa": "serviceaccount", "serviceaccounts": "serviceaccount", "roles": "role", "rolebindings": "rolebinding",
            "clusterroles": "clusterrole", "clusterrolebindings": "clusterrolebinding", "crd": "customresourcedefinition",
-           "crds": "customresourcedefinition", "customresourcedefinitions": "customresourcedefinition"}
+           "crds": "customresourcedefinition", "customresourcedefinitions": "customresourcedefinition",
+           "pdb": "poddisruptionbudget", "poddisruptionbudgets": "poddisruptionbudget"}
 
 
 CLUSTER_SCOPED: set[str] = {"customresourcedefinition"}  # (+ kinds learnt from discovery without a namespace)
