@@ -709,3 +709,51 @@ def test_pod_disruption_budget_and_eviction(cp):
         cp.evict("1a1", "default", _pods(cp, "srv")[0])
     d = cp.store.get("deployments", _key("1a1", "default", "srv"))["status"]
     assert {c["type"]: c["status"] for c in d["conditions"]} == {"Available": "True", "Progressing": "True"}
+
+
+def test_priority_classes_and_preemption(cp):
+    from tritonk8ssupervisor_amd.controlplane.objects import GPU
+
+    _nodes(cp, 2, gpus=2)
+    with pytest.raises(HttpError) as e:
+        cp.create("1a1", "priorityclasses", "", {"metadata": {"name": "system-mine"}, "value": 5})
+    assert e.value.status == 422
+    cp.create("1a1", "priorityclasses", "", {"metadata": {"name": "low"}, "value": 10, "globalDefault": True})
+    cp.create("1a1", "priorityclasses", "", {"metadata": {"name": "prod"}, "value": 1000})
+    cp.create("1a1", "priorityclasses", "", {"metadata": {"name": "polite"}, "value": 1000, "preemptionPolicy": "Never"})
+    with pytest.raises(HttpError):  # only one default
+        cp.create("1a1", "priorityclasses", "", {"metadata": {"name": "other"}, "value": 1, "globalDefault": True})
+    gpu_pod = lambda name, gpus, pc=None: {"metadata": {"name": name}, "spec": {
+        **({"priorityClassName": pc} if pc else {}),
+        "containers": [{"name": "c", "command": ["sleep", "60"], "resources": {"limits": {GPU: str(gpus)}}}]}}
+    with pytest.raises(HttpError) as e:
+        cp.create("1a1", "pods", "default", gpu_pod("x", 1, "nope"))
+    assert e.value.status == 403 and "no PriorityClass" in e.value.message
+    # a best-effort sweep fills all four GPUs (the default class)
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "sweep"}, "spec": {
+        "replicas": 4, "selector": {"matchLabels": {"app": "sweep"}}, "template": {
+            "metadata": {"labels": {"app": "sweep"}}, "spec": {"containers": [{"name": "c", "command": ["sleep", "60"],
+                                                                              "resources": {"limits": {GPU: "1"}}}]}}}})
+    sweep = _pods(cp, "sweep")
+    assert all(_node_of(cp, n) for n in sweep)
+    assert cp.store.get("pods", _key("1a1", "default", sweep[0]))["spec"]["priority"] == 10
+    # a polite high-priority pod waits
+    cp.create("1a1", "pods", "default", gpu_pod("polite", 2, "polite"))
+    assert _node_of(cp, "polite") is None
+    cp.store.delete("pods", _key("1a1", "default", "polite"))
+    # a production job takes a whole node: two sweep pods on one node are preempted
+    cp.create("1a1", "pods", "default", gpu_pod("train", 2, "prod"))
+    node = _node_of(cp, "train")
+    assert node is not None
+    p = cp.store.get("pods", _key("1a1", "default", "train"))
+    assert p["spec"]["priority"] == 1000 and p["status"]["nominatedNodeName"] == node
+    gone = [n for n in sweep if n not in _pods(cp)]
+    assert len(gone) == 2
+    assert len([e for e in cp.store.list("events") if e.get("reason") == "Preempted"]) == 2
+    # the sweep's replacements wait: lower priority cannot preempt the job back
+    new = [n for n in _pods(cp, "sweep") if n not in sweep]
+    assert len(new) == 2 and all(_node_of(cp, n) is None for n in new)
+    # the pod's priority comes from its class, not from the client
+    with pytest.raises(HttpError):
+        cp.create("1a1", "pods", "default", {**gpu_pod("cheat", 0, "low"), "spec": {
+            **gpu_pod("cheat", 0, "low")["spec"], "priority": 999999}})

@@ -7,6 +7,7 @@ from __future__ import annotations
 import copy
 import time
 
+from .httpserver import HttpError
 from .store import now_iso
 
 
@@ -86,6 +87,12 @@ class Controllers:
         pod = {"kind": "Pod", "apiVersion": "v1", "metadata": md, "spec": spec, "_project": pid,
                "status": {"phase": "Pending", "conditions": []}}
         spec.setdefault("restartPolicy", "Always")
+        try:
+            self._resolve_priority(pid, spec)
+        except HttpError as e:  # as the ReplicaSet controller's FailedCreate: nothing is created
+            self._event(pid, ns, {"kind": owner_kind, "name": owner["metadata"]["name"]}, "FailedCreate",
+                        f'Error creating: pods "{name}" is forbidden: {e.message}', "Warning")
+            return pod
         why = self._quota_block(pid, ns, name, pod)
         if why:  # as the ReplicaSet controller's 403: the pod waits (unscheduled) until the quota allows it
             from .objects import QUOTA_BLOCKED

@@ -828,6 +828,7 @@ class KubernetesAPI:
             spec = body.setdefault("spec", {})
             if not spec.get("containers"):
                 raise HttpError(422, "spec.containers is required")
+            self._resolve_priority(pid, spec)
             self._admit_quota(pid, ns, name, body)
             spec.setdefault("restartPolicy", "Always")
             body["status"] = {"phase": "Pending", "conditions": []}
@@ -848,6 +849,8 @@ class KubernetesAPI:
         elif kind == "poddisruptionbudgets":
             self._admit_pdb(name, body)
             md["generation"] = 1
+        elif kind == "priorityclasses":
+            self._admit_priority_class(pid, name, body)
         elif kind == "customresourcedefinitions":
             self._admit_crd(name, body)
         elif kind not in k8s_wire.RESOURCES:  # a custom resource: its type from the CRD
@@ -978,6 +981,11 @@ class KubernetesAPI:
                                      "after creation except resources.requests")
             new["status"] = {**cur.get("status", {}), "capacity": {"storage": (((new.get("spec") or {}).get("resources")
                                                                                   or {}).get("requests") or {}).get("storage", "")}}
+        if kind == "priorityclasses":
+            if new.get("value") != cur.get("value"):
+                raise HttpError(422, f'PriorityClass.scheduling.k8s.io "{name}" is invalid: value: Forbidden: may not be '
+                                     "changed in an update.")
+            self._admit_priority_class(pid, name, new)
         if kind in ("cronjobs", "poddisruptionbudgets"):
             (self._check_cronjob if kind == "cronjobs" else self._admit_pdb)(name, new.get("spec") if kind == "cronjobs" else new)
             md["generation"] = int(cur["metadata"].get("generation", 1)) + (1 if spec_changed else 0)

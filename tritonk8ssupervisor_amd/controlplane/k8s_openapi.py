@@ -43,6 +43,8 @@ _DESCRIPTIONS = {
     "CronJob": "A Job on a schedule.",
     "PersistentVolumeClaim": "Node-local storage that outlives pods (class tk8s-local).",
     "HorizontalPodAutoscaler": "Scales a workload by its pods' CPU or memory use.",
+    "PodDisruptionBudget": "How many of a set of pods voluntary disruptions (evictions, drains) may take down.",
+    "PriorityClass": "A named pod priority; higher-priority pods schedule first and may preempt lower ones.",
 }
 # the top-level fields each kind's objects may have (fieldValidation=Strict rejects others)
 _TOP = {"Pod": ("spec", "status"), "Service": ("spec", "status"), "Node": ("spec", "status"),
@@ -53,6 +55,8 @@ _TOP = {"Pod": ("spec", "status"), "Service": ("spec", "status"), "Node": ("spec
         "Role": ("rules",), "ClusterRole": ("rules", "aggregationRule"),
         "RoleBinding": ("roleRef", "subjects"), "ClusterRoleBinding": ("roleRef", "subjects"),
         "Secret": ("data", "stringData", "type", "immutable"),
+        "PriorityClass": ("value", "globalDefault", "description", "preemptionPolicy"),
+        "Endpoints": ("subsets",),
         "Event": ("involvedObject", "reason", "message", "source", "firstTimestamp", "lastTimestamp", "count",
                   "type", "eventTime", "series", "action", "related", "reportingComponent",
                   "reportingInstance")}

@@ -53,6 +53,7 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
                                   False, ("crd", "crds"), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
     "poddisruptionbudgets": ("policy", "v1", "PodDisruptionBudget", "poddisruptionbudget", True, ("pdb",), ("status",)),
+    "priorityclasses": ("scheduling.k8s.io", "v1", "PriorityClass", "priorityclass", False, ("pc",), ()),
 }
 READ_ONLY = {"namespaces": ("create", "delete", "get", "list", "patch", "watch"),
              "events": ("get", "list", "watch", "create", "delete")}

@@ -61,7 +61,8 @@ class Scheduler:
         by_name = {n["metadata"]["name"]: n for n in nodes}
         bound = [o for o in self.store.list("pods", lambda o: self._in(pid, o))
                  if o["spec"].get("nodeName") and o.get("status", {}).get("phase") not in TERMINAL] if rules else []
-        for pod in sorted(pending, key=lambda o: o["metadata"]["name"]):
+        # highest priority first (priority.py), then by name
+        for pod in sorted(pending, key=lambda o: (-int(o["spec"].get("priority") or 0), o["metadata"]["name"])):
             need = pod_gpus(pod)
             sel = pod["spec"].get("nodeSelector")
             key = _key(pid, pod["metadata"]["namespace"], pod["metadata"]["name"])
@@ -100,6 +101,10 @@ class Scheduler:
                 score = (-pref, count.get(nn, 0), -free, nn)
                 if best is None or score < best[0]:
                     best = (score, nn, free)
+            if best is None and not why and int(pod["spec"].get("priority") or 0) > 0:
+                nn = self._preempt(pid, pod, key, need, sel, nodes, used)
+                if nn is not None:
+                    best = (None, nn, 0)
             if best is None:
                 extra = "".join(f", {c} node(s) excluded by {w}" for w, c in sorted(why.items()))
                 self._unschedulable(pod, key, f"0/{len(nodes)} nodes available: need {need} {GPU}{extra}")

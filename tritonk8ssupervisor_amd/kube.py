@@ -35,6 +35,7 @@ KINDS = {
     "persistentvolumeclaim": ("PersistentVolumeClaim", "/api/v1", "persistentvolumeclaims"),
     "ingress": ("Ingress", "/apis/networking.k8s.io/v1", "ingresses"),
     "poddisruptionbudget": ("PodDisruptionBudget", "/apis/policy/v1", "poddisruptionbudgets"),
+    "priorityclass": ("PriorityClass", "/apis/scheduling.k8s.io/v1", "priorityclasses"),
 }
 ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", "ds": "daemonset",
            "daemonsets": "daemonset", "deploy": "deployment", "deployments": "deployment", "jobs": "job",
@@ -47,10 +48,11 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "sa": "serviceaccount", "serviceaccounts": "serviceaccount", "roles": "role", "rolebindings": "rolebinding",
            "clusterroles": "clusterrole", "clusterrolebindings": "clusterrolebinding", "crd": "customresourcedefinition",
            "crds": "customresourcedefinition", "customresourcedefinitions": "customresourcedefinition",
-           "pdb": "poddisruptionbudget", "poddisruptionbudgets": "poddisruptionbudget"}
+           "pdb": "poddisruptionbudget", "poddisruptionbudgets": "poddisruptionbudget",
+           "pc": "priorityclass", "priorityclasses": "priorityclass"}
 
 
-CLUSTER_SCOPED: set[str] = {"customresourcedefinition"}  # (+ kinds learnt from discovery without a namespace)
+CLUSTER_SCOPED: set[str] = {"customresourcedefinition", "priorityclass"}  # (+ kinds learnt from discovery without a namespace)
 
 
 def learn_kind(k: Client, name: str) -> str | None:
