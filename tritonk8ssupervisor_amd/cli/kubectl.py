@@ -31,6 +31,7 @@ from ..controlplane.client import ApiError, client_from_kubeconfig
 from ..kube import (apply_objects, collection_path, delete_objects, job_state, kind_key, load_manifests,
                     object_path, server_apply_objects, wait_job, wait_rollout)
 from ..utils.net import host_port
+from .kubectl_more import VERBS as MORE_VERBS, dispatch as more_dispatch
 
 GPU = "amd.com/gpu"
 
@@ -397,11 +398,13 @@ def _expose(k, a, ns: str) -> int:
     selecting the Deployment's pods."""
     if len(a.args) < 2 or kind_key(a.args[0]) != "deployment" or not a.port:
         raise SystemExit("usage: kubectl expose deployment NAME --port P [--target-port T] [--type TYPE] [--name SVC]")
+    if a.type not in (None, "ClusterIP", "NodePort", "LoadBalancer"):
+        raise SystemExit(f"error: --type must be ClusterIP, NodePort or LoadBalancer, not {a.type!r}")
     d = k.get(k.k8s(object_path("deployment", a.args[1], ns)))
     sel = d["spec"].get("selector", {}).get("matchLabels") or d["spec"]["template"]["metadata"].get("labels", {})
     name = a.name or a.args[1]
     body = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": name, "labels": dict(sel)},
-            "spec": {"type": a.type, "selector": sel,
+            "spec": {"type": a.type or "ClusterIP", "selector": sel,
                      "ports": [{"port": a.port, "targetPort": a.target_port or a.port, "protocol": "TCP"}]}}
     k.post(k.k8s(collection_path("service", ns)), body)
     print(f"service/{name} exposed")
@@ -532,7 +535,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--image")
     ap.add_argument("--port", type=int)
     ap.add_argument("--target-port", type=int)
-    ap.add_argument("--type", default="ClusterIP", choices=["ClusterIP", "NodePort", "LoadBalancer"])
+    ap.add_argument("--type")  # a Service type (expose) or a patch type (patch)
     ap.add_argument("--name")
     ap.add_argument("--server-side", action="store_true")
     ap.add_argument("--force-conflicts", action="store_true")
@@ -546,6 +549,19 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--disable-eviction", action="store_true")
     ap.add_argument("--delete-emptydir-data", action="store_true")  # (accepted: emptyDirs go with their pod)
     ap.add_argument("--force", action="store_true")
+    # run / set / autoscale / patch / api-resources / auth (kubectl_more.py)
+    ap.add_argument("--env", action="append", default=[])
+    ap.add_argument("--labels")
+    ap.add_argument("--restart", choices=["Always", "OnFailure", "Never"])
+    ap.add_argument("--limits")
+    ap.add_argument("--requests")
+    ap.add_argument("--command", dest="command_flag", action="store_true")
+    ap.add_argument("-p", "--patch")
+    ap.add_argument("--min", type=int)
+    ap.add_argument("--max", type=int)
+    ap.add_argument("--cpu-percent", type=int)
+    ap.add_argument("--namespaced", choices=["true", "false"])
+    ap.add_argument("--subresource")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -562,7 +578,10 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     a.command = command
     workdir = workdir or os.environ.get("TK8S_WORKDIR", os.getcwd())
     try:
-        k = client_from_kubeconfig(_load_kubeconfig(a.kubeconfig, workdir))
+        cfg = _load_kubeconfig(a.kubeconfig, workdir)
+        if a.verb == "config":
+            return more_dispatch(None, a, a.namespace, cfg)
+        k = client_from_kubeconfig(cfg)
     except (OSError, ValueError, KeyError, StopIteration) as e:
         print(f"error: no usable kubeconfig ({e}); run ./setup.sh first", file=sys.stderr)
         return 1
@@ -576,6 +595,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 learn_kind(k, word)  # a custom resource: ask discovery where it lives
         if a.verb in ("version",):
             print(json.dumps(k.get("/version"), indent=1))
+        elif a.verb in MORE_VERBS:
+            return more_dispatch(k, a, ns, cfg)
         elif a.verb == "cluster-info":
             print(f"Kubernetes control plane is running at {k.base}{k.prefix}")
         elif a.verb == "get":
@@ -672,8 +693,12 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
         elif a.verb == "rollout":
             sub = a.args[0] if a.args else ""
             what, name = _target(a.args[1:])
-            if kind_key(what) != "deployment" or sub not in ("status", "restart", "history", "undo"):
-                raise SystemExit("usage: kubectl rollout status|restart|history|undo deploy/NAME")
+            if kind_key(what) != "deployment" or sub not in ("status", "restart", "history", "undo", "pause", "resume"):
+                raise SystemExit("usage: kubectl rollout status|restart|history|undo|pause|resume deploy/NAME")
+            if sub in ("pause", "resume"):
+                from .kubectl_more import rollout_pause
+
+                return rollout_pause(k, name, ns, sub == "pause")
             if sub in ("history", "undo"):
                 return _rollout_history(k, name, ns, sub, a.to_revision)
             if sub == "restart":  # a new template annotation = a new pod-template-hash = a rolling update

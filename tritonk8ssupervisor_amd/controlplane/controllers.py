@@ -269,12 +269,22 @@ class Controllers:
         """Deployment controller with ReplicaSet-style generations: pods carry the
         ``pod-template-hash`` of the template they came from. A changed template rolls out with
         the RollingUpdate defaults (maxSurge 25 % rounded up, maxUnavailable 25 % rounded down;
-        an old pod goes only when a new one runs), ``strategy: Recreate`` drops the old pods first."""
+        an old pod goes only when a new one runs), ``strategy: Recreate`` drops the old pods first.
+        ``spec.paused`` (``kubectl rollout pause``) holds template changes back: the newest
+        ReplicaSet's template keeps being scaled until the rollout is resumed."""
         for d in self.store.list("deployments", lambda o: self._in(pid, o)):
             ns, dname = d["metadata"]["namespace"], d["metadata"]["name"]
             spec = d["spec"]
             want = int(spec.get("replicas", 1))
             h = template_hash(spec["template"])
+            tmpl = spec["template"]
+            if spec.get("paused"):
+                newest = max((rs for rs in self.store.list("replicasets", lambda o: self._in(pid, o) and any(
+                    r.get("uid") == d["metadata"]["uid"] for r in o["metadata"].get("ownerReferences", [])))),
+                    key=lambda rs: int((rs["metadata"].get("annotations") or {}).get(REVISION, "0") or 0), default=None)
+                if newest is not None:
+                    h = newest["metadata"]["labels"]["pod-template-hash"]
+                    tmpl = newest["spec"]["template"]
             match = (spec.get("selector") or {}).get("matchLabels") or {}
 
             def live():
@@ -293,7 +303,7 @@ class Controllers:
                 for _ in range(max(0, min(want - len(new), want + surge - len(pods)))):
                     self._seq += 1
                     new.append(self._new_pod(pid, ns, f"{dname}-{h[:8]}-{self._seq:x}", d, "Deployment",
-                                             spec["template"], labels={**match, "pod-template-hash": h}))
+                                             tmpl, labels={**match, "pod-template-hash": h}))
                 ready_new = sum(1 for o in new if o.get("status", {}).get("phase") == "Running")
                 keep_old = max(0, want - unavailable - ready_new)
                 for o in sorted(old, key=lambda o: o["metadata"]["name"])[keep_old:]:
@@ -301,7 +311,7 @@ class Controllers:
                 for o in sorted(new, key=lambda o: o["metadata"]["name"])[want:]:
                     self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
             pods = live()
-            self._sync_deployment_revisions(pid, d, h, pods)
+            self._sync_deployment_revisions(pid, d, h, pods, tmpl)
             running = sum(1 for o in pods if o.get("status", {}).get("phase") == "Running")
             status = {"observedGeneration": int(d["metadata"].get("generation", 1)), "replicas": len(pods),
                       "updatedReplicas": sum(1 for o in pods if o["metadata"].get("labels", {}).get("pod-template-hash") == h),
@@ -312,12 +322,13 @@ class Controllers:
                 ("Available", *(("True", "MinimumReplicasAvailable", "Deployment has minimum availability.")
                                 if running >= want - unavailable else
                                 ("False", "MinimumReplicasUnavailable", "Deployment does not have minimum availability."))),
+                ("Progressing", "Unknown", "DeploymentPaused", "Deployment is paused") if spec.get("paused") else
                 ("Progressing", "True", *(("NewReplicaSetAvailable", f'ReplicaSet "{dname}-{h}" has successfully progressed.')
                                           if done else ("ReplicaSetUpdated", f'ReplicaSet "{dname}-{h}" is progressing.')))])
             if d.get("status") != status:
                 self.store.patch("deployments", _key(pid, ns, dname), lambda o, s=status: o.__setitem__("status", s))
 
-    def _sync_deployment_revisions(self, pid: str, d: dict, h: str, pods: list[dict]) -> None:
+    def _sync_deployment_revisions(self, pid: str, d: dict, h: str, pods: list[dict], template: dict | None = None) -> None:
         """A ReplicaSet per pod template the Deployment has had (``<name>-<pod-template-hash>``,
         annotation ``deployment.kubernetes.io/revision``), as Kubernetes keeps them: what
         ``kubectl get rs``, ``kubectl rollout history`` and ``kubectl rollout undo`` read. The pods
@@ -344,7 +355,7 @@ class Controllers:
         for ph in set(owned) | {h}:
             rs = owned.get(ph)
             n = counts.get(ph, 0)
-            tmpl = copy.deepcopy(d["spec"]["template"]) if ph == h else (rs or {}).get("spec", {}).get("template")
+            tmpl = copy.deepcopy(template or d["spec"]["template"]) if ph == h else (rs or {}).get("spec", {}).get("template")
             if tmpl is None:
                 continue
             tmpl.setdefault("metadata", {}).setdefault("labels", {})["pod-template-hash"] = ph
