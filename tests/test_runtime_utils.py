@@ -428,3 +428,44 @@ def test_probe_handlers_and_prober(tmp_path):
     while not killed and tm.monotonic() < deadline:
         tm.sleep(0.02)
     assert killed and "livenessProbe failed 2 times" in p.last_message
+
+
+def test_prestop_hook_sigterm_then_sigkill_after_the_grace_period(tmp_path):
+    """Deleting a pod: preStop runs first, the container gets SIGTERM (a trainer's checkpoint
+    window), and what ignores it is SIGKILLed when terminationGracePeriodSeconds runs out; the
+    pod's GPUs stay held meanwhile."""
+    rt, events, wait_for = _runtime(tmp_path)
+    marks = tmp_path / "marks"
+    code = ("import signal,time,pathlib\n"
+            f"p=pathlib.Path({str(marks)!r})\n"
+            "def term(*_):\n    p.open('a').write('term\\n')\n"
+            "signal.signal(signal.SIGTERM, term)\n"
+            "p.open('a').write('up\\n')\n"
+            "while True: time.sleep(0.05)\n")
+    pp = _pod(tmp_path, "trainer", [sys.executable, "-c", code], "Always")
+    pp.grace, pp.gpu_ids = 1.5, ["gpu0"]
+    pp.container = {"lifecycle": {"preStop": {"exec": {"command": ["sh", "-c", f"echo prestop >> {marks}"]}}}}
+    rt.start(pp)
+    wait_for(lambda ev: marks.exists() and "up" in marks.read_text())
+    done = threading.Event()
+    t = time.monotonic()
+    rt.stop("default/trainer", wait=False, on_done=done.set)
+    assert rt.is_terminating("default/trainer") and rt.held_gpus() == {"gpu0"}
+    assert done.wait(10)
+    took = time.monotonic() - t
+    assert 1.4 < took < 6, took  # SIGTERM ignored: killed at the end of the grace period
+    assert marks.read_text().split() == ["up", "prestop", "term"]
+    assert not rt.is_terminating("default/trainer") and rt.held_gpus() == set()
+
+
+def test_poststart_hook_failure_restarts_the_container(tmp_path):
+    rt, events, wait_for = _runtime(tmp_path)
+    n = tmp_path / "starts"
+    pp = _pod(tmp_path, "hooked", ["sh", "-c", f"echo x >> {n}; sleep 30"], "Always")
+    flag = tmp_path / "ok"
+    pp.container = {"lifecycle": {"postStart": {"exec": {"command": ["sh", "-c", f"test -e {flag}"]}}}}
+    rt.start(pp)
+    wait_for(lambda ev: n.exists() and len(n.read_text().split()) >= 2)  # killed by the failing hook, restarted
+    flag.write_text("")
+    assert "FailedPostStartHook" in (tmp_path / "pods" / "hooked" / "log").read_text()
+    rt.stop("default/hooked", grace=1.0)

@@ -340,10 +340,7 @@ class Agent:
         return self.ip
 
     def _free_devices(self) -> list[str]:
-        used = set()
-        for pp in self.runtime.running().values():
-            if not pp.done.is_set():
-                used.update(pp.gpu_ids)
+        used = self.runtime.held_gpus()  # (a deleted pod's GPUs stay held through its grace period)
         if self.dp_client is not None:  # what the plugin's ListAndWatch last reported
             healthy = self.dp_client.healthy()
         else:
@@ -358,6 +355,9 @@ class Agent:
         md, spec = pod["metadata"], pod["spec"]
         key = f"{md['namespace']}/{md['name']}"
         if key in self.runtime.running():
+            return
+        if self.runtime.is_terminating(key):  # the same name's previous pod is still shutting down
+            self._config_wait[key] = pod
             return
         all_gpus = md.get("annotations", {}).get(ALL_GPUS) == "true"
         need = len(self.plugin.devices()) if all_gpus else pod_gpus(pod)
@@ -468,7 +468,8 @@ class Agent:
                                  gpu_ids=ids if first_app else [], ip=pod_ip,
                                  isolate=avail and not gpu_pod and built["image"] is None, jail=built["jail"],
                                  exec_prefix=built["exec_prefix"], name=cont.get("name") or f"c{n}", container=cont,
-                                 log_name="log" if first_app else f"log.{cont.get('name') or n}"))
+                                 log_name="log" if first_app else f"log.{cont.get('name') or n}",
+                                 grace=float(spec.get("terminationGracePeriodSeconds", 30))))
         pp = procs[len(inits)]
         pp.init, pp.sidecars = procs[:len(inits)], procs[len(inits) + 1:]
         self._pods_meta[key] = {"name": md["name"], "namespace": md["namespace"],
@@ -756,9 +757,8 @@ class Agent:
         key = f"{md['namespace']}/{md['name']}"
         if etype == "DELETED":
             self._config_wait.pop(key, None)
-            self.runtime.stop(key)
             self._pods_meta.pop(key, None)
-            self._pod_ips.pop(key, None)
+            self.runtime.stop(key, wait=False, on_done=lambda: self._terminated(key))
             return
         phase = pod.get("status", {}).get("phase", "Pending")
         if phase in TERMINAL:
@@ -766,12 +766,19 @@ class Agent:
         cur = self.runtime.running().get(key)
         if cur is not None and md.get("uid") and cur.uid and cur.uid != md["uid"]:
             # the same name, a new pod (a StatefulSet's replacement) whose deletion event this
-            # watch did not see: the old process goes first
-            self.runtime.stop(key)
-            self._pod_ips.pop(key, None)
+            # watch did not see: the old process goes first (the new one starts when it is gone)
+            self.runtime.stop(key, wait=False, on_done=lambda: self._terminated(key))
         if key not in self.runtime.running():
             trace(self.name, f"watch {etype} {key}")
             self._start_pod(pod)
+
+    def _terminated(self, key: str) -> None:
+        """A pod's termination is over: its IP is free, and a successor of the same name may start."""
+        if key not in self.runtime.running():
+            self._pod_ips.pop(key, None)
+        nxt = self._config_wait.get(key)
+        if nxt is not None:
+            self._start_pod(nxt)
 
     # ---- lifecycle --------------------------------------------------------------------
     def run(self, await_url: Path | None = None) -> int:

@@ -11,6 +11,14 @@ with back-off, or the pod fails with ``Init:Error`` under ``restartPolicy: Never
 app container runs as its own process group. The first is the pod's ``PodProc`` (log ``log``);
 the others are its ``sidecars`` (log ``log.<name>``), restarted under the same policy. The pod
 ends once every app container has ended, Succeeded if all exited 0.
+
+Lifecycle hooks and graceful termination, as the kubelet does them: a container's
+``lifecycle.postStart`` (exec, httpGet or sleep) runs right after it starts -- a failing hook kills
+the container, which restarts under the policy; deleting a pod runs every container's
+``lifecycle.preStop`` hook, then SIGTERMs all its process groups and SIGKILLs what is left when
+``terminationGracePeriodSeconds`` (default 30) runs out -- the window a training job gets to write
+its checkpoint. Termination runs off the caller's thread (``stop(wait=False)``); the pod's GPUs
+stay allocated until it is over.
 """
 from __future__ import annotations
 
@@ -79,6 +87,7 @@ class PodProc:
     sidecars: list = field(default_factory=list)  # the pod's other app containers (PodProc each)
     container: dict = field(default_factory=dict)  # its spec (probes, ports)
     prober: object = None         # agent/probes.Prober of the running process, if it has probes
+    grace: float = 30.0           # terminationGracePeriodSeconds
     proc: subprocess.Popen | None = None
     restarts: int = 0
     started: float = 0.0
@@ -92,6 +101,7 @@ class PodRuntime:
         self.sandbox = Path(sandbox)
         self.on_status = on_status        # callback(podproc, phase, extra: dict)
         self.pods: dict[str, PodProc] = {}
+        self.terminating: dict[str, PodProc] = {}  # deleted, within their grace period
         self.lock = threading.Lock()
         self.tool_dirs = tool_dirs or []
 
@@ -167,6 +177,7 @@ class PodRuntime:
             except OSError:
                 sc.exit_code = 127
                 break
+            self._post_start(sc, pp)
             self._probe(sc, pp)
             if pp.proc is not None and pp.proc.poll() is None:
                 self.on_status(pp, "Running", {})  # its container statuses now include this one
@@ -197,6 +208,7 @@ class PodRuntime:
                 self.on_status(pp, "Failed", {"message": f"failed to start {pp.argv[0]!r}: {e}", "reason": "StartError"})
                 break
             trace("runtime", f"spawned {pp.key}")
+            self._post_start(pp, pp)
             self._probe(pp, pp)
             self.on_status(pp, "Running", {})
             rc = pp.proc.wait()
@@ -232,19 +244,107 @@ class PodRuntime:
             backoff = min(backoff * 2, 10.0)
         pp.done.set()
 
-    def stop(self, key: str, grace: float = 2.0) -> PodProc | None:
+    def _hook(self, cp: PodProc, hook: dict, timeout: float) -> str | None:
+        """Run one lifecycle handler (exec / httpGet / sleep); None if it succeeded, else why not."""
+        if timeout <= 0:
+            return "no time left"
+        if "exec" in hook:
+            cmd = (hook["exec"] or {}).get("command") or []
+            try:
+                r = subprocess.run(container_exec_argv(cp, [expand(x, cp.env) for x in cmd]), env=dict(cp.env),
+                                   cwd=cp.dir, capture_output=True, timeout=timeout)
+            except (OSError, subprocess.TimeoutExpired) as e:
+                return str(e)
+            return None if r.returncode == 0 else f"exited {r.returncode}: {r.stderr.decode(errors='replace')[-200:]}"
+        if "httpGet" in hook:
+            import urllib.request
+
+            h = hook["httpGet"] or {}
+            port = h.get("port")
+            if isinstance(port, str) and not port.isdigit():
+                port = next((p.get("containerPort") for p in cp.container.get("ports") or [] if p.get("name") == port), port)
+            url = f"{(h.get('scheme') or 'HTTP').lower()}://{h.get('host') or cp.ip or '127.0.0.1'}:{port}{h.get('path') or '/'}"
+            try:
+                with urllib.request.urlopen(url, timeout=timeout) as r:
+                    return None if 200 <= r.status < 400 else f"HTTP {r.status}"
+            except OSError as e:
+                return str(e)
+        if "sleep" in hook:
+            time.sleep(min(float((hook["sleep"] or {}).get("seconds", 0)), timeout))
+            return None
+        return "unsupported handler"
+
+    def _post_start(self, cp: PodProc, pp: PodProc) -> None:
+        hook = (cp.container.get("lifecycle") or {}).get("postStart")
+        if not hook or cp.proc is None:
+            return
+        why = self._hook(cp, hook, 30.0)
+        if why is not None and cp.proc.poll() is None and not pp.stopping:
+            trace("runtime", f"postStart hook of {cp.key} failed: {why}")
+            with open(pp.dir / cp.log_name, "a") as f:
+                f.write(f"[tk8s] FailedPostStartHook: {why}\n")
+            kill_group(cp.proc.pid, 1.0)  # the container restarts under the pod's restartPolicy
+
+    def _terminate(self, pp: PodProc, grace: float) -> None:
+        """preStop hooks, SIGTERM to every container, SIGKILL at the end of the grace period."""
+        deadline = time.monotonic() + grace
+        conts = [c for c in (pp, *pp.sidecars) if c.proc is not None and c.proc.poll() is None]
+        hooks = [threading.Thread(target=self._hook, args=(c, c.container["lifecycle"]["preStop"], grace), daemon=True)
+                 for c in conts if (c.container.get("lifecycle") or {}).get("preStop")]
+        for t in hooks:
+            t.start()
+        for t in hooks:
+            t.join(max(0.0, deadline - time.monotonic()))
+        groups = [c.proc.pid for c in (pp, *pp.sidecars, *pp.init) if c.proc is not None and c.proc.poll() is None]
+        for g in groups:
+            try:
+                os.killpg(g, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+        for g in groups:  # the rest of the grace period, shared; kill_group SIGKILLs what outlives it
+            kill_group(g, max(0.0, deadline - time.monotonic()), term=False)
+
+    def stop(self, key: str, grace: float | None = None, wait: bool = True, on_done=None) -> PodProc | None:
+        """Stop a pod: ``grace`` defaults to its terminationGracePeriodSeconds. ``wait=False``
+        terminates in a thread (the pod is in ``terminating`` meanwhile) and calls ``on_done``."""
         with self.lock:
             pp = self.pods.pop(key, None)
+            if pp is not None:
+                self.terminating[key] = pp
         if pp is None:
+            if on_done is not None:
+                on_done()
             return None
         pp.stopping = True
         for c in (pp, *pp.sidecars):
             if c.prober is not None:
                 c.prober.stop.set()
-        for c in (pp, *pp.sidecars, *pp.init):
-            if c.proc is not None and c.proc.poll() is None:
-                kill_group(c.proc.pid, grace)
+
+        def run():
+            try:
+                self._terminate(pp, pp.grace if grace is None else grace)
+            finally:
+                with self.lock:
+                    if self.terminating.get(key) is pp:
+                        del self.terminating[key]
+                if on_done is not None:
+                    on_done()
+
+        if wait:
+            run()
+        else:
+            threading.Thread(target=run, name=f"stop-{key}", daemon=True).start()
         return pp
+
+    def is_terminating(self, key: str) -> bool:
+        with self.lock:
+            return key in self.terminating
+
+    def held_gpus(self) -> set[str]:
+        """GPUs of running pods and of pods still within their grace period."""
+        with self.lock:
+            return ({i for pp in self.pods.values() if not pp.done.is_set() for i in pp.gpu_ids}
+                    | {i for pp in self.terminating.values() for i in pp.gpu_ids})
 
     def stop_all(self) -> None:
         for key in list(self.pods):

@@ -114,10 +114,11 @@ def group_alive(pgid: int) -> bool:
     return False
 
 
-def kill_group(pgid: int, grace: float = 3.0) -> bool:
-    """SIGTERM the process group, wait up to `grace` s, then SIGKILL. True if it was alive."""
+def kill_group(pgid: int, grace: float = 3.0, term: bool = True) -> bool:
+    """SIGTERM the process group (unless ``term`` is False: the caller already did), wait up to
+    `grace` s, then SIGKILL. True if it was alive."""
     try:
-        os.killpg(pgid, signal.SIGTERM)
+        os.killpg(pgid, signal.SIGTERM if term else 0)
     except ProcessLookupError:
         return False
     except PermissionError:
