@@ -145,7 +145,7 @@ def cluster(tmp_path, monkeypatch):
         shutil.copy2(REPO / f, tmp_path / f)
     env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_FAKE_GPUS="8",
                TK8S_REMAP_PRIVILEGED_PORTS="1",  # exercise the non-root port shift even as root
-               TK8S_METRICS_PERIOD="0.5")
+               TK8S_METRICS_PERIOD="0.5", TK8S_VOLUME_SYNC_PERIOD="0.5")
     env.pop("TK8S_FAULTS", None)
     r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "2", "--rccl", "off"], cwd=tmp_path,
                        env=env, capture_output=True, text=True, timeout=180)
@@ -502,3 +502,27 @@ def test_kubectl_cp_both_ways(cluster, tmp_path_factory):
     back = tmp_path_factory.mktemp("cpback") / "out"
     kc("cp", "store:incoming", str(back))
     assert (back / "weights.bin").read_bytes() == bytes(range(256)) * 100 and (back / "cfg.txt").read_text() == "lr=3e-4\n"
+
+
+def test_configmap_volume_updates_reach_a_running_pod(cluster):
+    """kubectl apply of a changed ConfigMap: the running pod's volume shows the new data within a
+    sync period, and a lifecycle preStop hook runs when the pod is deleted."""
+    ws, env, kc, summary = cluster
+    cm = lambda v: {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "live"}, "data": {"mode": v}}
+    (ws / "cm.json").write_text(json.dumps(cm("slow")))
+    kc("apply", "-f", str(ws / "cm.json"))
+    (ws / "pod.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "watcher"}, "spec": {
+        "terminationGracePeriodSeconds": 5,
+        "containers": [{"name": "c", "command": ["sh", "-c", "sleep 300"],
+                        "volumeMounts": [{"name": "cfg", "mountPath": "/etc/live"}],
+                        "lifecycle": {"preStop": {"exec": {"command": ["sh", "-c", "echo bye > $TK8S_VOLUME_SCRATCH/bye"]}}}}],
+        "volumes": [{"name": "cfg", "configMap": {"name": "live"}}, {"name": "scratch", "hostPath": {
+            "path": str(ws / "scratch"), "type": "DirectoryOrCreate"}}]}}))
+    kc("apply", "-f", str(ws / "pod.json"))
+    read = lambda: kc("exec", "watcher", "--", "sh", "-c", "cat $TK8S_VOLUME_CFG/mode", check=False).stdout
+    assert _until(lambda: read() == "slow", timeout=30)
+    (ws / "cm.json").write_text(json.dumps(cm("fast")))
+    kc("apply", "-f", str(ws / "cm.json"))
+    assert _until(lambda: read() == "fast", timeout=20)
+    kc("delete", "pod", "watcher")
+    assert _until(lambda: (ws / "scratch" / "bye").exists(), timeout=20)

@@ -5,13 +5,21 @@
                          picks and renames keys; ``defaultMode``/item ``mode``; ``optional``)
 * ``secret``          -- the same for a Secret (``secretName``), decoded, mode 0644 by default
 * ``downwardAPI``     -- ``fieldRef`` items as files (metadata.name, labels, annotations, ...)
+* ``projected``       -- configMap, secret, downwardAPI and serviceAccountToken sources in one
+                         directory
 * ``hostPath``        -- a node path (``DirectoryOrCreate``/``FileOrCreate`` create it)
 * ``persistentVolumeClaim`` -- a node-local directory per claim (``<node dir>/volumes/<ns>_<claim>``),
                          on the node the scheduler bound the claim to (``volume.kubernetes.io/
                          selected-node``); it outlives pods, so a StatefulSet's ordinal finds its
                          data again
 
-``materialize`` returns the mounts of one container: (source path, mountPath, read-only), with
+ConfigMap, Secret, downwardAPI and projected volumes are published as the kubelet's atomic writer
+does: the files live in a timestamped ``..<time>`` directory, ``..data`` links to the current one
+and every top-level entry links through ``..data``, so ``refresh`` (the agent calls it every
+``TK8S_VOLUME_SYNC_PERIOD`` s) swaps a changed ConfigMap in with one rename -- a running pod
+sees the old set of files or the new one, never a mix. ``subPath`` mounts keep what they got.
+
+``mounts`` returns the mounts of one container: (source path, mountPath, read-only), with
 ``subPath`` applied. Image pods get them bind-mounted at ``mountPath`` (tk8s-container
 ``--bind``/``--bind-ro``); process pods share the host's file system, so they get each volume's
 directory in ``TK8S_VOLUME_<NAME>`` instead.
@@ -21,6 +29,8 @@ from __future__ import annotations
 import base64
 import os
 import re
+import shutil
+import time
 from pathlib import Path
 from typing import Callable
 
@@ -38,15 +48,48 @@ def _safe_rel(p: str) -> str:
     return str(Path(*parts))
 
 
-def _write_files(root: Path, files: dict[str, bytes], modes: dict[str, int]) -> None:
+def _current(root: Path) -> dict[str, tuple[bytes, int]]:
+    """What ``root/..data`` holds now: relative path -> (bytes, mode)."""
+    data = root / "..data"
+    out = {}
+    if data.is_dir():
+        for p in data.resolve().rglob("*"):
+            if p.is_file():
+                out[str(p.relative_to(data.resolve()))] = (p.read_bytes(), p.stat().st_mode & 0o777)
+    return out
+
+
+def _write_files(root: Path, files: dict[str, bytes], modes: dict[str, int]) -> bool:
+    """Publish ``files`` under ``root`` atomically (see the module doc); False if nothing changed."""
+    want = {_safe_rel(rel): (data, modes.get(rel, 0o644)) for rel, data in files.items()}
     root.mkdir(parents=True, exist_ok=True)
-    for rel, data in files.items():
-        dst = root / _safe_rel(rel)
+    if (root / "..data").exists() and _current(root) == want:
+        return False
+    ts = root / f"..{time.strftime('%Y_%m_%d_%H_%M_%S', time.gmtime())}.{time.time_ns() % 10**9:09d}"
+    ts.mkdir()
+    for rel, (data, mode) in want.items():
+        dst = ts / rel
         dst.parent.mkdir(parents=True, exist_ok=True)
-        tmp = dst.with_name(f".{dst.name}.tmp")
-        tmp.write_bytes(data)
-        os.chmod(tmp, modes.get(rel, 0o644))
-        os.replace(tmp, dst)
+        dst.write_bytes(data)
+        os.chmod(dst, mode)
+    tmp = root / "..data_tmp"
+    tmp.unlink(missing_ok=True)
+    os.symlink(ts.name, tmp)
+    os.replace(tmp, root / "..data")  # the switch: one rename
+    tops = {rel.split("/", 1)[0] for rel in want}
+    for top in tops:
+        link = root / top
+        if not link.is_symlink():
+            if link.is_file():  # a plain file from before (an older agent): replace it
+                link.unlink()
+            os.symlink(f"..data/{top}", link)
+    for p in root.iterdir():
+        if p.name.startswith(".."):
+            if p.name not in ("..data", ts.name) and p.is_dir() and not p.is_symlink():
+                shutil.rmtree(p, ignore_errors=True)
+        elif p.is_symlink() and p.name not in tops:
+            p.unlink()  # a key that is gone
+    return True
 
 
 def _key_files(vol: dict, data: dict[str, bytes], what: str) -> tuple[dict[str, bytes], dict[str, int]]:
@@ -68,6 +111,98 @@ def _key_files(vol: dict, data: dict[str, bytes], what: str) -> tuple[dict[str, 
 
 def env_name(volume: str) -> str:
     return "TK8S_VOLUME_" + re.sub(r"[^A-Z0-9_]", "_", volume.upper())
+
+
+def _config_files(src: dict, is_secret: bool, ns: str, fetch) -> tuple[dict[str, bytes], dict[str, int]]:
+    obj_name = src.get("secretName") if is_secret and "secretName" in src else src.get("name")
+    kind = "secrets" if is_secret else "configmaps"
+    o = fetch(kind, ns, obj_name)
+    if o is None:
+        if not src.get("optional"):
+            raise VolumeError(f'{kind[:-1]} "{obj_name}" not found')
+        o = {}
+    if is_secret:
+        data = {k: base64.b64decode(v) for k, v in (o.get("data") or {}).items()}
+    else:
+        data = {k: str(v).encode() for k, v in (o.get("data") or {}).items()}
+        data.update({k: base64.b64decode(v) for k, v in (o.get("binaryData") or {}).items()})
+    return _key_files(src, data, f"{kind[:-1]} {obj_name}")
+
+
+def _downward_files(pod: dict, src: dict, pod_ip: str, host_ip: str,
+                    default: int = 0o644) -> tuple[dict[str, bytes], dict[str, int]]:
+    files, modes = {}, {}
+    for it in src.get("items") or []:
+        ref = (it.get("fieldRef") or {}).get("fieldPath", "")
+        md = pod["metadata"]
+        if ref in ("metadata.labels", "metadata.annotations"):
+            d = md.get(ref.split(".")[1]) or {}
+            text = "".join(f'{k}="{v}"\n' for k, v in sorted(d.items()))
+        else:
+            try:
+                text = field_path(pod, ref, pod_ip, host_ip)
+            except ValueError as e:
+                raise VolumeError(str(e)) from e
+        files[it["path"]] = text.encode()
+        modes[it["path"]] = int(it.get("mode", src.get("defaultMode", default)))
+    return files, modes
+
+
+def _projected_files(pod: dict, vol: dict, ns: str, fetch, pod_ip: str, host_ip: str):
+    """A projected volume's sources merged into one directory (later sources win a clash)."""
+    default = int(vol.get("defaultMode", 0o644))
+    files, modes = {}, {}
+    for s in vol.get("sources") or []:
+        if "configMap" in s or "secret" in s:
+            sec = "secret" in s
+            f, m = _config_files({"defaultMode": default, **(s["secret"] if sec else s["configMap"])}, sec, ns, fetch)
+        elif "downwardAPI" in s:
+            f, m = _downward_files(pod, s["downwardAPI"], pod_ip, host_ip, default)
+        elif "serviceAccountToken" in s:
+            sa = pod["spec"].get("serviceAccountName") or pod["spec"].get("serviceAccount") or "default"
+            tok = fetch("secrets", ns, f"{sa}-token")
+            if tok is None:
+                raise VolumeError(f'serviceaccount "{sa}" has no token yet')
+            path = s["serviceAccountToken"].get("path", "token")
+            f, m = {path: base64.b64decode((tok.get("data") or {}).get("token", ""))}, {path: 0o600}
+        else:
+            raise VolumeError(f"projected source {sorted(s)} is not supported")
+        files.update(f)
+        modes.update(m)
+    return files, modes
+
+
+_DYNAMIC = ("configMap", "secret", "downwardAPI", "projected")
+
+
+def _render(pod: dict, vol: dict, fetch, pod_ip: str, host_ip: str) -> tuple[dict[str, bytes], dict[str, int]]:
+    ns = pod["metadata"]["namespace"]
+    if "configMap" in vol or "secret" in vol:
+        return _config_files(vol["secret"] if "secret" in vol else vol["configMap"], "secret" in vol, ns, fetch)
+    if "downwardAPI" in vol:
+        return _downward_files(pod, vol["downwardAPI"], pod_ip, host_ip)
+    return _projected_files(pod, vol["projected"], ns, fetch, pod_ip, host_ip)
+
+
+def refresh(pod: dict, pod_dir: Path, fetch: Callable[[str, str, str], dict | None], pod_ip: str = "",
+            host_ip: str = "") -> list[str]:
+    """Re-publish the pod's ConfigMap/Secret/downwardAPI/projected volumes; the names that changed.
+    A source that is gone (or unreachable) leaves the volume as it is, as the kubelet does."""
+    changed = []
+    for vol in pod["spec"].get("volumes") or []:
+        if not any(k in vol for k in _DYNAMIC):
+            continue
+        try:
+            files, modes = _render(pod, vol, fetch, pod_ip, host_ip)
+        except VolumeError:
+            continue
+        if _write_files(pod_dir / "volumes" / vol.get("name", ""), files, modes):
+            changed.append(vol.get("name", ""))
+    return changed
+
+
+def has_dynamic(pod: dict) -> bool:
+    return any(any(k in v for k in _DYNAMIC) for v in pod["spec"].get("volumes") or [])
 
 
 def volume_dirs(pod: dict, pod_dir: Path, node_dir: Path, fetch: Callable[[str, str, str], dict | None],
@@ -93,39 +228,8 @@ def volume_dirs(pod: dict, pod_dir: Path, node_dir: Path, fetch: Callable[[str, 
             elif kind in ("Directory", "File") and not p.exists():
                 raise VolumeError(f"hostPath {p} does not exist")
             out[name] = (p, False)
-        elif "configMap" in vol or "secret" in vol:
-            is_secret = "secret" in vol
-            src = vol["secret"] if is_secret else vol["configMap"]
-            obj_name = src.get("secretName") if is_secret else src.get("name")
-            kind = "secrets" if is_secret else "configmaps"
-            o = fetch(kind, ns, obj_name)
-            if o is None:
-                if not src.get("optional"):
-                    raise VolumeError(f'{kind[:-1]} "{obj_name}" not found')
-                o = {}
-            if is_secret:
-                data = {k: base64.b64decode(v) for k, v in (o.get("data") or {}).items()}
-            else:
-                data = {k: str(v).encode() for k, v in (o.get("data") or {}).items()}
-                data.update({k: base64.b64decode(v) for k, v in (o.get("binaryData") or {}).items()})
-            files, modes = _key_files(src, data, f"{kind[:-1]} {obj_name}")
-            _write_files(own, files, modes)
-            out[name] = (own, True)
-        elif "downwardAPI" in vol:
-            files, modes = {}, {}
-            for it in vol["downwardAPI"].get("items") or []:
-                ref = (it.get("fieldRef") or {}).get("fieldPath", "")
-                md = pod["metadata"]
-                if ref in ("metadata.labels", "metadata.annotations"):
-                    d = md.get(ref.split(".")[1]) or {}
-                    text = "".join(f'{k}="{v}"\n' for k, v in sorted(d.items()))
-                else:
-                    try:
-                        text = field_path(pod, ref, pod_ip, host_ip)
-                    except ValueError as e:
-                        raise VolumeError(str(e)) from e
-                files[it["path"]] = text.encode()
-                modes[it["path"]] = int(it.get("mode", vol["downwardAPI"].get("defaultMode", 0o644)))
+        elif any(k in vol for k in _DYNAMIC):
+            files, modes = _render(pod, vol, fetch, pod_ip, host_ip)
             _write_files(own, files, modes)
             out[name] = (own, True)
         elif "persistentVolumeClaim" in vol:
@@ -140,7 +244,7 @@ def volume_dirs(pod: dict, pod_dir: Path, node_dir: Path, fetch: Callable[[str, 
         else:
             kinds = [k for k in vol if k != "name"]
             raise VolumeError(f"volume {name!r}: type {kinds} is not supported on this node "
-                              "(emptyDir, configMap, secret, downwardAPI, hostPath, persistentVolumeClaim)")
+                              "(emptyDir, configMap, secret, downwardAPI, projected, hostPath, persistentVolumeClaim)")
     return out
 
 
