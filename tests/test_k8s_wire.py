@@ -500,3 +500,34 @@ def test_eviction_api_and_kubectl_drain_wait(kube, tmp_path, capsys):
     assert kc("get", "pdb") == 0
     out = capsys.readouterr().out
     assert "ALLOWED DISRUPTIONS" in out and out.splitlines()[1].split()[:3] == ["x", "0", "N/A"]
+
+
+def test_finalizers_and_propagation_policies(kube):
+    """DELETE of an object with finalizers only marks it (deletionTimestamp); removing the last
+    finalizer completes the deletion; propagationPolicy=Orphan keeps what the owner owned."""
+    cm = "/api/v1/namespaces/default/configmaps"
+    code, _, _ = _raw(kube, "POST", cm, {"apiVersion": "v1", "kind": "ConfigMap",
+                                         "metadata": {"name": "held", "finalizers": ["example.com/cleanup"]}, "data": {}})
+    assert code == 201
+    code, _, body = _raw(kube, "DELETE", cm + "/held")
+    assert code == 200 and body["metadata"]["deletionTimestamp"] and body["kind"] == "ConfigMap"
+    assert _raw(kube, "GET", cm + "/held")[0] == 200  # still there, being deleted
+    code, _, body = _raw(kube, "PATCH", cm + "/held", {"metadata": {"finalizers": ["example.com/cleanup", "more"]}},
+                         ctype="application/merge-patch+json")
+    assert code == 422 and "no new finalizers" in body["message"]
+    code, _, body = _raw(kube, "PATCH", cm + "/held", {"metadata": {"labels": {"x": "y"}, "deletionTimestamp": None}},
+                         ctype="application/merge-patch+json")
+    assert code == 200 and body["metadata"]["deletionTimestamp"]  # a client cannot undo the deletion
+    code, _, _ = _raw(kube, "PATCH", cm + "/held", {"metadata": {"finalizers": None}}, ctype="application/merge-patch+json")
+    assert code == 200 and _raw(kube, "GET", cm + "/held")[0] == 404
+    # Orphan: the Deployment goes, its pods stay without the ownerReference
+    dep = "/apis/apps/v1/namespaces/default/deployments"
+    assert _raw(kube, "POST", dep, DEPLOY)[0] == 201
+    pods = _raw(kube, "GET", "/api/v1/namespaces/default/pods", None)[2]["items"]
+    mine = [p["metadata"]["name"] for p in pods if any(r.get("kind") == "Deployment" for r in p["metadata"].get("ownerReferences", []))]
+    assert mine
+    code, _, _ = _raw(kube, "DELETE", dep + "/web?propagationPolicy=Orphan")
+    assert code == 200
+    left = {p["metadata"]["name"]: p for p in _raw(kube, "GET", "/api/v1/namespaces/default/pods")[2]["items"]}
+    assert set(mine) <= set(left) and all(not left[n]["metadata"].get("ownerReferences") for n in mine)
+    assert _raw(kube, "DELETE", dep + "/web?propagationPolicy=Sideways")[0] in (400, 404)

@@ -562,6 +562,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--cpu-percent", type=int)
     ap.add_argument("--namespaced", choices=["true", "false"])
     ap.add_argument("--subresource")
+    ap.add_argument("--cascade", choices=["background", "foreground", "orphan"])
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -750,7 +751,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 n = delete_objects(k, load_manifests(a.filename))
             else:
                 what, name = kind_key(a.args[0]), a.args[1]
-                k.delete(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns)))
+                k.delete(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns)),
+                         query={"propagationPolicy": a.cascade.capitalize()} if a.cascade else None)
                 n = 1
             print(f"{n} object(s) deleted")
         elif a.verb == "logs":

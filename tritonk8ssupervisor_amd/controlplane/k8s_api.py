@@ -521,30 +521,61 @@ class KubernetesAPI:
                            "selector": ",".join(f"{k}={v}" for k, v in sel.items())}}
 
     def _deleter(self, kind: str):
+        """DELETE: an object with ``metadata.finalizers`` only gets its ``deletionTimestamp`` (the
+        finalizers' controllers clean up, then remove them; the last removal deletes it, see
+        ``replace``); otherwise it goes at once. ``propagationPolicy`` (query or DeleteOptions):
+        Background (default) and Foreground delete what the object owns, Orphan keeps it and
+        drops the ownerReferences."""
         async def h(req: Request, ns: str, name: str, pid: str | None = None):
             p = self._pid(pid, req)
             self._auth(req, self.project(p))
-            if self._dry_run(req):
-                if self.store.get(kind, _key(p, ns, name)) is None:
-                    raise HttpError(404, f'{kind} "{name}" not found')
-                return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
-            o = self.store.delete(kind, _key(p, ns, name))
-            if o is None:
+            cur = self.store.get(kind, _key(p, ns, name))
+            if cur is None:
                 raise HttpError(404, f'{kind} "{name}" not found')
-            if kind in ("services", "ingresses"):
-                self._sync_proxy()
-            if kind == "customresourcedefinitions":  # its custom resources go with it
-                cr = name  # "<plural>.<group>" is also their store kind
-                for x in self.store.list(cr, lambda x: self._in(p, x)):
-                    self.store.delete(cr, _key(p, x["metadata"].get("namespace", ""), x["metadata"]["name"]))
-            if kind != "pods":  # garbage collection: what the object owned goes with it
-                for dep_kind in ("pods", "replicasets", "jobs"):
-                    for dep in self.store.list(dep_kind, lambda x: self._in(p, x) and any(
-                            r.get("uid") == o["metadata"]["uid"] for r in x["metadata"].get("ownerReferences", []))):
-                        self.store.delete(dep_kind, _key(p, ns, dep["metadata"]["name"]))
-            self.reconcile()
+            opts = {}
+            if req.body:
+                try:
+                    opts = req.json() or {}
+                except (HttpError, ValueError):
+                    opts = {}
+            policy = req.q("propagationPolicy") or opts.get("propagationPolicy") or "Background"
+            if policy not in ("Background", "Foreground", "Orphan"):
+                raise HttpError(400, f"propagationPolicy {policy!r}: must be Background, Foreground or Orphan")
+            if self._dry_run(req) or "All" in (opts.get("dryRun") or []):
+                return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
+            if cur["metadata"].get("finalizers"):
+                def mark(o):
+                    o["metadata"].setdefault("deletionTimestamp", now_iso())
+                    o["metadata"].setdefault("deletionGracePeriodSeconds", 0)
+                    o["_propagation"] = policy
+                return self._strip(self.store.patch(kind, _key(p, ns, name), mark))
+            self._remove(p, kind, ns, name, policy)
             return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
         return h
+
+    def _remove(self, p: str, kind: str, ns: str, name: str, policy: str = "Background") -> None:
+        """Delete an object for good, with garbage collection of what it owns (ownerReferences)."""
+        o = self.store.delete(kind, _key(p, ns, name))
+        if o is None:
+            return
+        if kind in ("services", "ingresses"):
+            self._sync_proxy()
+        if kind == "customresourcedefinitions":  # its custom resources go with it
+            cr = name  # "<plural>.<group>" is also their store kind
+            for x in self.store.list(cr, lambda x: self._in(p, x)):
+                self.store.delete(cr, _key(p, x["metadata"].get("namespace", ""), x["metadata"]["name"]))
+        if kind != "pods":  # garbage collection: what the object owned goes with it (or is orphaned)
+            uid = o["metadata"]["uid"]
+            for dep_kind in ("pods", "replicasets", "jobs"):
+                for dep in self.store.list(dep_kind, lambda x: self._in(p, x) and any(
+                        r.get("uid") == uid for r in x["metadata"].get("ownerReferences", []))):
+                    dkey = _key(p, dep["metadata"].get("namespace", ns), dep["metadata"]["name"])
+                    if policy == "Orphan":
+                        self.store.patch(dep_kind, dkey, lambda x: x["metadata"].__setitem__("ownerReferences", [
+                            r for r in x["metadata"].get("ownerReferences", []) if r.get("uid") != uid]))
+                    else:
+                        self.store.delete(dep_kind, dkey)
+        self.reconcile()
 
     # ---- networking: pod CIDRs, Service IPs / ports, endpoints --------------------------
     def _pod_cidr_block(self) -> int:
@@ -958,6 +989,14 @@ class KubernetesAPI:
                   creationTimestamp=cur["metadata"].get("creationTimestamp"))
         if not ns:
             md.pop("namespace")
+        deleting = cur["metadata"].get("deletionTimestamp")
+        for f in ("deletionTimestamp", "deletionGracePeriodSeconds"):  # set by DELETE only
+            md.pop(f, None)
+            if f in cur["metadata"]:
+                md[f] = cur["metadata"][f]
+        if deleting and set(md.get("finalizers") or []) - set(cur["metadata"].get("finalizers") or []):
+            raise HttpError(422, f'{kind} "{name}" is invalid: metadata.finalizers: Forbidden: no new finalizers can be '
+                                 "added if the object is being deleted")
         md.pop("resourceVersion", None)
         md.setdefault("labels", {})
         md.setdefault("annotations", {})
@@ -1024,6 +1063,12 @@ class KubernetesAPI:
             return {**copy.deepcopy(new), "metadata": {**copy.deepcopy(md),
                                                        "resourceVersion": cur["metadata"].get("resourceVersion")}}
         new["_project"] = pid
+        if deleting:
+            new["_propagation"] = cur.get("_propagation", "Background")
+            if not md.get("finalizers"):  # the last finalizer is gone: the deletion completes
+                self.store.put(kind, key, new)
+                self._remove(pid, kind, ns, name, new["_propagation"])
+                return {**new, "metadata": {**md}}
         o = self.store.put(kind, key, new)
         if kind in ("services", "ingresses"):
             self._sync_proxy()
