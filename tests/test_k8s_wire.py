@@ -531,3 +531,119 @@ def test_finalizers_and_propagation_policies(kube):
     left = {p["metadata"]["name"]: p for p in _raw(kube, "GET", "/api/v1/namespaces/default/pods")[2]["items"]}
     assert set(mine) <= set(left) and all(not left[n]["metadata"].get("ownerReferences") for n in mine)
     assert _raw(kube, "DELETE", dep + "/web?propagationPolicy=Sideways")[0] in (400, 404)
+
+
+def test_admission_webhooks(kube):
+    """A mutating webhook's JSONPatch lands on the object, a validating webhook's denial refuses
+    the request; failurePolicy decides about an unreachable webhook (webhooks.py)."""
+    import base64
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+    seen = []
+
+    class Hook(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_POST(self):
+            review = json.loads(self.rfile.read(int(self.headers["Content-Length"])))
+            req = review["request"]
+            seen.append((self.path, req["operation"], req["kind"]["kind"], req["userInfo"]["username"]))
+            resp = {"uid": req["uid"], "allowed": True}
+            if self.path == "/mutate":
+                patch = [{"op": "add", "path": "/metadata/labels/injected", "value": "yes"}]
+                resp.update(patchType="JSONPatch", patch=base64.b64encode(json.dumps(patch).encode()).decode())
+            elif self.path == "/validate" and "forbidden" in ((req.get("object") or {}).get("data") or {}):
+                resp.update(allowed=False, status={"code": 422, "message": "key 'forbidden' is not allowed"})
+            out = json.dumps({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "response": resp}).encode()
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(out)))
+            self.end_headers()
+            self.wfile.write(out)
+
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), Hook)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    base = f"http://127.0.0.1:{srv.server_address[1]}"
+    try:
+        rule = lambda res, ops=("CREATE", "UPDATE"): {"operations": list(ops), "apiGroups": [""], "apiVersions": ["v1"],
+                                                      "resources": [res]}
+        assert _raw(kube, "POST", "/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations", {
+            "apiVersion": "admissionregistration.k8s.io/v1", "kind": "MutatingWebhookConfiguration",
+            "metadata": {"name": "inject"}, "webhooks": [{
+                "name": "inject.example.com", "clientConfig": {"url": base + "/mutate"}, "rules": [rule("configmaps")],
+                "objectSelector": {"matchExpressions": [{"key": "skip", "operator": "DoesNotExist"}]},
+                "sideEffects": "None", "admissionReviewVersions": ["v1"]}]})[0] == 201
+        assert _raw(kube, "POST", "/apis/admissionregistration.k8s.io/v1/validatingwebhookconfigurations", {
+            "apiVersion": "admissionregistration.k8s.io/v1", "kind": "ValidatingWebhookConfiguration",
+            "metadata": {"name": "policy"}, "webhooks": [{
+                "name": "policy.example.com", "clientConfig": {"url": base + "/validate"},
+                "rules": [rule("configmaps", ("CREATE", "UPDATE", "DELETE"))], "sideEffects": "None",
+                "admissionReviewVersions": ["v1"]},
+                {"name": "gone.example.com", "clientConfig": {"url": "http://127.0.0.1:9/x"}, "failurePolicy": "Ignore",
+                 "rules": [rule("configmaps")], "sideEffects": "None", "admissionReviewVersions": ["v1"]}]})[0] == 201
+        cm = "/api/v1/namespaces/default/configmaps"
+        code, _, body = _raw(kube, "POST", cm, {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "a"},
+                                                "data": {"k": "v"}})
+        assert code == 201 and body["metadata"]["labels"]["injected"] == "yes", body
+        code, _, body = _raw(kube, "POST", cm, {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "b"},
+                                                "data": {"forbidden": "1"}})
+        assert code == 422 and 'admission webhook "policy.example.com" denied the request' in body["message"]
+        assert _raw(kube, "GET", cm + "/b")[0] == 404
+        code, _, body = _raw(kube, "POST", cm, {"apiVersion": "v1", "kind": "ConfigMap",
+                                                "metadata": {"name": "c", "labels": {"skip": "1"}}, "data": {}})
+        assert code == 201 and "injected" not in body["metadata"]["labels"]  # objectSelector
+        code, _, body = _raw(kube, "PATCH", cm + "/a", {"data": {"forbidden": "x"}}, ctype="application/merge-patch+json")
+        assert code == 422
+        assert _raw(kube, "DELETE", cm + "/a")[0] == 200
+        ops = [(p, op) for p, op, kind, _u in seen if kind == "ConfigMap"]
+        assert ("/mutate", "CREATE") in ops and ("/validate", "UPDATE") in ops and ("/validate", "DELETE") in ops
+        assert all(u == "tk8s:admin" for *_x, u in seen)
+        # a webhook that cannot be reached, failurePolicy Fail (the default): the request fails
+        assert _raw(kube, "POST", "/apis/admissionregistration.k8s.io/v1/validatingwebhookconfigurations", {
+            "apiVersion": "admissionregistration.k8s.io/v1", "kind": "ValidatingWebhookConfiguration",
+            "metadata": {"name": "strict"}, "webhooks": [{
+                "name": "strict.example.com", "clientConfig": {"url": "http://127.0.0.1:9/x"}, "timeoutSeconds": 2,
+                "rules": [rule("secrets")], "sideEffects": "None", "admissionReviewVersions": ["v1"]}]})[0] == 201
+        code, _, body = _raw(kube, "POST", "/api/v1/namespaces/default/secrets", {
+            "apiVersion": "v1", "kind": "Secret", "metadata": {"name": "s"}, "data": {}})
+        assert code == 500 and "failed calling webhook" in body["message"]
+        _https_webhook(kube, Hook, seen, rule)
+    finally:
+        srv.shutdown()
+
+
+def _https_webhook(kube, handler, seen, rule):
+    """The same webhook over HTTPS, verified against the configuration's caBundle."""
+    import base64
+    import shutil
+    import ssl
+    import subprocess
+    import tempfile
+    from http.server import ThreadingHTTPServer
+
+    if not shutil.which("openssl"):
+        return
+    d = tempfile.mkdtemp()
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", f"{d}/k.pem", "-out",
+                    f"{d}/c.pem", "-days", "1", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                   check=True, capture_output=True)
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), handler)
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.load_cert_chain(f"{d}/c.pem", f"{d}/k.pem")
+    srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        ca = base64.b64encode(open(f"{d}/c.pem", "rb").read()).decode()
+        assert _raw(kube, "POST", "/apis/admissionregistration.k8s.io/v1/validatingwebhookconfigurations", {
+            "apiVersion": "admissionregistration.k8s.io/v1", "kind": "ValidatingWebhookConfiguration",
+            "metadata": {"name": "tls"}, "webhooks": [{
+                "name": "tls.example.com", "clientConfig": {"url": f"https://127.0.0.1:{srv.server_address[1]}/tls",
+                                                            "caBundle": ca},
+                "rules": [rule("serviceaccounts")], "sideEffects": "None", "admissionReviewVersions": ["v1"]}]})[0] == 201
+        code, _, body = _raw(kube, "POST", "/api/v1/namespaces/default/serviceaccounts", {
+            "apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": "robot"}})
+        assert code == 201, body
+        assert any(p == "/tls" and k == "ServiceAccount" for p, _op, k, _u in seen)
+    finally:
+        srv.shutdown()

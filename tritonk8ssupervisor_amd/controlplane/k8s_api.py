@@ -117,6 +117,9 @@ class KubernetesAPI:
     def _guarded(self, h):
         async def g(req: Request, **kw):
             self._authorize(req, kw.get("pid"))
+            from .webhooks import CALLER
+
+            CALLER.set((kw.get("pid"), req.bearer))  # who asked, for admission webhooks' userInfo
             return await h(req, **kw)
         g.__name__ = getattr(h, "__name__", "handler")
         return g
@@ -541,7 +544,9 @@ class KubernetesAPI:
             policy = req.q("propagationPolicy") or opts.get("propagationPolicy") or "Background"
             if policy not in ("Background", "Foreground", "Orphan"):
                 raise HttpError(400, f"propagationPolicy {policy!r}: must be Background, Foreground or Orphan")
-            if self._dry_run(req) or "All" in (opts.get("dryRun") or []):
+            dry = self._dry_run(req) or "All" in (opts.get("dryRun") or [])
+            self._admit_webhooks(p, "DELETE", kind, ns, name, None, self._strip(cur), False, dry)
+            if dry:
                 return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
             if cur["metadata"].get("finalizers"):
                 def mark(o):
@@ -854,6 +859,11 @@ class KubernetesAPI:
         key = _key(pid, ns, name)
         if self.store.get(kind, key) is not None:
             raise HttpError(409, f'{kind} "{name}" already exists')
+        if self.store.keys("mutatingwebhookconfigurations"):  # webhooks.py: mutating admission first
+            body = {**self._admit_webhooks(pid, "CREATE", kind, ns, name, self._strip(body), None, True, dry_run),
+                    "_project": pid}
+            md = body.setdefault("metadata", {})
+            md.update(name=name, **({"namespace": ns} if ns else {}))
         _admit_gpu_visibility(kind, ns, body)
         if kind == "pods":
             spec = body.setdefault("spec", {})
@@ -911,6 +921,7 @@ class KubernetesAPI:
             m = ssa.Managed(None, self._kind_meta(kind)[0])
             m.update(None, body, manager)
             md["managedFields"] = m.entries()
+        self._admit_webhooks(pid, "CREATE", kind, ns, name, self._strip(body), None, False, dry_run)
         if dry_run:
             return {**copy.deepcopy(body), "metadata": {**copy.deepcopy(md), "uid": "dry-run",
                                                         "creationTimestamp": now_iso()}}
@@ -997,6 +1008,11 @@ class KubernetesAPI:
         if deleting and set(md.get("finalizers") or []) - set(cur["metadata"].get("finalizers") or []):
             raise HttpError(422, f'{kind} "{name}" is invalid: metadata.finalizers: Forbidden: no new finalizers can be '
                                  "added if the object is being deleted")
+        if self.store.keys("mutatingwebhookconfigurations"):
+            new = self._admit_webhooks(pid, "UPDATE", kind, ns, name, new, self._strip(cur), True, dry_run,
+                                       subresource or "")
+            md = new.setdefault("metadata", {})
+            md.update(name=name, uid=cur["metadata"]["uid"], **({"namespace": ns} if ns else {}))
         md.pop("resourceVersion", None)
         md.setdefault("labels", {})
         md.setdefault("annotations", {})
@@ -1059,6 +1075,7 @@ class KubernetesAPI:
                 md["managedFields"] = m.entries()
         if not md.get("managedFields"):
             md.pop("managedFields", None)
+        self._admit_webhooks(pid, "UPDATE", kind, ns, name, new, self._strip(cur), False, dry_run, subresource or "")
         if dry_run:
             return {**copy.deepcopy(new), "metadata": {**copy.deepcopy(md),
                                                        "resourceVersion": cur["metadata"].get("resourceVersion")}}

@@ -56,6 +56,7 @@ _TOP = {"Pod": ("spec", "status"), "Service": ("spec", "status"), "Node": ("spec
         "RoleBinding": ("roleRef", "subjects"), "ClusterRoleBinding": ("roleRef", "subjects"),
         "Secret": ("data", "stringData", "type", "immutable"),
         "PriorityClass": ("value", "globalDefault", "description", "preemptionPolicy"),
+        "MutatingWebhookConfiguration": ("webhooks",), "ValidatingWebhookConfiguration": ("webhooks",),
         "Endpoints": ("subsets",),
         "Event": ("involvedObject", "reason", "message", "source", "firstTimestamp", "lastTimestamp", "count",
                   "type", "eventTime", "series", "action", "related", "reportingComponent",

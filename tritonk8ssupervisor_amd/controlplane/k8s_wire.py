@@ -54,6 +54,10 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
     "poddisruptionbudgets": ("policy", "v1", "PodDisruptionBudget", "poddisruptionbudget", True, ("pdb",), ("status",)),
     "priorityclasses": ("scheduling.k8s.io", "v1", "PriorityClass", "priorityclass", False, ("pc",), ()),
+    "mutatingwebhookconfigurations": ("admissionregistration.k8s.io", "v1", "MutatingWebhookConfiguration",
+                                      "mutatingwebhookconfiguration", False, (), ()),
+    "validatingwebhookconfigurations": ("admissionregistration.k8s.io", "v1", "ValidatingWebhookConfiguration",
+                                        "validatingwebhookconfiguration", False, (), ()),
 }
 READ_ONLY = {"namespaces": ("create", "delete", "get", "list", "patch", "watch"),
              "events": ("get", "list", "watch", "create", "delete")}

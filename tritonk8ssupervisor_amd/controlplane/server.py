@@ -56,6 +56,7 @@ from .crds import CustomResources
 from .metrics_api import MetricsAPI
 from .disruption import Disruption
 from .priority import Priority
+from .webhooks import AdmissionWebhooks
 from .store import Store, now_iso
 
 
@@ -74,7 +75,7 @@ def _group_doc(group: str, versions: list[str]) -> dict:
 
 
 class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Disruption,
-                   Priority, Scheduler):
+                   Priority, AdmissionWebhooks, Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port

@@ -36,6 +36,10 @@ KINDS = {
     "ingress": ("Ingress", "/apis/networking.k8s.io/v1", "ingresses"),
     "poddisruptionbudget": ("PodDisruptionBudget", "/apis/policy/v1", "poddisruptionbudgets"),
     "priorityclass": ("PriorityClass", "/apis/scheduling.k8s.io/v1", "priorityclasses"),
+    "mutatingwebhookconfiguration": ("MutatingWebhookConfiguration", "/apis/admissionregistration.k8s.io/v1",
+                                     "mutatingwebhookconfigurations"),
+    "validatingwebhookconfiguration": ("ValidatingWebhookConfiguration", "/apis/admissionregistration.k8s.io/v1",
+                                       "validatingwebhookconfigurations"),
 }
 ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", "ds": "daemonset",
            "daemonsets": "daemonset", "deploy": "deployment", "deployments": "deployment", "jobs": "job",
@@ -52,7 +56,8 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "pc": "priorityclass", "priorityclasses": "priorityclass"}
 
 
-CLUSTER_SCOPED: set[str] = {"customresourcedefinition", "priorityclass"}  # (+ kinds learnt from discovery without a namespace)
+CLUSTER_SCOPED: set[str] = {"customresourcedefinition", "priorityclass", "mutatingwebhookconfiguration",
+                             "validatingwebhookconfiguration"}  # (+ kinds learnt from discovery without a namespace)
 
 
 def learn_kind(k: Client, name: str) -> str | None:
