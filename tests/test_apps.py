@@ -526,3 +526,27 @@ def test_configmap_volume_updates_reach_a_running_pod(cluster):
     assert _until(lambda: read() == "fast", timeout=20)
     kc("delete", "pod", "watcher")
     assert _until(lambda: (ws / "scratch" / "bye").exists(), timeout=20)
+
+
+def test_gpu_pod_waits_for_a_terminating_pods_gpus(cluster):
+    """A deleted GPU pod keeps its GPUs through its grace period (a trainer writing a checkpoint);
+    a new pod bound to them meanwhile waits (ContainerCreating) and starts once they are free."""
+    ws, env, kc, summary = cluster
+    node = json.loads(kc("get", "nodes", "-o", "json").stdout)["items"][0]
+    nn, gpus = node["metadata"]["name"], int(node["status"]["allocatable"]["amd.com/gpu"])
+    pod = lambda name, cmd, grace: {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name}, "spec": {
+        "nodeSelector": {"kubernetes.io/hostname": nn}, "terminationGracePeriodSeconds": grace,
+        "containers": [{"name": "c", "command": ["sh", "-c", cmd], "resources": {"limits": {"amd.com/gpu": str(gpus)}}}]}}
+    (ws / "old.json").write_text(json.dumps(pod("old", "trap '' TERM; while true; do sleep 0.1; done", 3)))
+    kc("apply", "-f", str(ws / "old.json"))
+    _until(lambda: json.loads(kc("get", "pod", "old", "-o", "json").stdout)["status"].get("phase") == "Running", 30)
+    kc("delete", "pod", "old")
+    t0 = time.monotonic()
+    (ws / "new.json").write_text(json.dumps(pod("new", "sleep 60", 30)))
+    kc("apply", "-f", str(ws / "new.json"))
+    st = _until(lambda: json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"].get("reason") == "ContainerCreating"
+                or json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"].get("phase") == "Running", 20)
+    assert st
+    _until(lambda: json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"].get("phase") == "Running", 30)
+    assert time.monotonic() - t0 > 1.5  # it waited for the old pod's grace period
+    assert json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"]["phase"] == "Running"

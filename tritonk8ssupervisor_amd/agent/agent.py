@@ -412,6 +412,14 @@ class Agent:
                              {"reason": "UnexpectedAdmissionError", "message": f"unreadable {HOST_CLAIMS}"}, None)
                 return
         free = self._free_devices()
+        if need > len(free) and need <= len(free) + len(self.runtime.terminating_gpus()):
+            # a deleted pod is still shutting down (its grace period): wait for its GPUs
+            if key not in self._config_wait:
+                self._report(key, md["name"], md["namespace"], "Pending",
+                             {"reason": "ContainerCreating",
+                              "message": f"waiting for {GPU} released by a terminating pod"}, None)
+            self._config_wait[key] = pod
+            return
         if need > len(free):
             self._report(key, md["name"], md["namespace"], "Failed",
                          {"reason": "UnexpectedAdmissionError",
@@ -798,9 +806,9 @@ class Agent:
         """A pod's termination is over: its IP is free, and a successor of the same name may start."""
         if key not in self.runtime.running():
             self._pod_ips.pop(key, None)
-        nxt = self._config_wait.get(key)
-        if nxt is not None:
-            self._start_pod(nxt)
+        for k, nxt in list(self._config_wait.items()):  # its name, its GPUs: what waited may start now
+            if k not in self.runtime.running():
+                self._start_pod(nxt)
 
     # ---- lifecycle --------------------------------------------------------------------
     def run(self, await_url: Path | None = None) -> int:

@@ -340,6 +340,10 @@ class PodRuntime:
         with self.lock:
             return key in self.terminating
 
+    def terminating_gpus(self) -> set[str]:
+        with self.lock:
+            return {i for pp in self.terminating.values() for i in pp.gpu_ids}
+
     def held_gpus(self) -> set[str]:
         """GPUs of running pods and of pods still within their grace period."""
         with self.lock:
