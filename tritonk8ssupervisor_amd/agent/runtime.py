@@ -351,8 +351,15 @@ class PodRuntime:
                     | {i for pp in self.terminating.values() for i in pp.gpu_ids})
 
     def stop_all(self) -> None:
+        """The agent is going away: every pod ends within a second, those already terminating too."""
         for key in list(self.pods):
             self.stop(key, grace=1.0)
+        with self.lock:
+            late = list(self.terminating.values())
+        for pp in late:
+            for c in (pp, *pp.sidecars, *pp.init):
+                if c.proc is not None and c.proc.poll() is None:
+                    kill_group(c.proc.pid, 1.0, term=False)
 
     def running(self) -> dict[str, PodProc]:
         with self.lock:
