@@ -303,6 +303,28 @@ def test_metrics_and_version(cp):
                  'tk8s_container_gpu_busy_percent{namespace="default",pod="train",container="c",node="kubenode1"} 87.0'):
         assert line in text, line
     assert "version" in json.dumps(cp.get("/version")).lower()
+    # kube-apiserver's request metrics: the node's status PUT, counted with its code and latency
+    text = cp.get("/metrics", raw=True)
+    assert 'apiserver_request_total{verb="PUT",group="",resource="nodes",subresource="status",code="200"} 1' in text
+    assert 'apiserver_request_duration_seconds_count{verb="PUT",group="",resource="nodes",subresource="status"} 1' in text
+
+
+def test_request_classification():
+    from tritonk8ssupervisor_amd.controlplane.reqmetrics import RequestMetrics, classify
+
+    assert classify("GET", "/api/v1/namespaces/default/pods", False) == ("LIST", "", "pods", "")
+    assert classify("GET", "/api/v1/pods", True) == ("WATCH", "", "pods", "")
+    assert classify("GET", "/r/projects/1a1/kubernetes/apis/apps/v1/namespaces/x/deployments/web/scale", False) == (
+        "GET", "apps", "deployments", "scale")
+    assert classify("POST", "/v2-beta/projects", False)[2] == "(other)"
+    assert classify("GET", "/apis/apps/v1", False)[2] == "(discovery)"
+    m = RequestMetrics()
+    m.observe("GET", "/api/v1/pods", False, 200, 0.003)
+    m.observe("GET", "/api/v1/pods", True, 200, 0.0)
+    lines = m.lines()
+    assert 'apiserver_request_duration_seconds_bucket{verb="LIST",group="",resource="pods",subresource="",le="0.0025"} 0' in lines
+    assert 'apiserver_request_duration_seconds_bucket{verb="LIST",group="",resource="pods",subresource="",le="0.005"} 1' in lines
+    assert not any('verb="WATCH"' in x and "duration" in x for x in lines)
 
 
 def test_put_patch_scale_and_rolling_update(cp):

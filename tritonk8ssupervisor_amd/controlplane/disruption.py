@@ -23,7 +23,6 @@ import math
 
 from .httpserver import HttpError, Request, Response
 from .objects import TERMINAL, _key
-from .placement import selector_matches
 from .store import now_iso
 
 PDB = "poddisruptionbudgets"
@@ -46,7 +45,7 @@ class Disruption:
     def _pdb_pods(self, pid: str, pdb: dict) -> list[dict]:
         ns, sel = pdb["metadata"]["namespace"], (pdb.get("spec") or {}).get("selector")
         return [o for o in self.store.list("pods", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns)
-                if o.get("status", {}).get("phase") not in TERMINAL and selector_matches(sel, o["metadata"].get("labels"))]
+                if o.get("status", {}).get("phase") not in TERMINAL and _sel(sel, o["metadata"].get("labels"))]
 
     def _expected(self, pid: str, pods: list[dict]) -> int:
         """What the pods' controllers want, counted once per controller; uncontrolled pods count themselves."""
@@ -122,7 +121,7 @@ class Disruption:
         if pod is None:
             raise HttpError(404, f'pods "{name}" not found')
         budgets = [b for b in self.store.list(PDB, lambda o: self._in(pid, o) and o["metadata"]["namespace"] == ns)
-                   if selector_matches((b.get("spec") or {}).get("selector"), pod["metadata"].get("labels"))]
+                   if _sel((b.get("spec") or {}).get("selector"), pod["metadata"].get("labels"))]
         if len(budgets) > 1:
             raise HttpError(500, "This pod has more than one PodDisruptionBudget, which the eviction subresource "
                                  "does not support.")
@@ -159,3 +158,9 @@ class Disruption:
         dry = self._dry_run(req) or bool((body.get("deleteOptions") or {}).get("dryRun"))
         self.evict(p, ns, name, dry_run=dry)
         return Response(201, {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201})
+
+
+def _sel(sel, labels) -> bool:
+    from .placement import selector_matches  # (lazy: off the control plane's start-up imports)
+
+    return selector_matches(sel, labels)

@@ -9,6 +9,7 @@ from __future__ import annotations
 import asyncio
 import json
 import re
+import time
 import traceback
 from typing import Any, AsyncIterator, Awaitable, Callable
 from urllib.parse import parse_qs, unquote, urlsplit
@@ -221,8 +222,10 @@ async def _read_request(reader: asyncio.StreamReader, peer: str) -> Request | No
 
 class HttpServer:
     def __init__(self, router: Router, on_error: Callable[[str], None] | None = None,
-                 error_body: Callable[[str, HttpError], Any] | None = None):
+                 error_body: Callable[[str, HttpError], Any] | None = None,
+                 observe: Callable[[str, str, bool, int, float], None] | None = None):
         self.router = router
+        self.observe = observe  # (method, path, watch, status, seconds) of every request
         self.on_error = on_error
         self.error_body = error_body  # path, error -> body (e.g. a Kubernetes Status on API paths)
         self.server: asyncio.base_events.Server | None = None
@@ -244,6 +247,7 @@ class HttpServer:
                     return
                 if req is None:
                     return
+                t0 = time.perf_counter()
                 try:
                     handler, params = self.router.match(req.method, req.path)
                     res = await handler(req, **params)
@@ -255,6 +259,10 @@ class HttpServer:
                     if self.on_error:
                         self.on_error(traceback.format_exc())
                     res = self._error(req.path, HttpError(500, repr(e)))
+                if self.observe is not None:
+                    self.observe(req.method, req.path, req.query.get("watch") in ("1", "true"),
+                                 101 if isinstance(res, WebSocketResponse) else getattr(res, "status", 200),
+                                 time.perf_counter() - t0)
                 keep = req.headers.get("connection", "").lower() != "close"
                 if isinstance(res, WebSocketResponse):
                     hdr = ["HTTP/1.1 101 Switching Protocols", "Upgrade: websocket", "Connection: Upgrade",

@@ -85,7 +85,11 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         self.store = Store()
         self.store.type_meta = k8s_wire.type_meta()
         self.router = Router()
-        self.http = HttpServer(self.router, on_error=self._log_error, error_body=self._error_body)
+        from .reqmetrics import RequestMetrics
+
+        self.reqmetrics = RequestMetrics()
+        self.http = HttpServer(self.router, on_error=self._log_error, error_body=self._error_body,
+                               observe=self.reqmetrics.observe)
         self.leases: dict[str, float] = {}   # node key -> monotonic time of last heartbeat
         self.started = time.time()
         self._stop = None
@@ -326,6 +330,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             lines.append(f'tk8s_node_heartbeat_age_seconds{{node="{k}"}} {now - t:.3f}')
         lines += self._gpu_metric_lines()
         lines.append(f"tk8s_store_resource_version {self.store.rv}")
+        lines += self.reqmetrics.lines()
         return Response(200, "\n".join(lines) + "\n", content_type="text/plain; version=0.0.4")
 
     def _gpu_metric_lines(self) -> list[str]:

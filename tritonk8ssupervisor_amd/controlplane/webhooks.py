@@ -19,13 +19,11 @@ name is not checked when a pod is called by its IP).
 """
 from __future__ import annotations
 
-import base64
 import contextvars
 import json
 
 from .httpserver import HttpError
 from .objects import _key
-from .placement import selector_matches
 
 MUTATING = "mutatingwebhookconfigurations"
 VALIDATING = "validatingwebhookconfigurations"
@@ -75,7 +73,7 @@ class AdmissionWebhooks:
         for pod in self.store.list("pods", lambda x: x.get("_project") == pid and x["metadata"].get("namespace") == ns):
             if (pod.get("status") or {}).get("phase") != "Running" or not pod["status"].get("podIP"):
                 continue
-            if not selector_matches({"matchLabels": o["spec"].get("selector") or {}}, pod["metadata"].get("labels")):
+            if not _sel({"matchLabels": o["spec"].get("selector") or {}}, pod["metadata"].get("labels")):
                 continue
             tp = sp.get("targetPort", sp["port"])
             if isinstance(tp, str) and not tp.isdigit():
@@ -89,6 +87,8 @@ class AdmissionWebhooks:
     def _post_review(url: str, review: dict, cc: dict, timeout: float) -> dict:
         import http.client
         from urllib.parse import urlsplit
+
+        import base64
 
         u = urlsplit(url)
         body = json.dumps(review).encode()
@@ -141,9 +141,9 @@ class AdmissionWebhooks:
             for wh in cfg.get("webhooks") or []:
                 if not any(_match_rule(r, op, group, version, resource, namespaced) for r in wh.get("rules") or []):
                     continue
-                if ns and not selector_matches(wh.get("namespaceSelector"), ns_labels):
+                if ns and not _sel(wh.get("namespaceSelector"), ns_labels):
                     continue
-                if not selector_matches(wh.get("objectSelector"), labels):
+                if not _sel(wh.get("objectSelector"), labels):
                     continue
                 if dry_run and wh.get("sideEffects", "None") not in ("None", "NoneOnDryRun"):
                     raise HttpError(400, f'admission webhook "{wh.get("name")}" does not support dry run')
@@ -175,6 +175,8 @@ class AdmissionWebhooks:
                     msg = st.get("message") or "denied the request"
                     raise HttpError(code, f'admission webhook "{wh.get("name")}" denied the request: {msg}')
                 if mutating and resp.get("patch"):
+                    import base64
+
                     if resp.get("patchType", "JSONPatch") != "JSONPatch":
                         raise HttpError(500, f'admission webhook "{wh.get("name")}": unsupported patchType')
                     from . import k8s_wire
@@ -184,3 +186,9 @@ class AdmissionWebhooks:
                     except (k8s_wire.PatchError, ValueError) as e:
                         raise HttpError(500, f'admission webhook "{wh.get("name")}" returned a bad patch: {e}') from e
         return obj
+
+
+def _sel(sel, labels) -> bool:
+    from .placement import selector_matches  # (lazy: off the control plane's start-up imports)
+
+    return selector_matches(sel, labels)
