@@ -793,3 +793,35 @@ def test_priority_classes_and_preemption(cp):
     with pytest.raises(HttpError):
         cp.create("1a1", "pods", "default", {**gpu_pod("cheat", 0, "low"), "spec": {
             **gpu_pod("cheat", 0, "low")["spec"], "priority": 999999}})
+
+
+def test_limit_ranges_default_and_bound_containers(cp):
+    _nodes(cp, 1, gpus=8)
+    cp.create("1a1", "limitranges", "team", {"metadata": {"name": "lr"}, "spec": {"limits": [
+        {"type": "Container", "default": {"cpu": "1", "memory": "1Gi"}, "defaultRequest": {"cpu": "500m"},
+         "max": {"cpu": "4"}, "min": {"cpu": "100m"}, "maxLimitRequestRatio": {"cpu": "4"}},
+        {"type": "Pod", "max": {"amd.com/gpu": "4"}}]}})
+    pod = lambda name, res=None, n=1: {"metadata": {"name": name}, "spec": {"containers": [
+        {"name": f"c{i}", "command": ["true"], **({"resources": res} if res else {})} for i in range(n)]}}
+    p = cp.create("1a1", "pods", "team", pod("plain"))
+    r = p["spec"]["containers"][0]["resources"]
+    assert r == {"limits": {"cpu": "1", "memory": "1Gi"}, "requests": {"cpu": "500m", "memory": "1Gi"}}
+    p = cp.create("1a1", "pods", "team", pod("own", {"limits": {"cpu": "2"}}))
+    assert p["spec"]["containers"][0]["resources"]["requests"]["cpu"] == "2"  # its own limit, not defaultRequest
+    for name, res, n, want in (("big", {"limits": {"cpu": "8"}}, 1, "maximum cpu usage per Container is 4"),
+                               ("tiny", {"requests": {"cpu": "50m"}, "limits": {"cpu": "100m"}}, 1, "minimum cpu"),
+                               ("ratio", {"requests": {"cpu": "100m"}, "limits": {"cpu": "1"}}, 1, "ratio"),
+                               ("gpus", {"limits": {"amd.com/gpu": "3"}}, 2, "maximum amd.com/gpu usage per Pod is 4"),
+                               ("nolimit", None, 1, None)):
+        if want is None:  # (the defaults make this one fine)
+            cp.create("1a1", "pods", "team", pod(name, res, n))
+            continue
+        with pytest.raises(HttpError) as e:
+            cp.create("1a1", "pods", "team", pod(name, res, n))
+        assert e.value.status == 403 and want in e.value.message, e.value.message
+    cp.create("1a1", "pods", "other", pod("free", {"limits": {"cpu": "64"}}))  # other namespaces: no LimitRange
+    # a controller's pod gets the defaults too
+    cp.create("1a1", "jobs", "team", {"metadata": {"name": "j"}, "spec": {"template": {"spec": {
+        "restartPolicy": "Never", "containers": [{"name": "c", "command": ["true"]}]}}}})
+    (jp,) = [o for o in cp.store.list("pods") if o["metadata"]["name"].startswith("j-")]
+    assert jp["spec"]["containers"][0]["resources"]["limits"]["cpu"] == "1"

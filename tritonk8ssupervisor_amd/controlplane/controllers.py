@@ -89,6 +89,7 @@ class Controllers:
         spec.setdefault("restartPolicy", "Always")
         try:
             self._resolve_priority(pid, spec)
+            self._admit_limit_ranges(pid, ns, name, pod)
         except HttpError as e:  # as the ReplicaSet controller's FailedCreate: nothing is created
             self._event(pid, ns, {"kind": owner_kind, "name": owner["metadata"]["name"]}, "FailedCreate",
                         f'Error creating: pods "{name}" is forbidden: {e.message}', "Warning")

@@ -800,6 +800,18 @@ class KubernetesAPI:
                 return f'exceeded quota: {q["metadata"]["name"]}, ' + "; ".join(bad)
         return None
 
+    def _admit_limit_ranges(self, pid: str, ns: str, name: str, pod: dict) -> None:
+        """The namespace's LimitRanges: defaults filled in, bounds enforced (objects.apply_limit_ranges)."""
+        if not self.store.keys("limitranges"):
+            return
+        ranges = self.store.list("limitranges", lambda o: self._in(pid, o) and o["metadata"].get("namespace") == ns)
+        if ranges:
+            from .objects import apply_limit_ranges
+
+            bad = apply_limit_ranges(ranges, pod)
+            if bad:
+                raise HttpError(403, f'pods "{name}" is forbidden: [{", ".join(bad)}]')
+
     def _admit_quota(self, pid: str, ns: str, name: str, pod: dict) -> None:
         """ResourceQuota admission of a pod a client creates: refused, as the API server does."""
         why = self._quota_block(pid, ns, name, pod)
@@ -870,6 +882,7 @@ class KubernetesAPI:
             if not spec.get("containers"):
                 raise HttpError(422, "spec.containers is required")
             self._resolve_priority(pid, spec)
+            self._admit_limit_ranges(pid, ns, name, body)
             self._admit_quota(pid, ns, name, body)
             spec.setdefault("restartPolicy", "Always")
             body["status"] = {"phase": "Pending", "conditions": []}

@@ -44,6 +44,7 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "serviceaccounts": ("", "v1", "ServiceAccount", "serviceaccount", True, ("sa",), ()),
     "endpoints": ("", "v1", "Endpoints", "endpoints", True, ("ep",), ()),
     "resourcequotas": ("", "v1", "ResourceQuota", "resourcequota", True, ("quota",), ()),
+    "limitranges": ("", "v1", "LimitRange", "limitrange", True, ("limits",), ()),
     "leases": ("coordination.k8s.io", "v1", "Lease", "lease", True, (), ()),
     "roles": ("rbac.authorization.k8s.io", "v1", "Role", "role", True, (), ()),
     "rolebindings": ("rbac.authorization.k8s.io", "v1", "RoleBinding", "rolebinding", True, (), ()),

@@ -242,3 +242,58 @@ def quota_excess(hard: dict, used: dict, add: dict) -> list[str]:
 
 def _fmt(v: float) -> str:
     return str(int(v)) if float(v).is_integer() else f"{v:g}"
+
+
+def apply_limit_ranges(ranges: list[dict], pod: dict) -> list[str]:
+    """LimitRange admission of a pod (in place): each ``type: Container`` item's ``default``
+    (limits) and ``defaultRequest`` (requests) fill what a container leaves out -- a request
+    defaults to the limit when only that is given -- then ``min``/``max`` and
+    ``maxLimitRequestRatio`` are checked; ``type: Pod`` items check the containers' sums. The
+    violations, as the API server words them (empty: admitted)."""
+    from ..utils import quantity
+
+    bad = []
+    conts = pod.get("spec", {}).get("containers", []) + pod.get("spec", {}).get("initContainers", [])
+    for lr in ranges:
+        for item in (lr.get("spec") or {}).get("limits") or []:
+            typ = item.get("type", "Container")
+            if typ == "Container":
+                for c in conts:
+                    r = c.setdefault("resources", {})
+                    lim, req = r.setdefault("limits", {}), r.setdefault("requests", {})
+                    for res, v in list(lim.items()):  # the API's own defaulting: a request is its limit
+                        req.setdefault(res, v)
+                    for res, v in (item.get("default") or {}).items():
+                        lim.setdefault(res, v)
+                    for res, v in (item.get("defaultRequest") or {}).items():
+                        req.setdefault(res, v)
+                    for res, v in lim.items():  # no defaultRequest: the default limit
+                        req.setdefault(res, v)
+                    if not lim:
+                        r.pop("limits")
+                    if not req:
+                        r.pop("requests")
+                    for res, v in (item.get("min") or {}).items():
+                        for what, d in (("request", req), ("limit", lim)):
+                            if res in d and quantity.parse(d[res]) < quantity.parse(v):
+                                bad.append(f"minimum {res} usage per Container is {v}, but {what} is {d[res]}")
+                    for res, v in (item.get("max") or {}).items():
+                        if res not in lim:
+                            bad.append(f"maximum {res} usage per Container is {v}.  No limit is specified")
+                        elif quantity.parse(lim[res]) > quantity.parse(v):
+                            bad.append(f"maximum {res} usage per Container is {v}, but limit is {lim[res]}")
+                    for res, v in (item.get("maxLimitRequestRatio") or {}).items():
+                        if res in lim and res in req and quantity.parse(req[res]) > 0 and \
+                                quantity.parse(lim[res]) / quantity.parse(req[res]) > float(quantity.parse(v)):
+                            bad.append(f"{res} max limit to request ratio per Container is {v}, but provided ratio is "
+                                       f"{quantity.parse(lim[res]) / quantity.parse(req[res]):g}")
+            elif typ == "Pod":
+                for res, v in (item.get("max") or {}).items():
+                    tot = sum(quantity.parse(((c.get("resources") or {}).get("limits") or {}).get(res, 0)) for c in conts)
+                    if tot > quantity.parse(v):
+                        bad.append(f"maximum {res} usage per Pod is {v}, but limit is {_fmt(tot)}")
+                for res, v in (item.get("min") or {}).items():
+                    tot = sum(quantity.parse(((c.get("resources") or {}).get("requests") or {}).get(res, 0)) for c in conts)
+                    if tot < quantity.parse(v):
+                        bad.append(f"minimum {res} usage per Pod is {v}, but request is {_fmt(tot)}")
+    return bad

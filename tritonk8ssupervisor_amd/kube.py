@@ -36,6 +36,8 @@ KINDS = {
     "ingress": ("Ingress", "/apis/networking.k8s.io/v1", "ingresses"),
     "poddisruptionbudget": ("PodDisruptionBudget", "/apis/policy/v1", "poddisruptionbudgets"),
     "priorityclass": ("PriorityClass", "/apis/scheduling.k8s.io/v1", "priorityclasses"),
+    "limitrange": ("LimitRange", "/api/v1", "limitranges"),
+    "resourcequota": ("ResourceQuota", "/api/v1", "resourcequotas"),
     "mutatingwebhookconfiguration": ("MutatingWebhookConfiguration", "/apis/admissionregistration.k8s.io/v1",
                                      "mutatingwebhookconfigurations"),
     "validatingwebhookconfiguration": ("ValidatingWebhookConfiguration", "/apis/admissionregistration.k8s.io/v1",
@@ -53,7 +55,8 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "clusterroles": "clusterrole", "clusterrolebindings": "clusterrolebinding", "crd": "customresourcedefinition",
            "crds": "customresourcedefinition", "customresourcedefinitions": "customresourcedefinition",
            "pdb": "poddisruptionbudget", "poddisruptionbudgets": "poddisruptionbudget",
-           "pc": "priorityclass", "priorityclasses": "priorityclass"}
+           "pc": "priorityclass", "priorityclasses": "priorityclass", "limits": "limitrange",
+           "limitranges": "limitrange", "quota": "resourcequota", "resourcequotas": "resourcequota"}
 
 
 CLUSTER_SCOPED: set[str] = {"customresourcedefinition", "priorityclass", "mutatingwebhookconfiguration",
