@@ -550,3 +550,23 @@ def test_gpu_pod_waits_for_a_terminating_pods_gpus(cluster):
     _until(lambda: json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"].get("phase") == "Running", 30)
     assert time.monotonic() - t0 > 1.5  # it waited for the old pod's grace period
     assert json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"]["phase"] == "Running"
+
+
+def test_logs_previous_selector_and_all_containers(cluster):
+    ws, env, kc, summary = cluster
+    (ws / "crash.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod",
+        "metadata": {"name": "crashy", "labels": {"app": "crashy"}}, "spec": {"restartPolicy": "Always", "containers": [
+            {"name": "main", "command": ["sh", "-c", "n=$(cat $TK8S_VOLUME_S/n 2>/dev/null || echo 0); n=$((n+1)); "
+                                                     "echo $n > $TK8S_VOLUME_S/n; echo run $n; "
+                                                     "if [ $n -lt 2 ]; then exit 1; fi; sleep 60"],
+             "volumeMounts": [{"name": "s", "mountPath": "/s"}]},
+            {"name": "side", "command": ["sh", "-c", "echo from side; sleep 60"]}],
+            "volumes": [{"name": "s", "emptyDir": {}}]}}))
+    kc("apply", "-f", str(ws / "crash.json"))
+    assert _until(lambda: kc("logs", "crashy", check=False).stdout == "run 2\n", 30)
+    assert kc("logs", "crashy", "-p").stdout == "run 1\n"
+    out = kc("logs", "-l", "app=crashy", "--prefix").stdout
+    assert "[pod/crashy/main] run 2" in out and "[pod/crashy/side] from side" in out
+    assert "from side" in kc("logs", "crashy", "--all-containers").stdout
+    r = kc("logs", "crashy", "-c", "side", "--previous", check=False)
+    assert r.returncode != 0 and "previous terminated container" in r.stderr

@@ -4,7 +4,8 @@ The reference's nodes run Docker containers started by the Rancher agent (ranche
 ansible/roles/rancherhost/tasks/main.yml:26-34). Here a pod is a process group: its env gets the
 device plugin's Allocate() result and the downward-API values, ``$(VAR)`` references in
 command/args are expanded like Kubernetes does, stdout/stderr go to ``pods/<pod>/log``, and
-restartPolicy Always/OnFailure/Never is honoured with capped exponential back-off.
+restartPolicy Always/OnFailure/Never is honoured with capped exponential back-off; a restarted
+container's previous log is kept as ``<log>.previous`` (``kubectl logs --previous``).
 
 A pod's containers: ``initContainers`` run one after the other, each to a zero exit (retried
 with back-off, or the pod fails with ``Init:Error`` under ``restartPolicy: Never``), then every
@@ -22,6 +23,7 @@ stay allocated until it is over.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import re
@@ -118,6 +120,9 @@ class PodRuntime:
         argv = [*pp.jail, *pp.argv]  # nothing the pod runs can leave the jail
         if pp.isolate and namespace_isolation()[0]:  # outside the jail: a Landlocked process may not mount /proc
             argv = [*UNSHARE, "--", *argv]
+        if pp.exit_code is not None:  # a restart: the last instance's log is `kubectl logs --previous`
+            with contextlib.suppress(OSError):
+                os.replace(pp.dir / pp.log_name, pp.dir / f"{pp.log_name}.previous")
         log = open(pp.dir / pp.log_name, "ab", buffering=0)
         try:
             p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,

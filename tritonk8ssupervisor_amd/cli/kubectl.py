@@ -309,6 +309,41 @@ def _wait(k, ns: str, args: list[str], cond: str, selector: str | None, timeout:
     return rc
 
 
+def _logs_many(k, ns: str, a) -> int:
+    """kubectl logs -l SELECTOR | TYPE/NAME | --all-containers | --previous [--prefix]: every
+    selected pod's (and container's) log, one after the other."""
+    if a.selector:
+        pods = k.get(k.k8s(collection_path("pod", ns)), query={"labelSelector": a.selector})["items"]
+    elif a.args and "/" in a.args[0] and kind_key(a.args[0].split("/")[0]) != "pod":
+        what, name = a.args[0].split("/", 1)  # deploy/web, job/x, ...: its pods, as kubectl picks them
+        obj = k.get(k.k8s(object_path(what, name, ns)))
+        sel = ((obj.get("spec") or {}).get("selector") or {}).get("matchLabels") or (
+            {"job-name": name} if kind_key(what) == "job" else {})
+        pods = k.get(k.k8s(collection_path("pod", ns)),
+                     query={"labelSelector": ",".join(f"{x}={y}" for x, y in sel.items())})["items"][:1]
+    else:
+        name = a.args[0].split("/", 1)[-1]
+        pods = [k.get(k.k8s(object_path("pod", name, ns)))]
+    rc = 0
+    for p in pods:
+        names = [c["name"] for c in p["spec"].get("containers") or []]
+        conts = names if (a.all_containers or a.selector) and not a.container else [a.container or names[0]]
+        for c in conts:
+            q = {"container": c, **({"previous": "true"} if a.previous else {}),
+                 **({"tailLines": str(a.tail)} if a.tail else {})}
+            try:
+                text = k.get(k.k8s(object_path("pod", p["metadata"]["name"], ns) + "/log"), query=q, raw=True)
+            except ApiError as e:
+                print(f"Error from server: {e}", file=sys.stderr)
+                rc = 1
+                continue
+            pre = f"[pod/{p['metadata']['name']}/{c}] " if a.prefix else ""
+            for line in text.splitlines(keepends=True):
+                sys.stdout.write(pre + line)
+    sys.stdout.flush()
+    return rc
+
+
 def _drain(k, node: str, timeout: float, disable_eviction: bool) -> int:
     """Cordon, then evict every pod but DaemonSets' and finished ones through the Eviction API,
     retrying those a PodDisruptionBudget holds back (429) until ``timeout``."""
@@ -532,6 +567,9 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--from-file", action="append", default=[])
     ap.add_argument("--ignore-daemonsets", action="store_true")
     ap.add_argument("--follow", dest="follow", action="store_true")
+    ap.add_argument("--previous", action="store_true")
+    ap.add_argument("--all-containers", action="store_true")
+    ap.add_argument("--prefix", action="store_true")
     ap.add_argument("--image")
     ap.add_argument("--port", type=int)
     ap.add_argument("--target-port", type=int)
@@ -573,8 +611,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     if "--" in argv:  # kubectl exec POD -- CMD ARGS...
         command = argv[argv.index("--") + 1:]
         argv = argv[:argv.index("--")]
-    if argv[:1] == ["logs"] and "-f" in argv:  # `-f` means --filename everywhere but logs
-        argv = [x if x != "-f" else "--follow" for x in argv]
+    if argv[:1] == ["logs"]:  # `-f` means --filename and `-p` --patch everywhere but logs
+        argv = [{"-f": "--follow", "-p": "--previous"}.get(x, x) for x in argv]
     a = ap.parse_args(argv)
     a.command = command
     workdir = workdir or os.environ.get("TK8S_WORKDIR", os.getcwd())
@@ -755,6 +793,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                          query={"propagationPolicy": a.cascade.capitalize()} if a.cascade else None)
                 n = 1
             print(f"{n} object(s) deleted")
+        elif a.verb == "logs" and (a.selector or a.all_containers or a.previous or (a.args and "/" in a.args[0])):
+            return _logs_many(k, ns, a)
         elif a.verb == "logs":
             path = k.k8s(object_path("pod", a.args[0], ns) + "/log")
             full = k.get(path, query={"container": a.container}, raw=True)  # one read: nothing slips between

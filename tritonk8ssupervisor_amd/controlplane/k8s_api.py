@@ -1152,6 +1152,10 @@ class KubernetesAPI:
         if path and c and c != names[0]:  # the pod's other containers log next to the first (agent/runtime.py)
             path = str(Path(path).with_name(f"log.{c}"))
         follow = req.q("follow") in ("true", "1")
+        if req.q("previous") in ("true", "1"):  # the container's last instance before its restart
+            if not path or not os.path.exists(path + ".previous"):
+                raise HttpError(400, f'previous terminated container "{c or names[0]}" in pod "{name}" not found')
+            path, follow = path + ".previous", False
         if not path or not os.path.exists(path):
             if not follow:
                 return Response(200, "", content_type="text/plain")
