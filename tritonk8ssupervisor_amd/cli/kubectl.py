@@ -309,6 +309,20 @@ def _wait(k, ns: str, args: list[str], cond: str, selector: str | None, timeout:
     return rc
 
 
+def _manifests(a) -> list[dict]:
+    """The objects of ``-f FILE`` or ``-k DIR`` (a kustomization, kustomize.py)."""
+    if a.kustomize:
+        from .. import kustomize
+
+        try:
+            return kustomize.build(a.kustomize)
+        except kustomize.KustomizeError as e:
+            raise SystemExit(f"error: {e}") from e
+    if not a.filename:
+        raise SystemExit("error: must specify one of -f and -k")
+    return load_manifests(a.filename)
+
+
 def _logs_many(k, ns: str, a) -> int:
     """kubectl logs -l SELECTOR | TYPE/NAME | --all-containers | --previous [--prefix]: every
     selected pod's (and container's) log, one after the other."""
@@ -560,6 +574,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("-o", "--output")
     ap.add_argument("-l", "--selector")
     ap.add_argument("-f", "--filename")
+    ap.add_argument("-k", "--kustomize")
     ap.add_argument("--tail", type=int, default=0)
     ap.add_argument("--timeout", default="300s")
     ap.add_argument("--replicas", type=int)
@@ -616,6 +631,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     a = ap.parse_args(argv)
     a.command = command
     workdir = workdir or os.environ.get("TK8S_WORKDIR", os.getcwd())
+    if a.verb == "kustomize":  # a local build: no cluster needed
+        return more_dispatch(None, a, a.namespace, {})
     try:
         cfg = _load_kubeconfig(a.kubeconfig, workdir)
         if a.verb == "config":
@@ -711,15 +728,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
         elif a.verb == "expose":
             return _expose(k, a, ns)
         elif a.verb == "apply" and a.server_side:
-            if not a.filename:
-                raise SystemExit("error: must specify -f FILE")
-            for r in server_apply_objects(k, load_manifests(a.filename), a.field_manager, a.force_conflicts,
+            for r in server_apply_objects(k, _manifests(a), a.field_manager, a.force_conflicts,
                                           dry_run=a.dry_run == "server"):
                 print(f"{r['kind'].lower()}/{r['name']} {r['action']}" + (" (server dry run)" if a.dry_run == "server" else ""))
         elif a.verb in ("create", "apply"):
-            if not a.filename:
-                raise SystemExit("error: must specify -f FILE")
-            res = apply_objects(k, load_manifests(a.filename))
+            res = apply_objects(k, _manifests(a))
             for r in res:
                 print(f"{r['kind'].lower()}/{r['name']} {r['action'] if a.verb == 'apply' else ('created' if r['created'] else 'unchanged')}")
         elif a.verb == "scale":
@@ -785,8 +798,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                     f"{int(sum(quantity.parse(c['usage']['memory']) for c in m['containers']) / 2**20)}Mi"] for m in items]
                 print(_table(rows))
         elif a.verb == "delete":
-            if a.filename:
-                n = delete_objects(k, load_manifests(a.filename))
+            if a.filename or a.kustomize:
+                n = delete_objects(k, _manifests(a))
             else:
                 what, name = kind_key(a.args[0]), a.args[1]
                 k.delete(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns)),

@@ -21,10 +21,10 @@ import time
 import yaml
 
 from ..controlplane.client import ApiError
-from ..kube import KINDS, collection_path, kind_key, load_manifests, object_path
+from ..kube import KINDS, collection_path, kind_key, object_path
 
 VERBS = ("run", "set", "autoscale", "patch", "replace", "edit", "diff", "events", "explain", "api-resources",
-         "api-versions", "auth", "config")
+         "api-versions", "auth", "config", "kustomize")
 _WORKLOADS = ("deployment", "statefulset", "daemonset", "replicaset", "job", "pod")
 
 
@@ -173,11 +173,27 @@ def _patch(k, a, ns: str) -> int:
     return 0
 
 
+def _objects(a) -> list[dict]:
+    from .kubectl import _manifests
+
+    return _manifests(a)
+
+
+def _kustomize(a) -> int:
+    """kubectl kustomize DIR: the built objects as one YAML stream."""
+    from .. import kustomize
+
+    try:
+        objs = kustomize.build(a.args[0] if a.args else ".")
+    except kustomize.KustomizeError as e:
+        raise SystemExit(f"error: {e}") from e
+    print("\n---\n".join(yaml.safe_dump(o, sort_keys=False).rstrip() for o in objs))
+    return 0
+
+
 def _replace(k, a, ns: str) -> int:
-    """kubectl replace -f FILE: PUT each object (it must exist)."""
-    if not a.filename:
-        raise SystemExit("usage: kubectl replace -f FILE")
-    for obj in load_manifests(a.filename):
+    """kubectl replace -f FILE|-k DIR: PUT each object (it must exist)."""
+    for obj in _objects(a):
         kind, name = kind_key(obj["kind"]), obj["metadata"]["name"]
         path = _path(k, kind, name, obj["metadata"].get("namespace", ns))
         cur = k.get(path)
@@ -196,12 +212,10 @@ def _strip_volatile(obj: dict) -> dict:
 def _diff(k, a, ns: str) -> int:
     """kubectl diff -f FILE: live objects against what a server-side dry-run apply would make of
     them, as a unified YAML diff. Exit 0 without differences, 1 with."""
-    if not a.filename:
-        raise SystemExit("usage: kubectl diff -f FILE")
     from ..controlplane.k8s_wire import APPLY_PATCH
 
     changed = False
-    for obj in load_manifests(a.filename):
+    for obj in _objects(a):
         kind, name = kind_key(obj["kind"]), obj["metadata"]["name"]
         path = _path(k, kind, name, obj["metadata"].get("namespace", ns))
         try:
@@ -437,4 +451,6 @@ def dispatch(k, a, ns: str, cfg: dict) -> int:
         return _api_versions(k)
     if a.verb == "auth":
         return _auth(k, a, ns)
+    if a.verb == "kustomize":
+        return _kustomize(a)
     return _config(a, cfg)
