@@ -825,3 +825,25 @@ def test_limit_ranges_default_and_bound_containers(cp):
         "restartPolicy": "Never", "containers": [{"name": "c", "command": ["true"]}]}}}})
     (jp,) = [o for o in cp.store.list("pods") if o["metadata"]["name"].startswith("j-")]
     assert jp["spec"]["containers"][0]["resources"]["limits"]["cpu"] == "1"
+
+
+def test_job_pod_failure_policy(cp):
+    pol = {"rules": [{"action": "FailJob", "onExitCodes": {"containerName": "c", "operator": "In", "values": [42]}},
+                     {"action": "Ignore", "onExitCodes": {"operator": "In", "values": [137]}}]}
+    cp.create("1a1", "jobs", "default", {"metadata": {"name": "t"}, "spec": {"backoffLimit": 0, "podFailurePolicy": pol,
+        "template": {"spec": {"restartPolicy": "Never", "containers": [{"name": "c", "command": ["true"]}]}}}})
+
+    def fail(name, code):
+        cp.store.patch("pods", _key("1a1", "default", name), lambda o: o["status"].update(phase="Failed", containerStatuses=[
+            {"name": "c", "state": {"terminated": {"exitCode": code}}}]))
+        cp.reconcile()
+
+    (first,) = _pods(cp, "t-")
+    fail(first, 137)  # a SIGKILL (node pressure, preemption): ignored, not counted, replaced
+    j = cp.store.get("jobs", _key("1a1", "default", "t"))
+    assert j["status"]["failed"] == 0 and not any(c["type"] == "Failed" for c in j["status"]["conditions"])
+    (second,) = [n for n in _pods(cp, "t-") if n != first]
+    fail(second, 42)  # the program's "bad config" code: the Job fails at once
+    j = cp.store.get("jobs", _key("1a1", "default", "t"))
+    failed = [c for c in j["status"]["conditions"] if c["type"] == "Failed"]
+    assert failed and failed[0]["reason"] == "PodFailurePolicy" and "exit code 42" in failed[0]["message"]

@@ -11,6 +11,38 @@ from .httpserver import HttpError
 from .store import now_iso
 
 
+def _failure_action(policy: dict | None, pod: dict) -> tuple[str, str]:
+    """A Job's ``podFailurePolicy`` verdict on one failed pod: (FailJob|Ignore|Count, why). The
+    first rule that matches decides -- ``onExitCodes`` (``containerName``, ``In``/``NotIn``) on the
+    containers' terminated exit codes, ``onPodConditions`` on the pod's conditions; none: Count.
+    How a training Job fails at once on a bad-config exit code but retries a node's hardware fault."""
+    if not policy:
+        return "Count", ""
+    st = pod.get("status") or {}
+    codes = [(c.get("name"), ((c.get("state") or {}).get("terminated") or {}).get("exitCode"))
+             for c in st.get("containerStatuses") or []]
+    codes = [(n, int(x)) for n, x in codes if x is not None]
+    if not codes and st.get("exitCode") is not None:
+        codes = [(None, int(st["exitCode"]))]
+    conds = {(c.get("type"), c.get("status")) for c in st.get("conditions") or []}
+    for i, rule in enumerate(policy.get("rules") or []):
+        ec = rule.get("onExitCodes")
+        if ec:
+            vals = {int(v) for v in ec.get("values") or []}
+            for name, code in codes:
+                if ec.get("containerName") not in (None, name) or code == 0:
+                    continue
+                if (code in vals) == (ec.get("operator", "In") == "In"):
+                    ns, pn = pod["metadata"].get("namespace", "default"), pod["metadata"]["name"]
+                    return rule.get("action", "Count"), (f"Container {name or 'main'} for pod {ns}/{pn} failed with exit code "
+                                                         f"{code} matching {rule.get('action')} rule at index {i}")
+        for pc in rule.get("onPodConditions") or []:
+            if (pc.get("type"), pc.get("status", "True")) in conds:
+                return rule.get("action", "Count"), (f"Pod {pod['metadata']['name']} has condition {pc.get('type')} "
+                                                     f"matching {rule.get('action')} rule at index {i}")
+    return "Count", ""
+
+
 def _conditions(obj: dict, want: list[tuple[str, str, str, str]]) -> list[dict]:
     """Status conditions (type, status, reason, message), keeping an old entry's times while its
     status and reason hold, so an unchanged object is not rewritten."""
@@ -204,13 +236,18 @@ class Controllers:
             indexed = spec.get("completionMode") == "Indexed"
             pods = self._owned(pid, job)
             succeeded_idx, active, failed = set(), 0, 0
+            fail_job = None  # (message) of a podFailurePolicy FailJob match
             for o in pods:
                 ph = o.get("status", {}).get("phase")
                 idx = int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
                 if ph == "Succeeded":
                     succeeded_idx.add(idx if indexed else o["metadata"]["name"])
                 elif ph == "Failed":
-                    failed += 1
+                    action, why = _failure_action(spec.get("podFailurePolicy"), o)
+                    if action == "FailJob" and fail_job is None:
+                        fail_job = why
+                    if action != "Ignore":  # Ignore: not counted, the pod is replaced
+                        failed += 1
                 else:
                     active += 1
             done = fin is not None
@@ -219,7 +256,7 @@ class Controllers:
             started = st0.get("startTime") if not suspended else None
             over = (not done and not suspended and started is not None and deadline is not None
                     and now - _epoch(started) >= float(deadline))
-            if not done and (failed > backoff or over or suspended):
+            if not done and (failed > backoff or over or suspended or fail_job):
                 for o in pods:  # stop the rest (a gang job cannot finish without all ranks)
                     if o.get("status", {}).get("phase") not in TERMINAL:
                         self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
@@ -254,6 +291,9 @@ class Controllers:
                 if len(succeeded_idx) >= completions:
                     conds.append({"type": "Complete", "status": "True", "lastTransitionTime": now_iso()})
                     status["completionTime"] = now_iso()
+                elif fail_job:
+                    conds.append({"type": "Failed", "status": "True", "reason": "PodFailurePolicy", "message": fail_job,
+                                  "lastTransitionTime": now_iso()})
                 elif failed > backoff:
                     conds.append({"type": "Failed", "status": "True", "reason": "BackoffLimitExceeded",
                                   "lastTransitionTime": now_iso()})
