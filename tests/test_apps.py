@@ -529,8 +529,8 @@ def test_configmap_volume_updates_reach_a_running_pod(cluster):
 
 
 def test_gpu_pod_waits_for_a_terminating_pods_gpus(cluster):
-    """A deleted GPU pod keeps its GPUs through its grace period (a trainer writing a checkpoint);
-    a new pod bound to them meanwhile waits (ContainerCreating) and starts once they are free."""
+    """A deleted GPU pod is Terminating and keeps its GPUs through its grace period (a trainer
+    writing a checkpoint); a new pod that needs them waits and starts once they are free."""
     ws, env, kc, summary = cluster
     node = json.loads(kc("get", "nodes", "-o", "json").stdout)["items"][0]
     nn, gpus = node["metadata"]["name"], int(node["status"]["allocatable"]["amd.com/gpu"])
@@ -540,13 +540,11 @@ def test_gpu_pod_waits_for_a_terminating_pods_gpus(cluster):
     (ws / "old.json").write_text(json.dumps(pod("old", "trap '' TERM; while true; do sleep 0.1; done", 3)))
     kc("apply", "-f", str(ws / "old.json"))
     _until(lambda: json.loads(kc("get", "pod", "old", "-o", "json").stdout)["status"].get("phase") == "Running", 30)
-    kc("delete", "pod", "old")
+    kc("delete", "pod", "old", "--wait=false")
     t0 = time.monotonic()
+    assert any(l.split()[:1] == ["old"] and "Terminating" in l for l in kc("get", "pods").stdout.splitlines())
     (ws / "new.json").write_text(json.dumps(pod("new", "sleep 60", 30)))
     kc("apply", "-f", str(ws / "new.json"))
-    st = _until(lambda: json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"].get("reason") == "ContainerCreating"
-                or json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"].get("phase") == "Running", 20)
-    assert st
     _until(lambda: json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"].get("phase") == "Running", 30)
     assert time.monotonic() - t0 > 1.5  # it waited for the old pod's grace period
     assert json.loads(kc("get", "pod", "new", "-o", "json").stdout)["status"]["phase"] == "Running"

@@ -353,18 +353,26 @@ def test_put_patch_scale_and_rolling_update(cp):
     now = pods()
     new = [p for p in now if p["spec"]["containers"][0]["command"] == ["v2"]]
     assert len(now) == 3 and len(new) == 1
-    # each new pod that runs releases one old pod, until the rollout is complete
+    # each new pod that runs releases one old pod, until the rollout is complete; a released pod
+    # is Terminating until its node's agent (played here) confirms it has stopped
+    terminating = set()
     for _ in range(4):
         for p in pods():
-            if p["spec"]["containers"][0]["command"] == ["v2"] and p["status"].get("phase") != "Running":
+            if p["metadata"].get("deletionTimestamp"):
+                terminating.add(p["metadata"]["name"])
+                nc.delete(nc.k8s(f"/api/v1/namespaces/default/pods/{p['metadata']['name']}"),
+                          query={"gracePeriodSeconds": "0"})
+            elif p["spec"]["containers"][0]["command"] == ["v2"] and p["status"].get("phase") != "Running":
                 _set_pod(nc, "default", p["metadata"]["name"], "Running")
+    assert terminating == {p["metadata"]["name"] for p in v1}
     final = pods()
     assert len(final) == 2 and all(p["spec"]["containers"][0]["command"] == ["v2"] for p in final)
     st = k.get(k.k8s(base + "/web"))["status"]
     assert st["updatedReplicas"] == 2 and st["readyReplicas"] == 2 and st["observedGeneration"] == 2
     # scale subresource
     sc = k.request("PATCH", k.k8s(base + "/web/scale"), body={"spec": {"replicas": 1}})
-    assert sc["kind"] == "Scale" and sc["spec"]["replicas"] == 1 and len(pods()) == 1
+    live = [p for p in pods() if not p["metadata"].get("deletionTimestamp")]
+    assert sc["kind"] == "Scale" and sc["spec"]["replicas"] == 1 and len(live) == 1 and len(pods()) == 2
     with pytest.raises(ApiError) as ei:
         k.request("PATCH", k.k8s(base + "/web/scale"), body={"spec": {"replicas": -1}})
     assert ei.value.status == 422

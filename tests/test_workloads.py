@@ -847,3 +847,35 @@ def test_job_pod_failure_policy(cp):
     j = cp.store.get("jobs", _key("1a1", "default", "t"))
     failed = [c for c in j["status"]["conditions"] if c["type"] == "Failed"]
     assert failed and failed[0]["reason"] == "PodFailurePolicy" and "exit code 42" in failed[0]["message"]
+
+
+def test_graceful_pod_deletion_and_pod_gc(cp):
+    """A running pod on a node with a live agent goes Terminating (deletionTimestamp) and keeps its
+    GPUs; its controller replaces it at once; the pod GC force-deletes it if no agent confirms."""
+    import time as _time
+
+    from tritonk8ssupervisor_amd.controlplane.objects import GPU
+
+    _nodes(cp, 1, gpus=1)
+    cp.leases[_key("1a1", "kubenode1")] = _time.monotonic()
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "g"}, "spec": {
+        "replicas": 1, "selector": {"matchLabels": {"app": "g"}}, "template": {
+            "metadata": {"labels": {"app": "g"}}, "spec": {"terminationGracePeriodSeconds": 5, "containers": [
+                {"name": "c", "command": ["sleep", "60"], "resources": {"limits": {GPU: "1"}}}]}}}})
+    (old,) = _pods(cp, "g")
+    _run(cp, old)
+    cp._delete_pod("1a1", "default", old)
+    p = cp.store.get("pods", _key("1a1", "default", old))
+    assert p["metadata"]["deletionTimestamp"] and p["metadata"]["deletionGracePeriodSeconds"] == 5
+    cp.reconcile()
+    new = [n for n in _pods(cp, "g") if n != old]
+    assert len(new) == 1 and _node_of(cp, new[0]) is None  # replaced, but the GPU is still held
+    assert not cp._pod_gc()  # within its grace period (+15 s)
+    cp.store.patch("pods", _key("1a1", "default", old), lambda o: o["metadata"].__setitem__(
+        "deletionTimestamp", _time.strftime("%Y-%m-%dT%H:%M:%SZ", _time.gmtime(_time.time() - 20))))
+    assert cp._pod_gc()
+    cp.reconcile()
+    assert old not in _pods(cp) and _node_of(cp, new[0]) == "kubenode1"
+    # a pod that is not running (or on a node without a live agent) goes at once
+    cp._delete_pod("1a1", "default", new[0])
+    assert new[0] not in _pods(cp)

@@ -660,7 +660,7 @@ class Agent:
                 alive = cp.proc is not None and cp.proc.poll() is None
                 ready = alive and (cp.prober is None or cp.prober.ready)
                 if alive:
-                    state = {"running": {"startedAt": cp.started}}
+                    state = {"running": {"startedAt": _rfc3339(cp.started)}}
                 elif cp.exit_code is not None:
                     state = {"terminated": {"exitCode": cp.exit_code, "reason": "Completed" if cp.exit_code == 0 else "Error"}}
                 else:
@@ -677,12 +677,12 @@ class Agent:
                 main["state"] = {"terminated": {"exitCode": extra.get("exitCode", pp.exit_code),
                                                 "reason": "Completed" if phase == "Succeeded" else "Error"}}
             if phase == "Running" and "running" not in main["state"] and pp.proc is not None:
-                main.update(state={"running": {"startedAt": pp.started}}, ready=pp.prober is None or pp.prober.ready,
+                main.update(state={"running": {"startedAt": _rfc3339(pp.started)}}, ready=pp.prober is None or pp.prober.ready,
                             started=True)
             st["containerStatuses"] = [main] + [cstatus(sc, images.get(sc.name, "")) for sc in pp.sidecars]
             if pp.init:
                 st["initContainerStatuses"] = [cstatus(ic, images.get(ic.name, "")) for ic in pp.init]
-            st["startTime"] = pp.started
+            st["startTime"] = _rfc3339(pp.started)
         for k in ("message", "reason", "result"):
             if extra.get(k) is not None:
                 st[k] = extra[k]
@@ -773,6 +773,19 @@ class Agent:
             self._pods_meta.pop(key, None)
             self.runtime.stop(key, wait=False, on_done=lambda: self._terminated(key))
             return
+        if md.get("deletionTimestamp"):  # graceful deletion: stop it, then confirm the delete
+            self._config_wait.pop(key, None)
+            if self.runtime.is_terminating(key):
+                return  # already under way; its end confirms
+            cur = self.runtime.running().get(key)
+            uid = md.get("uid", "")
+            if cur is not None and (not uid or cur.uid == uid):
+                self.runtime.stop(key, grace=float(md.get("deletionGracePeriodSeconds", 30)), wait=False,
+                                  on_done=lambda: (self._confirm_deleted(md["namespace"], md["name"], uid),
+                                                   self._terminated(key)))
+            else:
+                self._confirm_deleted(md["namespace"], md["name"], uid)
+            return
         phase = pod.get("status", {}).get("phase", "Pending")
         if phase in TERMINAL:
             return
@@ -801,6 +814,18 @@ class Agent:
                 continue
             if changed:
                 trace(self.name, f"volumes of {key} updated: {','.join(changed)}")
+
+    def _confirm_deleted(self, ns: str, name: str, uid: str) -> None:
+        """The kubelet's last word on a gracefully deleted pod: its containers are gone."""
+        try:
+            self.api.delete(self.api.k8s(f"/api/v1/namespaces/{ns}/pods/{name}"), query={"gracePeriodSeconds": "0"},
+                            body={"apiVersion": "v1", "kind": "DeleteOptions", "gracePeriodSeconds": 0,
+                                  **({"preconditions": {"uid": uid}} if uid else {})})
+        except ApiError as e:
+            if e.status not in (404, 409):
+                print(f"{self.name}: pod {ns}/{name} not confirmed deleted: {e}", flush=True)
+        except OSError as e:
+            print(f"{self.name}: pod {ns}/{name} not confirmed deleted: {e}", flush=True)
 
     def _terminated(self, key: str) -> None:
         """A pod's termination is over: its IP is free, and a successor of the same name may start."""
@@ -869,6 +894,11 @@ def host_scope_env(ordinals: list[int]) -> dict:
     env["TK8S_GPU_DEVICES"] = ",".join(str(i) for i in range(len(ordinals)))
     env["TK8S_GPU_DEVICE"] = "0" if ordinals else ""
     return env
+
+
+def _rfc3339(t: float) -> str:
+    """A Kubernetes timestamp (what client-go parses), from a time.time() value."""
+    return time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))
 
 
 def pod_gpu_env(alloc_env: dict, ordinals: list[int], visibility: str = "allocated") -> dict:

@@ -92,6 +92,8 @@ def fmt_pods(items: list[dict], wide: bool, all_ns: bool) -> str:
         phase = st.get("phase", "Pending")
         if phase == "Pending" and _cond(p, "PodScheduled").get("status") == "False":
             phase = "Pending(Unschedulable)"
+        if p["metadata"].get("deletionTimestamp"):
+            phase = "Terminating"
         row = ([p["metadata"].get("namespace", "")] if all_ns else []) + [
             p["metadata"]["name"], "1/1" if phase == "Running" else "0/1", phase, str(cs.get("restartCount", 0)), _age(p)]
         if wide:
@@ -616,6 +618,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--namespaced", choices=["true", "false"])
     ap.add_argument("--subresource")
     ap.add_argument("--cascade", choices=["background", "foreground", "orphan"])
+    ap.add_argument("--grace-period", type=int)
+    ap.add_argument("--wait", choices=["true", "false"], default="true")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -662,10 +666,12 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 what, name = kind_key(a.args[0].split("/")[0]), a.args[0].split("/")[1]
             q = {"labelSelector": a.selector} if a.selector else None
             if name:
-                _print(k.get(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns))), a.output or "yaml",
-                       a.show_managed_fields)
-                return 0
-            if what == "node":
+                obj = k.get(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns)))
+                if a.output in ("json", "yaml"):
+                    _print(obj, a.output, a.show_managed_fields)
+                    return 0
+                items = [obj]  # a one-row table, as kubectl prints it
+            elif what == "node":
                 items = k.get(k.k8s("/api/v1/nodes"), query=q)["items"]
             elif a.all_namespaces:
                 path = "/api/v1/pods" if what == "pod" else collection_path(what).replace("/namespaces/default", "")
@@ -801,9 +807,23 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             if a.filename or a.kustomize:
                 n = delete_objects(k, _manifests(a))
             else:
-                what, name = kind_key(a.args[0]), a.args[1]
-                k.delete(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns)),
-                         query={"propagationPolicy": a.cascade.capitalize()} if a.cascade else None)
+                what, name = kind_key(a.args[0].split("/")[0]), (a.args[0].split("/", 1)[1] if "/" in a.args[0] else a.args[1])
+                q = {**({"propagationPolicy": a.cascade.capitalize()} if a.cascade else {}),
+                     **({"gracePeriodSeconds": "0"} if a.force else {"gracePeriodSeconds": str(a.grace_period)}
+                        if a.grace_period is not None and a.grace_period >= 0 else {})}
+                path = k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns))
+                out = k.delete(path, query=q or None)
+                if a.wait != "false" and isinstance(out, dict) and (out.get("metadata") or {}).get("deletionTimestamp"):
+                    # a Terminating pod (or an object held by finalizers): wait until it is gone, as kubectl does
+                    deadline = time.monotonic() + float(a.timeout.rstrip("s"))
+                    while time.monotonic() < deadline:
+                        try:
+                            k.get(path)
+                        except ApiError as e:
+                            if e.status == 404:
+                                break
+                            raise
+                        time.sleep(0.1)
                 n = 1
             print(f"{n} object(s) deleted")
         elif a.verb == "logs" and (a.selector or a.all_containers or a.previous or (a.args and "/" in a.args[0])):

@@ -70,7 +70,7 @@ def _epoch(iso: str | None) -> float:
 
 REVISION = "deployment.kubernetes.io/revision"
 from .objects import (
-    VALIDATION_LABEL, TERMINAL, _key, _cond, _set_cond, _set_ready, _xgmi_view, template_hash, labels_match,
+    VALIDATION_LABEL, TERMINAL, _key, _cond, _set_cond, _set_ready, _xgmi_view, template_hash, labels_match, node_ready,
 )
 
 
@@ -135,6 +135,34 @@ class Controllers:
             self._event(pid, ns, {"kind": owner_kind, "name": owner["metadata"]["name"]}, "FailedCreate",
                         f"Error creating: pods \"{name}\" is forbidden: {why}", "Warning")
         return self.store.put("pods", _key(pid, ns, name), pod)
+
+    def _delete_pod(self, pid: str, ns: str, name: str, grace: float | None = None, force: bool = False) -> dict | None:
+        """Delete a pod gracefully, as the API server does: a pod running on a node whose agent is
+        alive gets ``metadata.deletionTimestamp`` (now + grace, ``terminationGracePeriodSeconds``
+        by default) and stays, Terminating, until that agent has stopped it (preStop hook, SIGTERM,
+        SIGKILL at the deadline) and confirms with a forced delete; controllers stop counting it at
+        once and the scheduler keeps counting its GPUs. Any other pod -- not started, finished, on
+        a node no agent answers for -- or ``force``/``grace == 0`` goes at once. The lease loop
+        force-deletes a Terminating pod whose agent never confirmed (``_pod_gc``)."""
+        key = _key(pid, ns, name)
+        pod = self.store.get("pods", key)
+        if pod is None:
+            return None
+        nn = pod["spec"].get("nodeName")
+        if grace is None:
+            grace = float(pod["spec"].get("terminationGracePeriodSeconds", 30))
+        graceful = (not force and grace > 0 and nn and pod.get("status", {}).get("phase") == "Running"
+                    and _key(pid, nn) in getattr(self, "leases", {}) and node_ready(self.store.get("nodes", _key(pid, nn)) or {}))
+        if not graceful:
+            return self.store.delete("pods", key)
+        if pod["metadata"].get("deletionTimestamp"):
+            return pod  # already terminating (a second delete may only shorten it; not modelled)
+
+        def mark(o):
+            o["metadata"]["deletionTimestamp"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(time.time() + grace))
+            o["metadata"]["deletionGracePeriodSeconds"] = int(grace)
+        self._again = True  # controllers replace it now
+        return self.store.patch("pods", key, mark)
 
     def _owned(self, pid: str, owner: dict) -> list[dict]:
         uid = owner["metadata"]["uid"]
@@ -242,6 +270,8 @@ class Controllers:
                 idx = int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
                 if ph == "Succeeded":
                     succeeded_idx.add(idx if indexed else o["metadata"]["name"])
+                elif o["metadata"].get("deletionTimestamp"):
+                    continue  # terminating: neither active nor failed (its replacement may start)
                 elif ph == "Failed":
                     action, why = _failure_action(spec.get("podFailurePolicy"), o)
                     if action == "FailJob" and fail_job is None:
@@ -258,8 +288,8 @@ class Controllers:
                     and now - _epoch(started) >= float(deadline))
             if not done and (failed > backoff or over or suspended or fail_job):
                 for o in pods:  # stop the rest (a gang job cannot finish without all ranks)
-                    if o.get("status", {}).get("phase") not in TERMINAL:
-                        self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                    if o.get("status", {}).get("phase") not in TERMINAL and not o["metadata"].get("deletionTimestamp"):
+                        self._delete_pod(pid, ns, o["metadata"]["name"])
                         active -= 1
             elif not done:
                 running_idx = {int(o["metadata"].get("annotations", {}).get("batch.kubernetes.io/job-completion-index", -1))
@@ -329,7 +359,8 @@ class Controllers:
             match = (spec.get("selector") or {}).get("matchLabels") or {}
 
             def live():
-                return [o for o in self._owned(pid, d) if o.get("status", {}).get("phase") not in TERMINAL]
+                return [o for o in self._owned(pid, d) if o.get("status", {}).get("phase") not in TERMINAL
+                        and not o["metadata"].get("deletionTimestamp")]
 
             unavailable = want // 4
             for _ in range(2):  # scale down old -> room to surge again, in the same pass
@@ -338,7 +369,7 @@ class Controllers:
                 old = [o for o in pods if o not in new]
                 if (spec.get("strategy") or {}).get("type") == "Recreate" and old:
                     for o in old:
-                        self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                        self._delete_pod(pid, ns, o["metadata"]["name"])
                     pods, old = new, []
                 surge = max(1, -(-want // 4)) if old else 0
                 for _ in range(max(0, min(want - len(new), want + surge - len(pods)))):
@@ -348,9 +379,9 @@ class Controllers:
                 ready_new = sum(1 for o in new if o.get("status", {}).get("phase") == "Running")
                 keep_old = max(0, want - unavailable - ready_new)
                 for o in sorted(old, key=lambda o: o["metadata"]["name"])[keep_old:]:
-                    self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                    self._delete_pod(pid, ns, o["metadata"]["name"])
                 for o in sorted(new, key=lambda o: o["metadata"]["name"])[want:]:
-                    self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                    self._delete_pod(pid, ns, o["metadata"]["name"])
             pods = live()
             self._sync_deployment_revisions(pid, d, h, pods, tmpl)
             running = sum(1 for o in pods if o.get("status", {}).get("phase") == "Running")
@@ -450,8 +481,8 @@ class Controllers:
                 addr = {"ip": ip, "nodeName": o["spec"].get("nodeName"),
                         "targetRef": {"kind": "Pod", "name": o["metadata"]["name"], "namespace": ns,
                                       "uid": o["metadata"].get("uid")}}
-                is_ready = not any(c.get("type") == "Ready" and c.get("status") == "False"
-                                   for c in o["status"].get("conditions") or [])
+                is_ready = not o["metadata"].get("deletionTimestamp") and not any(
+                    c.get("type") == "Ready" and c.get("status") == "False" for c in o["status"].get("conditions") or [])
                 (ready if is_ready else not_ready).append(addr)
                 for p in svc["spec"].get("ports") or []:
                     tp = p.get("targetPort", p.get("port"))

@@ -37,7 +37,7 @@ def _amount(v, total: int) -> int:
 
 def _healthy(pod: dict) -> bool:
     st = pod.get("status") or {}
-    return st.get("phase") == "Running" and not any(
+    return st.get("phase") == "Running" and not (pod.get("metadata") or {}).get("deletionTimestamp") and not any(
         c.get("type") == "Ready" and c.get("status") == "False" for c in st.get("conditions") or [])
 
 
@@ -144,7 +144,7 @@ class Disruption:
                 "disruptedPods", {}).__setitem__(name, now_iso()))
         if dry_run:
             return
-        self.store.delete("pods", _key(pid, ns, name))
+        self._delete_pod(pid, ns, name)
         self._event(pid, ns, {"kind": "Pod", "name": name}, "Evicted", "Evicted through the eviction API", "Normal")
         self.reconcile()
 

@@ -265,6 +265,10 @@ class KubernetesAPI:
         self.leases.pop(key, None)
         if n is None:
             raise HttpError(404, f"node {name} not found")
+        # pod GC: what was Terminating on the node has no agent left to confirm it
+        for o in self.store.list("pods", lambda o: self._in(p, o) and o["spec"].get("nodeName") == name
+                                 and o["metadata"].get("deletionTimestamp")):
+            self.store.delete("pods", _key(p, o["metadata"]["namespace"], o["metadata"]["name"]))
         self.reconcile()
         return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": "nodes"}}
 
@@ -548,6 +552,19 @@ class KubernetesAPI:
             self._admit_webhooks(p, "DELETE", kind, ns, name, None, self._strip(cur), False, dry)
             if dry:
                 return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
+            pre = opts.get("preconditions") or {}
+            if pre.get("uid") and pre["uid"] != cur["metadata"].get("uid"):
+                raise HttpError(409, f'Precondition failed: UID in precondition: {pre["uid"]}, UID in object meta: '
+                                     f'{cur["metadata"].get("uid")}')
+            if kind == "pods" and not cur["metadata"].get("finalizers"):
+                g = req.q("gracePeriodSeconds")
+                g = g if g not in (None, "") else opts.get("gracePeriodSeconds")
+                self._delete_pod(p, ns, name, grace=None if g is None else float(g))
+                still = self.store.get(kind, _key(p, ns, name))
+                self.reconcile()
+                if still is not None:  # Terminating: the API server answers with the object
+                    return self._strip(still)
+                return {"kind": "Status", "status": "Success", "details": {"name": name, "kind": kind}}
             if cur["metadata"].get("finalizers"):
                 def mark(o):
                     o["metadata"].setdefault("deletionTimestamp", now_iso())
@@ -578,6 +595,8 @@ class KubernetesAPI:
                     if policy == "Orphan":
                         self.store.patch(dep_kind, dkey, lambda x: x["metadata"].__setitem__("ownerReferences", [
                             r for r in x["metadata"].get("ownerReferences", []) if r.get("uid") != uid]))
+                    elif dep_kind == "pods":
+                        self._delete_pod(p, dep["metadata"].get("namespace", ns), dep["metadata"]["name"])
                     else:
                         self.store.delete(dep_kind, dkey)
         self.reconcile()

@@ -420,7 +420,10 @@ def _pod_row(p: dict) -> list:
     ready = sum(1 for c in cs if c.get("ready"))
     restarts = sum(int(c.get("restartCount", 0)) for c in cs)
     phase = (p.get("status") or {}).get("phase", "Pending")
-    return [p["metadata"]["name"], f"{ready}/{n}", (p.get("status") or {}).get("reason") or phase, restarts, _age(p),
+    if p["metadata"].get("deletionTimestamp"):
+        phase = "Terminating"
+    return [p["metadata"]["name"], f"{ready}/{n}", phase if phase == "Terminating" else (p.get("status") or {}).get("reason")
+            or phase, restarts, _age(p),
             (p.get("status") or {}).get("podIP", "<none>"), (p.get("spec") or {}).get("nodeName", "<none>")]
 
 

@@ -76,7 +76,8 @@ class Priority:
         if need <= 0 or pod["spec"].get("preemptionPolicy") == "Never":
             return None
         live = [o for o in self.store.list("pods", lambda o: self._in(pid, o))
-                if o["spec"].get("nodeName") and o.get("status", {}).get("phase") not in TERMINAL]
+                if o["spec"].get("nodeName") and o.get("status", {}).get("phase") not in TERMINAL
+                and not o["metadata"].get("deletionTimestamp")]
         protected = self._pdb_protected(pid) if self.store.keys("poddisruptionbudgets") else set()
         best = None
         for n in nodes:
@@ -105,7 +106,7 @@ class Priority:
         ns, name = pod["metadata"]["namespace"], pod["metadata"]["name"]
         for o in victims:
             vns, vname = o["metadata"]["namespace"], o["metadata"]["name"]
-            self.store.delete("pods", _key(pid, vns, vname))
+            self._delete_pod(pid, vns, vname)  # (its GPUs: the agent starts the preemptor once they are free)
             used[nn] = used.get(nn, 0) - pod_gpus(o)
             self._event(pid, vns, {"kind": "Pod", "name": vname}, "Preempted",
                         f"Preempted by pod {ns}/{name} (priority {priority(pod)}) on node {nn}", "Normal")

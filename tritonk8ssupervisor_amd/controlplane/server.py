@@ -388,6 +388,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
                         self._node_lost(key, f"lease expired after {self.node_grace:.1f}s")
                         changed = True
             changed |= self._taint_manager()
+            changed |= self._pod_gc()
             if changed:
                 self.reconcile()
 
@@ -404,6 +405,23 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         n = self.store.patch("nodes", key, lost)
         self._event(key.split("/", 1)[0], "default", {"kind": "Node", "name": n["metadata"]["name"]}, "NodeNotReady",
                     why, "Warning")
+
+    def _pod_gc(self) -> bool:
+        """Terminating pods whose agent never confirmed (it died, or lost its node): force-deleted
+        15 s after their deadline (``metadata.deletionTimestamp``)."""
+        import calendar
+
+        now, gone = time.time(), False
+        for pod in self.store.list("pods", lambda o: bool(o["metadata"].get("deletionTimestamp"))):
+            try:
+                deadline = calendar.timegm(time.strptime(pod["metadata"]["deletionTimestamp"], "%Y-%m-%dT%H:%M:%SZ"))
+            except ValueError:
+                deadline = 0
+            nn = pod["spec"].get("nodeName")
+            if now > deadline + 15 or (nn and self.store.get("nodes", _key(pod["_project"], nn)) is None):
+                self.store.delete("pods", _key(pod["_project"], pod["metadata"]["namespace"], pod["metadata"]["name"]))
+                gone = True
+        return gone
 
     def _taint_manager(self) -> bool:
         """Evict pods from nodes with NoExecute taints they do not tolerate: at once for a taint
@@ -437,7 +455,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
                         added = now
                     if not tols or now - added >= min(float(s) for s in secs):
                         ns, name = pod["metadata"].get("namespace", "default"), pod["metadata"]["name"]
-                        self.store.delete("pods", _key(pid, ns, name))
+                        self._delete_pod(pid, ns, name)
                         self._event(pid, ns, {"kind": "Pod", "name": name}, "TaintManagerEviction",
                                     f"Marking for deletion Pod {ns}/{name}: node {nn} has taint {t.get('key')}:NoExecute",
                                     "Warning")

@@ -80,13 +80,13 @@ class Workloads:
                     continue
 
             def running(o):
-                return o.get("status", {}).get("phase") == "Running"
+                return o.get("status", {}).get("phase") == "Running" and not o["metadata"].get("deletionTimestamp")
 
             # a pod of a StatefulSet that ended (restartPolicy is Always, so only a failure) is
             # replaced under the same name
             for i, o in list(pods.items()):
                 if o.get("status", {}).get("phase") in TERMINAL:
-                    self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                    self._delete_pod(pid, ns, o["metadata"]["name"])
                     del pods[i]
             # scale up, in order unless Parallel
             for i in range(want):
@@ -120,13 +120,13 @@ class Workloads:
             extra = sorted((i for i in pods if i >= want), reverse=True)
             for i in extra[: len(extra) if parallel else 1]:
                 if parallel or all(running(pods[j]) for j in pods if j < want):
-                    self.store.delete("pods", _key(pid, ns, pods.pop(i)["metadata"]["name"]))
+                    self._delete_pod(pid, ns, pods.pop(i)["metadata"]["name"])
             # rolling update: one stale pod at a time, highest ordinal first, once all others run
             if rolling and len(pods) == want and all(running(o) for o in pods.values()):
                 stale = [i for i, o in pods.items() if i >= partition and o["metadata"]["labels"].get(REVISION) != h]
                 if stale:
                     i = max(stale)
-                    self.store.delete("pods", _key(pid, ns, pods.pop(i)["metadata"]["name"]))
+                    self._delete_pod(pid, ns, pods.pop(i)["metadata"]["name"])
                     self._again = True  # the next pass re-creates it from the new template
             ready = sum(1 for o in pods.values() if running(o))
             updated = sum(1 for o in pods.values() if o["metadata"]["labels"].get(REVISION) == h)
@@ -149,7 +149,8 @@ class Workloads:
             spec = rs["spec"]
             want = int(spec.get("replicas", 1))
             match = (spec.get("selector") or {}).get("matchLabels") or {}
-            live = [o for o in self._owned(pid, rs) if o.get("status", {}).get("phase") not in TERMINAL]
+            live = [o for o in self._owned(pid, rs) if o.get("status", {}).get("phase") not in TERMINAL
+                    and not o["metadata"].get("deletionTimestamp")]
             for _ in range(max(0, want - len(live))):
                 self._seq += 1
                 live.append(self._new_pod(pid, ns, f"{name}-{self._seq:05x}", rs, "ReplicaSet", spec["template"],
@@ -157,7 +158,7 @@ class Workloads:
             # scale down: pods not yet running go first, then the youngest
             order = sorted(live, key=lambda o: (o.get("status", {}).get("phase") == "Running", o["metadata"]["name"]))
             for o in order[: max(0, len(live) - want)]:
-                self.store.delete("pods", _key(pid, ns, o["metadata"]["name"]))
+                self._delete_pod(pid, ns, o["metadata"]["name"])
                 live.remove(o)
             ready = sum(1 for o in live if o.get("status", {}).get("phase") == "Running")
             status = {"observedGeneration": int(rs["metadata"].get("generation", 1)), "replicas": len(live),
@@ -171,7 +172,7 @@ class Workloads:
         if job is None:
             return
         for pod in self._owned(pid, job):
-            self.store.delete("pods", _key(pid, ns, pod["metadata"]["name"]))
+            self._delete_pod(pid, ns, pod["metadata"]["name"])
 
     def _ctl_cronjobs(self, pid: str, now=None) -> None:
         from datetime import datetime, timezone
