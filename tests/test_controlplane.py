@@ -428,3 +428,61 @@ def test_cluster_dns_names():
     assert labels == ["cart", "shop", "svc", "cluster", "local"] and qtype == 1
     assert dns.parse_reply(dns.build_reply(qid, flags, question, 0, ["127.96.0.9"])) == (0, ["127.96.0.9"])
     assert dns.parse_reply(dns.build_reply(qid, flags, question, dns.NXDOMAIN, [])) == (dns.NXDOMAIN, [])
+
+
+def test_external_name_services_and_session_affinity():
+    """An ExternalName Service is a DNS alias (CNAME, no IP, no proxy); ClientIP session affinity
+    keeps a client on one endpoint."""
+    import asyncio
+
+    from tritonk8ssupervisor_amd.controlplane import dns
+    from tritonk8ssupervisor_amd.controlplane.httpserver import HttpError
+    from tritonk8ssupervisor_amd.controlplane.proxy import ServiceProxy
+    from tritonk8ssupervisor_amd.controlplane.server import ControlPlane
+
+    cpl = ControlPlane("127.0.0.1", 0)
+    cpl.store.put("projects", "1a1", {"id": "1a1", "created_seq": 1, "metadata": {"name": "1a1"}})
+    o = cpl.create("1a1", "services", "shop", {"metadata": {"name": "db"}, "spec": {
+        "type": "ExternalName", "externalName": "db.prod.example.com"}})
+    assert "clusterIP" not in o["spec"] and not any(k[0].endswith("/db") for k in cpl._proxy_wanted())
+    ans = cpl.dns_resolve("db.shop.svc.cluster.local")
+    assert isinstance(ans, dns.CName) and ans == "db.prod.example.com"
+    qid, flags, _l, _t, _c, question = dns.parse_query(dns.query("db.shop.svc.cluster.local"))
+    cn = []
+    assert dns.parse_reply(dns.build_reply(qid, flags, question, 0, [], cname=ans), cn) == (0, []) and cn == [ans]
+    with pytest.raises(HttpError):
+        cpl.create("1a1", "services", "shop", {"metadata": {"name": "bad"}, "spec": {"type": "ExternalName"}})
+    s = cpl.create("1a1", "services", "shop", {"metadata": {"name": "web"}, "spec": {
+        "ports": [{"port": 80}], "sessionAffinity": "ClientIP"}})
+    assert cpl._svc_affinity("1a1/shop/web") == 10800.0
+
+    async def run():  # two backends; with affinity every connection from 127.0.0.1 lands on the same one
+        hits = []
+
+        async def backend(tag, r, w):
+            hits.append(tag)
+            w.close()
+
+        s1 = await asyncio.start_server(lambda r, w: backend("a", r, w), "127.0.0.1", 0)
+        s2 = await asyncio.start_server(lambda r, w: backend("b", r, w), "127.0.0.1", 0)
+        eps = [("127.0.0.1", s1.sockets[0].getsockname()[1]), ("127.0.0.1", s2.sockets[0].getsockname()[1])]
+        for aff in (0, 60):
+            hits.clear()
+            px = ServiceProxy(lambda svc, pk: eps, affinity=lambda svc, a=aff: a)
+            await px.sync({("svc", "127.0.0.1", 0): "80"})
+            port = next(iter(px.listeners.values())).sockets[0].getsockname()[1]
+            for _ in range(4):
+                r, w = await asyncio.open_connection("127.0.0.1", port)
+                await r.read()
+                w.close()
+            await asyncio.sleep(0.05)
+            await px.close()
+            yield sorted(set(hits))
+        s1.close()
+        s2.close()
+
+    async def collect():
+        return [x async for x in run()]
+
+    spread, sticky = asyncio.run(collect())
+    assert spread == ["a", "b"] and len(sticky) == 1

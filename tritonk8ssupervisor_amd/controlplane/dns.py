@@ -6,6 +6,7 @@ docs/img/infrastructure-containers.png): authoritative A records under ``cluster
   <host>.<svc>.<ns>.svc.cluster.local                                  -> the pod with that hostname
                                  and subdomain (a StatefulSet's <name>-<ordinal> under its Service)
   <a-b-c-d>.<ns>.pod.cluster.local                                     -> a.b.c.d
+  <svc>.<ns>.svc.cluster.local of an ExternalName Service              -> a CNAME to its externalName
   any other name under cluster.local                                   -> NXDOMAIN
   names outside the cluster domain                                     -> REFUSED (not a recursor)
 
@@ -23,7 +24,11 @@ from typing import Callable
 
 DOMAIN = "cluster.local"
 NOERROR, NXDOMAIN, REFUSED, FORMERR = 0, 3, 5, 1
-QTYPE_A, QTYPE_ANY, QCLASS_IN = 1, 255, 1
+QTYPE_A, QTYPE_CNAME, QTYPE_ANY, QCLASS_IN = 1, 5, 255, 1
+
+
+class CName(str):
+    """A resolver answer that is an alias (an ExternalName Service): the target's name."""
 
 
 def parse_query(data: bytes) -> tuple[int, int, list[str], int, int, bytes]:
@@ -47,11 +52,29 @@ def parse_query(data: bytes) -> tuple[int, int, list[str], int, int, bytes]:
     return qid, flags, labels, qtype, qclass, data[12:i + 4]
 
 
-def build_reply(qid: int, flags: int, question: bytes, rcode: int, ips: list[str], ttl: int = 5) -> bytes:
-    hdr = struct.pack("!HHHHHH", qid, 0x8000 | 0x0400 | (flags & 0x0100) | rcode, 1, len(ips), 0, 0)
-    answers = b"".join(b"\xc0\x0c" + struct.pack("!HHIH", QTYPE_A, QCLASS_IN, ttl, 4) + socket.inet_aton(ip)
-                       for ip in ips)
-    return hdr + question + answers
+def _name(n: str) -> bytes:
+    return b"".join(bytes([len(p)]) + p.encode() for p in n.rstrip(".").split(".") if p) + b"\x00"
+
+
+def build_reply(qid: int, flags: int, question: bytes, rcode: int, ips: list[str], ttl: int = 5,
+                cname: str | None = None) -> bytes:
+    answers = []
+    if cname:
+        target = _name(cname)
+        answers.append(b"\xc0\x0c" + struct.pack("!HHIH", QTYPE_CNAME, QCLASS_IN, ttl, len(target)) + target)
+    answers += [b"\xc0\x0c" + struct.pack("!HHIH", QTYPE_A, QCLASS_IN, ttl, 4) + socket.inet_aton(ip) for ip in ips]
+    hdr = struct.pack("!HHHHHH", qid, 0x8000 | 0x0400 | (flags & 0x0100) | rcode, 1, len(answers), 0, 0)
+    return hdr + question + b"".join(answers)
+
+
+def _read_name(data: bytes, i: int) -> str:
+    parts = []
+    while data[i]:
+        if data[i] & 0xC0:
+            return ".".join(parts + [_read_name(data, ((data[i] & 0x3F) << 8) | data[i + 1])])
+        parts.append(data[i + 1:i + 1 + data[i]].decode())
+        i += data[i] + 1
+    return ".".join(parts)
 
 
 def query(name: str, qid: int = 0x1234) -> bytes:
@@ -60,8 +83,8 @@ def query(name: str, qid: int = 0x1234) -> bytes:
     return struct.pack("!HHHHHH", qid, 0x0100, 1, 0, 0, 0) + q + struct.pack("!HH", QTYPE_A, QCLASS_IN)
 
 
-def parse_reply(data: bytes) -> tuple[int, list[str]]:
-    """(rcode, A addresses) of a reply to ``query``."""
+def parse_reply(data: bytes, cnames: list | None = None) -> tuple[int, list[str]]:
+    """(rcode, A addresses) of a reply to ``query``; CNAME targets are appended to ``cnames``."""
     _, flags, _, an, _, _ = struct.unpack("!HHHHHH", data[:12])
     i = 12
     while data[i]:
@@ -74,6 +97,8 @@ def parse_reply(data: bytes) -> tuple[int, list[str]]:
         i += 10
         if rtype == QTYPE_A and rdlen == 4:
             ips.append(socket.inet_ntoa(data[i:i + 4]))
+        elif rtype == QTYPE_CNAME and cnames is not None:
+            cnames.append(_read_name(data, i))
         i += rdlen
     return flags & 0xF, ips
 
@@ -96,6 +121,8 @@ class DnsProtocol(asyncio.DatagramProtocol):
             reply = build_reply(qid, flags, question, REFUSED, [])
         elif ips is None:
             reply = build_reply(qid, flags, question, NXDOMAIN, [])
+        elif isinstance(ips, CName):  # an alias answers every type with the CNAME
+            reply = build_reply(qid, flags, question, NOERROR, [], cname=str(ips))
         elif qclass == QCLASS_IN and qtype in (QTYPE_A, QTYPE_ANY):
             reply = build_reply(qid, flags, question, NOERROR, ips)
         else:

@@ -626,8 +626,17 @@ class KubernetesAPI:
     def _alloc_service(self, body: dict, exclude: str | None = None) -> None:
         spec = body.setdefault("spec", {})
         stype = spec.setdefault("type", "ClusterIP")
+        if stype == "ExternalName":  # a DNS alias (dns.py answers a CNAME): no IP, no proxy
+            ext = spec.get("externalName") or ""
+            if not ext or len(ext) > 253 or not all(x and len(x) <= 63 for x in ext.rstrip(".").split(".")):
+                raise HttpError(422, 'Service is invalid: spec.externalName: Required value: a DNS name')
+            spec.pop("clusterIP", None)
+            return
         if stype not in ("ClusterIP", "NodePort", "LoadBalancer"):
             raise HttpError(422, f"service type {stype!r} is not supported")
+        aff = spec.setdefault("sessionAffinity", "None")
+        if aff not in ("None", "ClientIP"):
+            raise HttpError(422, f"spec.sessionAffinity: Unsupported value: {aff!r}")
         ports = spec.get("ports") or []
         if spec.get("clusterIP") == "None":  # headless: DNS answers with the pods, no proxy
             if stype != "ClusterIP":
@@ -693,7 +702,7 @@ class KubernetesAPI:
         for svc in self.store.list("services"):
             key = _key(svc["_project"], svc["metadata"]["namespace"], svc["metadata"]["name"])
             spec = svc["spec"]
-            if spec.get("clusterIP") == "None":
+            if spec.get("clusterIP") in (None, "None") or spec.get("type") == "ExternalName":
                 continue
             for p in spec.get("ports", []):
                 wanted[(key, spec["clusterIP"], host_port(p["port"]))] = p["name"]
@@ -703,6 +712,14 @@ class KubernetesAPI:
                 if spec.get("type") == "LoadBalancer":
                     wanted[(key, lb_host, host_port(p["port"]))] = p["name"]
         return wanted
+
+    def _svc_affinity(self, key: str) -> float:
+        """ClientIP session affinity timeout of a Service (0: none), for the proxy."""
+        o = self.store.get("services", key)
+        spec = (o or {}).get("spec") or {}
+        if spec.get("sessionAffinity") != "ClientIP":
+            return 0.0
+        return float(((spec.get("sessionAffinityConfig") or {}).get("clientIP") or {}).get("timeoutSeconds", 10800))
 
     def _sync_proxy(self) -> None:
         try:
@@ -774,6 +791,10 @@ class KubernetesAPI:
             o = self.store.get("services", _key(p["id"], ns, svc))
             if o is None:
                 continue
+            if o["spec"].get("type") == "ExternalName":
+                from .dns import CName
+
+                return CName(o["spec"].get("externalName", "")) if host is None else None
             if host is None and o["spec"].get("clusterIP") not in (None, "", "None"):
                 return [o["spec"]["clusterIP"]]
             # headless Service: its running pods; <host>.<svc>: the pod with that hostname and

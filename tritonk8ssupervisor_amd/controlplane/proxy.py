@@ -12,19 +12,25 @@ event loop:
   (docs/detailed.md:329-364) exposed its frontend exactly this way.
 
 Connections go round-robin to the Service's endpoints: Running pods of the same
-project/namespace whose labels match ``spec.selector``, at ``status.podIP:targetPort``.
+project/namespace whose labels match ``spec.selector``, at ``status.podIP:targetPort``; with
+``sessionAffinity: ClientIP`` a client address keeps its endpoint for
+``sessionAffinityConfig.clientIP.timeoutSeconds`` (10800) after its last connection.
 """
 from __future__ import annotations
 
 import asyncio
 import itertools
+import time
 from typing import Callable
 
 
 class ServiceProxy:
-    def __init__(self, endpoints: Callable[[str, str], list[tuple[str, int]]], log: Callable[[str], None] = print):
+    def __init__(self, endpoints: Callable[[str, str], list[tuple[str, int]]], log: Callable[[str], None] = print,
+                 affinity: Callable[[str], float] | None = None):
         self.endpoints = endpoints          # (service key, port name/number) -> [(ip, port)]
         self.log = log
+        self.affinity = affinity            # service key -> ClientIP affinity timeout in s (0: none)
+        self._sticky: dict[tuple[str, str, str], tuple[tuple[str, int], float]] = {}
         self.listeners: dict[tuple[str, str, int], asyncio.AbstractServer] = {}  # (svc key, host, port)
         self._rr: dict[tuple[str, str], itertools.count] = {}
 
@@ -56,9 +62,16 @@ class ServiceProxy:
             writer.close()
             return
         n = next(self._rr.setdefault((svc, port_key), itertools.count()))
+        order = [eps[(n + i) % len(eps)] for i in range(len(eps))]
+        ttl = self.affinity(svc) if self.affinity is not None else 0
+        client = (writer.get_extra_info("peername") or ("?",))[0]
+        if ttl:
+            hit = self._sticky.get((svc, port_key, client))
+            if hit and hit[1] > time.monotonic() and hit[0] in order:
+                order.remove(hit[0])
+                order.insert(0, hit[0])  # the client's endpoint, while it is still one
         up_r = up_w = None
-        for i in range(len(eps)):  # round robin, skipping endpoints that refuse
-            host, port = eps[(n + i) % len(eps)]
+        for host, port in order:  # round robin, skipping endpoints that refuse
             try:
                 up_r, up_w = await asyncio.wait_for(asyncio.open_connection(host, port), 5.0)
                 break
@@ -67,6 +80,8 @@ class ServiceProxy:
         if up_w is None:
             writer.close()
             return
+        if ttl:
+            self._sticky[(svc, port_key, client)] = ((host, port), time.monotonic() + ttl)
         await asyncio.gather(_pump(reader, up_w), _pump(up_r, writer), return_exceptions=True)
         for w in (writer, up_w):
             w.close()

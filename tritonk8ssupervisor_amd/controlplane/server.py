@@ -100,7 +100,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
 
         from .ingress import IngressController
 
-        self.proxy = ServiceProxy(self._endpoints, log=lambda m: self._log_error(m + "\n"))
+        self.proxy = ServiceProxy(self._endpoints, log=lambda m: self._log_error(m + "\n"), affinity=self._svc_affinity)
         self.ingress = IngressController(self._ingress_routes, self._endpoints, log=lambda m: self._log_error(m + "\n"))
         self.dns_port = host_port(53) if dns_port is None else dns_port          # 0 disables
         self.ingress_port = host_port(80) if ingress_port is None else ingress_port
