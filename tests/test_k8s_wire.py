@@ -647,3 +647,28 @@ def _https_webhook(kube, handler, seen, rule):
         assert any(p == "/tls" and k == "ServiceAccount" for p, _op, k, _u in seen)
     finally:
         srv.shutdown()
+
+
+def test_pod_security_admission(kube):
+    """Namespace labels pick the Pod Security Standard: enforce refuses, warn answers with a
+    Warning header (podsecurity.py)."""
+    for ns, labels in (("tenant", {"pod-security.kubernetes.io/enforce": "baseline"}),
+                       ("strict", {"pod-security.kubernetes.io/warn": "restricted"})):
+        assert _raw(kube, "POST", "/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace",
+                                                         "metadata": {"name": ns, "labels": labels}})[0] == 201
+    pod = lambda name, **spec: {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name},
+                                "spec": {"containers": [{"name": "c", "command": ["true"]}], **spec}}
+    code, _, body = _raw(kube, "POST", "/api/v1/namespaces/tenant/pods", pod("dev", volumes=[
+        {"name": "d", "hostPath": {"path": "/dev"}}]))
+    assert code == 403 and 'violates PodSecurity "baseline:latest"' in body["message"] and "hostPath" in body["message"]
+    code, _, body = _raw(kube, "POST", "/api/v1/namespaces/tenant/pods", pod("net", hostNetwork=True))
+    assert code == 403 and "host namespaces" in body["message"]
+    assert _raw(kube, "POST", "/api/v1/namespaces/tenant/pods", pod("ok"))[0] == 201
+    conn = http.client.HTTPConnection(kube.host, kube.port, timeout=10)
+    conn.request("POST", kube.k8s("/api/v1/namespaces/strict/pods"), body=json.dumps(pod("loose")),
+                 headers={"Authorization": f"Bearer {kube.token}", "Content-Type": "application/json"})
+    r = conn.getresponse()
+    r.read()
+    assert r.status == 201 and "restricted:latest" in (r.getheader("Warning") or "")
+    assert "runAsNonRoot" in r.getheader("Warning")
+    conn.close()

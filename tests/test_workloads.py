@@ -879,3 +879,19 @@ def test_graceful_pod_deletion_and_pod_gc(cp):
     # a pod that is not running (or on a node without a live agent) goes at once
     cp._delete_pod("1a1", "default", new[0])
     assert new[0] not in _pods(cp)
+
+
+def test_pod_security_standards_unit():
+    from tritonk8ssupervisor_amd.controlplane.podsecurity import violations
+
+    good = {"spec": {"securityContext": {"runAsNonRoot": True, "seccompProfile": {"type": "RuntimeDefault"}},
+                     "containers": [{"name": "c", "securityContext": {
+                         "allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}}}],
+                     "volumes": [{"name": "v", "emptyDir": {}}]}}
+    assert violations(good, "restricted") == [] and violations(good, "baseline") == []
+    bad = {"spec": {"containers": [{"name": "c", "securityContext": {"privileged": True, "capabilities": {"add": ["SYS_ADMIN"]}},
+                                    "ports": [{"containerPort": 80, "hostPort": 80}]}]}}
+    v = violations(bad, "baseline")
+    assert any("privileged" in x for x in v) and any("SYS_ADMIN" in x for x in v) and any("hostPort" in x for x in v)
+    assert violations(bad, "privileged") == []
+    assert any("runAsNonRoot" in x for x in violations({"spec": {"containers": [{"name": "c"}]}}, "restricted"))

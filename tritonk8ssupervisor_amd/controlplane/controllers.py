@@ -121,6 +121,7 @@ class Controllers:
         spec.setdefault("restartPolicy", "Always")
         try:
             self._resolve_priority(pid, spec)
+            self._pod_security(pid, ns, name, pod)
             self._admit_limit_ranges(pid, ns, name, pod)
         except HttpError as e:  # as the ReplicaSet controller's FailedCreate: nothing is created
             self._event(pid, ns, {"kind": owner_kind, "name": owner["metadata"]["name"]}, "FailedCreate",

@@ -117,10 +117,19 @@ class KubernetesAPI:
     def _guarded(self, h):
         async def g(req: Request, **kw):
             self._authorize(req, kw.get("pid"))
-            from .webhooks import CALLER
+            from .webhooks import CALLER, WARNINGS
 
             CALLER.set((kw.get("pid"), req.bearer))  # who asked, for admission webhooks' userInfo
-            return await h(req, **kw)
+            warnings: list[str] = []
+            WARNINGS.set(warnings)
+            res = await h(req, **kw)
+            if warnings:  # admission warnings (webhooks, PodSecurity warn) as Warning headers
+                hdr = ", ".join('299 - "%s"' % w.replace('"', "'") for w in warnings)
+                if isinstance(res, Response):
+                    res.headers["Warning"] = ", ".join(x for x in (res.headers.get("Warning"), hdr) if x)
+                elif isinstance(res, (dict, list)):
+                    res = Response(200, res, headers={"Warning": hdr})
+            return res
         g.__name__ = getattr(h, "__name__", "handler")
         return g
 
@@ -922,6 +931,10 @@ class KubernetesAPI:
             if not spec.get("containers"):
                 raise HttpError(422, "spec.containers is required")
             self._resolve_priority(pid, spec)
+            from .webhooks import warn
+
+            for w in self._pod_security(pid, ns, name, body):
+                warn(w)
             self._admit_limit_ranges(pid, ns, name, body)
             self._admit_quota(pid, ns, name, body)
             spec.setdefault("restartPolicy", "Always")

@@ -57,6 +57,7 @@ from .metrics_api import MetricsAPI
 from .disruption import Disruption
 from .priority import Priority
 from .webhooks import AdmissionWebhooks
+from .podsecurity import PodSecurity
 from .store import Store, now_iso
 
 
@@ -75,7 +76,7 @@ def _group_doc(group: str, versions: list[str]) -> dict:
 
 
 class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Disruption,
-                   Priority, AdmissionWebhooks, Scheduler):
+                   Priority, AdmissionWebhooks, PodSecurity, Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port

@@ -28,6 +28,14 @@ from .objects import _key
 MUTATING = "mutatingwebhookconfigurations"
 VALIDATING = "validatingwebhookconfigurations"
 CALLER: contextvars.ContextVar = contextvars.ContextVar("tk8s_caller", default=None)  # (pid, bearer)
+# admission warnings of the current request (webhook warnings, PodSecurity warn level): Warning headers
+WARNINGS: contextvars.ContextVar = contextvars.ContextVar("tk8s_warnings", default=None)
+
+
+def warn(text: str) -> None:
+    w = WARNINGS.get()
+    if w is not None:
+        w.append(text)
 
 
 def _match_rule(rule: dict, op: str, group: str, version: str, resource: str, namespaced: bool) -> bool:
@@ -169,6 +177,8 @@ class AdmissionWebhooks:
                     if wh.get("failurePolicy", "Fail") == "Ignore":
                         continue
                     raise HttpError(500, f'Internal error occurred: failed calling webhook "{wh.get("name")}": {e}') from e
+                for w in resp.get("warnings") or []:
+                    warn(str(w))
                 if not resp.get("allowed"):
                     st = resp.get("status") or {}
                     code = int(st.get("code") or 403)
