@@ -109,3 +109,30 @@ def test_discovery_auth_events_explain_and_config(kc):
     rc, out, _ = kc("config", "view")
     assert rc == 0 and "REDACTED" in out
     assert kc("config", "get-contexts")[0] == 0
+
+
+def test_get_output_formats_sort_and_watch(kc):
+    import threading
+    import time as _time
+
+    for n, r in (("b", 3), ("a", 1), ("c", 2)):
+        kc.kube.post(kc.kube.k8s("/api/v1/namespaces/default/configmaps"), {
+            "apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": n, "labels": {"rank": str(r)}}, "data": {"r": str(r)}})
+    rc, out, _ = kc("get", "cm", "-o", "name")
+    assert rc == 0 and {"configmap/a", "configmap/b", "configmap/c"} <= set(out.split())
+    rc, out, _ = kc("get", "cm", "-l", "rank", "--sort-by=.data.r", "-o", "jsonpath={.items[*].metadata.name}")
+    assert out.strip() == "a c b"
+    rc, out, _ = kc("get", "cm", "a", "-o", "jsonpath={.metadata.name}={.data.r}")
+    assert out.strip() == "a=1"
+    rc, out, _ = kc("get", "cm", "-l", "rank", "-o", "custom-columns=NAME:.metadata.name,RANK:.metadata.labels.rank",
+                    "--sort-by=.metadata.name")
+    lines = out.split("\n")
+    assert lines[0].split() == ["NAME", "RANK"] and lines[1].split() == ["a", "1"]
+    # -w: rows as the objects change, until --timeout
+    def later():
+        _time.sleep(0.5)
+        kc.kube.post(kc.kube.k8s("/api/v1/namespaces/default/configmaps"), {
+            "apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "late"}, "data": {}})
+    threading.Thread(target=later, daemon=True).start()
+    rc, out, _ = kc("get", "cm", "-w", "--timeout=2s")
+    assert rc == 0 and any(l.split()[:1] == ["late"] for l in out.splitlines()[-3:])

@@ -257,6 +257,73 @@ def _jsonpath(obj, expr: str):
     return cur
 
 
+def _jsonpath_all(obj, expr: str) -> list:
+    """Every value a JSONPath selects, ``[*]`` fanning out over list elements (or map values)."""
+    import re
+
+    cur = [obj]
+    for name, idx in re.findall(r"\.([^.\[\]]+)|\[(\*|-?\d+)\]", expr.strip().strip("{}")):
+        nxt = []
+        for x in cur:
+            if name:
+                if isinstance(x, dict) and name in x:
+                    nxt.append(x[name])
+            elif idx == "*":
+                nxt += list(x) if isinstance(x, list) else list(x.values()) if isinstance(x, dict) else []
+            elif isinstance(x, list) and -len(x) <= int(idx) < len(x):
+                nxt.append(x[int(idx)])
+        cur = nxt
+    return cur
+
+
+def _fmt_value(v) -> str:
+    return v if isinstance(v, str) else json.dumps(v, separators=(",", ":")) if isinstance(v, (dict, list)) else str(v)
+
+
+def render_jsonpath(obj, template: str) -> str:
+    """kubectl's ``-o jsonpath=TEMPLATE``: literal text with ``{...}`` expressions (values
+    joined by spaces)."""
+    import re
+
+    out, pos = [], 0
+    for m in re.finditer(r"\{([^{}]*)\}", template):
+        out.append(template[pos:m.start()].replace("\\n", "\n").replace("\\t", "\t"))
+        out.append(" ".join(_fmt_value(v) for v in _jsonpath_all(obj, m.group(1))))
+        pos = m.end()
+    out.append(template[pos:].replace("\\n", "\n").replace("\\t", "\t"))
+    return "".join(out)
+
+
+def render_custom_columns(items: list[dict], spec: str) -> str:
+    cols = [c.split(":", 1) for c in spec.split(",") if c]
+    rows = [[h for h, _ in cols]] + [[",".join(_fmt_value(v) for v in _jsonpath_all(o, e)) or "<none>" for _h, e in cols]
+                                     for o in items]
+    return _table(rows)
+
+
+def _watch_rows(k, what: str, ns: str, name: str | None, q: dict | None, a) -> int:
+    path = k.k8s("/api/v1/nodes" if what == "node" else "/api/v1/pods" if what == "pod" and a.all_namespaces
+                 else collection_path(what, ns))
+    query = dict(q or {})
+    if name:
+        query["fieldSelector"] = f"metadata.name={name}"
+    rv = int(k.get(path, query=query)["metadata"]["resourceVersion"])
+    deadline = time.monotonic() + float(a.timeout.rstrip("s"))
+    try:
+        while time.monotonic() < deadline:
+            rv, events = k.watch(path, rv, timeout=min(5.0, max(0.1, deadline - time.monotonic())), query=query)
+            for ev in events:
+                o = ev["object"]
+                if ev["type"] == "DELETED" and what == "pod":
+                    o = {**o, "metadata": {**o["metadata"], "deletionTimestamp": o["metadata"].get("deletionTimestamp") or "-"}}
+                table = (fmt_pods([o], a.output == "wide", a.all_namespaces) if what == "pod" else
+                         fmt_nodes([o], a.output == "wide") if what == "node" else fmt_generic(what, [o], a.all_namespaces))
+                print(table.splitlines()[-1], flush=True)
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
 def _wait_met(obj: dict | None, cond: str) -> bool:
     if cond == "delete":
         return obj is None
@@ -619,6 +686,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--subresource")
     ap.add_argument("--cascade", choices=["background", "foreground", "orphan"])
     ap.add_argument("--grace-period", type=int)
+    ap.add_argument("--sort-by")
+    ap.add_argument("-w", "--watch", action="store_true")
     ap.add_argument("--wait", choices=["true", "false"], default="true")
     ap.add_argument("verb")
     ap.add_argument("args", nargs="*")
@@ -678,14 +747,30 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 items = k.get(k.k8s(path), query=q)["items"]
             else:
                 items = k.get(k.k8s(collection_path(what, ns)), query=q)["items"]
-            if a.output in ("json", "yaml"):
-                _print({"apiVersion": "v1", "kind": "List", "items": items}, a.output, a.show_managed_fields)
+            if a.sort_by:
+                def key(o):
+                    v = (_jsonpath_all(o, a.sort_by) or [""])[0]
+                    return (0, float(v), "") if isinstance(v, (int, float)) else (1, 0.0, _fmt_value(v))
+                items.sort(key=key)
+            out = (a.output or "")
+            if out in ("json", "yaml"):
+                _print({"apiVersion": "v1", "kind": "List", "items": items} if not name else items[0], a.output,
+                       a.show_managed_fields)
+            elif out == "name":
+                print("\n".join(f"{what}/{o['metadata']['name']}" for o in items))
+            elif out.startswith("jsonpath="):
+                print(render_jsonpath({"apiVersion": "v1", "kind": "List", "items": items} if not name else items[0],
+                                      out[len("jsonpath="):]))
+            elif out.startswith("custom-columns="):
+                print(render_custom_columns(items, out[len("custom-columns="):]))
             elif what == "node":
                 print(fmt_nodes(items, a.output == "wide"))
             elif what == "pod":
                 print(fmt_pods(items, a.output == "wide", a.all_namespaces))
             else:
                 print(fmt_generic(what, items, a.all_namespaces))
+            if a.watch:  # -w: a row per change until --timeout (kubectl runs until interrupted)
+                return _watch_rows(k, what, ns, name, q, a)
         elif a.verb == "describe":
             what, name = kind_key(a.args[0]), a.args[1]
             o = k.get(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns)))
