@@ -895,3 +895,16 @@ def test_pod_security_standards_unit():
     assert any("privileged" in x for x in v) and any("SYS_ADMIN" in x for x in v) and any("hostPort" in x for x in v)
     assert violations(bad, "privileged") == []
     assert any("runAsNonRoot" in x for x in violations({"spec": {"containers": [{"name": "c"}]}}, "restricted"))
+
+
+def test_evicted_pod_carries_a_disruption_target(cp):
+    import time as _time
+
+    _nodes(cp, 1)
+    cp.leases[_key("1a1", "kubenode1")] = _time.monotonic()
+    cp.create("1a1", "pods", "default", {"metadata": {"name": "p"}, "spec": {"containers": [{"name": "c", "command": ["x"]}]}})
+    cp.store.patch("pods", _key("1a1", "default", "p"), lambda o: o["status"].update(phase="Running"))
+    cp.evict("1a1", "default", "p")
+    p = cp.store.get("pods", _key("1a1", "default", "p"))
+    dt = [c for c in p["status"]["conditions"] if c["type"] == "DisruptionTarget"]
+    assert p["metadata"]["deletionTimestamp"] and dt and dt[0]["reason"] == "EvictionByEvictionAPI"

@@ -137,14 +137,17 @@ class Controllers:
                         f"Error creating: pods \"{name}\" is forbidden: {why}", "Warning")
         return self.store.put("pods", _key(pid, ns, name), pod)
 
-    def _delete_pod(self, pid: str, ns: str, name: str, grace: float | None = None, force: bool = False) -> dict | None:
+    def _delete_pod(self, pid: str, ns: str, name: str, grace: float | None = None, force: bool = False,
+                    disruption: str | None = None) -> dict | None:
         """Delete a pod gracefully, as the API server does: a pod running on a node whose agent is
         alive gets ``metadata.deletionTimestamp`` (now + grace, ``terminationGracePeriodSeconds``
         by default) and stays, Terminating, until that agent has stopped it (preStop hook, SIGTERM,
         SIGKILL at the deadline) and confirms with a forced delete; controllers stop counting it at
         once and the scheduler keeps counting its GPUs. Any other pod -- not started, finished, on
         a node no agent answers for -- or ``force``/``grace == 0`` goes at once. The lease loop
-        force-deletes a Terminating pod whose agent never confirmed (``_pod_gc``)."""
+        force-deletes a Terminating pod whose agent never confirmed (``_pod_gc``). ``disruption``:
+        the ``DisruptionTarget`` condition's reason (EvictionByEvictionAPI, PreemptionByScheduler,
+        DeletionByTaintManager), what a Job's podFailurePolicy ``onPodConditions`` can match."""
         key = _key(pid, ns, name)
         pod = self.store.get("pods", key)
         if pod is None:
@@ -162,6 +165,8 @@ class Controllers:
         def mark(o):
             o["metadata"]["deletionTimestamp"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(time.time() + grace))
             o["metadata"]["deletionGracePeriodSeconds"] = int(grace)
+            if disruption:
+                _set_cond(o, "DisruptionTarget", "True", disruption, "the pod is being deleted for a disruption")
         self._again = True  # controllers replace it now
         return self.store.patch("pods", key, mark)
 

@@ -144,7 +144,7 @@ class Disruption:
                 "disruptedPods", {}).__setitem__(name, now_iso()))
         if dry_run:
             return
-        self._delete_pod(pid, ns, name)
+        self._delete_pod(pid, ns, name, disruption="EvictionByEvictionAPI")
         self._event(pid, ns, {"kind": "Pod", "name": name}, "Evicted", "Evicted through the eviction API", "Normal")
         self.reconcile()
 

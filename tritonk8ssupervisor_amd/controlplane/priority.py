@@ -106,7 +106,7 @@ class Priority:
         ns, name = pod["metadata"]["namespace"], pod["metadata"]["name"]
         for o in victims:
             vns, vname = o["metadata"]["namespace"], o["metadata"]["name"]
-            self._delete_pod(pid, vns, vname)  # (its GPUs: the agent starts the preemptor once they are free)
+            self._delete_pod(pid, vns, vname, disruption="PreemptionByScheduler")  # (its GPUs: the agent starts the preemptor once they are free)
             used[nn] = used.get(nn, 0) - pod_gpus(o)
             self._event(pid, vns, {"kind": "Pod", "name": vname}, "Preempted",
                         f"Preempted by pod {ns}/{name} (priority {priority(pod)}) on node {nn}", "Normal")

@@ -456,7 +456,7 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
                         added = now
                     if not tols or now - added >= min(float(s) for s in secs):
                         ns, name = pod["metadata"].get("namespace", "default"), pod["metadata"]["name"]
-                        self._delete_pod(pid, ns, name)
+                        self._delete_pod(pid, ns, name, disruption="DeletionByTaintManager")
                         self._event(pid, ns, {"kind": "Pod", "name": name}, "TaintManagerEviction",
                                     f"Marking for deletion Pod {ns}/{name}: node {nn} has taint {t.get('key')}:NoExecute",
                                     "Warning")
