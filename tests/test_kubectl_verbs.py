@@ -136,3 +136,13 @@ def test_get_output_formats_sort_and_watch(kc):
     threading.Thread(target=later, daemon=True).start()
     rc, out, _ = kc("get", "cm", "-w", "--timeout=2s")
     assert rc == 0 and any(l.split()[:1] == ["late"] for l in out.splitlines()[-3:])
+
+
+def test_describe_node_and_pod(kc):
+    rc, out, _ = kc("describe", "node", "kubenode1")
+    assert rc == 0 and "Taints:       <none>" in out and "Allocated resources:" in out and "amd.com/gpu: 0 of" in out
+    assert kc("taint", "nodes", "kubenode1", "gpu=mi355x:NoSchedule")[0] == 0
+    assert "gpu=mi355x:NoSchedule" in kc("describe", "no/kubenode1")[1]
+    kc("run", "d", "--image=python", "--", "sleep", "5")
+    rc, out, _ = kc("describe", "pod/d")
+    assert rc == 0 and "Name:         d" in out and "Status:" in out

@@ -772,7 +772,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             if a.watch:  # -w: a row per change until --timeout (kubectl runs until interrupted)
                 return _watch_rows(k, what, ns, name, q, a)
         elif a.verb == "describe":
-            what, name = kind_key(a.args[0]), a.args[1]
+            what, name = _target(a.args)
+            what = kind_key(what)
             o = k.get(k.k8s(f"/api/v1/nodes/{name}" if what == "node" else object_path(what, name, ns)))
             print(f"Name:         {o['metadata']['name']}")
             print(f"Labels:       {', '.join(f'{x}={y}' for x, y in o['metadata'].get('labels', {}).items())}")
@@ -782,10 +783,27 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 print("Capacity:\n" + "\n".join(f"  {x}: {y}" for x, y in st.get("capacity", {}).items()))
                 print("Allocatable:\n" + "\n".join(f"  {x}: {y}" for x, y in st.get("allocatable", {}).items()))
                 print("Devices:\n" + "\n".join(_device_line(d) for d in st.get("devices", [])))
+                taints = (o.get("spec") or {}).get("taints") or []
+                print("Taints:       " + (", ".join(f"{t['key']}{'=' + str(t['value']) if t.get('value') else ''}:{t['effect']}"
+                                                   for t in taints) or "<none>"))
+                print(f"Unschedulable: {str(bool((o.get('spec') or {}).get('unschedulable'))).lower()}")
+                pods = [p for p in k.get(k.k8s("/api/v1/pods"), query={"fieldSelector": f"spec.nodeName={name}"})["items"]
+                        if p.get("status", {}).get("phase") not in ("Succeeded", "Failed")]
+                used = sum(int(((c.get("resources") or {}).get("limits") or {}).get(GPU, 0) or 0)
+                           for p in pods for c in p["spec"].get("containers", []))
+                print(f"Non-terminated Pods: ({len(pods)} in total)\n"
+                      + "".join(f"  {p['metadata'].get('namespace', 'default'):<14} {p['metadata']['name']}\n" for p in pods)
+                      + f"Allocated resources:\n  {GPU}: {used} of {st.get('allocatable', {}).get(GPU, '0')}")
             print("Conditions:\n" + "\n".join(f"  {c['type']:<18} {c['status']:<8} {c.get('reason', '')}  {c.get('message', '')}"
                                               for c in st.get("conditions", [])))
             if what == "pod":
-                print(f"Node:         {o['spec'].get('nodeName')}\nStatus:       {st.get('phase')}")
+                status = st.get("phase")
+                if o["metadata"].get("deletionTimestamp"):
+                    status = (f"Terminating (lasts until {o['metadata']['deletionTimestamp']}, grace period "
+                              f"{o['metadata'].get('deletionGracePeriodSeconds', '?')}s)")
+                print(f"Node:         {o['spec'].get('nodeName')}\nStatus:       {status}")
+                if o["spec"].get("priorityClassName") or o["spec"].get("priority"):
+                    print(f"Priority:     {o['spec'].get('priority', 0)} ({o['spec'].get('priorityClassName', '')})")
                 vols = o["spec"].get("volumes") or []
                 if vols:
                     print("Volumes:\n" + "\n".join(f"  {v.get('name')}: {next((k for k in v if k != 'name'), '?')}"
