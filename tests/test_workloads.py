@@ -908,3 +908,25 @@ def test_evicted_pod_carries_a_disruption_target(cp):
     p = cp.store.get("pods", _key("1a1", "default", "p"))
     dt = [c for c in p["status"]["conditions"] if c["type"] == "DisruptionTarget"]
     assert p["metadata"]["deletionTimestamp"] and dt and dt[0]["reason"] == "EvictionByEvictionAPI"
+
+
+def test_lease_loop_forgives_its_own_stalls(cp):
+    """A stalled event loop (a slow webhook) must not mark heartbeating nodes lost."""
+    import asyncio
+    import time as _time
+
+    _nodes(cp, 1)
+    key = _key("1a1", "kubenode1")
+
+    async def run():
+        cp.leases[key] = _time.monotonic()
+        task = asyncio.ensure_future(cp.lease_loop())
+        await asyncio.sleep(0.3)
+        _time.sleep(cp.node_grace + 1)  # the loop is blocked longer than the grace period
+        cp.leases[key] = cp.leases[key]  # (no heartbeat got through meanwhile)
+        await asyncio.sleep(0.6)
+        task.cancel()
+
+    asyncio.run(run())
+    n = cp.store.get("nodes", key)
+    assert [c["status"] for c in n["status"]["conditions"] if c["type"] == "Ready"] == ["True"]

@@ -374,9 +374,18 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
 
     # ---- node lifecycle ---------------------------------------------------------------
     async def lease_loop(self) -> None:
+        period = min(0.25, self.node_grace / 4)
+        last = time.monotonic()
         while True:
-            await asyncio.sleep(min(0.25, self.node_grace / 4))
+            await asyncio.sleep(period)
             now = time.monotonic()
+            stall = now - last - period
+            last = now
+            if stall > 0.5:
+                # this event loop did not run for a while (a slow admission webhook, a GC pause): the
+                # heartbeats that came meanwhile are still queued, so the stall counts for no node
+                for key in list(self.leases):
+                    self.leases[key] += stall
             changed = False
             for key, t in list(self.leases.items()):
                 if now - t > self.node_grace:

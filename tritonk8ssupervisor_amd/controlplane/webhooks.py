@@ -16,6 +16,10 @@ requests go only to ``sideEffects: None|NoneOnDryRun`` webhooks.
 behind the Service (its Endpoints) and called directly -- not through the Service proxy, which
 runs on this server's own event loop. HTTPS verifies the server against ``caBundle`` (the host
 name is not checked when a pod is called by its IP).
+
+The call is made on the control plane's event loop, so a webhook holds every other request for
+as long as it takes (``timeoutSeconds``): keep webhooks fast. The node lease loop forgives such a
+stall (server.lease_loop), so a slow webhook cannot mark heartbeating nodes lost.
 """
 from __future__ import annotations
 
