@@ -354,6 +354,11 @@ def test_statefulset_cronjob_and_port_forward_on_a_real_cluster(cluster):
         s.sendto(dns.query("web-0.web.default.svc.cluster.local"), (ip, host_port(53)))
         assert dns.parse_reply(s.recv(512)) == (0, [p0])
     assert "web" in kc("get", "sts").stdout
+    assert "roll out complete" in kc("rollout", "status", "sts/web", "--timeout", "30s").stdout
+    kc("rollout", "restart", "sts/web")  # a new template: the ordinals are replaced, highest first
+    out = kc("rollout", "status", "sts/web", "--timeout", "60s").stdout
+    assert "roll out complete" in out
+    assert "roll out complete" in kc("rollout", "status", "sts/web").stdout
     # a CronJob's Jobs run to completion
     _until(lambda: any(j.get("status", {}).get("succeeded") for j in json.loads(kc("get", "jobs", "-o", "json").stdout)["items"]
                        if j["metadata"]["name"].startswith("tick-")), 30)

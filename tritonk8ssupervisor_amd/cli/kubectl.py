@@ -378,6 +378,44 @@ def _wait(k, ns: str, args: list[str], cond: str, selector: str | None, timeout:
     return rc
 
 
+def _rollout_other(k, kind: str, name: str, ns: str, sub: str, timeout: float) -> int:
+    """rollout status|restart of a StatefulSet (and status of a DaemonSet)."""
+    path = k.k8s(object_path(kind, name, ns))
+    if sub == "restart":
+        if kind != "statefulset":
+            raise SystemExit("error: rollout restart is served for Deployments and StatefulSets")
+        k.request("PATCH", path, body={"spec": {"template": {"metadata": {"annotations": {
+            "kubectl.kubernetes.io/restartedAt": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}}}}})
+        print(f"statefulset.apps/{name} restarted")
+        return 0
+    deadline = time.monotonic() + timeout
+    last = None
+    while True:
+        o = k.get(path)
+        st = o.get("status") or {}
+        if kind == "statefulset":
+            want = int(o["spec"].get("replicas", 1))
+            have, upd = int(st.get("readyReplicas", 0)), int(st.get("updatedReplicas", 0))
+            done = have == want and upd == want and st.get("currentRevision") == st.get("updateRevision")
+            msg = f"Waiting for {want - have} pods to be ready..." if have < want else \
+                f"Waiting for partitioned roll out to finish: {upd} out of {want} new pods have been updated..."
+        else:
+            want, have = int(st.get("desiredNumberScheduled", 0)), int(st.get("numberReady", 0))
+            done = have == want
+            msg = f'Waiting for daemon set "{name}" rollout to finish: {have} of {want} updated pods are available...'
+        if done:
+            print(f"partitioned roll out complete: {want} new pods have been updated..." if kind == "statefulset"
+                  else f'daemon set "{name}" successfully rolled out')
+            return 0
+        if msg != last:
+            print(msg, flush=True)
+            last = msg
+        if time.monotonic() > deadline:
+            print(f"error: timed out waiting for the condition", file=sys.stderr)
+            return 1
+        time.sleep(0.2)
+
+
 def _manifests(a) -> list[dict]:
     """The objects of ``-f FILE`` or ``-k DIR`` (a kustomization, kustomize.py)."""
     if a.kustomize:
@@ -854,6 +892,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
         elif a.verb == "rollout":
             sub = a.args[0] if a.args else ""
             what, name = _target(a.args[1:])
+            if kind_key(what) in ("statefulset", "daemonset") and sub in ("status", "restart"):
+                return _rollout_other(k, kind_key(what), name, ns, sub, float(a.timeout.rstrip("s")))
             if kind_key(what) != "deployment" or sub not in ("status", "restart", "history", "undo", "pause", "resume"):
                 raise SystemExit("usage: kubectl rollout status|restart|history|undo|pause|resume deploy/NAME")
             if sub in ("pause", "resume"):
