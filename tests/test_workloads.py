@@ -930,3 +930,26 @@ def test_lease_loop_forgives_its_own_stalls(cp):
     asyncio.run(run())
     n = cp.store.get("nodes", key)
     assert [c["status"] for c in n["status"]["conditions"] if c["type"] == "Ready"] == ["True"]
+
+
+def test_topology_spread_constraints(cp):
+    _nodes(cp, 3)  # zone a: kubenode1, kubenode2; zone b: kubenode3
+    spread = [{"maxSkew": 1, "topologyKey": "zone", "whenUnsatisfiable": "DoNotSchedule",
+               "labelSelector": {"matchLabels": {"app": "web"}}}]
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "web"}, "spec": {
+        "replicas": 4, "selector": {"matchLabels": {"app": "web"}}, "template": {
+            "metadata": {"labels": {"app": "web"}}, "spec": {"topologySpreadConstraints": spread,
+                                                              "containers": [{"name": "c", "command": ["x"]}]}}}})
+    zones = {}
+    for n in _pods(cp, "web"):
+        nn = _node_of(cp, n)
+        zones[nn] = zones.get(nn, 0) + 1
+    per_zone = {"a": zones.get("kubenode1", 0) + zones.get("kubenode2", 0), "b": zones.get("kubenode3", 0)}
+    assert per_zone == {"a": 2, "b": 2}  # skew <= 1 across the two zones
+    # ScheduleAnyway only prefers: hostname spread over three nodes
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "soft"}, "spec": {
+        "replicas": 3, "selector": {"matchLabels": {"app": "soft"}}, "template": {
+            "metadata": {"labels": {"app": "soft"}}, "spec": {"topologySpreadConstraints": [
+                {"maxSkew": 1, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "ScheduleAnyway",
+                 "labelSelector": {"matchLabels": {"app": "soft"}}}], "containers": [{"name": "c", "command": ["x"]}]}}}})
+    assert sorted(_node_of(cp, n) for n in _pods(cp, "soft")) == ["kubenode1", "kubenode2", "kubenode3"]

@@ -11,6 +11,11 @@
   domain; preferred terms add or subtract their weight. Anti-affinity on
   ``kubernetes.io/hostname`` is how a job spreads one rank per MI355X node.
 
+* **topology spread** -- ``topologySpreadConstraints`` (``maxSkew``, ``topologyKey``,
+  ``labelSelector``, ``whenUnsatisfiable``): ``DoNotSchedule`` keeps a pod out of a domain that
+  would then hold more than ``maxSkew`` matching pods above the emptiest eligible domain;
+  ``ScheduleAnyway`` prefers the domains with fewer matching pods.
+
 The scheduler keeps its GPU-packing order and uses these scores first (higher is better).
 """
 from __future__ import annotations
@@ -101,6 +106,41 @@ def _domain_has(term: dict, pod: dict, node: dict, nodes_by_name: dict, bound: l
     return False
 
 
+def _domain(node: dict, key: str) -> str | None:
+    labels = node["metadata"].get("labels") or {}
+    return labels.get(key, node["metadata"]["name"] if key == "kubernetes.io/hostname" else None)
+
+
+def _spread_counts(pod: dict, c: dict, nodes_by_name: dict, bound: list[dict]) -> dict[str, int]:
+    """Matching pods per topology domain of the eligible nodes (every domain listed, 0 if empty)."""
+    key = c.get("topologyKey") or "kubernetes.io/hostname"
+    ns = pod["metadata"].get("namespace", "default")
+    counts = {d: 0 for d in (_domain(n, key) for n in nodes_by_name.values()) if d is not None}
+    for o in bound:
+        if o is pod or o["metadata"].get("namespace", "default") != ns:
+            continue
+        if not selector_matches(c.get("labelSelector"), o["metadata"].get("labels")):
+            continue
+        n = nodes_by_name.get(o["spec"].get("nodeName"))
+        d = _domain(n, key) if n is not None else None
+        if d is not None:
+            counts[d] = counts.get(d, 0) + 1
+    return counts
+
+
+def _spread_ok(pod: dict, node: dict, nodes_by_name: dict, bound: list[dict]) -> bool:
+    for c in pod["spec"].get("topologySpreadConstraints") or []:
+        if c.get("whenUnsatisfiable", "DoNotSchedule") != "DoNotSchedule":
+            continue
+        counts = _spread_counts(pod, c, nodes_by_name, bound)
+        d = _domain(node, c.get("topologyKey") or "kubernetes.io/hostname")
+        if d is None or not counts:
+            return False  # a node without the key is not a place for this pod
+        if counts.get(d, 0) + 1 - min(counts.values()) > int(c.get("maxSkew", 1)):
+            return False
+    return True
+
+
 def feasible(pod: dict, node: dict, nodes_by_name: dict, bound: list[dict]) -> str | None:
     """None if ``pod`` may go to ``node``, else why not."""
     if not tolerates(pod, node):
@@ -116,6 +156,8 @@ def feasible(pod: dict, node: dict, nodes_by_name: dict, bound: list[dict]) -> s
     for _w, t in _pod_terms(pod, "podAntiAffinity", True):
         if _domain_has(t, pod, node, nodes_by_name, bound):
             return "pod anti-affinity"
+    if pod["spec"].get("topologySpreadConstraints") and not _spread_ok(pod, node, nodes_by_name, bound):
+        return "topology spread constraints"
     return None
 
 
@@ -132,4 +174,8 @@ def score(pod: dict, node: dict, nodes_by_name: dict, bound: list[dict]) -> int:
     if any(t.get("effect") == "PreferNoSchedule" and not any(_tolerates(x, t) for x in pod["spec"].get("tolerations") or [])
            for t in (node.get("spec") or {}).get("taints") or []):
         s -= 1000
+    for c in pod["spec"].get("topologySpreadConstraints") or []:
+        if c.get("whenUnsatisfiable") == "ScheduleAnyway":
+            d = _domain(node, c.get("topologyKey") or "kubernetes.io/hostname")
+            s -= 10 * _spread_counts(pod, c, nodes_by_name, bound).get(d, 0)
     return s

@@ -57,7 +57,8 @@ class Scheduler:
                     count[cn] = count.get(cn, 0) + 1
         # taints, node affinity, inter-pod (anti-)affinity (placement.py): only when something asks
         rules = any((n.get("spec") or {}).get("taints") for n in nodes) or any(
-            p["spec"].get("affinity") or p["spec"].get("tolerations") for p in pending)
+            p["spec"].get("affinity") or p["spec"].get("tolerations") or p["spec"].get("topologySpreadConstraints")
+            for p in pending)
         by_name = {n["metadata"]["name"]: n for n in nodes}
         bound = [o for o in self.store.list("pods", lambda o: self._in(pid, o))
                  if o["spec"].get("nodeName") and o.get("status", {}).get("phase") not in TERMINAL] if rules else []
