@@ -953,3 +953,22 @@ def test_topology_spread_constraints(cp):
                 {"maxSkew": 1, "topologyKey": "kubernetes.io/hostname", "whenUnsatisfiable": "ScheduleAnyway",
                  "labelSelector": {"matchLabels": {"app": "soft"}}}], "containers": [{"name": "c", "command": ["x"]}]}}}})
     assert sorted(_node_of(cp, n) for n in _pods(cp, "soft")) == ["kubenode1", "kubenode2", "kubenode3"]
+
+
+def test_persistent_volumes_and_storage_class(cp):
+    _nodes(cp, 2)
+    cp.create("1a1", "persistentvolumeclaims", "default", {"metadata": {"name": "data"}, "spec": {
+        "resources": {"requests": {"storage": "10Gi"}}}})
+    sc = cp.store.get("storageclasses", _key("1a1", "", "tk8s-local"))
+    assert sc["volumeBindingMode"] == "WaitForFirstConsumer"
+    pvc = cp.store.get("persistentvolumeclaims", _key("1a1", "default", "data"))
+    pv = cp.store.get("persistentvolumes", _key("1a1", "", pvc["spec"]["volumeName"]))
+    assert pv["spec"]["claimRef"]["name"] == "data" and pv["spec"]["capacity"]["storage"] == "10Gi"
+    assert "nodeAffinity" not in pv["spec"]
+    cp.create("1a1", "pods", "default", {"metadata": {"name": "user"}, "spec": {
+        "containers": [{"name": "c", "command": ["x"]}], "volumes": [{"name": "d", "persistentVolumeClaim": {"claimName": "data"}}]}})
+    node = _node_of(cp, "user")
+    pv = cp.store.get("persistentvolumes", _key("1a1", "", pvc["spec"]["volumeName"]))
+    assert pv["spec"]["nodeAffinity"]["required"]["nodeSelectorTerms"][0]["matchExpressions"][0]["values"] == [node]
+    cp._remove("1a1", "persistentvolumeclaims", "default", "data")
+    assert cp.store.get("persistentvolumes", _key("1a1", "", pvc["spec"]["volumeName"])) is None

@@ -57,6 +57,8 @@ _TOP = {"Pod": ("spec", "status"), "Service": ("spec", "status"), "Node": ("spec
         "Secret": ("data", "stringData", "type", "immutable"),
         "PriorityClass": ("value", "globalDefault", "description", "preemptionPolicy"),
         "MutatingWebhookConfiguration": ("webhooks",), "ValidatingWebhookConfiguration": ("webhooks",),
+        "StorageClass": ("provisioner", "parameters", "reclaimPolicy", "volumeBindingMode", "allowVolumeExpansion",
+                         "mountOptions", "allowedTopologies"),
         "Endpoints": ("subsets",),
         "Event": ("involvedObject", "reason", "message", "source", "firstTimestamp", "lastTimestamp", "count",
                   "type", "eventTime", "series", "action", "related", "reportingComponent",

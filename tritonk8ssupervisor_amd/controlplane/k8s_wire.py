@@ -31,6 +31,8 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "configmaps": ("", "v1", "ConfigMap", "configmap", True, ("cm",), ()),
     "secrets": ("", "v1", "Secret", "secret", True, (), ()),
     "persistentvolumeclaims": ("", "v1", "PersistentVolumeClaim", "persistentvolumeclaim", True, ("pvc",), ()),
+    "persistentvolumes": ("", "v1", "PersistentVolume", "persistentvolume", False, ("pv",), ()),
+    "storageclasses": ("storage.k8s.io", "v1", "StorageClass", "storageclass", False, ("sc",), ()),
     "namespaces": ("", "v1", "Namespace", "namespace", False, ("ns",), ()),
     "nodes": ("", "v1", "Node", "node", False, ("no",), ("status",)),
     "daemonsets": ("apps", "v1", "DaemonSet", "daemonset", True, ("ds",), ()),

@@ -116,8 +116,12 @@ class Scheduler:
             if rules:  # what the next pods of this pass see (anti-affinity spreads replicas at once)
                 bound.append({**pod, "spec": {**pod["spec"], "nodeName": nn}})
             for c in claims:  # WaitForFirstConsumer: the first pod's node holds the claim's data
-                self.store.patch("persistentvolumeclaims", _key(pid, pod["metadata"]["namespace"], c),
-                                 lambda o, nn=nn: o["metadata"].setdefault("annotations", {}).setdefault(SELECTED_NODE, nn))
+                ckey = _key(pid, pod["metadata"]["namespace"], c)
+                if SELECTED_NODE not in ((self.store.get("persistentvolumeclaims", ckey) or {}).get("metadata", {})
+                                         .get("annotations") or {}):
+                    pvc = self.store.patch("persistentvolumeclaims", ckey, lambda o, nn=nn: o["metadata"].setdefault(
+                        "annotations", {}).__setitem__(SELECTED_NODE, nn))
+                    self._provision_pv(pid, pod["metadata"]["namespace"], pvc, node=nn)
             self._bind(pid, pod, key, nn)
 
     def _pod_claims_nodes(self, pid: str, pod: dict) -> tuple[list[str], str | None, str | None]:

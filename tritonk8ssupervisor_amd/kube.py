@@ -37,6 +37,8 @@ KINDS = {
     "poddisruptionbudget": ("PodDisruptionBudget", "/apis/policy/v1", "poddisruptionbudgets"),
     "priorityclass": ("PriorityClass", "/apis/scheduling.k8s.io/v1", "priorityclasses"),
     "limitrange": ("LimitRange", "/api/v1", "limitranges"),
+    "persistentvolume": ("PersistentVolume", "/api/v1", "persistentvolumes"),
+    "storageclass": ("StorageClass", "/apis/storage.k8s.io/v1", "storageclasses"),
     "resourcequota": ("ResourceQuota", "/api/v1", "resourcequotas"),
     "mutatingwebhookconfiguration": ("MutatingWebhookConfiguration", "/apis/admissionregistration.k8s.io/v1",
                                      "mutatingwebhookconfigurations"),
@@ -56,11 +58,13 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "crds": "customresourcedefinition", "customresourcedefinitions": "customresourcedefinition",
            "pdb": "poddisruptionbudget", "poddisruptionbudgets": "poddisruptionbudget",
            "pc": "priorityclass", "priorityclasses": "priorityclass", "limits": "limitrange",
-           "limitranges": "limitrange", "quota": "resourcequota", "resourcequotas": "resourcequota"}
+           "limitranges": "limitrange", "quota": "resourcequota", "resourcequotas": "resourcequota",
+           "pv": "persistentvolume", "persistentvolumes": "persistentvolume", "sc": "storageclass",
+           "storageclasses": "storageclass"}
 
 
 CLUSTER_SCOPED: set[str] = {"customresourcedefinition", "priorityclass", "mutatingwebhookconfiguration",
-                             "validatingwebhookconfiguration"}  # (+ kinds learnt from discovery without a namespace)
+                             "validatingwebhookconfiguration", "persistentvolume", "storageclass"}  # (+ kinds learnt from discovery without a namespace)
 
 
 def learn_kind(k: Client, name: str) -> str | None:
