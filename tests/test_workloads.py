@@ -972,3 +972,22 @@ def test_persistent_volumes_and_storage_class(cp):
     assert pv["spec"]["nodeAffinity"]["required"]["nodeSelectorTerms"][0]["matchExpressions"][0]["values"] == [node]
     cp._remove("1a1", "persistentvolumeclaims", "default", "data")
     assert cp.store.get("persistentvolumes", _key("1a1", "", pvc["spec"]["volumeName"])) is None
+
+
+def test_scheduler_fits_cpu_and_memory_requests(cp):
+    _nodes(cp, 2)
+    for i in (1, 2):
+        cp.store.patch("nodes", _key("1a1", f"kubenode{i}"), lambda o: o["status"]["allocatable"].update(
+            cpu="2", memory="4Gi", pods="110"))
+    pod = lambda name, cpu, mem="1Gi": {"metadata": {"name": name}, "spec": {"containers": [
+        {"name": "c", "command": ["x"], "resources": {"requests": {"cpu": cpu, "memory": mem}}}]}}
+    cp.create("1a1", "pods", "default", pod("a", "1500m"))
+    cp.create("1a1", "pods", "default", pod("b", "1500m"))
+    assert {_node_of(cp, "a"), _node_of(cp, "b")} == {"kubenode1", "kubenode2"}  # one per node: 3 CPUs do not fit 2
+    cp.create("1a1", "pods", "default", pod("c", "1"))
+    p = cp.store.get("pods", _key("1a1", "default", "c"))
+    assert p["spec"].get("nodeName") is None and "Insufficient cpu" in p["status"]["conditions"][0]["message"]
+    cp.create("1a1", "pods", "default", pod("d", "100m", "8Gi"))
+    assert "Insufficient memory" in cp.store.get("pods", _key("1a1", "default", "d"))["status"]["conditions"][0]["message"]
+    cp.create("1a1", "pods", "default", pod("e", "100m"))  # small enough for either node
+    assert _node_of(cp, "e") is not None

@@ -49,12 +49,20 @@ class Scheduler:
                  if node_ready(n) and not n["spec"].get("unschedulable")]
         used: dict[str, int] = {}
         count: dict[str, int] = {}
+        reqs: dict[str, list[float]] = {}  # node -> [cpu, memory] requested by its pods
+        from .objects import pod_usage
+        from ..utils import quantity
+
         for o in self.store.list("pods", lambda o: self._in(pid, o)):
             nn = o["spec"].get("nodeName")
             if nn and o.get("status", {}).get("phase") not in TERMINAL:
                 for cn, g in pod_claims(o).items():
                     used[cn] = used.get(cn, 0) + g
                     count[cn] = count.get(cn, 0) + 1
+                u = pod_usage(o)
+                r = reqs.setdefault(nn, [0.0, 0.0])
+                r[0] += u.get("requests.cpu", 0.0)
+                r[1] += u.get("requests.memory", 0.0)
         # taints, node affinity, inter-pod (anti-)affinity (placement.py): only when something asks
         rules = any((n.get("spec") or {}).get("taints") for n in nodes) or any(
             p["spec"].get("affinity") or p["spec"].get("tolerations") or p["spec"].get("topologySpreadConstraints")
@@ -83,6 +91,7 @@ class Scheduler:
                 continue
             best = None
             why: dict[str, int] = {}
+            mine = pod_usage(pod)
             for n in nodes:
                 nn = n["metadata"]["name"]
                 free = int(n["status"]["allocatable"].get(GPU, 0)) - used.get(nn, 0)
@@ -90,6 +99,17 @@ class Scheduler:
                     continue
                 if need and not node_validated(n):
                     continue  # GPU pods only land on validated nodes
+                alloc = n["status"]["allocatable"]
+                short = next((res for i, res in enumerate(("cpu", "memory"))
+                              if alloc.get(res) and mine.get(f"requests.{res}", 0.0)
+                              and reqs.get(nn, [0.0, 0.0])[i] + mine[f"requests.{res}"] > quantity.parse(alloc[res]) + 1e-9),
+                             None)
+                if short is None and alloc.get("pods") and count.get(nn, 0) >= int(alloc["pods"]):
+                    short = "pods"
+                if short is not None:  # the pods' requests do not fit the node's allocatable cpu/memory/pods
+                    reason = "Too many pods" if short == "pods" else f"Insufficient {short}"
+                    why[reason] = why.get(reason, 0) + 1
+                    continue
                 pref = 0
                 if rules:
                     from . import placement
@@ -113,6 +133,9 @@ class Scheduler:
             nn = best[1]
             used[nn] = used.get(nn, 0) + need
             count[nn] = count.get(nn, 0) + 1
+            r = reqs.setdefault(nn, [0.0, 0.0])
+            r[0] += mine.get("requests.cpu", 0.0)
+            r[1] += mine.get("requests.memory", 0.0)
             if rules:  # what the next pods of this pass see (anti-affinity spreads replicas at once)
                 bound.append({**pod, "spec": {**pod["spec"], "nodeName": nn}})
             for c in claims:  # WaitForFirstConsumer: the first pod's node holds the claim's data
