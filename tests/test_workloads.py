@@ -991,3 +991,18 @@ def test_scheduler_fits_cpu_and_memory_requests(cp):
     assert "Insufficient memory" in cp.store.get("pods", _key("1a1", "default", "d"))["status"]["conditions"][0]["message"]
     cp.create("1a1", "pods", "default", pod("e", "100m"))  # small enough for either node
     assert _node_of(cp, "e") is not None
+
+
+def test_repeated_events_are_aggregated(cp):
+    import time as _time
+
+    for _ in range(50):  # a controller failing the same way on every pass
+        cp._event("1a1", "default", {"kind": "Job", "name": "j"}, "FailedCreate", "no room", "Warning")
+    evs = [e for e in cp.store.list("events") if e["reason"] == "FailedCreate"]
+    assert len(evs) == 1 and evs[0]["count"] == 1
+    _time.sleep(1.05)
+    cp._event("1a1", "default", {"kind": "Job", "name": "j"}, "FailedCreate", "no room", "Warning")
+    evs = [e for e in cp.store.list("events") if e["reason"] == "FailedCreate"]
+    assert len(evs) == 1 and evs[0]["count"] == 2
+    cp._event("1a1", "default", {"kind": "Job", "name": "j"}, "FailedCreate", "other reason", "Warning")
+    assert len([e for e in cp.store.list("events") if e["reason"] == "FailedCreate"]) == 2

@@ -137,6 +137,23 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
             if obj is not None:
                 involved.setdefault("uid", obj["metadata"].get("uid", ""))
         now = now_iso()
+        # the event correlator: the same event again (object, reason, message, type) bumps the
+        # count of the first one instead of adding another -- at most one write a second per event
+        # (a controller that fails the same way on every reconcile pass cannot flood the store)
+        agg = (project, ns, involved.get("kind"), involved.get("name"), involved.get("uid"), reason, message, etype)
+        index = self.__dict__.setdefault("_event_index", {})
+        hit = index.get(agg)
+        if hit is not None:
+            ekey, last = hit
+            if self.store.get("events", ekey) is not None:
+                if time.monotonic() - last >= 1.0:
+                    index[agg] = (ekey, time.monotonic())
+                    self.store.patch("events", ekey, lambda o: o.update(count=int(o.get("count", 1)) + 1,
+                                                                          lastTimestamp=now))
+                return
+        if len(index) > 10000:
+            index.clear()
+        index[agg] = (_key(project, ns, name), time.monotonic())
         self.store.put("events", _key(project, ns, name), {
             "kind": "Event", "metadata": {"name": name, "namespace": ns}, "_project": project,
             "involvedObject": involved, "reason": reason, "message": message, "type": etype,
