@@ -257,7 +257,7 @@ def test_config_env_ingress_dns_and_drain(cluster, tmp_path_factory):
     assert pods and all(p["spec"]["nodeName"] != node for p in pods if p["status"].get("phase") == "Running")
     assert "SchedulingDisabled" in kc("get", "nodes").stdout
     top = kc("top", "nodes").stdout
-    assert "GPU(USED/ALLOC)" in top and "kubenode1" in top
+    assert "GPU(USED/ALLOC)" in top and "kubenode1" in top and "CPU(cores)" in top
     kc("label", "node", node, "pool=mi355x")
     assert json.loads(kc("get", "node", node, "-o", "json").stdout)["metadata"]["labels"]["pool"] == "mi355x"
     kc("label", "node", node, "pool-")

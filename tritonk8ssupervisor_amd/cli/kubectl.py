@@ -592,22 +592,29 @@ def _create_data(k, a, ns: str) -> int:
     return 0
 
 
-def fmt_top(nodes: list[dict], pods: list[dict]) -> str:
-    """Per node: amd.com/gpu in use / allocatable and the last AMD SMI sample of its GPUs."""
+def fmt_top(nodes: list[dict], pods: list[dict], usage: dict | None = None) -> str:
+    """Per node: CPU and memory in use (metrics.k8s.io, when the agents have sampled), amd.com/gpu
+    in use / allocatable and the last AMD SMI sample of its GPUs."""
     used: dict[str, int] = {}
     for p in pods:
         nn = p["spec"].get("nodeName")
         if nn and p.get("status", {}).get("phase") not in ("Succeeded", "Failed"):
             used[nn] = used.get(nn, 0) + sum(int(c.get("resources", {}).get("limits", {}).get(GPU, 0) or 0)
                                              for c in p["spec"].get("containers", []))
-    rows = [["NAME", "GPU(USED/ALLOC)", "HOTSPOT-MAX", "POWER", "VRAM-USED"]]
+    from ..utils import quantity
+
+    usage = usage or {}
+    rows = [["NAME", "CPU(cores)", "MEMORY(bytes)", "GPU(USED/ALLOC)", "HOTSPOT-MAX", "POWER", "VRAM-USED"]]
     for n in nodes:
         tel = [d.get("telemetry") or {} for d in n["status"].get("devices", [])]
         hot = [t["temp_c"]["hotspot"] for t in tel if "hotspot" in t.get("temp_c", {})]
         watts = [t["power"]["current_w"] for t in tel if "current_w" in t.get("power", {})]
         vram = [t["vram_used_bytes"] for t in tel if "vram_used_bytes" in t]
         name = n["metadata"]["name"]
-        rows.append([name, f"{used.get(name, 0)}/{n['status']['allocatable'].get(GPU, '0')}",
+        u = usage.get(name) or {}
+        rows.append([name, f"{int(quantity.parse(u['cpu']) * 1000)}m" if u.get("cpu") else "<unknown>",
+                     f"{int(quantity.parse(u['memory']) / 2**20)}Mi" if u.get("memory") else "<unknown>",
+                     f"{used.get(name, 0)}/{n['status']['allocatable'].get(GPU, '0')}",
                      f"{max(hot)}C" if hot else "-", f"{sum(watts):.0f}W" if watts else "-",
                      f"{sum(vram) / 2**30:.1f}GiB" if vram else "-"])
     return _table(rows)
@@ -935,7 +942,12 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             if not a.args or kind_key(a.args[0]) not in ("node", "pod"):
                 raise SystemExit("usage: kubectl top nodes|pods")
             if kind_key(a.args[0]) == "node":
-                print(fmt_top(k.get(k.k8s("/api/v1/nodes"))["items"], k.get(k.k8s("/api/v1/pods"))["items"]))
+                try:
+                    usage = {m["metadata"]["name"]: m["usage"] for m in
+                             k.get(k.k8s("/apis/metrics.k8s.io/v1beta1/nodes"))["items"]}
+                except ApiError:
+                    usage = {}
+                print(fmt_top(k.get(k.k8s("/api/v1/nodes"))["items"], k.get(k.k8s("/api/v1/pods"))["items"], usage))
             else:  # the resource metrics API (metrics.k8s.io), as a stock kubectl top pods reads it
                 from ..utils import quantity
 
