@@ -1006,3 +1006,16 @@ def test_repeated_events_are_aggregated(cp):
     assert len(evs) == 1 and evs[0]["count"] == 2
     cp._event("1a1", "default", {"kind": "Job", "name": "j"}, "FailedCreate", "other reason", "Warning")
     assert len([e for e in cp.store.list("events") if e["reason"] == "FailedCreate"]) == 2
+
+
+def test_ingress_classes(cp):
+    cp.create("1a1", "services", "default", {"metadata": {"name": "web"}, "spec": {"ports": [{"port": 80}]}})
+    ing = lambda name, **spec: {"metadata": {"name": name}, "spec": {**spec, "rules": [{"host": f"{name}.local", "http": {
+        "paths": [{"path": "/", "pathType": "Prefix", "backend": {"service": {"name": "web", "port": {"number": 80}}}}]}}]}}
+    cp.create("1a1", "ingresses", "default", ing("plain"))
+    cp.create("1a1", "ingresses", "default", ing("mine", ingressClassName="tk8s"))
+    cp.create("1a1", "ingresses", "default", ing("theirs", ingressClassName="nginx"))
+    hosts = {r[0] for r in cp._ingress_routes()}
+    assert hosts == {"plain.local", "mine.local"}
+    ic = cp.store.get("ingressclasses", _key("1a1", "", "tk8s"))
+    assert ic["metadata"]["annotations"]["ingressclass.kubernetes.io/is-default-class"] == "true"

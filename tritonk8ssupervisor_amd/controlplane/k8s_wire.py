@@ -55,6 +55,7 @@ RESOURCES: dict[str, tuple[str, str, str, str, bool, tuple[str, ...], tuple[str,
     "customresourcedefinitions": ("apiextensions.k8s.io", "v1", "CustomResourceDefinition", "customresourcedefinition",
                                   False, ("crd", "crds"), ()),
     "ingresses": ("networking.k8s.io", "v1", "Ingress", "ingress", True, ("ing",), ()),
+    "ingressclasses": ("networking.k8s.io", "v1", "IngressClass", "ingressclass", False, (), ()),
     "poddisruptionbudgets": ("policy", "v1", "PodDisruptionBudget", "poddisruptionbudget", True, ("pdb",), ("status",)),
     "priorityclasses": ("scheduling.k8s.io", "v1", "PriorityClass", "priorityclass", False, ("pc",), ()),
     "mutatingwebhookconfigurations": ("admissionregistration.k8s.io", "v1", "MutatingWebhookConfiguration",

@@ -39,6 +39,7 @@ KINDS = {
     "limitrange": ("LimitRange", "/api/v1", "limitranges"),
     "persistentvolume": ("PersistentVolume", "/api/v1", "persistentvolumes"),
     "storageclass": ("StorageClass", "/apis/storage.k8s.io/v1", "storageclasses"),
+    "ingressclass": ("IngressClass", "/apis/networking.k8s.io/v1", "ingressclasses"),
     "resourcequota": ("ResourceQuota", "/api/v1", "resourcequotas"),
     "mutatingwebhookconfiguration": ("MutatingWebhookConfiguration", "/apis/admissionregistration.k8s.io/v1",
                                      "mutatingwebhookconfigurations"),
@@ -60,11 +61,11 @@ ALIASES = {"po": "pod", "pods": "pod", "svc": "service", "services": "service", 
            "pc": "priorityclass", "priorityclasses": "priorityclass", "limits": "limitrange",
            "limitranges": "limitrange", "quota": "resourcequota", "resourcequotas": "resourcequota",
            "pv": "persistentvolume", "persistentvolumes": "persistentvolume", "sc": "storageclass",
-           "storageclasses": "storageclass"}
+           "storageclasses": "storageclass", "ingressclasses": "ingressclass"}
 
 
 CLUSTER_SCOPED: set[str] = {"customresourcedefinition", "priorityclass", "mutatingwebhookconfiguration",
-                             "validatingwebhookconfiguration", "persistentvolume", "storageclass"}  # (+ kinds learnt from discovery without a namespace)
+                             "validatingwebhookconfiguration", "persistentvolume", "storageclass", "ingressclass"}  # (+ kinds learnt from discovery without a namespace)
 
 
 def learn_kind(k: Client, name: str) -> str | None:
