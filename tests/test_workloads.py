@@ -1019,3 +1019,16 @@ def test_ingress_classes(cp):
     assert hosts == {"plain.local", "mine.local"}
     ic = cp.store.get("ingressclasses", _key("1a1", "", "tk8s"))
     assert ic["metadata"]["annotations"]["ingressclass.kubernetes.io/is-default-class"] == "true"
+
+
+def test_hpa_rate_limit_policies():
+    from tritonk8ssupervisor_amd.controlplane.metrics_api import _rate_limit
+
+    assert _rate_limit({}, 2, 20) == 6  # default up: max(+100 % = 4, +4 pods = 6)
+    assert _rate_limit({}, 10, 1) == 1  # default down: up to 100 %
+    beh = {"scaleUp": {"policies": [{"type": "Pods", "value": 1, "periodSeconds": 60}]},
+           "scaleDown": {"policies": [{"type": "Percent", "value": 50, "periodSeconds": 60}]}}
+    assert _rate_limit(beh, 3, 10) == 4 and _rate_limit(beh, 10, 1) == 5
+    assert _rate_limit({"scaleDown": {"selectPolicy": "Disabled"}}, 10, 1) == 10
+    two = {"scaleUp": {"selectPolicy": "Min", "policies": [{"type": "Pods", "value": 2}, {"type": "Percent", "value": 10}]}}
+    assert _rate_limit(two, 10, 30) == 11  # the smaller of +2 and +10 %

@@ -37,6 +37,31 @@ def resource_list() -> dict:
         {"name": "pods", "singularName": "", "namespaced": True, "kind": "PodMetrics", "verbs": ["get", "list"]}]}
 
 
+def _rate_limit(behavior: dict, current: int, desired: int) -> int:
+    """The HPA's scaling policies: how far one step may go (``behavior.scaleUp|scaleDown``:
+    ``policies`` of ``Pods``/``Percent`` per ``periodSeconds``, ``selectPolicy`` Max|Min|Disabled).
+    Defaults as Kubernetes': up by max(100 %, 4 pods), down by up to 100 %."""
+    import math
+
+    up = desired > current
+    rules = behavior.get("scaleUp" if up else "scaleDown") or {}
+    if rules.get("selectPolicy") == "Disabled":
+        return current
+    pols = rules.get("policies") or ([{"type": "Percent", "value": 100}, {"type": "Pods", "value": 4}] if up
+                                     else [{"type": "Percent", "value": 100}])
+    limits = []
+    for p in pols:
+        v = int(p.get("value", 0))
+        step = v if p.get("type") == "Pods" else math.ceil(current * v / 100.0)
+        limits.append(current + step if up else max(0, current - step))
+    if not limits:
+        return desired
+    pick = (max if rules.get("selectPolicy", "Max") == "Max" else min) if up else \
+        (min if rules.get("selectPolicy", "Max") == "Max" else max)
+    bound = pick(limits)
+    return min(desired, bound) if up else max(desired, bound)
+
+
 class MetricsAPI:
     # ---- ingest ---------------------------------------------------------------------------
     def _ingest_metrics(self, pid: str, node: str, m: dict) -> None:
@@ -198,12 +223,19 @@ class MetricsAPI:
                 continue
             _set_cond(holder, "ScalingActive", "True", "ValidMetricFound", "the HPA was able to compute the replica count")
             desired = min(hi, max(lo, desired))
-            # scale-down stabilization: the highest recommendation of the window wins
-            window = float((((spec.get("behavior") or {}).get("scaleDown") or {}).get("stabilizationWindowSeconds", 300)))
-            recs = [(t, r) for t, r in self._hpa_recs.get((pid, ns, name), []) if now - t <= window] + [(now, desired)]
+            # stabilization: scaling down takes the highest recommendation of its window (300 s by
+            # default), scaling up the lowest of its own (0 s by default)
+            beh = spec.get("behavior") or {}
+            down_w = float((beh.get("scaleDown") or {}).get("stabilizationWindowSeconds", 300))
+            up_w = float((beh.get("scaleUp") or {}).get("stabilizationWindowSeconds", 0))
+            recs = [(t, r) for t, r in self._hpa_recs.get((pid, ns, name), []) if now - t <= max(down_w, up_w)]
+            recs.append((now, desired))
             self._hpa_recs[(pid, ns, name)] = recs
             if desired < current:
-                desired = min(current, max(r for _t, r in recs))
+                desired = min(current, max(r for t, r in recs if now - t <= down_w))
+            elif desired > current:
+                desired = max(current, min(r for t, r in recs if now - t <= up_w))
+            desired = min(hi, max(lo, _rate_limit(beh, current, desired)))
             status = {**st, "currentReplicas": current, "desiredReplicas": desired, "currentMetrics": current_metrics,
                       "conditions": conds["conditions"]}
             if desired != current:
