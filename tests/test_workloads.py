@@ -1032,3 +1032,26 @@ def test_hpa_rate_limit_policies():
     assert _rate_limit({"scaleDown": {"selectPolicy": "Disabled"}}, 10, 1) == 10
     two = {"scaleUp": {"selectPolicy": "Min", "policies": [{"type": "Pods", "value": 2}, {"type": "Percent", "value": 10}]}}
     assert _rate_limit(two, 10, 30) == 11  # the smaller of +2 and +10 %
+
+
+def test_daemonset_rolling_update(cp):
+    _nodes(cp, 3)
+    cp.create("1a1", "daemonsets", "default", {"metadata": {"name": "mon"}, "spec": {
+        "selector": {"matchLabels": {"app": "mon"}}, "template": {"metadata": {"labels": {"app": "mon"}},
+                                                                  "spec": {"containers": [{"name": "c", "command": ["v1"]}]}}}})
+    names = _pods(cp, "mon")
+    assert len(names) == 3
+    for n in names:
+        cp.store.patch("pods", _key("1a1", "default", n), lambda o: o["status"].update(phase="Running"))
+    body = json.loads(json.dumps(cp._strip(cp.store.get("daemonsets", _key("1a1", "default", "mon")))))
+    body["spec"]["template"]["spec"]["containers"][0]["command"] = ["v2"]
+    cp.replace("1a1", "daemonsets", "default", "mon", body)
+    cmds = lambda: sorted(cp.store.get("pods", _key("1a1", "default", n))["spec"]["containers"][0]["command"][0]
+                          for n in _pods(cp, "mon"))
+    assert cmds() == ["v1", "v1", "v2"]  # one node at a time (maxUnavailable 1)
+    for _ in range(3):
+        for n in _pods(cp, "mon"):
+            cp.store.patch("pods", _key("1a1", "default", n), lambda o: o["status"].update(phase="Running"))
+        cp.reconcile()
+    assert cmds() == ["v2", "v2", "v2"]
+    assert cp.store.get("daemonsets", _key("1a1", "default", "mon"))["status"]["updatedNumberScheduled"] == 3

@@ -184,15 +184,34 @@ class Controllers:
             pods = {o["spec"].get("nodeName"): o for o in self._owned(pid, ds)}
             eligible = [n for n in nodes if labels_match(sel, n["metadata"].get("labels"))
                         and not n["spec"].get("unschedulable")]
+            h = template_hash(tmpl)
             for n in eligible:
                 nn = n["metadata"]["name"]
                 if nn not in pods:
                     pods[nn] = self._new_pod(pid, ns, f"{ds['metadata']['name']}-{nn}", ds, "DaemonSet", tmpl, node=nn,
-                                             labels=ds["spec"].get("selector", {}).get("matchLabels"))
+                                             labels={**(ds["spec"].get("selector", {}).get("matchLabels") or {}),
+                                                     "controller-revision-hash": h})
+            # RollingUpdate (the default; OnDelete leaves it to the user): a changed template replaces
+            # the running pods node by node, at most maxUnavailable (1) at a time
+            upd = ds["spec"].get("updateStrategy") or {}
+            if upd.get("type", "RollingUpdate") == "RollingUpdate":
+                budget = int((upd.get("rollingUpdate") or {}).get("maxUnavailable", 1) or 1)
+                down = sum(1 for o in pods.values() if o["metadata"].get("deletionTimestamp")
+                           or o.get("status", {}).get("phase") == "Pending")
+                for nn, o in sorted(pods.items()):
+                    if down >= budget:
+                        break
+                    stale = (o["metadata"].get("labels") or {}).get("controller-revision-hash") not in (None, h)
+                    if stale and o.get("status", {}).get("phase") == "Running" and not o["metadata"].get("deletionTimestamp"):
+                        self._delete_pod(pid, ns, o["metadata"]["name"])
+                        self._again = True  # its node gets the new template's pod once it is gone
+                        down += 1
             phases = [o.get("status", {}).get("phase") for o in pods.values()]
             status = {"desiredNumberScheduled": len(eligible), "currentNumberScheduled": len(pods),
                       "numberReady": phases.count("Running") + phases.count("Succeeded"),
-                      "numberSucceeded": phases.count("Succeeded"), "numberFailed": phases.count("Failed")}
+                      "numberSucceeded": phases.count("Succeeded"), "numberFailed": phases.count("Failed"),
+                      "updatedNumberScheduled": sum(1 for o in pods.values() if (o["metadata"].get("labels") or {}).get(
+                          "controller-revision-hash") == h)}
             if ds.get("status") != status:
                 self.store.patch("daemonsets", _key(pid, ns, ds["metadata"]["name"]), lambda o, s=status: o.__setitem__("status", s))
 
