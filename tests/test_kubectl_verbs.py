@@ -146,3 +146,18 @@ def test_describe_node_and_pod(kc):
     kc("run", "d", "--image=python", "--", "sleep", "5")
     rc, out, _ = kc("describe", "pod/d")
     assert rc == 0 and "Name:         d" in out and "Status:" in out
+
+
+def test_create_job_from_a_cronjob(kc):
+    kc.kube.post(kc.kube.k8s("/apis/batch/v1/namespaces/default/cronjobs"), {
+        "apiVersion": "batch/v1", "kind": "CronJob", "metadata": {"name": "nightly"},
+        "spec": {"schedule": "0 3 * * *", "jobTemplate": {"metadata": {"labels": {"team": "ml"}}, "spec": {"template": {
+            "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "command": ["true"]}]}}}}}})
+    rc, out, _ = kc("create", "job", "now", "--from=cronjob/nightly")
+    assert rc == 0 and out == "job.batch/now created\n"
+    j = kc.kube.get(kc.kube.k8s("/apis/batch/v1/namespaces/default/jobs/now"))
+    assert j["metadata"]["labels"]["team"] == "ml"
+    assert j["metadata"]["annotations"]["cronjob.kubernetes.io/instantiate"] == "manual"
+    rc, out, _ = kc("create", "job", "once", "--image=python", "--", "echo", "hi")
+    assert rc == 0 and kc.kube.get(kc.kube.k8s("/apis/batch/v1/namespaces/default/jobs/once"))["spec"]["template"][
+        "spec"]["containers"][0]["command"] == ["echo", "hi"]

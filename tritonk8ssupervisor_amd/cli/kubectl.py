@@ -416,6 +416,33 @@ def _rollout_other(k, kind: str, name: str, ns: str, sub: str, timeout: float) -
         time.sleep(0.2)
 
 
+def _create_job(k, a, ns: str) -> int:
+    """kubectl create job NAME --image=IMG [-- CMD...] | --from=cronjob/CJ (run a CronJob now)."""
+    if len(a.args) < 2:
+        raise SystemExit("usage: kubectl create job NAME (--image=IMAGE [-- COMMAND...] | --from=cronjob/NAME)")
+    name = a.args[1]
+    if a.from_:
+        what, _, src = a.from_.partition("/")
+        if kind_key(what) != "cronjob":
+            raise SystemExit("error: --from must be cronjob/NAME")
+        cj = k.get(k.k8s(object_path("cronjob", src, ns)))
+        jt = cj["spec"].get("jobTemplate") or {}
+        body = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {
+            "name": name, "labels": dict((jt.get("metadata") or {}).get("labels") or {}),
+            "annotations": {**((jt.get("metadata") or {}).get("annotations") or {}), "cronjob.kubernetes.io/instantiate": "manual"},
+            "ownerReferences": [{"apiVersion": "batch/v1", "kind": "CronJob", "name": src, "uid": cj["metadata"]["uid"]}]},
+            "spec": jt.get("spec") or {}}
+    else:
+        if not a.image:
+            raise SystemExit("error: --image or --from is required")
+        c = {"name": name, "image": a.image, **({"command": list(a.command)} if a.command else {})}
+        body = {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": name},
+                "spec": {"template": {"spec": {"restartPolicy": "Never", "containers": [c]}}}}
+    k.post(k.k8s(collection_path("job", ns)), body)
+    print(f"job.batch/{name} created")
+    return 0
+
+
 def _manifests(a) -> list[dict]:
     """The objects of ``-f FILE`` or ``-k DIR`` (a kustomization, kustomize.py)."""
     if a.kustomize:
@@ -732,6 +759,7 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--cascade", choices=["background", "foreground", "orphan"])
     ap.add_argument("--grace-period", type=int)
     ap.add_argument("--sort-by")
+    ap.add_argument("--from", dest="from_")
     ap.add_argument("-w", "--watch", action="store_true")
     ap.add_argument("--wait", choices=["true", "false"], default="true")
     ap.add_argument("verb")
@@ -879,6 +907,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             print(f"namespace/{a.args[1]} created")
         elif a.verb == "create" and a.args and kind_key(a.args[0]) == "deployment":
             return _create_deployment(k, a, ns)
+        elif a.verb == "create" and a.args and kind_key(a.args[0]) == "job":
+            return _create_job(k, a, ns)
         elif a.verb == "expose":
             return _expose(k, a, ns)
         elif a.verb == "apply" and a.server_side:
