@@ -161,3 +161,11 @@ def test_create_job_from_a_cronjob(kc):
     rc, out, _ = kc("create", "job", "once", "--image=python", "--", "echo", "hi")
     assert rc == 0 and kc.kube.get(kc.kube.k8s("/apis/batch/v1/namespaces/default/jobs/once"))["spec"]["template"][
         "spec"]["containers"][0]["command"] == ["echo", "hi"]
+
+
+def test_get_all(kc):
+    kc("run", "solo", "--image=python", "--", "sleep", "5")
+    kc.kube.post(kc.kube.k8s("/api/v1/namespaces/default/services"), {
+        "apiVersion": "v1", "kind": "Service", "metadata": {"name": "front"}, "spec": {"ports": [{"port": 80}]}})
+    rc, out, _ = kc("get", "all")
+    assert rc == 0 and "pod/solo" in out and "service/front" in out

@@ -801,6 +801,24 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             return more_dispatch(k, a, ns, cfg)
         elif a.verb == "cluster-info":
             print(f"Kubernetes control plane is running at {k.base}{k.prefix}")
+        elif a.verb == "get" and a.args[:1] == ["all"]:
+            # the "all" category: every workload kind and Services, one table each (empty ones left out)
+            first = True
+            for kind in ("pod", "service", "daemonset", "deployment", "replicaset", "statefulset", "job", "cronjob",
+                         "horizontalpodautoscaler"):
+                path = ("/api/v1/pods" if kind == "pod" else collection_path(kind).replace("/namespaces/default", "")) \
+                    if a.all_namespaces else collection_path(kind, ns)
+                items = k.get(k.k8s(path), query={"labelSelector": a.selector} if a.selector else None)["items"]
+                if not items:
+                    continue
+                for o in items:
+                    o["metadata"] = {**o["metadata"], "name": f"{kind}/{o['metadata']['name']}"}
+                table = fmt_pods(items, a.output == "wide", a.all_namespaces) if kind == "pod" else \
+                    fmt_generic(kind, items, a.all_namespaces)
+                print(("" if first else "\n") + table)
+                first = False
+            if first:
+                print(f"No resources found in {ns} namespace.")
         elif a.verb == "get":
             what = kind_key(a.args[0]) if a.args else "pod"
             name = a.args[1] if len(a.args) > 1 else None
