@@ -184,7 +184,13 @@ class Controllers:
             pods = {o["spec"].get("nodeName"): o for o in self._owned(pid, ds)}
             eligible = [n for n in nodes if labels_match(sel, n["metadata"].get("labels"))
                         and not n["spec"].get("unschedulable")]
-            h = template_hash(tmpl)
+            hc = self.__dict__.setdefault("_ds_hash", {})  # (uid, resourceVersion) -> template hash
+            ck = (ds["metadata"].get("uid"), ds["metadata"].get("resourceVersion"))
+            h = hc.get(ck)
+            if h is None:
+                if len(hc) > 1000:
+                    hc.clear()
+                h = hc[ck] = template_hash(tmpl)
             for n in eligible:
                 nn = n["metadata"]["name"]
                 if nn not in pods:
