@@ -405,7 +405,7 @@ def test_readiness_and_liveness_probes_on_a_real_cluster(cluster):
     (ws / "probes.json").write_text(json.dumps({"apiVersion": "v1", "kind": "List", "items": [
         {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "slow", "labels": {"app": "slow"}},
          "spec": {"containers": [{"name": "c", "image": "busybox",
-                                  "command": ["sh", "-c", "sleep 1.5; touch marker; sleep 60"],
+                                  "command": ["sh", "-c", "sleep 4; touch marker; sleep 60"],
                                   "readinessProbe": {"exec": {"command": ["test", "-f", "marker"]}, "periodSeconds": 0.2,
                                                      "failureThreshold": 1}}]}},
         {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "sick"},
