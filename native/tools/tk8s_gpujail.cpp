@@ -1,7 +1,9 @@
-// tk8s-gpujail: run a pod's command so that it can open only the GPUs it was allocated.
+// tk8s-gpujail: run a pod's command so that it can open only the GPUs it was allocated, and none
+// of the node's credentials.
 //
 //   tk8s-gpujail [--allow-render M]... [--dri-root DIR] [--hide-topology [--allow-node N]...
-//                [--kfd-root DIR]] [--best-effort] -- CMD ARGS...
+//                [--kfd-root DIR]] [--deny PATH]... [--allow PATH]... [--scope-signals]
+//                [--best-effort] -- CMD ARGS...
 //   tk8s-gpujail --probe            (prints {"landlock_abi": N, ...}; exit 0 when usable)
 //
 // The reference ran every workload in a Docker container (ansible/roles/rancherhost/tasks/
@@ -9,8 +11,9 @@
 // open. tk8s process pods are children of the node agent, and HIP_VISIBLE_DEVICES alone is
 // advice a pod can clear. This jail makes it a kernel rule with no privilege (the node agent and
 // the GPU tier run as an ordinary user; user namespaces are off on the GPU hosts): Landlock
-// denies opening the render nodes of every GPU the pod does not hold (gpujail.h has the policy
-// and why it is the render nodes). Image pods get the same jail inside tk8s-container.
+// denies opening the render nodes of every GPU the pod does not hold, and the --deny paths (the
+// node's state: kubeconfig, keys, other pods' tokens) but the --allow paths beneath them
+// (gpujail.h has the policy). Image pods get the same jail inside tk8s-container.
 //
 // The child's environment gets TK8S_GPU_ISOLATION=landlock:abi<N>:denied=<k> (or none:<why>
 // under --best-effort when Landlock is unavailable; without --best-effort that is exit 125).
@@ -23,7 +26,8 @@ namespace {
 int usage() {
   std::fprintf(stderr,
                "usage: tk8s-gpujail [--allow-render M]... [--dri-root DIR] [--hide-topology [--allow-node N]...\n"
-               "                    [--kfd-root DIR]] [--best-effort] -- CMD ARGS...\n       tk8s-gpujail --probe\n");
+               "                    [--kfd-root DIR]] [--deny PATH]... [--allow PATH]... [--scope-signals]\n"
+               "                    [--best-effort] -- CMD ARGS...\n       tk8s-gpujail --probe\n");
   return 2;
 }
 
@@ -52,7 +56,8 @@ int main(int argc, char** argv) {
   if (probe) {
     const int abi = tk8s::jail::abi();
     const std::string err = abi > 0 ? "" : std::string(", \"error\": \"") + std::strerror(-abi) + "\"";
-    std::printf("{\"landlock_abi\": %d, \"usable\": %s%s}\n", abi > 0 ? abi : 0, abi > 0 ? "true" : "false", err.c_str());
+    std::printf("{\"landlock_abi\": %d, \"usable\": %s, \"signal_scoping\": %s%s}\n", abi > 0 ? abi : 0,
+                abi > 0 ? "true" : "false", abi >= 6 ? "true" : "false", err.c_str());
     return abi > 0 ? 0 : 1;
   }
   if (i >= argc) return usage();

@@ -16,7 +16,7 @@ echo "[pmc] RCCL pod counter pass"
 PYTHONPATH="$ROOT" timeout -k 10 300 ./setup.sh --nodes 1 --yes --json --port 0 --timeout 120 --rccl on \
   --rccl-timeout 120 --rccl-max-bytes $((16 << 20)) --rocprof --rocprof-counters "$COUNTERS" > "$OUT/setup.log" 2>&1 &&
 tail -1 "$OUT/setup.log" > "$OUT/setup_summary.json" &&
-cp -r .tk8s/profiles "$OUT/rccl_profiles" &&
+cp -r rocprof "$OUT/rccl_profiles" &&
 PYTHONPATH="$ROOT" timeout -k 10 120 ./setup.sh -c --yes > /dev/null 2>&1 &&
 cd /tmp &&
 echo "[pmc] validation payload counter pass" &&

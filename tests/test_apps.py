@@ -11,6 +11,7 @@ import subprocess
 import sys
 import threading
 import time
+import urllib.error
 import urllib.request
 from pathlib import Path
 
@@ -270,8 +271,14 @@ def test_ghost_from_the_dashboard_deploy_form(cluster):
     dash = summary["dashboard"]
     body = json.dumps({"name": "ghost", "containerImage": "ghost", "replicas": 1, "isExternal": True,
                        "portMappings": [{"port": 2368, "targetPort": 2368, "protocol": "TCP"}]}).encode()
-    r = urllib.request.urlopen(urllib.request.Request(dash + "api/v1/appdeployment", data=body, method="POST",
+    tok = json.loads((ws / ".tk8s" / "kubeconfig.json").read_text())["users"][0]["user"]["token"]
+    with pytest.raises(urllib.error.HTTPError) as ei:  # the form needs the environment's token (authn.py)
+        urllib.request.urlopen(urllib.request.Request(dash + "api/v1/appdeployment", data=body, method="POST",
                                                       headers={"Content-Type": "application/json"}), timeout=10)
+    assert ei.value.code == 401
+    r = urllib.request.urlopen(urllib.request.Request(dash + "api/v1/appdeployment", data=body, method="POST",
+                                                      headers={"Content-Type": "application/json",
+                                                               "Authorization": f"Bearer {tok}"}), timeout=10)
     assert r.status == 201
     kc("rollout", "status", "deploy/ghost", "--timeout", "60s")
     svc = json.loads(kc("get", "svc", "ghost", "-o", "json").stdout)
@@ -281,7 +288,8 @@ def test_ghost_from_the_dashboard_deploy_form(cluster):
     urllib.request.urlopen(urllib.request.Request(url + "/ghost/api/v0.1/posts", data=post, method="POST",
                                                   headers={"Content-Type": "application/json"}), timeout=5)
     assert "MI355X is Ready" in _get(url + "/")
-    page = _get(dash)
+    assert "Deploy a containerized app" not in _get(dash)  # anonymous: the node table only
+    page = _get(dash + f"?token={tok}")
     assert "Deploy a containerized app" in page and "ghost" in page
 
 

@@ -264,6 +264,7 @@ def test_manual_flow(ws):
     """docs/manual-setup.md, command for command: tk8s env/networks/packages, a hand-written
     rancher.tf, tk8s terraform get/plan/apply, hand-written inventory + vars, tk8s
     ansible-playbook (--check, then for real), kubectl with the served kubeconfig."""
+    import urllib.error
     import urllib.request
 
     env = _env()
@@ -296,10 +297,16 @@ def test_manual_flow(ws):
     assert r.returncode == 0, r.stdout[-2000:]
     env_id = (ws / "ansible" / "tmp" / "kubernetes_environment.id").read_text().strip()
     base = f"http://{m_ip}:{port}"
-    w = json.loads(urllib.request.urlopen(f"{base}/v1/cluster/wait?project={env_id}&nodes=1&gpus=1&timeout=30",
-                                          timeout=40).read())
+    # the control plane's admin token, as ranchermaster kept it (controlplane/authn.py)
+    auth = {"Authorization": "Bearer " + (ws / ".tk8s" / "admin-token").read_text().strip()}
+    with pytest.raises(urllib.error.HTTPError) as ei:  # nothing but health and discovery without it
+        urllib.request.urlopen(f"{base}/env/{env_id}/kubernetes/kubectl?format=json")
+    assert ei.value.code == 401
+    w = json.loads(urllib.request.urlopen(urllib.request.Request(
+        f"{base}/v1/cluster/wait?project={env_id}&nodes=1&gpus=1&timeout=30", headers=auth), timeout=40).read())
     assert w["ready"], w
-    (ws / "kc.json").write_bytes(urllib.request.urlopen(f"{base}/env/{env_id}/kubernetes/kubectl?format=json").read())
+    (ws / "kc.json").write_bytes(urllib.request.urlopen(urllib.request.Request(
+        f"{base}/env/{env_id}/kubernetes/kubectl?format=json", headers=auth)).read())
     out = sh("./kubectl", "--kubeconfig", "kc.json", "get", "nodes").stdout
     assert "kubenode1" in out and "Ready" in out
 

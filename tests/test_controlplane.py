@@ -28,7 +28,8 @@ def _start(tmp_path, grace=0.6, state_dir=None):
         assert time.monotonic() < deadline
         time.sleep(0.01)
     info = json.loads(ready.read_text())
-    return p, Client(info["base"], timeout=10)
+    # the server admin token (controlplane/authn.py): what the roles read from the master
+    return p, Client(info["base"], token=info["adminToken"], timeout=10)
 
 
 def _stop(p):
@@ -115,7 +116,7 @@ def test_writes_need_the_project_token(cp):
     proj = _env(cp)
     pod = {"metadata": {"name": "p"}, "spec": {"containers": [{"name": "c", "command": ["true"]}]}}
     with pytest.raises(ApiError) as ei:
-        cp.post(f"/r/projects/{proj['id']}/kubernetes/api/v1/namespaces/default/pods", pod)
+        Client(cp.base).post(f"/r/projects/{proj['id']}/kubernetes/api/v1/namespaces/default/pods", pod)
     assert ei.value.status == 401
     k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
     assert k.post(k.k8s("/api/v1/namespaces/default/pods"), pod)["metadata"]["name"] == "p"
@@ -254,7 +255,10 @@ def test_kv_rendezvous_long_poll(cp):
     t = threading.Thread(target=reader)
     t.start()
     time.sleep(0.2)
-    Client(cp.base).put("/v1/kv/job/uid", "abc123")
+    with pytest.raises(ApiError) as ei:  # the KV answers no anonymous caller (controlplane/authn.py)
+        Client(cp.base).put("/v1/kv/job/uid", "evil")
+    assert ei.value.status == 401
+    Client(cp.base, token=cp.token).put("/v1/kv/job/uid", "abc123")
     t.join(10)
     assert got["v"] == "abc123"
     with pytest.raises(ApiError):

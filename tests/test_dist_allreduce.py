@@ -1,6 +1,7 @@
 """Multi-process all-reduce validator on CPU (gloo): the CPU twin of tk8s-rccl (N3/N6), with the
 rank-0 address exchanged through the control-plane KV store exactly like the RCCL unique id."""
 import json
+import os
 import subprocess
 import sys
 from pathlib import Path
@@ -19,7 +20,8 @@ def test_gloo_allreduce_ranks_agree_exactly(tmp_path, nranks, dtype):
         url = f"{c.base}/v1/kv/job-{nranks}/uid"
         procs = [subprocess.Popen([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", str(r),
                                    "--nranks", str(nranks), "--kv-url", url, "--max-bytes", str(256 << 10), "--dtype", dtype],
-                                  cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                                  cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                  env={**os.environ, "TK8S_KV_TOKEN": c.token})  # the KV answers no anonymous caller
                  for r in range(nranks)]
         outs = [json.loads(pr.communicate(timeout=120)[0].strip().splitlines()[-1]) for pr in procs]
     finally:
@@ -38,7 +40,7 @@ def test_missing_peer_times_out_with_a_json_error(tmp_path):
     try:
         r = subprocess.run([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--rank", "1",
                             "--nranks", "2", "--kv-url", f"{c.base}/v1/kv/none/uid", "--timeout", "1"],
-                           cwd=REPO, capture_output=True, text=True, timeout=60)
+                           cwd=REPO, capture_output=True, text=True, timeout=60, env={**os.environ, "TK8S_KV_TOKEN": c.token})
     finally:
         _stop(p)
     out = json.loads(r.stdout.strip().splitlines()[-1])

@@ -193,7 +193,7 @@ def test_strategic_merge_directives_unit():
 # ---- watch stream ---------------------------------------------------------------------------
 def _stream(k, path, timeout=10):
     conn = http.client.HTTPConnection(k.host, k.port, timeout=timeout)
-    conn.request("GET", k.k8s(path), headers={"Accept": "application/json"})
+    conn.request("GET", k.k8s(path), headers={"Accept": "application/json", "Authorization": f"Bearer {k.token}"})
     r = conn.getresponse()
     return conn, r
 
@@ -380,9 +380,11 @@ def test_service_accounts_and_rbac(kube):
     assert as_(tok, "POST", "/apis/rbac.authorization.k8s.io/v1/clusterrolebindings", {"metadata": {"name": "x"}})[0] == 403
     names = [o["metadata"]["name"] for o in _raw(kube, "GET", "/apis/rbac.authorization.k8s.io/v1/clusterroles")[2]["items"]]
     assert {"cluster-admin", "admin", "edit", "view"} <= set(names)
-    # anonymous: reads but Secrets, no writes
-    assert as_(None, "GET", "/api/v1/namespaces/default/pods")[0] == 200
-    assert as_(None, "GET", "/api/v1/namespaces/default/secrets")[0] == 401
+    # anonymous: discovery only (controlplane/authn.py) -- no object, log or write
+    assert as_(None, "GET", "/api/v1")[0] == 200
+    for path in ("/api/v1/namespaces/default/pods", "/api/v1/namespaces/default/configmaps",
+                 "/api/v1/namespaces/default/secrets", "/api/v1/nodes"):
+        assert as_(None, "GET", path)[0] == 401, path
     assert as_(None, "POST", "/api/v1/namespaces/default/configmaps", cm)[0] == 401
 
 

@@ -33,6 +33,7 @@ from .deviceplugin import DevicePlugin
 from .volumes import VolumeError, env_name as volume_env_name, mounts as volume_mounts, volume_dirs
 from .runtime import (
     PodProc, PodRuntime, container_argv, container_exec_argv, container_runtime, gpu_jail, gpu_jail_argv,
+    jail_signal_scoping,
     install_sigterm, namespace_isolation,
 )
 
@@ -465,11 +466,17 @@ class Agent:
         mine = [by_ord[o] for o in view if o in by_ord]
         gpu_isolation = (f"{jail_how}: may open {', '.join(f'gpu{g.ordinal}' for g in mine) or 'no GPU'}" if jail_ok
                          else f"none: {jail_how}")
+        layers = self._jail_layers(pod, pp_dir, vol_dirs)
+        if jail_ok:
+            gpu_isolation += f"; node state denied ({', '.join(layers['deny'])})" + (
+                "; signals scoped to the pod" if gpu_pod and jail_signal_scoping() else
+                "; shares the host PID namespace: signals not scoped (Landlock ABI < 6)" if gpu_pod else "")
         procs = []
         for n, cont in enumerate(inits + apps):
             first_app = cont is apps[0]
             try:
-                built = self._container_cmd(pod, cont, env, cfg[id(cont)], mine, gpu_pod, jail_ok, pp_dir, first_app)
+                built = self._container_cmd(pod, cont, env, cfg[id(cont)], mine, gpu_pod, jail_ok, pp_dir, first_app,
+                                            layers)
             except _PodFail as e:
                 self._report(key, md["name"], md["namespace"], "Failed", {"reason": e.reason, "message": e.message}, None)
                 return
@@ -493,8 +500,39 @@ class Agent:
                                                 "tk8s.amd.com/gpu-isolation": gpu_isolation}}
         self.runtime.start(pp)
 
+    def _jail_layers(self, pod: dict, pp_dir: Path, vol_dirs: dict) -> dict:
+        """What a jailed pod may not read, may only read, and may write again beneath those
+        (gpujail.h; the most specific path decides):
+
+        * denied: the node's state root (the workspace's ``.tk8s/``: admin kubeconfig and token,
+          the cluster key, every machine's registration URL, other pods' directories with their
+          ServiceAccount tokens and secret volumes), the workspace's Terraform state and
+          ``ansible/tmp``, the operator's ``~/.ssh``;
+        * read-only: the tk8s install and the workspace (the operator runs them: a pod that could
+          rewrite them would run as the operator), the operator's shell start-up files;
+        * read-write: the pod's own directory, its hostPath volumes (read-only ones read-only);
+          validation pods (kube-system, the DaemonSet's label) consume their machine's ``run/``
+          burn-in result."""
+        md = pod["metadata"]
+        sb = self.sandbox.resolve()
+        state = sb.parent.parent if sb.parent.name == "machines" else sb
+        deny, ro, rw = [str(state)], [TK8S_HOME], [str(pp_dir)]
+        if state.name == ".tk8s":
+            ws = state.parent
+            ro.append(str(ws))
+            deny += [str(x) for x in sorted((ws / "terraform").glob("terraform.tfstate*"))] + [str(ws / "ansible" / "tmp")]
+        home = Path.home()
+        deny.append(str(home / ".ssh"))
+        ro += [str(home / f) for f in (".bashrc", ".profile", ".bash_profile", ".bash_login", ".zshrc", ".zprofile",
+                                       ".config/systemd", ".config/autostart")]
+        for d, read_only in vol_dirs.values():
+            (ro if read_only else rw).append(str(d))
+        if md.get("namespace") == "kube-system" and (md.get("labels") or {}).get(VALIDATION_LABEL) == "true":
+            rw.append(str(self.sandbox / "run"))  # it consumes the result (renames it: single use)
+        return {"deny": deny, "read_only": ro, "allow": rw}
+
     def _container_cmd(self, pod: dict, c: dict, pod_env: dict, cfg: tuple, mine: list, gpu_pod: bool, jail_ok: bool,
-                       pp_dir: Path, first_app: bool) -> dict:
+                       pp_dir: Path, first_app: bool, layers: dict | None = None) -> dict:
         """One container's process: argv, env, and the prefix it runs under (GPU jail, or
         tk8s-container for a loaded image); raises _PodFail with the pod's failure reason."""
         md, spec = pod["metadata"], pod["spec"]
@@ -523,7 +561,11 @@ class Agent:
             raise _PodFail("ErrImageNeverPull", f"container {c.get('name')!r} has no command and image {c.get('image')!r} "
                                                 "is neither loaded on this node (./tk8s image load) nor in the tk8s app "
                                                 "catalogue (tritonk8ssupervisor_amd/apps)")
-        jail = gpu_jail_argv(mine) if jail_ok else []
+        jail = gpu_jail_argv(mine, **(layers or {}), scope_signals=gpu_pod) if jail_ok else []
+        if jail and image is None and "TMPDIR" not in cenv:
+            # its own temporary directory: /tmp may be on the way to a denied path (gpujail.h)
+            (pp_dir / "tmp").mkdir(parents=True, exist_ok=True)
+            env["TMPDIR"] = str(pp_dir / "tmp")
         exec_prefix: list[str] = []
         if image is not None:  # tk8s-container: namespaces, the image's root, the same GPU jail inside
             store, ref = image
@@ -532,10 +574,13 @@ class Agent:
             except Exception as e:  # noqa: BLE001 - an unreadable image fails the pod, not the agent
                 raise _PodFail("ErrImageUnpack", str(e)[:500]) from e
             workdir = c.get("workingDir") or store.container_argv(ref, None, None)[2]
-            upper = pp_dir / ("rootfs" if first_app else f"rootfs-{c.get('name')}")
+            cname = str(c.get("name") or "")
+            if "/" in cname or cname in ("", ".", ".."):  # a path component only (the API admits DNS labels)
+                raise _PodFail("InvalidContainerName", f"container name {cname!r} is not a DNS label")
+            upper = pp_dir / ("rootfs" if first_app else f"rootfs-{cname}")
             jail = container_argv(str(rootfs), str(upper), workdir, pid_ns=not gpu_pod, gpus=mine,
-                                  binds=mounts, hostname=spec.get("hostname") or md["name"])
-            exec_prefix = ["--workdir", workdir, *gpu_jail_argv(mine)[1:-1], "--"]
+                                  binds=mounts, hostname=spec.get("hostname") or md["name"], scope_signals=gpu_pod)
+            exec_prefix = ["--workdir", workdir, *gpu_jail_argv(mine, scope_signals=gpu_pod)[1:-1], "--"]
         return {"argv": argv, "env": env, "jail": jail, "exec_prefix": exec_prefix,
                 "image": image[1] if image is not None else None}
 

@@ -194,16 +194,26 @@ def refresh(pod: dict, pod_dir: Path, fetch: Callable[[str, str, str], dict | No
         if not any(k in vol for k in _DYNAMIC):
             continue
         try:
+            name = _vol_name(vol)
             files, modes = _render(pod, vol, fetch, pod_ip, host_ip)
         except VolumeError:
             continue
-        if _write_files(pod_dir / "volumes" / vol.get("name", ""), files, modes):
-            changed.append(vol.get("name", ""))
+        if _write_files(pod_dir / "volumes" / name, files, modes):
+            changed.append(name)
     return changed
 
 
 def has_dynamic(pod: dict) -> bool:
     return any(any(k in v for k in _DYNAMIC) for v in pod["spec"].get("volumes") or [])
+
+
+def _vol_name(vol: dict) -> str:
+    """A volume's name, refused unless it is one path component (the API admits DNS labels only;
+    this holds even against an object that reached the node some other way)."""
+    name = str(vol.get("name", ""))
+    if not name or "/" in name or name in (".", "..") or "\0" in name:
+        raise VolumeError(f"volume name {name!r} is not a DNS label")
+    return name
 
 
 def volume_dirs(pod: dict, pod_dir: Path, node_dir: Path, fetch: Callable[[str, str, str], dict | None],
@@ -212,7 +222,7 @@ def volume_dirs(pod: dict, pod_dir: Path, node_dir: Path, fetch: Callable[[str, 
     ns = pod["metadata"]["namespace"]
     out: dict[str, tuple[Path, bool]] = {}
     for vol in pod["spec"].get("volumes") or []:
-        name = vol.get("name", "")
+        name = _vol_name(vol)
         own = pod_dir / "volumes" / name
         if "emptyDir" in vol:
             own.mkdir(parents=True, exist_ok=True)

@@ -49,6 +49,7 @@ ARG_SPECS: dict[str, dict] = {
     "tk8s_kube": {
         "api": {"type": "str", "required": True},
         "project": {"type": "str", "required": True},
+        "token": {"type": "str", "no_log": True},
         "state": {"type": "str", "default": "present", "choices": ["present", "absent", "wait"]},
         "definition": {"type": "raw"},
         "src": {"type": "path"},

@@ -122,7 +122,8 @@ def cmd_status(args) -> int:
         from ..controlplane.client import Client
 
         try:
-            out["cluster"] = Client(summ["api"], timeout=5).get("/v1/cluster/status", query={"project": summ.get("project")})
+            out["cluster"] = Client(summ["api"], token=ws.admin_token(), timeout=5).get(
+                "/v1/cluster/status", query={"project": summ.get("project")})
         except Exception as e:  # noqa: BLE001
             out["cluster"] = {"error": str(e)}
     if args.json:
@@ -359,7 +360,7 @@ SETUP_OPTIONS: list[tuple[tuple[str, ...], dict]] = [
     (("--probe-iters",), {"type": int, "default": 3}),
     (("--node-grace",), {"type": float, "default": 5.0}),
     (("--rocprof",), {"action": "store_true",
-                      "help": "run the RCCL Job's ranks under rocprofv3 --kernel-trace --stats (.tk8s/profiles/)"}),
+                      "help": "run the RCCL Job's ranks under rocprofv3 --kernel-trace --stats (rocprof/<job>/)"}),
     (("--rocprof-counters",), {"default": None, "metavar": "C1,C2,...",
                                "help": "with --rocprof: also collect these PMC counters per kernel (their own --pmc "
                                        "pass with --kernel-trace/--stats only; at most 8 SQ_ and 2 GRBM_ counters), "

@@ -1,0 +1,202 @@
+"""Who a request is, and the limits of the identities that are not ServiceAccounts.
+
+The reference ran Rancher 1.x with access control off: anyone who could reach ``:8080`` could
+create environments, read registration URLs and fetch the kubeconfig
+(ansible/roles/ranchermaster/tasks/main.yml:29-52, rancherhost/tasks/main.yml:11-24 call the API
+with no credentials). Here the server is on a shared host, next to the cluster's own workloads,
+so every request names a bearer token except a short public list (``PUBLIC``):
+
+* the **server admin token** -- created with the control plane (``<state-dir>/admin-token``,
+  mode 0600, or ``$TK8S_ADMIN_TOKEN``); the roles read it on the master and keep a copy in the
+  workspace's ``.tk8s/`` (which the pod jail denies, agent/runtime.py). It creates environments
+  and registration tokens and reads every environment's kubeconfig;
+* a **project API token** (the kubeconfig's) -- the administrator of that environment;
+* a **node token** (handed out at registration) -- the kubelet's powers and no more, as the
+  Node authorizer + NodeRestriction admission give them (``node_allows``): reads of what nodes
+  read, Secrets and ConfigMaps only when a pod bound to the node uses them, writes only to its
+  own Node, Lease, exec results and the pods bound to it, Events;
+* a **ServiceAccount token** -- RBAC (rbac.py);
+* none -- anonymous: health, version, discovery, the readiness dashboard, node registration
+  (its token is in the URL) and nothing else (401).
+
+Tokens resolve through one dict rebuilt only when projects, node secrets or Secrets change
+(``Store.version``), not a scan of them per request.
+"""
+from __future__ import annotations
+
+import base64
+import os
+import re
+from pathlib import Path
+
+from ..utils.fsutil import atomic_write
+from ..utils.ids import token_hex
+from .httpserver import HttpError, Request
+
+ADMIN_TOKEN_FILE = "admin-token"
+
+# (method, path) anyone may call: liveness, version, discovery, node registration (token-gated
+# by its URL), the Rancher template list, and the dashboard (it shows anonymous callers only the
+# node table the readiness oracle of setup.sh:66-68 needs).
+_K8S = r"(/r/projects/[^/]+/kubernetes)?"
+PUBLIC = [
+    ("GET", re.compile(r"^/(ping|healthz|readyz|livez)?/?$")),
+    ("GET", re.compile(r"^/version/?$")),
+    ("GET", re.compile(r"^/v2-beta/projectTemplates/?$")),
+    ("GET", re.compile(r"^/v1/scripts/[^/]+$")),
+    ("POST", re.compile(r"^/v1/scripts/[^/]+$")),
+    ("GET", re.compile(r"^/r/projects/[^/]+/kubernetes-dashboard:9090/?$")),
+    ("GET", re.compile(r"^" + _K8S + r"/(api|apis|api/v1|apis/[^/]+|apis/[^/]+/[^/]+|openapi/v3(/.*)?)/?$")),
+    ("POST", re.compile(r"^" + _K8S + r"/apis/authorization\.k8s\.io/v1/selfsubjectaccessreviews$")),
+]
+
+
+def is_public(method: str, path: str) -> bool:
+    m = "GET" if method == "HEAD" else method
+    return any(m == pm and rx.match(path) for pm, rx in PUBLIC)
+
+
+def load_admin_token(state_dir: Path | None) -> str:
+    """``$TK8S_ADMIN_TOKEN``, else ``<state_dir>/admin-token`` (created 0600 on first start),
+    else a fresh one for this process only."""
+    env = os.environ.get("TK8S_ADMIN_TOKEN", "").strip()
+    if env:
+        return env
+    if state_dir is None:
+        return token_hex(24)
+    p = Path(state_dir) / ADMIN_TOKEN_FILE
+    try:
+        tok = p.read_text().strip()
+        if tok:
+            return tok
+    except OSError:
+        pass
+    tok = token_hex(24)
+    atomic_write(p, tok + "\n", mode=0o600)
+    return tok
+
+
+def _pod_refs(pod: dict, kind: str) -> set[str]:
+    """Names of the Secrets (``kind`` "secrets") or ConfigMaps a pod's kubelet must read."""
+    spec = pod.get("spec") or {}
+    out: set[str] = set()
+    vol_key, ref_key, env_key = (("secret", "secretRef", "secretKeyRef") if kind == "secrets"
+                                 else ("configMap", "configMapRef", "configMapKeyRef"))
+    for v in spec.get("volumes") or []:
+        src = v.get(vol_key) or {}
+        name = src.get("secretName") if kind == "secrets" else src.get("name")
+        if name:
+            out.add(name)
+        for s in (v.get("projected") or {}).get("sources") or []:
+            if (s.get(vol_key) or {}).get("name"):
+                out.add(s[vol_key]["name"])
+    for c in (spec.get("containers") or []) + (spec.get("initContainers") or []):
+        for e in c.get("envFrom") or []:
+            if (e.get(ref_key) or {}).get("name"):
+                out.add(e[ref_key]["name"])
+        for e in c.get("env") or []:
+            ref = (e.get("valueFrom") or {}).get(env_key) or {}
+            if ref.get("name"):
+                out.add(ref["name"])
+    if kind == "secrets":
+        out |= {s.get("name") for s in spec.get("imagePullSecrets") or [] if s.get("name")}
+        if spec.get("automountServiceAccountToken") is not False:
+            out.add(f"{spec.get('serviceAccountName') or spec.get('serviceAccount') or 'default'}-token")
+    return out
+
+
+class Authentication:
+    # ---- tokens --------------------------------------------------------------------------
+    def _tokens(self) -> dict[str, tuple]:
+        """token -> ("admin", pid|None) | ("node", pid, name) | ("sa", pid, ns, name)."""
+        ver = self.store.version("projects", "nodesecrets", "secrets")
+        if getattr(self, "_tok_ver", None) != ver:
+            idx: dict[str, tuple] = {}
+            for s in self.store.list("secrets", lambda o: o.get("type") == "kubernetes.io/service-account-token"):
+                t = (s.get("data") or {}).get("token")
+                sa = (s["metadata"].get("annotations") or {}).get("kubernetes.io/service-account.name")
+                if t and sa:
+                    idx[base64.b64decode(t).decode(errors="replace")] = ("sa", s.get("_project"), s["metadata"]["namespace"], sa)
+            for n in self.store.list("nodesecrets"):
+                if n.get("nodeToken"):
+                    idx[n["nodeToken"]] = ("node", n.get("_project"), n["metadata"]["name"])
+            for p in self.store.list("projects"):
+                if p.get("apiToken"):
+                    idx[p["apiToken"]] = ("admin", p["id"])
+            idx[self.admin_token] = ("admin", None)
+            self._tok_idx, self._tok_ver = idx, ver
+        return self._tok_idx
+
+    def _identity(self, p: str | None, tok: str | None) -> str | None:
+        """``admin`` (the server admin token, or project ``p``'s API token), ``node:<name>``,
+        ``sa:<ns>:<name>`` -- a node or ServiceAccount of project ``p`` -- or None."""
+        if not tok:
+            return None
+        hit = self._tokens().get(tok)
+        if hit is None:
+            return None
+        if hit[0] == "admin":
+            return "admin" if hit[1] is None or p is None or hit[1] == p else None
+        if p is not None and hit[1] != p:
+            return None
+        return f"node:{hit[2]}" if hit[0] == "node" else f"sa:{hit[2]}:{hit[3]}"
+
+    def _server_admin(self, req: Request) -> bool:
+        return bool(req.bearer) and req.bearer == self.admin_token
+
+    def _authenticate(self, req: Request) -> None:
+        """The gate in front of every route: a public path, or a token this server knows."""
+        if is_public(req.method, req.path):
+            return
+        if req.bearer and req.bearer in self._tokens():
+            return
+        raise HttpError(401, "Unauthorized: this request needs a bearer token "
+                             "(the kubeconfig's, a ServiceAccount's, a node's or the server admin token)")
+
+    def _require_admin(self, req: Request, pid: str | None) -> None:
+        """The server admin token, or the API token of project ``pid``."""
+        hit = self._tokens().get(req.bearer or "")
+        if hit is None or hit[0] != "admin" or (hit[1] is not None and hit[1] != pid):
+            raise HttpError(403 if hit else 401, "this needs the server admin token or the environment's API token")
+
+    # ---- the Node authorizer + NodeRestriction ---------------------------------------------
+    def node_allows(self, node: str, p: str | None, info) -> bool:
+        """May node ``node`` (of project ``p``) do ``info`` (rbac.RequestInfo)?"""
+        res = info.resource.split("/")[0]
+        sub = info.resource.partition("/")[2]
+        read = info.verb in ("get", "list", "watch")
+        if res in ("secrets", "configmaps"):
+            if info.verb != "get" or not info.name:
+                return False
+            return any(info.name in _pod_refs(o, res) for o in self._node_pods(node, p, info.namespace))
+        if res == "nodes":
+            if sub in ("execs",) or (not read and info.verb in ("update", "patch")):
+                return info.name == node
+            return read and not sub
+        if res == "pods":
+            if sub in ("log", "exec", "attach", "portforward", "eviction"):
+                return False
+            if read and not sub:
+                return True
+            if sub == "status" and info.verb in ("update", "patch", "get"):
+                return self._bound_to(node, p, info.namespace, info.name)
+            if info.verb == "delete" and not sub:
+                return self._bound_to(node, p, info.namespace, info.name)
+            return False
+        if res == "leases":
+            return read or info.name == node
+        if res == "events":
+            return info.verb in ("create", "patch", "update") or read
+        return read and res not in ("serviceaccounts",)
+
+    def _node_pods(self, node: str, p: str | None, ns: str) -> list[dict]:
+        return self.store.list("pods", lambda o: o["spec"].get("nodeName") == node
+                               and o["metadata"].get("namespace") == ns and (p is None or o.get("_project") == p))
+
+    def _bound_to(self, node: str, p: str | None, ns: str, name: str) -> bool:
+        from .objects import _key
+
+        if p is None:
+            return False
+        o = self.store.get("pods", _key(p, ns, name))
+        return o is None or o["spec"].get("nodeName") == node  # None: the handler answers 404

@@ -196,7 +196,11 @@ class Controllers:
                 if nn not in pods:
                     pods[nn] = self._new_pod(pid, ns, f"{ds['metadata']['name']}-{nn}", ds, "DaemonSet", tmpl, node=nn,
                                              labels={**(ds["spec"].get("selector", {}).get("matchLabels") or {}),
-                                                     "controller-revision-hash": h})
+                                                     "controller-revision-hash": h,
+                                                     # the validation DaemonSet's pods say so (the agent
+                                                     # lets them read their machine's burn-in result)
+                                                     **({VALIDATION_LABEL: "true"} if (ds["metadata"].get("labels")
+                                                        or {}).get(VALIDATION_LABEL) == "true" else {})})
             # RollingUpdate (the default; OnDelete leaves it to the user): a changed template replaces
             # the running pods node by node, at most maxUnavailable (1) at a time
             upd = ds["spec"].get("updateStrategy") or {}

@@ -20,6 +20,7 @@ from .httpserver import HttpError, Request, Response, StreamResponse
 from .store import now_iso
 from .objects import (
     GPU, _key, _set_ready, merge_patch, _admit_gpu_visibility, _normalize_data, labels_match, _parse_selector,
+    check_pod_spec_names,
 )
 
 
@@ -28,36 +29,10 @@ class KubernetesAPI:
     def _pid(self, pid: str | None, req: Request) -> str:
         return self.project(pid or req.q("project")).get("id")
 
-    # ---- authentication / authorization (rbac.py) ------------------------------------------
-    def _identity(self, p: str | None, tok: str | None) -> str | None:
-        """``admin`` (the project's API token), ``node:<name>``, ``sa:<ns>:<name>``, or None."""
-        if not tok:
-            return None
-        try:
-            if tok == self.project(p).get("apiToken"):
-                return "admin"
-        except HttpError:
-            pass
-        for n in self.store.list("nodesecrets"):
-            if n.get("nodeToken") == tok:
-                return f"node:{n['metadata']['name']}"
-        if getattr(self, "_sa_tokens_rv", None) != self.store.rv:  # token -> ServiceAccount, rebuilt on change
-            import base64
-
-            self._sa_tokens = {}
-            for s in self.store.list("secrets", lambda o: o.get("type") == "kubernetes.io/service-account-token"):
-                t = (s.get("data") or {}).get("token")
-                sa = (s["metadata"].get("annotations") or {}).get("kubernetes.io/service-account.name")
-                if t and sa:
-                    self._sa_tokens[base64.b64decode(t).decode()] = (s["_project"], s["metadata"]["namespace"], sa)
-            self._sa_tokens_rv = self.store.rv
-        hit = self._sa_tokens.get(tok)
-        if hit and (p is None or hit[0] == p):
-            return f"sa:{hit[1]}:{hit[2]}"
-        return None
-
+    # ---- authorization (authn.py: who; rbac.py: what a ServiceAccount may) ------------------
     def _authorize(self, req: Request, pid: str | None) -> None:
-        """RBAC for ServiceAccounts; the admin and nodes as before; anonymous reads but Secrets."""
+        """The admin may do anything; a node what the Node authorizer allows (authn.node_allows);
+        a ServiceAccount what RBAC grants; anonymous callers only discovery (authn.PUBLIC)."""
         from . import rbac
 
         try:
@@ -67,16 +42,18 @@ class KubernetesAPI:
         ident = self._identity(p, req.bearer)
         req.identity = ident
         info = rbac.request_info(req.method, req.path, req.query)
-        if info is None or ident == "admin" or (ident or "").startswith("node:"):
+        if info is None or ident == "admin":
             return
         if info.group == "authorization.k8s.io":  # anyone may ask what it may do (system:basic-user)
             return
         if ident is None:
-            if req.method in ("GET", "HEAD") and info.resource.split("/")[0] != "secrets":
-                return
-            if req.method in ("GET", "HEAD"):
-                raise HttpError(401, "Unauthorized: reading secrets needs a bearer token")
-            return  # a write: the handler's _auth answers 401
+            raise HttpError(401, "Unauthorized: this request needs a bearer token")
+        if ident.startswith("node:"):
+            node = ident[5:]
+            if not self.node_allows(node, p, info):
+                raise HttpError(403, f'{info.resource} is forbidden: User "system:node:{node}" {info.describe()}'
+                                     " (the Node authorizer: a node reaches its own Node and the pods bound to it)")
+            return
         _sa, sns, sname = ident.split(":", 2)
         roles = {(o["metadata"]["namespace"], o["metadata"]["name"]): o.get("rules") or []
                  for o in self.store.list("roles", lambda o: self._in(p, o))}
@@ -96,11 +73,12 @@ class KubernetesAPI:
         info = rbac.RequestInfo(ra.get("verb", "get"), ra.get("group", ""), res, ra.get("namespace", ""), ra.get("name", ""))
         ident = getattr(req, "identity", None)
         p = self._pid(pid, req)
-        if ident == "admin" or (ident or "").startswith("node:"):
-            ok, why = True, "the cluster administrator" if ident == "admin" else "a node"
+        if ident == "admin":
+            ok, why = True, "the cluster administrator"
+        elif (ident or "").startswith("node:"):
+            ok, why = self.node_allows(ident[5:], p, info), "the Node authorizer"
         elif ident is None:
-            ok = info.verb in ("get", "list", "watch") and info.resource.split("/")[0] != "secrets"
-            why = "anonymous: read-only, no Secrets"
+            ok, why = False, "anonymous: discovery only"
         else:
             _sa, sns, sname = ident.split(":", 2)
             ok = rbac.allowed({(o["metadata"]["namespace"], o["metadata"]["name"]): o.get("rules") or []
@@ -901,6 +879,7 @@ class KubernetesAPI:
         tmpl = ((spec.get("jobTemplate") or {}).get("spec") or {}).get("template") or {}
         if not (tmpl.get("spec") or {}).get("containers"):
             raise HttpError(422, "spec.jobTemplate.spec.template.spec.containers is required")
+        check_pod_spec_names(f'CronJob.batch "{name}"', tmpl["spec"])
         if spec.get("concurrencyPolicy", "Allow") not in ("Allow", "Forbid", "Replace"):
             raise HttpError(422, "spec.concurrencyPolicy must be Allow, Forbid or Replace")
 
@@ -937,6 +916,7 @@ class KubernetesAPI:
             spec = body.setdefault("spec", {})
             if not spec.get("containers"):
                 raise HttpError(422, "spec.containers is required")
+            check_pod_spec_names(f'Pod "{name}"', spec)
             self._resolve_priority(pid, spec)
             from .webhooks import warn
 
@@ -950,6 +930,7 @@ class KubernetesAPI:
             tmpl = body.get("spec", {}).get("template", {})
             if not tmpl.get("spec", {}).get("containers"):
                 raise HttpError(422, "spec.template.spec.containers is required")
+            check_pod_spec_names(f'{kind[:-1]} "{name}"', tmpl["spec"])
             if kind in ("statefulsets", "replicasets"):
                 self._check_selector(kind, name, body["spec"])
             body.setdefault("status", {})
@@ -1157,6 +1138,7 @@ class KubernetesAPI:
         if kind in ("daemonsets", "deployments", "jobs", "statefulsets", "replicasets"):
             if not new.get("spec", {}).get("template", {}).get("spec", {}).get("containers"):
                 raise HttpError(422, "spec.template.spec.containers is required")
+            check_pod_spec_names(f'{kind[:-1]} "{name}"', new["spec"]["template"]["spec"])
             gen = int(cur["metadata"].get("generation", 1))
             md["generation"] = gen + 1 if spec_changed else gen
         if kind == "services":
@@ -1397,11 +1379,9 @@ class KubernetesAPI:
     def _ws_upgrade(self, req: Request, p: str, what: str, protocols: tuple[str, ...], allow_none: bool = False) -> str:
         """Authorise a WebSocket stream request (project API token or a node token) and pick the
         subprotocol: the first of ``protocols`` the client offers."""
-        tok = req.bearer
-        sa_ok = (getattr(req, "identity", None) or "").startswith("sa:")  # RBAC allowed it (_authorize)
-        if not (sa_ok or tok and (tok == self.project(p).get("apiToken") or any(
-                n.get("nodeToken") == tok for n in self.store.list("nodesecrets")))):
-            raise HttpError(401, f"{what} needs a bearer token")
+        ident = getattr(req, "identity", None)  # _authorize let it through: admin, RBAC'd SA
+        if ident is None or ident.startswith("node:"):
+            raise HttpError(401 if ident is None else 403, f"{what} needs the kubeconfig's or an authorized ServiceAccount's token")
         offered = [x.strip() for x in (req.headers.get("sec-websocket-protocol") or "").split(",") if x.strip()]
         proto = next((x for x in protocols if x in offered), None)
         if proto is None and allow_none and not offered:

@@ -41,6 +41,8 @@ class RancherAPI:
         return {k: v for k, v in p.items() if k not in ("apiToken",)}
 
     async def h_project_create(self, req: Request):
+        if not self._server_admin(req):  # authn.py: environments are the server administrator's
+            raise HttpError(403, "creating an environment needs the server admin token")
         self._ensure_templates()
         body = req.json()
         name = str(body.get("name") or "").strip()
@@ -68,6 +70,7 @@ class RancherAPI:
 
     async def h_project_delete(self, req: Request, pid: str):
         p = self.project(pid)
+        self._require_admin(req, p["id"])
         for kind in list(self.store.objs):
             for k in self.store.keys(kind):
                 if k.startswith(pid + "/"):
@@ -78,6 +81,7 @@ class RancherAPI:
     async def h_token_create(self, req: Request):
         pid = req.q("projectId") or req.json().get("projectId")
         p = self.project(pid)
+        self._require_admin(req, p["id"])
         tid = self._next_id("1c")
         token = token_hex(20)
         t = {"id": tid, "type": "registrationToken", "projectId": p["id"], "token": token, "state": "active",
@@ -91,6 +95,7 @@ class RancherAPI:
         t = self.store.get("registrationtokens", tid)
         if t is None:
             raise HttpError(404, f"registration token {tid} not found")
+        self._require_admin(req, t["projectId"])
         return t
 
     def _token(self, token: str) -> dict:
@@ -161,6 +166,16 @@ class RancherAPI:
             f"<tr><td>{esc(n['metadata']['name'])}</td><td>{'Ready' if node_ready(n) else 'NotReady'}</td>"
             f"<td>{n['status']['allocatable'].get(GPU, '0')}</td><td>{'yes' if node_validated(n) else 'no'}</td></tr>"
             for n in self.store.list("nodes", lambda n: self._in(p['id'], n)))
+        # the node table is the readiness oracle anyone may poll (setup.sh:66-68); workloads and the
+        # deploy form need the environment's token (authn.py), as a header or ?token= for a browser
+        hit = self._tokens().get(req.bearer or req.q("token") or "")
+        if not (hit is not None and hit[0] == "admin" and hit[1] in (None, p["id"])):
+            body = (f"<html><head><title>Kubernetes Dashboard - {esc(p['name'])}</title></head><body>"
+                    f"<h1>kubernetes dashboard</h1><p>environment {esc(p['name'])} ({p['id']})</p>"
+                    f"<h2>Nodes</h2><table><tr><th>node</th><th>status</th><th>{GPU}</th><th>validated</th></tr>{rows}"
+                    "</table><p>Workloads: open this page with <code>?token=</code> the kubeconfig's token.</p>"
+                    "</body></html>")
+            return Response(200, body, content_type="text/html; charset=utf-8")
         deps = "".join(
             f"<tr><td>{esc(d['metadata']['namespace'])}</td><td>{esc(d['metadata']['name'])}</td>"
             f"<td>{d.get('status', {}).get('readyReplicas', 0)}/{d['spec'].get('replicas', 1)}</td>"
@@ -188,7 +203,9 @@ class RancherAPI:
                 " replicas: parseInt(f.get('replicas') || '1'), isExternal: f.get('isExternal') === 'on',"
                 " gpuRequirement: parseInt(f.get('gpus') || '0'), namespace: 'default',"
                 " portMappings: port ? [{port: parseInt(port), targetPort: parseInt(port), protocol: 'TCP'}] : []};"
-                "await fetch('api/v1/appdeployment', {method: 'POST', headers: {'Content-Type': 'application/json'},"
+                "const tok = new URLSearchParams(location.search).get('token');"
+                "await fetch('api/v1/appdeployment', {method: 'POST', headers: {'Content-Type': 'application/json',"
+                " 'Authorization': 'Bearer ' + tok},"
                 " body: JSON.stringify(body)}); location.reload(); });</script>"
                 f"<pre>{esc(json.dumps(s, indent=1))}</pre></body></html>")
         return Response(200, body, content_type="text/html; charset=utf-8")
@@ -196,11 +213,12 @@ class RancherAPI:
     async def h_app_deploy(self, req: Request, pid: str):
         """The dashboard's "Deploy a containerized app" form (kubernetes-dashboard
         ``POST api/v1/appdeployment``): a Deployment plus, with port mappings, a Service --
-        how the reference's walkthrough launched Ghost (docs/detailed.md:261-283). Like the
-        Rancher 1.x UI the reference used, the dashboard needs no API token."""
+        how the reference's walkthrough launched Ghost (docs/detailed.md:261-283). Unlike the
+        Rancher 1.x UI the reference used (access control off), it needs the environment's token."""
         import shlex
 
         p = self.project(pid)
+        self._require_admin(req, p["id"])
         b = req.json()
         name = str(b.get("name") or "").strip()
         image = str(b.get("containerImage") or "").strip()
@@ -235,6 +253,7 @@ class RancherAPI:
 
     async def h_kubeconfig(self, req: Request, pid: str):
         p = self.project(pid)
+        self._require_admin(req, p["id"])  # it holds the environment's API token
         server = f"{self.base}/r/projects/{p['id']}/kubernetes"
         cfg = {"apiVersion": "v1", "kind": "Config", "current-context": p["name"].replace(" ", "-"),
                "clusters": [{"name": p["name"].replace(" ", "-"), "cluster": {"server": server}}],
@@ -249,6 +268,7 @@ class RancherAPI:
 
     async def h_containers(self, req: Request, pid: str):
         p = self.project(pid)
+        self._require_admin(req, p["id"])
         pods = self.store.list("pods", lambda o: self._in(p["id"], o))
         return {"project": p["id"], "containers": [
             {"name": o["metadata"]["name"], "namespace": o["metadata"].get("namespace"),

@@ -59,6 +59,7 @@ from .priority import Priority
 from .webhooks import AdmissionWebhooks
 from .podsecurity import PodSecurity
 from .store import Store, now_iso
+from .authn import Authentication, load_admin_token
 
 
 _KIND_PLURAL = {r[2]: plural for plural, r in k8s_wire.RESOURCES.items()}
@@ -75,13 +76,14 @@ def _group_doc(group: str, versions: list[str]) -> dict:
             "preferredVersion": {"groupVersion": f"{group}/{versions[0]}", "version": versions[0]}}
 
 
-class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Disruption,
+class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI, CustomResources, Disruption,
                    Priority, AdmissionWebhooks, PodSecurity, Scheduler):
     def __init__(self, host: str, port: int, state_dir: str | None = None, node_grace: float = 5.0,
                  advertise: str | None = None, dns_port: int | None = None, ingress_port: int | None = None):
         self.host, self.port = host, port
         self.advertise = advertise
         self.state_dir = Path(state_dir) if state_dir else None
+        self.admin_token = load_admin_token(self.state_dir)  # authn.py: before anything can listen
         self.node_grace = node_grace
         self.store = Store()
         self.store.type_meta = k8s_wire.type_meta()
@@ -177,22 +179,32 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         return p
 
     def _auth(self, req: Request, project: dict) -> None:
-        tok = req.bearer
-        if req.method in ("GET", "HEAD"):
-            return
-        if (getattr(req, "identity", None) or "").startswith("sa:"):
-            return  # a ServiceAccount this request's RBAC check (_authorize) already allowed
-        valid = {project.get("apiToken")}
-        if tok in valid:
-            return
-        # node tokens may update their own node / pods
-        if tok and any(n.get("nodeToken") == tok for n in self.store.list("nodesecrets")):
-            return
-        raise HttpError(401, "missing or invalid bearer token")
+        """A write to ``project``: its administrator, or a node / ServiceAccount the request's
+        authorization (k8s_api._authorize: the Node authorizer, RBAC) already let through."""
+        ident = getattr(req, "identity", None)
+        if ident is None:
+            ident = self._identity(project.get("id"), req.bearer)
+        if ident is None:
+            raise HttpError(401, "missing or invalid bearer token")
+
+    def _gate(self, h):
+        """Every route: authn.PUBLIC paths, or a bearer token the server knows (else 401)."""
+        async def g(req: Request, **kw):
+            self._authenticate(req)
+            return await h(req, **kw)
+        g.__name__ = getattr(h, "__name__", "handler")
+        return g
 
     # ---- routes -----------------------------------------------------------------------
     def _routes(self) -> None:
-        r = self.router
+        gate = self._gate
+
+        class _Gated:  # every route behind the authentication gate
+            @staticmethod
+            def add(method, path, h):
+                self.router.add(method, path, gate(h))
+
+        r = _Gated
         r.add("GET", r"/(ping|healthz)?", self.h_ping)
         r.add("GET", r"/version", self.h_version)
         r.add("GET", r"/metrics", self.h_metrics)
@@ -525,7 +537,8 @@ class ControlPlane(RancherAPI, KubernetesAPI, Controllers, Workloads, MetricsAPI
         if ready_file:
             from ..utils.fsutil import atomic_write_json
 
-            atomic_write_json(ready_file, {"host": host, "port": port, "pid": os.getpid(), "base": self.base})
+            atomic_write_json(ready_file, {"host": host, "port": port, "pid": os.getpid(), "base": self.base,
+                                           "adminToken": self.admin_token})  # 0600, like every atomic_write
         dns_transport = None  # after "Listening on": not on the bring-up's critical path
         if self.dns_port:
             from .dns import DnsProtocol

@@ -34,6 +34,7 @@ class Store:
         self._waiters: list[asyncio.Future] = []
         self.listeners: list[Callable[[str, str, dict], None]] = []
         self.type_meta: dict[str, tuple[str, str]] = {}  # kind -> (apiVersion, Kind) stamped on put
+        self.kind_rv: dict[str, int] = {}  # kind -> resourceVersion of its last write (caches key on it)
 
     # ---- reads ------------------------------------------------------------------------
     def get(self, kind: str, key: str) -> dict | None:
@@ -45,6 +46,10 @@ class Store:
 
     def keys(self, kind: str) -> Iterable[str]:
         return list(self.objs.get(kind, {}).keys())
+
+    def version(self, *kinds: str) -> tuple[int, ...]:
+        """The last write to each of ``kinds``: an index over them is current while this is."""
+        return tuple(self.kind_rv.get(k, 0) for k in kinds)
 
     # ---- writes -----------------------------------------------------------------------
     def _notify(self, kind: str, etype: str, obj: dict) -> None:
@@ -82,6 +87,7 @@ class Store:
         md.setdefault("uid", old["metadata"]["uid"] if old else uuid4())
         md.setdefault("creationTimestamp", old["metadata"].get("creationTimestamp") if old else now_iso())
         table[key] = obj
+        self.kind_rv[kind] = self.rv
         self._notify(kind, "MODIFIED" if old else "ADDED", obj)
         return obj
 
@@ -100,6 +106,7 @@ class Store:
             self.rv += 1
             old = copy.deepcopy(old)
             old["metadata"]["resourceVersion"] = str(self.rv)
+            self.kind_rv[kind] = self.rv
             self._notify(kind, "DELETED", old)
         return old
 
@@ -144,4 +151,5 @@ class Store:
             return False
         self.rv = int(d.get("rv", 0))
         self.objs = d.get("objs", {})
+        self.kind_rv = {k: self.rv for k in self.objs}
         return True

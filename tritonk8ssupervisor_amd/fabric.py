@@ -88,7 +88,8 @@ class FabricCheck:
             else:
                 # N8 (BASELINE.json config 5): kernel trace + per-kernel stats of every rank. Counter
                 # collection (--pmc) is a separate run by design: never mixed with tracing.
-                prof_dir = self.ws.state_dir / "profiles" / job
+                # in the workspace, not .tk8s/: the ranks write it, and the pod jail denies .tk8s/
+                prof_dir = self.ws.root / "rocprof" / job
                 prof_dir.mkdir(parents=True, exist_ok=True)
                 pmc = []
                 if self.rocprof_counters:  # a counter pass: --pmc with --kernel-trace/--stats only
@@ -99,6 +100,10 @@ class FabricCheck:
         objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
                               {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd,
                                "gpu_scope": layout["scope"]})
+        if prof_dir is not None:  # the ranks write their traces there: a hostPath volume, which the pod jail allows
+            pspec = objs[0]["spec"]["template"]["spec"]
+            pspec["volumes"] = [{"name": "rocprof", "hostPath": {"path": str(prof_dir), "type": "DirectoryOrCreate"}}]
+            pspec["containers"][0]["volumeMounts"] = [{"name": "rocprof", "mountPath": str(prof_dir)}]
         apply_objects(k, objs)
         self.out(f"Running RCCL all-reduce over {g} GPU(s) (job kube-system/{job}, {npods} pod(s) x {per_pod} GPU(s)"
                  + (", one process per host" if layout["scope"] == "host" else "") + ")")

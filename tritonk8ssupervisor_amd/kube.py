@@ -117,7 +117,14 @@ def object_path(kind: str, name: str, ns: str = "default") -> str:
 
 
 def load_manifests(path: str | Path, variables: dict | None = None) -> list[dict]:
-    docs = [d for d in yamlio.load_all(Path(path).read_text()) if d]
+    """The objects of a manifest file (``-``: standard input, as ``kubectl apply -f -``)."""
+    if str(path) == "-":
+        import sys
+
+        text = sys.stdin.read()
+    else:
+        text = Path(path).read_text()
+    docs = [d for d in yamlio.load_all(text) if d]
     if variables:
         docs = templating.render(docs, variables)
     out = []

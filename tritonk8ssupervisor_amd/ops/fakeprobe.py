@@ -83,7 +83,11 @@ def main():
         return 139  # the burn-in dies without a result; the validation pod must probe by itself
     if os.environ.get("TK8S_FAKE_PROBE_HANG", "") == node:
         time.sleep(3600)  # a wedged validation (the analogue of the reference's stuck dashboard)
-    n = len([x for x in (os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES", "")).split(",") if x])
+    visible = [x for x in (os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES", "")).split(",") if x]
+    n = len(visible)
+    # the fake inventory's bus ids (models/hostinfo.py, ops/fakesmi.py: 0x10 + host ordinal), as
+    # the real probe reports the devices' own: the agent joins probe, SMI and inventory on them
+    bus = [0x10 + int(x) if x.isdigit() else i for i, x in enumerate(visible)]
     fail = os.environ.get("TK8S_FAKE_PROBE_FAIL", "") == node
     dev = {"ok": not fail, "hbm": {"ok": True, "gbps": 6200.0}, "md5": {"ok": True, "mbps": 2.3e6}}
     devices = [dict(dev, device=i) for i in range(n)]
@@ -95,7 +99,7 @@ def main():
             d["peers_ok"] = True
     out = {"ok": not fail, "fake": True, "device_count": n, "probed": n, "devices": devices,
            "hbm": dev["hbm"], "md5": dev["md5"],
-           "gpuinfo": {"ok": True, "device_count": n, "devices": [{"index": i, "gfx": "gfx950", "pci_bus_id": f"0000:{i:02x}:00.0",
+           "gpuinfo": {"ok": True, "device_count": n, "devices": [{"index": i, "gfx": "gfx950", "pci_bus_id": f"0000:{bus[i]:02x}:00.0",
                                                                     "uuid": f"fake-{i}"} for i in range(n)]}}
     _emit(out, _arg("--out"))
     return 0 if not fail else 1

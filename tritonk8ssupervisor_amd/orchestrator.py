@@ -57,6 +57,7 @@ def playbook_extra_vars(ws: Workspace, cfg: ClusterConfig, machines: dict[str, M
         "tk8s_master_port": int(cfg.TK8S_MASTER_PORT),
         "tk8s_bind_host": m.primaryip,
         "tk8s_cp_state_dir": str(Path(m.sandbox) / "controlplane"),
+        "tk8s_admin_token_file": str(ws.admin_token_file),
         "tk8s_node_grace": node_grace,
         "tk8s_controlplane_argv": controlplane_argv(m.primaryip, int(cfg.TK8S_MASTER_PORT), m.primaryip,
                                                     str(Path(m.sandbox) / "controlplane"), node_grace),
@@ -388,7 +389,7 @@ class Setup(KubeadmPlatform, FabricCheck):
         from .controlplane.client import Client
 
         m = self.engine.machines()[self.cfg.RANCHER_MASTER_HOSTNAME]
-        return Client(f"{m.primaryip}:{self.cfg.TK8S_MASTER_PORT}", timeout=30.0)
+        return Client(f"{m.primaryip}:{self.cfg.TK8S_MASTER_PORT}", token=self.ws.admin_token(), timeout=30.0)
 
     def project_id(self) -> str:
         return self.ws.env_id_file.read_text().strip()
@@ -665,7 +666,7 @@ class Setup(KubeadmPlatform, FabricCheck):
     def _write_kubeconfig(self, base: str, pid: str) -> None:
         from .controlplane.client import Client
 
-        kc = Client(base).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
+        kc = Client(base, token=self.ws.admin_token()).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
         atomic_write_json(self.ws.state_dir / "kubeconfig.json", kc)
 
 

@@ -28,15 +28,36 @@ import time
 import urllib.request
 
 
+SA_TOKEN = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+
+
+def _kv_headers() -> dict:
+    """The pod's ServiceAccount token (the control plane's KV answers no anonymous caller):
+    TK8S_KV_TOKEN, else the token file the agent mounted (process pods name it in
+    TK8S_SERVICEACCOUNT_TOKEN_FILE, image pods have it at the Kubernetes path)."""
+    tok = os.environ.get("TK8S_KV_TOKEN", "")
+    for path in (os.environ.get("TK8S_SERVICEACCOUNT_TOKEN_FILE", ""), SA_TOKEN):
+        if tok or not path:
+            continue
+        try:
+            with open(path) as f:
+                tok = f.read().strip()
+        except OSError:
+            pass
+    return {"Authorization": f"Bearer {tok}"} if tok else {}
+
+
 def _publish(url: str, value: str) -> None:
-    urllib.request.urlopen(urllib.request.Request(url, data=value.encode(), method="PUT"), timeout=10).read()
+    urllib.request.urlopen(urllib.request.Request(url, data=value.encode(), method="PUT", headers=_kv_headers()),
+                           timeout=10).read()
 
 
 def _fetch(url: str, timeout: float) -> str:
     deadline = time.monotonic() + timeout
     while time.monotonic() < deadline:
         try:
-            v = urllib.request.urlopen(url + "?wait=10", timeout=15).read().decode().strip()
+            v = urllib.request.urlopen(urllib.request.Request(url + "?wait=10", headers=_kv_headers()),
+                                       timeout=15).read().decode().strip()
             if v:
                 return v
         except OSError:

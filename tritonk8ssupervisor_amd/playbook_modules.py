@@ -669,7 +669,8 @@ def _artefacts(bn) -> dict:
 
 
 def m_tk8s_kube(args, *, ctx, check, **_):
-    """api, project, state present|absent|wait, definition|src, timeout."""
+    """api, project, token (the control plane's admin token), state present|absent|wait,
+    definition|src, timeout."""
     from .controlplane.client import ApiError, Client
     from .kube import apply_objects, delete_objects, load_manifests
 
@@ -684,7 +685,8 @@ def m_tk8s_kube(args, *, ctx, check, **_):
         return {"changed": state != "wait", "objects": len(objs), "msg": "check mode"}
     api = str(args["api"])
     pid = str(args["project"])
-    kc = Client(api).get(f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
+    kc = Client(api, token=str(args["token"]) if args.get("token") else None).get(
+        f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
     k = client_from_kubeconfig(kc)
     try:
         if state == "absent":

@@ -73,6 +73,7 @@ def clean(ws: Workspace, *, assume_yes: bool = False, inp=None, out=print,
         _set_ini_value(ws.ansible / "ansible.cfg", "private_key_file", "")
     remove_paths([ws.ansible / "hosts", ws.vars_file, *ws.ansible.glob("*.retry"), *(p for p in (ws.ansible / "tmp").glob("*") if not p.name.startswith(".")),
                   ws.config, ws.state_dir / "machines", ws.state_dir / "alloc.json", ws.state_dir / "alloc.lock",
-                  ws.state_dir / "state.json", ws.state_dir / "kubeconfig.json", ws.state_dir / "ansible.log"])
+                  ws.state_dir / "state.json", ws.state_dir / "kubeconfig.json", ws.state_dir / "ansible.log",
+                  ws.admin_token_file])
     out("    All clear!")
     return 0

@@ -51,6 +51,15 @@ class Workspace:
     def env_id_file(self) -> Path: return self.ansible / "tmp" / "kubernetes_environment.id"
     @property
     def vars_file(self) -> Path: return self.ansible / "roles" / "ranchermaster" / "vars" / "vars.yml"
+    @property
+    def admin_token_file(self) -> Path: return self.state_dir / "admin-token"
+
+    def admin_token(self) -> str | None:
+        """The control plane's admin token, as ranchermaster keeps it (controlplane/authn.py)."""
+        try:
+            return self.admin_token_file.read_text().strip() or None
+        except OSError:
+            return None
 
     def state(self) -> dict:
         return read_json(self.state_file, {}) or {}
