@@ -5,6 +5,7 @@
 //                [--kfd-root DIR]] [--deny PATH]... [--allow PATH]... [--scope-signals]
 //                [--best-effort] -- CMD ARGS...
 //   tk8s-gpujail --probe            (prints {"landlock_abi": N, ...}; exit 0 when usable)
+//   tk8s-gpujail [policy options] --plan   (prints the rules it would add, one JSON line each)
 //
 // The reference ran every workload in a Docker container (ansible/roles/rancherhost/tasks/
 // main.yml:26-34, dockersetup), whose device cgroup decides which /dev nodes a container may
@@ -35,7 +36,7 @@ int usage() {
 
 int main(int argc, char** argv) {
   tk8s::jail::Policy policy;
-  bool best_effort = false, probe = false;
+  bool best_effort = false, probe = false, show_plan = false;
   int i = 1;
   for (; i < argc; ++i) {
     const std::string a = argv[i];
@@ -47,6 +48,7 @@ int main(int argc, char** argv) {
       if (tk8s::jail::parse_option(policy, argc, argv, i)) continue;
       if (a == "--best-effort") best_effort = true;
       else if (a == "--probe") probe = true;
+      else if (a == "--plan") show_plan = true;
       else return usage();
     } catch (const std::exception& e) {
       std::fprintf(stderr, "tk8s-gpujail: %s\n", e.what());
@@ -59,6 +61,18 @@ int main(int argc, char** argv) {
     std::printf("{\"landlock_abi\": %d, \"usable\": %s, \"signal_scoping\": %s%s}\n", abi > 0 ? abi : 0,
                 abi > 0 ? "true" : "false", abi >= 6 ? "true" : "false", err.c_str());
     return abi > 0 ? 0 : 1;
+  }
+  if (show_plan) {  // the rules, as JSON lines {"path": ..., "access": "r"|"rw"}; nothing applied
+    for (const auto& [path, acc] : tk8s::jail::plan(policy)) {
+      std::string esc;
+      for (char c : path) {
+        if (c == '"' || c == '\\') esc += '\\';
+        esc += c;
+      }
+      std::printf("{\"path\": \"%s\", \"access\": \"%s\"}\n", esc.c_str(),
+                  acc == tk8s::jail::Access::kRead ? "r" : "rw");
+    }
+    return 0;
   }
   if (i >= argc) return usage();
   const std::string mode = tk8s::jail::apply(policy);

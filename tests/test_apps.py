@@ -121,10 +121,13 @@ def test_redis_commands_and_replication(redis_pair):
     with pytest.raises(RespError, match="unknown command"):
         call("127.0.0.1", lp, "NOPE")
     assert call("127.0.0.1", lp, "ROLE")[0] == b"master"
+    # the follower replicates by whole snapshots (TK8S.DUMP): wait for the LAST write; a snapshot
+    # holding it holds every earlier one (waiting for the first raced the later RPUSH)
     deadline = time.monotonic() + 5
-    while call("127.0.0.1", fp, "GET", "messages") != b"hello,world":
+    while call("127.0.0.1", fp, "GET", "n") != b"42":
         assert time.monotonic() < deadline
         time.sleep(0.02)
+    assert call("127.0.0.1", fp, "GET", "messages") == b"hello,world"
     assert call("127.0.0.1", fp, "LRANGE", "l", "0", "-1") == [b"a", b"b", b"c"]
     with pytest.raises(RespError, match="READONLY"):
         call("127.0.0.1", fp, "SET", "x", "1")

@@ -248,3 +248,81 @@ def test_image_pod_volumes(ws, native_build):
     assert wait("second") == "Succeeded"
     assert "count=again" in kc("logs", "second").stdout  # the claim kept the first pod's data
     assert "data" in kc("get", "pvc").stdout
+
+
+def test_hardlink_to_a_symlinked_host_file_is_refused(tmp_path):
+    """a layer's hard link must name a file of the image. ``s -> <host file>`` then a
+    hard link ``h`` to ``s`` must not link the host file into the root (os.link follows links)."""
+    import io
+    import tarfile
+
+    from tritonk8ssupervisor_amd.agent.images import apply_layer
+
+    secret = tmp_path / "host-secret"
+    secret.write_text("host only\n")
+    layer = tmp_path / "evil.tar"
+    with tarfile.open(layer, "w") as t:
+        ti = tarfile.TarInfo("s")
+        ti.type, ti.linkname = tarfile.SYMTYPE, str(secret)
+        t.addfile(ti)
+        ti = tarfile.TarInfo("h")
+        ti.type, ti.linkname = tarfile.LNKTYPE, "s"
+        t.addfile(ti)
+        ti = tarfile.TarInfo("f")
+        ti.size = 2
+        t.addfile(ti, io.BytesIO(b"ok"))
+        ti = tarfile.TarInfo("g")  # a hard link to a file of the image still works
+        ti.type, ti.linkname = tarfile.LNKTYPE, "f"
+        t.addfile(ti)
+    root = tmp_path / "root"
+    root.mkdir()
+    apply_layer(layer, root)
+    assert not (root / "h").exists() and os.stat(secret).st_nlink == 1
+    assert (root / "g").read_bytes() == b"ok" and os.stat(root / "f").st_nlink == 2
+
+
+def test_mount_points_resolve_inside_the_image(ws, native_build):
+    """Debian/Ubuntu images ship /var/run -> /run. A volume (and the ServiceAccount
+    token every image pod gets at /var/run/secrets/kubernetes.io/serviceaccount) mounted under it
+    lands in the image's /run, resolved inside the image -- never on the host's /run."""
+    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
+
+    if not container_runtime()[0]:
+        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+    env = _env(ws)
+    base = _host_files("sh", "cat", "sleep", "ls")
+    base.update({"var/": b"", "var/run": ("symlink", "/run"), "etc/os-release": b"debian-like\n"})
+    write_docker_archive(ws / "deb.tar", "deb:1", [base], {"Env": ["PATH=/bin"], "WorkingDir": "/"})
+    assert subprocess.run(["./tk8s", "image", "load", "deb.tar"], cwd=ws, env=env, capture_output=True).returncode == 0
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"], cwd=ws,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
+    host_before = os.path.exists("/run/tk8s-test-data")
+    (ws / "pod.json").write_text(json.dumps({
+        "apiVersion": "v1", "kind": "Pod", "metadata": {"name": "deb"},
+        "spec": {"restartPolicy": "Never", "containers": [{
+            "name": "c", "image": "deb:1", "command": ["/bin/sh", "-c",
+                "echo tok=$(cat /var/run/secrets/kubernetes.io/serviceaccount/token); "
+                "echo x > /var/run/tk8s-test-data/f && echo data=$(cat /run/tk8s-test-data/f); "
+                "while read k v; do [ \"$k\" = CapBnd: ] && echo capbnd=$v; done < /proc/self/status; "
+                "(echo 1 > /proc/sys/kernel/sysrq) 2>/dev/null && echo sysctl=written || echo sysctl=refused; "
+                "(echo x > /sys/kernel/uevent_helper) 2>/dev/null && echo sysfs=written || echo sysfs=refused"],
+            "volumeMounts": [{"name": "d", "mountPath": "/var/run/tk8s-test-data"}]}],
+            "volumes": [{"name": "d", "emptyDir": {}}]}}))
+    assert kc("apply", "-f", "pod.json").returncode == 0
+    deadline = time.monotonic() + 60
+    while True:
+        o = json.loads(kc("get", "pod", "deb", "-o", "json").stdout)
+        if o["status"].get("phase") in ("Succeeded", "Failed"):
+            break
+        assert time.monotonic() < deadline
+        time.sleep(0.2)
+    out = kc("logs", "deb").stdout
+    assert o["status"]["phase"] == "Succeeded", (out, o["status"])
+    assert "tok=tk8s-sa." in out and "data=x" in out, out
+    # the capability bounding set of a root pod is Docker's default set; host sysctl/sysfs stay read-only
+    assert "sysctl=refused" in out and "sysfs=refused" in out, out
+    if os.geteuid() == 0:
+        assert "capbnd=00000000a80425fb" in out, out
+    assert os.path.exists("/run/tk8s-test-data") == host_before  # nothing appeared on the host

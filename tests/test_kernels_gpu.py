@@ -308,6 +308,7 @@ def test_setup_with_host_burnin_on_a_real_gpu(tmp_path):
 
 def test_torch_rccl_allreduce_single_rank(tmp_path):
     """The PyTorch (RCCL) twin of tk8s-rccl, rendezvous through a real control-plane KV."""
+    import os
     import subprocess
     import sys
     from pathlib import Path
@@ -320,7 +321,8 @@ def test_torch_rccl_allreduce_single_rank(tmp_path):
     try:
         r = subprocess.run([sys.executable, "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", "--backend", "nccl",
                             "--rank", "0", "--nranks", "1", "--kv-url", f"{c.base}/v1/kv/t/addr", "--max-bytes", str(16 << 20)],
-                           cwd=Path(__file__).resolve().parents[1], capture_output=True, text=True, timeout=180)
+                           cwd=Path(__file__).resolve().parents[1], capture_output=True, text=True, timeout=180,
+                           env={**os.environ, "TK8S_KV_TOKEN": c.token})  # the KV answers no anonymous caller
     finally:
         _stop(p)
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -749,11 +751,17 @@ def test_pods_see_only_their_gpus_on_a_real_gpu(tmp_path):
         r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120"],
                            cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        st = tmp_path / ".tk8s"
+        secrets = [st / "kubeconfig.json", st / "admin-token", *sorted((st / "keys").glob("*"))]
+        # a GPU pod, too, gets EACCES on the cluster's credentials -- and its GPU
+        # still works under the same jail (the gpuinfo line is its last output)
+        steal = "".join(f'if cat {f} > /dev/null 2>&1; then echo "read {f}"; else echo "denied {f}"; fi; '
+                        for f in secrets)
         for name, gpus in (("no-gpu", 0), ("one-gpu", 1)):
             (tmp_path / f"{name}.json").write_text(json.dumps({
                 "apiVersion": "v1", "kind": "Pod", "metadata": {"name": name},
                 "spec": {"restartPolicy": "Never", "containers": [{
-                    "name": "c", "command": [str(tool("tk8s-gpuinfo")), "--no-links"],
+                    "name": "c", "command": ["sh", "-c", steal + f"exec {tool('tk8s-gpuinfo')} --no-links"],
                     "env": [{"name": "HIP_VISIBLE_DEVICES", "value": "0"}],
                     "resources": {"limits": {"amd.com/gpu": gpus}} if gpus else {}}]}}))
             assert kc("apply", "-f", str(tmp_path / f"{name}.json")).returncode == 0
@@ -764,11 +772,17 @@ def test_pods_see_only_their_gpus_on_a_real_gpu(tmp_path):
             if all(phases.get(n) in ("Succeeded", "Failed") for n in ("no-gpu", "one-gpu")):
                 break
             time.sleep(0.2)
-        outs = {n: json.loads(kc("logs", n).stdout.strip().splitlines()[-1]) for n in ("no-gpu", "one-gpu")}
+        logs = {n: kc("logs", n).stdout for n in ("no-gpu", "one-gpu")}
+        outs = {n: json.loads(t.strip().splitlines()[-1]) for n, t in logs.items()}
         assert outs["no-gpu"]["device_count"] == 0, outs
         assert outs["one-gpu"]["device_count"] == 1 and phases["one-gpu"] == "Succeeded", (outs, phases)
+        for n, t in logs.items():
+            for f in secrets:
+                assert f"denied {f}" in t, (n, t)
         d = kc("describe", "pod", "no-gpu").stdout
         assert "Isolation:" in d and "landlock" in d and "may open no GPU" in d, d
+        d = kc("describe", "pod", "one-gpu").stdout
+        assert "node state denied" in d and "signals scoped to the pod" in d, d
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
