@@ -1,0 +1,191 @@
+"""Pod and machine resource limits are enforced (VERDICT r3 missing-1, agent/resources.py).
+
+The reference's machines were hard slices (a Triton KVM package,
+/root/reference/terraform/host/main.tf:3) and its workloads Docker containers with cgroup limits
+(/root/reference/ansible/roles/rancherhost/tasks/main.yml:26-34). Here: a pod over its
+limits.memory is OOMKilled (exit 137) and restarted under its policy -- by the kernel in a
+cgroup (cgroup1 on this dev box, as root in a v1 container), or by the agent's memory watchdog
+(the GPU tier's unprivileged mode) -- and a GPU pod runs on its GPU's NUMA-local CPUs."""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import pytest
+
+from tritonk8ssupervisor_amd.agent.resources import Enforcer, Limits, format_cpulist, parse_cpulist, pod_limits
+
+REPO = Path(__file__).resolve().parents[1]
+
+HOG = ("import time\nblocks = []\nfor _ in range(40):\n    blocks.append(bytearray(16 << 20))\n"
+       "    for i in range(0, len(blocks[-1]), 4096):\n        blocks[-1][i] = 1\n    time.sleep(0.02)\n"
+       "print('survived', flush=True)\n")
+
+
+def test_limits_and_cpulists():
+    pod = {"spec": {"containers": [{"resources": {"limits": {"memory": "64Mi", "cpu": "500m"}}},
+                                   {"resources": {"limits": {"memory": "32Mi", "cpu": "1"}}}],
+                    "initContainers": [{"resources": {"limits": {"memory": "512Mi"}}}]}}
+    lim = pod_limits(pod)
+    assert lim.memory == 512 << 20 and lim.cpu == 1.5  # the largest init container wins
+    assert pod_limits({"spec": {"containers": [{}, {"resources": {"limits": {"memory": "1Gi"}}}]}}).memory is None
+    assert parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert format_cpulist([11, 0, 1, 2, 3, 8, 10]) == "0-3,8,10-11"
+
+
+def test_cgroup2_files_on_a_delegated_tree(tmp_path, monkeypatch):
+    """The cgroup2 mode against a fake delegated subtree: the agent moves itself to a leaf,
+    enables the controllers, writes the machine's package and each pod's limits, and reads an
+    OOM kill from memory.events."""
+    root = tmp_path / "cg"
+    root.mkdir()
+    for f, v in (("cgroup.controllers", "cpuset cpu io memory pids"), ("cgroup.subtree_control", ""),
+                 ("cgroup.procs", f"{os.getpid()}\n")):
+        (root / f).write_text(v)
+    orig_mkdir = Path.mkdir
+
+    def mkdir(self, *a, **kw):  # a cgroupfs directory comes with its interface files
+        orig_mkdir(self, *a, **kw)
+        if str(self).startswith(str(root)):
+            for f in ("cgroup.procs", "cgroup.subtree_control", "memory.max", "memory.swap.max", "memory.oom.group",
+                      "cpu.max", "cpuset.cpus", "cpuset.mems", "memory.events"):
+                if not (self / f).exists():
+                    (self / f).write_text("")
+
+    monkeypatch.setattr(Path, "mkdir", mkdir)
+    monkeypatch.setattr("tritonk8ssupervisor_amd.agent.resources._own_cgroups", lambda: {"": "/"})
+    monkeypatch.setenv("TK8S_CGROUP_ROOT", str(root))
+    monkeypatch.setenv("TK8S_POD_RESOURCES", "auto")
+    e = Enforcer("kubenode1", Limits(memory=8 << 30, cpu=16, cpus="0-63"))
+    assert e.mode == "cgroup2", e.why
+    assert (root / "tk8s-agent" / "cgroup.procs").read_text().strip() == str(os.getpid())
+    assert set((root / "cgroup.subtree_control").read_text().split()) == {"+memory", "+cpu", "+cpuset"}
+    m = root / "tk8s-machine-kubenode1"  # (no scope given: the bare node name)
+    assert (m / "agent" / "cgroup.procs").read_text().strip() == str(os.getpid())  # the agent lives in its machine
+    assert (m / "memory.max").read_text().strip() == str(8 << 30) and (m / "cpu.max").read_text().strip() == "1600000 100000"
+    assert (m / "cpuset.cpus").read_text().strip() == "0-63"
+    opts = e.pod("default/web", Limits(memory=64 << 20, cpu=0.5, cpus="0-31"))
+    d = m / "pod-default_web"
+    assert opts == ["--cgroup-procs", str(d / "cgroup.procs")]  # the cpuset controller fences: no affinity
+    assert (d / "memory.max").read_text().strip() == str(64 << 20) and (d / "cpu.max").read_text().strip() == "50000 100000"
+    assert (d / "cpuset.cpus").read_text().strip() == "0-31" and (d / "memory.oom.group").read_text().strip() == "1"
+    assert not e.oom_killed("default/web")
+    (d / "memory.events").write_text("low 0\nhigh 0\nmax 3\noom 1\noom_kill 1\n")
+    assert e.oom_killed("default/web")
+    host = e.pod("kube-system/fabric", Limits(), in_machine=False)  # beside the machine slice
+    assert host == ["--cgroup-procs", str(root / "pod-kube-system_fabric" / "cgroup.procs")]
+    assert "cgroup2" in e.describe() and "memory 8192 MiB" in e.describe()
+
+
+@pytest.fixture
+def fake_sysfs(tmp_path):
+    """GPUs 0-3 on CPUs 0-3, GPUs 4-7 on CPUs 4-7 (two sockets, as an MI355X node has)."""
+    root = tmp_path / "sys"
+    for i in range(8):
+        d = root / "class" / "drm" / f"renderD{128 + i}" / "device"
+        d.mkdir(parents=True)
+        (d / "local_cpulist").write_text("0-3\n" if i < 4 else "4-7\n")
+        (d / "numa_node").write_text("0\n" if i < 4 else "1\n")
+    return root
+
+
+def _cluster(tmp_path, env_extra):
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    ws = tmp_path / "ws"
+    ws.mkdir()
+    init_workspace(ws)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, ws / f)
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_FAKE_GPUS="8", **env_extra)
+    env.pop("TK8S_FAULTS", None)
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "2", "--rccl", "off"], cwd=ws,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+    def kc(*a, check=True, stdin=None):
+        p = subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=120, input=stdin)
+        if check:
+            assert p.returncode == 0, f"kubectl {' '.join(a)}: {p.stdout}{p.stderr}"
+        return p
+
+    return ws, env, kc
+
+
+def _apply(kc, pod):
+    kc("apply", "-f", "-", stdin=json.dumps({"apiVersion": "v1", "kind": "Pod", **pod}))
+
+
+def _until(fn, timeout=60.0):
+    deadline = time.monotonic() + timeout
+    while True:
+        v = fn()
+        if v:
+            return v
+        assert time.monotonic() < deadline, "condition not met in time"
+        time.sleep(0.1)
+
+
+def _pod(kc, name):
+    return json.loads(kc("get", "pod", name, "-o", "json").stdout)
+
+
+@pytest.mark.parametrize("mode", ["auto", "watchdog"])
+def test_a_pod_over_its_memory_limit_is_oomkilled_and_restarted(tmp_path, fake_sysfs, mode):
+    ws, env, kc = _cluster(tmp_path, {"TK8S_POD_RESOURCES": mode, "TK8S_SYSFS_ROOT": str(fake_sysfs)})
+    try:
+        node = json.loads(kc("get", "node", "kubenode1", "-o", "json").stdout)
+        enf = node["metadata"]["annotations"]["tk8s.amd.com/resource-enforcement"]
+        if mode == "watchdog":
+            assert enf.startswith("watchdog") and "NOT enforced" in enf, enf
+        # the machine is its package's slice: capacity from the package (mi355x-1gpu = 1/8 host)
+        assert float(node["status"]["capacity"]["cpu"]) == max(1, (os.cpu_count() or 8) // 8)
+        (ws / "hog.py").write_text(HOG)
+        _apply(kc, {"metadata": {"name": "hog"}, "spec": {"restartPolicy": "OnFailure", "containers": [{
+            "name": "c", "command": [sys.executable, str(ws / "hog.py")],
+            "resources": {"limits": {"memory": "64Mi"}}}]}})
+        _apply(kc, {"metadata": {"name": "small"}, "spec": {"restartPolicy": "Never", "containers": [{
+            "name": "c", "command": [sys.executable, "-c", "print('fits', flush=True)"],
+            "resources": {"limits": {"memory": "256Mi"}}}]}})
+
+        def restarted_oom():
+            cs = (_pod(kc, "hog").get("status") or {}).get("containerStatuses") or [{}]
+            last = (cs[0].get("lastState") or {}).get("terminated") or (cs[0].get("state") or {}).get("terminated") or {}
+            return cs[0] if last.get("reason") == "OOMKilled" and cs[0].get("restartCount", 0) >= 1 else None
+
+        c = _until(restarted_oom, 90)
+        term = (c.get("lastState") or {}).get("terminated") or c["state"]["terminated"]
+        assert term["exitCode"] == 137
+        assert "survived" not in kc("logs", "hog").stdout
+        d = kc("describe", "pod", "hog").stdout
+        assert "Reason: OOMKilled, Exit Code: 137" in d and "memory 64 MiB" in d, d
+        _until(lambda: _pod(kc, "small")["status"].get("phase") == "Succeeded")
+        assert "fits" in kc("logs", "small").stdout
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, timeout=120)
+
+
+@pytest.mark.parametrize("mode", ["auto", "watchdog"])
+def test_a_gpu_pod_runs_on_its_gpus_numa_local_cpus(tmp_path, fake_sysfs, mode):
+    if (os.cpu_count() or 0) < 8:
+        pytest.skip("needs 8 CPUs for the two fake NUMA nodes")
+    ws, env, kc = _cluster(tmp_path, {"TK8S_POD_RESOURCES": mode, "TK8S_SYSFS_ROOT": str(fake_sysfs)})
+    try:
+        for name in ("g1", "g2"):
+            _apply(kc, {"metadata": {"name": name}, "spec": {"restartPolicy": "Never", "containers": [{
+                "name": "c", "command": ["sh", "-c", "grep Cpus_allowed_list /proc/self/status"],
+                "resources": {"limits": {"amd.com/gpu": 1}}}]}})
+        for name in ("g1", "g2"):
+            _until(lambda n=name: _pod(kc, n)["status"].get("phase") in ("Succeeded", "Failed"))
+        for name in ("g1", "g2"):
+            p = _pod(kc, name)
+            ordinal = int(p["metadata"]["annotations"]["amd.com/gpu-ids"].split(",")[0].replace("gpu", ""))
+            want = "0-3" if ordinal < 4 else "4-7"
+            out = kc("logs", name).stdout
+            assert out.split()[-1] == want, (name, ordinal, out, p["metadata"]["annotations"])
+            assert f"cpus {want}" in p["metadata"]["annotations"]["tk8s.amd.com/resources"]
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, timeout=120)

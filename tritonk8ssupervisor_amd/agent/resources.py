@@ -1,0 +1,404 @@
+"""Pod and machine resource limits, enforced (VERDICT r3 missing-1).
+
+The reference's nodes were hard slices: a Triton KVM ``package`` per machine
+(/root/reference/terraform/host/main.tf:3, chosen at /root/reference/setup.sh:402-449), and its
+workloads ran in Docker containers with cgroup limits
+(/root/reference/ansible/roles/rancherhost/tasks/main.yml:26-34). Here a worker is a sandbox of
+the MI355X host and a pod is a process group, so the agent enforces the shapes itself, in the
+strongest mode the host allows (``Enforcer.mode``):
+
+* ``cgroup2`` -- a writable (delegated) cgroup v2 subtree: a machine cgroup with the package's
+  ``memory.max`` / ``cpu.max`` / ``cpuset.cpus``, one cgroup per pod beneath it with the pod's
+  ``limits.memory`` / ``limits.cpu`` and, for GPU pods, ``cpuset.cpus`` = the NUMA-local CPUs of
+  its GPUs. The kernel throttles and OOM-kills; ``memory.events`` says which kill was an OOM.
+* ``cgroup1`` -- the same on writable v1 memory / cpu / cpuset hierarchies (root on a v1 host,
+  e.g. inside a container): ``memory.limit_in_bytes``, ``cpu.cfs_quota_us``, ``cpuset.cpus``.
+* ``watchdog`` -- unprivileged (the GPU tier: an ordinary user, no delegation): GPU pods are
+  pinned to their GPUs' NUMA-local CPUs (``sched_setaffinity``; a pod may widen its own
+  affinity, so this is placement, not a fence), and a memory watchdog samples every pod's
+  resident set and kills a pod over its ``limits.memory`` (``OOMKilled``, exit 137, restarted
+  under its policy). CPU limits are not enforced in this mode and ``describe node`` says so.
+
+Processes join their cgroups and CPUs inside the pod jail before anything runs
+(``tk8s-gpujail --cgroup-procs/--cpus``, gpujail.h ``join_limits``), so no process of a pod ever
+runs outside them. ``TK8S_POD_RESOURCES`` = auto|cgroup2|cgroup1|watchdog|none picks the mode;
+``TK8S_CGROUP_ROOT`` and ``TK8S_SYSFS_ROOT`` point at other trees (the CPU tests' fakes).
+"""
+from __future__ import annotations
+
+import os
+import re
+import signal
+import threading
+import time
+from pathlib import Path
+
+from ..utils import quantity
+from ..utils.record import record as dataclass
+
+CFS_PERIOD_US = 100_000
+_NAME = re.compile(r"[^A-Za-z0-9_.-]")
+
+
+@dataclass
+class Limits:
+    memory: int | None = None    # bytes (limits.memory)
+    cpu: float | None = None     # cores (limits.cpu)
+    cpus: str = ""               # cpuset / affinity list ("0-63,128-191"), "" = any
+
+
+def pod_limits(pod: dict) -> Limits:
+    """The pod's cgroup limits, as the kubelet sizes the pod cgroup: the sum over its app
+    containers when every one has the limit, at least the largest init container's."""
+    spec = pod.get("spec") or {}
+
+    def total(kind: str, parse) -> float | None:
+        vals = [((c.get("resources") or {}).get("limits") or {}).get(kind) for c in spec.get("containers") or []]
+        if not vals or any(v is None for v in vals):
+            return None
+        s = sum(parse(v) for v in vals)
+        inits = [((c.get("resources") or {}).get("limits") or {}).get(kind) for c in spec.get("initContainers") or []]
+        return max([s] + [parse(v) for v in inits if v is not None])
+
+    mem = total("memory", quantity.parse)
+    cpu = total("cpu", quantity.parse)
+    return Limits(memory=int(mem) if mem is not None else None, cpu=cpu)
+
+
+def parse_cpulist(text: str) -> list[int]:
+    out: list[int] = []
+    for part in (text or "").strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        out += range(int(lo), int(hi or lo) + 1)
+    return out
+
+
+def format_cpulist(cpus) -> str:
+    cpus = sorted(set(cpus))
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def sysfs_root() -> Path:
+    return Path(os.environ.get("TK8S_SYSFS_ROOT", "/sys"))
+
+
+def gpu_local_cpus(render_minors) -> str:
+    """The CPUs NUMA-local to these GPUs (``/sys/class/drm/renderD<m>/device/local_cpulist``),
+    as one list; "" when unknown. On an MI355X node, GPUs 0-3 sit on socket 0 and 4-7 on 1."""
+    cpus: set[int] = set()
+    for m in render_minors:
+        if m is None or int(m) < 0:
+            continue
+        try:
+            cpus |= set(parse_cpulist((sysfs_root() / "class" / "drm" / f"renderD{int(m)}" / "device" /
+                                       "local_cpulist").read_text()))
+        except (OSError, ValueError):
+            continue
+    return format_cpulist(cpus) if cpus else ""
+
+
+def _own_cgroups() -> dict[str, str]:
+    """controller (or "" for v2) -> this process's cgroup path, from /proc/self/cgroup."""
+    out = {}
+    try:
+        for line in Path("/proc/self/cgroup").read_text().splitlines():
+            _, ctrls, path = line.split(":", 2)
+            for c in (ctrls.split(",") if ctrls else [""]):
+                out[c] = path
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _sweep(parent: Path) -> None:
+    """Remove the machine cgroups under ``parent`` that hold no process any more (an agent killed
+    before it could clean up): rmdir of a cgroup fails while anything lives in it, and a live
+    agent lives in its own machine's (``Enforcer``), so a live cluster's cgroups stay."""
+    def live(m: Path) -> bool:  # its agent still runs in it (v1: the machine itself, v2: its leaf)
+        for f in (m / "cgroup.procs", m / "agent" / "cgroup.procs"):
+            try:
+                if f.read_text().split():
+                    return True
+            except OSError:
+                pass
+        return False
+
+    try:
+        for m in parent.glob("tk8s-machine-*"):
+            if live(m):
+                continue
+            for d in m.glob("pod-*"):
+                try:
+                    os.rmdir(d)
+                except OSError:
+                    pass
+            try:
+                os.rmdir(m)
+            except OSError:
+                pass
+    except OSError:
+        pass
+
+
+def _write(path: Path, value) -> None:
+    with open(path, "w") as f:
+        f.write(f"{value}\n")
+
+
+class Enforcer:
+    """One per node agent: ``pod(key, limits)`` before a pod starts (its cgroup, the jail options
+    that put it there), ``oom_killed(key)`` after a container exits, ``release(key)`` when the pod
+    is gone; ``watch(...)`` runs the memory watchdog (watchdog mode)."""
+
+    def __init__(self, node: str, machine: Limits | None = None, scope: str = ""):
+        # the machine cgroup's name: the node's, plus a hash of ``scope`` (its sandbox) -- clusters
+        # side by side on one host may each have a kubenode1
+        import hashlib
+
+        self.node = _NAME.sub("_", node) + (f"-{hashlib.sha1(scope.encode()).hexdigest()[:8]}" if scope else "")
+        self.machine = machine or Limits()
+        self.root = Path(os.environ.get("TK8S_CGROUP_ROOT", "/sys/fs/cgroup"))
+        self.mode, self.why = "none", ""
+        self.base: dict[str, Path] = {}    # controller -> the machine cgroup ("" = v2)
+        self.pods: dict[str, dict[str, Path]] = {}
+        self.limits: dict[str, Limits] = {}
+        self.oom: set[str] = set()          # pods the watchdog killed for memory
+        self.lock = threading.Lock()
+        want = os.environ.get("TK8S_POD_RESOURCES", "auto")
+        if want == "none":
+            self.why = "disabled (TK8S_POD_RESOURCES=none)"
+            return
+        for mode in (("cgroup2", "cgroup1", "watchdog") if want == "auto" else (want,)):
+            try:
+                if getattr(self, f"_setup_{mode}")():
+                    self.mode = mode
+                    return
+            except OSError as e:
+                self.why += f"{mode}: {e}; "
+        if self.mode == "none":
+            self.why = self.why or "no mode available"
+
+    # ---- modes -----------------------------------------------------------------------------
+    def _setup_cgroup2(self) -> bool:
+        if not (self.root / "cgroup.controllers").exists():
+            self.why += "cgroup2: not a unified hierarchy; "
+            return False
+        own = self.root / _own_cgroups().get("", "/").lstrip("/")
+        have = set((own / "cgroup.controllers").read_text().split())
+        if not {"memory", "cpu"} <= have or not os.access(own / "cgroup.subtree_control", os.W_OK):
+            self.why += f"cgroup2: {own} is not delegated to this user (controllers {sorted(have)}); "
+            return False
+        # no internal processes: this agent (and whatever shares its cgroup) moves to a leaf first
+        leaf = own / "tk8s-agent"
+        leaf.mkdir(exist_ok=True)
+        for pid in (own / "cgroup.procs").read_text().split():
+            try:
+                _write(leaf / "cgroup.procs", pid)
+            except OSError:
+                pass
+        ctrls = [c for c in ("memory", "cpu", "cpuset") if c in have]
+        _write(own / "cgroup.subtree_control", " ".join(f"+{c}" for c in ctrls))
+        _sweep(own)
+        m = own / f"tk8s-machine-{self.node}"
+        m.mkdir(exist_ok=True)
+        (m / "agent").mkdir(exist_ok=True)  # the agent lives in its machine (a leaf: no internal processes)
+        _write(m / "agent" / "cgroup.procs", os.getpid())
+        _write(m / "cgroup.subtree_control", " ".join(f"+{c}" for c in ctrls))
+        self._limit(m, "", self.machine)
+        self.base = {"": m}
+        return True
+
+    def _setup_cgroup1(self) -> bool:
+        own = _own_cgroups()
+        base = {}
+        for c in ("memory", "cpu", "cpuset"):
+            hier = self.root / c
+            if c not in own or not (hier / "cgroup.procs").exists():
+                continue
+            d = hier / own[c].lstrip("/")
+            if not os.access(d, os.W_OK):
+                continue
+            _sweep(d)
+            m = d / f"tk8s-machine-{self.node}"
+            m.mkdir(exist_ok=True)
+            if c == "cpuset":  # a v1 cpuset starts empty: inherit the parent's before any task joins
+                for f in ("cpuset.cpus", "cpuset.mems"):
+                    if not (m / f).read_text().strip():
+                        _write(m / f, (d / f).read_text().strip())
+            base[c] = m
+        if "memory" not in base:
+            self.why += "cgroup1: no writable memory hierarchy; "
+            return False
+        self.base = base
+        for c, m in base.items():
+            self._limit(m, c, self.machine)
+            _write(m / "cgroup.procs", os.getpid())  # the agent lives in its machine: no sweep takes it
+        return True
+
+    def _setup_watchdog(self) -> bool:
+        return True
+
+    # ---- limits ----------------------------------------------------------------------------
+    def _limit(self, d: Path, ctrl: str, lim: Limits) -> None:
+        """Write ``lim`` into cgroup ``d`` (``ctrl`` "" = v2, else the v1 controller)."""
+        if ctrl == "":
+            if lim.memory:
+                _write(d / "memory.max", int(lim.memory))
+                if (d / "memory.swap.max").exists():
+                    _write(d / "memory.swap.max", 0)
+                if (d / "memory.oom.group").exists():
+                    _write(d / "memory.oom.group", 1)  # an OOM kill takes the whole pod, as the kubelet sets it
+            if lim.cpu:
+                _write(d / "cpu.max", f"{max(1000, int(lim.cpu * CFS_PERIOD_US))} {CFS_PERIOD_US}")
+            if lim.cpus and (d / "cpuset.cpus").exists():
+                _write(d / "cpuset.cpus", lim.cpus)
+        elif ctrl == "memory" and lim.memory:
+            _write(d / "memory.limit_in_bytes", int(lim.memory))
+        elif ctrl == "cpu" and lim.cpu:
+            _write(d / "cpu.cfs_period_us", CFS_PERIOD_US)
+            _write(d / "cpu.cfs_quota_us", max(1000, int(lim.cpu * CFS_PERIOD_US)))
+        elif ctrl == "cpuset" and lim.cpus:
+            _write(d / "cpuset.cpus", lim.cpus)
+
+    def pod(self, key: str, lim: Limits, in_machine: bool = True) -> list[str]:
+        """Prepare pod ``key``: its cgroups, and the jail options that put its processes in them
+        (and on its CPUs). ``in_machine=False``: a host-scoped pod (the fabric check's one
+        process over the GPUs of several machines) sits beside the machine, not inside its slice."""
+        with self.lock:
+            self.limits[key] = lim
+            self.oom.discard(key)
+        opts: list[str] = []
+        if self.mode in ("cgroup2", "cgroup1"):
+            name = "pod-" + _NAME.sub("_", key)
+            dirs = {}
+            for ctrl, base in self.base.items():
+                d = (base if in_machine else base.parent) / name
+                d.mkdir(exist_ok=True)
+                if ctrl == "cpuset":
+                    for f in ("cpuset.cpus", "cpuset.mems"):
+                        if not (d / f).read_text().strip():
+                            _write(d / f, (d.parent / f).read_text().strip())
+                self._limit(d, ctrl, lim)
+                dirs[ctrl] = d
+                opts += ["--cgroup-procs", str(d / "cgroup.procs")]
+            with self.lock:
+                self.pods[key] = dirs
+        if lim.cpus and not (self.mode == "cgroup2" and (self.base[""] / "cpuset.cpus").exists()) \
+                and "cpuset" not in self.base:
+            opts += ["--cpus", lim.cpus]  # no cpuset controller: affinity
+        return opts
+
+    def oom_killed(self, key: str) -> bool:
+        """Was the last kill in pod ``key`` an out-of-memory kill?"""
+        with self.lock:
+            if key in self.oom:
+                return True
+            dirs = self.pods.get(key) or {}
+        try:
+            if "" in dirs:
+                ev = dict(line.split() for line in (dirs[""] / "memory.events").read_text().splitlines() if line.strip())
+                return int(ev.get("oom_kill", 0)) > 0
+            if "memory" in dirs:
+                ctl = dict(line.split() for line in (dirs["memory"] / "memory.oom_control").read_text().splitlines()
+                           if len(line.split()) == 2)
+                return int(ctl.get("oom_kill", 0)) > 0 or int((dirs["memory"] / "memory.failcnt").read_text()) > 0
+        except (OSError, ValueError):
+            pass
+        return False
+
+    def reset_oom(self, key: str) -> None:
+        """A container restarts: the next exit is judged on its own."""
+        with self.lock:
+            self.oom.discard(key)
+            dirs = self.pods.get(key) or {}
+        if "memory" in dirs:  # v1 counts failures cumulatively: reset between instances
+            try:
+                _write(dirs["memory"] / "memory.failcnt", 0)
+            except OSError:
+                pass
+
+    def release(self, key: str) -> None:
+        with self.lock:
+            dirs = self.pods.pop(key, {})
+            self.limits.pop(key, None)
+            self.oom.discard(key)
+        for d in dirs.values():
+            try:
+                os.rmdir(d)
+            except OSError:
+                pass
+
+    def close(self) -> None:
+        """The agent is going away: every pod cgroup it made, then its machine's, are removed
+        (those still holding a process stay)."""
+        for key in list(self.pods):
+            self.release(key)
+        for ctrl, base in self.base.items():
+            try:  # leave it for the parent (v1: the agent itself; v2: its leaf) and remove it
+                if ctrl == "":
+                    _write(base.parent / "tk8s-agent" / "cgroup.procs", os.getpid())
+                    os.rmdir(base / "agent")
+                else:
+                    _write(base.parent / "cgroup.procs", os.getpid())
+                os.rmdir(base)
+            except OSError:
+                pass
+
+    def describe(self) -> str:
+        m = self.machine
+        shape = ", ".join(x for x in (f"memory {m.memory >> 20} MiB" if m.memory else "",
+                                      f"cpu {m.cpu:g}" if m.cpu else "", f"cpus {m.cpus}" if m.cpus else "") if x)
+        if self.mode == "cgroup2":
+            return f"cgroup2 ({self.base[''].parent}): pod memory.max, cpu.max, cpuset; machine {shape or 'unbounded'}"
+        if self.mode == "cgroup1":
+            return (f"cgroup1 ({', '.join(sorted(self.base))}): pod memory, cfs quota, cpuset; "
+                    f"machine {shape or 'unbounded'}")
+        if self.mode == "watchdog":
+            return ("watchdog: limits.memory by resident-set sampling (OOMKilled), GPU pods pinned to NUMA-local "
+                    "CPUs; limits.cpu and the machine shape NOT enforced (no delegated cgroup: " + self.why.strip("; ")
+                    + ")")
+        return f"none: {self.why.strip('; ')}"
+
+    # ---- the watchdog (watchdog mode) -------------------------------------------------------
+    def over_limit(self, rss: dict[str, int]) -> list[str]:
+        """Pods whose resident set (``rss``: key -> bytes) is over their limits.memory."""
+        with self.lock:
+            return [k for k, b in rss.items() if (self.limits.get(k) or Limits()).memory and b > self.limits[k].memory]
+
+    def kill_oom(self, key: str, groups: list[int]) -> None:
+        with self.lock:
+            self.oom.add(key)
+        for g in groups:
+            try:
+                os.killpg(g, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+
+    def watch(self, groups_of, stop: threading.Event, period: float = 0.5) -> None:
+        """Watchdog loop: ``groups_of()`` -> {pod key: [process group ids]}."""
+        if self.mode != "watchdog":
+            return
+        from .usage import _proc_table
+
+        while not stop.wait(period):
+            with self.lock:
+                if not any(lim.memory for lim in self.limits.values()):
+                    continue
+            groups = groups_of()
+            table = _proc_table()
+            rss: dict[str, int] = {}
+            for key, gs in groups.items():
+                want = set(gs)
+                rss[key] = sum(r for _pid, (pg, _t, r) in table.items() if pg in want)
+            for key in self.over_limit(rss):
+                self.kill_oom(key, groups.get(key, []))
+                time.sleep(0)  # the runtime's wait() sees the kill; oom_killed() names it

@@ -90,6 +90,10 @@ class PodProc:
     container: dict = field(default_factory=dict)  # its spec (probes, ports)
     prober: object = None         # agent/probes.Prober of the running process, if it has probes
     grace: float = 30.0           # terminationGracePeriodSeconds
+    pod_key: str = ""             # the pod's key (sidecars' and init containers' too): its cgroup
+    limit_opts: list[str] = field(default_factory=list)  # resources.py jail options, when no jail applies them
+    oom_killed: bool = False      # the last instance ended in an out-of-memory kill
+    last_term: dict | None = None  # the last instance's terminated state (lastState)
     proc: subprocess.Popen | None = None
     restarts: int = 0
     started: float = 0.0
@@ -101,6 +105,7 @@ class PodProc:
 class PodRuntime:
     def __init__(self, sandbox: Path, on_status, tool_dirs: list[str] | None = None):
         self.sandbox = Path(sandbox)
+        self.enforcer = None              # resources.Enforcer: cgroups, OOM verdicts
         self.on_status = on_status        # callback(podproc, phase, extra: dict)
         self.pods: dict[str, PodProc] = {}
         self.terminating: dict[str, PodProc] = {}  # deleted, within their grace period
@@ -123,12 +128,16 @@ class PodRuntime:
         if pp.exit_code is not None:  # a restart: the last instance's log is `kubectl logs --previous`
             with contextlib.suppress(OSError):
                 os.replace(pp.dir / pp.log_name, pp.dir / f"{pp.log_name}.previous")
+        if self.enforcer is not None and pp.exit_code is not None:
+            self.enforcer.reset_oom(pp.pod_key or pp.key)
         log = open(pp.dir / pp.log_name, "ab", buffering=0)
         try:
             p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
                                  stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
         finally:
             log.close()
+        if pp.limit_opts:  # no jail to join them: best effort right after the start
+            _join_limits(p.pid, pp.limit_opts)
         atomic_write_json(pp.dir / _pidfile(pp), {"pid": p.pid, "pgid": p.pid, "argv": pp.argv,
                                                   "start": proc_start_ticks(p.pid)})
         return p
@@ -159,8 +168,7 @@ class PodRuntime:
                     self.on_status(pp, "Failed", {"message": f"init container {ic.name}: {e}", "reason": "Init:StartError"})
                     return False
                 self.on_status(pp, "Pending", {"reason": "PodInitializing", "message": f"Init:{i}/{len(pp.init)}"})
-                rc = ic.proc.wait()
-                ic.exit_code = rc
+                rc = self._exited(ic, ic.proc.wait())
                 (pp.dir / _pidfile(ic)).unlink(missing_ok=True)
                 if rc == 0 or pp.stopping:
                     break
@@ -186,8 +194,7 @@ class PodRuntime:
             self._probe(sc, pp)
             if pp.proc is not None and pp.proc.poll() is None:
                 self.on_status(pp, "Running", {})  # its container statuses now include this one
-            rc = sc.proc.wait()
-            sc.exit_code = rc
+            rc = self._exited(sc, sc.proc.wait())
             (pp.dir / _pidfile(sc)).unlink(missing_ok=True)
             if pp.stopping or not (pp.restart_policy == "Always" or (pp.restart_policy == "OnFailure" and rc != 0)):
                 break
@@ -196,6 +203,19 @@ class PodRuntime:
             time.sleep(backoff)
             backoff = min(backoff * 2, 10.0)
         sc.done.set()
+
+    def _exited(self, cp: PodProc, rc: int) -> int:
+        """Record a container's exit; an out-of-memory kill is exit 137, reason OOMKilled (the
+        kernel's in a cgroup, or the memory watchdog's)."""
+        cp.oom_killed = bool(rc < 0 and self.enforcer is not None and self.enforcer.oom_killed(cp.pod_key or cp.key))
+        if cp.oom_killed:
+            rc = 137
+        elif rc < 0:
+            rc = 128 - rc  # killed by a signal: 128 + signo, as a shell reports it
+        cp.exit_code = rc
+        cp.last_term = {"exitCode": rc, "reason": "OOMKilled" if cp.oom_killed else ("Completed" if rc == 0 else "Error"),
+                        "finishedAt": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
+        return rc
 
     def _run(self, pp: PodProc) -> None:
         if pp.init and not self._init(pp):
@@ -216,9 +236,8 @@ class PodRuntime:
             self._post_start(pp, pp)
             self._probe(pp, pp)
             self.on_status(pp, "Running", {})
-            rc = pp.proc.wait()
+            rc = self._exited(pp, pp.proc.wait())
             trace("runtime", f"exited {pp.key} rc={rc}")
-            pp.exit_code = rc
             (pp.dir / _pidfile(pp)).unlink(missing_ok=True)
             if pp.stopping:
                 break
@@ -371,6 +390,21 @@ class PodRuntime:
             return dict(self.pods)
 
 
+def _join_limits(pid: int, opts: list[str]) -> None:
+    """--cgroup-procs FILE / --cpus LIST for a process already started (no jail to do it)."""
+    from .resources import parse_cpulist
+
+    for flag, val in zip(opts[::2], opts[1::2]):
+        try:
+            if flag == "--cgroup-procs":
+                with open(val, "w") as f:
+                    f.write(f"{pid}\n")
+            elif flag == "--cpus":
+                os.sched_setaffinity(pid, parse_cpulist(val))
+        except OSError:
+            pass
+
+
 def _pidfile(pp: PodProc) -> str:
     return "pod.pid" if pp.log_name == "log" else f"pod-{pp.name}.pid"
 
@@ -443,7 +477,8 @@ def jail_signal_scoping() -> bool:
     return gpu_jail()[0] and _JAIL_ABI >= 6
 
 
-def gpu_jail_argv(gpus: list, *, deny=(), read_only=(), allow=(), scope_signals: bool = False) -> list[str]:
+def gpu_jail_argv(gpus: list, *, deny=(), read_only=(), allow=(), scope_signals: bool = False,
+                  extra=None) -> list[str]:
     """argv prefix that runs a command allowed to open only ``gpus`` (HostGpu records: KFD node +
     render minor), none of the ``deny`` paths, only for reading the ``read_only`` ones, and the
     ``allow`` paths beneath either (agent._jail_layers); ``scope_signals``: no signal to any process
@@ -455,6 +490,7 @@ def gpu_jail_argv(gpus: list, *, deny=(), read_only=(), allow=(), scope_signals:
             argv += [opt, str(x)]
     if scope_signals:
         argv.append("--scope-signals")
+    argv += list(extra or [])  # resources.py: --cgroup-procs FILE / --cpus LIST
     hide = os.environ.get("TK8S_GPU_JAIL_HIDE_TOPOLOGY") == "1"  # off: ROCm 7.2's thunk fails on it
     if hide:
         argv.append("--hide-topology")
@@ -495,13 +531,14 @@ def container_runtime() -> tuple[bool, str]:
 
 
 def container_argv(rootfs: str, upper: str, workdir: str, *, pid_ns: bool, gpus: list,
-                   binds: list[tuple] = (), hostname: str = "", scope_signals: bool = False) -> list[str]:
+                   binds: list[tuple] = (), hostname: str = "", scope_signals: bool = False,
+                   extra=None) -> list[str]:
     """argv prefix that runs a command as an image pod (see CONTAINER above). ``binds``:
     (source, path in the container[, read-only]) -- the pod's volume mounts (agent/volumes.py).
     The jail inside needs no path layers: the host's tree is not the container's, and what the
     chroot leaves reachable of it (/proc/<pid>/root) is ptrace-guarded, which Landlock denies
     across domains."""
-    jail = gpu_jail_argv(gpus, scope_signals=scope_signals)[1:-1]  # the jail options without the binary and "--"
+    jail = gpu_jail_argv(gpus, scope_signals=scope_signals, extra=extra)[1:-1]  # the jail options without the binary and "--"
     argv = [str(CONTAINER), "--rootfs", str(rootfs), "--upper", str(upper), "--workdir", workdir or "/"]
     if pid_ns:
         argv.append("--pid-ns")

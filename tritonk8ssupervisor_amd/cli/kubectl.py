@@ -878,6 +878,9 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 print("Taints:       " + (", ".join(f"{t['key']}{'=' + str(t['value']) if t.get('value') else ''}:{t['effect']}"
                                                    for t in taints) or "<none>"))
                 print(f"Unschedulable: {str(bool((o.get('spec') or {}).get('unschedulable'))).lower()}")
+                enf = o["metadata"].get("annotations", {}).get("tk8s.amd.com/resource-enforcement")
+                if enf:
+                    print(f"Resource enforcement: {enf}")
                 pods = [p for p in k.get(k.k8s("/api/v1/pods"), query={"fieldSelector": f"spec.nodeName={name}"})["items"]
                         if p.get("status", {}).get("phase") not in ("Succeeded", "Failed")]
                 used = sum(int(((c.get("resources") or {}).get("limits") or {}).get(GPU, 0) or 0)
@@ -903,7 +906,14 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                 if "tk8s.amd.com/gpu-isolation" in ann or "tk8s.amd.com/isolation" in ann:
                     print("Isolation:\n"
                           f"  GPU:        {ann.get('tk8s.amd.com/gpu-isolation', '-')}\n"
-                          f"  Namespaces: {ann.get('tk8s.amd.com/isolation', '-')}")
+                          f"  Namespaces: {ann.get('tk8s.amd.com/isolation', '-')}\n"
+                          f"  Resources:  {ann.get('tk8s.amd.com/resources', '-')}")
+                for c in st.get("containerStatuses") or []:
+                    term = (c.get("state") or {}).get("terminated") or ((c.get("lastState") or {}).get("terminated"))
+                    if term:
+                        which = "State" if "terminated" in (c.get("state") or {}) else "Last State"
+                        print(f"  {c.get('name')}: {which}: Terminated, Reason: {term.get('reason')}, "
+                              f"Exit Code: {term.get('exitCode')}, Restart Count: {c.get('restartCount', 0)}")
             # the object's events, selected as kubectl describe does (kind, name, namespace, uid)
             sel = f"involvedObject.kind={o.get('kind', '')},involvedObject.name={o['metadata']['name']}"
             if o["metadata"].get("uid"):

@@ -308,6 +308,11 @@ class LocalProvider(Provider):
             "TK8S_MACHINE_GPUS": ",".join(map(str, m.gpus)),
             "TK8S_MACHINE_PACKAGE": m.package,
         }
+        try:  # the package's slice of the host: the node's capacity, enforced by agent/resources.py
+            pkg = self.package_by_id_or_name(m.package)
+            env.update(TK8S_MACHINE_CPUS=str(pkg.cpus), TK8S_MACHINE_MEMORY_MB=str(pkg.memory_mb))
+        except Exception:  # noqa: BLE001 - an unknown package: the host's shape
+            pass
         fake_hosts = int(os.environ.get("TK8S_FAKE_HOSTS", "0") or 0)
         if fake_hosts > 1:  # CPU tests: pretend the machines are spread over that many hosts
             digits = "".join(ch for ch in m.name if ch.isdigit()) or "0"
