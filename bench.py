@@ -32,6 +32,11 @@ bring-up time (BASELINE.json ``published: {}``); ``vs_baseline`` is quoted again
 reference can never go below (setup.sh:36,41,46; terraform/*/main.tf:22;
 ansible/roles/ranchermaster/tasks/main.yml:25).
 
+A timed step whose post-Ready RCCL check fails is left out of ``value`` and listed in
+``post_ready_errors`` (its Ready time stood, the cluster did not). After the headline, a
+single-rank run also measures BASELINE.json configs[1], ``curve_config2``: 1 master + 1/2/4/8
+``cpu-only`` workers (no GPU, no device plugin), ``--curve-steps`` timed bring-ups per point.
+
 Multi-GPU launch (driver): ``torch.distributed.run --nproc-per-node N bench.py --gpus N``.
 Rank 0 drives the bring-up (it is the operator's shell); every rank joins the barriers
 and synchronises its own device around the timed region; the time reported is the MAX
@@ -264,15 +269,16 @@ def slow_start_cause(census: dict, runtime_init_ms: float | None, limit_ms: floa
     return "no KFD process change within 0.3 s before or during the start (driver-internal)"
 
 
-def one_bringup(ws: Path, n: int, args, env: dict, log, census: KfdCensus | None = None) -> dict:
-    answers = {"nodes": n, "package": args.package, "name": "k8s bench", "confirm": "yes"}
+def one_bringup(ws: Path, n: int, args, env: dict, log, census: KfdCensus | None = None, package: str | None = None,
+                rccl: str | None = None) -> dict:
+    answers = {"nodes": n, "package": package or args.package, "name": "k8s bench", "confirm": "yes"}
     (ws / "answers.json").write_text(json.dumps(answers))
     cmd = ["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", str(_free_port()),
            "--timeout", str(args.timeout), "--rccl-timeout", str(args.rccl_timeout)]
     if args.no_validate:
         cmd.append("--no-validate")
-    if args.rccl:
-        cmd += ["--rccl", args.rccl]
+    if rccl or args.rccl:
+        cmd += ["--rccl", rccl or args.rccl]
     import threading
 
     census = census or KfdCensus()
@@ -360,6 +366,42 @@ def teardown(ws: Path, env: dict, log) -> float:
     return time.perf_counter() - t0
 
 
+CURVE_NODES = (1, 2, 4, 8)
+
+
+def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1) -> dict:
+    """BASELINE.json configs[1]: 1 master + N ``cpu-only`` workers (no GPU, no device plugin),
+    N = 1/2/4/8 -- the worker-count curve of the bring-up itself, measurable on a 1-GPU box. Each
+    point: ``warmup`` untimed bring-ups then ``steps`` timed ones, each bracketed like the
+    headline's (the whole ./setup.sh process; value = launch -> ALL NODES READY), teardown and
+    workspace creation outside the brackets."""
+    points = []
+    t_curve = time.perf_counter()
+    for n in CURVE_NODES:
+        ready, proc = [], []
+        for i in range(warmup + steps):
+            ws = root / f"curve{n}-{i}"
+            make_workspace(ws)
+            t0 = time.perf_counter()
+            s = one_bringup(ws, n, args, env, log, package="cpu-only", rccl="off")
+            dt = time.perf_counter() - t0
+            teardown(ws, env, log)
+            shutil.rmtree(ws, ignore_errors=True)
+            if i >= warmup:
+                ready.append(s["ready_wall_seconds"])
+                proc.append(dt)
+        srt = sorted(ready)
+        points.append({"workers": n, "steps": steps, "mean_s": round(sum(ready) / len(ready), 4),
+                       "median_s": round(srt[len(srt) // 2] if len(srt) % 2 else (srt[len(srt) // 2 - 1] + srt[len(srt) // 2]) / 2, 4),
+                       "min_s": round(srt[0], 4), "max_s": round(srt[-1], 4),
+                       "ms_per_step": round(sum(proc) / len(proc) * 1000.0, 2), "gpus_allocatable": s.get("gpus_allocatable"),
+                       "nodes": s.get("nodes")})
+    return {"config": "BASELINE.json configs[1]: 1 master + N cpu-only workers, no GPU device plugin",
+            "package": "cpu-only", "warmup": warmup, "points": points,
+            "wall_s": round(time.perf_counter() - t_curve, 3),
+            "scaling_8_vs_1": round(points[-1]["mean_s"] / points[0]["mean_s"], 3) if points else None}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1, help="workers (one MI355X each)")
@@ -378,6 +420,9 @@ def main(argv=None) -> int:
     ap.add_argument("--back-to-back", type=int, default=None,
                     help="after the timed steps, this many extra bring-ups with NO settle pause (a rebuild right "
                          "after a teardown), reported separately as back_to_back_* (default: 2 with real GPUs)")
+    ap.add_argument("--curve-steps", type=int, default=5,
+                    help="timed steps per point of the cpu-only worker curve (BASELINE configs[1], 1/2/4/8 workers) "
+                         "run after the headline on a single-rank run; 0 skips it")
     ap.add_argument("--settle", type=float, default=None,
                     help="pause after each teardown, outside the timed region, so the driver has released the "
                          "previous step's GPU processes (default: 1.0 s with real GPUs, 0 with fake ones)")
@@ -392,6 +437,7 @@ def main(argv=None) -> int:
     root = Path(args.workdir) if args.workdir else Path(tempfile.mkdtemp(prefix="tk8s-bench-", dir=os.environ.get("TMPDIR", "/tmp")))
     root.mkdir(parents=True, exist_ok=True)
     times: list[float] = []
+    excluded: list[dict] = []   # timed steps whose post-Ready RCCL check failed
     summaries: list[dict] = []
     teardown_s: list[float] = []
     ready_times: list[float] = []
@@ -457,10 +503,14 @@ def main(argv=None) -> int:
             if extra:
                 b2b_ready.append(d.max(s["ready_wall_seconds"] if s else 0.0))
             if timed:
-                times.append(d.max(dt))
-                ready_times.append(d.max(s["ready_wall_seconds"] if s else 0.0))
-                if s is not None:
-                    summaries.append(s)
+                bad = d.bcast_obj(bool(s and s.get("post_ready_error")) if d.rank == 0 else None)
+                if bad:  # Ready was reached but the post-Ready fabric check failed: flagged, not counted
+                    excluded.append({"step": i, "error": s["post_ready_error"][-600:] if s else ""})
+                else:
+                    times.append(d.max(dt))
+                    ready_times.append(d.max(s["ready_wall_seconds"] if s else 0.0))
+                    if s is not None:
+                        summaries.append(s)
             if d.rank == 0:
                 kind = "timed" if timed else "back-to-back" if extra else "warmup"
                 print(f"[bench] step {i} ({kind}): {dt:.3f}s", file=sys.stderr, flush=True)
@@ -473,9 +523,22 @@ def main(argv=None) -> int:
     d.close()
     if d.rank != 0:
         return 0 if err is None else 1
+    if err is None and not times:
+        err = f"every timed step failed its post-Ready RCCL check: {excluded[-1]['error'] if excluded else ''}"
     if err is not None:
-        print(json.dumps({"metric": METRIC, "value": None, "error": err[-2000:]}))
+        print(json.dumps({"metric": METRIC, "value": None, "error": err[-2000:],
+                          **({"excluded_steps": excluded} if excluded else {})}))
         return 1
+    curve = None
+    if args.curve_steps > 0 and d.world == 1:
+        croot = Path(tempfile.mkdtemp(prefix="tk8s-curve-", dir=os.environ.get("TMPDIR", "/tmp")))
+        try:
+            with open(args.log, "a") if args.log else open(os.devnull, "w") as clog:
+                curve = config2_curve(croot, args, env, clog, args.curve_steps)
+        except Exception as e:  # noqa: BLE001 - the headline stands; the curve says why it is missing
+            curve = {"error": str(e)[-1500:]}
+        finally:
+            shutil.rmtree(croot, ignore_errors=True)
     step_mean = sum(times) / len(times)
     mean = sum(ready_times) / len(ready_times)
     ready = [s["ready_seconds"] for s in summaries if s.get("ready_seconds") is not None]
@@ -562,9 +625,11 @@ def main(argv=None) -> int:
                                "max_s": round(max(b2b_ready), 4),
                                "what": "./setup.sh -c && ./setup.sh with no settle pause: Ready includes the driver "
                                        "still releasing the previous bring-up's GPU processes"}
-    errs = [s["post_ready_error"] for s in summaries if s.get("post_ready_error")]
-    if errs:
-        out["post_ready_errors"] = {"count": len(errs), "last": errs[-1][-600:]}
+    if excluded:  # timed steps left out of value: Ready, then the post-Ready RCCL check failed
+        out["post_ready_errors"] = {"count": len(excluded), "excluded_steps": [x["step"] for x in excluded],
+                                    "last": excluded[-1]["error"]}
+    if curve is not None:
+        out["curve_config2"] = curve
     print(json.dumps(out), flush=True)
     return 0
 

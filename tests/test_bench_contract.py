@@ -56,12 +56,27 @@ def _check(out: dict, n: int, steps: int, warmup: int) -> None:
 
 @pytest.mark.timeout(300)
 def test_bench_single_process(tmp_path):
+    import time
+
+    t0 = time.monotonic()
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "2", "--warmup", "1",
-                        "--fake-gpus", "2"], cwd=REPO, env=_env(tmp_path), capture_output=True, text=True,
-                       timeout=280)
+                        "--fake-gpus", "2", "--curve-steps", "2"], cwd=REPO, env=_env(tmp_path), capture_output=True,
+                       text=True, timeout=280)
+    run_wall = time.monotonic() - t0
     assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
     out = _json_line(p.stdout)
     _check(out, 1, 2, 1)
+    # BASELINE configs[1]'s worker curve rides along -- 1/2/4/8 cpu-only workers,
+    # no GPU -- and every point's timed steps fit inside the run's own wall time
+    curve = out["curve_config2"]
+    assert [pt["workers"] for pt in curve["points"]] == [1, 2, 4, 8] and curve["package"] == "cpu-only"
+    spent = 0.0
+    for pt in curve["points"]:
+        assert pt["steps"] == 2 and pt["nodes"] == pt["workers"] and pt["gpus_allocatable"] == 0
+        assert pt["min_s"] <= pt["mean_s"] <= pt["max_s"] and pt["ms_per_step"] >= pt["min_s"] * 1000.0
+        spent += pt["steps"] * pt["ms_per_step"] / 1000.0
+    assert spent <= curve["wall_s"] <= run_wall, (spent, curve["wall_s"], run_wall)
+    assert curve["scaling_8_vs_1"] == round(curve["points"][-1]["mean_s"] / curve["points"][0]["mean_s"], 3)
     assert p.stderr.count("(timed)") == 2 and p.stderr.count("(warmup)") == 1
     # the step bracket is the Ready time plus what ./setup.sh does after
     # Ready, not a polling quantum on top
@@ -92,14 +107,15 @@ def test_bench_real_gpu(tmp_path):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "0"], cwd=REPO,
-                       env=_env(tmp_path), capture_output=True, text=True, timeout=220)
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "0", "--curve-steps", "1"],
+                       cwd=REPO, env=_env(tmp_path), capture_output=True, text=True, timeout=220)
     assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
     out = _json_line(p.stdout)
     assert out["n_gpus"] == 1 and out["gpus_allocatable"] == 1 and out["nodes_validated"] == 1
     assert "fake" not in out["data"] and out["value"] < 5.0
     v = next(iter(out["validation_last_step"].values()))
     assert float(v["hbm-write-gbps"]) > 1000.0 and float(v["md5-mbps"]) > 1000.0
+    assert [pt["workers"] for pt in out["curve_config2"]["points"]] == [1, 2, 4, 8]
 
 
 def test_bench_reports_post_ready_failures(monkeypatch, capsys, tmp_path):
@@ -111,7 +127,7 @@ def test_bench_reports_post_ready_failures(monkeypatch, capsys, tmp_path):
     monkeypatch.setenv("TMPDIR", str(tmp_path))
     calls = {"n": 0}
 
-    def fake_bringup(ws, n, args, env, log, census=None):
+    def fake_bringup(ws, n, args, env, log, census=None, package=None, rccl=None):
         calls["n"] += 1
         if calls["n"] == 2:
             return {"wall_seconds": 0.3, "ready_wall_seconds": 0.2, "phases": {}, "post_ready_error": "exit 2: RCCL"}
@@ -122,10 +138,12 @@ def test_bench_reports_post_ready_failures(monkeypatch, capsys, tmp_path):
     monkeypatch.setattr(bench, "teardown", lambda ws, env, log: 0.01)
     monkeypatch.setattr(bench, "make_workspace", lambda root: root)
     monkeypatch.setattr("tritonk8ssupervisor_amd.utils.build_native.build", lambda: {})
-    assert bench.main(["--gpus", "1", "--steps", "3", "--warmup", "0", "--fake-gpus", "1"]) == 0
+    assert bench.main(["--gpus", "1", "--steps", "3", "--warmup", "0", "--fake-gpus", "1", "--curve-steps", "0"]) == 0
     out = _json_line(capsys.readouterr().out)
     assert out["post_ready_errors"]["count"] == 1 and "RCCL" in out["post_ready_errors"]["last"]
-    assert out["min_s"] == 0.2 and out["ready_s_inside_setup"] == 0.24
+    # the failed step is flagged and left out of value
+    assert out["post_ready_errors"]["excluded_steps"] == [1]
+    assert out["min_s"] == out["max_s"] == out["value"] == 0.25 and out["ready_s_inside_setup"] == 0.24
     assert "not like-for-like" in out["vs_baseline_note"].replace("NOT", "not")
 
 
