@@ -157,6 +157,8 @@ def test_single_node_check_plan(tmp_path):
 def test_kubeadm_refused_on_colocated_sandboxes(tmp_path, monkeypatch):
     from tritonk8ssupervisor_amd.orchestrator import Setup, SetupError, init_workspace
 
+    monkeypatch.setattr(os, "geteuid", lambda: 1000)  # not root: no kubeadm on this host itself
+    monkeypatch.delenv("TK8S_LOCAL_HOST_ROOT", raising=False)
     monkeypatch.setenv("TK8S_FAKE_GPUS", "2")
     ws = init_workspace(tmp_path)
     s = Setup(ws, answers={"nodes": 1}, assume_yes=True, platform="kubeadm", out=lambda _l: None)
@@ -169,6 +171,8 @@ def test_kubeadm_readiness_from_kubectl(tmp_path, monkeypatch):
 
     from tritonk8ssupervisor_amd.orchestrator import Setup, SetupError, init_workspace
 
+    monkeypatch.setattr(os, "geteuid", lambda: 1000)  # the multi-host form (as root, kubeadm would use this host)
+    monkeypatch.delenv("TK8S_LOCAL_HOST_ROOT", raising=False)
     ws = init_workspace(tmp_path)
     s = Setup(ws, platform="kubeadm", out=lambda _l: None)
     s.cfg = SimpleNamespace(RANCHER_MASTER_HOSTNAME="kubemaster", node_names=lambda: ["kubenode1", "kubenode2"],
@@ -458,3 +462,101 @@ def test_both_platforms_report_ready_and_rccl_alike():
     # the kubeadm playbook's last play waits for nodes + GPUs only; no RCCL object is created in it
     role = (REPO / "ansible" / "roles" / "kubeadmvalidate" / "tasks" / "main.yml").read_text()
     assert "rccl-tests" not in role.split("\n- name:", 1)[1].lower().replace("rccl-tests select", "")
+
+
+def test_kubeadm_single_node_as_root_on_this_host(tmp_path, monkeypatch):
+    """the natural command on the north-star box -- ``./setup.sh --platform
+    kubeadm --nodes 8`` as root with the default (local) backend -- runs the kubeadm roles on THIS
+    host through a one-host inventory reached without ssh (``connection: local``): kubeadm init,
+    the control-plane taint removed, 8 x amd.com/gpu on the one node; ``-c`` resets it. The host
+    here is a fake root (its apt-get/kubeadm/kubectl/systemctl are tests/fakeroot stand-ins, its
+    system paths under a staging root), the same simulation the ssh tests use."""
+    import subprocess
+    import sys
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    state = tmp_path / "cluster.json"
+    ws = tmp_path / "ws"
+    ws.mkdir()
+    init_workspace(ws)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, ws / f)
+    gv = ws / "ansible" / "group_vars" / "all.yml"
+    gv.write_text(gv.read_text().replace('tk8s_sysroot: ""', 'tk8s_sysroot: "{{ ansible_env.HOME }}/sysroot"'))
+    host = _fake_root_host(tmp_path / "hosts", "this-host", "", state, gpus=8)
+    (host / ".ssh" / "authorized_keys").unlink()  # no ssh involved at all
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_LOCAL_HOST_ROOT=str(host),
+               TK8S_LOCAL_HOST_GPUS="8", TK8S_SSH="false", TK8S_RCCL_POLL="0.05")
+    for k in ("TK8S_FAKE_GPUS", "TK8S_BACKEND", "TK8S_INVENTORY"):
+        env.pop(k, None)
+    r = subprocess.run(["./setup.sh", "--platform", "kubeadm", "--yes", "--json", "--nodes", "8", "--timeout", "60"],
+                       cwd=ws, env=env, capture_output=True, text=True, timeout=300)
+    try:
+        assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["single_node"] is True and s["nodes"] == 8 and s["kubernetes_nodes"] == 1
+        assert s["gpus_allocatable"] == 8 and s["rccl"]["ok"]
+        inv = json.loads((ws / ".tk8s" / "local-host-inventory.json").read_text())
+        assert inv["hosts"][0]["connection"] == "local" and inv["hosts"][0]["gpus"] == 8
+        assert "TK8S_BACKEND=baremetal" in (ws / "config").read_text()
+        assert "ansible_connection=local" in (ws / "ansible" / "hosts").read_text()
+        log = (host / "sysroot" / "var" / "log" / "fake-tools.log").read_text()
+        assert log.count("kubeadm init") == 1 and "kubeadm join" not in log
+        assert "taint nodes" in log and "NoSchedule-" in log
+        nodes = json.loads(state.read_text())["nodes"]
+        assert len(nodes) == 1 and next(iter(nodes.values()))["gpus"] == 8
+    finally:
+        c = subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, text=True, timeout=120)
+    assert c.returncode == 0, c.stdout + c.stderr
+    assert "kubeadm reset on" in c.stdout and ": ok" in c.stdout
+    assert not (host / "sysroot" / "etc" / "kubernetes" / "admin.conf").exists()
+
+
+def test_kubeadm_refused_on_this_host_without_root(tmp_path, monkeypatch):
+    from tritonk8ssupervisor_amd.orchestrator import Setup, SetupError, init_workspace
+
+    monkeypatch.setattr(os, "geteuid", lambda: 1000)
+    monkeypatch.delenv("TK8S_LOCAL_HOST_ROOT", raising=False)
+    monkeypatch.setenv("TK8S_FAKE_GPUS", "2")
+    ws = init_workspace(tmp_path)
+    s = Setup(ws, answers={"nodes": 1}, assume_yes=True, platform="kubeadm", out=lambda _l: None)
+    with pytest.raises(SetupError, match="as root"):
+        s.configure()
+
+
+GOLDEN_LOCAL = REPO / "tests" / "golden" / "kubeadm_check_local_root.txt"
+
+
+def test_kubeadm_as_root_on_this_host_check_plan(tmp_path):
+    """``./setup.sh --platform kubeadm --nodes 8 --dry-run`` as root on this host
+    (simulated root): the Terraform plan (1 master machine = the host, 8 GPU slots) and the kubeadm
+    playbook in check mode, task by task, pinned by a golden file (TK8S_REGOLDEN=1 rewrites it)."""
+    import subprocess
+    import sys
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    ws = tmp_path / "ws"
+    ws.mkdir()
+    init_workspace(ws)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, ws / f)
+    host = _fake_root_host(tmp_path / "hosts", "this-host", "", tmp_path / "cluster.json", gpus=8)
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_LOCAL_HOST_ROOT=str(host),
+               TK8S_LOCAL_HOST_GPUS="8", TK8S_SSH="false")
+    for k in ("TK8S_FAKE_GPUS", "TK8S_BACKEND", "TK8S_INVENTORY"):
+        env.pop(k, None)
+    r = subprocess.run(["./setup.sh", "--platform", "kubeadm", "--yes", "--json", "--nodes", "8", "--dry-run"],
+                       cwd=ws, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-3000:]
+    s = json.loads(r.stdout.strip().splitlines()[-1])
+    assert s["dry_run"] and s["platform"] == "kubeadm" and s["backend"] == "baremetal" and s["check_ok"]
+    assert len(s["plan"]) == 9 and all(p["action"] == "create" for p in s["plan"])
+    plan = s["check_plan"]
+    if os.environ.get("TK8S_REGOLDEN") == "1":
+        GOLDEN_LOCAL.write_text("\n".join(plan) + "\n")
+    assert plan == GOLDEN_LOCAL.read_text().splitlines()
+    assert {ln.split(":", 1)[0] for ln in plan} == {"kubemaster"}  # the GPU slots run nothing
+    assert "kubemaster: kubeadm init (etcd, kube-apiserver, kube-scheduler, kube-controller-manager)" in plan
+    assert not (ws / "config").exists() and not (ws / "terraform" / "rancher.tf").exists()  # nothing written

@@ -40,6 +40,12 @@ from .workspace import (  # noqa: F401 - the orchestrator's public names, re-exp
 )
 
 
+def local_kubeadm_allowed() -> bool:
+    """May ``--platform kubeadm`` run on this host itself (the local backend)? As root -- it installs
+    the node runtime -- or against a simulated root (TK8S_LOCAL_HOST_ROOT, the CPU tests)."""
+    return os.geteuid() == 0 or bool(os.environ.get("TK8S_LOCAL_HOST_ROOT"))
+
+
 # ---- machine executor for the playbook engine ---------------------------------------------
 # executor.py: LocalExecutor for colocated sandboxes, RemoteExecutor (ssh) for everything else.
 from .executor import MachineExecutor  # noqa: E402,F401 - re-exported (./tk8s ansible-playbook)
@@ -100,7 +106,15 @@ class Setup(KubeadmPlatform, FabricCheck):
         self.rccl_timeout = rccl_timeout
         ws.state_dir.mkdir(parents=True, exist_ok=True)
         self.events = EventLog(ws.events, echo=False)
-        self.provider = get_provider(self.backend, ws.state_dir)
+        if self.platform == "kubeadm" and self.backend == "local" and local_kubeadm_allowed():
+            # one command on one box (the reference's setup.sh:8-92): kubeadm single-node on THIS host,
+            # as root, through the bare-metal path with a one-host inventory reached without ssh
+            from .provider.baremetal import BareMetalProvider, local_host_inventory
+
+            self.backend = "baremetal"
+            self.provider = BareMetalProvider(ws.state_dir, inventory=local_host_inventory(ws.state_dir))
+        else:
+            self.provider = get_provider(self.backend, ws.state_dir)
         self.engine = Engine(ws.tf, self.provider, self.events, on_created=self._machine_booted)
         self.cfg: ClusterConfig | None = None
         self.summary: dict = {}
@@ -153,8 +167,9 @@ class Setup(KubeadmPlatform, FabricCheck):
         self.cfg = cfg
         self.platform = cfg.TK8S_PLATFORM or "tk8s"
         if self.platform == "kubeadm" and self.provider.colocated:
-            raise SetupError("error: the kubeadm platform installs ROCm, amdgpu-dkms, containerd and Kubernetes as root on "
-                             "its machines: use machines you own (--backend baremetal with an SSH inventory, or triton)")
+            raise SetupError("error: the kubeadm platform installs ROCm, amdgpu-dkms, containerd and Kubernetes as root: "
+                             "run ./setup.sh --platform kubeadm as root for a single-node cluster on this host, or use "
+                             "machines you own (--backend baremetal with an SSH inventory, or triton)")
         if self.platform == "kubeadm" and hasattr(self.provider, "whole_hosts"):
             # a kubelet per host: machines are whole hosts, not slices -- except on a one-host
             # inventory (single-node mode), where the workers are GPU slots of the master's node
@@ -474,10 +489,13 @@ class Setup(KubeadmPlatform, FabricCheck):
                      "tk8s_home": str(REPO)}
             if twin.platform == "kubeadm":
                 extra.update(kubeadm_extra_vars(twin, cfg))
-            res = Playbook(sws.ansible / PLAYBOOKS[twin.platform], sws.ansible / "hosts", check=True,
-                           extra_vars=extra, out=self.out).run()
+            pb = Playbook(sws.ansible / PLAYBOOKS[twin.platform], sws.ansible / "hosts", check=True,
+                          extra_vars=extra, out=self.out)
+            res = pb.run()
             return {"dry_run": True, "platform": twin.platform, "backend": self.backend,
                     "plan": [{"address": a.address, "action": a.action} for a in plan],
+                    # the playbook's plan, task by task ("host: task"), what a --check golden pins
+                    "check_plan": [f"{t['host']}: {t['task']}" for t in pb.trace if t.get("module") != "setup"],
                     "check_ok": res.ok, "check_failures": res.failures, "check_stats": res.stats}
         finally:
             shutil.rmtree(scratch, ignore_errors=True)

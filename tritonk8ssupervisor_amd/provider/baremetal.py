@@ -84,9 +84,12 @@ def normalize_inventory(inv: dict) -> dict:
         seen.add(name)
         g = h.get("gpus", 0)
         gpus = list(range(int(g))) if isinstance(g, (int, str)) else [int(x) for x in g]
+        conn = str(h.get("connection", "ssh"))
+        if conn not in ("ssh", "local"):
+            raise ProvisionError(f"inventory host {name!r}: connection {conn!r} is not ssh or local")
         hosts.append({"name": name, "address": addr, "gpus": gpus, "role": str(h.get("role", "")),
                       "addresses": {str(k): str(v) for k, v in (h.get("addresses") or {}).items()},
-                      "ssh": dict(h.get("ssh") or {})})
+                      "ssh": dict(h.get("ssh") or {}), "connection": conn})
     if not hosts:
         raise ProvisionError("bare-metal inventory lists no hosts")
     nets = [{"name": DEFAULT_NETWORK, "public": True}]
@@ -97,6 +100,52 @@ def normalize_inventory(inv: dict) -> dict:
     return {"ssh": dict(inv.get("ssh") or {}), "workdir": str(inv.get("workdir", "tk8s")),
             "python": str(inv.get("python", "python3")), "dist_root": str(inv.get("dist_root", ".tk8s/dist")),
             "networks": nets, "hosts": hosts}
+
+
+def primary_ipv4() -> str:
+    """This host's primary IPv4 address -- the one its default route leaves from (a UDP
+    "connect" sends nothing) -- which kubeadm advertises: 127.0.0.1 would be every pod's own
+    loopback. 127.0.0.1 only when the host has no route at all."""
+    import socket
+
+    for probe in ("10.255.255.255", "192.0.2.1"):
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        try:
+            s.connect((probe, 9))
+            ip = s.getsockname()[0]
+            if ip and not ip.startswith("127."):
+                return ip
+        except OSError:
+            pass
+        finally:
+            s.close()
+    return "127.0.0.1"
+
+
+def local_host_inventory(state_dir: str | os.PathLike, gpus: int | None = None) -> Path:
+    """A one-host inventory naming THIS host, reached without ssh (``connection: local``): the
+    kubeadm platform's single-node bring-up run as root on the 8x MI355X box itself -- the
+    reference's one command on one machine (/root/reference/setup.sh:8-92) -- with no
+    SSH-to-self. Written to ``<state_dir>/local-host-inventory.json``."""
+    import socket
+    import sys
+
+    if gpus is None:
+        env = os.environ.get("TK8S_LOCAL_HOST_GPUS")
+        if env:
+            gpus = int(env)
+        else:
+            from ..models.hostinfo import discover
+
+            gpus = discover().count
+    name = (socket.gethostname() or "localhost").split(".")[0]
+    priv, _pub, _fp = keys.ensure_cluster_key(Path(state_dir) / "keys")  # the wizard's SDC_KEY (no ssh uses it)
+    inv = {"hosts": [{"name": name, "address": primary_ipv4(), "gpus": int(gpus), "role": "master",
+                      "connection": "local"}], "ssh": {"key": str(priv)},
+           "python": sys.executable, "workdir": str(Path(state_dir).resolve() / "host")}
+    p = Path(state_dir) / "local-host-inventory.json"
+    atomic_write_json(p, inv)
+    return p
 
 
 class BareMetalProvider(Provider):
@@ -142,6 +191,8 @@ class BareMetalProvider(Provider):
         raise ProvisionError(f"host {name!r} is not in the bare-metal inventory")
 
     def target(self, host: dict) -> ssh.SSHTarget:
+        if host.get("connection") == "local":  # the orchestrator's own host (local_host_inventory)
+            return ssh.SSHTarget(host=host["address"], local=True)
         inv = self.inventory()
         o = {**inv["ssh"], **host.get("ssh", {})}
         ctl = ssh.control_dir_for(self.state_dir)
@@ -322,6 +373,8 @@ class BareMetalProvider(Provider):
         hv = {"ansible_user": t.user, "ansible_port": t.port, "tk8s_home": m.home, "tk8s_machine_dir": m.sandbox,
               "tk8s_gpus": ",".join(map(str, m.gpus)),
               "ansible_python_interpreter": m.python or "python3"}
+        if t.local:
+            return {**hv, "ansible_connection": "local"}
         if t.key:
             hv["ansible_ssh_private_key_file"] = os.path.expanduser(t.key)
         if t.known_hosts:

@@ -40,6 +40,7 @@ class SSHTarget:
     control_dir: str = ""          # where multiplexing sockets live ("" = no multiplexing)
     connect_timeout: int = 10
     extra_opts: tuple = field(default_factory=tuple)
+    local: bool = False            # this very host (inventory ``connection: local``): no ssh at all
 
     def argv(self, command: str | None = None, *, tty: bool = False) -> list[str]:
         prog = shlex.split(os.environ.get("TK8S_SSH", "ssh"))
@@ -81,6 +82,8 @@ def run(target: SSHTarget, command: str, *, timeout: float = 300, stdin: bytes |
     failure (unreachable, auth): retried ``retries_on_connect`` times (a machine still booting)."""
     import time
 
+    if target.local:
+        return _run_local(command, timeout=timeout, stdin=stdin)
     attempt = 0
     while True:
         try:
@@ -97,6 +100,52 @@ def run(target: SSHTarget, command: str, *, timeout: float = 300, stdin: bytes |
             time.sleep(min(2.0 * attempt, 10.0))
             continue
         return r.returncode, out
+
+
+def local_login_env() -> dict:
+    """The environment a command gets on a ``connection: local`` host: what a login over ssh would
+    give it (PATH, HOME, USER, LANG, SHELL), none of the orchestrator's own variables.
+    ``TK8S_LOCAL_HOST_ROOT`` (CPU tests): the host is a fake root -- a directory laid out like
+    tests/fakessh.py's (its ``bin/`` the whole PATH, ``sysroot/`` the system paths, ``.env`` its
+    /etc/environment) -- so the kubeadm roles run against simulated tools."""
+    import getpass
+
+    env = {"PATH": os.environ.get("PATH", "/usr/local/sbin:/usr/local/bin:/usr/sbin:/usr/bin:/sbin:/bin"),
+           "HOME": os.path.expanduser("~"), "USER": getpass.getuser(), "LOGNAME": getpass.getuser(),
+           "LANG": "C.UTF-8", "SHELL": "/bin/bash"}
+    fake = os.environ.get("TK8S_LOCAL_HOST_ROOT")
+    if fake:
+        hd = Path(fake)
+        env.update(HOME=str(hd), PATH=str(hd / "bin"), TK8S_SYSROOT=str(hd / "sysroot"))
+        envf = hd / ".env"
+        if envf.exists():
+            for ln in envf.read_text().splitlines():
+                if "=" in ln and not ln.startswith("#"):
+                    k, v = ln.split("=", 1)
+                    env[k.strip()] = v.strip()
+    return env
+
+
+def _run_local(command: str, *, timeout: float, stdin: bytes | None) -> tuple[int, str]:
+    """``run`` on this host itself: the login shell's command in the login home, like ssh."""
+    env = local_login_env()
+    if os.environ.get("TK8S_LOCAL_HOST_ROOT"):  # a simulated root: nothing may touch the real system paths
+        import re
+
+        free = re.sub(r"\$\{?TK8S_SYSROOT(:-)?\}?/[^\s'\"]*", "",
+                      re.sub(re.escape(env["TK8S_SYSROOT"]) + r"/[^\s'\"]*", "", command))
+        for word in ("/etc/apt", "/etc/kubernetes", "/etc/containerd", "/etc/modules-load.d", "/etc/sysctl.d",
+                     "/etc/fstab", "/opt/tk8s", "/root/.kube"):
+            if word in free:
+                return 126, f"local: refusing a system path outside the simulated root ({word})"
+    try:
+        r = subprocess.run(["bash", "-c", command], input=stdin if stdin is not None else b"", capture_output=True,
+                           timeout=timeout, env=env, cwd=env["HOME"])
+    except subprocess.TimeoutExpired:
+        return 124, f"local: timeout after {timeout}s"
+    except OSError as e:
+        return 127, f"local: {e}"
+    return r.returncode, (r.stdout or b"").decode(errors="replace") + (r.stderr or b"").decode(errors="replace")
 
 
 def remote_script(command: str, *, cwd: str | None = None, env: dict | None = None) -> str:
