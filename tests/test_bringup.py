@@ -693,8 +693,11 @@ def test_shared_burnin_result_is_single_use(ws):
             if p.get("status", {}).get("phase") == "Succeeded":
                 break
         except Exception:  # noqa: BLE001 - not re-created yet
-            pass
-        assert time.monotonic() < deadline
+            p = None
+        if time.monotonic() >= deadline:
+            log = ws / ".tk8s" / "machines" / "kubenode1" / "pods" / "kube-system_amd-gpu-validation-kubenode1" / "log"
+            raise AssertionError(json.dumps({"status": (p or {}).get("status"), "run": sorted(x.name for x in run.iterdir()),
+                                             "log": log.read_text()[-1500:] if log.exists() else None})[:4000])
         time.sleep(0.05)
     res = p["status"]["result"]
     assert res["ok"] and not res.get("host_burnin")  # its own probe, not the shared burn-in

@@ -185,7 +185,9 @@ def test_a_gpu_pod_runs_on_its_gpus_numa_local_cpus(tmp_path, fake_sysfs, mode):
             ordinal = int(p["metadata"]["annotations"]["amd.com/gpu-ids"].split(",")[0].replace("gpu", ""))
             want = "0-3" if ordinal < 4 else "4-7"
             out = kc("logs", name).stdout
-            assert out.split()[-1] == want, (name, ordinal, out, p["metadata"]["annotations"])
+            node = json.loads(kc("get", "node", p["spec"]["nodeName"], "-o", "json").stdout)
+            assert out.split()[-1] == want, (name, ordinal, out, p["metadata"]["annotations"].get("tk8s.amd.com/resources"),
+                                             node["metadata"]["annotations"].get("tk8s.amd.com/resource-enforcement"))
             assert f"cpus {want}" in p["metadata"]["annotations"]["tk8s.amd.com/resources"]
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, timeout=120)

@@ -112,6 +112,16 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
         self.pod_eviction_timeout = float(os.environ.get("TK8S_POD_EVICTION_TIMEOUT", "300"))
         self._routes()
 
+    @property
+    def _seq(self) -> int:
+        """The server's name sequence (generated names, ids): kept with the store, so it survives
+        a restart (snapshot + journal) and no name is ever handed out twice."""
+        return self.store.meta.get("seq", 0)
+
+    @_seq.setter
+    def _seq(self, v: int) -> None:
+        self.store.meta["seq"] = v
+
     # ---- utilities --------------------------------------------------------------------
     def _log_error(self, text: str) -> None:
         sys.stderr.write(text)
@@ -516,11 +526,14 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
     async def run(self, ready_file: str | None = None) -> None:
         if self.state_dir:
             self.state_dir.mkdir(parents=True, exist_ok=True)
-            if self.store.restore(self.state_dir / "controlplane.json"):
+            restored = self.store.restore(self.state_dir / "controlplane.json")
+            replayed = self.store.open_journal(self.state_dir / "controlplane.journal")
+            if restored or replayed:
                 now = time.monotonic()
                 for key in self.store.keys("nodes"):
                     self.leases[key] = now  # grace period for agents to resume heartbeats
-                self._seq = self.store.rv + 1000
+                # names the server derives from its sequence never repeat one it handed out before
+                self._seq = max(self._seq, self.store.rv) + 1000
         self._ensure_templates()
         host, port = await self.http.start(self.host, self.port)
         self.port = port
