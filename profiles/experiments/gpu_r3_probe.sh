@@ -22,13 +22,13 @@ BIN="$ROOT/tritonk8ssupervisor_amd/bin"
   echo "--- mounts"; grep -E ' /dev| /sys' /proc/self/mountinfo
   echo "--- unshare"; timeout -k 5 20 unshare -Urm sh -c 'id; mount -t tmpfs none /tmp && echo tmpfs-on-tmp-ok'; echo "rc=$?"
 } > "$OUT/userns.log" 2>&1
-timeout -k 5 30 python3 "$ROOT/scripts/r3_isolation_try.py" >> "$OUT/userns.log" 2>&1; echo "isolation try rc=$?" >> "$OUT/userns.log"
+timeout -k 5 30 python3 "$ROOT/profiles/experiments/r3_isolation_try.py" >> "$OUT/userns.log" 2>&1; echo "isolation try rc=$?" >> "$OUT/userns.log"
 echo "[r3probe] userns done"
 # RCCL start-up, stamped line by line
-timeout -k 10 120 python3 "$ROOT/scripts/r3_stamp.py" "$OUT/rccl_info.log" NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=ALL -- \
+timeout -k 10 120 python3 "$ROOT/profiles/experiments/r3_stamp.py" "$OUT/rccl_info.log" NCCL_DEBUG=INFO NCCL_DEBUG_SUBSYS=ALL -- \
   "$BIN/tk8s-rccl" --ngpus 1 --max-bytes 1048576 --factor 4 > "$OUT/rccl_info.json" &&
 echo "[r3probe] rccl stamped done" &&
-timeout -k 10 120 python3 "$ROOT/scripts/r3_stamp.py" "$OUT/rccl_plain.log" -- "$BIN/tk8s-rccl" --ngpus 1 --max-bytes 1048576 --factor 4 > "$OUT/rccl_plain.json" &&
+timeout -k 10 120 python3 "$ROOT/profiles/experiments/r3_stamp.py" "$OUT/rccl_plain.log" -- "$BIN/tk8s-rccl" --ngpus 1 --max-bytes 1048576 --factor 4 > "$OUT/rccl_plain.json" &&
 cd /tmp && timeout -k 10 180 rocprofv3 --hip-trace --kernel-trace --stats -d "$OUT/prof_rccl" -o rccl --output-format csv -- \
   "$BIN/tk8s-rccl" --ngpus 1 --max-bytes 1048576 --factor 4 > "$OUT/rocprof_rccl.log" 2>&1 &&
 echo "[r3probe] done"
