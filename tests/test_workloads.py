@@ -1034,6 +1034,48 @@ def test_hpa_rate_limit_policies():
     assert _rate_limit(two, 10, 30) == 11  # the smaller of +2 and +10 %
 
 
+def test_hpa_rate_limit_counts_each_policys_period():
+    """a policy's budget is per periodSeconds, not per reconcile -- two steps inside
+    one window add up to what the policy allows, and the budget comes back when it ends."""
+    from tritonk8ssupervisor_amd.controlplane.metrics_api import _rate_limit
+
+    beh = {"scaleUp": {"policies": [{"type": "Pods", "value": 1, "periodSeconds": 60}]},
+           "scaleDown": {"policies": [{"type": "Percent", "value": 50, "periodSeconds": 120}]}}
+    assert _rate_limit(beh, 4, 10, [(0.0, 1)], now=15.0) == 4  # 3 -> 4 at t=0 spent the minute
+    assert _rate_limit(beh, 4, 10, [(0.0, 1)], now=61.0) == 5  # a new window
+    # down: 50 % of the 10 replicas at the window's start, whatever steps it took to get there
+    assert _rate_limit(beh, 7, 1, [(0.0, -3)], now=30.0) == 5
+    assert _rate_limit(beh, 5, 1, [(0.0, -3), (30.0, -2)], now=60.0) == 5
+    assert _rate_limit(beh, 5, 1, [(0.0, -3), (30.0, -2)], now=125.0) == 3  # 50 % of 7 (the t=0 step aged out)
+    # the default scale-up policy (100 % or 4 pods per 15 s): 2 -> 6 -> hold -> 6 -> 12
+    assert _rate_limit({}, 6, 40, [(0.0, 4)], now=5.0) == 6
+    assert _rate_limit({}, 6, 40, [(0.0, 4)], now=16.0) == 12
+
+
+def test_hpa_controller_honours_period_seconds(cp):
+    """The controller records its own scale events: with 1 pod per 60 s, reconciles 15 s apart
+    move the target by one replica per minute, not one per reconcile."""
+    cp.create("1a1", "deployments", "default", {"metadata": {"name": "web"}, "spec": {
+        "replicas": 1, "selector": {"matchLabels": {"app": "web"}},
+        "template": {"metadata": {"labels": {"app": "web"}}, "spec": {"containers": [{
+            "name": "c", "command": ["x"], "resources": {"requests": {"cpu": "100m"}}}]}}}})
+    cp.create("1a1", "horizontalpodautoscalers", "default", {"metadata": {"name": "web"}, "spec": {
+        "scaleTargetRef": {"apiVersion": "apps/v1", "kind": "Deployment", "name": "web"},
+        "minReplicas": 1, "maxReplicas": 10,
+        "metrics": [{"type": "Resource", "resource": {"name": "cpu", "target": {"type": "Utilization",
+                                                                                "averageUtilization": 50}}}],
+        "behavior": {"scaleUp": {"policies": [{"type": "Pods", "value": 1, "periodSeconds": 60}]}}}})
+    seen = []
+    for t in (1000.0, 1015.0, 1030.0, 1061.0):
+        for n in _pods(cp, "web-"):
+            cp.store.patch("pods", _key("1a1", "default", n), lambda o: o["status"].update(phase="Running"))
+        cp._ingest_metrics("1a1", "kubenode1", {"pods": {f"default/{n}": [{"name": "c", "cpu_cores": 0.5, "memory_bytes": 0}]
+                                                         for n in _pods(cp, "web-")}})
+        cp._ctl_hpas("1a1", now=t)
+        seen.append(cp.store.get("deployments", _key("1a1", "default", "web"))["spec"]["replicas"])
+    assert seen == [2, 2, 2, 3], seen
+
+
 def test_daemonset_rolling_update(cp):
     _nodes(cp, 3)
     cp.create("1a1", "daemonsets", "default", {"metadata": {"name": "mon"}, "spec": {

@@ -14,7 +14,8 @@ its target's pods' usage and requests, and scales the target's ``replicas`` to
 node agents) -- within
 [minReplicas, maxReplicas], ignoring changes inside a 10 % tolerance, and keeping the highest
 recommendation of the scale-down stabilization window (``behavior.scaleDown.
-stabilizationWindowSeconds``, default 300). Pods that are not Running or have no sample yet
+stabilizationWindowSeconds``, default 300), and moving no further than ``behavior``'s policies
+allow within each policy's ``periodSeconds`` (the controller keeps its own scale events). Pods that are not Running or have no sample yet
 are left out, as Kubernetes does for unready pods.
 """
 from __future__ import annotations
@@ -37,29 +38,35 @@ def resource_list() -> dict:
         {"name": "pods", "singularName": "", "namespaced": True, "kind": "PodMetrics", "verbs": ["get", "list"]}]}
 
 
-def _rate_limit(behavior: dict, current: int, desired: int) -> int:
-    """The HPA's scaling policies: how far one step may go (``behavior.scaleUp|scaleDown``:
-    ``policies`` of ``Pods``/``Percent`` per ``periodSeconds``, ``selectPolicy`` Max|Min|Disabled).
-    Defaults as Kubernetes': up by max(100 %, 4 pods), down by up to 100 %."""
-    import math
-
+def _rate_limit(behavior: dict, current: int, desired: int, events=(), now: float = 0.0) -> int:
+    """The HPA's scaling policies: how far the target may move within each policy's window
+    (``behavior.scaleUp|scaleDown``: ``policies`` of ``Pods``/``Percent`` per ``periodSeconds``,
+    ``selectPolicy`` Max|Min|Disabled). ``events`` are this autoscaler's past changes as
+    ``(time, replica delta)``: a policy's budget is counted from the replica count at
+    the start of its window, so two quick steps cannot add up to more than one policy allows.
+    Defaults as Kubernetes': up by max(100 %, 4 pods) per 15 s, down by up to 100 % per 15 s."""
     up = desired > current
     rules = behavior.get("scaleUp" if up else "scaleDown") or {}
     if rules.get("selectPolicy") == "Disabled":
         return current
-    pols = rules.get("policies") or ([{"type": "Percent", "value": 100}, {"type": "Pods", "value": 4}] if up
-                                     else [{"type": "Percent", "value": 100}])
+    pols = rules.get("policies") or ([{"type": "Percent", "value": 100, "periodSeconds": 15},
+                                      {"type": "Pods", "value": 4, "periodSeconds": 15}] if up
+                                     else [{"type": "Percent", "value": 100, "periodSeconds": 15}])
     limits = []
     for p in pols:
         v = int(p.get("value", 0))
-        step = v if p.get("type") == "Pods" else math.ceil(current * v / 100.0)
-        limits.append(current + step if up else max(0, current - step))
+        period = float(p.get("periodSeconds", 15))
+        moved = sum(d for t, d in events if now - t < period and (d > 0) == up)
+        start = current - moved  # the replica count when this policy's window opened
+        step = v if p.get("type") == "Pods" else math.ceil(start * v / 100.0)
+        limits.append(start + step if up else max(0, start - step))
     if not limits:
         return desired
     pick = (max if rules.get("selectPolicy", "Max") == "Max" else min) if up else \
         (min if rules.get("selectPolicy", "Max") == "Max" else max)
     bound = pick(limits)
-    return min(desired, bound) if up else max(desired, bound)
+    # a window already spent holds the target where it is, never moves it back
+    return max(current, min(desired, bound)) if up else min(current, max(desired, bound))
 
 
 class MetricsAPI:
@@ -144,7 +151,7 @@ class MetricsAPI:
         now = time.time() if now is None else now
         samples = self._pod_samples(pid)
         if not hasattr(self, "_hpa_recs"):
-            self._hpa_recs = {}
+            self._hpa_recs, self._hpa_events = {}, {}
         for hpa in self.store.list("horizontalpodautoscalers", lambda o: self._in(pid, o)):
             ns, name = hpa["metadata"]["namespace"], hpa["metadata"]["name"]
             spec = hpa["spec"]
@@ -235,10 +242,12 @@ class MetricsAPI:
                 desired = min(current, max(r for t, r in recs if now - t <= down_w))
             elif desired > current:
                 desired = max(current, min(r for t, r in recs if now - t <= up_w))
-            desired = min(hi, max(lo, _rate_limit(beh, current, desired)))
+            events = [(t, d) for t, d in self._hpa_events.get((pid, ns, name), []) if now - t < 1800]
+            desired = min(hi, max(lo, _rate_limit(beh, current, desired, events, now)))
             status = {**st, "currentReplicas": current, "desiredReplicas": desired, "currentMetrics": current_metrics,
                       "conditions": conds["conditions"]}
             if desired != current:
+                self._hpa_events[(pid, ns, name)] = events + [(now, desired - current)]
                 self.replace(pid, plural, ns, ref["name"], {"spec": {"replicas": desired}}, merge=True,
                              manager="horizontal-pod-autoscaler", subresource="scale")
                 status["lastScaleTime"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(now))
