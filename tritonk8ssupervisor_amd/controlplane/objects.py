@@ -131,6 +131,10 @@ GPU_SCOPE = "tk8s.amd.com/gpu-scope"
 _RESERVED = ((GPU_VISIBILITY, "node"), (GPU_SCOPE, "host"))
 # set by the scheduler on host-scoped pods (scheduler.py): never by a client
 _SCHEDULER_OWNED = ("tk8s.amd.com/host-claims", "tk8s.amd.com/host-devices")
+# an Indexed Job's pods on one host open each other's GPUs (agent.py _gather_peers): from the
+# Job's template only; the GPUs each pod was given are published by its node agent (pod status)
+GPU_PEERS = "tk8s.amd.com/gpu-peers"
+_AGENT_OWNED = ("tk8s.amd.com/gpu-devices", GPU_PEERS)
 
 
 def _reserved(ann: dict) -> str | None:
@@ -172,6 +176,11 @@ def _admit_gpu_visibility(kind: str, ns: str, body: dict, cur: dict | None = Non
         for k in _SCHEDULER_OWNED:
             if ann.get(k) != old.get(k):
                 raise HttpError(403, f"pods is forbidden: annotation {k} is set by the scheduler")
+        for k in _AGENT_OWNED:
+            if ann.get(k) != old.get(k):
+                raise HttpError(403, f"pods is forbidden: annotation {k} comes from an Indexed Job's pod template "
+                                     "and the pod's node" if k == GPU_PEERS else
+                                f"pods is forbidden: annotation {k} is set by the pod's node")
     elif kind in ("jobs", "daemonsets", "deployments", "statefulsets", "replicasets", "cronjobs"):
         spec = body.get("spec") or {}
         if kind == "cronjobs":
@@ -180,6 +189,12 @@ def _admit_gpu_visibility(kind: str, ns: str, body: dict, cur: dict | None = Non
         what = _reserved(ann)
         if what and (kind != "jobs" or ns != "kube-system"):
             raise HttpError(403, f"{kind} is forbidden: annotation {what} is reserved for kube-system Jobs")
+        if GPU_PEERS in ann:
+            if kind not in ("jobs", "cronjobs") or spec.get("completionMode") != "Indexed":
+                raise HttpError(422, f"{kind} is invalid: annotation {GPU_PEERS} is for the pod template of an "
+                                     "Indexed Job (completionMode: Indexed)")
+            if ann[GPU_PEERS] != "job":
+                raise HttpError(422, f'{kind} is invalid: annotation {GPU_PEERS}: supported value: "job"')
 
 
 def _normalize_data(kind: str, body: dict) -> None:

@@ -13,6 +13,12 @@ as native/tools/tk8s_rccl.cpp (``ok``, ``nranks``, ``rank``, ``peak_busbw_gbps``
 I*k .. I*k+k-1, like ``tk8s-rccl --group-index``): torch.distributed has one default group per
 process, so the pod runs its k ranks as child processes and prints ONE merged line for the pod.
 
+With ``NCCL_DEBUG`` set (INFO), RCCL's log goes to a file of the rank's own (``NCCL_DEBUG_FILE``,
+unless the caller named one); the rank copies it to stderr and reports in its JSON line which
+transport RCCL's channels took (``transport``: counts of ``via P2P/...``, ``via SHM/...``,
+``via NET/...`` connections, and whether the communicator's init completed) -- what tells
+whether ranks in separate pods still go GPU to GPU over xGMI.
+
 Check (N6 semantics): rank r contributes ``(r + 1) * p[i]`` with ``p[i] = (i % m) + 1``;
 every element must equal ``n (n + 1) / 2 * p[i]`` exactly. ``m`` keeps every partial sum an
 exactly representable integer: 251 for fp32 (< 2^24), 4 for bf16 (sums <= 256 up to n = 8).
@@ -63,6 +69,33 @@ def _fetch(url: str, timeout: float) -> str:
         except OSError:
             time.sleep(0.02)
     raise TimeoutError(f"no rendezvous address at {url} after {timeout:.0f}s")
+
+
+def rccl_transport(text: str) -> dict:
+    """What RCCL's ``NCCL_DEBUG=INFO`` log says about the channels it connected: per transport
+    (P2P, SHM, NET, ...) the number of ``via <transport>/...`` connections and their forms, and
+    whether ``Init COMPLETE`` was logged."""
+    import re
+
+    counts: dict[str, int] = {}
+    forms: dict[str, int] = {}
+    for m in re.finditer(r"\bvia ([A-Z0-9]+)(/[\w/.:-]*)?", text):
+        counts[m.group(1)] = counts.get(m.group(1), 0) + 1
+        form = m.group(1) + (m.group(2) or "")
+        forms[form] = forms.get(form, 0) + 1
+    return {"counts": counts, "forms": forms, "init_complete": "Init COMPLETE" in text,
+            "lines": text.count("\n")}
+
+
+def _debug_file() -> str | None:
+    """Route RCCL's INFO log to a file of this rank's (before RCCL is loaded), if NCCL_DEBUG is on."""
+    if not os.environ.get("NCCL_DEBUG"):
+        return None
+    if not os.environ.get("NCCL_DEBUG_FILE"):
+        import tempfile
+
+        os.environ["NCCL_DEBUG_FILE"] = os.path.join(tempfile.gettempdir(), f"tk8s-rccl-{os.getpid()}.log")
+    return os.environ["NCCL_DEBUG_FILE"]
 
 
 def _free_port(host: str) -> int:
@@ -173,6 +206,7 @@ def main(argv=None) -> int:
             return _rank_group(a, argv if argv is not None else sys.argv[1:], len(devs))
         a.rank = a.group_index
     t0 = time.monotonic()
+    debug_file = _debug_file() if a.backend == "nccl" else None
     host = os.environ.get("NODE_IP", "127.0.0.1")
     try:
         if a.rank == 0:
@@ -205,6 +239,15 @@ def main(argv=None) -> int:
         for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS"):
             out[k.lower()] = os.environ.get(k) or "auto"
         out["peak_links_equivalent"] = res["peak_busbw_gbps"] / 153.0 if a.nranks > 1 else 0.0
+    if debug_file and "%" not in debug_file:
+        try:
+            with open(debug_file, errors="replace") as f:
+                text = f.read()
+            sys.stderr.write(text)
+            sys.stderr.flush()
+            out["transport"] = rccl_transport(text)
+        except OSError as e:
+            out["transport"] = {"error": f"{debug_file}: {e}"}
     print(json.dumps(out))
     return 0 if res["ok"] else 1
 
