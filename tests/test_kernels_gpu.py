@@ -967,6 +967,16 @@ def test_torch_allreduce_job_manifest_on_one_gpu(tmp_path):
             got = set(parse_cpulist(next(x for x in log.splitlines() if x.startswith("Cpus_allowed_list")).split()[-1]))
             want = local & os.sched_getaffinity(0) or os.sched_getaffinity(0)
             assert got == want, (sorted(got)[:8], len(got), sorted(local)[:8], len(local))
+        if os.environ.get("GRAFT_REPO_ROOT"):  # evidence for profiles/: what the rank saw
+            from pathlib import Path
+
+            ev = Path(os.environ["GRAFT_REPO_ROOT"]) / "gpurun_out" / "torch_job_1gpu.json"
+            ev.parent.mkdir(parents=True, exist_ok=True)
+            ev.write_text(json.dumps({"result": res, "describe": d, "render_minor": minor,
+                                      "cpus_allowed": next((x for x in log.splitlines()
+                                                            if x.startswith("Cpus_allowed_list")), ""),
+                                      "local_cpulist": open(local_f).read().strip() if os.path.exists(local_f) else None,
+                                      "rccl_log_tail": [x for x in log.splitlines() if "NCCL INFO" in x][-40:]}, indent=1))
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
