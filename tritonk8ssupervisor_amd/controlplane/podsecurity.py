@@ -14,8 +14,13 @@ The checks are the standards' (v1.30) for what a pod spec can say here:
   and no ``runAsUser: 0``, ``allowPrivilegeEscalation: false``, capabilities dropping ``ALL``
   (adding at most ``NET_BIND_SERVICE``), a ``RuntimeDefault`` or ``Localhost`` seccomp profile.
 
-A multi-tenant GPU cluster uses ``baseline`` to keep tenants from mounting the host's ``/dev``
-or ``/sys`` -- the GPU jail limits the render nodes a pod may open, this keeps the rest out.
+What every pod gets whatever its level (the node's runtime, not this admission): the jail
+(native/tools/gpujail.h) opens no render node of a GPU the pod does not hold, never creates a
+device node (MAKE_CHAR / MAKE_BLOCK are handled and never granted) and denies the cluster's state
+(the workspace's ``.tk8s/``: kubeconfig, tokens, keys, other pods' directories); image pods run
+after ``pivot_root`` with Docker's default capability bounding set, the host's ``/sys`` and
+``/proc/sys`` read-only (native/tools/tk8s_container.cpp). A multi-tenant GPU cluster adds
+``baseline`` to keep tenants from ``hostPath`` volumes and the host's namespaces.
 """
 from __future__ import annotations
 
