@@ -163,7 +163,7 @@ class Agent:
         # (published in GPU_DEVICES so the peers can find them) until the pod starts or goes away
         self._reserved: dict[str, tuple[list[str], dict, float]] = {}
         self._node_hosts: dict[str, str] = {}
-        self._start_lock = threading.Lock()
+        self._start_lock = threading.RLock()
         self._execs_seen: set[str] = set()
         if url:
             self.set_url(url)
@@ -415,6 +415,7 @@ class Agent:
             self._config_wait[key] = pod
             return
         self._config_wait.pop(key, None)
+        trace(self.name, f"start {key}: config and volumes ready")
         ann = md.get("annotations", {})
         visibility = ann.get(GPU_VISIBILITY, "allocated")
         scope = ann.get(GPU_SCOPE, "node")
@@ -476,6 +477,7 @@ class Agent:
             self._report(key, md["name"], md["namespace"], "Failed",
                          {"reason": "UnexpectedAdmissionError", "message": f"Allocate failed: {e}"}, None)
             return
+        trace(self.name, f"start {key}: allocated {','.join(ids) or 'no GPU'}")
         ordinals = [self._ordinal(i) for i in ids]
         peer_devs: list[dict] = []
         if peers is not None:
@@ -518,6 +520,7 @@ class Agent:
         if peers is not None:
             gpu_isolation += ("; Job peers on this host: " + ", ".join(f"{d['node']}/{d['id']}" for d in peer_devs)
                               if peer_devs else "; no Job peer on this host")
+        trace(self.name, f"start {key}: isolation probed")
         layers = self._jail_layers(pod, pp_dir, vol_dirs)
         from .resources import gpu_local_cpus, pod_limits
 
@@ -538,6 +541,7 @@ class Agent:
             gpu_isolation += f"; node state denied ({', '.join(layers['deny'])})" + (
                 "; signals scoped to the pod" if gpu_pod and jail_signal_scoping() else
                 "; shares the host PID namespace: signals not scoped (Landlock ABI < 6)" if gpu_pod else "")
+        trace(self.name, f"start {key}: limits set")
         procs = []
         for n, cont in enumerate(inits + apps):
             first_app = cont is apps[0]
@@ -567,6 +571,7 @@ class Agent:
                                                 "tk8s.amd.com/isolation": isolation,
                                                 "tk8s.amd.com/gpu-isolation": gpu_isolation,
                                                 "tk8s.amd.com/resources": resources}}
+        trace(self.name, f"start {key}: handed to the runtime")
         self.runtime.start(pp)
 
     def _peers_forbidden(self, pod: dict, value: str, need: int, scope: str, visibility: str) -> str | None:
@@ -1044,9 +1049,12 @@ class Agent:
 
     def _terminated(self, key: str) -> None:
         """A pod's termination is over: its IP is free, and a successor of the same name may start."""
-        if key not in self.runtime.running():
-            self._pod_ips.pop(key, None)
-            self.enforcer.release(key)
+        # under the start lock: a successor of the same name (a DaemonSet's re-created pod) may be
+        # between its set-up -- its cgroup, its IP, both keyed by the name -- and its start
+        with self._start_lock:
+            if key not in self.runtime.running():
+                self._pod_ips.pop(key, None)
+                self.enforcer.release(key)
         for k, nxt in list(self._config_wait.items()):  # its name, its GPUs: what waited may start now
             if k not in self.runtime.running():
                 self._start_pod(nxt)
