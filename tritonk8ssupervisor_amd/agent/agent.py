@@ -1060,8 +1060,17 @@ class Agent:
                 self._start_pod(nxt)
 
     # ---- lifecycle --------------------------------------------------------------------
+    def _probe_isolation(self) -> None:
+        """The pod runtime's one-time probes (the GPU jail's Landlock ABI, user namespaces), each a
+        child process: run while the agent waits for its registration URL, not when the first pod
+        (the validation pod, on the bring-up's critical path) starts."""
+        gpu_jail()
+        namespace_isolation(str(Path(TK8S_HOME) / "tritonk8ssupervisor_amd" / "__init__.py"), str(self.sandbox / "pods"))
+        trace(self.name, "isolation probed")
+
     def run(self, await_url: Path | None = None) -> int:
         install_sigterm()
+        threading.Thread(target=self._probe_isolation, name="isolation-probe", daemon=True).start()
         if self.device_plugin == "grpc":  # before the URL wait: off the join's critical path
             self.start_grpc_plugin()
         if not self.reg_url and await_url is not None:

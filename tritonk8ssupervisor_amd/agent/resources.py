@@ -119,10 +119,14 @@ def _own_cgroups() -> dict[str, str]:
     return out
 
 
+SWEEP_MIN_AGE_S = 60.0
+
+
 def _sweep(parent: Path) -> None:
     """Remove the machine cgroups under ``parent`` that hold no process any more (an agent killed
     before it could clean up): rmdir of a cgroup fails while anything lives in it, and a live
-    agent lives in its own machine's (``Enforcer``), so a live cluster's cgroups stay."""
+    agent lives in its own machine's (``Enforcer``), so a live cluster's cgroups stay. One made in
+    the last minute is left alone: its agent may be between the mkdir and moving itself in."""
     def live(m: Path) -> bool:  # its agent still runs in it (v1: the machine itself, v2: its leaf)
         for f in (m / "cgroup.procs", m / "agent" / "cgroup.procs"):
             try:
@@ -132,9 +136,15 @@ def _sweep(parent: Path) -> None:
                 pass
         return False
 
+    import time
+
     try:
         for m in parent.glob("tk8s-machine-*"):
-            if live(m):
+            try:
+                young = time.time() - m.stat().st_ctime < SWEEP_MIN_AGE_S
+            except OSError:
+                continue
+            if young or live(m):
                 continue
             for d in m.glob("pod-*"):
                 try:
@@ -184,6 +194,7 @@ class Enforcer:
                     return
             except OSError as e:
                 self.why += f"{mode}: {e}; "
+                self._undo()
         if self.mode == "none":
             self.why = self.why or "no mode available"
 
@@ -210,6 +221,7 @@ class Enforcer:
         _sweep(own)
         m = own / f"tk8s-machine-{self.node}"
         m.mkdir(exist_ok=True)
+        self.base = {"": m}  # (what _undo removes if this mode fails)
         (m / "agent").mkdir(exist_ok=True)  # the agent lives in its machine (a leaf: no internal processes)
         _write(m / "agent" / "cgroup.procs", os.getpid())
         _write(m / "cgroup.subtree_control", " ".join(f"+{c}" for c in ctrls))
@@ -230,13 +242,14 @@ class Enforcer:
             _sweep(d)
             m = d / f"tk8s-machine-{self.node}"
             m.mkdir(exist_ok=True)
+            base[c] = self.base[c] = m  # (self.base: what _undo removes if this mode fails)
             if c == "cpuset":  # a v1 cpuset starts empty: inherit the parent's before any task joins
                 for f in ("cpuset.cpus", "cpuset.mems"):
                     if not (m / f).read_text().strip():
                         _write(m / f, (d / f).read_text().strip())
-            base[c] = m
         if "memory" not in base:
             self.why += "cgroup1: no writable memory hierarchy; "
+            self._undo()
             return False
         self.base = base
         for c, m in base.items():
@@ -246,6 +259,21 @@ class Enforcer:
 
     def _setup_watchdog(self) -> bool:
         return True
+
+    def _undo(self) -> None:
+        """A cgroup mode failed half way: the agent goes back where it was, nothing of the mode
+        stays (a later mode must not think a cpuset fences its pods)."""
+        for ctrl, m in self.base.items():
+            try:
+                if ctrl == "":
+                    _write(m.parent / "tk8s-agent" / "cgroup.procs", os.getpid())
+                    os.rmdir(m / "agent")
+                else:
+                    _write(m.parent / "cgroup.procs", os.getpid())
+                os.rmdir(m)
+            except OSError:
+                pass
+        self.base = {}
 
     # ---- limits ----------------------------------------------------------------------------
     def _limit(self, d: Path, ctrl: str, lim: Limits) -> None:

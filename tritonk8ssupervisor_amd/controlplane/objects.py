@@ -118,10 +118,14 @@ def merge_patch(target, patch):
 
 
 def template_hash(template: dict) -> str:
-    """``pod-template-hash`` of a Deployment's pod template (names its ReplicaSet generation)."""
-    import hashlib  # off the control plane's start-up path (it is on the bring-up's)
+    """``pod-template-hash`` of a Deployment's pod template (names its ReplicaSet generation):
+    CRC-32 and Adler-32 of its canonical JSON, 10 hex digits -- a name, not a security check
+    (Kubernetes uses FNV-32). zlib, not hashlib: OpenSSL's binding costs the first DaemonSet
+    create ~2.5 ms of imports, on the bring-up's critical path."""
+    import zlib
 
-    return hashlib.sha1(json.dumps(template, sort_keys=True, separators=(",", ":")).encode()).hexdigest()[:10]
+    b = json.dumps(template, sort_keys=True, separators=(",", ":")).encode()
+    return f"{zlib.crc32(b):08x}{zlib.adler32(b):08x}"[:10]
 
 
 GPU_VISIBILITY = "tk8s.amd.com/gpu-visibility"

@@ -9,7 +9,7 @@ Identities (``identity_of``):
   keeps for every ServiceAccount, mounted into pods) -- ``system:serviceaccount:<ns>:<name>``,
   authorized by Roles/ClusterRoles bound to it (or to ``system:serviceaccounts[:<ns>]`` /
   ``system:authenticated``) through RoleBindings/ClusterRoleBindings;
-* no token -- anonymous: it may read, except Secrets (and may not write).
+* no token -- anonymous: discovery, ``/version`` and health only (authn.PUBLIC).
 
 Request attributes (``request_info``) follow the API server's: verb (get, list, watch, create,
 update, patch, delete, deletecollection), API group, resource[/subresource], namespace, name.
@@ -20,7 +20,7 @@ Secrets, no RBAC; ``admin``: edit + namespaced RBAC).
 from __future__ import annotations
 
 import re
-from dataclasses import dataclass
+from collections import namedtuple
 
 _PREFIX = re.compile(r"^/r/projects/[^/]+/kubernetes(?=/)")
 
@@ -43,13 +43,12 @@ BUILTIN_CLUSTER_ROLES = {
 }
 
 
-@dataclass
-class RequestInfo:
-    verb: str
-    group: str
-    resource: str          # "pods", or "pods/log" for a subresource
-    namespace: str
-    name: str
+class RequestInfo(namedtuple("RequestInfo", "verb group resource namespace name")):
+    """What a request does: verb, API group, resource ("pods", or "pods/log" for a subresource),
+    namespace, name. (A named tuple: ``dataclasses`` costs the first authorised request ~1 ms of
+    imports, and that request is on the bring-up's critical path.)"""
+
+    __slots__ = ()
 
     def describe(self) -> str:
         where = f' in the namespace "{self.namespace}"' if self.namespace else " at the cluster scope"
