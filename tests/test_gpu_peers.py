@@ -15,7 +15,7 @@ from test_bringup import _env, _fake_gpu_tree, _setup, _summary, ws  # noqa: F40
 
 PROBE = ("for m in 128 129; do cat {dri}/renderD$m >/dev/null 2>&1 && echo render$m=open || echo render$m=denied; done; "
          "echo rocr=$ROCR_VISIBLE_DEVICES; echo own=$TK8S_GPU_DEVICES; echo peers=$TK8S_GPU_PEER_DEVICES; "
-         "echo ids=$TK8S_GPU_IDS")
+         "echo ids=$TK8S_GPU_IDS; sleep 1")  # (alive a while, as ranks are: a peer that already finished is no peer)
 
 
 def _job(name: str, dri, peers: bool, indexed: bool = True) -> dict:

@@ -163,6 +163,7 @@ class Agent:
         # (published in GPU_DEVICES so the peers can find them) until the pod starts or goes away
         self._reserved: dict[str, tuple[list[str], dict, float]] = {}
         self._node_hosts: dict[str, str] = {}
+        self._peer_poller: threading.Thread | None = None
         self._start_lock = threading.RLock()
         self._execs_seen: set[str] = set()
         if url:
@@ -649,12 +650,26 @@ class Agent:
             waiting.append(f"(pod list: {e})")
         if waiting and time.monotonic() - since < PEER_WAIT_S:
             self._config_wait[key] = pod
+            if self._peer_poller is None or not self._peer_poller.is_alive():
+                self._peer_poller = threading.Thread(target=self._poll_peers, name="gpu-peers", daemon=True)
+                self._peer_poller.start()
             return None
         if waiting:
             print(f"{self.name}: {key} starts without Job peers {', '.join(waiting)} (not placed after "
                   f"{PEER_WAIT_S:.0f}s)", flush=True)
         self._reserved.pop(key, None)  # (under _start_lock: nothing allocates before the pod starts)
         return sorted(devices, key=lambda d: (d["node"], d["id"]))
+
+    def _poll_peers(self) -> None:
+        """Retry the gpu-peers pods waiting for their peers every 0.1 s (not on the 1 s config
+        tick): a Job's ranks start within a poll of each other."""
+        while not self.stop.wait(0.1):
+            waiting = [self._config_wait.get(k) for k in list(self._reserved)]
+            waiting = [p for p in waiting if p is not None]
+            if not waiting:
+                return
+            for p in waiting:
+                self._start_pod(p)
 
     def _jail_layers(self, pod: dict, pp_dir: Path, vol_dirs: dict) -> dict:
         """What a jailed pod may not read, may only read, and may write again beneath those
