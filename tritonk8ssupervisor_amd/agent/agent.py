@@ -164,6 +164,7 @@ class Agent:
         self._reserved: dict[str, tuple[list[str], dict, float]] = {}
         self._node_hosts: dict[str, str] = {}
         self._peer_poller: threading.Thread | None = None
+        self._registered_pods: dict | None = None   # the node's pods as the registration returned them
         self._start_lock = threading.RLock()
         self._execs_seen: set[str] = set()
         if url:
@@ -222,17 +223,6 @@ class Agent:
     # ---- join -------------------------------------------------------------------------
     def join(self) -> None:
         c = Client(self.base, timeout=10.0)
-        deadline = time.monotonic() + self.timeout
-        delay = 0.01
-        while True:
-            try:
-                boot = c.get(self.reg_path)
-                break
-            except (ApiError, OSError) as e:
-                if time.monotonic() > deadline:
-                    raise RuntimeError(f"{self.name}: control plane unreachable at {self.base}: {e}") from e
-                time.sleep(delay)
-                delay = min(delay * 2, 1.0)
         # a machine is its package's slice of the host (TK8S_MACHINE_CPUS / _MEMORY_MB): what the
         # scheduler may fit onto it, and what resources.py enforces
         cap = {"cpu": f"{self.shape.cpu:g}" if self.shape.cpu else str(os.cpu_count() or 1), "pods": "110"}
@@ -247,8 +237,20 @@ class Agent:
                 "nodeInfo": {"osImage": _os_image(), "kernelVersion": os.uname().release,
                              "architecture": os.uname().machine, "containerRuntimeVersion": "tk8s-process://0.1",
                              "kubeletVersion": "tk8s-agent/0.1", "gpuInventory": self.plugin.inventory.source}}
-        r = c.post(self.reg_path, body)
-        self.hb_period = float(r.get("heartbeatSeconds", boot.get("heartbeatSeconds", 1.0)))
+        deadline = time.monotonic() + self.timeout
+        delay = 0.01
+        while True:  # (the registration itself is the reachability check: one request, not two)
+            try:
+                r = c.post(self.reg_path, body)
+                break
+            except (ApiError, OSError) as e:
+                if isinstance(e, ApiError) and e.status < 500 or time.monotonic() > deadline:
+                    raise RuntimeError(f"{self.name}: control plane unreachable at {self.base}: {e}") from e
+                c.close()
+                time.sleep(delay)
+                delay = min(delay * 2, 1.0)
+        self.hb_period = float(r.get("heartbeatSeconds", 1.0))
+        self._registered_pods = r.get("pods")  # the watch's first list (watch_loop)
         self.api = Client(self.base, token=r["nodeToken"], prefix=r["apiPrefix"], timeout=10.0)
         self.pod_cidr = r.get("podCIDR") or ""
         c.close()
@@ -928,8 +930,8 @@ class Agent:
         while not self.stop.is_set():
             try:
                 if first:
-                    lst = api.get(path, query=q)
-                    rv = int(lst["metadata"]["resourceVersion"])
+                    lst, self._registered_pods = self._registered_pods or api.get(path, query=q), None
+                    rv = int(lst.get("resourceVersion") or lst["metadata"]["resourceVersion"])
                     for pod in lst["items"]:
                         self._handle("ADDED", pod)
                     first = False

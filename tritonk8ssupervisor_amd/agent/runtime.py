@@ -39,6 +39,7 @@ from ..utils.record import field, record as dataclass
 from ..utils.trace import trace
 
 _VAR = re.compile(r"\$\(([A-Za-z_][A-Za-z0-9_]*)\)")
+RUNNING_GRACE_S = 0.005  # a container that ends within this after its start never reports Running
 
 
 def expand(s: str, env: dict) -> str:
@@ -235,8 +236,16 @@ class PodRuntime:
             trace("runtime", f"spawned {pp.key}")
             self._post_start(pp, pp)
             self._probe(pp, pp)
-            self.on_status(pp, "Running", {})
-            rc = self._exited(pp, pp.proc.wait())
+            status = None
+            if not pp.sidecars:  # a container done within the grace is reported once, as done: a
+                try:             # Running report first would only hold up its result (the
+                    status = pp.proc.wait(timeout=RUNNING_GRACE_S)  # validation pod's ~1 ms payload)
+                except subprocess.TimeoutExpired:
+                    pass
+            if status is None:
+                self.on_status(pp, "Running", {})
+                status = pp.proc.wait()
+            rc = self._exited(pp, status)
             trace("runtime", f"exited {pp.key} rc={rc}")
             (pp.dir / _pidfile(pp)).unlink(missing_ok=True)
             if pp.stopping:

@@ -150,9 +150,15 @@ class RancherAPI:
         self._event(pid, "default", {"kind": "Node", "name": name}, "RegisteredNode", f"Node {name} registered ({len(gpus)} GPU)")
         self.reconcile()
         trace("cp", f"node {name} registered")
+        # the pods already bound to it (the validation DaemonSet's, made by the reconcile above) and
+        # the version they are at: the agent starts them and watches from there, no list first
+        pods = sorted((self._strip(o) for o in self.store.list(
+            "pods", lambda o: o["spec"].get("nodeName") == name and self._in(pid, o))),
+            key=lambda o: (o["metadata"].get("namespace", ""), o["metadata"]["name"]))
         return Response(201, {"node": name, "nodeToken": ntok, "projectId": pid, "podCIDR": cidr,
                               "apiPrefix": f"/r/projects/{pid}/kubernetes",
-                              "heartbeatSeconds": max(0.2, self.node_grace / 5)})
+                              "heartbeatSeconds": max(0.2, self.node_grace / 5),
+                              "pods": {"resourceVersion": str(self.store.rv), "items": pods}})
 
     async def h_dashboard(self, req: Request, pid: str):
         p = self.project(pid)
