@@ -238,3 +238,26 @@ def test_control_plane_killed_mid_rollout_recovers(tmp_path):
             _stop(p)
         if p2 is not None:
             _stop(p2)
+
+
+def test_a_torn_journal_tail_does_not_hide_later_writes(tmp_path):
+    """A kill in the middle of a journal write leaves a torn last line. The restart replays up to
+    it and must cut it off before appending: otherwise the next restart stops at the torn line and
+    loses every write acknowledged after the first restart."""
+    from tritonk8ssupervisor_amd.controlplane.store import Store
+
+    j = tmp_path / "controlplane.journal"
+    s = Store()
+    s.open_journal(j)
+    for i in range(3):
+        s.put("configmaps", f"p/default/c{i}", {"metadata": {"name": f"c{i}"}, "data": {"i": str(i)}})
+    s._journal.flush()
+    with open(j, "ab") as f:  # the write a SIGKILL cut short
+        f.write(b'{"rv": 4, "op": "put", "kind": "configmaps", "key": "p/def')
+    s2 = Store()
+    assert s2.open_journal(j) == 3
+    s2.put("configmaps", "p/default/after", {"metadata": {"name": "after"}, "data": {}})
+    s2._journal.flush()
+    s3 = Store()
+    assert s3.open_journal(j) == 4
+    assert s3.get("configmaps", "p/default/after") is not None and s3.get("configmaps", "p/default/c2") is not None

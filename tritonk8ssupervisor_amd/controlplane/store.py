@@ -163,13 +163,20 @@ class Store:
         import os
 
         n = 0
+        good = 0  # the end of the last whole entry: appends go on from there, past a torn tail
         try:
             with open(path, "rb") as f:
-                for raw in f:
+                while True:
+                    raw = f.readline()
+                    if not raw:
+                        break
                     try:
                         e = _json.loads(raw)
                     except ValueError:
                         break  # the tail a kill cut short
+                    if not raw.endswith(b"\n"):
+                        break  # (a whole object without its newline: cut short all the same)
+                    good = f.tell()
                     if e["rv"] <= self.rv:
                         continue
                     table = self.objs.setdefault(e["kind"], {})
@@ -183,6 +190,8 @@ class Store:
                     n += 1
         except FileNotFoundError:
             pass
+        if os.path.exists(path) and os.path.getsize(path) > good:
+            os.truncate(path, good)  # or the next replay would stop at the torn line, before these
         self._journal = open(path, "a", buffering=1 << 16)
         os.chmod(path, 0o600)
         return n
