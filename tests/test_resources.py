@@ -243,3 +243,41 @@ def test_the_sweep_spares_a_machine_cgroup_being_set_up(tmp_path, monkeypatch):
     monkeypatch.setattr(resources, "SWEEP_MIN_AGE_S", -1.0)
     resources._sweep(tmp_path)  # old enough and empty: an agent that died without cleaning up
     assert list(tmp_path.iterdir()) == []
+
+
+def test_usage_follows_children_that_leave_the_process_group(monkeypatch):
+    """A container's processes are its session, its process group and their descendants: a child
+    that moved to a new process group (job control) or a new session (setsid) still counts -- for
+    kubectl top / the HPA, and for the memory watchdog's sum and kill."""
+    from tritonk8ssupervisor_amd.agent.usage import _proc_table, members
+
+    script = ("import os, time, sys\n"
+              "if os.fork() == 0:\n    os.setsid()\n    time.sleep(30)\n    sys.exit(0)\n"
+              "if os.fork() == 0:\n    os.setpgid(0, 0)\n    time.sleep(30)\n    sys.exit(0)\n"
+              "print('forked', flush=True)\ntime.sleep(30)\n")
+    p = subprocess.Popen([sys.executable, "-c", script], start_new_session=True, stdout=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().strip() == "forked"
+        deadline = time.monotonic() + 10
+        while True:
+            table = _proc_table()
+            kids = [q for q, v in table.items() if v[3] == p.pid]
+            if len(kids) == 2 or time.monotonic() > deadline:
+                break
+            time.sleep(0.05)
+        assert len(kids) == 2 and {table[k][0] for k in kids} != {p.pid}  # they left the group
+        assert members(table, p.pid) == {p.pid, *kids}
+        from tritonk8ssupervisor_amd.agent.resources import Enforcer
+
+        monkeypatch.setenv("TK8S_POD_RESOURCES", "none")  # (no cgroup of the test's own)
+        e = Enforcer("n", scope="t")
+        e.kill_oom("default/p", [p.pid], sorted(members(table, p.pid)))
+        assert p.wait(10) == -9
+        for k in kids:
+            deadline = time.monotonic() + 10
+            while os.path.exists(f"/proc/{k}") and open(f"/proc/{k}/stat").read().split(") ")[1][0] != "Z":
+                assert time.monotonic() < deadline, f"child {k} survived the kill"
+                time.sleep(0.05)
+    finally:
+        if p.poll() is None:
+            p.kill()

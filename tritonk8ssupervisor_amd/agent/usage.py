@@ -1,8 +1,9 @@
 """CPU and memory usage of the node and of its pods, for the metrics API (``kubectl top``) and the
 HorizontalPodAutoscaler: what the kubelet's resource metrics endpoint answers.
 
-A pod's usage is the sum over the processes in its containers' process groups (every container
-runs in a session of its own, agent/runtime.py): CPU from ``utime + stime`` deltas between two
+A pod's usage is the sum over the processes of its containers (``members``: every container runs
+in a session of its own, agent/runtime.py; a child that moved to another process group or session
+is still followed through its parent chain): CPU from ``utime + stime`` deltas between two
 samples, memory from the resident set. The node's comes from ``/proc/stat`` and ``/proc/meminfo``.
 """
 from __future__ import annotations
@@ -14,8 +15,9 @@ _TICK = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
 _PAGE = os.sysconf("SC_PAGE_SIZE") if hasattr(os, "sysconf") else 4096
 
 
-def _proc_table() -> dict[int, tuple[int, int, int]]:
-    """pid -> (process group, cpu ticks, resident bytes) for every readable process."""
+def _proc_table() -> dict[int, tuple[int, int, int, int, int]]:
+    """pid -> (process group, cpu ticks, resident bytes, parent pid, session) for every readable
+    process."""
     out = {}
     for d in os.listdir("/proc"):
         if not d.isdigit():
@@ -25,9 +27,35 @@ def _proc_table() -> dict[int, tuple[int, int, int]]:
                 raw = f.read().decode(errors="replace")
             rest = raw[raw.rindex(")") + 2:].split()
             # fields after "(comm)": state ppid pgrp session ... utime(14) stime(15) ... rss(24)
-            out[int(d)] = (int(rest[2]), int(rest[11]) + int(rest[12]), int(rest[21]) * _PAGE)
+            out[int(d)] = (int(rest[2]), int(rest[11]) + int(rest[12]), int(rest[21]) * _PAGE, int(rest[1]),
+                           int(rest[3]))
         except (OSError, ValueError, IndexError):
             continue
+    return out
+
+
+def members(table: dict, root: int, children: dict | None = None) -> set[int]:
+    """The processes of the container whose first process is ``root`` (the leader of a session and
+    process group of its own): its session and process group, and everything descending from
+    them -- a job-control shell's pipelines (new process groups) and ``setsid`` children stay
+    counted while their parent chain leads back. (A double fork that orphans itself to init
+    leaves the chain: the limits of a watchdog without cgroups.)"""
+    if children is None:
+        children = child_map(table)
+    mine = {p for p, v in table.items() if p == root or v[0] == root or v[4] == root}
+    stack = list(mine)
+    while stack:
+        for c in children.get(stack.pop(), ()):
+            if c not in mine:
+                mine.add(c)
+                stack.append(c)
+    return mine
+
+
+def child_map(table: dict) -> dict[int, list[int]]:
+    out: dict[int, list[int]] = {}
+    for p, v in table.items():
+        out.setdefault(v[3], []).append(p)
     return out
 
 
@@ -57,16 +85,14 @@ class UsageSampler:
     def sample(self, groups: dict[str, dict[str, int]]) -> dict:
         now = time.time()
         table = _proc_table()
-        by_group: dict[int, list[tuple[int, int]]] = {}
-        for _pid, (pg, ticks, rss) in table.items():
-            by_group.setdefault(pg, []).append((ticks, rss))
+        kids = child_map(table)
         pods = {}
         for key, containers in groups.items():
             cs = []
             for name, pgid in containers.items():
-                procs = by_group.get(pgid, [])
-                ticks = sum(t for t, _ in procs)
-                rss = sum(r for _, r in procs)
+                procs = [table[p] for p in members(table, pgid, kids)]
+                ticks = sum(v[1] for v in procs)
+                rss = sum(v[2] for v in procs)
                 last = self.prev.get((key, name))
                 self.prev[(key, name)] = (now, ticks)
                 cores = 0.0
