@@ -211,3 +211,40 @@ def test_node_tokens_reach_their_own_node_only(tmp_path):
         assert ei.value.status == 403
     finally:
         _stop(p)
+
+
+@needs_jail
+def test_a_pod_without_a_pid_namespace_cannot_signal_the_agent(tmp_path):
+    """On a node without user namespaces (the GPU tier) a CPU pod shares the host's PID namespace,
+    as GPU pods always do: the jail scopes its signals to the pod (Landlock ABI >= 6), so it
+    cannot kill the node agent or another pod, while signalling its own processes still works."""
+    from tritonk8ssupervisor_amd.agent.runtime import jail_signal_scoping
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not jail_signal_scoping():
+        pytest.skip("Landlock ABI < 6: no signal scoping on this kernel")
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, tmp_path / f)
+    env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_FAKE_GPUS="1",
+               TK8S_POD_ISOLATION="none")
+    env.pop("TK8S_FAULTS", None)
+    try:
+        r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+        agent = json.loads((tmp_path / ".tk8s" / "machines" / "kubenode1" / "run" / "agent.pid").read_text())["pid"]
+        kc = lambda *a, stdin=None: subprocess.run(["./kubectl", *a], cwd=tmp_path, env=env, capture_output=True,
+                                                   text=True, timeout=60, input=stdin)
+        script = (f"if kill -0 {agent} 2>/dev/null; then echo agent-signalled; else echo agent-refused; fi; "
+                  "sleep 30 & if kill $! 2>/dev/null; then echo own-ok; fi")
+        kc("apply", "-f", "-", stdin=json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "sig"},
+                                                  "spec": {"restartPolicy": "Never", "containers": [
+                                                      {"name": "c", "command": ["sh", "-c", script]}]}}))
+        _wait(lambda *a, **k: kc(*a), "sig")
+        out = kc("logs", "sig").stdout
+        assert "agent-refused" in out and "own-ok" in out, out
+        d = kc("describe", "pod", "sig").stdout
+        assert "signals scoped to the pod" in d, d
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
