@@ -125,6 +125,26 @@ def test_writes_need_the_project_token(cp):
     assert ei.value.status == 409
 
 
+def test_only_the_bound_node_writes_agent_annotations(cp):
+    """A pod's agent-owned annotations (tk8s.amd.com/gpu-devices: which GPUs a gpu-peers rank may
+    open) arrive with its status, from the node it is bound to: not through the pod API, and not
+    on an unbound pod's status from anyone else."""
+    proj = _env(cp)
+    k = client_from_kubeconfig(cp.get(f"/env/{proj['id']}/kubernetes/kubectl", query={"format": "json"}))
+    k.post(k.k8s("/api/v1/namespaces/default/pods"),
+           {"metadata": {"name": "u"}, "spec": {"nodeSelector": {"none": "x"}, "containers": [{"name": "c", "command": ["true"]}]}})
+    forged = {"status": {"phase": "Pending"}, "annotations": {"tk8s.amd.com/gpu-devices": '[{"renderMinor": 129}]'}}
+    with pytest.raises(ApiError) as ei:
+        k.put(k.k8s("/api/v1/namespaces/default/pods/u/status"), forged)
+    assert ei.value.status == 403
+    with pytest.raises(ApiError) as ei:
+        k.request("PATCH", k.k8s("/api/v1/namespaces/default/pods/u"), {"metadata": {"annotations": forged["annotations"]}},
+                  content_type="application/merge-patch+json")
+    assert ei.value.status == 403
+    assert "tk8s.amd.com/gpu-devices" not in (k.get(k.k8s("/api/v1/namespaces/default/pods/u"))["metadata"].get(
+        "annotations") or {})
+
+
 def test_node_lease_expiry_and_recovery(cp):
     proj = _env(cp)
     nc, _ = _join(cp, proj["id"], "kubenode1", ngpu=1)

@@ -644,10 +644,16 @@ class Agent:
                         or (o.get("status") or {}).get("phase") in TERMINAL
                         or not any(r.get("uid") == job.get("uid") for r in om.get("ownerReferences") or [])):
                     continue
+                nn = o["spec"].get("nodeName")
+                if not nn:
+                    waiting.append(om["name"])
+                    continue
+                if self._node_host(nn) != host:
+                    continue  # on another host: RCCL reaches it over the network, nothing to open
                 published = (om.get("annotations") or {}).get(GPU_DEVICES)
-                if published:
-                    devices += [d for d in json.loads(published) if d.get("host") == host]
-                elif not o["spec"].get("nodeName") or self._node_host(o["spec"]["nodeName"]) == host:
+                if published:  # (written by that node's agent: only its own GPUs are taken)
+                    devices += [d for d in json.loads(published) if d.get("node") == nn]
+                else:
                     waiting.append(om["name"])
         except (ApiError, OSError, ValueError, KeyError) as e:
             waiting.append(f"(pod list: {e})")

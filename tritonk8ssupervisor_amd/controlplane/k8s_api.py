@@ -1196,6 +1196,8 @@ class KubernetesAPI:
         body = req.json()
         st = body.get("status", body)
         ann = body.get("annotations")
+        if ann and not node:  # the agent-owned annotations (gpu-devices, ...) come from the pod's node only
+            raise HttpError(403, f'pod "{name}" is not bound to a node: its status carries no annotations')
 
         def fn(o):
             o.setdefault("status", {}).update(st)
