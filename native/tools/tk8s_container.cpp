@@ -84,11 +84,6 @@ int open_in_root(int rootfd, const std::string& rel, int flags) {
   return static_cast<int>(syscall(SYS_openat2, rootfd, rel.empty() ? "." : rel.c_str(), &how, sizeof(how)));
 }
 
-std::string parent_of(const std::string& rel) {
-  const auto k = rel.rfind('/');
-  return k == std::string::npos ? std::string() : rel.substr(0, k);
-}
-
 // An O_PATH fd of `rel` (a path inside the image) resolved inside it, creating what is missing
 // on the way: directories, and the last component as an empty file when `as_file`. A dangling
 // symlink on the way is followed (inside the image) and its target created.
