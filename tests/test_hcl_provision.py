@@ -338,3 +338,25 @@ def test_machine_cli_is_what_the_compat_provisioners_run(ws):
     assert run("delete", "--name", "kubenode1").returncode == 0
     assert prov.list_machines() == []
     assert "already deleted" in run("delete", "--name", "kubenode1").stdout  # destroy is idempotent
+
+
+def test_bootstrap_refuses_a_node_runtime_older_than_python_3_8(ws, tmp_path, monkeypatch):
+    """The modules' bootstrap checks the machine's python3 by its --version (no interpreter start
+    on the critical path): 3.8 and later pass, an older one fails the machine, tainted."""
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 1)
+    old = tmp_path / "oldpy"
+    old.mkdir()
+    (old / "python3").write_text("#!/bin/sh\necho 'Python 3.6.9'\n")
+    (old / "python3").chmod(0o755)
+    monkeypatch.setenv("PATH", f"{old}:{os.environ['PATH']}")
+    eng = Engine(ws.tf, prov, retries=0)
+    eng.get()
+    res = eng.apply()
+    assert not res.ok and "python3 >= 3.8 required" in json.dumps(res.failed), res.failed
+    assert any(r.get("tainted") for r in eng.state()["resources"].values())
+    monkeypatch.setenv("PATH", os.environ["PATH"].split(":", 1)[1])
+    (old / "python3").write_text("#!/bin/sh\necho 'Python 3.12.3'\n")
+    monkeypatch.setenv("PATH", f"{old}:{os.environ['PATH']}")
+    assert eng.apply().ok  # the tainted machines are replaced, and 3.12 passes
+    eng.destroy()

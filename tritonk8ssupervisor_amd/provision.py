@@ -38,7 +38,7 @@ RESOURCE_TYPE = "tk8s_machine"
 # The engine plans it identically and creates it through the same provider fast path.
 COMPAT_TYPE = "terraform_data"
 BOOTSTRAP = ["test -d run && test -d logs && test -d pods",
-             "python3 -S -E -c 'import sys; sys.exit(0 if sys.version_info >= (3, 8) else 1)'"]
+             "case $(python3 --version 2>&1) in 'Python 3.'[89]*|'Python 3.'[1-9][0-9]*) ;; *) echo 'python3 >= 3.8 required' >&2; exit 1 ;; esac"]
 
 
 _APPEND = None
