@@ -510,6 +510,8 @@ class Setup(KubeadmPlatform, FabricCheck):
         self.events.emit("setup_start", backend=self.backend, resume=self.resume)
         if not self.resume:
             ws.save_state(completed=[], timings={}, started=time.time())
+        if not self.done("provision") and hasattr(self.provider, "prefetch"):
+            self.provider.prefetch()  # (local machines: the host's state, read while configuring)
         steps = [("configure", self.configure, None), ("provision", self.provision, "Starting terraform tasks..."),
                  ("ansible-config", self.ansible_config, "Creating ansible configs..."),
                  ("ansible", self.ansible, "Running ansible tasks...")]

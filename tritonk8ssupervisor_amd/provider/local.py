@@ -136,6 +136,26 @@ class LocalProvider(Provider):
         return sorted(out, key=lambda p: p.name)
 
     # ---- allocation ---------------------------------------------------------------
+    def prefetch(self) -> None:
+        """Warm what the first create_machine reads under the workspace and host locks -- the
+        host's bound loopback addresses (/proc/net/{tcp,udp}: 1-4 ms on a host with many sockets),
+        the GPU inventory, the topology allocator -- in a thread while the configure phase runs."""
+        import threading
+
+        def warm() -> None:
+            try:
+                if self._multi():
+                    self._bound_ips_cached()
+                inv = discover()
+                if inv.count:
+                    from ..ops import topo
+
+                    topo()
+            except Exception:  # noqa: BLE001 - a cache warm-up: create_machine does it all itself
+                pass
+
+        threading.Thread(target=warm, name="provider-prefetch", daemon=True).start()
+
     def _multi(self) -> bool:
         if self._multi_ip is None:
             self._multi_ip = _loopback_multi_ok()
