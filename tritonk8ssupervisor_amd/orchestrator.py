@@ -691,11 +691,14 @@ class Setup(KubeadmPlatform, FabricCheck):
 
 
 def _free_port() -> int:
-    import socket
+    import _socket  # (not ``socket``: its enum set-up is ~1.5 ms of the bring-up, utils/http1.py)
 
-    with socket.socket() as s:
+    s = _socket.socket(_socket.AF_INET, _socket.SOCK_STREAM)
+    try:
         s.bind(("0.0.0.0", 0))
         return s.getsockname()[1]
+    finally:
+        s.close()
 
 
 def _flush_print(s: str) -> None:

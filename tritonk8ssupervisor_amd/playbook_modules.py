@@ -16,7 +16,6 @@ import json
 import os
 import re
 import shlex
-import socket
 import subprocess
 import time
 from pathlib import Path
@@ -528,6 +527,8 @@ def m_wait_for(args, *, ctx, target, local, check, **_):
     while time.monotonic() < deadline:
         if "port" in args:
             host = args.get("host", "127.0.0.1")
+            import socket
+
             s = socket.socket()
             s.settimeout(1.0)
             try:

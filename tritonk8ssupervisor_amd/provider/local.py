@@ -17,9 +17,9 @@ share the host never share an address or a GPU.
 """
 from __future__ import annotations
 
+import _socket as socket  # (the C module: inet_ntoa, gethostname, a bind probe -- utils/http1.py)
 import getpass
 import os
-import socket
 import subprocess
 from pathlib import Path
 

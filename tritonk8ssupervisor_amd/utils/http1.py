@@ -10,7 +10,40 @@ Content-Length, chunked transfer encoding or connection close. HTTPS is not hand
 """
 from __future__ import annotations
 
-import socket
+import _socket
+import io
+
+# ``_socket``, not ``socket``: the latter turns hundreds of constants into enums on import (~3 ms,
+# ~1.5 ms on the MI355X host) in every process on the bring-up's path that only needs a TCP
+# connection to the control plane.
+
+
+class _SockReader(io.RawIOBase):
+    """What ``socket.makefile("rb")`` wraps, for a bare ``_socket.socket``."""
+
+    def __init__(self, sock):
+        self._sock = sock
+
+    def readable(self) -> bool:
+        return True
+
+    def readinto(self, b) -> int:
+        return self._sock.recv_into(b)
+
+
+def create_connection(host, port: int, timeout: float | None):
+    """``socket.create_connection`` on ``_socket``: the first address of ``host`` that connects."""
+    err: OSError | None = None
+    for af, st, proto, _canon, addr in _socket.getaddrinfo(host, port, 0, _socket.SOCK_STREAM):
+        s = _socket.socket(af, st, proto)
+        try:
+            s.settimeout(timeout)
+            s.connect(addr)
+            return s
+        except OSError as e:
+            err = e
+            s.close()
+    raise err or OSError(f"no address for {host!r}")
 
 
 class ProtocolError(OSError):
@@ -32,16 +65,16 @@ class Connection:
 
     def __init__(self, host: str, port: int, timeout: float | None = 30.0):
         self.host, self.port, self.timeout = host, port, timeout
-        self.sock: socket.socket | None = None
+        self.sock = None  # a _socket.socket once connected
         self._rf = None
 
     def _connect(self) -> None:
         # an ASCII host goes to getaddrinfo as bytes: a str host is IDNA-encoded first, which
         # imports encodings.idna + stringprep + unicodedata (~1 ms) for a dotted-quad address
         host = self.host.encode("ascii") if self.host.isascii() else self.host
-        self.sock = socket.create_connection((host, self.port), timeout=self.timeout)
-        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-        self._rf = self.sock.makefile("rb")
+        self.sock = create_connection(host, self.port, self.timeout)
+        self.sock.setsockopt(_socket.IPPROTO_TCP, _socket.TCP_NODELAY, 1)
+        self._rf = io.BufferedReader(_SockReader(self.sock))
 
     def set_timeout(self, timeout: float | None) -> None:
         self.timeout = timeout
