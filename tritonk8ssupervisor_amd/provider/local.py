@@ -138,19 +138,14 @@ class LocalProvider(Provider):
     # ---- allocation ---------------------------------------------------------------
     def prefetch(self) -> None:
         """Warm what the first create_machine reads under the workspace and host locks -- the
-        host's bound loopback addresses (/proc/net/{tcp,udp}: 1-4 ms on a host with many sockets),
-        the GPU inventory, the topology allocator -- in a thread while the configure phase runs."""
+        host's bound loopback addresses (/proc/net/{tcp,udp}) -- in a thread while the configure
+        phase runs."""
         import threading
 
-        def warm() -> None:
+        def warm() -> None:  # (the GPU inventory and the allocator: predict_gpus warms those)
             try:
                 if self._multi():
                     self._bound_ips_cached()
-                inv = discover()
-                if inv.count:
-                    from ..ops import topo
-
-                    topo()
             except Exception:  # noqa: BLE001 - a cache warm-up: create_machine does it all itself
                 pass
 
@@ -185,21 +180,24 @@ class LocalProvider(Provider):
         """Loopback addresses something on this host already serves on (a TCP listener or a
         UDP socket bound to that address): a cluster the registry does not know about -- another
         user's, or one whose registry is gone -- still owns its master's DNS / ingress / API
-        sockets there, and a new machine on the same address would answer for neither."""
+        sockets there, and a new machine on the same address would answer for neither. (One
+        regex pass over each table: a shared host lists thousands of sockets.)"""
+        import re
+
         out: set[str] = set()
-        for table, listen_only in (("/proc/net/tcp", True), ("/proc/net/udp", False)):
+        # local address column "XXXXXX7F:PORT" (127.x.y.z, little-endian hex), then the remote
+        # address, then the state (0A = LISTEN; any state for UDP)
+        for table, state in (("/proc/net/tcp", rb"0A"), ("/proc/net/udp", rb"[0-9A-F]{2}")):
             try:
-                with open(table) as f:
-                    next(f, None)
-                    for line in f:
-                        cols = line.split()
-                        if len(cols) < 4 or (listen_only and cols[3] != "0A"):
-                            continue
-                        ip = socket.inet_ntoa(bytes.fromhex(cols[1].split(":")[0])[::-1])
-                        if ip.startswith("127.") and ip != "127.0.0.1":
-                            out.add(ip)
-            except (OSError, ValueError):
+                with open(table, "rb") as f:
+                    data = f.read()
+            except OSError:
                 continue
+            for hexip in re.findall(rb"^ *\d+: ([0-9A-F]{6}7F):[0-9A-F]{4} [0-9A-F]{8}:[0-9A-F]{4} " + state,
+                                    data, re.M):
+                ip = socket.inet_ntoa(bytes.fromhex(hexip.decode())[::-1])
+                if ip != "127.0.0.1":
+                    out.add(ip)
         return out
 
     def _alloc_ips(self, alloc: dict, name: str, nets: list[Network], host: dict) -> list[str]:
