@@ -281,3 +281,18 @@ def test_usage_follows_children_that_leave_the_process_group(monkeypatch):
     finally:
         if p.poll() is None:
             p.kill()
+
+
+def test_numa_cpus_outside_the_agents_own_are_not_pinned(tmp_path, monkeypatch):
+    """A GPU's NUMA-local CPUs that the agent may not use (a cpuset keeping it off that socket)
+    are dropped: the pod runs unpinned instead of failing sched_setaffinity."""
+    from tritonk8ssupervisor_amd.agent import resources
+
+    d = tmp_path / "class" / "drm" / "renderD128" / "device"
+    d.mkdir(parents=True)
+    (d / "local_cpulist").write_text("0-3,8-11\n")
+    monkeypatch.setenv("TK8S_SYSFS_ROOT", str(tmp_path))
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: {2, 3, 4, 5})
+    assert resources.gpu_local_cpus([128]) == "2-3"
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: {4, 5})
+    assert resources.gpu_local_cpus([128]) == ""

@@ -92,8 +92,10 @@ def sysfs_root() -> Path:
 
 
 def gpu_local_cpus(render_minors) -> str:
-    """The CPUs NUMA-local to these GPUs (``/sys/class/drm/renderD<m>/device/local_cpulist``),
-    as one list; "" when unknown. On an MI355X node, GPUs 0-3 sit on socket 0 and 4-7 on 1."""
+    """The CPUs NUMA-local to these GPUs (``/sys/class/drm/renderD<m>/device/local_cpulist``)
+    that this process may run on, as one list; "" when unknown or none of them is ours (a
+    cpuset that keeps the agent off that socket: the pod is then not pinned rather than
+    unstartable). On an MI355X node, GPUs 0-3 sit on socket 0 and 4-7 on 1."""
     cpus: set[int] = set()
     for m in render_minors:
         if m is None or int(m) < 0:
@@ -103,6 +105,8 @@ def gpu_local_cpus(render_minors) -> str:
                                        "local_cpulist").read_text()))
         except (OSError, ValueError):
             continue
+    if cpus and hasattr(os, "sched_getaffinity"):
+        cpus &= os.sched_getaffinity(0)
     return format_cpulist(cpus) if cpus else ""
 
 
