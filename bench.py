@@ -579,7 +579,7 @@ def main(argv=None) -> int:
         # what persists between steps (all of it per-user and content-checked; every step still
         # creates its machines, starts every process and runs every GPU validation kernel)
         "host_caches": "Python byte code (build/pycache), parsed YAML of the unchanged playbook/role/"
-                       "manifest files and rewritten Jinja expressions (~/.cache/tk8s; entries carry "
+                       "manifest files and rewritten Jinja expressions (~/.local/state/tk8s; entries carry "
                        "their source text); filled by the warmup steps",
         "min_s": round(min(ready_times), 4),
         "max_s": round(max(ready_times), 4),

@@ -62,6 +62,28 @@ POD_ENV_KEEP = {"PATH", "HOME", "USER", "LOGNAME", "SHELL", "LANG", "LANGUAGE", 
 POD_ENV_KEEP_PREFIXES = ("LC_", "HSA_", "HIP_", "ROCR_", "AMD_", "NCCL_", "RCCL_", "TK8S_FAKE_", "TK8S_PROBE_")
 
 
+def operator_state_dirs() -> list[Path]:
+    """What tk8s itself keeps for the operator outside the workspace and reads back later -- its
+    state home (utils/pcache.state_home: parse/rewrite caches a poisoned entry of which the next
+    ./setup.sh would run, the image store other pods' containers are made from), an explicit
+    TK8S_YAML_CACHE / TK8S_IMAGE_STORE, the host registry of IP/GPU claims -- created if missing,
+    so that a pod's jail can deny them (a Landlock rule needs the directory to exist)."""
+    from ..provider.hostreg import registry_dir
+    from ..utils.pcache import state_home
+
+    dirs = [Path(state_home()), registry_dir()]
+    for env in ("TK8S_YAML_CACHE", "TK8S_IMAGE_STORE"):
+        v = os.environ.get(env, "")
+        if v and v != "off":
+            dirs.append(Path(v))
+    for d in dirs:
+        try:
+            d.mkdir(parents=True, exist_ok=True, mode=0o700)
+        except OSError:
+            pass
+    return dirs
+
+
 def pod_base_env(environ=None) -> dict:
     env = os.environ if environ is None else environ
     out = {k: v for k, v in env.items() if k in POD_ENV_KEEP or k.startswith(POD_ENV_KEEP_PREFIXES)}
@@ -687,9 +709,11 @@ class Agent:
         * denied: the node's state root (the workspace's ``.tk8s/``: admin kubeconfig and token,
           the cluster key, every machine's registration URL, other pods' directories with their
           ServiceAccount tokens and secret volumes), the workspace's Terraform state and
-          ``ansible/tmp``, the operator's ``~/.ssh``;
-        * read-only: the tk8s install and the workspace (the operator runs them: a pod that could
-          rewrite them would run as the operator), the operator's shell start-up files;
+          ``ansible/tmp``, the operator's ``~/.ssh``, tk8s's parse caches and the host registry
+          (``operator_state_dirs``: what the operator's next bring-up reads back);
+        * read-only: the tk8s install, the workspace and the operator's home (the operator runs
+          them: a pod that could rewrite them would run as the operator), except its ``~/.cache``
+          and MIOpen's ``~/.config/miopen``;
         * read-write: the pod's own directory, its hostPath volumes (read-only ones read-only);
           validation pods (kube-system, the DaemonSet's label) consume their machine's ``run/``
           burn-in result."""
@@ -702,9 +726,18 @@ class Agent:
             ro.append(str(ws))
             deny += [str(x) for x in sorted((ws / "terraform").glob("terraform.tfstate*"))] + [str(ws / "ansible" / "tmp")]
         home = Path.home()
-        deny.append(str(home / ".ssh"))
-        ro += [str(home / f) for f in (".bashrc", ".profile", ".bash_profile", ".bash_login", ".zshrc", ".zprofile",
-                                       ".config/systemd", ".config/autostart")]
+        deny += [str(home / ".ssh"), *(str(d) for d in operator_state_dirs())]
+        if str(home) != "/":
+            # the operator's home, read-only: its shell start-up files, ~/.local/bin on its PATH
+            # and the user site-packages its interpreters load are ways into the operator's next
+            # login or bring-up; the workloads' caches (~/.cache: MIOpen, torch, HF) stay writable
+            ro.append(str(home))
+            for d in (home / ".cache", home / ".config" / "miopen"):
+                try:
+                    d.mkdir(parents=True, exist_ok=True)  # (a rule needs it; under a read-only home
+                except OSError:                          # the pod could not make it itself)
+                    pass
+                rw.append(str(d))
         for d, read_only in vol_dirs.values():
             (ro if read_only else rw).append(str(d))
         if md.get("namespace") == "kube-system" and (md.get("labels") or {}).get(VALIDATION_LABEL) == "true":

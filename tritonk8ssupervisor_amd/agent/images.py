@@ -6,7 +6,7 @@ stack, the demo apps; ansible/roles/*/tasks/main.yml, docs/detailed.md:261-370).
 no registry to pull from (the GPU hosts are offline), so images come from files, the way an
 air-gapped node is fed: ``./tk8s image load FILE`` takes a ``docker save`` tarball or an OCI image
 layout (directory or tar), checks every blob against its sha256, and keeps them in a
-content-addressed store (``$TK8S_IMAGE_STORE``, default ``$XDG_CACHE_HOME/tk8s/images``):
+content-addressed store (``$TK8S_IMAGE_STORE``, default ``$XDG_STATE_HOME/tk8s/images``):
 
     blobs/sha256/<hex>         layers (tar, tar+gzip), configs, manifests
     refs.json                  {"docker.io/library/nginx:1.27": {"manifest": <digest>, ...}}
@@ -46,8 +46,9 @@ def store_dir() -> Path:
     d = os.environ.get("TK8S_IMAGE_STORE")
     if d:
         return Path(d)
-    base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
-    return Path(base) / "tk8s" / "images"
+    from ..utils.pcache import state_home  # (not ~/.cache: pods write there, agent._jail_layers)
+
+    return Path(state_home()) / "images"
 
 
 def normalize(ref: str) -> str:

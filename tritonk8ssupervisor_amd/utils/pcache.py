@@ -1,6 +1,6 @@
 """A small persistent string -> marshal-able cache shared by the processes of this user
-(``$XDG_CACHE_HOME/tk8s``, the same root as utils/yamlio.py's parse cache; ``TK8S_YAML_CACHE=off``
-disables both).
+(``state_home()``, ``$XDG_STATE_HOME/tk8s``: the same root as utils/yamlio.py's parse cache;
+``TK8S_YAML_CACHE=off`` disables both).
 
 For derived data that is expensive to compute the first time in every process but identical
 across bring-ups -- e.g. the templating engine's rewrite of a Jinja expression needs the stdlib
@@ -16,6 +16,15 @@ import os
 import threading
 
 
+def state_home() -> str:
+    """Where tk8s keeps what it reads back on the operator's next run -- parse and rewrite caches,
+    the image store: ``$XDG_STATE_HOME/tk8s`` (default ``~/.local/state/tk8s``). Not under
+    ``~/.cache``: pods may write there (their own caches), and a poisoned entry here would run as
+    the operator; the home around it is read-only to pods (agent._jail_layers)."""
+    base = os.environ.get("XDG_STATE_HOME") or os.path.join(os.path.expanduser("~"), ".local", "state")
+    return os.path.join(base, "tk8s")
+
+
 class PersistentCache:
     def __init__(self, name: str, limit: int = 20000):
         self.name, self.limit = name, limit
@@ -28,8 +37,7 @@ class PersistentCache:
             return None
         if d:
             return os.path.join(d, f"{self.name}.marshal")
-        base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
-        return os.path.join(base, "tk8s", f"{self.name}.marshal")
+        return os.path.join(state_home(), f"{self.name}.marshal")
 
     def _load(self) -> dict:
         if self._table is None:

@@ -6,7 +6,7 @@ Importing PyYAML costs more than parsing every file of a bring-up (its resolver 
 compile dozens of regexes at import: ~10 ms on the MI355X host, on the critical path of
 ``./setup.sh``). The playbooks, roles, group_vars and manifests are the same text on every
 bring-up, so -- like Python's own .pyc cache -- a parse result is kept in
-``$XDG_CACHE_HOME/tk8s/yaml`` (``TK8S_YAML_CACHE=<dir>`` or ``off``), keyed by the text's
+``$XDG_STATE_HOME/tk8s/yaml`` (``TK8S_YAML_CACHE=<dir>`` or ``off``), keyed by the text's
 length and checksums and stored WITH the text, which must match exactly before the cached
 data is used: a hit returns exactly what the parser would. The entries are ``marshal`` data this
 module wrote itself (plain dicts, lists and scalars; a document with types marshal cannot hold,
@@ -36,8 +36,9 @@ def _cache_path(raw: bytes, kind: str) -> str | None:
     if d == "off":
         return None
     if not d:
-        base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
-        d = os.path.join(base, "tk8s", "yaml")
+        from .pcache import state_home
+
+        d = os.path.join(state_home(), "yaml")
     return os.path.join(d, f"{len(raw)}-{zlib.crc32(raw):08x}-{zlib.adler32(raw):08x}-{kind}{_VERSION}.marshal")
 
 
