@@ -36,9 +36,20 @@ def test_local_backend_without_a_gpu_fails():
     assert r.returncode == 1 and "FAIL" in r.stdout and "/dev/kfd" in r.stdout
 
 
-def test_kubeadm_platform_needs_machines_it_owns():
+def test_kubeadm_platform_on_the_local_backend_needs_root():
     rc, checks = _doctor("--platform", "kubeadm", env={"TK8S_FAKE_GPUS": "2"})
-    assert rc == 1 and checks["kubeadm platform"]["status"] == "FAIL"
+    if os.geteuid() == 0:  # one-command single-node kubeadm on this host
+        assert checks["kubeadm platform"]["status"] == "OK" and "single-node" in checks["kubeadm platform"]["detail"]
+    else:
+        assert rc == 1 and checks["kubeadm platform"]["status"] == "FAIL" and "root" in checks["kubeadm platform"]["detail"]
+
+
+def test_doctor_reports_pod_signals_and_resource_limits():
+    _rc, checks = _doctor(env={"TK8S_FAKE_GPUS": "2"})
+    assert checks["resource limits"]["status"] in ("OK", "WARN") and checks["resource limits"]["detail"]
+    assert checks["pod signals"]["status"] in ("OK", "WARN")
+    _rc, checks = _doctor(env={"TK8S_FAKE_GPUS": "2", "TK8S_POD_RESOURCES": "watchdog"})
+    assert checks["resource limits"]["status"] == "WARN" and "watchdog" in checks["resource limits"]["detail"]
 
 
 def test_baremetal_hosts_are_checked_over_ssh(tmp_path):

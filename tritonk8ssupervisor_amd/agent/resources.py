@@ -163,6 +163,36 @@ def _sweep(parent: Path) -> None:
         pass
 
 
+def detect_mode() -> tuple[str, str]:
+    """(mode, why) the Enforcer of a node agent on this host would pick, found without creating
+    or moving anything (``./tk8s doctor``)."""
+    want = os.environ.get("TK8S_POD_RESOURCES", "auto")
+    if want == "none":
+        return "none", "disabled (TK8S_POD_RESOURCES=none)"
+    if want not in ("auto", "cgroup2", "cgroup1", "watchdog"):
+        return "none", f"unknown TK8S_POD_RESOURCES={want!r}"
+    root = Path(os.environ.get("TK8S_CGROUP_ROOT", "/sys/fs/cgroup"))
+    own = _own_cgroups()
+    why = []
+    if want in ("auto", "cgroup2"):
+        d = root / own.get("", "/").lstrip("/")
+        try:
+            have = set((d / "cgroup.controllers").read_text().split()) if (root / "cgroup.controllers").exists() else set()
+        except OSError:
+            have = set()
+        if {"memory", "cpu"} <= have and os.access(d / "cgroup.subtree_control", os.W_OK):
+            return "cgroup2", f"delegated subtree {d}"
+        why.append(f"cgroup2: {d} not delegated" if have else "cgroup2: not a unified hierarchy")
+    if want in ("auto", "cgroup1"):
+        d = root / "memory" / own.get("memory", "/").lstrip("/")
+        if "memory" in own and (root / "memory" / "cgroup.procs").exists() and os.access(d, os.W_OK):
+            return "cgroup1", f"writable memory hierarchy {d}"
+        why.append("cgroup1: no writable memory hierarchy")
+    if want in ("auto", "watchdog"):
+        return "watchdog", "; ".join(why)
+    return "none", "; ".join(why)
+
+
 def _write(path: Path, value) -> None:
     with open(path, "w") as f:
         f.write(f"{value}\n")

@@ -121,6 +121,19 @@ def local_checks(workdir: str) -> list[dict]:
     out.append(_check("gpu jail", OK if jail else WARN,
                       f"{jhow}: a pod can open only its own GPUs' render nodes" if jail else
                       f"{jhow}: a pod's GPU view is its *_VISIBLE_DEVICES only"))
+    from .agent.resources import detect_mode
+    from .agent.runtime import jail_signal_scoping
+
+    out.append(_check("pod signals", OK if jail_signal_scoping() else WARN,
+                      "Landlock scopes a pod's signals: GPU pods (host PID namespace) cannot signal the agent"
+                      if jail_signal_scoping() else "Landlock ABI < 6: pods sharing the host PID namespace may "
+                                                   "signal other processes of the operator"))
+    mode, mwhy = detect_mode()
+    out.append(_check("resource limits", OK if mode in ("cgroup2", "cgroup1") else WARN, {
+        "cgroup2": f"cgroup v2 ({mwhy}): memory, cpu and cpuset limits per pod and per machine",
+        "cgroup1": f"cgroup v1 ({mwhy}): memory, cpu and cpuset limits per pod and per machine",
+        "watchdog": f"memory watchdog (OOMKilled) and NUMA pinning only; limits.cpu not enforced ({mwhy})",
+    }.get(mode, f"none: {mwhy}")))
     cont, chow = container_runtime()
     out.append(_check("image pods", OK if cont else WARN,
                       f"{chow}: pods can run loaded images (./tk8s image load)" if cont else
@@ -202,8 +215,14 @@ def triton_checks() -> list[dict]:
 
 def kubeadm_checks(backend: str, workdir: str = ".") -> list[dict]:
     if backend == "local":
-        return [_check("kubeadm platform", FAIL, "needs machines it owns: --backend baremetal or triton "
-                                                 "(one host in the inventory: single-node mode)")]
+        from .orchestrator import local_kubeadm_allowed
+
+        if local_kubeadm_allowed():
+            return [_check("kubeadm platform", OK, "single-node on this host (as root, no ssh): installs ROCm, "
+                                                   "amdgpu-dkms, containerd and kubeadm here (needs apt and network "
+                                                   "access)")]
+        return [_check("kubeadm platform", FAIL, "installs a node runtime: as root on this host (single-node), or "
+                                                 "--backend baremetal / triton with machines it owns")]
     layout = ""
     if backend == "baremetal":
         try:
