@@ -1,0 +1,35 @@
+"""utils/lazymod.py: the control plane's stand-ins for logging / concurrent.futures load the real
+modules on first use, so nothing asyncio does behaves differently."""
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+
+SCRIPT = r"""
+import sys
+from tritonk8ssupervisor_amd.utils import lazymod
+lazymod.install()
+import asyncio
+assert type(sys.modules["logging"]).__name__ == "_LazyModule", "asyncio's import loaded logging"
+assert type(sys.modules["concurrent.futures"]).__name__ == "_LazyModule"
+
+async def main():
+    loop = asyncio.get_running_loop()
+    r = await loop.run_in_executor(None, sum, [1, 2, 3])  # a thread pool: the real module loads
+    done, _ = await asyncio.wait([asyncio.ensure_future(asyncio.sleep(0, 7))], return_when=asyncio.FIRST_COMPLETED)
+    return r, [t.result() for t in done]
+
+assert asyncio.run(main()) == (6, [7])
+import concurrent.futures, logging
+assert concurrent.futures.ThreadPoolExecutor.__module__ == "concurrent.futures.thread"
+logging.getLogger("asyncio").error("through the stand-in: %s", "ok")  # the real logger, last resort handler
+print("lazy ok")
+"""
+
+
+def test_stand_ins_load_the_real_modules_on_use():
+    r = subprocess.run([sys.executable, "-S", "-c", SCRIPT], cwd=REPO, capture_output=True, text=True, timeout=60,
+                       env={"PYTHONPATH": str(REPO), "PATH": "/usr/bin:/bin"})
+    assert r.returncode == 0 and "lazy ok" in r.stdout, r.stdout + r.stderr
+    assert "through the stand-in: ok" in r.stderr

@@ -3,11 +3,17 @@
 and the start is on the bring-up's critical path; ``sys.argv`` has the same positions either way).
 
 The control plane serves plain HTTP only, so ``ssl`` is kept out: asyncio imports it when it can
-(~4 ms, libssl included) and runs without it when the import fails.
+(~4 ms, libssl included) and runs without it when the import fails. ``logging`` and
+``concurrent.futures``, which asyncio imports and the control plane never calls, load on first
+use (utils/lazymod.py).
 """
 import sys
 
 sys.modules.setdefault("ssl", None)  # type: ignore[arg-type]  -- `import ssl` -> ImportError
+
+from ..utils import lazymod  # noqa: E402
+
+lazymod.install()  # logging / concurrent.futures: loaded when first used (utils/lazymod.py)
 
 from .server import main  # noqa: E402
 
