@@ -13,6 +13,7 @@ lazymod.install()
 import asyncio
 assert type(sys.modules["logging"]).__name__ == "_LazyModule", "asyncio's import loaded logging"
 assert type(sys.modules["concurrent.futures"]).__name__ == "_LazyModule"
+assert type(sys.modules["inspect"]).__name__ == "_LazyModule"
 
 async def main():
     loop = asyncio.get_running_loop()
@@ -21,7 +22,8 @@ async def main():
     return r, [t.result() for t in done]
 
 assert asyncio.run(main()) == (6, [7])
-import concurrent.futures, logging
+import concurrent.futures, inspect, logging
+assert inspect.isawaitable(asyncio.sleep(0).__await__()) is False and inspect.signature(sum) is not None
 assert concurrent.futures.ThreadPoolExecutor.__module__ == "concurrent.futures.thread"
 logging.getLogger("asyncio").error("through the stand-in: %s", "ok")  # the real logger, last resort handler
 print("lazy ok")

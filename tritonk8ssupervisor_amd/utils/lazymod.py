@@ -3,8 +3,9 @@ statements and may never use: the real module loads on the first attribute the s
 carry itself.
 
 The control plane imports ``asyncio``, which imports ``logging`` (a logger for its debug and
-error messages) and ``concurrent.futures`` (thread pools and cross-thread futures, which the
-control plane never uses). Together they are about a third of ``asyncio``'s import, and the
+error messages), ``concurrent.futures`` (thread pools and cross-thread futures, which the
+control plane never uses) and ``inspect`` (debug reprs, and checks on error paths and on
+awaitables that are not coroutines). Together they are about 40 % of ``asyncio``'s import, and the
 control plane's start is on the bring-up's critical path (controlplane/__main__.py). asyncio only
 needs a few constants of them at import time; those are given here, and anything else -- an
 error asyncio logs, a ``run_in_executor`` -- loads the real module then and is answered by it.
@@ -45,13 +46,15 @@ class _LazyLogger:
 
 
 def install() -> None:
-    """Stand in for ``logging`` and ``concurrent.futures`` unless they are imported already."""
+    """Stand in for ``logging``, ``inspect`` and ``concurrent.futures`` unless imported already."""
     if "logging" not in sys.modules:
         log = _LazyModule("logging", {"CRITICAL": 50, "FATAL": 50, "ERROR": 40, "WARNING": 30, "WARN": 30,
                                       "INFO": 20, "DEBUG": 10, "NOTSET": 0})
         log.getLogger = lambda name=None, _m=log: _LazyLogger(_m, name)
         log.getLogger_real = lambda name=None, _m=log: _m.__getattr__("getLogger")(name)
         sys.modules["logging"] = log
+    if "inspect" not in sys.modules:
+        sys.modules["inspect"] = _LazyModule("inspect", {})
     if "concurrent.futures" not in sys.modules:
         import concurrent  # the (empty) package itself is cheap
 
