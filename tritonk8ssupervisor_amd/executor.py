@@ -278,16 +278,23 @@ class LocalExecutor(_Base):
         _, log = self._paths(host, name)
         t = time.monotonic()
         deadline = t + timeout
+        want, seen, n = text.encode(), 0, 0
         while time.monotonic() < deadline:
-            try:
+            try:  # only what the log gained since the last look (a long log is not re-read)
                 with open(log, "rb") as f:
-                    if text.encode() in f.read():
+                    f.seek(max(0, seen - len(want)))
+                    chunk = f.read()
+                    if want in chunk:
                         return {"ok": True, "wait_seconds": round(time.monotonic() - t, 6)}
+                    seen = f.tell()
             except OSError:
                 pass
-            if not self.daemon_status(host, name).get("running"):
+            n += 1
+            # a fine poll (the control plane's "Listening on" is on the bring-up's critical path);
+            # whether the daemon died, every 10th look
+            if n % 10 == 0 and not self.daemon_status(host, name).get("running"):
                 break
-            time.sleep(0.002)
+            time.sleep(0.0005 if n < 2000 else 0.01)
         tail = log.read_text(errors="replace")[-600:] if log.exists() else ""
         return {"ok": False, "msg": f"{name} on {host} did not log {text!r} within {timeout}s: {tail}"}
 
