@@ -7,7 +7,7 @@ OUT="$ROOT/gpurun_out/${1:-ab}"
 STEPS="${2:-10}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for round in 1 2; do
+for round in ${ROUNDS:-1 2}; do
   for side in old new; do
     dir="$ROOT"; [ "$side" = old ] && dir="$ROOT/gpurun_ab/old"
     echo "[ab] round $round $side"
