@@ -13,7 +13,8 @@ sys.modules.setdefault("ssl", None)  # type: ignore[arg-type]  -- `import ssl` -
 
 from ..utils import lazymod  # noqa: E402
 
-lazymod.install()  # logging / concurrent.futures: loaded when first used (utils/lazymod.py)
+if __import__("os").environ.get("TK8S_LAZY_STDLIB", "1") != "0":
+    lazymod.install()  # logging / inspect / concurrent.futures: loaded when first used (utils/lazymod.py)
 
 from .server import main  # noqa: E402
 
