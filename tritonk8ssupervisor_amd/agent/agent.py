@@ -62,12 +62,18 @@ POD_ENV_KEEP = {"PATH", "HOME", "USER", "LOGNAME", "SHELL", "LANG", "LANGUAGE", 
 POD_ENV_KEEP_PREFIXES = ("LC_", "HSA_", "HIP_", "ROCR_", "AMD_", "NCCL_", "RCCL_", "TK8S_FAKE_", "TK8S_PROBE_")
 
 
+_STATE_DIRS: list[Path] | None = None
+
+
 def operator_state_dirs() -> list[Path]:
     """What tk8s itself keeps for the operator outside the workspace and reads back later -- its
     state home (utils/pcache.state_home: parse/rewrite caches a poisoned entry of which the next
     ./setup.sh would run, the image store other pods' containers are made from), an explicit
     TK8S_YAML_CACHE / TK8S_IMAGE_STORE, the host registry of IP/GPU claims -- created if missing,
     so that a pod's jail can deny them (a Landlock rule needs the directory to exist)."""
+    global _STATE_DIRS
+    if _STATE_DIRS is not None:  # (once per agent: the agent's standby thread warms it)
+        return _STATE_DIRS
     from ..provider.hostreg import registry_dir
     from ..utils.pcache import state_home
 
@@ -76,11 +82,18 @@ def operator_state_dirs() -> list[Path]:
         v = os.environ.get(env, "")
         if v and v != "off":
             dirs.append(Path(v))
+    home = Path.home()
     for d in dirs:
         try:
             d.mkdir(parents=True, exist_ok=True, mode=0o700)
         except OSError:
             pass
+    for d in (home / ".cache", home / ".config" / "miopen"):  # the pod-writable ones (_jail_layers)
+        try:  # (a rule needs them; under a read-only home a pod could not make them itself)
+            d.mkdir(parents=True, exist_ok=True)
+        except OSError:
+            pass
+    _STATE_DIRS = dirs
     return dirs
 
 
@@ -732,12 +745,7 @@ class Agent:
             # and the user site-packages its interpreters load are ways into the operator's next
             # login or bring-up; the workloads' caches (~/.cache: MIOpen, torch, HF) stay writable
             ro.append(str(home))
-            for d in (home / ".cache", home / ".config" / "miopen"):
-                try:
-                    d.mkdir(parents=True, exist_ok=True)  # (a rule needs it; under a read-only home
-                except OSError:                          # the pod could not make it itself)
-                    pass
-                rw.append(str(d))
+            rw += [str(home / ".cache"), str(home / ".config" / "miopen")]  # (made by operator_state_dirs)
         for d, read_only in vol_dirs.values():
             (ro if read_only else rw).append(str(d))
         if md.get("namespace") == "kube-system" and (md.get("labels") or {}).get(VALIDATION_LABEL) == "true":
@@ -1128,6 +1136,7 @@ class Agent:
         (the validation pod, on the bring-up's critical path) starts."""
         gpu_jail()
         namespace_isolation(str(Path(TK8S_HOME) / "tritonk8ssupervisor_amd" / "__init__.py"), str(self.sandbox / "pods"))
+        operator_state_dirs()
         trace(self.name, "isolation probed")
 
     def run(self, await_url: Path | None = None) -> int:

@@ -565,6 +565,7 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
         loop = asyncio.get_running_loop()
         for sig in (signal.SIGTERM, signal.SIGINT):
             loop.add_signal_handler(sig, self._stop.set)
+        loop.call_soon(_warm_up)
         await self._stop.wait()
         for t in tasks:
             t.cancel()
@@ -575,6 +576,12 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
         if self.state_dir:
             self.store.snapshot(self.state_dir / "controlplane.json")
         await self.http.close()
+
+
+def _warm_up() -> None:
+    """What the first authorised write of a bring-up imports (RBAC's request attributes, managed
+    fields), loaded in the idle moment after "Listening on" rather than inside that request."""
+    from . import rbac, ssa  # noqa: F401
 
 
 def await_args(path: str, timeout: float | None = None) -> list[str]:
