@@ -360,3 +360,28 @@ def test_bootstrap_refuses_a_node_runtime_older_than_python_3_8(ws, tmp_path, mo
     monkeypatch.setenv("PATH", f"{old}:{os.environ['PATH']}")
     assert eng.apply().ok  # the tainted machines are replaced, and 3.12 passes
     eng.destroy()
+
+
+def test_engine_reserves_all_machines_in_one_allocation(ws, monkeypatch):
+    """The local provider allocates every planned machine's address and GPU slice under one take
+    of the locks (reserve), and a machine whose create fails for good gives its reservation back."""
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 3)
+    writes = []
+    import tritonk8ssupervisor_amd.provider.local as local
+
+    real = local.atomic_write_json
+    monkeypatch.setattr(local, "atomic_write_json", lambda p, o: (writes.append(Path(p).name), real(p, o))[1])
+    eng = Engine(ws.tf, prov)
+    eng.get()
+    assert eng.apply().ok
+    assert writes.count("alloc.json") == 1, writes  # one allocation for the four machines
+    eng.destroy()
+    # a create that fails for good (injected, no retries): its reservation is released
+    monkeypatch.setenv("TK8S_FAULTS", "provision.create@kubenode2")
+    eng2 = Engine(ws.tf, LocalProvider(ws.state_dir), retries=0)
+    res = eng2.apply()
+    assert not res.ok and list(res.failed) == ["module.kubenode2.tk8s_machine.host"], res.failed
+    alloc = json.loads((ws.state_dir / "alloc.json").read_text())
+    assert sorted(alloc["machines"]) == ["kubemaster", "kubenode1", "kubenode3"], alloc["machines"]
+    eng2.destroy()

@@ -95,6 +95,7 @@ class LocalProvider(Provider):
         self.host = HostRegistry()
         self._multi_ip = None
         self.preferred_gpus: list[int] = []  # an early burn-in is already validating these
+        self._reserved: dict[str, tuple[list[str], list[int]]] = {}  # reserve(): name -> (ips, gpus)
 
     def prefer_gpus(self, gpus: list[int]) -> None:
         """Hand workers these GPUs first (when enough of them are free): the early burn-in
@@ -278,23 +279,61 @@ class LocalProvider(Provider):
         return sorted(out)
 
     # ---- lifecycle ----------------------------------------------------------------
+    def reserve(self, machines: list[tuple[str, str, list[str], str]]) -> None:
+        """Allocate the addresses and GPU slices of several machines -- (name, package, networks,
+        role) -- under one take of the workspace and host locks and one write of the allocation
+        table and the host registry, instead of one per machine (the engine's parallel creates
+        queue on those locks: ~2-5 ms each, 9 machines deep at 8 workers). Best effort: if any
+        machine cannot be allocated, nothing is reserved and each create allocates (and reports)
+        on its own."""
+        todo = []
+        try:
+            for name, package, networks, role in machines:
+                nets = [self.network_by_id_or_name(n) for n in networks] or [
+                    self.network_by_id_or_name(self.default_network)]
+                todo.append((name, self.package_by_id_or_name(package), nets, role))
+            with file_lock(self.lock_file):
+                alloc = read_json(self.alloc_file, {}) or {}
+                got = {}
+                with self.host.locked() as host:
+                    for name, pkg, nets, role in todo:
+                        if name in alloc.get("machines", {}):
+                            raise ProvisionError(f"machine {name} already exists")
+                        ips = self._alloc_ips(alloc, name, nets, host)
+                        gpus = self._alloc_gpus(alloc, name, 0 if role == "master" else pkg.gpus, host)
+                        alloc.setdefault("machines", {})[name] = {"ips": ips, "gpus": gpus}
+                        got[name] = (ips, gpus)
+                    atomic_write_json(self.alloc_file, alloc)
+                self._reserved.update(got)
+        except (ProvisionError, OSError, KeyError, ValueError):
+            return
+
+    def release_reservation(self, name: str) -> None:
+        """A reserved machine that will not be created after all (its create failed for good)."""
+        if self._reserved.pop(name, None) is not None:
+            self.delete_machine(Machine(name=name, id="", package="", networks=[], primaryip="", ips=[], gpus=[],
+                                        image="", tags={}, sandbox=str(self.machines_dir / name)))
+
     def create_machine(self, name: str, package: str, networks: list[str], image: str = "",
                        root_authorized_keys: str = "", tags: dict | None = None) -> Machine:
         pkg = self.package_by_id_or_name(package)
         nets = [self.network_by_id_or_name(n) for n in networks] or [self.network_by_id_or_name(self.default_network)]
         role = (tags or {}).get("role", "host")
         sandbox = self.machines_dir / name
-        with file_lock(self.lock_file):
-            alloc = read_json(self.alloc_file, {}) or {}
-            if name in alloc.get("machines", {}):
-                raise ProvisionError(f"machine {name} already exists")
-            # the owner's alloc.json is written under the host lock too: a concurrent reaper
-            # must never see a claim whose machine its owner does not list yet
-            with self.host.locked() as host:
-                ips = self._alloc_ips(alloc, name, nets, host)
-                gpus = self._alloc_gpus(alloc, name, 0 if role == "master" else pkg.gpus, host)
-                alloc.setdefault("machines", {})[name] = {"ips": ips, "gpus": gpus}
-                atomic_write_json(self.alloc_file, alloc)
+        if name in self._reserved:  # allocated with its siblings (reserve)
+            ips, gpus = self._reserved.pop(name)
+        else:
+            with file_lock(self.lock_file):
+                alloc = read_json(self.alloc_file, {}) or {}
+                if name in alloc.get("machines", {}):
+                    raise ProvisionError(f"machine {name} already exists")
+                # the owner's alloc.json is written under the host lock too: a concurrent reaper
+                # must never see a claim whose machine its owner does not list yet
+                with self.host.locked() as host:
+                    ips = self._alloc_ips(alloc, name, nets, host)
+                    gpus = self._alloc_gpus(alloc, name, 0 if role == "master" else pkg.gpus, host)
+                    alloc.setdefault("machines", {})[name] = {"ips": ips, "gpus": gpus}
+                    atomic_write_json(self.alloc_file, alloc)
         for sub in ("run", "logs", "pods", "etc"):
             (sandbox / sub).mkdir(parents=True, exist_ok=True)
         if root_authorized_keys:

@@ -272,6 +272,8 @@ class Engine:
             # gained nothing, profiles/r2_n8) -- a machine that failed it never starts services
             self._boot(m, spec)
             return m
+        if hasattr(self.provider, "release_reservation"):
+            self.provider.release_reservation(a["name"])
         raise ProvisionError(f"{spec.address}: create failed after {self.retries + 1} attempts: {last_err}")
 
     def apply(self) -> ApplyResult:
@@ -298,6 +300,9 @@ class Engine:
                 self.provider.delete_machine(Machine.from_dict(cur["machine"]))
                 self._save_resource(s.address, None)
             todo.append(s)
+        if todo and hasattr(self.provider, "reserve"):  # one allocation for all (local machines)
+            self.provider.reserve([(s.attrs["name"], s.attrs["package"], list(s.attrs.get("networks", [])),
+                                    (s.attrs.get("tags") or {}).get("role", "host")) for s in todo])
         workers = self.parallelism or max(1, len(todo))
         with Pool(workers, "provision") as ex:
             futs = {ex.submit(self._create, s): s for s in todo}
