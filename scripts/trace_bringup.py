@@ -23,13 +23,13 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 
-def one(root: Path, nodes: int) -> list[tuple[float, str, str]]:
+def one(root: Path, nodes: int, package: str = "mi355x-1gpu") -> list[tuple[float, str, str]]:
     from tritonk8ssupervisor_amd.orchestrator import init_workspace
 
     init_workspace(root)
     for f in ("setup.sh", "tk8s", "kubectl"):
         shutil.copy2(REPO / f, root / f)
-    (root / "answers.json").write_text(json.dumps({"nodes": nodes, "package": "mi355x-1gpu", "confirm": "yes"}))
+    (root / "answers.json").write_text(json.dumps({"nodes": nodes, "package": package, "confirm": "yes"}))
     env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_TRACE="1",
                TK8S_HOST_REGISTRY=str(root / "hostreg"))
     t0 = time.time()
@@ -64,13 +64,14 @@ def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--nodes", type=int, default=1)
+    ap.add_argument("--package", default="mi355x-1gpu", help="cpu-only: BASELINE configs[1]'s workers")
     ap.add_argument("--out")
     a = ap.parse_args()
     runs = []
     for i in range(a.runs):
         root = Path(tempfile.mkdtemp(prefix="tk8s-trace-"))
         try:
-            tl = one(root, a.nodes)
+            tl = one(root, a.nodes, a.package)
         finally:
             shutil.rmtree(root, ignore_errors=True)
         runs.append([{"ms": round(t, 2), "where": w, "what": x} for t, w, x in tl])
