@@ -362,6 +362,34 @@ def test_bootstrap_refuses_a_node_runtime_older_than_python_3_8(ws, tmp_path, mo
     eng.destroy()
 
 
+@pytest.mark.parametrize("in_process", [True, False])
+def test_bootstrap_in_process_and_its_off_switch(ws, monkeypatch, in_process):
+    """A local machine's standard bootstrap is checked in the engine (no shell per machine);
+    TK8S_INPROCESS_BOOTSTRAP=0 sends it to the provider's shell. Both refuse a sandbox whose
+    directories are missing."""
+    from tritonk8ssupervisor_amd import provision
+    from tritonk8ssupervisor_amd.provider.base import Machine
+
+    monkeypatch.setenv("TK8S_INPROCESS_BOOTSTRAP", "1" if in_process else "0")
+    prov = LocalProvider(ws.state_dir)
+    _rancher_tf(ws, prov, 2)
+    scripts = []
+    real = prov.exec
+    monkeypatch.setattr(prov, "exec", lambda m, c, *a, **k: (scripts.append(c), real(m, c, *a, **k))[1])
+    eng = Engine(ws.tf, prov, retries=0)
+    eng.get()
+    assert eng.apply().ok
+    boots = [c for c in scripts if provision.BOOTSTRAP[0] in c]
+    assert len(boots) == (0 if in_process else 3), scripts
+    m = Machine(name="x", id="x", package="p", networks=[], primaryip="127.0.0.9", sandbox=str(ws.state_dir))
+    done = provision._bootstrap_in_process(prov, m, list(provision.BOOTSTRAP))
+    if in_process:
+        assert done is not None and done[0] != 0 and "missing" in done[1]
+    else:
+        assert done is None
+    eng.destroy()
+
+
 def test_engine_reserves_all_machines_in_one_allocation(ws, monkeypatch):
     """The local provider allocates every planned machine's address and GPU slice under one take
     of the locks (reserve), and a machine whose create fails for good gives its reservation back."""
