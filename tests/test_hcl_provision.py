@@ -413,3 +413,25 @@ def test_engine_reserves_all_machines_in_one_allocation(ws, monkeypatch):
     alloc = json.loads((ws.state_dir / "alloc.json").read_text())
     assert sorted(alloc["machines"]) == ["kubemaster", "kubenode1", "kubenode3"], alloc["machines"]
     eng2.destroy()
+
+
+def test_hcl_token_cache_round_trips_and_is_keyed_by_text(tmp_path, monkeypatch):
+    """The parser's tokens are remembered across runs (utils/pcache.py, keyed by the file's whole
+    text): a later process parses from the cache to the same tree, and a changed text is
+    tokenized afresh."""
+    from tritonk8ssupervisor_amd.utils.pcache import PersistentCache
+
+    monkeypatch.setenv("TK8S_YAML_CACHE", str(tmp_path))
+    monkeypatch.setattr(hcl, "_TOKEN_MEMO", {})
+    monkeypatch.setattr(hcl, "_TOKEN_CACHE", None)
+    text = 'module "m" {\n  source = "host"\n  n = 3\n  ok = true\n  nets = ["a", "${var.x}"]\n}\n'
+    first = hcl.parse(text)
+    table = PersistentCache(f"hcl-tokens-{hcl._TOKENS_VERSION}")
+    assert table.get(text) == hcl._tokens(text)
+    monkeypatch.setattr(hcl, "_TOKEN_MEMO", {})  # a new process: from the file
+    monkeypatch.setattr(hcl, "_TOKEN_CACHE", None)
+    calls = []
+    real = hcl._tokens
+    monkeypatch.setattr(hcl, "_tokens", lambda t: (calls.append(t), real(t))[1])
+    assert hcl.parse(text) == first and calls == []
+    assert hcl.parse(text.replace("3", "4")).children("module")[0].attrs["n"] == 4 and len(calls) == 1

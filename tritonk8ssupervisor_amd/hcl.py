@@ -208,8 +208,33 @@ class _Parser:
         raise HclError(f"line {tok[2]}: unexpected {tok[1]!r}")
 
 
+_TOKENS_VERSION = 1
+_TOKEN_MEMO: dict[str, list] = {}
+_TOKEN_CACHE = None
+
+
+def _cached_tokens(text: str) -> list[tuple[str, Any, int]]:
+    """_tokens(text), remembered in this process (the engine reads one module directory per
+    machine: the host module's files nine times at 8 workers) and across runs in the parse cache
+    (utils/pcache.py, keyed by the whole text: the character scanner was ~2-4 ms of every
+    provision on the MI355X host). Tokens are immutable tuples, so callers can share them."""
+    global _TOKEN_CACHE
+    toks = _TOKEN_MEMO.get(text)
+    if toks is None:
+        if _TOKEN_CACHE is None:
+            from .utils.pcache import PersistentCache
+
+            _TOKEN_CACHE = PersistentCache(f"hcl-tokens-{_TOKENS_VERSION}", limit=2000)
+        toks = _TOKEN_CACHE.get(text)
+        if not isinstance(toks, list):
+            toks = _tokens(text)
+            _TOKEN_CACHE.put(text, toks)
+        _TOKEN_MEMO[text] = toks
+    return toks
+
+
 def parse(text: str) -> Block:
-    return _Parser(_tokens(text)).body(None)
+    return _Parser(_cached_tokens(text)).body(None)
 
 
 def parse_file(path: str | os.PathLike) -> Block:

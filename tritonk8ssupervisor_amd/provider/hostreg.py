@@ -41,10 +41,17 @@ def _sandbox_alive(sandbox: Path) -> bool:
     return False
 
 
-def _stale(claim: dict) -> bool:
+def _stale(claim: dict, owners: dict | None = None) -> bool:
+    """``owners``: allocation tables already read during this reap (one read per workspace, not
+    one per claimed machine)."""
     alloc_file = Path(claim.get("alloc", ""))
     machine = claim.get("machine", "")
-    owner = read_json(alloc_file, {}) or {}
+    if owners is None or str(alloc_file) not in owners:
+        owner = read_json(alloc_file, {}) or {}
+        if owners is not None:
+            owners[str(alloc_file)] = owner
+    else:
+        owner = owners[str(alloc_file)]
     if machine not in owner.get("machines", {}):
         return True
     if pid_alive(int(claim.get("pid") or 0)):
@@ -65,6 +72,7 @@ class HostRegistry:
         with file_lock(self.lock_file):
             table = read_json(self.file, {}) or {}
             before = repr(table)
+            tables: dict[str, dict] = {}
             for kind in ("ips", "gpus"):
                 claims = table.setdefault(kind, {})
                 owners: dict[tuple, bool] = {}
@@ -72,7 +80,7 @@ class HostRegistry:
                     c = claims[key]
                     k = (c.get("alloc"), c.get("machine"), c.get("pid"))
                     if k not in owners:
-                        owners[k] = _stale(c)
+                        owners[k] = _stale(c, tables)
                     if owners[k]:
                         del claims[key]
             yield table

@@ -162,10 +162,11 @@ class Engine:
 
     def specs(self) -> list[ResourceSpec]:
         out = []
+        mods: dict[Path, hcl.Block] = {}  # one parse per module source (8 workers share "host")
         for m in self.root().children("module"):
             name = m.labels[0]
             src = (self.dir / str(m.attrs["source"])).resolve()
-            mod = hcl.parse_dir(src)
+            mod = mods.get(src) or mods.setdefault(src, hcl.parse_dir(src))
             variables = {}
             for v in mod.children("variable"):
                 vname = v.labels[0]
