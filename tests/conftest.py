@@ -16,6 +16,19 @@ os.environ.setdefault("TK8S_HOST_REGISTRY", os.path.join(
     os.environ.get("TMPDIR", "/tmp"), f"tk8s-hostreg-{os.environ.get('PYTEST_XDIST_TESTRUNUID') or os.getpid()}"))
 
 
+def die_with_parent():
+    """preexec_fn for a daemon a test starts: SIGTERM when the test process dies (an interrupted
+    or timed-out pytest worker must not leave its control planes running)."""
+    import ctypes
+
+    prctl = ctypes.CDLL(None, use_errno=True).prctl
+
+    def arm() -> None:
+        prctl(1, 15)  # PR_SET_PDEATHSIG, SIGTERM
+
+    return arm
+
+
 @pytest.fixture(autouse=True)
 def _restore_environ():
     """Setup.configure exports the cluster config into os.environ (the reference's exportVars,

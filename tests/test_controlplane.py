@@ -21,7 +21,9 @@ def _start(tmp_path, grace=0.6, state_dir=None):
             "--node-grace", str(grace), "--ready-file", str(ready)]
     if state_dir:
         argv += ["--state-dir", str(state_dir)]
-    p = subprocess.Popen(argv, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    from conftest import die_with_parent
+
+    p = subprocess.Popen(argv, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, preexec_fn=die_with_parent())
     deadline = time.monotonic() + 30
     while not ready.exists():
         assert p.poll() is None, p.stdout.read().decode()

@@ -23,6 +23,10 @@ def test_plan_for_a_plain_non_interactive_bring_up(tmp_path):
     four = earlyburn.plan(["--answers", "answers.json", "--package", "mi355x-4gpu"], env, ws)
     assert four["gpus"] == list(range(8))
     assert earlyburn.plan(["--answers", "answers.json", "--nodes", "3", "--package", "mi355x-4gpu"], env, ws) is None
+    # cpu-only workers: nothing to burn in, but the control-plane and agent zygotes are planned
+    cpu = earlyburn.plan(["--answers", "answers.json", "--package", "cpu-only"], env, ws)
+    assert cpu["gpus"] == [] and cpu["command"] is None
+    assert cpu["workers"] == ["kubenode1", "kubenode2"] and cpu["master"] == "kubemaster"
 
 
 def test_anything_unusual_is_left_to_the_orchestrator(tmp_path):
@@ -33,7 +37,6 @@ def test_anything_unusual_is_left_to_the_orchestrator(tmp_path):
                  ["--answers", "answers.json", "--no-validate"],
                  ["--answers", "answers.json", "--hbm-bytes", "1024"],
                  ["--answers", "answers.json", "--rocprof"],
-                 ["--answers", "answers.json", "--package", "cpu-only"],
                  ["--answers", "answers.json", "--package", "2"]):  # a menu index: the wizard maps it
         assert earlyburn.plan(argv, env, ws) is None, argv
     assert earlyburn.plan(["--answers", "answers.json"], dict(env, TK8S_HOST_BURNIN="0"), ws) is None

@@ -425,7 +425,7 @@ def test_hcl_token_cache_round_trips_and_is_keyed_by_text(tmp_path, monkeypatch)
     monkeypatch.setattr(hcl, "_TOKEN_MEMO", {})
     monkeypatch.setattr(hcl, "_TOKEN_CACHE", None)
     text = 'module "m" {\n  source = "host"\n  n = 3\n  ok = true\n  nets = ["a", "${var.x}"]\n}\n'
-    first = hcl.parse(text)
+    first = hcl.parse(text, cache=True)
     table = PersistentCache(f"hcl-tokens-{hcl._TOKENS_VERSION}")
     assert table.get(text) == hcl._tokens(text)
     monkeypatch.setattr(hcl, "_TOKEN_MEMO", {})  # a new process: from the file
@@ -433,5 +433,6 @@ def test_hcl_token_cache_round_trips_and_is_keyed_by_text(tmp_path, monkeypatch)
     calls = []
     real = hcl._tokens
     monkeypatch.setattr(hcl, "_tokens", lambda t: (calls.append(t), real(t))[1])
-    assert hcl.parse(text) == first and calls == []
-    assert hcl.parse(text.replace("3", "4")).children("module")[0].attrs["n"] == 4 and len(calls) == 1
+    assert hcl.parse(text, cache=True) == first and calls == []
+    assert hcl.parse(text.replace("3", "4"), cache=True).children("module")[0].attrs["n"] == 4 and len(calls) == 1
+    assert hcl.parse(text) == first and len(calls) == 2  # the generated root: never cached

@@ -246,21 +246,24 @@ def plan(argv: list[str], environ=None, cwd: str | None = None, kfd_root: str = 
         return None
     nodes = str(opts.get("--nodes", answers.get("nodes", 1)) or 1)
     per = package_gpus(opts.get("--package", answers.get("package") or "mi355x-1gpu"))
-    if not (len(nodes) == 1 and nodes in "123456789") or not per:
+    if not (len(nodes) == 1 and nodes in "123456789") or per is None:
         return None
     count = int(nodes) * per
-    fake = env.get("TK8S_FAKE_GPUS")
-    if fake:
-        free = list(range(int(fake)))
-    else:
-        n = len(kfd_gpu_nodes(kfd_root))
-        vis = visible_filter(n, env)
-        claimed = _host_claimed_gpus(env)
-        free = [i for i in range(len(vis) if vis is not None else n) if i not in claimed]
-    if len(free) < count:
-        return None
-    # the per-machine command (peers inside a multi-GPU machine), with the host-wide pulls added
-    cmd = host_burnin_command(default_validation_command(peers=per > 1), free[:count])
+    free: list[int] = []
+    cmd = None  # cpu-only workers: nothing to burn in, but the zygotes still pay off
+    if count:
+        fake = env.get("TK8S_FAKE_GPUS")
+        if fake:
+            free = list(range(int(fake)))
+        else:
+            n = len(kfd_gpu_nodes(kfd_root))
+            vis = visible_filter(n, env)
+            claimed = _host_claimed_gpus(env)
+            free = [i for i in range(len(vis) if vis is not None else n) if i not in claimed]
+        if len(free) < count:
+            return None
+        # the per-machine command (peers inside a multi-GPU machine), with the host-wide pulls added
+        cmd = host_burnin_command(default_validation_command(peers=per > 1), free[:count])
     state = os.path.join(ws, ".tk8s")
     master = str(opts.get("--master-hostname", answers.get("master_hostname") or "kubemaster"))
     prefix = str(opts.get("--node-prefix", answers.get("node_prefix") or "kubenode"))
@@ -479,8 +482,34 @@ def _send_plan(pre: tuple[int, int, str], cmd: list[str], env: dict, log: str) -
     return True
 
 
+def _spawn_burnin(p: dict, pre) -> Early:
+    run = os.path.join(p["state_dir"], "run")
+    vis = dict(compose_visible_devices(p["gpus"]))
+    vis["NODE_NAME"] = "host"
+    cmd = p["command"] + ["--out", p["result"]]
+    log = os.path.join(run, "host-burnin.log")
+    import time
+
+    if pre is not None and os.environ.get("TK8S_FAULTS", "").find("preload.kill") >= 0:
+        _kill_preloaded(pre)  # fault injection (tests/test_startup_fallbacks.py): dead before the plan
+    if pre is not None and os.path.realpath(pre[2]) == os.path.realpath(cmd[0]) and _send_plan(pre, cmd, vis, log):
+        pid = pre[1]  # the preloaded probe: same binary, same environment plus the plan's
+    else:
+        _release(pre)
+        pid = os.posix_spawn(cmd[0], cmd, {**os.environ, **vis}, setsid=True, file_actions=[
+            (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
+            (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
+            (os.POSIX_SPAWN_OPEN, 2, log, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644),
+        ])
+    spawned = time.time()
+    with open(os.path.join(run, "host-burnin.pid"), "w") as f:
+        f.write(f"{pid}\n")
+    return Early(Spawned(pid), p["gpus"], p["command"], p["result"], spawned)
+
+
 def launch(argv: list[str]) -> Early | None:
-    """Called first thing by ``./setup.sh`` (cli/fast.py) for ``setup ...``."""
+    """Called first thing by ``./setup.sh`` (cli/fast.py) for ``setup ...``: the host burn-in
+    (none for cpu-only workers) and the control-plane and node-agent zygotes."""
     global _LAUNCHED, _ZYGOTE
     pre = _preloaded()
     try:
@@ -488,37 +517,19 @@ def launch(argv: list[str]) -> Early | None:
         if p is None:
             _release(pre)
             return None
-        run = os.path.join(p["state_dir"], "run")
-        os.makedirs(run, exist_ok=True)
+        os.makedirs(os.path.join(p["state_dir"], "run"), exist_ok=True)
         try:
             os.unlink(p["result"])
         except FileNotFoundError:
             pass
-        vis = dict(compose_visible_devices(p["gpus"]))
-        vis["NODE_NAME"] = "host"
-        cmd = p["command"] + ["--out", p["result"]]
-        log = os.path.join(run, "host-burnin.log")
-        import time
-
-        if pre is not None and os.environ.get("TK8S_FAULTS", "").find("preload.kill") >= 0:
-            _kill_preloaded(pre)  # fault injection (tests/test_startup_fallbacks.py): dead before the plan
-        if pre is not None and os.path.realpath(pre[2]) == os.path.realpath(cmd[0]) and _send_plan(pre, cmd, vis, log):
-            pid = pre[1]  # the preloaded probe: same binary, same environment plus the plan's
-        else:
+        if p["command"] is None:  # nothing to burn in: the preloaded probe is not needed
             _release(pre)
-            pid = os.posix_spawn(cmd[0], cmd, {**os.environ, **vis}, setsid=True, file_actions=[
-                (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
-                (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
-                (os.POSIX_SPAWN_OPEN, 2, log, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644),
-            ])
-        pre = None
-        spawned = time.time()
-        with open(os.path.join(run, "host-burnin.pid"), "w") as f:
-            f.write(f"{pid}\n")
+            _LAUNCHED = None
+        else:
+            _LAUNCHED = _spawn_burnin(p, pre)
     except Exception:  # noqa: BLE001 - an optimisation only: the orchestrator starts its own
         _release(pre)
         return None
-    _LAUNCHED = Early(Spawned(pid), p["gpus"], p["command"], p["result"], spawned)
     try:
         _ZYGOTE = controlplane_zygote(p)
     except Exception:  # noqa: BLE001 - the boot hook starts the control plane the usual way

@@ -214,17 +214,19 @@ _TOKEN_CACHE = None
 
 
 def _cached_tokens(text: str) -> list[tuple[str, Any, int]]:
-    """_tokens(text), remembered in this process (the engine reads one module directory per
-    machine: the host module's files nine times at 8 workers) and across runs in the parse cache
+    """_tokens(text), remembered in this process and across runs in the parse cache
     (utils/pcache.py, keyed by the whole text: the character scanner was ~2-4 ms of every
-    provision on the MI355X host). Tokens are immutable tuples, so callers can share them."""
+    provision on the MI355X host). Only for the module files (parse_dir), which are the same in
+    every workspace: the generated root (rancher.tf) names the workspace's own paths, and caching
+    it would grow the table by one entry per workspace. Tokens are immutable tuples, so callers
+    can share them."""
     global _TOKEN_CACHE
     toks = _TOKEN_MEMO.get(text)
     if toks is None:
         if _TOKEN_CACHE is None:
             from .utils.pcache import PersistentCache
 
-            _TOKEN_CACHE = PersistentCache(f"hcl-tokens-{_TOKENS_VERSION}", limit=2000)
+            _TOKEN_CACHE = PersistentCache(f"hcl-tokens-{_TOKENS_VERSION}", limit=64)
         toks = _TOKEN_CACHE.get(text)
         if not isinstance(toks, list):
             toks = _tokens(text)
@@ -233,19 +235,19 @@ def _cached_tokens(text: str) -> list[tuple[str, Any, int]]:
     return toks
 
 
-def parse(text: str) -> Block:
-    return _Parser(_cached_tokens(text)).body(None)
+def parse(text: str, cache: bool = False) -> Block:
+    return _Parser(_cached_tokens(text) if cache else _tokens(text)).body(None)
 
 
-def parse_file(path: str | os.PathLike) -> Block:
-    return parse(Path(path).read_text())
+def parse_file(path: str | os.PathLike, cache: bool = False) -> Block:
+    return parse(Path(path).read_text(), cache)
 
 
 def parse_dir(path: str | os.PathLike) -> Block:
     """Merge every *.tf in a directory (Terraform module semantics)."""
     root = Block("body", [])
     for f in sorted(Path(path).glob("*.tf")):
-        b = parse_file(f)
+        b = parse_file(f, cache=True)
         root.attrs.update(b.attrs)
         root.blocks.extend(b.blocks)
         root.duplicates.extend(b.duplicates)
