@@ -1,0 +1,18 @@
+"""The local executor gathers a host's node facts once for all of its sandboxes (executor.py)."""
+from tritonk8ssupervisor_amd import executor as ex_mod
+from tritonk8ssupervisor_amd.provider.base import Machine
+
+
+def test_local_facts_are_gathered_once_per_ttl(monkeypatch):
+    import tritonk8ssupervisor_amd.nodefacts as nf
+
+    calls = []
+    monkeypatch.setattr(nf, "node_facts", lambda: (calls.append(1), {"tk8s_host_gpus": len(calls)})[1])
+    ms = {n: Machine(name=n, id=n, package="p", networks=[], primaryip="127.0.0.1", sandbox="/tmp") for n in ("a", "b")}
+    ex = ex_mod.LocalExecutor(None, ms)
+    a, b = ex.facts("a"), ex.facts("b")
+    assert a == b == {"tk8s_host_gpus": 1} and len(calls) == 1
+    a["x"] = 1  # callers get their own copy
+    assert "x" not in ex.facts("a")
+    monkeypatch.setattr(ex, "FACTS_TTL_S", -1.0)  # expired: gathered again
+    assert ex.facts("b") == {"tk8s_host_gpus": 2}
