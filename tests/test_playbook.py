@@ -278,3 +278,30 @@ def test_outside_the_subset_goes_to_jinja2(tmp_path):
     assert T.render("{% for x in xs %}{{ x }}{% endfor %}", v) == "123"
     with pytest.raises(T.Undefined):
         T.evaluate("nope | map('int') | list", {})
+
+
+def test_cheap_tasks_on_local_machines_run_inline(tmp_path, monkeypatch):
+    """Sandboxes of this host: file-only modules run host after host in the engine's thread;
+    blocking modules, retries, loops, delegation and remote machines keep a thread per host."""
+    plays = [{"hosts": "all", "gather_facts": False, "tasks": [
+        {"name": "fact", "set_fact": {"x": "{{ inventory_hostname }}"}}]}]
+
+    class Local:
+        remote = False
+
+    class Remote:
+        remote = True
+
+    pb, res, _ = _play(tmp_path, plays)
+    assert res.ok and [pb.hostvars[h]["x"] for h in ("m1", "h1", "h2")] == ["m1", "h1", "h2"]
+    pb.executor = Local()
+    assert pb._inline({"set_fact": {"a": 1}}) and pb._inline({"ansible.builtin.copy": {"dest": "x", "content": ""}})
+    assert not pb._inline({"command": "sleep 1"}) and not pb._inline({"uri": {"url": "http://x"}})
+    assert not pb._inline({"stat": {"path": "x"}, "until": "r.stat.exists"})
+    assert not pb._inline({"debug": {"msg": "x"}, "loop": [1, 2]})
+    assert not pb._inline({"debug": {"msg": "x"}, "delegate_to": "localhost"})
+    monkeypatch.setenv("TK8S_PLAY_INLINE", "0")
+    assert not pb._inline({"set_fact": {"a": 1}})
+    monkeypatch.delenv("TK8S_PLAY_INLINE")
+    pb.executor = Remote()
+    assert not pb._inline({"set_fact": {"a": 1}})

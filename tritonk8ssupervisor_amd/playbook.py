@@ -309,8 +309,8 @@ class Playbook:
                 for h in hosts[1:]:
                     if task.get("register"):
                         self.hostvars[h.name][task["register"]] = res[0].result
-        elif len(hosts) == 1:
-            res = [self._run_on_host(task, hosts[0], play_vars)]
+        elif len(hosts) == 1 or self._inline(task):
+            res = [self._run_on_host(task, h, play_vars) for h in hosts]
         else:
             start = len(self.trace)
             res = list(self._executor().map(lambda h: self._run_on_host(task, h, play_vars), hosts))
@@ -393,6 +393,28 @@ class Playbook:
 
     def _facts_done(self, hosts: list[Host]) -> bool:
         return all("ansible_kernel" in self.hostvars.get(h.name, {}) for h in hosts)
+
+    # modules that only read or write a few local files when the machines are sandboxes of this
+    # host: nothing to overlap, so one thread per host only adds interpreter-lock contention
+    _INLINE_MODULES = frozenset({"set_fact", "debug", "stat", "file", "copy", "lineinfile", "slurp", "assert",
+                                 "fail", "tk8s_gpu_facts"})
+
+    def _inline(self, task: dict) -> bool:
+        """Run this task's hosts one after another in this thread (local machines, a module of
+        _INLINE_MODULES, no retries/loops/delegation). ``TK8S_PLAY_INLINE=0``: always a thread
+        per host."""
+        ex = self.executor
+        if ex is None or getattr(ex, "remote", True) or os.environ.get("TK8S_PLAY_INLINE", "1") == "0":
+            return False
+        if task.get("delegate_to") or "until" in task or task.get("with_items", task.get("loop")) is not None:
+            return False
+        try:
+            mod = self._module_of(task)[0]
+        except PlaybookError:
+            return False
+        from .playbook_modules import module_name
+
+        return module_name(mod) in self._INLINE_MODULES
 
     def _executor(self) -> Pool:
         """One pool for the whole run (``forks`` workers; 0 = every host): starting fresh threads
