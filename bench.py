@@ -269,6 +269,68 @@ def slow_start_cause(census: dict, runtime_init_ms: float | None, limit_ms: floa
     return "no KFD process change within 0.3 s before or during the start (driver-internal)"
 
 
+def _probe_libraries() -> list[str]:
+    """The shared libraries the GPU burn-in (tk8s-hsaprobe) maps, as the dynamic loader resolves
+    them -- the files a first bring-up on a fresh machine reads from disk."""
+    probe = REPO / "tritonk8ssupervisor_amd" / "bin" / "tk8s-hsaprobe"
+    try:
+        out = subprocess.run(["ldd", str(probe)], capture_output=True, text=True, timeout=10).stdout
+    except (OSError, subprocess.SubprocessError):
+        return []
+    libs = [probe.as_posix()]
+    for line in out.splitlines():
+        parts = line.split("=>")
+        if len(parts) == 2 and parts[1].strip().startswith("/"):
+            libs.append(parts[1].split("(")[0].strip())
+    return libs
+
+
+def page_cache_residency(paths: list[str]) -> dict:
+    """Fraction of each file's pages in the page cache (mincore(2) over a read-only map): what a
+    cold first run has to read from disk. Outside the timed region; {} where it cannot be asked."""
+    import ctypes
+    import mmap
+
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.mmap.restype = ctypes.c_void_p
+        libc.mmap.argtypes = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long)
+        libc.munmap.argtypes = (ctypes.c_void_p, ctypes.c_size_t)
+        libc.mincore.argtypes = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+    except (OSError, AttributeError):
+        return {}
+    page = mmap.PAGESIZE
+    out, total, resident = {}, 0, 0
+    for p in paths:
+        try:
+            fd = os.open(p, os.O_RDONLY)
+        except OSError:
+            continue
+        try:
+            size = os.fstat(fd).st_size
+            if size == 0:
+                continue
+            addr = libc.mmap(None, size, mmap.PROT_READ, mmap.MAP_SHARED, fd, 0)
+            if addr in (None, ctypes.c_void_p(-1).value):
+                continue
+            try:
+                npages = (size + page - 1) // page
+                vec = (ctypes.c_ubyte * npages)()
+                if libc.mincore(ctypes.c_void_p(addr), size, vec) != 0:
+                    continue
+                res = sum(b & 1 for b in vec)
+            finally:
+                libc.munmap(ctypes.c_void_p(addr), size)
+            out[os.path.basename(p)] = {"mib": round(size / 2**20, 1), "resident": round(res / npages, 3)}
+            total += npages
+            resident += res
+        finally:
+            os.close(fd)
+    if total:
+        out["_all"] = {"mib": round(total * page / 2**20, 1), "resident": round(resident / total, 3)}
+    return out
+
+
 def one_bringup(ws: Path, n: int, args, env: dict, log, census: KfdCensus | None = None, package: str | None = None,
                 rccl: str | None = None) -> dict:
     answers = {"nodes": n, "package": package or args.package, "name": "k8s bench", "confirm": "yes"}
@@ -366,6 +428,43 @@ def teardown(ws: Path, env: dict, log) -> float:
     return time.perf_counter() - t0
 
 
+def _stats(xs: list[float]) -> dict:
+    srt = sorted(xs)
+    mid = len(srt) // 2
+    return {"mean_s": round(sum(xs) / len(xs), 4),
+            "median_s": round(srt[mid] if len(srt) % 2 else (srt[mid - 1] + srt[mid]) / 2, 4),
+            "min_s": round(srt[0], 4), "max_s": round(srt[-1], 4)}
+
+
+def series(root: Path, name: str, n: int, args, env: dict, log, steps: int, warmup: int = 1, settle: float = 0.0,
+           rccl: str | None = None, env_over: dict | None = None) -> dict:
+    """``warmup`` untimed then ``steps`` timed bring-ups of 1 master + ``n`` workers of the
+    headline's package, each bracketed like a headline step, teardown and workspace outside."""
+    step_env = dict(env, **(env_over or {}))
+    ready, proc, fabric, rccl_s, last = [], [], [], [], {}
+    for i in range(warmup + steps):
+        ws = root / f"{name}{i}"
+        make_workspace(ws)
+        t0 = time.perf_counter()
+        s = one_bringup(ws, n, args, step_env, log, rccl=rccl)
+        dt = time.perf_counter() - t0
+        teardown(ws, env, log)
+        shutil.rmtree(ws, ignore_errors=True)
+        if s.get("post_ready_error"):
+            raise RuntimeError(f"{name} step {i}: {s['post_ready_error'][-800:]}")
+        if i >= warmup:
+            ready.append(s["ready_wall_seconds"])
+            proc.append(dt)
+            fabric.append(s["wall_seconds"])
+            rccl_s.append(s.get("phases", {}).get("rccl", 0.0))
+            last = s
+        if settle > 0:
+            time.sleep(settle)
+    return {"steps": steps, "warmup": warmup, "ready": _stats(ready), "process": _stats(proc),
+            "setup_exit": _stats(fabric), "rccl_phase_mean_s": round(sum(rccl_s) / len(rccl_s), 4),
+            "last": last}
+
+
 CURVE_NODES = (1, 2, 4, 8)
 
 
@@ -423,6 +522,12 @@ def main(argv=None) -> int:
     ap.add_argument("--curve-steps", type=int, default=5,
                     help="timed steps per point of the cpu-only worker curve (BASELINE configs[1], 1/2/4/8 workers) "
                          "run after the headline on a single-rank run; 0 skips it")
+    ap.add_argument("--plain-steps", type=int, default=5,
+                    help="timed bring-ups with TK8S_SHORTCUTS=0 (every start-up shortcut off), reported as "
+                         "plain_path_s on a single-rank run; 0 skips them")
+    ap.add_argument("--fabric-steps", type=int, default=None,
+                    help="timed bring-ups with --rccl on, reported as fabric_validated_s (launch -> ./setup.sh exits "
+                         "after a passing RCCL all-reduce Job); default 5 with real GPUs, 0 with fake ones")
     ap.add_argument("--settle", type=float, default=None,
                     help="pause after each teardown, outside the timed region, so the driver has released the "
                          "previous step's GPU processes (default: 1.0 s with real GPUs, 0 with fake ones)")
@@ -442,7 +547,13 @@ def main(argv=None) -> int:
     teardown_s: list[float] = []
     ready_times: list[float] = []
     err = None
+    # what the cold first run starts from: the byte-code cache the tree came
+    # with, and how much of the burn-in's shared libraries the page cache already holds
+    cold_start_state: dict = {}
     if d.rank == 0:
+        pyc = REPO / "build" / "pycache"
+        cold_start_state = {"build_pycache_files_at_start": sum(1 for _ in pyc.rglob("*.pyc")) if pyc.is_dir() else 0,
+                            "probe_libs_page_cache_at_start": page_cache_residency(_probe_libraries())}
         from tritonk8ssupervisor_amd.utils.build_native import build
 
         build()  # incremental; no-op when the in-tree build is current
@@ -539,6 +650,23 @@ def main(argv=None) -> int:
             curve = {"error": str(e)[-1500:]}
         finally:
             shutil.rmtree(croot, ignore_errors=True)
+    plain = fabric = None
+    fabric_steps = args.fabric_steps if args.fabric_steps is not None else (0 if fake else 5)
+    if d.world == 1 and (args.plain_steps > 0 or fabric_steps > 0):
+        xroot = Path(tempfile.mkdtemp(prefix="tk8s-extra-", dir=os.environ.get("TMPDIR", "/tmp")))
+        with open(args.log, "a") if args.log else open(os.devnull, "w") as xlog:
+            if args.plain_steps > 0:
+                try:
+                    plain = series(xroot, "plain", n, args, env, xlog, args.plain_steps, settle=settle,
+                                   env_over={"TK8S_SHORTCUTS": "0"})
+                except Exception as e:  # noqa: BLE001 - the headline stands; the key says why it is missing
+                    plain = {"error": str(e)[-1500:]}
+            if fabric_steps > 0:
+                try:
+                    fabric = series(xroot, "fabric", n, args, env, xlog, fabric_steps, settle=settle, rccl="on")
+                except Exception as e:  # noqa: BLE001
+                    fabric = {"error": str(e)[-1500:]}
+        shutil.rmtree(xroot, ignore_errors=True)
     step_mean = sum(times) / len(times)
     mean = sum(ready_times) / len(ready_times)
     ready = [s["ready_seconds"] for s in summaries if s.get("ready_seconds") is not None]
@@ -593,6 +721,16 @@ def main(argv=None) -> int:
         "cold_first_run_s": round(cold["ready_wall_seconds"], 4) if cold else None,
         "cold_first_run_what": "step 0 (a warmup step) with empty byte-code and parse caches: a first "
                                "./setup.sh on a fresh install" if cold else None,
+        # where the cold first run's time went, and what it started from
+        "cold_first_run_phases_s": {k: round(v, 4) for k, v in (cold.get("phases") or {}).items()} if cold else None,
+        "cold_first_run_burnin": {k: v for k, v in (
+            ("runtime_init_ms", (cold.get("host_burnin") or {}).get("runtime_init_ms")),
+            ("total_ms", (cold.get("host_burnin") or {}).get("total_ms")),
+            ("spawn_ms", cold.get("burnin_spawn_ms")), ("exec_ms", cold.get("burnin_exec_ms")),
+            ("notice_ms", cold.get("burnin_notice_ms")))} if cold else None,
+        "cold_first_run_kfd_census": cold.get("kfd_census") if cold else None,
+        "cold_first_run_slow_start_cause": cold.get("slow_start_cause") if cold else None,
+        "cold_first_run_start_state": cold_start_state or None,
         "rccl_check_s": round(sum(s.get("phases", {}).get("rccl", 0.0) for s in summaries) / len(summaries), 4)
         if summaries else None,
         "ready_s_inside_setup": round(sum(ready) / len(ready), 4) if ready else None,
@@ -630,6 +768,20 @@ def main(argv=None) -> int:
                                     "last": excluded[-1]["error"]}
     if curve is not None:
         out["curve_config2"] = curve
+    if plain is not None:  # the bring-up with every start-up shortcut off
+        out["plain_path_s"] = plain.get("ready", {}).get("mean_s")
+        out["plain_path"] = {k: v for k, v in plain.items() if k != "last"}
+        out["plain_path"]["what"] = ("TK8S_SHORTCUTS=0: every start-up shortcut of docs/architecture.md off "
+                                     "(preloaded/early burn-in, zygotes, caches, stand-ins, inline tasks, ...)")
+    if fabric is not None:  # launch -> a passing RCCL all-reduce Job, N GPUs
+        last_rccl = (fabric.get("last") or {}).get("rccl") or {}
+        out["fabric_validated_s"] = fabric.get("setup_exit", {}).get("mean_s")
+        out["fabric_validated"] = {k: v for k, v in fabric.items() if k != "last"}
+        out["fabric_validated"].update({
+            "what": "--rccl on: wall-clock from launching ./setup.sh to its exit after the RCCL all-reduce Job "
+                    "over every GPU passed its exact check",
+            "rccl": {k: last_rccl.get(k) for k in ("ok", "nranks", "pods", "comm_init_ms_max", "init_spread_ms",
+                                                   "peak_busbw_gbps", "transport", "prestarted")}})
     print(json.dumps(out), flush=True)
     return 0
 

@@ -9,9 +9,17 @@ set -o pipefail
 # the script's directory comes from a parameter expansion, not $(dirname))
 case "$0" in */*) cd "${0%/*}" ;; esac
 PY="${TK8S_PYTHON:-python3}"
+# TK8S_SHORTCUTS=0: the plain path, every start-up shortcut off (tritonk8ssupervisor_amd/__init__.py
+# SHORTCUT_SWITCHES has the full list; these are the ones acted on before Python starts)
+if [[ "${TK8S_SHORTCUTS:-1}" == 0 ]]; then
+    export TK8S_PRELOAD_BURNIN=0 TK8S_HOST_BURNIN=0 TK8S_NO_PYCACHE_PREFIX=1
+    PYFLAGS=""  # site processing as usual (-S and the late site finder are a shortcut too)
+else
+    PYFLAGS="-S"
+fi
 if [[ "${1:-}" == "-c" ]]; then
     shift
-    exec "$PY" -S -c 'from tritonk8ssupervisor_amd.cli.fast import run; run()' clean "$@"
+    exec "$PY" $PYFLAGS -c 'from tritonk8ssupervisor_amd.cli.fast import run; run()' clean "$@"
 fi
 # A non-interactive bring-up (--answers) preloads the GPU burn-in: tk8s-hsaprobe starts now, maps
 # the ROCr runtime (~11 ms before its main()) while the CLI's interpreter starts, and waits on
@@ -30,4 +38,4 @@ fi
 # -S: skip site-packages .pth processing at start-up (tritonk8ssupervisor_amd/__init__.py adds
 # the site directories back); -c instead of -m: no runpy. The CLI's start-up is part of the
 # bring-up time.
-exec "$PY" -S -c 'from tritonk8ssupervisor_amd.cli.fast import run; run()' setup "$@"
+exec "$PY" $PYFLAGS -c 'from tritonk8ssupervisor_amd.cli.fast import run; run()' setup "$@"

@@ -73,5 +73,42 @@ def _pycache_prefix() -> None:
         os.environ["PYTHONPYCACHEPREFIX"] = d
 
 
+# TK8S_SHORTCUTS=0: every start-up shortcut of docs/architecture.md ("Start-up shortcuts and their
+# off-switches") off at once, the bring-up's plain path. setup.sh sets the same switches for the
+# ones it acts on before Python starts; bench.py reports this path as plain_path_s.
+SHORTCUT_SWITCHES = {
+    "TK8S_PRELOAD_BURNIN": "0",       # setup.sh's preloaded tk8s-hsaprobe
+    "TK8S_HOST_BURNIN": "0",          # the early host burn-in (earlyburn.py)
+    "TK8S_CP_ZYGOTE": "0",            # the control-plane zygote
+    "TK8S_AGENT_ZYGOTE": "0",         # the node-agent zygotes
+    "TK8S_HSA_CPU_CACHES": "1",       # ROCr's per-CPU cache walk runs as usual
+    "TK8S_YAML_CACHE": "off",         # the parse caches
+    "TK8S_NO_PYCACHE_PREFIX": "1",    # the shared byte-code prefix
+    "TK8S_LAZY_STDLIB": "0",          # the control plane's lazy logging/inspect/concurrent.futures
+    "TK8S_LOCAL_PREFETCH": "0",       # the local provider's prefetch
+    "TK8S_PROVISION_SERIAL": "0",     # serial local creates
+    "TK8S_PLAY_INLINE": "0",          # inline file-only tasks
+    "TK8S_INPROCESS_BOOTSTRAP": "0",  # the in-process machine bootstrap
+    "TK8S_FAST_ARGS": "0",            # the hand-written argument parsers (argparse instead)
+    "TK8S_SKIP_SITE": "0",            # daemons' interpreters start without -S (utils/procs.plain_argv)
+}
+
+
+def _shortcuts_off() -> None:
+    import os
+
+    if os.environ.get("TK8S_SHORTCUTS", "1") == "0":
+        os.environ.update(SHORTCUT_SWITCHES)
+
+
+def shortcut_on(switch: str) -> bool:
+    """Whether the shortcut behind ``switch`` (a key of SHORTCUT_SWITCHES) is on."""
+    import os
+
+    v = os.environ.get(switch)
+    return v is None or v != SHORTCUT_SWITCHES[switch]
+
+
+_shortcuts_off()
 _fast_site()
 _pycache_prefix()

@@ -1352,7 +1352,9 @@ def _parse_argparse(argv: list[str] | None) -> dict:
 def main(argv: list[str] | None = None) -> int:
     trace("agent", "imported")
     argv = sys.argv[1:] if argv is None else argv
-    a = _parse_fast(argv)
+    from .. import shortcut_on
+
+    a = _parse_fast(argv) if shortcut_on("TK8S_FAST_ARGS") else None
     if a is None or not (a["url_opt"] or a["url"] or a["await_url"]):
         a = _parse_argparse(argv)
     url = a["url_opt"] or a["url"]

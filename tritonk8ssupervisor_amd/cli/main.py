@@ -516,7 +516,9 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv: list[str] | None = None) -> int:
     argv = sys.argv[1:] if argv is None else argv
-    args = _fast_setup_args(argv) or build_parser().parse_args(argv)
+    from .. import shortcut_on
+
+    args = (_fast_setup_args(argv) if shortcut_on("TK8S_FAST_ARGS") else None) or build_parser().parse_args(argv)
     if getattr(args, "inventory", None):
         os.environ["TK8S_INVENTORY"] = str(Path(args.inventory).resolve())
     if getattr(args, "backend", None):

@@ -34,6 +34,11 @@ from ..utils.ids import token_hex
 from .httpserver import HttpError, Request
 
 ADMIN_TOKEN_FILE = "admin-token"
+_NS_RE = re.compile(r"^[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?$")
+# store kinds whose names and contents are credentials or other callers' data: never in the change
+# feed of a node or ServiceAccount token
+_PRIVATE_KINDS = frozenset({"secrets", "kv", "nodesecrets", "registrationtokens", "projects", "projecttemplates",
+                            "serviceaccounts"})
 
 # (method, path) anyone may call: liveness, version, discovery, node registration (token-gated
 # by its URL), the Rancher template list, and the dashboard (it shows anonymous callers only the
@@ -152,6 +157,83 @@ class Authentication:
             return
         raise HttpError(401, "Unauthorized: this request needs a bearer token "
                              "(the kubeconfig's, a ServiceAccount's, a node's or the server admin token)")
+
+    # ---- the side channels: KV, /v1/events, /v1/cluster/*, /metrics, /v2-beta/projects ------
+    # In the reference every environment is its own Rancher project and hosts join it with a
+    # registration token bound to its projectId (ranchermaster/tasks/main.yml:37-49,
+    # rancherhost/tasks/main.yml:11-17). The control plane's own side channels keep that scope:
+    # a token acts inside its environment -- and a ServiceAccount's inside its namespace -- only.
+    def _caller(self, req: Request) -> tuple:
+        hit = self._tokens().get(req.bearer or "")
+        if hit is None:
+            raise HttpError(401, "missing or invalid bearer token")
+        return hit
+
+    def _caller_project(self, req: Request, asked: str | None) -> dict:
+        """The environment a side-channel request acts in: any one the server admin asks for
+        (the oldest by default), otherwise the caller's own -- naming another one is 403."""
+        hit = self._caller(req)
+        if hit[0] == "admin" and hit[1] is None:
+            return self.project(asked)
+        if asked not in (None, "", "default", hit[1]):
+            raise HttpError(403, f"this token belongs to environment {hit[1]}, not {asked}")
+        return self.project(hit[1])
+
+    def _require_project_admin(self, req: Request, pid: str | None = None) -> tuple:
+        """The server admin token, or an environment's API token (of ``pid`` when given):
+        node and ServiceAccount tokens get 403."""
+        hit = self._caller(req)
+        if hit[0] != "admin" or (pid is not None and hit[1] not in (None, pid)):
+            raise HttpError(403, "this needs the server admin token or the environment's API token")
+        return hit
+
+    def kv_key(self, req: Request, key: str) -> str:
+        """The store key of KV ``key`` for this caller: ``<project>/<namespace>/<key>``.
+
+        * a ServiceAccount token: its own environment and namespace (``?namespace=`` may only
+          repeat it), so a pod reaches its own namespace's keys and nothing else;
+        * a node token: its environment, ``?namespace=`` (default ``default``), and only a
+          namespace that has a pod bound to the node that is not finished;
+        * an environment's API token: its environment, any namespace; the server admin token:
+          ``?project=`` (default: the oldest environment), any namespace."""
+        if not key or len(key) > 512 or "\0" in key:
+            raise HttpError(422, "a KV key is 1-512 characters")
+        hit = self._caller(req)
+        ns = req.q("namespace") or None
+        if ns is not None and not _NS_RE.match(ns):
+            raise HttpError(422, f"invalid namespace {ns!r}")
+        if hit[0] == "sa":
+            if ns not in (None, hit[2]):
+                raise HttpError(403, f"a ServiceAccount of namespace {hit[2]} cannot reach the keys of {ns}")
+            return f"{hit[1]}/{hit[2]}/{key}"
+        ns = ns or "default"
+        if hit[0] == "node":
+            live = [o for o in self._node_pods(hit[2], hit[1], ns)
+                    if (o.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
+            if not live:
+                raise HttpError(403, f"node {hit[2]} has no pod in namespace {ns}")
+            return f"{hit[1]}/{ns}/{key}"
+        try:
+            pid = self._caller_project(req, req.q("project"))["id"]
+        except HttpError as e:
+            if e.status != 404 or hit[1] is not None:
+                raise
+            pid = "-"  # the server admin before any environment exists
+        return f"{pid}/{ns}/{key}"
+
+    def event_filter(self, req: Request):
+        """What of the store's change feed (``/v1/events``) the caller may see: everything for the
+        server admin, its environment for an API token, for a node its environment minus the
+        credential-bearing kinds, for a ServiceAccount its namespace minus those."""
+        hit = self._caller(req)
+        if hit[0] == "admin":
+            return (lambda kind, o: True) if hit[1] is None else (lambda kind, o: o.get("_project") == hit[1])
+        pid = hit[1]
+        if hit[0] == "node":
+            return lambda kind, o: o.get("_project") == pid and kind not in _PRIVATE_KINDS
+        ns = hit[2]
+        return lambda kind, o: (o.get("_project") == pid and (o.get("metadata") or {}).get("namespace") == ns
+                                and kind not in _PRIVATE_KINDS)
 
     def _require_admin(self, req: Request, pid: str | None) -> None:
         """The server admin token, or the API token of project ``pid``."""

@@ -35,7 +35,9 @@ class RancherAPI:
         return {"type": "collection", "resourceType": "projectTemplate", "data": data}
 
     async def h_projects(self, req: Request):
-        return {"type": "collection", "resourceType": "project", "data": [self._public_project(p) for p in self.store.list("projects")]}
+        hit = self._require_project_admin(req)  # the server admin sees every environment, an API token its own
+        return {"type": "collection", "resourceType": "project",
+                "data": [self._public_project(p) for p in self.store.list("projects") if hit[1] in (None, p["id"])]}
 
     def _public_project(self, p: dict) -> dict:
         return {k: v for k, v in p.items() if k not in ("apiToken",)}
@@ -66,7 +68,9 @@ class RancherAPI:
         return Response(201, self._public_project(p))
 
     async def h_project_get(self, req: Request, pid: str):
-        return self._public_project(self.project(pid))
+        p = self.project(pid)
+        self._require_project_admin(req, p["id"])
+        return self._public_project(p)
 
     async def h_project_delete(self, req: Request, pid: str):
         p = self.project(pid)
@@ -282,19 +286,27 @@ class RancherAPI:
              "gpus": o["metadata"].get("annotations", {}).get(GPU + "-ids")} for o in pods]}
 
     # ---- KV -------------------------------------------------------------------------
+    # The rendezvous store of multi-process jobs (RCCL unique ids, torch addresses). Keys live in
+    # the caller's keyspace, <project>/<namespace>/<key> (authn.kv_key): a pod's ServiceAccount
+    # token reaches its own namespace only, so no other tenant can read or overwrite a Job's
+    # rendezvous, and the URL a pod uses ($TK8S_KV_URL/<job>/uid) is unchanged.
     async def h_kv_get(self, req: Request, key: str):
+        sk = self.kv_key(req, key)
         wait = float(req.q("wait", "0") or 0)
-        v = await self.store.wait_until(lambda: self.store.get("kv", key), min(wait, 120.0))
+        v = await self.store.wait_until(lambda: self.store.get("kv", sk), min(wait, 120.0))
         if not v:
             raise HttpError(404, f"key {key} not found")
         return Response(200, v["value"], content_type="text/plain")
 
     async def h_kv_put(self, req: Request, key: str):
-        self.store.put("kv", key, {"metadata": {"name": key}, "value": req.body.decode()})
+        sk = self.kv_key(req, key)
+        pid, ns, _ = sk.split("/", 2)
+        self.store.put("kv", sk, {"metadata": {"name": key, "namespace": ns}, "_project": pid,
+                                  "value": req.body.decode()})
         return Response(201, {"key": key})
 
     async def h_kv_delete(self, req: Request, key: str):
-        self.store.delete("kv", key)
+        self.store.delete("kv", self.kv_key(req, key))
         return Response(200, {"key": key, "deleted": True})
 
     # ---- readiness -----------------------------------------------------------------------
@@ -338,14 +350,14 @@ class RancherAPI:
         return "Running"
 
     async def h_cluster_status(self, req: Request):
-        p = self.project(req.q("project"))
+        p = self._caller_project(req, req.q("project"))
         s = self.summary(p["id"])
         s["job"] = self._job_state(p["id"], req.q("job"))
         return s
 
     async def h_cluster_wait(self, req: Request):
         """Long-poll until `nodes` Ready (+validated) with >= `gpus` allocatable (+ job done)."""
-        pid = req.q("project")
+        pid = self._caller_project(req, req.q("project"))["id"]
         want_nodes = int(req.q("nodes", "1"))
         want_gpus = int(req.q("gpus", "0"))
         validated = req.q("validated", "1") not in ("0", "false")
@@ -377,9 +389,16 @@ class RancherAPI:
         return Response(200, s)
 
     async def h_cp_events(self, req: Request):
+        """The store's change feed, filtered to what the caller's token may see (authn.event_filter)."""
+        allowed = self.event_filter(req)
         since = int(req.q("resourceVersion", "0") or 0)
-        wait = min(float(req.q("timeoutSeconds", "0") or 0), 60.0)
-        ev = await self.store.wait_events(since, None, wait)
+        deadline = time.monotonic() + min(float(req.q("timeoutSeconds", "0") or 0), 60.0)
+        while True:
+            ev = [e for e in self.store.events_since(since, None) if allowed(e["kind"], e["object"])]
+            left = deadline - time.monotonic()
+            if ev or left <= 0:
+                break
+            await self.store.wait_change(left)
         return {"resourceVersion": self.store.rv,
                 "events": [{"type": e["type"], "kind": e["kind"], "name": e["object"].get("metadata", {}).get("name"),
                             "resourceVersion": e["resourceVersion"]} for e in ev]}

@@ -353,31 +353,41 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
                 "tk8sVersion": __version__}
 
     async def h_metrics(self, req: Request):
+        """Prometheus text: the server admin sees every environment and the host-wide series, an
+        environment's API token its own environment's; node and ServiceAccount tokens get 403."""
+        hit = self._require_project_admin(req)
+        if hit[1] is not None:
+            return Response(200, "\n".join(self._project_metric_lines(hit[1])) + "\n",
+                            content_type="text/plain; version=0.0.4")
         lines = []
         for p in self.store.list("projects"):
-            pid = p["id"]
-            s = self.summary(pid)
-            lab = f'project="{pid}"'
-            lines += [f"tk8s_nodes{{{lab}}} {s['nodes']}", f"tk8s_nodes_ready{{{lab}}} {s['nodes_ready']}",
-                      f"tk8s_nodes_validated{{{lab}}} {s['nodes_validated']}",
-                      f"tk8s_gpus_capacity{{{lab}}} {s['gpus_capacity']}",
-                      f"tk8s_gpus_allocatable{{{lab}}} {s['gpus_allocatable']}",
-                      f"tk8s_gpus_in_use{{{lab}}} {s['gpus_in_use']}"]
-            for phase, n in s["pods_by_phase"].items():
-                lines.append(f'tk8s_pods{{{lab},phase="{phase}"}} {n}')
-        now = time.monotonic()
-        for k, t in self.leases.items():
-            lines.append(f'tk8s_node_heartbeat_age_seconds{{node="{k}"}} {now - t:.3f}')
-        lines += self._gpu_metric_lines()
+            lines += self._project_metric_lines(p["id"])
         lines.append(f"tk8s_store_resource_version {self.store.rv}")
         lines += self.reqmetrics.lines()
         return Response(200, "\n".join(lines) + "\n", content_type="text/plain; version=0.0.4")
 
-    def _gpu_metric_lines(self) -> list[str]:
-        """Per-GPU telemetry (AMD SMI, as the nodes report it), validation results and pod usage,
-        in the Prometheus text format -- what a device-metrics exporter would scrape."""
+    def _project_metric_lines(self, pid: str) -> list[str]:
+        s = self.summary(pid)
+        lab = f'project="{pid}"'
+        lines = [f"tk8s_nodes{{{lab}}} {s['nodes']}", f"tk8s_nodes_ready{{{lab}}} {s['nodes_ready']}",
+                 f"tk8s_nodes_validated{{{lab}}} {s['nodes_validated']}",
+                 f"tk8s_gpus_capacity{{{lab}}} {s['gpus_capacity']}",
+                 f"tk8s_gpus_allocatable{{{lab}}} {s['gpus_allocatable']}",
+                 f"tk8s_gpus_in_use{{{lab}}} {s['gpus_in_use']}"]
+        for phase, n in s["pods_by_phase"].items():
+            lines.append(f'tk8s_pods{{{lab},phase="{phase}"}} {n}')
+        now = time.monotonic()
+        for k, t in self.leases.items():
+            if k.startswith(pid + "/"):
+                lines.append(f'tk8s_node_heartbeat_age_seconds{{node="{k}"}} {now - t:.3f}')
+        return lines + self._gpu_metric_lines(pid)
+
+    def _gpu_metric_lines(self, pid: str) -> list[str]:
+        """Per-GPU telemetry (AMD SMI, as the nodes report it), validation results and pod usage
+        of environment ``pid``, in the Prometheus text format -- what a device-metrics exporter
+        would scrape."""
         out = []
-        for n in self.store.list("nodes"):
+        for n in self.store.list("nodes", lambda o: o.get("_project") == pid):
             node = n["metadata"]["name"]
             ann = n["metadata"].get("annotations") or {}
             for d in n.get("status", {}).get("devices") or []:
@@ -400,7 +410,9 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
                     out.append(f'{metric}{{node="{node}"}} {float(ann[key])}')
                 except (KeyError, ValueError):
                     pass
-        for (pid, node), m in sorted(getattr(self, "metrics", {}).items()):
+        for (mpid, node), m in sorted(getattr(self, "metrics", {}).items()):
+            if mpid != pid:
+                continue
             for key, cs in (m.get("pods") or {}).items():
                 ns, pod = key.split("/", 1)
                 for c in cs:
@@ -619,7 +631,9 @@ def _parse_fast(argv: list[str]) -> dict | None:
 
 def main(argv: list[str] | None = None) -> int:
     argv = sys.argv[1:] if argv is None else argv
-    a = _parse_fast(argv)
+    from .. import shortcut_on
+
+    a = _parse_fast(argv) if shortcut_on("TK8S_FAST_ARGS") else None
     if a is None:
         import argparse
 

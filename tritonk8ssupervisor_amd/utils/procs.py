@@ -17,8 +17,23 @@ import time
 from pathlib import Path
 
 
+def plain_argv(argv: list[str], env: dict | None = None) -> list[str]:
+    """``argv`` without the ``-S`` after a Python interpreter when the site-skipping shortcut is
+    off (``TK8S_SHORTCUTS=0`` / ``TK8S_SKIP_SITE=0``, in ``env`` or this process's environment)."""
+    e = env if env is not None else os.environ
+    if e.get("TK8S_SKIP_SITE", "1") != "0" and e.get("TK8S_SHORTCUTS", "1") != "0":
+        return argv
+    out = []
+    for i, a in enumerate(argv):
+        if a == "-S" and i > 0 and os.path.basename(argv[i - 1]).startswith("python"):
+            continue
+        out.append(a)
+    return out
+
+
 def spawn_daemon(argv: list[str], *, env: dict | None = None, cwd: str | None = None,
                  log_path: str | None = None, pidfile: str | None = None) -> subprocess.Popen:
+    argv = plain_argv(argv, env)
     log = open(log_path, "ab", buffering=0) if log_path else subprocess.DEVNULL
     try:
         p = subprocess.Popen(argv, env=env, cwd=cwd, stdin=subprocess.DEVNULL, stdout=log,
