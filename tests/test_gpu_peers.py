@@ -157,3 +157,62 @@ def test_the_example_torch_allreduce_job_runs_across_two_pods(ws):
         assert res["ok"] and res["nranks"] == 2 and res["backend"] == "gloo", res
     assert sorted(json.loads(kc("get", "pods", "-o", "json").stdout)["items"][i]["spec"]["nodeName"]
                   for i in range(2)) == ["kubenode1", "kubenode2"]
+
+
+def test_a_forged_peer_record_is_not_opened():
+    """the agent cross-checks every entry of a peer pod's gpu-devices record before
+    its pod may open that GPU -- the GPU must be one the peer's node allocated to that pod
+    (amd.com/gpu-ids, node-written) and registered as its own; ordinal and render minor come from
+    the node's registration and the host inventory, not from the record."""
+    import types
+
+    from tritonk8ssupervisor_amd.agent.agent import Agent
+
+    gpus = [types.SimpleNamespace(ordinal=i, render_minor=128 + i) for i in range(4)]
+    fake = types.SimpleNamespace(
+        name="kubenode1", plugin=types.SimpleNamespace(inventory=types.SimpleNamespace(gpus=gpus)),
+        _node_devices=lambda node: {"kubenode2": {"gpu1": 1}, "kubenode3": {"gpu2": 2}}[node])
+    peer = {"metadata": {"name": "rank1", "annotations": {"amd.com/gpu-ids": "gpu1"}}}
+    honest = json.dumps([{"node": "kubenode2", "id": "gpu1", "ordinal": 1, "renderMinor": 129}])
+    got = Agent._peer_record(fake, peer, "kubenode2", honest, "host0")
+    assert got == [{"node": "kubenode2", "id": "gpu1", "ordinal": 1, "host": "host0", "renderMinor": 129}]
+    # naming another node's GPU (gpu2 is kubenode3's), a GPU not allocated to the pod, or a lying
+    # ordinal / render minor: the first two are dropped, the last is re-derived
+    forged = json.dumps([{"node": "kubenode2", "id": "gpu2", "ordinal": 2, "renderMinor": 130},
+                         {"node": "kubenode2", "id": "gpu3", "ordinal": 3, "renderMinor": 131},
+                         {"node": "kubenode2", "id": "gpu1", "ordinal": 3, "renderMinor": 131}])
+    got = Agent._peer_record(fake, peer, "kubenode2", forged, "host0")
+    assert got == [{"node": "kubenode2", "id": "gpu1", "ordinal": 1, "host": "host0", "renderMinor": 129}]
+    peer["metadata"]["annotations"]["amd.com/gpu-ids"] = "gpu2"  # kubenode2 never had gpu2
+    assert Agent._peer_record(fake, peer, "kubenode2", forged, "host0") == []
+
+
+def test_a_deleted_waiting_pod_is_not_started_from_a_stale_snapshot():
+    """the peer poller and the config-retry tick work from a snapshot of the waiting
+    pods; one deleted meanwhile (DELETED, bookkept under the start lock) must not start -- nor
+    get its GPUs reserved again -- and a successor of the same name is not started from the old
+    pod's snapshot entry."""
+    import threading
+    import types
+
+    from tritonk8ssupervisor_amd.agent.agent import Agent
+
+    started = []
+    fake = types.SimpleNamespace(_config_wait={}, _reserved={}, _pods_meta={}, _start_lock=threading.RLock(),
+                                 runtime=types.SimpleNamespace(stop=lambda *a, **k: None),
+                                 _terminated=lambda key: None)
+    fake._start_pod_locked = lambda p: started.append(p["metadata"]["uid"])
+    old = {"metadata": {"namespace": "default", "name": "rank0", "uid": "u1"}, "spec": {}}
+    fake._config_wait["default/rank0"] = old
+    fake._reserved["default/rank0"] = (["gpu0"], {}, 0.0)
+    snapshot = list(fake._config_wait.values())     # what _poll_peers iterates over
+    Agent._handle(fake, "DELETED", old)             # the delete lands in between
+    assert fake._config_wait == {} and fake._reserved == {}
+    Agent._start_if_waiting(fake, snapshot[0])
+    assert started == []
+    new = {"metadata": {"namespace": "default", "name": "rank0", "uid": "u2"}, "spec": {}}
+    fake._config_wait["default/rank0"] = new        # a successor with the same name waits
+    Agent._start_if_waiting(fake, snapshot[0])      # the stale entry does not start it
+    assert started == []
+    Agent._start_if_waiting(fake, new)
+    assert started == ["u2"]

@@ -198,6 +198,7 @@ class Agent:
         # (published in GPU_DEVICES so the peers can find them) until the pod starts or goes away
         self._reserved: dict[str, tuple[list[str], dict, float]] = {}
         self._node_hosts: dict[str, str] = {}
+        self._node_devs: dict[str, dict[str, int]] = {}
         self._peer_poller: threading.Thread | None = None
         self._registered_pods: dict | None = None   # the node's pods as the registration returned them
         self._start_lock = threading.RLock()
@@ -329,7 +330,7 @@ class Agent:
                     body["metrics"] = self._usage_sample()
                 for key, pod in list(self._config_wait.items()):  # kubelet retries config errors
                     if key not in self.runtime.running():
-                        self._start_pod(pod)
+                        self._start_if_waiting(pod)
                 if time.monotonic() >= next_volumes:  # ConfigMap/Secret/downwardAPI changes reach running pods
                     next_volumes = time.monotonic() + volume_period
                     self._sync_volumes()
@@ -416,6 +417,19 @@ class Agent:
     def _start_pod(self, pod: dict) -> None:
         with self._start_lock:  # the pod watch and the config-retry tick both start pods
             self._start_pod_locked(pod)
+
+    def _start_if_waiting(self, pod: dict) -> None:
+        """Retry a pod taken from a snapshot of ``_config_wait`` -- only if, under the start lock,
+        it still waits there with the same uid: a pod deleted since (DELETED or a deletion
+        timestamp, also handled under the lock) must not get its GPUs reserved again and start
+        with no later event to stop it."""
+        md = pod["metadata"]
+        key = f"{md['namespace']}/{md['name']}"
+        with self._start_lock:
+            cur = self._config_wait.get(key)
+            if cur is None or cur["metadata"].get("uid") != md.get("uid"):
+                return
+            self._start_pod_locked(cur)
 
     def _start_pod_locked(self, pod: dict) -> None:
         md, spec = pod["metadata"], pod["spec"]
@@ -560,6 +574,15 @@ class Agent:
                               if peer_devs else "; no Job peer on this host")
         trace(self.name, f"start {key}: isolation probed")
         layers = self._jail_layers(pod, pp_dir, vol_dirs)
+        clash = hostpath_clashes(layers["deny"], [v["hostPath"].get("path", "") for v in spec.get("volumes") or []
+                                                  if "hostPath" in v])
+        if clash:  # the jail's most specific layer wins: such a volume would re-open what is denied
+            self._report(key, md["name"], md["namespace"], "Failed",
+                         {"reason": "HostPathDenied",
+                          "message": f"hostPath {clash[0]} is at or beneath {clash[1]}, which no pod may reach (the "
+                                     "node's state, the operator's keys and caches); whatever the namespace's level"},
+                         None)
+            return
         from .resources import gpu_local_cpus, pod_limits
 
         lim = pod_limits(pod)
@@ -567,7 +590,7 @@ class Agent:
             own = set(ordinals)
             lim.cpus = gpu_local_cpus([g.render_minor for g in mine if g.ordinal in own or not peer_devs]) or self.shape.cpus
         try:
-            limit_opts = self.enforcer.pod(key, lim, in_machine=scope != "host")
+            limit_opts = self.enforcer.pod(key, lim, in_machine=scope != "host", gpu=gpu_pod)
         except OSError as e:
             self._report(key, md["name"], md["namespace"], "Failed",
                          {"reason": "CreateContainerError", "message": f"pod cgroup: {e}"}, None)
@@ -649,6 +672,38 @@ class Agent:
             self._node_hosts[node] = (n["metadata"].get("labels") or {}).get(HOST_LABEL, f"node:{node}")
         return self._node_hosts[node]
 
+    def _node_devices(self, node: str) -> dict[str, int]:
+        """A node's GPUs as it registered them (its Node's ``status.devices``): id -> host ordinal."""
+        if node == self.name:
+            return {d.id: d.ordinal for d in self.plugin.devices_}
+        if node not in self._node_devs:
+            n = self.api.get(self.api.k8s(f"/api/v1/nodes/{node}"))
+            self._node_devs[node] = {str(d.get("id")): int(d.get("ordinal", -1))
+                                     for d in (n.get("status") or {}).get("devices") or [] if d.get("id")}
+        return self._node_devs[node]
+
+    def _peer_record(self, o: dict, node: str, published: str, host: str) -> list[dict]:
+        """A peer pod's published GPUs, each one checked before this pod may open it:
+        the record must name a GPU that the peer's node allocated to that pod (``amd.com/gpu-ids``,
+        which only that node writes: admission refuses it in pods and pod templates) and that the
+        node registered as its own; the ordinal and render minor are taken from the node's
+        registration and this host's inventory, never from the record."""
+        ann = o["metadata"].get("annotations") or {}
+        given = {x for x in (ann.get("amd.com/gpu-ids") or "").split(",") if x}
+        owned = self._node_devices(node)
+        by_ord = {g.ordinal: g for g in self.plugin.inventory.gpus}
+        out = []
+        for d in json.loads(published):
+            gid = str(d.get("id"))
+            if d.get("node") != node or gid not in given or gid not in owned or owned[gid] not in by_ord:
+                print(f"{self.name}: ignoring a gpu-devices entry of pod {o['metadata']['name']} that its node "
+                      f"{node} did not allocate to it: {d}", flush=True)
+                continue
+            ordinal = owned[gid]
+            out.append({"node": node, "id": gid, "ordinal": ordinal, "host": host,
+                        "renderMinor": getattr(by_ord[ordinal], "render_minor", -1)})
+        return out
+
     def _gather_peers(self, pod: dict, key: str, ids: list[str], alloc: dict) -> list[dict] | None:
         """The GPUs of the other live pods of this pod's Job on this host, or None while some of
         them (bound here, or not yet bound) have no GPUs yet -- for up to PEER_WAIT_S, after which
@@ -666,8 +721,8 @@ class Agent:
             self._report(key, md["name"], md["namespace"], "Pending",
                          {"reason": "ContainerCreating",
                           "message": f"waiting for the GPUs of the Job's pods on this host ({GPU_PEERS}: job)"},
-                         None, {GPU_DEVICES: md["annotations"][GPU_DEVICES]})
-        since = self._reserved[key][2]
+                         None, {**(alloc.get("annotations") or {}), GPU_DEVICES: md["annotations"][GPU_DEVICES]})
+        since = self._reserved[key][2]  # (set above: deletions pop it under the same lock)
         job = next(r for r in md.get("ownerReferences") or [] if r.get("kind") == "Job")
         devices, waiting = [], []
         try:
@@ -687,7 +742,7 @@ class Agent:
                     continue  # on another host: RCCL reaches it over the network, nothing to open
                 published = (om.get("annotations") or {}).get(GPU_DEVICES)
                 if published:  # (written by that node's agent: only its own GPUs are taken)
-                    devices += [d for d in json.loads(published) if d.get("node") == nn]
+                    devices += self._peer_record(o, nn, published, host)
                 else:
                     waiting.append(om["name"])
         except (ApiError, OSError, ValueError, KeyError) as e:
@@ -713,7 +768,7 @@ class Agent:
             if not waiting:
                 return
             for p in waiting:
-                self._start_pod(p)
+                self._start_if_waiting(p)
 
     def _jail_layers(self, pod: dict, pp_dir: Path, vol_dirs: dict) -> dict:
         """What a jailed pod may not read, may only read, and may write again beneath those
@@ -1048,14 +1103,16 @@ class Agent:
         md = pod["metadata"]
         key = f"{md['namespace']}/{md['name']}"
         if etype == "DELETED":
-            self._config_wait.pop(key, None)
-            self._reserved.pop(key, None)
-            self._pods_meta.pop(key, None)
+            with self._start_lock:  # (a waiting pod is retried under it: see _start_if_waiting)
+                self._config_wait.pop(key, None)
+                self._reserved.pop(key, None)
+                self._pods_meta.pop(key, None)
             self.runtime.stop(key, wait=False, on_done=lambda: self._terminated(key))
             return
         if md.get("deletionTimestamp"):  # graceful deletion: stop it, then confirm the delete
-            self._config_wait.pop(key, None)
-            self._reserved.pop(key, None)
+            with self._start_lock:
+                self._config_wait.pop(key, None)
+                self._reserved.pop(key, None)
             if self.runtime.is_terminating(key):
                 return  # already under way; its end confirms
             cur = self.runtime.running().get(key)
@@ -1127,7 +1184,7 @@ class Agent:
                 self.enforcer.release(key)
         for k, nxt in list(self._config_wait.items()):  # its name, its GPUs: what waited may start now
             if k not in self.runtime.running():
-                self._start_pod(nxt)
+                self._start_if_waiting(nxt)
 
     # ---- lifecycle --------------------------------------------------------------------
     def _probe_isolation(self) -> None:
@@ -1190,6 +1247,20 @@ class Agent:
 
     def _ordinal(self, dev_id: str) -> int:
         return next(d.ordinal for d in self.plugin.devices_ if d.id == dev_id)
+
+
+def hostpath_clashes(deny: list[str], volumes: list) -> tuple[str, str] | None:
+    """The first (volume, denied path) pair where a pod's volume directory is a denied path or lies
+    beneath one: in gpujail.h's layers the most specific path decides, so such a
+    read-write -- or read-only -- grant would re-open the admin token, the cluster key or other
+    pods' ServiceAccount tokens. A volume ABOVE a denied path is fine: the deny stays deeper."""
+    den = [Path(d).resolve() for d in deny]
+    for v in volumes:
+        rv = Path(v).resolve()
+        for d in den:
+            if rv == d or d in rv.parents:
+                return str(rv), str(d)
+    return None
 
 
 def host_scope_env(ordinals: list[int]) -> dict:

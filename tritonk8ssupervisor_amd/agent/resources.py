@@ -13,11 +13,20 @@ strongest mode the host allows (``Enforcer.mode``):
   its GPUs. The kernel throttles and OOM-kills; ``memory.events`` says which kill was an OOM.
 * ``cgroup1`` -- the same on writable v1 memory / cpu / cpuset hierarchies (root on a v1 host,
   e.g. inside a container): ``memory.limit_in_bytes``, ``cpu.cfs_quota_us``, ``cpuset.cpus``.
-* ``watchdog`` -- unprivileged (the GPU tier: an ordinary user, no delegation): GPU pods are
-  pinned to their GPUs' NUMA-local CPUs (``sched_setaffinity``; a pod may widen its own
-  affinity, so this is placement, not a fence), and a memory watchdog samples every pod's
-  resident set and kills a pod over its ``limits.memory`` (``OOMKilled``, exit 137, restarted
-  under its policy). CPU limits are not enforced in this mode and ``describe node`` says so.
+* ``watchdog`` -- unprivileged (the GPU tier: an ordinary user, no delegation), the agent
+  enforces the shapes from ``/proc``:
+  - ``limits.cpu``: a duty cycle over the pod's processes, as cpulimit does -- every
+    ``TICK_S`` the CPU time its processes used (``/proc/<pid>/stat`` utime+stime deltas) is
+    charged to a token bucket filled at ``limits.cpu`` cores; while the bucket is negative the
+    pod's process groups are SIGSTOPped, and SIGCONTed when it has refilled (``CpuThrottle``);
+  - ``limits.memory``: every pod's resident set is sampled, a pod over its limit is killed
+    (``OOMKilled``, exit 137, restarted under its policy); CPU pods also get a hard
+    ``RLIMIT_DATA`` backstop from the jail (``--rlimit-data``: an allocation burst between two
+    samples fails with ENOMEM instead of taking the host's memory);
+  - the machine's package (its ``cpu`` / ``memory`` shape, the reference's KVM slice): the same
+    bucket over the CPU time of ALL the machine's pods, and when their resident sets together
+    exceed the package's memory the newest pod is OOMKilled;
+  - GPU pods are pinned to their GPUs' NUMA-local CPUs (``sched_setaffinity``; placement).
 
 Processes join their cgroups and CPUs inside the pod jail before anything runs
 (``tk8s-gpujail --cgroup-procs/--cpus``, gpujail.h ``join_limits``), so no process of a pod ever
@@ -38,6 +47,120 @@ from ..utils.record import record as dataclass
 
 CFS_PERIOD_US = 100_000
 _NAME = re.compile(r"[^A-Za-z0-9_.-]")
+TICK_S = 0.05             # the watchdog's CPU duty-cycle tick
+BURST_S = 0.1             # how far ahead of its rate a pod may run (seconds of its limit)
+_HZ = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
+RLIMIT_DATA_SLACK = 256 << 20   # the backstop sits above the sampled limit: 2 x limits.memory + this
+
+
+def rlimit_data_for(memory: int) -> int:
+    """The per-process RLIMIT_DATA backstop of a CPU pod with ``limits.memory``: above the limit
+    the sampler enforces (its private writable memory includes thread stacks and arenas it has not
+    touched), well below what would take the host."""
+    return 2 * int(memory) + RLIMIT_DATA_SLACK
+
+
+def _cpu_seconds(pid: int) -> float | None:
+    """CPU time (user + system, all threads) process ``pid`` has used, from /proc/<pid>/stat."""
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as f:
+            raw = f.read()
+        rest = raw[raw.rindex(b")") + 2:].split()
+        return (int(rest[11]) + int(rest[12])) / _HZ
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+class CpuThrottle:
+    """The watchdog mode's CPU limits: token buckets filled at ``limits.cpu`` cores per pod (and
+    at the package's ``cpu`` for the machine as a whole), charged with the CPU time the pods'
+    processes used each tick; a pod whose bucket -- or whose machine's -- is negative is stopped
+    (SIGSTOP to its process groups and members) until it has refilled (SIGCONT). Over a window the
+    pod then runs ``limits.cpu`` / (its parallelism) of the time: a 250m busy loop runs one tick
+    in four."""
+
+    def __init__(self, machine_cpu: float | None = None):
+        self.machine_cpu = machine_cpu or None
+        self.balance: dict[str, float] = {}      # pod key (and "" = the machine) -> CPU seconds
+        self.last: dict[int, float] = {}          # pid -> CPU seconds at the previous tick
+        self.stopped: dict[str, tuple[list[int], list[int]]] = {}  # pod key -> (groups, pids) it stopped
+        self.exempt: set[str] = set()             # pods being terminated: never stopped again
+        self.stops = 0                            # pod stops so far (describe, tests)
+
+    @staticmethod
+    def _signal(groups, pids, sig) -> None:
+        for g in groups:
+            try:
+                os.killpg(g, sig)
+            except (ProcessLookupError, PermissionError):
+                pass
+        for p in pids:
+            try:
+                os.kill(p, sig)
+            except (ProcessLookupError, PermissionError):
+                pass
+
+    def terminating(self, key: str) -> None:
+        """Pod ``key`` is being stopped: running again at once, so its processes see SIGTERM and
+        have their grace period, and not throttled any more."""
+        self.exempt.add(key)
+        self.resume(key)
+
+    def resume(self, key: str) -> None:
+        hit = self.stopped.pop(key, None)
+        if hit is not None:
+            self._signal(hit[0], hit[1], signal.SIGCONT)
+
+    def resume_all(self) -> None:
+        for key in list(self.stopped):
+            self.resume(key)
+
+    def step(self, pods: dict[str, tuple[list[int], set[int]]], limits: dict[str, "Limits"], dt: float,
+             in_machine=lambda key: True) -> None:
+        """One tick: ``pods`` -> {key: (process groups, member pids)} of the running pods."""
+        for key in [k for k in self.stopped if k not in pods]:  # gone (or terminating): never left stopped
+            self.resume(key)
+        for key in [k for k in self.balance if k and k not in pods]:
+            del self.balance[key]
+        used: dict[str, float] = {}
+        seen: dict[int, float] = {}
+        for key, (_groups, pids) in pods.items():
+            u = 0.0
+            for pid in pids:
+                t = _cpu_seconds(pid)
+                if t is None:
+                    continue
+                seen[pid] = t
+                u += max(0.0, t - self.last.get(pid, t))
+            used[key] = u
+        self.last = seen
+        machine_neg = False
+        if self.machine_cpu:
+            u = sum(v for k, v in used.items() if in_machine(k))
+            b = min(self.balance.get("", 0.0) + self.machine_cpu * dt - u, self.machine_cpu * BURST_S)
+            self.balance[""] = b
+            machine_neg = b < 0
+        for key, (groups, pids) in pods.items():
+            if key in self.exempt:
+                continue
+            lim = limits.get(key)
+            neg = machine_neg and in_machine(key)
+            if lim is not None and lim.cpu:
+                b = min(self.balance.get(key, 0.0) + lim.cpu * dt - used[key], lim.cpu * BURST_S)
+                self.balance[key] = b
+                neg = neg or b < 0
+            if neg and key not in self.stopped:
+                self.stopped[key] = (list(groups), sorted(pids))
+                self._signal(groups, pids, signal.SIGSTOP)
+                self.stops += 1
+            elif neg:  # members that appeared since it was stopped
+                g0, p0 = self.stopped[key]
+                new = sorted(set(pids) - set(p0))
+                if new:
+                    self._signal([], new, signal.SIGSTOP)
+                    self.stopped[key] = (g0, p0 + new)
+            elif key in self.stopped:
+                self.resume(key)
 
 
 @dataclass
@@ -216,6 +339,9 @@ class Enforcer:
         self.pods: dict[str, dict[str, Path]] = {}
         self.limits: dict[str, Limits] = {}
         self.oom: set[str] = set()          # pods the watchdog killed for memory
+        self.oom_base: dict[str, int] = {}  # pod key -> the cgroup's oom_kill count when its container started
+        self.outside: set[str] = set()      # host-scoped pods: beside the machine's slice, not in it
+        self.throttle = CpuThrottle(self.machine.cpu)
         self.lock = threading.Lock()
         want = os.environ.get("TK8S_POD_RESOURCES", "auto")
         if want == "none":
@@ -242,14 +368,18 @@ class Enforcer:
         if not {"memory", "cpu"} <= have or not os.access(own / "cgroup.subtree_control", os.W_OK):
             self.why += f"cgroup2: {own} is not delegated to this user (controllers {sorted(have)}); "
             return False
-        # no internal processes: this agent (and whatever shares its cgroup) moves to a leaf first
+        # no internal processes: this agent moves to a leaf first -- and only this agent (ADVICE r4:
+        # other processes sharing the cgroup, say the other node agents of the host starting at the
+        # same moment, are not ours to move; with them there the subtree cannot be enabled)
         leaf = own / "tk8s-agent"
         leaf.mkdir(exist_ok=True)
-        for pid in (own / "cgroup.procs").read_text().split():
-            try:
-                _write(leaf / "cgroup.procs", pid)
-            except OSError:
-                pass
+        _write(leaf / "cgroup.procs", os.getpid())
+        others = [p for p in (own / "cgroup.procs").read_text().split() if p != str(os.getpid())]
+        if others and not (own / "cgroup.subtree_control").read_text().split():
+            _write(own / "cgroup.procs", os.getpid())  # back where it was
+            self.why += (f"cgroup2: {own} also holds processes that are not this agent's ({', '.join(others[:5])}); "
+                         "give each agent a delegated cgroup of its own; ")
+            return False
         ctrls = [c for c in ("memory", "cpu", "cpuset") if c in have]
         _write(own / "cgroup.subtree_control", " ".join(f"+{c}" for c in ctrls))
         _sweep(own)
@@ -331,14 +461,25 @@ class Enforcer:
         elif ctrl == "cpuset" and lim.cpus:
             _write(d / "cpuset.cpus", lim.cpus)
 
-    def pod(self, key: str, lim: Limits, in_machine: bool = True) -> list[str]:
+    def pod(self, key: str, lim: Limits, in_machine: bool = True, gpu: bool = False) -> list[str]:
         """Prepare pod ``key``: its cgroups, and the jail options that put its processes in them
         (and on its CPUs). ``in_machine=False``: a host-scoped pod (the fabric check's one
-        process over the GPUs of several machines) sits beside the machine, not inside its slice."""
+        process over the GPUs of several machines) sits beside the machine, not inside its slice.
+        ``gpu``: the pod holds GPUs (no RLIMIT_DATA backstop: the GPU runtime maps host memory
+        for its queues and buffers)."""
         with self.lock:
-            self.limits[key] = lim
+            self.limits.pop(key, None)
+            self.limits[key] = lim  # (insertion order: the newest pod last, for the machine's memory)
             self.oom.discard(key)
+            self.oom_base.pop(key, None)
+            self.throttle.exempt.discard(key)
+            if in_machine:
+                self.outside.discard(key)
+            else:
+                self.outside.add(key)
         opts: list[str] = []
+        if self.mode == "watchdog" and lim.memory and not gpu:
+            opts += ["--rlimit-data", str(rlimit_data_for(lim.memory))]
         if self.mode in ("cgroup2", "cgroup1"):
             name = "pod-" + _NAME.sub("_", key)
             dirs = {}
@@ -354,6 +495,7 @@ class Enforcer:
                 opts += ["--cgroup-procs", str(d / "cgroup.procs")]
             with self.lock:
                 self.pods[key] = dirs
+            self.reset_oom(key)  # (the baseline of a cgroup that outlived an earlier pod of this name)
         if lim.cpus and not (self.mode == "cgroup2" and (self.base[""] / "cpuset.cpus").exists()) \
                 and "cpuset" not in self.base:
             opts += ["--cpus", lim.cpus]  # no cpuset controller: affinity
@@ -365,23 +507,45 @@ class Enforcer:
             if key in self.oom:
                 return True
             dirs = self.pods.get(key) or {}
+        n = self._oom_kills(dirs)
+        if n is None:
+            return False
+        with self.lock:
+            base = self.oom_base.get(key, 0)
+        # the counters are cumulative over the cgroup's life: only a kill since this container
+        # instance started counts, not one of an earlier instance
+        if n > base:
+            return True
+        if "memory" in dirs and "" not in dirs:
+            try:
+                return int((dirs["memory"] / "memory.failcnt").read_text()) > 0
+            except (OSError, ValueError):
+                pass
+        return False
+
+    @staticmethod
+    def _oom_kills(dirs: dict) -> int | None:
+        """The pod cgroup's cumulative oom_kill count (v2 memory.events, v1 memory.oom_control)."""
         try:
             if "" in dirs:
                 ev = dict(line.split() for line in (dirs[""] / "memory.events").read_text().splitlines() if line.strip())
-                return int(ev.get("oom_kill", 0)) > 0
+                return int(ev.get("oom_kill", 0))
             if "memory" in dirs:
                 ctl = dict(line.split() for line in (dirs["memory"] / "memory.oom_control").read_text().splitlines()
                            if len(line.split()) == 2)
-                return int(ctl.get("oom_kill", 0)) > 0 or int((dirs["memory"] / "memory.failcnt").read_text()) > 0
+                return int(ctl.get("oom_kill", 0))
         except (OSError, ValueError):
             pass
-        return False
+        return None
 
     def reset_oom(self, key: str) -> None:
-        """A container restarts: the next exit is judged on its own."""
+        """A container (re)starts: its exit is judged on its own -- the oom_kill count from here on."""
         with self.lock:
             self.oom.discard(key)
             dirs = self.pods.get(key) or {}
+        n = self._oom_kills(dirs)
+        with self.lock:
+            self.oom_base[key] = n or 0
         if "memory" in dirs:  # v1 counts failures cumulatively: reset between instances
             try:
                 _write(dirs["memory"] / "memory.failcnt", 0)
@@ -393,6 +557,9 @@ class Enforcer:
             dirs = self.pods.pop(key, {})
             self.limits.pop(key, None)
             self.oom.discard(key)
+            self.oom_base.pop(key, None)
+            self.outside.discard(key)
+        self.throttle.resume(key)
         for d in dirs.values():
             try:
                 os.rmdir(d)
@@ -404,6 +571,7 @@ class Enforcer:
         (those still holding a process stay)."""
         for key in list(self.pods):
             self.release(key)
+        self.throttle.resume_all()
         for ctrl, base in self.base.items():
             try:  # leave it for the parent (v1: the agent itself; v2: its leaf) and remove it
                 if ctrl == "":
@@ -425,9 +593,13 @@ class Enforcer:
             return (f"cgroup1 ({', '.join(sorted(self.base))}): pod memory, cfs quota, cpuset; "
                     f"machine {shape or 'unbounded'}")
         if self.mode == "watchdog":
-            return ("watchdog: limits.memory by resident-set sampling (OOMKilled), GPU pods pinned to NUMA-local "
-                    "CPUs; limits.cpu and the machine shape NOT enforced (no delegated cgroup: " + self.why.strip("; ")
-                    + ")")
+            mach = ", ".join(x for x in (f"cpu {m.cpu:g} by the same duty cycle over all its pods" if m.cpu else "",
+                                          f"memory {m.memory >> 20} MiB over all its pods' resident sets (the newest "
+                                          "pod OOMKilled)" if m.memory else "") if x)
+            return ("watchdog: limits.cpu by a SIGSTOP/SIGCONT duty cycle over each pod's processes (/proc CPU-time "
+                    f"deltas every {TICK_S * 1000:.0f} ms); limits.memory by resident-set sampling (OOMKilled) with an "
+                    "RLIMIT_DATA backstop for CPU pods; machine package: " + (mach or "unbounded")
+                    + "; GPU pods pinned to NUMA-local CPUs (no delegated cgroup: " + self.why.strip("; ") + ")")
         return f"none: {self.why.strip('; ')}"
 
     # ---- the watchdog (watchdog mode) -------------------------------------------------------
@@ -450,24 +622,63 @@ class Enforcer:
             except (ProcessLookupError, PermissionError):
                 pass
 
+    def over_machine(self, rss: dict[str, int]) -> list[str]:
+        """When the machine's pods together are over its package's memory: the pods to kill, the
+        newest first, until the rest fit (host-scoped pods sit outside the slice)."""
+        if not self.machine.memory:
+            return []
+        with self.lock:
+            order = [k for k in self.limits if k in rss and k not in self.outside]
+        order += [k for k in rss if k not in order and k not in self.outside]  # (pods started before any limit)
+        total = sum(rss[k] for k in order)
+        out = []
+        while order and total > self.machine.memory:
+            k = order.pop()  # the newest
+            out.append(k)
+            total -= rss[k]
+        return out
+
     def watch(self, groups_of, stop: threading.Event, period: float = 0.5) -> None:
-        """Watchdog loop: ``groups_of()`` -> {pod key: [process group ids]}."""
+        """Watchdog loop: ``groups_of()`` -> {pod key: [process group ids]}. Every ``period`` s a
+        /proc scan finds each pod's processes and resident set (memory limits, the machine's
+        memory); every ``TICK_S`` the CPU duty cycle runs over the processes last found."""
         if self.mode != "watchdog":
             return
         from .usage import _proc_table, child_map, members
 
-        while not stop.wait(period):
-            with self.lock:
-                if not any(lim.memory for lim in self.limits.values()):
+        pods: dict[str, tuple[list[int], set[int]]] = {}
+        next_scan = last = time.monotonic()
+        try:
+            while not stop.wait(TICK_S):
+                with self.lock:
+                    limits = dict(self.limits)
+                cpu_on = any(lim.cpu for lim in limits.values()) or bool(self.machine.cpu and limits)
+                mem_on = any(lim.memory for lim in limits.values()) or bool(self.machine.memory and limits)
+                now = time.monotonic()
+                if not (cpu_on or mem_on):
+                    self.throttle.resume_all()
+                    pods, last = {}, now
                     continue
-            groups = groups_of()
-            table = _proc_table()
-            kids = child_map(table)
-            rss: dict[str, int] = {}
-            pids: dict[str, set[int]] = {}
-            for key, gs in groups.items():
-                pids[key] = set().union(*(members(table, g, kids) for g in gs)) if gs else set()
-                rss[key] = sum(table[p][2] for p in pids[key])
-            for key in self.over_limit(rss):
-                self.kill_oom(key, groups.get(key, []), sorted(pids.get(key, ())))
-                time.sleep(0)  # the runtime's wait() sees the kill; oom_killed() names it
+                if now >= next_scan:
+                    next_scan = now + period
+                    groups = groups_of()
+                    table = _proc_table()
+                    kids = child_map(table)
+                    pods, rss = {}, {}
+                    for key, gs in groups.items():
+                        ps = set().union(*(members(table, g, kids) for g in gs)) if gs else set()
+                        pods[key] = (list(gs), ps)
+                        rss[key] = sum(table[p][2] for p in ps if p in table)
+                    if mem_on:
+                        for key in dict.fromkeys(self.over_limit(rss) + self.over_machine(rss)):
+                            self.throttle.resume(key)  # (a stopped process dies of SIGKILL all the same)
+                            self.kill_oom(key, pods[key][0], sorted(pods[key][1]))
+                            pods.pop(key, None)
+                            time.sleep(0)  # the runtime's wait() sees the kill; oom_killed() names it
+                if cpu_on:
+                    self.throttle.step(pods, limits, now - last, in_machine=lambda k: k not in self.outside)
+                elif self.throttle.stopped:
+                    self.throttle.resume_all()
+                last = now
+        finally:
+            self.throttle.resume_all()

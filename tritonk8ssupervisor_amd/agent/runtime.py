@@ -347,6 +347,8 @@ class PodRuntime:
                 on_done()
             return None
         pp.stopping = True
+        if self.enforcer is not None:  # a pod the CPU duty cycle stopped runs again for its SIGTERM
+            self.enforcer.throttle.terminating(key)
         for c in (pp, *pp.sidecars):
             if c.prober is not None:
                 c.prober.stop.set()

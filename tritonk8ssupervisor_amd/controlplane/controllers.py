@@ -71,6 +71,7 @@ def _epoch(iso: str | None) -> float:
 REVISION = "deployment.kubernetes.io/revision"
 from .objects import (
     VALIDATION_LABEL, TERMINAL, _key, _cond, _set_cond, _set_ready, _xgmi_view, template_hash, labels_match, node_ready,
+    strip_owned,
 )
 
 
@@ -112,6 +113,8 @@ class Controllers:
         if node:
             spec["nodeName"] = node
         md = copy.deepcopy(template.get("metadata", {}))
+        if md.get("annotations"):  # (admission refuses them in templates; a restored old object may have them)
+            md["annotations"] = strip_owned(md["annotations"])
         md.update(name=name, namespace=ns)
         md.setdefault("labels", {}).update(labels or {})
         md.setdefault("annotations", {}).update(annotations or {})

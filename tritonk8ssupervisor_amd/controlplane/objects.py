@@ -138,7 +138,16 @@ _SCHEDULER_OWNED = ("tk8s.amd.com/host-claims", "tk8s.amd.com/host-devices")
 # an Indexed Job's pods on one host open each other's GPUs (agent.py _gather_peers): from the
 # Job's template only; the GPUs each pod was given are published by its node agent (pod status)
 GPU_PEERS = "tk8s.amd.com/gpu-peers"
-_AGENT_OWNED = ("tk8s.amd.com/gpu-devices", GPU_PEERS)
+GPU_DEVICES = "tk8s.amd.com/gpu-devices"
+_AGENT_OWNED = (GPU_DEVICES, GPU_PEERS, "amd.com/gpu-ids")
+# what a workload's pod template may never carry: the controllers copy template
+# annotations into the pods they create, so a forged record there would reach a pod unchecked
+_TEMPLATE_FORBIDDEN = (GPU_DEVICES, "amd.com/gpu-ids") + _SCHEDULER_OWNED
+
+
+def strip_owned(annotations: dict) -> dict:
+    """A pod template's annotations without the node's and the scheduler's own records."""
+    return {k: v for k, v in annotations.items() if k not in _TEMPLATE_FORBIDDEN}
 
 
 def _reserved(ann: dict) -> str | None:
@@ -190,6 +199,10 @@ def _admit_gpu_visibility(kind: str, ns: str, body: dict, cur: dict | None = Non
         if kind == "cronjobs":
             spec = (spec.get("jobTemplate") or {}).get("spec") or {}
         ann = (spec.get("template") or {}).get("metadata", {}).get("annotations") or {}
+        for k in _TEMPLATE_FORBIDDEN:
+            if k in ann:
+                raise HttpError(403, f"{kind} is forbidden: annotation {k} in a pod template: it is set "
+                                     + ("by the scheduler" if k in _SCHEDULER_OWNED else "by the pod's node"))
         what = _reserved(ann)
         if what and (kind != "jobs" or ns != "kube-system"):
             raise HttpError(403, f"{kind} is forbidden: annotation {what} is reserved for kube-system Jobs")
