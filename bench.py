@@ -331,6 +331,45 @@ def page_cache_residency(paths: list[str]) -> dict:
     return out
 
 
+def slowest_tasks(events: Path, launched_unix: float | None = None, top: int = 6) -> list[dict]:
+    """The slowest playbook tasks and provisioning steps of one bring-up (its .tk8s/events.jsonl),
+    and the CLI's own start (launch -> its first event): where a slow step's time went, kept in
+    the JSON line for the cold first run."""
+    out = []
+    try:
+        for k, line in enumerate(events.read_text().splitlines()):
+            e = json.loads(line)
+            if k == 0 and launched_unix and e.get("ts"):
+                out.append({"what": "CLI start: interpreter + imports (launch -> first event)",
+                            "s": round(e["ts"] - launched_unix, 4)})
+            if e.get("event") in ("task", "phase_end") and isinstance(e.get("seconds"), (int, float)):
+                out.append({"what": e.get("task") or f"phase {e.get('phase')}", "s": round(e["seconds"], 4)})
+    except (OSError, ValueError):
+        return []
+    return sorted(out, key=lambda x: -x["s"])[:top]
+
+
+def evict_page_cache(paths: list[str]) -> dict:
+    """Drop these files' clean pages from the page cache (posix_fadvise DONTNEED: no privilege
+    needed, nothing but the cache changes), so the next bring-up reads them from disk -- a first
+    ./setup.sh on a machine that has never run it."""
+    n, size = 0, 0
+    for p in paths:
+        try:
+            fd = os.open(p, os.O_RDONLY)
+        except OSError:
+            continue
+        try:
+            size += os.fstat(fd).st_size
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            n += 1
+        except OSError:
+            pass
+        finally:
+            os.close(fd)
+    return {"files": n, "mib": round(size / 2**20, 1)}
+
+
 def one_bringup(ws: Path, n: int, args, env: dict, log, census: KfdCensus | None = None, package: str | None = None,
                 rccl: str | None = None) -> dict:
     answers = {"nodes": n, "package": package or args.package, "name": "k8s bench", "confirm": "yes"}
@@ -399,6 +438,7 @@ def one_bringup(ws: Path, n: int, args, env: dict, log, census: KfdCensus | None
                 "post_ready_error": f"exit {rc}: " + out.strip()[-1500:]}
     summary = json.loads(out.strip().splitlines()[-1])
     summary["wall_seconds"] = wall
+    summary["launched_unix"] = launched_unix
     summary["ready_wall_seconds"] = t_ready
     summary["post_ready_seconds"] = post_ready
     hb = summary.get("host_burnin") or {}
@@ -528,6 +568,9 @@ def main(argv=None) -> int:
     ap.add_argument("--fabric-steps", type=int, default=None,
                     help="timed bring-ups with --rccl on, reported as fabric_validated_s (launch -> ./setup.sh exits "
                          "after a passing RCCL all-reduce Job); default 5 with real GPUs, 0 with fake ones")
+    ap.add_argument("--cold-evict", action="store_true",
+                    help="before the cold first run, evict every file a bring-up reads from the page cache "
+                         "(posix_fadvise DONTNEED), so it also reads them from disk")
     ap.add_argument("--settle", type=float, default=None,
                     help="pause after each teardown, outside the timed region, so the driver has released the "
                          "previous step's GPU processes (default: 1.0 s with real GPUs, 0 with fake ones)")
@@ -582,10 +625,21 @@ def main(argv=None) -> int:
                     # first ./setup.sh on a fresh install
                     step_env = dict(env, PYTHONPYCACHEPREFIX=str(root / "cold-pycache"),
                                     TK8S_YAML_CACHE=str(root / "cold-cache"))
+                    if args.cold_evict:  # ... and on a machine whose disk cache has never seen it
+                        from tritonk8ssupervisor_amd.utils.build_native import bringup_files
+
+                        files = bringup_files(env, relative=False)
+                        cold_start_state["evicted"] = evict_page_cache(files)
+                        cold_start_state["bringup_files_page_cache_after_evict"] = (
+                            page_cache_residency(files).get("_all"))
                 try:
+                    if i == 0 and args.warmup > 0:
+                        cold_start_state.update(loadavg_1m=round(os.getloadavg()[0], 2),
+                                                cpus=len(os.sched_getaffinity(0)))
                     s = one_bringup(ws, n, args, step_env, log, census)
                     if i == 0 and args.warmup > 0:
                         cold = s
+                        cold["slowest_tasks"] = slowest_tasks(ws / ".tk8s" / "events.jsonl", s.get("launched_unix"))
                 except Exception as e:  # noqa: BLE001 - reported after the collective
                     err = str(e)
             d.sync()
@@ -729,6 +783,7 @@ def main(argv=None) -> int:
             ("spawn_ms", cold.get("burnin_spawn_ms")), ("exec_ms", cold.get("burnin_exec_ms")),
             ("notice_ms", cold.get("burnin_notice_ms")))} if cold else None,
         "cold_first_run_kfd_census": cold.get("kfd_census") if cold else None,
+        "cold_first_run_slowest_tasks": cold.get("slowest_tasks") if cold else None,
         "cold_first_run_slow_start_cause": cold.get("slow_start_cause") if cold else None,
         "cold_first_run_start_state": cold_start_state or None,
         "rccl_check_s": round(sum(s.get("phases", {}).get("rccl", 0.0) for s in summaries) / len(summaries), 4)

@@ -60,8 +60,8 @@ def test_bench_single_process(tmp_path):
 
     t0 = time.monotonic()
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "2", "--warmup", "1",
-                        "--fake-gpus", "2", "--curve-steps", "2"], cwd=REPO, env=_env(tmp_path), capture_output=True,
-                       text=True, timeout=280)
+                        "--fake-gpus", "2", "--curve-steps", "2", "--plain-steps", "2", "--fabric-steps", "1"],
+                       cwd=REPO, env=_env(tmp_path), capture_output=True, text=True, timeout=280)
     run_wall = time.monotonic() - t0
     assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
     out = _json_line(p.stdout)
@@ -87,6 +87,20 @@ def test_bench_single_process(tmp_path):
     # the cold first run (empty caches) is reported next to the warm one
     assert out["cold_first_run_s"] > 0 and "empty" in out["cold_first_run_what"]
     assert isinstance(out["slow_start_cause"], dict)
+    # the cold first run explains itself -- its phases, its slowest tasks (the
+    # CLI's own start first among them), its burn-in timings, its KFD census and what it started from
+    assert "ansible" in out["cold_first_run_phases_s"] and "provision" in out["cold_first_run_phases_s"]
+    assert set(out["cold_first_run_burnin"]) == {"runtime_init_ms", "total_ms", "spawn_ms", "exec_ms", "notice_ms"}
+    assert out["cold_first_run_kfd_census"] is not None and "cold_first_run_slow_start_cause" in out
+    tasks = out["cold_first_run_slowest_tasks"]
+    assert tasks and all(t["s"] >= 0 for t in tasks) and any(t["what"].startswith("CLI start") for t in tasks)
+    st = out["cold_first_run_start_state"]
+    assert "build_pycache_files_at_start" in st and "probe_libs_page_cache_at_start" in st and st["cpus"] >= 1
+    # the plain path (TK8S_SHORTCUTS=0) on the same line
+    assert out["plain_path_s"] > 0 and out["plain_path"]["steps"] == 2 and "TK8S_SHORTCUTS=0" in out["plain_path"]["what"]
+    # launch -> a passing RCCL all-reduce Job (gloo ranks on the fake GPUs)
+    fv = out["fabric_validated"]
+    assert out["fabric_validated_s"] >= fv["ready"]["mean_s"] > 0 and fv["rccl"]["ok"] is True and fv["steps"] == 1
 
 
 @pytest.mark.timeout(400)

@@ -812,6 +812,30 @@ def test_setup_without_a_startup_shortcut_on_a_real_gpu(tmp_path, knob):
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
 
+def test_setup_on_the_plain_path_on_a_real_gpu(tmp_path):
+    """TK8S_SHORTCUTS=0 turns every start-up shortcut off at once (no preloaded
+    or early burn-in, no zygotes, no caches, interpreters with site processing): the validation
+    DaemonSet then probes the GPU itself, and the bring-up still reaches Ready, validated."""
+    import subprocess
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = _real_ws(tmp_path)
+    env["TK8S_SHORTCUTS"] = "0"
+    (tmp_path / "answers.json").write_text(json.dumps({"nodes": 1, "package": "mi355x-1gpu", "confirm": "yes"}))
+    try:
+        r = subprocess.run(["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", "0", "--timeout",
+                            "120"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        s = json.loads(r.stdout.strip().splitlines()[-1])
+        assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1, s
+        assert not s.get("host_burnin"), s.get("host_burnin")  # the plain path: no early burn-in
+        v = next(iter(s["validation"].values()))
+        assert float(v["hbm-write-gbps"]) > 1000.0 and float(v["md5-mbps"]) > 1000.0, v
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
 def test_multi_gpu_burnin_command_runs_on_one_gpu(tmp_path):
     """The host burn-in command a >= 2-GPU bring-up runs (HIP probe, --peers with the light pull
     options, earlyburn.host_burnin_command) parses and passes on the one GPU here, and its JSON is

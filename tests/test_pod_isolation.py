@@ -201,6 +201,28 @@ def test_node_tokens_reach_their_own_node_only(tmp_path):
         assert status(n1, "GET", "/api/v1/namespaces/default/pods/p1/log") == 403
         # reads a kubelet needs
         assert status(n2, "GET", "/api/v1/pods") == 200 and status(n2, "GET", "/api/v1/namespaces/default/services") == 200
+        assert status(n2, "GET", "/api/v1/nodes") == 200 and status(n2, "GET", "/api/v1/namespaces/default/endpoints") == 200
+        # ... and nothing a kubelet's system:node role does not grant: no
+        # workload specs, no RBAC, no Secret lists, no ServiceAccounts
+        k.post(k.k8s("/apis/apps/v1/namespaces/default/deployments"), {"metadata": {"name": "d"}, "spec": {
+            "replicas": 0, "selector": {"matchLabels": {"a": "d"}},
+            "template": {"metadata": {"labels": {"a": "d"}}, "spec": {"containers": [{"name": "c", "command": ["true"]}]}}}})
+        for path in ("/apis/apps/v1/namespaces/default/deployments", "/apis/apps/v1/namespaces/default/deployments/d",
+                     "/apis/apps/v1/deployments", "/apis/rbac.authorization.k8s.io/v1/namespaces/default/roles",
+                     "/apis/rbac.authorization.k8s.io/v1/namespaces/default/rolebindings",
+                     "/apis/rbac.authorization.k8s.io/v1/clusterroles", "/apis/rbac.authorization.k8s.io/v1/clusterrolebindings",
+                     "/api/v1/secrets", "/api/v1/namespaces/default/secrets", "/api/v1/namespaces/default/serviceaccounts",
+                     "/api/v1/namespaces/default/configmaps", "/apis/batch/v1/namespaces/default/jobs",
+                     "/apis/apps/v1/namespaces/default/statefulsets", "/api/v1/namespaces/default/persistentvolumeclaims"):
+            assert status(n1, "GET", path) == 403, path
+        # a PVC and the Job of a pod bound to it: yes; of another node's pod: no
+        k.post(k.k8s("/api/v1/namespaces/default/persistentvolumeclaims"), {"metadata": {"name": "data"}, "spec": {
+            "accessModes": ["ReadWriteOnce"], "resources": {"requests": {"storage": "1Gi"}}}})
+        k.post(k.k8s("/api/v1/namespaces/default/pods"), {"metadata": {"name": "p2"}, "spec": {
+            "nodeName": "kubenode2", "volumes": [{"name": "v", "persistentVolumeClaim": {"claimName": "data"}}],
+            "containers": [{"name": "c", "command": ["true"]}]}})
+        assert status(n2, "GET", "/api/v1/namespaces/default/persistentvolumeclaims/data") == 200
+        assert status(n1, "GET", "/api/v1/namespaces/default/persistentvolumeclaims/data") == 403
         # node tokens do not open the Rancher side either
         nc = Client(c.base, token=n1.token)
         with pytest.raises(ApiError) as ei:

@@ -20,6 +20,7 @@ Incremental: an output is rebuilt when any of its inputs or any header is newer.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import json
 import os
 import shutil
 import subprocess
@@ -233,6 +234,19 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     return out
 
 
+# what the CLI, the control plane and the agents import: warmed into the byte-code cache by
+# precompile_python, evicted from the page cache by bench.py --cold-evict
+BRINGUP_MODULES = [
+    "tritonk8ssupervisor_amd.cli.main", "tritonk8ssupervisor_amd.cli.kubectl", "tritonk8ssupervisor_amd.orchestrator",
+    "tritonk8ssupervisor_amd.playbook", "tritonk8ssupervisor_amd.playbook_modules", "tritonk8ssupervisor_amd.kube",
+    "tritonk8ssupervisor_amd.wizard", "tritonk8ssupervisor_amd.controlplane.server", "tritonk8ssupervisor_amd.burnin",
+    "tritonk8ssupervisor_amd.agent.agent", "tritonk8ssupervisor_amd.ops.fakeprobe", "yaml", "argparse", "asyncio",
+    "tritonk8ssupervisor_amd.controlplane.client", "tritonk8ssupervisor_amd.controlplane.ingress",
+    "tritonk8ssupervisor_amd.controlplane.dns", "tritonk8ssupervisor_amd.utils.k8senv",
+    "tritonk8ssupervisor_amd.earlyburn", "tritonk8ssupervisor_amd.provider.hostreg",
+    "tritonk8ssupervisor_amd.parallel.dist_allreduce"]
+
+
 def precompile_python() -> None:
     """Byte-compile the package with source-HASH-checked .pyc files.
 
@@ -257,17 +271,57 @@ def precompile_python() -> None:
     # the control plane and the agents import, stdlib and PyYAML included.
     env = dict(os.environ)
     env["PYTHONPATH"] = os.pathsep.join([str(REPO)] + [p for p in env.get("PYTHONPATH", "").split(os.pathsep) if p])
-    mods = ["tritonk8ssupervisor_amd.cli.main", "tritonk8ssupervisor_amd.cli.kubectl", "tritonk8ssupervisor_amd.orchestrator",
-            "tritonk8ssupervisor_amd.playbook", "tritonk8ssupervisor_amd.playbook_modules", "tritonk8ssupervisor_amd.kube",
-            "tritonk8ssupervisor_amd.wizard", "tritonk8ssupervisor_amd.controlplane.server", "tritonk8ssupervisor_amd.burnin",
-            "tritonk8ssupervisor_amd.agent.agent", "tritonk8ssupervisor_amd.ops.fakeprobe", "yaml", "argparse", "asyncio",
-            "tritonk8ssupervisor_amd.controlplane.client", "tritonk8ssupervisor_amd.controlplane.ingress",
-            "tritonk8ssupervisor_amd.controlplane.dns", "tritonk8ssupervisor_amd.utils.k8senv",
-            "tritonk8ssupervisor_amd.earlyburn", "tritonk8ssupervisor_amd.provider.hostreg",
-            "tritonk8ssupervisor_amd.parallel.dist_allreduce"]
+    mods = BRINGUP_MODULES
     code = "import importlib\nfor m in %r:\n    importlib.import_module(m)\n" % (mods[:-1] + ["tritonk8ssupervisor_amd.provision"],)
     for flag in (["-S"], []):
         subprocess.run([sys.executable, *flag, "-c", code], env=env, cwd=str(REPO), capture_output=True, timeout=120)
+
+
+def _probe_libraries() -> list[str]:
+    """The shared libraries the GPU burn-in (tk8s-hsaprobe) maps, as the dynamic loader resolves them."""
+    try:
+        out = subprocess.run(["ldd", str(tool_path("tk8s-hsaprobe"))], capture_output=True, text=True, timeout=10).stdout
+    except (OSError, subprocess.SubprocessError):
+        return []
+    return [parts[1].split("(")[0].strip() for parts in (line.split("=>") for line in out.splitlines())
+            if len(parts) == 2 and parts[1].strip().startswith("/")]
+
+
+def bringup_files(env: dict | None = None, relative: bool = True) -> list[str]:
+    """Every file a bring-up's processes read from disk, in about the order they read them: the
+    interpreter and its shared library, the stdlib and third-party modules the CLI, the control
+    plane and the agents import (asked of a child interpreter: import order), the tk8s package,
+    its playbook / manifest / Terraform files and native tools, the shared libraries the GPU
+    burn-in maps (bench.py --cold-evict). Paths under the tree are relative to it (``relative``)."""
+    import sysconfig
+
+    code = ("import importlib, json, sys\nfor m in %r:\n    importlib.import_module(m)\n"
+            "print(json.dumps([getattr(m, '__file__', None) or '' for m in list(sys.modules.values())]))"
+            % (BRINGUP_MODULES,))
+    files: list[str] = [os.path.realpath(sys.executable)]
+    lib = sysconfig.get_config_var("INSTSONAME")
+    if lib:
+        files.append(os.path.join(sysconfig.get_config_var("LIBDIR") or "/usr/lib", lib))
+    try:
+        out = subprocess.run([sys.executable, "-S", "-c", code], env=env, cwd=str(REPO), capture_output=True,
+                             text=True, timeout=120)
+        files += [f for f in json.loads(out.stdout.strip().splitlines()[-1]) if f]
+    except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+        pass
+    for sub in ("tritonk8ssupervisor_amd", "ansible", "terraform", "manifests"):
+        for dirpath, dirnames, names in os.walk(REPO / sub):
+            dirnames[:] = sorted(d for d in dirnames if d != "__pycache__")
+            files += [os.path.join(dirpath, f) for f in sorted(names)]
+    files += _probe_libraries()
+    out_list, seen = [], set()
+    for f in files:
+        real = os.path.realpath(f)
+        if real in seen or not os.path.isfile(real):
+            continue
+        seen.add(real)
+        rel = os.path.relpath(real, REPO)
+        out_list.append(rel if relative and not rel.startswith("..") else real)
+    return out_list
 
 
 def main(argv: list[str] | None = None) -> int:
