@@ -270,8 +270,40 @@ def test_setup_with_grpc_device_plugin_and_rccl_on_a_real_gpu(tmp_path):
         assert s["gpus_allocatable"] == 1 and s["nodes_validated"] == 1 and s["rccl"]["ok"]
         log = (tmp_path / ".tk8s" / "machines" / "kubenode1" / "logs" / "agent.log").read_text()
         assert "via gRPC v1beta1" in log, log[-2000:]
+        # the rank used RCCL with its device code unpacked (utils/rccl_unpack.py): no 5.3 GB inflation
+        assert s["rccl"]["rccl_library"] == "unpacked", s["rccl"]
+        assert s["rccl"]["comm_init_ms_max"] < 1500, s["rccl"]
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+def test_unpacked_rccl_starts_faster_on_a_real_gpu(native_build):
+    """RCCL with its gfx950 device code unpacked once (utils/rccl_unpack.py)
+    loads, all-reduces exactly, and starts its communicator without inflating the 5.3 GB bundle:
+    well under the installed library's ~1.8 s."""
+    import os
+    import subprocess
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.utils.rccl_unpack import library_dir
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    lib = library_dir()
+    assert lib is not None, native_build.get("rccl-unpacked")
+    tool = Path(__file__).resolve().parents[1] / "tritonk8ssupervisor_amd" / "bin" / "tk8s-rccl"
+    args = [str(tool), "--ngpus", "1", "--max-bytes", str(1 << 20), "--iters", "3", "--warmup", "1"]
+    out = {}
+    for name, extra in (("installed", {}), ("unpacked", {"LD_LIBRARY_PATH": str(lib)})):
+        r = subprocess.run(args, capture_output=True, text=True, timeout=120, env={**os.environ, **extra})
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        out[name] = json.loads(r.stdout.strip().splitlines()[-1])
+        out[name]["path"] = next((ln.split(":", 1)[1].strip() for ln in r.stdout.splitlines()
+                                  if ln.startswith("Librccl path")), "")
+    assert out["unpacked"]["ok"] and all(x["bad"] == 0 for x in out["unpacked"]["results"])
+    assert out["unpacked"]["path"].startswith(str(lib)), out["unpacked"]["path"]
+    assert out["unpacked"]["comm_init_ms"] < 1000.0 < out["installed"]["comm_init_ms"], \
+        (out["unpacked"]["comm_init_ms"], out["installed"]["comm_init_ms"])
 
 
 def test_setup_with_host_burnin_on_a_real_gpu(tmp_path):

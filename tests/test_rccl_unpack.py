@@ -1,0 +1,95 @@
+"""RCCL's gfx950 device code unpacked once per host (utils/rccl_unpack.py).
+
+The copy must be the installed library byte for byte outside its .hip_fatbin section, and that
+section must hold an uncompressed offload bundle with exactly the host and gfx950 entries, the
+gfx950 entry an AMDGPU code object without DWARF. A copy that is missing or keyed to another
+library is not used (the installed one is). On the MI355X the ranks load it and pass
+(tests/test_kernels_gpu.py::test_unpacked_rccl_starts_faster_on_a_real_gpu)."""
+from __future__ import annotations
+
+import json
+import struct
+from pathlib import Path
+
+import pytest
+
+from tritonk8ssupervisor_amd.utils import rccl_unpack as ru
+
+pytestmark = pytest.mark.skipif(ru.installed_library() is None, reason="no librccl under ROCm")
+
+
+def _bundle_entries(f, off: int) -> list[tuple[int, int, str]]:
+    f.seek(off)
+    head = f.read(32)
+    assert head[:24] == b"__CLANG_OFFLOAD_BUNDLE__", head[:24]
+    n, = struct.unpack("<Q", head[24:32])
+    out = []
+    for _ in range(n):
+        o, s, tl = struct.unpack("<QQQ", f.read(24))
+        out.append((o, s, f.read(tl).decode()))
+    return out
+
+
+def _section_names(f, base: int) -> list[str]:
+    f.seek(base)
+    eh = f.read(64)
+    assert eh[:4] == b"\x7fELF" and struct.unpack_from("<H", eh, 0x12)[0] == 0xE0  # EM_AMDGPU
+    shoff, = struct.unpack_from("<Q", eh, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", eh, 0x3A)
+    f.seek(base + shoff)
+    table = f.read(shentsize * shnum)
+    sh = [struct.unpack_from("<IIQQQQIIQQ", table, i * shentsize) for i in range(shnum)]
+    f.seek(base + sh[shstrndx][4])
+    names = f.read(sh[shstrndx][5])
+    return [names[s[0]:names.index(b"\0", s[0])].decode() for s in sh]
+
+
+@pytest.mark.timeout(600)
+def test_the_unpacked_copy_differs_only_in_its_device_code():
+    res = ru.unpack()
+    if not res["ok"]:
+        pytest.skip(res["why"])
+    src, dst = ru.installed_library(), ru.OUT / ru.LIB_NAME
+    assert ru.library_dir() == ru.OUT
+    off, size = ru.elf_section(src, ".hip_fatbin")
+    assert ru.elf_section(dst, ".hip_fatbin") == (off, size)
+    assert dst.stat().st_size == src.stat().st_size
+    with open(src, "rb") as a, open(dst, "rb") as b:
+        assert a.read(off) == b.read(off)  # headers, tables, host code before the section
+        for pos in range(off + size, src.stat().st_size, 8 << 20):  # everything after it
+            a.seek(pos)
+            b.seek(pos)
+            assert a.read(8 << 20) == b.read(8 << 20), pos
+        a.seek(off)
+        assert a.read(4) == b"CCOB"  # the installed one: compressed, every target
+        entries = _bundle_entries(b, off)
+        assert sorted(t for _, _, t in entries) == sorted([ru.HOST_TRIPLE, ru.TRIPLE])
+        o, s, _ = next(e for e in entries if e[2] == ru.TRIPLE)
+        assert o % 4096 == 0 and 0 < o + s <= size and s > (16 << 20)
+        names = _section_names(b, off + o)
+        assert ".text" in names and not any(n.startswith(".debug") for n in names)
+        b.seek(off + o + s)  # zero padding to the end of the section
+        assert b.read(min(1 << 20, size - o - s)).count(0) == min(1 << 20, size - o - s)
+    assert json.loads((ru.OUT / "stamp.json").read_text())["source"] == str(src)
+    assert ru.unpack()["changed"] is False  # current: nothing to redo
+
+
+def test_a_stale_or_disabled_copy_is_not_used(monkeypatch, tmp_path):
+    monkeypatch.setattr(ru, "OUT", tmp_path)
+    assert ru.library_dir() is None  # none made here
+    (tmp_path / ru.LIB_NAME).write_bytes(b"x")
+    src = ru.installed_library()
+    stamp = ru._stamp(src)
+    (tmp_path / "stamp.json").write_text(json.dumps(stamp))
+    assert ru.library_dir() == tmp_path
+    (tmp_path / "stamp.json").write_text(json.dumps({**stamp, "size": stamp["size"] + 1}))  # RCCL was upgraded
+    assert ru.library_dir() is None
+    (tmp_path / "stamp.json").write_text(json.dumps(stamp))
+    monkeypatch.setenv("TK8S_RCCL_UNPACKED", "0")
+    assert ru.library_dir() is None
+
+
+def test_elf_section_reader(tmp_path):
+    assert ru.elf_section(Path("/bin/sh").resolve(), ".text") is not None
+    (tmp_path / "x").write_bytes(b"not an elf" * 10)
+    assert ru.elf_section(tmp_path / "x", ".text") is None

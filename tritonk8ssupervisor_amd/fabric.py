@@ -100,6 +100,16 @@ class FabricCheck:
         objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
                               {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd,
                                "gpu_scope": layout["scope"]})
+        rccl_lib = None
+        if not os.environ.get("TK8S_FAKE_GPUS"):
+            from .utils.rccl_unpack import library_dir
+
+            # RCCL with its gfx950 device code unpacked once per host (utils/rccl_unpack.py): no
+            # 5.3 GB inflation in every rank's communicator start; the installed one otherwise
+            rccl_lib = library_dir()
+            if rccl_lib is not None:
+                c0 = objs[0]["spec"]["template"]["spec"]["containers"][0]
+                c0.setdefault("env", []).append({"name": "LD_LIBRARY_PATH", "value": str(rccl_lib)})
         if prof_dir is not None:  # the ranks write their traces there: a hostPath volume, which the pod jail allows
             pspec = objs[0]["spec"]["template"]["spec"]
             pspec["volumes"] = [{"name": "rocprof", "hostPath": {"path": str(prof_dir), "type": "DirectoryOrCreate"}}]
@@ -118,7 +128,7 @@ class FabricCheck:
         ok = j["status"].get("succeeded", 0) >= npods and all(r.get("ok") for r in results)
         first = next((r for r in results if r), {})
         rep = {"job": job, "ok": ok, "nranks": g, "pods": npods, "gpus_per_pod": per_pod, "scope": layout["scope"],
-               "peak_busbw_gbps": peak,
+               "peak_busbw_gbps": peak, "rccl_library": "unpacked" if rccl_lib is not None else "installed",
                "tuning": {k: first.get(k) for k in ("nccl_algo", "nccl_proto", "nccl_min_nchannels",
                                                     "nccl_max_nchannels", "peak_links_equivalent") if k in first},
                "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),

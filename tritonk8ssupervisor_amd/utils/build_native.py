@@ -99,11 +99,23 @@ def _stale(out: Path, inputs: list[Path]) -> bool:
 
 
 def _run(cmd: list[str], verbose: bool) -> None:
+    """Run one compiler/linker command. Its ``-o`` output is written beside the target and renamed
+    over it: a process executing or mapping the old file (a test, a running bring-up) never sees a
+    half-written one."""
+    out = cmd[cmd.index("-o") + 1] if "-o" in cmd[:-1] else None
+    tmp = f"{out}.tmp{os.getpid()}" if out else None
+    if tmp:
+        cmd = list(cmd)
+        cmd[cmd.index("-o") + 1] = tmp
     if verbose:
         print("+", " ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
+        if tmp and os.path.exists(tmp):
+            os.unlink(tmp)
         raise RuntimeError(f"native build failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    if tmp:
+        os.replace(tmp, out)
 
 
 def _pybind_includes() -> list[str]:
@@ -227,9 +239,16 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
               f"-Wl,-rpath,{ROCM / 'lib'}", "-Wl,--export-dynamic-symbol=opendir", "-ldl", "-lpthread"], verbose)  # cachewalk.h
 
     precompile_python()
+    from .rccl_unpack import unpack
+
+    try:  # RCCL's gfx950 device code unpacked once per host (the fabric check's communicator start)
+        rccl_unpacked = unpack(verbose=verbose)
+    except (OSError, subprocess.SubprocessError, ValueError) as e:  # the installed library stays usable
+        rccl_unpacked = {"ok": False, "why": str(e)}
     out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,
            "tk8s-gpujail": jail, "tk8s-container": tool_path("tk8s-container"),
-           "tk8s-smi": smi, "tk8s-reuse": reuse_bin, "tk8s-hsaprobe": hsa_bin, **cos}
+           "tk8s-smi": smi, "tk8s-reuse": reuse_bin, "tk8s-hsaprobe": hsa_bin, **cos,
+           "rccl-unpacked": rccl_unpacked.get("path") or f"no ({rccl_unpacked.get('why')})"}
     out.update({n: tool_path(n) for n in TOOLS})
     return out
 
