@@ -32,6 +32,10 @@ struct AllReduceConfig {
   int warmup = 5;        // untimed iterations per size
   DType dtype = DType::kF32;
   bool check = true;     // run the N6 checker on the result of each size
+  // free the communicators, streams and buffers before returning: a process that exits right
+  // after (tk8s-rccl) skips it -- the driver reclaims all of it at exit, and ncclCommDestroy plus
+  // the runtime's teardown were ~0.18 s of the fabric check's rank
+  bool teardown = true;
 };
 
 std::string nccl_unique_id_hex(const ncclUniqueId& id);

@@ -68,6 +68,7 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
   const size_t es = elem_size(cfg.dtype);
   const auto sizes = sweep_sizes(cfg, cfg.dtype);
   const size_t maxb = sizes.back();
+  const auto t_buf = std::chrono::steady_clock::now();
   for (auto& r : ranks) {
     TK8S_HIP_CHECK(hipSetDevice(r.device));
     r.send = std::make_unique<DeviceBuffer>(maxb);
@@ -86,6 +87,8 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
     TK8S_NCCL_CHECK(ncclGroupEnd());
   };
 
+  for (auto& r : ranks) TK8S_HIP_CHECK(hipStreamSynchronize(r.stream));
+  const auto t_sweep = std::chrono::steady_clock::now();
   std::vector<std::string> rows;
   double peak_bus = 0.0;
   bool all_ok = true;
@@ -147,6 +150,8 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
     return std::string(v && *v ? v : "auto");
   };
   constexpr double kXgmiLinkGBps = 153.0;
+  const auto t_end = std::chrono::steady_clock::now();
+  auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   return Json()
       .kv("ok", all_ok)
       .kv("mode", mode)
@@ -165,6 +170,8 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
       .kv("peak_busbw_gbps", peak_bus)
       .kv("comm_init_ms", init_ms)
       .kv("init_done_unix_ms", init_done)
+      .kv("buffers_ms", ms(t_buf, t_sweep))  // allocation + pattern fill of the largest size
+      .kv("sweep_ms", ms(t_sweep, t_end))     // every size: warm-up, timed iterations, exact check
       .raw("results", Json::array(rows))
       .str();
 }
@@ -237,7 +244,7 @@ std::string allreduce_single_process(const std::vector<int>& devices, const AllR
       TK8S_HIP_CHECK(hipStreamCreateWithFlags(&ranks[i].stream, hipStreamNonBlocking));
     }
     std::string out = run_sweep(ranks, static_cast<int>(devices.size()), cfg, "single_process", init_ms, init_done);
-    release(ranks);
+    if (cfg.teardown) release(ranks);
     return out;
   } catch (const std::exception& ex) {
     release(ranks);
@@ -272,7 +279,7 @@ std::string allreduce_rank_group(int first_rank, int nranks, const std::vector<i
     const double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     std::string out = run_sweep(ranks, nranks, cfg, ranks.size() > 1 ? "rank_group" : "multi_process", init_ms,
                                 unix_ms());
-    release(ranks);
+    if (cfg.teardown) release(ranks);
     return out;
   } catch (const std::exception& ex) {
     release(ranks);

@@ -8,6 +8,7 @@
 //   The process holding rank 0 creates the RCCL unique id and publishes it (atomic file rename,
 //   or HTTP PUT to the control-plane KV); the others wait for it (file poll, or HTTP long-poll).
 // Sweep: --min-bytes B --max-bytes B --factor F --iters K --warmup W --dtype float32|bfloat16
+// [--teardown]: free the communicators before exiting (default: print the result and _Exit)
 // Prints one JSON object; exit 0 iff every size reduced exactly.
 #include <chrono>
 #include <cstdlib>
@@ -81,9 +82,19 @@ std::vector<int> parse_devices(const std::string& s) {
   return out;
 }
 
+// TK8S_TRACE=1: "TRACE <unix s> rccl <what>" on stderr, merged into the bring-up's timeline by
+// scripts/trace_bringup.py (the same format as utils/trace.py)
+void trace(const char* what) {
+  static const bool on = std::getenv("TK8S_TRACE") != nullptr;
+  if (!on) return;
+  const double t = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+  std::fprintf(stderr, "TRACE %.6f rccl %s\n", t, what);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
+  trace("main");
   tk8s::cachewalk::configure();  // before the HIP runtime starts (cachewalk.h)
   try {
     tk8s::Args a(argc, argv);
@@ -95,6 +106,7 @@ int main(int argc, char** argv) {
     cfg.warmup = static_cast<int>(a.num("warmup", 5));
     cfg.dtype = a.str("dtype", "float32") == "bfloat16" ? tk8s::DType::kBF16 : tk8s::DType::kF32;
     cfg.check = !a.has("no-check");
+    cfg.teardown = a.has("teardown");  // the process exits right after its JSON line (see below)
     std::string out;
     if (a.has("rank") || a.has("group-index")) {
       const int nranks = static_cast<int>(a.num("nranks", 1));
@@ -112,7 +124,13 @@ int main(int argc, char** argv) {
       }
       ncclUniqueId id;
       std::string hex;
+      {
+        int n = 0;  // the runtime's start, on its own (RCCL would start it inside ncclGetUniqueId)
+        (void)hipGetDeviceCount(&n);
+        trace("hip runtime up");
+      }
       if (first == 0) {
+        trace("ncclGetUniqueId");
         if (ncclGetUniqueId(&id) != ncclSuccess) {
           std::fprintf(stderr, "tk8s-rccl: ncclGetUniqueId failed\n");
           return 2;
@@ -129,7 +147,9 @@ int main(int argc, char** argv) {
           return 2;
         }
       }
+      trace(first == 0 ? "unique id published" : "unique id fetched");
       out = tk8s::allreduce_rank_group(first, nranks, devices, id, cfg);
+      trace("sweep done");
     } else {
       int n = 0;
       if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
@@ -142,7 +162,14 @@ int main(int argc, char** argv) {
       out = tk8s::allreduce_single_process(devs, cfg);
     }
     std::printf("%s\n", out.c_str());
-    return out.find("\"ok\":true") != std::string::npos ? 0 : 1;
+    const int rc = out.find("\"ok\":true") != std::string::npos ? 0 : 1;
+    if (!cfg.teardown) {  // the result is out: leave without the communicators' and runtime's teardown
+      std::fflush(stdout);
+      std::fflush(stderr);
+      trace("exit");
+      std::_Exit(rc);
+    }
+    return rc;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "tk8s-rccl: %s\n", e.what());
     return 2;

@@ -23,7 +23,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 
-def one(root: Path, nodes: int, package: str = "mi355x-1gpu") -> list[tuple[float, str, str]]:
+def one(root: Path, nodes: int, package: str = "mi355x-1gpu", rccl: str = "off") -> list[tuple[float, str, str]]:
     from tritonk8ssupervisor_amd.orchestrator import init_workspace
 
     init_workspace(root)
@@ -33,7 +33,7 @@ def one(root: Path, nodes: int, package: str = "mi355x-1gpu") -> list[tuple[floa
     env = dict(os.environ, PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_TRACE="1",
                TK8S_HOST_REGISTRY=str(root / "hostreg"))
     t0 = time.time()
-    p = subprocess.run(["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", "0", "--rccl", "off"],
+    p = subprocess.run(["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", "0", "--rccl", rccl],
                        cwd=root, env=env, capture_output=True, text=True, timeout=300)
     out: list[tuple[float, str, str]] = [(0.0, "launcher", "./setup.sh launched")]
     for line in p.stdout.splitlines():
@@ -65,13 +65,14 @@ def main() -> int:
     ap.add_argument("--runs", type=int, default=3)
     ap.add_argument("--nodes", type=int, default=1)
     ap.add_argument("--package", default="mi355x-1gpu", help="cpu-only: BASELINE configs[1]'s workers")
+    ap.add_argument("--rccl", default="off", help="on: also time the post-Ready RCCL fabric Job")
     ap.add_argument("--out")
     a = ap.parse_args()
     runs = []
     for i in range(a.runs):
         root = Path(tempfile.mkdtemp(prefix="tk8s-trace-"))
         try:
-            tl = one(root, a.nodes, a.package)
+            tl = one(root, a.nodes, a.package, a.rccl)
         finally:
             shutil.rmtree(root, ignore_errors=True)
         runs.append([{"ms": round(t, 2), "where": w, "what": x} for t, w, x in tl])

@@ -93,3 +93,21 @@ def test_elf_section_reader(tmp_path):
     assert ru.elf_section(Path("/bin/sh").resolve(), ".text") is not None
     (tmp_path / "x").write_bytes(b"not an elf" * 10)
     assert ru.elf_section(tmp_path / "x", ".text") is None
+
+
+def test_transport_report_of_a_one_rank_log(tmp_path):
+    """a 1-rank communicator connects no channel, but its INFO log is there
+    -- the report says it was logged, that init completed, and which library the rank loaded."""
+    from tritonk8ssupervisor_amd.fabric import rccl_transports
+
+    one = tmp_path / "rank0.log"
+    one.write_text("host:1:1 [0] NCCL INFO ROCr version 1.18\nLibrccl path : /x/build/rccl-gfx950/librccl.so.1\n"
+                   "host:1:1 [0] NCCL INFO comm 0x1 rank 0 nranks 1 cudaDev 0 busId 5000 - Init COMPLETE\n")
+    r = rccl_transports([str(one)])
+    assert r["logged"] and r["init_complete"] and r["p2p"] == 0 and r["library"].endswith("rccl-gfx950/librccl.so.1")
+    two = tmp_path / "rank1.log"
+    two.write_text("host:1:1 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC\n")
+    r = rccl_transports([str(one), str(two), None])
+    assert r["p2p"] == 1 and r["logged"]
+    assert rccl_transports([str(tmp_path / "none.log")]) == {"p2p": 0, "shm": 0, "net": 0, "collnet": 0,
+                                                              "logged": False, "init_complete": False, "library": None}

@@ -647,7 +647,8 @@ class Enforcer:
         from .usage import _proc_table, child_map, members
 
         pods: dict[str, tuple[list[int], set[int]]] = {}
-        next_scan = last = time.monotonic()
+        last = time.monotonic()
+        next_scan = last + period  # (never a /proc scan in the agent right as its first pod starts)
         try:
             while not stop.wait(TICK_S):
                 with self.lock:
@@ -657,7 +658,7 @@ class Enforcer:
                 now = time.monotonic()
                 if not (cpu_on or mem_on):
                     self.throttle.resume_all()
-                    pods, last = {}, now
+                    pods, last, next_scan = {}, now, now + period
                     continue
                 if now >= next_scan:
                     next_scan = now + period

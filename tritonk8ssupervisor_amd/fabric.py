@@ -137,6 +137,7 @@ class FabricCheck:
         if done:  # how unevenly the ranks' runtimes + communicators came up
             rep["init_spread_ms"] = round(max(done) - min(done), 3)
             rep["comm_init_ms_max"] = round(max(r.get("comm_init_ms", 0.0) for r in results), 3)
+            rep["sweep_ms_max"] = round(max(r.get("sweep_ms", 0.0) for r in results), 3)
         rep["transport"] = rccl_transports([(p.get("metadata", {}).get("annotations") or {}).get("tk8s.amd.com/log-path")
                                             for p in pods])
         if prof_dir is not None:
@@ -153,7 +154,8 @@ def rccl_transports(log_paths: list) -> dict:
     import re
 
     counts = {"p2p": 0, "shm": 0, "net": 0, "collnet": 0}
-    seen = False
+    seen = complete = False
+    lib = None
     for p in log_paths:
         try:
             text = Path(p).read_text(errors="replace") if p else ""
@@ -161,8 +163,13 @@ def rccl_transports(log_paths: list) -> dict:
             continue
         for m in re.finditer(r" via (P2P|SHM|NET|COLLNET)\b", text):
             counts[m.group(1).lower()] += 1
-            seen = True
-    counts["logged"] = seen  # False: NCCL_DEBUG=INFO was not set, nothing to judge
+        seen |= "NCCL INFO" in text
+        complete |= "Init COMPLETE" in text
+        m = re.search(r"Librccl path\s*:\s*(\S+)", text)
+        lib = lib or (m.group(1) if m else None)
+    # logged: RCCL's INFO log was there to judge (NCCL_DEBUG=INFO); a 1-rank communicator logs
+    # its init but connects no channel, so its counts stay 0 with logged true
+    counts.update(logged=seen, init_complete=complete, library=lib)
     return counts
 
 
