@@ -445,3 +445,27 @@ def test_a_watchdog_pod_over_its_cpu_limit_is_throttled_in_a_cluster(tmp_path, f
         assert used <= 0.35 * 5.0 + 0.2, out  # (+ the interpreter's start, before the first scan saw it)
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=ws, env=env, capture_output=True, timeout=120)
+
+
+def test_signals_go_only_to_the_processes_the_scan_saw():
+    """A pid (or process group id) reused since the watchdog's last /proc scan is never signalled:
+    the recorded start time must still match."""
+    import signal as _signal
+
+    from tritonk8ssupervisor_amd.agent.resources import signal_ids
+    from tritonk8ssupervisor_amd.utils.procs import proc_start_ticks
+
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"], start_new_session=True)
+    try:
+        real = proc_start_ticks(p.pid)
+        signal_ids([p.pid], [p.pid], _signal.SIGKILL, {p.pid: real + 1})  # "another process" with this pid
+        time.sleep(0.2)
+        assert p.poll() is None
+        signal_ids([], [p.pid], _signal.SIGKILL, {})  # no record: left alone
+        time.sleep(0.2)
+        assert p.poll() is None
+        signal_ids([p.pid], [], _signal.SIGKILL, {p.pid: real})
+        assert p.wait(10) == -9
+    finally:
+        if p.poll() is None:
+            p.kill()

@@ -16,8 +16,9 @@ _PAGE = os.sysconf("SC_PAGE_SIZE") if hasattr(os, "sysconf") else 4096
 
 
 def _proc_table() -> dict[int, tuple[int, int, int, int, int]]:
-    """pid -> (process group, cpu ticks, resident bytes, parent pid, session) for every readable
-    process."""
+    """pid -> (process group, cpu ticks, resident bytes, parent pid, session, start time in clock
+    ticks since boot) for every readable process: with its start time a pid names one process
+    even after the pid is reused."""
     out = {}
     for d in os.listdir("/proc"):
         if not d.isdigit():
@@ -28,7 +29,7 @@ def _proc_table() -> dict[int, tuple[int, int, int, int, int]]:
             rest = raw[raw.rindex(")") + 2:].split()
             # fields after "(comm)": state ppid pgrp session ... utime(14) stime(15) ... rss(24)
             out[int(d)] = (int(rest[2]), int(rest[11]) + int(rest[12]), int(rest[21]) * _PAGE, int(rest[1]),
-                           int(rest[3]))
+                           int(rest[3]), int(rest[19]))
         except (OSError, ValueError, IndexError):
             continue
     return out
