@@ -101,9 +101,9 @@ class FabricCheck:
                               {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd,
                                "gpu_scope": layout["scope"]})
         c0 = objs[0]["spec"]["template"]["spec"]["containers"][0]
-        for k in ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS"):  # (pods get an env allowlist: pass RCCL's logging on)
-            if os.environ.get(k):
-                c0.setdefault("env", []).append({"name": k, "value": os.environ[k]})
+        for var in ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS"):  # (pods get an env allowlist: pass RCCL's logging on)
+            if os.environ.get(var):
+                c0.setdefault("env", []).append({"name": var, "value": os.environ[var]})
         rccl_lib = None
         if not os.environ.get("TK8S_FAKE_GPUS"):
             from .utils.rccl_unpack import library_dir
