@@ -194,8 +194,9 @@ class Authentication:
 
         * a ServiceAccount token: its own environment and namespace (``?namespace=`` may only
           repeat it), so a pod reaches its own namespace's keys and nothing else;
-        * a node token: its environment, ``?namespace=`` (default ``default``), and only a
-          namespace that has a pod bound to the node that is not finished;
+        * a node token: none -- the keys are the workloads' rendezvous (RCCL unique ids, torch
+          addresses), which no kubelet reads or writes, and the pods of one namespace run on many
+          nodes, so a node could not be held to its own pods' keys by namespace;
         * an environment's API token: its environment, any namespace; the server admin token:
           ``?project=`` (default: the oldest environment), any namespace."""
         if not key or len(key) > 512 or "\0" in key:
@@ -210,11 +211,8 @@ class Authentication:
             return f"{hit[1]}/{hit[2]}/{key}"
         ns = ns or "default"
         if hit[0] == "node":
-            live = [o for o in self._node_pods(hit[2], hit[1], ns)
-                    if (o.get("status") or {}).get("phase") not in ("Succeeded", "Failed")]
-            if not live:
-                raise HttpError(403, f"node {hit[2]} has no pod in namespace {ns}")
-            return f"{hit[1]}/{ns}/{key}"
+            raise HttpError(403, f"node {hit[2]}: the KV store holds the workloads' rendezvous keys, "
+                                 "which nodes have no access to")
         try:
             pid = self._caller_project(req, req.q("project"))["id"]
         except HttpError as e:
