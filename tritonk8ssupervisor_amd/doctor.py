@@ -54,6 +54,13 @@ def common_checks() -> list[dict]:
     out.append(_check("native build", FAIL if "tk8s-supervise" in missing or "tk8s-probe" in missing
                       else (WARN if missing else OK),
                       "all tools built" if not missing else f"missing {', '.join(missing)} (python3 __graft_entry__.py build)"))
+    from .utils.rccl_unpack import OUT, installed_library, library_dir
+
+    src = installed_library()
+    if src is not None:  # the fabric check's communicator start: 0.4 s unpacked, 1.8 s installed
+        out.append(_check("rccl device code", OK if library_dir() else WARN,
+                          f"gfx950 code unpacked once ({OUT})" if library_dir() else
+                          f"{src} inflates its 5.3 GB bundle in every rank (~1.7 s): python3 __graft_entry__.py build"))
     return out
 
 
