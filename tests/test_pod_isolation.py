@@ -159,6 +159,34 @@ def test_anonymous_callers_get_discovery_and_nothing_else(cluster):
     assert "secret-log-line" in k.get(k.k8s("/api/v1/namespaces/default/pods/logger/log"), raw=True)
 
 
+@needs_jail
+def test_a_hostpath_into_the_node_state_is_refused(cluster):
+    """a hostPath volume at or beneath a denied path (the workspace's .tk8s/) would
+    win over the jail's deny (the most specific layer decides) and re-open the admin token: the
+    agent refuses the pod, whatever the namespace's Pod Security level. One above it is fine."""
+    ws, env, kc, _ = cluster
+    st = ws / ".tk8s"
+    for name, path in (("grab-state", st), ("grab-machine", st / "machines" / "kubenode1")):
+        pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name}, "spec": {
+            "restartPolicy": "Never", "nodeName": "kubenode1",
+            "volumes": [{"name": "s", "hostPath": {"path": str(path)}}],
+            "containers": [{"name": "c", "command": ["sh", "-c", f"cat {st}/admin-token"],
+                            "volumeMounts": [{"name": "s", "mountPath": str(path)}]}]}}
+        kc("apply", "-f", "-", stdin=json.dumps(pod))
+        o = _wait(kc, name)
+        assert o["status"]["phase"] == "Failed", o["status"]
+        assert "HostPathDenied" in json.dumps(o["status"]), o["status"]
+    data = ws / "shared-data"
+    data.mkdir(exist_ok=True)
+    pod = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "data-ok"}, "spec": {
+        "restartPolicy": "Never", "nodeName": "kubenode1",
+        "volumes": [{"name": "s", "hostPath": {"path": str(data)}}],
+        "containers": [{"name": "c", "command": ["sh", "-c", f"echo ok > {data}/x && cat {data}/x"],
+                        "volumeMounts": [{"name": "s", "mountPath": str(data)}]}]}}
+    kc("apply", "-f", "-", stdin=json.dumps(pod))
+    assert _wait(kc, "data-ok")["status"]["phase"] == "Succeeded"
+
+
 def test_node_tokens_reach_their_own_node_only(tmp_path):
     """NodeRestriction + the Node authorizer (authn.node_allows)."""
     p, c = _start(tmp_path)
