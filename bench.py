@@ -797,7 +797,8 @@ def main(argv=None) -> int:
         # the fabric check of the last step, for the multi-GPU runs: communicator start-up, how
         # unevenly the ranks came up, the channel transports RCCL logged, the Job's shape
         "rccl_last_step": {k: (last.get("rccl") or {}).get(k) for k in (
-            "ok", "nranks", "pods", "gpus_per_pod", "comm_init_ms_max", "init_spread_ms", "transport")}
+            "ok", "nranks", "pods", "gpus_per_pod", "comm_init_ms_max", "sweep_ms_max", "init_spread_ms", "transport",
+            "rccl_library")}
         if last.get("rccl") else None,
         "xgmi_last_step": last.get("xgmi"),
         "validation_last_step": last.get("validation"),
@@ -835,7 +836,7 @@ def main(argv=None) -> int:
         out["fabric_validated"].update({
             "what": "--rccl on: wall-clock from launching ./setup.sh to its exit after the RCCL all-reduce Job "
                     "over every GPU passed its exact check",
-            "rccl": {k: last_rccl.get(k) for k in ("ok", "nranks", "pods", "comm_init_ms_max", "sweep_ms_max", "init_spread_ms",
+            "rccl": {k: last_rccl.get(k) for k in ("ok", "nranks", "pods", "comm_init_ms_max", "sweep_ms_max", "init_spread_ms", "rccl_library",
                                                    "peak_busbw_gbps", "transport", "prestarted")}})
     print(json.dumps(out), flush=True)
     return 0
