@@ -98,3 +98,27 @@ def test_library_files_are_the_generated_front_ends():
     assert set(gen) == {p.stem for p in LIB.glob("tk8s_*.py")}
     for name, text in gen.items():
         assert (LIB / f"{name}.py").read_text() == text, name
+
+
+def test_the_library_modules_document_every_option_for_ansible_doc():
+    """What ansible-doc reads: DOCUMENTATION's options match ARG_SPECS (type, default, choices,
+    required), every option has a real description, and EXAMPLES / RETURN are valid YAML."""
+    import yaml
+
+    from tritonk8ssupervisor_amd.ansible_bridge import ARG_SPECS
+
+    lib = Path(__file__).resolve().parents[1] / "ansible" / "library"
+    for name, spec in ARG_SPECS.items():
+        src = (lib / f"{name}.py").read_text()
+        ns: dict = {}
+        exec(compile(src.split("def _home")[0], str(lib / f"{name}.py"), "exec"), ns)  # the module's constants only
+        doc = yaml.safe_load(ns["DOCUMENTATION"])
+        assert doc["module"] == name and set(doc["options"]) == set(spec), name
+        for opt, o in doc["options"].items():
+            assert o["type"] == spec[opt]["type"] and o["description"] != opt and len(o["description"]) > 15, (name, opt)
+            assert o.get("required", False) == spec[opt].get("required", False), (name, opt)
+            assert o.get("default") == spec[opt].get("default"), (name, opt)
+            assert o.get("choices") == spec[opt].get("choices"), (name, opt)
+        examples = yaml.safe_load(ns["EXAMPLES"])
+        assert any(name in task for task in examples), name
+        assert yaml.safe_load(ns["RETURN"]), name

@@ -122,6 +122,115 @@ SHORT_DESCRIPTIONS = {
     "tk8s_kube": "Create, delete or wait for Kubernetes objects through the tk8s control plane",
 }
 
+# What ansible-doc shows for each option (the generated DOCUMENTATION's ``options``; the types,
+# defaults, choices and required flags come from ARG_SPECS itself).
+OPTION_DOCS = {
+    "machine_dir": "The machine's work directory (its sandbox; host var C(tk8s_machine_dir)).",
+    "gpus": "The machine's GPU ordinals on the host, comma separated (host var C(tk8s_gpus)); empty for a CPU-only machine.",
+    "tk8s_home": "The tk8s install on the machine (default C($TK8S_HOME), else the newest C(~/.tk8s/dist/<digest>) a provider pushed).",
+    "machine": "The machine's name (default C($TK8S_MACHINE), else the host name).",
+    "name": "The daemon's name on this machine: its pidfile is C(run/<name>.pid), its log C(logs/<name>.log).",
+    "state": "What to do: start it (idempotent), stop it, or only report whether it runs.",
+    "argv": "The daemon's command as a list (no shell).",
+    "cmd": "The daemon's command as one shell string (when I(argv) is not given).",
+    "env": "Extra environment of the daemon, on top of the machine's C(TK8S_MACHINE*) variables.",
+    "restart_policy": "Restarts by C(tk8s-supervise), as Docker's restart policies (C(no): run it unsupervised).",
+    "wait_for_log": "Return only once the daemon's log has this text (the reference waited for rancher/server's C(Listening on)).",
+    "timeout": "Seconds to wait (for I(wait_for_log), or for the objects' readiness with C(state=wait)).",
+    "command": "The burn-in probe's command (C(tk8s-hsaprobe) / C(tk8s-probe) and its arguments; the machine's GPUs are appended).",
+    "out": "Where the burn-in writes its JSON result, relative to the machine directory; the validation pod reads it once.",
+    "api": "The control plane's base URL (C(http://<master>:<port>)).",
+    "project": "The environment (Rancher project) id whose Kubernetes API receives the objects.",
+    "token": "The control plane's admin token (or the environment's API token).",
+    "definition": "The objects, inline: one mapping or a list of them.",
+    "src": "A manifest file (YAML, several documents allowed; Jinja2 variables from I(vars)).",
+    "vars": "Variables for the manifest template in I(src).",
+    # per module, where an option means something else there
+    ("tk8s_kube", "state"): "C(present): create the objects or update them; C(absent): delete them; C(wait): until "
+                            "they are ready.",
+    ("tk8s_kube", "timeout"): "Seconds to wait for the objects' readiness with C(state=wait).",
+    ("tk8s_burnin", "name"): "The burn-in's name on this machine: its pidfile is C(run/<name>.pid).",
+    ("tk8s_daemon", "timeout"): "Seconds to wait for I(wait_for_log).",
+}
+# (module, state) -> what ansible-doc shows: examples from the shipped roles, and the results
+MODULE_EXAMPLES = {
+    "tk8s_build": """- name: Build the native validation stack once (hipcc, gfx950)
+  tk8s_build:
+  run_once: true
+  delegate_to: localhost
+  when: not tk8s_native_built""",
+    "tk8s_burnin": """- name: Start the GPU burn-in on this machine's MI355X GPUs (background)
+  tk8s_burnin:
+    command: "{{ tk8s_validation_command }}"
+    out: run/gpu-burnin.json
+    machine_dir: "{{ tk8s_machine_dir }}"
+    gpus: "{{ tk8s_gpus }}"
+""",
+    "tk8s_daemon": """- name: Start the control plane (restart policy unless-stopped)
+  tk8s_daemon:
+    name: controlplane
+    argv: ["{{ tk8s_python }}", "-S", "-c", "import tritonk8ssupervisor_amd.controlplane.__main__",
+           "--host", "{{ tk8s_bind }}", "--port", "{{ tk8s_master_port }}"]
+    restart_policy: unless-stopped
+    wait_for_log: Listening on
+    machine_dir: "{{ tk8s_machine_dir }}"
+""",
+    "tk8s_gpu_facts": """- name: Gather ROCm / GPU facts for this machine
+  tk8s_gpu_facts:
+    machine_dir: "{{ tk8s_machine_dir }}"
+    gpus: "{{ tk8s_gpus }}"
+- assert:
+    that: [tk8s_rocm_version != '', tk8s_kfd]""",
+    "tk8s_kube": """- name: Deploy the GPU validation DaemonSet (tk8s-probe on every MI355X worker)
+  tk8s_kube:
+    api: "http://{{ master }}:{{ tk8s_master_port }}"
+    project: "{{ kubernetes_environment_id }}"
+    token: "{{ tk8s_admin_token }}"
+    src: "{{ tk8s_manifests }}/gpu-validation-daemonset.yaml"
+""",
+}
+MODULE_RETURNS = {
+    "tk8s_build": {"changed": "whether any artefact was rebuilt", "seconds": "how long the build took"},
+    "tk8s_burnin": {"gpus": "the GPU ordinals the burn-in validates", "out": "the result file, relative to the machine directory",
+                    "pid": "the burn-in process"},
+    "tk8s_daemon": {"running": "whether the daemon runs after the task", "pid": "its process id",
+                    "log": "its log file", "wait_seconds": "how long I(wait_for_log) waited"},
+    "tk8s_gpu_facts": {"ansible_facts": "tk8s_rocm_version, tk8s_kfd, tk8s_host_gpus, tk8s_inventory_source, "
+                                        "tk8s_native_built, tk8s_node_python, tk8s_node_kernel, tk8s_machine_gpus"},
+    "tk8s_kube": {"objects": "per object: kind, name, namespace and whether it was created",
+                  "deleted": "how many objects C(state=absent) deleted"},
+}
+
+
+def documentation(name: str) -> str:
+    """The module's DOCUMENTATION block (YAML, what ansible-doc reads), from ARG_SPECS + OPTION_DOCS."""
+    import json
+
+    lines = [f"module: {name}", f"short_description: {SHORT_DESCRIPTIONS[name]}",
+             "description:", "  - Runs the same implementation as the tk8s playbook engine "
+             "(tritonk8ssupervisor_amd/playbook_modules.py) on the target machine.", "options:"]
+    for opt, spec in sorted(ARG_SPECS[name].items()):
+        lines.append(f"  {opt}:")
+        lines.append(f"    description: {json.dumps(OPTION_DOCS.get((name, opt), OPTION_DOCS.get(opt, opt)))}")
+        lines.append(f"    type: {spec['type']}")
+        if spec.get("elements"):
+            lines.append(f"    elements: {spec['elements']}")
+        if spec.get("required"):
+            lines.append("    required: true")
+        if "default" in spec:
+            lines.append(f"    default: {json.dumps(spec['default'])}")
+        if spec.get("choices"):
+            lines.append(f"    choices: {json.dumps(spec['choices'])}")
+    lines.append("author: tk8s")
+    return "\n".join(lines)
+
+
+def returns(name: str) -> str:
+    import json
+
+    return "\n".join(f"{k}:\n  description: {json.dumps(v)}\n  returned: success" for k, v in MODULE_RETURNS[name].items())
+
+
 LIBRARY_TEMPLATE = '''#!/usr/bin/python
 # -*- coding: utf-8 -*-
 # GENERATED by tritonk8ssupervisor_amd/ansible_bridge.py (--write-library): edit the template there.
@@ -137,9 +246,15 @@ import os
 import sys
 
 DOCUMENTATION = r"""
-module: {name}
-short_description: {short}
-description: see tritonk8ssupervisor_amd/ansible_bridge.py (ARG_SPECS) and playbook_modules.py
+{documentation}
+"""
+
+EXAMPLES = r"""
+{examples}
+"""
+
+RETURN = r"""
+{returns}
 """
 
 
@@ -164,7 +279,8 @@ if __name__ == "__main__":
 
 def library_sources() -> dict[str, str]:
     """{module name: the text of ansible/library/<name>.py}, one per ARG_SPECS entry."""
-    return {n: LIBRARY_TEMPLATE.format(name=n, short=SHORT_DESCRIPTIONS[n]) for n in sorted(ARG_SPECS)}
+    return {n: LIBRARY_TEMPLATE.format(name=n, short=SHORT_DESCRIPTIONS[n], documentation=documentation(n),
+                                       examples=MODULE_EXAMPLES[n].rstrip(), returns=returns(n)) for n in sorted(ARG_SPECS)}
 
 
 def write_library(directory: str | os.PathLike) -> list[str]:
