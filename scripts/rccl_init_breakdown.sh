@@ -13,3 +13,14 @@ for i in 1 2; do
       --max-bytes 1048576 --iters 3 --warmup 1 > $out/run$i.log 2>&1 || exit $?
 done
 echo done
+# RCCL start-up knobs, 3 fresh processes each: which of RCCL's optional subsystems cost start time
+for variant in "BASE=1" "NCCL_IB_DISABLE=1" "RCCL_MSCCL_ENABLE=0 RCCL_MSCCLPP_ENABLE=0" "NCCL_NET_PLUGIN=none" \
+               "NCCL_IB_DISABLE=1 RCCL_MSCCL_ENABLE=0 RCCL_MSCCLPP_ENABLE=0 NCCL_NET_PLUGIN=none"; do
+  for i in 1 2 3; do
+    env $variant LD_LIBRARY_PATH=$lib timeout -k 10 120 ./tritonk8ssupervisor_amd/bin/tk8s-rccl --ngpus 1 \
+      --max-bytes 1048576 --iters 3 --warmup 1 2>/dev/null | tail -1 | \
+      python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$variant', d['comm_init_ms'], d.get('sweep_ms'))" \
+      >> $out/knobs.txt || exit $?
+  done
+done
+echo knobs done
