@@ -343,7 +343,8 @@ def slowest_tasks(events: Path, launched_unix: float | None = None, top: int = 6
                 out.append({"what": "CLI start: interpreter + imports (launch -> first event)",
                             "s": round(e["ts"] - launched_unix, 4)})
             if e.get("event") in ("task", "phase_end") and isinstance(e.get("seconds"), (int, float)):
-                out.append({"what": e.get("task") or f"phase {e.get('phase')}", "s": round(e["seconds"], 4)})
+                out.append({"what": e.get("task") or f"phase {e.get('phase')}", "s": round(e["seconds"], 4),
+                            **({"timing_ms": e["timing_ms"]} if e.get("timing_ms") else {})})
     except (OSError, ValueError):
         return []
     return sorted(out, key=lambda x: -x["s"])[:top]

@@ -7,7 +7,7 @@ def test_local_facts_are_gathered_once_per_ttl(monkeypatch):
     import tritonk8ssupervisor_amd.nodefacts as nf
 
     calls = []
-    monkeypatch.setattr(nf, "node_facts", lambda: (calls.append(1), {"tk8s_host_gpus": len(calls)})[1])
+    monkeypatch.setattr(nf, "node_facts", lambda timing=None: (calls.append(1), {"tk8s_host_gpus": len(calls)})[1])
     ms = {n: Machine(name=n, id=n, package="p", networks=[], primaryip="127.0.0.1", sandbox="/tmp") for n in ("a", "b")}
     ex = ex_mod.LocalExecutor(None, ms)
     a, b = ex.facts("a"), ex.facts("b")
@@ -16,3 +16,19 @@ def test_local_facts_are_gathered_once_per_ttl(monkeypatch):
     assert "x" not in ex.facts("a")
     monkeypatch.setattr(ex, "FACTS_TTL_S", -1.0)  # expired: gathered again
     assert ex.facts("b") == {"tk8s_host_gpus": 2}
+
+
+def test_facts_gathering_reports_where_its_time_went():
+    """The cold first run's slowest task was this gathering (0.33 s on a busy fresh box): its
+    parts are timed into the task's event (timing_ms), so a slow one names its part."""
+    import tritonk8ssupervisor_amd.nodefacts as nf
+
+    timing: dict = {}
+    facts = nf.node_facts(timing)
+    assert "tk8s_rocm_version" in facts
+    assert list(timing) == ["import", "rocm_version", "kfd_access", "gpu_inventory", "native_tools"]
+    assert all(v >= 0 for v in timing.values())
+    ms = {"a": Machine(name="a", id="a", package="p", networks=[], primaryip="127.0.0.1", sandbox="/tmp")}
+    t2: dict = {}
+    ex_mod.LocalExecutor(None, ms).facts("a", t2)
+    assert "lock_wait" in t2 and "gpu_inventory" in t2

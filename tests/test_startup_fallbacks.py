@@ -108,12 +108,3 @@ def test_preloaded_burnin_killed_before_the_plan(tmp_path, monkeypatch):
             early.proc.wait()
         earlyburn.take()
 
-
-def test_control_plane_without_its_lazy_stdlib(ws):
-    """TK8S_LAZY_STDLIB=0: the control plane imports logging / inspect / concurrent.futures the
-    plain way (utils/lazymod.py off) and the bring-up is the same."""
-    r = subprocess.run(["./setup.sh", "--answers", "answers.json", "--yes", "--json", "--port", "0", "--rccl", "off"],
-                       cwd=ws, env=_env(TK8S_LAZY_STDLIB="0"), capture_output=True, text=True, timeout=180)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    s = json.loads(r.stdout.strip().splitlines()[-1])
-    assert s["nodes"] == 2 and s["nodes_validated"] == 2

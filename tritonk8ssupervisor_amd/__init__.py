@@ -84,7 +84,6 @@ SHORTCUT_SWITCHES = {
     "TK8S_HSA_CPU_CACHES": "1",       # ROCr's per-CPU cache walk runs as usual
     "TK8S_YAML_CACHE": "off",         # the parse caches
     "TK8S_NO_PYCACHE_PREFIX": "1",    # the shared byte-code prefix
-    "TK8S_LAZY_STDLIB": "0",          # the control plane's lazy logging/inspect/concurrent.futures
     "TK8S_LOCAL_PREFETCH": "0",       # the local provider's prefetch
     "TK8S_PROVISION_SERIAL": "0",     # serial local creates
     "TK8S_PLAY_INLINE": "0",          # inline file-only tasks

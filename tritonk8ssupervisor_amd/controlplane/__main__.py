@@ -3,18 +3,14 @@
 and the start is on the bring-up's critical path; ``sys.argv`` has the same positions either way).
 
 The control plane serves plain HTTP only, so ``ssl`` is kept out: asyncio imports it when it can
-(~4 ms, libssl included) and runs without it when the import fails. ``logging`` and
-``concurrent.futures``, which asyncio imports and the control plane never calls, load on first
-use (utils/lazymod.py).
+(~4 ms, libssl included) and runs without it when the import fails. (Round 4 also stood in for
+``logging`` / ``inspect`` / ``concurrent.futures`` until first use; round 5 measured it on the
+MI355X -- headline medians 0.0649/0.0638 s with it, 0.0654/0.0637 s without,
+profiles/r5_lazy_ab/ -- and removed it: the zygote imports them before its arguments arrive.)
 """
 import sys
 
 sys.modules.setdefault("ssl", None)  # type: ignore[arg-type]  -- `import ssl` -> ImportError
-
-from ..utils import lazymod  # noqa: E402
-
-if __import__("os").environ.get("TK8S_LAZY_STDLIB", "1") != "0":
-    lazymod.install()  # logging / inspect / concurrent.futures: loaded when first used (utils/lazymod.py)
 
 from .server import main  # noqa: E402
 

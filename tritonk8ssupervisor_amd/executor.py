@@ -225,16 +225,20 @@ class LocalExecutor(_Base):
 
     FACTS_TTL_S = 2.0
 
-    def facts(self, host: str) -> dict:
+    def facts(self, host: str, timing: dict | None = None) -> dict:
         """Every machine here is a sandbox of this host: one gathering answers all of a play's
         hosts (at 8 workers nine concurrent KFD-topology walks were ~16 ms of play 1 on the
-        MI355X host). Kept FACTS_TTL_S, so a later gathering sees a changed host."""
+        MI355X host). Kept FACTS_TTL_S, so a later gathering sees a changed host. ``timing``
+        receives the lock wait and, for the gathering call, its parts (nodefacts.node_facts)."""
         from .nodefacts import node_facts
 
+        t = time.perf_counter()
         with self._facts_lock:
+            if timing is not None:
+                timing["lock_wait"] = round((time.perf_counter() - t) * 1e3, 3)
             now = time.monotonic()
             if self._facts is None or now - self._facts[0] > self.FACTS_TTL_S:
-                self._facts = (now, node_facts())
+                self._facts = (now, node_facts(timing))
             return dict(self._facts[1])
 
     def _paths(self, host: str, name: str) -> tuple[Path, Path]:
@@ -347,7 +351,7 @@ class RemoteExecutor(_Base):
         rc, _ = self.exec(host, _SH_FUNCS + f"_alive {int(pid)}", timeout=60)
         return rc == 0
 
-    def facts(self, host: str) -> dict:
+    def facts(self, host: str, timing: dict | None = None) -> dict:
         import json
 
         rc, out = self.exec(host, f"{shlex.quote(self.python(host))} -S -m tritonk8ssupervisor_amd.nodefacts",

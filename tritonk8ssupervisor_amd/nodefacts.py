@@ -18,21 +18,43 @@ PKG = Path(__file__).resolve().parent
 NATIVE_TOOLS = ("tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl")
 
 
-def node_facts() -> dict:
+def node_facts(timing: dict | None = None) -> dict:
+    """The facts; ``timing`` (when given) receives how long each part took, in ms: a slow
+    gathering on the bring-up's critical path names its part (bench.py's cold first run)."""
+    import time
+
+    t = time.perf_counter()
+    marks = []
+
+    def mark(what: str) -> None:
+        nonlocal t
+        now = time.perf_counter()
+        marks.append((what, round((now - t) * 1e3, 3)))
+        t = now
+
     from .models.hostinfo import discover
 
+    mark("import")
     ver = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / ".info" / "version"
     try:
         rocm = ver.read_text().strip()
     except OSError:
         rocm = ""
+    mark("rocm_version")
+    kfd = os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK | os.W_OK)
+    mark("kfd_access")
     inv = discover()
+    mark("gpu_inventory")
+    built = all((PKG / "bin" / t).exists() for t in NATIVE_TOOLS)
+    mark("native_tools")
+    if timing is not None:
+        timing.update(marks)
     return {
         "tk8s_rocm_version": rocm,
-        "tk8s_kfd": os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK | os.W_OK),
+        "tk8s_kfd": kfd,
         "tk8s_host_gpus": inv.count,
         "tk8s_inventory_source": inv.source,
-        "tk8s_native_built": all((PKG / "bin" / t).exists() for t in NATIVE_TOOLS),
+        "tk8s_native_built": built,
         "tk8s_node_python": sys.version.split()[0],
         "tk8s_node_kernel": os.uname().release,
     }

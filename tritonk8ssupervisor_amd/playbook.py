@@ -319,8 +319,9 @@ class Playbook:
             order = {h.name: i for i, h in enumerate(hosts)}
             with self._trace_lock:
                 self.trace[start:] = sorted(self.trace[start:], key=lambda e: order.get(e["host"], len(order)))
+        timing = {r.host: r.result["timing_ms"] for r in res if isinstance(r.result, dict) and r.result.get("timing_ms")}
         self.events.emit("task", task=f"{prefix}{title}", seconds=round(time.monotonic() - t, 6),
-                         results={r.host: r.status for r in res})
+                         results={r.host: r.status for r in res}, **({"timing_ms": timing} if timing else {}))
         return res
 
     def _run_on_host(self, task: dict, host: Host, play_vars: dict) -> TaskResult:

@@ -639,16 +639,17 @@ def m_tk8s_gpu_facts(args, *, ctx, target, local, **_):
     remote machine) -- plus the GPU slice the provider gave it."""
     from .models.hostinfo import compose_visible_devices
 
+    timing: dict = {}
     if ctx.executor is not None and not local:
-        facts = dict(ctx.executor.facts(target.name))
+        facts = dict(ctx.executor.facts(target.name, timing))
         facts["tk8s_machine_gpus"] = ctx.executor.machine_gpus(target.name)
     else:
         from .nodefacts import node_facts
 
-        facts = dict(node_facts())
+        facts = dict(node_facts(timing))
         facts["tk8s_machine_gpus"] = []
     facts["tk8s_machine_visible_devices"] = compose_visible_devices(facts["tk8s_machine_gpus"])["ROCR_VISIBLE_DEVICES"]
-    return {"ansible_facts": facts, "changed": False}
+    return {"ansible_facts": facts, "changed": False, "timing_ms": timing}
 
 
 def m_tk8s_build(args, *, check, **_):
