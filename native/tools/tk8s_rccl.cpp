@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -106,7 +107,10 @@ int main(int argc, char** argv) {
     cfg.warmup = static_cast<int>(a.num("warmup", 5));
     cfg.dtype = a.str("dtype", "float32") == "bfloat16" ? tk8s::DType::kBF16 : tk8s::DType::kF32;
     cfg.check = !a.has("no-check");
-    cfg.teardown = a.has("teardown");  // the process exits right after its JSON line (see below)
+    // the process exits right after its JSON line (see below) -- unless a profiler's library is
+    // preloaded: its exit handlers write the trace, and _Exit would skip them
+    const char* preload = std::getenv("LD_PRELOAD");
+    cfg.teardown = a.has("teardown") || (preload && std::strstr(preload, "rocprof"));
     std::string out;
     if (a.has("rank") || a.has("group-index")) {
       const int nranks = static_cast<int>(a.num("nranks", 1));

@@ -95,8 +95,10 @@ class FabricCheck:
                 if self.rocprof_counters:  # a counter pass: --pmc with --kernel-trace/--stats only
                     check_pmc_counters(self.rocprof_counters)
                     pmc = ["--pmc", *self.rocprof_counters]
+                # (--teardown: the rank returns from main, so the profiler's exit handlers write its
+                # trace -- tk8s-rccl otherwise leaves with _Exit right after its result)
                 cmd = [rp, *pmc, "--kernel-trace", "--stats", "-d", str(prof_dir), "-o", "rank$(JOB_COMPLETION_INDEX)",
-                       "--output-format", "csv", "--", *cmd]
+                       "--output-format", "csv", "--", *cmd, *([] if os.environ.get("TK8S_FAKE_GPUS") else ["--teardown"])]
         objs = load_manifests(self.ws.manifests / "rccl-allreduce-job.yaml",
                               {"job_name": job, "npods": npods, "gpus_per_pod": per_pod, "rccl_command": cmd,
                                "gpu_scope": layout["scope"]})
