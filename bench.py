@@ -517,7 +517,7 @@ def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1)
     workspace creation outside the brackets."""
     points = []
     t_curve = time.perf_counter()
-    for n in CURVE_NODES:
+    for n in getattr(args, "curve_workers", None) or CURVE_NODES:
         ready, proc = [], []
         for i in range(warmup + steps):
             ws = root / f"curve{n}-{i}"
@@ -539,7 +539,8 @@ def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1)
     return {"config": "BASELINE.json configs[1]: 1 master + N cpu-only workers, no GPU device plugin",
             "package": "cpu-only", "warmup": warmup, "points": points,
             "wall_s": round(time.perf_counter() - t_curve, 3),
-            "scaling_8_vs_1": round(points[-1]["mean_s"] / points[0]["mean_s"], 3) if points else None}
+            "scaling_8_vs_1": round(points[-1]["mean_s"] / points[0]["mean_s"], 3)
+            if len(points) > 1 and points[0]["workers"] == 1 and points[-1]["workers"] == 8 else None}
 
 
 def main(argv=None) -> int:
@@ -563,6 +564,8 @@ def main(argv=None) -> int:
     ap.add_argument("--curve-steps", type=int, default=5,
                     help="timed steps per point of the cpu-only worker curve (BASELINE configs[1], 1/2/4/8 workers) "
                          "run after the headline on a single-rank run; 0 skips it")
+    ap.add_argument("--curve-workers", type=lambda s: [int(x) for x in s.split(",") if x.strip()], default=None,
+                    help="the curve's worker counts, comma separated (default 1,2,4,8)")
     ap.add_argument("--plain-steps", type=int, default=5,
                     help="timed bring-ups with TK8S_SHORTCUTS=0 (every start-up shortcut off), reported as "
                          "plain_path_s on a single-rank run; 0 skips them")
