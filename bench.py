@@ -832,7 +832,7 @@ def main(argv=None) -> int:
         out["plain_path_s"] = plain.get("ready", {}).get("mean_s")
         out["plain_path"] = {k: v for k, v in plain.items() if k != "last"}
         out["plain_path"]["what"] = ("TK8S_SHORTCUTS=0: every start-up shortcut of docs/architecture.md off "
-                                     "(preloaded/early burn-in, zygotes, caches, stand-ins, inline tasks, ...)")
+                                     "(early burn-in, zygotes, caches, fast parsers, -S, inline tasks, ...)")
     if fabric is not None:  # launch -> a passing RCCL all-reduce Job, N GPUs
         last_rccl = (fabric.get("last") or {}).get("rccl") or {}
         out["fabric_validated_s"] = fabric.get("setup_exit", {}).get("mean_s")

@@ -32,18 +32,10 @@
 // bring-up judges the link matrix (tritonk8ssupervisor_amd/xgmi.py). With one GPU there is no
 // pair and the phase costs nothing. --peers-host runs the same pull path from a host-memory
 // source (granted the same way): the part of the mechanism a 1-GPU box can exercise.
-//
-// --plan-stdin (the preloaded burn-in): mapping libhsa-runtime64 costs ~11 ms before main()
-// runs (its static initialisers; the other libraries ~1 ms, profiles/r2_exec/). ./setup.sh starts
-// the probe this way first thing, so that cost overlaps the CLI interpreter's own start; the CLI
-// then writes the plan on the probe's stdin, one item per line -- "ARG <arg>" (the options
-// above, in order), "ENV <NAME>=<value>" (the GPU visibility, set before hsa_init), "LOG <path>"
-// (stderr) -- and "GO". EOF before "GO" (no early burn-in for this run) exits 0 silently; so
-// does no plan within 60 s. The probe makes itself a session leader (teardown kills its group).
+
 #include <fcntl.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
-#include <poll.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -981,67 +973,11 @@ std::string with_device(const std::string& j, int d) {
 
 }  // namespace
 
-// --plan-stdin: read "ARG"/"ENV"/"LOG" lines until "GO" (see the header). False: no plan.
-bool read_plan(std::vector<std::string>* args) {
-  std::string buf;
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(60);
-  while (true) {
-    size_t nl;
-    while ((nl = buf.find('\n')) != std::string::npos) {
-      const std::string line = buf.substr(0, nl);
-      buf.erase(0, nl + 1);
-      if (line == "GO") return true;
-      if (line.rfind("ARG ", 0) == 0) {
-        args->push_back(line.substr(4));
-      } else if (line.rfind("ENV ", 0) == 0) {
-        const std::string kv = line.substr(4);
-        const auto eq = kv.find('=');
-        if (eq == std::string::npos || eq == 0) return false;
-        if (setenv(kv.substr(0, eq).c_str(), kv.substr(eq + 1).c_str(), 1) != 0) return false;
-      } else if (line.rfind("LOG ", 0) == 0) {
-        const int fd = open(line.substr(4).c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
-        if (fd >= 0) {
-          dup2(fd, 2);
-          close(fd);
-        }
-      } else {
-        return false;  // not a plan this probe understands
-      }
-    }
-    const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
-    if (left.count() <= 0) return false;
-    pollfd pfd{0, POLLIN, 0};
-    if (poll(&pfd, 1, static_cast<int>(left.count())) <= 0) return false;
-    char chunk[4096];
-    const ssize_t n = read(0, chunk, sizeof chunk);
-    if (n <= 0) return false;  // EOF: this run has no early burn-in
-    buf.append(chunk, static_cast<size_t>(n));
-  }
-}
-
 int main(int argc, char** argv) {
-  auto t0 = std::chrono::steady_clock::now();
+  const auto t0 = std::chrono::steady_clock::now();
   // wall clock at main(): against the launcher's spawn time it shows the exec + loader cost
   const double main_unix_ms =
       std::chrono::duration<double, std::milli>(std::chrono::system_clock::now().time_since_epoch()).count();
-  double plan_unix_ms = 0;
-  std::vector<std::string> planned;
-  std::vector<char*> pargv;
-  if (argc == 2 && std::strcmp(argv[1], "--plan-stdin") == 0) {
-    setsid();
-    const int null = open("/dev/null", O_RDWR | O_CLOEXEC);
-    if (null >= 0) dup2(null, 1);  // the plan's result goes to --out; stdout is nobody's
-    if (!read_plan(&planned)) _exit(0);
-    if (null >= 0) close(null);
-    pargv.push_back(argv[0]);
-    for (auto& x : planned) pargv.push_back(x.data());
-    pargv.push_back(nullptr);
-    argc = static_cast<int>(pargv.size()) - 1;
-    argv = pargv.data();
-    t0 = std::chrono::steady_clock::now();  // the burn-in's own clock starts with its plan
-    plan_unix_ms =
-        std::chrono::duration<double, std::milli>(std::chrono::system_clock::now().time_since_epoch()).count();
-  }
   std::string out_file;
   try {
     tk8s::Args a(argc, argv);
@@ -1167,8 +1103,7 @@ int main(int argc, char** argv) {
     if (c.peers) out.kv("peer_bytes", static_cast<uint64_t>(c.peer)).kv("peer_rounds", static_cast<int>(devices.size()) - 1);
     out.raw("timings_ms", Json().kv("hip_init", init_ms).kv("runtime_init", init_ms).kv("gpuinfo", gpuinfo_ms)
                               .kv("peers", peers_ms).kv("total", ms_since(t0))
-                              .kv("main_unix_ms", plan_unix_ms > 0 ? plan_unix_ms : main_unix_ms)
-                              .kv("preloaded", plan_unix_ms > 0).kv("exec_unix_ms", main_unix_ms)
+                              .kv("main_unix_ms", main_unix_ms).kv("exec_unix_ms", main_unix_ms)
                               .kv("cpu_cache_walk", tk8s::cachewalk::mode())
                               .kv("cpu_cache_dirs_hidden", tk8s::cachewalk::g_hidden).str());
     emit(out.str(), out_file);

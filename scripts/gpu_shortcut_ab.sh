@@ -9,9 +9,9 @@ STEPS="${2:-10}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$ROOT"
-variants=("none" "TK8S_PRELOAD_BURNIN=0" "TK8S_HOST_BURNIN=0" "TK8S_CP_ZYGOTE=0" "TK8S_AGENT_ZYGOTE=0"
-          "TK8S_HSA_CPU_CACHES=1" "TK8S_YAML_CACHE=off" "TK8S_NO_PYCACHE_PREFIX=1" "TK8S_LOCAL_PREFETCH=0"
-          "TK8S_PROVISION_SERIAL=0" "TK8S_PLAY_INLINE=0" "TK8S_INPROCESS_BOOTSTRAP=0" "TK8S_FAST_ARGS=0"
+variants=("none" "TK8S_HOST_BURNIN=0" "TK8S_CP_ZYGOTE=0" "TK8S_AGENT_ZYGOTE=0"
+          "TK8S_HSA_CPU_CACHES=1" "TK8S_YAML_CACHE=off" "TK8S_NO_PYCACHE_PREFIX=1"
+          "TK8S_PLAY_INLINE=0" "TK8S_INPROCESS_BOOTSTRAP=0" "TK8S_FAST_ARGS=0"
           "TK8S_SKIP_SITE=0" "TK8S_SHORTCUTS=0")
 [ -n "${VARIANTS:-}" ] && read -ra variants <<< "$VARIANTS"   # a subset: VARIANTS="none TK8S_X=0 ..."
 CURVE=(--curve-steps "${CURVE_STEPS:-0}")

@@ -178,66 +178,6 @@ def _hsaprobe():
     return p
 
 
-def test_preloaded_probe_runs_the_plan_it_is_sent(tmp_path):
-    """--plan-stdin: the probe waits for ARG/ENV/LOG lines and GO, then runs exactly that (here,
-    on a CPU host, it reports that no GPU agent is visible -- into the planned --out file, with
-    the planned environment applied before the runtime starts)."""
-    import subprocess
-
-    out, log = tmp_path / "r.json", tmp_path / "burn.log"
-    p = subprocess.Popen([str(_hsaprobe()), "--plan-stdin"], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                         stderr=subprocess.PIPE)
-    plan = f"ARG --all-devices\nARG --hbm-bytes\nARG 1048576\nARG --out\nARG {out}\nENV ROCR_VISIBLE_DEVICES=0\nLOG {log}\nGO\n"
-    stdout, _ = p.communicate(plan.encode(), timeout=60)
-    assert out.exists(), (p.returncode, stdout)
-    res = json.loads(out.read_text())
-    assert res["ok"] is False and res.get("runtime") == "hsa"
-    assert stdout == b""  # the result goes to --out only
-
-
-def test_preloaded_probe_without_a_plan_exits_quietly(tmp_path):
-    import subprocess
-    import time
-
-    p = subprocess.Popen([str(_hsaprobe()), "--plan-stdin"], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                         stderr=subprocess.PIPE, cwd=tmp_path)
-    t = time.monotonic()
-    stdout, stderr = p.communicate(b"", timeout=60)  # EOF: this run has no early burn-in
-    assert p.returncode == 0 and stdout == b"" and time.monotonic() - t < 10
-    assert list(tmp_path.iterdir()) == []
-    p = subprocess.Popen([str(_hsaprobe()), "--plan-stdin"], stdin=subprocess.PIPE, stdout=subprocess.PIPE)
-    assert p.communicate(b"BOGUS line\nGO\n", timeout=60)[0] == b"" and p.returncode == 0  # not a plan
-
-
-def test_launch_hands_the_plan_to_the_preloaded_probe(tmp_path, monkeypatch):
-    """earlyburn.launch with a probe setup.sh preloaded: the plan goes down the pipe (no second
-    process), the preload variables leave the environment, the pipe end is not inherited."""
-    import subprocess
-
-    from tritonk8ssupervisor_amd import earlyburn
-
-    ws = _ws(tmp_path)
-    r, w = os.pipe()
-    reader = subprocess.Popen(["cat"], stdin=r, stdout=subprocess.PIPE)
-    os.close(r)
-    fake_plan = {"gpus": [0], "command": [str(tmp_path / "probe"), "--all-devices"], "state_dir": str(tmp_path / ".tk8s"),
-                 "result": str(tmp_path / ".tk8s" / "run" / "host-burnin.json"), "master": None}
-    (tmp_path / "probe").write_text("")
-    monkeypatch.setattr(earlyburn, "plan", lambda argv: fake_plan)
-    monkeypatch.setenv("TK8S_EARLY_PROBE_FD", str(w))
-    monkeypatch.setenv("TK8S_EARLY_PROBE_PID", str(reader.pid))
-    monkeypatch.setenv("TK8S_EARLY_PROBE_BIN", str(tmp_path / "probe"))
-    e = earlyburn.launch(["--answers", "a.json"])
-    try:
-        assert e is not None and e.proc.pid == reader.pid
-        text = reader.communicate(timeout=10)[0].decode()
-        assert text.splitlines()[0] == "ARG --all-devices" and text.splitlines()[-1] == "GO"
-        assert f"ARG {fake_plan['result']}" in text and "ENV ROCR_VISIBLE_DEVICES=0" in text and "LOG " in text
-        assert not any(k.startswith("TK8S_EARLY_PROBE") for k in os.environ)
-        with pytest.raises(OSError):
-            os.fstat(w)  # closed once the plan is sent
-    finally:
-        earlyburn.take()
     del ws
 
 

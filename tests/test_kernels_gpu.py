@@ -821,11 +821,11 @@ def test_pods_see_only_their_gpus_on_a_real_gpu(tmp_path):
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
 
 
-@pytest.mark.parametrize("knob", [{"TK8S_HSA_CPU_CACHES": "1"}, {"TK8S_FAULTS": "preload.kill"}],
-                         ids=["cpu-cache-walk-kept", "preloaded-burnin-killed"])
+@pytest.mark.parametrize("knob", [{"TK8S_HSA_CPU_CACHES": "1"}, {"TK8S_HOST_BURNIN": "0"}],
+                         ids=["cpu-cache-walk-kept", "no-early-burnin"])
 def test_setup_without_a_startup_shortcut_on_a_real_gpu(tmp_path, knob):
-    """with the CPU-cache-walk skip switched off, or with setup.sh's preloaded
-    burn-in killed before its plan, the bring-up takes the plain path and still validates."""
+    """with the CPU-cache-walk skip switched off, or without the early host
+    burn-in, the bring-up takes the plain path and still validates."""
     import subprocess
 
     if not torch.cuda.is_available():

@@ -41,7 +41,7 @@ def test_every_documented_off_switch_is_in_the_master_switch():
     assert named and named <= set(SHORTCUT_SWITCHES), named - set(SHORTCUT_SWITCHES)
     # and setup.sh sets the ones it acts on before any interpreter starts
     sh = (REPO / "setup.sh").read_text()
-    for k in ("TK8S_PRELOAD_BURNIN=0", "TK8S_HOST_BURNIN=0", "TK8S_NO_PYCACHE_PREFIX=1"):
+    for k in ("TK8S_HOST_BURNIN=0", "TK8S_NO_PYCACHE_PREFIX=1", "TK8S_SKIP_SITE=0"):
         assert k in sh
 
 

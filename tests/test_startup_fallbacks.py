@@ -3,8 +3,6 @@ fall back to a correct, slower bring-up when it breaks.
 
 * control-plane / node-agent zygotes (earlyburn.controlplane_zygote / agent_zygotes): an
   interpreter started early that waits for its arguments -- here never handed them;
-* the burn-in setup.sh preloads (``tk8s-hsaprobe --plan-stdin`` on fd 7) -- here killed before
-  the plan reaches it;
 * the CPU-cache-walk skip of the GPU tools (native/tools/cachewalk.h) -- here switched off with
   ``TK8S_HSA_CPU_CACHES=1`` (GPU test: tests/test_kernels_gpu.py).
 
@@ -69,42 +67,3 @@ def test_zygotes_never_handed_their_arguments_are_replaced(ws):
         assert "--await-args" not in _cmdline(child), _cmdline(child)  # the running one is a plain start
     # the other agent's zygote was handed its arguments as usual
     assert (machines / "kubenode2" / "run" / "agent.args").exists()
-
-
-def test_preloaded_burnin_killed_before_the_plan(tmp_path, monkeypatch):
-    """setup.sh's preloaded burn-in dies before the CLI writes its plan: the plan write fails,
-    the CLI spawns the burn-in itself and the run goes on with a result."""
-    from tritonk8ssupervisor_amd import earlyburn
-
-    monkeypatch.chdir(tmp_path)
-    monkeypatch.setenv("TK8S_FAKE_GPUS", "8")
-    monkeypatch.setenv("TK8S_CP_ZYGOTE", "0")
-    monkeypatch.setenv("TK8S_AGENT_ZYGOTE", "0")
-    monkeypatch.setenv("TK8S_HOST_REGISTRY", str(tmp_path / "hostreg"))
-    monkeypatch.setenv("PYTHONPATH", str(REPO))
-    (tmp_path / "answers.json").write_text(json.dumps({"nodes": 2}))
-    p = earlyburn.plan(["--answers", "answers.json", "--yes"])
-    assert p is not None
-    r, w = os.pipe()
-    pre = subprocess.Popen(["sleep", "30"], start_new_session=True)
-    pre.kill()
-    pre.wait()
-    os.close(r)  # nobody reads the plan pipe any more
-    monkeypatch.setenv("TK8S_EARLY_PROBE_FD", str(w))
-    monkeypatch.setenv("TK8S_EARLY_PROBE_PID", str(pre.pid))
-    monkeypatch.setenv("TK8S_EARLY_PROBE_BIN", p["command"][0])
-    early = earlyburn.launch(["--answers", "answers.json", "--yes"])
-    try:
-        assert early is not None and early.proc.pid != pre.pid
-        deadline = time.monotonic() + 30
-        while time.monotonic() < deadline and not Path(early.result).exists():
-            time.sleep(0.05)
-        log = Path(early.result).parent / "host-burnin.log"
-        assert Path(early.result).exists(), log.read_text() if log.exists() else "no log"
-        assert json.loads(Path(early.result).read_text())["ok"]
-    finally:
-        if early is not None:
-            early.kill()
-            early.proc.wait()
-        earlyburn.take()
-

@@ -77,15 +77,12 @@ def _pycache_prefix() -> None:
 # off-switches") off at once, the bring-up's plain path. setup.sh sets the same switches for the
 # ones it acts on before Python starts; bench.py reports this path as plain_path_s.
 SHORTCUT_SWITCHES = {
-    "TK8S_PRELOAD_BURNIN": "0",       # setup.sh's preloaded tk8s-hsaprobe
     "TK8S_HOST_BURNIN": "0",          # the early host burn-in (earlyburn.py)
     "TK8S_CP_ZYGOTE": "0",            # the control-plane zygote
     "TK8S_AGENT_ZYGOTE": "0",         # the node-agent zygotes
     "TK8S_HSA_CPU_CACHES": "1",       # ROCr's per-CPU cache walk runs as usual
     "TK8S_YAML_CACHE": "off",         # the parse caches
     "TK8S_NO_PYCACHE_PREFIX": "1",    # the shared byte-code prefix
-    "TK8S_LOCAL_PREFETCH": "0",       # the local provider's prefetch
-    "TK8S_PROVISION_SERIAL": "0",     # serial local creates
     "TK8S_PLAY_INLINE": "0",          # inline file-only tasks
     "TK8S_INPROCESS_BOOTSTRAP": "0",  # the in-process machine bootstrap
     "TK8S_FAST_ARGS": "0",            # the hand-written argument parsers (argparse instead)

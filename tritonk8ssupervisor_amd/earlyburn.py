@@ -426,63 +426,7 @@ def zygote_for(sandbox: str) -> dict | None:
     return None
 
 
-def _preloaded() -> tuple[int, int, str] | None:
-    """The burn-in setup.sh preloaded (``--plan-stdin``): (plan fd, pid, binary), taken out of
-    the environment so no child of this process sees them; the fd is not inherited either."""
-    env = os.environ
-    try:
-        fd, pid, binary = int(env.pop("TK8S_EARLY_PROBE_FD")), int(env.pop("TK8S_EARLY_PROBE_PID")), env.pop("TK8S_EARLY_PROBE_BIN")
-    except (KeyError, ValueError):
-        for k in ("TK8S_EARLY_PROBE_FD", "TK8S_EARLY_PROBE_PID", "TK8S_EARLY_PROBE_BIN"):
-            env.pop(k, None)
-        return None
-    try:
-        os.set_inheritable(fd, False)
-    except OSError:
-        return None
-    return fd, pid, binary
-
-
-def _release(pre: tuple[int, int, str] | None) -> None:
-    """No early burn-in after all: EOF on the plan pipe makes the preloaded probe exit; reap it."""
-    if pre is None:
-        return
-    try:
-        os.close(pre[0])
-    except OSError:
-        pass
-    import threading
-
-    threading.Thread(target=Spawned(pre[1]).wait, name="preload-reap", daemon=True).start()
-
-
-def _kill_preloaded(pre: tuple[int, int, str]) -> None:
-    try:
-        os.kill(pre[1], 9)
-        os.waitpid(pre[1], 0)
-    except OSError:
-        pass
-
-
-def _send_plan(pre: tuple[int, int, str], cmd: list[str], env: dict, log: str) -> bool:
-    lines = [f"ARG {a}" for a in cmd[1:]] + [f"ENV {k}={v}" for k, v in env.items()] + [f"LOG {log}", "GO"]
-    if any("\n" in ln for ln in lines):
-        return False
-    data = ("\n".join(lines) + "\n").encode()
-    try:
-        while data:
-            data = data[os.write(pre[0], data):]
-    except OSError:
-        return False
-    finally:
-        try:
-            os.close(pre[0])
-        except OSError:
-            pass
-    return True
-
-
-def _spawn_burnin(p: dict, pre) -> Early:
+def _spawn_burnin(p: dict) -> Early:
     run = os.path.join(p["state_dir"], "run")
     vis = dict(compose_visible_devices(p["gpus"]))
     vis["NODE_NAME"] = "host"
@@ -490,17 +434,11 @@ def _spawn_burnin(p: dict, pre) -> Early:
     log = os.path.join(run, "host-burnin.log")
     import time
 
-    if pre is not None and os.environ.get("TK8S_FAULTS", "").find("preload.kill") >= 0:
-        _kill_preloaded(pre)  # fault injection (tests/test_startup_fallbacks.py): dead before the plan
-    if pre is not None and os.path.realpath(pre[2]) == os.path.realpath(cmd[0]) and _send_plan(pre, cmd, vis, log):
-        pid = pre[1]  # the preloaded probe: same binary, same environment plus the plan's
-    else:
-        _release(pre)
-        pid = os.posix_spawn(cmd[0], cmd, {**os.environ, **vis}, setsid=True, file_actions=[
-            (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
-            (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
-            (os.POSIX_SPAWN_OPEN, 2, log, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644),
-        ])
+    pid = os.posix_spawn(cmd[0], cmd, {**os.environ, **vis}, setsid=True, file_actions=[
+        (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
+        (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
+        (os.POSIX_SPAWN_OPEN, 2, log, os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644),
+    ])
     spawned = time.time()
     with open(os.path.join(run, "host-burnin.pid"), "w") as f:
         f.write(f"{pid}\n")
@@ -511,24 +449,20 @@ def launch(argv: list[str]) -> Early | None:
     """Called first thing by ``./setup.sh`` (cli/fast.py) for ``setup ...``: the host burn-in
     (none for cpu-only workers) and the control-plane and node-agent zygotes."""
     global _LAUNCHED, _ZYGOTE
-    pre = _preloaded()
     try:
         p = plan(argv)
         if p is None:
-            _release(pre)
             return None
         os.makedirs(os.path.join(p["state_dir"], "run"), exist_ok=True)
         try:
             os.unlink(p["result"])
         except FileNotFoundError:
             pass
-        if p["command"] is None:  # nothing to burn in: the preloaded probe is not needed
-            _release(pre)
+        if p["command"] is None:  # nothing to burn in (cpu-only workers)
             _LAUNCHED = None
         else:
-            _LAUNCHED = _spawn_burnin(p, pre)
+            _LAUNCHED = _spawn_burnin(p)
     except Exception:  # noqa: BLE001 - an optimisation only: the orchestrator starts its own
-        _release(pre)
         return None
     try:
         _ZYGOTE = controlplane_zygote(p)

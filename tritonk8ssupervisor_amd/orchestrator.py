@@ -22,7 +22,7 @@ import threading
 import time
 from pathlib import Path
 
-from . import hcl, shortcut_on
+from . import hcl
 from .config import ClusterConfig, export_vars, read_config, write_config
 from .earlyburn import default_validation_command  # noqa: F401 - shared with the early burn-in
 from .fabric import FabricCheck, check_pmc_counters, rccl_transports, summarize_rocprof  # noqa: F401
@@ -510,8 +510,6 @@ class Setup(KubeadmPlatform, FabricCheck):
         self.events.emit("setup_start", backend=self.backend, resume=self.resume)
         if not self.resume:
             ws.save_state(completed=[], timings={}, started=time.time())
-        if not self.done("provision") and hasattr(self.provider, "prefetch") and shortcut_on("TK8S_LOCAL_PREFETCH"):
-            self.provider.prefetch()  # (local machines: the host's state, read while configuring)
         steps = [("configure", self.configure, None), ("provision", self.provision, "Starting terraform tasks..."),
                  ("ansible-config", self.ansible_config, "Creating ansible configs..."),
                  ("ansible", self.ansible, "Running ansible tasks...")]

@@ -137,21 +137,6 @@ class LocalProvider(Provider):
         return sorted(out, key=lambda p: p.name)
 
     # ---- allocation ---------------------------------------------------------------
-    def prefetch(self) -> None:
-        """Warm what the first create_machine reads under the workspace and host locks -- the
-        host's bound loopback addresses (/proc/net/{tcp,udp}) -- in a thread while the configure
-        phase runs."""
-        import threading
-
-        def warm() -> None:  # (the GPU inventory and the allocator: predict_gpus warms those)
-            try:
-                if self._multi():
-                    self._bound_ips_cached()
-            except Exception:  # noqa: BLE001 - a cache warm-up: create_machine does it all itself
-                pass
-
-        threading.Thread(target=warm, name="provider-prefetch", daemon=True).start()
-
     def _multi(self) -> bool:
         if self._multi_ip is None:
             self._multi_ip = _loopback_multi_ok()

@@ -45,14 +45,6 @@ BOOTSTRAP = ["test -d run && test -d logs && test -d pods",
 _APPEND = None
 
 
-def serial_local(provider, parallelism: int | None) -> bool:
-    """Create machines on this host one after another. A local create is a few file writes of
-    Python (no network round trip to overlap): nine threads only contend for the interpreter
-    lock, and at 8 workers the master -- whose control plane the rest of the bring-up waits
-    for -- came out of that queue ~20 ms in. Serially, master first, it is out in ~1-2 ms.
-    ``TK8S_PROVISION_SERIAL=0`` (or an explicit parallelism) restores the thread per machine."""
-    return (parallelism is None and getattr(provider, "colocated", False)
-            and os.environ.get("TK8S_PROVISION_SERIAL", "1") != "0")
 _PY3_OK: dict[tuple, tuple[int, str]] = {}
 
 
@@ -352,10 +344,6 @@ class Engine:
             self.provider.reserve([(s.attrs["name"], s.attrs["package"], list(s.attrs.get("networks", [])),
                                     (s.attrs.get("tags") or {}).get("role", "host")) for s in todo])
         workers = self.parallelism or max(1, len(todo))
-        if serial_local(self.provider, self.parallelism):
-            # master first: its control plane boots while the workers are created
-            todo.sort(key=lambda s: not s.source.rstrip("/").endswith("master"))
-            workers = 1
         with Pool(workers, "provision") as ex:
             futs = {ex.submit(self._create, s): s for s in todo}
             for f in as_completed(futs):
