@@ -97,12 +97,24 @@ def _bundler() -> str:
 def unpack(force: bool = False, verbose: bool = False) -> dict:
     """Make (or confirm) the unpacked copy. Returns what was done; never raises for a library it
     cannot unpack (not compressed, no gfx950 entry, the code object does not fit): the installed
-    one is then used as it is."""
+    one is then used as it is. One process at a time makes it (a lock beside it): inflating the
+    bundle takes ~5 GB of memory, and concurrent builds (test workers) wait for the first."""
+    import fcntl
+
     src = installed_library()
     if src is None:
         return {"ok": False, "why": "no librccl under ROCm"}
     if not force and library_dir() is not None:
         return {"ok": True, "path": str(OUT / LIB_NAME), "changed": False}
+    OUT.mkdir(parents=True, exist_ok=True)
+    with open(OUT / ".lock", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not force and library_dir() is not None:  # made by another process meanwhile
+            return {"ok": True, "path": str(OUT / LIB_NAME), "changed": False}
+        return _unpack(src, verbose)
+
+
+def _unpack(src: Path, verbose: bool) -> dict:
     sec = elf_section(src, ".hip_fatbin")
     if sec is None:
         return {"ok": False, "why": f"{src}: no .hip_fatbin section"}
