@@ -487,8 +487,11 @@ class Enforcer:
         """Prepare pod ``key``: its cgroups, and the jail options that put its processes in them
         (and on its CPUs). ``in_machine=False``: a host-scoped pod (the fabric check's one
         process over the GPUs of several machines) sits beside the machine, not inside its slice.
-        ``gpu``: the pod holds GPUs (no RLIMIT_DATA backstop: the GPU runtime maps host memory
-        for its queues and buffers)."""
+        ``gpu``: the pod holds GPUs (no RLIMIT_DATA backstop: the GPU runtime's private writable
+        reservations are not resident memory -- on the MI355X a HIP process with one GPU holds
+        ~400 MiB VmData, torch 1.44 GiB VmData for 1.0 GiB RSS, plus every pinned host buffer,
+        profiles/r5_rlimit_gpu -- and grow with the GPUs it opens, so a bound fitted to one GPU
+        would fail an 8-GPU pod at start; the sampler enforces its limit)."""
         with self.lock:
             self.limits.pop(key, None)
             self.limits[key] = lim  # (insertion order: the newest pod last, for the machine's memory)
