@@ -609,6 +609,7 @@ def main(argv=None) -> int:
     log = open(args.log, "a") if (args.log and d.rank == 0) else open(os.devnull, "w")
     b2b = args.back_to_back if args.back_to_back is not None else (0 if fake else 2)
     b2b_ready: list[float] = []
+    b2b_detail: list[dict] = []
     cold: dict | None = None
     total = args.warmup + args.steps
     census = KfdCensus().start() if d.rank == 0 else None
@@ -671,6 +672,13 @@ def main(argv=None) -> int:
                 break
             if extra:
                 b2b_ready.append(d.max(s["ready_wall_seconds"] if s else 0.0))
+                if s is not None:  # where a rebuild right after a teardown spends its extra time
+                    hb = s.get("host_burnin") or {}
+                    b2b_detail.append({"ready_s": s.get("ready_wall_seconds"), "burnin_runtime_init_ms": hb.get("runtime_init_ms"),
+                                       "burnin_total_ms": hb.get("total_ms"), "previous_teardown_s": teardown_s[-2] if len(teardown_s) > 1 else None,
+                                       "phases_s": {k: round(v, 4) for k, v in (s.get("phases") or {}).items()},
+                                       "slow_start_cause": slow_start_cause(s.get("kfd_census") or {}, hb.get("runtime_init_ms")),
+                                       "kfd_census": s.get("kfd_census")})
             if timed:
                 bad = d.bcast_obj(bool(s and s.get("post_ready_error")) if d.rank == 0 else None)
                 if bad:  # Ready was reached but the post-Ready fabric check failed: flagged, not counted
@@ -820,7 +828,7 @@ def main(argv=None) -> int:
     }
     if b2b_ready:
         out["back_to_back"] = {"steps": len(b2b_ready), "mean_s": round(sum(b2b_ready) / len(b2b_ready), 4),
-                               "max_s": round(max(b2b_ready), 4),
+                               "max_s": round(max(b2b_ready), 4), "per_step": b2b_detail,
                                "what": "./setup.sh -c && ./setup.sh with no settle pause: Ready includes the driver "
                                        "still releasing the previous bring-up's GPU processes"}
     if excluded:  # timed steps left out of value: Ready, then the post-Ready RCCL check failed

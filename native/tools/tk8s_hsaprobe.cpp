@@ -20,7 +20,10 @@
 //   tk8s-hsaprobe [--all-devices | --device D] [--gpuinfo] [--hbm-bytes B] [--md5-bytes B]
 //                 [--chunk C] [--seed S] [--copy-bytes B] [--iters K] [--mode plain|nontemporal]
 //                 [--peers [--peer-bytes B] [--peer-iters K]] [--peers-host]
-//                 [--out FILE] [--reuse FILE [--reuse-wait S]]
+//                 [--out FILE] [--reuse FILE [--reuse-wait S]] [--release-after]
+//
+// --release-after: once the result is written, free every device's queue and VRAM and shut the
+// runtime down before exiting (by default the process _exits and the driver reclaims it all).
 //
 // --peers (N7, the xGMI link check before Ready): once every device has passed its own probes,
 // each one fills a source buffer with a pattern naming it, grants every other GPU access to it
@@ -1108,6 +1111,10 @@ int main(int argc, char** argv) {
                               .kv("cpu_cache_dirs_hidden", tk8s::cachewalk::g_hidden).str());
     emit(out.str(), out_file);
     std::fflush(stdout);
+    if (a.has("release-after")) {  // after the result: the reader is not kept waiting for this
+      for (auto& r : res) delete r.dev;
+      hsa_shut_down();
+    }
     // No runtime teardown on the way out (see run_device) -- unless a tool that finalises in
     // exit handlers is attached (rocprofv3: TK8S_PROBE_CLEAN_EXIT=1).
     if (!std::getenv("TK8S_PROBE_CLEAN_EXIT")) _exit(ok ? 0 : 1);
