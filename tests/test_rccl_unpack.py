@@ -111,3 +111,28 @@ def test_transport_report_of_a_one_rank_log(tmp_path):
     assert r["p2p"] == 1 and r["logged"]
     assert rccl_transports([str(tmp_path / "none.log")]) == {"p2p": 0, "shm": 0, "net": 0, "collnet": 0,
                                                               "logged": False, "init_complete": False, "library": None}
+
+
+def test_the_fabric_rank_env_carries_the_unpacked_library_and_huge_page_malloc(monkeypatch, tmp_path):
+    """fabric.rccl_rank_env: LD_LIBRARY_PATH to the unpacked copy and glibc's malloc on huge pages
+    (profiles/r5_thp: 318 -> 202 ms communicator start), each with its own off-switch; fake GPUs
+    get neither. A GLIBC_TUNABLES already set is kept."""
+    from tritonk8ssupervisor_amd import fabric
+    from tritonk8ssupervisor_amd.utils import rccl_unpack
+
+    monkeypatch.setattr(rccl_unpack, "library_dir", lambda: tmp_path)
+    for var in ("TK8S_RCCL_THP", "GLIBC_TUNABLES", "NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "TK8S_SHORTCUTS"):
+        monkeypatch.delenv(var, raising=False)
+    env, lib = fabric.rccl_rank_env()
+    assert lib == tmp_path
+    assert {e["name"]: e["value"] for e in env} == {"LD_LIBRARY_PATH": str(tmp_path),
+                                                     "GLIBC_TUNABLES": "glibc.malloc.hugetlb=1"}
+    monkeypatch.setenv("GLIBC_TUNABLES", "glibc.malloc.arena_max=2")
+    monkeypatch.setenv("NCCL_DEBUG", "INFO")
+    env, _ = fabric.rccl_rank_env()
+    got = {e["name"]: e["value"] for e in env}
+    assert got["GLIBC_TUNABLES"] == "glibc.malloc.arena_max=2:glibc.malloc.hugetlb=1" and got["NCCL_DEBUG"] == "INFO"
+    monkeypatch.setenv("TK8S_RCCL_THP", "0")
+    assert "GLIBC_TUNABLES" not in {e["name"] for e in fabric.rccl_rank_env()[0]}
+    env, lib = fabric.rccl_rank_env(fake=True)
+    assert lib is None and [e["name"] for e in env] == ["NCCL_DEBUG"]

@@ -87,6 +87,8 @@ SHORTCUT_SWITCHES = {
     "TK8S_INPROCESS_BOOTSTRAP": "0",  # the in-process machine bootstrap
     "TK8S_FAST_ARGS": "0",            # the hand-written argument parsers (argparse instead)
     "TK8S_SKIP_SITE": "0",            # daemons' interpreters start without -S (utils/procs.plain_argv)
+    "TK8S_RCCL_UNPACKED": "0",        # the fabric Job's RCCL with its device code unpacked (utils/rccl_unpack.py)
+    "TK8S_RCCL_THP": "0",             # the fabric Job's malloc on transparent huge pages (fabric.py)
 }
 
 
