@@ -71,37 +71,42 @@ static double ms_since(std::chrono::steady_clock::time_point t) {
 
 int main(int argc, char** argv) {
   if (argc < 3) return 2;
+  const char* mode = std::getenv("COLOAD_SAMPLE");
+  const bool sample = mode != nullptr, real = sample && std::string(mode) == "real";
+  auto start_sampler = [&] {
+    void* warm[4];
+    backtrace(warm, 4);  // loads the unwinder outside the handler
+    g_n = 0;
+    struct sigaction sa{};
+    sa.sa_handler = on_prof;
+    sa.sa_flags = SA_RESTART;
+    sigaction(real ? SIGALRM : SIGPROF, &sa, nullptr);
+    itimerval it{{0, 1000}, {0, 1000}};
+    setitimer(real ? ITIMER_REAL : ITIMER_PROF, &it, nullptr);
+  };
+  auto stop_sampler = [&](const char* what) {
+    itimerval off{{0, 0}, {0, 0}};
+    setitimer(real ? ITIMER_REAL : ITIMER_PROF, &off, nullptr);
+    report(what);
+  };
+  if (sample) start_sampler();
   auto t = std::chrono::steady_clock::now();
   if (hipInit(0) != hipSuccess || hipSetDevice(0) != hipSuccess) return 3;
-  hipFree(nullptr);
-  std::printf("{\"hip_init_ms\":%.2f}\n", ms_since(t));
+  (void)hipFree(nullptr);
+  const double init_ms = ms_since(t);
+  if (sample) stop_sampler("hip_init");
+  std::printf("{\"hip_init_ms\":%.2f}\n", init_ms);
   for (int i = 2; i < argc; ++i) {
     std::ifstream f(argv[i], std::ios::binary);
     std::stringstream ss;
     ss << f.rdbuf();
     const std::string img = ss.str();
-    const char* mode = std::getenv("COLOAD_SAMPLE");
-    const bool sample = mode != nullptr, real = sample && std::string(mode) == "real";
-    if (sample) {
-      void* warm[4];
-      backtrace(warm, 4);  // loads the unwinder outside the handler
-      g_n = 0;
-      struct sigaction sa{};
-      sa.sa_handler = on_prof;
-      sa.sa_flags = SA_RESTART;
-      sigaction(real ? SIGALRM : SIGPROF, &sa, nullptr);
-      itimerval it{{0, 1000}, {0, 1000}};
-      setitimer(real ? ITIMER_REAL : ITIMER_PROF, &it, nullptr);
-    }
+    if (sample) start_sampler();
     t = std::chrono::steady_clock::now();
     hipModule_t m;
     const hipError_t e = hipModuleLoadData(&m, img.data());
     const double load_ms = ms_since(t);
-    if (sample) {
-      itimerval off{{0, 0}, {0, 0}};
-      setitimer(real ? ITIMER_REAL : ITIMER_PROF, &off, nullptr);
-      report(argv[i]);
-    }
+    if (sample) stop_sampler(argv[i]);
     double fn_ms = -1;
     if (e == hipSuccess && std::string(argv[1]) != "-") {
       t = std::chrono::steady_clock::now();
