@@ -1,0 +1,63 @@
+"""httpserver.Router compiles a route's regex only when a path with its literal prefix reaches it
+(the control plane's ~120 routes were 3.8 ms of its start on the MI355X host). The lazy router
+must answer exactly as trying every compiled route in order would."""
+from __future__ import annotations
+
+import re
+
+import pytest
+
+from tritonk8ssupervisor_amd.controlplane.httpserver import HttpError, Router, _literal_prefix
+
+
+@pytest.mark.parametrize("pattern,prefix", [
+    (r"/(ping|healthz)?", "/"), (r"/api/?", "/api"), (r"/v1/kv/(?P<key>.+)", "/v1/kv/"),
+    (r"/apis/metrics.k8s.io/v1beta1/?", "/apis/metrics"), (r"/api/v1/nodes", "/api/v1/nodes"),
+    (r"/a+b", "/a"), (r"/x{2}", "/"), (r"/p*q", "/"), (r"/\.well-known", "/"), (r"/a[bc]", "/a"),
+])
+def test_literal_prefix(pattern, prefix):
+    assert _literal_prefix(pattern) == prefix
+    assert all(m.startswith(prefix) for m in ("/", "/api", "/aab") if re.fullmatch(pattern, m))
+
+
+def _eager(routes, method, path):
+    allowed = False
+    for m, _, pat, _, h in routes:
+        mt = re.compile("^" + pat + "$").match(path)
+        if mt:
+            if m == method or (m == "GET" and method == "HEAD"):
+                return h, mt.groupdict()
+            allowed = True
+    return 405 if allowed else 404
+
+
+def test_the_control_planes_routes_answer_as_eager_matching(tmp_path):
+    from tritonk8ssupervisor_amd.controlplane.server import ControlPlane
+
+    cp = ControlPlane("127.0.0.1", 0, str(tmp_path), 5.0, None, 0, 0)
+    assert all(r[3] is None for r in cp.router.routes)  # nothing compiled up front
+    paths = ["/", "/ping", "/healthz", "/version", "/metrics", "/api", "/api/", "/api/v1", "/api/v1/nodes",
+             "/api/v1/nodes/x", "/api/v1/nodes/x/status", "/apis/apps/v1", "/apis/metrics.k8s.io/v1beta1",
+             "/apis/metricsXk8s.io/v1beta1", "/v1/kv/a/b/c", "/v1/cluster/wait", "/v1/scripts/t:1:s",
+             "/r/projects/1a7/kubernetes/api/v1/namespaces/default/pods", "/r/projects/1a7/kubernetes-dashboard:9090",
+             "/api/v1/namespaces/kube-system/pods/p/log", "/api/v1/namespaces/ns/pods/p/status",
+             "/apis/batch/v1/namespaces/ns/jobs/j", "/openapi/v3/apis/apps/v1", "/v2-beta/projects/1a7", "/nope",
+             "/api/v1/watch/pods", "/apis/apps/v1/namespaces/kube-system/daemonsets"]
+    for method in ("GET", "POST", "PUT", "DELETE", "PATCH", "HEAD"):
+        for path in paths:
+            try:
+                got = cp.router.match(method, path)
+            except HttpError as e:
+                got = e.status
+            want = _eager(cp.router.routes, method, path)
+            assert got == want, (method, path)
+
+
+def test_a_route_added_later_still_matches_in_order():
+    r = Router()
+    r.add("GET", r"/a/(?P<x>[^/]+)", "first")
+    r.add("GET", r"/a/b", "second")
+    assert r.match("GET", "/a/b") == ("first", {"x": "b"})
+    with pytest.raises(HttpError) as e:
+        r.match("POST", "/a/b")
+    assert e.value.status == 405

@@ -536,6 +536,7 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
 
     # ---- run --------------------------------------------------------------------------
     async def run(self, ready_file: str | None = None) -> None:
+        trace("cp", "event loop up")
         if self.state_dir:
             self.state_dir.mkdir(parents=True, exist_ok=True)
             restored = self.store.restore(self.state_dir / "controlplane.json")
@@ -547,6 +548,7 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
                 # names the server derives from its sequence never repeat one it handed out before
                 self._seq = max(self._seq, self.store.rv) + 1000
         self._ensure_templates()
+        trace("cp", "state ready")
         host, port = await self.http.start(self.host, self.port)
         self.port = port
         if self.store.keys("services"):
@@ -651,6 +653,7 @@ def main(argv: list[str] | None = None) -> int:
         a = vars(ap.parse_args(argv))
     cp = ControlPlane(a["host"], a["port"], a["state_dir"], a["node_grace"], a["advertise"], a["dns_port"],
                       a["ingress_port"])
+    trace("cp", "constructed")
     asyncio.run(cp.run(a["ready_file"]))
     return 0
 
