@@ -14,9 +14,11 @@ and their start-up time is part of the bring-up metric.
 __version__ = "0.1.0"
 
 
-# optional modules the stdlib probes for on Linux (subprocess: msvcrt, _winapi; ntpath: nt, ...)
+# optional modules the stdlib probes for on Linux (subprocess: msvcrt, _winapi; ntpath: nt, ...;
+# copy and pickle: Jython's org.python.core -- an "org" namespace package in site-packages made
+# that probe load `site` and three packages, ~2.6 ms of the first `import copy`)
 _PLATFORM_PROBES = frozenset({"msvcrt", "_winapi", "nt", "winreg", "_winreg", "_overlapped", "_scproxy", "vms_lib",
-                              "java", "_wmi"})
+                              "java", "_wmi", "org"})
 
 
 def _fast_site() -> None:
