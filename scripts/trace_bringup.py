@@ -41,8 +41,10 @@ def one(root: Path, nodes: int, package: str = "mi355x-1gpu", rccl: str = "off")
             out.append((float("nan"), "setup", line))
     for line in (root / ".tk8s" / "events.jsonl").read_text().splitlines():
         e = json.loads(line)
-        what = e["event"] + "".join(f" {k}={e[k]}" for k in ("phase", "task", "name") if k in e)
-        out.append(((e["ts"] - t0) * 1000, "setup", what[:110]))
+        what = (e["event"] + "".join(f" {k}={e[k]}" for k in ("phase", "task", "name") if k in e))[:110]
+        if e.get("timing_ms"):  # the module's own breakdown (facts gathering, tk8s_kube, ...)
+            what += " " + json.dumps(e["timing_ms"], separators=(",", ":"))
+        out.append(((e["ts"] - t0) * 1000, "setup", what))
     for log in (root / ".tk8s").rglob("*"):
         if not log.is_file() or log.suffix in (".json", ".jsonl", ".pid", ".lock"):
             continue

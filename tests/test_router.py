@@ -1,13 +1,14 @@
-"""httpserver.Router compiles a route's regex only when a path with its literal prefix reaches it
-(the control plane's ~120 routes were 3.8 ms of its start on the MI355X host). The lazy router
-must answer exactly as trying every compiled route in order would."""
+"""httpserver.Router matches plain segment patterns without a regex and compiles the others on
+first use (compiling the control plane's ~120 routes up front was 3.8 ms of its start on the
+MI355X host). It must answer as trying every route's regex in order would -- with dots in
+literal segments taken literally."""
 from __future__ import annotations
 
 import re
 
 import pytest
 
-from tritonk8ssupervisor_amd.controlplane.httpserver import HttpError, Router, _literal_prefix
+from tritonk8ssupervisor_amd.controlplane.httpserver import HttpError, Router, _literal_prefix, _segments
 
 
 @pytest.mark.parametrize("pattern,prefix", [
@@ -22,8 +23,8 @@ def test_literal_prefix(pattern, prefix):
 
 def _eager(routes, method, path):
     allowed = False
-    for m, _, pat, _, h in routes:
-        mt = re.compile("^" + pat + "$").match(path)
+    for m, _, pat, _, h, _ in routes:
+        mt = re.compile("^" + re.sub(r"\.(?!\+)", r"\\.", pat) + "$").match(path)
         if mt:
             if m == method or (m == "GET" and method == "HEAD"):
                 return h, mt.groupdict()
@@ -36,13 +37,17 @@ def test_the_control_planes_routes_answer_as_eager_matching(tmp_path):
 
     cp = ControlPlane("127.0.0.1", 0, str(tmp_path), 5.0, None, 0, 0)
     assert all(r[3] is None for r in cp.router.routes)  # nothing compiled up front
+    assert sum(_segments(r[2]) is None for r in cp.router.routes) <= 4  # nearly all are plain segments
     paths = ["/", "/ping", "/healthz", "/version", "/metrics", "/api", "/api/", "/api/v1", "/api/v1/nodes",
              "/api/v1/nodes/x", "/api/v1/nodes/x/status", "/apis/apps/v1", "/apis/metrics.k8s.io/v1beta1",
              "/apis/metricsXk8s.io/v1beta1", "/v1/kv/a/b/c", "/v1/cluster/wait", "/v1/scripts/t:1:s",
              "/r/projects/1a7/kubernetes/api/v1/namespaces/default/pods", "/r/projects/1a7/kubernetes-dashboard:9090",
              "/api/v1/namespaces/kube-system/pods/p/log", "/api/v1/namespaces/ns/pods/p/status",
              "/apis/batch/v1/namespaces/ns/jobs/j", "/openapi/v3/apis/apps/v1", "/v2-beta/projects/1a7", "/nope",
-             "/api/v1/watch/pods", "/apis/apps/v1/namespaces/kube-system/daemonsets"]
+             "/api/v1/watch/pods", "/apis/apps/v1/namespaces/kube-system/daemonsets", "/api/v1/nodes/",
+             "/apis/apps/v1/namespaces/ns/deployments/d/scale", "/apis/apps/v1/namespaces/ns/jobs/d/scale",
+             "/api/v1/namespaces//pods", "/apis//v1/x", "/v1/kv/", "/api/v1/", "/apis/apps/", "/apis/apps/v1/",
+             "/r/projects/1a7/kubernetes/apis/metrics.k8s.io/v1beta1/", "/openapi/v3/api/v1", "no-slash"]
     for method in ("GET", "POST", "PUT", "DELETE", "PATCH", "HEAD"):
         for path in paths:
             try:
@@ -61,3 +66,24 @@ def test_a_route_added_later_still_matches_in_order():
     with pytest.raises(HttpError) as e:
         r.match("POST", "/a/b")
     assert e.value.status == 405
+
+
+@pytest.mark.parametrize("pattern,spec", [
+    (r"/api/v1/nodes", ((("lit", "api"), ("lit", "v1"), ("lit", "nodes")), False)),
+    (r"/api/?", ((("lit", "api"),), True)),
+    (r"/v1/kv/(?P<key>.+)", ((("lit", "v1"), ("lit", "kv"), ("rest", "key")), False)),
+    (r"/a/(?P<k>x|y)/(?P<n>[^/]+)", ((("lit", "a"), ("choice", "k", frozenset({"x", "y"})), ("param", "n")), False)),
+    (r"/(ping|healthz)?", None), (r"/o/(?P<gv>api/[^/]+|apis/[^/]+/[^/]+)", None), (r"/x/(?P<r>.+)/?", None),
+])
+def test_segment_specs(pattern, spec):
+    assert _segments(pattern) == spec
+
+
+def test_routes_added_after_a_match_are_seen():
+    r = Router()
+    r.add("GET", r"/a/b", "ab")
+    assert r.match("GET", "/a/b")[0] == "ab"
+    r.add("GET", r"/c/(?P<x>[^/]+)", "c")
+    r.add("GET", r"/(ping|healthz)?", "ping")
+    assert r.match("GET", "/c/1") == ("c", {"x": "1"})
+    assert r.match("GET", "/healthz")[0] == "ping" and r.match("GET", "/")[0] == "ping"

@@ -168,32 +168,120 @@ class HttpError(Exception):
 Handler = Callable[..., Awaitable[Response | Any]]
 
 
+_PREFIX = re.compile(r"[^.^$*+?{}\[\]|()\\]*")
+
+
 def _literal_prefix(pattern: str) -> str:
     """The literal text every match of ``pattern`` starts with: up to the first regex
     metacharacter, less a character a quantifier makes optional."""
-    out: list[str] = []
-    for ch in pattern:
-        if ch in "*?{":
-            if out:
-                out.pop()
-            break
-        if ch in ".^$+[]|()\\":
-            break
-        out.append(ch)
-    return "".join(out)
+    n = _PREFIX.match(pattern).end()
+    if n and n < len(pattern) and pattern[n] in "*?{":
+        n -= 1
+    return pattern[:n]
+
+
+_SEG = re.compile(r"/((?:\([^()]*\)|[^/()])*)")      # one path segment; a group may hold "/"
+_LIT = re.compile(r"[A-Za-z0-9_.:\-]+")
+_GROUP = re.compile(r"\(\?P<(\w+)>(.*)\)")
+_CHOICE = re.compile(r"[A-Za-z0-9_\-]+(?:\|[A-Za-z0-9_\-]+)*")
+
+
+def _segments(pattern: str):
+    """A path pattern made of ``/``-separated literal segments (dots taken literally), named
+    segments ``(?P<n>[^/]+)``, named choices ``(?P<n>a|b)`` and a final ``(?P<n>.+)``, with an
+    optional trailing ``/?``, as ``(spec, trailing_slash_allowed)``; None for anything else
+    (matched as a regex)."""
+    trailing = pattern.endswith("/?")
+    body = pattern[:-2] if trailing else pattern
+    parts = _SEG.findall(body)
+    if not parts or "".join("/" + x for x in parts) != body:
+        return None
+    spec = []
+    last = len(parts) - 1
+    for i, part in enumerate(parts):
+        g = _GROUP.fullmatch(part)
+        if g is not None:
+            name, expr = g.groups()
+            if expr == "[^/]+":
+                spec.append(("param", name))
+            elif expr == ".+" and i == last and not trailing:
+                spec.append(("rest", name))
+            elif _CHOICE.fullmatch(expr):
+                spec.append(("choice", name, frozenset(expr.split("|"))))
+            else:
+                return None
+        elif _LIT.fullmatch(part):
+            spec.append(("lit", part))
+        else:
+            return None
+    return tuple(spec), trailing
+
+
+def _match_segments(spec, segs: list[str]):
+    out = {}
+    for i, s in enumerate(spec):
+        if s[0] == "rest":
+            rest = "/".join(segs[i:])
+            if not rest:
+                return None
+            out[s[1]] = rest
+            return out
+        if i >= len(segs):
+            return None
+        seg = segs[i]
+        if s[0] == "lit":
+            if seg != s[1]:
+                return None
+        elif s[0] == "param":
+            if not seg:
+                return None
+            out[s[1]] = seg
+        elif seg not in s[2]:
+            return None
+        else:
+            out[s[1]] = seg
+    return out if len(segs) == len(spec) else None
+
+
+_UNSET = object()
 
 
 class Router:
-    """Method + path-pattern routes, tried in order. A route's regex is compiled the first time a
-    path carrying its literal prefix reaches it: building the control plane's ~120 routes up
-    front was 3.8 ms of the daemon's start on the MI355X host (profiles/r5_cp_trace/), on the
-    bring-up's critical path, and most routes never see a request during a bring-up."""
+    """Method + path-pattern routes, tried in order. Patterns built from plain segments (nearly
+    all of the control plane's ~120) are matched segment by segment, without a regex; the rest
+    are compiled. Either form is worked out the first time a path carrying the route's literal
+    prefix reaches it. Compiling
+    every route up front was 3.8 ms of the daemon's start on the MI355X host
+    (profiles/r5_cp_trace/), and compiling on first use moved most of it into the bring-up's
+    first workload request -- both on its critical path."""
 
     def __init__(self):
-        self.routes: list[list] = []   # [method, literal prefix, pattern, compiled or None, handler]
+        # [method, literal prefix, pattern, compiled regex or None, handler, segment spec or None
+        #  (_UNSET until a path first reaches the route)]
+        self.routes: list[list] = []
+        self._by_first: dict[str, list[list]] | None = None  # first path segment -> its routes, in order
+        self._any_first: list[list] = []                      # routes whose first segment is not literal
 
     def add(self, method: str, pattern: str, handler: Handler) -> None:
-        self.routes.append([method, _literal_prefix(pattern), pattern, None, handler])
+        self.routes.append([method, _literal_prefix(pattern), pattern, None, handler, _UNSET])
+        self._by_first = None
+
+    @staticmethod
+    def _first(prefix: str, pattern: str) -> str | None:
+        """The route's literal first path segment, or None when a path of any first segment could
+        match it."""
+        if not prefix.startswith("/"):
+            return None
+        end = prefix.find("/", 1)
+        if end > 0:
+            return prefix[1:end]
+        return prefix[1:] if prefix == pattern and len(prefix) > 1 else None
+
+    def _index(self) -> None:
+        firsts = [self._first(r[1], r[2]) for r in self.routes]
+        keys = {f for f in firsts if f is not None}
+        self._by_first = {k: [r for r, f in zip(self.routes, firsts) if f is None or f == k] for k in keys}
+        self._any_first = [r for r, f in zip(self.routes, firsts) if f is None]
 
     def route(self, method: str, pattern: str):
         def deco(fn):
@@ -203,18 +291,38 @@ class Router:
 
     def match(self, method: str, path: str):
         allowed = False
-        for r in self.routes:
+        segs = path.split("/")[1:] if path.startswith("/") else None
+        segs_t = segs[:-1] if segs and len(segs) > 1 and segs[-1] == "" else segs
+        if self._by_first is None:
+            self._index()
+        routes = self._by_first.get(segs[0], self._any_first) if segs else self._any_first
+        for r in routes:
             if not path.startswith(r[1]):
                 continue
-            rx = r[3]
-            if rx is None:
-                rx = r[3] = re.compile("^" + r[2] + "$")
-            mt = rx.match(path)
-            if mt:
-                m = r[0]
-                if m == method or (m == "GET" and method == "HEAD"):
-                    return r[4], {k: unquote(v) for k, v in mt.groupdict().items()}
-                allowed = True
+            seg = r[5]
+            if seg is _UNSET:
+                seg = r[5] = _segments(r[2])
+            if seg is not None:
+                if segs is None:
+                    continue
+                ps = segs_t if seg[1] else segs
+                if len(ps) != len(seg[0]) and seg[0][-1][0] != "rest":
+                    continue
+                groups = _match_segments(seg[0], ps)
+                if groups is None:
+                    continue
+            else:
+                rx = r[3]
+                if rx is None:
+                    rx = r[3] = re.compile("^" + r[2] + "$")
+                mt = rx.match(path)
+                if not mt:
+                    continue
+                groups = mt.groupdict()
+            m = r[0]
+            if m == method or (m == "GET" and method == "HEAD"):
+                return r[4], {k: unquote(v) for k, v in groups.items()}
+            allowed = True
         if allowed:
             raise HttpError(405, f"method {method} not allowed on {path}")
         raise HttpError(404, f"no route for {method} {path}")

@@ -672,16 +672,26 @@ def _artefacts(bn) -> dict:
 
 def m_tk8s_kube(args, *, ctx, check, **_):
     """api, project, token (the control plane's admin token), state present|absent|wait,
-    definition|src, timeout."""
-    from .controlplane.client import ApiError, Client
+    definition|src, timeout. The result's ``timing_ms`` says where the task's time went (the
+    validation DaemonSet's deploy is on the bring-up's critical path)."""
+    t0 = time.perf_counter()
+    timing: dict[str, float] = {}
+
+    def mark(part: str) -> None:
+        nonlocal t0
+        t = time.perf_counter()
+        timing[part] = round((t - t0) * 1e3, 3)
+        t0 = t
+
+    from .controlplane.client import ApiError, Client, client_from_kubeconfig
     from .kube import apply_objects, delete_objects, load_manifests
 
-    from .controlplane.client import client_from_kubeconfig
-
+    mark("import")
     if "definition" in args:
         objs = args["definition"] if isinstance(args["definition"], list) else [args["definition"]]
     else:
         objs = load_manifests(_path(args["src"], ctx, None, True), args.get("vars") or {})
+    mark("manifests")
     state = args.get("state", "present")
     if check:
         return {"changed": state != "wait", "objects": len(objs), "msg": "check mode"}
@@ -690,12 +700,15 @@ def m_tk8s_kube(args, *, ctx, check, **_):
     kc = Client(api, token=str(args["token"]) if args.get("token") else None).get(
         f"/env/{pid}/kubernetes/kubectl", query={"format": "json"})
     k = client_from_kubeconfig(kc)
+    mark("kubeconfig")
     try:
         if state == "absent":
             n = delete_objects(k, objs)
-            return {"changed": n > 0, "deleted": n}
+            mark("delete")
+            return {"changed": n > 0, "deleted": n, "timing_ms": timing}
         res = apply_objects(k, objs)
-        return {"changed": any(r["created"] for r in res), "objects": res}
+        mark("apply")
+        return {"changed": any(r["created"] for r in res), "objects": res, "timing_ms": timing}
     except ApiError as e:
         return {"failed": True, "msg": str(e)}
 
