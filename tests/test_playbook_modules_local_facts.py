@@ -32,3 +32,20 @@ def test_facts_gathering_reports_where_its_time_went():
     t2: dict = {}
     ex_mod.LocalExecutor(None, ms).facts("a", t2)
     assert "lock_wait" in t2 and "gpu_inventory" in t2
+
+
+def test_rocm_version_comes_from_the_install_directory_name(tmp_path):
+    """The cold first run's 0.8 s was the first read of .info/version on a fresh GPU box (its
+    image pages files in on first read): the versioned directory's name is read instead."""
+    from tritonk8ssupervisor_amd.nodefacts import rocm_version
+
+    real = tmp_path / "rocm-7.2.0"
+    (real / ".info").mkdir(parents=True)
+    (real / ".info" / "version").write_text("should-not-be-read\n")
+    (tmp_path / "rocm").symlink_to(real)
+    assert rocm_version(tmp_path / "rocm") == "7.2.0"
+    plain = tmp_path / "rocm-dev"
+    (plain / ".info").mkdir(parents=True)
+    (plain / ".info" / "version").write_text("6.4.1-120\n")
+    assert rocm_version(plain) == "6.4.1-120"
+    assert rocm_version(tmp_path / "missing") == ""

@@ -18,6 +18,24 @@ PKG = Path(__file__).resolve().parent
 NATIVE_TOOLS = ("tk8s-gpuinfo", "tk8s-probe", "tk8s-rccl")
 
 
+def rocm_version(root: str | os.PathLike | None = None) -> str:
+    """The installed ROCm version, from the install directory's name when it carries one
+    (``/opt/rocm`` -> ``/opt/rocm-7.2.0``: a symlink, metadata only) and from ``.info/version``
+    otherwise. On the GPU hosts the image's files are paged in on their first read: on a fresh
+    box the first read of ``.info/version`` took 0.80 s of the first bring-up's critical path
+    (node facts, play 1; ``profiles/r5_cold_facts/``) -- the cold first run of BENCH_r04."""
+    import re
+
+    base = Path(root or os.environ.get("ROCM_PATH", "/opt/rocm"))
+    m = re.fullmatch(r"rocm-(\d+\.\d+\.\d+)", os.path.basename(os.path.realpath(base)))
+    if m:
+        return m.group(1)
+    try:
+        return (base / ".info" / "version").read_text().strip()
+    except OSError:
+        return ""
+
+
 def node_facts(timing: dict | None = None) -> dict:
     """The facts; ``timing`` (when given) receives how long each part took, in ms: a slow
     gathering on the bring-up's critical path names its part (bench.py's cold first run)."""
@@ -35,11 +53,7 @@ def node_facts(timing: dict | None = None) -> dict:
     from .models.hostinfo import discover
 
     mark("import")
-    ver = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / ".info" / "version"
-    try:
-        rocm = ver.read_text().strip()
-    except OSError:
-        rocm = ""
+    rocm = rocm_version()
     mark("rocm_version")
     kfd = os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK | os.W_OK)
     mark("kfd_access")
