@@ -469,3 +469,39 @@ def test_signals_go_only_to_the_processes_the_scan_saw():
     finally:
         if p.poll() is None:
             p.kill()
+
+
+def test_a_restarted_agent_ends_what_a_killed_one_left_behind(tmp_path):
+    """runtime.reap_leftovers: an agent killed outright runs no stop_all, and its duty cycle may
+    have left a pod SIGSTOPped; the next agent of the machine SIGCONTs and SIGKILLs each group
+    its pidfile still names -- and leaves a pid that now belongs to another process alone."""
+    import json
+    import os
+    import signal
+    import subprocess
+    import time
+
+    from tritonk8ssupervisor_amd.agent.runtime import reap_leftovers
+    from tritonk8ssupervisor_amd.utils.procs import proc_start_ticks
+
+    pods = tmp_path / "pods"
+    (pods / "a").mkdir(parents=True)
+    (pods / "b").mkdir(parents=True)
+    left = subprocess.Popen(["sleep", "60"], start_new_session=True)
+    other = subprocess.Popen(["sleep", "60"], start_new_session=True)
+    try:
+        os.kill(left.pid, signal.SIGSTOP)
+        (pods / "a" / "pod.pid").write_text(json.dumps({"pid": left.pid, "pgid": left.pid,
+                                                        "start": proc_start_ticks(left.pid)}))
+        (pods / "b" / "pod-side.pid").write_text(json.dumps({"pid": other.pid, "pgid": other.pid, "start": 1}))
+        assert reap_leftovers(pods) == [left.pid]
+        assert left.wait(timeout=10) == -signal.SIGKILL
+        time.sleep(0.05)
+        assert other.poll() is None  # start ticks differ: not the process the pidfile named
+        assert not list(pods.glob("*/*.pid"))
+        assert reap_leftovers(pods) == []
+    finally:
+        for p in (left, other):
+            if p.poll() is None:
+                p.kill()
+                p.wait()

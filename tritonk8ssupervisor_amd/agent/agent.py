@@ -1198,6 +1198,11 @@ class Agent:
 
     def run(self, await_url: Path | None = None) -> int:
         install_sigterm()
+        from .runtime import reap_leftovers
+
+        left = reap_leftovers(self.sandbox / "pods")  # an earlier agent of this machine was killed
+        if left:
+            print(f"{self.name}: ended {len(left)} process group(s) a previous agent left running: {left}", flush=True)
         threading.Thread(target=self._probe_isolation, name="isolation-probe", daemon=True).start()
         if self.device_plugin == "grpc":  # before the URL wait: off the join's critical path
             self.start_grpc_plugin()

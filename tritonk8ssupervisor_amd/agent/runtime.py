@@ -435,6 +435,30 @@ def _join_limits(pid: int, opts: list[str]) -> None:
             pass
 
 
+def reap_leftovers(pods_dir: Path) -> list[int]:
+    """A (re)starting agent's first act: the process groups an earlier agent of this machine
+    started and left behind -- it was killed, so no ``stop_all`` ran -- are ended, each only while
+    it is still the process its pidfile names (pid and start ticks; a reused pid is left alone).
+    SIGCONT goes first: the watchdog's CPU duty cycle may have left them SIGSTOPped, and a stopped
+    group would otherwise hold its GPUs and memory forever. The pods themselves come back from
+    the control plane's desired state, so a leftover would only run twice. Returns the groups."""
+    ended = []
+    for pf in sorted(Path(pods_dir).glob("*/*.pid")):
+        try:
+            rec = json.loads(pf.read_text())
+            pgid, start = int(rec.get("pgid") or rec["pid"]), rec.get("start")
+        except (OSError, ValueError, KeyError, TypeError):
+            continue
+        if start is not None and proc_start_ticks(pgid) == start:
+            for sig in (signal.SIGCONT, signal.SIGKILL):
+                with contextlib.suppress(ProcessLookupError, PermissionError):
+                    os.killpg(pgid, sig)
+            ended.append(pgid)
+        with contextlib.suppress(OSError):
+            pf.unlink()
+    return ended
+
+
 def _pidfile(pp: PodProc) -> str:
     return "pod.pid" if pp.log_name == "log" else f"pod-{pp.name}.pid"
 
