@@ -817,6 +817,10 @@ def main(argv=None) -> int:
         "hip_init_ms_steps": hip_init,
         "settle_s": settle,
         "burnin_runtime_init_ms_steps": [(s.get("host_burnin") or {}).get("runtime_init_ms") for s in summaries],
+        "burnin_runtime_steps": [(s.get("host_burnin") or {}).get("runtime") for s in summaries],
+        "burnin_device_wall_ms_max_steps": [max((s.get("host_burnin") or {}).get("device_wall_ms") or [0.0]) or None
+                                            for s in summaries],
+        "burnin_peers_ms_steps": [(s.get("host_burnin") or {}).get("peers_ms") for s in summaries],
         "burnin_total_ms_steps": [(s.get("host_burnin") or {}).get("total_ms") for s in summaries],
         "burnin_spawn_ms_steps": [s.get("burnin_spawn_ms") for s in summaries],
         "burnin_exec_ms_steps": [s.get("burnin_exec_ms") for s in summaries],

@@ -567,7 +567,13 @@ class Setup(KubeadmPlatform, FabricCheck):
                                            "peers_ms": t.get("peers"), "total_ms": t.get("total"),
                                            "spawned_unix": hb.spawned_unix or None,
                                            "main_unix_ms": t.get("main_unix_ms"),
-                                           "seen_unix": getattr(hb, "seen_unix", 0.0) or None}
+                                           "seen_unix": getattr(hb, "seen_unix", 0.0) or None,
+                                           # which payload ran (the HSA one on 1 GPU, the HIP one for
+                                           # xGMI pulls) and each GPU's own time: where an N-GPU
+                                           # bring-up's burn-in went (the driver's SCALE runs)
+                                           "runtime": (hb.result or {}).get("runtime", "hip"),
+                                           "device_wall_ms": [round(d.get("wall_ms") or 0.0, 2)
+                                                              for d in (hb.result or {}).get("devices", [])]}
             if hb.xgmi is not None:
                 self.summary["xgmi"] = {k: hb.xgmi[k] for k in ("pulls", "median_gbps", "min_gbps", "floor_gbps",
                                                                  "min_fraction")}
