@@ -853,7 +853,7 @@ def main(argv=None) -> int:
             "what": "--rccl on: wall-clock from launching ./setup.sh to its exit after the RCCL all-reduce Job "
                     "over every GPU passed its exact check",
             "rccl": {k: last_rccl.get(k) for k in ("ok", "nranks", "pods", "comm_init_ms_max", "sweep_ms_max", "init_spread_ms", "rccl_library",
-                                                   "peak_busbw_gbps", "transport", "prestarted")}})
+                                                   "peak_busbw_gbps", "transport")}})
     print(json.dumps(out), flush=True)
     return 0
 
