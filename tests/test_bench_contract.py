@@ -60,7 +60,8 @@ def test_bench_single_process(tmp_path):
 
     t0 = time.monotonic()
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", "2", "--warmup", "1",
-                        "--fake-gpus", "2", "--curve-steps", "2", "--plain-steps", "2", "--fabric-steps", "1"],
+                        "--fake-gpus", "2", "--curve-steps", "2", "--plain-steps", "2", "--fabric-steps", "1",
+                        "--back-to-back", "1"],
                        cwd=REPO, env=_env(tmp_path), capture_output=True, text=True, timeout=280)
     run_wall = time.monotonic() - t0
     assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
@@ -101,6 +102,12 @@ def test_bench_single_process(tmp_path):
     # launch -> a passing RCCL all-reduce Job (gloo ranks on the fake GPUs)
     fv = out["fabric_validated"]
     assert out["fabric_validated_s"] >= fv["ready"]["mean_s"] > 0 and fv["rccl"]["ok"] is True and fv["steps"] == 1
+    # round 5: a rebuild right after a teardown names where its extra time went, and every step
+    # says which burn-in payload ran and how long its slowest GPU took
+    b2b = out["back_to_back"]
+    assert b2b["steps"] == 1 and len(b2b["per_step"]) == 1 and p.stderr.count("(back-to-back)") == 1
+    assert {"ready_s", "burnin_runtime_init_ms", "previous_teardown_s", "phases_s", "kfd_census"} <= set(b2b["per_step"][0])
+    assert len(out["burnin_runtime_steps"]) == len(out["burnin_device_wall_ms_max_steps"]) == 2
 
 
 @pytest.mark.timeout(400)
