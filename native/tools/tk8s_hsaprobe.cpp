@@ -17,7 +17,7 @@
 // memory by a last kernel, so no SDMA engine and no host-memory atomics are involved.
 // Kernel times are GPU timestamps of the dispatches (hsa_amd_profiling_get_dispatch_time).
 //
-//   tk8s-hsaprobe [--all-devices | --device D] [--gpuinfo] [--hbm-bytes B] [--md5-bytes B]
+//   tk8s-hsaprobe [--all-devices | --device D | --devices D,D,...] [--gpuinfo] [--hbm-bytes B] [--md5-bytes B]
 //                 [--chunk C] [--seed S] [--copy-bytes B] [--iters K] [--mode plain|nontemporal]
 //                 [--peers [--peer-bytes B] [--peer-iters K]] [--peers-host]
 //                 [--out FILE] [--reuse FILE [--reuse-wait S]] [--release-after]
@@ -1021,6 +1021,23 @@ int main(int argc, char** argv) {
     std::vector<int> devices;
     if (a.has("all-devices")) {
       for (int d = 0; d < n; ++d) devices.push_back(d);
+    } else if (a.has("devices")) {
+      // An explicit list; a device may repeat (two queues and arenas on one GPU): on a one-GPU
+      // box that runs the multi-device path -- threads, peer grants, rounds of pulls -- end to end.
+      const std::string list = a.str("devices");
+      size_t pos = 0;
+      while (pos <= list.size()) {
+        const size_t end = std::min(list.find(',', pos), list.size());
+        const std::string item = list.substr(pos, end - pos);
+        char* tail = nullptr;
+        const long d = std::strtol(item.c_str(), &tail, 10);
+        if (item.empty() || *tail != '\0' || d < 0 || d >= n) {
+          emit("{\"ok\":false,\"error\":\"bad --devices " + list + "\"}", out_file);
+          return 2;
+        }
+        devices.push_back(static_cast<int>(d));
+        pos = end + 1;
+      }
     } else {
       const int d = static_cast<int>(a.num("device", 0));
       if (d < 0 || d >= n) {

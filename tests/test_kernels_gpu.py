@@ -646,6 +646,33 @@ def test_hsaprobe_pull_from_granted_non_local_memory(nat):
     assert 1.0 < hp["kernel_gbps"] < 1000.0, hp  # PCIe/host-link rate, not a local-HBM copy
 
 
+def test_hsaprobe_multi_device_path_on_one_gpu(nat):
+    """--devices 0,0,0: three queues and arenas on the one GPU run the multi-device path end to
+    end -- a thread per device, the peer grants (hsa_amd_agents_allow_access on each source
+    arena for the other devices' agents), two rounds of pulls at system-scope acquire, each
+    checked against its source's pattern -- and the result splits and judges as a host burn-in's
+    would (burnin.split_host_result, xgmi.link_report). Only the cross-GPU mapping itself needs
+    a second GPU."""
+    from tritonk8ssupervisor_amd.burnin import split_host_result
+    from tritonk8ssupervisor_amd.xgmi import link_report
+
+    rc, out = _hsaprobe("--devices", "0,0,0", "--gpuinfo", "--peers", "--peer-bytes", str(16 << 20),
+                        "--hbm-bytes", str(256 << 20), "--md5-bytes", str(16 << 20), "--copy-bytes", str(16 << 20),
+                        "--iters", "2")
+    assert rc == 0 and out["ok"], out
+    assert out["peer_rounds"] == 2 and [d["device"] for d in out["devices"]] == [0, 0, 0]
+    for d in out["devices"]:
+        assert d["ok"] and d["peers_ok"] and len(d["peers"]) == 2, d
+        for p in d["peers"]:
+            assert p["ok"] and p["access"] == "allowed" and p["bad_words"] == 0 and p["kernel_gbps"] > 50, p
+    rep = link_report(out, [0, 1, 2])
+    assert rep["pulls"] == 6 and not rep["degraded"], rep
+    share = split_host_result(out, [0, 1, 2], [0], rep)  # (every entry names GPU 0)
+    assert share is not None and share["ok"] and share["device_count"] == 1
+    rc, bad = _hsaprobe("--devices", "0,x", "--iters", "1")
+    assert rc == 2 and not bad["ok"] and "--devices" in bad["error"]
+
+
 def test_hsaprobe_md5_unpinned_for_other_inputs(nat):
     rc, out = _hsaprobe("--md5-bytes", str(1 << 20), "--hbm-bytes", str(16 << 20), "--copy-bytes", str(1 << 20),
                         "--iters", "1")
