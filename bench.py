@@ -730,6 +730,11 @@ def main(argv=None) -> int:
             if fabric_steps > 0:
                 try:
                     fabric = series(xroot, "fabric", n, args, env, xlog, fabric_steps, settle=settle, rccl="on")
+                    # one more, untimed, with RCCL's INIT/P2P log on: the rank's transport record
+                    # (which channels it built) without logging inside the timed steps
+                    logged = series(xroot, "fabric-logged", n, args, env, xlog, 1, warmup=0, settle=settle, rccl="on",
+                                    env_over={"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT,P2P"})
+                    fabric["transport_logged_run"] = (logged["last"].get("rccl") or {}).get("transport")
                 except Exception as e:  # noqa: BLE001
                     fabric = {"error": str(e)[-1500:]}
         shutil.rmtree(xroot, ignore_errors=True)

@@ -102,6 +102,7 @@ def test_bench_single_process(tmp_path):
     # launch -> a passing RCCL all-reduce Job (gloo ranks on the fake GPUs)
     fv = out["fabric_validated"]
     assert out["fabric_validated_s"] >= fv["ready"]["mean_s"] > 0 and fv["rccl"]["ok"] is True and fv["steps"] == 1
+    assert "transport_logged_run" in fv  # an untimed run with RCCL's INIT/P2P log on
     # round 5: a rebuild right after a teardown names where its extra time went, and every step
     # says which burn-in payload ran and how long its slowest GPU took
     b2b = out["back_to_back"]
