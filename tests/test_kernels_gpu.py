@@ -1096,3 +1096,75 @@ def test_torch_allreduce_job_two_pods_goes_p2p_over_xgmi(tmp_path):
             assert "Job peers on this host" in kc("describe", "pod", name).stdout
     finally:
         subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+
+
+def test_resource_limits_are_enforced_unprivileged_on_the_gpu_box(tmp_path):
+    """VERDICT r4 next-3 on the target box itself (an ordinary user, no delegated cgroup): a real
+    1-GPU bring-up picks the watchdog, a CPU pod with limits.cpu 250m spinning for 3 s of wall
+    time gets at most ~0.35 CPU from the SIGSTOP/SIGCONT duty cycle, and a pod that grows past
+    limits.memory 64Mi is OOMKilled."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    repo = Path(__file__).resolve().parents[1]
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(repo / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k not in ("TK8S_FAKE_GPUS", "TK8S_POD_RESOURCES")}
+    env.update(PYTHONPATH=str(repo), TK8S_PYTHON=sys.executable)
+
+    def kc(*a, stdin=None):
+        p = subprocess.run(["./kubectl", *a], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120,
+                           input=stdin)
+        assert p.returncode == 0, f"kubectl {' '.join(a)}: {p.stdout}{p.stderr}"
+        return p
+
+    def until_done(name, timeout=60.0):
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            pod = json.loads(kc("get", "pod", name, "-o", "json").stdout)
+            if pod["status"].get("phase") in ("Succeeded", "Failed"):
+                return pod
+            time.sleep(0.2)
+        raise AssertionError(f"pod {name} did not finish")
+
+    try:
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--rccl", "off"],
+                           cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        node = json.loads(kc("get", "node", "kubenode1", "-o", "json").stdout)
+        enf = node["metadata"]["annotations"]["tk8s.amd.com/resource-enforcement"]
+        if not enf.startswith("watchdog"):
+            pytest.skip(f"this box delegates cgroups ({enf[:80]}): the kernel enforces, not the duty cycle")
+        assert "duty cycle" in enf and "NOT enforced" not in enf, enf
+        busy = ("import os, time\nt = time.time()\nwhile time.time() - t < 3:\n    pass\n"
+                "u = os.times()\nprint('cpu', round(u.user + u.system, 3), flush=True)\n")
+        kc("apply", "-f", "-", stdin=json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "spin"},
+                                                  "spec": {"restartPolicy": "Never", "containers": [{
+                                                      "name": "c", "command": [sys.executable, "-c", busy],
+                                                      "resources": {"limits": {"cpu": "250m"}}}]}}))
+        until_done("spin")
+        out = kc("logs", "spin").stdout.split()
+        used = float(out[out.index("cpu") + 1])
+        assert used <= 0.35 * 3.0 + 0.2, out
+        # 8 MiB a tenth of a second, every page touched: the resident-set sampler (0.5 s) sees it
+        # far below the RLIMIT_DATA backstop (2 x 64Mi + 256Mi), which would end it differently
+        grow = ("import time\nb = []\nwhile True:\n    b.append(bytearray(8 << 20))\n"
+                "    for i in range(0, len(b[-1]), 4096):\n        b[-1][i] = 1\n    time.sleep(0.1)\n")
+        kc("apply", "-f", "-", stdin=json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "grow"},
+                                                  "spec": {"restartPolicy": "Never", "containers": [{
+                                                      "name": "c", "command": [sys.executable, "-c", grow],
+                                                      "resources": {"limits": {"memory": "64Mi"}}}]}}))
+        pod = until_done("grow")
+        term = (pod["status"].get("containerStatuses") or [{}])[0].get("state", {}).get("terminated", {})
+        assert pod["status"]["phase"] == "Failed" and term.get("reason") == "OOMKilled", pod["status"]
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
