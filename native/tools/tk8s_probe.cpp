@@ -200,7 +200,8 @@ int main(int argc, char** argv) {
       per_dev.push_back(d.str());
     }
     tk8s::Json out;
-    out.kv("ok", ok).kv("device", devices[0]).kv("device_count", n).kv("probed", static_cast<int>(devices.size()));
+    out.kv("ok", ok).kv("runtime", "hip").kv("device", devices[0]).kv("device_count", n)
+        .kv("probed", static_cast<int>(devices.size()));
     // Top-level copies of the first device's results (what the control plane annotates).
     out.raw("hbm", res[0].hbm);
     if (md5) out.raw("md5", res[0].md5).kv("md5_expected", want).kv("md5_pinned", pinned);

@@ -97,7 +97,7 @@ def main():
                            "iters": 2, "access": "allowed", "kernel_ms": 0.6, "kernel_gbps": 55.0 + 0.1 * ((i + j) % 5),
                            "bad_words": 0} for j in range(n) if j != i]
             d["peers_ok"] = True
-    out = {"ok": not fail, "fake": True, "device_count": n, "probed": n, "devices": devices,
+    out = {"ok": not fail, "fake": True, "runtime": "fake", "device_count": n, "probed": n, "devices": devices,
            "hbm": dev["hbm"], "md5": dev["md5"],
            "gpuinfo": {"ok": True, "device_count": n, "devices": [{"index": i, "gfx": "gfx950", "pci_bus_id": f"0000:{bus[i]:02x}:00.0",
                                                                     "uuid": f"fake-{i}"} for i in range(n)]}}

@@ -571,7 +571,7 @@ class Setup(KubeadmPlatform, FabricCheck):
                                            # which payload ran (the HSA one on 1 GPU, the HIP one for
                                            # xGMI pulls) and each GPU's own time: where an N-GPU
                                            # bring-up's burn-in went (the driver's SCALE runs)
-                                           "runtime": (hb.result or {}).get("runtime", "hip"),
+                                           "runtime": (hb.result or {}).get("runtime"),
                                            "device_wall_ms": [round(d.get("wall_ms") or 0.0, 2)
                                                               for d in (hb.result or {}).get("devices", [])]}
             if hb.xgmi is not None:
