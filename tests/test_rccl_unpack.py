@@ -136,3 +136,14 @@ def test_the_fabric_rank_env_carries_the_unpacked_library_and_huge_page_malloc(m
     assert "GLIBC_TUNABLES" not in {e["name"] for e in fabric.rccl_rank_env()[0]}
     env, lib = fabric.rccl_rank_env(fake=True)
     assert lib is None and [e["name"] for e in env] == ["NCCL_DEBUG"]
+
+
+def test_doctor_reports_the_huge_page_mode(tmp_path):
+    from tritonk8ssupervisor_amd.doctor import transparent_huge_pages
+
+    f = tmp_path / "enabled"
+    f.write_text("always [madvise] never\n")
+    assert transparent_huge_pages(str(f))["status"] == "OK" and "madvise" in transparent_huge_pages(str(f))["detail"]
+    f.write_text("always madvise [never]\n")
+    assert transparent_huge_pages(str(f))["status"] == "WARN"
+    assert transparent_huge_pages(str(tmp_path / "missing"))["status"] == "WARN"
