@@ -826,6 +826,12 @@ def main(argv=None) -> int:
         "burnin_device_wall_ms_max_steps": [max((s.get("host_burnin") or {}).get("device_wall_ms") or [0.0]) or None
                                             for s in summaries],
         "burnin_peers_ms_steps": [(s.get("host_burnin") or {}).get("peers_ms") for s in summaries],
+        # how long before Ready the burn-in's result was seen: near 0, the GPU burn-in (not the
+        # control-plane / agent chain) set the step's Ready time
+        "burnin_result_before_ready_ms_steps": [
+            round((s["launched_unix"] + s["ready_wall_seconds"] - s["host_burnin"]["seen_unix"]) * 1e3, 1)
+            if (s.get("host_burnin") or {}).get("seen_unix") and s.get("launched_unix") and s.get("ready_wall_seconds")
+            else None for s in summaries],
         "burnin_total_ms_steps": [(s.get("host_burnin") or {}).get("total_ms") for s in summaries],
         "burnin_spawn_ms_steps": [s.get("burnin_spawn_ms") for s in summaries],
         "burnin_exec_ms_steps": [s.get("burnin_exec_ms") for s in summaries],

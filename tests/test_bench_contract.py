@@ -109,6 +109,7 @@ def test_bench_single_process(tmp_path):
     assert b2b["steps"] == 1 and len(b2b["per_step"]) == 1 and p.stderr.count("(back-to-back)") == 1
     assert {"ready_s", "burnin_runtime_init_ms", "previous_teardown_s", "phases_s", "kfd_census"} <= set(b2b["per_step"][0])
     assert len(out["burnin_runtime_steps"]) == len(out["burnin_device_wall_ms_max_steps"]) == 2
+    assert len(out["burnin_result_before_ready_ms_steps"]) == 2
 
 
 @pytest.mark.timeout(400)
