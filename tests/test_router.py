@@ -5,6 +5,7 @@ literal segments taken literally."""
 from __future__ import annotations
 
 import re
+from urllib.parse import unquote
 
 import pytest
 
@@ -27,7 +28,7 @@ def _eager(routes, method, path):
         mt = re.compile("^" + re.sub(r"\.(?!\+)", r"\\.", pat) + "$").match(path)
         if mt:
             if m == method or (m == "GET" and method == "HEAD"):
-                return h, mt.groupdict()
+                return h, {k: unquote(v) for k, v in mt.groupdict().items()}
             allowed = True
     return 405 if allowed else 404
 
@@ -47,7 +48,8 @@ def test_the_control_planes_routes_answer_as_eager_matching(tmp_path):
              "/api/v1/watch/pods", "/apis/apps/v1/namespaces/kube-system/daemonsets", "/api/v1/nodes/",
              "/apis/apps/v1/namespaces/ns/deployments/d/scale", "/apis/apps/v1/namespaces/ns/jobs/d/scale",
              "/api/v1/namespaces//pods", "/apis//v1/x", "/v1/kv/", "/api/v1/", "/apis/apps/", "/apis/apps/v1/",
-             "/r/projects/1a7/kubernetes/apis/metrics.k8s.io/v1beta1/", "/openapi/v3/api/v1", "no-slash"]
+             "/r/projects/1a7/kubernetes/apis/metrics.k8s.io/v1beta1/", "/openapi/v3/api/v1", "no-slash",
+             "/api/v1/nodes/a%2Fb", "/v1/kv/a%20b/c"]
     for method in ("GET", "POST", "PUT", "DELETE", "PATCH", "HEAD"):
         for path in paths:
             try:
@@ -87,3 +89,31 @@ def test_routes_added_after_a_match_are_seen():
     r.add("GET", r"/(ping|healthz)?", "ping")
     assert r.match("GET", "/c/1") == ("c", {"x": "1"})
     assert r.match("GET", "/healthz")[0] == "ping" and r.match("GET", "/")[0] == "ping"
+
+
+def test_random_paths_route_as_eager_matching(tmp_path):
+    """Property check over generated paths: the lazy/segment router and trying every route's regex
+    in order (dots in literal segments taken literally) pick the same handler and groups, or fail
+    with the same status."""
+    from hypothesis import given, settings, strategies as st
+
+    from tritonk8ssupervisor_amd.controlplane.server import ControlPlane
+
+    cp = ControlPlane("127.0.0.1", 0, str(tmp_path), 5.0, None, 0, 0)
+    words = st.sampled_from(["api", "apis", "v1", "v1beta1", "apps", "batch", "namespaces", "kube-system", "default",
+                             "pods", "nodes", "status", "log", "exec", "scale", "deployments", "jobs", "watch", "kv",
+                             "metrics.k8s.io", "metricsXk8sXio", "r", "projects", "1a7", "kubernetes", "openapi", "v3",
+                             "v2-beta", "registrationtokens", "scripts", "env", "kubectl", "cluster", "wait", "events",
+                             "x:y", "", "%2F", "ping", "healthz", "version"])
+
+    @settings(max_examples=400, deadline=None)
+    @given(st.lists(words, min_size=0, max_size=9), st.booleans(), st.sampled_from(["GET", "POST", "PUT", "DELETE", "HEAD"]))
+    def check(parts, trailing, method):
+        path = "/" + "/".join(parts) + ("/" if trailing and parts else "")
+        try:
+            got = cp.router.match(method, path)
+        except HttpError as e:
+            got = e.status
+        assert got == _eager(cp.router.routes, method, path), (method, path)
+
+    check()
