@@ -250,6 +250,11 @@ def slow_start_cause(census: dict, runtime_init_ms: float | None, limit_ms: floa
         return "unknown: /sys/class/kfd/kfd/proc not readable here"
     window = runtime_init_ms + 1.0  # changes up to the end of the runtime start count
     ch = [c for c in census.get("changes", []) if c["dt_ms"] <= window]
+    # The KFD names processes by their pid on the host; inside a container the burn-in's own pid
+    # differs, so its entry is recognised by when it appears: as its runtime start ends.
+    ours = [c for c in ch if c["what"] == "start" and not c["own"] and abs(c["dt_ms"] - runtime_init_ms) <= 3.0]
+    if ours:
+        ch = [c for c in ch if c is not ours[0]]
     exits = [c for c in ch if c["what"] == "exit" and c["dt_ms"] <= 0]
     foreign_exit = [c for c in exits if not c["own"]]
     if foreign_exit:
@@ -258,6 +263,11 @@ def slow_start_cause(census: dict, runtime_init_ms: float | None, limit_ms: floa
     if exits:
         c = exits[-1]
         return f"this bring-up's KFD process {c['pid']} exited {-c['dt_ms']:.0f} ms before the burn-in spawned"
+    held = [c for c in ch if c["what"] == "exit" and 0 < c["dt_ms"] and ours and abs(c["dt_ms"] - ours[0]["dt_ms"]) <= 3.0]
+    if held:  # its KFD open completed the moment another process's KFD state was released
+        c = held[-1]
+        return (f"waited for KFD process {c['pid']}'s release: it went away {c['dt_ms']:.0f} ms into the start, "
+                f"as the burn-in's own KFD process appeared")
     starts = [c for c in ch if c["what"] == "start" and not c["own"]]
     if starts:
         c = starts[0]

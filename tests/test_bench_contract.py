@@ -217,6 +217,11 @@ def test_slow_start_attribution():
     c = {"available": True, "changes": [{"dt_ms": -50.0, "what": "start", "pid": 7, "own": False}]}
     assert "foreign KFD process 7 started" in bench.slow_start_cause(c, 90.0)
     assert "driver-internal" in bench.slow_start_cause({"available": True, "changes": []}, 90.0)
+    # a rebuild right after a teardown (profiles/r5_kfd_release): the previous bring-up's KFD process
+    # goes away and, in the same sample, the burn-in's own entry (another pid inside a container) appears
+    c = {"available": True, "changes": [{"dt_ms": 149.8, "what": "start", "pid": 2444076, "own": False},
+                                        {"dt_ms": 149.8, "what": "exit", "pid": 2444040, "own": False}]}
+    assert "waited for KFD process 2444040's release" in bench.slow_start_cause(c, 151.1)
 
 
 def test_kfd_census_sees_process_changes(tmp_path, monkeypatch):
