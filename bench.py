@@ -251,8 +251,9 @@ def slow_start_cause(census: dict, runtime_init_ms: float | None, limit_ms: floa
     window = runtime_init_ms + 1.0  # changes up to the end of the runtime start count
     ch = [c for c in census.get("changes", []) if c["dt_ms"] <= window]
     # The KFD names processes by their pid on the host; inside a container the burn-in's own pid
-    # differs, so its entry is recognised by when it appears: as its runtime start ends.
-    ours = [c for c in ch if c["what"] == "start" and not c["own"] and abs(c["dt_ms"] - runtime_init_ms) <= 3.0]
+    # differs, so its entry is recognised by when it appears: as its runtime start ends (within
+    # about one sample of the census, 5 ms).
+    ours = [c for c in ch if c["what"] == "start" and not c["own"] and abs(c["dt_ms"] - runtime_init_ms) <= 6.0]
     if ours:
         ch = [c for c in ch if c is not ours[0]]
     exits = [c for c in ch if c["what"] == "exit" and c["dt_ms"] <= 0]
@@ -263,7 +264,7 @@ def slow_start_cause(census: dict, runtime_init_ms: float | None, limit_ms: floa
     if exits:
         c = exits[-1]
         return f"this bring-up's KFD process {c['pid']} exited {-c['dt_ms']:.0f} ms before the burn-in spawned"
-    held = [c for c in ch if c["what"] == "exit" and 0 < c["dt_ms"] and ours and abs(c["dt_ms"] - ours[0]["dt_ms"]) <= 3.0]
+    held = [c for c in ch if c["what"] == "exit" and 0 < c["dt_ms"] and ours and abs(c["dt_ms"] - ours[0]["dt_ms"]) <= 6.0]
     if held:  # its KFD open completed the moment another process's KFD state was released
         c = held[-1]
         return (f"waited for KFD process {c['pid']}'s release: it went away {c['dt_ms']:.0f} ms into the start, "
