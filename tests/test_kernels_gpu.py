@@ -665,7 +665,9 @@ def test_hsaprobe_multi_device_path_on_one_gpu(nat):
         assert d["ok"] and d["peers_ok"] and len(d["peers"]) == 2, d
         for p in d["peers"]:
             assert p["ok"] and p["access"] == "allowed" and p["bad_words"] == 0 and p["kernel_gbps"] > 50, p
-    rep = link_report(out, [0, 1, 2])
+    # three queues on one GPU contend for its HBM, so their rates say nothing about links: the
+    # verdict is asked for dead pulls only (fraction 0), which none may be
+    rep = link_report(out, [0, 1, 2], fraction=0.0)
     assert rep["pulls"] == 6 and not rep["degraded"], rep
     share = split_host_result(out, [0, 1, 2], [0], rep)  # (every entry names GPU 0)
     assert share is not None and share["ok"] and share["device_count"] == 1
