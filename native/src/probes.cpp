@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -110,6 +111,47 @@ struct CachedStream {
 constexpr size_t kAlign = 4096;
 size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
+// The xGMI pulls' buffers, kept per device for the life of the process: a source per GPU, filled
+// once with the pull pattern and then only read (by every other GPU), and a destination + error
+// counter per pulling GPU (its slot lock is held for the whole pull). Allocating and freeing them
+// per pull cost a hipMalloc/hipFree each -- and hipFree synchronises the whole device, so a pull
+// from GPU s waited for everything else running on s, its own probes and other GPUs' pulls.
+struct PeerSlot {
+  std::mutex mu;
+  void* p = nullptr;
+  size_t n = 0;
+  bool filled = false;
+};
+std::mutex g_peer_mu;  // guards the maps only (node-based: slots never move)
+std::map<int, PeerSlot> g_peer_src, g_peer_dst;
+
+PeerSlot& peer_slot(std::map<int, PeerSlot>& m, int device) {
+  std::lock_guard<std::mutex> lock(g_peer_mu);
+  return m[device];
+}
+
+std::vector<std::pair<int, void*>> g_peer_retired;  // outgrown buffers (guarded by g_peer_mu)
+
+// Grow `slot` (held locked by the caller) to at least `bytes` on `device`. An outgrown buffer is
+// retired, not freed: another GPU may still be reading an outgrown source.
+void* peer_buffer(PeerSlot& slot, int device, size_t bytes) {
+  if (slot.n < bytes) {
+    DeviceGuard g(device);
+    void* p = nullptr;
+    TK8S_HIP_CHECK(hipMalloc(&p, bytes));
+    if (slot.p) {
+      std::lock_guard<std::mutex> lock(g_peer_mu);
+      g_peer_retired.emplace_back(device, slot.p);
+    }
+    slot.p = p;
+    slot.n = bytes;
+    slot.filled = false;
+  }
+  return slot.p;
+}
+
+constexpr uint32_t kPeerPattern = 0xA5A5A5A5u;
+
 }  // namespace
 
 void release_probe_scratch() {
@@ -117,6 +159,32 @@ void release_probe_scratch() {
     std::lock_guard<std::mutex> lock(g_stream_mu);
     for (auto& kv : g_streams) (void)hipStreamDestroy(kv.second);
     g_streams.clear();
+  }
+  {
+    std::lock_guard<std::mutex> lock(g_peer_mu);
+    for (auto* m : {&g_peer_src, &g_peer_dst})
+      for (auto& kv : *m) {
+        std::lock_guard<std::mutex> slot_lock(kv.second.mu);
+        if (!kv.second.p) continue;
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second.p);
+        (void)hipSetDevice(prev);
+        kv.second.p = nullptr;
+        kv.second.n = 0;
+        kv.second.filled = false;
+      }
+    g_peer_src.clear();
+    g_peer_dst.clear();
+    for (const auto& r : g_peer_retired) {
+      int prev = 0;
+      (void)hipGetDevice(&prev);
+      (void)hipSetDevice(r.first);
+      (void)hipFree(r.second);
+      (void)hipSetDevice(prev);
+    }
+    g_peer_retired.clear();
   }
   std::lock_guard<std::mutex> lock(g_scratch_mu);
   for (auto& kv : g_scratch) {
@@ -335,43 +403,51 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
   try {
     if (bytes % 16 || bytes == 0) return error_json("bytes must be a positive multiple of 16");
     iters = std::max(iters, 1);
-    const bool peer = src_device != dst_device;
+    // TK8S_PROBE_PEER_PATH=1: a copy within one GPU takes the peer path (its cached buffers, no
+    // peer grant needed) -- how a one-GPU box exercises the code the xGMI pulls run
+    const bool forced = std::getenv("TK8S_PROBE_PEER_PATH") != nullptr && src_device == dst_device;
+    const bool peer = src_device != dst_device || forced;
     int can = 1;
-    if (peer) {
+    if (peer && !forced) {
       TK8S_HIP_CHECK(hipDeviceCanAccessPeer(&can, dst_device, src_device));
       if (!can) return link_error("no peer access from dst to src");
     }
     // Local: src, dst and the error counter are carved from this device's scratch arena.
-    // Peer: own buffers (the source device's arena may be busy in another thread).
-    std::unique_ptr<DeviceBuffer> src_own, dst_own, bad_own;
+    // Peer: the cached peer buffers (PeerSlot): the source filled once, the destination held.
     void *src = nullptr, *dst = nullptr;
     unsigned long long* bad = nullptr;
+    std::unique_lock<std::mutex> dst_hold;
     if (!peer) {
       DeviceGuard g(src_device);
       char* base = scratch(src_device, 2 * align_up(bytes) + kAlign);
       src = base;
       dst = base + align_up(bytes);
       bad = reinterpret_cast<unsigned long long*>(base + 2 * align_up(bytes));
-    } else {
-      DeviceGuard g(src_device);
-      src_own.reset(new DeviceBuffer(bytes));
-      src = src_own->get();
-    }
-    {
-      DeviceGuard g(src_device);
       const hipStream_t ss = probe_stream(src_device);
-      hbm_fill(src, bytes, 0xA5A5A5A5u, StoreMode::kPlain, ss);
+      hbm_fill(src, bytes, kPeerPattern, StoreMode::kPlain, ss);
       TK8S_HIP_CHECK(hipStreamSynchronize(ss));
+    } else {
+      PeerSlot& ps = peer_slot(g_peer_src, src_device);
+      std::lock_guard<std::mutex> lock(ps.mu);
+      src = peer_buffer(ps, src_device, align_up(bytes));
+      if (!ps.filled) {
+        DeviceGuard g(src_device);
+        const hipStream_t ss = probe_stream(src_device);
+        hbm_fill(src, ps.n, kPeerPattern, StoreMode::kPlain, ss);
+        TK8S_HIP_CHECK(hipStreamSynchronize(ss));
+        ps.filled = true;
+      }
+      PeerSlot& pd = peer_slot(g_peer_dst, dst_device);
+      dst_hold = std::unique_lock<std::mutex>(pd.mu);
+      char* base = static_cast<char*>(peer_buffer(pd, dst_device, align_up(bytes) + kAlign));
+      dst = base;
+      bad = reinterpret_cast<unsigned long long*>(base + align_up(bytes));
     }
     DeviceGuard g(dst_device);
-    if (peer) {
+    if (peer && !forced) {
       const hipError_t pe = hipDeviceEnablePeerAccess(src_device, 0);
       if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) TK8S_HIP_CHECK(pe);
       (void)hipGetLastError();
-      dst_own.reset(new DeviceBuffer(bytes));
-      bad_own.reset(new DeviceBuffer(sizeof(unsigned long long)));
-      dst = dst_own->get();
-      bad = bad_own->as<unsigned long long>();
     }
     CachedStream st(dst_device);
     stream_copy(dst, src, bytes, st.s);  // warm-up
@@ -381,7 +457,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
     kt.stop(st.s);
     const float kernel_ms = kt.elapsed_ms() / iters;
     TK8S_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), st.s));
-    verify_fill(dst, bytes, 0xA5A5A5A5u, bad, st.s);
+    verify_fill(dst, bytes, kPeerPattern, bad, st.s);
     unsigned long long nbad = 0;
     TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad, sizeof nbad, hipMemcpyDeviceToHost, st.s));
     // The SDMA-engine path only for peers (where it is a separate xGMI data path worth

@@ -675,6 +675,22 @@ def test_hsaprobe_multi_device_path_on_one_gpu(nat):
     assert rc == 2 and not bad["ok"] and "--devices" in bad["error"]
 
 
+def test_hip_peer_pull_path_on_one_gpu(nat, monkeypatch):
+    """The HIP probe's xGMI pull path (copy_probe with src != dst) keeps its buffers per device --
+    a source filled once and only read, a destination held for the pull -- instead of a
+    hipMalloc/hipFree per pull (hipFree synchronises the whole device). TK8S_PROBE_PEER_PATH=1
+    routes a copy within one GPU through that path: repeated pulls, a larger one (the source
+    buffer regrows and is refilled), the SDMA pass, and the local copy afterwards."""
+    monkeypatch.setenv("TK8S_PROBE_PEER_PATH", "1")
+    for nbytes in (16 << 20, 16 << 20, 48 << 20, 16 << 20):
+        c = json.loads(nat.copy_probe(0, 0, nbytes, 3))
+        assert c["ok"] and c["probe"] == "xgmi_peer_copy" and c["bad_words"] == 0, c
+        assert c["kernel_gbps"] > 100 and c["dma_gbps"] > 10, c
+    monkeypatch.delenv("TK8S_PROBE_PEER_PATH")
+    c = json.loads(nat.copy_probe(0, 0, 16 << 20, 3))
+    assert c["ok"] and c["probe"] == "local_copy" and c["bad_words"] == 0, c
+
+
 def test_hsaprobe_md5_unpinned_for_other_inputs(nat):
     rc, out = _hsaprobe("--md5-bytes", str(1 << 20), "--hbm-bytes", str(16 << 20), "--copy-bytes", str(1 << 20),
                         "--iters", "1")
