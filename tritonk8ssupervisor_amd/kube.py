@@ -10,8 +10,12 @@ from pathlib import Path
 
 from . import templating
 from .controlplane.client import ApiError, Client
-from .controlplane.k8s_wire import APPLY_PATCH
 from .utils import yamlio
+
+# server-side apply's content type (= controlplane/k8s_wire.APPLY_PATCH, pinned by
+# tests/test_kube_helpers.py): spelled out here so setup's deploy task, on the bring-up's critical
+# path, does not import the control plane's wire module (and `copy`, `weakref`) for one string
+APPLY_PATCH = "application/apply-patch+yaml"
 
 KINDS = {
     "pod": ("Pod", "/api/v1", "pods"),
