@@ -28,7 +28,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import sys
 import time
 import urllib.request
@@ -96,12 +95,6 @@ def _debug_file() -> str | None:
 
         os.environ["NCCL_DEBUG_FILE"] = os.path.join(tempfile.gettempdir(), f"tk8s-rccl-{os.getpid()}.log")
     return os.environ["NCCL_DEBUG_FILE"]
-
-
-def _free_port(host: str) -> int:
-    with socket.socket() as s:
-        s.bind((host, 0))
-        return s.getsockname()[1]
 
 
 def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters: int, warmup: int,
@@ -209,21 +202,27 @@ def main(argv=None) -> int:
     debug_file = _debug_file() if a.backend == "nccl" else None
     host = os.environ.get("NODE_IP", "127.0.0.1")
     try:
-        if a.rank == 0:
-            addr = f"{host}:{_free_port(host)}"
-            _publish(a.kv_url, addr)
-        else:
-            addr = _fetch(a.kv_url, a.timeout)
         import torch.distributed as dist
         from datetime import timedelta
 
+        # Rank 0 binds the rendezvous store on an ephemeral port itself and publishes the port it
+        # got: picking a free port and binding it later left a window in which another process on
+        # the host took it (EADDRINUSE on the shared GPU box).
+        if a.rank == 0:
+            store = dist.TCPStore(host, 0, world_size=a.nranks, is_master=True,
+                                  timeout=timedelta(seconds=a.timeout), wait_for_workers=False)
+            _publish(a.kv_url, f"{host}:{store.port}")
+        else:
+            sh, sp = _fetch(a.kv_url, a.timeout).rsplit(":", 1)
+            store = dist.TCPStore(sh, int(sp), world_size=a.nranks, is_master=False,
+                                  timeout=timedelta(seconds=a.timeout))
         device = "cpu"
         if a.backend == "nccl":
             import torch
 
             torch.cuda.set_device(0)  # the device plugin exposes exactly this pod's GPU(s)
             device = "cuda:0"
-        dist.init_process_group(a.backend, init_method=f"tcp://{addr}", rank=a.rank, world_size=a.nranks,
+        dist.init_process_group(a.backend, store=store, rank=a.rank, world_size=a.nranks,
                                 timeout=timedelta(seconds=a.timeout))
         init_s = time.monotonic() - t0
         res = sweep(a.rank, a.nranks, a.min_bytes, a.max_bytes, a.factor, a.iters, a.warmup, a.dtype, device)
