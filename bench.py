@@ -557,8 +557,8 @@ def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1)
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1, help="workers (one MI355X each)")
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)  # one 150 ms KFD wait (another process's release) moves a 3-step mean by 50 ms
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--package", default="mi355x-1gpu")
     ap.add_argument("--timeout", type=float, default=300.0, help="bound on one bring-up's readiness wait (s)")
     ap.add_argument("--no-validate", action="store_true", help="skip per-worker GPU validation (not the headline)")
