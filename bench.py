@@ -48,7 +48,6 @@ import argparse
 import json
 import os
 import shutil
-import socket
 import subprocess
 import sys
 import tempfile
@@ -64,11 +63,9 @@ METRIC = "wall-clock (s) ./setup.sh → all nodes Ready; 1/2/4/8 workers"
 
 
 def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    from tritonk8ssupervisor_amd.utils.net import pick_port
+
+    return pick_port("127.0.0.1")
 
 
 class Dist:

@@ -695,14 +695,9 @@ class Setup(KubeadmPlatform, FabricCheck):
 
 
 def _free_port() -> int:
-    import _socket  # (not ``socket``: its enum set-up is ~1.5 ms of the bring-up, utils/http1.py)
+    from .utils.net import pick_port
 
-    s = _socket.socket(_socket.AF_INET, _socket.SOCK_STREAM)
-    try:
-        s.bind(("0.0.0.0", 0))
-        return s.getsockname()[1]
-    finally:
-        s.close()
+    return pick_port("0.0.0.0")
 
 
 def _flush_print(s: str) -> None:
