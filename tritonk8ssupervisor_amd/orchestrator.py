@@ -146,7 +146,7 @@ class Setup(KubeadmPlatform, FabricCheck):
             if ws.config.exists():
                 raise SetupError("error: old configuration found\n    clean the configuration (./setup.sh -c)")
             cfg = ClusterConfig(TK8S_BACKEND=self.backend, TK8S_PLATFORM=self.platform)
-            if self.master_port == 0:  # any free port (benchmarks / tests run clusters side by side)
+            if self.master_port == 0:  # a free port outside the ephemeral and NodePort ranges (utils/net.pick_port; clusters side by side)
                 cfg.TK8S_MASTER_PORT = _free_port()
             elif self.master_port:
                 cfg.TK8S_MASTER_PORT = self.master_port
