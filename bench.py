@@ -33,7 +33,10 @@ reference can never go below (setup.sh:36,41,46; terraform/*/main.tf:22;
 ansible/roles/ranchermaster/tasks/main.yml:25).
 
 A timed step whose post-Ready RCCL check fails is left out of ``value`` and listed in
-``post_ready_errors`` (its Ready time stood, the cluster did not). After the headline, a
+``post_ready_errors`` (its Ready time stood, the cluster did not). The first such failure
+(warmup steps included) turns the RCCL check off for every later step -- recorded once as
+``fabric_disabled_after_step`` with the error's tail -- so a broken fabric costs one bounded
+check (``--rccl-op-timeout``, 20 s per wait inside the ranks), never one per step. After the headline, a
 single-rank run also measures BASELINE.json configs[1], ``curve_config2``: 1 master + 1/2/4/8
 ``cpu-only`` workers (no GPU, no device plugin), ``--curve-steps`` timed bring-ups per point.
 
@@ -389,6 +392,8 @@ def one_bringup(ws: Path, n: int, args, env: dict, log, census: KfdCensus | None
         cmd.append("--no-validate")
     if rccl or args.rccl:
         cmd += ["--rccl", rccl or args.rccl]
+    if getattr(args, "rccl_op_timeout", None):
+        cmd += ["--rccl-op-timeout", str(args.rccl_op_timeout)]
     import threading
 
     census = census or KfdCensus()
@@ -517,6 +522,28 @@ def series(root: Path, name: str, n: int, args, env: dict, log, steps: int, warm
 CURVE_NODES = (1, 2, 4, 8)
 
 
+def mean_phases(per_step: list[dict]) -> dict:
+    """Mean seconds per bring-up phase over a point's timed steps."""
+    out: dict[str, float] = {}
+    for ph in per_step:
+        for k, v in ph.items():
+            if isinstance(v, (int, float)):
+                out[k] = out.get(k, 0.0) + v / len(per_step)
+    return {k: round(v, 4) for k, v in out.items()}
+
+
+def mean_tasks(per_step: list[list[dict]], top: int = 6) -> list[dict]:
+    """A point's slowest tasks: each task's mean over the steps that listed it (slowest_tasks of
+    each step), slowest first."""
+    acc: dict[str, list[float]] = {}
+    for step in per_step:
+        for t in step:
+            acc.setdefault(t["what"], []).append(t["s"])
+    n = max(len(per_step), 1)
+    rows = [{"what": k, "mean_s": round(sum(v) / n, 4), "steps": len(v)} for k, v in acc.items()]
+    return sorted(rows, key=lambda r: -r["mean_s"])[:top]
+
+
 def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1) -> dict:
     """BASELINE.json configs[1]: 1 master + N ``cpu-only`` workers (no GPU, no device plugin),
     N = 1/2/4/8 -- the worker-count curve of the bring-up itself, measurable on a 1-GPU box. Each
@@ -526,13 +553,16 @@ def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1)
     points = []
     t_curve = time.perf_counter()
     for n in getattr(args, "curve_workers", None) or CURVE_NODES:
-        ready, proc = [], []
+        ready, proc, phases, tasks = [], [], [], []
         for i in range(warmup + steps):
             ws = root / f"curve{n}-{i}"
             make_workspace(ws)
             t0 = time.perf_counter()
             s = one_bringup(ws, n, args, env, log, package="cpu-only", rccl="off")
             dt = time.perf_counter() - t0
+            if i >= warmup:  # where this point's time went, read before the teardown
+                phases.append(s.get("phases") or {})
+                tasks.append(slowest_tasks(ws / ".tk8s" / "events.jsonl", s.get("launched_unix"), top=12))
             teardown(ws, env, log)
             shutil.rmtree(ws, ignore_errors=True)
             if i >= warmup:
@@ -543,7 +573,8 @@ def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1)
                        "median_s": round(srt[len(srt) // 2] if len(srt) % 2 else (srt[len(srt) // 2 - 1] + srt[len(srt) // 2]) / 2, 4),
                        "min_s": round(srt[0], 4), "max_s": round(srt[-1], 4),
                        "ms_per_step": round(sum(proc) / len(proc) * 1000.0, 2), "gpus_allocatable": s.get("gpus_allocatable"),
-                       "nodes": s.get("nodes")})
+                       "nodes": s.get("nodes"), "phases_s": mean_phases(phases),
+                       "slowest_tasks": mean_tasks(tasks)})
     return {"config": "BASELINE.json configs[1]: 1 master + N cpu-only workers, no GPU device plugin",
             "package": "cpu-only", "warmup": warmup, "points": points,
             "wall_s": round(time.perf_counter() - t_curve, 3),
@@ -561,6 +592,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-validate", action="store_true", help="skip per-worker GPU validation (not the headline)")
     ap.add_argument("--rccl", choices=["on", "off"], default=None)
     ap.add_argument("--rccl-timeout", type=float, default=120.0, help="bound on the post-Ready RCCL Job (s)")
+    ap.add_argument("--rccl-op-timeout", type=float, default=None,
+                    help="bound on each wait inside an RCCL rank (default: ./setup.sh's, 20 s)")
     ap.add_argument("--fake-gpus", type=int, default=None,
                     help="CPU rehearsal: N fake gfx950 devices (default: fake 8 when no GPU is present)")
     ap.add_argument("--workdir", default=None, help="parent of the per-step workspaces (default: a tempdir)")
@@ -619,6 +652,9 @@ def main(argv=None) -> int:
     b2b_ready: list[float] = []
     b2b_detail: list[dict] = []
     cold: dict | None = None
+    # the first post-Ready fabric failure turns the RCCL check off for every later
+    # step (recorded once), so a broken fabric costs one deadline, not one per step
+    fabric_disabled: dict | None = None
     total = args.warmup + args.steps
     census = KfdCensus().start() if d.rank == 0 else None
     try:
@@ -649,7 +685,11 @@ def main(argv=None) -> int:
                     if i == 0 and args.warmup > 0:
                         cold_start_state.update(loadavg_1m=round(os.getloadavg()[0], 2),
                                                 cpus=len(os.sched_getaffinity(0)))
-                    s = one_bringup(ws, n, args, step_env, log, census)
+                    s = one_bringup(ws, n, args, step_env, log, census,
+                                    rccl="off" if fabric_disabled is not None else None)
+                    if s.get("post_ready_error") and fabric_disabled is None:
+                        fabric_disabled = {"after_step": i, "kind": "timed" if timed else "back-to-back" if extra
+                                           else "warmup", "error_tail": s["post_ready_error"][-800:]}
                     if i == 0 and args.warmup > 0:
                         cold = s
                         cold["slowest_tasks"] = slowest_tasks(ws / ".tk8s" / "events.jsonl", s.get("launched_unix"))
@@ -726,16 +766,20 @@ def main(argv=None) -> int:
             shutil.rmtree(croot, ignore_errors=True)
     plain = fabric = None
     fabric_steps = args.fabric_steps if args.fabric_steps is not None else (0 if fake else 5)
+    off = "off" if fabric_disabled is not None else None
     if d.world == 1 and (args.plain_steps > 0 or fabric_steps > 0):
         xroot = Path(tempfile.mkdtemp(prefix="tk8s-extra-", dir=os.environ.get("TMPDIR", "/tmp")))
         with open(args.log, "a") if args.log else open(os.devnull, "w") as xlog:
             if args.plain_steps > 0:
                 try:
                     plain = series(xroot, "plain", n, args, env, xlog, args.plain_steps, settle=settle,
-                                   env_over={"TK8S_SHORTCUTS": "0"})
+                                   rccl=off, env_over={"TK8S_SHORTCUTS": "0"})
                 except Exception as e:  # noqa: BLE001 - the headline stands; the key says why it is missing
                     plain = {"error": str(e)[-1500:]}
-            if fabric_steps > 0:
+            if fabric_steps > 0 and fabric_disabled is not None:
+                fabric = {"skipped": f"the fabric check failed after step {fabric_disabled['after_step']}",
+                          "error_tail": fabric_disabled["error_tail"]}
+            elif fabric_steps > 0:
                 try:
                     fabric = series(xroot, "fabric", n, args, env, xlog, fabric_steps, settle=settle, rccl="on")
                     # one more, untimed, with RCCL's INIT/P2P log on: the rank's transport record
@@ -823,7 +867,7 @@ def main(argv=None) -> int:
         # unevenly the ranks came up, the channel transports RCCL logged, the Job's shape
         "rccl_last_step": {k: (last.get("rccl") or {}).get(k) for k in (
             "ok", "nranks", "pods", "gpus_per_pod", "comm_init_ms_max", "sweep_ms_max", "init_spread_ms", "transport",
-            "rccl_library")}
+            "rccl_library", "peak_algbw_gbps", "fabric", "sweep", "op_timeout_s")}
         if last.get("rccl") else None,
         "xgmi_last_step": last.get("xgmi"),
         "validation_last_step": last.get("validation"),
@@ -854,6 +898,10 @@ def main(argv=None) -> int:
                                "max_s": round(max(b2b_ready), 4), "per_step": b2b_detail,
                                "what": "./setup.sh -c && ./setup.sh with no settle pause: Ready includes the driver "
                                        "still releasing the previous bring-up's GPU processes"}
+    if fabric_disabled is not None:  # the steps after it ran with --rccl off
+        out["fabric_disabled_after_step"] = fabric_disabled["after_step"]
+        out["fabric_disabled"] = fabric_disabled
+        out["config"]["rccl"] = f"on until step {fabric_disabled['after_step']}, then off (fabric check failed)"
     if excluded:  # timed steps left out of value: Ready, then the post-Ready RCCL check failed
         out["post_ready_errors"] = {"count": len(excluded), "excluded_steps": [x["step"] for x in excluded],
                                     "last": excluded[-1]["error"]}
@@ -864,7 +912,10 @@ def main(argv=None) -> int:
         out["plain_path"] = {k: v for k, v in plain.items() if k != "last"}
         out["plain_path"]["what"] = ("TK8S_SHORTCUTS=0: every start-up shortcut of docs/architecture.md off "
                                      "(early burn-in, zygotes, caches, fast parsers, -S, inline tasks, ...)")
-    if fabric is not None:  # launch -> a passing RCCL all-reduce Job, N GPUs
+    if fabric is not None and "skipped" in fabric:
+        out["fabric_validated_s"] = None
+        out["fabric_validated"] = fabric
+    elif fabric is not None:  # launch -> a passing RCCL all-reduce Job, N GPUs
         last_rccl = (fabric.get("last") or {}).get("rccl") or {}
         out["fabric_validated_s"] = fabric.get("setup_exit", {}).get("mean_s")
         out["fabric_validated"] = {k: v for k, v in fabric.items() if k != "last"}
@@ -872,7 +923,8 @@ def main(argv=None) -> int:
             "what": "--rccl on: wall-clock from launching ./setup.sh to its exit after the RCCL all-reduce Job "
                     "over every GPU passed its exact check",
             "rccl": {k: last_rccl.get(k) for k in ("ok", "nranks", "pods", "comm_init_ms_max", "sweep_ms_max", "init_spread_ms", "rccl_library",
-                                                   "peak_busbw_gbps", "transport")}})
+                                                   "peak_busbw_gbps", "peak_algbw_gbps", "fabric", "sweep",
+                                                   "op_timeout_s", "transport")}})
     print(json.dumps(out), flush=True)
     return 0
 

@@ -62,7 +62,7 @@ PYBIND11_MODULE(_tk8s_native, m) {
         c.factor = factor;
         c.iters = iters;
         c.warmup = warmup;
-        c.dtype = dtype_of(dtype);
+        c.dtypes = {dtype_of(dtype)};
         c.check = check;
         return tk8s::allreduce_single_process(devices, c);
       },

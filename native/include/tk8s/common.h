@@ -14,6 +14,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "tk8s/failfast.h"
 #include "tk8s/json.h"
 
 namespace tk8s {
@@ -32,6 +33,38 @@ struct HipError : std::runtime_error {
     if (_tk8s_e != hipSuccess)                                            \
       throw ::tk8s::HipError(#expr, _tk8s_e, __FILE__, __LINE__);         \
   } while (0)
+
+// A bounded wait ran out: the GPU work (or the collective) did not finish in time.
+struct GpuTimeout : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// Releases a stall kernel armed by a fault point (stream_kernels.hip); a no-op when none is
+// armed. Every bounded wait calls it before giving up, so the stalled queue drains.
+void gpu_stall_release();
+
+// hipStreamSynchronize under a deadline (TK8S_GPU_SYNC_TIMEOUT_S, default 30 s): the probes'
+// kernels are finite, so a wait that runs out means a wedged GPU or a dead link, and the payload
+// must report it rather than hang the bring-up.
+inline void wait_stream(hipStream_t s, const char* what, double timeout_s = gpu_sync_timeout_s()) {
+  hipError_t last = hipSuccess;
+  const std::string r = poll_until([&] { return (last = hipStreamQuery(s)) != hipErrorNotReady; }, timeout_s);
+  if (!r.empty()) {
+    gpu_stall_release();
+    throw GpuTimeout(std::string(what) + ": GPU work " + r);
+  }
+  if (last != hipSuccess) throw HipError(what, last, __FILE__, __LINE__);
+}
+
+inline void wait_event(hipEvent_t e, const char* what, double timeout_s = gpu_sync_timeout_s()) {
+  hipError_t last = hipSuccess;
+  const std::string r = poll_until([&] { return (last = hipEventQuery(e)) != hipErrorNotReady; }, timeout_s);
+  if (!r.empty()) {
+    gpu_stall_release();
+    throw GpuTimeout(std::string(what) + ": GPU work " + r);
+  }
+  if (last != hipSuccess) throw HipError(what, last, __FILE__, __LINE__);
+}
 
 // RAII device buffer (hipMalloc / hipFree on the current device).
 class DeviceBuffer {
@@ -68,9 +101,9 @@ class EventTimer {
   }
   void start(hipStream_t s) { TK8S_HIP_CHECK(hipEventRecord(start_, s)); }
   void stop(hipStream_t s) { TK8S_HIP_CHECK(hipEventRecord(stop_, s)); }
-  // Milliseconds between start and stop (synchronises on stop).
+  // Milliseconds between start and stop (waits for stop, bounded: wait_event).
   float elapsed_ms() {
-    TK8S_HIP_CHECK(hipEventSynchronize(stop_));
+    wait_event(stop_, "timed region");
     float ms = 0.f;
     TK8S_HIP_CHECK(hipEventElapsedTime(&ms, start_, stop_));
     return ms;

@@ -66,4 +66,10 @@ void ar_check(const void* buf, size_t count, int nranks, DType dtype, float tol,
 // N7: dst[i] = src[i] for nbytes (multiple of 16). src may live on a peer GPU (xGMI pull).
 void stream_copy(void* dst, const void* src, size_t nbytes, hipStream_t stream);
 
+// Fault injection (TK8S_FAULTS "...hang@<phase>" on a GPU phase, failfast.h): enqueue on `stream`
+// a one-wave kernel that spins until gpu_stall_release() (common.h) is called or `max_s` seconds
+// of GPU wall clock pass -- so a stalled queue always drains, whoever forgets to release it.
+// Everything queued behind it on `stream` waits: a hung collective or pull, made on purpose.
+void gpu_stall(hipStream_t stream, double max_s);
+
 }  // namespace tk8s

@@ -5,16 +5,28 @@
 // xGMI and produce the exact reduced value before the cluster is declared GPU-Ready.
 //
 // Two launch shapes:
-//  * allreduce_single_process: one process drives n GPUs (ncclCommInitAll + group calls).
+//  * allreduce_single_process: one process drives n GPUs (one communicator of n ranks, all of
+//    them local: a fresh unique id and the ranks' inits in one group).
 //  * allreduce_rank_group: one process per NODE, driving all of that node's GPUs as consecutive
-//    ranks of one multi-process communicator (ncclCommInitRank per device inside one group).
+//    ranks of one multi-process communicator (ncclCommInitRankConfig per device inside one group).
 //    On an 8-GPU node that is one runtime start instead of eight concurrent ones, each of which
 //    would initialise all eight agents (the fabric Job's start-up cost).
 //    allreduce_rank is the one-device case. Rank 0 creates the unique id and the caller ships it
 //    to the other processes (file or control-plane KV, see tools/tk8s_rccl.cpp).
+//
+// Fail fast: the communicators are non-blocking (ncclConfig_t.blocking = 0), and
+// every wait -- the init, each sweep point's collectives, each check -- polls the streams and
+// ncclCommGetAsyncError under op_timeout_s. A timeout or an async error aborts every local
+// communicator (ncclCommAbort) and returns {"ok":false,"phase":...,"error":...} at once, so a
+// dead or hung peer costs one deadline, not the Job's whole wait.
+//
+// Bandwidth: algbw = bytes / time; busbw = algbw * 2(n-1)/n, the per-GPU
+// link traffic of a ring all-reduce -- 0 at n = 1, where the "all-reduce" is a local copy and no
+// fabric exists ("peak_busbw_gbps": null, "fabric": "1 GPU: no fabric").
 #pragma once
 
 #include <cstddef>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -30,19 +42,33 @@ struct AllReduceConfig {
   int factor = 2;        // size multiplier between sweep points
   int iters = 20;        // timed iterations per size
   int warmup = 5;        // untimed iterations per size
-  DType dtype = DType::kF32;
+  std::vector<DType> dtypes{DType::kF32};  // one full sweep per dtype, on the same communicator
   bool check = true;     // run the N6 checker on the result of each size
   // free the communicators, streams and buffers before returning: a process that exits right
   // after (tk8s-rccl) skips it -- the driver reclaims all of it at exit, and ncclCommDestroy plus
   // the runtime's teardown were ~0.18 s of the fabric check's rank
   bool teardown = true;
+  // bound on each wait (init, one sweep point, one check); <= 0: unbounded (blocking waits)
+  double op_timeout_s = 20.0;
+  // RCCL's blocking calls (TK8S_RCCL_BLOCKING=1): the init is then bounded only by the caller's
+  // watchdog, not by an abort
+  bool blocking = false;
+  // called when a bounded wait starts (phase, its bound in s): the tool re-arms its watchdog
+  std::function<void(const std::string&, double)> on_phase;
+  // GPU-side fault point (TK8S_FAULTS rccl.hang@sweep / rccl.hang@check): stall the local ranks'
+  // streams in that phase (kernels.h gpu_stall), as a rank whose GPU stopped would
+  std::string stall_phase;
 };
 
 std::string nccl_unique_id_hex(const ncclUniqueId& id);
 bool nccl_unique_id_from_hex(const std::string& hex, ncclUniqueId* id);
 
-// Returns {"ok":..,"mode":"single_process","nranks":n,"rccl_version":v,"results":[{bytes,count,
-// time_us,algbw_gbps,busbw_gbps,max_err,bad}...],"peak_busbw_gbps":..}
+// busbw of a ring all-reduce over n ranks for a given algbw: algbw * 2(n-1)/n (0 at n <= 1).
+double allreduce_busbw(double algbw_gbps, int nranks);
+
+// Returns {"ok":..,"mode":"single_process","nranks":n,"rccl_version":v,"sweep":{..},
+// "results":[{dtype,bytes,count,time_us,algbw_gbps,busbw_gbps,max_err,bad}...],
+// "peak_algbw_gbps":..,"peak_busbw_gbps":.. (null at n = 1)}; on failure {"ok":false,"phase":..}
 std::string allreduce_single_process(const std::vector<int>& devices, const AllReduceConfig& cfg);
 
 // Same record for ranks first_rank .. first_rank+devices.size()-1 of an nranks communicator,

@@ -318,7 +318,7 @@ std::string hbm_write_probe(size_t bytes, int iters, StoreMode mode, int device,
     const float read_ms = rd.elapsed_ms();
     unsigned long long nbad = 0;
     TK8S_HIP_CHECK(hipMemcpyAsync(&nbad, bad, sizeof nbad, hipMemcpyDeviceToHost, st.s));
-    TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
+    wait_stream(st.s, "hbm probe");
     return Json()
         .kv("ok", nbad == 0)
         .kv("probe", "hbm_write")
@@ -372,7 +372,7 @@ std::string md5_probe(size_t bytes, uint32_t chunk_bytes, uint64_t seed, int ite
     const float ms = warm_t.elapsed_ms() / iters;
     unsigned char digest[16];
     TK8S_HIP_CHECK(hipMemcpyAsync(digest, out, 16, hipMemcpyDeviceToHost, st.s));
-    TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
+    wait_stream(st.s, "md5 probe");
     return Json()
         .kv("ok", true)
         .kv("probe", "md5_tree")
@@ -425,7 +425,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
       bad = reinterpret_cast<unsigned long long*>(base + 2 * align_up(bytes));
       const hipStream_t ss = probe_stream(src_device);
       hbm_fill(src, bytes, kPeerPattern, StoreMode::kPlain, ss);
-      TK8S_HIP_CHECK(hipStreamSynchronize(ss));
+      wait_stream(ss, "copy source fill");
     } else {
       PeerSlot& ps = peer_slot(g_peer_src, src_device);
       std::lock_guard<std::mutex> lock(ps.mu);
@@ -434,7 +434,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
         DeviceGuard g(src_device);
         const hipStream_t ss = probe_stream(src_device);
         hbm_fill(src, ps.n, kPeerPattern, StoreMode::kPlain, ss);
-        TK8S_HIP_CHECK(hipStreamSynchronize(ss));
+        wait_stream(ss, "peer source fill");
         ps.filled = true;
       }
       PeerSlot& pd = peer_slot(g_peer_dst, dst_device);
@@ -450,6 +450,12 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
       (void)hipGetLastError();
     }
     CachedStream st(dst_device);
+    if (peer) {
+      // TK8S_FAULTS probe.exit|crash@peers end the process here; probe.hang@peers stalls this
+      // pull's queue, so the bounded waits below must give up and name the link (failfast.h)
+      fault_point("probe", "peers", /*host_hang=*/false);
+      if (fault_armed("probe", "hang", "peers")) gpu_stall(st.s, 2 * gpu_sync_timeout_s() + 5);
+    }
     stream_copy(dst, src, bytes, st.s);  // warm-up
     EventTimer kt, dt;
     kt.start(st.s);
@@ -472,7 +478,7 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
       dt.stop(st.s);
       dma_ms = dt.elapsed_ms() / iters;
     }
-    TK8S_HIP_CHECK(hipStreamSynchronize(st.s));
+    wait_stream(st.s, "copy probe");
     Json j;
     j.kv("ok", nbad == 0)
         .kv("probe", peer ? "xgmi_peer_copy" : "local_copy")

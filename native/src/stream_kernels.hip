@@ -10,13 +10,20 @@
 //    a new page per instruction. Measured on 1 GiB fill: grid-stride 4.3 TB/s -> slab 6.2 TB/s
 //    (hipMemsetD32 6.66); 256 MiB copy (read + write counted): 4.96 -> 6.42 TB/s (hipMemcpy
 //    D2D 4.96-5.43). HBM3E spec peak is 8 TB/s.
-//  * Grid = CUs x 16 blocks of 256 threads for the fill, CUs x 32 for the copy (best of the
-//    4/8/16/32 per-CU sweep); plain stores for the fill (non-temporal measured 3-9 % slower),
-//    non-temporal loads+stores for the once-touched copy.
+//  * The plain HBM fill is the exception (round 6, native/bench/fill_roofline.hip, four sweeps,
+//    profiles/r6_fill/): ONE block of 128 threads per CU, grid-stride, each lane storing 32
+//    contiguous bytes (two dwordx4) per step. The whole chip's write front is then one
+//    contiguous 1 MiB window moving through memory: 1 GiB in 153-156 us (6.9 TB/s, ~86 % of the
+//    8 TB/s HBM3E peak) against 162-166 us for the runtime's own hipMemsetD32 (one 256-thread
+//    block per CU, grid-stride, 16 B per lane) and 171-176 us for the old slab form. More waves
+//    per CU, wider or narrower windows, non-temporal and sc1 stores were all slower.
+//  * Grid = CUs x 16 blocks of 256 threads for the other streams, CUs x 32 for the copy (best
+//    of the 4/8/16/32 per-CU sweep); non-temporal loads+stores for the once-touched copy.
 //  * Reductions: wave64 __shfl_xor butterfly -> LDS across the 4 waves -> ONE atomic per block
 //    (cdna_hip_programming.md Guideline 12).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -62,23 +69,33 @@ __device__ __forceinline__ void slab_bounds(size_t n, size_t* lo, size_t* hi) {
   *hi = end < n ? end : n;
 }
 
+// kNT = false (the probe's default, StoreMode::kPlain): the write-front walk above, launched as
+// CUs x kFillBlock; kNT = true: non-temporal stores in the slab walk, launched as CUs x 16 x
+// kBlock (the write-front walk with nt stores measured 2.4 TB/s).
+constexpr int kFillBlock = 128;
+
 template <bool kNT>
 __global__ __launch_bounds__(kBlock) void hbm_fill_kernel(u32x4* __restrict__ dst, size_t n16,
                                                           unsigned value) {
-  size_t lo, hi;
-  slab_bounds(n16, &lo, &hi);
   const u32x4 v = {value, value, value, value};
-  size_t i = lo + threadIdx.x;
-  for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if constexpr (kNT) __builtin_nontemporal_store(v, dst + i + u * kBlock);
-      else dst[i + u * kBlock] = v;
+  if constexpr (!kNT) {
+    const size_t threads = static_cast<size_t>(gridDim.x) * blockDim.x;
+    const size_t tid = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const size_t pairs = n16 / 2;
+    for (size_t i = tid; i < pairs; i += threads) {
+      dst[2 * i] = v;
+      dst[2 * i + 1] = v;
     }
-  }
-  for (; i < hi; i += kBlock) {
-    if constexpr (kNT) __builtin_nontemporal_store(v, dst + i);
-    else dst[i] = v;
+    if ((n16 & 1) && tid == 0) dst[n16 - 1] = v;  // an odd count: the last 16 B
+  } else {
+    size_t lo, hi;
+    slab_bounds(n16, &lo, &hi);
+    size_t i = lo + threadIdx.x;
+    for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v, dst + i + u * kBlock);
+    }
+    for (; i < hi; i += kBlock) __builtin_nontemporal_store(v, dst + i);
   }
 }
 
@@ -86,12 +103,11 @@ void hbm_fill(void* dst, size_t nbytes, uint32_t value, StoreMode mode, hipStrea
   if (nbytes % 16) throw std::invalid_argument("hbm_fill: nbytes must be a multiple of 16");
   const size_t n16 = nbytes / 16;
   if (!n16) return;
-  const unsigned grid = grid_for(n16 / 4, 16);
   if (mode == StoreMode::kNonTemporal)
-    hipLaunchKernelGGL(hbm_fill_kernel<true>, dim3(grid), dim3(kBlock), 0, stream,
+    hipLaunchKernelGGL(hbm_fill_kernel<true>, dim3(grid_for(n16 / 4, 16)), dim3(kBlock), 0, stream,
                        static_cast<u32x4*>(dst), n16, value);
   else
-    hipLaunchKernelGGL(hbm_fill_kernel<false>, dim3(grid), dim3(kBlock), 0, stream,
+    hipLaunchKernelGGL(hbm_fill_kernel<false>, dim3(streaming_grid(1)), dim3(kFillBlock), 0, stream,
                        static_cast<u32x4*>(dst), n16, value);
   TK8S_HIP_CHECK(hipGetLastError());
 }
@@ -321,6 +337,53 @@ void ar_check(const void* buf, size_t count, int nranks, DType dtype, float tol,
                        static_cast<const unsigned short*>(buf), count, base, per_mod, tol,
                        max_err_bits, bad);
   TK8S_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// Fault injection: a queue stall that always ends (kernels.h gpu_stall). One wave; lane 0 polls
+// a flag in fine-grained host memory at system scope, sleeping between polls, and gives up after
+// max_ticks of the GPU's constant-rate wall clock: the grid drains whether or not the host ever
+// releases it. The flag is only read here; the host writes it.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void stall_kernel(const unsigned* flag, unsigned long long max_ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u &&
+         wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(127);
+}
+
+namespace {
+std::mutex g_stall_mu;
+unsigned* g_stall_flag = nullptr;  // fine-grained host memory; never freed (a kernel may read it)
+std::atomic<bool> g_stall_armed{false};
+}  // namespace
+
+void gpu_stall(hipStream_t stream, double max_s) {
+  int dev = 0, khz = 0;
+  TK8S_HIP_CHECK(hipGetDevice(&dev));
+  TK8S_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) khz = 100000;  // gfx9: 100 MHz
+  {
+    std::lock_guard<std::mutex> lock(g_stall_mu);
+    if (!g_stall_flag) {
+      void* p = nullptr;
+      TK8S_HIP_CHECK(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+      g_stall_flag = static_cast<unsigned*>(p);
+    }
+    __atomic_store_n(g_stall_flag, 0u, __ATOMIC_SEQ_CST);
+    g_stall_armed = true;
+  }
+  const double s = max_s > 0 ? (max_s < 600 ? max_s : 600) : 1;
+  const auto ticks = static_cast<unsigned long long>(s * khz * 1000.0);
+  hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, stream, g_stall_flag, ticks);
+  TK8S_HIP_CHECK(hipGetLastError());
+}
+
+void gpu_stall_release() {
+  if (!g_stall_armed.exchange(false)) return;
+  std::lock_guard<std::mutex> lock(g_stall_mu);
+  if (g_stall_flag) __atomic_store_n(g_stall_flag, 1u, __ATOMIC_SEQ_CST);
 }
 
 }  // namespace tk8s

@@ -57,6 +57,7 @@
 #include "args.h"
 #include "cachewalk.h"
 #include "reuse.h"
+#include "tk8s/failfast.h"
 #include "tk8s/json.h"
 
 namespace {
@@ -65,6 +66,7 @@ using tk8s::Json;
 
 constexpr const char* kKnownDigest256M = "55af80380d572d36cc8cc7d50edd90ab";
 constexpr uint32_t kBlock = 256;     // stream kernels: 4 wave64s (stream_kernels.hip kBlock)
+constexpr uint16_t kFillBlock = 128; // the plain HBM fill: one 2-wave block per CU (stream_kernels.hip)
 constexpr uint32_t kMd5Block = 256;  // md5_kernels.hip kMd5Block
 constexpr uint64_t kWaveChunks = 64;
 constexpr size_t kAlign = 4096;
@@ -319,7 +321,16 @@ struct Kernel {
 
 struct KernelSet {
   Kernel fill_plain, fill_nt, verify, philox, copy, md5c, md5;
+  Kernel stall;  // fault injection only (TK8S_FAULTS probe.hang@peers): not required
 };
+
+// The stall kernel's release flag (fine-grained host memory every GPU agent may read; the
+// stall_kernel of stream_kernels.hip polls it) -- set by every bounded wait that gives up, so a
+// stalled queue drains (failfast.h).
+std::atomic<uint32_t*> g_stall_flag{nullptr};
+void stall_release() {
+  if (uint32_t* f = g_stall_flag.load()) __atomic_store_n(f, 1u, __ATOMIC_SEQ_CST);
+}
 
 hsa_status_t find_kernels(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t sym, void* data) {
   auto* ks = static_cast<KernelSet*>(data);
@@ -340,6 +351,7 @@ hsa_status_t find_kernels(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t
   else if (name.find("18stream_copy_kernel") != std::string::npos) k = &ks->copy;
   else if (name.find("27md5_chunks_coalesced_kernel") != std::string::npos) k = &ks->md5c;
   else if (name.find("17md5_chunks_kernel") != std::string::npos) k = &ks->md5;
+  else if (name.find("12stall_kernel") != std::string::npos) k = &ks->stall;
   if (!k) return HSA_STATUS_SUCCESS;
   HSA_OK(hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k->object));
   HSA_OK(hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k->kernarg_size));
@@ -523,10 +535,29 @@ class Device {
               d.system ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT, d.sig);
     }
     const hsa_signal_t last = batch_.back().sig;
-    // Bounded active wait: the kernels are finite; a wedged GPU must not hang the bring-up.
+    // Bounded active wait: the kernels are finite; a wedged GPU must not hang the bring-up
+    // (TK8S_GPU_SYNC_TIMEOUT_S, default 30 s). On expiry a fault-injected stall is released and
+    // the queue gets a few seconds to drain; the batch is dropped either way, so the next pull
+    // starts clean.
+    const double bound_ms = tk8s::gpu_sync_timeout_s() * 1000.0;
     const auto t0 = std::chrono::steady_clock::now();
     while (hsa_signal_wait_scacquire(last, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_ACTIVE) >= 1) {
-      if (ms_since(t0) > 30000) throw std::runtime_error("GPU dispatch did not complete within 30 s");
+      if (ms_since(t0) > bound_ms) {
+        stall_release();
+        const auto td = std::chrono::steady_clock::now();
+        bool drained = false;
+        while (!(drained = hsa_signal_load_scacquire(last) < 1) && ms_since(td) < 5000)
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        for (auto& d : batch_) {
+          times_.push_back({0.0, 0.0});
+          if (drained) hsa_signal_destroy(d.sig);
+        }
+        batch_.clear();
+        stage_off_ = 0;
+        char msg[96];
+        std::snprintf(msg, sizeof msg, "GPU dispatch did not complete within %.0f s", bound_ms / 1000.0);
+        throw std::runtime_error(msg);
+      }
     }
     for (auto& d : batch_) {
       hsa_amd_profiling_dispatch_time_t t{};
@@ -546,9 +577,11 @@ class Device {
 
   // ---- the kernels, with the same launch shapes as the HIP wrappers ----
   size_t fill(void* dst, size_t bytes, uint32_t value, bool nt, bool system = false) {
+    // stream_kernels.hip hbm_fill: plain = one 128-thread block per CU (the write-front walk),
+    // non-temporal = the slab walk over CUs x 16 blocks
     const size_t n16 = bytes / 16;
-    const unsigned grid = grid_for(n16 / 4, 16);
-    return launch(nt ? ks_.fill_nt : ks_.fill_plain, grid, kBlock,
+    const unsigned grid = nt ? grid_for(n16 / 4, 16) : static_cast<unsigned>(std::max(g_.cus, 1u));
+    return launch(nt ? ks_.fill_nt : ks_.fill_plain, grid, nt ? kBlock : kFillBlock,
                   [&](KernArgs& a) { a.ptr(dst).u64(n16).u32(value); }, system);
   }
   size_t verify(const void* src, size_t bytes, uint32_t value, void* bad) {
@@ -561,6 +594,13 @@ class Device {
     return launch(ks_.philox, grid_for(n16 / 4, 16), kBlock, [&](KernArgs& a) {
              a.ptr(dst).u64(n16).u32(static_cast<uint32_t>(seed)).u32(static_cast<uint32_t>(seed >> 32));
            });
+  }
+  // Fault injection: one wave that holds the queue until stall_release() or max_s of GPU wall
+  // clock (gfx9: 100 MHz) -- kernels.h gpu_stall, dispatched on ROCr.
+  size_t stall(const uint32_t* flag, double max_s) {
+    if (!ks_.stall.found) throw std::runtime_error("stall kernel missing from the code objects");
+    const auto ticks = static_cast<uint64_t>(max_s * 100e6);
+    return launch(ks_.stall, 1, 64, [&](KernArgs& a) { a.ptr(flag).u64(ticks); });
   }
   size_t copy(void* dst, const void* src, size_t bytes, bool to_host = false, bool from_remote = false) {
     const size_t n16 = bytes / 16;
@@ -836,6 +876,12 @@ std::pair<double, uint64_t> pull(DeviceResult& r, const void* src, uint32_t patt
   char* dst = r.base + align_up(c.peer);
   char* bad = dst + align_up(c.peer);
   const int it = std::max(c.peer_iters, 1);
+  if (tk8s::fault_armed("probe", "hang", "peers")) {  // TK8S_FAULTS probe.hang@peers: a pull that never ends
+    if (uint32_t* f = g_stall_flag.load()) {
+      __atomic_store_n(f, 0u, __ATOMIC_SEQ_CST);
+      d->stall(f, 2 * tk8s::gpu_sync_timeout_s() + 5);
+    }
+  }
   d->copy(dst, src, c.peer, false, /*from_remote=*/true);  // warm-up (and the system-scope acquire)
   size_t first = 0, last = 0;
   for (int i = 0; i < it; ++i) {
@@ -852,8 +898,18 @@ std::pair<double, uint64_t> pull(DeviceResult& r, const void* src, uint32_t patt
   return {d->span_ms(first, last) / it, nbad};
 }
 
-void run_peers(const std::vector<int>& devices, const Config& c, std::vector<DeviceResult>& res) {
+void run_peers(const std::vector<int>& devices, const Config& c, std::vector<DeviceResult>& res, const Host& h) {
   const size_t m = devices.size();
+  tk8s::fault_point("probe", "peers", /*host_hang=*/false);  // TK8S_FAULTS probe.exit|crash@peers
+  if (tk8s::fault_armed("probe", "hang", "peers") && !g_stall_flag.load()) {
+    void* f = nullptr;
+    HSA_OK(hsa_amd_memory_pool_allocate(h.kernarg, 64, 0, &f));
+    std::vector<hsa_agent_t> agents;
+    for (size_t k = 0; k < m; ++k)
+      if (res[k].dev) agents.push_back(res[k].dev->gpu().agent);
+    HSA_OK(hsa_amd_agents_allow_access(static_cast<uint32_t>(agents.size()), agents.data(), nullptr, f));
+    g_stall_flag = static_cast<uint32_t*>(f);
+  }
   // 1. every source buffer gets its pattern, released at system scope (peers read it next).
   for (size_t k = 0; k < m; ++k) {
     if (!res[k].dev) continue;
@@ -1067,7 +1123,7 @@ int main(int argc, char** argv) {
     run_one(0);
     for (auto& th : threads) th.join();
     const auto tp = std::chrono::steady_clock::now();
-    if (c.peers && devices.size() > 1) run_peers(devices, c, res);
+    if (c.peers && devices.size() > 1) run_peers(devices, c, res, t.host);
     if (c.peers_host) run_host_pull(t.host, devices[0], c, res[0]);
     const double peers_ms = ms_since(tp);
 

@@ -7,9 +7,19 @@
 //                           ... (--uid-file PATH | --kv-url http://host:port/v1/kv/KEY)
 //   The process holding rank 0 creates the RCCL unique id and publishes it (atomic file rename,
 //   or HTTP PUT to the control-plane KV); the others wait for it (file poll, or HTTP long-poll).
-// Sweep: --min-bytes B --max-bytes B --factor F --iters K --warmup W --dtype float32|bfloat16
+// Sweep: --min-bytes B (8) --max-bytes B (1 GiB) --factor F (2) --iters K --warmup W
+//        --dtype float32|bfloat16|both (default both: the RCCL-tests sweep of SURVEY.md N3)
 // [--teardown]: free the communicators before exiting (default: print the result and _Exit)
 // Prints one JSON object; exit 0 iff every size reduced exactly.
+//
+// Fail fast: --op-timeout S (default 20) bounds every wait --
+// the unique id fetch, the communicator init, each sweep point, each check; a wait that runs
+// out, or an RCCL async error, aborts the communicators and prints {"ok":false,"phase":..,
+// "error":..} (exit 1). A watchdog thread ends the process (same JSON, "watchdog":true, exit 4)
+// if a phase makes no progress for op-timeout + 10 s at all -- a call blocked inside RCCL.
+// Fault points (TK8S_FAULTS): rccl.hang@uid|init (host stops), rccl.hang@sweep|check (the GPU
+// queue stalls), rccl.exit@<phase> (exit 3), rccl.crash@<phase> (abort).
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstdio>
@@ -20,9 +30,12 @@
 #include <thread>
 #include <vector>
 
+#include <atomic>
+
 #include "args.h"
 #include "httpkv.h"
 #include "tk8s/common.h"
+#include "tk8s/failfast.h"
 #include "tk8s/rccl_bench.h"
 #include "cachewalk.h"
 
@@ -42,8 +55,9 @@ bool publish_uid(const tk8s::Args& a, const std::string& hex) {
   return tk8s::http_request("PUT", a.str("kv-url"), hex, &r) && r.status / 100 == 2;
 }
 
-bool fetch_uid(const tk8s::Args& a, std::string* hex, int timeout_s) {
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+bool fetch_uid(const tk8s::Args& a, std::string* hex, double timeout_s) {
+  const auto deadline = std::chrono::steady_clock::now() +
+                        std::chrono::milliseconds(static_cast<long long>(timeout_s * 1000));
   while (std::chrono::steady_clock::now() < deadline) {
     if (a.has("uid-file")) {
       std::ifstream f(a.str("uid-file"));
@@ -56,8 +70,12 @@ bool fetch_uid(const tk8s::Args& a, std::string* hex, int timeout_s) {
       std::this_thread::sleep_for(std::chrono::milliseconds(5));
     } else {
       tk8s::HttpResponse r;
-      // Long-poll: the control plane holds the request until the key exists (or ~wait s).
-      if (tk8s::http_request("GET", a.str("kv-url") + "?wait=10", "", &r, 15) && r.status == 200) {
+      // Long-poll: the control plane holds the request until the key exists (or ~wait s), never
+      // past the deadline
+      const double left = std::chrono::duration<double>(deadline - std::chrono::steady_clock::now()).count();
+      const int wait = static_cast<int>(std::max(1.0, std::min(10.0, left)));
+      if (tk8s::http_request("GET", a.str("kv-url") + "?wait=" + std::to_string(wait), "", &r, wait + 5) &&
+          r.status == 200) {
         *hex = r.body;
         while (!hex->empty() && (hex->back() == '\n' || hex->back() == '\r')) hex->pop_back();
         if (hex->size() == 2 * NCCL_UNIQUE_ID_BYTES) return true;
@@ -92,6 +110,17 @@ void trace(const char* what) {
   std::fprintf(stderr, "TRACE %.6f rccl %s\n", t, what);
 }
 
+// TK8S_FAULTS rccl.hang@sweep|check: the GPU-side hang (a stall kernel on the ranks' streams);
+// exit / crash at those phases end the process when the validator enters them (on_phase).
+std::string stall_phase() {
+  for (const char* ph : {"sweep", "check"})
+    if (tk8s::fault_armed("rccl", "hang", ph)) return ph;
+  return "";
+}
+
+// What the process is doing, for the watchdog's error line.
+std::atomic<int> g_nranks{1}, g_first{0}, g_local{1};
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -101,16 +130,48 @@ int main(int argc, char** argv) {
     tk8s::Args a(argc, argv);
     tk8s::AllReduceConfig cfg;
     cfg.min_bytes = static_cast<size_t>(a.num("min-bytes", 8));
-    cfg.max_bytes = static_cast<size_t>(a.num("max-bytes", 1LL << 28));
+    cfg.max_bytes = static_cast<size_t>(a.num("max-bytes", 1LL << 30));
     cfg.factor = static_cast<int>(a.num("factor", 2));
     cfg.iters = static_cast<int>(a.num("iters", 20));
     cfg.warmup = static_cast<int>(a.num("warmup", 5));
-    cfg.dtype = a.str("dtype", "float32") == "bfloat16" ? tk8s::DType::kBF16 : tk8s::DType::kF32;
+    const std::string dt = a.str("dtype", "both");
+    if (dt == "float32") cfg.dtypes = {tk8s::DType::kF32};
+    else if (dt == "bfloat16") cfg.dtypes = {tk8s::DType::kBF16};
+    else if (dt == "both") cfg.dtypes = {tk8s::DType::kF32, tk8s::DType::kBF16};
+    else {
+      std::fprintf(stderr, "tk8s-rccl: --dtype must be float32, bfloat16 or both\n");
+      return 2;
+    }
     cfg.check = !a.has("no-check");
+    cfg.op_timeout_s = std::strtod(a.str("op-timeout", "20").c_str(), nullptr);
+    cfg.blocking = std::getenv("TK8S_RCCL_BLOCKING") && std::string(std::getenv("TK8S_RCCL_BLOCKING")) == "1";
     // the process exits right after its JSON line (see below) -- unless a profiler's library is
     // preloaded: its exit handlers write the trace, and _Exit would skip them
     const char* preload = std::getenv("LD_PRELOAD");
     cfg.teardown = a.has("teardown") || (preload && std::strstr(preload, "rocprof"));
+    // The backstop: no progress in a phase for op-timeout + 10 s (a call blocked inside a library)
+    // ends the process with the phase named.
+    const double grace = 10.0;
+    tk8s::Watchdog dog([](const std::string& phase, double waited) {
+      std::printf("%s\n", tk8s::Json()
+                              .kv("ok", false)
+                              .kv("phase", phase)
+                              .kv("error", "watchdog: no progress in phase " + phase + " for " +
+                                               std::to_string(static_cast<int>(waited)) + " s")
+                              .kv("timed_out", true)
+                              .kv("watchdog", true)
+                              .kv("nranks", g_nranks.load())
+                              .kv("first_rank", g_first.load())
+                              .kv("local_ranks", g_local.load())
+                              .str()
+                              .c_str());
+      trace("watchdog");
+    });
+    const bool bounded = cfg.op_timeout_s > 0;
+    cfg.on_phase = [&dog, bounded, grace](const std::string& phase, double s) {
+      if (bounded) dog.arm(phase, s + grace);
+      tk8s::fault_point("rccl", phase, /*host_hang=*/false);  // rccl.exit|crash@sweep|check
+    };
     std::string out;
     if (a.has("rank") || a.has("group-index")) {
       const int nranks = static_cast<int>(a.num("nranks", 1));
@@ -122,6 +183,10 @@ int main(int argc, char** argv) {
       }
       const int first = a.has("rank") ? static_cast<int>(a.num("rank", 0))
                                       : static_cast<int>(a.num("group-index", 0)) * static_cast<int>(devices.size());
+      g_nranks = nranks;
+      g_first = first;
+      g_local = static_cast<int>(devices.size());
+      tk8s::set_fault_ranks(first, static_cast<long>(devices.size()));  // ":<rank>"-targeted fault points
       if (!a.has("uid-file") && !a.has("kv-url")) {
         std::fprintf(stderr, "tk8s-rccl: --rank/--group-index needs --uid-file or --kv-url\n");
         return 2;
@@ -133,25 +198,40 @@ int main(int argc, char** argv) {
         (void)hipGetDeviceCount(&n);
         trace("hip runtime up");
       }
+      // the uid exchange is bounded by the same budget as every other wait
+      const double uid_timeout = std::strtod(a.str("uid-timeout", a.str("op-timeout", "20")).c_str(), nullptr);
+      if (bounded) dog.arm("uid", uid_timeout + grace);
+      tk8s::fault_point("rccl", "uid");
       if (first == 0) {
         trace("ncclGetUniqueId");
         if (ncclGetUniqueId(&id) != ncclSuccess) {
-          std::fprintf(stderr, "tk8s-rccl: ncclGetUniqueId failed\n");
+          std::printf("{\"ok\":false,\"phase\":\"uid\",\"error\":\"ncclGetUniqueId failed\"}\n");
           return 2;
         }
         hex = tk8s::nccl_unique_id_hex(id);
         if (!publish_uid(a, hex)) {
-          std::fprintf(stderr, "tk8s-rccl: could not publish unique id\n");
+          std::printf("{\"ok\":false,\"phase\":\"uid\",\"error\":\"could not publish the unique id\"}\n");
           return 2;
         }
       } else {
-        if (!fetch_uid(a, &hex, static_cast<int>(a.num("uid-timeout", 120))) ||
-            !tk8s::nccl_unique_id_from_hex(hex, &id)) {
-          std::fprintf(stderr, "tk8s-rccl: timed out waiting for the unique id\n");
-          return 2;
+        if (!fetch_uid(a, &hex, uid_timeout > 0 ? uid_timeout : 1e9) || !tk8s::nccl_unique_id_from_hex(hex, &id)) {
+          std::printf("%s\n", tk8s::Json()
+                                  .kv("ok", false)
+                                  .kv("phase", "uid")
+                                  .kv("error", "no unique id from rank 0 within " + a.str("uid-timeout", a.str("op-timeout", "20")) + " s")
+                                  .kv("timed_out", true)
+                                  .kv("nranks", nranks)
+                                  .kv("first_rank", first)
+                                  .str()
+                                  .c_str());
+          std::fflush(stdout);
+          std::_Exit(1);
         }
       }
       trace(first == 0 ? "unique id published" : "unique id fetched");
+      if (bounded) dog.arm("init", cfg.op_timeout_s + grace);
+      tk8s::fault_point("rccl", "init");
+      cfg.stall_phase = stall_phase();
       out = tk8s::allreduce_rank_group(first, nranks, devices, id, cfg);
       trace("sweep done");
     } else {
@@ -163,11 +243,21 @@ int main(int argc, char** argv) {
       const int want = static_cast<int>(a.num("ngpus", n));
       std::vector<int> devs;
       for (int i = 0; i < want && i < n; ++i) devs.push_back(i);
+      g_nranks = static_cast<int>(devs.size());
+      g_local = static_cast<int>(devs.size());
+      tk8s::set_fault_ranks(0, static_cast<long>(devs.size()));
+      if (bounded) dog.arm("init", cfg.op_timeout_s + grace);
+      tk8s::fault_point("rccl", "init");
+      cfg.stall_phase = stall_phase();
       out = tk8s::allreduce_single_process(devs, cfg);
     }
+    dog.disarm();
     std::printf("%s\n", out.c_str());
-    const int rc = out.find("\"ok\":true") != std::string::npos ? 0 : 1;
-    if (!cfg.teardown) {  // the result is out: leave without the communicators' and runtime's teardown
+    const bool ok = out.find("\"ok\":true") != std::string::npos;
+    const int rc = ok ? 0 : 1;
+    // the result is out: leave without the communicators' and runtime's teardown (always after a
+    // failure: an aborted communicator has nothing left worth a clean exit)
+    if (!cfg.teardown || !ok) {
       std::fflush(stdout);
       std::fflush(stderr);
       trace("exit");
@@ -175,6 +265,7 @@ int main(int argc, char** argv) {
     }
     return rc;
   } catch (const std::exception& e) {
+    std::printf("%s\n", tk8s::Json().kv("ok", false).kv("phase", "setup").kv("error", e.what()).str().c_str());
     std::fprintf(stderr, "tk8s-rccl: %s\n", e.what());
     return 2;
   }

@@ -78,6 +78,11 @@ def test_bench_single_process(tmp_path):
         spent += pt["steps"] * pt["ms_per_step"] / 1000.0
     assert spent <= curve["wall_s"] <= run_wall, (spent, curve["wall_s"], run_wall)
     assert curve["scaling_8_vs_1"] == round(curve["points"][-1]["mean_s"] / curve["points"][0]["mean_s"], 3)
+    # every point says where its time went -- mean phases and its slowest tasks
+    for pt in curve["points"]:
+        assert {"provision", "ansible"} <= set(pt["phases_s"]), pt
+        assert pt["slowest_tasks"] and all({"what", "mean_s", "steps"} <= set(t) for t in pt["slowest_tasks"]), pt
+        assert pt["slowest_tasks"] == sorted(pt["slowest_tasks"], key=lambda t: -t["mean_s"])
     assert p.stderr.count("(timed)") == 2 and p.stderr.count("(warmup)") == 1
     # the step bracket is the Ready time plus what ./setup.sh does after
     # Ready, not a polling quantum on top
@@ -150,8 +155,11 @@ def test_bench_reports_post_ready_failures(monkeypatch, capsys, tmp_path):
     monkeypatch.setenv("TMPDIR", str(tmp_path))
     calls = {"n": 0}
 
+    rccls = []
+
     def fake_bringup(ws, n, args, env, log, census=None, package=None, rccl=None):
         calls["n"] += 1
+        rccls.append(rccl)
         if calls["n"] == 2:
             return {"wall_seconds": 0.3, "ready_wall_seconds": 0.2, "phases": {}, "post_ready_error": "exit 2: RCCL"}
         return {"wall_seconds": 0.3, "ready_wall_seconds": 0.25, "ready_seconds": 0.24, "phases": {"ready": 0.1},
@@ -167,7 +175,33 @@ def test_bench_reports_post_ready_failures(monkeypatch, capsys, tmp_path):
     # the failed step is flagged and left out of value
     assert out["post_ready_errors"]["excluded_steps"] == [1]
     assert out["min_s"] == out["max_s"] == out["value"] == 0.25 and out["ready_s_inside_setup"] == 0.24
+    # after the first post-Ready failure the fabric check is off for every later step
+    assert rccls[:3] == [None, None, "off"] and set(rccls[3:]) <= {"off"} and out["fabric_disabled_after_step"] == 1
+    assert "RCCL" in out["fabric_disabled"]["error_tail"] and "then off" in out["config"]["rccl"]
     assert "not like-for-like" in out["vs_baseline_note"].replace("NOT", "not")
+
+
+@pytest.mark.timeout(400)
+def test_bench_with_a_hung_rank_still_prints_its_line(tmp_path):
+    """VERDICT r5 #1 'done when': a fault armed in one fabric rank (a hang in the sweep) costs one
+    bounded check; the bench finishes every step with the check off afterwards and prints value."""
+    import time
+
+    env = _env(tmp_path)
+    env["TK8S_FAULTS"] = "rccl.hang@sweep:1"
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--fake-gpus", "2",
+                        "--curve-steps", "0", "--plain-steps", "0", "--fabric-steps", "1", "--rccl-op-timeout", "3"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=380)
+    wall = time.monotonic() - t0
+    assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
+    out = _json_line(p.stdout)
+    assert out["value"] > 0 and out["fabric_disabled_after_step"] == 0, out
+    assert out["fabric_disabled"]["kind"] == "warmup" and "phase" in out["fabric_disabled"]["error_tail"]
+    assert out["fabric_validated_s"] is None and "skipped" in out["fabric_validated"]
+    assert "post_ready_errors" not in out  # the failure was in the warmup step; every timed step counted
+    assert p.stderr.count("(timed)") == 3
+    assert wall < 200, wall
 
 
 def test_bench_kills_a_silent_hang(tmp_path):

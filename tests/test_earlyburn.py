@@ -181,18 +181,24 @@ def _hsaprobe():
     del ws
 
 
-def test_multi_gpu_pulls_take_the_hip_peer_path_unless_asked(monkeypatch):
-    """the HSA probe's peer grants have not run on a multi-GPU box, so the
-    host burn-in's xGMI pulls go through the HIP probe (hipDeviceEnablePeerAccess, RCCL's own P2P
-    path) unless TK8S_PEERS_RUNTIME=hsa; one-GPU burn-ins keep the faster HSA start."""
+def test_multi_gpu_pulls_take_the_hsa_payload_unless_asked(monkeypatch):
+    """one burn-in runtime at every N -- the HSA payload pulls the xGMI links too
+    (its peer phase falls back to the HIP probe when it fails, burnin.HostBurnin), unless
+    TK8S_PEERS_RUNTIME=hip; the Ready path pulls 16 MiB per link."""
     monkeypatch.delenv("TK8S_FAKE_GPUS", raising=False)
     monkeypatch.delenv("TK8S_PEERS_RUNTIME", raising=False)
+    monkeypatch.delenv("TK8S_PROBE_RUNTIME", raising=False)
     base = earlyburn.default_validation_command(peers=False)
     one = earlyburn.host_burnin_command(base, [0])
     many = earlyburn.host_burnin_command(base, [0, 1])
     assert "--peers" not in one and "--peers" in many
-    assert os.path.basename(many[0]) == "tk8s-probe"
-    if os.path.basename(base[0]) == "tk8s-hsaprobe":
-        assert os.path.basename(one[0]) == "tk8s-hsaprobe"
-    monkeypatch.setenv("TK8S_PEERS_RUNTIME", "hsa")
-    assert os.path.basename(earlyburn.probe_tool(peers=True)) == os.path.basename(earlyburn.probe_tool())
+    assert many[many.index("--peer-bytes") + 1] == str(16 << 20)
+    assert os.path.basename(many[0]) == os.path.basename(base[0])  # the same runtime as the local probes
+    if os.path.basename(many[0]) == "tk8s-hsaprobe":
+        assert "--no-peer-dma" not in many
+    monkeypatch.setenv("TK8S_PEERS_RUNTIME", "hip")
+    hip = earlyburn.host_burnin_command(base, [0, 1])
+    assert os.path.basename(hip[0]) == "tk8s-probe" and "--no-peer-dma" in hip
+    fb = earlyburn.hip_peer_command(many)
+    assert os.path.basename(fb[0]) == "tk8s-probe" and fb[fb.index("--peer-bytes") + 1] == str(16 << 20)
+    assert fb[fb.index("--hbm-bytes") + 1] == "0" and "--skip-md5" in fb and fb[fb.index("--copy-bytes") + 1] == "0"

@@ -114,18 +114,20 @@ def test_transport_report_of_a_one_rank_log(tmp_path):
 
 
 def test_the_fabric_rank_env_carries_the_unpacked_library_and_huge_page_malloc(monkeypatch, tmp_path):
-    """fabric.rccl_rank_env: LD_LIBRARY_PATH to the unpacked copy and glibc's malloc on huge pages
-    (profiles/r5_thp: 318 -> 202 ms communicator start), each with its own off-switch; fake GPUs
-    get neither. A GLIBC_TUNABLES already set is kept."""
+    """fabric.rccl_rank_env: the unpacked copy asked for (the node's agent prepends ITS copy to the
+    rank's LD_LIBRARY_PATH) and glibc's malloc on huge pages (profiles/r5_thp: 318 -> 202 ms
+    communicator start), each with its own off-switch; fake GPUs get neither. A GLIBC_TUNABLES
+    already set is kept."""
     from tritonk8ssupervisor_amd import fabric
     from tritonk8ssupervisor_amd.utils import rccl_unpack
 
     monkeypatch.setattr(rccl_unpack, "library_dir", lambda: tmp_path)
-    for var in ("TK8S_RCCL_THP", "GLIBC_TUNABLES", "NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "TK8S_SHORTCUTS"):
+    for var in ("TK8S_RCCL_THP", "GLIBC_TUNABLES", "NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "TK8S_SHORTCUTS", "TK8S_FAULTS",
+                "TK8S_GPU_SYNC_TIMEOUT_S", "TK8S_RCCL_BLOCKING"):
         monkeypatch.delenv(var, raising=False)
     env, lib = fabric.rccl_rank_env()
     assert lib == tmp_path
-    assert {e["name"]: e["value"] for e in env} == {"LD_LIBRARY_PATH": str(tmp_path),
+    assert {e["name"]: e["value"] for e in env} == {"TK8S_RCCL_UNPACKED": "1",
                                                      "GLIBC_TUNABLES": "glibc.malloc.hugetlb=1"}
     monkeypatch.setenv("GLIBC_TUNABLES", "glibc.malloc.arena_max=2")
     monkeypatch.setenv("NCCL_DEBUG", "INFO")
@@ -136,6 +138,42 @@ def test_the_fabric_rank_env_carries_the_unpacked_library_and_huge_page_malloc(m
     assert "GLIBC_TUNABLES" not in {e["name"] for e in fabric.rccl_rank_env()[0]}
     env, lib = fabric.rccl_rank_env(fake=True)
     assert lib is None and [e["name"] for e in env] == ["NCCL_DEBUG"]
+
+
+def test_the_agent_prepends_its_own_unpacked_copy(tmp_path):
+    """the rank's LD_LIBRARY_PATH is the node's copy IN FRONT of the path the node's
+    runtime passes on (not replacing it); no request, or no current copy on that node: unchanged."""
+    from tritonk8ssupervisor_amd.agent.agent import unpacked_rccl_env
+
+    ask = {"TK8S_RCCL_UNPACKED": "1"}
+    assert unpacked_rccl_env(ask, {"LD_LIBRARY_PATH": "/opt/x/lib"}, lambda: tmp_path) == {
+        "LD_LIBRARY_PATH": f"{tmp_path}:/opt/x/lib"}
+    assert unpacked_rccl_env(ask, {}, lambda: tmp_path) == {"LD_LIBRARY_PATH": str(tmp_path)}
+    assert unpacked_rccl_env(ask, {"LD_LIBRARY_PATH": "/opt/x/lib"}, lambda: None) == {}
+    assert unpacked_rccl_env({}, {"LD_LIBRARY_PATH": "/opt/x/lib"}, lambda: tmp_path) == {}
+
+
+def test_the_fabric_rank_env_passes_the_fail_fast_knobs_and_rccl_faults(monkeypatch):
+    from tritonk8ssupervisor_amd import fabric
+
+    monkeypatch.setenv("TK8S_FAULTS", "agent.crash@kubenode1, rccl.hang@sweep:1,xgmi.degrade@0-1:0.1,rccl.exit@uid")
+    monkeypatch.setenv("TK8S_GPU_SYNC_TIMEOUT_S", "3")
+    env, _ = fabric.rccl_rank_env(fake=True)
+    got = {e["name"]: e["value"] for e in env}
+    assert got["TK8S_FAULTS"] == "rccl.hang@sweep:1,rccl.exit@uid" and got["TK8S_GPU_SYNC_TIMEOUT_S"] == "3"
+
+
+def test_elf_section_survives_truncated_and_odd_files(tmp_path):
+    """a truncated or malformed library must not raise out of the optional unpack."""
+    sh = Path("/bin/sh").resolve().read_bytes()
+    for n in (0, 10, 64, 200, len(sh) // 2):
+        f = tmp_path / f"t{n}"
+        f.write_bytes(sh[:n])
+        ru.elf_section(f, ".hip_fatbin")  # None or a tuple; never struct.error / IndexError
+    odd = bytearray(sh[:64]) + bytes(64)
+    odd[0x3C:0x3E] = (0xFFFF).to_bytes(2, "little")  # e_shnum far beyond the file
+    (tmp_path / "odd").write_bytes(bytes(odd))
+    assert ru.elf_section(tmp_path / "odd", ".text") is None
 
 
 def test_doctor_reports_the_huge_page_mode(tmp_path):

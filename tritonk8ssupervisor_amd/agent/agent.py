@@ -97,6 +97,22 @@ def operator_state_dirs() -> list[Path]:
     return dirs
 
 
+def unpacked_rccl_env(container_env: dict, merged: dict, library_dir=None) -> dict:
+    """The fabric Job's ranks ask (``TK8S_RCCL_UNPACKED=1``) for RCCL with its gfx950 device code
+    unpacked (utils/rccl_unpack.py): THIS node's copy -- checked against THIS node's ROCm -- goes
+    in front of the library path the rank would otherwise have (the host's own path is
+    kept, and a node whose copy is stale or missing loads its installed RCCL)."""
+    if container_env.get("TK8S_RCCL_UNPACKED") != "1":
+        return {}
+    if library_dir is None:
+        from ..utils.rccl_unpack import library_dir
+    lib = library_dir()
+    if lib is None:
+        return {}
+    rest = merged.get("LD_LIBRARY_PATH", "")
+    return {"LD_LIBRARY_PATH": str(lib) + (":" + rest if rest else "")}
+
+
 def pod_base_env(environ=None) -> dict:
     env = os.environ if environ is None else environ
     out = {k: v for k, v in env.items() if k in POD_ENV_KEEP or k.startswith(POD_ENV_KEEP_PREFIXES)}
@@ -893,6 +909,7 @@ class Agent:
             else:
                 v = _expand(str(e.get("value", "")), merged)
             out[e["name"]] = merged[e["name"]] = v
+        out.update(unpacked_rccl_env(out, merged))
         return out
 
     def _service_account_dir(self, pod: dict, pp_dir: Path) -> Path | None:

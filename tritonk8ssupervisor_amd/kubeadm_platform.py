@@ -140,10 +140,13 @@ class KubeadmPlatform:
                 raise SetupError(f"RCCL all-reduce validation failed on {node}: pod {pod} reported "
                                  f"{json.dumps(res)[:400] if res else repr(log.strip()[-400:])}", code=2)
             results[node] = res
-        peak = max((r.get("peak_busbw_gbps", 0.0) for r in results.values()), default=0.0)
+        from .fabric import bandwidth_summary
+
+        # one Job per node: each node's ranks form their own communicator (busbw null for a 1-GPU node)
+        bw = bandwidth_summary(list(results.values()), max(gpu_nodes.values()))
         return {"ok": True, "platform": "kubeadm", "run": run_id, "jobs": [f"kube-system/{j}" for j in jobs.values()],
                 "pods": len(results), "nranks": sum(gpu_nodes.values()), "gpus_per_pod": max(gpu_nodes.values()),
-                "peak_busbw_gbps": peak,
+                **bw,
                 "rank_results": [{"pod": verdict["pods"][n], "node": n, "ok": True,
                                   "peak_busbw_gbps": r.get("peak_busbw_gbps"), "comm_init_ms": r.get("comm_init_ms")}
                                  for n, r in sorted(results.items())]}
@@ -190,8 +193,9 @@ class KubeadmPlatform:
             self.out(f"----> {self.summary['nodes']} node(s) Ready, {self.summary['gpus_allocatable']} x amd.com/gpu "
                      "allocatable")
         if rccl:
-            self.out(f"----> RCCL all-reduce: {rccl['pods']} node(s), {rccl['nranks']} GPU(s), peak busbw "
-                     f"{rccl['peak_busbw_gbps']:.1f} GB/s")
+            bw = (f"peak busbw {rccl['peak_busbw_gbps']:.1f} GB/s" if rccl.get("peak_busbw_gbps") is not None
+                  else "1 GPU per node: no fabric")
+            self.out(f"----> RCCL all-reduce: {rccl['pods']} node(s), {rccl['nranks']} GPU(s), {bw}")
         self.out(f"----> bring-up: {t_ready:.3f}s to all nodes Ready ({total:.3f}s including fabric validation)")
         return self.summary
 

@@ -25,7 +25,7 @@ from pathlib import Path
 from . import hcl
 from .config import ClusterConfig, export_vars, read_config, write_config
 from .earlyburn import default_validation_command  # noqa: F401 - shared with the early burn-in
-from .fabric import FabricCheck, check_pmc_counters, rccl_transports, summarize_rocprof  # noqa: F401
+from .fabric import FabricCheck, check_pmc_counters, fabric_line, rccl_transports, summarize_rocprof  # noqa: F401
 from .kubeadm_platform import KUBEADM_RESET, KubeadmPlatform, kubeadm_extra_vars
 from .provider import get_provider
 from .provider.base import Machine, ProvisionError
@@ -83,7 +83,7 @@ class Setup(KubeadmPlatform, FabricCheck):
                  md5_bytes: int = 256 << 20, probe_iters: int = 3, rccl_max_bytes: int = 64 << 20,
                  node_grace: float = 5.0, backend: str | None = None, master_port: int | None = None,
                  rocprof: bool = False, rccl_timeout: float | None = None, rocprof_counters: str | None = None,
-                 platform: str | None = None):
+                 platform: str | None = None, rccl_op_timeout: float = 20.0):
         self.ws = ws
         self.answers = answers
         self.assume_yes = assume_yes
@@ -104,6 +104,7 @@ class Setup(KubeadmPlatform, FabricCheck):
         self.rocprof = rocprof
         self.rocprof_counters = [c for c in (rocprof_counters or "").replace(" ", ",").split(",") if c]
         self.rccl_timeout = rccl_timeout
+        self.rccl_op_timeout = rccl_op_timeout
         ws.state_dir.mkdir(parents=True, exist_ok=True)
         self.events = EventLog(ws.events, echo=False)
         if self.platform == "kubeadm" and self.backend == "local" and local_kubeadm_allowed():
@@ -586,7 +587,7 @@ class Setup(KubeadmPlatform, FabricCheck):
         self.out(f"----> Kubernetes dashboard is at {self.summary['dashboard']}")
         self.out(f"----> Kubernetes CLI config is at {self.summary['kubectl_config']}")
         self.out(f"----> {self.summary['nodes']} node(s) Ready, {self.summary['gpus_allocatable']} x amd.com/gpu allocatable"
-                 + (f", RCCL all-reduce peak busbw {rccl['peak_busbw_gbps']:.1f} GB/s over {rccl['nranks']} GPU(s)" if rccl else ""))
+                 + (f", {fabric_line(rccl)}" if rccl else ""))
         self.out(f"----> bring-up: {t_ready:.3f}s to all nodes Ready ({total:.3f}s including fabric validation)")
         self.out("")
         self.out("    CONGRATULATIONS, YOU HAVE CONFIGURED YOUR KUBERNETES ENVIRONMENT!")

@@ -19,6 +19,15 @@ transport RCCL's channels took (``transport``: counts of ``via P2P/...``, ``via 
 ``via NET/...`` connections, and whether the communicator's init completed) -- what tells
 whether ranks in separate pods still go GPU to GPU over xGMI.
 
+Fail fast (the same contract as tk8s-rccl, native/include/tk8s/failfast.h):
+``--op-timeout`` (alias ``--timeout``, default 20 s) bounds the rendezvous fetch, the process
+group's init and every collective (gloo's own timeout); a failure prints ``{"ok": false,
+"phase": ...}`` and exits 2; a watchdog thread ends a rank whose phase makes no progress for
+op-timeout + 10 s (exit 4, as tk8s-rccl's). Fault points (``TK8S_FAULTS``, ``[:rank]`` targets one rank):
+``rccl.hang@<phase>`` (the rank stops), ``rccl.exit@<phase>`` (exit 3), ``rccl.crash@<phase>``
+(abort) for phases uid / init / sweep / check -- how the CPU tests kill or hang one rank of a
+2- or 8-rank job and show every other rank still ends within its deadline.
+
 Check (N6 semantics): rank r contributes ``(r + 1) * p[i]`` with ``p[i] = (i % m) + 1``;
 every element must equal ``n (n + 1) / 2 * p[i]`` exactly. ``m`` keeps every partial sum an
 exactly representable integer: 251 for fp32 (< 2^24), 4 for bf16 (sums <= 256 up to n = 8).
@@ -34,6 +43,58 @@ import urllib.request
 
 
 SA_TOKEN = "/var/run/secrets/kubernetes.io/serviceaccount/token"
+WATCHDOG_GRACE_S = 10.0
+WATCHDOG_EXIT = 4  # = tk8s::kWatchdogExit (native/include/tk8s/failfast.h)
+
+
+class Phases:
+    """The rank's current phase, a no-progress watchdog over it, and its fault points."""
+
+    def __init__(self, rank: int | None, nranks: int, op_timeout: float):
+        import threading
+
+        self.rank, self.nranks, self.op_timeout = rank, nranks, op_timeout
+        self.phase, self.deadline, self.started = "start", 0.0, 0.0
+        self.lock = threading.Lock()
+        if op_timeout > 0:
+            threading.Thread(target=self._watch, name="watchdog", daemon=True).start()
+
+    def enter(self, phase: str) -> None:
+        with self.lock:
+            self.phase, self.started = phase, time.monotonic()
+            self.deadline = self.started + self.op_timeout + WATCHDOG_GRACE_S
+        self._faults(phase)
+
+    def _watch(self) -> None:
+        while True:
+            time.sleep(0.05)
+            with self.lock:
+                if not self.deadline or time.monotonic() < self.deadline:
+                    continue
+                phase, waited = self.phase, time.monotonic() - self.started
+            print(json.dumps({"ok": False, "rank": self.rank, "nranks": self.nranks, "phase": phase, "timed_out": True,
+                              "watchdog": True, "error": f"watchdog: no progress in phase {phase} for {waited:.0f} s"}),
+                  flush=True)
+            os._exit(WATCHDOG_EXIT)
+
+    def _faults(self, phase: str) -> None:
+        from ..utils.faults import _parse
+
+        for point, target, arg in _parse(os.environ.get("TK8S_FAULTS", "")):
+            if target != phase or not point.startswith("rccl."):
+                continue
+            if arg is not None and (self.rank is None or arg != str(self.rank)):
+                continue
+            kind = point[len("rccl."):]
+            sys.stderr.write(f"dist_allreduce rank {self.rank}: TK8S_FAULTS {point}@{phase}\n")
+            sys.stderr.flush()
+            if kind == "exit":
+                os._exit(3)
+            if kind == "crash":
+                os.abort()
+            if kind == "hang":
+                while True:
+                    time.sleep(1)
 
 
 def _kv_headers() -> dict:
@@ -60,9 +121,10 @@ def _publish(url: str, value: str) -> None:
 def _fetch(url: str, timeout: float) -> str:
     deadline = time.monotonic() + timeout
     while time.monotonic() < deadline:
+        wait = max(1, min(10, int(deadline - time.monotonic())))  # a long-poll never outlives the deadline
         try:
-            v = urllib.request.urlopen(urllib.request.Request(url + "?wait=10", headers=_kv_headers()),
-                                       timeout=15).read().decode().strip()
+            v = urllib.request.urlopen(urllib.request.Request(url + f"?wait={wait}", headers=_kv_headers()),
+                                       timeout=wait + 5).read().decode().strip()
             if v:
                 return v
         except OSError:
@@ -98,7 +160,7 @@ def _debug_file() -> str | None:
 
 
 def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters: int, warmup: int,
-          dtype: str = "float32", device: str = "cpu") -> dict:
+          dtype: str = "float32", device: str = "cpu", phases: Phases | None = None) -> dict:
     import torch
     import torch.distributed as dist
 
@@ -112,6 +174,8 @@ def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters:
         pat = (torch.arange(count, dtype=torch.int64, device=device) % (251 if dt == torch.float32 else 4) + 1)
         want = (pat * (n * (n + 1) // 2)).to(dt)
         buf = torch.empty(count, dtype=dt, device=device)
+        if phases is not None:
+            phases.enter("sweep")
         for _ in range(warmup):
             buf.copy_(pat * (rank + 1))
             dist.all_reduce(buf)
@@ -125,16 +189,19 @@ def sweep(rank: int, n: int, min_bytes: int, max_bytes: int, factor: int, iters:
             dist.all_reduce(buf)
             sync()
             times.append(time.perf_counter() - t)
+            if phases is not None and phases.phase != "check":
+                phases.enter("check")
             bad = max(bad, int((buf != want).sum()))
         sec = sorted(times)[len(times) // 2]
         algbw = count * esize / sec / 1e9
-        busbw = algbw * (2 * (n - 1) / n if n > 1 else 1.0)
+        busbw = algbw * 2 * (n - 1) / n if n > 1 else 0.0  # 0 at n = 1 (no fabric)
         peak = max(peak, busbw)
         ok &= bad == 0
         results.append({"bytes": count * esize, "count": count, "time_us": sec * 1e6, "algbw_gbps": algbw,
                         "busbw_gbps": busbw, "bad": bad})
         size *= factor
-    return {"ok": ok, "results": results, "peak_busbw_gbps": peak}
+    return {"ok": ok, "results": results, "peak_busbw_gbps": peak if n > 1 else None,
+            "peak_algbw_gbps": max((r["algbw_gbps"] for r in results), default=0.0)}
 
 
 def _rank_group(a, argv: list[str], k: int) -> int:
@@ -157,8 +224,15 @@ def _rank_group(a, argv: list[str], k: int) -> int:
                                "--rank", str(first + j), *rest], stdout=subprocess.PIPE, text=True)
              for j in range(k)]
     outs = []
+    # every child is bounded by its own deadlines and watchdog; this is the backstop over them
+    bound = 6 * a.timeout + 4 * WATCHDOG_GRACE_S if a.timeout > 0 else None
     for pr in procs:
-        out, _ = pr.communicate()
+        try:
+            out, _ = pr.communicate(timeout=bound)
+        except subprocess.TimeoutExpired:
+            pr.kill()
+            out, _ = pr.communicate()
+            out = json.dumps({"ok": False, "error": f"rank process did not end within {bound:.0f}s", "timed_out": True})
         line = (out or "").strip().splitlines()
         try:
             outs.append(json.loads(line[-1]) if line else {"ok": False, "error": f"rank exited {pr.returncode}"})
@@ -166,7 +240,8 @@ def _rank_group(a, argv: list[str], k: int) -> int:
             outs.append({"ok": False, "error": line[-1][:200]})
     merged = dict(outs[0])
     merged.update(ok=all(o.get("ok") for o in outs), mode="rank_group", rank=first, first_rank=first, local_ranks=k,
-                  peak_busbw_gbps=min((o.get("peak_busbw_gbps", 0.0) for o in outs), default=0.0),
+                  peak_busbw_gbps=(min((o.get("peak_busbw_gbps") or 0.0 for o in outs), default=0.0)
+                                   if a.nranks > 1 else None),
                   init_seconds=max((o.get("init_seconds", 0.0) for o in outs), default=0.0))
     errs = [o["error"] for o in outs if o.get("error")]
     if errs:
@@ -188,7 +263,8 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--dtype", choices=["float32", "bfloat16"], default="float32")
-    ap.add_argument("--timeout", type=float, default=60.0)
+    ap.add_argument("--op-timeout", "--timeout", dest="timeout", type=float, default=20.0,
+                    help="bound on each wait: rendezvous, init, every collective (s)")
     ap.add_argument("--backend", choices=["gloo", "nccl"], default="gloo", help="nccl = RCCL on ROCm (GPU tensors)")
     a = ap.parse_args(argv)
     if a.rank is None:
@@ -201,7 +277,9 @@ def main(argv=None) -> int:
     t0 = time.monotonic()
     debug_file = _debug_file() if a.backend == "nccl" else None
     host = os.environ.get("NODE_IP", "127.0.0.1")
+    ph = Phases(a.rank, a.nranks, a.timeout)
     try:
+        ph.enter("uid")
         import torch.distributed as dist
         from datetime import timedelta
 
@@ -216,6 +294,7 @@ def main(argv=None) -> int:
             sh, sp = _fetch(a.kv_url, a.timeout).rsplit(":", 1)
             store = dist.TCPStore(sh, int(sp), world_size=a.nranks, is_master=False,
                                   timeout=timedelta(seconds=a.timeout))
+        ph.enter("init")
         device = "cpu"
         if a.backend == "nccl":
             import torch
@@ -225,19 +304,27 @@ def main(argv=None) -> int:
         dist.init_process_group(a.backend, store=store, rank=a.rank, world_size=a.nranks,
                                 timeout=timedelta(seconds=a.timeout))
         init_s = time.monotonic() - t0
-        res = sweep(a.rank, a.nranks, a.min_bytes, a.max_bytes, a.factor, a.iters, a.warmup, a.dtype, device)
+        res = sweep(a.rank, a.nranks, a.min_bytes, a.max_bytes, a.factor, a.iters, a.warmup, a.dtype, device, ph)
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001 - reported as the pod result
-        print(json.dumps({"ok": False, "rank": a.rank, "nranks": a.nranks, "error": f"{type(e).__name__}: {e}"}))
-        return 2
+        print(json.dumps({"ok": False, "rank": a.rank, "nranks": a.nranks, "phase": ph.phase,
+                          "timed_out": "timeout" in str(e).lower() or isinstance(e, TimeoutError),
+                          "error": f"{type(e).__name__}: {e}"}), flush=True)
+        os._exit(2)  # a failed process group's teardown can block on the dead peer
+    with ph.lock:
+        ph.deadline = 0.0
     out = {"ok": res["ok"], "backend": a.backend, "mode": "multi_process", "nranks": a.nranks, "rank": a.rank,
            "dtype": a.dtype, "init_seconds": round(init_s, 4), "peak_busbw_gbps": res["peak_busbw_gbps"],
-           "results": res["results"]}
+           "peak_algbw_gbps": res["peak_algbw_gbps"], "op_timeout_s": a.timeout,
+           "sweep": {"min_bytes": a.min_bytes, "max_bytes": a.max_bytes, "factor": a.factor, "iters": a.iters,
+                     "warmup": a.warmup, "dtypes": [a.dtype]}, "results": res["results"]}
+    if a.nranks == 1:
+        out["fabric"] = "1 GPU: no fabric"
     if a.backend == "nccl":  # same tuning report as tk8s-rccl
         for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS"):
             out[k.lower()] = os.environ.get(k) or "auto"
-        out["peak_links_equivalent"] = res["peak_busbw_gbps"] / 153.0 if a.nranks > 1 else 0.0
+        out["peak_links_equivalent"] = res["peak_busbw_gbps"] / 153.0 if a.nranks > 1 else None
     if debug_file and "%" not in debug_file:
         try:
             with open(debug_file, errors="replace") as f:

@@ -243,7 +243,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
     try:  # RCCL's gfx950 device code unpacked once per host (the fabric check's communicator start)
         rccl_unpacked = unpack(verbose=verbose)
-    except (OSError, subprocess.SubprocessError, ValueError) as e:  # the installed library stays usable
+    except Exception as e:  # noqa: BLE001 - an optional speed-up: the installed library stays usable
         rccl_unpacked = {"ok": False, "why": str(e)}
     out = {"libtk8s": lib, "libtk8s_rccl": rlib, "native_module": nat, "topo_module": topo, "tk8s-supervise": sup,
            "tk8s-gpujail": jail, "tk8s-container": tool_path("tk8s-container"),

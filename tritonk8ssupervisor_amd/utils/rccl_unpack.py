@@ -47,7 +47,16 @@ def installed_library() -> Path | None:
 
 
 def elf_section(path: Path, name: str) -> tuple[int, int] | None:
-    """(file offset, size) of section ``name`` of a 64-bit little-endian ELF file."""
+    """(file offset, size) of section ``name`` of a 64-bit little-endian ELF file; None for a file
+    that is not one, or is truncated or malformed (an optional speed-up must never
+    abort the native build)."""
+    try:
+        return _elf_section(path, name)
+    except (struct.error, IndexError, ValueError, UnicodeDecodeError):
+        return None
+
+
+def _elf_section(path: Path, name: str) -> tuple[int, int] | None:
     with open(path, "rb") as f:
         eh = f.read(64)
         if eh[:4] != b"\x7fELF" or eh[4] != 2 or eh[5] != 1:

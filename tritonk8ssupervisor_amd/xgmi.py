@@ -81,6 +81,7 @@ def link_report(result: dict, gpus: list[int] | None = None, fraction: float | N
     host = (lambda i: gpus[i] if gpus is not None and 0 <= i < len(gpus) else i)
     faults = _injected()
     links = []
+    default_rt = result.get("peers_runtime") or result.get("runtime") or "hip"
     for d in result.get("devices") or []:
         for p in d.get("peers") or []:
             src, dst = host(int(p.get("src_device", -1))), host(int(p.get("dst_device", d.get("device", -1))))
@@ -88,8 +89,11 @@ def link_report(result: dict, gpus: list[int] | None = None, fraction: float | N
             ok = bool(p.get("ok")) and gbps is not None
             if ok and (src, dst) in faults:
                 gbps = gbps * faults[(src, dst)]
+            rt = p.get("runtime") or default_rt
+            if rt == "hip" and default_rt == "hip-fallback":
+                rt = "hip-fallback"
             links.append({"src": src, "dst": dst, "gbps": round(float(gbps), 2) if gbps is not None else None,
-                          "ok": ok, **({"error": p["error"]} if p.get("error") else {})})
+                          "ok": ok, "runtime": rt, **({"error": p["error"]} if p.get("error") else {})})
     links.sort(key=lambda e: (e["src"], e["dst"]))
     good = sorted(e["gbps"] for e in links if e["ok"])
     median = 0.0
@@ -116,6 +120,7 @@ def node_view(report: dict, gpus: list[int]) -> dict:
     bad = [e for e in report.get("degraded", []) if e["src"] in mine or e["dst"] in mine]
     good = [e["gbps"] for e in links if e["ok"]]
     return {"gpus": sorted(mine), "pulls": len(links), "median_gbps": report.get("median_gbps"),
+            "runtimes": sorted({e.get("runtime") or "hip" for e in links}),
             "floor_gbps": report.get("floor_gbps"), "min_fraction": report.get("min_fraction"),
             "min_gbps": min(good) if good else None, "links": links, "degraded": bad, "healthy": not bad}
 
@@ -127,7 +132,10 @@ def annotations(view: dict) -> dict[str, str]:
     out = {"tk8s.amd.com/xgmi-links": ",".join(
         f"{e['src']}->{e['dst']}:{e['gbps']:.1f}" if e["ok"] else f"{e['src']}->{e['dst']}:failed" for e in view["links"]),
         "tk8s.amd.com/xgmi-median-gbps": f"{view.get('median_gbps') or 0:.1f}",
-        "tk8s.amd.com/xgmi-healthy": "true" if view.get("healthy") else "false"}
+        "tk8s.amd.com/xgmi-healthy": "true" if view.get("healthy") else "false",
+        # which burn-in runtime validated the links: hsa (the payload's own pulls), hip-fallback
+        # (its peer phase failed and the HIP probe re-ran them), hip (TK8S_PEERS_RUNTIME=hip)
+        "tk8s.amd.com/xgmi-runtime": ",".join(view.get("runtimes") or ["hip"])}
     if view.get("min_gbps") is not None:
         out["tk8s.amd.com/xgmi-min-gbps"] = f"{view['min_gbps']:.1f}"
     if view.get("degraded"):
