@@ -59,13 +59,28 @@ def _run(args, faults="", timeout=90, **env):
 _BEFORE: set = set()
 
 
+def _holders(pids):
+    out = {}
+    for p in sorted(pids):
+        try:
+            with open(f"/proc/{p}/comm") as f:
+                out[p] = f.read().strip()
+        except OSError:
+            out[p] = "?"
+    return out
+
+
 def _no_gpu_holder(pid):
     """Nothing the run started still holds the GPU: the KFD's process list is back to what it was
-    before it (KFD names host pids, so inside a container the child's own pid cannot be matched)."""
+    before it (KFD names host pids, so inside a container the child's own pid cannot be matched).
+    This process itself is not counted (its first HIP use may fall inside the window)."""
     deadline = time.monotonic() + 10
-    while (_kfd_pids() - _BEFORE) and time.monotonic() < deadline:
+    mine = {str(os.getpid())}
+    while (_kfd_pids() - _BEFORE - mine) and time.monotonic() < deadline:
         time.sleep(0.05)
-    return not (_kfd_pids() - _BEFORE)
+    left = _kfd_pids() - _BEFORE - mine
+    assert not left, {"left": _holders(left), "child": pid, "me": os.getpid(), "before": _holders(_BEFORE)}
+    return True
 
 
 def _healthy_rccl():

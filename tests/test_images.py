@@ -320,7 +320,7 @@ def test_mount_points_resolve_inside_the_image(ws, native_build):
         time.sleep(0.2)
     out = kc("logs", "deb").stdout
     assert o["status"]["phase"] == "Succeeded", (out, o["status"])
-    assert "tok=tk8s-sa." in out and "data=x" in out, out
+    assert "tok=tk8sb." in out and "data=x" in out, out  # the pod-bound token
     # the capability bounding set of a root pod is Docker's default set; host sysctl/sysfs stay read-only
     assert "sysctl=refused" in out and "sysfs=refused" in out, out
     if os.geteuid() == 0:

@@ -137,3 +137,109 @@ def test_cluster_status_events_metrics_and_projects_are_scoped(two_envs):
     assert _status(env_a.get, f"/v2-beta/projects/{b['id']}") == 403
     assert _status(sa_a.get, f"/v2-beta/projects/{a['id']}") == 403
     assert env_a.get(f"/v2-beta/projects/{a['id']}")["id"] == a["id"]
+
+
+def _pod(k, ns, name, job=None, node=None, sa="default"):
+    md = {"name": name}
+    if job:
+        md["ownerReferences"] = [{"apiVersion": "batch/v1", "kind": "Job", "name": job, "uid": f"uid-{job}",
+                                  "controller": True}]
+    spec = {"serviceAccountName": sa, "containers": [{"name": "c", "command": ["sleep", "60"]}]}
+    if node:
+        spec["nodeName"] = node
+    return k.post(k.k8s(f"/api/v1/namespaces/{ns}/pods"), {"apiVersion": "v1", "kind": "Pod", "metadata": md, "spec": spec})
+
+
+def _bound(k, ns, pod, sa="default", **spec):
+    body = {"spec": {"boundObjectRef": {"kind": "Pod", "name": pod["metadata"]["name"], "uid": pod["metadata"]["uid"]},
+                     **spec}}
+    return k.post(k.k8s(f"/api/v1/namespaces/{ns}/serviceaccounts/{sa}/token"), body)
+
+
+def test_a_pod_bound_token_reaches_only_its_own_jobs_keys(two_envs):
+    """the rendezvous is scoped to the Job. Two Jobs' pods -- same namespace, same
+    ServiceAccount -- each reach their own Job's keys: another Job's rank can neither read nor
+    overwrite ``rccl-allreduce-X/uid``; the token dies with its pod."""
+    admin, a, _b, ka, _kb = two_envs
+    pa = _pod(ka, "team-a", "rccl-x-0", job="rccl-allreduce-x")
+    pb = _pod(ka, "team-a", "other-0", job="other-job")
+    ta, tb = _bound(ka, "team-a", pa), _bound(ka, "team-a", pb)
+    assert ta["kind"] == "TokenRequest" and ta["status"]["token"].startswith("tk8sb.")
+    assert ta["spec"]["audiences"] and 3500 <= ta["spec"]["expirationSeconds"] <= 3600
+    ra, rb = _kv(admin.base, ta["status"]["token"]), _kv(admin.base, tb["status"]["token"])
+    ra.put("/v1/kv/rccl-allreduce-x/uid", "the-real-unique-id")
+    assert ra.get("/v1/kv/rccl-allreduce-x/uid", raw=True) == "the-real-unique-id"
+    # the other Job's pod: its own (empty) keyspace; its writes never reach the fabric Job's key
+    assert _status(rb.get, "/v1/kv/rccl-allreduce-x/uid", raw=True) == 404
+    rb.put("/v1/kv/rccl-allreduce-x/uid", "forged")
+    rb.delete("/v1/kv/rccl-allreduce-x/uid")
+    assert ra.get("/v1/kv/rccl-allreduce-x/uid", raw=True) == "the-real-unique-id"
+    # naming the other Job's keyspace is refused
+    assert _status(rb.get, "/v1/kv/rccl-allreduce-x/uid", query={"job": "rccl-allreduce-x"}, raw=True) == 403
+    # the legacy namespace-wide token of the same ServiceAccount does not see the Job's key either
+    legacy = _kv(admin.base, _sa_token(ka, "team-a", "default"))
+    assert _status(legacy.get, "/v1/kv/rccl-allreduce-x/uid", raw=True) == 404
+    # the environment's administrator reaches the Job's keyspace by name
+    assert _kv(admin.base, ka.token).get("/v1/kv/rccl-allreduce-x/uid", query={"namespace": "team-a", "job":
+                                                                               "rccl-allreduce-x"}, raw=True) == \
+        "the-real-unique-id"
+    # a pod no Job owns shares its namespace's keys (as a legacy token does)
+    free = _kv(admin.base, _bound(ka, "team-a", _pod(ka, "team-a", "solo"))["status"]["token"])
+    free.put("/v1/kv/shared/x", "1")
+    assert legacy.get("/v1/kv/shared/x", raw=True) == "1"
+    # deleting the pod revokes its token
+    ka.delete(ka.k8s("/api/v1/namespaces/team-a/pods/rccl-x-0"), query={"gracePeriodSeconds": "0"})
+    import time
+
+    deadline = time.monotonic() + 10
+    while _status(ra.get, "/v1/kv/rccl-allreduce-x/uid", raw=True) != 401 and time.monotonic() < deadline:
+        time.sleep(0.05)
+    assert _status(ra.get, "/v1/kv/rccl-allreduce-x/uid", raw=True) == 401
+
+
+def test_token_requests_are_bound_checked_and_node_restricted(two_envs):
+    admin, a, _b, ka, _kb = two_envs
+    nc1, r1 = _join(admin, a["id"], "kubenode1", ngpu=0)
+    _join(admin, a["id"], "kubenode2", ngpu=0)
+    mine = _pod(ka, "team-a", "on-1", node="kubenode1")
+    theirs = _pod(ka, "team-a", "on-2", node="kubenode2")
+    n1 = Client(admin.base, token=r1["nodeToken"], prefix=ka.prefix, timeout=10)
+    assert _bound(n1, "team-a", mine)["status"]["token"]
+    assert _status(_bound, n1, "team-a", theirs) == 403            # a pod bound to another node
+    _sa_token(ka, "team-a", "other-sa")
+    assert _status(_bound, n1, "team-a", mine, sa="other-sa") == 403  # not the pod's own ServiceAccount
+    assert _status(n1.post, n1.k8s("/api/v1/namespaces/team-a/serviceaccounts/default/token"), {"spec": {}}) == 403
+    stale = {**mine, "metadata": {**mine["metadata"], "uid": "not-the-uid"}}
+    assert _status(_bound, ka, "team-a", stale) == 409
+    # an audience this server does not serve: the token is not accepted here
+    odd = _bound(ka, "team-a", mine, audiences=["https://vault.example"])["status"]["token"]
+    assert _status(_kv(admin.base, odd).get, "/v1/kv/x", raw=True) == 401
+    # a forged signature is nobody
+    good = _bound(ka, "team-a", mine)["status"]["token"]
+    assert _status(_kv(admin.base, good[:-2] + ("AA" if not good.endswith("AA") else "BB")).get, "/v1/kv/x", raw=True) == 401
+
+
+def test_an_expired_bound_token_is_refused(monkeypatch):
+    """Expiry, pod uid and audience checks of authn._bound, on the class itself (no server)."""
+    import time
+
+    from tritonk8ssupervisor_amd.controlplane.authn import Authentication
+
+    pod = {"metadata": {"name": "p0", "namespace": "ns", "uid": "u1",
+                        "ownerReferences": [{"kind": "Job", "name": "j1"}]}}
+
+    class Store:
+        def get(self, kind, key):
+            return pod if kind == "pods" and key.endswith("p0") else None
+
+    auth = Authentication()
+    auth.store, auth.state_dir = Store(), None
+    tok, exp = auth.issue_bound_token("1a1", "ns", "default", pod, ["tk8s"], 60)  # clamped to 10 min
+    assert 590 <= exp - time.time() <= 600
+    assert auth._bound(tok) == ("sa", "1a1", "ns", "default", {"pod": "p0", "uid": "u1", "job": "j1"})
+    real = time.time
+    monkeypatch.setattr(time, "time", lambda: real() + 601)
+    assert auth._bound(tok) is None  # expired
+    monkeypatch.setattr(time, "time", real)
+    pod["metadata"]["uid"] = "u2"  # the pod was deleted and re-created under the same name
+    assert auth._bound(tok) is None

@@ -210,6 +210,7 @@ class Agent:
         self.dp_servicer = None
         self.kubelet = None
         self._config_wait: dict[str, dict] = {}   # pods held in CreateContainerConfigError
+        self._sa_tokens: dict[str, dict] = {}     # pod -> its bound ServiceAccount token (renewed by the heartbeat loop)
         # gpu-peers pods waiting for their Job's other pods on this host: their GPUs stay allocated
         # (published in GPU_DEVICES so the peers can find them) until the pod starts or goes away
         self._reserved: dict[str, tuple[list[str], dict, float]] = {}
@@ -350,6 +351,7 @@ class Agent:
                 if time.monotonic() >= next_volumes:  # ConfigMap/Secret/downwardAPI changes reach running pods
                     next_volumes = time.monotonic() + volume_period
                     self._sync_volumes()
+                    self._renew_tokens(api)
                 try:
                     api.put(api.k8s(f"/api/v1/nodes/{self.name}/status"), body)
                 except ApiError as e:
@@ -914,23 +916,64 @@ class Agent:
 
     def _service_account_dir(self, pod: dict, pp_dir: Path) -> Path | None:
         """The pod's ServiceAccount token, namespace and CA files (kubelet's projected token
-        volume), unless ``automountServiceAccountToken: false``."""
+        volume), unless ``automountServiceAccountToken: false``. The token is a BOUND one
+        (TokenRequest): made for this pod (its uid), for the API server's audience,
+        expiring after ``TK8S_SA_TOKEN_TTL_S`` (default 1 h) and renewed by the heartbeat loop at
+        80 % of its life; deleting the pod revokes it -- not the namespace-wide ``<sa>-token``
+        Secret every pod of the ServiceAccount used to share."""
         spec, ns = pod["spec"], pod["metadata"]["namespace"]
         if spec.get("automountServiceAccountToken") is False:
             return None
         sa = spec.get("serviceAccountName") or spec.get("serviceAccount") or "default"
-        s = self._fetch_object("secrets", ns, f"{sa}-token")
-        if s is None:
+        tok = self._request_token(pod, sa)
+        if tok is None:
             return None
-        import base64
-
         d = pp_dir / "serviceaccount"
         d.mkdir(parents=True, exist_ok=True)
-        for name, data in (("token", base64.b64decode((s.get("data") or {}).get("token", ""))), ("namespace", ns.encode()),
-                           ("ca.crt", b"")):
+        for name, data in (("token", tok[0].encode()), ("namespace", ns.encode()), ("ca.crt", b"")):
             (d / name).write_bytes(data)
             os.chmod(d / name, 0o600 if name == "token" else 0o644)
+        md = pod["metadata"]
+        self._sa_tokens[f"{ns}/{md['name']}"] = {"dir": d, "sa": sa, "pod": pod, "exp": tok[1], "iat": time.time()}
         return d
+
+    def _request_token(self, pod: dict, sa: str, api=None) -> tuple[str, float] | None:
+        """A bound token for ``pod`` as ServiceAccount ``sa`` (POST .../serviceaccounts/<sa>/token)."""
+        md = pod["metadata"]
+        ttl = float(os.environ.get("TK8S_SA_TOKEN_TTL_S", "3600"))
+        body = {"apiVersion": "authentication.k8s.io/v1", "kind": "TokenRequest",
+                "spec": {"expirationSeconds": int(ttl),
+                         "boundObjectRef": {"kind": "Pod", "apiVersion": "v1", "name": md["name"], "uid": md.get("uid", "")}}}
+        api = api or self.api
+        try:
+            r = api.post(api.k8s(f"/api/v1/namespaces/{md['namespace']}/serviceaccounts/{sa}/token"), body)
+        except (ApiError, OSError) as e:
+            print(f"{self.name}: {md['namespace']}/{md['name']}: no ServiceAccount token ({e})", flush=True)
+            return None
+        st = (r or {}).get("status") or {}
+        if not st.get("token"):
+            return None
+        left = float(((r.get("spec") or {}).get("expirationSeconds")) or ttl)
+        return st["token"], time.time() + left
+
+    def _renew_tokens(self, api) -> None:
+        """Renew every running pod's bound token at 80 % of its life (kubelet's rule); drop the
+        entries of pods that are gone."""
+        running = self.runtime.running()
+        now = time.time()
+        for key, t in list(self._sa_tokens.items()):
+            if key not in running:
+                self._sa_tokens.pop(key, None)
+                continue
+            if now < t["iat"] + 0.8 * (t["exp"] - t["iat"]):
+                continue
+            tok = self._request_token(t["pod"], t["sa"], api)
+            if tok is None:
+                continue
+            from ..utils.fsutil import atomic_write
+
+            atomic_write(t["dir"] / "token", tok[0], mode=0o600)
+            t.update(exp=tok[1], iat=now)
 
     def _fetch_object(self, kind: str, ns: str, name: str) -> dict | None:
         """A namespaced object the pod's volumes need (None: it does not exist)."""

@@ -15,7 +15,13 @@ so every request names a bearer token except a short public list (``PUBLIC``):
   Node authorizer + NodeRestriction admission give them (``node_allows``): reads of what nodes
   read, Secrets and ConfigMaps only when a pod bound to the node uses them, writes only to its
   own Node, Lease, exec results and the pods bound to it, Events;
-* a **ServiceAccount token** -- RBAC (rbac.py);
+* a **ServiceAccount token** -- RBAC (rbac.py). What pods get is a *bound*
+  token, TokenRequest-style (``POST .../serviceaccounts/<sa>/token``, ``issue_bound_token``): an
+  HMAC-signed claim set naming the pod it was made for, an audience and an expiry, valid only
+  while that pod (same uid) exists -- deleting the pod revokes it. The node agent requests one per
+  pod (NodeRestriction: only for pods bound to it, as their own ServiceAccount) and renews it
+  before it expires. The legacy ``<sa>-token`` Secret still authenticates, for clients that
+  mount it explicitly;
 * none -- anonymous: health, version, discovery, the readiness dashboard, node registration
   (its token is in the URL) and nothing else (401).
 
@@ -34,6 +40,11 @@ from ..utils.ids import token_hex
 from .httpserver import HttpError, Request
 
 ADMIN_TOKEN_FILE = "admin-token"
+SIGNING_KEY_FILE = "sa-signing-key"
+BOUND_PREFIX = "tk8sb."
+# audiences this API server accepts in a bound token (TokenRequest's default is the first)
+API_AUDIENCES = ("https://kubernetes.default.svc.cluster.local", "https://kubernetes.default.svc", "tk8s")
+BOUND_TTL_MIN_S, BOUND_TTL_MAX_S, BOUND_TTL_DEFAULT_S = 600, 7 * 86400, 3600
 # kinds a node reads in full, as the kubelet's system:node role does
 _NODE_READABLE = frozenset({"nodes", "pods", "services", "endpoints", "endpointslices", "runtimeclasses", "csinodes"})
 _NS_RE = re.compile(r"^[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?$")
@@ -81,6 +92,39 @@ def load_admin_token(state_dir: Path | None) -> str:
     tok = token_hex(24)
     atomic_write(p, tok + "\n", mode=0o600)
     return tok
+
+
+def load_signing_key(state_dir: Path | None) -> bytes:
+    """The key bound ServiceAccount tokens are signed with: ``<state_dir>/sa-signing-key`` (0600,
+    made on first start, so tokens survive a control-plane restart), else one for this process."""
+    if state_dir is None:
+        return token_hex(32).encode()
+    p = Path(state_dir) / SIGNING_KEY_FILE
+    try:
+        k = p.read_text().strip()
+        if k:
+            return k.encode()
+    except OSError:
+        pass
+    k = token_hex(32)
+    atomic_write(p, k + "\n", mode=0o600)
+    return k.encode()
+
+
+def _b64(b: bytes) -> str:
+    return base64.urlsafe_b64encode(b).rstrip(b"=").decode()
+
+
+def _unb64(s: str) -> bytes:
+    return base64.urlsafe_b64decode(s + "=" * (-len(s) % 4))
+
+
+def pod_job(pod: dict) -> str | None:
+    """The Job that owns a pod (its controller ownerReference), if any."""
+    for r in (pod.get("metadata") or {}).get("ownerReferences") or []:
+        if r.get("kind") == "Job":
+            return r.get("name")
+    return None
 
 
 def _pod_refs(pod: dict, kind: str) -> set[str]:
@@ -134,12 +178,76 @@ class Authentication:
             self._tok_idx, self._tok_ver = idx, ver
         return self._tok_idx
 
-    def _identity(self, p: str | None, tok: str | None) -> str | None:
-        """``admin`` (the server admin token, or project ``p``'s API token), ``node:<name>``,
-        ``sa:<ns>:<name>`` -- a node or ServiceAccount of project ``p`` -- or None."""
+    # ---- bound ServiceAccount tokens (TokenRequest) -------------------------------------------
+    def _signing_key(self) -> bytes:
+        k = getattr(self, "_sa_key", None)
+        if k is None:
+            k = self._sa_key = load_signing_key(getattr(self, "state_dir", None))
+        return k
+
+    def issue_bound_token(self, pid: str | None, ns: str, sa: str, pod: dict | None, audiences: list[str],
+                          ttl: float) -> tuple[str, float]:
+        """A token for ServiceAccount ``ns/sa`` of project ``pid``, bound to ``pod`` (its name and
+        uid; None: unbound, it only expires), for ``audiences``, valid ``ttl`` s (clamped to
+        10 min .. 7 days). Returns (token, expiry unix time)."""
+        import hashlib
+        import hmac
+        import json
+        import time
+
+        ttl = min(max(float(ttl), BOUND_TTL_MIN_S), BOUND_TTL_MAX_S)
+        exp = time.time() + ttl
+        claims = {"p": pid, "ns": ns, "sa": sa, "aud": list(audiences), "exp": round(exp, 3), "jti": token_hex(8)}
+        if pod is not None:
+            claims.update(pod=pod["metadata"]["name"], uid=pod["metadata"].get("uid", ""))
+        body = _b64(json.dumps(claims, separators=(",", ":"), sort_keys=True).encode())
+        sig = _b64(hmac.new(self._signing_key(), body.encode(), hashlib.sha256).digest())
+        return f"{BOUND_PREFIX}{body}.{sig}", exp
+
+    def _bound(self, tok: str) -> tuple | None:
+        """("sa", pid, ns, sa, {"pod", "uid", "job"}) for a valid bound token: signature, expiry,
+        audience, and -- when bound to a pod -- that pod still exists with the same uid."""
+        import hashlib
+        import hmac
+        import json
+        import time
+
+        from .objects import _key
+
+        try:
+            body, sig = tok[len(BOUND_PREFIX):].split(".", 1)
+            want = _b64(hmac.new(self._signing_key(), body.encode(), hashlib.sha256).digest())
+            if not hmac.compare_digest(want, sig):
+                return None
+            c = json.loads(_unb64(body))
+        except (ValueError, TypeError, UnicodeDecodeError):
+            return None
+        if not isinstance(c, dict) or float(c.get("exp") or 0) <= time.time():
+            return None
+        if not set(c.get("aud") or []) & set(API_AUDIENCES):
+            return None
+        bound = {"pod": None, "uid": None, "job": None}
+        if c.get("pod"):
+            pod = self.store.get("pods", _key(c.get("p"), c.get("ns"), c["pod"]))
+            if pod is None or pod["metadata"].get("uid", "") != c.get("uid", "") or \
+                    pod["metadata"].get("deletionTimestamp"):
+                return None  # the pod it was made for is gone (or going): revoked
+            bound = {"pod": c["pod"], "uid": c.get("uid"), "job": pod_job(pod)}
+        return ("sa", c.get("p"), c.get("ns"), c.get("sa"), bound)
+
+    def _lookup(self, tok: str | None) -> tuple | None:
+        """Any token this server knows: admin, project, node, legacy ServiceAccount, or bound."""
         if not tok:
             return None
         hit = self._tokens().get(tok)
+        if hit is None and tok.startswith(BOUND_PREFIX):
+            hit = self._bound(tok)
+        return hit
+
+    def _identity(self, p: str | None, tok: str | None) -> str | None:
+        """``admin`` (the server admin token, or project ``p``'s API token), ``node:<name>``,
+        ``sa:<ns>:<name>`` -- a node or ServiceAccount of project ``p`` -- or None."""
+        hit = self._lookup(tok)
         if hit is None:
             return None
         if hit[0] == "admin":
@@ -155,7 +263,7 @@ class Authentication:
         """The gate in front of every route: a public path, or a token this server knows."""
         if is_public(req.method, req.path):
             return
-        if req.bearer and req.bearer in self._tokens():
+        if self._lookup(req.bearer) is not None:
             return
         raise HttpError(401, "Unauthorized: this request needs a bearer token "
                              "(the kubeconfig's, a ServiceAccount's, a node's or the server admin token)")
@@ -166,7 +274,7 @@ class Authentication:
     # rancherhost/tasks/main.yml:11-17). The control plane's own side channels keep that scope:
     # a token acts inside its environment -- and a ServiceAccount's inside its namespace -- only.
     def _caller(self, req: Request) -> tuple:
-        hit = self._tokens().get(req.bearer or "")
+        hit = self._lookup(req.bearer)
         if hit is None:
             raise HttpError(401, "missing or invalid bearer token")
         return hit
@@ -190,25 +298,38 @@ class Authentication:
         return hit
 
     def kv_key(self, req: Request, key: str) -> str:
-        """The store key of KV ``key`` for this caller: ``<project>/<namespace>/<key>``.
+        """The store key of KV ``key`` for this caller: ``<project>/<namespace>/<key>``, or
+        ``<project>/<namespace>/job:<job>/<key>`` in a Job's own keyspace.
 
-        * a ServiceAccount token: its own environment and namespace (``?namespace=`` may only
+        * a pod's bound token: a pod owned by a Job reaches its Job's keyspace
+          only -- the RCCL unique id or torch address of ``rccl-allreduce-X`` is out of reach of
+          every other pod, same namespace and ServiceAccount included; a pod no Job owns gets its
+          namespace's shared keys, as a legacy ServiceAccount token does;
+        * a legacy ServiceAccount token: its own environment and namespace (``?namespace=`` may only
           repeat it), so a pod reaches its own namespace's keys and nothing else;
         * a node token: none -- the keys are the workloads' rendezvous (RCCL unique ids, torch
           addresses), which no kubelet reads or writes, and the pods of one namespace run on many
           nodes, so a node could not be held to its own pods' keys by namespace;
-        * an environment's API token: its environment, any namespace; the server admin token:
-          ``?project=`` (default: the oldest environment), any namespace."""
+        * an environment's API token: its environment, any namespace (``?job=`` a Job's
+          keyspace); the server admin token: ``?project=`` (default: the oldest environment), any
+          namespace."""
         if not key or len(key) > 512 or "\0" in key:
             raise HttpError(422, "a KV key is 1-512 characters")
         hit = self._caller(req)
         ns = req.q("namespace") or None
         if ns is not None and not _NS_RE.match(ns):
             raise HttpError(422, f"invalid namespace {ns!r}")
+        job = req.q("job") or None
+        if job is not None and not _NS_RE.match(job):
+            raise HttpError(422, f"invalid job name {job!r}")
         if hit[0] == "sa":
             if ns not in (None, hit[2]):
                 raise HttpError(403, f"a ServiceAccount of namespace {hit[2]} cannot reach the keys of {ns}")
-            return f"{hit[1]}/{hit[2]}/{key}"
+            own = (hit[4] if len(hit) > 4 else {}).get("job")
+            if job not in (None, own):
+                raise HttpError(403, f"this pod's token reaches the keys of {'job ' + own if own else 'its namespace'}, "
+                                     f"not of job {job}")
+            return f"{hit[1]}/{hit[2]}/job:{own}/{key}" if own else f"{hit[1]}/{hit[2]}/{key}"
         ns = ns or "default"
         if hit[0] == "node":
             raise HttpError(403, f"node {hit[2]}: the KV store holds the workloads' rendezvous keys, "
@@ -219,7 +340,7 @@ class Authentication:
             if e.status != 404 or hit[1] is not None:
                 raise
             pid = "-"  # the server admin before any environment exists
-        return f"{pid}/{ns}/{key}"
+        return f"{pid}/{ns}/job:{job}/{key}" if job else f"{pid}/{ns}/{key}"
 
     def event_filter(self, req: Request):
         """What of the store's change feed (``/v1/events``) the caller may see: everything for the
@@ -237,7 +358,7 @@ class Authentication:
 
     def _require_admin(self, req: Request, pid: str | None) -> None:
         """The server admin token, or the API token of project ``pid``."""
-        hit = self._tokens().get(req.bearer or "")
+        hit = self._lookup(req.bearer)
         if hit is None or hit[0] != "admin" or (hit[1] is not None and hit[1] != pid):
             raise HttpError(403 if hit else 401, "this needs the server admin token or the environment's API token")
 
@@ -267,6 +388,10 @@ class Authentication:
             return False
         if res == "leases":
             return read or info.name == node
+        if res == "serviceaccounts" and sub == "token":
+            # TokenRequest: the handler holds a node to pods bound to it, as their own
+            # ServiceAccount (NodeRestriction; k8s_api.h_token_request)
+            return info.verb == "create"
         if res == "events":
             return info.verb in ("create", "patch", "update") or read
         # what the kubelet's system:node role reads, and no more: no workload

@@ -92,6 +92,47 @@ class KubernetesAPI:
                               "metadata": {}, "spec": body.get("spec", {}),
                               "status": {"allowed": ok, **({"reason": why} if ok else {"reason": why, "denied": False})}})
 
+    async def h_token_request(self, req: Request, ns: str, name: str, pid: str | None = None):
+        """``POST .../serviceaccounts/<name>/token`` (authentication.k8s.io/v1 TokenRequest): a
+        bound token for the ServiceAccount (authn.issue_bound_token). ``boundObjectRef`` may name a
+        Pod (its uid must match): the token then dies with that pod. A node may ask only for a pod
+        bound to it, as the pod's own ServiceAccount, and only pod-bound (NodeRestriction)."""
+        import time as _t
+
+        from .authn import API_AUDIENCES, BOUND_TTL_DEFAULT_S
+
+        p = self._pid(pid, req)
+        if self.store.get("serviceaccounts", _key(p, ns, name)) is None:
+            raise HttpError(404, f'serviceaccounts "{name}" not found')
+        body = req.json() or {}
+        spec = body.get("spec") or {}
+        ref = spec.get("boundObjectRef") or None
+        pod = None
+        if ref is not None:
+            if ref.get("kind") != "Pod":
+                raise HttpError(422, "boundObjectRef: only kind Pod is supported")
+            pod = self.store.get("pods", _key(p, ns, ref.get("name") or ""))
+            if pod is None:
+                raise HttpError(404, f'pods "{ref.get("name")}" not found')
+            if ref.get("uid") and ref["uid"] != pod["metadata"].get("uid"):
+                raise HttpError(409, f'pod "{ref.get("name")}": uid {ref["uid"]} is not the current one')
+        ident = getattr(req, "identity", None) or ""
+        if ident.startswith("node:"):
+            sa = None if pod is None else (pod["spec"].get("serviceAccountName") or pod["spec"].get("serviceAccount")
+                                           or "default")
+            if pod is None or pod["spec"].get("nodeName") != ident[5:] or sa != name:
+                raise HttpError(403, f'serviceaccounts/token is forbidden: User "system:node:{ident[5:]}" may only '
+                                     "request tokens bound to pods on its node, as their own ServiceAccount")
+        auds = [str(a) for a in spec.get("audiences") or []] or [API_AUDIENCES[0]]
+        ttl = float(spec.get("expirationSeconds") or BOUND_TTL_DEFAULT_S)
+        tok, exp = self.issue_bound_token(p, ns, name, pod, auds, ttl)
+        stamp = _t.strftime("%Y-%m-%dT%H:%M:%SZ", _t.gmtime(exp))
+        return Response(201, {"apiVersion": "authentication.k8s.io/v1", "kind": "TokenRequest",
+                              "metadata": {"name": name, "namespace": ns},
+                              "spec": {"audiences": auds, "expirationSeconds": int(round(exp - _t.time())),
+                                       **({"boundObjectRef": ref} if ref else {})},
+                              "status": {"token": tok, "expirationTimestamp": stamp}})
+
     def _guarded(self, h):
         async def g(req: Request, **kw):
             self._authorize(req, kw.get("pid"))

@@ -279,6 +279,7 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/portforward", self.h_pod_portforward_ws)
             add("GET", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/attach", self.h_pod_attach_ws)
             add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/pods/(?P<name>[^/]+)/eviction", self.h_pod_eviction)
+            add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/serviceaccounts/(?P<name>[^/]+)/token", self.h_token_request)
             add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs", self.h_node_execs)
             add("PUT", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)", self.h_exec_result)
             # every other object path, built-in kinds (KIND_GROUPS, CLUSTER_KIND_GROUPS) and custom
