@@ -8,11 +8,13 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
+#include <thread>
 
 #include "tk8s/common.h"
 
@@ -321,27 +323,39 @@ void release(std::vector<Rank>& ranks) {
 
 // After a failure: let any stalled queue go, abort every local communicator (its kernels give up
 // on the peers) and keep the memory -- freeing it would synchronise with whatever still runs;
-// the process exits right after.
-void abort_all(std::vector<Rank>& ranks) {
+// the process exits right after. The aborts run on a helper thread given 2 s: aborting an init
+// that still waits for an absent peer can block inside RCCL's bootstrap, and a failure report
+// must never wait on that (measured on the MI355X: the dead-peer init case). Returns whether
+// every abort returned in time.
+bool abort_all(std::vector<Rank>& ranks) {
   gpu_stall_release();
+  std::vector<ncclComm_t> comms;
   for (auto& r : ranks) {
-    if (r.comm) (void)ncclCommAbort(r.comm);
+    if (r.comm) comms.push_back(r.comm);
     r.comm = nullptr;
     (void)r.send.release();
     (void)r.recv.release();
     (void)r.scratch.release();
     (void)r.timer.release();
   }
+  if (comms.empty()) return true;
+  auto done = std::make_shared<std::atomic<bool>>(false);
+  std::thread([comms, done] {
+    for (ncclComm_t c : comms) (void)ncclCommAbort(c);
+    *done = true;
+  }).detach();
+  return poll_until([&] { return done->load(); }, 2.0).empty();
 }
 
 std::string error_json(const std::string& phase, const std::string& what, bool timed_out, bool aborted,
-                       int nranks, int first, int local) {
+                       int nranks, int first, int local, bool abort_returned = true) {
   return Json()
       .kv("ok", false)
       .kv("phase", phase)
       .kv("error", what)
       .kv("timed_out", timed_out)
       .kv("aborted", aborted)
+      .kv("abort_returned", abort_returned)
       .kv("nranks", nranks)
       .kv("first_rank", first)
       .kv("local_ranks", local)
@@ -369,30 +383,57 @@ std::string run_group(int first_rank, int nranks, const std::vector<int>& device
     enter(cfg, "init");
     const auto t0 = std::chrono::steady_clock::now();
     // Several ranks of one communicator in one thread: the inits must be one group, or the first
-    // would wait forever for its local peers. Non-blocking: the group returns at once and
-    // settle() polls the inits, so an absent peer ends in an abort, not a hang.
-    ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
-    conf.blocking = cfg.blocking ? 1 : 0;
-    TK8S_NCCL_CHECK(ncclGroupStart());
-    for (auto& r : ranks) {
-      TK8S_HIP_CHECK(hipSetDevice(r.device));
-      TK8S_NCCL_CHECK(ncclCommInitRankConfig(&r.comm, nranks, id, r.rank, &conf));
-    }
-    TK8S_NCCL_CHECK(ncclGroupEnd());
-    settle(ranks, cfg);
+    // would wait forever for its local peers. They run on a helper thread, waited for under the
+    // deadline: even with the non-blocking config RCCL's bootstrap blocks the calling thread
+    // until every rank has connected (measured on the MI355X: rank 0 of a 2-rank communicator
+    // whose peer never came sat in ncclGroupEnd), so the init is bounded from outside; a thread
+    // left behind that way holds only its own copy of the inputs, and the process exits next.
+    struct Init {
+      std::atomic<bool> done{false};
+      std::string err;
+      std::vector<ncclComm_t> comms;
+    };
+    auto st = std::make_shared<Init>();
+    st->comms.assign(ranks.size(), nullptr);
+    std::vector<std::pair<int, int>> who;  // (device, rank)
+    for (const auto& r : ranks) who.emplace_back(r.device, r.rank);
+    const bool blocking = cfg.blocking;
+    std::thread([st, who, nranks, id, blocking] {
+      ncclConfig_t conf = NCCL_CONFIG_INITIALIZER;
+      conf.blocking = blocking ? 1 : 0;
+      ncclResult_t r = ncclGroupStart();
+      for (size_t i = 0; i < who.size() && (r == ncclSuccess || r == ncclInProgress); ++i) {
+        if (hipSetDevice(who[i].first) != hipSuccess) {
+          st->err = "hipSetDevice failed";
+          break;
+        }
+        r = ncclCommInitRankConfig(&st->comms[i], nranks, id, who[i].second, &conf);
+      }
+      const ncclResult_t g = ncclGroupEnd();
+      if (st->err.empty() && r != ncclSuccess && r != ncclInProgress)
+        st->err = std::string("ncclCommInitRankConfig failed: ") + ncclGetErrorString(r);
+      else if (st->err.empty() && g != ncclSuccess && g != ncclInProgress)
+        st->err = std::string("ncclGroupEnd failed: ") + ncclGetErrorString(g);
+      st->done = true;
+    }).detach();
+    const std::string w = poll_until([&] { return st->done.load(); }, cfg.op_timeout_s > 0 ? cfg.op_timeout_s : 1e9);
+    if (!w.empty()) throw PhaseError("init", "communicator init " + w + " (a rank never joined)", true);
+    if (!st->err.empty()) throw PhaseError("init", st->err, false);
+    for (size_t i = 0; i < ranks.size(); ++i) ranks[i].comm = st->comms[i];
+    settle(ranks, cfg);  // non-blocking: the inits may still be finishing
     const double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     std::string out = run_sweep(ranks, nranks, cfg, mode, init_ms, unix_ms());
     if (cfg.teardown) release(ranks);
     return out;
   } catch (const PhaseError& ex) {
-    abort_all(ranks);
-    return error_json(ex.phase, ex.what(), ex.timed_out, true, nranks, first_rank, local);
+    const bool back = abort_all(ranks);
+    return error_json(ex.phase, ex.what(), ex.timed_out, true, nranks, first_rank, local, back);
   } catch (const GpuTimeout& ex) {
-    abort_all(ranks);
-    return error_json(t_phase, ex.what(), true, true, nranks, first_rank, local);
+    const bool back = abort_all(ranks);
+    return error_json(t_phase, ex.what(), true, true, nranks, first_rank, local, back);
   } catch (const std::exception& ex) {
-    abort_all(ranks);
-    return error_json(t_phase, ex.what(), false, true, nranks, first_rank, local);
+    const bool back = abort_all(ranks);
+    return error_json(t_phase, ex.what(), false, true, nranks, first_rank, local, back);
   }
 }
 

@@ -595,11 +595,15 @@ class Device {
              a.ptr(dst).u64(n16).u32(static_cast<uint32_t>(seed)).u32(static_cast<uint32_t>(seed >> 32));
            });
   }
-  // Fault injection: one wave that holds the queue until stall_release() or max_s of GPU wall
-  // clock (gfx9: 100 MHz) -- kernels.h gpu_stall, dispatched on ROCr.
+  // Fault injection: one wave that holds the queue until stall_release() or max_s of the GPU's
+  // steady clock -- kernels.h gpu_stall, dispatched on ROCr.
   size_t stall(const uint32_t* flag, double max_s) {
     if (!ks_.stall.found) throw std::runtime_error("stall kernel missing from the code objects");
-    const auto ticks = static_cast<uint64_t>(max_s * 100e6);
+    uint64_t hz = 0;  // the steady counter the kernel reads (wall_clock64), 1-400 MHz
+    if (hsa_agent_get_info(g_.agent, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_TIMESTAMP_FREQUENCY), &hz) !=
+            HSA_STATUS_SUCCESS || hz == 0)
+      hz = 100000000;
+    const auto ticks = static_cast<uint64_t>(max_s * static_cast<double>(hz));
     return launch(ks_.stall, 1, 64, [&](KernArgs& a) { a.ptr(flag).u64(ticks); });
   }
   size_t copy(void* dst, const void* src, size_t bytes, bool to_host = false, bool from_remote = false) {

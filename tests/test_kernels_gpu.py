@@ -917,9 +917,10 @@ def test_setup_on_the_plain_path_on_a_real_gpu(tmp_path):
 
 
 def test_multi_gpu_burnin_command_runs_on_one_gpu(tmp_path):
-    """The host burn-in command a >= 2-GPU bring-up runs (HIP probe, --peers with the light pull
-    options, earlyburn.host_burnin_command) parses and passes on the one GPU here, and its JSON is
-    what the burn-in split and the xGMI judge read."""
+    """The host burn-in command a >= 2-GPU bring-up runs (the HSA payload by default, VERDICT r5
+    #5, --peers with the Ready path's 16 MiB pulls, earlyburn.host_burnin_command) parses and
+    passes on the one GPU here, and its JSON is what the burn-in split and the xGMI judge read;
+    its HIP fallback command too."""
     import os
     import subprocess
 
@@ -929,14 +930,17 @@ def test_multi_gpu_burnin_command_runs_on_one_gpu(tmp_path):
 
     env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
     cmd = earlyburn.host_burnin_command(earlyburn.default_validation_command(peers=False), [0, 1])
-    assert os.path.basename(cmd[0]) == "tk8s-probe" and "--no-peer-dma" in cmd, cmd
-    r = subprocess.run(cmd + ["--out", str(tmp_path / "r.json")], capture_output=True, text=True, timeout=120,
-                       env={**env, "ROCR_VISIBLE_DEVICES": "0"})
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    res = json.loads((tmp_path / "r.json").read_text())
-    assert res["ok"] and res["device_count"] == 1 and res["md5"]["digest"] == res["md5_expected"], res
-    rep = xgmi.link_report(res, [0])
-    assert rep["pulls"] == 0 and not rep["degraded"]
+    assert os.path.basename(cmd[0]) == "tk8s-hsaprobe" and cmd[cmd.index("--peer-bytes") + 1] == str(16 << 20), cmd
+    for c in (cmd, earlyburn.hip_peer_command(cmd)):
+        r = subprocess.run(c + ["--out", str(tmp_path / "r.json")], capture_output=True, text=True, timeout=120,
+                           env={**env, "ROCR_VISIBLE_DEVICES": "0"})
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        res = json.loads((tmp_path / "r.json").read_text())
+        assert res["ok"] and res["device_count"] == 1, res
+        if c is cmd:
+            assert res["md5"]["digest"] == res["md5_expected"], res
+        rep = xgmi.link_report(res, [0])
+        assert rep["pulls"] == 0 and not rep["degraded"]
 
 
 def test_gpu_busy_metric_and_hpa_on_a_real_gpu(tmp_path):
@@ -1163,7 +1167,7 @@ def test_resource_limits_are_enforced_unprivileged_on_the_gpu_box(tmp_path):
         if not enf.startswith("watchdog"):
             pytest.skip(f"this box delegates cgroups ({enf[:80]}): the kernel enforces, not the duty cycle")
         assert "duty cycle" in enf and "NOT enforced" not in enf, enf
-        busy = ("import os, time\nt = time.time()\nwhile time.time() - t < 3:\n    pass\n"
+        busy = ("import os, time\nt = time.time()\nwhile time.time() - t < 5:\n    pass\n"
                 "u = os.times()\nprint('cpu', round(u.user + u.system, 3), flush=True)\n")
         kc("apply", "-f", "-", stdin=json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "spin"},
                                                   "spec": {"restartPolicy": "Never", "containers": [{
@@ -1172,7 +1176,7 @@ def test_resource_limits_are_enforced_unprivileged_on_the_gpu_box(tmp_path):
         until_done("spin")
         out = kc("logs", "spin").stdout.split()
         used = float(out[out.index("cpu") + 1])
-        assert used <= 0.35 * 3.0 + 0.2, out
+        assert used <= 0.35 * 5.0, out  # <= 0.35 CPU over 5 s (interpreter start included)
         # 8 MiB a tenth of a second, every page touched: the resident-set sampler (0.5 s) sees it
         # far below the RLIMIT_DATA backstop (2 x 64Mi + 256Mi), which would end it differently
         grow = ("import time\nb = []\nwhile True:\n    b.append(bytearray(8 << 20))\n"

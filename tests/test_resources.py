@@ -505,3 +505,98 @@ def test_a_restarted_agent_ends_what_a_killed_one_left_behind(tmp_path):
             if p.poll() is None:
                 p.kill()
                 p.wait()
+
+
+FORKER = ("import os, time\nt = time.time()\nwhile time.time() - t < {secs}:\n"
+          "    pid = os.fork()\n    if pid == 0:\n        s = time.time()\n        while time.time() - s < 0.03:\n"
+          "            pass\n        os._exit(0)\n    os.waitpid(pid, 0)\n")
+
+
+def _cpu_with_children(pid: int) -> float:
+    with open(f"/proc/{pid}/stat") as f:
+        rest = f.read().rsplit(")", 1)[1].split()
+    return sum(int(x) for x in rest[11:15]) / os.sysconf("SC_CLK_TCK")
+
+
+def test_short_lived_children_cannot_escape_the_cpu_limit(monkeypatch):
+    """a 250m pod that burns its CPU in a loop of short-lived children (30 ms each,
+    gone before the next scan) is still held to its limit -- their CPU reaches the bill through the
+    parent that reaps them (cutime/cstime)."""
+    import threading
+
+    monkeypatch.setenv("TK8S_POD_RESOURCES", "watchdog")
+    e = Enforcer("n", Limits(), scope="forks")
+    p = subprocess.Popen([sys.executable, "-c", FORKER.format(secs=30)], start_new_session=True)
+    stop = threading.Event()
+    try:
+        e.pod("default/forks", Limits(cpu=0.25))
+        th = threading.Thread(target=e.watch, args=(lambda: {"default/forks": [p.pid]}, stop), daemon=True)
+        th.start()
+        time.sleep(0.6)
+        c0, t0 = _cpu_with_children(p.pid), time.monotonic()
+        time.sleep(5.0)
+        used = (_cpu_with_children(p.pid) - c0) / (time.monotonic() - t0)
+        assert used <= 0.35, used
+        assert e.throttle.stops > 5
+    finally:
+        stop.set()
+        p.kill()
+        p.wait(10)
+
+
+def test_cgroup2_takes_the_agents_own_supervisor_along(tmp_path, monkeypatch):
+    """ADVICE r5: the agent's restart supervisor (tk8s-supervise, its parent) shares its cgroup;
+    it is moved into the leaf with the agent rather than counted as a stranger -- cgroup2 mode is
+    taken, not dropped to the watchdog."""
+    from tritonk8ssupervisor_amd.agent import resources
+
+    root = tmp_path / "cg"
+    root.mkdir()
+    sup = 4343
+    for f, v in (("cgroup.controllers", "cpuset cpu io memory pids"), ("cgroup.subtree_control", ""),
+                 ("cgroup.procs", f"{os.getpid()}\n{sup}\n")):
+        (root / f).write_text(v)
+    orig_mkdir = Path.mkdir
+
+    def mkdir(self, *a, **kw):
+        orig_mkdir(self, *a, **kw)
+        if str(self).startswith(str(root)) and not (self / "cgroup.procs").exists():
+            (self / "cgroup.procs").write_text("")
+
+    writes = []
+    orig_write = resources._write
+
+    def write(path, value):
+        writes.append((Path(path).relative_to(root).as_posix(), str(value)))
+        orig_write(path, value)
+
+    monkeypatch.setattr(Path, "mkdir", mkdir)
+    monkeypatch.setattr(resources, "_write", write)
+    monkeypatch.setattr(resources, "_own_cgroups", lambda: {"": "/"})
+    monkeypatch.setattr(resources, "_own_supervisor", lambda: sup)
+    monkeypatch.setenv("TK8S_CGROUP_ROOT", str(root))
+    monkeypatch.setenv("TK8S_POD_RESOURCES", "cgroup2")
+    e = Enforcer("kubenode1", Limits(memory=1 << 30))
+    assert e.mode == "cgroup2", e.why
+    assert ("tk8s-agent/cgroup.procs", str(os.getpid())) in writes and ("tk8s-agent/cgroup.procs", str(sup)) in writes
+    # a parent that is not tk8s-supervise is no excuse
+    monkeypatch.setattr(resources, "_own_supervisor", lambda: None)
+    (root / "cgroup.subtree_control").write_text("")
+    e = Enforcer("kubenode2", Limits(memory=1 << 30))
+    assert e.mode == "none" and str(sup) in e.why
+
+
+def test_a_thread_heavy_cpu_pod_starts_under_a_small_limit():
+    """RLIMIT_DATA counts virtual stacks and arenas, not the resident set: a 64Mi pod
+    starting 40 threads (8 MiB stack each) must not fail at pthread_create under the backstop."""
+    import resource
+
+    from tritonk8ssupervisor_amd.agent.resources import rlimit_data_for
+
+    lim = rlimit_data_for(64 << 20)
+    assert lim >= 1 << 30
+    code = ("import threading, time\nts = [threading.Thread(target=time.sleep, args=(0.2,)) for _ in range(40)]\n"
+            "[t.start() for t in ts]\n[t.join() for t in ts]\nprint('ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       preexec_fn=lambda: resource.setrlimit(resource.RLIMIT_DATA, (lim, lim)))
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-1000:]

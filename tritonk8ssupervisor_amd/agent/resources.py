@@ -51,13 +51,16 @@ TICK_S = 0.05             # the watchdog's CPU duty-cycle tick
 BURST_S = 0.1             # how far ahead of its rate a pod may run (seconds of its limit)
 _HZ = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
 RLIMIT_DATA_SLACK = 256 << 20   # the backstop sits above the sampled limit: 2 x limits.memory + this
+RLIMIT_DATA_FLOOR = 1 << 30     # ... and never below 1 GiB
 
 
 def rlimit_data_for(memory: int) -> int:
     """The per-process RLIMIT_DATA backstop of a CPU pod with ``limits.memory``: above the limit
-    the sampler enforces (its private writable memory includes thread stacks and arenas it has not
-    touched), well below what would take the host."""
-    return 2 * int(memory) + RLIMIT_DATA_SLACK
+    the sampler enforces, well below what would take the host. RLIMIT_DATA counts private
+    writable VIRTUAL memory -- 8 MiB per thread stack, malloc arenas not yet touched -- not the
+    resident set Kubernetes limits, so it has a 1 GiB floor (a thread-heavy pod with a
+    small limit must start; its resident set is what the sampler holds to the limit)."""
+    return max(2 * int(memory) + RLIMIT_DATA_SLACK, RLIMIT_DATA_FLOOR)
 
 
 def signal_ids(groups, pids, sig, starts: dict[int, int]) -> None:
@@ -80,12 +83,15 @@ def signal_ids(groups, pids, sig, starts: dict[int, int]) -> None:
 
 
 def _cpu_seconds(pid: int) -> float | None:
-    """CPU time (user + system, all threads) process ``pid`` has used, from /proc/<pid>/stat."""
+    """CPU time process ``pid`` and its waited-for children have used: utime + stime + cutime +
+    cstime (/proc/<pid>/stat fields 14-17, all threads). With the children's part, the CPU of a
+    child that lived and died between two scans still reaches the pod's bill (through its parent),
+    and so does the part of a sampled child's life after its last sample."""
     try:
         with open(f"/proc/{pid}/stat", "rb") as f:
             raw = f.read()
         rest = raw[raw.rindex(b")") + 2:].split()
-        return (int(rest[11]) + int(rest[12])) / _HZ
+        return (int(rest[11]) + int(rest[12]) + int(rest[13]) + int(rest[14])) / _HZ
     except (OSError, ValueError, IndexError):
         return None
 
@@ -101,7 +107,7 @@ class CpuThrottle:
     def __init__(self, machine_cpu: float | None = None):
         self.machine_cpu = machine_cpu or None
         self.balance: dict[str, float] = {}      # pod key (and "" = the machine) -> CPU seconds
-        self.last: dict[int, float] = {}          # pid -> CPU seconds at the previous tick
+        self.total: dict[str, float] = {}         # pod key -> its members' CPU seconds at the previous tick
         self.stopped: dict[str, tuple[list[int], list[int]]] = {}  # pod key -> (groups, pids) it stopped
         self.starts: dict[int, int] = {}          # pid -> its start time (ticks since boot) at the last scan
         self.exempt: set[str] = set()             # pods being terminated: never stopped again
@@ -144,18 +150,18 @@ class CpuThrottle:
             self.resume(key)
         for key in [k for k in self.balance if k and k not in pods]:
             del self.balance[key]
+        # A pod's bill is the change of ONE sum over its members -- each member's own CPU plus that
+        # of its children it has waited for: a member that appeared since the last tick brings its
+        # whole life in (its CPU before the first sample is charged too), and one that exited and
+        # was reaped by a member moves its total into that member's children's part (nothing is
+        # charged twice; a child re-parented outside the pod takes only its unsampled tail along).
         used: dict[str, float] = {}
-        seen: dict[int, float] = {}
+        totals: dict[str, float] = {}
         for key, (_groups, pids) in pods.items():
-            u = 0.0
-            for pid in pids:
-                t = _cpu_seconds(pid)
-                if t is None:
-                    continue
-                seen[pid] = t
-                u += max(0.0, t - self.last.get(pid, t))
-            used[key] = u
-        self.last = seen
+            t = sum(x for x in (_cpu_seconds(p) for p in pids) if x is not None)
+            totals[key] = t
+            used[key] = max(0.0, t - self.total.get(key, 0.0))
+        self.total = totals
         machine_neg = False
         if self.machine_cpu:
             u = sum(v for k, v in used.items() if in_machine(k))
@@ -338,6 +344,17 @@ def detect_mode() -> tuple[str, str]:
     return "none", "; ".join(why)
 
 
+def _own_supervisor() -> int | None:
+    """This agent's restart supervisor: its parent, when that is ``tk8s-supervise``."""
+    ppid = os.getppid()
+    try:
+        with open(f"/proc/{ppid}/comm") as f:
+            comm = f.read().strip()
+    except OSError:
+        return None
+    return ppid if comm == "tk8s-supervise" else None
+
+
 def _write(path: Path, value) -> None:
     with open(path, "w") as f:
         f.write(f"{value}\n")
@@ -390,15 +407,24 @@ class Enforcer:
         if not {"memory", "cpu"} <= have or not os.access(own / "cgroup.subtree_control", os.W_OK):
             self.why += f"cgroup2: {own} is not delegated to this user (controllers {sorted(have)}); "
             return False
-        # no internal processes: this agent moves to a leaf first -- and only this agent (ADVICE r4:
-        # other processes sharing the cgroup, say the other node agents of the host starting at the
-        # same moment, are not ours to move; with them there the subtree cannot be enabled)
+        # no internal processes: this agent moves to a leaf first -- with its own restart supervisor
+        # (tk8s-supervise, the agent's parent, always shares its cgroup and supervises
+        # nothing else) -- and nothing else (other processes sharing the cgroup, say the
+        # other node agents of the host starting at the same moment, are not ours to move; with
+        # them there the subtree cannot be enabled)
         leaf = own / "tk8s-agent"
         leaf.mkdir(exist_ok=True)
-        _write(leaf / "cgroup.procs", os.getpid())
-        others = [p for p in (own / "cgroup.procs").read_text().split() if p != str(os.getpid())]
+        mine = [str(os.getpid())]
+        sup = _own_supervisor()
+        procs = (own / "cgroup.procs").read_text().split()
+        if sup is not None and str(sup) in procs:
+            mine.append(str(sup))
+        for p in mine:
+            _write(leaf / "cgroup.procs", p)
+        others = [p for p in procs if p not in mine]
         if others and not (own / "cgroup.subtree_control").read_text().split():
-            _write(own / "cgroup.procs", os.getpid())  # back where it was
+            for p in mine:
+                _write(own / "cgroup.procs", p)  # back where they were
             self.why += (f"cgroup2: {own} also holds processes that are not this agent's ({', '.join(others[:5])}); "
                          "give each agent a delegated cgroup of its own; ")
             return False
