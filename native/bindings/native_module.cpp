@@ -70,6 +70,8 @@ PYBIND11_MODULE(_tk8s_native, m) {
       py::arg("factor") = 4, py::arg("iters") = 10, py::arg("warmup") = 2,
       py::arg("dtype") = "float32", py::arg("check") = true, G());
   m.def("rccl_version", &tk8s::rccl_version);
+  m.def("allreduce_busbw", &tk8s::allreduce_busbw, py::arg("algbw_gbps"), py::arg("nranks"),
+        "busbw of a ring all-reduce: algbw * 2(n-1)/n, 0 at n <= 1 (SURVEY.md N3)");
   m.def("release_probe_scratch", &tk8s::release_probe_scratch, G());
 
   // ---- raw launchers --------------------------------------------------------------------

@@ -96,7 +96,8 @@ int main(int argc, char** argv) {
     }
     const size_t hbm = static_cast<size_t>(a.num("hbm-bytes", 1LL << 30));
     const size_t md5 = a.has("skip-md5") ? 0 : static_cast<size_t>(a.num("md5-bytes", 256LL << 20));
-    const size_t copy = static_cast<size_t>(a.num("copy-bytes", 256LL << 20));
+    // 1 GiB each way: 8 x the 256 MB Infinity Cache, so the copy rate is an HBM rate
+    const size_t copy = static_cast<size_t>(a.num("copy-bytes", 1LL << 30));
     const size_t peer_bytes = static_cast<size_t>(a.num("peer-bytes", 64LL << 20));
     const auto chunk = static_cast<uint32_t>(a.num("chunk", 1024));
     const auto seed = static_cast<uint64_t>(a.num("seed", 0));

@@ -11,7 +11,8 @@ from pathlib import Path
 
 import pytest
 
-BIN = Path(__file__).resolve().parents[1] / "tritonk8ssupervisor_amd" / "bin"
+REPO = Path(__file__).resolve().parents[1]
+BIN = REPO / "tritonk8ssupervisor_amd" / "bin"
 
 
 def test_build_produces_gfx950_code_objects(native_build):
@@ -77,6 +78,33 @@ def test_native_module_imports_without_a_gpu(native_build):
     if info.get("ok"):
         pytest.skip("a GPU is visible here")
     assert info["device_count"] == 0 and "error" in info
+
+
+def test_busbw_is_the_n3_formula_at_every_n(native_build):
+    """busbw = algbw * 2(n-1)/n -- 0 at one rank, where the
+    all-reduce is a local copy (the fabric line then says "1 GPU: no fabric", busbw null) -- in
+    the native validator, its gloo twin and the fabric report alike."""
+    from tritonk8ssupervisor_amd.fabric import bandwidth_summary, fabric_line
+    from tritonk8ssupervisor_amd.ops import native
+
+    nat = native()
+    for n, want in ((1, 0.0), (2, 100.0), (4, 150.0), (8, 175.0)):
+        assert nat.allreduce_busbw(100.0, n) == pytest.approx(want)
+    one = bandwidth_summary([{"ok": True, "peak_algbw_gbps": 3381.0, "peak_busbw_gbps": None}], 1)
+    assert one == {"peak_busbw_gbps": None, "peak_algbw_gbps": 3381.0, "fabric": "1 GPU: no fabric"}
+    assert "no fabric" in fabric_line({**one, "nranks": 1})
+    eight = bandwidth_summary([{"peak_algbw_gbps": 100.0, "peak_busbw_gbps": 175.0},
+                               {"peak_algbw_gbps": 90.0, "peak_busbw_gbps": 157.5}], 8)
+    assert eight == {"peak_busbw_gbps": 175.0, "peak_algbw_gbps": 100.0}
+    assert fabric_line({**eight, "nranks": 8}) == "RCCL all-reduce peak busbw 175.0 GB/s over 8 GPU(s)"
+
+
+def test_the_validator_defaults_are_the_rccl_tests_sweep():
+    """8 B x2 to >= 1 GiB, fp32 and bf16 -- tk8s-rccl's defaults (the fabric check on
+    the Ready path asks for its shorter sweep explicitly and says so)."""
+    src = (REPO / "native" / "tools" / "tk8s_rccl.cpp").read_text()
+    assert 'a.num("min-bytes", 8)' in src and 'a.num("max-bytes", 1LL << 30)' in src
+    assert 'a.num("factor", 2)' in src and 'a.str("dtype", "both")' in src
 
 
 @pytest.mark.parametrize("tool", ["tk8s-gpuinfo", "tk8s-probe"])
