@@ -34,4 +34,8 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
 // free them (e.g. from a long-lived process once validation is done).
 void release_probe_scratch();
 
+// Size that allocation once, up front, for a run of the local probes with these sizes (0 = the
+// probe is skipped): growing it between probes costs a hipFree, which synchronises the device.
+void reserve_probe_scratch(int device, size_t hbm_bytes, size_t md5_bytes, uint32_t chunk_bytes, size_t copy_bytes);
+
 }  // namespace tk8s

@@ -202,6 +202,18 @@ void release_probe_scratch() {
   g_scratch.clear();
 }
 
+void reserve_probe_scratch(int device, size_t hbm_bytes, size_t md5_bytes, uint32_t chunk_bytes, size_t copy_bytes) {
+  size_t need = kAlign;
+  if (hbm_bytes) need = std::max(need, align_up(hbm_bytes) + kAlign);
+  if (md5_bytes && chunk_bytes) {
+    const size_t ws = md5_tree_workspace(md5_bytes, chunk_bytes);
+    need = std::max(need, align_up(std::max<size_t>(md5_bytes, 16)) + 2 * align_up(ws) + kAlign + kMallFlush);
+  }
+  if (copy_bytes) need = std::max(need, 2 * align_up(copy_bytes) + kAlign);
+  DeviceGuard g(device);
+  (void)scratch(device, need);
+}
+
 std::string gpuinfo_json(bool with_links) {
   const auto t0 = std::chrono::steady_clock::now();
   int n = 0;

@@ -131,6 +131,10 @@ int main(int argc, char** argv) {
       const auto td = std::chrono::steady_clock::now();
       DeviceResult& r = res[k];
       const int dev = devices[k];
+      try {  // one allocation for every local probe (a regrow between them synchronises the device)
+        tk8s::reserve_probe_scratch(dev, hbm, md5, chunk, copy);
+      } catch (const std::exception&) {  // the probes grow it themselves, and report what fails
+      }
       auto t = std::chrono::steady_clock::now();
       r.hbm = hbm ? tk8s::hbm_write_probe(hbm, iters, mode, dev) : std::string("{\"ok\":true,\"skipped\":true}");
       r.hbm_ms = ms_since(t);

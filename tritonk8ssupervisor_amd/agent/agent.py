@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import json
 import os
+import signal
 import subprocess
 import sys
 import threading
@@ -1134,6 +1135,9 @@ class Agent:
             return
         self._execs_seen.add(xid)
         pp = self.runtime.running().get(f"{x['namespace']}/{x['pod']}")
+        if x.get("stream"):
+            self._run_exec_stream(x, pp)
+            return
         if pp is None or pp.done.is_set():
             res = {"stdout": "", "stderr": f"pod {x['pod']} is not running on {self.name}\n", "exitCode": 1}
         else:
@@ -1158,6 +1162,108 @@ class Agent:
             self.api.put(self.api.k8s(f"/api/v1/nodes/{self.name}/execs/{xid}"), res)
         except (ApiError, OSError) as e:
             print(f"{self.name}: exec {xid} result not delivered: {e}", flush=True)
+
+    def _run_exec_stream(self, x: dict, pp) -> None:
+        """An interactive exec (``kubectl exec -it``): the command runs on a pseudo-terminal
+        inside the pod's container or GPU jail (container_exec_argv, like every exec), and its
+        bytes stream over a WebSocket to the control plane (k8s_api.h_exec_stream), which relays
+        them to the client with the channel bytes of the Kubernetes protocol: 0 stdin and 4
+        resize ({"Width", "Height"}) come in, 1 the terminal's output and 3 the final Status go
+        out. [255, 0] (the client closed stdin) is the terminal's end of file; the client going
+        away (0xfe from the relay, or the stream closing) hangs the terminal up (SIGHUP)."""
+        import fcntl
+        import pty
+        import struct
+        import termios
+        from urllib.parse import urlsplit
+
+        from ..controlplane.k8s_api import exec_status
+        from ..controlplane.wsclient import WSClient
+
+        xid = x["metadata"]["name"]
+        u = urlsplit(self.api.base)
+        try:
+            ws = WSClient.connect(u.hostname, u.port or 80, f"{self.api.prefix}/api/v1/nodes/{self.name}/execs/{xid}/stream",
+                                  token=self.api.token, protocols=("tk8s.exec.v1",))
+        except OSError as e:
+            print(f"{self.name}: exec {xid}: stream not opened: {e}", flush=True)
+            return
+        send_lock = threading.Lock()
+
+        def send(b: bytes) -> None:
+            with send_lock:
+                try:
+                    ws.send(b)
+                except OSError:
+                    pass
+
+        if pp is None or pp.done.is_set():
+            send(b"\x01" + f"pod {x['pod']} is not running on {self.name}\r\n".encode())
+            send(b"\x03" + json.dumps(exec_status(1)).encode())
+            ws.close()
+            return
+        env = dict(pp.env)
+        env.setdefault("TERM", "xterm")
+        if self.runtime.tool_dirs:
+            env["PATH"] = os.pathsep.join(self.runtime.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
+        master, slave = pty.openpty()
+
+        def controlling_tty():  # the child's own session, the terminal as its controlling tty
+            os.setsid()
+            fcntl.ioctl(0, termios.TIOCSCTTY, 0)
+
+        try:
+            proc = subprocess.Popen(container_exec_argv(pp, list(x["command"])), stdin=slave, stdout=slave, stderr=slave,
+                                    env=env, cwd=pp.dir, preexec_fn=controlling_tty, close_fds=True)
+        except OSError as e:
+            os.close(master)
+            os.close(slave)
+            send(b"\x01" + f"exec: {e}\r\n".encode())
+            send(b"\x03" + json.dumps(exec_status(127)).encode())
+            ws.close()
+            return
+        os.close(slave)
+
+        def inbound():  # stdin and resizes from the client
+            while True:
+                m = ws.recv()
+                if m is not None and m[:2] == b"\xff\x00":  # stdin closed: ^D, end of file on the terminal
+                    try:
+                        os.write(master, b"\x04")
+                    except OSError:
+                        pass
+                    continue
+                if m is None or m[:1] == b"\xfe":
+                    if proc.poll() is None:  # the client hung up: so does the terminal
+                        try:
+                            os.killpg(proc.pid, signal.SIGHUP)
+                        except OSError:
+                            pass
+                    return
+                ch, data = m[:1], m[1:]
+                try:
+                    if ch == b"\x00" and data:
+                        os.write(master, data)
+                    elif ch == b"\x04" and data:
+                        sz = json.loads(data)
+                        fcntl.ioctl(master, termios.TIOCSWINSZ,
+                                    struct.pack("HHHH", int(sz.get("Height", 24)), int(sz.get("Width", 80)), 0, 0))
+                except (OSError, ValueError, TypeError):
+                    pass
+
+        threading.Thread(target=inbound, name=f"exec-{xid}-in", daemon=True).start()
+        while True:  # the terminal's output until the command has exited and the pty is drained
+            try:
+                data = os.read(master, 65536)
+            except OSError:  # EIO: every slave end is closed
+                break
+            if not data:
+                break
+            send(b"\x01" + data)
+        code = proc.wait()
+        os.close(master)
+        send(b"\x03" + json.dumps(exec_status(code if code >= 0 else 128 - code)).encode())
+        ws.close()
 
     def _handle(self, etype: str, pod: dict) -> None:
         md = pod["metadata"]

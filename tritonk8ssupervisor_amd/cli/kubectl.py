@@ -8,7 +8,7 @@
   kubectl rollout status|restart deploy/NAME
   kubectl label|annotate KIND NAME k=v k-
   kubectl logs POD [--tail N] [-f]    kubectl cordon|uncordon|drain NODE
-  kubectl exec POD -- CMD [ARGS...]   (non-interactive: stdout/stderr/exit code)
+  kubectl exec [-it] POD -- CMD [ARGS...]   (-it: a terminal in the pod, streaming; else stdout/stderr/exit code)
   kubectl top nodes                   (amd.com/gpu in use, hotspot temperature, power, VRAM)
   kubectl wait job/NAME [--timeout S] kubectl cluster-info | version
 
@@ -738,6 +738,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("--show-managed-fields", action="store_true")
     ap.add_argument("--address", default="127.0.0.1")
     ap.add_argument("-c", "--container")
+    ap.add_argument("-i", "--stdin", action="store_true")  # exec: pass stdin (with -t: interactive)
+    ap.add_argument("-t", "--tty", action="store_true")    # exec: a terminal in the pod
     ap.add_argument("--to-revision", type=int, default=0)
     ap.add_argument("--for", dest="for_")
     ap.add_argument("--disable-eviction", action="store_true")
@@ -772,6 +774,9 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     if "--" in argv:  # kubectl exec POD -- CMD ARGS...
         command = argv[argv.index("--") + 1:]
         argv = argv[:argv.index("--")]
+    if argv[:1] == ["exec"]:  # `kubectl exec -it POD`: the flags may come before the pod name
+        flags = [x for x in argv if x in ("-i", "-t", "-it", "-ti", "--stdin", "--tty")]
+        argv = [x for x in argv if x not in flags] + flags
     if argv[:1] == ["logs"]:  # `-f` means --filename and `-p` --patch everywhere but logs
         argv = [{"-f": "--follow", "-p": "--previous"}.get(x, x) for x in argv]
     a = ap.parse_args(argv)
@@ -1058,7 +1063,11 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
                     time.sleep(0.2)
         elif a.verb == "exec":
             if not a.command:
-                raise SystemExit("usage: kubectl exec POD -- COMMAND [ARGS...]")
+                raise SystemExit("usage: kubectl exec [-it] POD -- COMMAND [ARGS...]")
+            if a.tty:  # interactive: a terminal in the pod, bytes streaming both ways
+                from .kubectl_streams import exec_tty
+
+                return exec_tty(k, ns, a.args[0], a.command, a.stdin)
             r = k.post(k.k8s(object_path("pod", a.args[0], ns) + "/exec"),
                        {"command": a.command, "timeoutSeconds": float(a.timeout.rstrip("s"))},
                        timeout=float(a.timeout.rstrip("s")) + 30)

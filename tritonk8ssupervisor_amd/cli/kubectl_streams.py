@@ -166,3 +166,92 @@ def attach(k, ns: str, pod: str) -> int:
         pass
     ws.close()
     return code
+
+
+def exec_tty(k, ns: str, pod: str, command: list[str], stdin: bool = True, inp=None, out=None) -> int:
+    """``kubectl exec -it POD -- CMD``: a pseudo-terminal in the pod (k8s_api.h_pod_exec_ws with
+    tty=true). This terminal goes raw while it runs, its size is sent first and on every SIGWINCH
+    (channel 4), keystrokes go on channel 0, the pod's terminal output comes back on channel 1;
+    the exit code is the command's."""
+    import os
+    import signal
+    import threading
+
+    inp = sys.stdin if inp is None else inp
+    out = sys.stdout.buffer if out is None else out
+    q = [("command", c) for c in command] + [("stdout", "true"), ("tty", "true")]
+    if stdin:
+        q.append(("stdin", "true"))
+    try:
+        ws = WSClient.connect(k.host, k.port, k.k8s(object_path("pod", pod, ns) + "/exec"), q, k.token,
+                              ("v5.channel.k8s.io", "v4.channel.k8s.io"), timeout=30)
+    except (OSError, WSClosed) as e:
+        print(f"error: {e}", file=sys.stderr)
+        return 1
+    lock = threading.Lock()
+
+    def send(b: bytes) -> None:
+        with lock:
+            try:
+                ws.send(b)
+            except OSError:
+                pass
+
+    fd = inp.fileno() if hasattr(inp, "fileno") else None
+    is_tty = fd is not None and os.isatty(fd)
+
+    def resize(*_):
+        try:
+            sz = os.get_terminal_size(fd)
+            send(b"\x04" + json.dumps({"Width": sz.columns, "Height": sz.lines}).encode())
+        except OSError:
+            pass
+
+    saved = None
+    if is_tty:
+        import termios
+        import tty as _tty
+
+        saved = termios.tcgetattr(fd)
+        _tty.setraw(fd)
+        resize()
+        old_winch = signal.signal(signal.SIGWINCH, resize)
+
+    def pump():
+        while True:
+            try:
+                data = os.read(fd, 4096) if fd is not None else inp.read(4096)
+            except OSError:
+                data = b""
+            if not data:
+                send(b"\xff\x00")  # stdin closed (v5)
+                return
+            send(b"\x00" + (data if isinstance(data, bytes) else data.encode()))
+
+    if stdin:
+        threading.Thread(target=pump, name="exec-stdin", daemon=True).start()
+    code = 1
+    try:
+        while (msg := ws.recv()) is not None:
+            if msg[:1] in (b"\x01", b"\x02"):
+                out.write(msg[1:])
+                out.flush()
+            elif msg[:1] == b"\x03":
+                st = json.loads(msg[1:] or b"{}")
+                code = 0 if st.get("status") == "Success" else 1
+                for c in ((st.get("details") or {}).get("causes") or []):
+                    if c.get("reason") == "ExitCode":
+                        code = int(c.get("message") or 1)
+                if st.get("status") != "Success" and st.get("reason") != "NonZeroExitCode":
+                    print(f"error: {st.get('message', 'exec failed')}", file=sys.stderr)
+                break
+    except KeyboardInterrupt:
+        pass
+    finally:
+        if saved is not None:
+            import termios
+
+            termios.tcsetattr(fd, termios.TCSADRAIN, saved)
+            signal.signal(signal.SIGWINCH, old_winch)
+        ws.close()
+    return code

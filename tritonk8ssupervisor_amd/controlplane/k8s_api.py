@@ -1375,8 +1375,14 @@ class KubernetesAPI:
     async def h_pod_exec_ws(self, req: Request, ns: str, name: str, pid: str | None = None):
         """A stock ``kubectl exec`` (Kubernetes >= 1.29 clients): GET .../pods/NAME/exec?command=..
         upgraded to a WebSocket with subprotocol v5.channel.k8s.io (or v4). Frames carry a channel
-        byte: 0 stdin, 1 stdout, 2 stderr, 3 the final Status, 255 (v5) closes a stream. The command
-        runs like the request/response exec (non-interactive: no TTY, output after it exits)."""
+        byte: 0 stdin, 1 stdout, 2 stderr, 3 the final Status, 4 a terminal resize, 255 (v5)
+        closes a stream.
+
+        * ``tty=true`` (``kubectl exec -it``): INTERACTIVE -- the node agent runs the command on a
+          pseudo-terminal inside the pod's container or GPU jail and the bytes stream both ways
+          while it runs (stdin and resizes in, the terminal's output out); ``_exec_stream_relay``.
+        * otherwise: the command runs to completion with the stdin the client sent (until it
+          closes stdin, v5), then its stdout, stderr and exit status come back."""
         from .httpserver import WebSocketResponse
 
         p = self._pid(pid, req)
@@ -1384,9 +1390,10 @@ class KubernetesAPI:
         cmd = req.q_all("command")
         if not cmd:
             raise HttpError(422, "command must be given (?command=...)")
-        if req.q("tty") == "true":
-            raise HttpError(400, "exec with a TTY is not supported (non-interactive exec only)")
         want_stdin = req.q("stdin") == "true"
+        if req.q("tty") == "true":
+            pod = self._running_pod(p, ns, name)
+            return WebSocketResponse(lambda ws: self._exec_stream_relay(ws, p, ns, name, pod, cmd, want_stdin), proto)
 
         async def session(ws):
             data = b""
@@ -1409,15 +1416,80 @@ class KubernetesAPI:
                 if data and req.q(f, "true") != "false":
                     for i in range(0, len(data), 1 << 20):  # frames of at most 1 MiB
                         await ws.send(ch + data[i:i + (1 << 20)])
-            if r["exitCode"] == 0:
-                status = {"metadata": {}, "status": "Success"}
-            else:
-                status = {"metadata": {}, "status": "Failure", "reason": "NonZeroExitCode",
-                          "message": f"command terminated with non-zero exit code: {r['exitCode']}",
-                          "details": {"causes": [{"reason": "ExitCode", "message": str(r["exitCode"])}]}}
-            await ws.send(b"\x03" + json.dumps(status).encode())
+            await ws.send(b"\x03" + json.dumps(exec_status(r["exitCode"])).encode())
 
         return WebSocketResponse(session, proto)
+
+    async def _exec_stream_relay(self, ws, p: str, ns: str, name: str, pod: dict, cmd: list[str], stdin: bool):
+        """An interactive exec: an exec request marked ``stream`` for the pod's node; the node
+        agent connects back to ``.../nodes/<node>/execs/<id>/stream`` (h_exec_stream) and this
+        relays frames between the client and it, channel bytes unchanged, until the node sends the
+        final Status (channel 3) or either side goes away."""
+        self._seq += 1
+        xid = f"x{self._seq:x}"
+        node = pod["spec"]["nodeName"]
+        key = _key(p, node, xid)
+        streams = self.__dict__.setdefault("_exec_streams", {})
+        loop = asyncio.get_running_loop()
+        sess = {"node_ws": loop.create_future(), "done": asyncio.Event()}
+        streams[key] = sess
+        self.store.put("execs", key, {"metadata": {"name": xid}, "_project": p, "node": node, "pod": name,
+                                      "namespace": ns, "command": [str(c) for c in cmd], "stream": True,
+                                      "tty": True, "stdin": stdin, "status": {"phase": "Pending"}})
+        try:
+            try:
+                nws = await asyncio.wait_for(asyncio.shield(sess["node_ws"]), 30.0)
+            except asyncio.TimeoutError:
+                await ws.send(b"\x03" + json.dumps({"metadata": {}, "status": "Failure", "reason": "InternalError",
+                                                    "message": f"node {node} did not start the exec in 30s",
+                                                    "code": 504}).encode())
+                return
+
+            async def client_to_node():
+                while True:
+                    m = await ws.recv()
+                    if m is None:
+                        await nws.send(b"\xfe")  # the client is gone: hang up the terminal (tk8s-internal)
+                        return
+                    if m[:1] in (b"\x00", b"\x04", b"\xff"):
+                        await nws.send(m)
+
+            async def node_to_client():
+                while True:
+                    m = await nws.recv()
+                    if m is None:
+                        return
+                    await ws.send(m)
+                    if m[:1] == b"\x03":  # the final Status: done
+                        return
+
+            up = asyncio.ensure_future(client_to_node())
+            try:
+                await node_to_client()
+            finally:
+                up.cancel()
+        finally:
+            sess["done"].set()
+            streams.pop(key, None)
+            self.store.delete("execs", key)
+
+    async def h_exec_stream(self, req: Request, node: str, xid: str, pid: str | None = None):
+        """The node agent's side of an interactive exec (WebSocket, node token)."""
+        from .httpserver import WebSocketResponse
+
+        p = self._pid(pid, req)
+        self._node_secret_ok(req, _key(p, node))
+        sess = (self.__dict__.get("_exec_streams") or {}).get(_key(p, node, xid))
+        if sess is None or sess["node_ws"].done():
+            raise HttpError(404, f"no interactive exec {xid} waiting for node {node}")
+        if "websocket" not in (req.headers.get("upgrade") or "").lower():
+            raise HttpError(400, "the exec stream needs a WebSocket upgrade")
+
+        async def session(nws):
+            sess["node_ws"].set_result(nws)
+            await sess["done"].wait()
+
+        return WebSocketResponse(session, "tk8s.exec.v1")
 
     def _ws_upgrade(self, req: Request, p: str, what: str, protocols: tuple[str, ...], allow_none: bool = False) -> str:
         """Authorise a WebSocket stream request (project API token or a node token) and pick the
@@ -1609,6 +1681,15 @@ class KubernetesAPI:
         if x is None:
             raise HttpError(404, f"exec {xid} not found (timed out?)")
         return {"ok": True}
+
+
+def exec_status(code: int) -> dict:
+    """The channel-3 Status of an exec that ended with exit ``code``."""
+    if code == 0:
+        return {"metadata": {}, "status": "Success"}
+    return {"metadata": {}, "status": "Failure", "reason": "NonZeroExitCode",
+            "message": f"command terminated with non-zero exit code: {code}",
+            "details": {"causes": [{"reason": "ExitCode", "message": str(code)}]}}
 
 
 def _pod_conditions(pod: dict) -> None:

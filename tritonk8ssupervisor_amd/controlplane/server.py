@@ -282,6 +282,7 @@ class ControlPlane(Authentication, RancherAPI, KubernetesAPI, Controllers, Workl
             add("POST", r"/api/v1/namespaces/(?P<ns>[^/]+)/serviceaccounts/(?P<name>[^/]+)/token", self.h_token_request)
             add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs", self.h_node_execs)
             add("PUT", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)", self.h_exec_result)
+            add("GET", r"/api/v1/nodes/(?P<node>[^/]+)/execs/(?P<xid>[^/]+)/stream", self.h_exec_stream)
             # every other object path, built-in kinds (KIND_GROUPS, CLUSTER_KIND_GROUPS) and custom
             # resources alike: two patterns resolved by plural (crds.h_resource), not a regex per
             # kind -- fewer routes to compile at start-up and to scan per request
