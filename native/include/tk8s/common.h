@@ -102,8 +102,8 @@ class EventTimer {
   void start(hipStream_t s) { TK8S_HIP_CHECK(hipEventRecord(start_, s)); }
   void stop(hipStream_t s) { TK8S_HIP_CHECK(hipEventRecord(stop_, s)); }
   // Milliseconds between start and stop (waits for stop, bounded: wait_event).
-  float elapsed_ms() {
-    wait_event(stop_, "timed region");
+  float elapsed_ms(double bound_s = gpu_sync_timeout_s()) {
+    wait_event(stop_, "timed region", bound_s);
     float ms = 0.f;
     TK8S_HIP_CHECK(hipEventElapsedTime(&ms, start_, stop_));
     return ms;

@@ -59,6 +59,18 @@ inline double env_seconds(const char* name, double def) {
 // TK8S_GPU_SYNC_TIMEOUT_S, default 30 s -- the HSA payload's long-standing bound.
 inline double gpu_sync_timeout_s() { return env_seconds("TK8S_GPU_SYNC_TIMEOUT_S", 30.0); }
 
+// Bound on one xGMI pull's wait (TK8S_PEER_SYNC_TIMEOUT_S, default 5 s, never above the general
+// bound): a 16-64 MiB pull takes milliseconds even over PCIe, so a link that has not finished by
+// then is reported rather than waited for.
+inline double peer_sync_timeout_s() {
+  const double g = gpu_sync_timeout_s();
+  return env_seconds("TK8S_PEER_SYNC_TIMEOUT_S", g < 5.0 ? g : 5.0);
+}
+
+// Bound on a payload's whole peer phase (TK8S_PEER_PHASE_TIMEOUT_S, default 20 s): pulls not yet
+// started when it has passed are reported as not run.
+inline double peer_phase_timeout_s() { return env_seconds("TK8S_PEER_PHASE_TIMEOUT_S", 20.0); }
+
 // ---- TK8S_FAULTS ---------------------------------------------------------------------------
 struct FaultEntry {
   std::string point;  // "<tool>.<kind>@<phase>"

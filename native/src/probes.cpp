@@ -485,7 +485,8 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
     kt.start(st.s);
     for (int i = 0; i < iters; ++i) stream_copy(dst, src, bytes, st.s);
     kt.stop(st.s);
-    const float kernel_ms = kt.elapsed_ms() / iters;
+    const double bound = peer ? peer_sync_timeout_s() : gpu_sync_timeout_s();  // a link is not waited for
+    const float kernel_ms = kt.elapsed_ms(bound) / iters;
     TK8S_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(unsigned long long), st.s));
     verify_fill(dst, bytes, kPeerPattern, bad, st.s);
     unsigned long long nbad = 0;
@@ -500,9 +501,9 @@ std::string copy_probe(int src_device, int dst_device, size_t bytes, int iters, 
       for (int i = 0; i < iters; ++i)
         TK8S_HIP_CHECK(hipMemcpyPeerAsync(dst, dst_device, src, src_device, bytes, st.s));
       dt.stop(st.s);
-      dma_ms = dt.elapsed_ms() / iters;
+      dma_ms = dt.elapsed_ms(bound) / iters;
     }
-    wait_stream(st.s, "copy probe");
+    wait_stream(st.s, "copy probe", bound);
     Json j;
     j.kv("ok", nbad == 0)
         .kv("probe", peer ? "xgmi_peer_copy" : "local_copy")

@@ -517,7 +517,8 @@ class Device {
   // kernel arguments in device memory. So the batch's arguments are staged in host memory, one
   // small copy kernel (its own few arguments read from the host) moves them into a VRAM arena,
   // and the batch's packets point there.
-  void sync() {
+  // bound_s <= 0: the general GPU bound (TK8S_GPU_SYNC_TIMEOUT_S, 30 s)
+  void sync(double bound_s = 0) {
     if (batch_.empty()) return;
     const size_t bytes = align_up(stage_off_, 16);
     KernArgs cargs(stage_ + kKernargArena, static_cast<uint32_t>(kStageSlot));
@@ -541,7 +542,7 @@ class Device {
     // (TK8S_GPU_SYNC_TIMEOUT_S, default 30 s). On expiry a fault-injected stall is released and
     // the queue gets a few seconds to drain; the batch is dropped either way, so the next pull
     // starts clean.
-    const double bound_ms = tk8s::gpu_sync_timeout_s() * 1000.0;
+    const double bound_ms = (bound_s > 0 ? bound_s : tk8s::gpu_sync_timeout_s()) * 1000.0;
     const auto t0 = std::chrono::steady_clock::now();
     while (hsa_signal_wait_scacquire(last, HSA_SIGNAL_CONDITION_LT, 1, 1000000, HSA_WAIT_STATE_ACTIVE) >= 1) {
       if (ms_since(t0) > bound_ms) {
@@ -965,8 +966,21 @@ void run_peers(const std::vector<int>& devices, const Config& c, std::vector<Dev
                                                         res[j].base);
     for (size_t k : idx) access[k][j] = st == HSA_STATUS_SUCCESS ? "allowed" : "denied";
   }
-  // 3. rounds: in round r every GPU i pulls from GPU (i + r) mod m, all at once.
+  // 3. rounds: in round r every GPU i pulls from GPU (i + r) mod m, all at once -- all of them
+  // inside TK8S_PEER_PHASE_TIMEOUT_S (default 20 s): once it has passed, the remaining rounds are
+  // reported as not run, so a fabric where every pull times out costs one bound, not m - 1 of
+  // them (the host burn-in then re-runs the pulls through the HIP probe: burnin.HostBurnin)
+  const auto phase_t0 = std::chrono::steady_clock::now();
+  const double phase_ms = tk8s::peer_phase_timeout_s() * 1000.0;
   for (size_t r = 1; r < m; ++r) {
+    if (ms_since(phase_t0) > phase_ms) {
+      for (size_t k = 0; k < m; ++k) {
+        res[k].peers.push_back(pull_json("xgmi_peer_pull", devices[(k + r) % m], devices[k], c, access[k][(k + r) % m], 0,
+                                         0, "not run: the peer phase's deadline passed"));
+        res[k].peers_ok = false;
+      }
+      continue;
+    }
     std::vector<std::thread> th;
     for (size_t k = 0; k < m; ++k) {
       th.emplace_back([&, k, r] {

@@ -152,8 +152,15 @@ int main(int argc, char** argv) {
       if (a.has("peers"))
         // Offset order: device k pulls from k+1, k+2, ... (mod m), so at any moment the devices
         // read from different sources over different links instead of all from device 0 first.
+        // All of it inside the peer phase's bound (failfast.h peer_phase_timeout_s).
         for (size_t off = 1; off < devices.size(); ++off) {
           const int s = devices[(k + off) % devices.size()];
+          if (ms_since(t) > tk8s::peer_phase_timeout_s() * 1000.0) {
+            r.peers.push_back(tk8s::Json().kv("ok", false).kv("probe", "xgmi_peer_copy").kv("src_device", s)
+                                  .kv("dst_device", dev).kv("error", "not run: the peer phase's deadline passed").str());
+            r.peers_ok = false;
+            continue;
+          }
           // A failed pull is a link verdict (xgmi.link_report: dead link -> the nodes at both
           // ends NotReady), not a device one: the device keeps its own result, so every machine
           // still gets its share of the burn-in.

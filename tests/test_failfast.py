@@ -176,6 +176,8 @@ def test_hsa_peer_phase_failure_falls_back_to_the_hip_probe(tmp_path, monkeypatc
     from tritonk8ssupervisor_amd.xgmi import annotations
 
     monkeypatch.setenv("TK8S_FAKE_GPUS", "2")  # (visibility env only; the tools above are what runs)
+    monkeypatch.setenv("TK8S_HOST_REGISTRY", str(tmp_path / "hostreg"))
+    monkeypatch.delenv("TK8S_PEERS_RUNTIME", raising=False)
     hsa = _fake_tools(tmp_path, hsa_mode)
     events = []
     cmd = [str(hsa), "--all-devices", "--gpuinfo", "--peers", "--peer-bytes", str(16 << 20), "--iters", "2"]
@@ -195,6 +197,13 @@ def test_hsa_peer_phase_failure_falls_back_to_the_hip_probe(tmp_path, monkeypatc
     share = split_host_result(r, [0, 1], [0], hb.xgmi)
     assert share["ok"] and share["xgmi"]["healthy"] and share["xgmi"]["runtimes"] == ["hip-fallback"]
     assert annotations(share["xgmi"])["tk8s.amd.com/xgmi-runtime"] == "hip-fallback"
+    # learned: the next bring-ups on this host pull through the HIP probe directly
+    from tritonk8ssupervisor_amd import earlyburn
+
+    assert earlyburn.hsa_peers_failed()
+    assert os.path.basename(earlyburn.probe_tool(peers=True)) == "tk8s-probe"
+    monkeypatch.setenv("TK8S_PEERS_RUNTIME", "hsa")
+    assert not earlyburn.hsa_peers_failed()
 
 
 def test_no_fallback_for_a_passing_hsa_run_or_a_bad_word_verdict():

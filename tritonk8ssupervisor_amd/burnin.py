@@ -148,6 +148,22 @@ def peer_fallback_reason(command: list, result: dict | None, rc: int | None, ngp
     return None
 
 
+def mark_hsa_peers_failed(reason: str) -> None:
+    """Record in the host registry that the HSA payload's pulls failed here and the HIP probe's
+    passed (earlyburn.hsa_peers_failed reads it)."""
+    import json
+    import time
+
+    from .earlyburn import PEERS_MARK, registry_dir
+    from .utils.fsutil import atomic_write
+
+    try:
+        os.makedirs(registry_dir(), exist_ok=True)
+        atomic_write(os.path.join(registry_dir(), PEERS_MARK), json.dumps({"unix": time.time(), "reason": reason[:300]}))
+    except OSError:
+        pass
+
+
 def merge_peer_fallback(result: dict | None, hip: dict | None, reason: str) -> dict | None:
     """The burn-in result with its pulls taken from the HIP probe's re-run. Without an HSA result
     at all, the HIP probe ran the whole validation and IS the result. Each device's ``peers`` are
@@ -372,6 +388,8 @@ class HostBurnin:
         self.log("gpu_burnin_peer_fallback", reason=reason, hip_rc=hrc, ok=bool(hip and hip.get("ok")),
                  seconds=round(time.time() - t0, 3))
         merged = merge_peer_fallback(result, hip, reason)
+        if hip is not None and hip.get("ok"):
+            mark_hsa_peers_failed(reason)  # the next bring-ups here pull through HIP directly
         if merged is not None:
             import json
 

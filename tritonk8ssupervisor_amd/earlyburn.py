@@ -67,12 +67,34 @@ def probe_tool(peers: bool = False) -> str:
     in a fresh child process, and each link records which runtime validated it."""
     hsa = os.path.join(BIN, "tk8s-hsaprobe")
     lib = os.path.join(PKG, "lib")
-    if peers and os.environ.get("TK8S_PEERS_RUNTIME", "hsa") == "hip":
+    if peers and (os.environ.get("TK8S_PEERS_RUNTIME", "hsa") == "hip" or hsa_peers_failed()):
         return os.path.join(BIN, "tk8s-probe")
     if (os.environ.get("TK8S_PROBE_RUNTIME", "hsa") != "hip" and os.access(hsa, os.X_OK)
             and os.path.exists(os.path.join(lib, "tk8s_stream.co")) and os.path.exists(os.path.join(lib, "tk8s_md5.co"))):
         return hsa
     return os.path.join(BIN, "tk8s-probe")
+
+
+PEERS_MARK = "hsa-peers-failed.json"
+PEERS_MARK_TTL_S = 24 * 3600.0
+
+
+def hsa_peers_failed(environ=None) -> bool:
+    """The host burn-in had to fall back from the HSA payload's pulls to the HIP probe within the
+    last day (burnin.HostBurnin records it in the host registry): the next bring-ups on this host
+    pull through the HIP probe directly, so a fabric the HSA path cannot pull costs one bring-up
+    the fallback, not every one. ``TK8S_PEERS_RUNTIME=hsa`` insists on the HSA path."""
+    env = os.environ if environ is None else environ
+    if env.get("TK8S_PEERS_RUNTIME") == "hsa":
+        return False
+    import time
+
+    try:
+        with open(os.path.join(registry_dir(env), PEERS_MARK)) as f:
+            mark = _loads(f.read())
+        return time.time() - float(mark.get("unix", 0)) < PEERS_MARK_TTL_S
+    except (OSError, ValueError, AttributeError, TypeError, StopIteration):
+        return False
 
 
 def default_validation_command(hbm_bytes: int = 1 << 30, md5_bytes: int = 256 << 20, iters: int = 3,
