@@ -563,6 +563,9 @@ def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1)
             if i >= warmup:  # where this point's time went, read before the teardown
                 phases.append(s.get("phases") or {})
                 tasks.append(slowest_tasks(ws / ".tk8s" / "events.jsonl", s.get("launched_unix"), top=12))
+                if getattr(args, "keep_events", None) and (ws / ".tk8s" / "events.jsonl").exists():
+                    Path(args.keep_events).mkdir(parents=True, exist_ok=True)
+                    shutil.copy2(ws / ".tk8s" / "events.jsonl", Path(args.keep_events) / f"curve{n}-{i}.events.jsonl")
             teardown(ws, env, log)
             shutil.rmtree(ws, ignore_errors=True)
             if i >= warmup:

@@ -6,8 +6,8 @@
 # device-to-device memcpy (the control with known bytes).
 #   scripts/r6_kernel_profile.sh OUTDIR
 set -u
-out=$1
 R=${GRAFT_REPO_ROOT:-$PWD}
+out=$(realpath -m "$1")
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 G=$((1 << 30)); M256=$((256 << 20))

@@ -78,6 +78,7 @@ def _healthy_rccl():
 
 
 def test_rccl_stalled_sweep_aborts_within_the_deadline():
+    _healthy_rccl()  # a cold box's first communicator init can itself take longer than 3 s
     rc, out, dt, pid, err = _run([BIN / "tk8s-rccl", "--ngpus", "1", "--max-bytes", 1 << 20, "--iters", 2,
                                   "--warmup", 1, "--op-timeout", 3], faults="rccl.hang@sweep")
     assert rc == 1 and out["ok"] is False and out["phase"] == "sweep", (out, err[-1500:])
