@@ -3,7 +3,9 @@
 //   tk8s-container --rootfs DIR [--upper DIR] [--workdir D] [--hostname H] [--pid-ns]
 //                  [--bind|--bind-ro SRC:DST]... [jail options, gpujail.h] [--no-gpu-jail] -- ARGV...
 //   tk8s-container --exec-in PID [--workdir D] [jail options] -- ARGV...   (kubectl exec)
-//   tk8s-container --probe      {"usable": bool, "how": "root"|"userns", "error": ...}
+//   tk8s-container --probe      {"usable": bool, "how": "root"|"userns"|"ptrace", "error": ...}
+//   --mode auto|namespaces|ptrace (before the others; default auto: namespaces when this user
+//   can make them, else ptrace)
 //
 // The reference's workloads ran in Docker containers (ansible/roles/rancherhost/tasks/main.yml:
 // 26-34, dockersetup/tasks/main.yml:42-46). This is the part of a container runtime a tk8s node
@@ -29,6 +31,14 @@
 //
 // GPU pods keep the host PID namespace (HIP/RCCL IPC identifies peers by pid). Exit status: the
 // command's; 125 = the container could not be set up (message on stderr); 127 = exec failed.
+//
+// Where no mount namespace can be had (not root and user namespaces off: the MI355X GPU tier),
+// the "ptrace" mode gives the pod the same view by path translation (ptrace_root.h): the pod's
+// own tree of hard links to the image with copy-up on write, the host's /dev /proc /sys and the
+// volumes at their paths, the image's own loader and interpreters -- and, since the host's tree
+// is not detached there, the jail's path layers (--deny/--read-only/--allow, the process pods'
+// rules) plus the host's "/" read-only outside the pod's directory. In namespace mode those
+// layers are dropped: inside the container they would name the image's paths, not the host's.
 #include <fcntl.h>
 #include <linux/capability.h>
 #include <linux/openat2.h>
@@ -52,6 +62,7 @@
 #include <vector>
 
 #include "gpujail.h"
+#include "ptrace_root.h"
 
 namespace {
 
@@ -197,7 +208,7 @@ std::string enter(bool pid_ns) {
   return uid == 0 ? "root" : "userns";
 }
 
-int probe() {
+bool namespaces_usable() {
   const pid_t pid = fork();
   if (pid == 0) {
     // quiet: the probe only asks whether the namespaces can be had
@@ -208,10 +219,38 @@ int probe() {
   }
   int st = 0;
   waitpid(pid, &st, 0);
-  const bool ok = WIFEXITED(st) && WEXITSTATUS(st) == 0;
-  std::printf("{\"usable\": %s, \"how\": \"%s\"%s}\n", ok ? "true" : "false", geteuid() == 0 ? "root" : "userns",
-              ok ? "" : ", \"error\": \"no mount namespace for this user (not root, and user namespaces are off)\"");
-  return ok ? 0 : 1;
+  return WIFEXITED(st) && WEXITSTATUS(st) == 0;
+}
+
+std::string json_str(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    if (static_cast<unsigned char>(c) >= 0x20) o += c;
+  }
+  return o + "\"";
+}
+
+// "namespaces" or "ptrace" for --mode auto|namespaces|ptrace; "" when neither can be had (`why`).
+std::string pick_mode(const std::string& mode, std::string* why) {
+  if (mode != "ptrace" && namespaces_usable()) return "namespaces";
+  if (mode == "namespaces") {
+    *why = "no mount namespace for this user (not root, and user namespaces are off)";
+    return "";
+  }
+  const std::string p = tk8s::troot::probe();
+  if (p.empty()) return "ptrace";
+  *why = (mode == "ptrace" ? "" : "no mount namespace for this user, and ") + std::string("no ptrace supervision: ") + p;
+  return "";
+}
+
+int probe(const std::string& mode) {
+  std::string why;
+  const std::string m = pick_mode(mode, &why);
+  const std::string how = m == "ptrace" ? "ptrace" : geteuid() == 0 ? "root" : "userns";
+  std::printf("{\"usable\": %s, \"how\": \"%s\"%s}\n", m.empty() ? "false" : "true", how.c_str(),
+              m.empty() ? (", \"error\": " + json_str(why)).c_str() : "");
+  return m.empty() ? 1 : 0;
 }
 
 // --exec-in PID: run a command inside a running image pod (kubectl exec): its user, mount and
@@ -284,6 +323,136 @@ int exec_in(pid_t pid, const std::string& workdir, const tk8s::jail::Policy& pol
   _exit(127);
 }
 
+struct Bind {
+  std::string src, dst;
+  bool read_only;
+};
+
+// ptrace mode (ptrace_root.h): the pod's own tree, the jail with the host's "/" read-only outside
+// it, the command under a supervisor that translates its paths.
+int run_traced(const std::string& rootfs, const std::string& upper, const std::string& workdir,
+               const std::string& hostname, const std::vector<Bind>& binds, tk8s::jail::Policy policy, bool jail,
+               char** argv) {
+  if (upper.empty()) {
+    errno = EINVAL;
+    die("ptrace mode needs --upper (the pod's own tree)");
+  }
+  tk8s::troot::View view;
+  if (const std::string e = tk8s::troot::make_farm(view, rootfs, upper + "/farm"); !e.empty()) {
+    std::fprintf(stderr, "tk8s-container: %s\n", e.c_str());
+    return 125;
+  }
+  view.hostname = hostname;
+  for (const char* d : {"/dev", "/proc", "/sys"}) view.add_mount(d, d);
+  if (!hostname.empty()) {  // what a UTS namespace would answer there (uname is answered by the supervisor)
+    const std::string hf = upper + "/hostname";
+    const int fd = open(hf.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0 || write(fd, (hostname + "\n").data(), hostname.size() + 1) != static_cast<ssize_t>(hostname.size() + 1))
+      die("write " + hf);
+    close(fd);
+    view.add_mount("/proc/sys/kernel/hostname", hf);
+    view.add_mount("/etc/hostname", hf);
+  }
+  for (const auto& b : binds) {
+    const std::string src = tk8s::jail::real(b.src);
+    if (src.empty()) die("bind source " + b.src);
+    // the mount point resolved inside the image, as in namespace mode (Debian's /var/run -> /run
+    // puts /var/run/secrets/... at /run/secrets/...), and made in the pod's tree so listings show it
+    std::string at = b.dst, h;
+    if (view.resolve(b.dst, true, &h) == 0 && tk8s::troot::under(view.farm, h)) {
+      at = view.to_guest(h);
+      struct stat st {};
+      const bool dir = stat(src.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+      std::string cur = view.farm;
+      const auto parts = tk8s::troot::split_path(at);
+      for (size_t k = 0; k < parts.size(); ++k) {
+        cur += "/" + parts[k];
+        if (k + 1 < parts.size() || dir) {
+          mkdir(cur.c_str(), 0755);
+        } else if (const int fd = open(cur.c_str(), O_WRONLY | O_CREAT | O_NOFOLLOW | O_CLOEXEC, 0644); fd >= 0) {
+          close(fd);
+        }
+      }
+    }
+    view.add_mount(at, src);
+    (b.read_only ? policy.read_only_paths : policy.allow_paths).push_back(src);
+  }
+  // the host's tree stays in view: read-only, but for the pod's own tree and its GPU nodes
+  // (the deny set still takes the other GPUs' render nodes and the node's secrets)
+  policy.read_only_paths.push_back("/");
+  policy.allow_paths.push_back(view.farm);
+  policy.allow_paths.push_back("/dev");
+  std::string host_wd;
+  if (view.resolve(workdir, true, &host_wd) != 0) die("workdir " + workdir);
+  int pfd[2];
+  if (pipe2(pfd, O_CLOEXEC) != 0) die("pipe");
+  const pid_t child = fork();
+  if (child < 0) die("fork");
+  if (child == 0) {
+    close(pfd[1]);
+    prctl(PR_SET_PDEATHSIG, SIGKILL);
+    if (geteuid() == 0) drop_capabilities();
+    std::string mode = "none:--no-gpu-jail";
+    if (jail) {
+      mode = tk8s::jail::apply(policy);
+      if (mode.rfind("none:", 0) == 0) {
+        std::fprintf(stderr, "tk8s-container: GPU jail: %s\n", mode.c_str());
+        _exit(125);
+      }
+    }
+    if (chdir(host_wd.c_str()) != 0) die("chdir " + workdir);
+    setenv("TK8S_GPU_ISOLATION", mode.c_str(), 1);
+    setenv("TK8S_CONTAINER", (std::string("ptrace:") + (geteuid() == 0 ? "root" : "user") + ";rootfs:farm").c_str(), 1);
+    char c;
+    if (read(pfd[0], &c, 1) != 1) _exit(125);  // released once the supervisor traces this process
+    if (const int rc = tk8s::troot::install_filter(); rc != 0) {
+      errno = -rc;
+      die("seccomp filter");
+    }
+    execvp(argv[0], argv);
+    std::fprintf(stderr, "tk8s-container: exec %s: %s\n", argv[0], std::strerror(errno));
+    _exit(127);
+  }
+  close(pfd[0]);
+  for (int s : {SIGTERM, SIGINT, SIGHUP}) signal(s, [](int) {});  // the pod's group gets them
+  tk8s::troot::Tracer tracer(view);
+  const int rc = tracer.run(child, pfd[1]);
+  if (rc < 0) {
+    kill(child, SIGKILL);
+    waitpid(child, nullptr, 0);
+    errno = -rc;
+    die("supervise the container");
+  }
+  return rc;
+}
+
+// A running pod in ptrace mode: its tk8s-container process shares our mount namespace (it made
+// none) and was started with --rootfs. Its settings come from its command line.
+bool traced_pod(pid_t pid, std::string* rootfs, std::string* upper, std::string* hostname, std::vector<Bind>* binds) {
+  struct stat mine {}, theirs {};
+  const std::string proc = "/proc/" + std::to_string(pid);
+  if (stat((proc + "/ns/mnt").c_str(), &theirs) != 0 || stat("/proc/self/ns/mnt", &mine) != 0 ||
+      mine.st_ino != theirs.st_ino)
+    return false;
+  std::ifstream f(proc + "/cmdline", std::ios::binary);
+  std::vector<std::string> args;
+  for (std::string a; std::getline(f, a, '\0');) args.push_back(a);
+  bool found = false;
+  for (size_t k = 1; k + 1 < args.size(); ++k) {
+    const std::string& a = args[k];
+    if (a == "--") break;
+    if (a == "--rootfs") *rootfs = args[++k], found = true;
+    else if (a == "--upper") *upper = args[++k];
+    else if (a == "--hostname") *hostname = args[++k];
+    else if (a == "--bind" || a == "--bind-ro") {
+      const std::string v = args[++k];
+      const auto c = v.find(':');
+      if (c != std::string::npos) binds->push_back({v.substr(0, c), v.substr(c + 1), a == "--bind-ro"});
+    }
+  }
+  return found && !upper->empty();
+}
+
 int usage() {
   std::fprintf(stderr,
                "usage: tk8s-container --rootfs DIR [--upper DIR] [--workdir D] [--hostname H] [--pid-ns]\n"
@@ -296,11 +465,7 @@ int usage() {
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string rootfs, upper, workdir = "/", hostname;
-  struct Bind {
-    std::string src, dst;
-    bool read_only;
-  };
+  std::string rootfs, upper, workdir = "/", hostname, mode = "auto";
   std::vector<Bind> binds;
   bool pid_ns = false, jail = true;
   pid_t exec_pid = 0;
@@ -318,7 +483,12 @@ int main(int argc, char** argv) {
         break;
       }
       if (tk8s::jail::parse_option(policy, argc, argv, i)) continue;
-      if (a == "--probe") return probe();
+      if (a == "--probe") return probe(mode);
+      if (a == "--mode") {
+        mode = next();
+        if (mode != "auto" && mode != "namespaces" && mode != "ptrace") throw std::invalid_argument("--mode auto|namespaces|ptrace");
+        continue;
+      }
       if (a == "--rootfs") rootfs = next();
       else if (a == "--upper") upper = next();
       else if (a == "--workdir") workdir = next();
@@ -344,10 +514,25 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "tk8s-container: %s\n", why.c_str());
     return 125;
   }
-  if (exec_pid > 0 && i < argc) return exec_in(exec_pid, workdir, policy, jail, argv + i);
+  if (exec_pid > 0 && i < argc) {
+    std::string r, u, h;
+    std::vector<Bind> b;
+    if (traced_pod(exec_pid, &r, &u, &h, &b)) return run_traced(r, u, workdir, h, b, policy, jail, argv + i);
+    policy.deny_paths.clear(), policy.read_only_paths.clear(), policy.allow_paths.clear();  // host paths
+    return exec_in(exec_pid, workdir, policy, jail, argv + i);
+  }
   if (rootfs.empty() || i >= argc) return usage();
   rootfs = tk8s::jail::real(rootfs);
   if (rootfs.empty()) die("--rootfs");
+  std::string why;
+  const std::string picked = pick_mode(mode, &why);
+  if (picked.empty()) {
+    std::fprintf(stderr, "tk8s-container: %s\n", why.c_str());
+    return 125;
+  }
+  if (picked == "ptrace") return run_traced(rootfs, upper, workdir, hostname, binds, policy, jail, argv + i);
+  // namespaces: the path layers name host paths, which the container's root does not show
+  policy.deny_paths.clear(), policy.read_only_paths.clear(), policy.allow_paths.clear();
 
   const std::string how = enter(pid_ns);
   if (pid_ns) {  // the command becomes pid 1 of its namespace; this process waits and relays
@@ -396,16 +581,16 @@ int main(int argc, char** argv) {
   if (!hostname.empty() && sethostname(hostname.c_str(), hostname.size()) != 0) die("sethostname");
   pivot_into(root);
   drop_capabilities();
-  std::string mode = "none:--no-gpu-jail";
+  std::string jail_mode = "none:--no-gpu-jail";
   if (jail) {
-    mode = tk8s::jail::apply(policy);  // on the container's own paths (see the header comment)
-    if (mode.rfind("none:", 0) == 0) {
-      std::fprintf(stderr, "tk8s-container: GPU jail: %s\n", mode.c_str());
+    jail_mode = tk8s::jail::apply(policy);  // on the container's own paths (see the header comment)
+    if (jail_mode.rfind("none:", 0) == 0) {
+      std::fprintf(stderr, "tk8s-container: GPU jail: %s\n", jail_mode.c_str());
       return 125;
     }
   }
   if (chdir(workdir.c_str()) != 0) die("chdir " + workdir);
-  setenv("TK8S_GPU_ISOLATION", mode.c_str(), 1);
+  setenv("TK8S_GPU_ISOLATION", jail_mode.c_str(), 1);
   setenv("TK8S_CONTAINER", ("namespaces:" + how + (pid_ns ? "+pid" : "") + ";rootfs:" + fs_mode).c_str(), 1);
   execvp(argv[i], argv + i);
   std::fprintf(stderr, "tk8s-container: exec %s: %s\n", argv[i], std::strerror(errno));

@@ -41,7 +41,7 @@ def _host_files(*binaries: str) -> dict[str, bytes]:
 
 
 def _hello_archive(path: Path) -> str:
-    base = _host_files("sh", "cat", "sleep")
+    base = _host_files("sh", "cat", "sleep", "uname")
     base.update({"etc/hello-release": b"tk8s hello 1\n", "etc/removed": b"gone in layer 1\n", "app/": b""})
     top = {"etc/.wh.removed": b"", "app/run.sh": (
         b"#!/bin/sh\necho greeting=$GREETING\necho cwd=$(pwd)\necho pid=$$\ncat /etc/hello-release\n"
@@ -113,15 +113,32 @@ def _env(ws: Path) -> dict:
     return env
 
 
-def test_a_pod_runs_in_its_image(ws, native_build):
-    """./tk8s image load, then a pod naming the image (no command): it runs the image's entrypoint
-    in the image's root file system, with the image's env and working dir, as pid 1 of its own PID
-    namespace, writes into its own overlay layer, and is GPU-jailed; describe pod says so."""
-    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
+def _probe_mode(mode: str) -> str:
+    """What tk8s-container runs image pods with under --mode ``mode``: root/userns (namespaces),
+    ptrace, or "" (skip: neither is available here)."""
+    from tritonk8ssupervisor_amd.agent.runtime import CONTAINER
 
-    if not container_runtime()[0]:
-        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+    if not CONTAINER.exists():
+        return ""
+    r = subprocess.run([str(CONTAINER), "--mode", mode, "--probe"], capture_output=True, text=True, timeout=20)
+    info = json.loads(r.stdout or "{}")
+    return info.get("how", "") if info.get("usable") else ""
+
+
+@pytest.mark.parametrize("mode", ["auto", "ptrace"])
+def test_a_pod_runs_in_its_image(ws, native_build, mode):
+    """./tk8s image load, then a pod naming the image (no command): it runs the image's entrypoint
+    in the image's root file system, with the image's env and working dir, writes into its own
+    layer (the image stays pristine), and is GPU-jailed; describe pod says so. With namespaces it
+    is pid 1 of its own PID namespace over an overlay; in ptrace mode (the GPU tier: no user
+    namespaces -- native/tools/ptrace_root.h) its root is the pod's own tree of links to the image,
+    by path translation, with the image's own loader."""
+    how = _probe_mode(mode)
+    if not how:
+        pytest.skip(f"no container runtime for --mode {mode} here")
     env = _env(ws)
+    if mode != "auto":
+        env["TK8S_CONTAINER_MODE"] = mode
     ref = _hello_archive(ws / "hello.tar")
     r = subprocess.run(["./tk8s", "image", "load", "hello.tar"], cwd=ws, env=env, capture_output=True, text=True)
     assert r.returncode == 0 and f"Loaded image: {ref}" in r.stdout, r.stderr
@@ -144,25 +161,33 @@ def test_a_pod_runs_in_its_image(ws, native_build):
     log = kc("logs", "hello").stdout
     assert phase == "Succeeded", (phase, log, kc("describe", "pod", "hello").stdout)
     lines = dict(x.split("=", 1) for x in log.split() if "=" in x)
-    assert lines["greeting"] == "hello" and lines["cwd"] == "/app" and lines["pid"] == "1", log
+    assert lines["greeting"] == "hello" and lines["cwd"] == "/app", log
     assert "tk8s hello 1" in log and lines["removed"] == "yes" and lines["args"] == "from-k8s", log
-    assert lines["iso"].startswith("landlock:abi") and "rootfs:overlay" in lines["container"], log
+    assert lines["iso"].startswith("landlock:abi"), log
     # the write went to the pod's own layer, never into the shared image
     store = ImageStore(ws / "images")
     assert not (store.rootfs(ref) / "app" / "out.txt").exists()
     d = kc("describe", "pod", "hello").stdout
-    assert "container: namespaces (root)" in d or "container: namespaces (userns)" in d, d
-    assert "image hello:1" in d and "own PID namespace" in d, d
+    assert "image hello:1" in d, d
+    if how == "ptrace":
+        assert lines["container"].startswith("ptrace:") and "rootfs:farm" in lines["container"], log
+        assert "container: ptrace (path translation" in d and "own PID namespace" not in d, d
+    else:
+        assert lines["pid"] == "1" and "rootfs:overlay" in lines["container"], log
+        assert "container: namespaces (root)" in d or "container: namespaces (userns)" in d, d
+        assert "own PID namespace" in d, d
 
 
-def test_kubectl_exec_enters_the_container(ws, native_build):
-    """kubectl exec into an image pod runs inside its container (its root, its PID namespace, the
-    same GPU jail), not on the host."""
-    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
-
-    if not container_runtime()[0]:
-        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+@pytest.mark.parametrize("mode", ["auto", "ptrace"])
+def test_kubectl_exec_enters_the_container(ws, native_build, mode):
+    """kubectl exec into an image pod runs inside its container (its root, its PID namespace --
+    with namespaces --, the same GPU jail), not on the host."""
+    how = _probe_mode(mode)
+    if not how:
+        pytest.skip(f"no container runtime for --mode {mode} here")
     env = _env(ws)
+    if mode != "auto":
+        env["TK8S_CONTAINER_MODE"] = mode
     _hello_archive(ws / "hello.tar")
     assert subprocess.run(["./tk8s", "image", "load", "hello.tar"], cwd=ws, env=env, capture_output=True).returncode == 0
     r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"], cwd=ws,
@@ -182,19 +207,21 @@ def test_kubectl_exec_enters_the_container(ws, native_build):
     r = kc("exec", "sleeper", "--", "/bin/sh", "-c", "cat /etc/hello-release; echo pid=$$; echo iso=$TK8S_GPU_ISOLATION")
     assert r.returncode == 0, r.stdout + r.stderr
     out = dict(x.split("=", 1) for x in r.stdout.split() if "=" in x)
-    assert "tk8s hello 1" in r.stdout and int(out["pid"]) < 100 and out["iso"].startswith("landlock"), r.stdout
+    assert "tk8s hello 1" in r.stdout and out["iso"].startswith("landlock"), r.stdout
+    assert how == "ptrace" or int(out["pid"]) < 100, r.stdout  # its own PID namespace
     assert kc("exec", "sleeper", "--", "/bin/cat", "/etc/removed").returncode != 0  # the image's view, not the host's
 
 
-def test_image_pod_volumes(ws, native_build):
+@pytest.mark.parametrize("mode", ["auto", "ptrace"])
+def test_image_pod_volumes(ws, native_build, mode):
     """An image pod mounts its volumes where the spec says: a ConfigMap (read-only), a Secret, an
     emptyDir, a PersistentVolumeClaim (data kept for the next pod), the downward API; and gets
-    its own hostname (UTS namespace)."""
-    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
-
-    if not container_runtime()[0]:
-        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+    its own hostname (UTS namespace; in ptrace mode uname's answer and the hostname files)."""
+    if not _probe_mode(mode):
+        pytest.skip(f"no container runtime for --mode {mode} here")
     env = _env(ws)
+    if mode != "auto":
+        env["TK8S_CONTAINER_MODE"] = mode
     _hello_archive(ws / "hello.tar")
     assert subprocess.run(["./tk8s", "image", "load", "hello.tar"], cwd=ws, env=env, capture_output=True).returncode == 0
     r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"], cwd=ws,
@@ -202,7 +229,7 @@ def test_image_pod_volumes(ws, native_build):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
     script = ("cat /etc/app/app.conf; cat /etc/pw/password; echo; cat /info/name; echo; "
-              "echo hostname=$(cat /proc/sys/kernel/hostname); cat /data/count 2>/dev/null || echo count=none; "
+              "echo hostname=$(cat /proc/sys/kernel/hostname); echo uname=$(uname -n); cat /data/count 2>/dev/null || echo count=none; "
               "echo count=again > /data/count; echo x > /scratch/f && echo scratch=ok; "
               "echo y > /etc/app/new 2>/dev/null || echo cfg=readonly")
 
@@ -242,6 +269,7 @@ def test_image_pod_volumes(ws, native_build):
     assert wait("first") == "Succeeded", kc("describe", "pod", "first").stdout
     log = kc("logs", "first").stdout
     assert "greeting=hi" in log and "s3cr3t" in log and "first" in log and "hostname=box" in log, log
+    assert "uname=box" in log, log
     assert "count=none" in log and "scratch=ok" in log and "cfg=readonly" in log, log
     (ws / "second.json").write_text(json.dumps(pod("second")))
     assert kc("apply", "-f", "second.json").returncode == 0
@@ -281,15 +309,17 @@ def test_hardlink_to_a_symlinked_host_file_is_refused(tmp_path):
     assert (root / "g").read_bytes() == b"ok" and os.stat(root / "f").st_nlink == 2
 
 
-def test_mount_points_resolve_inside_the_image(ws, native_build):
+@pytest.mark.parametrize("mode", ["auto", "ptrace"])
+def test_mount_points_resolve_inside_the_image(ws, native_build, mode):
     """Debian/Ubuntu images ship /var/run -> /run. A volume (and the ServiceAccount
     token every image pod gets at /var/run/secrets/kubernetes.io/serviceaccount) mounted under it
     lands in the image's /run, resolved inside the image -- never on the host's /run."""
-    from tritonk8ssupervisor_amd.agent.runtime import container_runtime
-
-    if not container_runtime()[0]:
-        pytest.skip(f"no container runtime here: {container_runtime()[1]}")
+    how = _probe_mode(mode)
+    if not how:
+        pytest.skip(f"no container runtime for --mode {mode} here")
     env = _env(ws)
+    if mode != "auto":
+        env["TK8S_CONTAINER_MODE"] = mode
     base = _host_files("sh", "cat", "sleep", "ls")
     base.update({"var/": b"", "var/run": ("symlink", "/run"), "etc/os-release": b"debian-like\n"})
     write_docker_archive(ws / "deb.tar", "deb:1", [base], {"Env": ["PATH=/bin"], "WorkingDir": "/"})

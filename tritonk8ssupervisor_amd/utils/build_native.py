@@ -212,7 +212,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     jail_hdr = NATIVE / "tools" / "gpujail.h"
     for tname, tsrc in (("tk8s-gpujail", "tk8s_gpujail.cpp"), ("tk8s-container", "tk8s_container.cpp")):
         src = NATIVE / "tools" / tsrc
-        if force or _stale(tool_path(tname), [src, jail_hdr, Path(__file__)]):
+        if force or _stale(tool_path(tname), [src, jail_hdr, NATIVE / "tools" / "ptrace_root.h", Path(__file__)]):
             _run([CXX, "-O2", "-std=c++17", "-Wall", "-Wextra", *static, str(src), "-o", str(tool_path(tname))],
                  verbose)
     jail = tool_path("tk8s-gpujail")
