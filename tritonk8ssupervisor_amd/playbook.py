@@ -309,7 +309,7 @@ class Playbook:
                 for h in hosts[1:]:
                     if task.get("register"):
                         self.hostvars[h.name][task["register"]] = res[0].result
-        elif len(hosts) == 1 or self._inline(task):
+        elif len(hosts) == 1 or self._inline(task, hosts):
             res = [self._run_on_host(task, h, play_vars) for h in hosts]
         else:
             start = len(self.trace)
@@ -400,22 +400,35 @@ class Playbook:
     _INLINE_MODULES = frozenset({"set_fact", "debug", "stat", "file", "copy", "lineinfile", "slurp", "assert",
                                  "fail", "tk8s_gpu_facts"})
 
-    def _inline(self, task: dict) -> bool:
+    def _inline(self, task: dict, hosts: list[Host] = ()) -> bool:
         """Run this task's hosts one after another in this thread (local machines, a module of
         _INLINE_MODULES, no retries/loops/delegation). ``TK8S_PLAY_INLINE=0``: always a thread
-        per host."""
+        per host. ``tk8s_daemon`` too when it only reads pidfiles: a query, or a start of a daemon
+        that already runs on every host (the standby agent its machine's boot hook started) --
+        8 threads for 8 pidfile reads cost ~1 ms per host in interpreter-lock hand-offs."""
         ex = self.executor
         if ex is None or getattr(ex, "remote", True) or os.environ.get("TK8S_PLAY_INLINE", "1") == "0":
             return False
         if task.get("delegate_to") or "until" in task or task.get("with_items", task.get("loop")) is not None:
             return False
         try:
-            mod = self._module_of(task)[0]
+            mod, raw, _ = self._module_of(task)
         except PlaybookError:
             return False
         from .playbook_modules import module_name
 
-        return module_name(mod) in self._INLINE_MODULES
+        name = module_name(mod)
+        if name == "tk8s_daemon" and isinstance(raw, dict):
+            state, dname = raw.get("state", "started"), raw.get("name")
+            if state == "query":
+                return True
+            if state == "started" and isinstance(dname, str) and "{" not in dname and hosts:
+                try:
+                    return all(ex.daemon_status(h.name, dname).get("running") for h in hosts)
+                except Exception:  # noqa: BLE001 - undecided: the threads decide
+                    return False
+            return False
+        return name in self._INLINE_MODULES
 
     def _executor(self) -> Pool:
         """One pool for the whole run (``forks`` workers; 0 = every host): starting fresh threads
