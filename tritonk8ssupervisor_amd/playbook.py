@@ -313,7 +313,21 @@ class Playbook:
             res = [self._run_on_host(task, h, play_vars) for h in hosts]
         else:
             start = len(self.trace)
-            res = list(self._executor().map(lambda h: self._run_on_host(task, h, play_vars), hosts))
+            # `when:` first, here: a host it skips needs no thread, and when it leaves one host
+            # (or only hosts whose work is a pidfile read) that runs inline too
+            done: dict[str, TaskResult] = {}
+            if "when" in task:
+                for h in hosts:
+                    r = self._when(task, h, play_vars)
+                    if r is not None:
+                        done[h.name] = r
+            todo = [h for h in hosts if h.name not in done]
+            if len(todo) <= 1 or (done and self._inline(task, todo)):
+                ran = [self._run_on_host(task, h, play_vars, when_checked=True) for h in todo]
+            else:
+                ran = list(self._executor().map(lambda h: self._run_on_host(task, h, play_vars, when_checked=True), todo))
+            by_host = {**done, **{r.host: r for r in ran}}
+            res = [by_host[h.name] for h in hosts]
             # hosts ran in parallel: the trace of this task in host order (each host's own
             # entries keep their order), so --check plans read the same on every run
             order = {h.name: i for i, h in enumerate(hosts)}
@@ -324,17 +338,28 @@ class Playbook:
                          results={r.host: r.status for r in res}, **({"timing_ms": timing} if timing else {}))
         return res
 
-    def _run_on_host(self, task: dict, host: Host, play_vars: dict) -> TaskResult:
-        t0 = time.monotonic()
-        v = self.host_vars(host, {**play_vars, **(task.get("vars") or {})})
+    def _when(self, task: dict, host: Host, play_vars: dict, v: dict | None = None) -> TaskResult | None:
+        """The recorded result of a host that the task's ``when:`` skips (or fails on), else None."""
+        if "when" not in task:
+            return None
+        if v is None:
+            v = self.host_vars(host, {**play_vars, **(task.get("vars") or {})})
         try:
-            if "when" in task and not templating.test(task["when"], v):
-                r = TaskResult(host.name, "skipped", {"skipped": True, "changed": False})
-                return self._record(task, host, r)
+            if not templating.test(task["when"], v):
+                return self._record(task, host, TaskResult(host.name, "skipped", {"skipped": True, "changed": False}))
         except Undefined as e:
             if self.check:
                 return self._record(task, host, TaskResult(host.name, "skipped", {"skipped": True, "msg": f"check mode: {e}"}))
             return self._record(task, host, TaskResult(host.name, "failed", {"failed": True, "msg": f"when: {e}"}))
+        return None
+
+    def _run_on_host(self, task: dict, host: Host, play_vars: dict, when_checked: bool = False) -> TaskResult:
+        t0 = time.monotonic()
+        v = self.host_vars(host, {**play_vars, **(task.get("vars") or {})})
+        if not when_checked:
+            r = self._when(task, host, play_vars, v)
+            if r is not None:
+                return r
         mod, raw, local = self._module_of(task)
         if task.get("delegate_to"):
             target = templating.render(task["delegate_to"], v)
