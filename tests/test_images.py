@@ -356,3 +356,69 @@ def test_mount_points_resolve_inside_the_image(ws, native_build, mode):
     if os.geteuid() == 0:
         assert "capbnd=00000000a80425fb" in out, out
     assert os.path.exists("/run/tk8s-test-data") == host_before  # nothing appeared on the host
+
+
+@pytest.mark.gpu
+def test_gpu_image_pod_runs_hip_in_its_image(tmp_path, native_build):
+    """A GPU pod from an image: the image holds tk8s-gpuinfo, libtk8s and the C/C++ runtime; the
+    node's ROCm comes in as a read-only hostPath volume (as a GPU container gets it). On the
+    MI355X box (no namespaces) it runs in ptrace mode: HIP's device discovery -- /dev/kfd, its
+    render node, the KFD topology in /sys, all through the path translation; the GPU ioctls
+    themselves never stop -- finds the pod's one MI355X, and the jail keeps it to that one."""
+    import shutil
+
+    import torch
+
+    from tritonk8ssupervisor_amd.orchestrator import init_workspace
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    how = _probe_mode("auto")
+    if not how:
+        pytest.skip("no container runtime here")
+    init_workspace(tmp_path)
+    for f in ("setup.sh", "tk8s", "kubectl"):
+        shutil.copy2(REPO / f, tmp_path / f)
+    env = {k: v for k, v in os.environ.items() if k != "TK8S_FAKE_GPUS"}
+    env.update(PYTHONPATH=str(REPO), TK8S_PYTHON=sys.executable, TK8S_IMAGE_STORE=str(tmp_path / "images"))
+    gi = REPO / "tritonk8ssupervisor_amd" / "bin" / "tk8s-gpuinfo"
+    files = {k: v for k, v in _host_files("sh", "cat").items()}
+    files["opt/tk8s/bin/tk8s-gpuinfo"] = gi.read_bytes()
+    files["opt/tk8s/lib/libtk8s.so"] = (REPO / "tritonk8ssupervisor_amd" / "lib" / "libtk8s.so").read_bytes()
+    for tok in subprocess.run(["ldd", str(gi)], capture_output=True, text=True).stdout.split():
+        if tok.startswith("/") and not tok.startswith("/opt/rocm") and "tritonk8ssupervisor_amd" not in tok \
+                and Path(tok).exists():
+            files[tok.lstrip("/")] = Path(tok).resolve().read_bytes()
+    write_docker_archive(tmp_path / "gpu.tar", "gpuinfo:1", [files], {"Env": ["PATH=/bin"], "WorkingDir": "/"})
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=tmp_path, env=env, capture_output=True, text=True,
+                                   timeout=60)
+    try:
+        assert subprocess.run(["./tk8s", "image", "load", "gpu.tar"], cwd=tmp_path, env=env,
+                              capture_output=True).returncode == 0
+        r = subprocess.run(["./setup.sh", "--nodes", "1", "--yes", "--json", "--port", "0", "--timeout", "120",
+                            "--rccl", "off"], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        (tmp_path / "pod.json").write_text(json.dumps({
+            "apiVersion": "v1", "kind": "Pod", "metadata": {"name": "gpuinfo"},
+            "spec": {"restartPolicy": "Never", "containers": [{
+                "name": "c", "image": "gpuinfo:1", "command": ["/opt/tk8s/bin/tk8s-gpuinfo", "--no-links"],
+                "env": [{"name": "LD_LIBRARY_PATH", "value": "/opt/tk8s/lib:/opt/rocm/lib"}],
+                "resources": {"limits": {"amd.com/gpu": 1}},
+                "volumeMounts": [{"name": "rocm", "mountPath": "/opt/rocm", "readOnly": True}]}],
+                "volumes": [{"name": "rocm", "hostPath": {"path": os.path.realpath("/opt/rocm")}}]}}))
+        assert kc("apply", "-f", "pod.json").returncode == 0
+        deadline = time.monotonic() + 120
+        phase = None
+        while time.monotonic() < deadline:
+            phase = json.loads(kc("get", "pod", "gpuinfo", "-o", "json").stdout)["status"].get("phase")
+            if phase in ("Succeeded", "Failed"):
+                break
+            time.sleep(0.3)
+        log = kc("logs", "gpuinfo").stdout
+        assert phase == "Succeeded", (phase, log[-2000:], kc("describe", "pod", "gpuinfo").stdout[-3000:])
+        info = json.loads(log.strip().splitlines()[-1])
+        assert info["ok"] and len(info["devices"]) == 1 and info["devices"][0]["gfx"] == "gfx950", info
+        d = kc("describe", "pod", "gpuinfo").stdout
+        assert "image gpuinfo:1" in d and ("container: ptrace" in d or "container: namespaces" in d), d
+    finally:
+        subprocess.run(["./setup.sh", "-c", "--yes"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
