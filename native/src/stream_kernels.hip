@@ -218,18 +218,23 @@ void philox_fill(void* dst, size_t nbytes, uint64_t seed, hipStream_t stream) {
 // ------------------------------------------------------------------------------------------
 // N7: copy (local D2D, or peer pull when src is another GPU's memory with peer access enabled)
 // ------------------------------------------------------------------------------------------
+// 8 loads in flight per lane, then 8 stores, non-temporal both ways, 16 blocks per CU: the best
+// of a 20-shape sweep on the MI355X (profiles/r6_copy/: 381.5 us for 1 GiB -> 1 GiB, 5.63 TB/s
+// read + write, against 387.5 us for the former 4-deep x 32 and 456.5 us for hipMemcpyAsync's
+// copy kernel in the same process; the fill's single-write-front shape loses here, 5.3 TB/s).
+constexpr int kCopyDepth = 8;
 __global__ __launch_bounds__(kBlock) void stream_copy_kernel(u32x4* __restrict__ dst,
                                                              const u32x4* __restrict__ src,
                                                              size_t n16) {
   size_t lo, hi;
   slab_bounds(n16, &lo, &hi);
   size_t i = lo + threadIdx.x;
-  for (; i + 3 * kBlock < hi; i += 4 * kBlock) {
-    u32x4 v[4];
+  for (; i + (kCopyDepth - 1) * kBlock < hi; i += kCopyDepth * kBlock) {
+    u32x4 v[kCopyDepth];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(src + i + u * kBlock);
+    for (int u = 0; u < kCopyDepth; ++u) v[u] = __builtin_nontemporal_load(src + i + u * kBlock);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], dst + i + u * kBlock);
+    for (int u = 0; u < kCopyDepth; ++u) __builtin_nontemporal_store(v[u], dst + i + u * kBlock);
   }
   for (; i < hi; i += kBlock) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
@@ -238,7 +243,7 @@ void stream_copy(void* dst, const void* src, size_t nbytes, hipStream_t stream) 
   if (nbytes % 16) throw std::invalid_argument("stream_copy: nbytes must be a multiple of 16");
   const size_t n16 = nbytes / 16;
   if (!n16) return;
-  hipLaunchKernelGGL(stream_copy_kernel, dim3(grid_for(n16 / 4, 32)), dim3(kBlock), 0, stream,
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(grid_for(n16 / kCopyDepth, 16)), dim3(kBlock), 0, stream,
                      static_cast<u32x4*>(dst), static_cast<const u32x4*>(src), n16);
   TK8S_HIP_CHECK(hipGetLastError());
 }

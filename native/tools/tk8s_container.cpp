@@ -415,7 +415,9 @@ int run_traced(const std::string& rootfs, const std::string& upper, const std::s
   }
   close(pfd[0]);
   for (int s : {SIGTERM, SIGINT, SIGHUP}) signal(s, [](int) {});  // the pod's group gets them
-  tk8s::troot::Tracer tracer(view);
+  FILE* log = nullptr;
+  if (const char* lp = getenv("TK8S_PTRACE_LOG"); lp != nullptr && *lp) log = std::fopen(lp, "a");
+  tk8s::troot::Tracer tracer(view, log);
   const int rc = tracer.run(child, pfd[1]);
   if (rc < 0) {
     kill(child, SIGKILL);

@@ -611,7 +611,7 @@ class Device {
   }
   size_t copy(void* dst, const void* src, size_t bytes, bool to_host = false, bool from_remote = false) {
     const size_t n16 = bytes / 16;
-    return launch(ks_.copy, grid_for(n16 / 4, 32), kBlock,
+    return launch(ks_.copy, grid_for(n16 / 8, 16), kBlock,  // stream_kernels.hip: kCopyDepth 8, 16 blocks/CU
                   [&](KernArgs& a) { a.ptr(dst).ptr(src).u64(n16); }, to_host, from_remote);
   }
   // md5_kernels.hip md5_tree: level by level until one digest; returns (first, last) dispatch.
