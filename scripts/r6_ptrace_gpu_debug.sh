@@ -9,7 +9,7 @@ mkdir -p $img/opt/tk8s/bin $img/opt/tk8s/lib $img/opt/rocm $img/bin
 cp $R/tritonk8ssupervisor_amd/bin/tk8s-gpuinfo $img/opt/tk8s/bin/
 cp $R/tritonk8ssupervisor_amd/lib/libtk8s.so $img/opt/tk8s/lib/
 for b in /bin/sh; do cp -L $b $img/bin/; done
-for l in $( (ldd $R/tritonk8ssupervisor_amd/bin/tk8s-gpuinfo; ldd /bin/sh) | awk '{for(i=1;i<=NF;i++) if ($i ~ /^\/(lib|usr)/) print $i}' | sort -u); do
+for l in $( (ldd $R/tritonk8ssupervisor_amd/bin/tk8s-gpuinfo; ldd /bin/sh; ldd /opt/rocm/lib/libamd_comgr.so.3) | awk '{for(i=1;i<=NF;i++) if ($i ~ /^\/(lib|usr)/) print $i}' | sort -u); do
   mkdir -p $img$(dirname $l); cp -L $l $img$l; done
 ROCM=$(realpath /opt/rocm)
 run() { timeout -k 5 60 "$@"; }

@@ -385,10 +385,16 @@ def test_gpu_image_pod_runs_hip_in_its_image(tmp_path, native_build):
     files = {k: v for k, v in _host_files("sh", "cat").items()}
     files["opt/tk8s/bin/tk8s-gpuinfo"] = gi.read_bytes()
     files["opt/tk8s/lib/libtk8s.so"] = (REPO / "tritonk8ssupervisor_amd" / "lib" / "libtk8s.so").read_bytes()
-    for tok in subprocess.run(["ldd", str(gi)], capture_output=True, text=True).stdout.split():
-        if tok.startswith("/") and not tok.startswith("/opt/rocm") and "tritonk8ssupervisor_amd" not in tok \
-                and Path(tok).exists():
-            files[tok.lstrip("/")] = Path(tok).resolve().read_bytes()
+    # the C/C++ runtime of the tool and of what HIP loads on its own (comgr: libzstd, libz, ...);
+    # ROCm itself stays on the node
+    rocm_lib = Path(os.path.realpath("/opt/rocm")) / "lib"
+    for so in (gi, rocm_lib / "libamd_comgr.so.3", rocm_lib / "libhsa-runtime64.so.1", rocm_lib / "libamdhip64.so.7"):
+        if not so.exists():
+            continue
+        for tok in subprocess.run(["ldd", str(so)], capture_output=True, text=True).stdout.split():
+            if tok.startswith("/") and not tok.startswith("/opt/") and "tritonk8ssupervisor_amd" not in tok \
+                    and Path(tok).exists():
+                files[tok.lstrip("/")] = Path(tok).resolve().read_bytes()
     write_docker_archive(tmp_path / "gpu.tar", "gpuinfo:1", [files], {"Env": ["PATH=/bin"], "WorkingDir": "/"})
     kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=tmp_path, env=env, capture_output=True, text=True,
                                    timeout=60)
