@@ -295,7 +295,7 @@ inline int build_tree(View& view, int src, int dst, bool make) {
 // The pod's tree at `farm` from image `rootfs` (made once; a restarted container keeps its
 // writes, as with an overlay's upper layer), plus the directories the host trees are seen at.
 inline std::string make_farm(View& view, const std::string& rootfs, const std::string& farm) {
-  const std::string done = farm + "/.tk8s-farm-complete";
+  const std::string done = farm + ".complete";  // beside the tree: the guest's "/" lists only the image's entries
   const bool exists = access(done.c_str(), F_OK) == 0;
   if (!exists) {
     std::string cur;

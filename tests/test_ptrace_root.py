@@ -64,7 +64,7 @@ def test_symlinks_resolve_inside_the_image(image, tmp_path):
     assert r.stdout.count("tk8s hello 1") == 3, r.stdout
     listing = r.stdout.split()
     assert "app" in listing and "abs" in listing and "dev" in listing and "proc" in listing, r.stdout
-    assert ".tk8s-farm-complete" in os.listdir(tmp_path / "up" / "farm")
+    assert (tmp_path / "up" / "farm.complete").exists() and "farm.complete" not in listing
 
 
 def test_writes_copy_up_and_the_image_stays_pristine(image, tmp_path):
