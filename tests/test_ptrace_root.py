@@ -124,10 +124,16 @@ def test_exit_status_and_stop_continue(image, tmp_path):
 
 
 def test_children_and_a_missing_program(image, tmp_path):
+    """Background children; a missing program is 127; a program without its execute bit is
+    refused (126) although the supervisor would start it through the image's loader."""
+    (image / "app" / "plain").write_bytes((image / "bin" / "cat").read_bytes())
+    (image / "app" / "plain").chmod(0o644)
     r = _run(image, tmp_path / "up", "(cat /abs/hello-release) & (sleep 0.1; echo child) & wait\n"
-                                     "/bin/nothere 2>/dev/null; echo rc=$?\n", "--no-gpu-jail")
+                                     "/bin/nothere 2>/dev/null; echo rc=$?\n"
+                                     "/app/plain /etc/hello-release 2>/dev/null; echo rc2=$?\n", "--no-gpu-jail")
     assert r.returncode == 0, r.stderr
     assert "tk8s hello 1" in r.stdout and "child" in r.stdout and "rc=127" in r.stdout, r.stdout
+    assert "rc2=126" in r.stdout, r.stdout
 
 
 THREADS_C = r"""
