@@ -56,10 +56,19 @@ def one(root: Path, nodes: int, package: str = "mi355x-1gpu", rccl: str = "off")
             if line.startswith("TRACE "):
                 _, ts, where, what = (line.split(" ", 3) + [""])[:4]
                 out.append(((float(ts) - t0) * 1000, where, what))
+    for log in (root / ".tk8s").rglob("pods/kube-system_rccl-allreduce-*/log"):  # the ranks' own reports
+        for line in log.read_text(errors="replace").splitlines():
+            if line.startswith("{"):
+                try:
+                    r = json.loads(line)
+                except ValueError:
+                    continue
+                keep = {k: v for k, v in r.items() if not isinstance(v, (list, dict))}
+                out.append((float("inf"), "rank", json.dumps(keep)))
     subprocess.run(["./setup.sh", "-c", "--yes"], cwd=root, env=env, capture_output=True, timeout=120)
     if p.returncode != 0:
         raise SystemExit(f"setup failed ({p.returncode}):\n{p.stdout[-2000:]}\n{p.stderr[-2000:]}")
-    return sorted((x for x in out if x[0] == x[0]), key=lambda x: x[0])
+    return sorted((x for x in out if x[0] == x[0]), key=lambda x: x[0])  # (reports last: ms = inf)
 
 
 def main() -> int:
@@ -70,6 +79,9 @@ def main() -> int:
     ap.add_argument("--rccl", default="off", help="on: also time the post-Ready RCCL fabric Job")
     ap.add_argument("--out")
     a = ap.parse_args()
+    from tritonk8ssupervisor_amd.utils.build_native import build
+
+    build()  # as bench.py does: incremental, and it makes the host's unpacked RCCL (fabric Job ranks)
     runs = []
     for i in range(a.runs):
         root = Path(tempfile.mkdtemp(prefix="tk8s-trace-"))
@@ -77,7 +89,7 @@ def main() -> int:
             tl = one(root, a.nodes, a.package, a.rccl)
         finally:
             shutil.rmtree(root, ignore_errors=True)
-        runs.append([{"ms": round(t, 2), "where": w, "what": x} for t, w, x in tl])
+        runs.append([{"ms": round(t, 2) if t != float("inf") else None, "where": w, "what": x} for t, w, x in tl])
         print(f"--- run {i}", flush=True)
         for t, w, x in tl:
             print(f"{t:8.2f} {w:10s} {x}", flush=True)
