@@ -12,7 +12,7 @@ for b in /bin/sh; do cp -L $b $img/bin/; done
 for l in $( (ldd $R/tritonk8ssupervisor_amd/bin/tk8s-gpuinfo; ldd /bin/sh; ldd /opt/rocm/lib/libamd_comgr.so.3) | awk '{for(i=1;i<=NF;i++) if ($i ~ /^\/(lib|usr)/) print $i}' | sort -u); do
   mkdir -p $img$(dirname $l); cp -L $l $img$l; done
 ROCM=$(realpath /opt/rocm)
-run() { timeout -k 5 60 "$@"; }
+run() { sleep 1; timeout -k 5 60 "$@"; }  # 1 s apart: a GPU process's KFD release takes 0.1-0.2 s
 run $R/tritonk8ssupervisor_amd/bin/tk8s-gpuinfo --no-links > $out/host.json 2> $out/host.err; echo "host rc=$?" > $out/status
 minor=$(ls /dev/dri | grep -o 'renderD[0-9]*' | head -1 | tr -dc 0-9)
 TK8S_PTRACE_LOG=$out/nojail.log run $R/tritonk8ssupervisor_amd/bin/tk8s-container --mode ptrace --rootfs $img \
