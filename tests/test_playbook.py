@@ -305,3 +305,38 @@ def test_cheap_tasks_on_local_machines_run_inline(tmp_path, monkeypatch):
     monkeypatch.delenv("TK8S_PLAY_INLINE")
     pb.executor = Remote()
     assert not pb._inline({"set_fact": {"a": 1}})
+
+
+def test_pidfile_only_daemon_tasks_and_when_run_in_the_engine_thread(tmp_path, monkeypatch):
+    """tk8s_daemon reads only pidfiles for a query, or for a start of a daemon already running
+    on every host the task applies to: inline. `when:` is evaluated before any host goes to a
+    thread, so a task that skips one host (the master) does not send the others to threads."""
+    import threading
+
+    class Local:
+        remote = False
+
+        def __init__(self):
+            self.calls = []
+
+        def daemon_status(self, host, name):
+            self.calls.append((host, threading.get_ident()))
+            return {"running": host != "m1", "pid": 1}
+
+    pb, res, _ = _play(tmp_path, [{"hosts": "all", "gather_facts": False, "tasks": []}])
+    ex = Local()
+    pb.executor = ex
+    assert pb._inline({"tk8s_daemon": {"name": "agent", "state": "query"}})
+    hosts = [pb.hosts[h] for h in ("h1", "h2")]
+    assert pb._inline({"tk8s_daemon": {"name": "agent", "argv": ["x"]}}, hosts)  # running on both
+    assert not pb._inline({"tk8s_daemon": {"name": "agent", "argv": ["x"]}}, [pb.hosts["m1"], *hosts])
+    assert not pb._inline({"tk8s_daemon": {"name": "{{ n }}", "argv": ["x"]}}, hosts)  # templated: undecided
+    # a run: `when:` skips the master in the engine's thread; the two hosts left run inline
+    ran = []
+    monkeypatch.setattr(pb, "_exec", lambda task, mod, raw, v, host, deleg, local: (
+        ran.append((host.name, threading.get_ident())) or {"changed": False}))
+    task = {"name": "standby", "tk8s_daemon": {"name": "agent", "argv": ["x"]},
+            "when": "inventory_hostname != 'm1'"}
+    res = pb.run_task(task, [pb.hosts[h] for h in ("m1", "h1", "h2")], {})
+    assert [r.status for r in res] == ["skipped", "ok", "ok"]
+    assert sorted(h for h, _ in ran) == ["h1", "h2"] and {t for _, t in ran} == {threading.get_ident()}
