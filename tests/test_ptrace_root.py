@@ -203,3 +203,29 @@ def test_threads_and_spawn_under_the_supervisor(image, tmp_path):
     r = _run(image, tmp_path / "up", "/bin/threads\n", "--no-gpu-jail", timeout=120)
     assert r.returncode == 0, (r.stdout, r.stderr)
     assert "bad=0 spawned=8" in r.stdout, r.stdout
+
+
+def test_a_duty_cycle_of_stops_never_strands_a_traced_pod(image, tmp_path):
+    """The agent's unprivileged CPU limit stops and resumes a pod's process group many times a
+    second. A traced pod's stop signals pass through the supervisor (itself stopped with the
+    group); however the SIGSTOPs and SIGCONTs interleave, the pod ends up running and finishes."""
+    import random
+
+    (image / "app" / "t.sh").write_text("#!/bin/sh\ni=0; while [ $i -lt 100000 ]; do i=$((i+1)); done\n"
+                                        "cat /etc/hello-release\n")
+    (image / "app" / "t.sh").chmod(0o755)
+    p = subprocess.Popen([str(TOOL), "--mode", "ptrace", "--rootfs", str(image), "--upper", str(tmp_path / "up"),
+                          "--workdir", "/app", "--no-gpu-jail", "--", "/app/t.sh"], start_new_session=True,
+                         stdout=subprocess.PIPE, text=True, env={"PATH": "/bin"})
+    rnd = random.Random(7)
+    for _ in range(30):
+        os.killpg(p.pid, signal.SIGSTOP)
+        time.sleep(rnd.uniform(0.001, 0.02))
+        os.killpg(p.pid, signal.SIGCONT)
+        time.sleep(rnd.uniform(0.001, 0.02))
+    try:
+        out, _ = p.communicate(timeout=60)
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+    assert p.returncode == 0 and "tk8s hello 1" in out, out
