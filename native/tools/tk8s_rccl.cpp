@@ -19,6 +19,8 @@
 // if a phase makes no progress for op-timeout + 10 s at all -- a call blocked inside RCCL.
 // Fault points (TK8S_FAULTS): rccl.hang@uid|init (host stops), rccl.hang@sweep|check (the GPU
 // queue stalls), rccl.exit@<phase> (exit 3), rccl.crash@<phase> (abort).
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -118,6 +120,39 @@ std::string stall_phase() {
   return "";
 }
 
+// RCCL's device code is one 108 MB code object (the host's unpacked copy, utils/rccl_unpack.py);
+// HIP loads it onto a device the first time one of its kernels is referenced there -- inside
+// the communicator start, ~160 ms of its ~205 ms on the MI355X (profiles/r5_thp/). Referencing
+// a kernel of it right after the runtime's start, on a thread per device, lets that load overlap
+// the unique id's creation (~26 ms) or its wait (the other ranks). TK8S_RCCL_PREWARM=0: off.
+struct Prewarm {
+  std::vector<std::thread> threads;
+  std::chrono::steady_clock::time_point t0;
+  bool started = false;
+};
+
+Prewarm prewarm_rccl_code(const std::vector<int>& devices) {
+  Prewarm p;
+  const char* off = std::getenv("TK8S_RCCL_PREWARM");
+  if (off != nullptr && std::string(off) == "0") return p;
+  const void* sym = nullptr;
+  for (const char* name : {"_Z23ncclDevKernel_Generic_124ncclDevKernelArgsStorageILm4096EE",
+                           "_Z23ncclDevKernel_Generic_224ncclDevKernelArgsStorageILm4096EE"}) {
+    if ((sym = dlsym(RTLD_DEFAULT, name)) != nullptr) break;
+  }
+  if (sym == nullptr) return p;  // another RCCL's names: its start loads the code as before
+  p.t0 = std::chrono::steady_clock::now();
+  p.started = true;
+  for (int d : devices) {
+    p.threads.emplace_back([d, sym] {
+      if (hipSetDevice(d) != hipSuccess) return;
+      hipFuncAttributes attr;
+      (void)hipFuncGetAttributes(&attr, sym);
+    });
+  }
+  return p;
+}
+
 // What the process is doing, for the watchdog's error line.
 std::atomic<int> g_nranks{1}, g_first{0}, g_local{1};
 
@@ -198,6 +233,7 @@ int main(int argc, char** argv) {
         (void)hipGetDeviceCount(&n);
         trace("hip runtime up");
       }
+      Prewarm warm = prewarm_rccl_code(devices);
       // the uid exchange is bounded by the same budget as every other wait
       const double uid_timeout = std::strtod(a.str("uid-timeout", a.str("op-timeout", "20")).c_str(), nullptr);
       if (bounded) dog.arm("uid", uid_timeout + grace);
@@ -229,10 +265,20 @@ int main(int argc, char** argv) {
         }
       }
       trace(first == 0 ? "unique id published" : "unique id fetched");
-      if (bounded) dog.arm("init", cfg.op_timeout_s + grace);
+      if (bounded) dog.arm("init", cfg.op_timeout_s + grace);  // (the code load below included)
+      for (auto& th : warm.threads) th.join();
+      const double prewarm_ms =
+          warm.started ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - warm.t0).count() : -1;
+      if (warm.started) trace("rccl code loaded");
       tk8s::fault_point("rccl", "init");
       cfg.stall_phase = stall_phase();
       out = tk8s::allreduce_rank_group(first, nranks, devices, id, cfg);
+      if (warm.started && !out.empty() && out.back() == '}') {  // how long the code load still took past the uid
+        char buf[64];
+        std::snprintf(buf, sizeof(buf), ",\"rccl_code_prewarm_ms\":%.3f}", prewarm_ms);
+        out.pop_back();
+        out += buf;
+      }
       trace("sweep done");
     } else {
       int n = 0;
