@@ -976,3 +976,77 @@ def test_stock_kubectl_exec_with_a_tty_is_interactive(ws, tmp_path_factory):
     r = subprocess.run(["./kubectl", "exec", "-it", "tty", "--", "sh"], cwd=ws, env=_env(), capture_output=True,
                        input="echo hi-$((2+3)); exit 3\n", text=True, timeout=60)
     assert r.returncode == 3 and "hi-5" in r.stdout, (r.returncode, r.stdout, r.stderr)
+
+
+def test_attach_to_a_pods_stdin_and_tty_and_kubectl_run_it(ws, tmp_path_factory):
+    """`kubectl attach -it` and `kubectl run -it --rm`: a container started with `stdin: true` /
+    `tty: true` keeps its input open (a pipe, or a pty whose output the agent pumps to the log
+    and to attached sessions). A session sees the resize and the typed input while the container
+    runs; a client that detaches leaves it running; its exit status ends the last session."""
+    from urllib.parse import urlsplit
+
+    from tritonk8ssupervisor_amd.controlplane.wsclient import WSClient, WSClosed
+
+    _summary(_setup(ws, "--nodes", "1", "--rccl", "off"))
+    d = tmp_path_factory.mktemp("wsat")
+    kc = lambda *a, **kw: subprocess.run(["./kubectl", *a], cwd=ws, env=_env(), capture_output=True, text=True,
+                                         timeout=60, **kw)
+
+    def pod(name, c):
+        (d / f"{name}.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": name},
+                                                    "spec": {"restartPolicy": "Never",
+                                                             "containers": [{"name": "c", **c}]}}))
+        assert kc("apply", "-f", str(d / f"{name}.json")).returncode == 0
+        deadline = time.monotonic() + 30
+        while time.monotonic() < deadline and json.loads(kc("get", "pod", name, "-o", "json").stdout)["status"].get("phase") != "Running":
+            time.sleep(0.1)
+
+    cfg = json.loads((ws / ".tk8s" / "kubeconfig.json").read_text())
+    server = urlsplit(cfg["clusters"][0]["cluster"]["server"])
+    token = cfg["users"][0]["user"]["token"]
+
+    def attach(name, query):
+        return WSClient.connect(server.hostname, server.port, f"{server.path}/api/v1/namespaces/default/pods/{name}/attach",
+                                query=query, token=token, protocols=("v5.channel.k8s.io",), timeout=30)
+
+    def read_until(w, needle):
+        out, status, deadline = b"", None, time.monotonic() + 30
+        while time.monotonic() < deadline and needle not in out and status is None:
+            m = w.recv()
+            if m is None:
+                break
+            if m[:1] == b"\x01":
+                out += m[1:]
+            elif m[:1] == b"\x03":
+                status = json.loads(m[1:])
+        return out.decode(errors="replace"), status
+
+    # a container without stdin: true refuses -i
+    pod("plain", {"command": ["sleep", "120"]})
+    with pytest.raises(WSClosed, match="stdin"):
+        attach("plain", [("stdin", "true"), ("stdout", "true")])
+    # a tty container: resize, input, detach (it runs on), a second session sees its exit status
+    pod("term", {"command": ["sh"], "stdin": True, "tty": True})
+    w = attach("term", [("stdin", "true"), ("stdout", "true"), ("tty", "true")])
+    w.send(b"\x04" + json.dumps({"Width": 99, "Height": 33}).encode())
+    time.sleep(0.2)
+    w.send(b"\x00" + b"stty size; echo v=$((6*7))\n")
+    text, status = read_until(w, b"v=42")
+    assert "33 99" in text and "v=42" in text and status is None, (text, status)
+    w.close()  # detach
+    time.sleep(0.5)
+    assert json.loads(kc("get", "pod", "term", "-o", "json").stdout)["status"]["phase"] == "Running"
+    w = attach("term", [("stdin", "true"), ("stdout", "true"), ("tty", "true")])
+    w.send(b"\x00" + b"echo again-$((1+1)); exit 4\n")
+    text, status = read_until(w, b"never")
+    w.close()
+    assert "again-2" in text and status and status["details"]["causes"][0]["message"] == "4", (text, status)
+    # stdin without a tty: the bundled kubectl's `attach -i`, the output from the container's log
+    pod("pipe", {"command": ["sh", "-c", "read x; echo got-$x; exit 0"], "stdin": True, "stdinOnce": True})
+    r = kc("attach", "-i", "pipe", input="hello\n")
+    assert r.returncode == 0 and "got-hello" in r.stdout, (r.returncode, r.stdout, r.stderr)
+    # kubectl run -it --rm: created, attached, the container's exit code, deleted
+    r = kc("run", "-i", "-t", "--rm", "--restart=Never", "oneoff", "--image=busybox", "--command", "--",
+           "sh", "-c", "read a; echo run-$a; exit 6", input="yes\n")
+    assert r.returncode == 6 and "run-yes" in r.stdout and 'pod "oneoff" deleted' in r.stderr, (r.returncode, r.stdout, r.stderr)
+    assert kc("get", "pod", "oneoff").returncode != 0

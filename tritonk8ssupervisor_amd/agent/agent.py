@@ -17,6 +17,7 @@ stops heartbeats (lease expiry -> NotReady).
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import signal
@@ -1142,7 +1143,7 @@ class Agent:
         self._execs_seen.add(xid)
         pp = self.runtime.running().get(f"{x['namespace']}/{x['pod']}")
         if x.get("stream"):
-            self._run_exec_stream(x, pp)
+            (self._run_attach_stream if x.get("attach") else self._run_exec_stream)(x, pp)
             return
         if pp is None or pp.done.is_set():
             res = {"stdout": "", "stderr": f"pod {x['pod']} is not running on {self.name}\n", "exitCode": 1}
@@ -1269,6 +1270,130 @@ class Agent:
         code = proc.wait()
         os.close(master)
         send(b"\x03" + json.dumps(exec_status(code if code >= 0 else 128 - code)).encode())
+        ws.close()
+
+    def _run_attach_stream(self, x: dict, pp) -> None:
+        """``kubectl attach -i [-t]`` (and ``kubectl run -it``): a session on the stdin and output
+        of a container started with ``stdin: true`` (runtime._spawn: a pipe) or ``tty: true`` (a
+        pty and its output pump), over the same node stream as an interactive exec. Channel 0
+        writes to the container, 4 resizes its terminal, [255, 0] ends its input when the
+        container has ``stdinOnce`` (for a tty: ^D); the output goes out on channel 1 -- the pty's
+        bytes, or the container log's new bytes without a tty -- and when the container ends, its
+        exit status on channel 3. A client that goes away detaches: the container runs on (with
+        ``stdinOnce`` its input is closed, as the kubelet does after the first session)."""
+        import fcntl
+        import queue
+        import struct
+        import termios
+        from urllib.parse import urlsplit
+
+        from ..controlplane.k8s_api import exec_status
+        from ..controlplane.wsclient import WSClient
+        from .runtime import close_stdin
+
+        xid = x["metadata"]["name"]
+        u = urlsplit(self.api.base)
+        try:
+            ws = WSClient.connect(u.hostname, u.port or 80, f"{self.api.prefix}/api/v1/nodes/{self.name}/execs/{xid}/stream",
+                                  token=self.api.token, protocols=("tk8s.exec.v1",))
+        except OSError as e:
+            print(f"{self.name}: attach {xid}: stream not opened: {e}", flush=True)
+            return
+        send_lock = threading.Lock()
+
+        def send(b: bytes) -> None:
+            with send_lock:
+                try:
+                    ws.send(b)
+                except OSError:
+                    pass
+
+        cp = None
+        if pp is not None and not pp.done.is_set():
+            cp = next((c for c in (pp, *pp.sidecars) if c.name == x.get("container")), pp) if x.get("container") else pp
+        proc = cp.proc if cp is not None else None
+        if proc is None or proc.poll() is not None:
+            send(b"\x01" + f"container {x.get('container') or x['pod']} is not running on {self.name}\r\n".encode())
+            send(b"\x03" + json.dumps(exec_status(1)).encode())
+            ws.close()
+            return
+        once = bool(cp.container.get("stdinOnce"))
+        tty = bool(x.get("tty")) and cp.tty_master >= 0
+        detached = threading.Event()
+        q: queue.Queue = queue.Queue()
+        if tty:
+            with cp.io_lock:
+                if cp.tty_master >= 0:
+                    cp.io_subs.append(q)
+                else:
+                    q.put(None)
+
+        def to_container(data: bytes) -> None:
+            with cp.io_lock:  # a dup: the pump may close the master while this write blocks
+                fd = os.dup(cp.tty_master) if cp.tty_master >= 0 else (os.dup(cp.stdin_w) if cp.stdin_w >= 0 else -1)
+            if fd < 0:
+                return
+            try:
+                os.write(fd, data)
+            finally:
+                os.close(fd)
+
+        def inbound():
+            while True:
+                m = ws.recv()
+                if m is None or m[:1] == b"\xfe":
+                    detached.set()
+                    q.put(b"")
+                    if once:
+                        close_stdin(cp)
+                    return
+                ch, data = m[:1], m[1:]
+                try:
+                    if m[:2] == b"\xff\x00":  # the client closed its stdin
+                        if once:
+                            to_container(b"\x04") if tty else close_stdin(cp)
+                    elif ch == b"\x00" and data and x.get("stdin", True):
+                        to_container(data)
+                    elif ch == b"\x04" and data and tty:
+                        sz = json.loads(data)
+                        with cp.io_lock:
+                            if cp.tty_master >= 0:
+                                fcntl.ioctl(cp.tty_master, termios.TIOCSWINSZ,
+                                            struct.pack("HHHH", int(sz.get("Height", 24)), int(sz.get("Width", 80)), 0, 0))
+                except (OSError, ValueError, TypeError):
+                    pass
+
+        threading.Thread(target=inbound, name=f"attach-{xid}-in", daemon=True).start()
+        try:
+            if tty:
+                while not detached.is_set():
+                    data = q.get()
+                    if data is None:  # the pty's last holder is gone
+                        break
+                    if data:
+                        send(b"\x01" + data)
+            else:  # the container log's new bytes
+                log = cp.dir / cp.log_name
+                with contextlib.suppress(OSError), open(log, "rb") as f:
+                    f.seek(0, os.SEEK_END)
+                    while not detached.is_set():
+                        chunk = f.read(1 << 20)
+                        if chunk:
+                            send(b"\x01" + chunk)
+                        elif proc.poll() is not None:
+                            break
+                        else:
+                            time.sleep(0.05)
+        finally:
+            with cp.io_lock:
+                if q in cp.io_subs:
+                    cp.io_subs.remove(q)
+        if not detached.is_set():
+            try:
+                code = proc.wait(timeout=10.0)
+            except subprocess.TimeoutExpired:
+                code = 1
+            send(b"\x03" + json.dumps(exec_status(code if code >= 0 else 128 - code)).encode())
         ws.close()
 
     def _handle(self, etype: str, pod: dict) -> None:

@@ -60,6 +60,43 @@ def expand(s: str, env: dict) -> str:
     return "".join(out)
 
 
+def _tty_pump(pp, master: int, logfd: int) -> None:
+    """Copy a tty container's output to its log and its attached sessions until every holder of
+    the pty's slave side is gone (EIO); then the sessions get None: the container ended."""
+    try:
+        while True:
+            try:
+                data = os.read(master, 65536)
+            except OSError:
+                break
+            if not data:
+                break
+            with contextlib.suppress(OSError):
+                os.write(logfd, data)
+            with pp.io_lock:
+                subs = list(pp.io_subs)
+            for q in subs:
+                q.put(data)
+    finally:
+        os.close(logfd)
+        with pp.io_lock:
+            if pp.tty_master == master:
+                pp.tty_master = -1
+            subs = list(pp.io_subs)
+        os.close(master)
+        for q in subs:
+            q.put(None)
+
+
+def close_stdin(cp) -> None:
+    """End a `stdin: true` container's input: EOF on its pipe (a tty's ends with the container)."""
+    with cp.io_lock:
+        w, cp.stdin_w = cp.stdin_w, -1
+    if w >= 0:
+        with contextlib.suppress(OSError):
+            os.close(w)
+
+
 def last_json_line(text: str) -> dict | None:
     for line in reversed(text.strip().splitlines()):
         line = line.strip()
@@ -101,6 +138,10 @@ class PodProc:
     exit_code: int | None = None
     stopping: bool = False
     done: threading.Event = field(default_factory=threading.Event)
+    tty_master: int = -1          # `tty: true`: the pty's master side (the pump reads it, attach writes it)
+    stdin_w: int = -1             # `stdin: true` without a tty: the write end of the container's stdin
+    io_subs: list = field(default_factory=list)  # attached sessions' output queues (tty containers)
+    io_lock: threading.Lock = field(default_factory=threading.Lock)
 
 
 class PodRuntime:
@@ -132,15 +173,56 @@ class PodRuntime:
         if self.enforcer is not None and pp.exit_code is not None:
             self.enforcer.reset_oom(pp.pod_key or pp.key)
         log = open(pp.dir / pp.log_name, "ab", buffering=0)
+        c = pp.container or {}
         try:
-            p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
-                                 stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
+            if c.get("tty"):
+                p = self._spawn_tty(pp, argv, env, log)
+            elif c.get("stdin"):
+                r, w = os.pipe()
+                try:
+                    p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=r, stdout=log, stderr=subprocess.STDOUT,
+                                         start_new_session=True, close_fds=True)
+                except BaseException:
+                    os.close(w)
+                    raise
+                finally:
+                    os.close(r)
+                with pp.io_lock:
+                    pp.stdin_w = w
+            else:
+                p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
+                                     stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
         finally:
             log.close()
         if pp.limit_opts:  # no jail to join them: best effort right after the start
             _join_limits(p.pid, pp.limit_opts)
         atomic_write_json(pp.dir / _pidfile(pp), {"pid": p.pid, "pgid": p.pid, "argv": pp.argv,
                                                   "start": proc_start_ticks(p.pid)})
+        return p
+
+    def _spawn_tty(self, pp: PodProc, argv: list[str], env: dict, log) -> subprocess.Popen:
+        """`tty: true`: the container gets a pty as its controlling terminal (stdin, stdout and
+        stderr), like the kubelet's; a pump thread copies what it writes to the container's log and
+        to every `kubectl attach` session, which write keystrokes and resizes to the master side."""
+        import fcntl
+        import pty
+        import termios
+
+        master, slave = pty.openpty()
+        env.setdefault("TERM", "xterm")
+        try:
+            p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=slave, stdout=slave, stderr=slave,
+                                 start_new_session=True, close_fds=True,
+                                 preexec_fn=lambda: fcntl.ioctl(0, termios.TIOCSCTTY, 0))
+        except BaseException:
+            os.close(master)
+            raise
+        finally:
+            os.close(slave)
+        logfd = os.dup(log.fileno())
+        with pp.io_lock:
+            pp.tty_master = master
+        threading.Thread(target=_tty_pump, args=(pp, master, logfd), name=f"tty-{pp.key}-{pp.name}", daemon=True).start()
         return p
 
     def _probe(self, cp: PodProc, pp: PodProc) -> None:
@@ -208,6 +290,7 @@ class PodRuntime:
     def _exited(self, cp: PodProc, rc: int) -> int:
         """Record a container's exit; an out-of-memory kill is exit 137, reason OOMKilled (the
         kernel's in a cgroup, or the memory watchdog's)."""
+        close_stdin(cp)
         cp.oom_killed = bool(rc < 0 and self.enforcer is not None and self.enforcer.oom_killed(cp.pod_key or cp.key))
         if cp.oom_killed:
             rc = 137

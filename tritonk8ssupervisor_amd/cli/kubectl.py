@@ -740,6 +740,8 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     ap.add_argument("-c", "--container")
     ap.add_argument("-i", "--stdin", action="store_true")  # exec: pass stdin (with -t: interactive)
     ap.add_argument("-t", "--tty", action="store_true")    # exec: a terminal in the pod
+    ap.add_argument("--rm", action="store_true")           # run -it: delete the pod after the session
+    ap.add_argument("-q", "--quiet", action="store_true")
     ap.add_argument("--to-revision", type=int, default=0)
     ap.add_argument("--for", dest="for_")
     ap.add_argument("--disable-eviction", action="store_true")
@@ -774,12 +776,12 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
     if "--" in argv:  # kubectl exec POD -- CMD ARGS...
         command = argv[argv.index("--") + 1:]
         argv = argv[:argv.index("--")]
-    if argv[:1] == ["exec"]:  # `kubectl exec -it POD`: the flags may come before the pod name
-        flags = [x for x in argv if x in ("-i", "-t", "-it", "-ti", "--stdin", "--tty")]
+    if argv[:1] in (["exec"], ["attach"], ["run"]):  # `kubectl exec -it POD`: flags may precede the name
+        flags = [x for x in argv if x in ("-i", "-t", "-it", "-ti", "--stdin", "--tty", "--rm", "-q", "--quiet")]
         argv = [x for x in argv if x not in flags] + flags
     if argv[:1] == ["logs"]:  # `-f` means --filename and `-p` --patch everywhere but logs
         argv = [{"-f": "--follow", "-p": "--previous"}.get(x, x) for x in argv]
-    a = ap.parse_args(argv)
+    a = ap.parse_intermixed_args(argv) if argv[:1] in (["run"], ["attach"]) else ap.parse_args(argv)
     a.command = command
     workdir = workdir or os.environ.get("TK8S_WORKDIR", os.getcwd())
     if a.verb == "kustomize":  # a local build: no cluster needed
@@ -1084,6 +1086,10 @@ def main(argv: list[str] | None = None, workdir: str | None = None) -> int:
             from .kubectl_streams import attach
 
             what, name = _target(a.args) if "/" in (a.args[0] if a.args else "") else ("pod", (a.args or [""])[0])
+            if a.stdin or a.tty:
+                from .kubectl_streams import attach_interactive
+
+                return attach_interactive(k, ns, name, a.stdin, a.tty, a.container, quiet=a.quiet)
             return attach(k, ns, name)
         elif a.verb == "taint":
             # kubectl taint nodes NAME key[=value]:Effect ... (a trailing "-" removes the taint)

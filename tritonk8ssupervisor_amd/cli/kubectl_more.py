@@ -67,7 +67,10 @@ def _dump(obj: dict, output: str | None) -> str:
 # ---- run / set / autoscale -------------------------------------------------------------------
 def _run(k, a, ns: str) -> int:
     """kubectl run NAME --image=IMG [--env K=V] [--port P] [--labels k=v] [--restart Never|OnFailure|Always]
-    [--limits amd.com/gpu=1,cpu=2] [--command] [-- ARGS...]: one Pod labelled run=NAME."""
+    [--limits amd.com/gpu=1,cpu=2] [--command] [-i] [-t] [--rm] [-- ARGS...]: one Pod labelled run=NAME.
+    ``-i`` starts the container with ``stdin: true, stdinOnce: true`` and ``-t`` with ``tty: true``;
+    either attaches this terminal once the pod runs (``kubectl_streams.attach_interactive``) and
+    returns the container's exit code; ``--rm`` deletes the pod after the session."""
     if not a.args or not a.image:
         raise SystemExit("usage: kubectl run NAME --image=IMAGE [--env K=V] [--port P] [--limits R=Q] [-- ARGS...]")
     name = a.args[0]
@@ -78,6 +81,12 @@ def _run(k, a, ns: str) -> int:
         c["env"] = [{"name": key, "value": val} for key, val in _kv_list(a.env).items()]
     if a.port:
         c["ports"] = [{"containerPort": a.port}]
+    if a.stdin:
+        c["stdin"] = c["stdinOnce"] = True
+    if a.tty:
+        c["tty"] = True
+    if a.rm and not (a.stdin or a.tty):
+        raise SystemExit("error: --rm should only be used for attached containers")
     if a.limits or a.requests:
         c["resources"] = {**({"limits": _kv_list([a.limits])} if a.limits else {}),
                           **({"requests": _kv_list([a.requests])} if a.requests else {})}
@@ -89,8 +98,50 @@ def _run(k, a, ns: str) -> int:
         return 0
     query = {"dryRun": "All"} if a.dry_run == "server" else None
     k.request("POST", k.k8s(collection_path("pod", ns)), body=pod, query=query)
-    print(f"pod/{name} created" + (" (server dry run)" if query else ""))
-    return 0
+    if query or not (a.stdin or a.tty):
+        print(f"pod/{name} created" + (" (server dry run)" if query else ""))
+        return 0
+    return _run_attached(k, a, ns, name)
+
+
+def _run_attached(k, a, ns: str, name: str) -> int:
+    """`kubectl run -i/-t`: wait (up to a minute) for the pod to run, attach, and return the
+    container's exit code; a pod that ended before the attach prints its log instead, like kubectl."""
+    from .kubectl_streams import attach_interactive
+
+    path = k.k8s(object_path("pod", name, ns))
+    code, phase, st, deadline = 1, None, {}, time.time() + 60.0
+    try:
+        while time.time() < deadline:
+            st = k.get(path).get("status") or {}
+            phase = st.get("phase")
+            if phase in ("Running", "Succeeded", "Failed"):
+                break
+            time.sleep(0.1)
+        if phase == "Running":
+            code = attach_interactive(k, ns, name, a.stdin, a.tty, name)
+            for _ in range(50):  # the agent reports the end a moment after the session's Status
+                st = k.get(path).get("status") or {}
+                if st.get("phase") != "Running":
+                    break
+                time.sleep(0.1)
+            phase = st.get("phase")
+        elif phase in ("Succeeded", "Failed"):
+            sys.stdout.write(k.get(path + "/log", raw=True))
+        if phase in ("Succeeded", "Failed"):
+            term = next(((cs.get("state") or {}).get("terminated") for cs in st.get("containerStatuses") or []
+                         if (cs.get("state") or {}).get("terminated")), None)
+            code = int(term.get("exitCode", 1)) if term else (0 if phase == "Succeeded" else 1)
+        elif phase != "Running":
+            print(f"error: timed out waiting for pod {name} to run (phase {phase})", file=sys.stderr)
+    finally:
+        if a.rm:
+            try:
+                k.request("DELETE", path)
+                print(f'pod "{name}" deleted', file=sys.stderr)
+            except ApiError as e:
+                print(f"error: deleting pod {name}: {e}", file=sys.stderr)
+    return code
 
 
 def _set(k, a, ns: str) -> int:

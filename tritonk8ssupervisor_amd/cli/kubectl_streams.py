@@ -173,17 +173,36 @@ def exec_tty(k, ns: str, pod: str, command: list[str], stdin: bool = True, inp=N
     tty=true). This terminal goes raw while it runs, its size is sent first and on every SIGWINCH
     (channel 4), keystrokes go on channel 0, the pod's terminal output comes back on channel 1;
     the exit code is the command's."""
+    q = [("command", c) for c in command] + [("stdout", "true"), ("tty", "true")]
+    if stdin:
+        q.append(("stdin", "true"))
+    return _interactive(k, object_path("pod", pod, ns) + "/exec", q, stdin, True, inp, out)
+
+
+def attach_interactive(k, ns: str, pod: str, stdin: bool, tty: bool, container: str | None = None,
+                       inp=None, out=None, quiet: bool = False) -> int:
+    """``kubectl attach -i [-t] POD`` (and ``kubectl run -it``): a session on the container's own
+    stdin and output (k8s_api.h_pod_attach_ws with stdin/tty: the node agent's
+    ``_run_attach_stream``); with ``-t`` this terminal goes raw like ``exec -it``. The exit code is
+    the container's when it ends during the session."""
+    q = [("stdout", "true"), ("stderr", "true")]
+    q += [("stdin", "true")] if stdin else []
+    q += [("tty", "true")] if tty else []
+    q += [("container", container)] if container else []
+    if tty and not quiet:
+        print("If you don't see a command prompt, try pressing enter.", file=sys.stderr)
+    return _interactive(k, object_path("pod", pod, ns) + "/attach", q, stdin, tty, inp, out)
+
+
+def _interactive(k, path: str, q: list, stdin: bool, tty: bool, inp=None, out=None) -> int:
     import os
     import signal
     import threading
 
     inp = sys.stdin if inp is None else inp
     out = sys.stdout.buffer if out is None else out
-    q = [("command", c) for c in command] + [("stdout", "true"), ("tty", "true")]
-    if stdin:
-        q.append(("stdin", "true"))
     try:
-        ws = WSClient.connect(k.host, k.port, k.k8s(object_path("pod", pod, ns) + "/exec"), q, k.token,
+        ws = WSClient.connect(k.host, k.port, k.k8s(path), q, k.token,
                               ("v5.channel.k8s.io", "v4.channel.k8s.io"), timeout=30)
     except (OSError, WSClosed) as e:
         print(f"error: {e}", file=sys.stderr)
@@ -198,7 +217,7 @@ def exec_tty(k, ns: str, pod: str, command: list[str], stdin: bool = True, inp=N
                 pass
 
     fd = inp.fileno() if hasattr(inp, "fileno") else None
-    is_tty = fd is not None and os.isatty(fd)
+    is_tty = tty and fd is not None and os.isatty(fd)
 
     def resize(*_):
         try:
