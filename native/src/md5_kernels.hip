@@ -3,16 +3,28 @@
 //
 // MD5 is a Merkle-Damgard chain, so one digest over 256 MiB is a serial dependency chain.
 // The GPU form splits the input into fixed chunks (default 1 KiB), one chunk per lane, hashes
-// every chunk with standard RFC 1321 MD5 (padding + length included), then hashes the
-// concatenated 16-byte digests the same way, level after level, until one digest remains.
+// every chunk with standard RFC 1321 MD5 (padding + length included), then folds the digests
+// FOUR at a time -- a parent is the MD5 of its (up to) four children's 16-byte digests, 64 B --
+// level after level until one digest remains. An input of one chunk is its plain MD5.
 // The exact host oracle is hashlib-based: tritonk8ssupervisor_amd/ops/reference.py:md5_tree.
+//
+// Why fan-in 4 above the leaves: every level is a serial chain of (bytes per node / 64 + 1)
+// dependent compressions that no amount of parallelism shortens. Folding 1 KiB of digests per
+// node (the r1-r6 tree) cost 17 compressions per level and three nearly empty launches after
+// the leaves -- 47 us of a 108 us tree at 256 MiB (profiles/r6_kernels). A 64-byte node costs 2,
+// and a block of 256 threads folds 1024 nodes five levels up in one launch (md5_fold_kernel):
+// 256 MiB is the leaf launch plus two fold launches. The fold stays out of the leaf kernel: at
+// 16 waves per CU the leaves are VALU-bound, and a fold there runs on a quarter of the lanes
+// for the full wave's issue cost (+27 us measured, profiles/r6_md5).
 //
 // Per lane: 16 message words per 64-byte block via four 16-byte loads (the next block is
 // loaded before the current one is compressed, so its latency hides under 64 ALU steps);
-// the 64 steps are fully unrolled with constant K/s (VALU: v_bfi / v_alignbit / v_add3).
+// the 64 steps are fully unrolled with constant K/s (VALU: v_bitop3 / v_alignbit / v_add3).
 // With 1 KiB chunks a 256 MiB input is 262144 lanes = 4096 wave64s = 16 waves per CU on
 // 256 CUs, enough to keep the HBM stream and the integer pipes busy together.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "tk8s/common.h"
 #include "tk8s/kernels.h"
@@ -148,6 +160,10 @@ __device__ void md5_finish(unsigned st[4], const unsigned char* __restrict__ p, 
   md5_compress(st, m);
 }
 
+// ------------------------------------------------------------------------------------------
+// Leaves, one lane per chunk: chunk sizes the coalesced kernel does not take, and the chunks
+// after its whole groups.
+// ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kMd5Block) void md5_chunks_kernel(const unsigned char* __restrict__ src,
                                                               unsigned long long nbytes,
                                                               unsigned chunk_bytes,
@@ -180,16 +196,18 @@ __global__ __launch_bounds__(kMd5Block) void md5_chunks_kernel(const unsigned ch
 }
 
 // ------------------------------------------------------------------------------------------
-// Coalesced form for full chunks whose size is a multiple of 128 B (the default 1 KiB):
+// Coalesced leaves for full chunks whose size is a multiple of 128 B (the default 1 KiB):
 // one wave owns 64 consecutive chunks. Per step it pulls the next 128 B of all 64 chunks with
 // 8 wave-instructions (lane l of instruction i loads 16 B of chunk 8i + l/8), i.e. every
 // instruction reads 8 whole 128-B lines instead of 64 scattered 16-B pieces (the one-lane-
 // per-chunk loads above), stages them in a wave-private LDS tile and each lane reads its own
 // chunk's 32 words back. Rows are padded to 144 B (36 dwords): the 16 lanes of a ds_read_b128
 // phase then start on banks 36*l mod 64, all distinct, so the read-back is conflict-free.
-// The next step's global loads are issued before the current step's two compressions, so
-// HBM latency hides under 128 MD5 steps. LDS: 4 waves x 9 KiB per block -> 4 blocks (16 waves)
-// per CU.
+// The next step's global loads are issued before the current step's two compressions and
+// staged only after them, so HBM latency hides under 128 MD5 steps. (Left to itself the
+// compiler hoists the staging -- and its wait for those loads -- above the compressions, which
+// are pure register work: the empty asm below pins the order. profiles/r6_md5.) LDS: 4 waves x
+// 9 KiB per block -> 4 blocks (16 waves) per CU.
 // ------------------------------------------------------------------------------------------
 constexpr int kWaveChunks = 64;
 constexpr int kRowVec = 9;  // u32x4 per LDS row: 8 of data + 1 of padding
@@ -251,6 +269,8 @@ __global__ __launch_bounds__(kMd5Block) void md5_chunks_coalesced_kernel(const u
       m[4 * q + 3] = v[4 + q].w;
     }
     md5_compress(st, m);
+    // The compressions first, then the staging that waits for the next step's loads.
+    asm volatile("" ::"v"(st[0]), "v"(st[1]), "v"(st[2]), "v"(st[3]) : "memory");
     wave_sync_lds();
     if (step + 1 < steps) stage();
   }
@@ -266,8 +286,94 @@ __global__ __launch_bounds__(kMd5Block) void md5_chunks_coalesced_kernel(const u
   digests[group * kWaveChunks + lane] = u32x4{st[0], st[1], st[2], st[3]};
 }
 
+// ------------------------------------------------------------------------------------------
+// The levels above the leaves, fan-in 4. Block b of B threads folds the 4B nodes
+// [4Bb, 4Bb + 4B) of a level of n nodes up `levels` (<= 1 + log4 B) levels: every thread makes
+// one parent from four children read from global memory (all lanes busy), then the block's
+// parents fold in LDS -- B/4 threads, B/16, ... -- until one node, node b of that level. Each
+// level is 2 dependent compressions (one if a parent has fewer than 4 children) and nothing
+// else: the fold is latency-bound, so a launch takes as many levels as a block can hold.
+// ------------------------------------------------------------------------------------------
+constexpr int kFanIn = 4;
+constexpr int kFoldBlock = 256;  // 5 levels (1024 -> 1) per launch
+
+// MD5 of a node: `count` (1..4) child digests, 16 * count bytes. Four children fill one block
+// and the padding takes a second; fewer leave room for the padding in the first.
+__device__ __forceinline__ u32x4 md5_node(const u32x4 (&c)[kFanIn], unsigned count) {
+  unsigned st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  unsigned m[16];
+#pragma unroll
+  for (int q = 0; q < kFanIn; ++q) {
+    const bool have = static_cast<unsigned>(q) < count;
+    m[4 * q + 0] = have ? c[q].x : (static_cast<unsigned>(q) == count ? 0x80u : 0u);
+    m[4 * q + 1] = have ? c[q].y : 0u;
+    m[4 * q + 2] = have ? c[q].z : 0u;
+    m[4 * q + 3] = have ? c[q].w : 0u;
+  }
+  if (count < kFanIn) m[14] = 128u * count;  // bit length; m[15] stays 0
+  md5_compress(st, m);
+  if (count == kFanIn) {
+#pragma unroll
+    for (int w = 0; w < 16; ++w) m[w] = 0;
+    m[0] = 0x80u;
+    m[14] = 512u;
+    md5_compress(st, m);
+  }
+  return u32x4{st[0], st[1], st[2], st[3]};
+}
+
+__device__ __forceinline__ unsigned children(unsigned long long first, unsigned long long n) {
+  return first >= n ? 0u : (n - first >= kFanIn ? kFanIn : static_cast<unsigned>(n - first));
+}
+
+template <int B>
+__global__ __launch_bounds__(B) void md5_fold_kernel(const u32x4* __restrict__ in, unsigned long long n, int levels,
+                                                    u32x4* __restrict__ out) {
+  __shared__ u32x4 nodes[B];
+  const int t = threadIdx.x;
+  unsigned long long base = static_cast<unsigned long long>(blockIdx.x) * B;  // first parent of this block
+  u32x4 d = u32x4{0u, 0u, 0u, 0u};
+  {
+    const unsigned long long p = base + t;
+    const unsigned count = children(kFanIn * p, n);
+    if (count) {
+      u32x4 c[kFanIn];
+#pragma unroll
+      for (int i = 0; i < kFanIn; ++i) c[i] = static_cast<unsigned>(i) < count ? in[kFanIn * p + i] : u32x4{0u, 0u, 0u, 0u};
+      d = md5_node(c, count);
+    }
+  }
+  unsigned long long nl = (n + kFanIn - 1) / kFanIn;  // nodes of the level just made
+  for (int l = 1; l < levels; ++l) {
+    nodes[t] = d;
+    __syncthreads();
+    const unsigned long long p = base / kFanIn + t;  // parent (global index) this thread makes
+    const unsigned count = t < (B >> (2 * l)) ? children(kFanIn * p, nl) : 0u;
+    if (count) {
+      u32x4 c[kFanIn];
+#pragma unroll
+      for (int i = 0; i < kFanIn; ++i) c[i] = nodes[kFanIn * t + i];
+      d = md5_node(c, count);
+    }
+    __syncthreads();
+    base /= kFanIn;
+    nl = (nl + kFanIn - 1) / kFanIn;
+  }
+  if (t == 0) out[blockIdx.x] = d;
+}
+
+template __global__ void md5_fold_kernel<64>(const u32x4*, unsigned long long, int, u32x4*);
+template __global__ void md5_fold_kernel<256>(const u32x4*, unsigned long long, int, u32x4*);
+
 static unsigned long long n_chunks(size_t nbytes, uint32_t chunk_bytes) {
   return nbytes == 0 ? 1ull : (nbytes + chunk_bytes - 1) / chunk_bytes;
+}
+
+// Levels left until one node, above a level of n.
+static int levels_to_root(unsigned long long n) {
+  int f = 0;
+  for (; n > 1; ++f) n = (n + kFanIn - 1) / kFanIn;
+  return f;
 }
 
 void md5_chunks(const void* src, size_t nbytes, uint32_t chunk_bytes, void* digests,
@@ -305,19 +411,34 @@ size_t md5_tree_workspace(size_t nbytes, uint32_t chunk_bytes) {
   return static_cast<size_t>(n_chunks(nbytes, chunk_bytes)) * 16;
 }
 
+// The fold launches over a level of n nodes at `in`, ending with the root in out16.
+template <int B>
+static void fold(const void* in, unsigned long long n, void* ws_a, void* ws_b, void* out16, hipStream_t stream) {
+  constexpr int kMax = B == 64 ? 4 : B == 256 ? 5 : 0;
+  static_assert(kMax, "fold block: 64 or 256 threads");
+  void* bufs[2] = {ws_b, ws_a};
+  for (int launch = 0; n > 1; ++launch) {
+    const int left = levels_to_root(n), levels = left < kMax ? left : kMax;
+    void* dst = levels == left ? out16 : bufs[launch & 1];
+    const unsigned long long parents = (n + kFanIn - 1) / kFanIn;
+    const unsigned grid = static_cast<unsigned>((parents + B - 1) / B);
+    hipLaunchKernelGGL(md5_fold_kernel<B>, dim3(grid), dim3(B), 0, stream, static_cast<const u32x4*>(in), n, levels,
+                       static_cast<u32x4*>(dst));
+    TK8S_HIP_CHECK(hipGetLastError());
+    n = grid;  // one node per block
+    in = dst;
+  }
+}
+
 void md5_tree(const void* src, size_t nbytes, uint32_t chunk_bytes, void* ws_a, void* ws_b,
               void* out16, hipStream_t stream) {
-  const void* in = src;
-  size_t n = nbytes;
-  void* bufs[2] = {ws_a, ws_b};
-  for (int level = 0;; ++level) {
-    const unsigned long long nchunks = n_chunks(n, chunk_bytes);
-    void* dst = nchunks == 1 ? out16 : bufs[level & 1];
-    md5_chunks(in, n, chunk_bytes, dst, stream);
-    if (nchunks == 1) return;
-    in = dst;
-    n = static_cast<size_t>(nchunks) * 16;
+  const unsigned long long n = n_chunks(nbytes, chunk_bytes);
+  if (n == 1) {  // one chunk: its plain MD5
+    md5_chunks(src, nbytes, chunk_bytes, out16, stream);
+    return;
   }
+  md5_chunks(src, nbytes, chunk_bytes, ws_a, stream);
+  fold<kFoldBlock>(ws_a, n, ws_a, ws_b, out16, stream);
 }
 
 }  // namespace tk8s

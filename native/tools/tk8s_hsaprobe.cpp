@@ -64,12 +64,14 @@ namespace {
 
 using tk8s::Json;
 
-constexpr const char* kKnownDigest256M = "55af80380d572d36cc8cc7d50edd90ab";
+constexpr const char* kKnownDigest256M = "6a21931a145024b03ee4405e01204ce2";
 constexpr uint32_t kBlock = 256;     // stream kernels: 4 wave64s (stream_kernels.hip kBlock)
 constexpr uint16_t kFillBlock = 128; // the plain HBM fill: one 2-wave block per CU (stream_kernels.hip)
 constexpr size_t kMallFlush = size_t(512) << 20;  // 2 x the MI355X's 256 MB Infinity Cache (MALL)
 constexpr uint32_t kMd5Block = 256;  // md5_kernels.hip kMd5Block
 constexpr uint64_t kWaveChunks = 64;
+constexpr uint32_t kFoldBlock = 256;  // md5_kernels.hip kFoldBlock: 1024 nodes -> 1 per block
+constexpr int kFoldLevels = 5;
 constexpr size_t kAlign = 4096;
 constexpr double kHbmPeakGBps = 8000.0;  // MI355X HBM3E, 8 TB/s per GPU
 
@@ -321,7 +323,7 @@ struct Kernel {
 };
 
 struct KernelSet {
-  Kernel fill_plain, fill_nt, verify, philox, copy, md5c, md5;
+  Kernel fill_plain, fill_nt, verify, philox, copy, md5c, md5, md5f;
   Kernel stall;  // fault injection only (TK8S_FAULTS probe.hang@peers): not required
 };
 
@@ -352,6 +354,7 @@ hsa_status_t find_kernels(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t
   else if (name.find("18stream_copy_kernel") != std::string::npos) k = &ks->copy;
   else if (name.find("27md5_chunks_coalesced_kernel") != std::string::npos) k = &ks->md5c;
   else if (name.find("17md5_chunks_kernel") != std::string::npos) k = &ks->md5;
+  else if (name.find("15md5_fold_kernelILi256E") != std::string::npos) k = &ks->md5f;  // kFoldBlock
   else if (name.find("12stall_kernel") != std::string::npos) k = &ks->stall;
   if (!k) return HSA_STATUS_SUCCESS;
   HSA_OK(hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k->object));
@@ -454,7 +457,8 @@ class Device {
     }
     HSA_OK(hsa_executable_freeze(exe_, nullptr));
     HSA_OK(hsa_executable_iterate_agent_symbols(exe_, g_.agent, find_kernels, &ks_));
-    for (const Kernel* k : {&ks_.fill_plain, &ks_.fill_nt, &ks_.verify, &ks_.philox, &ks_.copy, &ks_.md5c, &ks_.md5})
+    for (const Kernel* k : {&ks_.fill_plain, &ks_.fill_nt, &ks_.verify, &ks_.philox, &ks_.copy, &ks_.md5c, &ks_.md5,
+                             &ks_.md5f})
       if (!k->found) throw std::runtime_error("kernel missing from the code objects");
     code_ms = ms_since(t);
   }
@@ -614,41 +618,51 @@ class Device {
     return launch(ks_.copy, grid_for(n16 / 8, 16), kBlock,  // stream_kernels.hip: kCopyDepth 8, 16 blocks/CU
                   [&](KernArgs& a) { a.ptr(dst).ptr(src).u64(n16); }, to_host, from_remote);
   }
-  // md5_kernels.hip md5_tree: level by level until one digest; returns (first, last) dispatch.
+  // md5_kernels.hip md5_tree: the leaf digests, then fold launches (fan-in 4, a block of 256
+  // folding 1024 nodes up to five levels) until one digest; returns (first, last) dispatch.
   std::pair<size_t, size_t> md5_tree(const void* src, size_t nbytes, uint32_t chunk, void* wa, void* wb, void* out) {
-    const void* in = src;
-    size_t n = nbytes;
-    void* bufs[2] = {wa, wb};
+    const uint64_t nleaves = nbytes == 0 ? 1 : (nbytes + chunk - 1) / chunk;
+    void* leaf_dst = nleaves == 1 ? out : wa;
     size_t first = SIZE_MAX, last = 0;
-    for (int level = 0;; ++level) {
-      const uint64_t nchunks = n == 0 ? 1 : (n + chunk - 1) / chunk;
-      void* dst = nchunks == 1 ? out : bufs[level & 1];
-      uint64_t ngroups = chunk % 128 == 0 ? (n / chunk) / kWaveChunks : 0;
-      if (ngroups) {
-        const unsigned grid = static_cast<unsigned>((ngroups + kMd5Block / 64 - 1) / (kMd5Block / 64));
-        const size_t i = launch(ks_.md5c, grid, kMd5Block, [&](KernArgs& a) {
-                           a.ptr(in).u32(chunk).u64(ngroups).ptr(dst);
-                         });
-        first = std::min(first, i);
-        last = i;
-      }
-      const uint64_t done = ngroups * kWaveChunks;
-      if (!(done >= nchunks && n)) {
-        const size_t off = static_cast<size_t>(done) * chunk;
-        const uint64_t rest = nchunks - done;
-        const unsigned grid = static_cast<unsigned>((rest + kMd5Block - 1) / kMd5Block);
-        const auto* s = static_cast<const unsigned char*>(in) + off;
-        auto* d = static_cast<unsigned char*>(dst) + done * 16;
-        const size_t i = launch(ks_.md5, grid, kMd5Block, [&](KernArgs& a) {
-                           a.ptr(s).u64(static_cast<uint64_t>(n - off)).u32(chunk).u64(rest).ptr(d);
-                         });
-        first = std::min(first, i);
-        last = i;
-      }
-      if (nchunks == 1) return {first, last};
-      in = dst;
-      n = static_cast<size_t>(nchunks) * 16;
+    const uint64_t ngroups = chunk % 128 == 0 ? (nbytes / chunk) / kWaveChunks : 0;
+    if (ngroups) {
+      const unsigned grid = static_cast<unsigned>((ngroups + kMd5Block / 64 - 1) / (kMd5Block / 64));
+      last = first = launch(ks_.md5c, grid, kMd5Block, [&](KernArgs& a) {
+        a.ptr(src).u32(chunk).u64(ngroups).ptr(leaf_dst);
+      });
     }
+    const uint64_t done = ngroups * kWaveChunks;
+    if (!(done >= nleaves && nbytes)) {
+      const size_t off = static_cast<size_t>(done) * chunk;
+      const uint64_t rest = nleaves - done;
+      const unsigned grid = static_cast<unsigned>((rest + kMd5Block - 1) / kMd5Block);
+      const auto* s = static_cast<const unsigned char*>(src) + off;
+      auto* d = static_cast<unsigned char*>(leaf_dst) + done * 16;
+      last = launch(ks_.md5, grid, kMd5Block, [&](KernArgs& a) {
+        a.ptr(s).u64(static_cast<uint64_t>(nbytes - off)).u32(chunk).u64(rest).ptr(d);
+      });
+      first = std::min(first, last);
+    }
+    auto levels_to_root = [](uint64_t n) {
+      int f = 0;
+      for (; n > 1; ++f) n = (n + 3) / 4;
+      return f;
+    };
+    const void* in = wa;
+    void* bufs[2] = {wb, wa};
+    uint64_t n = nleaves;
+    for (int k = 0; n > 1; ++k) {
+      const int left = levels_to_root(n), levels = std::min(kFoldLevels, left);
+      void* dst = levels == left ? out : bufs[k & 1];
+      const uint64_t parents = (n + 3) / 4;
+      const unsigned grid = static_cast<unsigned>((parents + kFoldBlock - 1) / kFoldBlock);
+      last = launch(ks_.md5f, grid, kFoldBlock, [&](KernArgs& a) {
+        a.ptr(in).u64(n).u32(static_cast<uint32_t>(levels)).ptr(dst);
+      });
+      n = grid;
+      in = dst;
+    }
+    return {first, last};
   }
   uint8_t* host() { return host_; }
   const Gpu& gpu() const { return g_; }

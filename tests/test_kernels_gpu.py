@@ -43,8 +43,9 @@ def test_philox_fill_matches_host(nat, nbytes):
     assert bytes(buf.cpu().numpy()) == ref.philox_bytes(nbytes, 0x1234_5678_9ABC)
 
 
-@pytest.mark.parametrize("nbytes,chunk", [(0, 1024), (16, 1024), (1024, 1024), (1040, 1024),
-                                          (70000 * 16, 1024), (2**20, 256), (5 * 2**20 + 32, 4096)])
+@pytest.mark.parametrize("nbytes,chunk", [(0, 1024), (16, 1024), (1024, 1024), (1040, 1024), (16384, 1024),
+                                          (17408, 1024), (65536, 1024), (70000 * 16, 1024), (100000, 192),
+                                          (2**20, 256), (5 * 2**20 + 32, 4096)])
 def test_md5_tree_matches_hashlib(nat, nbytes, chunk):
     data = ref.philox_bytes(nbytes, seed=11) if nbytes else b""
     src = torch.frombuffer(bytearray(data) or bytearray(16), dtype=torch.uint8).cuda()
@@ -155,7 +156,7 @@ def test_probe_cli_all_devices_known_answer(nat):
                      "--peer-bytes", str(16 << 20))
     assert rc == 0 and out["ok"], out
     assert out["probed"] == out["device_count"] >= 1
-    assert out["md5_expected"] == "55af80380d572d36cc8cc7d50edd90ab"  # host oracle, 256 MiB seed 0
+    assert out["md5_expected"] == "6a21931a145024b03ee4405e01204ce2"  # host oracle, 256 MiB seed 0
     for d in out["devices"]:
         assert d["ok"] and d["digest_ok"] and d["hbm"]["bad_words"] == 0
         assert d["hbm"]["gbps"] > 3000 and d["copy"]["kernel_gbps"] > 1500
@@ -586,7 +587,7 @@ def test_hsaprobe_digests_match_the_host_oracle(nat):
 def test_hsaprobe_known_answer_and_gpuinfo_agree_with_the_hip_probe(nat):
     rc, hsa = _hsaprobe("--all-devices", "--gpuinfo", "--iters", "2")
     assert rc == 0 and hsa["ok"], hsa
-    assert hsa["md5_expected"] == "55af80380d572d36cc8cc7d50edd90ab" and hsa["md5"]["digest"] == hsa["md5_expected"]
+    assert hsa["md5_expected"] == "6a21931a145024b03ee4405e01204ce2" and hsa["md5"]["digest"] == hsa["md5_expected"]
     for d in hsa["devices"]:
         assert d["ok"] and d["digest_ok"] and d["hbm"]["gbps"] > 3000 and d["copy"]["kernel_gbps"] > 1500
     rc, hip = _probe("--all-devices", "--gpuinfo", "--iters", "1", "--hbm-bytes", str(64 << 20))

@@ -36,14 +36,21 @@ def test_md5_tree_small_is_plain_md5():
 
 
 def test_md5_tree_levels():
+    md5 = lambda b: hashlib.md5(b).digest()
+    # 5 leaves (the last partial): a parent of four and a parent of one, then the root
     data = ref.philox_bytes(4096 + 512, seed=7)
-    d = [hashlib.md5(data[i : i + 1024]).digest() for i in range(0, len(data), 1024)]
-    assert ref.md5_tree(data, 1024) == hashlib.md5(b"".join(d)).digest()
-    # 3 levels: 64 KiB of chunks -> 1 KiB of digests -> one
+    d = [md5(data[i : i + 1024]) for i in range(0, len(data), 1024)]
+    assert ref.md5_tree(data, 1024) == md5(md5(b"".join(d[:4])) + md5(d[4]))
+    # 128 leaves: 32 -> 8 -> 2 -> 1
     big = ref.philox_bytes(1 << 17, seed=3)
-    l1 = b"".join(hashlib.md5(big[i : i + 1024]).digest() for i in range(0, len(big), 1024))
-    l2 = b"".join(hashlib.md5(l1[i : i + 1024]).digest() for i in range(0, len(l1), 1024))
-    assert ref.md5_tree(big, 1024) == hashlib.md5(l2).digest()
+    level = [md5(big[i : i + 1024]) for i in range(0, len(big), 1024)]
+    for want in (32, 8, 2, 1):
+        level = [md5(b"".join(level[i : i + 4])) for i in range(0, len(level), 4)]
+        assert len(level) == want
+    assert ref.md5_tree(big, 1024) == level[0]
+    # two chunks: the root hashes the two leaf digests (32 bytes)
+    two = data[:2048]
+    assert ref.md5_tree(two, 1024) == md5(md5(two[:1024]) + md5(two[1024:]))
 
 
 def test_allreduce_expected():

@@ -1363,6 +1363,13 @@ class Agent:
                 except (OSError, ValueError, TypeError):
                     pass
 
+        f = None
+        if not tty:  # the container log's new bytes: from before the first keystroke can reach it
+            try:
+                f = open(cp.dir / cp.log_name, "rb")
+                f.seek(0, os.SEEK_END)
+            except OSError:
+                pass
         threading.Thread(target=inbound, name=f"attach-{xid}-in", daemon=True).start()
         try:
             if tty:
@@ -1372,19 +1379,22 @@ class Agent:
                         break
                     if data:
                         send(b"\x01" + data)
-            else:  # the container log's new bytes
-                log = cp.dir / cp.log_name
-                with contextlib.suppress(OSError), open(log, "rb") as f:
-                    f.seek(0, os.SEEK_END)
-                    while not detached.is_set():
-                        chunk = f.read(1 << 20)
-                        if chunk:
-                            send(b"\x01" + chunk)
-                        elif proc.poll() is not None:
-                            break
-                        else:
-                            time.sleep(0.05)
+            elif f is not None:
+                while not detached.is_set():
+                    ended = proc.poll() is not None  # before the read: what it wrote last is in it
+                    chunk = f.read(1 << 20)
+                    if chunk:
+                        send(b"\x01" + chunk)
+                    elif ended:
+                        break
+                    else:
+                        time.sleep(0.05)
+            else:
+                while not detached.is_set() and proc.poll() is None:
+                    time.sleep(0.05)
         finally:
+            if f is not None:
+                f.close()
             with cp.io_lock:
                 if q in cp.io_subs:
                     cp.io_subs.remove(q)

@@ -3,7 +3,7 @@
 * :func:`philox4x32_10` / :func:`philox_bytes` — bit-exact model of ``philox_fill``
   (native/src/stream_kernels.hip): Random123 Philox4x32-10, counter = (block index lo, hi, 0, 0),
   key = (seed lo, seed hi).
-* :func:`md5_tree` — the chunked MD5 tree of ``md5_tree`` (native/src/md5_kernels.hip), built
+* :func:`md5_tree` — the chunked, fan-in-4 MD5 tree of ``md5_tree`` (native/src/md5_kernels.hip), built
   from :mod:`hashlib` MD5 so the GPU digest can be checked against an independent implementation.
 * :func:`allreduce_expected` — value of the N6 pattern after a sum all-reduce.
 
@@ -52,17 +52,19 @@ def philox_bytes(nbytes: int, seed: int) -> bytes:
     return out.astype("<u4").tobytes()
 
 
-def md5_tree(data: bytes, chunk_bytes: int = 1024) -> bytes:
-    """MD5 tree: hash each chunk, then hash the concatenated digests, until one remains."""
+def md5_tree(data: bytes, chunk_bytes: int = 1024, fan_in: int = 4) -> bytes:
+    """MD5 tree: hash each ``chunk_bytes`` chunk (one chunk: its plain MD5), then fold the
+    digests ``fan_in`` at a time -- a parent is the MD5 of its children's concatenated digests --
+    until one remains."""
     if chunk_bytes <= 0 or chunk_bytes % 64:
         raise ValueError("chunk_bytes must be a positive multiple of 64")
-    level = bytes(data)
-    while True:
-        if len(level) <= chunk_bytes:
-            return hashlib.md5(level).digest()
-        level = b"".join(
-            hashlib.md5(level[i : i + chunk_bytes]).digest() for i in range(0, len(level), chunk_bytes)
-        )
+    data = bytes(data)
+    if len(data) <= chunk_bytes:
+        return hashlib.md5(data).digest()
+    level = [hashlib.md5(data[i : i + chunk_bytes]).digest() for i in range(0, len(data), chunk_bytes)]
+    while len(level) > 1:
+        level = [hashlib.md5(b"".join(level[i : i + fan_in])).digest() for i in range(0, len(level), fan_in)]
+    return level[0]
 
 
 def allreduce_expected(count: int, nranks: int) -> np.ndarray:
