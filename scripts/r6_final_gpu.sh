@@ -17,3 +17,5 @@ echo "bench_fault rc=$rc" >> "$out/status"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py > "$out/bench_default.json" 2> "$out/bench_default.err"
 echo "bench_default rc=$?" >> "$out/status"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
+echo "smoke rc=$?" >> "$out/status"
