@@ -27,6 +27,7 @@
 
 #include <cstddef>
 #include <functional>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -58,6 +59,9 @@ struct AllReduceConfig {
   // GPU-side fault point (TK8S_FAULTS rccl.hang@sweep / rccl.hang@check): stall the local ranks'
   // streams in that phase (kernels.h gpu_stall), as a rank whose GPU stopped would
   std::string stall_phase;
+  // streams made ahead of the run (tk8s-rccl makes them while the unique id is exchanged), by
+  // device; a device without one gets a fresh stream
+  std::map<int, hipStream_t> streams;
 };
 
 std::string nccl_unique_id_hex(const ncclUniqueId& id);

@@ -10,6 +10,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -21,6 +22,15 @@
 namespace tk8s {
 
 namespace {
+
+// TK8S_TRACE=1: the rank's phases as "TRACE <unix s> rccl <what>" on stderr, in the bring-up's
+// merged timeline (tools/tk8s_rccl.cpp traces the steps around them; scripts/trace_bringup.py).
+void trace(const char* what) {
+  static const bool on = std::getenv("TK8S_TRACE") != nullptr;
+  if (!on) return;
+  const double t = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+  std::fprintf(stderr, "TRACE %.6f rccl %s\n", t, what);
+}
 
 // A failure of one phase of the validator: what ran out or broke, and where.
 struct PhaseError : std::runtime_error {
@@ -153,6 +163,7 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
     r.timer = std::make_unique<EventTimer>();
   }
   wait_ranks(ranks, cfg);
+  trace("buffers ready");
   const auto t_sweep = std::chrono::steady_clock::now();
   if (cfg.stall_phase == "sweep")
     for (auto& r : ranks) {
@@ -257,6 +268,7 @@ std::string run_sweep(std::vector<Rank>& ranks, int all_ranks, const AllReduceCo
   };
   constexpr double kXgmiLinkGBps = 153.0;
   const auto t_end = std::chrono::steady_clock::now();
+  trace("sweep checked");
   auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   std::string dtypes;
   std::vector<std::string> dnames;
@@ -378,8 +390,11 @@ std::string run_group(int first_rank, int nranks, const std::vector<int>& device
       ranks[i].device = devices[i];
       ranks[i].rank = first_rank + static_cast<int>(i);
       TK8S_HIP_CHECK(hipSetDevice(devices[i]));
-      TK8S_HIP_CHECK(hipStreamCreateWithFlags(&ranks[i].stream, hipStreamNonBlocking));
+      const auto made = cfg.streams.find(devices[i]);
+      if (made != cfg.streams.end() && made->second != nullptr) ranks[i].stream = made->second;
+      else TK8S_HIP_CHECK(hipStreamCreateWithFlags(&ranks[i].stream, hipStreamNonBlocking));
     }
+    trace("streams created");
     enter(cfg, "init");
     const auto t0 = std::chrono::steady_clock::now();
     // Several ranks of one communicator in one thread: the inits must be one group, or the first
@@ -421,6 +436,7 @@ std::string run_group(int first_rank, int nranks, const std::vector<int>& device
     if (!st->err.empty()) throw PhaseError("init", st->err, false);
     for (size_t i = 0; i < ranks.size(); ++i) ranks[i].comm = st->comms[i];
     settle(ranks, cfg);  // non-blocking: the inits may still be finishing
+    trace("communicator ready");
     const double init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     std::string out = run_sweep(ranks, nranks, cfg, mode, init_ms, unix_ms());
     if (cfg.teardown) release(ranks);

@@ -27,6 +27,8 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <map>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -124,33 +126,41 @@ std::string stall_phase() {
 // HIP loads it onto a device the first time one of its kernels is referenced there -- inside
 // the communicator start, ~160 ms of its ~205 ms on the MI355X (profiles/r5_thp/). Referencing
 // a kernel of it right after the runtime's start, on a thread per device, lets that load overlap
-// the unique id's creation (~26 ms) or its wait (the other ranks). TK8S_RCCL_PREWARM=0: off.
+// the unique id's creation (~26 ms) or its wait (the other ranks). A second thread per device
+// makes the rank's stream meanwhile: the device's first queue, 15-85 ms measured between the
+// code load and the communicator start (profiles/r6_rccl_prewarm/). TK8S_RCCL_PREWARM=0: off.
 struct Prewarm {
   std::vector<std::thread> threads;
   std::chrono::steady_clock::time_point t0;
   bool started = false;
+  std::map<int, hipStream_t> streams;  // each device's rank stream (filled by its own thread)
+  std::mutex mu;
 };
 
-Prewarm prewarm_rccl_code(const std::vector<int>& devices) {
-  Prewarm p;
+void prewarm_rccl_code(Prewarm& p, const std::vector<int>& devices) {
   const char* off = std::getenv("TK8S_RCCL_PREWARM");
-  if (off != nullptr && std::string(off) == "0") return p;
+  if (off != nullptr && std::string(off) == "0") return;
   const void* sym = nullptr;
   for (const char* name : {"_Z23ncclDevKernel_Generic_124ncclDevKernelArgsStorageILm4096EE",
                            "_Z23ncclDevKernel_Generic_224ncclDevKernelArgsStorageILm4096EE"}) {
     if ((sym = dlsym(RTLD_DEFAULT, name)) != nullptr) break;
   }
-  if (sym == nullptr) return p;  // another RCCL's names: its start loads the code as before
+  if (sym == nullptr) return;  // another RCCL's names: its start loads the code as before
   p.t0 = std::chrono::steady_clock::now();
   p.started = true;
   for (int d : devices) {
-    p.threads.emplace_back([d, sym] {
+    p.threads.emplace_back([d, sym] {  // the code load
       if (hipSetDevice(d) != hipSuccess) return;
       hipFuncAttributes attr;
       (void)hipFuncGetAttributes(&attr, sym);
     });
+    p.threads.emplace_back([d, &p] {  // the rank's stream: the device's first queue (15-85 ms)
+      hipStream_t s = nullptr;
+      if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+      std::lock_guard<std::mutex> g(p.mu);
+      p.streams[d] = s;
+    });
   }
-  return p;
 }
 
 // What the process is doing, for the watchdog's error line.
@@ -233,7 +243,8 @@ int main(int argc, char** argv) {
         (void)hipGetDeviceCount(&n);
         trace("hip runtime up");
       }
-      Prewarm warm = prewarm_rccl_code(devices);
+      Prewarm warm;
+      prewarm_rccl_code(warm, devices);
       // the uid exchange is bounded by the same budget as every other wait
       const double uid_timeout = std::strtod(a.str("uid-timeout", a.str("op-timeout", "20")).c_str(), nullptr);
       if (bounded) dog.arm("uid", uid_timeout + grace);
@@ -270,6 +281,7 @@ int main(int argc, char** argv) {
       const double prewarm_ms =
           warm.started ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - warm.t0).count() : -1;
       if (warm.started) trace("rccl code loaded");
+      cfg.streams = warm.streams;
       tk8s::fault_point("rccl", "init");
       cfg.stall_phase = stall_phase();
       out = tk8s::allreduce_rank_group(first, nranks, devices, id, cfg);
