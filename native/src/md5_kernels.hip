@@ -36,7 +36,7 @@ constexpr int kMd5Block = 256;
 
 #define TK8S_F(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
 #define TK8S_G(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
-#define TK8S_H(x, y, z) ((x) ^ (y) ^ (z))
+#define TK8S_H(x, y, z) __builtin_amdgcn_bitop3_b32((x), (y), (z), 0x96)  // x ^ y ^ z in one VALU op
 #define TK8S_I(x, y, z) ((y) ^ ((x) | ~(z)))
 #define TK8S_STEP(f, a, b, c, d, x, k, s)               \
   do {                                                  \
