@@ -213,6 +213,60 @@ def test_kubectl_exec_enters_the_container(ws, native_build, mode):
 
 
 @pytest.mark.parametrize("mode", ["auto", "ptrace"])
+def test_attach_to_an_image_pods_terminal(ws, native_build, mode):
+    """`kubectl attach -it` to an image pod started with `stdin: true, tty: true`: its shell, in
+    the image's root, reads the keystrokes from the pty the agent holds and answers on it -- through
+    tk8s-container in either mode -- and its exit code ends the session."""
+    from urllib.parse import urlsplit
+
+    from tritonk8ssupervisor_amd.controlplane.wsclient import WSClient
+
+    how = _probe_mode(mode)
+    if not how:
+        pytest.skip(f"no container runtime for --mode {mode} here")
+    env = _env(ws)
+    if mode != "auto":
+        env["TK8S_CONTAINER_MODE"] = mode
+    _hello_archive(ws / "hello.tar")
+    assert subprocess.run(["./tk8s", "image", "load", "hello.tar"], cwd=ws, env=env, capture_output=True).returncode == 0
+    r = subprocess.run(["./setup.sh", "--yes", "--json", "--port", "0", "--nodes", "1", "--rccl", "off"], cwd=ws,
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    (ws / "pod.json").write_text(json.dumps({
+        "apiVersion": "v1", "kind": "Pod", "metadata": {"name": "term"},
+        "spec": {"restartPolicy": "Never", "containers": [{"name": "c", "image": "hello:1", "command": ["/bin/sh"],
+                                                           "stdin": True, "tty": True}]}}))
+    kc = lambda *a: subprocess.run(["./kubectl", *a], cwd=ws, env=env, capture_output=True, text=True, timeout=60)
+    assert kc("apply", "-f", "pod.json").returncode == 0
+    deadline = time.monotonic() + 30
+    while time.monotonic() < deadline:
+        if json.loads(kc("get", "pod", "term", "-o", "json").stdout)["status"].get("phase") == "Running":
+            break
+        time.sleep(0.2)
+    cfg = json.loads((ws / ".tk8s" / "kubeconfig.json").read_text())
+    server = urlsplit(cfg["clusters"][0]["cluster"]["server"])
+    w = WSClient.connect(server.hostname, server.port, f"{server.path}/api/v1/namespaces/default/pods/term/attach",
+                         query=[("stdin", "true"), ("stdout", "true"), ("tty", "true")],
+                         token=cfg["users"][0]["user"]["token"], protocols=("v5.channel.k8s.io",), timeout=30)
+    w.send(b"\x00" + b"cat /etc/hello-release; [ -t 0 ] && echo tty=yes; cat /etc/removed || echo img=yes; exit 7\n")
+    out, status, deadline = b"", None, time.monotonic() + 30
+    while time.monotonic() < deadline and status is None:
+        m = w.recv()
+        if m is None:
+            break
+        if m[:1] == b"\x01":
+            out += m[1:]
+        elif m[:1] == b"\x03":
+            status = json.loads(m[1:])
+    w.close()
+    text = out.decode(errors="replace")
+    assert "tk8s hello 1" in text and "tty=yes" in text and "img=yes" in text, (text, kc("logs", "term").stdout,
+                                                                                 kc("describe", "pod", "term").stdout)
+    time.sleep(1)
+    assert status and status["details"]["causes"][0]["message"] == "7", (status, kc("get", "pod", "term", "-o", "json").stdout[-1500:], text)
+
+
+@pytest.mark.parametrize("mode", ["auto", "ptrace"])
 def test_image_pod_volumes(ws, native_build, mode):
     """An image pod mounts its volumes where the spec says: a ConfigMap (read-only), a Secret, an
     emptyDir, a PersistentVolumeClaim (data kept for the next pod), the downward API; and gets
