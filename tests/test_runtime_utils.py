@@ -469,3 +469,27 @@ def test_poststart_hook_failure_restarts_the_container(tmp_path):
     flag.write_text("")
     assert "FailedPostStartHook" in (tmp_path / "pods" / "hooked" / "log").read_text()
     rt.stop("default/hooked", grace=1.0)
+
+
+def test_tty_pod_on_a_node_without_ptys_runs_with_its_stdin_pipe(tmp_path, monkeypatch):
+    """`tty: true` where no pseudo-terminal can be had (the MI355X GPU boxes mount no devpts): the
+    container runs as with `tty: false` -- its stdin a pipe when `stdin: true` -- and its log says
+    why, instead of the pod failing to start."""
+    import pty
+
+    from tritonk8ssupervisor_amd.agent.runtime import PodProc, PodRuntime, close_stdin
+
+    def no_pty():
+        raise OSError("out of pty devices")
+
+    monkeypatch.setattr(pty, "openpty", no_pty)
+    rt = PodRuntime(tmp_path, on_status=lambda *a: None)
+    pp = PodProc(key="default/t", uid="u1", dir=tmp_path / "pods" / "t", argv=["sh", "-c", "read x; echo got-$x"],
+                 env={"PATH": "/usr/bin:/bin"}, restart_policy="Never", container={"tty": True, "stdin": True})
+    p = rt._spawn(pp)
+    assert pp.tty_master == -1 and pp.stdin_w >= 0
+    os.write(pp.stdin_w, b"hi\n")
+    close_stdin(pp)
+    assert p.wait(10) == 0
+    log = (pp.dir / "log").read_text()
+    assert "no pseudo-terminal on this node" in log and "got-hi" in log, log

@@ -1213,7 +1213,13 @@ class Agent:
         env.setdefault("TERM", "xterm")
         if self.runtime.tool_dirs:
             env["PATH"] = os.pathsep.join(self.runtime.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
-        master, slave = pty.openpty()
+        try:
+            master, slave = pty.openpty()
+        except OSError as e:  # a node without pseudo-terminals (no devpts)
+            send(b"\x01" + f"exec: no pseudo-terminal on node {self.name}: {e}\r\n".encode())
+            send(b"\x03" + json.dumps(exec_status(126)).encode())
+            ws.close()
+            return
 
         def controlling_tty():  # the child's own session, the terminal as its controlling tty
             os.setsid()

@@ -175,9 +175,8 @@ class PodRuntime:
         log = open(pp.dir / pp.log_name, "ab", buffering=0)
         c = pp.container or {}
         try:
-            if c.get("tty"):
-                p = self._spawn_tty(pp, argv, env, log)
-            elif c.get("stdin"):
+            p = self._spawn_tty(pp, argv, env, log) if c.get("tty") else None
+            if p is None and c.get("stdin"):
                 r, w = os.pipe()
                 try:
                     p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=r, stdout=log, stderr=subprocess.STDOUT,
@@ -189,7 +188,7 @@ class PodRuntime:
                     os.close(r)
                 with pp.io_lock:
                     pp.stdin_w = w
-            else:
+            elif p is None:
                 p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=subprocess.DEVNULL, stdout=log,
                                      stderr=subprocess.STDOUT, start_new_session=True, close_fds=True)
         finally:
@@ -200,15 +199,22 @@ class PodRuntime:
                                                   "start": proc_start_ticks(p.pid)})
         return p
 
-    def _spawn_tty(self, pp: PodProc, argv: list[str], env: dict, log) -> subprocess.Popen:
+    def _spawn_tty(self, pp: PodProc, argv: list[str], env: dict, log) -> subprocess.Popen | None:
         """`tty: true`: the container gets a pty as its controlling terminal (stdin, stdout and
         stderr), like the kubelet's; a pump thread copies what it writes to the container's log and
-        to every `kubectl attach` session, which write keystrokes and resizes to the master side."""
+        to every `kubectl attach` session, which write keystrokes and resizes to the master side.
+        None on a node without pseudo-terminals (no devpts: the MI355X GPU boxes): the container
+        then runs as with `tty: false`, and its log says so."""
         import fcntl
         import pty
         import termios
 
-        master, slave = pty.openpty()
+        try:
+            master, slave = pty.openpty()
+        except OSError as e:
+            log.write(f"tk8s: no pseudo-terminal on this node ({e}): the container runs without a tty\n".encode())
+            return None
+
         env.setdefault("TERM", "xterm")
         try:
             p = subprocess.Popen(argv, env=env, cwd=pp.dir, stdin=slave, stdout=slave, stderr=slave,
