@@ -123,7 +123,7 @@ def test_the_fabric_rank_env_carries_the_unpacked_library_and_huge_page_malloc(m
 
     monkeypatch.setattr(rccl_unpack, "library_dir", lambda: tmp_path)
     for var in ("TK8S_RCCL_THP", "GLIBC_TUNABLES", "NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "TK8S_SHORTCUTS", "TK8S_FAULTS",
-                "TK8S_GPU_SYNC_TIMEOUT_S", "TK8S_RCCL_BLOCKING"):
+                "TK8S_GPU_SYNC_TIMEOUT_S", "TK8S_RCCL_BLOCKING", "TK8S_RCCL_PREWARM"):
         monkeypatch.delenv(var, raising=False)
     env, lib = fabric.rccl_rank_env()
     assert lib == tmp_path
@@ -136,6 +136,8 @@ def test_the_fabric_rank_env_carries_the_unpacked_library_and_huge_page_malloc(m
     assert got["GLIBC_TUNABLES"] == "glibc.malloc.arena_max=2:glibc.malloc.hugetlb=1" and got["NCCL_DEBUG"] == "INFO"
     monkeypatch.setenv("TK8S_RCCL_THP", "0")
     assert "GLIBC_TUNABLES" not in {e["name"] for e in fabric.rccl_rank_env()[0]}
+    monkeypatch.setenv("TK8S_RCCL_PREWARM", "0")  # the rank's code load on threads: off in the rank too
+    assert {"name": "TK8S_RCCL_PREWARM", "value": "0"} in fabric.rccl_rank_env()[0]
     env, lib = fabric.rccl_rank_env(fake=True)
     assert lib is None and [e["name"] for e in env] == ["NCCL_DEBUG"]
 

@@ -91,6 +91,7 @@ SHORTCUT_SWITCHES = {
     "TK8S_SKIP_SITE": "0",            # daemons' interpreters start without -S (utils/procs.plain_argv)
     "TK8S_RCCL_UNPACKED": "0",        # the fabric Job's RCCL with its device code unpacked (utils/rccl_unpack.py)
     "TK8S_RCCL_THP": "0",             # the fabric Job's malloc on transparent huge pages (fabric.py)
+    "TK8S_RCCL_PREWARM": "0",         # the rank's RCCL code load and stream on threads (tk8s_rccl.cpp)
 }
 
 

@@ -37,8 +37,9 @@ def rccl_rank_env(fake: bool = False) -> tuple[list[dict], Path | None]:
     huge pages: HIP copies RCCL's 108 MB code object several times while loading it (its stream
     read, comgr's set_data, ...), each copy into freshly faulted 4 KiB pages -- ~190 ms of a
     285 ms load was memcpy; on huge pages (the kernel's madvise mode is enough) the communicator
-    start went from 318 to 202 ms on the MI355X (profiles/r5_thp/). Off-switches:
-    TK8S_RCCL_UNPACKED=0, TK8S_RCCL_THP=0.
+    start went from 318 to 202 ms on the MI355X (profiles/r5_thp/); the rank then loads that code
+    and makes its stream on threads while the unique id is made (profiles/r6_rccl_prewarm/).
+    Off-switches: TK8S_RCCL_UNPACKED=0, TK8S_RCCL_THP=0, TK8S_RCCL_PREWARM=0.
 
     The unpacked copy is asked for, not named: ``TK8S_RCCL_UNPACKED=1`` makes the agent of the
     node that runs the rank PREPEND its own current copy to the rank's LD_LIBRARY_PATH
@@ -60,6 +61,8 @@ def rccl_rank_env(fake: bool = False) -> tuple[list[dict], Path | None]:
     if shortcut_on("TK8S_RCCL_THP"):
         tun = os.environ.get("GLIBC_TUNABLES")
         env.append({"name": "GLIBC_TUNABLES", "value": (tun + ":" if tun else "") + "glibc.malloc.hugetlb=1"})
+    if not shortcut_on("TK8S_RCCL_PREWARM"):  # the rank's code load and stream on threads (tk8s_rccl.cpp)
+        env.append({"name": "TK8S_RCCL_PREWARM", "value": "0"})
     return env, lib
 
 
