@@ -13,9 +13,10 @@
 // node (the r1-r6 tree) cost 17 compressions per level and three nearly empty launches after
 // the leaves -- 47 us of a 108 us tree at 256 MiB (profiles/r6_kernels). A 64-byte node costs 2,
 // and a block of 256 threads folds 1024 nodes five levels up in one launch (md5_fold_kernel):
-// 256 MiB is the leaf launch plus two fold launches. The fold stays out of the leaf kernel: at
-// 16 waves per CU the leaves are VALU-bound, and a fold there runs on a quarter of the lanes
-// for the full wave's issue cost (+27 us measured, profiles/r6_md5).
+// 256 MiB is the leaf launch plus two fold launches. The fold stays out of the leaf kernel: each
+// leaf wave's own serial chain sets the leaves' time (4 chains per SIMD at the grid's 16 waves
+// per CU), and a fold there adds 6 compressions to it, on a quarter of the lanes (+27 us
+// measured, profiles/r6_md5).
 //
 // Per lane: 16 message words per 64-byte block via four 16-byte loads (the next block is
 // loaded before the current one is compressed, so its latency hides under 64 ALU steps);
