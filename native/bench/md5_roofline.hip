@@ -93,6 +93,72 @@ __global__ __launch_bounds__(kMd5Block) void md5_chunks_coalesced_unpinned(const
 
 }  // namespace tk8s
 
+namespace tk8s {
+// Leaf-kernel variants for the leaf-size question: kStep bytes of each of a wave's 64 chunks per
+// step (128: the production kernel's shape; 64: a 5 KiB LDS tile per wave, so 8 waves per SIMD
+// fit -- the grid has that many only with 512-byte leaves).
+template <int kStep>
+__global__ __launch_bounds__(256, kStep == 64 ? 8 : 4) void md5_leaves_step(const unsigned char* __restrict__ src,
+                                                                           unsigned chunk_bytes,
+                                                                           unsigned long long ngroups,
+                                                                           u32x4* __restrict__ digests) {
+  constexpr int kVec = kStep / 16, kRowV = kVec + 1, kPerInst = 64 / kVec;
+  __shared__ u32x4 tile[4][64 * kRowV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long group = static_cast<unsigned long long>(blockIdx.x) * 4 + w;
+  if (group >= ngroups) return;
+  u32x4* my = tile[w];
+  const unsigned char* gbase = src + group * 64ull * chunk_bytes;
+  const int sub = lane / kVec, piece = lane % kVec;
+  const unsigned steps = chunk_bytes / kStep;
+  u32x4 r[kVec];
+  auto load = [&](unsigned step) {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i)
+      r[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+          gbase + static_cast<size_t>(kPerInst * i + sub) * chunk_bytes + step * kStep + piece * 16u));
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) my[(kPerInst * i + sub) * kRowV + piece] = r[i];
+  };
+  unsigned st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+  load(0);
+  stage();
+  for (unsigned step = 0; step < steps; ++step) {
+    if (step + 1 < steps) load(step + 1);
+    wave_sync_lds();
+    u32x4 v[kVec];
+#pragma unroll
+    for (int k = 0; k < kVec; ++k) v[k] = my[lane * kRowV + k];
+#pragma unroll
+    for (int b = 0; b < kVec / 4; ++b) {
+      unsigned m[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        m[4 * q + 0] = v[4 * b + q].x;
+        m[4 * q + 1] = v[4 * b + q].y;
+        m[4 * q + 2] = v[4 * b + q].z;
+        m[4 * q + 3] = v[4 * b + q].w;
+      }
+      md5_compress(st, m);
+    }
+    asm volatile("" ::"v"(st[0]), "v"(st[1]), "v"(st[2]), "v"(st[3]) : "memory");
+    wave_sync_lds();
+    if (step + 1 < steps) stage();
+  }
+  unsigned m[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) m[q] = 0;
+  m[0] = 0x80u;
+  const unsigned long long bits = static_cast<unsigned long long>(chunk_bytes) * 8ull;
+  m[14] = static_cast<unsigned>(bits);
+  m[15] = static_cast<unsigned>(bits >> 32);
+  md5_compress(st, m);
+  digests[group * 64 + lane] = u32x4{st[0], st[1], st[2], st[3]};
+}
+}  // namespace tk8s
+
 int main(int argc, char** argv) {
   using namespace tk8s;
   const size_t mib = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 256;
@@ -108,8 +174,9 @@ int main(int argc, char** argv) {
   unsigned char* src = nullptr;
   u32x4 *wa = nullptr, *wb = nullptr, *out = nullptr;
   CK(hipMalloc(&src, bytes));
-  CK(hipMalloc(&wa, nleaves * 16));
-  CK(hipMalloc(&wb, nleaves * 16));
+  const size_t ws = (bytes / 512) * 16;  // the digests of the smallest leaves timed below (512 B)
+  CK(hipMalloc(&wa, ws));
+  CK(hipMalloc(&wb, ws));
   CK(hipMalloc(&out, 16));
   constexpr size_t kFlush = 512ull << 20;
   void* flush = nullptr;
@@ -131,6 +198,23 @@ int main(int argc, char** argv) {
                                      ngroups, wa);
                 }});
   vs.push_back({"leaves_again", [&] { md5_chunks(src, bytes, chunk, wa, s); }});  // order control
+  // the leaf-size question: 1 KiB vs 512-byte leaves, 128- vs 64-byte steps, and one lane per
+  // chunk without LDS (the tail kernel), each over the same 256 MiB
+  for (unsigned cb : {1024u, 512u}) {
+    const unsigned long long ng = bytes / cb / 64;
+    const std::string tag = std::to_string(cb);
+    vs.push_back({"step128_c" + tag, [&, cb, ng] {
+                    hipLaunchKernelGGL(md5_leaves_step<128>, dim3((ng + 3) / 4), dim3(256), 0, s, src, cb, ng, wa);
+                  }});
+    vs.push_back({"step64_c" + tag, [&, cb, ng] {
+                    hipLaunchKernelGGL(md5_leaves_step<64>, dim3((ng + 3) / 4), dim3(256), 0, s, src, cb, ng, wa);
+                  }});
+    vs.push_back({"lane_c" + tag, [&, cb] {
+                    const unsigned long long n = bytes / cb;
+                    hipLaunchKernelGGL(md5_chunks_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src,
+                                       static_cast<unsigned long long>(bytes), cb, n, wa);
+                  }});
+  }
   for (unsigned long long n : {nleaves, nleaves / 1024, 4096ull, 256ull, 64ull, 4ull}) {
     if (n > nleaves) continue;
     const std::string tag = std::to_string(n);
