@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import os
 import sys
-import threading
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 BIN = os.path.join(PKG, "bin")
@@ -442,6 +441,8 @@ def agent_zygotes(p: dict) -> None:
             except OSError:
                 continue
             _AGENTS[os.path.realpath(sb)] = {"pid": pid, "sandbox": sb, "args": args, "pidfile": pidfile}
+
+    import threading  # here, not at the top: the burn-in is spawned before this import's ~1-2 ms
 
     _AGENTS_STARTED = threading.Thread(target=spawn_all, name="agent-zygotes", daemon=True)
     _AGENTS_STARTED.start()
