@@ -1050,3 +1050,25 @@ def test_attach_to_a_pods_stdin_and_tty_and_kubectl_run_it(ws, tmp_path_factory)
            "sh", "-c", "read a; echo run-$a; exit 6", input="yes\n")
     assert r.returncode == 6 and "run-yes" in r.stdout and 'pod "oneoff" deleted' in r.stderr, (r.returncode, r.stdout, r.stderr)
     assert kc("get", "pod", "oneoff").returncode != 0
+
+
+def test_exec_it_on_a_node_without_pseudo_terminals_runs_on_pipes(ws):
+    """The MI355X GPU boxes mount no devpts: `kubectl exec -it` there runs the command on pipes
+    (keystrokes in, output back as it comes, its exit code last) and says so, and a `tty: true`
+    pod runs as `tty: false` with its stdin pipe (node.no_pty injects the missing devpts)."""
+    _summary(_setup(ws, "--nodes", "1", "--rccl", "off", env=_env(TK8S_FAULTS="node.no_pty")))
+    kc = lambda *a, **kw: subprocess.run(["./kubectl", *a], cwd=ws, env=_env(), capture_output=True, text=True,
+                                         timeout=60, **kw)
+    (ws / "p.json").write_text(json.dumps({"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "np"},
+                                           "spec": {"containers": [{"name": "c", "command": ["sleep", "120"]}]}}))
+    assert kc("apply", "-f", str(ws / "p.json")).returncode == 0
+    deadline = time.monotonic() + 30
+    while time.monotonic() < deadline and json.loads(kc("get", "pod", "np", "-o", "json").stdout)["status"].get("phase") != "Running":
+        time.sleep(0.1)
+    r = kc("exec", "-it", "np", "--", "sh", input="echo piped-$((4+5)); [ -t 0 ] || echo notty; exit 4\n")
+    assert r.returncode == 4 and "piped-9" in r.stdout and "notty" in r.stdout, (r.returncode, r.stdout, r.stderr)
+    assert "no pseudo-terminal on node" in r.stdout, r.stdout
+    # a tty pod: no pty to give it, so its stdin is a pipe (the bundled kubectl run -it still works)
+    r = kc("run", "-i", "-t", "--rm", "--restart=Never", "tt", "--image=busybox", "--command", "--",
+           "sh", "-c", "read a; echo run-$a; [ -t 0 ] || echo nopty", input="ok\n")
+    assert r.returncode == 0 and "run-ok" in r.stdout and "nopty" in r.stdout, (r.returncode, r.stdout, r.stderr)

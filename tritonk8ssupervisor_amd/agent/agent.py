@@ -1214,11 +1214,11 @@ class Agent:
         if self.runtime.tool_dirs:
             env["PATH"] = os.pathsep.join(self.runtime.tool_dirs + [env.get("PATH", os.environ.get("PATH", ""))])
         try:
+            if fault("node.no_pty", self.name) is not None:
+                raise OSError("out of pty devices (injected: node.no_pty)")
             master, slave = pty.openpty()
-        except OSError as e:  # a node without pseudo-terminals (no devpts)
-            send(b"\x01" + f"exec: no pseudo-terminal on node {self.name}: {e}\r\n".encode())
-            send(b"\x03" + json.dumps(exec_status(126)).encode())
-            ws.close()
+        except OSError as e:  # a node without pseudo-terminals (no devpts: the MI355X GPU boxes)
+            self._run_exec_pipes(x, pp, ws, send, env, e)
             return
 
         def controlling_tty():  # the child's own session, the terminal as its controlling tty
@@ -1275,6 +1275,52 @@ class Agent:
             send(b"\x01" + data)
         code = proc.wait()
         os.close(master)
+        send(b"\x03" + json.dumps(exec_status(code if code >= 0 else 128 - code)).encode())
+        ws.close()
+
+    def _run_exec_pipes(self, x: dict, pp, ws, send, env: dict, why: Exception) -> None:
+        """``exec -it`` on a node with no pseudo-terminal (no devpts): the command runs on pipes
+        instead -- the keystrokes to its stdin, its stdout and stderr back as they come, [255, 0]
+        its end of file, the client going away its SIGHUP -- a line-based session rather than a
+        terminal, which its first line says."""
+        from ..controlplane.k8s_api import exec_status
+
+        send(b"\x01" + f"(no pseudo-terminal on node {self.name}: {why}; running without a tty)\r\n".encode())
+        try:
+            proc = subprocess.Popen(container_exec_argv(pp, list(x["command"])), stdin=subprocess.PIPE,
+                                    stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, cwd=pp.dir,
+                                    start_new_session=True, close_fds=True)
+        except OSError as e:
+            send(b"\x01" + f"exec: {e}\r\n".encode())
+            send(b"\x03" + json.dumps(exec_status(127)).encode())
+            ws.close()
+            return
+
+        def inbound():
+            while True:
+                m = ws.recv()
+                if m is None or m[:1] == b"\xfe":
+                    if proc.poll() is None:
+                        with contextlib.suppress(OSError):
+                            os.killpg(proc.pid, signal.SIGHUP)
+                    return
+                with contextlib.suppress(OSError, ValueError):
+                    if m[:2] == b"\xff\x00":  # the client closed its stdin
+                        proc.stdin.close()
+                    elif m[:1] == b"\x00" and len(m) > 1:
+                        proc.stdin.write(m[1:])
+                        proc.stdin.flush()
+
+        threading.Thread(target=inbound, name=f"exec-{x['metadata']['name']}-in", daemon=True).start()
+        while True:
+            try:
+                data = os.read(proc.stdout.fileno(), 65536)
+            except OSError:
+                break
+            if not data:
+                break
+            send(b"\x01" + data)
+        code = proc.wait()
         send(b"\x03" + json.dumps(exec_status(code if code >= 0 else 128 - code)).encode())
         ws.close()
 

@@ -33,6 +33,7 @@ import threading
 import time
 from pathlib import Path
 
+from ..utils.faults import fault
 from ..utils.fsutil import atomic_write_json
 from ..utils.procs import kill_group, proc_start_ticks
 from ..utils.record import field, record as dataclass
@@ -210,6 +211,8 @@ class PodRuntime:
         import termios
 
         try:
+            if fault("node.no_pty") is not None:
+                raise OSError("out of pty devices (injected: node.no_pty)")
             master, slave = pty.openpty()
         except OSError as e:
             log.write(f"tk8s: no pseudo-terminal on this node ({e}): the container runs without a tty\n".encode())
