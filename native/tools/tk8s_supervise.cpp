@@ -4,6 +4,12 @@
 //
 //   tk8s-supervise --pidfile F [--log L] [--restart no|on-failure|always|unless-stopped]
 //                  [--max-restarts N] [--backoff-ms M] -- PROGRAM [ARGS...]
+//   tk8s-supervise --spawn-list FILE
+//
+// --spawn-list: start one supervisor per line of FILE (its arguments, tab-separated), each in its
+// own session, and exit. The bring-up's CLI hands its node-agent zygotes to this one process
+// instead of spawning N supervisors itself: Python's os.posix_spawn keeps the GIL through each
+// vfork until the exec, ~5 ms of the CLI's own start at 8 workers (profiles/r6_curve/).
 //
 // * Starts a new session; the child stays in the supervisor's process group, so one
 //   killpg(pgid) from teardown stops both.
@@ -79,6 +85,44 @@ void write_pidfile(const std::string& path, pid_t child, int restarts) {
   std::rename(tmp.c_str(), path.c_str());
 }
 
+int spawn_list(const char* list) {
+  FILE* f = std::fopen(list, "r");
+  if (!f) {
+    std::fprintf(stderr, "tk8s-supervise: %s: %s\n", list, std::strerror(errno));
+    return 2;
+  }
+  std::string text;
+  char buf[4096];
+  for (size_t n; (n = std::fread(buf, 1, sizeof buf, f)) > 0;) text.append(buf, n);
+  std::fclose(f);
+  int started = 0;
+  size_t at = 0;
+  while (at < text.size()) {
+    size_t eol = text.find('\n', at);
+    if (eol == std::string::npos) eol = text.size();
+    std::vector<std::string> args{"tk8s-supervise"};
+    for (size_t i = at; i <= eol;) {
+      size_t tab = text.find('\t', i);
+      if (tab == std::string::npos || tab > eol) tab = eol;
+      args.push_back(text.substr(i, tab - i));
+      i = tab + 1;
+    }
+    at = eol + 1;
+    if (args.size() < 3) continue;  // a blank line
+    const pid_t pid = fork();
+    if (pid < 0) return 1;
+    if (pid == 0) {
+      std::vector<char*> av;
+      for (auto& a : args) av.push_back(&a[0]);
+      av.push_back(nullptr);
+      execv("/proc/self/exe", av.data());
+      _exit(127);
+    }
+    ++started;
+  }
+  return started > 0 ? 0 : 1;
+}
+
 int usage() {
   std::fprintf(stderr,
                "usage: tk8s-supervise --pidfile F [--log L] [--restart no|on-failure|always|unless-stopped]\n"
@@ -89,6 +133,7 @@ int usage() {
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (argc == 3 && std::strcmp(argv[1], "--spawn-list") == 0) return spawn_list(argv[2]);
   std::string pidfile, log, policy = "unless-stopped";
   long max_restarts = -1, backoff_ms = 100;
   int i = 1;

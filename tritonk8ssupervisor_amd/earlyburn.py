@@ -402,57 +402,76 @@ def _mark_zygote(path: str) -> None:
 
 AGENT_ENTRY = "import tritonk8ssupervisor_amd.agent.__main__"  # = workspace.AGENT_ENTRY
 _AGENTS: dict[str, dict] = {}
-_AGENTS_STARTED: threading.Thread | None = None
 
 
 def agent_zygotes(p: dict) -> None:
-    """Start each planned worker's node agent interpreter now (in a thread: a spawn per worker),
-    under its supervisor, in the worker's future sandbox: it imports everything while the
-    orchestrator provisions, then waits in ``run/agent.args`` for what only the created machine
-    knows -- its argv (name, address) and environment (sandbox, GPUs) -- which the worker's boot
-    hook (orchestrator._boot_agent) writes. The agent then runs exactly as if started then."""
-    global _AGENTS_STARTED
+    """Start each planned worker's node agent interpreter now, under its supervisor, in the
+    worker's future sandbox: it imports everything while the orchestrator provisions, then waits
+    in ``run/agent.args`` for what only the created machine knows -- its argv (name, address) and
+    environment (sandbox, GPUs) -- which the worker's boot hook (orchestrator._boot_agent) writes.
+    The agent then runs exactly as if started then. The supervisors are started by ONE helper
+    (``tk8s-supervise --spawn-list``): os.posix_spawn holds this interpreter's GIL through each
+    vfork until the exec, so N spawns here were ~5 ms of the CLI's own start at 8 workers on the
+    MI355X host (profiles/r6_curve/ab_agent_zygote). Their pids come from their pidfiles."""
     if os.environ.get("TK8S_AGENT_ZYGOTE", "1") == "0" or not p.get("workers"):
         return
     sup = os.path.join(BIN, "tk8s-supervise")
     if not os.access(sup, os.X_OK):
         return
+    lines = []
+    for name in p["workers"]:
+        sb = os.path.join(p["state_dir"], "machines", name)
+        pidfile = os.path.join(sb, "run", "agent.pid")
+        try:
+            if os.path.exists(pidfile):  # something of an earlier run: leave it to the orchestrator
+                continue
+            os.makedirs(os.path.join(sb, "run"), exist_ok=True)
+            os.makedirs(os.path.join(sb, "logs"), exist_ok=True)
+            args = os.path.join(sb, "run", "agent.args")
+            _mark_zygote(os.path.join(sb, "run", "agent.zygote"))
+        except OSError:
+            continue
+        argv = ["--pidfile", pidfile, "--log", os.path.join(sb, "logs", "agent.log"), "--restart", "unless-stopped",
+                "--", sys.executable, "-S", "-c", AGENT_ENTRY, "--await-args", args]
+        if any("\t" in a or "\n" in a for a in argv):
+            continue  # (the list is tab-separated; such a path gets no zygote)
+        lines.append("\t".join(argv))
+        _AGENTS[os.path.realpath(sb)] = {"pid": None, "sandbox": sb, "args": args, "pidfile": pidfile}
+    if not lines:
+        return
+    spec = os.path.join(p["state_dir"], "run", "agent-zygotes.list")
     env = dict(os.environ)
     env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(PKG)] + [x for x in env.get("PYTHONPATH", "").split(os.pathsep) if x])
-
-    def spawn_all():
-        for name in p["workers"]:
-            sb = os.path.join(p["state_dir"], "machines", name)
-            pidfile = os.path.join(sb, "run", "agent.pid")
-            try:
-                if os.path.exists(pidfile):  # something of an earlier run: leave it to the orchestrator
-                    continue
-                os.makedirs(os.path.join(sb, "run"), exist_ok=True)
-                os.makedirs(os.path.join(sb, "logs"), exist_ok=True)
-                args = os.path.join(sb, "run", "agent.args")
-                _mark_zygote(os.path.join(sb, "run", "agent.zygote"))
-                argv = [sup, "--pidfile", pidfile, "--log", os.path.join(sb, "logs", "agent.log"), "--restart",
-                        "unless-stopped", "--", sys.executable, "-S", "-c", AGENT_ENTRY, "--await-args", args]
-                pid = os.posix_spawn(sup, argv, env, setsid=True, file_actions=[
-                    (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
-                    (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
-                    (os.POSIX_SPAWN_OPEN, 2, os.devnull, os.O_WRONLY, 0),
-                ])
-            except OSError:
-                continue
-            _AGENTS[os.path.realpath(sb)] = {"pid": pid, "sandbox": sb, "args": args, "pidfile": pidfile}
-
-    import threading  # here, not at the top: the burn-in is spawned before this import's ~1-2 ms
-
-    _AGENTS_STARTED = threading.Thread(target=spawn_all, name="agent-zygotes", daemon=True)
-    _AGENTS_STARTED.start()
+    try:
+        with open(spec, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        os.posix_spawn(sup, [sup, "--spawn-list", spec], env, file_actions=[
+            (os.POSIX_SPAWN_OPEN, 0, os.devnull, os.O_RDONLY, 0),
+            (os.POSIX_SPAWN_OPEN, 1, os.devnull, os.O_WRONLY, 0),
+            (os.POSIX_SPAWN_OPEN, 2, os.devnull, os.O_WRONLY, 0),
+        ])
+    except OSError:
+        _AGENTS.clear()
 
 
-def agent_zygote_for(sandbox: str) -> dict | None:
-    """The node agent zygote started for this worker sandbox, if any (once)."""
-    if _AGENTS_STARTED is not None:
-        _AGENTS_STARTED.join()
-    return _AGENTS.pop(os.path.realpath(sandbox), None)
+def agent_zygote_for(sandbox: str, wait_s: float = 2.0) -> dict | None:
+    """The node agent zygote started for this worker sandbox, if any (once), with its
+    supervisor's pid from the pidfile the supervisor writes as it starts (waited for briefly)."""
+    import time
+
+    z = _AGENTS.pop(os.path.realpath(sandbox), None)
+    if z is None:
+        return None
+    deadline = time.monotonic() + wait_s
+    while True:
+        try:
+            with open(z["pidfile"]) as f:
+                z["pid"] = int(_loads(f.read())["pid"])
+            return z
+        except (OSError, ValueError, KeyError, TypeError):
+            if time.monotonic() > deadline:
+                return None
+            time.sleep(0.001)
 
 
 def zygote_for(sandbox: str) -> dict | None:
