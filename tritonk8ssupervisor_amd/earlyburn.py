@@ -454,7 +454,7 @@ def agent_zygotes(p: dict) -> None:
         _AGENTS.clear()
 
 
-def agent_zygote_for(sandbox: str, wait_s: float = 2.0) -> dict | None:
+def agent_zygote_for(sandbox: str, wait_s: float = 0.5) -> dict | None:
     """The node agent zygote started for this worker sandbox, if any (once), with its
     supervisor's pid from the pidfile the supervisor writes as it starts (waited for briefly)."""
     import time
