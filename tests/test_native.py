@@ -180,3 +180,30 @@ def test_summarize_rocprof_stats(tmp_path):
     s = summarize_rocprof(tmp_path / "prof")
     assert list(s["ranks"]) == ["rank0"]
     assert s["ranks"]["rank0"][0] == {"kernel": "ncclDevKernel_Generic", "calls": 10, "total_us": 90.0, "avg_us": 9.0}
+
+
+def test_supervise_spawn_list_starts_one_supervisor_per_line_each_in_its_own_session(native_build, tmp_path):
+    """`tk8s-supervise --spawn-list FILE` (how the CLI hands over its node-agent zygotes): one
+    supervisor per tab-separated line, each a session leader with its pidfile, the helper gone."""
+    sup = native_build["tk8s-supervise"]
+    import shutil
+
+    sleep = shutil.which("sleep")
+    lines = [f"--pidfile\t{tmp_path / f'{n}.pid'}\t--restart\tno\t--\t{sleep}\t30" for n in ("a", "b")]
+    (tmp_path / "list").write_text("\n".join(lines) + "\n\n")
+    # (stdio not captured: the supervisors inherit it, as the CLI's helper gives them /dev/null)
+    r = subprocess.run([str(sup), "--spawn-list", str(tmp_path / "list")], stdout=subprocess.DEVNULL,
+                       stderr=subprocess.DEVNULL, timeout=10)
+    assert r.returncode == 0
+    pids = []
+    deadline = time.monotonic() + 5
+    for n in ("a", "b"):
+        while not (tmp_path / f"{n}.pid").exists() and time.monotonic() < deadline:
+            time.sleep(0.01)
+        rec = json.loads((tmp_path / f"{n}.pid").read_text())
+        assert rec["pid"] == rec["pgid"] == os.getsid(rec["pid"]) and rec["child"] > 0, rec
+        pids.append(rec["pid"])
+    assert len(set(pids)) == 2
+    for pid in pids:
+        os.killpg(pid, signal.SIGTERM)
+    assert subprocess.run([str(sup), "--spawn-list", str(tmp_path / "missing")], capture_output=True, timeout=10).returncode == 2
