@@ -582,6 +582,9 @@ def config2_curve(root: Path, args, env: dict, log, steps: int, warmup: int = 1)
             "package": "cpu-only", "warmup": warmup, "points": points,
             "wall_s": round(time.perf_counter() - t_curve, 3),
             "scaling_8_vs_1": round(points[-1]["mean_s"] / points[0]["mean_s"], 3)
+            if len(points) > 1 and points[0]["workers"] == 1 and points[-1]["workers"] == 8 else None,
+            # the same ratio of the medians: one slow step among 5 moves the means' ratio by ~0.1
+            "scaling_8_vs_1_median": round(points[-1]["median_s"] / points[0]["median_s"], 3)
             if len(points) > 1 and points[0]["workers"] == 1 and points[-1]["workers"] == 8 else None}
 
 
